@@ -1,0 +1,197 @@
+"""Benchmark: HetroGIN training steps on MI355X (BASELINE.json metric), one process per GPU.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config cfg2]
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
+        --master-port P bench.py --gpus N --steps K --warmup W
+
+A step is one train.py iteration (train.py:31-44) on a resident synthetic hetero graph: zero_grad,
+forward through every relation of every layer (as PyG computes them), sqrt(MAPE), backward, the RCCL
+gradient all-reduce (N > 1), Adam.  Each rank owns one whole graph of the configured size (data parallel
+over graph components), so per-GPU work is fixed as N grows ("weak" scaling).
+
+value = N * E_conv / t_step, E_conv = edges of the four convolved relations (p->l, l->p, l->n, n->l),
+counted once per step.  t_step = max over ranks of (barrier + hipDeviceSynchronize
+bracketed K steps) / K.  Rank 0 prints one JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+for _p in (ROOT, os.path.join(ROOT, "gnn-link-prediction_amd")):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+METRIC = json.load(open(os.path.join(ROOT, "BASELINE.json")))["metric"]
+HBM_PEAK_GBS = 8000.0        # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+F32_MFMA_PEAK_TFS = 157.3    # v_mfma_f32_32x32x2_f32 dense peak (= f32 vector peak)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="cfg2", help="cfg2 (default, BASELINE configs[1]), cfg3, cfg4c")
+    ap.add_argument("--prune-dead", action="store_true", help="skip dead relations (reported separately)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-steps", type=int, default=2)
+    ap.add_argument("--no-probe", action="store_true", help="no per-kernel events in the timed region")
+    return ap.parse_args()
+
+
+def cpu_threads() -> int:
+    n = len(os.sched_getaffinity(0))
+    env = os.environ.get("OMP_NUM_THREADS")
+    if env and env.isdigit() and int(env) > 0:
+        n = min(n, int(env))
+    return max(1, n)
+
+
+def cpu_baseline(cfg, steps: int) -> dict:
+    """The oracle (torch CPU ops == the PyG CPU path) on the same workload, on this box's host cores."""
+    from hgin.data import synthetic_graph
+    from oracle.pyg_cpu import OracleHetroGIN, train_step
+    threads = cpu_threads()
+    prev = torch.get_num_threads()
+    torch.set_num_threads(threads)
+    try:
+        g = synthetic_graph(cfg, seed=0, device="cpu")
+        torch.manual_seed(1997)
+        model = OracleHetroGIN(**cfg.model_kwargs({"link": cfg.f_link, "path": cfg.f_path, "node": cfg.f_node}))
+        opt = torch.optim.Adam(lr=1e-3, params=model.parameters())
+        train_step(model, opt, g.x_dict(), g.edge_index_dict(), g.batch["path"], g.y)   # warm-up
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            train_step(model, opt, g.x_dict(), g.edge_index_dict(), g.batch["path"], g.y)
+        dt = (time.perf_counter() - t0) / steps
+    finally:
+        torch.set_num_threads(prev)
+    cpu_model = ""
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                cpu_model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return {"value": cfg.conv_edges / dt, "unit": "edges/s", "cores": threads, "kind": "port",
+            "sample": f"{cfg.name} full graph ({cfg.nodes} nodes / {cfg.graph_edges} edges), 1 warm-up + {steps} "
+                      f"timed train steps (fwd + sqrt-MAPE + bwd + Adam) of oracle/pyg_cpu.py (torch CPU ops = "
+                      f"the reference's PyG CPU path), {threads} threads, {cpu_model}",
+            "ms_per_step": dt * 1e3}
+
+
+def main():
+    args = parse()
+    from hgin import HetroGIN, _lib, profiling
+    from hgin.data import CONFIGS, synthetic_graph
+    from hgin.dist import GradAllReducer
+    from hgin.train import train_step
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus and rank == 0:
+        print(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+    _lib.lib()
+
+    cfg = CONFIGS[args.config]
+    graph = synthetic_graph(cfg, seed=rank, device=dev)      # one independent component per rank
+    torch.manual_seed(1997)
+    model = HetroGIN(**cfg.model_kwargs({"link": cfg.f_link, "path": cfg.f_path, "node": cfg.f_node})).to(dev)
+    if args.prune_dead:
+        model.prune_dead(True)
+    opt = torch.optim.Adam(lr=1e-3, params=model.parameters(), weight_decay=0)
+    reducer = GradAllReducer(model.parameters()) if world > 1 else None
+
+    def barrier():
+        if world > 1:
+            dist.barrier(device_ids=[local])
+
+    for _ in range(args.warmup):
+        train_step(model, opt, graph, reducer=reducer)
+    barrier()
+    torch.cuda.synchronize()
+
+    probe = None if args.no_probe else profiling.start()
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        loss = train_step(model, opt, graph, reducer=reducer)
+    torch.cuda.synchronize()
+    barrier()
+    t1 = time.perf_counter()
+    profiling.stop()
+    dt = torch.tensor([(t1 - t0) / args.steps], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(dt, op=dist.ReduceOp.MAX)
+    t_step = float(dt.item())
+    final_loss = float(loss)
+
+    out = None
+    if rank == 0:
+        value = world * cfg.conv_edges / t_step
+        roofline = mfma = None
+        if probe is not None:
+            s = probe.summary()
+            a = s.get("aggregate")
+            if a:
+                achieved = a["avg_work"] / (a["avg_ms"] / 1e3) / 1e9
+                roofline = {"bound": "hbm", "kernel": "hgin_aggregate_f32 (k_aggregate<4,32,8>)",
+                            "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                            "bytes_per_launch": a["avg_work"], "avg_launch_ms": round(a["avg_ms"], 5),
+                            "launches_per_step": a["launches"] / args.steps,
+                            "share_of_step": round(a["total_ms"] / args.steps / (t_step * 1e3), 4)}
+                tf = os.path.join(ROOT, "profiles", f"traffic_{cfg.name}.json")
+                if os.path.exists(tf):
+                    tr = json.load(open(tf))
+                    roofline["traffic"] = tr.get("bytes_per_launch")
+                    roofline["traffic_source"] = tr.get("source")
+            m = s.get("gin_mlp")
+            if m:
+                tfs = m["avg_work"] / (m["avg_ms"] / 1e3) / 1e12
+                mfma = {"bound": "mfma", "kernel": "hgin_gin_mlp_fwd_f32", "achieved": round(tfs, 2),
+                        "peak": F32_MFMA_PEAK_TFS, "unit": "TFLOP/s", "frac": round(tfs / F32_MFMA_PEAK_TFS, 4),
+                        "avg_launch_ms": round(m["avg_ms"], 5),
+                        "share_of_step": round(m["total_ms"] / args.steps / (t_step * 1e3), 4)}
+        out = {"metric": METRIC, "value": round(value, 1), "unit": "edges/s", "n_gpus": world,
+               "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(t_step * 1e3, 4),
+               "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+               "data": "synthetic: SURVEY.md §8.D generator (uniform endpoints, reverse relations = flips, randn "
+                       "features, rand+0.5 labels), random-init weights (seed 1997); one graph per rank",
+               "config": {"workload": f"{cfg.name}: {cfg.layers}-layer HeteroGIN, {cfg.nodes} nodes / "
+                                      f"{cfg.graph_edges} edges per GPU, 3 node types x "
+                                      f"{len(graph.edge_index)} edge types, hidden {cfg.hidden} fp32",
+                          "nodes_per_gpu": cfg.nodes, "graph_edges_per_gpu": cfg.graph_edges,
+                          "conv_edges_per_gpu": cfg.conv_edges, "hidden": cfg.hidden, "layers": cfg.layers,
+                          "global_batch": world, "parallelism": f"dp{world} (graph component per rank, RCCL "
+                                                                f"gradient all-reduce)",
+                          "prune_dead": bool(args.prune_dead)},
+               "roofline": roofline, "mfma": mfma, "final_loss": final_loss}
+        if world == 1 and not args.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline(cfg, args.cpu_steps)
+        else:
+            out["cpu_baseline"] = None
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier(device_ids=[local])
+        dist.destroy_process_group()
+    return out
+
+
+if __name__ == "__main__":
+    main()

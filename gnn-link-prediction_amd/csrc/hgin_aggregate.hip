@@ -1,0 +1,178 @@
+// A3 + A4 — GINConv message + sum aggregate + (1 + eps) self term, fused.
+//
+// Reference: PyG MessagePassing.propagate at models.py:208 = index_select gather (x_j = x_src[ei[0]],
+// an [E, F] tensor written and re-read) + torch_scatter.scatter(..., reduce='sum') (zeros +
+// scatter_add_, atomics on the GPU), then models.py:212-215 (cat or +=) as separate kernels.
+//
+// Here: one pass over a stable CSR (hgin_csr.hip).  A lane group of G lanes owns one destination row;
+// each lane holds VEC consecutive features (float4 when the layout allows: 16 B per lane, the row read
+// as one contiguous G*16-byte segment), walks the row's neighbours in edge order and accumulates
+// sequentially — acc = ((0 + x_1) + x_2) + ...  — exactly CPU scatter_add_'s order, with no FMA
+// contraction (explicit __fadd_rn / __fmul_rn), so results are bit-identical to the reference's CPU path.
+// U neighbour rows are loaded before any of them is added, keeping U * G * 16 B in flight per group
+// while the add order stays sequential.  The self term is applied in the epilogue of the same pass,
+// writing straight into the concat layout: no [E, F] messages, no atomics, no cat.
+//
+// HBM bytes per launch (the roofline model):
+//   E * (4 + 4 * F_src) + (N + 1) * 4 + N * 4 * F_out  [+ N * 4 * F_dst when a self term is read]
+#include "hgin_common.h"
+
+namespace hgin {
+namespace {
+
+template <int VEC>
+struct Vec;
+template <>
+struct Vec<1> {
+  using T = float;
+  static __device__ __forceinline__ T load(const float* p) { return *p; }
+  static __device__ __forceinline__ void store(float* p, T v) { *p = v; }
+  static __device__ __forceinline__ float get(const T& v, int) { return v; }
+  static __device__ __forceinline__ void set(T& v, int, float x) { v = x; }
+};
+template <>
+struct Vec<4> {
+  using T = float4;
+  static __device__ __forceinline__ T load(const float* p) { return *reinterpret_cast<const float4*>(p); }
+  static __device__ __forceinline__ void store(float* p, T v) { *reinterpret_cast<float4*>(p) = v; }
+  static __device__ __forceinline__ float get(const T& v, int c) {
+    return c == 0 ? v.x : (c == 1 ? v.y : (c == 2 ? v.z : v.w));
+  }
+  static __device__ __forceinline__ void set(T& v, int c, float x) {
+    if (c == 0) v.x = x; else if (c == 1) v.y = x; else if (c == 2) v.z = x; else v.w = x;
+  }
+};
+
+template <int VEC, int G, int U>
+__global__ __launch_bounds__(256) void k_aggregate(const int32_t* __restrict__ rowptr, const int32_t* __restrict__ col,
+                                                   int64_t n_rows, const float* __restrict__ x_src, int64_t ld_src,
+                                                   int f_src, const float* __restrict__ x_dst, int64_t ld_dst,
+                                                   int f_dst, const float* __restrict__ eps, int combine,
+                                                   float* __restrict__ out, int64_t ld_out) {
+  using V = Vec<VEC>;
+  using T = typename V::T;
+  constexpr int kRowsPerWave = kWave / G;
+  const int lane = threadIdx.x & (kWave - 1);
+  const int grp = lane / G;
+  const int gl = lane % G;
+  const int64_t wave_id = (int64_t)blockIdx.x * (blockDim.x / kWave) + (threadIdx.x / kWave);
+  const int64_t r = wave_id * kRowsPerWave + grp;
+  if (r >= n_rows) return;
+  const int beg = rowptr[r];
+  const int end = rowptr[r + 1];
+  const float s = combine != HGIN_COMBINE_NONE ? __fadd_rn(1.0f, eps[0]) : 1.0f;
+  float* __restrict__ orow = out + r * ld_out;
+
+  for (int f0 = gl * VEC; f0 < f_src; f0 += G * VEC) {
+    float acc[VEC];
+#pragma unroll
+    for (int c = 0; c < VEC; ++c) acc[c] = 0.0f;
+    int k = beg;
+    for (; k + U <= end; k += U) {
+      int idx[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) idx[u] = col[k + u];
+      T v[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) v[u] = V::load(x_src + (int64_t)idx[u] * ld_src + f0);
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+#pragma unroll
+        for (int c = 0; c < VEC; ++c) acc[c] = __fadd_rn(acc[c], V::get(v[u], c));
+      }
+    }
+    for (; k < end; ++k) {
+      const T v = V::load(x_src + (int64_t)col[k] * ld_src + f0);
+#pragma unroll
+      for (int c = 0; c < VEC; ++c) acc[c] = __fadd_rn(acc[c], V::get(v, c));
+    }
+    T o;
+    if (combine == HGIN_COMBINE_ADD) {
+      const T xd = V::load(x_dst + r * ld_dst + f0);
+#pragma unroll
+      for (int c = 0; c < VEC; ++c) V::set(o, c, __fadd_rn(acc[c], __fmul_rn(s, V::get(xd, c))));
+    } else {
+#pragma unroll
+      for (int c = 0; c < VEC; ++c) V::set(o, c, acc[c]);
+    }
+    V::store(orow + f0, o);
+  }
+  if (combine == HGIN_COMBINE_CONCAT) {
+    for (int f0 = gl * VEC; f0 < f_dst; f0 += G * VEC) {
+      const T xd = V::load(x_dst + r * ld_dst + f0);
+      T o;
+#pragma unroll
+      for (int c = 0; c < VEC; ++c) V::set(o, c, __fmul_rn(s, V::get(xd, c)));
+      V::store(orow + f_src + f0, o);
+    }
+  }
+}
+
+template <int VEC, int G>
+int launch_aggregate(const int32_t* rowptr, const int32_t* col, int64_t n_rows, const float* x_src, int64_t ld_src,
+                     int f_src, const float* x_dst, int64_t ld_dst, int f_dst, const float* eps, int combine,
+                     float* out, int64_t ld_out, hipStream_t s) {
+  constexpr int kRowsPerWave = kWave / G;
+  constexpr int kU = 8;
+  const int64_t waves = ceil_div(n_rows, kRowsPerWave);
+  const int64_t blocks = ceil_div(waves, 256 / kWave);
+  k_aggregate<VEC, G, kU><<<dim3((unsigned)blocks), 256, 0, s>>>(rowptr, col, n_rows, x_src, ld_src, f_src, x_dst,
+                                                                   ld_dst, f_dst, eps, combine, out, ld_out);
+  return check_launch("hgin_aggregate_f32");
+}
+
+template <int VEC>
+int dispatch_g(int lanes_needed, const int32_t* rowptr, const int32_t* col, int64_t n_rows, const float* x_src,
+               int64_t ld_src, int f_src, const float* x_dst, int64_t ld_dst, int f_dst, const float* eps,
+               int combine, float* out, int64_t ld_out, hipStream_t s) {
+#define HGIN_AGG_CASE(GV)                                                                                     \
+  if (lanes_needed <= GV)                                                                                    \
+    return launch_aggregate<VEC, GV>(rowptr, col, n_rows, x_src, ld_src, f_src, x_dst, ld_dst, f_dst, eps, \
+                                     combine, out, ld_out, s);
+  HGIN_AGG_CASE(4)
+  HGIN_AGG_CASE(8)
+  HGIN_AGG_CASE(16)
+  HGIN_AGG_CASE(32)
+#undef HGIN_AGG_CASE
+  return launch_aggregate<VEC, 64>(rowptr, col, n_rows, x_src, ld_src, f_src, x_dst, ld_dst, f_dst, eps, combine,
+                                   out, ld_out, s);
+}
+
+}  // namespace
+}  // namespace hgin
+
+using namespace hgin;
+
+extern "C" int hgin_aggregate_f32(const int32_t* rowptr, const int32_t* col, int64_t n_rows, const float* x_src,
+                                  int64_t ld_src, int64_t f_src, const float* x_dst, int64_t ld_dst, int64_t f_dst,
+                                  const float* eps, int combine, float* out, int64_t ld_out, void* stream) {
+  HGIN_ARG_CHECK(combine == HGIN_COMBINE_NONE || combine == HGIN_COMBINE_ADD || combine == HGIN_COMBINE_CONCAT,
+                 "hgin_aggregate_f32: bad combine mode %d", combine);
+  HGIN_ARG_CHECK(n_rows >= 0 && f_src >= 0 && f_src < (1 << 24), "hgin_aggregate_f32: bad sizes");
+  if (n_rows == 0) return HGIN_OK;
+  HGIN_ARG_CHECK(rowptr != nullptr && out != nullptr, "hgin_aggregate_f32: rowptr/out NULL");
+  int64_t out_w = f_src;
+  if (combine != HGIN_COMBINE_NONE) {
+    HGIN_ARG_CHECK(x_dst != nullptr && eps != nullptr, "hgin_aggregate_f32: combine needs x_dst and eps");
+    HGIN_ARG_CHECK(f_dst >= 0 && f_dst < (1 << 24), "hgin_aggregate_f32: bad f_dst");
+    if (combine == HGIN_COMBINE_ADD)
+      HGIN_ARG_CHECK(f_dst == f_src, "hgin_aggregate_f32: ADD needs f_dst == f_src (%lld vs %lld)",
+                     (long long)f_dst, (long long)f_src);
+    if (combine == HGIN_COMBINE_CONCAT) out_w = f_src + f_dst;
+    HGIN_ARG_CHECK(ld_dst >= f_dst, "hgin_aggregate_f32: ld_dst < f_dst");
+  }
+  HGIN_ARG_CHECK(ld_src >= f_src && ld_out >= out_w, "hgin_aggregate_f32: leading dimension too small");
+  hipStream_t s = as_stream(stream);
+  const bool dst_ok = combine == HGIN_COMBINE_NONE || (aligned16(x_dst) && ld_dst % 4 == 0 && f_dst % 4 == 0);
+  const bool vec4 = f_src % 4 == 0 && aligned16(x_src) && ld_src % 4 == 0 && aligned16(out) && ld_out % 4 == 0 &&
+                    dst_ok && (f_src > 0 || f_dst > 0);
+  const int fd = combine == HGIN_COMBINE_CONCAT ? (int)f_dst : 0;
+  if (vec4) {
+    const int64_t widest = f_src > fd ? f_src : fd;
+    return dispatch_g<4>((int)ceil_div(widest, 4), rowptr, col, n_rows, x_src, ld_src, (int)f_src, x_dst, ld_dst,
+                         (int)f_dst, eps, combine, out, ld_out, s);
+  }
+  const int64_t widest = f_src > fd ? f_src : fd;
+  return dispatch_g<1>((int)widest, rowptr, col, n_rows, x_src, ld_src, (int)f_src, x_dst, ld_dst, (int)f_dst, eps,
+                       combine, out, ld_out, s);
+}

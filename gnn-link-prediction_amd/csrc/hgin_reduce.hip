@@ -1,0 +1,174 @@
+// A9 — backward of the GIN update's elementwise parts, with deterministic reductions.
+//
+// Reference: autograd of PReLU (models.py:238), Linear's bias (models.py:237) and of the self term
+// `(1 + eps) * x_r` (models.py:212-215), reached from loss.backward() at train.py:43.  On the GPU,
+// PyTorch reduces these with atomics / split reductions whose order varies; here every reduction has a
+// fixed shape — per block: a fixed per-thread order over a 256-row chunk, then an LDS combine in fixed
+// order; then one pass that adds the block partials in block order — so gradients are bitwise
+// reproducible run to run.
+#include "hgin_common.h"
+
+namespace hgin {
+namespace {
+
+constexpr int kRowsPerBlock = 256;
+
+__device__ __forceinline__ float block_sum_fixed(float v, float* red) {
+  // fixed-order tree over 256 threads (same pairing every launch)
+  const int t = threadIdx.x;
+  red[t] = v;
+  __syncthreads();
+  for (int off = 128; off > 0; off >>= 1) {
+    if (t < off) red[t] = __fadd_rn(red[t], red[t + off]);
+    __syncthreads();
+  }
+  const float r = red[0];
+  __syncthreads();
+  return r;
+}
+
+// MODE 0: PReLU backward.  in0 = g_y, in1 = z; out = g_z; colsum(g_z) -> part_col; sum(z<=0 ? z*g : 0) -> part_s
+// MODE 1: combine backward.  in0 = g (self-term columns), in1 = x_dst; out = s*g (optional);
+//         part_s = sum(g * x_dst); no column sums.
+template <int MODE>
+__global__ __launch_bounds__(256) void k_rows_bwd(const float* __restrict__ in0, int64_t ld0,
+                                                  const float* __restrict__ in1, int64_t ld1, int64_t M, int N,
+                                                  const float* __restrict__ scalar, float* __restrict__ out,
+                                                  int64_t ldo, float* __restrict__ part_col,
+                                                  float* __restrict__ part_s) {
+  __shared__ float red[256];
+  const int t = threadIdx.x;
+  const int CW = N < 256 ? N : 256;
+  const int RL = 256 / CW;
+  const bool active = t < CW * RL;
+  const int c0 = t % CW;
+  const int rl = t / CW;
+  const int64_t r0 = (int64_t)blockIdx.x * kRowsPerBlock;
+  const int64_t r1 = r0 + kRowsPerBlock < M ? r0 + kRowsPerBlock : M;
+  float sc = 0.0f;
+  if (MODE == 0) sc = scalar[0];
+  else sc = __fadd_rn(1.0f, scalar[0]);
+  float ssum = 0.0f;
+  const int iters = (N + CW - 1) / CW;
+  for (int it = 0; it < iters; ++it) {
+    const int c = c0 + it * CW;
+    float csum = 0.0f;
+    if (active && c < N) {
+      for (int64_t r = r0 + rl; r < r1; r += RL) {
+        const float g = in0[r * ld0 + c];
+        const float x = in1[r * ld1 + c];
+        if (MODE == 0) {
+          const bool pos = x > 0.0f;
+          const float gz = pos ? g : __fmul_rn(sc, g);
+          out[r * ldo + c] = gz;
+          csum = __fadd_rn(csum, gz);
+          if (!pos) ssum = __fadd_rn(ssum, __fmul_rn(x, g));
+        } else {
+          if (out) out[r * ldo + c] = __fmul_rn(sc, g);
+          ssum = __fadd_rn(ssum, __fmul_rn(g, x));
+        }
+      }
+    }
+    if (MODE == 0) {
+      red[t] = csum;
+      __syncthreads();
+      if (active && rl == 0 && c < N) {
+        float tot = 0.0f;
+        for (int j = 0; j < RL; ++j) tot = __fadd_rn(tot, red[j * CW + c0]);
+        part_col[(int64_t)blockIdx.x * N + c] = tot;
+      }
+      __syncthreads();
+    }
+  }
+  const float bs = block_sum_fixed(ssum, red);
+  if (t == 0) part_s[blockIdx.x] = bs;
+}
+
+// Sum block partials in block order: one thread per column (+ one block-wide pass for the scalar).
+__global__ __launch_bounds__(256) void k_final_cols(const float* __restrict__ part, int64_t nblk, int N,
+                                                    float* __restrict__ out) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= N) return;
+  float s = 0.0f;
+  for (int64_t b = 0; b < nblk; ++b) s = __fadd_rn(s, part[b * N + c]);
+  out[c] = s;
+}
+
+__global__ __launch_bounds__(256) void k_final_scalar(const float* __restrict__ part, int64_t nblk,
+                                                      float* __restrict__ out) {
+  __shared__ float red[256];
+  float s = 0.0f;
+  for (int64_t b = threadIdx.x; b < nblk; b += 256) s = __fadd_rn(s, part[b]);
+  const float tot = block_sum_fixed(s, red);
+  if (threadIdx.x == 0) out[0] = tot;
+}
+
+}  // namespace
+}  // namespace hgin
+
+using namespace hgin;
+
+extern "C" int hgin_prelu_bwd_workspace_size(int64_t M, int64_t N, size_t* bytes) {
+  HGIN_ARG_CHECK(bytes && M >= 0 && N >= 0, "hgin_prelu_bwd_workspace_size: bad args");
+  const int64_t nblk = ceil_div(M > 0 ? M : 1, kRowsPerBlock);
+  *bytes = align_up(sizeof(float) * (size_t)(nblk * N), 256) + align_up(sizeof(float) * (size_t)nblk, 256);
+  return HGIN_OK;
+}
+
+extern "C" int hgin_prelu_bwd_f32(const float* g_y, const float* z, int64_t M, int64_t N, const float* prelu,
+                                  float* g_z, float* g_prelu, float* g_bias, void* workspace, size_t workspace_bytes,
+                                  void* stream) {
+  HGIN_ARG_CHECK(M >= 0 && N >= 0 && N < (1 << 24), "hgin_prelu_bwd_f32: bad sizes");
+  HGIN_ARG_CHECK(g_prelu && g_bias && prelu, "hgin_prelu_bwd_f32: NULL output");
+  size_t need = 0;
+  hgin_prelu_bwd_workspace_size(M, N, &need);
+  if (workspace_bytes < need || !workspace) {
+    set_error("hgin_prelu_bwd_f32: workspace %zu < %zu", workspace_bytes, need);
+    return HGIN_E_WORKSPACE;
+  }
+  hipStream_t s = as_stream(stream);
+  if (M == 0 || N == 0) {
+    int rc = N ? memset_async(g_bias, 0, sizeof(float) * (size_t)N, s, "hgin_prelu_bwd_f32") : HGIN_OK;
+    if (rc == HGIN_OK) rc = memset_async(g_prelu, 0, sizeof(float), s, "hgin_prelu_bwd_f32");
+    return rc;
+  }
+  HGIN_ARG_CHECK(g_y && z && g_z, "hgin_prelu_bwd_f32: NULL operand");
+  const int64_t nblk = ceil_div(M, kRowsPerBlock);
+  float* part_col = static_cast<float*>(workspace);
+  float* part_s = reinterpret_cast<float*>(static_cast<char*>(workspace) +
+                                           align_up(sizeof(float) * (size_t)(nblk * N), 256));
+  k_rows_bwd<0><<<(unsigned)nblk, 256, 0, s>>>(g_y, N, z, N, M, (int)N, prelu, g_z, N, part_col, part_s);
+  k_final_cols<<<(unsigned)ceil_div(N, 256), 256, 0, s>>>(part_col, nblk, (int)N, g_bias);
+  k_final_scalar<<<1, 256, 0, s>>>(part_s, nblk, g_prelu);
+  return check_launch("hgin_prelu_bwd_f32");
+}
+
+extern "C" int hgin_combine_bwd_workspace_size(int64_t n_rows, size_t* bytes) {
+  HGIN_ARG_CHECK(bytes && n_rows >= 0, "hgin_combine_bwd_workspace_size: bad args");
+  *bytes = align_up(sizeof(float) * (size_t)ceil_div(n_rows > 0 ? n_rows : 1, kRowsPerBlock), 256);
+  return HGIN_OK;
+}
+
+extern "C" int hgin_combine_bwd_f32(const float* g, int64_t ld_g, const float* x_dst, int64_t ld_dst, int64_t n_rows,
+                                    int64_t f_dst, const float* eps, float* g_x_dst, int64_t ld_gx, float* g_eps,
+                                    void* workspace, size_t workspace_bytes, void* stream) {
+  HGIN_ARG_CHECK(n_rows >= 0 && f_dst >= 0 && f_dst < (1 << 24), "hgin_combine_bwd_f32: bad sizes");
+  HGIN_ARG_CHECK(eps && g_eps, "hgin_combine_bwd_f32: NULL eps/g_eps");
+  size_t need = 0;
+  hgin_combine_bwd_workspace_size(n_rows, &need);
+  if (workspace_bytes < need || !workspace) {
+    set_error("hgin_combine_bwd_f32: workspace %zu < %zu", workspace_bytes, need);
+    return HGIN_E_WORKSPACE;
+  }
+  hipStream_t s = as_stream(stream);
+  if (n_rows == 0 || f_dst == 0) {
+    return memset_async(g_eps, 0, sizeof(float), s, "hgin_combine_bwd_f32");
+  }
+  HGIN_ARG_CHECK(g && x_dst, "hgin_combine_bwd_f32: NULL operand");
+  const int64_t nblk = ceil_div(n_rows, kRowsPerBlock);
+  float* part_s = static_cast<float*>(workspace);
+  k_rows_bwd<1><<<(unsigned)nblk, 256, 0, s>>>(g, ld_g, x_dst, ld_dst, n_rows, (int)f_dst, eps, g_x_dst, ld_gx,
+                                               nullptr, part_s);
+  k_final_scalar<<<1, 256, 0, s>>>(part_s, nblk, g_eps);
+  return check_launch("hgin_combine_bwd_f32");
+}

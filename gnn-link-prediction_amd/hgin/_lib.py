@@ -1,0 +1,142 @@
+"""Build + ctypes binding of libhgin.so (the C ABI in include/hgin.h).
+
+The library is compiled in-tree for gfx950 with hipcc (``build()``), so the shared object travels with the
+repository snapshot to the GPU box.  Loading order matters: ``torch`` is imported first so that its bundled
+HIP runtime (SONAME ``libamdhip64.so.7``) is the one libhgin.so binds to — one HIP runtime per process,
+hence torch's device pointers and streams are valid in our kernels.
+
+There is no fallback: if the library cannot be built or loaded, every op raises ``HginUnavailable``.
+"""
+from __future__ import annotations
+
+import ctypes
+import glob
+import os
+import shutil
+import subprocess
+import tempfile
+import threading
+
+import torch  # noqa: F401  (must be loaded before libhgin.so; see module docstring)
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(PKG_DIR)                      # gnn-link-prediction_amd/
+REPO = os.path.dirname(ROOT)
+CSRC = os.path.join(ROOT, "csrc")
+INCLUDE = os.path.join(REPO, "include")
+BUILD_DIR = os.path.join(PKG_DIR, "_build")
+LIB_PATH = os.path.join(BUILD_DIR, "libhgin.so")
+ARCH = os.environ.get("HGIN_OFFLOAD_ARCH", "gfx950")
+HIPCC_FLAGS = ["-O3", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off", f"--offload-arch={ARCH}"]
+
+_lock = threading.Lock()
+_lib = None
+
+
+class HginUnavailable(RuntimeError):
+    """libhgin.so (the HIP hot path) could not be built or loaded; there is no CPU fallback."""
+
+
+class HginError(RuntimeError):
+    """A libhgin.so entry point returned a non-zero status."""
+
+
+def sources():
+    return sorted(glob.glob(os.path.join(CSRC, "*.hip")))
+
+
+def _deps():
+    return sources() + sorted(glob.glob(os.path.join(CSRC, "*.h"))) + [os.path.join(INCLUDE, "hgin.h")]
+
+
+def _hipcc() -> str:
+    for cand in (os.environ.get("HIPCC"), shutil.which("hipcc"), "/opt/rocm/bin/hipcc"):
+        if cand and os.path.exists(cand):
+            return cand
+    raise HginUnavailable("hipcc not found (set HIPCC)")
+
+
+def is_stale() -> bool:
+    if not os.path.exists(LIB_PATH):
+        return True
+    t = os.path.getmtime(LIB_PATH)
+    return any(os.path.getmtime(p) > t for p in _deps())
+
+
+def build(force: bool = False, verbose: bool = False) -> str:
+    """Compile every HIP source into libhgin.so for gfx950 (atomic replace).  Returns the path."""
+    if not force and not is_stale():
+        return LIB_PATH
+    os.makedirs(BUILD_DIR, exist_ok=True)
+    fd, tmp = tempfile.mkstemp(prefix=".libhgin.", suffix=".so", dir=BUILD_DIR)
+    os.close(fd)
+    cmd = [_hipcc()] + HIPCC_FLAGS + ["-I", INCLUDE, "-o", tmp] + sources()
+    if verbose:
+        print(" ".join(cmd))
+    try:
+        res = subprocess.run(cmd, capture_output=True, text=True)
+        if res.returncode != 0:
+            raise HginUnavailable(f"hipcc failed ({res.returncode}):\n{res.stderr[-4000:]}")
+        os.replace(tmp, LIB_PATH)
+    finally:
+        if os.path.exists(tmp):
+            os.unlink(tmp)
+    return LIB_PATH
+
+
+_I64, _I32, _U64, _SZ = ctypes.c_int64, ctypes.c_int, ctypes.c_uint64, ctypes.c_size_t
+_P = ctypes.c_void_p
+_SIGS = {
+    "hgin_abi_version": ([], _I32),
+    "hgin_last_error": ([], ctypes.c_char_p),
+    "hgin_csr_workspace_size": ([_I64, _I64, ctypes.POINTER(_SZ)], _I32),
+    "hgin_csr_build": ([_P, _I64, _I32, _I64, _I64, _P, _P, _P, _P, _P, _SZ, _P], _I32),
+    "hgin_aggregate_f32": ([_P, _P, _I64, _P, _I64, _I64, _P, _I64, _I64, _P, _I32, _P, _I64, _P], _I32),
+    "hgin_combine_bwd_workspace_size": ([_I64, ctypes.POINTER(_SZ)], _I32),
+    "hgin_combine_bwd_f32": ([_P, _I64, _P, _I64, _I64, _I64, _P, _P, _I64, _P, _P, _SZ, _P], _I32),
+    "hgin_gin_mlp_fwd_f32": ([_P, _I64, _P, _P, _P, _P, _P, _P, _I64, _I64, _I64, _P], _I32),
+    "hgin_prelu_bwd_workspace_size": ([_I64, _I64, ctypes.POINTER(_SZ)], _I32),
+    "hgin_prelu_bwd_f32": ([_P, _P, _I64, _I64, _P, _P, _P, _P, _P, _SZ, _P], _I32),
+    "hgin_gemm_nt_f32": ([_P, _I64, _P, _I64, _P, _I64, _I64, _I64, _I64, _P], _I32),
+    "hgin_neg_sample": ([_U64, _U64, _I64, _I64, _P, _P], _I32),
+    "hgin_dot_decode_fwd_f32": ([_P, _P, _I64, _P, _I64, _P, _I64, _I64, _P, _P], _I32),
+    "hgin_dot_decode_bwd_f32": ([_P, _P, _P, _I64, _P, _P, _I64, _I64, _P, _I64, _P], _I32),
+}
+ABI_VERSION = 1
+
+
+def lib() -> ctypes.CDLL:
+    """The loaded libhgin.so (built on first use if missing or stale)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        try:
+            path = build()
+            handle = ctypes.CDLL(path, mode=ctypes.RTLD_LOCAL)
+        except (OSError, HginUnavailable) as e:
+            raise HginUnavailable(f"libhgin.so unavailable: {e}") from e
+        for name, (args, res) in _SIGS.items():
+            fn = getattr(handle, name)
+            fn.argtypes = args
+            fn.restype = res
+        if handle.hgin_abi_version() != ABI_VERSION:
+            raise HginUnavailable("libhgin.so ABI version mismatch")
+        _lib = handle
+        return _lib
+
+
+def check(rc: int, what: str) -> None:
+    if rc != 0:
+        msg = lib().hgin_last_error().decode(errors="replace")
+        raise HginError(f"{what} failed with status {rc}: {msg}")
+
+
+def call(name: str, *args) -> None:
+    check(getattr(lib(), name)(*args), name)
+
+
+def exported_symbols():
+    return list(_SIGS.keys())

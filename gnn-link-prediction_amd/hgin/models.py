@@ -1,0 +1,172 @@
+"""HetroGIN — drop-in for the reference's ``models.py:248-376`` on the MI355X HIP path.
+
+Constructor keywords, the (mutated) ``input_channels`` dict, parameter initialisation order (and therefore
+the values under a given ``torch.manual_seed``), ``state_dict`` keys and ``forward(x_dict,
+edge_index_dict, path_batch) -> Tensor[N_path, 1]`` are those of the reference, so ``train.py``'s
+``load_model`` (``train.py:116-137``), the training loop (``train.py:16-67``) and ``load_state_dict`` of a
+reference checkpoint (``train.py:327``) work unchanged.  Message passing runs on libhgin.so; the readout
+MLP and the optional global pooling are small dense torch ops on the device.
+
+``HetroGAT`` (``models.py:380-506``) is out of scope (the north star names GIN only) and
+raises on construction.
+"""
+from __future__ import annotations
+
+from typing import List
+
+import torch
+
+from .conv import GINLayer, HeteroConv
+
+_ACTS = {"torch.nn.PReLU()": torch.nn.PReLU, "torch.nn.ReLU()": torch.nn.ReLU, "torch.nn.ELU()": torch.nn.ELU,
+         "torch.nn.LeakyReLU()": torch.nn.LeakyReLU, "torch.nn.Tanh()": torch.nn.Tanh,
+         "torch.nn.Sigmoid()": torch.nn.Sigmoid, "torch.nn.GELU()": torch.nn.GELU,
+         "torch.nn.SiLU()": torch.nn.SiLU, "torch.nn.Identity()": torch.nn.Identity}
+
+
+def make_activation(spec):
+    """The reference ``eval``s the activation string (models.py:301, :328-330); here a whitelist."""
+    if isinstance(spec, torch.nn.Module):
+        return spec
+    try:
+        return _ACTS[spec]()
+    except KeyError:
+        raise ValueError(f"unsupported activation {spec!r}; expected one of {sorted(_ACTS)}") from None
+
+
+def _global_pool(x: torch.Tensor, batch: torch.Tensor, reduce: str) -> torch.Tensor:
+    size = int(batch.max().item()) + 1 if batch.numel() else 0
+    idx = batch.view(-1, 1).expand_as(x)
+    return torch.zeros(size, x.size(1), dtype=x.dtype, device=x.device).scatter_reduce(
+        0, idx, x, reduce=reduce, include_self=False)
+
+
+class HetroGIN(torch.nn.Module):
+    def __init__(self, input_channels: dict, node_embedding_size: int, message_passing_layers: int, dropout: float,
+                 concat_path: bool, bl_features: bool, divided_features: bool, global_feats: bool,
+                 mlp_layers: list, act, mlp_head_act, mlp_bn: bool):
+        super().__init__()
+        self.num_layers = message_passing_layers
+        self.concat_path = concat_path
+        self.bl_features = bl_features
+        self.divided_features = divided_features
+        self.mlp_layers = mlp_layers
+        self.dropout = dropout
+        self.global_feats = global_feats
+
+        # models.py:260-269 (mutates the caller's dict, as the reference does)
+        if not self.divided_features:
+            input_channels["path"] = input_channels["path"] - 3
+            input_channels["link"] = input_channels["link"] - 1
+            if not self.bl_features:
+                input_channels["path"] = input_channels["path"] - 1
+                input_channels["link"] = input_channels["link"] - 3
+        else:
+            if not self.bl_features:
+                input_channels["path"] = input_channels["path"] - 1
+                input_channels["link"] = input_channels["link"] - 3
+
+        self.global_feats_size = 8 if global_feats else 0
+        self.concat_size = input_channels["path"] if concat_path else 0
+
+        self.convs = torch.nn.ModuleList()
+        self.readout = torch.nn.ModuleList()
+        ic, H = input_channels, node_embedding_size
+        # models.py:286-290 first conv layer (concat self term)
+        self.convs.append(HeteroConv({
+            ("path", "uses", "link"): GINLayer(ic["path"] + ic["link"], H, concat=True),
+            ("link", "includes", "path"): GINLayer(ic["link"] + ic["path"], H, concat=True),
+            ("link", "connects", "node"): GINLayer(ic["link"] + ic["node"], H, concat=True),
+            ("node", "has", "link"): GINLayer(ic["node"] + ic["link"], H, concat=True)}, aggr="sum"))
+        # models.py:293-298 remaining conv layers (add self term)
+        for _ in range(self.num_layers - 1):
+            self.convs.append(HeteroConv({
+                ("path", "uses", "link"): GINLayer(H, H),
+                ("link", "includes", "path"): GINLayer(H, H),
+                ("link", "connects", "node"): GINLayer(H, H),
+                ("node", "has", "link"): GINLayer(H, H)}, aggr="sum"))
+
+        # models.py:301-330 readout (ONE activation instance shared by the hidden readout layers)
+        act = make_activation(act)
+        width0 = H + self.concat_size + self.global_feats_size
+        for i in range(len(mlp_layers)):
+            lin = torch.nn.Linear(width0 if i == 0 else mlp_layers[i - 1], mlp_layers[i])
+            if mlp_bn:
+                self.readout.append(torch.nn.Sequential(lin, torch.nn.BatchNorm1d(num_features=mlp_layers[i]), act))
+            else:
+                self.readout.append(torch.nn.Sequential(lin, act))
+        if mlp_head_act is None:
+            self.readout.append(torch.nn.Sequential(torch.nn.Linear(mlp_layers[-1], 1)))
+        else:
+            self.readout.append(torch.nn.Sequential(torch.nn.Linear(mlp_layers[-1], 1),
+                                                    make_activation(mlp_head_act)))
+
+    def prune_dead(self, enable: bool = True) -> List[str]:
+        """Skip relations whose outputs cannot reach the readout.  Off by default: the
+        reference computes every relation in every layer; pruned runs are reported separately."""
+        dead: List[str] = []
+        live_types = {"path"}
+        for li in range(self.num_layers - 1, -1, -1):
+            conv = self.convs[li]
+            conv.skip = set()
+            needed = set()
+            for key in conv.convs.keys():
+                src, _, dst = key.split("__")
+                if dst in live_types:
+                    needed.add(src)
+                    needed.add(dst)
+                elif enable:
+                    conv.skip.add(key)
+                    dead.append(f"{li}:{key}")
+            live_types = needed
+        return dead
+
+    def forward(self, x_dict, edge_index_dict, path_batch):
+        # models.py:333-342 feature slicing (assigns into the caller's dict, as the reference does)
+        if not self.divided_features:
+            x_dict["path"] = torch.cat([x_dict["path"][:, 0:3], x_dict["path"][:, 6].reshape(-1, 1)], axis=1)
+            x_dict["link"] = torch.cat([x_dict["link"][:, 0:3], x_dict["link"][:, 4:7]], axis=1)
+            if not self.bl_features:
+                x_dict["path"] = x_dict["path"][:, 0:3]
+                x_dict["link"] = x_dict["link"][:, 0:3]
+        else:
+            if not self.bl_features:
+                x_dict["path"] = x_dict["path"][:, 0:6]
+                x_dict["link"] = x_dict["link"][:, 0:3]
+
+        origin_input = x_dict.copy()
+
+        if self.global_feats:   # models.py:347-352
+            mean_f = _global_pool(origin_input["path"], path_batch, "mean")
+            max_f = _global_pool(origin_input["path"], path_batch, "amax")
+            mean_f = torch.gather(mean_f, 0, path_batch.unsqueeze(1).repeat(1, mean_f.shape[1]))
+            max_f = torch.gather(max_f, 0, path_batch.unsqueeze(1).repeat(1, max_f.shape[1]))
+
+        for i in range(self.num_layers):   # models.py:355-359
+            x_dict = self.convs[i](x_dict, edge_index_dict)
+            if self.dropout > 0.0 and self.training:
+                for k in list(x_dict.keys()):
+                    x_dict[k] = torch.nn.functional.dropout(x_dict[k], p=self.dropout, training=True)
+
+        if self.concat_path:   # models.py:362-371
+            if self.global_feats:
+                x = torch.cat((x_dict["path"], origin_input["path"], mean_f, max_f), 1)
+            else:
+                x = torch.cat((x_dict["path"], origin_input["path"]), 1)
+        else:
+            if self.global_feats:
+                x = torch.cat((x_dict["path"], mean_f, max_f), 1)
+            else:
+                x = x_dict["path"]
+
+        for i in range(len(self.mlp_layers) + 1):   # models.py:373-374
+            x = self.readout[i](x)
+        return x
+
+
+class HetroGAT(torch.nn.Module):
+    """models.py:380-506 — out of scope for the MI355X hot path."""
+
+    def __init__(self, *args, **kwargs):
+        super().__init__()
+        raise NotImplementedError("HetroGAT is not part of the MI355X hot path (SURVEY.md §2 / §8)")

@@ -1,0 +1,338 @@
+"""Autograd ops over libhgin.so (device tensors only — there is no CPU fallback).
+
+Reference call path being replaced:
+  GINConv.forward (models.py:201-217) -> MessagePassing.propagate (models.py:208: index_select +
+  torch_scatter.scatter sum) -> cat / add of (1 + eps) * x_r (models.py:210-215) -> self.nn(out) =
+  Linear + PReLU (models.py:236-239) ; HeteroConv's stack().sum(0) over relations into one node type.
+
+Ops:
+  * ``relation_graph(edge_index, n_src, n_dst)`` — validated stable CSR (by dst) + lazily a CSC (by src),
+    cached on the edge_index tensor (invalidated by in-place edits through ``_version``).
+  * ``aggregate(...)``      — A3/A4 fused aggregate + self term; autograd (backward: CSC aggregate +
+                              deterministic combine backward).
+  * ``gin_conv(...)``       — A3-A5 fused for the GINLayer case nn = Sequential(Linear, PReLU): aggregate
+                              + combine -> MFMA GEMM with bias / PReLU / relation-sum epilogue; backward
+                              PReLU+bias (deterministic), dW / dX GEMMs, CSC aggregate, eps grad.
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass
+from typing import Optional
+
+import torch
+from torch import Tensor
+
+from . import _lib, profiling
+
+COMBINE_NONE, COMBINE_ADD, COMBINE_CONCAT = 0, 1, 2
+STATUS_ROW_OOR, STATUS_COL_OOR = 1, 2
+
+
+def _p(t: Optional[Tensor]):
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+def _stream(t: Tensor):
+    return ctypes.c_void_p(torch.cuda.current_stream(t.device).cuda_stream)
+
+
+def require_device(*tensors, what: str = "hgin") -> None:
+    for t in tensors:
+        if t is not None and not t.is_cuda:
+            raise RuntimeError(f"{what}: expected HIP device tensors; the MI355X path has no CPU fallback "
+                               f"(got a tensor on {t.device})")
+
+
+def _f32(t: Tensor, what: str) -> Tensor:
+    if t.dtype != torch.float32:
+        raise TypeError(f"{what}: expected float32, got {t.dtype}")
+    return t
+
+
+def _workspace(nbytes: int, device) -> Tensor:
+    return torch.empty(max(int(nbytes), 1), dtype=torch.uint8, device=device)
+
+
+# ---------------------------------------------------------------------------------------------------
+# A12: CSR / CSC
+# ---------------------------------------------------------------------------------------------------
+@dataclass
+class Csr:
+    rowptr: Tensor   # int32 [n_rows + 1]
+    col: Tensor      # int32 [E]   other endpoint, in stable sorted order
+    perm: Tensor     # int32 [E]   original edge id of each sorted position
+    n_rows: int
+    n_cols: int
+
+    @property
+    def n_edges(self) -> int:
+        return int(self.col.numel())
+
+
+def build_csr(edge_index: Tensor, key_row: int, n_rows: int, n_cols: int, validate: bool = True) -> Csr:
+    """Stable COO->CSR of a [2, E] int64 edge_index on the device (key_row 1: by dst, 0: by src)."""
+    require_device(edge_index, what="build_csr")
+    check_edge_index(edge_index)
+    ei = edge_index.contiguous()
+    E = int(ei.size(1))
+    dev = ei.device
+    rowptr = torch.empty(n_rows + 1, dtype=torch.int32, device=dev)
+    col = torch.empty(E, dtype=torch.int32, device=dev)
+    perm = torch.empty(E, dtype=torch.int32, device=dev)
+    status = torch.zeros(1, dtype=torch.int32, device=dev)
+    nbytes = ctypes.c_size_t(0)
+    _lib.check(_lib.lib().hgin_csr_workspace_size(E, n_rows, ctypes.byref(nbytes)), "hgin_csr_workspace_size")
+    ws = _workspace(nbytes.value, dev)
+    _lib.call("hgin_csr_build", _p(ei), E, key_row, n_rows, n_cols, _p(rowptr), _p(col), _p(perm), _p(status),
+              _p(ws), nbytes.value, _stream(ei))
+    if validate:
+        st = int(status.item())
+        if st:
+            which = []
+            if st & STATUS_ROW_OOR:
+                which.append(f"{'dst' if key_row == 1 else 'src'} index out of range [0, {n_rows})")
+            if st & STATUS_COL_OOR:
+                which.append(f"{'src' if key_row == 1 else 'dst'} index out of range [0, {n_cols})")
+            raise IndexError("edge_index: " + "; ".join(which))
+    return Csr(rowptr, col, perm, n_rows, n_cols)
+
+
+def check_edge_index(edge_index: Tensor) -> None:
+    """PyG 2.0.x MessagePassing.__check_input__ for Tensor adjacency (AssertionError on violation)."""
+    assert edge_index.dtype == torch.long, "edge_index must be torch.long"
+    assert edge_index.dim() == 2, "edge_index must be 2-dimensional"
+    assert edge_index.size(0) == 2, "edge_index must have shape [2, num_edges]"
+
+
+class RelationGraph:
+    """CSR (by dst) for the forward aggregate + CSC (by src) for the backward, built once per edge_index."""
+
+    def __init__(self, edge_index: Tensor, n_src: int, n_dst: int):
+        self.edge_index = edge_index
+        self.n_src = int(n_src)
+        self.n_dst = int(n_dst)
+        self._csr: Optional[Csr] = None
+        self._csc: Optional[Csr] = None
+
+    @property
+    def n_edges(self) -> int:
+        return int(self.edge_index.size(1))
+
+    @property
+    def csr(self) -> Csr:
+        if self._csr is None:
+            self._csr = build_csr(self.edge_index, 1, self.n_dst, self.n_src)
+        return self._csr
+
+    @property
+    def csc(self) -> Csr:
+        if self._csc is None:
+            # the CSR build already validated both endpoint ranges
+            self._csc = build_csr(self.edge_index, 0, self.n_src, self.n_dst, validate=self._csr is None)
+        return self._csc
+
+
+def relation_graph(edge_index: Tensor, n_src: int, n_dst: int) -> RelationGraph:
+    """Cached RelationGraph for this edge_index tensor (cache lives on the tensor, keyed by sizes)."""
+    key = (int(n_src), int(n_dst))
+    cache = getattr(edge_index, "_hgin_graphs", None)
+    ver = edge_index._version
+    if cache is None or cache[0] != ver:
+        cache = (ver, {})
+        try:
+            edge_index._hgin_graphs = cache
+        except (AttributeError, RuntimeError):
+            return RelationGraph(edge_index, n_src, n_dst)
+    g = cache[1].get(key)
+    if g is None:
+        g = RelationGraph(edge_index, n_src, n_dst)
+        g.csr  # build + validate eagerly (errors surface at the call site, like PyG's)
+        cache[1][key] = g
+    return g
+
+
+# ---------------------------------------------------------------------------------------------------
+# raw launches
+# ---------------------------------------------------------------------------------------------------
+def aggregate_into(csr: Csr, x_src: Tensor, x_dst: Optional[Tensor], eps: Optional[Tensor], mode: int,
+                   out: Tensor) -> Tensor:
+    f_src = int(x_src.size(1))
+    f_dst = int(x_dst.size(1)) if x_dst is not None else 0
+
+    def launch():
+        _lib.call("hgin_aggregate_f32", _p(csr.rowptr), _p(csr.col), csr.n_rows, _p(x_src), x_src.stride(0),
+                  f_src, _p(x_dst), x_dst.stride(0) if x_dst is not None else 0, f_dst, _p(eps), mode, _p(out),
+                  out.stride(0), _stream(out))
+
+    probe = profiling.active()
+    if probe is None:
+        launch()
+    else:
+        probe.around("aggregate", profiling.aggregate_bytes(csr.n_edges, csr.n_rows, f_src, f_dst, mode), launch)
+    return out
+
+
+def _rowmajor(t: Tensor) -> Tensor:
+    return t if (t.dim() == 2 and t.stride(1) == 1) else t.contiguous()
+
+
+def prelu_bwd(g_y: Tensor, z: Tensor, prelu: Tensor):
+    M, N = z.shape
+    g_z = torch.empty_like(z)
+    g_a = torch.empty(1, dtype=torch.float32, device=z.device)
+    g_b = torch.empty(N, dtype=torch.float32, device=z.device)
+    nbytes = ctypes.c_size_t(0)
+    _lib.check(_lib.lib().hgin_prelu_bwd_workspace_size(M, N, ctypes.byref(nbytes)), "prelu_bwd_workspace_size")
+    ws = _workspace(nbytes.value, z.device)
+    _lib.call("hgin_prelu_bwd_f32", _p(g_y), _p(z), M, N, _p(prelu), _p(g_z), _p(g_a), _p(g_b), _p(ws),
+              nbytes.value, _stream(z))
+    return g_z, g_a, g_b
+
+
+def combine_bwd(g: Tensor, x_dst: Tensor, eps: Tensor, want_gx: bool):
+    n, f = x_dst.shape
+    gx = torch.empty_like(x_dst) if want_gx else None
+    g_eps = torch.empty(1, dtype=torch.float32, device=x_dst.device)
+    nbytes = ctypes.c_size_t(0)
+    _lib.check(_lib.lib().hgin_combine_bwd_workspace_size(n, ctypes.byref(nbytes)), "combine_bwd_workspace_size")
+    ws = _workspace(nbytes.value, x_dst.device)
+    _lib.call("hgin_combine_bwd_f32", _p(g), g.stride(0), _p(x_dst), x_dst.stride(0), n, f, _p(eps), _p(gx),
+              gx.stride(0) if gx is not None else 0, _p(g_eps), _p(ws), nbytes.value, _stream(x_dst))
+    return gx, g_eps
+
+
+def gemm_nt(a: Tensor, b: Tensor) -> Tensor:
+    """c = a @ b^T on the f32 matrix cores (a [M,K], b [N,K], both K-contiguous)."""
+    a, b = _rowmajor(a), _rowmajor(b)
+    M, K = a.shape
+    N = b.shape[0]
+    c = torch.empty(M, N, dtype=torch.float32, device=a.device)
+    _lib.call("hgin_gemm_nt_f32", _p(a), a.stride(0), _p(b), b.stride(0), _p(c), c.stride(0), M, N, K, _stream(a))
+    return c
+
+
+def gin_mlp_fwd(comb: Tensor, weight: Tensor, bias: Tensor, prelu: Tensor, accum: Optional[Tensor],
+                save_z: bool = True):
+    M, K = comb.shape
+    N = weight.shape[0]
+    z = torch.empty(M, N, dtype=torch.float32, device=comb.device) if save_z else None
+    y = torch.empty(M, N, dtype=torch.float32, device=comb.device)
+
+    def launch():
+        _lib.call("hgin_gin_mlp_fwd_f32", _p(comb), comb.stride(0), _p(weight), _p(bias), _p(prelu), _p(accum),
+                  _p(z), _p(y), M, N, K, _stream(comb))
+
+    probe = profiling.active()
+    if probe is None:
+        launch()
+    else:
+        probe.around("gin_mlp", 2.0 * M * N * K, launch)
+    return z, y
+
+
+# ---------------------------------------------------------------------------------------------------
+# autograd
+# ---------------------------------------------------------------------------------------------------
+def _backward_aggregate(graph: RelationGraph, g_agg: Tensor) -> Tensor:
+    """d x_src = index_add over the reversed relation = the A3 kernel on the CSC (edge order kept)."""
+    csc = graph.csc
+    g = torch.empty(graph.n_src, g_agg.size(1), dtype=torch.float32, device=g_agg.device)
+    return aggregate_into(csc, g_agg, None, None, COMBINE_NONE, g)
+
+
+class _AggregateFn(torch.autograd.Function):
+    """propagate + self term (generic path: any nn applied by the caller)."""
+
+    @staticmethod
+    def forward(ctx, x_src, x_dst, eps, graph: RelationGraph, mode: int):
+        f_src = x_src.size(1)
+        width = f_src + (x_dst.size(1) if mode == COMBINE_CONCAT else 0)
+        out = torch.empty(graph.n_dst, width, dtype=torch.float32, device=x_src.device)
+        aggregate_into(graph.csr, x_src, x_dst, eps, mode, out)
+        ctx.graph, ctx.mode, ctx.f_src = graph, mode, f_src
+        ctx.save_for_backward(x_dst, eps)
+        return out
+
+    @staticmethod
+    def backward(ctx, g_out):
+        x_dst, eps = ctx.saved_tensors
+        g_out = _rowmajor(g_out)
+        need_src, need_dst, need_eps = ctx.needs_input_grad[:3]
+        g_src = g_dst = g_eps = None
+        if need_src:
+            g_src = _backward_aggregate(ctx.graph, g_out[:, :ctx.f_src])
+        if ctx.mode != COMBINE_NONE and (need_dst or need_eps):
+            gs = g_out[:, ctx.f_src:] if ctx.mode == COMBINE_CONCAT else g_out
+            g_dst, g_eps = combine_bwd(gs, x_dst, eps, need_dst)
+        return g_src, g_dst, (g_eps.view_as(eps) if need_eps and g_eps is not None else None), None, None
+
+
+class _GINConvFn(torch.autograd.Function):
+    """Fused GINConv + GINLayer MLP: y = prelu(comb @ W^T + b) [+ accum], comb = aggregate + self term."""
+
+    @staticmethod
+    def forward(ctx, x_src, x_dst, eps, weight, bias, prelu, accum, graph: RelationGraph, mode: int):
+        f_src = x_src.size(1)
+        width = f_src + (x_dst.size(1) if mode == COMBINE_CONCAT else 0)
+        comb = torch.empty(graph.n_dst, width, dtype=torch.float32, device=x_src.device)
+        aggregate_into(graph.csr, x_src, x_dst, eps, mode, comb)
+        z, y = gin_mlp_fwd(comb, weight, bias, prelu, accum)
+        ctx.graph, ctx.mode, ctx.f_src = graph, mode, f_src
+        ctx.save_for_backward(x_dst, eps, weight, prelu, comb, z)
+        return y
+
+    @staticmethod
+    def backward(ctx, g_y):
+        x_dst, eps, weight, prelu, comb, z = ctx.saved_tensors
+        need = ctx.needs_input_grad
+        need_src, need_dst, need_eps, need_w, need_b, need_a, need_acc = need[:7]
+        g_y = _rowmajor(g_y)
+        g_z, g_a, g_b = prelu_bwd(g_y, z, prelu)
+        g_w = torch.mm(g_z.t(), comb) if need_w else None
+        g_src = g_dst = g_eps = None
+        f_src, mode = ctx.f_src, ctx.mode
+        if need_src or need_dst:
+            g_comb = torch.mm(g_z, weight)                      # [N_dst, K]
+            if need_src:
+                g_src = _backward_aggregate(ctx.graph, g_comb[:, :f_src])
+            if mode != COMBINE_NONE:
+                gs = g_comb[:, f_src:] if mode == COMBINE_CONCAT else g_comb
+                g_dst, g_eps = combine_bwd(gs, x_dst, eps, need_dst)
+        elif need_eps and mode != COMBINE_NONE:
+            # Only parameters need gradients (e.g. the first layer, whose inputs are data):
+            # sum(g_comb[:, self] * x_dst) = sum(W_self * (g_z^T x_dst))  — skips the [N_dst, K] dX GEMM.
+            w_self = weight[:, f_src:] if mode == COMBINE_CONCAT else weight
+            g_eps = (w_self * torch.mm(g_z.t(), x_dst)).sum().reshape(1)
+        g_acc = g_y if need_acc else None
+        return (g_src, g_dst, (g_eps.view_as(eps) if (need_eps and g_eps is not None) else None), g_w,
+                g_b if need_b else None, (g_a.view_as(prelu) if need_a else None), g_acc, None, None)
+
+
+def aggregate(x_src: Tensor, x_dst: Optional[Tensor], eps: Optional[Tensor], graph: RelationGraph,
+              mode: int) -> Tensor:
+    require_device(x_src, x_dst, eps, what="hgin.aggregate")
+    x_src = _rowmajor(_f32(x_src, "x_src"))
+    if x_dst is not None:
+        x_dst = _rowmajor(_f32(x_dst, "x_dst"))
+    if mode == COMBINE_ADD and x_dst.size(1) != x_src.size(1):
+        raise RuntimeError(f"GINConv add: feature sizes differ ({x_src.size(1)} vs {x_dst.size(1)})")
+    if mode != COMBINE_NONE and x_dst.size(0) != graph.n_dst:
+        raise RuntimeError("x_dst rows != number of destination nodes")
+    return _AggregateFn.apply(x_src, x_dst, eps, graph, mode)
+
+
+def gin_conv(x_src: Tensor, x_dst: Tensor, eps: Tensor, weight: Tensor, bias: Tensor, prelu: Tensor,
+             graph: RelationGraph, mode: int, accum: Optional[Tensor] = None) -> Tensor:
+    require_device(x_src, x_dst, eps, weight, bias, prelu, accum, what="hgin.gin_conv")
+    x_src = _rowmajor(_f32(x_src, "x_src"))
+    x_dst = _rowmajor(_f32(x_dst, "x_dst"))
+    width = x_src.size(1) + (x_dst.size(1) if mode == COMBINE_CONCAT else 0)
+    if mode == COMBINE_ADD and x_dst.size(1) != x_src.size(1):
+        raise RuntimeError(f"GINConv add: feature sizes differ ({x_src.size(1)} vs {x_dst.size(1)})")
+    if weight.size(1) != width:
+        raise RuntimeError(f"mat1 and mat2 shapes cannot be multiplied ({graph.n_dst}x{width} and "
+                           f"{weight.size(1)}x{weight.size(0)})")
+    if accum is not None:
+        accum = _rowmajor(accum)
+    return _GINConvFn.apply(x_src, x_dst, eps, _rowmajor(weight), bias.contiguous(), prelu, accum, graph, mode)

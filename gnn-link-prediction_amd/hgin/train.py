@@ -1,0 +1,52 @@
+"""Training-step harness mirroring the reference's ``train.py`` (train.py:12-13, 16-67, 140-148).
+
+``train_step`` is one iteration of ``train_one_epoch``'s loop body: zero_grad, forward through the model
+(``model(x_dict, edge_index_dict, path_batch)``, train.py:34), ``label = y.reshape(-1, 1)``, MAPE loss,
+``sqrt``, backward, [gradient all-reduce across ranks], ``opt.step()``.  The reference additionally calls
+``mape(out, label).item()`` every step (train.py:50); ``sync_metric=True`` reproduces that host sync, the
+benchmark leaves it off.
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+
+from .dist import GradAllReducer
+
+
+def mape(preds: torch.Tensor, actuals: torch.Tensor) -> torch.Tensor:
+    """train.py:12-13."""
+    return 100.0 * torch.mean(torch.abs((preds - actuals) / actuals))
+
+
+LOSSES = {"mape": mape}
+
+
+def load_optimizer(config: dict, model: torch.nn.Module) -> torch.optim.Optimizer:
+    """train.py:140-148."""
+    kind = config.get("OPTIMIZER", "adam")
+    lr, wd = config.get("LEARNING_RATE", 1e-3), config.get("WEIGHT_DECAY", 0)
+    if kind == "adam":
+        return torch.optim.Adam(lr=lr, params=model.parameters(), weight_decay=wd)
+    if kind == "adamW":
+        return torch.optim.AdamW(lr=lr, params=model.parameters(), weight_decay=wd)
+    if kind == "sgd":
+        return torch.optim.SGD(lr=lr, params=model.parameters(), weight_decay=wd)
+    raise ValueError(f"unknown optimizer {kind!r}")
+
+
+def train_step(model, opt, graph, loss_func=mape, reducer: Optional[GradAllReducer] = None,
+               sync_metric: bool = False):
+    opt.zero_grad()
+    out = model(graph.x_dict(), graph.edge_index_dict(), graph.batch["path"])
+    label = graph.y.reshape(-1, 1)
+    loss_value = loss_func(out, label)
+    loss = torch.sqrt(loss_value)
+    loss.backward()
+    if reducer is not None:
+        reducer.sync()
+    opt.step()
+    if sync_metric:
+        return float(mape(out, label).item())
+    return loss_value.detach()

@@ -1,0 +1,141 @@
+/*
+ * hgin.h — C ABI of libhgin.so, the MI355X (gfx950) heterogeneous-GIN hot path.
+ *
+ * The reference (youssefshoeb/GNN-Link-Prediction) has no native code: its hot path is PyG
+ * `MessagePassing.propagate` + `torch_scatter.scatter` + `torch.nn.Linear`/`PReLU` reached from
+ * `models.py`.  Each entry point below names the reference interface it replaces (file:line in the
+ * reference tree).  The Python host (gnn-link-prediction_amd/hgin) binds this header with ctypes;
+ * INTEGRATION.md shows the binding.
+ *
+ * Conventions (all functions):
+ *   - plain C types; device pointers are `void*`/typed pointers into HBM owned and allocated by the
+ *     caller; kernels never allocate.  Scratch comes from a `*_workspace_size` query + caller buffer.
+ *   - every call is asynchronous on the caller's HIP stream, passed as `void* stream`
+ *     (a `hipStream_t`; NULL = the default stream).  Nothing here synchronises the device, so the calls
+ *     can be captured into a hipGraph.
+ *   - return value: 0 = ok, > 0 = a hipError_t from the launch, < 0 = argument error (HGIN_E_*).
+ *     `hgin_last_error()` returns a thread-local message for the last failing call.
+ *   - row-major matrices carry an explicit leading dimension (elements, not bytes).
+ *   - stateless and re-entrant; one host thread per GPU process.
+ */
+#ifndef HGIN_H_
+#define HGIN_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define HGIN_ABI_VERSION 1
+
+#define HGIN_OK 0
+#define HGIN_E_ARG (-1)        /* bad size / null pointer / unsupported combination */
+#define HGIN_E_ALIGN (-2)      /* pointer or leading dimension misaligned for the chosen path */
+#define HGIN_E_WORKSPACE (-3)  /* workspace too small */
+
+/* combine modes of the GIN self term, models.py:210-215 */
+#define HGIN_COMBINE_NONE 0    /* out = aggregate only (also: every backward aggregate)          */
+#define HGIN_COMBINE_ADD 1     /* out = aggregate + (1 + eps) * x_dst          (models.py:215)    */
+#define HGIN_COMBINE_CONCAT 2  /* out = [aggregate | (1 + eps) * x_dst]        (models.py:212-213) */
+
+/* status word bits written by hgin_csr_build into *d_status (device int32) */
+#define HGIN_STATUS_ROW_OOR 1  /* a row index (the sorted key) was < 0 or >= n_rows */
+#define HGIN_STATUS_COL_OOR 2  /* a column index was < 0 or >= n_cols               */
+
+int hgin_abi_version(void);
+const char* hgin_last_error(void);
+
+/* ---- A12: COO -> CSR / CSC (stable) ------------------------------------------------------------
+ * Replaces nothing in the reference directly: PyG scatters unsorted COO with atomics
+ * (torch_scatter.scatter <- MessagePassing.propagate <- models.py:208).  The stable sort keeps, inside
+ * every row, the original edge order, which is exactly the order CPU `scatter_add_` / `index_add_`
+ * accumulate in, so segmented sums over this CSR are bit-identical to the reference's CPU path.
+ *
+ * edge_index: int64 [2, n_edges] row-major (the PyG layout, dataset.py:112-117).
+ * key_row = 1: rows are destinations (CSR for the forward aggregate); key_row = 0: rows are sources
+ *              (CSC, for the backward of index_select).
+ * Outputs: rowptr int32 [n_rows + 1]; col int32 [n_edges] = the other endpoint, in sorted order;
+ *          perm int32 [n_edges] = original edge id of each sorted position (may be NULL).
+ * d_status: device int32, OR-ed with HGIN_STATUS_* on out-of-range indices (caller zeroes it).
+ * n_edges, n_rows, n_cols < 2^31. */
+int hgin_csr_workspace_size(int64_t n_edges, int64_t n_rows, size_t* bytes);
+int hgin_csr_build(const int64_t* edge_index, int64_t n_edges, int key_row, int64_t n_rows,
+                   int64_t n_cols, int32_t* rowptr, int32_t* col, int32_t* perm, int32_t* d_status,
+                   void* workspace, size_t workspace_bytes, void* stream);
+
+/* ---- A3 + A4: GINConv message + aggregate + (1+eps) combine -------------------------------------
+ * Replaces: MessagePassing.propagate (models.py:208: index_select gather + torch_scatter sum with
+ * aggr='add', models.py:186; identity message models.py:219-220) fused with the self term
+ * (models.py:210-215) — no [E, F] message tensor, no atomics, no separate cat / add kernel.
+ *   agg[r, f]  = sum_{k = rowptr[r]}^{rowptr[r+1]-1} x_src[col[k], f]   (sequential in k, fp32, no FMA)
+ *   NONE:   out[r, 0:f_src]              = agg
+ *   ADD:    out[r, f]                    = agg + ((1 + eps[0]) * x_dst[r, f])   (f_dst == f_src)
+ *   CONCAT: out[r, 0:f_src] = agg;  out[r, f_src:f_src+f_dst] = (1 + eps[0]) * x_dst[r, :]
+ * eps: device float[1] (the GINConv eps Parameter, models.py:191-194).  Rows with no edges get 0.
+ * Bit-exact against CPU scatter_add_ + cat / add on the same inputs. */
+int hgin_aggregate_f32(const int32_t* rowptr, const int32_t* col, int64_t n_rows,
+                       const float* x_src, int64_t ld_src, int64_t f_src,
+                       const float* x_dst, int64_t ld_dst, int64_t f_dst,
+                       const float* eps, int combine, float* out, int64_t ld_out, void* stream);
+
+/* ---- A9: backward of the combine -----------------------------------------------------------------
+ * Replaces the autograd of `(1 + eps) * x_r` + cat/add (models.py:212-215):
+ *   g_x_dst[r, f] = (1 + eps) * g[r, f]                 (written if g_x_dst != NULL)
+ *   g_eps[0]      = sum_{r, f} g[r, f] * x_dst[r, f]    (deterministic two-level reduction)
+ * g points at the self-term columns of the combine gradient (ld_g is its row stride).
+ * workspace: hgin_combine_bwd_workspace_size(n_rows) bytes. */
+int hgin_combine_bwd_workspace_size(int64_t n_rows, size_t* bytes);
+int hgin_combine_bwd_f32(const float* g, int64_t ld_g, const float* x_dst, int64_t ld_dst,
+                         int64_t n_rows, int64_t f_dst, const float* eps, float* g_x_dst,
+                         int64_t ld_gx, float* g_eps, void* workspace, size_t workspace_bytes,
+                         void* stream);
+
+/* ---- A5: GIN MLP update on MFMA ------------------------------------------------------------------
+ * Replaces GINLayer.mlp = Sequential(Linear(K, N), PReLU()) applied at models.py:217 (built at
+ * models.py:236-239) and, when `accum` != NULL, the per-dst-type sum of HeteroConv(aggr='sum')
+ * (models.py:286-298) for the second relation into the same node type:
+ *   z = a @ w^T + bias;  y = (z > 0 ? z : prelu[0] * z) [+ accum]
+ * a: [M, K] (lda), w: [N, K] row-major (torch Linear.weight), bias: [N], prelu: device float[1].
+ * z (pre-activation, saved for backward) may be NULL.  fp32 in, fp32 MFMA (v_mfma_f32_32x32x2_f32). */
+int hgin_gin_mlp_fwd_f32(const float* a, int64_t lda, const float* w, const float* bias,
+                         const float* prelu, const float* accum, float* z, float* y,
+                         int64_t M, int64_t N, int64_t K, void* stream);
+
+/* ---- A9: PReLU + bias backward -------------------------------------------------------------------
+ *   g_z = z > 0 ? g_y : prelu[0] * g_y;  g_prelu[0] = sum (z > 0 ? 0 : z * g_y);  g_bias[n] = sum_m g_z[m, n]
+ * Deterministic (fixed-shape two-level reductions).  workspace: hgin_prelu_bwd_workspace_size. */
+int hgin_prelu_bwd_workspace_size(int64_t M, int64_t N, size_t* bytes);
+int hgin_prelu_bwd_f32(const float* g_y, const float* z, int64_t M, int64_t N, const float* prelu,
+                       float* g_z, float* g_prelu, float* g_bias, void* workspace,
+                       size_t workspace_bytes, void* stream);
+
+/* ---- plain GEMM on MFMA (backward of Linear) --------------------------------------------------------
+ * c[M, N] = a[M, K] @ b[N, K]^T   ("NT", both operands K-contiguous), fp32 MFMA. */
+int hgin_gemm_nt_f32(const float* a, int64_t lda, const float* b, int64_t ldb, float* c, int64_t ldc,
+                     int64_t M, int64_t N, int64_t K, void* stream);
+
+/* ---- A10: negative-edge sampler (NOT IN REFERENCE; build-defined) --------------
+ * out[i] = hi32( philox4x32_10(counter = {lo32(offset+i), hi32(offset+i), 0, 0},
+ *                              key = {lo32(seed), hi32(seed)}).x  *  n_dst ),  i in [0, n)
+ * (Lemire multiply-shift range reduction).  int32 output. */
+int hgin_neg_sample(uint64_t seed, uint64_t offset, int64_t n, int64_t n_dst, int32_t* out,
+                    void* stream);
+
+/* ---- A11: dot-product link decoder (NOT IN REFERENCE; build-defined) ------------
+ * score[e] = sum_f z_src[src[e], f] * z_dst[dst[e], f]   (fp32)
+ * Backward: g_z_src[s] = sum_{e: src[e]=s} g[e] * z_dst[dst[e]] over a CSR of the pairs by src
+ * (rowptr/col/perm from hgin_csr_build with key_row = 0), and symmetrically for g_z_dst. */
+int hgin_dot_decode_fwd_f32(const int32_t* src, const int32_t* dst, int64_t n_pairs,
+                            const float* z_src, int64_t ld_src, const float* z_dst, int64_t ld_dst,
+                            int64_t F, float* score, void* stream);
+int hgin_dot_decode_bwd_f32(const int32_t* rowptr, const int32_t* col, const int32_t* perm,
+                            int64_t n_rows, const float* g_score, const float* z_other,
+                            int64_t ld_other, int64_t F, float* g_z, int64_t ld_g, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* HGIN_H_ */

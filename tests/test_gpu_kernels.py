@@ -1,0 +1,231 @@
+"""GPU parity of every libhgin.so kernel against the CPU oracle (bit-exact for index and sequential-sum
+work; stated tolerances for the MFMA GEMM and the decoder's reduction)."""
+import numpy as np
+import pytest
+import torch
+
+from hgin import ops
+from oracle import c_oracle as co
+from oracle.pyg_cpu import propagate_sum
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _rand_graph(E, n_src, n_dst, seed, zipf=False):
+    rng = np.random.default_rng(seed)
+    src = rng.integers(0, n_src, E)
+    if zipf and n_dst > 0:
+        dst = np.minimum(rng.zipf(1.1, E) - 1, n_dst - 1)
+    else:
+        dst = rng.integers(0, max(n_dst, 1), E)
+    return np.stack([src, dst]).astype(np.int64)
+
+
+# ------------------------------------------------------------------------------------------ A12 CSR
+@pytest.mark.parametrize("E,n_src,n_dst", [(0, 4, 6), (1, 1, 1), (5, 3, 1), (1000, 50, 37), (4096, 10, 300),
+                                           (4097, 300, 10), (70000, 5000, 2000), (200000, 100, 70000)])
+@pytest.mark.parametrize("key_row", [1, 0])
+def test_csr_build_bit_exact(E, n_src, n_dst, key_row):
+    ei = _rand_graph(E, n_src, n_dst, seed=E + key_row)
+    n_rows, n_cols = (n_dst, n_src) if key_row == 1 else (n_src, n_dst)
+    ref_rowptr, ref_col, ref_perm, st = co.csr_build(ei, key_row, n_rows, n_cols)
+    assert st == 0
+    csr = ops.build_csr(torch.from_numpy(ei).to(DEV), key_row, n_rows, n_cols)
+    assert np.array_equal(csr.rowptr.cpu().numpy(), ref_rowptr)
+    assert np.array_equal(csr.col.cpu().numpy(), ref_col)
+    assert np.array_equal(csr.perm.cpu().numpy(), ref_perm)
+
+
+def test_csr_build_skewed_and_large():
+    ei = _rand_graph(1_000_000, 600_000, 300_000, seed=11, zipf=True)
+    ref = co.csr_build(ei, 1, 300_000, 600_000)
+    csr = ops.build_csr(torch.from_numpy(ei).to(DEV), 1, 300_000, 600_000)
+    assert np.array_equal(csr.rowptr.cpu().numpy(), ref[0])
+    assert np.array_equal(csr.col.cpu().numpy(), ref[1])
+
+
+def test_csr_build_full_size_properties():
+    """cfg2's largest relation (3M edges): round trip against a stable device sort (size-independent)."""
+    g = torch.Generator(device=DEV).manual_seed(0)
+    E, n_src, n_dst = 3_000_000, 600_000, 300_000
+    ei = torch.stack([torch.randint(0, n_src, (E,), device=DEV, generator=g),
+                      torch.randint(0, n_dst, (E,), device=DEV, generator=g)])
+    csr = ops.build_csr(ei, 1, n_dst, n_src)
+    order = torch.sort(ei[1], stable=True).indices
+    assert torch.equal(csr.perm.long(), order)
+    assert torch.equal(csr.col.long(), ei[0][order])
+    deg = torch.bincount(ei[1], minlength=n_dst)
+    assert torch.equal(csr.rowptr[1:].long() - csr.rowptr[:-1].long(), deg)
+    assert int(csr.rowptr[-1]) == E
+
+
+def test_csr_out_of_range_raises():
+    ei = torch.tensor([[0, 1, 2], [0, 5, 1]], device=DEV)
+    with pytest.raises(IndexError, match="dst index out of range"):
+        ops.build_csr(ei, 1, 3, 3)
+    ei = torch.tensor([[0, 7, 2], [0, 1, 1]], device=DEV)
+    with pytest.raises(IndexError, match="src index out of range"):
+        ops.build_csr(ei, 1, 3, 3)
+    ei = torch.tensor([[0, -1], [0, 1]], device=DEV)
+    with pytest.raises(IndexError):
+        ops.build_csr(ei, 1, 3, 3)
+
+
+# ----------------------------------------------------------------------------------- A3/A4 aggregate
+@pytest.mark.parametrize("F_src,F_dst", [(1, 1), (3, 3), (4, 4), (3, 7), (8, 8), (12, 4), (16, 16), (64, 64),
+                                         (128, 128), (256, 256), (260, 260), (128, 3)])
+@pytest.mark.parametrize("mode", [0, 1, 2])
+def test_aggregate_bit_exact(F_src, F_dst, mode):
+    if mode == 1 and F_src != F_dst:
+        pytest.skip("add needs equal widths")
+    E, n_src, n_dst = 9000, 700, 500
+    ei = _rand_graph(E, n_src, n_dst, seed=F_src * 7 + mode)
+    ei[1, :40] = 3            # a high-degree row
+    rng = np.random.default_rng(F_src)
+    x = rng.standard_normal((n_src, F_src)).astype(np.float32)
+    xd = rng.standard_normal((n_dst, F_dst)).astype(np.float32)
+    eps = np.float32(-0.171875)
+    rowptr, col, _, _ = co.csr_build(ei, 1, n_dst, n_src)
+    ref = co.aggregate(rowptr, col, x, xd if mode else None, float(eps), mode)
+    csr = ops.build_csr(torch.from_numpy(ei).to(DEV), 1, n_dst, n_src)
+    width = F_src + (F_dst if mode == 2 else 0)
+    out = torch.full((n_dst, width), float("nan"), device=DEV)
+    ops.aggregate_into(csr, torch.from_numpy(x).to(DEV), torch.from_numpy(xd).to(DEV) if mode else None,
+                       torch.tensor([eps], device=DEV) if mode else None, mode, out)
+    assert np.array_equal(out.cpu().numpy(), ref)
+
+
+def test_aggregate_matches_reference_cpu_op():
+    """Against PyG's CPU path itself (index_select + scatter_add_ + cat), bit for bit."""
+    g = torch.Generator().manual_seed(5)
+    n_src, n_dst, E, F = 3000, 1000, 40000, 128
+    ei = torch.stack([torch.randint(0, n_src, (E,), generator=g), torch.randint(0, n_dst, (E,), generator=g)])
+    x, xd = torch.randn(n_src, F, generator=g), torch.randn(n_dst, F, generator=g)
+    eps = torch.tensor([0.0625])
+    ref = torch.cat((propagate_sum(x, ei, n_dst), (1 + eps) * xd), 1)
+    graph = ops.relation_graph(ei.to(DEV), n_src, n_dst)
+    out = ops.aggregate(x.to(DEV), xd.to(DEV), eps.to(DEV), graph, ops.COMBINE_CONCAT)
+    assert torch.equal(out.cpu(), ref)
+    ref_add = propagate_sum(x, ei, n_dst)
+    ref_add += (1 + eps) * xd
+    out = ops.aggregate(x.to(DEV), xd.to(DEV), eps.to(DEV), graph, ops.COMBINE_ADD)
+    assert torch.equal(out.cpu(), ref_add)
+
+
+def test_aggregate_strided_views_and_empty():
+    rng = np.random.default_rng(3)
+    n_src, n_dst = 50, 40
+    ei = _rand_graph(300, n_src, n_dst, seed=9)
+    big = torch.from_numpy(rng.standard_normal((n_src, 200)).astype(np.float32)).to(DEV)
+    x = big[:, 8:72]                       # ld 200, 16-B aligned start
+    x_odd = big[:, 1:65]                   # misaligned start -> scalar path
+    csr = ops.build_csr(torch.from_numpy(ei).to(DEV), 1, n_dst, n_src)
+    rowptr, col, _, _ = co.csr_build(ei, 1, n_dst, n_src)
+    for view in (x, x_odd):
+        out = torch.empty(n_dst, 64, device=DEV)
+        ops.aggregate_into(csr, view, None, None, 0, out)
+        assert np.array_equal(out.cpu().numpy(), co.aggregate(rowptr, col, view.cpu().numpy(), None, 0.0, 0))
+    # no edges at all: zeros (+ self term)
+    empty = ops.build_csr(torch.zeros(2, 0, dtype=torch.long, device=DEV), 1, n_dst, n_src)
+    xd = torch.randn(n_dst, 64, device=DEV)
+    out = torch.empty(n_dst, 128, device=DEV)
+    ops.aggregate_into(empty, x.contiguous(), xd, torch.tensor([0.5], device=DEV), 2, out)
+    assert torch.equal(out[:, :64], torch.zeros(n_dst, 64, device=DEV))
+    assert torch.equal(out[:, 64:], 1.5 * xd)
+
+
+# ------------------------------------------------------------------------------------- A5 MFMA GEMM
+@pytest.mark.parametrize("M,N,K", [(1, 1, 1), (37, 8, 6), (1000, 128, 256), (513, 130, 129), (300, 256, 512),
+                                   (4096, 128, 128), (65, 3, 1000)])
+def test_gin_mlp_fwd(M, N, K):
+    g = torch.Generator(device=DEV).manual_seed(M + N + K)
+    a = torch.randn(M, K, device=DEV, generator=g)
+    w = torch.randn(N, K, device=DEV, generator=g) / K ** 0.5
+    b = torch.randn(N, device=DEV, generator=g)
+    s = torch.tensor([0.25], device=DEV)
+    acc = torch.randn(M, N, device=DEV, generator=g)
+    z, y = ops.gin_mlp_fwd(a, w, b, s, acc)
+    zr = (a.double() @ w.double().t() + b.double())
+    bound = 1e-5 * (a.double().abs() @ w.double().abs().t() + b.double().abs() + 1)
+    assert ((z.double() - zr).abs() <= bound).all()
+    assert torch.equal(y, acc + torch.where(z > 0, z, s * z))
+    _, y2 = ops.gin_mlp_fwd(a, w, b, s, None, save_z=False)
+    assert torch.equal(y2, torch.where(z > 0, z, s * z))
+
+
+def test_gemm_layout_identity_asymmetric():
+    """A = I with an asymmetric B must return B^T exactly (catches a transposed C/D map)."""
+    K = 64
+    a = torch.eye(K, device=DEV)
+    b = torch.arange(K * 40, device=DEV, dtype=torch.float32).reshape(40, K)   # [N=40, K]
+    c = ops.gemm_nt(a, b)                     # c = a @ b^T = b^T
+    assert torch.equal(c, b.t())
+
+
+@pytest.mark.parametrize("M,N,K", [(200, 64, 128), (1, 256, 3), (1031, 100, 77)])
+def test_gemm_nt(M, N, K):
+    a = torch.randn(M, K, device=DEV)
+    b = torch.randn(N, K, device=DEV)
+    c = ops.gemm_nt(a, b)
+    ref = a.double() @ b.double().t()
+    assert ((c.double() - ref).abs() <= 1e-5 * (a.double().abs() @ b.double().abs().t() + 1)).all()
+
+
+# --------------------------------------------------------------------------- A9 backward reductions
+@pytest.mark.parametrize("M,N", [(1, 1), (1000, 128), (777, 300), (5, 8)])
+def test_prelu_bwd(M, N):
+    z = torch.randn(M, N, device=DEV)
+    z[0, 0] = 0.0
+    gy = torch.randn(M, N, device=DEV)
+    a = torch.tensor([0.3], device=DEV)
+    g_z, g_a, g_b = ops.prelu_bwd(gy, z, a)
+    assert torch.equal(g_z, torch.where(z > 0, gy, a * gy))
+    zr = z.double()
+    ga_ref = (torch.where(zr > 0, torch.zeros_like(zr), zr) * gy.double()).sum()
+    assert abs(float(g_a) - float(ga_ref)) <= 1e-5 * (float((zr * gy.double()).abs().sum()) + 1)
+    assert torch.allclose(g_b.double(), g_z.double().sum(0), rtol=1e-5, atol=1e-5)
+    again = ops.prelu_bwd(gy, z, a)
+    assert torch.equal(again[1], g_a) and torch.equal(again[2], g_b)   # deterministic
+
+
+def test_combine_bwd():
+    g = torch.randn(900, 130, device=DEV)
+    x = torch.randn(900, 64, device=DEV)
+    eps = torch.tensor([0.125], device=DEV)
+    gx, ge = ops.combine_bwd(g[:, 66:], x, eps, True)
+    assert torch.equal(gx, (1 + eps) * g[:, 66:])
+    ref = (g[:, 66:].double() * x.double()).sum()
+    assert abs(float(ge) - float(ref)) <= 1e-5 * float((g[:, 66:] * x).abs().sum().double())
+    assert torch.equal(ops.combine_bwd(g[:, 66:], x, eps, False)[1], ge)
+
+
+# ---------------------------------------------------------------------------------- A10 / A11
+@pytest.mark.parametrize("seed,offset,n,n_dst", [(0, 0, 1, 1), (1234, 6, 10, 1000), (2**40 + 5, 3, 100003, 300000),
+                                                  (7, 2**33 + 1, 4096, 2**31 - 1)])
+def test_neg_sample_bit_exact(seed, offset, n, n_dst):
+    out = torch.empty(n + 1, dtype=torch.int32, device=DEV)
+    from hgin import _lib
+    _lib.call("hgin_neg_sample", seed, offset, n, n_dst, ops._p(out[1:]), ops._stream(out))   # unaligned too
+    assert np.array_equal(out[1:].cpu().numpy(), co.neg_sample(seed, offset, n, n_dst))
+
+
+def test_dot_decoder():
+    from hgin import linkpred
+    rng = np.random.default_rng(1)
+    n_src, n_dst, n, F = 300, 200, 5000, 64
+    src, dst = rng.integers(0, n_src, n), rng.integers(0, n_dst, n)
+    zs = rng.standard_normal((n_src, F)).astype(np.float32)
+    zd = rng.standard_normal((n_dst, F)).astype(np.float32)
+    ref = co.dot_decode_fwd(src, dst, zs, zd)
+    pairs = torch.from_numpy(np.stack([src, dst])).to(DEV)
+    zs_t = torch.from_numpy(zs).to(DEV).requires_grad_()
+    zd_t = torch.from_numpy(zd).to(DEV).requires_grad_()
+    score = linkpred.dot_decode(zs_t, zd_t, pairs)
+    assert np.allclose(score.detach().cpu().numpy(), ref, rtol=1e-5, atol=1e-5)
+    g = torch.randn(n, device=DEV)
+    score.backward(g)
+    rp, col, perm, _ = co.csr_build(np.stack([src, dst]), 0, n_src, n_dst)
+    assert np.array_equal(zs_t.grad.cpu().numpy(), co.dot_decode_bwd(rp, col, perm, g.cpu().numpy(), zd))
+    rp, col, perm, _ = co.csr_build(np.stack([src, dst]), 1, n_dst, n_src)
+    assert np.array_equal(zd_t.grad.cpu().numpy(), co.dot_decode_bwd(rp, col, perm, g.cpu().numpy(), zs))

@@ -1,0 +1,61 @@
+"""The CPU oracle (oracle/pyg_cpu.py) against the golden vectors made by executing the reference's own
+models.py (tests/golden/make_golden.py).  Everything is compared bit-for-bit: same torch CPU ops."""
+import pytest
+import torch
+
+from conftest import CASES, fixture_inputs, fixture_model_kwargs, load_fixture
+from oracle.pyg_cpu import OracleHetroGIN, mape, propagate_sum
+
+
+@pytest.fixture(autouse=True)
+def _one_thread():
+    n = torch.get_num_threads()
+    torch.set_num_threads(1)
+    yield
+    torch.set_num_threads(n)
+
+
+@pytest.mark.parametrize("case", CASES)
+def test_oracle_reproduces_reference(case):
+    fx = load_fixture(case)
+    torch.manual_seed(fx["meta"]["seed_model"])
+    kw = fixture_model_kwargs(fx)
+    model = OracleHetroGIN(**kw)
+    assert kw["input_channels"] == fx["meta"]["input_channels_after_ctor"]
+    sd = model.state_dict()
+    assert list(sd) == [k[3:] for k in fx if k.startswith("sd.")]
+    for k, v in sd.items():
+        assert torch.equal(v, fx["sd." + k]), k
+    x, ei, batch, y = fixture_inputs(fx)
+    model.set_record(True)
+    opt = torch.optim.Adam(lr=1e-3, params=model.parameters(), weight_decay=0)
+    opt.zero_grad()
+    out = model(dict(x), ei, batch)
+    assert torch.equal(out, fx["out"])
+    # per-relation aggregates (propagate results) in layer / relation order
+    for li, conv in enumerate(model.convs):
+        for key, layer in conv.convs.items():
+            assert torch.equal(layer.conv.trace[0], fx[f"agg.{li}.{key}"]), (li, key)
+    lv = mape(out, y.reshape(-1, 1))
+    assert torch.equal(lv, fx["loss_value"])
+    torch.sqrt(lv).backward()
+    for n, p in model.named_parameters():
+        g = p.grad if p.grad is not None else torch.zeros(0)
+        assert torch.equal(g, fx["grad." + n]), n
+    opt.step()
+    for n, p in model.named_parameters():
+        assert torch.equal(p, fx["step." + n]), n
+
+
+def test_propagate_equals_sequential_edge_order():
+    """scatter_add_ on CPU == per-destination sequential sum in original edge order."""
+    g = torch.Generator().manual_seed(7)
+    n_src, n_dst, E, F = 500, 300, 20000, 5
+    ei = torch.stack([torch.randint(0, n_src, (E,), generator=g), torch.randint(0, n_dst, (E,), generator=g)])
+    x = torch.randn(n_src, F, generator=g)
+    ref = propagate_sum(x, ei, n_dst)
+    order = torch.sort(ei[1], stable=True).indices
+    out = torch.zeros(n_dst, F)
+    for e in order.tolist():
+        out[ei[1, e]] += x[ei[0, e]]
+    assert torch.equal(ref, out)
