@@ -1,0 +1,263 @@
+// A9 — weight-gradient GEMMs of the GIN update and the readout (backward of Linear: dW = g_z^T X).
+//
+// Reference: the autograd of torch.nn.Linear inside GINLayer.mlp (models.py:236-239) and the readout
+// (models.py:300-330), reached from loss.backward() at train.py:43, where the reduction dimension is every
+// node of a type (1e5 .. 1e7 rows) and the output only H x K; a library GEMM tiles the small output and
+// leaves most CUs idle (hipBLASLt: 32 workgroups for 128 x 256).  Here the row range is split across
+// workgroups that each write an fp32 partial slab; the slabs are added in a fixed order (two levels), so
+// the result is bitwise reproducible.
+#include "hgin_common.h"
+
+namespace hgin {
+namespace {
+
+using f32x16 = __attribute__((ext_vector_type(16))) float;
+
+// ---------------------------------------------------------------------------------------------------
+// Weight-gradient GEMM "TN":  out[N, K] = A^T [B1 | B2],  A [M, N], B1 [M, K1], B2 [M, K - K1].
+// The reduction runs over M (every node of a type: 1e5..1e7 rows) and the output is small (H x K), so
+// the M range is split over S workgroups per output tile (S chosen to fill the 256 CUs); each writes an
+// fp32 partial slab, and k_slab_reduce adds the slabs in split order — deterministic, no atomics.
+// Inner tile: 32 rows of M staged in LDS as [m][n] and [m][k] (row stride 132 floats); an MFMA k-step
+// takes rows 2s (lane half 0) and 2s+1 (half 1), lanes i = 0..31 read 32 consecutive floats of a row
+// (ds_read_b32, conflict-free).  The B operand is concatenated from two sources so [aggregate | x_dst]
+// needs no materialised copy.
+constexpr int kTnBM = 32;       // rows of M per stage
+constexpr int kTnLd = 128 + 4;
+
+__global__ __launch_bounds__(256, 2) void k_gemm_tn_partial(const float* __restrict__ A, int64_t lda,
+                                                            const float* __restrict__ B1, int64_t ldb1,
+                                                            const float* __restrict__ B2, int64_t ldb2, int64_t K1,
+                                                            int64_t M, int64_t N, int64_t K, int64_t rows_per_split,
+                                                            bool vec, float* __restrict__ slab) {
+  __shared__ __attribute__((aligned(16))) float smem[2 * kTnBM * kTnLd];
+  float* As = smem;
+  float* Bs = smem + kTnBM * kTnLd;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int li = lane & 31, lh = lane >> 5;
+  const int64_t n0 = (int64_t)blockIdx.x * 128;
+  const int64_t k0 = (int64_t)blockIdx.y * 128;
+  const int64_t mb = (int64_t)blockIdx.z * rows_per_split;
+  const int64_t me = mb + rows_per_split < M ? mb + rows_per_split : M;
+
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[a][b][e] = 0.0f;
+
+  const int c4 = (tid & 31) * 4;   // column (x4) inside the 128-wide tile
+  for (int64_t m0 = mb; m0 < me; m0 += kTnBM) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int r = (tid >> 5) + 8 * i;
+      const int64_t gm = m0 + r;
+      float4 va = make_float4(0.f, 0.f, 0.f, 0.f), vb = va;
+      if (gm < me) {
+        const int64_t gn = n0 + c4;
+        const float* pa = A + gm * lda + gn;
+        if (vec && gn + 3 < N) {
+          va = *reinterpret_cast<const float4*>(pa);
+        } else {
+          if (gn + 0 < N) va.x = pa[0];
+          if (gn + 1 < N) va.y = pa[1];
+          if (gn + 2 < N) va.z = pa[2];
+          if (gn + 3 < N) va.w = pa[3];
+        }
+        const int64_t gk = k0 + c4;
+        if (vec && gk + 3 < K && (gk + 3 < K1 || gk >= K1)) {
+          const float* pb = gk < K1 ? B1 + gm * ldb1 + gk : B2 + gm * ldb2 + (gk - K1);
+          vb = *reinterpret_cast<const float4*>(pb);
+        } else {
+          float t[4];
+#pragma unroll
+          for (int c = 0; c < 4; ++c) {
+            const int64_t k = gk + c;
+            t[c] = k < K ? (k < K1 ? B1[gm * ldb1 + k] : B2[gm * ldb2 + (k - K1)]) : 0.0f;
+          }
+          vb = make_float4(t[0], t[1], t[2], t[3]);
+        }
+      }
+      *reinterpret_cast<float4*>(As + r * kTnLd + c4) = va;
+      *reinterpret_cast<float4*>(Bs + r * kTnLd + c4) = vb;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int st = 0; st < kTnBM / 2; ++st) {
+      const int row = 2 * st + lh;
+      float fa[2], fb[2];
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        fa[t] = As[row * kTnLd + wm * 64 + t * 32 + li];
+        fb[t] = Bs[row * kTnLd + wn * 64 + t * 32 + li];
+      }
+#pragma unroll
+      for (int tm = 0; tm < 2; ++tm)
+#pragma unroll
+        for (int tn = 0; tn < 2; ++tn)
+          acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[tm], fb[tn], acc[tm][tn], 0, 0, 0);
+    }
+    __syncthreads();
+  }
+  float* out = slab + (int64_t)blockIdx.z * N * K;
+#pragma unroll
+  for (int tm = 0; tm < 2; ++tm)
+#pragma unroll
+    for (int tn = 0; tn < 2; ++tn) {
+      const int64_t k = k0 + wn * 64 + tn * 32 + li;
+      if (k >= K) continue;
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int64_t n = n0 + wm * 64 + tm * 32 + (e & 3) + 8 * (e >> 2) + 4 * lh;
+        if (n < N) out[n * K + k] = acc[tm][tn][e];
+      }
+    }
+}
+
+// Small weight gradients (N or K < 16, e.g. the readout head Linear(32, 1)): no MFMA tile to fill, so a
+// block owns a chunk of M rows and thread (r, p) accumulates pair p = (n, k) over rows r, r + R, ... in
+// order; the R row-lanes are combined in LDS in lane order.  Output: the same [split][N*K] slabs.
+__global__ __launch_bounds__(256) void k_tn_small(const float* __restrict__ A, int64_t lda,
+                                                  const float* __restrict__ B1, int64_t ldb1,
+                                                  const float* __restrict__ B2, int64_t ldb2, int64_t K1, int64_t M,
+                                                  int N, int K, int64_t rows_per_split, float* __restrict__ slab) {
+  __shared__ float red[256];
+  const int P = N * K;
+  const int PW = P < 256 ? P : 256;
+  const int R = 256 / PW;
+  const int t = threadIdx.x;
+  const int rl = t / PW;
+  const int64_t mb = (int64_t)blockIdx.x * rows_per_split;
+  const int64_t me = mb + rows_per_split < M ? mb + rows_per_split : M;
+  for (int p0 = 0; p0 < P; p0 += PW) {
+    const int p = p0 + t % PW;
+    float acc = 0.0f;
+    if (rl < R && p < P) {
+      const int n = p / K, k = p % K;
+      const float* bcol = k < K1 ? B1 + k : B2 + (k - K1);
+      const int64_t ldb = k < K1 ? ldb1 : ldb2;
+      for (int64_t m = mb + rl; m < me; m += R) acc = __fadd_rn(acc, __fmul_rn(A[m * lda + n], bcol[m * ldb]));
+    }
+    red[t] = acc;
+    __syncthreads();
+    if (rl == 0 && p < P) {
+      float s = 0.0f;
+      for (int j = 0; j < R; ++j) s = __fadd_rn(s, red[j * PW + t]);
+      slab[(int64_t)blockIdx.x * P + p] = s;
+    }
+    __syncthreads();
+  }
+}
+
+// Deterministic two-level slab sum: level 1 adds groups of kSlabGroup consecutive slabs (float4 per
+// thread, many workgroups in flight), level 2 adds the group sums in group order.
+constexpr int kSlabGroup = 16;
+
+__global__ __launch_bounds__(256) void k_slab_reduce1(const float* __restrict__ slab, int64_t S, int64_t NK,
+                                                      float* __restrict__ part) {
+  const int64_t i4 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4;
+  if (i4 >= NK) return;
+  const int64_t g = blockIdx.y;
+  const int64_t s0 = g * kSlabGroup;
+  const int64_t s1 = s0 + kSlabGroup < S ? s0 + kSlabGroup : S;
+  float a[4] = {0.f, 0.f, 0.f, 0.f};
+  const bool full = i4 + 3 < NK && (NK & 3) == 0;
+  for (int64_t j = s0; j < s1; ++j) {
+    const float* p = slab + j * NK + i4;
+    if (full) {
+      const float4 v = *reinterpret_cast<const float4*>(p);
+      a[0] = __fadd_rn(a[0], v.x); a[1] = __fadd_rn(a[1], v.y); a[2] = __fadd_rn(a[2], v.z); a[3] = __fadd_rn(a[3], v.w);
+    } else {
+      for (int c = 0; c < 4 && i4 + c < NK; ++c) a[c] = __fadd_rn(a[c], p[c]);
+    }
+  }
+  float* q = part + g * NK + i4;
+  for (int c = 0; c < 4 && i4 + c < NK; ++c) q[c] = a[c];
+}
+
+__global__ __launch_bounds__(256) void k_slab_reduce2(const float* __restrict__ part, int64_t G, int64_t NK,
+                                                      float* __restrict__ out, int64_t K, int64_t ldo) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= NK) return;
+  float s = 0.0f;
+  for (int64_t j = 0; j < G; ++j) s = __fadd_rn(s, part[j * NK + i]);
+  out[(i / K) * ldo + (i % K)] = s;
+}
+
+bool tn_is_small(int64_t N, int64_t K) { return N < 16 || K < 16; }
+
+int64_t tn_splits(int64_t M, int64_t N, int64_t K) {
+  int64_t S;
+  if (tn_is_small(N, K)) {
+    S = ceil_div(M, 2048);                                 // 2048 rows per workgroup
+    if (S > 1024) S = 1024;
+  } else {
+    const int64_t tiles = ceil_div(N, 128) * ceil_div(K, 128);
+    S = ceil_div(1024, tiles);                             // ~4 workgroups per CU
+    const int64_t max_s = ceil_div(M, 8 * kTnBM);          // keep >= 8 stages per split
+    if (S > max_s) S = max_s;
+  }
+  return S < 1 ? 1 : S;
+}
+
+}  // namespace
+}  // namespace hgin
+
+using namespace hgin;
+
+extern "C" int hgin_gemm_tn_workspace_size(int64_t M, int64_t N, int64_t K, size_t* bytes) {
+  HGIN_ARG_CHECK(bytes && M >= 0 && N >= 0 && K >= 0, "hgin_gemm_tn_workspace_size: bad args");
+  const int64_t S = tn_splits(M, N, K);
+  *bytes = align_up(sizeof(float) * (size_t)(S * N * K), 256) +
+           sizeof(float) * (size_t)(ceil_div(S, kSlabGroup) * N * K) + 256;
+  return HGIN_OK;
+}
+
+extern "C" int hgin_gemm_tn_f32(const float* a, int64_t lda, const float* b1, int64_t ldb1, int64_t k1,
+                                const float* b2, int64_t ldb2, int64_t M, int64_t N, int64_t K, float* out,
+                                int64_t ldo, void* workspace, size_t workspace_bytes, void* stream) {
+  HGIN_ARG_CHECK(M >= 0 && N >= 0 && K >= 0 && k1 >= 0 && k1 <= K, "hgin_gemm_tn_f32: bad sizes");
+  HGIN_ARG_CHECK(N <= 65535 * 128 && K <= 65535 * 128, "hgin_gemm_tn_f32: N/K too large");
+  if (N == 0 || K == 0) return HGIN_OK;
+  HGIN_ARG_CHECK(out && ldo >= K, "hgin_gemm_tn_f32: bad output");
+  size_t need = 0;
+  hgin_gemm_tn_workspace_size(M, N, K, &need);
+  if (workspace_bytes < need || !workspace) {
+    set_error("hgin_gemm_tn_f32: workspace %zu < %zu", workspace_bytes, need);
+    return HGIN_E_WORKSPACE;
+  }
+  hipStream_t s = as_stream(stream);
+  if (M == 0) {
+    for (int64_t n = 0; n < N; ++n) {
+      int rc = memset_async(out + n * ldo, 0, sizeof(float) * (size_t)K, s, "hgin_gemm_tn_f32");
+      if (rc) return rc;
+    }
+    return HGIN_OK;
+  }
+  HGIN_ARG_CHECK(a && lda >= N && (k1 == 0 || (b1 && ldb1 >= k1)) && (k1 == K || (b2 && ldb2 >= K - k1)),
+                 "hgin_gemm_tn_f32: bad operand");
+  const bool vec = aligned16(a) && lda % 4 == 0 && (k1 == 0 || (aligned16(b1) && ldb1 % 4 == 0)) &&
+                   (k1 == K || (aligned16(b2) && ldb2 % 4 == 0)) && k1 % 4 == 0;
+  const int64_t S = tn_splits(M, N, K);
+  const int64_t rows = ceil_div(ceil_div(M, S), kTnBM) * kTnBM;
+  const int64_t S_eff = ceil_div(M, rows);
+  const int64_t NK = N * K;
+  float* slab = static_cast<float*>(workspace);
+  float* part = reinterpret_cast<float*>(static_cast<char*>(workspace) + align_up(sizeof(float) * (size_t)(S * NK), 256));
+  if (tn_is_small(N, K)) {
+    k_tn_small<<<(unsigned)S_eff, 256, 0, s>>>(a, lda, b1, ldb1, b2, ldb2, k1, M, (int)N, (int)K, rows, slab);
+  } else {
+    dim3 grid((unsigned)ceil_div(N, 128), (unsigned)ceil_div(K, 128), (unsigned)S_eff);
+    k_gemm_tn_partial<<<grid, 256, 0, s>>>(a, lda, b1, ldb1, b2, ldb2, k1, M, N, K, rows, vec, slab);
+  }
+  const int64_t G = ceil_div(S_eff, kSlabGroup);
+  dim3 g1((unsigned)ceil_div(ceil_div(NK, 4), 256), (unsigned)G);
+  k_slab_reduce1<<<g1, 256, 0, s>>>(slab, S_eff, NK, part);
+  k_slab_reduce2<<<(unsigned)ceil_div(NK, 256), 256, 0, s>>>(part, G, NK, out, K, ldo);
+  return check_launch("hgin_gemm_tn_f32");
+}

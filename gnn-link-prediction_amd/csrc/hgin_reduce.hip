@@ -75,7 +75,7 @@ __global__ __launch_bounds__(256) void k_rows_bwd(const float* __restrict__ in0,
       if (active && rl == 0 && c < N) {
         float tot = 0.0f;
         for (int j = 0; j < RL; ++j) tot = __fadd_rn(tot, red[j * CW + c0]);
-        part_col[(int64_t)blockIdx.x * N + c] = tot;
+        part_col[(int64_t)c * gridDim.x + blockIdx.x] = tot;   // [N][nblk]: coalesced final pass
       }
       __syncthreads();
     }
@@ -84,14 +84,16 @@ __global__ __launch_bounds__(256) void k_rows_bwd(const float* __restrict__ in0,
   if (t == 0) part_s[blockIdx.x] = bs;
 }
 
-// Sum block partials in block order: one thread per column (+ one block-wide pass for the scalar).
+// Sum block partials in a fixed order: one workgroup per column, strided per-thread sums + fixed tree.
 __global__ __launch_bounds__(256) void k_final_cols(const float* __restrict__ part, int64_t nblk, int N,
                                                     float* __restrict__ out) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= N) return;
+  __shared__ float red[256];
+  const int c = blockIdx.x;
+  const float* p = part + (int64_t)c * nblk;
   float s = 0.0f;
-  for (int64_t b = 0; b < nblk; ++b) s = __fadd_rn(s, part[b * N + c]);
-  out[c] = s;
+  for (int64_t b = threadIdx.x; b < nblk; b += 256) s = __fadd_rn(s, p[b]);
+  const float tot = block_sum_fixed(s, red);
+  if (threadIdx.x == 0) out[c] = tot;
 }
 
 __global__ __launch_bounds__(256) void k_final_scalar(const float* __restrict__ part, int64_t nblk,
@@ -115,7 +117,7 @@ extern "C" int hgin_prelu_bwd_workspace_size(int64_t M, int64_t N, size_t* bytes
   return HGIN_OK;
 }
 
-extern "C" int hgin_prelu_bwd_f32(const float* g_y, const float* z, int64_t M, int64_t N, const float* prelu,
+extern "C" int hgin_prelu_bwd_f32(const float* g_y, int64_t ld_gy, const float* z, int64_t M, int64_t N, const float* prelu,
                                   float* g_z, float* g_prelu, float* g_bias, void* workspace, size_t workspace_bytes,
                                   void* stream) {
   HGIN_ARG_CHECK(M >= 0 && N >= 0 && N < (1 << 24), "hgin_prelu_bwd_f32: bad sizes");
@@ -132,13 +134,13 @@ extern "C" int hgin_prelu_bwd_f32(const float* g_y, const float* z, int64_t M, i
     if (rc == HGIN_OK) rc = memset_async(g_prelu, 0, sizeof(float), s, "hgin_prelu_bwd_f32");
     return rc;
   }
-  HGIN_ARG_CHECK(g_y && z && g_z, "hgin_prelu_bwd_f32: NULL operand");
+  HGIN_ARG_CHECK(g_y && z && g_z && ld_gy >= N, "hgin_prelu_bwd_f32: NULL operand or ld_gy < N");
   const int64_t nblk = ceil_div(M, kRowsPerBlock);
   float* part_col = static_cast<float*>(workspace);
   float* part_s = reinterpret_cast<float*>(static_cast<char*>(workspace) +
                                            align_up(sizeof(float) * (size_t)(nblk * N), 256));
-  k_rows_bwd<0><<<(unsigned)nblk, 256, 0, s>>>(g_y, N, z, N, M, (int)N, prelu, g_z, N, part_col, part_s);
-  k_final_cols<<<(unsigned)ceil_div(N, 256), 256, 0, s>>>(part_col, nblk, (int)N, g_bias);
+  k_rows_bwd<0><<<(unsigned)nblk, 256, 0, s>>>(g_y, ld_gy, z, N, M, (int)N, prelu, g_z, N, part_col, part_s);
+  k_final_cols<<<(unsigned)N, 256, 0, s>>>(part_col, nblk, (int)N, g_bias);
   k_final_scalar<<<1, 256, 0, s>>>(part_s, nblk, g_prelu);
   return check_launch("hgin_prelu_bwd_f32");
 }

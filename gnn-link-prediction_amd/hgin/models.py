@@ -16,7 +16,8 @@ from typing import List
 
 import torch
 
-from .conv import GINLayer, HeteroConv
+from . import ops
+from .conv import GINLayer, HeteroConv, _fusable_mlp as _fusable_linear_prelu
 
 _ACTS = {"torch.nn.PReLU()": torch.nn.PReLU, "torch.nn.ReLU()": torch.nn.ReLU, "torch.nn.ELU()": torch.nn.ELU,
          "torch.nn.LeakyReLU()": torch.nn.LeakyReLU, "torch.nn.Tanh()": torch.nn.Tanh,
@@ -148,11 +149,12 @@ class HetroGIN(torch.nn.Module):
                 for k in list(x_dict.keys()):
                     x_dict[k] = torch.nn.functional.dropout(x_dict[k], p=self.dropout, training=True)
 
+        x2 = None   # second column block of the readout input, read in place instead of torch.cat
         if self.concat_path:   # models.py:362-371
             if self.global_feats:
                 x = torch.cat((x_dict["path"], origin_input["path"], mean_f, max_f), 1)
             else:
-                x = torch.cat((x_dict["path"], origin_input["path"]), 1)
+                x, x2 = x_dict["path"], origin_input["path"]
         else:
             if self.global_feats:
                 x = torch.cat((x_dict["path"], mean_f, max_f), 1)
@@ -160,7 +162,16 @@ class HetroGIN(torch.nn.Module):
                 x = x_dict["path"]
 
         for i in range(len(self.mlp_layers) + 1):   # models.py:373-374
-            x = self.readout[i](x)
+            seq = self.readout[i]
+            if _fusable_linear_prelu(seq):
+                x = ops.linear_prelu(x, seq[0].weight, seq[0].bias, seq[1].weight, x2=x2)
+            elif len(seq) == 1 and isinstance(seq[0], torch.nn.Linear) and seq[0].bias is not None:
+                x = ops.linear_prelu(x, seq[0].weight, seq[0].bias, None, x2=x2)
+            else:
+                if x2 is not None:
+                    x = torch.cat((x, x2), 1)
+                x = seq(x)
+            x2 = None
         return x
 
 

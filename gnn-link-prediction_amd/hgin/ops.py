@@ -185,7 +185,7 @@ def prelu_bwd(g_y: Tensor, z: Tensor, prelu: Tensor):
     nbytes = ctypes.c_size_t(0)
     _lib.check(_lib.lib().hgin_prelu_bwd_workspace_size(M, N, ctypes.byref(nbytes)), "prelu_bwd_workspace_size")
     ws = _workspace(nbytes.value, z.device)
-    _lib.call("hgin_prelu_bwd_f32", _p(g_y), _p(z), M, N, _p(prelu), _p(g_z), _p(g_a), _p(g_b), _p(ws),
+    _lib.call("hgin_prelu_bwd_f32", _p(g_y), g_y.stride(0), _p(z), M, N, _p(prelu), _p(g_z), _p(g_a), _p(g_b), _p(ws),
               nbytes.value, _stream(z))
     return g_z, g_a, g_b
 
@@ -212,16 +212,41 @@ def gemm_nt(a: Tensor, b: Tensor) -> Tensor:
     return c
 
 
-def gin_mlp_fwd(comb: Tensor, weight: Tensor, bias: Tensor, prelu: Tensor, accum: Optional[Tensor],
-                save_z: bool = True):
-    M, K = comb.shape
+def gemm_tn(a: Tensor, b1: Tensor, b2: Optional[Tensor] = None) -> Tensor:
+    """out[N, K] = a[M, N]^T @ [b1 | b2] (weight gradients), split-M MFMA + deterministic slab reduce."""
+    a, b1 = _rowmajor(a), _rowmajor(b1)
+    if b2 is not None:
+        b2 = _rowmajor(b2)
+    M, N = a.shape
+    k1 = b1.shape[1]
+    K = k1 + (b2.shape[1] if b2 is not None else 0)
+    out = torch.empty(N, K, dtype=torch.float32, device=a.device)
+    nbytes = ctypes.c_size_t(0)
+    _lib.check(_lib.lib().hgin_gemm_tn_workspace_size(M, N, K, ctypes.byref(nbytes)), "gemm_tn_workspace_size")
+    ws = _workspace(nbytes.value, a.device)
+    _lib.call("hgin_gemm_tn_f32", _p(a), a.stride(0), _p(b1), b1.stride(0), k1, _p(b2),
+              b2.stride(0) if b2 is not None else 0, M, N, K, _p(out), out.stride(0), _p(ws), nbytes.value,
+              _stream(a))
+    return out
+
+
+def gin_mlp_fwd(comb: Tensor, weight: Tensor, bias: Tensor, prelu: Optional[Tensor], accum: Optional[Tensor],
+                save_z: bool = True, comb2: Optional[Tensor] = None):
+    """y = prelu([comb | comb2] @ W^T + b) [+ accum]  (prelu None: plain Linear, y = z, nothing saved)."""
+    M, k1 = comb.shape
+    K = k1 + (comb2.shape[1] if comb2 is not None else 0)
     N = weight.shape[0]
-    z = torch.empty(M, N, dtype=torch.float32, device=comb.device) if save_z else None
+    z = torch.empty(M, N, dtype=torch.float32, device=comb.device) if (save_z and prelu is not None) else None
     y = torch.empty(M, N, dtype=torch.float32, device=comb.device)
+    ld2 = comb2.stride(0) if comb2 is not None else 0
 
     def launch():
-        _lib.call("hgin_gin_mlp_fwd_f32", _p(comb), comb.stride(0), _p(weight), _p(bias), _p(prelu), _p(accum),
-                  _p(z), _p(y), M, N, K, _stream(comb))
+        if prelu is None:
+            _lib.call("hgin_linear_fwd_f32", _p(comb), comb.stride(0), k1, _p(comb2), ld2, _p(weight), _p(bias),
+                      _p(y), M, N, K, _stream(comb))
+        else:
+            _lib.call("hgin_gin_mlp_fwd_f32", _p(comb), comb.stride(0), k1, _p(comb2), ld2, _p(weight), _p(bias),
+                      _p(prelu), _p(accum), _p(z), _p(y), M, N, K, _stream(comb))
 
     probe = profiling.active()
     if probe is None:
@@ -289,24 +314,90 @@ class _GINConvFn(torch.autograd.Function):
         need_src, need_dst, need_eps, need_w, need_b, need_a, need_acc = need[:7]
         g_y = _rowmajor(g_y)
         g_z, g_a, g_b = prelu_bwd(g_y, z, prelu)
-        g_w = torch.mm(g_z.t(), comb) if need_w else None
-        g_src = g_dst = g_eps = None
+        g_w = g_src = g_dst = g_eps = None
         f_src, mode = ctx.f_src, ctx.mode
         if need_src or need_dst:
-            g_comb = torch.mm(g_z, weight)                      # [N_dst, K]
+            if need_w:
+                g_w = gemm_tn(g_z, comb)                        # dW = g_z^T comb
+            g_comb = gemm_nt(g_z, weight.t().contiguous())      # dX = g_z W   [N_dst, K]
             if need_src:
                 g_src = _backward_aggregate(ctx.graph, g_comb[:, :f_src])
             if mode != COMBINE_NONE:
                 gs = g_comb[:, f_src:] if mode == COMBINE_CONCAT else g_comb
                 g_dst, g_eps = combine_bwd(gs, x_dst, eps, need_dst)
         elif need_eps and mode != COMBINE_NONE:
-            # Only parameters need gradients (e.g. the first layer, whose inputs are data):
-            # sum(g_comb[:, self] * x_dst) = sum(W_self * (g_z^T x_dst))  — skips the [N_dst, K] dX GEMM.
-            w_self = weight[:, f_src:] if mode == COMBINE_CONCAT else weight
-            g_eps = (w_self * torch.mm(g_z.t(), x_dst)).sum().reshape(1)
+            # Only parameters need gradients (the first layer, whose inputs are data):
+            # sum(g_comb[:, self] * x_dst) = sum(W_self * (g_z^T x_dst)), so one TN pass over
+            # [aggregate | x_dst] yields dW and the eps gradient and the [N_dst, K] dX GEMM is skipped.
+            if mode == COMBINE_CONCAT:
+                G = gemm_tn(g_z, comb[:, :f_src], x_dst)
+                gx = G[:, f_src:]
+                g_w = torch.cat((G[:, :f_src], (1 + eps) * gx), 1) if need_w else None
+                g_eps = (weight[:, f_src:] * gx).sum().reshape(1)
+            else:
+                G = gemm_tn(g_z, comb, x_dst)
+                g_w = G[:, :f_src].contiguous() if need_w else None
+                g_eps = (weight * G[:, f_src:]).sum().reshape(1)
+        elif need_w:
+            g_w = gemm_tn(g_z, comb)
         g_acc = g_y if need_acc else None
         return (g_src, g_dst, (g_eps.view_as(eps) if (need_eps and g_eps is not None) else None), g_w,
                 g_b if need_b else None, (g_a.view_as(prelu) if need_a else None), g_acc, None, None)
+
+
+_ONE = {}
+
+
+def _one(device) -> Tensor:
+    t = _ONE.get(device)
+    if t is None:
+        t = _ONE[device] = torch.ones(1, dtype=torch.float32, device=device)
+    return t
+
+
+class _LinearPReLUFn(torch.autograd.Function):
+    """Linear [+ PReLU] of the readout (models.py:300-330, :373-374) on the MFMA kernels.  The input is the
+    column concatenation [x1 | x2] (cat((x_path, raw path features)), models.py:362-371) read from its two
+    sources directly; ``prelu`` None is a plain Linear (the head)."""
+
+    @staticmethod
+    def forward(ctx, x1, x2, weight, bias, prelu):
+        z, y = gin_mlp_fwd(x1, weight, bias, prelu, None, comb2=x2)
+        ctx.save_for_backward(x1, x2, weight, prelu, z)
+        return y
+
+    @staticmethod
+    def backward(ctx, g_y):
+        x1, x2, weight, prelu, z = ctx.saved_tensors
+        need_x1, need_x2, need_w, need_b, need_a = ctx.needs_input_grad
+        g_y = _rowmajor(g_y)
+        if prelu is None:   # g_z = g_y; the PReLU-backward kernel with slope 1 yields the bias column sums
+            g_z, _, g_b = prelu_bwd(g_y, g_y, _one(g_y.device))
+            g_a = None
+        else:
+            g_z, g_a, g_b = prelu_bwd(g_y, z, prelu)
+        k1 = x1.size(1)
+        g_w = gemm_tn(g_z, x1, x2) if need_w else None
+        g_x1 = gemm_nt(g_z, weight[:, :k1].t().contiguous()) if need_x1 else None
+        g_x2 = gemm_nt(g_z, weight[:, k1:].t().contiguous()) if (need_x2 and x2 is not None) else None
+        return (g_x1, g_x2, g_w, (g_b if need_b else None),
+                (g_a.view_as(prelu) if (need_a and g_a is not None) else None))
+
+
+def linear_prelu(x1: Tensor, weight: Tensor, bias: Tensor, prelu: Optional[Tensor],
+                 x2: Optional[Tensor] = None) -> Tensor:
+    """prelu([x1 | x2] @ W^T + b) (prelu None: plain Linear), forward and backward on libhgin.so."""
+    require_device(x1, x2, weight, bias, prelu, what="hgin.linear_prelu")
+    x1 = _rowmajor(_f32(x1, "x"))
+    if x2 is not None:
+        x2 = _rowmajor(_f32(x2, "x2"))
+        if x2.size(0) != x1.size(0):
+            raise RuntimeError("linear_prelu: x1 / x2 row counts differ")
+    width = x1.size(1) + (x2.size(1) if x2 is not None else 0)
+    if weight.size(1) != width:
+        raise RuntimeError(f"mat1 and mat2 shapes cannot be multiplied ({x1.size(0)}x{width} and "
+                           f"{weight.size(1)}x{weight.size(0)})")
+    return _LinearPReLUFn.apply(x1, x2, _rowmajor(weight), bias.contiguous(), prelu)
 
 
 def aggregate(x_src: Tensor, x_dst: Optional[Tensor], eps: Optional[Tensor], graph: RelationGraph,
@@ -334,5 +425,5 @@ def gin_conv(x_src: Tensor, x_dst: Tensor, eps: Tensor, weight: Tensor, bias: Te
         raise RuntimeError(f"mat1 and mat2 shapes cannot be multiplied ({graph.n_dst}x{width} and "
                            f"{weight.size(1)}x{weight.size(0)})")
     if accum is not None:
-        accum = _rowmajor(accum)
+        accum = accum.contiguous()      # the epilogue reads accum with row stride N
     return _GINConvFn.apply(x_src, x_dst, eps, _rowmajor(weight), bias.contiguous(), prelu, accum, graph, mode)

@@ -96,18 +96,26 @@ int hgin_combine_bwd_f32(const float* g, int64_t ld_g, const float* x_dst, int64
  * Replaces GINLayer.mlp = Sequential(Linear(K, N), PReLU()) applied at models.py:217 (built at
  * models.py:236-239) and, when `accum` != NULL, the per-dst-type sum of HeteroConv(aggr='sum')
  * (models.py:286-298) for the second relation into the same node type:
- *   z = a @ w^T + bias;  y = (z > 0 ? z : prelu[0] * z) [+ accum]
- * a: [M, K] (lda), w: [N, K] row-major (torch Linear.weight), bias: [N], prelu: device float[1].
+ *   z = [a1 | a2] @ w^T + bias;  y = (z > 0 ? z : prelu[0] * z) [+ accum]
+ * The A operand is the column concatenation of a1 ([M, k1], lda1) and a2 ([M, K - k1], lda2; NULL when
+ * k1 == K), which also replaces the readout's torch.cat((x_path, raw path features)) (models.py:362-371).
+ * w: [N, K] row-major (torch Linear.weight), bias: [N], prelu: device float[1].  Output rows are N wide.
  * z (pre-activation, saved for backward) may be NULL.  fp32 in, fp32 MFMA (v_mfma_f32_32x32x2_f32). */
-int hgin_gin_mlp_fwd_f32(const float* a, int64_t lda, const float* w, const float* bias,
-                         const float* prelu, const float* accum, float* z, float* y,
-                         int64_t M, int64_t N, int64_t K, void* stream);
+int hgin_gin_mlp_fwd_f32(const float* a1, int64_t lda1, int64_t k1, const float* a2, int64_t lda2,
+                         const float* w, const float* bias, const float* prelu, const float* accum,
+                         float* z, float* y, int64_t M, int64_t N, int64_t K, void* stream);
+
+/* ---- readout Linear without activation (models.py:326-330, the head Linear(mlp_layers[-1], 1)) ------
+ *   y = [a1 | a2] @ w^T + bias     (same operand conventions as hgin_gin_mlp_fwd_f32) */
+int hgin_linear_fwd_f32(const float* a1, int64_t lda1, int64_t k1, const float* a2, int64_t lda2,
+                        const float* w, const float* bias, float* y, int64_t M, int64_t N, int64_t K,
+                        void* stream);
 
 /* ---- A9: PReLU + bias backward -------------------------------------------------------------------
  *   g_z = z > 0 ? g_y : prelu[0] * g_y;  g_prelu[0] = sum (z > 0 ? 0 : z * g_y);  g_bias[n] = sum_m g_z[m, n]
  * Deterministic (fixed-shape two-level reductions).  workspace: hgin_prelu_bwd_workspace_size. */
 int hgin_prelu_bwd_workspace_size(int64_t M, int64_t N, size_t* bytes);
-int hgin_prelu_bwd_f32(const float* g_y, const float* z, int64_t M, int64_t N, const float* prelu,
+int hgin_prelu_bwd_f32(const float* g_y, int64_t ld_gy, const float* z, int64_t M, int64_t N, const float* prelu,
                        float* g_z, float* g_prelu, float* g_bias, void* workspace,
                        size_t workspace_bytes, void* stream);
 
@@ -115,6 +123,15 @@ int hgin_prelu_bwd_f32(const float* g_y, const float* z, int64_t M, int64_t N, c
  * c[M, N] = a[M, K] @ b[N, K]^T   ("NT", both operands K-contiguous), fp32 MFMA. */
 int hgin_gemm_nt_f32(const float* a, int64_t lda, const float* b, int64_t ldb, float* c, int64_t ldc,
                      int64_t M, int64_t N, int64_t K, void* stream);
+
+/* ---- weight-gradient GEMM (backward of Linear: dW = g_z^T X) ----------------------------------------
+ * out[N, K] = a[M, N]^T @ [b1 | b2],  b1 = columns [0, k1) ([M, k1], ldb1), b2 = columns [k1, K) ([M, K-k1],
+ * ldb2; may be NULL when k1 == K).  Reduction over M split across workgroups into fp32 slabs summed in a
+ * fixed order (deterministic).  workspace: hgin_gemm_tn_workspace_size. */
+int hgin_gemm_tn_workspace_size(int64_t M, int64_t N, int64_t K, size_t* bytes);
+int hgin_gemm_tn_f32(const float* a, int64_t lda, const float* b1, int64_t ldb1, int64_t k1, const float* b2,
+                     int64_t ldb2, int64_t M, int64_t N, int64_t K, float* out, int64_t ldo, void* workspace,
+                     size_t workspace_bytes, void* stream);
 
 /* ---- A10: negative-edge sampler (NOT IN REFERENCE; build-defined) --------------
  * out[i] = hi32( philox4x32_10(counter = {lo32(offset+i), hi32(offset+i), 0, 0},

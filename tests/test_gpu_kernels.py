@@ -163,6 +163,40 @@ def test_gemm_layout_identity_asymmetric():
     assert torch.equal(c, b.t())
 
 
+@pytest.mark.parametrize("M,N,K1,K2", [(1, 1, 1, 0), (1000, 128, 256, 0), (600, 128, 128, 128), (777, 100, 6, 3),
+                                       (50000, 128, 256, 0), (33, 256, 64, 40), (0, 8, 4, 0)])
+def test_gemm_tn(M, N, K1, K2):
+    a = torch.randn(M, N, device=DEV)
+    b1 = torch.randn(M, K1, device=DEV)
+    b2 = torch.randn(M, K2, device=DEV) if K2 else None
+    out = ops.gemm_tn(a, b1, b2)
+    b = b1 if b2 is None else torch.cat((b1, b2), 1)
+    ref = a.double().t() @ b.double()
+    assert ((out.double() - ref).abs() <= 1e-5 * (a.double().abs().t() @ b.double().abs() + 1)).all()
+    again = ops.gemm_tn(a, b1, b2)
+    assert torch.equal(out, again)     # deterministic
+
+
+def test_linear_prelu_autograd():
+    x = torch.randn(3000, 256, device=DEV, requires_grad=True)
+    lin = torch.nn.Linear(256, 128).to(DEV)
+    act = torch.nn.PReLU().to(DEV)
+    y = ops.linear_prelu(x, lin.weight, lin.bias, act.weight)
+    g = torch.randn_like(y)
+    y.backward(g)
+    got = [x.grad, lin.weight.grad, lin.bias.grad, act.weight.grad]
+    x2 = x.detach().double().requires_grad_()
+    l2 = torch.nn.Linear(256, 128).double().to(DEV)
+    l2.load_state_dict(lin.state_dict())
+    a2 = torch.nn.PReLU().double().to(DEV)
+    a2.load_state_dict(act.state_dict())
+    y2 = a2(l2(x2))
+    assert torch.allclose(y.double(), y2, rtol=1e-5, atol=1e-5)
+    y2.backward(g.double())
+    for a, b in zip(got, [x2.grad, l2.weight.grad, l2.bias.grad, a2.weight.grad]):
+        assert float((a.double() - b).norm() / b.norm()) < 1e-5
+
+
 @pytest.mark.parametrize("M,N,K", [(200, 64, 128), (1, 256, 3), (1031, 100, 77)])
 def test_gemm_nt(M, N, K):
     a = torch.randn(M, K, device=DEV)
@@ -184,9 +218,19 @@ def test_prelu_bwd(M, N):
     zr = z.double()
     ga_ref = (torch.where(zr > 0, torch.zeros_like(zr), zr) * gy.double()).sum()
     assert abs(float(g_a) - float(ga_ref)) <= 1e-5 * (float((zr * gy.double()).abs().sum()) + 1)
-    assert torch.allclose(g_b.double(), g_z.double().sum(0), rtol=1e-5, atol=1e-5)
+    assert ((g_b.double() - g_z.double().sum(0)).abs() <= 1e-5 * g_z.double().abs().sum(0) + 1e-6).all()
     again = ops.prelu_bwd(gy, z, a)
     assert torch.equal(again[1], g_a) and torch.equal(again[2], g_b)   # deterministic
+
+
+def test_prelu_bwd_strided_grad():
+    """The incoming gradient is often a column slice (cat backward of the readout input)."""
+    z = torch.randn(500, 64, device=DEV)
+    big = torch.randn(500, 100, device=DEV)
+    gy = big[:, 7:71]
+    a = torch.tensor([0.2], device=DEV)
+    g_z, g_a, g_b = ops.prelu_bwd(gy, z, a)
+    assert torch.equal(g_z, torch.where(z > 0, gy, a * gy))
 
 
 def test_combine_bwd():
@@ -229,3 +273,34 @@ def test_dot_decoder():
     assert np.array_equal(zs_t.grad.cpu().numpy(), co.dot_decode_bwd(rp, col, perm, g.cpu().numpy(), zd))
     rp, col, perm, _ = co.csr_build(np.stack([src, dst]), 1, n_dst, n_src)
     assert np.array_equal(zd_t.grad.cpu().numpy(), co.dot_decode_bwd(rp, col, perm, g.cpu().numpy(), zs))
+
+
+@pytest.mark.parametrize("M,K1,K2,N,act", [(3000, 128, 128, 128, True), (777, 8, 3, 128, True), (2000, 32, 0, 1, False),
+                                           (513, 6, 5, 7, False)])
+def test_linear_two_source_autograd(M, K1, K2, N, act):
+    """The readout's Linear(+PReLU) reading cat((x1, x2)) from two sources, vs a float64 torch reference."""
+    x1 = torch.randn(M, K1, device=DEV, requires_grad=True)
+    x2 = torch.randn(M, K2, device=DEV, requires_grad=True) if K2 else None
+    lin = torch.nn.Linear(K1 + K2, N).to(DEV)
+    a = torch.nn.PReLU().to(DEV) if act else None
+    y = ops.linear_prelu(x1, lin.weight, lin.bias, a.weight if act else None, x2=x2)
+    g = torch.randn_like(y)
+    y.backward(g)
+    x = torch.cat((x1, x2), 1) if K2 else x1
+    xr = x.detach().double().requires_grad_()
+    wr = lin.weight.detach().double().requires_grad_()
+    br = lin.bias.detach().double().requires_grad_()
+    zr = xr @ wr.t() + br
+    if act:
+        ar = a.weight.detach().double().requires_grad_()
+        yr = torch.where(zr > 0, zr, ar * zr)
+    else:
+        yr = zr
+    assert torch.allclose(y.double(), yr, rtol=1e-5, atol=1e-5)
+    yr.backward(g.double())
+    gx = torch.cat((x1.grad, x2.grad), 1) if K2 else x1.grad
+    pairs = [(gx, xr.grad), (lin.weight.grad, wr.grad), (lin.bias.grad, br.grad)]
+    if act:
+        pairs.append((a.weight.grad, ar.grad))
+    for got, want in pairs:
+        assert float((got.double() - want).norm()) <= 1e-5 * float(want.norm()) + 1e-6

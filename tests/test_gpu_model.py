@@ -77,6 +77,7 @@ def test_forward_backward_step_vs_reference(case):
     assert _close(lv, fx["loss_value"])
     torch.sqrt(lv).backward()
     no_grad = set(fx["meta"]["no_grad_params"])
+    g_scale = max(float(fx["grad." + n].double().norm()) for n, _ in model.named_parameters() if n not in no_grad)
     grads = {}
     for n, p in model.named_parameters():
         if n in no_grad:
@@ -84,16 +85,22 @@ def test_forward_backward_step_vs_reference(case):
             continue
         ref = fx["grad." + n]
         grads[n] = ref
-        assert _rel(p.grad, ref) < 1e-4, (n, _rel(p.grad, ref))
+        # 1e-4 of the gradient's norm, with a floor of 1e-6 of the model's largest gradient norm for gradients
+        # that are identically zero in exact arithmetic (a Linear bias feeding a training-mode BatchNorm: both
+        # sides are rounding noise)
+        err = float((p.grad.double().cpu() - ref.double()).norm())
+        assert err <= 1e-4 * float(ref.double().norm()) + 1e-6 * g_scale, (n, err, float(ref.norm()))
     opt.step()
     for n, p in model.named_parameters():
         ref = fx["step." + n]
         if n in no_grad:
             assert torch.equal(p.detach().cpu(), ref), n
             continue
-        g = grads[n].abs()
-        # Adam's first step moves each weight by ~lr * sign(g); where g is ~0 the sign is noise.
-        tol = torch.where(g > 1e-3 * g.max(), torch.full_like(g, 2e-5), torch.full_like(g, 2.1e-3))
+        g = grads[n].abs().double()
+        # Adam's first step moves each weight by ~lr * sign(g): where |g| is within the gradient error bound
+        # asserted above, the sign may legitimately differ and the weight may move by up to 2 * lr.
+        bound = 1e-4 * float(g.norm()) + 1e-6 * g_scale
+        tol = torch.where(g > bound, torch.full_like(g, 2e-5), torch.full_like(g, 2.1e-3)).float()
         assert ((p.detach().cpu() - ref).abs() <= tol).all(), n
 
 
