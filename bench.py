@@ -101,10 +101,16 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus and rank == 0:
         print(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    # One rank per GPU.  HGIN_DIST_BACKEND=gloo (+ more ranks than GPUs) is only for rehearsing the
+    # multi-rank path on a 1-GPU box; the measured runs use RCCL ("nccl" on ROCm) over xGMI.
+    backend = os.environ.get("HGIN_DIST_BACKEND", "nccl")
+    dev = torch.device("cuda", local % max(torch.cuda.device_count(), 1))
+    torch.cuda.set_device(dev)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
     _lib.lib()
 
     cfg = CONFIGS[args.config]
@@ -118,7 +124,7 @@ def main():
 
     def barrier():
         if world > 1:
-            dist.barrier(device_ids=[local])
+            dist.barrier(device_ids=[dev.index]) if backend == "nccl" else dist.barrier()
 
     for _ in range(args.warmup):
         train_step(model, opt, graph, reducer=reducer)
@@ -188,7 +194,7 @@ def main():
             out["cpu_baseline"] = None
         print(json.dumps(out), flush=True)
     if world > 1:
-        dist.barrier(device_ids=[local])
+        barrier()
         dist.destroy_process_group()
     return out
 
