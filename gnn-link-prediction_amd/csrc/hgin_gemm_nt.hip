@@ -72,7 +72,7 @@ __device__ __forceinline__ void store_tile(float* __restrict__ dst, const float4
     *reinterpret_cast<float4*>(dst + ((tid >> 3) + 32 * i) * kLds + (tid & 7) * 4) = r[i];
 }
 
-template <int EPI, bool kVec, bool kPF, int kOcc>
+template <int EPI, bool kVec, bool kPF, int kOcc, bool kPersist>
 __global__ __launch_bounds__(256, kOcc) void k_gemm_nt(Src2 A, Src2 B, int64_t M, int64_t N, int64_t K,
                                                     const float* __restrict__ bias, const float* __restrict__ prelu,
                                                     const float* __restrict__ accum, float* __restrict__ Z,
@@ -85,10 +85,28 @@ __global__ __launch_bounds__(256, kOcc) void k_gemm_nt(Src2 A, Src2 B, int64_t M
   const int wave = tid >> 6;
   const int wm = wave >> 1;
   const int wn = wave & 1;
-  const int64_t m0 = (int64_t)blockIdx.x * kBM;
-  const int64_t n0 = (int64_t)blockIdx.y * kBN;
   const int li = lane & 31;
   const int lh = lane >> 5;
+  // Persistent: a workgroup walks output tiles tile, tile + gridDim.x, ... (M-tiles inner, so workgroups
+  // running together share the W tile in L2).  The first K-tile of the NEXT output tile is fetched into
+  // registers during the last K-tile's MFMAs and lands in LDS after the epilogue, so the z / y store tail
+  // overlaps the next tile's HBM reads.
+  const int64_t tiles_m = (M + kBM - 1) / kBM;
+  const int64_t n_tiles = tiles_m * ((N + kBN - 1) / kBN);
+  float4 ra[4], rb[4];
+  int64_t tile = blockIdx.x;
+  if (tile < n_tiles) {
+    load_tile<kVec>(ra, A, (tile % tiles_m) * kBM, M, 0, K, tid);
+    load_tile<kVec>(rb, B, (tile / tiles_m) * kBN, N, 0, K, tid);
+    store_tile(As, ra, tid);
+    store_tile(Bs, rb, tid);
+  }
+  __syncthreads();
+  for (; tile < n_tiles; tile += gridDim.x) {
+  const int64_t m0 = (tile % tiles_m) * kBM;
+  const int64_t n0 = (tile / tiles_m) * kBN;
+  const int64_t next = tile + gridDim.x;
+  const bool has_next = kPersist && next < n_tiles;
 
   f32x16 acc[2][2];
 #pragma unroll
@@ -98,17 +116,14 @@ __global__ __launch_bounds__(256, kOcc) void k_gemm_nt(Src2 A, Src2 B, int64_t M
 #pragma unroll
       for (int e = 0; e < 16; ++e) acc[a][b][e] = 0.0f;
 
-  float4 ra[4], rb[4];
-  load_tile<kVec>(ra, A, m0, M, 0, K, tid);
-  load_tile<kVec>(rb, B, n0, N, 0, K, tid);
-  store_tile(As, ra, tid);
-  store_tile(Bs, rb, tid);
-  __syncthreads();
   for (int64_t k0 = 0; k0 < K; k0 += kBK) {
     const bool more = k0 + kBK < K;
-    if (kPF && more) {   // next tile's global loads stay in flight under this tile's MFMAs
+    if (kPF && more) {   // next K-tile's global loads stay in flight under this K-tile's MFMAs
       load_tile<kVec>(ra, A, m0, M, k0 + kBK, K, tid);
       load_tile<kVec>(rb, B, n0, N, k0 + kBK, K, tid);
+    } else if (kPF && has_next) {   // last K-tile: fetch the next output tile's first K-tile
+      load_tile<kVec>(ra, A, (next % tiles_m) * kBM, M, 0, K, tid);
+      load_tile<kVec>(rb, B, (next / tiles_m) * kBN, N, 0, K, tid);
     }
 #pragma unroll
     for (int c = 0; c < kBK / 8; ++c) {
@@ -155,7 +170,7 @@ __global__ __launch_bounds__(256, kOcc) void k_gemm_nt(Src2 A, Src2 B, int64_t M
 #pragma unroll
       for (int e = 0; e < 16; ++e) Cw[((e & 3) + 8 * (e >> 2) + 4 * lh) * kLc + tn * 32 + li] = acc[tm][tn][e];
     __syncthreads();
-#pragma unroll
+#pragma unroll 2
     for (int j = 0; j < 8; ++j) {
       const int q = lane + 64 * j;
       const int r = q >> 4;
@@ -199,6 +214,27 @@ __global__ __launch_bounds__(256, kOcc) void k_gemm_nt(Src2 A, Src2 B, int64_t M
     }
     if (tm == 0) __syncthreads();
   }
+  if (has_next) {
+    __syncthreads();   // every wave has read its C tile out of LDS
+    if (!kPF) {
+      load_tile<kVec>(ra, A, (next % tiles_m) * kBM, M, 0, K, tid);
+      load_tile<kVec>(rb, B, (next / tiles_m) * kBN, N, 0, K, tid);
+    }
+    store_tile(As, ra, tid);
+    store_tile(Bs, rb, tid);
+    __syncthreads();
+  }
+  }  // tile loop
+}
+
+// Resident workgroups of one instantiation on this device (VGPR / LDS limited), for the persistent grid.
+template <typename Kern>
+int64_t resident_blocks(Kern kernel) {
+  int dev = 0, cus = 0, per_cu = 0;
+  if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) !=
+      hipSuccess || hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, 256, 0) != hipSuccess)
+    return 1024;
+  return (int64_t)cus * (per_cu > 0 ? per_cu : 1);
 }
 
 template <int EPI>
@@ -208,25 +244,26 @@ int launch_nt(const Src2& a, const Src2& b, int64_t M, int64_t N, int64_t K, con
                    a.ld2 % 4 == 0)) && aligned16(b.p1) && b.ld1 % 4 == 0;
   const bool vec_out = ldc % 4 == 0 && aligned16(y) && (z == nullptr || aligned16(z)) &&
                        (accum == nullptr || aligned16(accum));
-  dim3 grid((unsigned)ceil_div(M, kBM), (unsigned)ceil_div(N, kBN));
+  const int64_t n_tiles = ceil_div(M, kBM) * ceil_div(N, kBN);
   static const int variant = [] {
     const char* v = getenv("HGIN_NT_VARIANT");
     return v ? atoi(v) : 0;
   }();
-#define HGIN_NT_LAUNCH(PF, OCC)                                                                               \
-  do {                                                                                                     \
-    if (vec)                                                                                               \
-      k_gemm_nt<EPI, true, PF, OCC><<<grid, 256, 0, s>>>(a, b, M, N, K, bias, prelu, accum, z, y, ldc, vec_out);  \
-    else                                                                                                   \
-      k_gemm_nt<EPI, false, PF, OCC><<<grid, 256, 0, s>>>(a, b, M, N, K, bias, prelu, accum, z, y, ldc, vec_out); \
+#define HGIN_NT_LAUNCH(PF, OCC, PERSIST)                                                                         \
+  do {                                                                                                        \
+    auto kern = vec ? k_gemm_nt<EPI, true, PF, OCC, PERSIST> : k_gemm_nt<EPI, false, PF, OCC, PERSIST>;        \
+    static int64_t resident[2] = {0, 0};                                                                      \
+    if (PERSIST && !resident[vec]) resident[vec] = resident_blocks(kern);                                     \
+    const int64_t g = (PERSIST && n_tiles > resident[vec]) ? resident[vec] : n_tiles;                         \
+    kern<<<dim3((unsigned)(g > 0 ? g : 1)), 256, 0, s>>>(a, b, M, N, K, bias, prelu, accum, z, y, ldc, vec_out); \
   } while (0)
   // Measured on MI355X (tools/gemm_bench.py, profiles/r01_gemm_variants.txt): register prefetch at 3 waves
   // per SIMD (160 VGPRs) beats 2 waves (172 VGPRs) by 7-14 % and the unpipelined loop by 3-6 %; forcing 4
   // waves spills.  The other variants stay selectable for re-measurement (HGIN_NT_VARIANT).
   switch (variant) {
-    case 1: HGIN_NT_LAUNCH(true, 2); break;
-    case 2: HGIN_NT_LAUNCH(false, 3); break;
-    default: HGIN_NT_LAUNCH(true, 3); break;
+    case 1: HGIN_NT_LAUNCH(true, 2, true); break;
+    case 2: HGIN_NT_LAUNCH(true, 2, false); break;
+    default: HGIN_NT_LAUNCH(true, 3, false); break;
   }
 #undef HGIN_NT_LAUNCH
   return check_launch(what);

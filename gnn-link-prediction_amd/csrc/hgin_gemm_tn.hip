@@ -25,7 +25,8 @@ using f32x16 = __attribute__((ext_vector_type(16))) float;
 constexpr int kTnBM = 32;       // rows of M per stage
 constexpr int kTnLd = 128 + 4;
 
-__global__ __launch_bounds__(256, 2) void k_gemm_tn_partial(const float* __restrict__ A, int64_t lda,
+template <bool kPF, int kOcc>
+__global__ __launch_bounds__(256, kOcc) void k_gemm_tn_partial(const float* __restrict__ A, int64_t lda,
                                                             const float* __restrict__ B1, int64_t ldb1,
                                                             const float* __restrict__ B2, int64_t ldb2, int64_t K1,
                                                             int64_t M, int64_t N, int64_t K, int64_t rows_per_split,
@@ -52,27 +53,29 @@ __global__ __launch_bounds__(256, 2) void k_gemm_tn_partial(const float* __restr
       for (int e = 0; e < 16; ++e) acc[a][b][e] = 0.0f;
 
   const int c4 = (tid & 31) * 4;   // column (x4) inside the 128-wide tile
-  for (int64_t m0 = mb; m0 < me; m0 += kTnBM) {
+  float4 va[4], vb[4];
+  // one 32-row stage of A[:, n0:n0+128] and [B1|B2][:, k0:k0+128] into registers (4 + 4 float4 per thread)
+  auto load_stage = [&](int64_t m0) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const int r = (tid >> 5) + 8 * i;
-      const int64_t gm = m0 + r;
-      float4 va = make_float4(0.f, 0.f, 0.f, 0.f), vb = va;
+      const int64_t gm = m0 + (tid >> 5) + 8 * i;
+      va[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+      vb[i] = va[i];
       if (gm < me) {
         const int64_t gn = n0 + c4;
         const float* pa = A + gm * lda + gn;
         if (vec && gn + 3 < N) {
-          va = *reinterpret_cast<const float4*>(pa);
+          va[i] = *reinterpret_cast<const float4*>(pa);
         } else {
-          if (gn + 0 < N) va.x = pa[0];
-          if (gn + 1 < N) va.y = pa[1];
-          if (gn + 2 < N) va.z = pa[2];
-          if (gn + 3 < N) va.w = pa[3];
+          if (gn + 0 < N) va[i].x = pa[0];
+          if (gn + 1 < N) va[i].y = pa[1];
+          if (gn + 2 < N) va[i].z = pa[2];
+          if (gn + 3 < N) va[i].w = pa[3];
         }
         const int64_t gk = k0 + c4;
         if (vec && gk + 3 < K && (gk + 3 < K1 || gk >= K1)) {
           const float* pb = gk < K1 ? B1 + gm * ldb1 + gk : B2 + gm * ldb2 + (gk - K1);
-          vb = *reinterpret_cast<const float4*>(pb);
+          vb[i] = *reinterpret_cast<const float4*>(pb);
         } else {
           float t[4];
 #pragma unroll
@@ -80,13 +83,26 @@ __global__ __launch_bounds__(256, 2) void k_gemm_tn_partial(const float* __restr
             const int64_t k = gk + c;
             t[c] = k < K ? (k < K1 ? B1[gm * ldb1 + k] : B2[gm * ldb2 + (k - K1)]) : 0.0f;
           }
-          vb = make_float4(t[0], t[1], t[2], t[3]);
+          vb[i] = make_float4(t[0], t[1], t[2], t[3]);
         }
       }
-      *reinterpret_cast<float4*>(As + r * kTnLd + c4) = va;
-      *reinterpret_cast<float4*>(Bs + r * kTnLd + c4) = vb;
     }
-    __syncthreads();
+  };
+  auto store_stage = [&]() {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int r = (tid >> 5) + 8 * i;
+      *reinterpret_cast<float4*>(As + r * kTnLd + c4) = va[i];
+      *reinterpret_cast<float4*>(Bs + r * kTnLd + c4) = vb[i];
+    }
+  };
+  // Register-prefetch pipeline (as in hgin_gemm_nt.hip): stage s+1 is loaded under stage s's MFMAs.
+  load_stage(mb);
+  store_stage();
+  __syncthreads();
+  for (int64_t m0 = mb; m0 < me; m0 += kTnBM) {
+    const bool more = m0 + kTnBM < me;
+    if (kPF && more) load_stage(m0 + kTnBM);
 #pragma unroll
     for (int st = 0; st < kTnBM / 2; ++st) {
       const int row = 2 * st + lh;
@@ -102,7 +118,12 @@ __global__ __launch_bounds__(256, 2) void k_gemm_tn_partial(const float* __restr
         for (int tn = 0; tn < 2; ++tn)
           acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[tm], fb[tn], acc[tm][tn], 0, 0, 0);
     }
-    __syncthreads();
+    if (more) {
+      __syncthreads();
+      if (!kPF) load_stage(m0 + kTnBM);
+      store_stage();
+      __syncthreads();
+    }
   }
   float* out = slab + (int64_t)blockIdx.z * N * K;
 #pragma unroll
@@ -253,7 +274,18 @@ extern "C" int hgin_gemm_tn_f32(const float* a, int64_t lda, const float* b1, in
     k_tn_small<<<(unsigned)S_eff, 256, 0, s>>>(a, lda, b1, ldb1, b2, ldb2, k1, M, (int)N, (int)K, rows, slab);
   } else {
     dim3 grid((unsigned)ceil_div(N, 128), (unsigned)ceil_div(K, 128), (unsigned)S_eff);
-    k_gemm_tn_partial<<<grid, 256, 0, s>>>(a, lda, b1, ldb1, b2, ldb2, k1, M, N, K, rows, vec, slab);
+    static const int variant = [] {
+      const char* v = getenv("HGIN_TN_VARIANT");
+      return v ? atoi(v) : 0;
+    }();
+    // Measured (profiles/r01_tn_variants.txt): register prefetch at 3 waves/SIMD is 12 % faster than the
+    // unpipelined loop and 3-5 % faster than prefetch at 2 waves.
+    if (variant == 1)
+      k_gemm_tn_partial<false, 2><<<grid, 256, 0, s>>>(a, lda, b1, ldb1, b2, ldb2, k1, M, N, K, rows, vec, slab);
+    else if (variant == 2)
+      k_gemm_tn_partial<true, 2><<<grid, 256, 0, s>>>(a, lda, b1, ldb1, b2, ldb2, k1, M, N, K, rows, vec, slab);
+    else
+      k_gemm_tn_partial<true, 3><<<grid, 256, 0, s>>>(a, lda, b1, ldb1, b2, ldb2, k1, M, N, K, rows, vec, slab);
   }
   const int64_t G = ceil_div(S_eff, kSlabGroup);
   dim3 g1((unsigned)ceil_div(ceil_div(NK, 4), 256), (unsigned)G);

@@ -30,18 +30,38 @@ __device__ __forceinline__ float block_sum_fixed(float v, float* red) {
 // MODE 0: PReLU backward.  in0 = g_y, in1 = z; out = g_z; colsum(g_z) -> part_col; sum(z<=0 ? z*g : 0) -> part_s
 // MODE 1: combine backward.  in0 = g (self-term columns), in1 = x_dst; out = s*g (optional);
 //         part_s = sum(g * x_dst); no column sums.
-template <int MODE>
+// VEC = 4: each thread owns 4 consecutive columns (16-B loads / stores; needs N % 4 == 0 and aligned rows).
+template <int VEC>
+struct RowVec;
+template <>
+struct RowVec<1> {
+  static __device__ __forceinline__ void load(const float* p, float (&v)[1]) { v[0] = *p; }
+  static __device__ __forceinline__ void store(float* p, const float (&v)[1]) { *p = v[0]; }
+};
+template <>
+struct RowVec<4> {
+  static __device__ __forceinline__ void load(const float* p, float (&v)[4]) {
+    const float4 t = *reinterpret_cast<const float4*>(p);
+    v[0] = t.x; v[1] = t.y; v[2] = t.z; v[3] = t.w;
+  }
+  static __device__ __forceinline__ void store(float* p, const float (&v)[4]) {
+    *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
+  }
+};
+
+template <int MODE, int VEC>
 __global__ __launch_bounds__(256) void k_rows_bwd(const float* __restrict__ in0, int64_t ld0,
                                                   const float* __restrict__ in1, int64_t ld1, int64_t M, int N,
                                                   const float* __restrict__ scalar, float* __restrict__ out,
                                                   int64_t ldo, float* __restrict__ part_col,
                                                   float* __restrict__ part_s) {
-  __shared__ float red[256];
+  __shared__ float red[256 * VEC];
   const int t = threadIdx.x;
-  const int CW = N < 256 ? N : 256;
+  const int NU = N / VEC;                 // column units
+  const int CW = NU < 256 ? NU : 256;
   const int RL = 256 / CW;
   const bool active = t < CW * RL;
-  const int c0 = t % CW;
+  const int u0 = t % CW;
   const int rl = t / CW;
   const int64_t r0 = (int64_t)blockIdx.x * kRowsPerBlock;
   const int64_t r1 = r0 + kRowsPerBlock < M ? r0 + kRowsPerBlock : M;
@@ -49,39 +69,64 @@ __global__ __launch_bounds__(256) void k_rows_bwd(const float* __restrict__ in0,
   if (MODE == 0) sc = scalar[0];
   else sc = __fadd_rn(1.0f, scalar[0]);
   float ssum = 0.0f;
-  const int iters = (N + CW - 1) / CW;
+  const int iters = (NU + CW - 1) / CW;
   for (int it = 0; it < iters; ++it) {
-    const int c = c0 + it * CW;
-    float csum = 0.0f;
+    const int c = (u0 + it * CW) * VEC;
+    float csum[VEC];
+#pragma unroll
+    for (int q = 0; q < VEC; ++q) csum[q] = 0.0f;
     if (active && c < N) {
       for (int64_t r = r0 + rl; r < r1; r += RL) {
-        const float g = in0[r * ld0 + c];
-        const float x = in1[r * ld1 + c];
-        if (MODE == 0) {
-          const bool pos = x > 0.0f;
-          const float gz = pos ? g : __fmul_rn(sc, g);
-          out[r * ldo + c] = gz;
-          csum = __fadd_rn(csum, gz);
-          if (!pos) ssum = __fadd_rn(ssum, __fmul_rn(x, g));
-        } else {
-          if (out) out[r * ldo + c] = __fmul_rn(sc, g);
-          ssum = __fadd_rn(ssum, __fmul_rn(g, x));
+        float g[VEC], x[VEC], o[VEC];
+        RowVec<VEC>::load(in0 + r * ld0 + c, g);
+        RowVec<VEC>::load(in1 + r * ld1 + c, x);
+#pragma unroll
+        for (int q = 0; q < VEC; ++q) {
+          if (MODE == 0) {
+            const bool pos = x[q] > 0.0f;
+            o[q] = pos ? g[q] : __fmul_rn(sc, g[q]);
+            csum[q] = __fadd_rn(csum[q], o[q]);
+            if (!pos) ssum = __fadd_rn(ssum, __fmul_rn(x[q], g[q]));
+          } else {
+            o[q] = __fmul_rn(sc, g[q]);
+            ssum = __fadd_rn(ssum, __fmul_rn(g[q], x[q]));
+          }
         }
+        if (MODE == 0 || out) RowVec<VEC>::store(out + r * ldo + c, o);
       }
     }
     if (MODE == 0) {
-      red[t] = csum;
+#pragma unroll
+      for (int q = 0; q < VEC; ++q) red[t * VEC + q] = csum[q];
       __syncthreads();
       if (active && rl == 0 && c < N) {
-        float tot = 0.0f;
-        for (int j = 0; j < RL; ++j) tot = __fadd_rn(tot, red[j * CW + c0]);
-        part_col[(int64_t)c * gridDim.x + blockIdx.x] = tot;   // [N][nblk]: coalesced final pass
+#pragma unroll
+        for (int q = 0; q < VEC; ++q) {
+          float tot = 0.0f;
+          for (int j = 0; j < RL; ++j) tot = __fadd_rn(tot, red[(j * CW + u0) * VEC + q]);
+          part_col[(int64_t)(c + q) * gridDim.x + blockIdx.x] = tot;   // [N][nblk]: coalesced final pass
+        }
       }
       __syncthreads();
     }
   }
   const float bs = block_sum_fixed(ssum, red);
   if (t == 0) part_s[blockIdx.x] = bs;
+}
+
+template <int MODE>
+void launch_rows_bwd(bool vec, unsigned nblk, hipStream_t s, const float* in0, int64_t ld0, const float* in1,
+                     int64_t ld1, int64_t M, int N, const float* scalar, float* out, int64_t ldo, float* part_col,
+                     float* part_s) {
+  if (vec)
+    k_rows_bwd<MODE, 4><<<nblk, 256, 0, s>>>(in0, ld0, in1, ld1, M, N, scalar, out, ldo, part_col, part_s);
+  else
+    k_rows_bwd<MODE, 1><<<nblk, 256, 0, s>>>(in0, ld0, in1, ld1, M, N, scalar, out, ldo, part_col, part_s);
+}
+
+bool rows_vec_ok(int64_t N, const float* a, int64_t lda, const float* b, int64_t ldb, const float* c, int64_t ldc) {
+  return N % 4 == 0 && aligned16(a) && lda % 4 == 0 && aligned16(b) && ldb % 4 == 0 &&
+         (c == nullptr || (aligned16(c) && ldc % 4 == 0));
 }
 
 // Sum block partials in a fixed order: one workgroup per column, strided per-thread sums + fixed tree.
@@ -139,7 +184,8 @@ extern "C" int hgin_prelu_bwd_f32(const float* g_y, int64_t ld_gy, const float* 
   float* part_col = static_cast<float*>(workspace);
   float* part_s = reinterpret_cast<float*>(static_cast<char*>(workspace) +
                                            align_up(sizeof(float) * (size_t)(nblk * N), 256));
-  k_rows_bwd<0><<<(unsigned)nblk, 256, 0, s>>>(g_y, ld_gy, z, N, M, (int)N, prelu, g_z, N, part_col, part_s);
+  launch_rows_bwd<0>(rows_vec_ok(N, g_y, ld_gy, z, N, g_z, N), (unsigned)nblk, s, g_y, ld_gy, z, N, M, (int)N,
+                     prelu, g_z, N, part_col, part_s);
   k_final_cols<<<(unsigned)N, 256, 0, s>>>(part_col, nblk, (int)N, g_bias);
   k_final_scalar<<<1, 256, 0, s>>>(part_s, nblk, g_prelu);
   return check_launch("hgin_prelu_bwd_f32");
@@ -169,8 +215,8 @@ extern "C" int hgin_combine_bwd_f32(const float* g, int64_t ld_g, const float* x
   HGIN_ARG_CHECK(g && x_dst, "hgin_combine_bwd_f32: NULL operand");
   const int64_t nblk = ceil_div(n_rows, kRowsPerBlock);
   float* part_s = static_cast<float*>(workspace);
-  k_rows_bwd<1><<<(unsigned)nblk, 256, 0, s>>>(g, ld_g, x_dst, ld_dst, n_rows, (int)f_dst, eps, g_x_dst, ld_gx,
-                                               nullptr, part_s);
+  launch_rows_bwd<1>(rows_vec_ok(f_dst, g, ld_g, x_dst, ld_dst, g_x_dst, ld_gx), (unsigned)nblk, s, g, ld_g, x_dst,
+                     ld_dst, n_rows, (int)f_dst, eps, g_x_dst, ld_gx, nullptr, part_s);
   k_final_scalar<<<1, 256, 0, s>>>(part_s, nblk, g_eps);
   return check_launch("hgin_combine_bwd_f32");
 }
