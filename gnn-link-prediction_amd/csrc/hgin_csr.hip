@@ -83,6 +83,56 @@ __global__ __launch_bounds__(1024) void k_scan_exclusive(uint32_t* __restrict__ 
   }
 }
 
+// Multi-workgroup exclusive scan for large count arrays: (1) per-4096-chunk sums, (2) one-workgroup scan of
+// the chunk sums (k_scan_exclusive), (3) per-chunk scan with the chunk offset.
+constexpr int kScanChunk = 4096;   // 256 threads x 16
+
+__global__ __launch_bounds__(256) void k_scan_reduce(const uint32_t* __restrict__ data, int64_t n,
+                                                     uint32_t* __restrict__ sums) {
+  __shared__ uint32_t red[256];
+  const int t = threadIdx.x;
+  const int64_t b0 = (int64_t)blockIdx.x * kScanChunk + (int64_t)t * 16;
+  uint32_t s = 0;
+#pragma unroll
+  for (int i = 0; i < 16; ++i)
+    if (b0 + i < n) s += data[b0 + i];
+  red[t] = s;
+  __syncthreads();
+  for (int off = 128; off > 0; off >>= 1) {
+    if (t < off) red[t] += red[t + off];
+    __syncthreads();
+  }
+  if (t == 0) sums[blockIdx.x] = red[0];
+}
+
+__global__ __launch_bounds__(256) void k_scan_apply(uint32_t* __restrict__ data, int64_t n,
+                                                    const uint32_t* __restrict__ offs) {
+  __shared__ uint32_t part[256];
+  const int t = threadIdx.x;
+  const int64_t b0 = (int64_t)blockIdx.x * kScanChunk + (int64_t)t * 16;
+  uint32_t v[16];
+  uint32_t s = 0;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    v[i] = b0 + i < n ? data[b0 + i] : 0u;
+    s += v[i];
+  }
+  part[t] = s;
+  __syncthreads();
+  for (int off = 1; off < 256; off <<= 1) {
+    const uint32_t x = t >= off ? part[t - off] : 0u;
+    __syncthreads();
+    part[t] += x;
+    __syncthreads();
+  }
+  uint32_t run = offs[blockIdx.x] + part[t] - s;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    if (b0 + i < n) data[b0 + i] = run;
+    run += v[i];
+  }
+}
+
 __global__ __launch_bounds__(256) void k_radix_scatter(const uint32_t* __restrict__ kin,
                                                        const uint32_t* __restrict__ vin,
                                                        uint32_t* __restrict__ kout, uint32_t* __restrict__ vout,
@@ -160,7 +210,7 @@ __global__ __launch_bounds__(256) void k_finish(const uint32_t* __restrict__ val
 }
 
 struct CsrWorkspace {
-  size_t keys_a, keys_b, vals_a, vals_b, counts, total;
+  size_t keys_a, keys_b, vals_a, vals_b, counts, sums, total;
 };
 
 CsrWorkspace csr_layout(int64_t E) {
@@ -173,6 +223,7 @@ CsrWorkspace csr_layout(int64_t E) {
   w.vals_a = take(sizeof(uint32_t) * (size_t)(E > 0 ? E : 1));
   w.vals_b = take(sizeof(uint32_t) * (size_t)(E > 0 ? E : 1));
   w.counts = take(sizeof(uint32_t) * (size_t)kBuckets * (size_t)tiles);
+  w.sums = take(sizeof(uint32_t) * (size_t)ceil_div((int64_t)kBuckets * tiles, kScanChunk));
   w.total = off;
   return w;
 }
@@ -219,6 +270,7 @@ extern "C" int hgin_csr_build(const int64_t* edge_index, int64_t E, int key_row,
   uint32_t* va = reinterpret_cast<uint32_t*>(ws + w.vals_a);
   uint32_t* vb = reinterpret_cast<uint32_t*>(ws + w.vals_b);
   uint32_t* counts = reinterpret_cast<uint32_t*>(ws + w.counts);
+  uint32_t* sums = reinterpret_cast<uint32_t*>(ws + w.sums);
   const int64_t tiles = ceil_div(E, kTile);
 
   k_extract<<<grid_for(E), 256, 0, s>>>(edge_index, E, key_row, n_rows, n_cols, ka, va, d_status);
@@ -226,7 +278,15 @@ extern "C" int hgin_csr_build(const int64_t* edge_index, int64_t E, int key_row,
   if (n_rows > 1) bits = 64 - __builtin_clzll((unsigned long long)(n_rows - 1));
   for (int shift = 0; shift < bits; shift += 8) {
     k_radix_hist<<<(unsigned)tiles, kThreads, 0, s>>>(ka, E, shift, counts, tiles);
-    k_scan_exclusive<<<1, 1024, 0, s>>>(counts, (int64_t)kBuckets * tiles);
+    const int64_t nc = (int64_t)kBuckets * tiles;
+    if (nc <= 8 * 1024) {
+      k_scan_exclusive<<<1, 1024, 0, s>>>(counts, nc);
+    } else {
+      const int64_t chunks = ceil_div(nc, kScanChunk);
+      k_scan_reduce<<<(unsigned)chunks, 256, 0, s>>>(counts, nc, sums);
+      k_scan_exclusive<<<1, 1024, 0, s>>>(sums, chunks);
+      k_scan_apply<<<(unsigned)chunks, 256, 0, s>>>(counts, nc, sums);
+    }
     k_radix_scatter<<<(unsigned)tiles, kThreads, 0, s>>>(ka, va, kb, vb, E, shift, counts, tiles);
     uint32_t* t0 = ka; ka = kb; kb = t0;
     uint32_t* t1 = va; va = vb; vb = t1;

@@ -97,8 +97,11 @@ __global__ __launch_bounds__(256, 3) void k_gemm_nt(Src2 A, Src2 B, int64_t M, i
   const int wn = wave % WN;
   const int li = lane & 31;
   const int lh = lane >> 5;
-  const int64_t m0 = (int64_t)blockIdx.x * BM;
-  const int64_t n0 = (int64_t)blockIdx.y * BN;
+  // N-tiles vary fastest: the workgroups reading the same A rows are dispatched back to back, so the second
+  // N-tile finds those rows in the Infinity Cache instead of streaming A from HBM again (N = 256 layers).
+  const int64_t n_tiles_n = (N + BN - 1) / BN;
+  const int64_t m0 = ((int64_t)blockIdx.x / n_tiles_n) * BM;
+  const int64_t n0 = ((int64_t)blockIdx.x % n_tiles_n) * BN;
 
   f32x16 acc[2][TN];
 #pragma unroll
@@ -213,7 +216,7 @@ void launch_nt_tn(bool vec, const Src2& a, const Src2& b, int64_t M, int64_t N, 
                   hipStream_t s) {
   constexpr int BM = (TN == 2 ? 2 : 4) * 64;
   constexpr int BN = (TN == 2 ? 2 : 1) * TN * 32;
-  dim3 grid((unsigned)ceil_div(M, BM), (unsigned)ceil_div(N, BN));
+  dim3 grid((unsigned)(ceil_div(N, BN) * ceil_div(M, BM)));
   if (vec)
     k_gemm_nt<EPI, true, TN><<<grid, 256, 0, s>>>(a, b, M, N, K, bias, prelu, accum, z, y, ldc, vec_out);
   else
