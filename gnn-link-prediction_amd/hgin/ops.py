@@ -133,6 +133,14 @@ class RelationGraph:
         return self._csc
 
 
+def attach_relation_graph(edge_index: Tensor, n_src: int, n_dst: int, csr: Csr, csc: Optional[Csr]) -> RelationGraph:
+    """Register prebuilt CSR / CSC for this edge_index (F1 device collation builds them without a sort)."""
+    g = RelationGraph(edge_index, n_src, n_dst)
+    g._csr, g._csc = csr, csc
+    edge_index._hgin_graphs = (edge_index._version, {(int(n_src), int(n_dst)): g})
+    return g
+
+
 def relation_graph(edge_index: Tensor, n_src: int, n_dst: int) -> RelationGraph:
     """Cached RelationGraph for this edge_index tensor (cache lives on the tensor, keyed by sizes)."""
     key = (int(n_src), int(n_dst))

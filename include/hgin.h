@@ -133,6 +133,29 @@ int hgin_gemm_tn_f32(const float* a, int64_t lda, const float* b1, int64_t ldb1,
                      int64_t ldb2, int64_t M, int64_t N, int64_t K, float* out, int64_t ldo, void* workspace,
                      size_t workspace_bytes, void* stream);
 
+/* ---- F1: device-side batch collation (replaces PyG's host Collater, dataset.py:239-244) -------------
+ * Executes n_desc "segment copy with an integer shift" descriptors in one launch (device array `descs`);
+ * max_count = the largest descriptor count (sizes the grid).  Kinds:
+ *   HGIN_COPY_F32     dst[i] = src[i]            (float, count elements)
+ *   HGIN_COPY_I32_ADD dst[i] = src[i] + add      (int32)
+ *   HGIN_COPY_I64_ADD dst[i] = src[i] + add      (int64)
+ *   HGIN_FILL_I64     dst[i] = add               (int64)
+ *   HGIN_FILL_I32     dst[i] = (int32)add        (int32) */
+#define HGIN_COPY_F32 0
+#define HGIN_COPY_I32_ADD 1
+#define HGIN_COPY_I64_ADD 2
+#define HGIN_FILL_I64 3
+#define HGIN_FILL_I32 4
+typedef struct hgin_copy_desc {
+  const void* src;
+  void* dst;
+  int64_t count;
+  int64_t add;
+  int32_t kind;
+  int32_t reserved;
+} hgin_copy_desc;
+int hgin_batched_copy(const hgin_copy_desc* descs, int64_t n_desc, int64_t max_count, void* stream);
+
 /* ---- A10: negative-edge sampler (NOT IN REFERENCE; build-defined) --------------
  * out[i] = hi32( philox4x32_10(counter = {lo32(offset+i), hi32(offset+i), 0, 0},
  *                              key = {lo32(seed), hi32(seed)}).x  *  n_dst ),  i in [0, n)
