@@ -16,6 +16,7 @@ bracketed K steps) / K.  Rank 0 prints one JSON line.
 from __future__ import annotations
 
 import argparse
+import dataclasses
 import json
 import os
 import sys
@@ -32,6 +33,7 @@ import torch.distributed as dist  # noqa: E402
 METRIC = json.load(open(os.path.join(ROOT, "BASELINE.json")))["metric"]
 HBM_PEAK_GBS = 8000.0        # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
 F32_MFMA_PEAK_TFS = 157.3    # v_mfma_f32_32x32x2_f32 dense peak (= f32 vector peak)
+BF16_MFMA_PEAK_TFS = 2500.0  # v_mfma_f32_32x32x16_bf16 dense peak (no sparsity)
 
 
 def parse():
@@ -39,7 +41,8 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", default="cfg2", help="cfg2 (default, BASELINE configs[1]), cfg3, cfg4c")
+    ap.add_argument("--config", default="cfg2",
+                    help="cfg2 (default, BASELINE configs[1]), cfg3, cfg4c, cfg5 (bf16), cfg2bf (bf16 at cfg2 size)")
     ap.add_argument("--prune-dead", action="store_true", help="skip dead relations (reported separately)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-steps", type=int, default=2)
@@ -67,6 +70,8 @@ def cpu_baseline(cfg, steps: int) -> dict:
     # and are scaled to ~2.5M convolved edges (the rate is per edge, reported with the sample size)
     if cfg.conv_edges > 8_000_000:
         cfg = scaled_config(cfg, 2_500_000 / cfg.conv_edges, name=f"{cfg.name}-cpu-sample")
+    # the reference's CPU path is fp32 only: a bf16 config is timed on its fp32 counterpart
+    cfg = dataclasses.replace(cfg, feat_dtype="f32")
     try:
         g = synthetic_graph(cfg, seed=0, device="cpu")
         torch.manual_seed(1997)
@@ -88,7 +93,7 @@ def cpu_baseline(cfg, steps: int) -> dict:
     except OSError:
         pass
     return {"value": cfg.conv_edges / dt, "unit": "edges/s", "cores": threads, "kind": "port",
-            "sample": f"{cfg.name}{' full graph' if cfg is full else ''} ({cfg.nodes} nodes / {cfg.graph_edges} "
+            "sample": f"{cfg.name}{' full graph' if cfg.nodes == full.nodes else ''} ({cfg.nodes} nodes / {cfg.graph_edges} "
                       f"edges, hidden {cfg.hidden}, {cfg.layers} layers), 1 warm-up + {steps} "
                       f"timed train steps (fwd + sqrt-MAPE + bwd + Adam) of oracle/pyg_cpu.py (torch CPU ops = "
                       f"the reference's PyG CPU path), {threads} threads, {cpu_model}",
@@ -120,6 +125,8 @@ def main():
     _lib.lib()
 
     cfg = CONFIGS[args.config]
+    bf16 = cfg.feat_dtype == "bf16"
+    mfma_peak = BF16_MFMA_PEAK_TFS if bf16 else F32_MFMA_PEAK_TFS
     graph = synthetic_graph(cfg, seed=rank, device=dev)      # one independent component per rank
     torch.manual_seed(1997)
     model = HetroGIN(**cfg.model_kwargs({"link": cfg.f_link, "path": cfg.f_path, "node": cfg.f_node})).to(dev)
@@ -162,7 +169,8 @@ def main():
             a = s.get("aggregate")
             if a:
                 achieved = a["avg_work"] / (a["avg_ms"] / 1e3) / 1e9
-                roofline = {"bound": "hbm", "kernel": "hgin_aggregate_f32 (k_aggregate<4,32,8>)",
+                roofline = {"bound": "hbm", "kernel": "hgin_aggregate_bf16 (k_aggregate_bf16<8,G,8>)" if bf16 else
+                            "hgin_aggregate_f32 (k_aggregate<4,32,8>)",
                             "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                             "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
                             "bytes_per_launch": a["avg_work"], "avg_launch_ms": round(a["avg_ms"], 5),
@@ -176,18 +184,21 @@ def main():
             m = s.get("gin_mlp")
             if m:
                 tfs = m["avg_work"] / (m["avg_ms"] / 1e3) / 1e12
-                mfma = {"bound": "mfma", "kernel": "hgin_gin_mlp_fwd_f32", "achieved": round(tfs, 2),
-                        "peak": F32_MFMA_PEAK_TFS, "unit": "TFLOP/s", "frac": round(tfs / F32_MFMA_PEAK_TFS, 4),
+                mfma = {"bound": "mfma", "kernel": "hgin_gin_mlp_fwd_bf16" if bf16 else "hgin_gin_mlp_fwd_f32",
+                        "achieved": round(tfs, 2), "peak": mfma_peak, "unit": "TFLOP/s",
+                        "frac": round(tfs / mfma_peak, 4),
                         "avg_launch_ms": round(m["avg_ms"], 5),
                         "share_of_step": round(m["total_ms"] / args.steps / (t_step * 1e3), 4)}
         out = {"metric": METRIC, "value": round(value, 1), "unit": "edges/s", "n_gpus": world,
                "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(t_step * 1e3, 4),
-               "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+               "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+               "dtype": "bf16" if bf16 else "f32", "accumulate": "f32",
                "data": "synthetic: SURVEY.md §8.D generator (uniform endpoints, reverse relations = flips, randn "
                        "features, rand+0.5 labels), random-init weights (seed 1997); one graph per rank",
                "config": {"workload": f"{cfg.name}: {cfg.layers}-layer HeteroGIN, {cfg.nodes} nodes / "
                                       f"{cfg.graph_edges} edges per GPU, 3 node types x "
-                                      f"{len(graph.edge_index)} edge types, hidden {cfg.hidden} fp32",
+                                      f"{len(graph.edge_index)} edge types, hidden {cfg.hidden} "
+                                      f"{'bf16' if bf16 else 'fp32'}",
                           "nodes_per_gpu": cfg.nodes, "graph_edges_per_gpu": cfg.graph_edges,
                           "conv_edges_per_gpu": cfg.conv_edges, "hidden": cfg.hidden, "layers": cfg.layers,
                           "global_batch": world, "parallelism": f"dp{world} (graph component per rank, RCCL "

@@ -172,30 +172,197 @@ int dispatch_g(int lanes_needed, const int32_t* rowptr, const int32_t* col, int6
                                    out, ld_out, s);
 }
 
+// ---------------------------------------------------------------------------------------------------
+// bf16 storage (cfg5): the same row-per-lane-group walk, each lane owning 8 features (one 16-B load per
+// neighbour row), fp32 sequential accumulation in edge order, one RNE rounding per output element.
+// Bytes per launch: E * (4 + 2 * F_src) + (N + 1) * 4 + N * 2 * F_out [+ N * 2 * F_dst].
+template <int VEC>
+struct BVec;
+template <>
+struct BVec<1> {
+  using T = uint16_t;
+  static __device__ __forceinline__ T load(const uint16_t* p) { return *p; }
+  template <bool NT>
+  static __device__ __forceinline__ T load_s(const uint16_t* p) { return *p; }
+  static __device__ __forceinline__ void unpack(const T& v, float (&f)[1]) { f[0] = bf2f(v); }
+  template <bool NT>
+  static __device__ __forceinline__ void store(uint16_t* p, const float (&f)[1]) { *p = (uint16_t)f2bf(f[0]); }
+};
+using u4v = __attribute__((ext_vector_type(4))) unsigned int;
+template <>
+struct BVec<8> {
+  using T = uint4;
+  static __device__ __forceinline__ T load(const uint16_t* p) { return *reinterpret_cast<const uint4*>(p); }
+  template <bool NT>
+  static __device__ __forceinline__ T load_s(const uint16_t* p) {
+    if (!NT) return load(p);
+    const u4v v = __builtin_nontemporal_load(reinterpret_cast<const u4v*>(p));
+    return make_uint4(v.x, v.y, v.z, v.w);
+  }
+  static __device__ __forceinline__ void unpack(const T& v, float (&f)[8]) {
+    f[0] = bf_lo(v.x); f[1] = bf_hi(v.x); f[2] = bf_lo(v.y); f[3] = bf_hi(v.y);
+    f[4] = bf_lo(v.z); f[5] = bf_hi(v.z); f[6] = bf_lo(v.w); f[7] = bf_hi(v.w);
+  }
+  template <bool NT>
+  static __device__ __forceinline__ void store(uint16_t* p, const float (&f)[8]) {
+    const u4v t = {pack_bf2(f[0], f[1]), pack_bf2(f[2], f[3]), pack_bf2(f[4], f[5]), pack_bf2(f[6], f[7])};
+    if (NT) __builtin_nontemporal_store(t, reinterpret_cast<u4v*>(p));
+    else *reinterpret_cast<u4v*>(p) = t;
+  }
+};
+
+template <int VEC, int G, int U, bool NT>
+__global__ __launch_bounds__(256) void k_aggregate_bf16(const int32_t* __restrict__ rowptr,
+                                                        const int32_t* __restrict__ col, int64_t n_rows,
+                                                        const uint16_t* __restrict__ x_src, int64_t ld_src, int f_src,
+                                                        const uint16_t* __restrict__ x_dst, int64_t ld_dst, int f_dst,
+                                                        const float* __restrict__ eps, int combine,
+                                                        uint16_t* __restrict__ out, int64_t ld_out) {
+  using V = BVec<VEC>;
+  using T = typename V::T;
+  constexpr int kRowsPerWave = kWave / G;
+  const int lane = threadIdx.x & (kWave - 1);
+  const int grp = lane / G;
+  const int gl = lane % G;
+  const int64_t wave_id = (int64_t)blockIdx.x * (blockDim.x / kWave) + (threadIdx.x / kWave);
+  const int64_t r = wave_id * kRowsPerWave + grp;
+  if (r >= n_rows) return;
+  const int beg = rowptr[r];
+  const int end = rowptr[r + 1];
+  const float s = combine != HGIN_COMBINE_NONE ? __fadd_rn(1.0f, eps[0]) : 1.0f;
+  uint16_t* __restrict__ orow = out + r * ld_out;
+
+  for (int f0 = gl * VEC; f0 < f_src; f0 += G * VEC) {
+    float acc[VEC];
+#pragma unroll
+    for (int c = 0; c < VEC; ++c) acc[c] = 0.0f;
+    int k = beg;
+    for (; k + U <= end; k += U) {
+      int idx[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) idx[u] = col[k + u];
+      T v[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) v[u] = V::load(x_src + (int64_t)idx[u] * ld_src + f0);
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        float f[VEC];
+        V::unpack(v[u], f);
+#pragma unroll
+        for (int c = 0; c < VEC; ++c) acc[c] = __fadd_rn(acc[c], f[c]);
+      }
+    }
+    for (; k < end; ++k) {
+      float f[VEC];
+      V::unpack(V::load(x_src + (int64_t)col[k] * ld_src + f0), f);
+#pragma unroll
+      for (int c = 0; c < VEC; ++c) acc[c] = __fadd_rn(acc[c], f[c]);
+    }
+    if (combine == HGIN_COMBINE_ADD) {
+      float xd[VEC];
+      V::unpack(V::template load_s<NT>(x_dst + r * ld_dst + f0), xd);
+#pragma unroll
+      for (int c = 0; c < VEC; ++c) acc[c] = __fadd_rn(acc[c], __fmul_rn(s, xd[c]));
+    }
+    V::template store<NT>(orow + f0, acc);
+  }
+  if (combine == HGIN_COMBINE_CONCAT) {
+    for (int f0 = gl * VEC; f0 < f_dst; f0 += G * VEC) {
+      float xd[VEC];
+      V::unpack(V::template load_s<NT>(x_dst + r * ld_dst + f0), xd);
+#pragma unroll
+      for (int c = 0; c < VEC; ++c) xd[c] = __fmul_rn(s, xd[c]);
+      V::template store<NT>(orow + f_src + f0, xd);
+    }
+  }
+}
+
+template <int VEC, int G>
+int launch_aggregate_bf16(const int32_t* rowptr, const int32_t* col, int64_t n_rows, const uint16_t* x_src,
+                          int64_t ld_src, int f_src, const uint16_t* x_dst, int64_t ld_dst, int f_dst, const float* eps,
+                          int combine, uint16_t* out, int64_t ld_out, hipStream_t s) {
+  constexpr int kRowsPerWave = kWave / G;
+  const int64_t blocks = ceil_div(ceil_div(n_rows, kRowsPerWave), 256 / kWave);
+  if (combine == HGIN_COMBINE_CONCAT)
+    k_aggregate_bf16<VEC, G, 8, true><<<dim3((unsigned)blocks), 256, 0, s>>>(
+        rowptr, col, n_rows, x_src, ld_src, f_src, x_dst, ld_dst, f_dst, eps, combine, out, ld_out);
+  else
+    k_aggregate_bf16<VEC, G, 8, false><<<dim3((unsigned)blocks), 256, 0, s>>>(
+        rowptr, col, n_rows, x_src, ld_src, f_src, x_dst, ld_dst, f_dst, eps, combine, out, ld_out);
+  return check_launch("hgin_aggregate_bf16");
+}
+
+template <int VEC>
+int dispatch_g_bf16(int lanes_needed, const int32_t* rowptr, const int32_t* col, int64_t n_rows,
+                    const uint16_t* x_src, int64_t ld_src, int f_src, const uint16_t* x_dst, int64_t ld_dst, int f_dst,
+                    const float* eps, int combine, uint16_t* out, int64_t ld_out, hipStream_t s) {
+#define HGIN_AGG_CASE(GV)                                                                                    \
+  if (lanes_needed <= GV)                                                                                   \
+    return launch_aggregate_bf16<VEC, GV>(rowptr, col, n_rows, x_src, ld_src, f_src, x_dst, ld_dst, f_dst, \
+                                          eps, combine, out, ld_out, s);
+  HGIN_AGG_CASE(4)
+  HGIN_AGG_CASE(8)
+  HGIN_AGG_CASE(16)
+  HGIN_AGG_CASE(32)
+#undef HGIN_AGG_CASE
+  return launch_aggregate_bf16<VEC, 64>(rowptr, col, n_rows, x_src, ld_src, f_src, x_dst, ld_dst, f_dst, eps,
+                                        combine, out, ld_out, s);
+}
+
+int check_aggregate_args(const char* what, const int32_t* rowptr, int64_t n_rows, int64_t ld_src, int64_t f_src,
+                         const void* x_dst, int64_t ld_dst, int64_t f_dst, const float* eps, int combine,
+                         const void* out, int64_t ld_out) {
+  HGIN_ARG_CHECK(combine == HGIN_COMBINE_NONE || combine == HGIN_COMBINE_ADD || combine == HGIN_COMBINE_CONCAT,
+                 "%s: bad combine mode %d", what, combine);
+  HGIN_ARG_CHECK(n_rows >= 0 && f_src >= 0 && f_src < (1 << 24), "%s: bad sizes", what);
+  if (n_rows == 0) return HGIN_OK;
+  HGIN_ARG_CHECK(rowptr != nullptr && out != nullptr, "%s: rowptr/out NULL", what);
+  int64_t out_w = f_src;
+  if (combine != HGIN_COMBINE_NONE) {
+    HGIN_ARG_CHECK(x_dst != nullptr && eps != nullptr, "%s: combine needs x_dst and eps", what);
+    HGIN_ARG_CHECK(f_dst >= 0 && f_dst < (1 << 24), "%s: bad f_dst", what);
+    if (combine == HGIN_COMBINE_ADD)
+      HGIN_ARG_CHECK(f_dst == f_src, "%s: ADD needs f_dst == f_src (%lld vs %lld)", what, (long long)f_dst,
+                     (long long)f_src);
+    if (combine == HGIN_COMBINE_CONCAT) out_w = f_src + f_dst;
+    HGIN_ARG_CHECK(ld_dst >= f_dst, "%s: ld_dst < f_dst", what);
+  }
+  HGIN_ARG_CHECK(ld_src >= f_src && ld_out >= out_w, "%s: leading dimension too small", what);
+  return HGIN_OK;
+}
+
 }  // namespace
 }  // namespace hgin
 
 using namespace hgin;
 
+extern "C" int hgin_aggregate_bf16(const int32_t* rowptr, const int32_t* col, int64_t n_rows, const uint16_t* x_src,
+                                   int64_t ld_src, int64_t f_src, const uint16_t* x_dst, int64_t ld_dst, int64_t f_dst,
+                                   const float* eps, int combine, uint16_t* out, int64_t ld_out, void* stream) {
+  if (int rc = check_aggregate_args("hgin_aggregate_bf16", rowptr, n_rows, ld_src, f_src, x_dst, ld_dst, f_dst, eps,
+                                    combine, out, ld_out))
+    return rc;
+  if (n_rows == 0) return HGIN_OK;
+  hipStream_t s = as_stream(stream);
+  const bool dst_ok = combine == HGIN_COMBINE_NONE || (aligned16(x_dst) && ld_dst % 8 == 0 && f_dst % 8 == 0);
+  const bool vec8 = f_src % 8 == 0 && aligned16(x_src) && ld_src % 8 == 0 && aligned16(out) && ld_out % 8 == 0 &&
+                    dst_ok && (f_src > 0 || f_dst > 0);
+  const int fd = combine == HGIN_COMBINE_CONCAT ? (int)f_dst : 0;
+  const int64_t widest = f_src > fd ? f_src : fd;
+  if (vec8)
+    return dispatch_g_bf16<8>((int)ceil_div(widest, 8), rowptr, col, n_rows, x_src, ld_src, (int)f_src, x_dst, ld_dst,
+                              (int)f_dst, eps, combine, out, ld_out, s);
+  return dispatch_g_bf16<1>((int)widest, rowptr, col, n_rows, x_src, ld_src, (int)f_src, x_dst, ld_dst, (int)f_dst,
+                            eps, combine, out, ld_out, s);
+}
+
 extern "C" int hgin_aggregate_f32(const int32_t* rowptr, const int32_t* col, int64_t n_rows, const float* x_src,
                                   int64_t ld_src, int64_t f_src, const float* x_dst, int64_t ld_dst, int64_t f_dst,
                                   const float* eps, int combine, float* out, int64_t ld_out, void* stream) {
-  HGIN_ARG_CHECK(combine == HGIN_COMBINE_NONE || combine == HGIN_COMBINE_ADD || combine == HGIN_COMBINE_CONCAT,
-                 "hgin_aggregate_f32: bad combine mode %d", combine);
-  HGIN_ARG_CHECK(n_rows >= 0 && f_src >= 0 && f_src < (1 << 24), "hgin_aggregate_f32: bad sizes");
+  if (int rc = check_aggregate_args("hgin_aggregate_f32", rowptr, n_rows, ld_src, f_src, x_dst, ld_dst, f_dst, eps,
+                                    combine, out, ld_out))
+    return rc;
   if (n_rows == 0) return HGIN_OK;
-  HGIN_ARG_CHECK(rowptr != nullptr && out != nullptr, "hgin_aggregate_f32: rowptr/out NULL");
-  int64_t out_w = f_src;
-  if (combine != HGIN_COMBINE_NONE) {
-    HGIN_ARG_CHECK(x_dst != nullptr && eps != nullptr, "hgin_aggregate_f32: combine needs x_dst and eps");
-    HGIN_ARG_CHECK(f_dst >= 0 && f_dst < (1 << 24), "hgin_aggregate_f32: bad f_dst");
-    if (combine == HGIN_COMBINE_ADD)
-      HGIN_ARG_CHECK(f_dst == f_src, "hgin_aggregate_f32: ADD needs f_dst == f_src (%lld vs %lld)",
-                     (long long)f_dst, (long long)f_src);
-    if (combine == HGIN_COMBINE_CONCAT) out_w = f_src + f_dst;
-    HGIN_ARG_CHECK(ld_dst >= f_dst, "hgin_aggregate_f32: ld_dst < f_dst");
-  }
-  HGIN_ARG_CHECK(ld_src >= f_src && ld_out >= out_w, "hgin_aggregate_f32: leading dimension too small");
   hipStream_t s = as_stream(stream);
   const bool dst_ok = combine == HGIN_COMBINE_NONE || (aligned16(x_dst) && ld_dst % 4 == 0 && f_dst % 4 == 0);
   const bool vec4 = f_src % 4 == 0 && aligned16(x_src) && ld_src % 4 == 0 && aligned16(out) && ld_out % 4 == 0 &&

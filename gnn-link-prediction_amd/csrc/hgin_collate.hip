@@ -57,6 +57,19 @@ __global__ __launch_bounds__(256) void k_batched_copy(const hgin_copy_desc* __re
         for (int64_t i = t0; i < ds.count; i += stride) o[i] = (int32_t)ds.add;
         break;
       }
+      case HGIN_COPY_B16: {
+        const uint16_t* s = static_cast<const uint16_t*>(ds.src);
+        uint16_t* o = static_cast<uint16_t*>(ds.dst);
+        if (((reinterpret_cast<uintptr_t>(s) | reinterpret_cast<uintptr_t>(o)) & 15u) == 0) {
+          const int64_t n8 = ds.count >> 3;
+          for (int64_t i = t0; i < n8; i += stride)
+            reinterpret_cast<uint4*>(o)[i] = reinterpret_cast<const uint4*>(s)[i];
+          for (int64_t i = (n8 << 3) + t0; i < ds.count; i += stride) o[i] = s[i];
+        } else {
+          for (int64_t i = t0; i < ds.count; i += stride) o[i] = s[i];
+        }
+        break;
+      }
       default:
         break;
     }

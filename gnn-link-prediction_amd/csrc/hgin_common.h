@@ -43,6 +43,33 @@ inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
 inline size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
 
+// bf16 storage (cfg5): raw uint16_t bit patterns; arithmetic is always fp32.
+// Widening is exact; narrowing is round-to-nearest-even with NaN -> 0x7FC0, bit-identical to
+// torch's float -> bfloat16 conversion (c10::BFloat16), so the CPU oracle can pin every rounding.
+__device__ __forceinline__ float bf2f(uint32_t h) { return __uint_as_float(h << 16); }
+__device__ __forceinline__ float bf_lo(uint32_t w) { return __uint_as_float(w << 16); }
+__device__ __forceinline__ float bf_hi(uint32_t w) { return __uint_as_float(w & 0xffff0000u); }
+__device__ __forceinline__ uint32_t f2bf(float f) {
+  const uint32_t u = __float_as_uint(f);
+  if ((u & 0x7fffffffu) > 0x7f800000u) return 0x7fc0u;
+  return (u + 0x7fffu + ((u >> 16) & 1u)) >> 16;
+}
+__device__ __forceinline__ uint32_t pack_bf2(float lo, float hi) { return f2bf(lo) | (f2bf(hi) << 16); }
+
+// Element-type traits shared by the fp32 and bf16 instantiations of the memory-bound kernels.
+template <typename T>
+struct Elem;
+template <>
+struct Elem<float> {
+  static __device__ __forceinline__ float ld(const float* p) { return *p; }
+  static __device__ __forceinline__ void st(float* p, float v) { *p = v; }
+};
+template <>
+struct Elem<uint16_t> {
+  static __device__ __forceinline__ float ld(const uint16_t* p) { return bf2f(*p); }
+  static __device__ __forceinline__ void st(uint16_t* p, float v) { *p = (uint16_t)f2bf(v); }
+};
+
 }  // namespace hgin
 
 #define HGIN_ARG_CHECK(cond, ...)     \

@@ -244,10 +244,284 @@ int check_a(const char* what, const float* a1, int64_t lda1, int64_t k1, const f
   return HGIN_OK;
 }
 
+// ---------------------------------------------------------------------------------------------------
+// bf16 operands (cfg5): v_mfma_f32_32x32x16_bf16, fp32 accumulate.  Same workgroup tiles, wave grid,
+// register prefetch and LDS-staged epilogue as the fp32 kernel; a K-tile is 64 bf16 (128 B per row, so
+// the [row][72] LDS image has the fp32 kernel's 144-B row stride and its conflict-free ds_read_b128).
+// Operand maps (gfx950): lane (r = l & 31, h = l >> 5) holds A[row r][k = 8h + j] and B[k = 8h + j][col r],
+// j = 0..7, per 16-wide k-step: one ds_read_b128 per fragment.  C/D map as the f32 MFMA.
+// At the GIN shapes (K = 128..512, N = 128..256) these GEMMs are HBM-bound (A read once, Y/Z written
+// once: ~43 flop/B at K = 256, N = 128, far below the bf16 MFMA ridge), so the tile keeps the whole of N
+// per workgroup where it can and the epilogue writes 8-B bf16 quads.
+using bf16x8 = __attribute__((ext_vector_type(8))) __bf16;
+constexpr int kBKh = 64;
+constexpr int kLdsH = kBKh + 8;
+
+struct Src2h {
+  const uint16_t* p1;
+  int64_t ld1;
+  const uint16_t* p2;
+  int64_t ld2;
+  int64_t k1;
+};
+
+template <bool kVec, int ROWS>
+__device__ __forceinline__ void load_tile_h(uint4 (&r)[ROWS / 32], const Src2h& s, int64_t row0, int64_t rows,
+                                            int64_t k0, int64_t K, int tid) {
+  const int64_t kk = k0 + (tid & 7) * 8;
+#pragma unroll
+  for (int i = 0; i < ROWS / 32; ++i) {
+    const int64_t gr = row0 + (tid >> 3) + 32 * i;
+    uint4 v = make_uint4(0u, 0u, 0u, 0u);
+    if (gr < rows) {
+      if (kVec && kk + 7 < K && (kk + 7 < s.k1 || kk >= s.k1)) {
+        const uint16_t* p = kk < s.k1 ? s.p1 + gr * s.ld1 + kk : s.p2 + gr * s.ld2 + (kk - s.k1);
+        v = *reinterpret_cast<const uint4*>(p);
+      } else {
+        uint32_t t[8];
+#pragma unroll
+        for (int c = 0; c < 8; ++c) {
+          const int64_t k = kk + c;
+          t[c] = k < K ? (k < s.k1 ? s.p1[gr * s.ld1 + k] : s.p2[gr * s.ld2 + (k - s.k1)]) : 0u;
+        }
+        v = make_uint4(t[0] | (t[1] << 16), t[2] | (t[3] << 16), t[4] | (t[5] << 16), t[6] | (t[7] << 16));
+      }
+    }
+    r[i] = v;
+  }
+}
+
+template <int ROWS>
+__device__ __forceinline__ void store_tile_h(uint16_t* __restrict__ dst, const uint4 (&r)[ROWS / 32], int tid) {
+#pragma unroll
+  for (int i = 0; i < ROWS / 32; ++i)
+    *reinterpret_cast<uint4*>(dst + ((tid >> 3) + 32 * i) * kLdsH + (tid & 7) * 8) = r[i];
+}
+
+// 4 consecutive output columns of one row: fp32 (16-B) or bf16 (8-B) stores, scalar at the ragged edge.
+template <typename OutT>
+struct Out4;
+template <>
+struct Out4<float> {
+  static __device__ __forceinline__ void st(float* p, const float (&o)[4], bool full, int nv) {
+    if (full) *reinterpret_cast<float4*>(p) = make_float4(o[0], o[1], o[2], o[3]);
+    else for (int t = 0; t < nv; ++t) p[t] = o[t];
+  }
+  static __device__ __forceinline__ void ld(const float* p, float (&o)[4], bool full, int nv) {
+    if (full) {
+      const float4 v = *reinterpret_cast<const float4*>(p);
+      o[0] = v.x; o[1] = v.y; o[2] = v.z; o[3] = v.w;
+    } else {
+      for (int t = 0; t < nv; ++t) o[t] = p[t];
+    }
+  }
+};
+template <>
+struct Out4<uint16_t> {
+  static __device__ __forceinline__ void st(uint16_t* p, const float (&o)[4], bool full, int nv) {
+    if (full) *reinterpret_cast<uint2*>(p) = make_uint2(pack_bf2(o[0], o[1]), pack_bf2(o[2], o[3]));
+    else for (int t = 0; t < nv; ++t) p[t] = (uint16_t)f2bf(o[t]);
+  }
+  static __device__ __forceinline__ void ld(const uint16_t* p, float (&o)[4], bool full, int nv) {
+    if (full) {
+      const uint2 v = *reinterpret_cast<const uint2*>(p);
+      o[0] = bf_lo(v.x); o[1] = bf_hi(v.x); o[2] = bf_lo(v.y); o[3] = bf_hi(v.y);
+    } else {
+      for (int t = 0; t < nv; ++t) o[t] = bf2f(p[t]);
+    }
+  }
+};
+
+template <int EPI, bool kVec, int TN, typename OutT>
+__global__ __launch_bounds__(256, 3) void k_gemm_nt_bf16(Src2h A, Src2h B, int64_t M, int64_t N, int64_t K,
+                                                         const float* __restrict__ bias,
+                                                         const float* __restrict__ prelu,
+                                                         const OutT* __restrict__ accum, OutT* __restrict__ Z,
+                                                         OutT* __restrict__ Y, int64_t ldc, bool vec_out) {
+  constexpr int WN = TN == 2 ? 2 : 1;
+  constexpr int WM = 4 / WN;
+  constexpr int BM = WM * 64;
+  constexpr int BN = WN * TN * 32;
+  constexpr int WCOLS = TN * 32;
+  constexpr int kTileBytes = (BM + BN) * kLdsH * 2;
+  constexpr int kEpiBytes = 4 * 32 * (WCOLS + 4) * 4;
+  __shared__ __attribute__((aligned(16))) float smem[(kTileBytes > kEpiBytes ? kTileBytes : kEpiBytes) / 4];
+  uint16_t* As = reinterpret_cast<uint16_t*>(smem);
+  uint16_t* Bs = As + BM * kLdsH;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wm = wave / WN;
+  const int wn = wave % WN;
+  const int li = lane & 31;
+  const int lh = lane >> 5;
+  const int64_t n_tiles_n = (N + BN - 1) / BN;
+  const int64_t m0 = ((int64_t)blockIdx.x / n_tiles_n) * BM;
+  const int64_t n0 = ((int64_t)blockIdx.x % n_tiles_n) * BN;
+
+  f32x16 acc[2][TN];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < TN; ++b)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[a][b][e] = 0.0f;
+
+  uint4 ra[BM / 32], rb[BN >= 32 ? BN / 32 : 1];
+  load_tile_h<kVec, BM>(ra, A, m0, M, 0, K, tid);
+  load_tile_h<kVec, BN>(rb, B, n0, N, 0, K, tid);
+  store_tile_h<BM>(As, ra, tid);
+  store_tile_h<BN>(Bs, rb, tid);
+  __syncthreads();
+  for (int64_t k0 = 0; k0 < K; k0 += kBKh) {
+    const bool more = k0 + kBKh < K;
+    if (more) {
+      load_tile_h<kVec, BM>(ra, A, m0, M, k0 + kBKh, K, tid);
+      load_tile_h<kVec, BN>(rb, B, n0, N, k0 + kBKh, K, tid);
+    }
+#pragma unroll
+    for (int c = 0; c < kBKh / 16; ++c) {
+      bf16x8 fa[2], fb[TN];
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+        fa[t] = *reinterpret_cast<const bf16x8*>(As + (wm * 64 + t * 32 + li) * kLdsH + c * 16 + lh * 8);
+#pragma unroll
+      for (int t = 0; t < TN; ++t)
+        fb[t] = *reinterpret_cast<const bf16x8*>(Bs + (wn * WCOLS + t * 32 + li) * kLdsH + c * 16 + lh * 8);
+#pragma unroll
+      for (int tm = 0; tm < 2; ++tm)
+#pragma unroll
+        for (int tn = 0; tn < TN; ++tn)
+          acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[tm], fb[tn], acc[tm][tn], 0, 0, 0);
+    }
+    if (more) {
+      __syncthreads();
+      store_tile_h<BM>(As, ra, tid);
+      store_tile_h<BN>(Bs, rb, tid);
+      __syncthreads();
+    }
+  }
+
+  constexpr int kLc = WCOLS + 4;
+  constexpr int kQ = WCOLS / 4;
+  const float a_slope = EPI == 1 ? prelu[0] : 0.0f;
+  float* Cw = smem + wave * 32 * kLc;
+  __syncthreads();
+#pragma unroll
+  for (int tm = 0; tm < 2; ++tm) {
+#pragma unroll
+    for (int tn = 0; tn < TN; ++tn)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) Cw[((e & 3) + 8 * (e >> 2) + 4 * lh) * kLc + tn * 32 + li] = acc[tm][tn][e];
+    __syncthreads();
+#pragma unroll 2
+    for (int j = 0; j < (32 * kQ) / 64; ++j) {
+      const int q = lane + 64 * j;
+      const int r = q / kQ;
+      const int c = (q % kQ) * 4;
+      const int64_t row = m0 + wm * 64 + tm * 32 + r;
+      const int64_t col = n0 + wn * WCOLS + c;
+      if (row >= M || col >= N) continue;
+      const float4 v4 = *reinterpret_cast<const float4*>(Cw + r * kLc + c);
+      float o[4] = {v4.x, v4.y, v4.z, v4.w};
+      float zz[4] = {0.f, 0.f, 0.f, 0.f};
+      const bool full = vec_out && col + 3 < N;
+      const int nv = N - col < 4 ? (int)(N - col) : 4;
+      float acc_in[4] = {0.f, 0.f, 0.f, 0.f};
+      if (EPI == 1 && accum) Out4<OutT>::ld(accum + row * ldc + col, acc_in, full, nv);
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const float bcol = (EPI >= 1 && t < nv) ? bias[col + t] : 0.0f;
+        if (EPI == 2) {
+          o[t] = __fadd_rn(o[t], bcol);
+        } else if (EPI == 1) {
+          zz[t] = __fadd_rn(o[t], bcol);
+          const float y = zz[t] > 0.0f ? zz[t] : __fmul_rn(a_slope, zz[t]);
+          o[t] = accum ? __fadd_rn(acc_in[t], y) : y;
+        }
+      }
+      Out4<OutT>::st(Y + row * ldc + col, o, full, nv);
+      if (EPI == 1 && Z) Out4<OutT>::st(Z + row * ldc + col, zz, full, nv);
+    }
+    if (tm == 0) __syncthreads();
+  }
+}
+
+template <int EPI, typename OutT>
+int launch_nt_bf16(const Src2h& a, const Src2h& b, int64_t M, int64_t N, int64_t K, const float* bias,
+                   const float* prelu, const OutT* accum, OutT* z, OutT* y, int64_t ldc, hipStream_t s,
+                   const char* what) {
+  const bool vec = aligned16(a.p1) && a.ld1 % 8 == 0 && a.k1 % 8 == 0 &&
+                   (a.k1 == K || (aligned16(a.p2) && a.ld2 % 8 == 0)) && aligned16(b.p1) && b.ld1 % 8 == 0;
+  const bool vec_out = ldc % 4 == 0 && aligned16(y) && (z == nullptr || aligned16(z)) &&
+                       (accum == nullptr || aligned16(accum));
+#define HGIN_NT_BF16(TNV)                                                                                     \
+  {                                                                                                          \
+    constexpr int BM = (TNV == 2 ? 2 : 4) * 64;                                                              \
+    constexpr int BN = (TNV == 2 ? 2 : 1) * TNV * 32;                                                        \
+    dim3 grid((unsigned)(ceil_div(N, BN) * ceil_div(M, BM)));                                                \
+    if (vec)                                                                                                 \
+      k_gemm_nt_bf16<EPI, true, TNV, OutT><<<grid, 256, 0, s>>>(a, b, M, N, K, bias, prelu, accum, z, y, ldc, \
+                                                                vec_out);                                    \
+    else                                                                                                     \
+      k_gemm_nt_bf16<EPI, false, TNV, OutT><<<grid, 256, 0, s>>>(a, b, M, N, K, bias, prelu, accum, z, y,    \
+                                                                 ldc, vec_out);                              \
+  }
+  if (N <= 32)
+    HGIN_NT_BF16(1)
+  else
+    HGIN_NT_BF16(2)
+#undef HGIN_NT_BF16
+  return check_launch(what);
+}
+
+int check_a_h(const char* what, const uint16_t* a1, int64_t lda1, int64_t k1, const uint16_t* a2, int64_t lda2,
+              int64_t K) {
+  HGIN_ARG_CHECK(k1 >= 0 && k1 <= K, "%s: k1 out of [0, K]", what);
+  HGIN_ARG_CHECK(k1 == 0 || (a1 && lda1 >= k1), "%s: bad A1", what);
+  HGIN_ARG_CHECK(k1 == K || (a2 && lda2 >= K - k1), "%s: bad A2", what);
+  return HGIN_OK;
+}
+
 }  // namespace
 }  // namespace hgin
 
 using namespace hgin;
+
+extern "C" int hgin_gin_mlp_fwd_bf16(const uint16_t* a1, int64_t lda1, int64_t k1, const uint16_t* a2, int64_t lda2,
+                                     const uint16_t* w, const float* bias, const float* prelu, const uint16_t* accum,
+                                     uint16_t* z, uint16_t* y, int64_t M, int64_t N, int64_t K, void* stream) {
+  HGIN_ARG_CHECK(M >= 0 && N >= 0 && K >= 0, "hgin_gin_mlp_fwd_bf16: negative size");
+  HGIN_ARG_CHECK(M < (int64_t(1) << 31) && N <= 65535 * 128, "hgin_gin_mlp_fwd_bf16: size too large");
+  if (M == 0 || N == 0) return HGIN_OK;
+  HGIN_ARG_CHECK(w && bias && prelu && y, "hgin_gin_mlp_fwd_bf16: NULL operand");
+  if (int rc = check_a_h("hgin_gin_mlp_fwd_bf16", a1, lda1, k1, a2, lda2, K)) return rc;
+  return launch_nt_bf16<1, uint16_t>(Src2h{a1, lda1, a2, lda2, k1}, Src2h{w, K, nullptr, 0, K}, M, N, K, bias, prelu,
+                                     accum, z, y, N, as_stream(stream), "hgin_gin_mlp_fwd_bf16");
+}
+
+extern "C" int hgin_linear_fwd_bf16(const uint16_t* a1, int64_t lda1, int64_t k1, const uint16_t* a2, int64_t lda2,
+                                    const uint16_t* w, const float* bias, float* y, int64_t M, int64_t N, int64_t K,
+                                    void* stream) {
+  HGIN_ARG_CHECK(M >= 0 && N >= 0 && K >= 0, "hgin_linear_fwd_bf16: negative size");
+  HGIN_ARG_CHECK(M < (int64_t(1) << 31) && N <= 65535 * 128, "hgin_linear_fwd_bf16: size too large");
+  if (M == 0 || N == 0) return HGIN_OK;
+  HGIN_ARG_CHECK(w && bias && y, "hgin_linear_fwd_bf16: NULL operand");
+  if (int rc = check_a_h("hgin_linear_fwd_bf16", a1, lda1, k1, a2, lda2, K)) return rc;
+  return launch_nt_bf16<2, float>(Src2h{a1, lda1, a2, lda2, k1}, Src2h{w, K, nullptr, 0, K}, M, N, K, bias, nullptr,
+                                  nullptr, nullptr, y, N, as_stream(stream), "hgin_linear_fwd_bf16");
+}
+
+extern "C" int hgin_gemm_nt_bf16(const uint16_t* a, int64_t lda, const uint16_t* b, int64_t ldb, uint16_t* c,
+                                 int64_t ldc, int64_t M, int64_t N, int64_t K, void* stream) {
+  HGIN_ARG_CHECK(M >= 0 && N >= 0 && K >= 0, "hgin_gemm_nt_bf16: negative size");
+  HGIN_ARG_CHECK(N <= 65535 * 128, "hgin_gemm_nt_bf16: N too large");
+  if (M == 0 || N == 0) return HGIN_OK;
+  HGIN_ARG_CHECK(a && b && c, "hgin_gemm_nt_bf16: NULL operand");
+  HGIN_ARG_CHECK(lda >= K && ldb >= K && ldc >= N, "hgin_gemm_nt_bf16: leading dimension too small");
+  return launch_nt_bf16<0, uint16_t>(Src2h{a, lda, nullptr, 0, K}, Src2h{b, ldb, nullptr, 0, K}, M, N, K, nullptr,
+                                     nullptr, nullptr, nullptr, c, ldc, as_stream(stream), "hgin_gemm_nt_bf16");
+}
 
 extern "C" int hgin_gin_mlp_fwd_f32(const float* a1, int64_t lda1, int64_t k1, const float* a2, int64_t lda2,
                                     const float* w, const float* bias, const float* prelu, const float* accum, float* z,

@@ -143,10 +143,11 @@ __global__ __launch_bounds__(256, kOcc) void k_gemm_tn_partial(const float* __re
 // Small weight gradients (N or K < 16, e.g. the readout head Linear(32, 1)): no MFMA tile to fill, so a
 // block owns a chunk of M rows and thread (r, p) accumulates pair p = (n, k) over rows r, r + R, ... in
 // order; the R row-lanes are combined in LDS in lane order.  Output: the same [split][N*K] slabs.
-__global__ __launch_bounds__(256) void k_tn_small(const float* __restrict__ A, int64_t lda,
-                                                  const float* __restrict__ B1, int64_t ldb1,
-                                                  const float* __restrict__ B2, int64_t ldb2, int64_t K1, int64_t M,
-                                                  int N, int K, int64_t rows_per_split, float* __restrict__ slab) {
+template <typename T>
+__global__ __launch_bounds__(256) void k_tn_small(const T* __restrict__ A, int64_t lda, const T* __restrict__ B1,
+                                                  int64_t ldb1, const T* __restrict__ B2, int64_t ldb2, int64_t K1,
+                                                  int64_t M, int N, int K, int64_t rows_per_split,
+                                                  float* __restrict__ slab) {
   __shared__ float red[256];
   const int P = N * K;
   const int PW = P < 256 ? P : 256;
@@ -160,9 +161,10 @@ __global__ __launch_bounds__(256) void k_tn_small(const float* __restrict__ A, i
     float acc = 0.0f;
     if (rl < R && p < P) {
       const int n = p / K, k = p % K;
-      const float* bcol = k < K1 ? B1 + k : B2 + (k - K1);
+      const T* bcol = k < K1 ? B1 + k : B2 + (k - K1);
       const int64_t ldb = k < K1 ? ldb1 : ldb2;
-      for (int64_t m = mb + rl; m < me; m += R) acc = __fadd_rn(acc, __fmul_rn(A[m * lda + n], bcol[m * ldb]));
+      for (int64_t m = mb + rl; m < me; m += R)
+        acc = __fadd_rn(acc, __fmul_rn(Elem<T>::ld(A + m * lda + n), Elem<T>::ld(bcol + m * ldb)));
     }
     red[t] = acc;
     __syncthreads();
@@ -210,9 +212,144 @@ __global__ __launch_bounds__(256) void k_slab_reduce2(const float* __restrict__ 
   out[(i / K) * ldo + (i % K)] = s;
 }
 
+// ---------------------------------------------------------------------------------------------------
+// bf16 operands (cfg5): out[N, K] (fp32) = A^T [B1 | B2] on v_mfma_f32_32x32x16_bf16.  A bf16 fragment
+// holds 8 consecutive k (= 8 consecutive rows m here) of one column, but both operands are stored
+// m-major, so each stage is transposed on its way into LDS: a thread loads an 8 x 8 block (8 rows m x
+// 16 B of columns; 16 lanes cover a 256-B row segment, coalesced), transposes it in registers (16-bit
+// lane shuffles of 32 words) and writes 8 column-runs of 8 m as 16-B stores into [col][m] images with
+// 144-B rows, from which every fragment is one conflict-free ds_read_b128 as in the NT kernel.  Waves 0-1
+// stage A, waves 2-3 stage B.  64 rows of M per stage, register prefetch of the next stage.
+constexpr int kTnBMh = 64;
+constexpr int kTnLdH = kTnBMh + 8;
+using bf16x8 = __attribute__((ext_vector_type(8))) __bf16;
+
+template <bool kVec>
+__global__ __launch_bounds__(256, 2) void k_gemm_tn_bf16_partial(const uint16_t* __restrict__ A, int64_t lda,
+                                                                 const uint16_t* __restrict__ B1, int64_t ldb1,
+                                                                 const uint16_t* __restrict__ B2, int64_t ldb2,
+                                                                 int64_t K1, int64_t M, int64_t N, int64_t K,
+                                                                 int64_t rows_per_split, float* __restrict__ slab) {
+  __shared__ __attribute__((aligned(16))) uint16_t smem[2 * 128 * kTnLdH];
+  uint16_t* At = smem;
+  uint16_t* Bt = smem + 128 * kTnLdH;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int li = lane & 31, lh = lane >> 5;
+  const int64_t n0 = (int64_t)blockIdx.x * 128;
+  const int64_t k0 = (int64_t)blockIdx.y * 128;
+  const int64_t mb = (int64_t)blockIdx.z * rows_per_split;
+  const int64_t me = mb + rows_per_split < M ? mb + rows_per_split : M;
+  const bool isB = tid >= 128;
+  const int cq = tid & 15;          // 8-column chunk of the 128-wide tile
+  const int rb = (tid & 127) >> 4;  // 8-row block of the 64-row stage
+  uint16_t* T = isB ? Bt : At;
+
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[a][b][e] = 0.0f;
+
+  uint32_t v[8][4];
+  // vector path: k1 % 8 == 0, so a thread's 8-column chunk lies wholly in A, B1 or B2 — one base pointer
+  // and row stride per thread for the whole kernel
+  const int64_t c0 = (isB ? k0 : n0) + 8 * cq;
+  const int64_t lim = isB ? K : N;
+  const uint16_t* vbase = !isB ? A + c0 : (c0 < K1 ? B1 + c0 : B2 + (c0 - K1));
+  const int64_t vld = !isB ? lda : (c0 < K1 ? ldb1 : ldb2);
+  const bool vok = c0 + 7 < lim;
+  auto load_stage = [&](int64_t m0) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int64_t gm = m0 + 8 * rb + i;
+      v[i][0] = v[i][1] = v[i][2] = v[i][3] = 0u;
+      if (gm >= me) continue;
+      if (kVec) {
+        if (vok) {
+          const uint4 x = *reinterpret_cast<const uint4*>(vbase + gm * vld);
+          v[i][0] = x.x; v[i][1] = x.y; v[i][2] = x.z; v[i][3] = x.w;
+        } else {
+#pragma unroll
+          for (int w = 0; w < 4; ++w) {
+            const uint32_t lo = c0 + 2 * w < lim ? vbase[gm * vld + 2 * w] : 0u;
+            const uint32_t hi = c0 + 2 * w + 1 < lim ? vbase[gm * vld + 2 * w + 1] : 0u;
+            v[i][w] = lo | (hi << 16);
+          }
+        }
+      } else {
+        uint32_t t[8];
+#pragma unroll
+        for (int c = 0; c < 8; ++c) {
+          const int64_t k = c0 + c;
+          t[c] = 0u;
+          if (k < lim) t[c] = !isB ? A[gm * lda + k] : (k < K1 ? B1[gm * ldb1 + k] : B2[gm * ldb2 + (k - K1)]);
+        }
+#pragma unroll
+        for (int w = 0; w < 4; ++w) v[i][w] = t[2 * w] | (t[2 * w + 1] << 16);
+      }
+    }
+  };
+  auto store_stage = [&]() {
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+      uint32_t w[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const uint32_t a = v[2 * e][c >> 1], b = v[2 * e + 1][c >> 1];
+        w[e] = (c & 1) ? ((a >> 16) | (b & 0xffff0000u)) : ((a & 0xffffu) | (b << 16));
+      }
+      *reinterpret_cast<uint4*>(T + (8 * cq + c) * kTnLdH + 8 * rb) = make_uint4(w[0], w[1], w[2], w[3]);
+    }
+  };
+  load_stage(mb);
+  store_stage();
+  __syncthreads();
+  for (int64_t m0 = mb; m0 < me; m0 += kTnBMh) {
+    const bool more = m0 + kTnBMh < me;
+    if (more) load_stage(m0 + kTnBMh);
+#pragma unroll
+    for (int st = 0; st < kTnBMh / 16; ++st) {
+      bf16x8 fa[2], fb[2];
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        fa[t] = *reinterpret_cast<const bf16x8*>(At + (wm * 64 + t * 32 + li) * kTnLdH + st * 16 + lh * 8);
+        fb[t] = *reinterpret_cast<const bf16x8*>(Bt + (wn * 64 + t * 32 + li) * kTnLdH + st * 16 + lh * 8);
+      }
+#pragma unroll
+      for (int tm = 0; tm < 2; ++tm)
+#pragma unroll
+        for (int tn = 0; tn < 2; ++tn)
+          acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[tm], fb[tn], acc[tm][tn], 0, 0, 0);
+    }
+    if (more) {
+      __syncthreads();
+      store_stage();
+      __syncthreads();
+    }
+  }
+  float* out = slab + (int64_t)blockIdx.z * N * K;
+#pragma unroll
+  for (int tm = 0; tm < 2; ++tm)
+#pragma unroll
+    for (int tn = 0; tn < 2; ++tn) {
+      const int64_t k = k0 + wn * 64 + tn * 32 + li;
+      if (k >= K) continue;
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int64_t n = n0 + wm * 64 + tm * 32 + (e & 3) + 8 * (e >> 2) + 4 * lh;
+        if (n < N) out[n * K + k] = acc[tm][tn][e];
+      }
+    }
+}
+
 bool tn_is_small(int64_t N, int64_t K) { return N < 16 || K < 16; }
 
-int64_t tn_splits(int64_t M, int64_t N, int64_t K) {
+int64_t tn_splits(int64_t M, int64_t N, int64_t K, int64_t stage_rows = kTnBM) {
   int64_t S;
   if (tn_is_small(N, K)) {
     S = ceil_div(M, 2048);                                 // 2048 rows per workgroup
@@ -220,7 +357,7 @@ int64_t tn_splits(int64_t M, int64_t N, int64_t K) {
   } else {
     const int64_t tiles = ceil_div(N, 128) * ceil_div(K, 128);
     S = ceil_div(1024, tiles);                             // ~4 workgroups per CU
-    const int64_t max_s = ceil_div(M, 8 * kTnBM);          // keep >= 8 stages per split
+    const int64_t max_s = ceil_div(M, 8 * stage_rows);     // keep >= 8 stages per split
     if (S > max_s) S = max_s;
   }
   return S < 1 ? 1 : S;
@@ -271,7 +408,7 @@ extern "C" int hgin_gemm_tn_f32(const float* a, int64_t lda, const float* b1, in
   float* slab = static_cast<float*>(workspace);
   float* part = reinterpret_cast<float*>(static_cast<char*>(workspace) + align_up(sizeof(float) * (size_t)(S * NK), 256));
   if (tn_is_small(N, K)) {
-    k_tn_small<<<(unsigned)S_eff, 256, 0, s>>>(a, lda, b1, ldb1, b2, ldb2, k1, M, (int)N, (int)K, rows, slab);
+    k_tn_small<float><<<(unsigned)S_eff, 256, 0, s>>>(a, lda, b1, ldb1, b2, ldb2, k1, M, (int)N, (int)K, rows, slab);
   } else {
     dim3 grid((unsigned)ceil_div(N, 128), (unsigned)ceil_div(K, 128), (unsigned)S_eff);
     static const int variant = [] {
@@ -292,4 +429,55 @@ extern "C" int hgin_gemm_tn_f32(const float* a, int64_t lda, const float* b1, in
   k_slab_reduce1<<<g1, 256, 0, s>>>(slab, S_eff, NK, part);
   k_slab_reduce2<<<(unsigned)ceil_div(NK, 256), 256, 0, s>>>(part, G, NK, out, K, ldo);
   return check_launch("hgin_gemm_tn_f32");
+}
+
+extern "C" int hgin_gemm_tn_bf16(const uint16_t* a, int64_t lda, const uint16_t* b1, int64_t ldb1, int64_t k1,
+                                 const uint16_t* b2, int64_t ldb2, int64_t M, int64_t N, int64_t K, float* out,
+                                 int64_t ldo, void* workspace, size_t workspace_bytes, void* stream) {
+  HGIN_ARG_CHECK(M >= 0 && N >= 0 && K >= 0 && k1 >= 0 && k1 <= K, "hgin_gemm_tn_bf16: bad sizes");
+  HGIN_ARG_CHECK(N <= 65535 * 128 && K <= 65535 * 128, "hgin_gemm_tn_bf16: N/K too large");
+  if (N == 0 || K == 0) return HGIN_OK;
+  HGIN_ARG_CHECK(out && ldo >= K, "hgin_gemm_tn_bf16: bad output");
+  size_t need = 0;
+  hgin_gemm_tn_workspace_size(M, N, K, &need);
+  if (workspace_bytes < need || !workspace) {
+    set_error("hgin_gemm_tn_bf16: workspace %zu < %zu", workspace_bytes, need);
+    return HGIN_E_WORKSPACE;
+  }
+  hipStream_t s = as_stream(stream);
+  if (M == 0) {
+    for (int64_t n = 0; n < N; ++n) {
+      int rc = memset_async(out + n * ldo, 0, sizeof(float) * (size_t)K, s, "hgin_gemm_tn_bf16");
+      if (rc) return rc;
+    }
+    return HGIN_OK;
+  }
+  HGIN_ARG_CHECK(a && lda >= N && (k1 == 0 || (b1 && ldb1 >= k1)) && (k1 == K || (b2 && ldb2 >= K - k1)),
+                 "hgin_gemm_tn_bf16: bad operand");
+  const bool vec = aligned16(a) && lda % 8 == 0 && (k1 == 0 || (aligned16(b1) && ldb1 % 8 == 0)) &&
+                   (k1 == K || (aligned16(b2) && ldb2 % 8 == 0)) && k1 % 8 == 0;
+  const bool small = tn_is_small(N, K);
+  const int64_t stage = small ? kTnBM : kTnBMh;
+  const int64_t S = tn_splits(M, N, K, stage);     // <= the workspace's split count (stage >= kTnBM)
+  const int64_t rows = ceil_div(ceil_div(M, S), stage) * stage;
+  const int64_t S_eff = ceil_div(M, rows);
+  const int64_t NK = N * K;
+  float* slab = static_cast<float*>(workspace);
+  float* part = reinterpret_cast<float*>(static_cast<char*>(workspace) +
+                                         align_up(sizeof(float) * (size_t)(tn_splits(M, N, K) * NK), 256));
+  if (small) {
+    k_tn_small<uint16_t><<<(unsigned)S_eff, 256, 0, s>>>(a, lda, b1, ldb1, b2, ldb2, k1, M, (int)N, (int)K, rows,
+                                                          slab);
+  } else {
+    dim3 grid((unsigned)ceil_div(N, 128), (unsigned)ceil_div(K, 128), (unsigned)S_eff);
+    if (vec)
+      k_gemm_tn_bf16_partial<true><<<grid, 256, 0, s>>>(a, lda, b1, ldb1, b2, ldb2, k1, M, N, K, rows, slab);
+    else
+      k_gemm_tn_bf16_partial<false><<<grid, 256, 0, s>>>(a, lda, b1, ldb1, b2, ldb2, k1, M, N, K, rows, slab);
+  }
+  const int64_t G = ceil_div(S_eff, kSlabGroup);
+  dim3 g1((unsigned)ceil_div(ceil_div(NK, 4), 256), (unsigned)G);
+  k_slab_reduce1<<<g1, 256, 0, s>>>(slab, S_eff, NK, part);
+  k_slab_reduce2<<<(unsigned)ceil_div(NK, 256), 256, 0, s>>>(part, G, NK, out, K, ldo);
+  return check_launch("hgin_gemm_tn_bf16");
 }

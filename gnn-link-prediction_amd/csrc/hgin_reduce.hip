@@ -5,7 +5,8 @@
 // PyTorch reduces these with atomics / split reductions whose order varies; here every reduction has a
 // fixed shape — per block: a fixed per-thread order over a 256-row chunk, then an LDS combine in fixed
 // order; then one pass that adds the block partials in block order — so gradients are bitwise
-// reproducible run to run.
+// reproducible run to run.  The element type of the row streams is fp32 or bf16 (cfg5); reductions and
+// arithmetic are fp32 either way.
 #include "hgin_common.h"
 
 namespace hgin {
@@ -27,19 +28,21 @@ __device__ __forceinline__ float block_sum_fixed(float v, float* red) {
   return r;
 }
 
-// MODE 0: PReLU backward.  in0 = g_y, in1 = z; out = g_z; colsum(g_z) -> part_col; sum(z<=0 ? z*g : 0) -> part_s
-// MODE 1: combine backward.  in0 = g (self-term columns), in1 = x_dst; out = s*g (optional);
-//         part_s = sum(g * x_dst); no column sums.
-// VEC = 4: each thread owns 4 consecutive columns (16-B loads / stores; needs N % 4 == 0 and aligned rows).
-template <int VEC>
-struct RowVec;
-template <>
-struct RowVec<1> {
-  static __device__ __forceinline__ void load(const float* p, float (&v)[1]) { v[0] = *p; }
-  static __device__ __forceinline__ void store(float* p, const float (&v)[1]) { *p = v[0]; }
+// VEC = 4: each thread owns 4 consecutive columns (16-B fp32 / 8-B bf16 accesses; needs N % 4 == 0 and
+// aligned rows).
+template <int VEC, typename T>
+struct RowVec {
+  static __device__ __forceinline__ void load(const T* p, float (&v)[VEC]) {
+#pragma unroll
+    for (int q = 0; q < VEC; ++q) v[q] = Elem<T>::ld(p + q);
+  }
+  static __device__ __forceinline__ void store(T* p, const float (&v)[VEC]) {
+#pragma unroll
+    for (int q = 0; q < VEC; ++q) Elem<T>::st(p + q, v[q]);
+  }
 };
 template <>
-struct RowVec<4> {
+struct RowVec<4, float> {
   static __device__ __forceinline__ void load(const float* p, float (&v)[4]) {
     const float4 t = *reinterpret_cast<const float4*>(p);
     v[0] = t.x; v[1] = t.y; v[2] = t.z; v[3] = t.w;
@@ -48,12 +51,25 @@ struct RowVec<4> {
     *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
   }
 };
+template <>
+struct RowVec<4, uint16_t> {
+  static __device__ __forceinline__ void load(const uint16_t* p, float (&v)[4]) {
+    const uint2 t = *reinterpret_cast<const uint2*>(p);
+    v[0] = bf_lo(t.x); v[1] = bf_hi(t.x); v[2] = bf_lo(t.y); v[3] = bf_hi(t.y);
+  }
+  static __device__ __forceinline__ void store(uint16_t* p, const float (&v)[4]) {
+    *reinterpret_cast<uint2*>(p) = make_uint2(pack_bf2(v[0], v[1]), pack_bf2(v[2], v[3]));
+  }
+};
 
-template <int MODE, int VEC>
-__global__ __launch_bounds__(256) void k_rows_bwd(const float* __restrict__ in0, int64_t ld0,
-                                                  const float* __restrict__ in1, int64_t ld1, int64_t M, int N,
-                                                  const float* __restrict__ scalar, float* __restrict__ out,
-                                                  int64_t ldo, float* __restrict__ part_col,
+// MODE 0: PReLU backward.  in0 = g_y, in1 = z; out = g_z; colsum(g_z) -> part_col; sum(z<=0 ? z*g : 0) -> part_s
+//         (the column sums and the slope sum use the fp32 g_z before any bf16 rounding of the output)
+// MODE 1: combine backward.  in0 = g (self-term columns), in1 = x_dst; out = s*g (optional);
+//         part_s = sum(g * x_dst); no column sums.
+template <int MODE, int VEC, typename T>
+__global__ __launch_bounds__(256) void k_rows_bwd(const T* __restrict__ in0, int64_t ld0, const T* __restrict__ in1,
+                                                  int64_t ld1, int64_t M, int N, const float* __restrict__ scalar,
+                                                  T* __restrict__ out, int64_t ldo, float* __restrict__ part_col,
                                                   float* __restrict__ part_s) {
   __shared__ float red[256 * VEC];
   const int t = threadIdx.x;
@@ -78,8 +94,8 @@ __global__ __launch_bounds__(256) void k_rows_bwd(const float* __restrict__ in0,
     if (active && c < N) {
       for (int64_t r = r0 + rl; r < r1; r += RL) {
         float g[VEC], x[VEC], o[VEC];
-        RowVec<VEC>::load(in0 + r * ld0 + c, g);
-        RowVec<VEC>::load(in1 + r * ld1 + c, x);
+        RowVec<VEC, T>::load(in0 + r * ld0 + c, g);
+        RowVec<VEC, T>::load(in1 + r * ld1 + c, x);
 #pragma unroll
         for (int q = 0; q < VEC; ++q) {
           if (MODE == 0) {
@@ -92,7 +108,7 @@ __global__ __launch_bounds__(256) void k_rows_bwd(const float* __restrict__ in0,
             ssum = __fadd_rn(ssum, __fmul_rn(g[q], x[q]));
           }
         }
-        if (MODE == 0 || out) RowVec<VEC>::store(out + r * ldo + c, o);
+        if (MODE == 0 || out) RowVec<VEC, T>::store(out + r * ldo + c, o);
       }
     }
     if (MODE == 0) {
@@ -114,19 +130,20 @@ __global__ __launch_bounds__(256) void k_rows_bwd(const float* __restrict__ in0,
   if (t == 0) part_s[blockIdx.x] = bs;
 }
 
-template <int MODE>
-void launch_rows_bwd(bool vec, unsigned nblk, hipStream_t s, const float* in0, int64_t ld0, const float* in1,
-                     int64_t ld1, int64_t M, int N, const float* scalar, float* out, int64_t ldo, float* part_col,
-                     float* part_s) {
+template <int MODE, typename T>
+void launch_rows_bwd(bool vec, unsigned nblk, hipStream_t s, const T* in0, int64_t ld0, const T* in1, int64_t ld1,
+                     int64_t M, int N, const float* scalar, T* out, int64_t ldo, float* part_col, float* part_s) {
   if (vec)
-    k_rows_bwd<MODE, 4><<<nblk, 256, 0, s>>>(in0, ld0, in1, ld1, M, N, scalar, out, ldo, part_col, part_s);
+    k_rows_bwd<MODE, 4, T><<<nblk, 256, 0, s>>>(in0, ld0, in1, ld1, M, N, scalar, out, ldo, part_col, part_s);
   else
-    k_rows_bwd<MODE, 1><<<nblk, 256, 0, s>>>(in0, ld0, in1, ld1, M, N, scalar, out, ldo, part_col, part_s);
+    k_rows_bwd<MODE, 1, T><<<nblk, 256, 0, s>>>(in0, ld0, in1, ld1, M, N, scalar, out, ldo, part_col, part_s);
 }
 
-bool rows_vec_ok(int64_t N, const float* a, int64_t lda, const float* b, int64_t ldb, const float* c, int64_t ldc) {
-  return N % 4 == 0 && aligned16(a) && lda % 4 == 0 && aligned16(b) && ldb % 4 == 0 &&
-         (c == nullptr || (aligned16(c) && ldc % 4 == 0));
+template <typename T>
+bool rows_vec_ok(int64_t N, const T* a, int64_t lda, const T* b, int64_t ldb, const T* c, int64_t ldc) {
+  const uintptr_t align = 4 * sizeof(T);
+  auto ok = [&](const T* p) { return (reinterpret_cast<uintptr_t>(p) & (align - 1)) == 0; };
+  return N % 4 == 0 && ok(a) && lda % 4 == 0 && ok(b) && ldb % 4 == 0 && (c == nullptr || (ok(c) && ldc % 4 == 0));
 }
 
 // Sum block partials in a fixed order: one workgroup per column, strided per-thread sums + fixed tree.
@@ -150,6 +167,61 @@ __global__ __launch_bounds__(256) void k_final_scalar(const float* __restrict__ 
   if (threadIdx.x == 0) out[0] = tot;
 }
 
+size_t prelu_ws_bytes(int64_t M, int64_t N) {
+  const int64_t nblk = ceil_div(M > 0 ? M : 1, kRowsPerBlock);
+  return align_up(sizeof(float) * (size_t)(nblk * N), 256) + align_up(sizeof(float) * (size_t)nblk, 256);
+}
+
+template <typename T>
+int prelu_bwd(const char* what, const T* g_y, int64_t ld_gy, const T* z, int64_t M, int64_t N, const float* prelu,
+              T* g_z, float* g_prelu, float* g_bias, void* workspace, size_t workspace_bytes, void* stream) {
+  HGIN_ARG_CHECK(M >= 0 && N >= 0 && N < (1 << 24), "%s: bad sizes", what);
+  HGIN_ARG_CHECK(g_prelu && g_bias && prelu, "%s: NULL output", what);
+  const size_t need = prelu_ws_bytes(M, N);
+  if (workspace_bytes < need || !workspace) {
+    set_error("%s: workspace %zu < %zu", what, workspace_bytes, need);
+    return HGIN_E_WORKSPACE;
+  }
+  hipStream_t s = as_stream(stream);
+  if (M == 0 || N == 0) {
+    int rc = N ? memset_async(g_bias, 0, sizeof(float) * (size_t)N, s, what) : HGIN_OK;
+    if (rc == HGIN_OK) rc = memset_async(g_prelu, 0, sizeof(float), s, what);
+    return rc;
+  }
+  HGIN_ARG_CHECK(g_y && z && g_z && ld_gy >= N, "%s: NULL operand or ld_gy < N", what);
+  const int64_t nblk = ceil_div(M, kRowsPerBlock);
+  float* part_col = static_cast<float*>(workspace);
+  float* part_s = reinterpret_cast<float*>(static_cast<char*>(workspace) +
+                                           align_up(sizeof(float) * (size_t)(nblk * N), 256));
+  launch_rows_bwd<0, T>(rows_vec_ok<T>(N, g_y, ld_gy, z, N, g_z, N), (unsigned)nblk, s, g_y, ld_gy, z, N, M, (int)N,
+                        prelu, g_z, N, part_col, part_s);
+  k_final_cols<<<(unsigned)N, 256, 0, s>>>(part_col, nblk, (int)N, g_bias);
+  k_final_scalar<<<1, 256, 0, s>>>(part_s, nblk, g_prelu);
+  return check_launch(what);
+}
+
+template <typename T>
+int combine_bwd(const char* what, const T* g, int64_t ld_g, const T* x_dst, int64_t ld_dst, int64_t n_rows,
+                int64_t f_dst, const float* eps, T* g_x_dst, int64_t ld_gx, float* g_eps, void* workspace,
+                size_t workspace_bytes, void* stream) {
+  HGIN_ARG_CHECK(n_rows >= 0 && f_dst >= 0 && f_dst < (1 << 24), "%s: bad sizes", what);
+  HGIN_ARG_CHECK(eps && g_eps, "%s: NULL eps/g_eps", what);
+  const size_t need = align_up(sizeof(float) * (size_t)ceil_div(n_rows > 0 ? n_rows : 1, kRowsPerBlock), 256);
+  if (workspace_bytes < need || !workspace) {
+    set_error("%s: workspace %zu < %zu", what, workspace_bytes, need);
+    return HGIN_E_WORKSPACE;
+  }
+  hipStream_t s = as_stream(stream);
+  if (n_rows == 0 || f_dst == 0) return memset_async(g_eps, 0, sizeof(float), s, what);
+  HGIN_ARG_CHECK(g && x_dst, "%s: NULL operand", what);
+  const int64_t nblk = ceil_div(n_rows, kRowsPerBlock);
+  float* part_s = static_cast<float*>(workspace);
+  launch_rows_bwd<1, T>(rows_vec_ok<T>(f_dst, g, ld_g, x_dst, ld_dst, g_x_dst, ld_gx), (unsigned)nblk, s, g, ld_g,
+                        x_dst, ld_dst, n_rows, (int)f_dst, eps, g_x_dst, ld_gx, nullptr, part_s);
+  k_final_scalar<<<1, 256, 0, s>>>(part_s, nblk, g_eps);
+  return check_launch(what);
+}
+
 }  // namespace
 }  // namespace hgin
 
@@ -157,38 +229,22 @@ using namespace hgin;
 
 extern "C" int hgin_prelu_bwd_workspace_size(int64_t M, int64_t N, size_t* bytes) {
   HGIN_ARG_CHECK(bytes && M >= 0 && N >= 0, "hgin_prelu_bwd_workspace_size: bad args");
-  const int64_t nblk = ceil_div(M > 0 ? M : 1, kRowsPerBlock);
-  *bytes = align_up(sizeof(float) * (size_t)(nblk * N), 256) + align_up(sizeof(float) * (size_t)nblk, 256);
+  *bytes = prelu_ws_bytes(M, N);
   return HGIN_OK;
 }
 
-extern "C" int hgin_prelu_bwd_f32(const float* g_y, int64_t ld_gy, const float* z, int64_t M, int64_t N, const float* prelu,
-                                  float* g_z, float* g_prelu, float* g_bias, void* workspace, size_t workspace_bytes,
-                                  void* stream) {
-  HGIN_ARG_CHECK(M >= 0 && N >= 0 && N < (1 << 24), "hgin_prelu_bwd_f32: bad sizes");
-  HGIN_ARG_CHECK(g_prelu && g_bias && prelu, "hgin_prelu_bwd_f32: NULL output");
-  size_t need = 0;
-  hgin_prelu_bwd_workspace_size(M, N, &need);
-  if (workspace_bytes < need || !workspace) {
-    set_error("hgin_prelu_bwd_f32: workspace %zu < %zu", workspace_bytes, need);
-    return HGIN_E_WORKSPACE;
-  }
-  hipStream_t s = as_stream(stream);
-  if (M == 0 || N == 0) {
-    int rc = N ? memset_async(g_bias, 0, sizeof(float) * (size_t)N, s, "hgin_prelu_bwd_f32") : HGIN_OK;
-    if (rc == HGIN_OK) rc = memset_async(g_prelu, 0, sizeof(float), s, "hgin_prelu_bwd_f32");
-    return rc;
-  }
-  HGIN_ARG_CHECK(g_y && z && g_z && ld_gy >= N, "hgin_prelu_bwd_f32: NULL operand or ld_gy < N");
-  const int64_t nblk = ceil_div(M, kRowsPerBlock);
-  float* part_col = static_cast<float*>(workspace);
-  float* part_s = reinterpret_cast<float*>(static_cast<char*>(workspace) +
-                                           align_up(sizeof(float) * (size_t)(nblk * N), 256));
-  launch_rows_bwd<0>(rows_vec_ok(N, g_y, ld_gy, z, N, g_z, N), (unsigned)nblk, s, g_y, ld_gy, z, N, M, (int)N,
-                     prelu, g_z, N, part_col, part_s);
-  k_final_cols<<<(unsigned)N, 256, 0, s>>>(part_col, nblk, (int)N, g_bias);
-  k_final_scalar<<<1, 256, 0, s>>>(part_s, nblk, g_prelu);
-  return check_launch("hgin_prelu_bwd_f32");
+extern "C" int hgin_prelu_bwd_f32(const float* g_y, int64_t ld_gy, const float* z, int64_t M, int64_t N,
+                                  const float* prelu, float* g_z, float* g_prelu, float* g_bias, void* workspace,
+                                  size_t workspace_bytes, void* stream) {
+  return prelu_bwd<float>("hgin_prelu_bwd_f32", g_y, ld_gy, z, M, N, prelu, g_z, g_prelu, g_bias, workspace,
+                          workspace_bytes, stream);
+}
+
+extern "C" int hgin_prelu_bwd_bf16(const uint16_t* g_y, int64_t ld_gy, const uint16_t* z, int64_t M, int64_t N,
+                                   const float* prelu, uint16_t* g_z, float* g_prelu, float* g_bias, void* workspace,
+                                   size_t workspace_bytes, void* stream) {
+  return prelu_bwd<uint16_t>("hgin_prelu_bwd_bf16", g_y, ld_gy, z, M, N, prelu, g_z, g_prelu, g_bias, workspace,
+                             workspace_bytes, stream);
 }
 
 extern "C" int hgin_combine_bwd_workspace_size(int64_t n_rows, size_t* bytes) {
@@ -200,23 +256,13 @@ extern "C" int hgin_combine_bwd_workspace_size(int64_t n_rows, size_t* bytes) {
 extern "C" int hgin_combine_bwd_f32(const float* g, int64_t ld_g, const float* x_dst, int64_t ld_dst, int64_t n_rows,
                                     int64_t f_dst, const float* eps, float* g_x_dst, int64_t ld_gx, float* g_eps,
                                     void* workspace, size_t workspace_bytes, void* stream) {
-  HGIN_ARG_CHECK(n_rows >= 0 && f_dst >= 0 && f_dst < (1 << 24), "hgin_combine_bwd_f32: bad sizes");
-  HGIN_ARG_CHECK(eps && g_eps, "hgin_combine_bwd_f32: NULL eps/g_eps");
-  size_t need = 0;
-  hgin_combine_bwd_workspace_size(n_rows, &need);
-  if (workspace_bytes < need || !workspace) {
-    set_error("hgin_combine_bwd_f32: workspace %zu < %zu", workspace_bytes, need);
-    return HGIN_E_WORKSPACE;
-  }
-  hipStream_t s = as_stream(stream);
-  if (n_rows == 0 || f_dst == 0) {
-    return memset_async(g_eps, 0, sizeof(float), s, "hgin_combine_bwd_f32");
-  }
-  HGIN_ARG_CHECK(g && x_dst, "hgin_combine_bwd_f32: NULL operand");
-  const int64_t nblk = ceil_div(n_rows, kRowsPerBlock);
-  float* part_s = static_cast<float*>(workspace);
-  launch_rows_bwd<1>(rows_vec_ok(f_dst, g, ld_g, x_dst, ld_dst, g_x_dst, ld_gx), (unsigned)nblk, s, g, ld_g, x_dst,
-                     ld_dst, n_rows, (int)f_dst, eps, g_x_dst, ld_gx, nullptr, part_s);
-  k_final_scalar<<<1, 256, 0, s>>>(part_s, nblk, g_eps);
-  return check_launch("hgin_combine_bwd_f32");
+  return combine_bwd<float>("hgin_combine_bwd_f32", g, ld_g, x_dst, ld_dst, n_rows, f_dst, eps, g_x_dst, ld_gx, g_eps,
+                            workspace, workspace_bytes, stream);
+}
+
+extern "C" int hgin_combine_bwd_bf16(const uint16_t* g, int64_t ld_g, const uint16_t* x_dst, int64_t ld_dst,
+                                     int64_t n_rows, int64_t f_dst, const float* eps, uint16_t* g_x_dst, int64_t ld_gx,
+                                     float* g_eps, void* workspace, size_t workspace_bytes, void* stream) {
+  return combine_bwd<uint16_t>("hgin_combine_bwd_bf16", g, ld_g, x_dst, ld_dst, n_rows, f_dst, eps, g_x_dst, ld_gx,
+                               g_eps, workspace, workspace_bytes, stream);
 }

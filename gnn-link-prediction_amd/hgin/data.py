@@ -62,6 +62,7 @@ class GraphConfig:
     concat_path: bool = True         # config.json:24
     global_feats: bool = False       # config.json:25
     mlp_layers: List[int] = field(default_factory=lambda: [128, 32])   # config.json:26
+    feat_dtype: str = "f32"          # "bf16": cfg5 storage (features, activations, gradients); fp32 params
 
     @property
     def graph_edges(self) -> int:
@@ -98,6 +99,12 @@ CONFIGS: Dict[str, GraphConfig] = {
     # cfg4 component: one eighth of cfg3 (one per GPU of the 8-GPU node)
     "cfg4c": GraphConfig("cfg4c", 750_000, 375_000, 125_000, 3_750_000, 625_000, 3_750_000,
                          256, 256, 256, 256, 3),
+    # configs[4]: cfg3 with bf16 node features + bf16 MFMA update (fp32 accumulate, fp32 master weights)
+    "cfg5": GraphConfig("cfg5", 6_000_000, 3_000_000, 1_000_000, 30_000_000, 5_000_000, 30_000_000,
+                        256, 256, 256, 256, 3, feat_dtype="bf16"),
+    # cfg5 at cfg2 size (the bf16 counterpart of the headline fp32 config)
+    "cfg2bf": GraphConfig("cfg2bf", 600_000, 300_000, 100_000, 3_000_000, 500_000, 3_000_000,
+                          128, 128, 128, 128, 2, feat_dtype="bf16"),
 }
 
 
@@ -152,6 +159,8 @@ def synthetic_graph(cfg: GraphConfig, seed: int = 0, device="cpu") -> HeteroGrap
     rn = lambda n, f: torch.randn(n, f, generator=g, device=device)  # noqa: E731
     x = {"path": rn(cfg.n_path, cfg.f_path), "link": rn(cfg.n_link, cfg.f_link),
          "node": rn(cfg.n_node, cfg.f_node)}
+    if cfg.feat_dtype == "bf16":
+        x = {t: v.to(torch.bfloat16) for t, v in x.items()}
     y = torch.rand(cfg.n_path, generator=g, device=device) + 0.5
     batch = {t: torch.zeros(x[t].shape[0], dtype=torch.long, device=device) for t in NODE_TYPES}
     return HeteroGraph(x, ei, y, batch)

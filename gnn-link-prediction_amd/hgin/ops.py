@@ -45,9 +45,26 @@ def require_device(*tensors, what: str = "hgin") -> None:
 
 
 def _f32(t: Tensor, what: str) -> Tensor:
-    if t.dtype != torch.float32:
-        raise TypeError(f"{what}: expected float32, got {t.dtype}")
+    """Storage dtype check: float32, or bfloat16 for the cfg5 path (bf16 storage, fp32 arithmetic)."""
+    if t.dtype not in (torch.float32, torch.bfloat16):
+        raise TypeError(f"{what}: expected float32 or bfloat16, got {t.dtype}")
     return t
+
+
+def _sfx(t: Tensor) -> str:
+    """Entry-point suffix for a storage dtype (hgin_*_f32 / hgin_*_bf16)."""
+    return "bf16" if t.dtype == torch.bfloat16 else "f32"
+
+
+def _same_dtype(what: str, *ts) -> None:
+    dts = {t.dtype for t in ts if t is not None}
+    if len(dts) > 1:
+        raise TypeError(f"{what}: mixed feature dtypes {sorted(map(str, dts))}")
+
+
+def _as(t: Optional[Tensor], dtype) -> Optional[Tensor]:
+    """A GEMM operand copy of an fp32 master parameter in the storage dtype (bf16 path)."""
+    return t if (t is None or t.dtype == dtype) else t.to(dtype)
 
 
 def _workspace(nbytes: int, device) -> Tensor:
@@ -169,15 +186,16 @@ def aggregate_into(csr: Csr, x_src: Tensor, x_dst: Optional[Tensor], eps: Option
     f_dst = int(x_dst.size(1)) if x_dst is not None else 0
 
     def launch():
-        _lib.call("hgin_aggregate_f32", _p(csr.rowptr), _p(csr.col), csr.n_rows, _p(x_src), x_src.stride(0),
-                  f_src, _p(x_dst), x_dst.stride(0) if x_dst is not None else 0, f_dst, _p(eps), mode, _p(out),
-                  out.stride(0), _stream(out))
+        _lib.call(f"hgin_aggregate_{_sfx(x_src)}", _p(csr.rowptr), _p(csr.col), csr.n_rows, _p(x_src),
+                  x_src.stride(0), f_src, _p(x_dst), x_dst.stride(0) if x_dst is not None else 0, f_dst, _p(eps),
+                  mode, _p(out), out.stride(0), _stream(out))
 
     probe = profiling.active()
     if probe is None:
         launch()
     else:
-        probe.around("aggregate", profiling.aggregate_bytes(csr.n_edges, csr.n_rows, f_src, f_dst, mode), launch)
+        probe.around("aggregate", profiling.aggregate_bytes(csr.n_edges, csr.n_rows, f_src, f_dst, mode,
+                                                            x_src.element_size()), launch)
     return out
 
 
@@ -193,8 +211,9 @@ def prelu_bwd(g_y: Tensor, z: Tensor, prelu: Tensor):
     nbytes = ctypes.c_size_t(0)
     _lib.check(_lib.lib().hgin_prelu_bwd_workspace_size(M, N, ctypes.byref(nbytes)), "prelu_bwd_workspace_size")
     ws = _workspace(nbytes.value, z.device)
-    _lib.call("hgin_prelu_bwd_f32", _p(g_y), g_y.stride(0), _p(z), M, N, _p(prelu), _p(g_z), _p(g_a), _p(g_b), _p(ws),
-              nbytes.value, _stream(z))
+    _same_dtype("prelu_bwd", g_y, z)
+    _lib.call(f"hgin_prelu_bwd_{_sfx(z)}", _p(g_y), g_y.stride(0), _p(z), M, N, _p(prelu), _p(g_z), _p(g_a), _p(g_b),
+              _p(ws), nbytes.value, _stream(z))
     return g_z, g_a, g_b
 
 
@@ -205,26 +224,30 @@ def combine_bwd(g: Tensor, x_dst: Tensor, eps: Tensor, want_gx: bool):
     nbytes = ctypes.c_size_t(0)
     _lib.check(_lib.lib().hgin_combine_bwd_workspace_size(n, ctypes.byref(nbytes)), "combine_bwd_workspace_size")
     ws = _workspace(nbytes.value, x_dst.device)
-    _lib.call("hgin_combine_bwd_f32", _p(g), g.stride(0), _p(x_dst), x_dst.stride(0), n, f, _p(eps), _p(gx),
-              gx.stride(0) if gx is not None else 0, _p(g_eps), _p(ws), nbytes.value, _stream(x_dst))
+    _same_dtype("combine_bwd", g, x_dst)
+    _lib.call(f"hgin_combine_bwd_{_sfx(x_dst)}", _p(g), g.stride(0), _p(x_dst), x_dst.stride(0), n, f, _p(eps),
+              _p(gx), gx.stride(0) if gx is not None else 0, _p(g_eps), _p(ws), nbytes.value, _stream(x_dst))
     return gx, g_eps
 
 
 def gemm_nt(a: Tensor, b: Tensor) -> Tensor:
-    """c = a @ b^T on the f32 matrix cores (a [M,K], b [N,K], both K-contiguous)."""
+    """c = a @ b^T on the matrix cores (a [M,K], b [N,K], both K-contiguous; c in the operands' dtype)."""
     a, b = _rowmajor(a), _rowmajor(b)
+    _same_dtype("gemm_nt", a, b)
     M, K = a.shape
     N = b.shape[0]
-    c = torch.empty(M, N, dtype=torch.float32, device=a.device)
-    _lib.call("hgin_gemm_nt_f32", _p(a), a.stride(0), _p(b), b.stride(0), _p(c), c.stride(0), M, N, K, _stream(a))
+    c = torch.empty(M, N, dtype=a.dtype, device=a.device)
+    _lib.call(f"hgin_gemm_nt_{_sfx(a)}", _p(a), a.stride(0), _p(b), b.stride(0), _p(c), c.stride(0), M, N, K,
+              _stream(a))
     return c
 
 
 def gemm_tn(a: Tensor, b1: Tensor, b2: Optional[Tensor] = None) -> Tensor:
-    """out[N, K] = a[M, N]^T @ [b1 | b2] (weight gradients), split-M MFMA + deterministic slab reduce."""
+    """out[N, K] (fp32) = a[M, N]^T @ [b1 | b2] (weight gradients), split-M MFMA + deterministic slab reduce."""
     a, b1 = _rowmajor(a), _rowmajor(b1)
     if b2 is not None:
         b2 = _rowmajor(b2)
+    _same_dtype("gemm_tn", a, b1, b2)
     M, N = a.shape
     k1 = b1.shape[1]
     K = k1 + (b2.shape[1] if b2 is not None else 0)
@@ -232,7 +255,7 @@ def gemm_tn(a: Tensor, b1: Tensor, b2: Optional[Tensor] = None) -> Tensor:
     nbytes = ctypes.c_size_t(0)
     _lib.check(_lib.lib().hgin_gemm_tn_workspace_size(M, N, K, ctypes.byref(nbytes)), "gemm_tn_workspace_size")
     ws = _workspace(nbytes.value, a.device)
-    _lib.call("hgin_gemm_tn_f32", _p(a), a.stride(0), _p(b1), b1.stride(0), k1, _p(b2),
+    _lib.call(f"hgin_gemm_tn_{_sfx(a)}", _p(a), a.stride(0), _p(b1), b1.stride(0), k1, _p(b2),
               b2.stride(0) if b2 is not None else 0, M, N, K, _p(out), out.stride(0), _p(ws), nbytes.value,
               _stream(a))
     return out
@@ -240,21 +263,27 @@ def gemm_tn(a: Tensor, b1: Tensor, b2: Optional[Tensor] = None) -> Tensor:
 
 def gin_mlp_fwd(comb: Tensor, weight: Tensor, bias: Tensor, prelu: Optional[Tensor], accum: Optional[Tensor],
                 save_z: bool = True, comb2: Optional[Tensor] = None):
-    """y = prelu([comb | comb2] @ W^T + b) [+ accum]  (prelu None: plain Linear, y = z, nothing saved)."""
+    """y = prelu([comb | comb2] @ W^T + b) [+ accum]  (prelu None: plain Linear, y = z, nothing saved).
+
+    fp32 storage: everything fp32.  bf16 storage (cfg5): comb / comb2 / weight / accum / z / y bf16, bias and
+    prelu fp32; the plain Linear (the readout head) returns fp32."""
     M, k1 = comb.shape
     K = k1 + (comb2.shape[1] if comb2 is not None else 0)
     N = weight.shape[0]
-    z = torch.empty(M, N, dtype=torch.float32, device=comb.device) if (save_z and prelu is not None) else None
-    y = torch.empty(M, N, dtype=torch.float32, device=comb.device)
+    _same_dtype("gin_mlp_fwd", comb, comb2, weight, accum)
+    sfx = _sfx(comb)
+    dt = comb.dtype
+    z = torch.empty(M, N, dtype=dt, device=comb.device) if (save_z and prelu is not None) else None
+    y = torch.empty(M, N, dtype=dt if prelu is not None else torch.float32, device=comb.device)
     ld2 = comb2.stride(0) if comb2 is not None else 0
 
     def launch():
         if prelu is None:
-            _lib.call("hgin_linear_fwd_f32", _p(comb), comb.stride(0), k1, _p(comb2), ld2, _p(weight), _p(bias),
+            _lib.call(f"hgin_linear_fwd_{sfx}", _p(comb), comb.stride(0), k1, _p(comb2), ld2, _p(weight), _p(bias),
                       _p(y), M, N, K, _stream(comb))
         else:
-            _lib.call("hgin_gin_mlp_fwd_f32", _p(comb), comb.stride(0), k1, _p(comb2), ld2, _p(weight), _p(bias),
-                      _p(prelu), _p(accum), _p(z), _p(y), M, N, K, _stream(comb))
+            _lib.call(f"hgin_gin_mlp_fwd_{sfx}", _p(comb), comb.stride(0), k1, _p(comb2), ld2, _p(weight),
+                      _p(bias), _p(prelu), _p(accum), _p(z), _p(y), M, N, K, _stream(comb))
 
     probe = profiling.active()
     if probe is None:
@@ -270,7 +299,7 @@ def gin_mlp_fwd(comb: Tensor, weight: Tensor, bias: Tensor, prelu: Optional[Tens
 def _backward_aggregate(graph: RelationGraph, g_agg: Tensor) -> Tensor:
     """d x_src = index_add over the reversed relation = the A3 kernel on the CSC (edge order kept)."""
     csc = graph.csc
-    g = torch.empty(graph.n_src, g_agg.size(1), dtype=torch.float32, device=g_agg.device)
+    g = torch.empty(graph.n_src, g_agg.size(1), dtype=g_agg.dtype, device=g_agg.device)
     return aggregate_into(csc, g_agg, None, None, COMBINE_NONE, g)
 
 
@@ -281,7 +310,7 @@ class _AggregateFn(torch.autograd.Function):
     def forward(ctx, x_src, x_dst, eps, graph: RelationGraph, mode: int):
         f_src = x_src.size(1)
         width = f_src + (x_dst.size(1) if mode == COMBINE_CONCAT else 0)
-        out = torch.empty(graph.n_dst, width, dtype=torch.float32, device=x_src.device)
+        out = torch.empty(graph.n_dst, width, dtype=x_src.dtype, device=x_src.device)
         aggregate_into(graph.csr, x_src, x_dst, eps, mode, out)
         ctx.graph, ctx.mode, ctx.f_src = graph, mode, f_src
         ctx.save_for_backward(x_dst, eps)
@@ -308,16 +337,17 @@ class _GINConvFn(torch.autograd.Function):
     def forward(ctx, x_src, x_dst, eps, weight, bias, prelu, accum, graph: RelationGraph, mode: int):
         f_src = x_src.size(1)
         width = f_src + (x_dst.size(1) if mode == COMBINE_CONCAT else 0)
-        comb = torch.empty(graph.n_dst, width, dtype=torch.float32, device=x_src.device)
+        comb = torch.empty(graph.n_dst, width, dtype=x_src.dtype, device=x_src.device)
         aggregate_into(graph.csr, x_src, x_dst, eps, mode, comb)
-        z, y = gin_mlp_fwd(comb, weight, bias, prelu, accum)
+        w_op = _as(weight, x_src.dtype)          # bf16 path: the GEMM reads a bf16 copy of the fp32 master
+        z, y = gin_mlp_fwd(comb, w_op, bias, prelu, accum)
         ctx.graph, ctx.mode, ctx.f_src = graph, mode, f_src
-        ctx.save_for_backward(x_dst, eps, weight, prelu, comb, z)
+        ctx.save_for_backward(x_dst, eps, w_op, prelu, comb, z)
         return y
 
     @staticmethod
     def backward(ctx, g_y):
-        x_dst, eps, weight, prelu, comb, z = ctx.saved_tensors
+        x_dst, eps, weight, prelu, comb, z = ctx.saved_tensors   # weight: the operand copy the forward used
         need = ctx.needs_input_grad
         need_src, need_dst, need_eps, need_w, need_b, need_a, need_acc = need[:7]
         g_y = _rowmajor(g_y)
@@ -370,8 +400,9 @@ class _LinearPReLUFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x1, x2, weight, bias, prelu):
-        z, y = gin_mlp_fwd(x1, weight, bias, prelu, None, comb2=x2)
-        ctx.save_for_backward(x1, x2, weight, prelu, z)
+        w_op = _as(weight, x1.dtype)
+        z, y = gin_mlp_fwd(x1, w_op, bias, prelu, None, comb2=x2)
+        ctx.save_for_backward(x1, x2, w_op, prelu, z)
         return y
 
     @staticmethod
@@ -382,6 +413,7 @@ class _LinearPReLUFn(torch.autograd.Function):
         if prelu is None:   # g_z = g_y; the PReLU-backward kernel with slope 1 yields the bias column sums
             g_z, _, g_b = prelu_bwd(g_y, g_y, _one(g_y.device))
             g_a = None
+            g_z = g_z.to(x1.dtype)     # bf16 path: the head's output (and g_y) are fp32, its operands bf16
         else:
             g_z, g_a, g_b = prelu_bwd(g_y, z, prelu)
         k1 = x1.size(1)
@@ -401,6 +433,7 @@ def linear_prelu(x1: Tensor, weight: Tensor, bias: Tensor, prelu: Optional[Tenso
         x2 = _rowmajor(_f32(x2, "x2"))
         if x2.size(0) != x1.size(0):
             raise RuntimeError("linear_prelu: x1 / x2 row counts differ")
+    _same_dtype("hgin.linear_prelu", x1, x2)
     width = x1.size(1) + (x2.size(1) if x2 is not None else 0)
     if weight.size(1) != width:
         raise RuntimeError(f"mat1 and mat2 shapes cannot be multiplied ({x1.size(0)}x{width} and "
@@ -414,6 +447,7 @@ def aggregate(x_src: Tensor, x_dst: Optional[Tensor], eps: Optional[Tensor], gra
     x_src = _rowmajor(_f32(x_src, "x_src"))
     if x_dst is not None:
         x_dst = _rowmajor(_f32(x_dst, "x_dst"))
+    _same_dtype("hgin.aggregate", x_src, x_dst)
     if mode == COMBINE_ADD and x_dst.size(1) != x_src.size(1):
         raise RuntimeError(f"GINConv add: feature sizes differ ({x_src.size(1)} vs {x_dst.size(1)})")
     if mode != COMBINE_NONE and x_dst.size(0) != graph.n_dst:
@@ -432,6 +466,7 @@ def gin_conv(x_src: Tensor, x_dst: Tensor, eps: Tensor, weight: Tensor, bias: Te
     if weight.size(1) != width:
         raise RuntimeError(f"mat1 and mat2 shapes cannot be multiplied ({graph.n_dst}x{width} and "
                            f"{weight.size(1)}x{weight.size(0)})")
+    _same_dtype("hgin.gin_conv", x_src, x_dst, accum)
     if accum is not None:
         accum = accum.contiguous()      # the epilogue reads accum with row stride N
     return _GINConvFn.apply(x_src, x_dst, eps, _rowmajor(weight), bias.contiguous(), prelu, accum, graph, mode)

@@ -54,10 +54,11 @@ def active() -> Optional[KernelProbe]:
     return _probe
 
 
-def aggregate_bytes(n_edges: int, n_rows: int, f_src: int, f_dst: int, mode: int) -> int:
-    """E*(I + s*F) + (N+1)*I + N*s*F_out  [+ N*s*F_dst read for the self term]."""
+def aggregate_bytes(n_edges: int, n_rows: int, f_src: int, f_dst: int, mode: int, s: int = 4) -> int:
+    """SURVEY.md §8.D: E*(I + s*F) + (N+1)*I + N*s*F_out  [+ N*s*F_dst read for the self term];
+    s = 4 (fp32) or 2 (bf16)."""
     f_out = f_src + (f_dst if mode == 2 else 0)
-    b = n_edges * (4 + 4 * f_src) + (n_rows + 1) * 4 + n_rows * 4 * f_out
+    b = n_edges * (4 + s * f_src) + (n_rows + 1) * 4 + n_rows * s * f_out
     if mode != 0:
-        b += n_rows * 4 * f_dst
+        b += n_rows * s * f_dst
     return b

@@ -32,7 +32,8 @@ from torch import Tensor
 from . import _lib, ops
 from .data import EdgeType, HeteroGraph, collate
 
-COPY_F32, COPY_I32_ADD, COPY_I64_ADD, FILL_I64, FILL_I32 = 0, 1, 2, 3, 4
+COPY_F32, COPY_I32_ADD, COPY_I64_ADD, FILL_I64, FILL_I32, COPY_B16 = 0, 1, 2, 3, 4, 5
+_COPY_KIND = {4: COPY_F32, 2: COPY_B16}     # feature element size -> copy kind
 DESC_DTYPE = np.dtype([("src", "<u8"), ("dst", "<u8"), ("count", "<i8"), ("add", "<i8"), ("kind", "<i4"),
                        ("reserved", "<i4")])
 assert DESC_DTYPE.itemsize == 40   # sizeof(hgin_copy_desc)
@@ -173,7 +174,8 @@ class GraphStore:
                 if n == 0:
                     continue
                 s_off, b_off = int(self.node_off[t][g]), int(b_node[t][j])
-                descs.append((ptr(self.x[t], s_off * F), ptr(x_out[t], b_off * F), n * F, 0, COPY_F32))
+                descs.append((ptr(self.x[t], s_off * F), ptr(x_out[t], b_off * F), n * F, 0,
+                              _COPY_KIND[self.x[t].element_size()]))
                 descs.append((0, ptr(batch_out[t], b_off), n, j, FILL_I64))
         y_out = torch.empty(int(b_node["path"][-1]), dtype=self.y.dtype, device=dev)
         for j, g in enumerate(ids):

@@ -133,6 +133,41 @@ int hgin_gemm_tn_f32(const float* a, int64_t lda, const float* b1, int64_t ldb1,
                      int64_t ldb2, int64_t M, int64_t N, int64_t K, float* out, int64_t ldo, void* workspace,
                      size_t workspace_bytes, void* stream);
 
+/* ---- cfg5: bf16 storage + bf16 MFMA, fp32 accumulate (BASELINE.json configs[4]) ---------------------
+ * Same operations and operand conventions as the fp32 entry points above; `uint16_t` = a bfloat16 bit
+ * pattern.  Every sum / product is formed in fp32 and each stored bf16 value is rounded once
+ * (round-to-nearest-even, NaN -> 0x7FC0 — torch's float->bfloat16 conversion).  Parameters (eps, bias,
+ * prelu) stay fp32; GEMM weights are bf16 copies of the fp32 masters; weight gradients come out fp32.
+ *   hgin_aggregate_bf16     fp32 sequential edge-order sum of bf16 rows, then (1+eps)*x_dst, one rounding:
+ *                           bit-exact vs CPU scatter_add_ over the fp32-widened inputs + .bfloat16().
+ *   hgin_gin_mlp_fwd_bf16   z, y (and accum) bf16; v_mfma_f32_32x32x16_bf16.
+ *   hgin_linear_fwd_bf16    the readout head: bf16 operands, fp32 output.
+ *   hgin_gemm_nt_bf16       c (bf16) = a @ b^T.
+ *   hgin_gemm_tn_bf16       out (fp32) = a^T [b1 | b2]; workspace: hgin_gemm_tn_workspace_size.
+ *   hgin_prelu_bwd_bf16     g_z bf16; g_prelu / g_bias fp32 sums of the unrounded fp32 g_z.
+ *   hgin_combine_bwd_bf16   g_x_dst bf16; g_eps fp32. */
+int hgin_aggregate_bf16(const int32_t* rowptr, const int32_t* col, int64_t n_rows,
+                        const uint16_t* x_src, int64_t ld_src, int64_t f_src,
+                        const uint16_t* x_dst, int64_t ld_dst, int64_t f_dst,
+                        const float* eps, int combine, uint16_t* out, int64_t ld_out, void* stream);
+int hgin_gin_mlp_fwd_bf16(const uint16_t* a1, int64_t lda1, int64_t k1, const uint16_t* a2, int64_t lda2,
+                          const uint16_t* w, const float* bias, const float* prelu, const uint16_t* accum,
+                          uint16_t* z, uint16_t* y, int64_t M, int64_t N, int64_t K, void* stream);
+int hgin_linear_fwd_bf16(const uint16_t* a1, int64_t lda1, int64_t k1, const uint16_t* a2, int64_t lda2,
+                         const uint16_t* w, const float* bias, float* y, int64_t M, int64_t N, int64_t K,
+                         void* stream);
+int hgin_gemm_nt_bf16(const uint16_t* a, int64_t lda, const uint16_t* b, int64_t ldb, uint16_t* c, int64_t ldc,
+                      int64_t M, int64_t N, int64_t K, void* stream);
+int hgin_gemm_tn_bf16(const uint16_t* a, int64_t lda, const uint16_t* b1, int64_t ldb1, int64_t k1,
+                      const uint16_t* b2, int64_t ldb2, int64_t M, int64_t N, int64_t K, float* out, int64_t ldo,
+                      void* workspace, size_t workspace_bytes, void* stream);
+int hgin_prelu_bwd_bf16(const uint16_t* g_y, int64_t ld_gy, const uint16_t* z, int64_t M, int64_t N,
+                        const float* prelu, uint16_t* g_z, float* g_prelu, float* g_bias, void* workspace,
+                        size_t workspace_bytes, void* stream);
+int hgin_combine_bwd_bf16(const uint16_t* g, int64_t ld_g, const uint16_t* x_dst, int64_t ld_dst,
+                          int64_t n_rows, int64_t f_dst, const float* eps, uint16_t* g_x_dst, int64_t ld_gx,
+                          float* g_eps, void* workspace, size_t workspace_bytes, void* stream);
+
 /* ---- F1: device-side batch collation (replaces PyG's host Collater, dataset.py:239-244) -------------
  * Executes n_desc "segment copy with an integer shift" descriptors in one launch (device array `descs`);
  * max_count = the largest descriptor count (sizes the grid).  Kinds:
@@ -140,12 +175,14 @@ int hgin_gemm_tn_f32(const float* a, int64_t lda, const float* b1, int64_t ldb1,
  *   HGIN_COPY_I32_ADD dst[i] = src[i] + add      (int32)
  *   HGIN_COPY_I64_ADD dst[i] = src[i] + add      (int64)
  *   HGIN_FILL_I64     dst[i] = add               (int64)
- *   HGIN_FILL_I32     dst[i] = (int32)add        (int32) */
+ *   HGIN_FILL_I32     dst[i] = (int32)add        (int32)
+ *   HGIN_COPY_B16     dst[i] = src[i]            (16-bit elements: bf16 features, cfg5) */
 #define HGIN_COPY_F32 0
 #define HGIN_COPY_I32_ADD 1
 #define HGIN_COPY_I64_ADD 2
 #define HGIN_FILL_I64 3
 #define HGIN_FILL_I32 4
+#define HGIN_COPY_B16 5
 typedef struct hgin_copy_desc {
   const void* src;
   void* dst;

@@ -1,0 +1,247 @@
+"""cfg5 (BASELINE.json configs[4]): bf16 storage + bf16 MFMA with fp32 accumulation, on the GPU.
+
+Checkers: the aggregate is bit-exact against the C oracle run on the fp32-widened inputs followed by torch's
+float->bfloat16 rounding (the kernel sums in fp32 and rounds once); GEMMs are checked against float64
+products of the same bf16 operands (fp32 accumulation error bound + one bf16 rounding of the output);
+elementwise backward kernels are bit-exact; the whole model is a mixed-precision tolerance sweep against
+the fp32 oracle (bounds written in the test, measured values in profiles/)."""
+import numpy as np
+import pytest
+import torch
+
+from hgin import HetroGIN, ops
+from oracle import c_oracle as co
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+BF = torch.bfloat16
+
+
+def _bf(t):
+    return t.to(BF)
+
+
+def _rand_graph(E, n_src, n_dst, seed):
+    rng = np.random.default_rng(seed)
+    return np.stack([rng.integers(0, n_src, E), rng.integers(0, n_dst, E)]).astype(np.int64)
+
+
+# ---------------------------------------------------------------------------------------- aggregate
+@pytest.mark.parametrize("F_src,F_dst", [(1, 1), (3, 7), (8, 8), (16, 16), (128, 128), (256, 256), (264, 264),
+                                         (128, 3), (12, 4)])
+@pytest.mark.parametrize("mode", [0, 1, 2])
+def test_aggregate_bf16_bit_exact(F_src, F_dst, mode):
+    if mode == 1 and F_src != F_dst:
+        pytest.skip("add needs equal widths")
+    E, n_src, n_dst = 9000, 700, 500
+    ei = _rand_graph(E, n_src, n_dst, seed=F_src * 5 + mode)
+    ei[1, :60] = 4
+    g = torch.Generator().manual_seed(F_src + F_dst)
+    x = _bf(torch.randn(n_src, F_src, generator=g))
+    xd = _bf(torch.randn(n_dst, F_dst, generator=g))
+    eps = np.float32(0.1875)
+    rowptr, col, _, _ = co.csr_build(ei, 1, n_dst, n_src)
+    ref32 = co.aggregate(rowptr, col, x.float().numpy(), xd.float().numpy() if mode else None, float(eps), mode)
+    ref = torch.from_numpy(ref32).to(BF)
+    csr = ops.build_csr(torch.from_numpy(ei).to(DEV), 1, n_dst, n_src)
+    width = F_src + (F_dst if mode == 2 else 0)
+    out = torch.empty(n_dst, width, dtype=BF, device=DEV)
+    ops.aggregate_into(csr, x.to(DEV), xd.to(DEV) if mode else None,
+                       torch.tensor([eps], device=DEV) if mode else None, mode, out)
+    assert torch.equal(out.cpu().view(torch.int16), ref.view(torch.int16))
+
+
+def test_aggregate_bf16_autograd_matches_fp32_widened():
+    g = torch.Generator().manual_seed(2)
+    n_src, n_dst, E, F = 2000, 900, 30000, 128
+    ei = torch.stack([torch.randint(0, n_src, (E,), generator=g), torch.randint(0, n_dst, (E,), generator=g)])
+    graph = ops.relation_graph(ei.to(DEV), n_src, n_dst)
+    x = _bf(torch.randn(n_src, F, generator=g)).to(DEV).requires_grad_()
+    xd = _bf(torch.randn(n_dst, F, generator=g)).to(DEV).requires_grad_()
+    eps = torch.tensor([0.25], device=DEV, requires_grad=True)
+    out = ops.aggregate(x, xd, eps, graph, ops.COMBINE_CONCAT)
+    assert out.dtype == BF
+    go = _bf(torch.randn(n_dst, 2 * F, generator=g)).to(DEV)
+    out.backward(go)
+    # backward aggregate over the CSC: bit-exact vs the oracle on widened values, one rounding
+    rp, col, _, _ = co.csr_build(ei.numpy(), 0, n_src, n_dst)
+    ref_gx = torch.from_numpy(co.aggregate(rp, col, go[:, :F].float().cpu().numpy(), None, 0.0, 0)).to(BF)
+    assert torch.equal(x.grad.cpu().view(torch.int16), ref_gx.view(torch.int16))
+    assert torch.equal(xd.grad, (1.25 * go[:, F:].float()).to(BF))
+    ref_ge = (go[:, F:].double() * xd.detach().double()).sum()
+    assert abs(float(eps.grad) - float(ref_ge)) <= 1e-4 * float((go[:, F:].double() * xd.double()).abs().sum())
+
+
+# -------------------------------------------------------------------------------------------- GEMMs
+def _gemm_bound(a, b_t, out_is_bf16):
+    """|err| <= fp32-accumulation bound (+ half a bf16 ulp of the result when the output is bf16)."""
+    mag = a.double().abs() @ b_t.double().abs()
+    return 2e-6 * mag + 1e-6, (2.0 ** -8 if out_is_bf16 else 0.0)
+
+
+@pytest.mark.parametrize("M,N,K", [(1, 1, 1), (37, 8, 6), (1000, 128, 256), (513, 130, 129), (300, 256, 512),
+                                   (4096, 128, 128), (65, 3, 1000), (2000, 32, 128)])
+def test_gin_mlp_fwd_bf16(M, N, K):
+    g = torch.Generator(device=DEV).manual_seed(M * 3 + N + K)
+    a = _bf(torch.randn(M, K, device=DEV, generator=g))
+    w = _bf(torch.randn(N, K, device=DEV, generator=g) / K ** 0.5)
+    b = torch.randn(N, device=DEV, generator=g)
+    s = torch.tensor([0.25], device=DEV)
+    acc = _bf(torch.randn(M, N, device=DEV, generator=g))
+    z, y = ops.gin_mlp_fwd(a, w, b, s, acc)
+    assert z.dtype == BF and y.dtype == BF
+    zr = a.double() @ w.double().t() + b.double()
+    abs_b, rel = _gemm_bound(a, w.t(), True)
+    assert ((z.double() - zr).abs() <= abs_b + rel * zr.abs()).all()
+    # the epilogue from the (unrounded) fp32 z: y = bf16(acc + prelu(z)); check against the rounded z within
+    # one bf16 step of the sum
+    yr = acc.double() + torch.where(zr > 0, zr, 0.25 * zr)
+    assert ((y.double() - yr).abs() <= abs_b + 2.0 ** -7 * yr.abs() + 2.0 ** -7 * acc.double().abs()).all()
+
+
+def test_gemm_bf16_identity_asymmetric():
+    K = 64
+    a = _bf(torch.eye(K, device=DEV))
+    b = _bf(torch.arange(K * 40, device=DEV, dtype=torch.float32).reshape(40, K) % 251)   # exact in bf16
+    c = ops.gemm_nt(a, b)
+    assert torch.equal(c, b.t())
+
+
+@pytest.mark.parametrize("M,N,K", [(200, 64, 128), (1, 256, 3), (1031, 100, 77), (5000, 256, 128)])
+def test_gemm_nt_bf16(M, N, K):
+    a = _bf(torch.randn(M, K, device=DEV))
+    b = _bf(torch.randn(N, K, device=DEV))
+    c = ops.gemm_nt(a, b)
+    assert c.dtype == BF
+    ref = a.double() @ b.double().t()
+    abs_b, rel = _gemm_bound(a, b.t(), True)
+    assert ((c.double() - ref).abs() <= abs_b + rel * ref.abs()).all()
+
+
+@pytest.mark.parametrize("M,N,K1,K2", [(1, 1, 1, 0), (1000, 128, 256, 0), (600, 128, 128, 128), (777, 100, 6, 3),
+                                       (50000, 128, 256, 0), (33, 256, 64, 40), (0, 8, 8, 0), (3001, 130, 72, 56)])
+def test_gemm_tn_bf16(M, N, K1, K2):
+    a = _bf(torch.randn(M, N, device=DEV))
+    b1 = _bf(torch.randn(M, K1, device=DEV))
+    b2 = _bf(torch.randn(M, K2, device=DEV)) if K2 else None
+    out = ops.gemm_tn(a, b1, b2)
+    assert out.dtype == torch.float32
+    b = b1 if b2 is None else torch.cat((b1, b2), 1)
+    ref = a.double().t() @ b.double()
+    assert ((out.double() - ref).abs() <= 1e-5 * (a.double().abs().t() @ b.double().abs()) + 1e-6).all()
+    assert torch.equal(out, ops.gemm_tn(a, b1, b2))     # deterministic
+
+
+def test_gemm_tn_bf16_transpose_map():
+    """Integer-valued operands (exact in bf16 and fp32): the in-register 8x8 transpose must be exact."""
+    M, N, K = 256, 128, 128
+    a = _bf((torch.arange(M * N, device=DEV) % 7 - 3).float().reshape(M, N))
+    b = _bf((torch.arange(M * K, device=DEV) % 5 - 2).float().reshape(M, K))
+    out = ops.gemm_tn(a, b)
+    assert torch.equal(out, (a.float().t() @ b.float()))
+
+
+# ------------------------------------------------------------------------------ backward elementwise
+def test_prelu_bwd_bf16():
+    z = _bf(torch.randn(1000, 128, device=DEV))
+    gy_big = _bf(torch.randn(1000, 160, device=DEV))
+    gy = gy_big[:, 16:144]
+    a = torch.tensor([0.3], device=DEV)
+    g_z, g_a, g_b = ops.prelu_bwd(gy, z, a)
+    gz32 = torch.where(z.float() > 0, gy.float(), a * gy.float())
+    assert torch.equal(g_z, gz32.to(BF))
+    assert ((g_b.double() - gz32.double().sum(0)).abs() <= 1e-5 * gz32.double().abs().sum(0) + 1e-6).all()
+    ga_ref = (torch.where(z.float() > 0, torch.zeros_like(gz32), z.float() * gy.float())).double().sum()
+    assert abs(float(g_a) - float(ga_ref)) <= 1e-5 * float((z.double() * gy.double()).abs().sum()) + 1e-6
+
+
+def test_combine_bwd_bf16():
+    g = _bf(torch.randn(900, 136, device=DEV))
+    x = _bf(torch.randn(900, 64, device=DEV))
+    eps = torch.tensor([0.125], device=DEV)
+    gx, ge = ops.combine_bwd(g[:, 72:], x, eps, True)
+    assert torch.equal(gx, (1.125 * g[:, 72:].float()).to(BF))
+    ref = (g[:, 72:].double() * x.double()).sum()
+    assert abs(float(ge) - float(ref)) <= 1e-5 * float((g[:, 72:].double() * x.double()).abs().sum())
+
+
+def test_linear_prelu_bf16_autograd():
+    M, K1, K2 = 3000, 128, 128
+    x1 = _bf(torch.randn(M, K1, device=DEV)).requires_grad_()
+    x2 = _bf(torch.randn(M, K2, device=DEV)).requires_grad_()
+    lin = torch.nn.Linear(K1 + K2, 32).to(DEV)
+    act = torch.nn.PReLU().to(DEV)
+    head = torch.nn.Linear(32, 1).to(DEV)
+    h = ops.linear_prelu(x1, lin.weight, lin.bias, act.weight, x2=x2)
+    out = ops.linear_prelu(h, head.weight, head.bias, None)
+    assert h.dtype == BF and out.dtype == torch.float32
+    out.sum().backward()
+    # float64 reference on the same bf16 operand values (weights rounded like the kernels' operand copies)
+    xr = torch.cat((x1, x2), 1).detach().double().requires_grad_()
+    w1 = lin.weight.detach().to(BF).double().requires_grad_()
+    b1 = lin.bias.detach().double().requires_grad_()
+    a1 = act.weight.detach().double().requires_grad_()
+    z1 = xr @ w1.t() + b1
+    hr = torch.where(z1 > 0, z1, a1 * z1)
+    w2 = head.weight.detach().to(BF).double().requires_grad_()
+    b2 = head.bias.detach().double().requires_grad_()
+    outr = hr.to(BF).double() @ w2.t() + b2
+    assert float((out.double() - outr).norm() / outr.norm()) < 1e-2
+    outr.sum().backward()
+    for got, want in [(lin.weight.grad, w1.grad), (lin.bias.grad, b1.grad), (head.weight.grad, w2.grad),
+                      (head.bias.grad, b2.grad), (torch.cat((x1.grad, x2.grad), 1), xr.grad)]:
+        assert float((got.double() - want).norm()) <= 2e-2 * float(want.norm()) + 1e-6
+
+
+# ------------------------------------------------------------------------- model: tolerance sweep
+def _fixture_bf16_vs_fp32(case):
+    from conftest import fixture_inputs, fixture_model_kwargs, load_fixture
+    from hgin.train import mape
+    fx = load_fixture(case)
+    model = HetroGIN(**fixture_model_kwargs(fx))
+    model.load_state_dict({k[3:]: v for k, v in fx.items() if k.startswith("sd.")})
+    model = model.to(DEV).train()
+    x, ei, batch, y = fixture_inputs(fx, DEV)
+    out = model({t: v.to(BF) for t, v in x.items()}, ei, batch)
+    lv = mape(out, y.reshape(-1, 1))
+    torch.sqrt(lv).backward()
+    loss = lv.detach()
+    ref_out = fx["out"].double()
+    err_out = float((out.detach().cpu().double() - ref_out).norm() / ref_out.norm())
+    errs = {}
+    for name, p in model.named_parameters():
+        key = f"grad.{name}"
+        if key in fx and p.grad is not None and float(fx[key].norm()) > 0:
+            errs[name] = float((p.grad.cpu().double() - fx[key].double()).norm() / fx[key].double().norm())
+    return err_out, errs, float(loss), float(fx["loss_value"])
+
+
+@pytest.mark.parametrize("case", ["cfg1_L2", "wide_L3", "w128_L2"])
+def test_model_bf16_tolerance_sweep(case):
+    """bf16 features/activations vs the fp32 reference fixtures.  Bounds: output rel-L2 <= 3e-2, loss within
+    2 %, median parameter-gradient rel-L2 <= 5e-2 (bf16 has an 8-bit mantissa: 2^-9 = 2e-3 per rounding,
+    compounded over L layers and the readout)."""
+    err_out, errs, loss, ref_loss = _fixture_bf16_vs_fp32(case)
+    print(f"\n[bf16 sweep] {case}: out rel-L2 {err_out:.3e}, loss {loss:.6f} vs {ref_loss:.6f}, grad rel-L2 "
+          f"median {np.median(list(errs.values())):.3e} max {max(errs.values()):.3e}")
+    assert err_out <= 3e-2
+    assert abs(loss - ref_loss) <= 2e-2 * abs(ref_loss)
+    assert np.median(list(errs.values())) <= 5e-2
+
+
+def test_model_bf16_full_cfg2_step_runs():
+    """cfg2-sized bf16 training step (finite loss, every parameter gets a finite gradient)."""
+    from hgin.data import CONFIGS, synthetic_graph
+    from hgin.train import train_step
+    import dataclasses
+    cfg = dataclasses.replace(CONFIGS["cfg2"], feat_dtype="bf16")
+    g = synthetic_graph(cfg, seed=0, device=DEV)
+    assert g.x["path"].dtype == BF
+    torch.manual_seed(1997)
+    model = HetroGIN(**cfg.model_kwargs({"link": cfg.f_link, "path": cfg.f_path, "node": cfg.f_node})).to(DEV)
+    opt = torch.optim.Adam(model.parameters(), lr=1e-3)
+    loss = train_step(model, opt, g)
+    assert np.isfinite(float(loss))
+    for n, p in model.named_parameters():
+        if p.grad is not None:
+            assert torch.isfinite(p.grad).all(), n

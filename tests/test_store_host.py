@@ -28,7 +28,7 @@ def test_copy_kinds_match_header():
     from hgin import store
     for name, val in (("HGIN_COPY_F32", store.COPY_F32), ("HGIN_COPY_I32_ADD", store.COPY_I32_ADD),
                       ("HGIN_COPY_I64_ADD", store.COPY_I64_ADD), ("HGIN_FILL_I64", store.FILL_I64),
-                      ("HGIN_FILL_I32", store.FILL_I32)):
+                      ("HGIN_FILL_I32", store.FILL_I32), ("HGIN_COPY_B16", store.COPY_B16)):
         m = re.search(rf"#define\s+{name}\s+(\d+)", hdr)
         assert m and int(m.group(1)) == val, name
 

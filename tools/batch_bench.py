@@ -75,7 +75,8 @@ def main():
 
     def run(variant):
         torch.manual_seed(1997)
-        model = HetroGIN(**kw).to(dev)
+        # the ctor mutates input_channels (models.py:261-269): a fresh dict per model
+        model = HetroGIN(**{**kw, "input_channels": dict(kw["input_channels"])}).to(dev)
         opt = torch.optim.Adam(lr=1e-3, params=model.parameters())
         fixed = store.collate(order[0]) if variant == "static" else None
 
