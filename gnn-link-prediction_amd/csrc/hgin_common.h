@@ -43,6 +43,17 @@ inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
 inline size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
 
+// XCD-aware workgroup order.  gfx950 hands workgroup L of a launch to XCD L % 8, and each XCD has its own
+// L2, so workgroups that read the same rows should sit on one XCD.  Over a grid padded to a multiple of 8,
+// logical index q = (L % 8) * (total / 8) + L / 8 gives every XCD a contiguous run of logical work items
+// (e.g. all output tiles of one row range).  Callers launch round_up8(n) workgroups and return when q >= n.
+constexpr int kXcds = 8;
+inline int64_t round_up8(int64_t n) { return (n + kXcds - 1) / kXcds * kXcds; }
+__device__ __forceinline__ int64_t xcd_logical(int64_t L, int64_t padded_total) {
+  return (L % kXcds) * (padded_total / kXcds) + L / kXcds;
+}
+bool xcd_remap_enabled();   // HGIN_XCD=0 disables (A/B measurements); default on
+
 // bf16 storage (cfg5): raw uint16_t bit patterns; arithmetic is always fp32.
 // Widening is exact; narrowing is round-to-nearest-even with NaN -> 0x7FC0, bit-identical to
 // torch's float -> bfloat16 conversion (c10::BFloat16), so the CPU oracle can pin every rounding.

@@ -77,11 +77,136 @@ __device__ __forceinline__ void store_tile(float* __restrict__ dst, const float4
     *reinterpret_cast<float4*>(dst + ((tid >> 3) + 32 * i) * kLds + (tid & 7) * 4) = r[i];
 }
 
+// 4 consecutive output columns of one row: fp32 (16-B) or bf16 (8-B) accesses, scalar at the ragged edge.
+template <typename OutT>
+struct Out4;
+template <>
+struct Out4<float> {
+  using raw = float4;   // a prefetched group in its storage form (4 VGPRs)
+  static __device__ __forceinline__ raw ld_raw(const float* p, bool full, int nv) {
+    if (full) return *reinterpret_cast<const float4*>(p);
+    float t[4] = {0.f, 0.f, 0.f, 0.f};
+    for (int i = 0; i < nv; ++i) t[i] = p[i];
+    return make_float4(t[0], t[1], t[2], t[3]);
+  }
+  static __device__ __forceinline__ void unpack(const raw& v, float (&o)[4]) {
+    o[0] = v.x; o[1] = v.y; o[2] = v.z; o[3] = v.w;
+  }
+  static __device__ __forceinline__ void st(float* p, const float (&o)[4], bool full, int nv) {
+    if (full) *reinterpret_cast<float4*>(p) = make_float4(o[0], o[1], o[2], o[3]);
+    else for (int t = 0; t < nv; ++t) p[t] = o[t];
+  }
+  static __device__ __forceinline__ void ld(const float* p, float (&o)[4], bool full, int nv) {
+    if (full) {
+      const float4 v = *reinterpret_cast<const float4*>(p);
+      o[0] = v.x; o[1] = v.y; o[2] = v.z; o[3] = v.w;
+    } else {
+      for (int t = 0; t < nv; ++t) o[t] = p[t];
+    }
+  }
+};
+template <>
+struct Out4<uint16_t> {
+  using raw = uint2;    // 4 packed bf16 (2 VGPRs)
+  static __device__ __forceinline__ raw ld_raw(const uint16_t* p, bool full, int nv) {
+    if (full) return *reinterpret_cast<const uint2*>(p);
+    uint32_t t[4] = {0u, 0u, 0u, 0u};
+    for (int i = 0; i < nv; ++i) t[i] = p[i];
+    return make_uint2(t[0] | (t[1] << 16), t[2] | (t[3] << 16));
+  }
+  static __device__ __forceinline__ void unpack(const raw& v, float (&o)[4]) {
+    o[0] = bf_lo(v.x); o[1] = bf_hi(v.x); o[2] = bf_lo(v.y); o[3] = bf_hi(v.y);
+  }
+  static __device__ __forceinline__ void st(uint16_t* p, const float (&o)[4], bool full, int nv) {
+    if (full) *reinterpret_cast<uint2*>(p) = make_uint2(pack_bf2(o[0], o[1]), pack_bf2(o[2], o[3]));
+    else for (int t = 0; t < nv; ++t) p[t] = (uint16_t)f2bf(o[t]);
+  }
+  static __device__ __forceinline__ void ld(const uint16_t* p, float (&o)[4], bool full, int nv) {
+    if (full) {
+      const uint2 v = *reinterpret_cast<const uint2*>(p);
+      o[0] = bf_lo(v.x); o[1] = bf_hi(v.x); o[2] = bf_lo(v.y); o[3] = bf_hi(v.y);
+    } else {
+      for (int t = 0; t < nv; ++t) o[t] = bf2f(p[t]);
+    }
+  }
+};
+
+// Epilogue shared by the fp32 and bf16 kernels.  Per 32-row half (tm) each wave parks its 32 x WCOLS
+// results in LDS, then writes row-contiguous 4-column groups (bias, PReLU, accum applied on the way out).
+// A lane always owns the same 4 columns, so its bias values are loaded once, and the accum rows it will
+// need are loaded before the LDS round trip: no dependent global load inside the store loop.
+template <int EPI, int TN, typename OutT>
+__device__ __forceinline__ void epilogue(const f32x16 (&acc)[2][TN], float* smem, int wave, int wm, int wn, int lane,
+                                         int li, int lh, int64_t m0, int64_t n0, int64_t M, int64_t N,
+                                         const float* __restrict__ bias, const float* __restrict__ prelu,
+                                         const OutT* __restrict__ accum, OutT* __restrict__ Z, OutT* __restrict__ Y,
+                                         int64_t ldc, bool vec_out) {
+  constexpr int WCOLS = TN * 32;
+  constexpr int kLc = WCOLS + 4;
+  constexpr int kQ = WCOLS / 4;     // 4-column groups per row
+  constexpr int kRS = 64 / kQ;      // rows between a lane's consecutive rows
+  constexpr int kJ = 32 / kRS;      // rows per lane per 32-row half
+  const float a_slope = EPI == 1 ? prelu[0] : 0.0f;
+  float* Cw = smem + wave * 32 * kLc;
+  const int c = (lane % kQ) * 4;
+  const int r0 = lane / kQ;
+  const int64_t col = n0 + wn * WCOLS + c;
+  const int nv = col < N ? (N - col < 4 ? (int)(N - col) : 4) : 0;
+  const bool full = vec_out && nv == 4;
+  float bcol[4] = {0.f, 0.f, 0.f, 0.f};
+  if (EPI >= 1) {
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+      if (t < nv) bcol[t] = bias[col + t];
+  }
+  __syncthreads();   // every wave is done with the A/B tiles
+#pragma unroll
+  for (int tm = 0; tm < 2; ++tm) {
+    typename Out4<OutT>::raw acc_raw[kJ];
+#pragma unroll
+    for (int j = 0; j < kJ; ++j) {
+      acc_raw[j] = {};
+      const int64_t row = m0 + wm * 64 + tm * 32 + r0 + kRS * j;
+      if (EPI == 1 && accum && row < M && nv) acc_raw[j] = Out4<OutT>::ld_raw(accum + row * ldc + col, full, nv);
+    }
+#pragma unroll
+    for (int tn = 0; tn < TN; ++tn)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) Cw[((e & 3) + 8 * (e >> 2) + 4 * lh) * kLc + tn * 32 + li] = acc[tm][tn][e];
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < kJ; ++j) {
+      const int r = r0 + kRS * j;
+      const int64_t row = m0 + wm * 64 + tm * 32 + r;
+      if (row >= M || nv == 0) continue;
+      const float4 v4 = *reinterpret_cast<const float4*>(Cw + r * kLc + c);
+      float o[4] = {v4.x, v4.y, v4.z, v4.w};
+      float zz[4] = {0.f, 0.f, 0.f, 0.f};
+      float acc_in[4];
+      Out4<OutT>::unpack(acc_raw[j], acc_in);
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        if (EPI == 2) {
+          o[t] = __fadd_rn(o[t], bcol[t]);
+        } else if (EPI == 1) {
+          zz[t] = __fadd_rn(o[t], bcol[t]);
+          const float y = zz[t] > 0.0f ? zz[t] : __fmul_rn(a_slope, zz[t]);
+          o[t] = accum ? __fadd_rn(acc_in[t], y) : y;
+        }
+      }
+      Out4<OutT>::st(Y + row * ldc + col, o, full, nv);
+      if (EPI == 1 && Z) Out4<OutT>::st(Z + row * ldc + col, zz, full, nv);
+    }
+    if (tm == 0) __syncthreads();
+  }
+}
+
 template <int EPI, bool kVec, int TN>
 __global__ __launch_bounds__(256, 3) void k_gemm_nt(Src2 A, Src2 B, int64_t M, int64_t N, int64_t K,
                                                     const float* __restrict__ bias, const float* __restrict__ prelu,
                                                     const float* __restrict__ accum, float* __restrict__ Z,
-                                                    float* __restrict__ Y, int64_t ldc, bool vec_out) {
+                                                    float* __restrict__ Y, int64_t ldc, bool vec_out,
+                                                    int64_t n_tiles, bool xcd) {
   constexpr int WN = TN == 2 ? 2 : 1;     // waves along N
   constexpr int WM = 4 / WN;              // waves along M
   constexpr int BM = WM * 64;             // rows per workgroup tile
@@ -97,11 +222,14 @@ __global__ __launch_bounds__(256, 3) void k_gemm_nt(Src2 A, Src2 B, int64_t M, i
   const int wn = wave % WN;
   const int li = lane & 31;
   const int lh = lane >> 5;
-  // N-tiles vary fastest: the workgroups reading the same A rows are dispatched back to back, so the second
-  // N-tile finds those rows in the Infinity Cache instead of streaming A from HBM again (N = 256 layers).
+  // N-tiles vary fastest in the logical order and the logical order is XCD-contiguous: the workgroups
+  // reading the same A rows run on one XCD, so the second N-tile finds those rows in that XCD's L2 instead
+  // of streaming A from HBM again (N = 256 layers).
   const int64_t n_tiles_n = (N + BN - 1) / BN;
-  const int64_t m0 = ((int64_t)blockIdx.x / n_tiles_n) * BM;
-  const int64_t n0 = ((int64_t)blockIdx.x % n_tiles_n) * BN;
+  const int64_t q = xcd ? xcd_logical(blockIdx.x, gridDim.x) : (int64_t)blockIdx.x;
+  if (q >= n_tiles) return;
+  const int64_t m0 = (q / n_tiles_n) * BM;
+  const int64_t n0 = (q % n_tiles_n) * BN;
 
   f32x16 acc[2][TN];
 #pragma unroll
@@ -150,64 +278,8 @@ __global__ __launch_bounds__(256, 3) void k_gemm_nt(Src2 A, Src2 B, int64_t M, i
     }
   }
 
-  // Epilogue: per 32-row half (tm) each wave parks 32 x WCOLS results in LDS, then writes row-contiguous
-  // float4s (bias, PReLU, accum applied on the way out).
-  constexpr int kLc = WCOLS + 4;
-  constexpr int kQ = WCOLS / 4;            // float4 per row
-  const float a_slope = EPI == 1 ? prelu[0] : 0.0f;
-  float* Cw = smem + wave * 32 * kLc;
-  __syncthreads();   // every wave is done with the A/B tiles
-#pragma unroll
-  for (int tm = 0; tm < 2; ++tm) {
-#pragma unroll
-    for (int tn = 0; tn < TN; ++tn)
-#pragma unroll
-      for (int e = 0; e < 16; ++e) Cw[((e & 3) + 8 * (e >> 2) + 4 * lh) * kLc + tn * 32 + li] = acc[tm][tn][e];
-    __syncthreads();
-#pragma unroll 2
-    for (int j = 0; j < (32 * kQ) / 64; ++j) {
-      const int q = lane + 64 * j;
-      const int r = q / kQ;
-      const int c = (q % kQ) * 4;
-      const int64_t row = m0 + wm * 64 + tm * 32 + r;
-      const int64_t col = n0 + wn * WCOLS + c;
-      if (row >= M || col >= N) continue;
-      const float4 v4 = *reinterpret_cast<const float4*>(Cw + r * kLc + c);
-      float o[4] = {v4.x, v4.y, v4.z, v4.w};
-      float zz[4];
-      const bool full = vec_out && col + 3 < N;
-      float acc_in[4] = {0.f, 0.f, 0.f, 0.f};
-      if (EPI == 1 && accum) {
-        if (full) {
-          const float4 a4 = *reinterpret_cast<const float4*>(accum + row * ldc + col);
-          acc_in[0] = a4.x; acc_in[1] = a4.y; acc_in[2] = a4.z; acc_in[3] = a4.w;
-        } else {
-          for (int t = 0; t < 4 && col + t < N; ++t) acc_in[t] = accum[row * ldc + col + t];
-        }
-      }
-#pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        const float bcol = (EPI >= 1 && col + t < N) ? bias[col + t] : 0.0f;
-        if (EPI == 2) {
-          o[t] = __fadd_rn(o[t], bcol);
-        } else if (EPI == 1) {
-          zz[t] = __fadd_rn(o[t], bcol);
-          const float y = zz[t] > 0.0f ? zz[t] : __fmul_rn(a_slope, zz[t]);
-          o[t] = accum ? __fadd_rn(acc_in[t], y) : y;
-        }
-      }
-      if (full) {
-        *reinterpret_cast<float4*>(Y + row * ldc + col) = make_float4(o[0], o[1], o[2], o[3]);
-        if (EPI == 1 && Z) *reinterpret_cast<float4*>(Z + row * ldc + col) = make_float4(zz[0], zz[1], zz[2], zz[3]);
-      } else {
-        for (int t = 0; t < 4 && col + t < N; ++t) {
-          Y[row * ldc + col + t] = o[t];
-          if (EPI == 1 && Z) Z[row * ldc + col + t] = zz[t];
-        }
-      }
-    }
-    if (tm == 0) __syncthreads();
-  }
+  epilogue<EPI, TN, float>(acc, smem, wave, wm, wn, lane, li, lh, m0, n0, M, N, bias, prelu, accum, Z, Y, ldc,
+                           vec_out);
 }
 
 template <int EPI, int TN>
@@ -216,11 +288,14 @@ void launch_nt_tn(bool vec, const Src2& a, const Src2& b, int64_t M, int64_t N, 
                   hipStream_t s) {
   constexpr int BM = (TN == 2 ? 2 : 4) * 64;
   constexpr int BN = (TN == 2 ? 2 : 1) * TN * 32;
-  dim3 grid((unsigned)(ceil_div(N, BN) * ceil_div(M, BM)));
+  const int64_t tiles = ceil_div(N, BN) * ceil_div(M, BM);
+  const bool xcd = xcd_remap_enabled();
+  dim3 grid((unsigned)(xcd ? round_up8(tiles) : tiles));
   if (vec)
-    k_gemm_nt<EPI, true, TN><<<grid, 256, 0, s>>>(a, b, M, N, K, bias, prelu, accum, z, y, ldc, vec_out);
+    k_gemm_nt<EPI, true, TN><<<grid, 256, 0, s>>>(a, b, M, N, K, bias, prelu, accum, z, y, ldc, vec_out, tiles, xcd);
   else
-    k_gemm_nt<EPI, false, TN><<<grid, 256, 0, s>>>(a, b, M, N, K, bias, prelu, accum, z, y, ldc, vec_out);
+    k_gemm_nt<EPI, false, TN><<<grid, 256, 0, s>>>(a, b, M, N, K, bias, prelu, accum, z, y, ldc, vec_out, tiles,
+                                                   xcd);
 }
 
 template <int EPI>
@@ -298,46 +373,13 @@ __device__ __forceinline__ void store_tile_h(uint16_t* __restrict__ dst, const u
     *reinterpret_cast<uint4*>(dst + ((tid >> 3) + 32 * i) * kLdsH + (tid & 7) * 8) = r[i];
 }
 
-// 4 consecutive output columns of one row: fp32 (16-B) or bf16 (8-B) stores, scalar at the ragged edge.
-template <typename OutT>
-struct Out4;
-template <>
-struct Out4<float> {
-  static __device__ __forceinline__ void st(float* p, const float (&o)[4], bool full, int nv) {
-    if (full) *reinterpret_cast<float4*>(p) = make_float4(o[0], o[1], o[2], o[3]);
-    else for (int t = 0; t < nv; ++t) p[t] = o[t];
-  }
-  static __device__ __forceinline__ void ld(const float* p, float (&o)[4], bool full, int nv) {
-    if (full) {
-      const float4 v = *reinterpret_cast<const float4*>(p);
-      o[0] = v.x; o[1] = v.y; o[2] = v.z; o[3] = v.w;
-    } else {
-      for (int t = 0; t < nv; ++t) o[t] = p[t];
-    }
-  }
-};
-template <>
-struct Out4<uint16_t> {
-  static __device__ __forceinline__ void st(uint16_t* p, const float (&o)[4], bool full, int nv) {
-    if (full) *reinterpret_cast<uint2*>(p) = make_uint2(pack_bf2(o[0], o[1]), pack_bf2(o[2], o[3]));
-    else for (int t = 0; t < nv; ++t) p[t] = (uint16_t)f2bf(o[t]);
-  }
-  static __device__ __forceinline__ void ld(const uint16_t* p, float (&o)[4], bool full, int nv) {
-    if (full) {
-      const uint2 v = *reinterpret_cast<const uint2*>(p);
-      o[0] = bf_lo(v.x); o[1] = bf_hi(v.x); o[2] = bf_lo(v.y); o[3] = bf_hi(v.y);
-    } else {
-      for (int t = 0; t < nv; ++t) o[t] = bf2f(p[t]);
-    }
-  }
-};
-
 template <int EPI, bool kVec, int TN, typename OutT>
 __global__ __launch_bounds__(256, 3) void k_gemm_nt_bf16(Src2h A, Src2h B, int64_t M, int64_t N, int64_t K,
                                                          const float* __restrict__ bias,
                                                          const float* __restrict__ prelu,
                                                          const OutT* __restrict__ accum, OutT* __restrict__ Z,
-                                                         OutT* __restrict__ Y, int64_t ldc, bool vec_out) {
+                                                         OutT* __restrict__ Y, int64_t ldc, bool vec_out,
+                                                         int64_t n_tiles, bool xcd) {
   constexpr int WN = TN == 2 ? 2 : 1;
   constexpr int WM = 4 / WN;
   constexpr int BM = WM * 64;
@@ -356,8 +398,10 @@ __global__ __launch_bounds__(256, 3) void k_gemm_nt_bf16(Src2h A, Src2h B, int64
   const int li = lane & 31;
   const int lh = lane >> 5;
   const int64_t n_tiles_n = (N + BN - 1) / BN;
-  const int64_t m0 = ((int64_t)blockIdx.x / n_tiles_n) * BM;
-  const int64_t n0 = ((int64_t)blockIdx.x % n_tiles_n) * BN;
+  const int64_t q = xcd ? xcd_logical(blockIdx.x, gridDim.x) : (int64_t)blockIdx.x;
+  if (q >= n_tiles) return;
+  const int64_t m0 = (q / n_tiles_n) * BM;
+  const int64_t n0 = (q % n_tiles_n) * BN;
 
   f32x16 acc[2][TN];
 #pragma unroll
@@ -402,49 +446,8 @@ __global__ __launch_bounds__(256, 3) void k_gemm_nt_bf16(Src2h A, Src2h B, int64
     }
   }
 
-  constexpr int kLc = WCOLS + 4;
-  constexpr int kQ = WCOLS / 4;
-  const float a_slope = EPI == 1 ? prelu[0] : 0.0f;
-  float* Cw = smem + wave * 32 * kLc;
-  __syncthreads();
-#pragma unroll
-  for (int tm = 0; tm < 2; ++tm) {
-#pragma unroll
-    for (int tn = 0; tn < TN; ++tn)
-#pragma unroll
-      for (int e = 0; e < 16; ++e) Cw[((e & 3) + 8 * (e >> 2) + 4 * lh) * kLc + tn * 32 + li] = acc[tm][tn][e];
-    __syncthreads();
-#pragma unroll 2
-    for (int j = 0; j < (32 * kQ) / 64; ++j) {
-      const int q = lane + 64 * j;
-      const int r = q / kQ;
-      const int c = (q % kQ) * 4;
-      const int64_t row = m0 + wm * 64 + tm * 32 + r;
-      const int64_t col = n0 + wn * WCOLS + c;
-      if (row >= M || col >= N) continue;
-      const float4 v4 = *reinterpret_cast<const float4*>(Cw + r * kLc + c);
-      float o[4] = {v4.x, v4.y, v4.z, v4.w};
-      float zz[4] = {0.f, 0.f, 0.f, 0.f};
-      const bool full = vec_out && col + 3 < N;
-      const int nv = N - col < 4 ? (int)(N - col) : 4;
-      float acc_in[4] = {0.f, 0.f, 0.f, 0.f};
-      if (EPI == 1 && accum) Out4<OutT>::ld(accum + row * ldc + col, acc_in, full, nv);
-#pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        const float bcol = (EPI >= 1 && t < nv) ? bias[col + t] : 0.0f;
-        if (EPI == 2) {
-          o[t] = __fadd_rn(o[t], bcol);
-        } else if (EPI == 1) {
-          zz[t] = __fadd_rn(o[t], bcol);
-          const float y = zz[t] > 0.0f ? zz[t] : __fmul_rn(a_slope, zz[t]);
-          o[t] = accum ? __fadd_rn(acc_in[t], y) : y;
-        }
-      }
-      Out4<OutT>::st(Y + row * ldc + col, o, full, nv);
-      if (EPI == 1 && Z) Out4<OutT>::st(Z + row * ldc + col, zz, full, nv);
-    }
-    if (tm == 0) __syncthreads();
-  }
+  epilogue<EPI, TN, OutT>(acc, smem, wave, wm, wn, lane, li, lh, m0, n0, M, N, bias, prelu, accum, Z, Y, ldc,
+                          vec_out);
 }
 
 template <int EPI, typename OutT>
@@ -459,13 +462,15 @@ int launch_nt_bf16(const Src2h& a, const Src2h& b, int64_t M, int64_t N, int64_t
   {                                                                                                          \
     constexpr int BM = (TNV == 2 ? 2 : 4) * 64;                                                              \
     constexpr int BN = (TNV == 2 ? 2 : 1) * TNV * 32;                                                        \
-    dim3 grid((unsigned)(ceil_div(N, BN) * ceil_div(M, BM)));                                                \
+    const int64_t tiles = ceil_div(N, BN) * ceil_div(M, BM);                                                 \
+    const bool xcd = xcd_remap_enabled();                                                                    \
+    dim3 grid((unsigned)(xcd ? round_up8(tiles) : tiles));                                                   \
     if (vec)                                                                                                 \
       k_gemm_nt_bf16<EPI, true, TNV, OutT><<<grid, 256, 0, s>>>(a, b, M, N, K, bias, prelu, accum, z, y, ldc, \
-                                                                vec_out);                                    \
+                                                                vec_out, tiles, xcd);                        \
     else                                                                                                     \
       k_gemm_nt_bf16<EPI, false, TNV, OutT><<<grid, 256, 0, s>>>(a, b, M, N, K, bias, prelu, accum, z, y,    \
-                                                                 ldc, vec_out);                              \
+                                                                 ldc, vec_out, tiles, xcd);                  \
   }
   if (N <= 32)
     HGIN_NT_BF16(1)

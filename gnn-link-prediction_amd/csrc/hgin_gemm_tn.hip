@@ -25,12 +25,35 @@ using f32x16 = __attribute__((ext_vector_type(16))) float;
 constexpr int kTnBM = 32;       // rows of M per stage
 constexpr int kTnLd = 128 + 4;
 
+// 1-D grid over (output tile, split) pairs, tiles of one split consecutive in the logical order, which is
+// XCD-contiguous (hgin_common.h): the workgroups reading the same rows of A / B share one XCD's L2.
+struct TnGrid {
+  int64_t tiles_n;   // 128-wide tiles along N
+  int64_t tiles;     // tiles_n * tiles along K
+  int64_t n_work;    // tiles * splits
+  int xcd;
+};
+struct TnWork {
+  int64_t n0, k0, split;
+  bool valid;
+};
+__device__ __forceinline__ TnWork tn_work(const TnGrid& g) {
+  const int64_t q = g.xcd ? xcd_logical(blockIdx.x, gridDim.x) : (int64_t)blockIdx.x;
+  TnWork w;
+  w.valid = q < g.n_work;
+  const int64_t t = q % g.tiles;
+  w.split = q / g.tiles;
+  w.n0 = (t % g.tiles_n) * 128;
+  w.k0 = (t / g.tiles_n) * 128;
+  return w;
+}
+
 template <bool kPF, int kOcc>
 __global__ __launch_bounds__(256, kOcc) void k_gemm_tn_partial(const float* __restrict__ A, int64_t lda,
                                                             const float* __restrict__ B1, int64_t ldb1,
                                                             const float* __restrict__ B2, int64_t ldb2, int64_t K1,
                                                             int64_t M, int64_t N, int64_t K, int64_t rows_per_split,
-                                                            bool vec, float* __restrict__ slab) {
+                                                            bool vec, float* __restrict__ slab, TnGrid grid) {
   __shared__ __attribute__((aligned(16))) float smem[2 * kTnBM * kTnLd];
   float* As = smem;
   float* Bs = smem + kTnBM * kTnLd;
@@ -39,9 +62,11 @@ __global__ __launch_bounds__(256, kOcc) void k_gemm_tn_partial(const float* __re
   const int wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
   const int li = lane & 31, lh = lane >> 5;
-  const int64_t n0 = (int64_t)blockIdx.x * 128;
-  const int64_t k0 = (int64_t)blockIdx.y * 128;
-  const int64_t mb = (int64_t)blockIdx.z * rows_per_split;
+  const TnWork work = tn_work(grid);
+  if (!work.valid) return;
+  const int64_t n0 = work.n0;
+  const int64_t k0 = work.k0;
+  const int64_t mb = work.split * rows_per_split;
   const int64_t me = mb + rows_per_split < M ? mb + rows_per_split : M;
 
   f32x16 acc[2][2];
@@ -125,7 +150,7 @@ __global__ __launch_bounds__(256, kOcc) void k_gemm_tn_partial(const float* __re
       __syncthreads();
     }
   }
-  float* out = slab + (int64_t)blockIdx.z * N * K;
+  float* out = slab + work.split * N * K;
 #pragma unroll
   for (int tm = 0; tm < 2; ++tm)
 #pragma unroll
@@ -229,7 +254,8 @@ __global__ __launch_bounds__(256, 2) void k_gemm_tn_bf16_partial(const uint16_t*
                                                                  const uint16_t* __restrict__ B1, int64_t ldb1,
                                                                  const uint16_t* __restrict__ B2, int64_t ldb2,
                                                                  int64_t K1, int64_t M, int64_t N, int64_t K,
-                                                                 int64_t rows_per_split, float* __restrict__ slab) {
+                                                                 int64_t rows_per_split, float* __restrict__ slab,
+                                                                 TnGrid grid) {
   __shared__ __attribute__((aligned(16))) uint16_t smem[2 * 128 * kTnLdH];
   uint16_t* At = smem;
   uint16_t* Bt = smem + 128 * kTnLdH;
@@ -238,9 +264,11 @@ __global__ __launch_bounds__(256, 2) void k_gemm_tn_bf16_partial(const uint16_t*
   const int wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
   const int li = lane & 31, lh = lane >> 5;
-  const int64_t n0 = (int64_t)blockIdx.x * 128;
-  const int64_t k0 = (int64_t)blockIdx.y * 128;
-  const int64_t mb = (int64_t)blockIdx.z * rows_per_split;
+  const TnWork work = tn_work(grid);
+  if (!work.valid) return;
+  const int64_t n0 = work.n0;
+  const int64_t k0 = work.k0;
+  const int64_t mb = work.split * rows_per_split;
   const int64_t me = mb + rows_per_split < M ? mb + rows_per_split : M;
   const bool isB = tid >= 128;
   const int cq = tid & 15;          // 8-column chunk of the 128-wide tile
@@ -332,7 +360,7 @@ __global__ __launch_bounds__(256, 2) void k_gemm_tn_bf16_partial(const uint16_t*
       __syncthreads();
     }
   }
-  float* out = slab + (int64_t)blockIdx.z * N * K;
+  float* out = slab + work.split * N * K;
 #pragma unroll
   for (int tm = 0; tm < 2; ++tm)
 #pragma unroll
@@ -349,14 +377,26 @@ __global__ __launch_bounds__(256, 2) void k_gemm_tn_bf16_partial(const uint16_t*
 
 bool tn_is_small(int64_t N, int64_t K) { return N < 16 || K < 16; }
 
-int64_t tn_splits(int64_t M, int64_t N, int64_t K, int64_t stage_rows = kTnBM) {
+// Workgroups a split-M launch aims for (HGIN_TN_WGS, <= 1024 = the workspace sizing target).  768 = one
+// resident round at 3 workgroups per CU: measured (profiles/r01_gemm_variants_*.txt) 1.35x faster than 1024
+// (1.33 rounds, the last one a third full) for the bf16 kernel, 4-6 % for fp32.
+int64_t tn_target_wgs() {
+  static const int64_t t = [] {
+    const char* v = getenv("HGIN_TN_WGS");
+    const int64_t x = v ? atoll(v) : 768;
+    return x >= 64 && x <= 1024 ? x : (int64_t)1024;
+  }();
+  return t;
+}
+
+int64_t tn_splits(int64_t M, int64_t N, int64_t K, int64_t stage_rows = kTnBM, int64_t target = 1024) {
   int64_t S;
   if (tn_is_small(N, K)) {
     S = ceil_div(M, 2048);                                 // 2048 rows per workgroup
     if (S > 1024) S = 1024;
   } else {
     const int64_t tiles = ceil_div(N, 128) * ceil_div(K, 128);
-    S = ceil_div(1024, tiles);                             // ~4 workgroups per CU
+    S = ceil_div(target, tiles);                           // ~3-4 workgroups per CU
     const int64_t max_s = ceil_div(M, 8 * stage_rows);     // keep >= 8 stages per split
     if (S > max_s) S = max_s;
   }
@@ -401,7 +441,7 @@ extern "C" int hgin_gemm_tn_f32(const float* a, int64_t lda, const float* b1, in
                  "hgin_gemm_tn_f32: bad operand");
   const bool vec = aligned16(a) && lda % 4 == 0 && (k1 == 0 || (aligned16(b1) && ldb1 % 4 == 0)) &&
                    (k1 == K || (aligned16(b2) && ldb2 % 4 == 0)) && k1 % 4 == 0;
-  const int64_t S = tn_splits(M, N, K);
+  const int64_t S = tn_splits(M, N, K, kTnBM, tn_target_wgs());
   const int64_t rows = ceil_div(ceil_div(M, S), kTnBM) * kTnBM;
   const int64_t S_eff = ceil_div(M, rows);
   const int64_t NK = N * K;
@@ -410,7 +450,9 @@ extern "C" int hgin_gemm_tn_f32(const float* a, int64_t lda, const float* b1, in
   if (tn_is_small(N, K)) {
     k_tn_small<float><<<(unsigned)S_eff, 256, 0, s>>>(a, lda, b1, ldb1, b2, ldb2, k1, M, (int)N, (int)K, rows, slab);
   } else {
-    dim3 grid((unsigned)ceil_div(N, 128), (unsigned)ceil_div(K, 128), (unsigned)S_eff);
+    const int64_t tiles_n = ceil_div(N, 128);
+    const TnGrid tg{tiles_n, tiles_n * ceil_div(K, 128), tiles_n * ceil_div(K, 128) * S_eff, xcd_remap_enabled()};
+    dim3 grid((unsigned)(tg.xcd ? round_up8(tg.n_work) : tg.n_work));
     static const int variant = [] {
       const char* v = getenv("HGIN_TN_VARIANT");
       return v ? atoi(v) : 0;
@@ -418,11 +460,11 @@ extern "C" int hgin_gemm_tn_f32(const float* a, int64_t lda, const float* b1, in
     // Measured (profiles/r01_tn_variants.txt): register prefetch at 3 waves/SIMD is 12 % faster than the
     // unpipelined loop and 3-5 % faster than prefetch at 2 waves.
     if (variant == 1)
-      k_gemm_tn_partial<false, 2><<<grid, 256, 0, s>>>(a, lda, b1, ldb1, b2, ldb2, k1, M, N, K, rows, vec, slab);
+      k_gemm_tn_partial<false, 2><<<grid, 256, 0, s>>>(a, lda, b1, ldb1, b2, ldb2, k1, M, N, K, rows, vec, slab, tg);
     else if (variant == 2)
-      k_gemm_tn_partial<true, 2><<<grid, 256, 0, s>>>(a, lda, b1, ldb1, b2, ldb2, k1, M, N, K, rows, vec, slab);
+      k_gemm_tn_partial<true, 2><<<grid, 256, 0, s>>>(a, lda, b1, ldb1, b2, ldb2, k1, M, N, K, rows, vec, slab, tg);
     else
-      k_gemm_tn_partial<true, 3><<<grid, 256, 0, s>>>(a, lda, b1, ldb1, b2, ldb2, k1, M, N, K, rows, vec, slab);
+      k_gemm_tn_partial<true, 3><<<grid, 256, 0, s>>>(a, lda, b1, ldb1, b2, ldb2, k1, M, N, K, rows, vec, slab, tg);
   }
   const int64_t G = ceil_div(S_eff, kSlabGroup);
   dim3 g1((unsigned)ceil_div(ceil_div(NK, 4), 256), (unsigned)G);
@@ -458,7 +500,7 @@ extern "C" int hgin_gemm_tn_bf16(const uint16_t* a, int64_t lda, const uint16_t*
                    (k1 == K || (aligned16(b2) && ldb2 % 8 == 0)) && k1 % 8 == 0;
   const bool small = tn_is_small(N, K);
   const int64_t stage = small ? kTnBM : kTnBMh;
-  const int64_t S = tn_splits(M, N, K, stage);     // <= the workspace's split count (stage >= kTnBM)
+  const int64_t S = tn_splits(M, N, K, stage, tn_target_wgs());   // <= the workspace's split count
   const int64_t rows = ceil_div(ceil_div(M, S), stage) * stage;
   const int64_t S_eff = ceil_div(M, rows);
   const int64_t NK = N * K;
@@ -469,11 +511,13 @@ extern "C" int hgin_gemm_tn_bf16(const uint16_t* a, int64_t lda, const uint16_t*
     k_tn_small<uint16_t><<<(unsigned)S_eff, 256, 0, s>>>(a, lda, b1, ldb1, b2, ldb2, k1, M, (int)N, (int)K, rows,
                                                           slab);
   } else {
-    dim3 grid((unsigned)ceil_div(N, 128), (unsigned)ceil_div(K, 128), (unsigned)S_eff);
+    const int64_t tiles_n = ceil_div(N, 128);
+    const TnGrid tg{tiles_n, tiles_n * ceil_div(K, 128), tiles_n * ceil_div(K, 128) * S_eff, xcd_remap_enabled()};
+    dim3 grid((unsigned)(tg.xcd ? round_up8(tg.n_work) : tg.n_work));
     if (vec)
-      k_gemm_tn_bf16_partial<true><<<grid, 256, 0, s>>>(a, lda, b1, ldb1, b2, ldb2, k1, M, N, K, rows, slab);
+      k_gemm_tn_bf16_partial<true><<<grid, 256, 0, s>>>(a, lda, b1, ldb1, b2, ldb2, k1, M, N, K, rows, slab, tg);
     else
-      k_gemm_tn_bf16_partial<false><<<grid, 256, 0, s>>>(a, lda, b1, ldb1, b2, ldb2, k1, M, N, K, rows, slab);
+      k_gemm_tn_bf16_partial<false><<<grid, 256, 0, s>>>(a, lda, b1, ldb1, b2, ldb2, k1, M, N, K, rows, slab, tg);
   }
   const int64_t G = ceil_div(S_eff, kSlabGroup);
   dim3 g1((unsigned)ceil_div(ceil_div(NK, 4), 256), (unsigned)G);

@@ -12,7 +12,26 @@
 namespace hgin {
 namespace {
 
-constexpr int kRowsPerBlock = 256;
+constexpr int kMinRowsPerBlock = 64;   // workspace sizing: the most blocks any variant launches
+
+// Rows per block / rows in flight per thread (HGIN_ROWS_RPB, HGIN_ROWS_U; tools/rows_bench.py,
+// profiles/r01_rows_variants.txt): 256-row blocks; 4 rows in flight for fp32 rows (2-4 % faster), 1 for bf16
+// (4 in flight was 20-40 % slower there).  u = 0: choose by element type.
+struct RowsCfg {
+  int rpb = 256;
+  int u = 0;
+};
+const RowsCfg& rows_cfg() {
+  static const RowsCfg c = [] {
+    RowsCfg r;
+    if (const char* v = getenv("HGIN_ROWS_RPB")) r.rpb = atoi(v);
+    if (const char* v = getenv("HGIN_ROWS_U")) r.u = atoi(v);
+    if (r.rpb != 64 && r.rpb != 128 && r.rpb != 256) r.rpb = 256;
+    if (r.u != 0 && r.u != 1 && r.u != 4) r.u = 0;
+    return r;
+  }();
+  return c;
+}
 
 __device__ __forceinline__ float block_sum_fixed(float v, float* red) {
   // fixed-order tree over 256 threads (same pairing every launch)
@@ -66,11 +85,11 @@ struct RowVec<4, uint16_t> {
 //         (the column sums and the slope sum use the fp32 g_z before any bf16 rounding of the output)
 // MODE 1: combine backward.  in0 = g (self-term columns), in1 = x_dst; out = s*g (optional);
 //         part_s = sum(g * x_dst); no column sums.
-template <int MODE, int VEC, typename T>
+template <int MODE, int VEC, typename T, int kU>
 __global__ __launch_bounds__(256) void k_rows_bwd(const T* __restrict__ in0, int64_t ld0, const T* __restrict__ in1,
                                                   int64_t ld1, int64_t M, int N, const float* __restrict__ scalar,
                                                   T* __restrict__ out, int64_t ldo, float* __restrict__ part_col,
-                                                  float* __restrict__ part_s) {
+                                                  float* __restrict__ part_s, int rows_per_block) {
   __shared__ float red[256 * VEC];
   const int t = threadIdx.x;
   const int NU = N / VEC;                 // column units
@@ -79,8 +98,8 @@ __global__ __launch_bounds__(256) void k_rows_bwd(const T* __restrict__ in0, int
   const bool active = t < CW * RL;
   const int u0 = t % CW;
   const int rl = t / CW;
-  const int64_t r0 = (int64_t)blockIdx.x * kRowsPerBlock;
-  const int64_t r1 = r0 + kRowsPerBlock < M ? r0 + kRowsPerBlock : M;
+  const int64_t r0 = (int64_t)blockIdx.x * rows_per_block;
+  const int64_t r1 = r0 + rows_per_block < M ? r0 + rows_per_block : M;
   float sc = 0.0f;
   if (MODE == 0) sc = scalar[0];
   else sc = __fadd_rn(1.0f, scalar[0]);
@@ -92,10 +111,9 @@ __global__ __launch_bounds__(256) void k_rows_bwd(const T* __restrict__ in0, int
 #pragma unroll
     for (int q = 0; q < VEC; ++q) csum[q] = 0.0f;
     if (active && c < N) {
-      for (int64_t r = r0 + rl; r < r1; r += RL) {
-        float g[VEC], x[VEC], o[VEC];
-        RowVec<VEC, T>::load(in0 + r * ld0 + c, g);
-        RowVec<VEC, T>::load(in1 + r * ld1 + c, x);
+      // one row: fixed per-thread order (rows r0 + rl, r0 + rl + RL, ...), identical for any unrolling
+      auto row = [&](int64_t r, const float (&g)[VEC], const float (&x)[VEC]) {
+        float o[VEC];
 #pragma unroll
         for (int q = 0; q < VEC; ++q) {
           if (MODE == 0) {
@@ -109,6 +127,23 @@ __global__ __launch_bounds__(256) void k_rows_bwd(const T* __restrict__ in0, int
           }
         }
         if (MODE == 0 || out) RowVec<VEC, T>::store(out + r * ldo + c, o);
+      };
+      int64_t r = r0 + rl;     // kU rows' loads in flight together
+      for (; r + (kU - 1) * RL < r1; r += kU * RL) {
+        float g[kU][VEC], x[kU][VEC];
+#pragma unroll
+        for (int u = 0; u < kU; ++u) {
+          RowVec<VEC, T>::load(in0 + (r + u * RL) * ld0 + c, g[u]);
+          RowVec<VEC, T>::load(in1 + (r + u * RL) * ld1 + c, x[u]);
+        }
+#pragma unroll
+        for (int u = 0; u < kU; ++u) row(r + u * RL, g[u], x[u]);
+      }
+      for (; r < r1; r += RL) {
+        float g[VEC], x[VEC];
+        RowVec<VEC, T>::load(in0 + r * ld0 + c, g);
+        RowVec<VEC, T>::load(in1 + r * ld1 + c, x);
+        row(r, g, x);
       }
     }
     if (MODE == 0) {
@@ -131,12 +166,16 @@ __global__ __launch_bounds__(256) void k_rows_bwd(const T* __restrict__ in0, int
 }
 
 template <int MODE, typename T>
-void launch_rows_bwd(bool vec, unsigned nblk, hipStream_t s, const T* in0, int64_t ld0, const T* in1, int64_t ld1,
-                     int64_t M, int N, const float* scalar, T* out, int64_t ldo, float* part_col, float* part_s) {
-  if (vec)
-    k_rows_bwd<MODE, 4, T><<<nblk, 256, 0, s>>>(in0, ld0, in1, ld1, M, N, scalar, out, ldo, part_col, part_s);
+void launch_rows_bwd(bool vec, unsigned nblk, int rpb, hipStream_t s, const T* in0, int64_t ld0, const T* in1,
+                     int64_t ld1, int64_t M, int N, const float* scalar, T* out, int64_t ldo, float* part_col,
+                     float* part_s) {
+  const bool u4 = rows_cfg().u == 4 || (rows_cfg().u == 0 && sizeof(T) == 4);
+  if (vec && u4)
+    k_rows_bwd<MODE, 4, T, 4><<<nblk, 256, 0, s>>>(in0, ld0, in1, ld1, M, N, scalar, out, ldo, part_col, part_s, rpb);
+  else if (vec)
+    k_rows_bwd<MODE, 4, T, 1><<<nblk, 256, 0, s>>>(in0, ld0, in1, ld1, M, N, scalar, out, ldo, part_col, part_s, rpb);
   else
-    k_rows_bwd<MODE, 1, T><<<nblk, 256, 0, s>>>(in0, ld0, in1, ld1, M, N, scalar, out, ldo, part_col, part_s);
+    k_rows_bwd<MODE, 1, T, 1><<<nblk, 256, 0, s>>>(in0, ld0, in1, ld1, M, N, scalar, out, ldo, part_col, part_s, rpb);
 }
 
 template <typename T>
@@ -168,7 +207,7 @@ __global__ __launch_bounds__(256) void k_final_scalar(const float* __restrict__ 
 }
 
 size_t prelu_ws_bytes(int64_t M, int64_t N) {
-  const int64_t nblk = ceil_div(M > 0 ? M : 1, kRowsPerBlock);
+  const int64_t nblk = ceil_div(M > 0 ? M : 1, kMinRowsPerBlock);
   return align_up(sizeof(float) * (size_t)(nblk * N), 256) + align_up(sizeof(float) * (size_t)nblk, 256);
 }
 
@@ -189,11 +228,12 @@ int prelu_bwd(const char* what, const T* g_y, int64_t ld_gy, const T* z, int64_t
     return rc;
   }
   HGIN_ARG_CHECK(g_y && z && g_z && ld_gy >= N, "%s: NULL operand or ld_gy < N", what);
-  const int64_t nblk = ceil_div(M, kRowsPerBlock);
+  const int rpb = rows_cfg().rpb;
+  const int64_t nblk = ceil_div(M, rpb);
   float* part_col = static_cast<float*>(workspace);
   float* part_s = reinterpret_cast<float*>(static_cast<char*>(workspace) +
                                            align_up(sizeof(float) * (size_t)(nblk * N), 256));
-  launch_rows_bwd<0, T>(rows_vec_ok<T>(N, g_y, ld_gy, z, N, g_z, N), (unsigned)nblk, s, g_y, ld_gy, z, N, M, (int)N,
+  launch_rows_bwd<0, T>(rows_vec_ok<T>(N, g_y, ld_gy, z, N, g_z, N), (unsigned)nblk, rpb, s, g_y, ld_gy, z, N, M, (int)N,
                         prelu, g_z, N, part_col, part_s);
   k_final_cols<<<(unsigned)N, 256, 0, s>>>(part_col, nblk, (int)N, g_bias);
   k_final_scalar<<<1, 256, 0, s>>>(part_s, nblk, g_prelu);
@@ -206,7 +246,7 @@ int combine_bwd(const char* what, const T* g, int64_t ld_g, const T* x_dst, int6
                 size_t workspace_bytes, void* stream) {
   HGIN_ARG_CHECK(n_rows >= 0 && f_dst >= 0 && f_dst < (1 << 24), "%s: bad sizes", what);
   HGIN_ARG_CHECK(eps && g_eps, "%s: NULL eps/g_eps", what);
-  const size_t need = align_up(sizeof(float) * (size_t)ceil_div(n_rows > 0 ? n_rows : 1, kRowsPerBlock), 256);
+  const size_t need = align_up(sizeof(float) * (size_t)ceil_div(n_rows > 0 ? n_rows : 1, kMinRowsPerBlock), 256);
   if (workspace_bytes < need || !workspace) {
     set_error("%s: workspace %zu < %zu", what, workspace_bytes, need);
     return HGIN_E_WORKSPACE;
@@ -214,9 +254,10 @@ int combine_bwd(const char* what, const T* g, int64_t ld_g, const T* x_dst, int6
   hipStream_t s = as_stream(stream);
   if (n_rows == 0 || f_dst == 0) return memset_async(g_eps, 0, sizeof(float), s, what);
   HGIN_ARG_CHECK(g && x_dst, "%s: NULL operand", what);
-  const int64_t nblk = ceil_div(n_rows, kRowsPerBlock);
+  const int rpb = rows_cfg().rpb;
+  const int64_t nblk = ceil_div(n_rows, rpb);
   float* part_s = static_cast<float*>(workspace);
-  launch_rows_bwd<1, T>(rows_vec_ok<T>(f_dst, g, ld_g, x_dst, ld_dst, g_x_dst, ld_gx), (unsigned)nblk, s, g, ld_g,
+  launch_rows_bwd<1, T>(rows_vec_ok<T>(f_dst, g, ld_g, x_dst, ld_dst, g_x_dst, ld_gx), (unsigned)nblk, rpb, s, g, ld_g,
                         x_dst, ld_dst, n_rows, (int)f_dst, eps, g_x_dst, ld_gx, nullptr, part_s);
   k_final_scalar<<<1, 256, 0, s>>>(part_s, nblk, g_eps);
   return check_launch(what);
@@ -249,7 +290,7 @@ extern "C" int hgin_prelu_bwd_bf16(const uint16_t* g_y, int64_t ld_gy, const uin
 
 extern "C" int hgin_combine_bwd_workspace_size(int64_t n_rows, size_t* bytes) {
   HGIN_ARG_CHECK(bytes && n_rows >= 0, "hgin_combine_bwd_workspace_size: bad args");
-  *bytes = align_up(sizeof(float) * (size_t)ceil_div(n_rows > 0 ? n_rows : 1, kRowsPerBlock), 256);
+  *bytes = align_up(sizeof(float) * (size_t)ceil_div(n_rows > 0 ? n_rows : 1, kMinRowsPerBlock), 256);
   return HGIN_OK;
 }
 

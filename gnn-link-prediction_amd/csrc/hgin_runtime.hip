@@ -16,6 +16,14 @@ void set_error(const char* fmt, ...) {
   g_last_error = buf;
 }
 
+bool xcd_remap_enabled() {
+  static const bool on = [] {
+    const char* v = getenv("HGIN_XCD");
+    return !(v && v[0] == '0');
+  }();
+  return on;
+}
+
 }  // namespace hgin
 
 extern "C" int hgin_abi_version(void) { return HGIN_ABI_VERSION; }

@@ -38,7 +38,8 @@ def main():
         quick = "--quick" in sys.argv
         for _ in range(3):
             for name, fn in ([("mlp_fwd(z,y,accum)", lambda: ops.gin_mlp_fwd(a, w, b, s, acc)),
-                              ("gemm_nt", lambda: ops.gemm_nt(a, w))] if quick else [
+                              ("gemm_nt", lambda: ops.gemm_nt(a, w)),
+                              ("gemm_tn dW", lambda: ops.gemm_tn(gz, a))] if quick else [
                 ("mlp_fwd(z,y,accum)", lambda: ops.gin_mlp_fwd(a, w, b, s, acc)),
                 ("mlp_fwd(y only)", lambda: ops.gin_mlp_fwd(a, w, b, s, None, save_z=False)),
                 ("gemm_nt", lambda: ops.gemm_nt(a, w)),
