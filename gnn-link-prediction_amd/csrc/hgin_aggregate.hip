@@ -309,6 +309,204 @@ int dispatch_g_bf16(int lanes_needed, const int32_t* rowptr, const int32_t* col,
                                         combine, out, ld_out, s);
 }
 
+// ---------------------------------------------------------------------------------------------------
+// Wide-lane variant (both element types): each lane owns NQ 16-B quads (NQ*16 B of a row), so a wave
+// covers kWave/G rows with G = F / (NQ * elems-per-quad) — more rows, hence more independent neighbour
+// rows in flight per wave, for the short (degree 5-10) rows of the GIN relations.  Same per-feature
+// sequential edge-order sums as the kernels above (bit-identical results).
+template <typename T>
+struct Quad;
+template <>
+struct Quad<float> {
+  static constexpr int E = 4;
+  static __device__ __forceinline__ void unpack(const uint4& v, float* f) {
+    f[0] = __uint_as_float(v.x); f[1] = __uint_as_float(v.y); f[2] = __uint_as_float(v.z); f[3] = __uint_as_float(v.w);
+  }
+  static __device__ __forceinline__ uint4 pack(const float* f) {
+    return make_uint4(__float_as_uint(f[0]), __float_as_uint(f[1]), __float_as_uint(f[2]), __float_as_uint(f[3]));
+  }
+};
+template <>
+struct Quad<uint16_t> {
+  static constexpr int E = 8;
+  static __device__ __forceinline__ void unpack(const uint4& v, float* f) {
+    f[0] = bf_lo(v.x); f[1] = bf_hi(v.x); f[2] = bf_lo(v.y); f[3] = bf_hi(v.y);
+    f[4] = bf_lo(v.z); f[5] = bf_hi(v.z); f[6] = bf_lo(v.w); f[7] = bf_hi(v.w);
+  }
+  static __device__ __forceinline__ uint4 pack(const float* f) {
+    return make_uint4(pack_bf2(f[0], f[1]), pack_bf2(f[2], f[3]), pack_bf2(f[4], f[5]), pack_bf2(f[6], f[7]));
+  }
+};
+
+template <bool NT>
+__device__ __forceinline__ uint4 ld_quad(const void* p) {
+  if (!NT) return *reinterpret_cast<const uint4*>(p);
+  const u4v v = __builtin_nontemporal_load(reinterpret_cast<const u4v*>(p));
+  return make_uint4(v.x, v.y, v.z, v.w);
+}
+template <bool NT>
+__device__ __forceinline__ void st_quad(void* p, const uint4& v) {
+  const u4v t = {v.x, v.y, v.z, v.w};
+  if (NT) __builtin_nontemporal_store(t, reinterpret_cast<u4v*>(p));
+  else *reinterpret_cast<u4v*>(p) = t;
+}
+
+template <typename T, int NQ, int G, int U, bool NT>
+__global__ __launch_bounds__(256) void k_agg_q(const int32_t* __restrict__ rowptr, const int32_t* __restrict__ col,
+                                               int64_t n_rows, const T* __restrict__ x_src, int64_t ld_src, int f_src,
+                                               const T* __restrict__ x_dst, int64_t ld_dst, int f_dst,
+                                               const float* __restrict__ eps, int combine, T* __restrict__ out,
+                                               int64_t ld_out) {
+  constexpr int E = Quad<T>::E;
+  constexpr int VEC = E * NQ;
+  constexpr int kRowsPerWave = kWave / G;
+  const int lane = threadIdx.x & (kWave - 1);
+  const int grp = lane / G;
+  const int gl = lane % G;
+  const int64_t wave_id = (int64_t)blockIdx.x * (blockDim.x / kWave) + (threadIdx.x / kWave);
+  const int64_t r = wave_id * kRowsPerWave + grp;
+  if (r >= n_rows) return;
+  const int beg = rowptr[r];
+  const int end = rowptr[r + 1];
+  const float s = combine != HGIN_COMBINE_NONE ? __fadd_rn(1.0f, eps[0]) : 1.0f;
+  T* __restrict__ orow = out + r * ld_out;
+  for (int f0 = gl * VEC; f0 < f_src; f0 += G * VEC) {
+    float acc[VEC];
+#pragma unroll
+    for (int c = 0; c < VEC; ++c) acc[c] = 0.0f;
+    int k = beg;
+    for (; k + U <= end; k += U) {
+      int idx[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) idx[u] = col[k + u];
+      uint4 v[U][NQ];
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) v[u][q] = ld_quad<false>(x_src + (int64_t)idx[u] * ld_src + f0 + q * E);
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) {
+          float f[E];
+          Quad<T>::unpack(v[u][q], f);
+#pragma unroll
+          for (int c = 0; c < E; ++c) acc[q * E + c] = __fadd_rn(acc[q * E + c], f[c]);
+        }
+    }
+    for (; k < end; ++k) {
+      const T* p = x_src + (int64_t)col[k] * ld_src + f0;
+      uint4 v[NQ];
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) v[q] = ld_quad<false>(p + q * E);
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) {
+        float f[E];
+        Quad<T>::unpack(v[q], f);
+#pragma unroll
+        for (int c = 0; c < E; ++c) acc[q * E + c] = __fadd_rn(acc[q * E + c], f[c]);
+      }
+    }
+    if (combine == HGIN_COMBINE_ADD) {
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) {
+        float f[E];
+        Quad<T>::unpack(ld_quad<NT>(x_dst + r * ld_dst + f0 + q * E), f);
+#pragma unroll
+        for (int c = 0; c < E; ++c) acc[q * E + c] = __fadd_rn(acc[q * E + c], __fmul_rn(s, f[c]));
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) st_quad<NT>(orow + f0 + q * E, Quad<T>::pack(acc + q * E));
+  }
+  if (combine == HGIN_COMBINE_CONCAT) {
+    for (int f0 = gl * VEC; f0 < f_dst; f0 += G * VEC) {
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) {
+        float f[E];
+        Quad<T>::unpack(ld_quad<NT>(x_dst + r * ld_dst + f0 + q * E), f);
+#pragma unroll
+        for (int c = 0; c < E; ++c) f[c] = __fmul_rn(s, f[c]);
+        st_quad<NT>(orow + f_src + f0 + q * E, Quad<T>::pack(f));
+      }
+    }
+  }
+}
+
+// Quads per lane (HGIN_AGG_NQ = 1, 2 or 4 forces one; tools/agg_bench.py).  Default, measured
+// (profiles/r01_agg_nq_variants.txt): 4 quads for the ADD / NONE (backward) aggregates — +15-47 % for bf16,
+// 0-15 % for fp32 — and the 1-quad kernels for CONCAT, whose second output stream made wide lanes 10-60 %
+// slower.
+int agg_nq_env() {
+  static const int v = [] {
+    const char* e = getenv("HGIN_AGG_NQ");
+    const int x = e ? atoi(e) : 0;
+    return (x == 1 || x == 2 || x == 4) ? x : 0;
+  }();
+  return v;
+}
+int agg_nq(int combine) {
+  const int env = agg_nq_env();
+  if (env) return env;
+  return combine == HGIN_COMBINE_CONCAT ? 1 : 4;
+}
+
+template <typename T, int NQ>
+int launch_agg_q(int lanes_needed, const int32_t* rowptr, const int32_t* col, int64_t n_rows, const T* x_src,
+                 int64_t ld_src, int f_src, const T* x_dst, int64_t ld_dst, int f_dst, const float* eps, int combine,
+                 T* out, int64_t ld_out, hipStream_t s, const char* what) {
+  constexpr int kU = NQ >= 4 ? 4 : 8;
+  const bool nt = combine == HGIN_COMBINE_CONCAT;
+#define HGIN_AGGQ_CASE(GV)                                                                                       \
+  if (lanes_needed <= GV) {                                                                                     \
+    const int64_t blocks = ceil_div(ceil_div(n_rows, kWave / GV), 256 / kWave);                                 \
+    if (nt)                                                                                                     \
+      k_agg_q<T, NQ, GV, kU, true><<<dim3((unsigned)blocks), 256, 0, s>>>(rowptr, col, n_rows, x_src, ld_src,   \
+                                                                         f_src, x_dst, ld_dst, f_dst, eps,      \
+                                                                         combine, out, ld_out);                 \
+    else                                                                                                        \
+      k_agg_q<T, NQ, GV, kU, false><<<dim3((unsigned)blocks), 256, 0, s>>>(rowptr, col, n_rows, x_src, ld_src,  \
+                                                                          f_src, x_dst, ld_dst, f_dst, eps,     \
+                                                                          combine, out, ld_out);                \
+    return check_launch(what);                                                                                  \
+  }
+  HGIN_AGGQ_CASE(2)
+  HGIN_AGGQ_CASE(4)
+  HGIN_AGGQ_CASE(8)
+  HGIN_AGGQ_CASE(16)
+  HGIN_AGGQ_CASE(32)
+#undef HGIN_AGGQ_CASE
+  const int64_t blocks = ceil_div(n_rows, 256 / kWave);
+  if (nt)
+    k_agg_q<T, NQ, 64, kU, true><<<dim3((unsigned)blocks), 256, 0, s>>>(rowptr, col, n_rows, x_src, ld_src, f_src,
+                                                                        x_dst, ld_dst, f_dst, eps, combine, out,
+                                                                        ld_out);
+  else
+    k_agg_q<T, NQ, 64, kU, false><<<dim3((unsigned)blocks), 256, 0, s>>>(rowptr, col, n_rows, x_src, ld_src, f_src,
+                                                                         x_dst, ld_dst, f_dst, eps, combine, out,
+                                                                         ld_out);
+  return check_launch(what);
+}
+
+// Try the wide-lane kernel with nq quads per lane; returns -1000 when the shapes do not allow it.
+template <typename T>
+int try_agg_wide(int nq, const int32_t* rowptr, const int32_t* col, int64_t n_rows, const T* x_src, int64_t ld_src,
+                 int f_src, const T* x_dst, int64_t ld_dst, int f_dst, const float* eps, int combine, T* out,
+                 int64_t ld_out, hipStream_t s, const char* what) {
+  const int vec = Quad<T>::E * nq;
+  const int fd = combine == HGIN_COMBINE_CONCAT ? f_dst : 0;
+  if (f_src % vec || fd % vec || (combine == HGIN_COMBINE_ADD && f_dst % vec)) return -1000;
+  const int widest = f_src > fd ? f_src : fd;
+  const int lanes = (widest + vec - 1) / vec;
+  if (nq == 2)
+    return launch_agg_q<T, 2>(lanes, rowptr, col, n_rows, x_src, ld_src, f_src, x_dst, ld_dst, f_dst, eps, combine,
+                              out, ld_out, s, what);
+  if (nq == 4)
+    return launch_agg_q<T, 4>(lanes, rowptr, col, n_rows, x_src, ld_src, f_src, x_dst, ld_dst, f_dst, eps, combine,
+                              out, ld_out, s, what);
+  return -1000;
+}
+
 int check_aggregate_args(const char* what, const int32_t* rowptr, int64_t n_rows, int64_t ld_src, int64_t f_src,
                          const void* x_dst, int64_t ld_dst, int64_t f_dst, const float* eps, int combine,
                          const void* out, int64_t ld_out) {
@@ -349,6 +547,11 @@ extern "C" int hgin_aggregate_bf16(const int32_t* rowptr, const int32_t* col, in
                     dst_ok && (f_src > 0 || f_dst > 0);
   const int fd = combine == HGIN_COMBINE_CONCAT ? (int)f_dst : 0;
   const int64_t widest = f_src > fd ? f_src : fd;
+  if (vec8 && agg_nq(combine) > 1) {
+    const int rc = try_agg_wide<uint16_t>(agg_nq(combine), rowptr, col, n_rows, x_src, ld_src, (int)f_src, x_dst, ld_dst,
+                                          (int)f_dst, eps, combine, out, ld_out, s, "hgin_aggregate_bf16");
+    if (rc != -1000) return rc;
+  }
   if (vec8)
     return dispatch_g_bf16<8>((int)ceil_div(widest, 8), rowptr, col, n_rows, x_src, ld_src, (int)f_src, x_dst, ld_dst,
                               (int)f_dst, eps, combine, out, ld_out, s);
@@ -368,6 +571,11 @@ extern "C" int hgin_aggregate_f32(const int32_t* rowptr, const int32_t* col, int
   const bool vec4 = f_src % 4 == 0 && aligned16(x_src) && ld_src % 4 == 0 && aligned16(out) && ld_out % 4 == 0 &&
                     dst_ok && (f_src > 0 || f_dst > 0);
   const int fd = combine == HGIN_COMBINE_CONCAT ? (int)f_dst : 0;
+  if (vec4 && agg_nq(combine) > 1) {
+    const int rc = try_agg_wide<float>(agg_nq(combine), rowptr, col, n_rows, x_src, ld_src, (int)f_src, x_dst, ld_dst,
+                                       (int)f_dst, eps, combine, out, ld_out, s, "hgin_aggregate_f32");
+    if (rc != -1000) return rc;
+  }
   if (vec4) {
     const int64_t widest = f_src > fd ? f_src : fd;
     return dispatch_g<4>((int)ceil_div(widest, 4), rowptr, col, n_rows, x_src, ld_src, (int)f_src, x_dst, ld_dst,

@@ -108,6 +108,11 @@ _SIGS = {
     "hgin_gemm_tn_bf16": ([_P, _I64, _P, _I64, _I64, _P, _I64, _I64, _I64, _I64, _P, _I64, _P, _SZ, _P], _I32),
     "hgin_prelu_bwd_bf16": ([_P, _I64, _P, _I64, _I64, _P, _P, _P, _P, _P, _SZ, _P], _I32),
     "hgin_combine_bwd_bf16": ([_P, _I64, _P, _I64, _I64, _I64, _P, _P, _I64, _P, _P, _SZ, _P], _I32),
+    "hgin_head_mape_workspace_size": ([_I64, _I64, ctypes.POINTER(_SZ)], _I32),
+    "hgin_head_mape_fwd_f32": ([_P, _I64, _I64, _I64, _P, _P, _P, _P, _P, _P, _SZ, _P], _I32),
+    "hgin_head_mape_fwd_bf16": ([_P, _I64, _I64, _I64, _P, _P, _P, _P, _P, _P, _SZ, _P], _I32),
+    "hgin_head_mape_bwd_f32": ([_P, _I64, _I64, _I64, _P, _P, _P, _P, _P, _I64, _P, _P, _P, _SZ, _P], _I32),
+    "hgin_head_mape_bwd_bf16": ([_P, _I64, _I64, _I64, _P, _P, _P, _P, _P, _I64, _P, _P, _P, _SZ, _P], _I32),
     "hgin_batched_copy": ([_P, _I64, _I64, _P], _I32),
     "hgin_neg_sample": ([_U64, _U64, _I64, _I64, _P, _P], _I32),
     "hgin_dot_decode_fwd_f32": ([_P, _P, _I64, _P, _I64, _P, _I64, _I64, _P, _P], _I32),

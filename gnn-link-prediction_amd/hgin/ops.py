@@ -470,3 +470,60 @@ def gin_conv(x_src: Tensor, x_dst: Tensor, eps: Tensor, weight: Tensor, bias: Te
     if accum is not None:
         accum = accum.contiguous()      # the epilogue reads accum with row stride N
     return _GINConvFn.apply(x_src, x_dst, eps, _rowmajor(weight), bias.contiguous(), prelu, accum, graph, mode)
+
+
+# ---------------------------------------------------------------------------------------------------
+# F3: fused readout head + MAPE loss
+# ---------------------------------------------------------------------------------------------------
+class _HeadMapeFn(torch.autograd.Function):
+    """out = h @ w^T + b (the head Linear(K, 1), models.py:326-330) and loss_value = mape(out, y)
+    (train.py:12-13, :38-42) in one forward pass and one backward pass; ``out`` is returned for metrics
+    and carries no gradient (train.py back-propagates through the loss only)."""
+
+    @staticmethod
+    def forward(ctx, h, weight, bias, y):
+        M, K = h.shape
+        dev = h.device
+        out = torch.empty(M, 1, dtype=torch.float32, device=dev)
+        lv = torch.empty((), dtype=torch.float32, device=dev)
+        w = weight.reshape(-1).to(torch.float32).contiguous()
+        nbytes = ctypes.c_size_t(0)
+        _lib.check(_lib.lib().hgin_head_mape_workspace_size(M, K, ctypes.byref(nbytes)), "head_mape_workspace")
+        ws = _workspace(nbytes.value, dev)
+        _lib.call(f"hgin_head_mape_fwd_{_sfx(h)}", _p(h), h.stride(0), M, K, _p(w), _p(bias), _p(y), _p(out),
+                  _p(lv), _p(ws), nbytes.value, _stream(h))
+        ctx.save_for_backward(h, w, y, out)
+        ctx.mark_non_differentiable(out)
+        return out, lv
+
+    @staticmethod
+    def backward(ctx, g_out_unused, g_lv):
+        h, w, y, out = ctx.saved_tensors
+        need_h, need_w, need_b, _ = ctx.needs_input_grad
+        M, K = h.shape
+        dev = h.device
+        g_lv = g_lv.to(torch.float32).reshape(1).contiguous()
+        g_h = torch.empty_like(h) if need_h else None
+        g_w = torch.empty(1, K, dtype=torch.float32, device=dev)
+        g_b = torch.empty(1, dtype=torch.float32, device=dev)
+        nbytes = ctypes.c_size_t(0)
+        _lib.check(_lib.lib().hgin_head_mape_workspace_size(M, K, ctypes.byref(nbytes)), "head_mape_workspace")
+        ws = _workspace(nbytes.value, dev)
+        _lib.call(f"hgin_head_mape_bwd_{_sfx(h)}", _p(h), h.stride(0), M, K, _p(w), _p(y), _p(out), _p(g_lv),
+                  _p(g_h), g_h.stride(0) if g_h is not None else K, _p(g_w), _p(g_b), _p(ws), nbytes.value,
+                  _stream(h))
+        return g_h, (g_w if need_w else None), (g_b if need_b else None), None
+
+
+def head_mape(h: Tensor, weight: Tensor, bias: Tensor, y: Tensor):
+    """(out [M, 1], loss_value) = (h @ W^T + b, 100 * mean(|(out - y) / y|)) on libhgin.so (F3)."""
+    require_device(h, weight, bias, y, what="hgin.head_mape")
+    h = _rowmajor(_f32(h, "h"))
+    if weight.dim() != 2 or weight.size(0) != 1 or weight.size(1) != h.size(1):
+        raise RuntimeError(f"head_mape: weight must be [1, {h.size(1)}], got {list(weight.shape)}")
+    y = y.reshape(-1)
+    if y.numel() != h.size(0):
+        raise RuntimeError(f"head_mape: {y.numel()} labels for {h.size(0)} rows")
+    if y.dtype != torch.float32:
+        raise TypeError(f"head_mape: labels must be float32, got {y.dtype}")
+    return _HeadMapeFn.apply(h, weight, bias.reshape(1).to(torch.float32).contiguous(), y.contiguous())

@@ -37,11 +37,16 @@ def load_optimizer(config: dict, model: torch.nn.Module) -> torch.optim.Optimize
 
 
 def train_step(model, opt, graph, loss_func=mape, reducer: Optional[GradAllReducer] = None,
-               sync_metric: bool = False):
+               sync_metric: bool = False, fused_loss: bool = True):
+    """One train.py:31-44 iteration.  ``fused_loss`` (default): when the loss is train.py's ``mape`` and the
+    model offers ``forward_loss`` (hgin.HetroGIN), the readout head and the loss run fused (§8 F3)."""
     opt.zero_grad()
-    out = model(graph.x_dict(), graph.edge_index_dict(), graph.batch["path"])
     label = graph.y.reshape(-1, 1)
-    loss_value = loss_func(out, label)
+    if fused_loss and loss_func is mape and hasattr(model, "forward_loss"):
+        out, loss_value = model.forward_loss(graph.x_dict(), graph.edge_index_dict(), graph.batch["path"], graph.y)
+    else:
+        out = model(graph.x_dict(), graph.edge_index_dict(), graph.batch["path"])
+        loss_value = loss_func(out, label)
     loss = torch.sqrt(loss_value)
     loss.backward()
     if reducer is not None:

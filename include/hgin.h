@@ -168,6 +168,28 @@ int hgin_combine_bwd_bf16(const uint16_t* g, int64_t ld_g, const uint16_t* x_dst
                           int64_t n_rows, int64_t f_dst, const float* eps, uint16_t* g_x_dst, int64_t ld_gx,
                           float* g_eps, void* workspace, size_t workspace_bytes, void* stream);
 
+/* ---- F3: fused readout head + MAPE loss ------------------------------------------------------------
+ * Replaces the head Linear(K, 1) (models.py:326-330, :373-374) and train.py:38-42:
+ *   out[m] = sum_k h[m, k] w[k] + b[0];   *loss_value = 100 * mean_m |(out[m] - y[m]) / y[m]|   (train.py:12-13)
+ * written to device memory (no host sync).  Backward, given g_loss = d J / d loss_value (device float[1]):
+ *   g_out[m] = ((100 g_loss / M) * sgn(q[m])) / y[m],  q = (out - y) / y   (torch's autograd of mape)
+ *   g_h[m, k] = g_out[m] w[k] (g_h may be NULL);  g_w[k] = sum_m g_out[m] h[m, k];  g_b[0] = sum_m g_out[m]
+ * Fixed-order reductions (deterministic).  h: fp32 or bf16 [M, K] (ldh); w [K], b [1], y [M], out [M] fp32.
+ * workspace: hgin_head_mape_workspace_size(M, K). */
+int hgin_head_mape_workspace_size(int64_t M, int64_t K, size_t* bytes);
+int hgin_head_mape_fwd_f32(const float* h, int64_t ldh, int64_t M, int64_t K, const float* w, const float* b,
+                           const float* y, float* out, float* loss_value, void* workspace, size_t workspace_bytes,
+                           void* stream);
+int hgin_head_mape_fwd_bf16(const uint16_t* h, int64_t ldh, int64_t M, int64_t K, const float* w, const float* b,
+                            const float* y, float* out, float* loss_value, void* workspace, size_t workspace_bytes,
+                            void* stream);
+int hgin_head_mape_bwd_f32(const float* h, int64_t ldh, int64_t M, int64_t K, const float* w, const float* y,
+                           const float* out, const float* g_loss, float* g_h, int64_t ldg, float* g_w, float* g_b,
+                           void* workspace, size_t workspace_bytes, void* stream);
+int hgin_head_mape_bwd_bf16(const uint16_t* h, int64_t ldh, int64_t M, int64_t K, const float* w, const float* y,
+                            const float* out, const float* g_loss, uint16_t* g_h, int64_t ldg, float* g_w,
+                            float* g_b, void* workspace, size_t workspace_bytes, void* stream);
+
 /* ---- F1: device-side batch collation (replaces PyG's host Collater, dataset.py:239-244) -------------
  * Executes n_desc "segment copy with an integer shift" descriptors in one launch (device array `descs`);
  * max_count = the largest descriptor count (sizes the grid).  Kinds:
