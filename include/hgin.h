@@ -190,6 +190,27 @@ int hgin_head_mape_bwd_bf16(const uint16_t* h, int64_t ldh, int64_t M, int64_t K
                             const float* out, const float* g_loss, uint16_t* g_h, int64_t ldg, float* g_w,
                             float* g_b, void* workspace, size_t workspace_bytes, void* stream);
 
+/* ---- F4: queueing-theory baseline (replaces QTBaseline.forward, models.py:54-158, run on the CPU) ----
+ * Inputs prepared once per sample graph (hgin/qt.py): the path<->link edges (edge_type 0) as source runs
+ * (run_ptr int32 [n_runs + 1], run_src [n_runs], dst [E0]) and a CSR by destination over all vertices
+ * whose rows list edge ids by (position in run, edge id) (rowptr [N + 1], col [E0]; pos [E0]).
+ *   hgin_qt_traffic   val[e] = a[src] * prod_{earlier edges e' of the run} (1 - bp[dst[e']])   (models.py:103-121)
+ *   hgin_qt_link_sum  t[v] = sum over positions k (in order) of the in-order sum of val over row v's edges
+ *                     at position k  — the reference's `T += scatter(...)` per position, same rounding
+ *   hgin_qt_links     per link i (vertex link_ids[i]): rho = t / cap, bp = (1-rho) rho^B / ((1 - rho^(B+1))
+ *                     + 1e-8), pi_0 and the 32-term occupancy series, x[v] = occ * 32000 / cap_raw
+ *                     (models.py:125-145, :153); bp must be 0 at non-link vertices on entry
+ *   hgin_qt_delay     out[src] = in-order sum of x[dst] over the run (models.py:154-156) */
+int hgin_qt_traffic(const int32_t* run_ptr, int64_t n_runs, const int32_t* run_src, const int32_t* dst,
+                    const float* a, const float* bp, float* val, void* stream);
+int hgin_qt_link_sum(const int32_t* rowptr, const int32_t* col, const int32_t* pos, const float* val,
+                     int64_t n_rows, float* t_out, void* stream);
+int hgin_qt_links(const int32_t* link_ids, int64_t n_links, const float* t_sum, const float* cap,
+                  const float* cap_raw, int buffer, float* bp, float* rho, float* pi0, float* occ, float* x,
+                  void* stream);
+int hgin_qt_delay(const int32_t* run_ptr, int64_t n_runs, const int32_t* run_src, const int32_t* dst,
+                  const float* x, float* out, void* stream);
+
 /* ---- F1: device-side batch collation (replaces PyG's host Collater, dataset.py:239-244) -------------
  * Executes n_desc "segment copy with an integer shift" descriptors in one launch (device array `descs`);
  * max_count = the largest descriptor count (sizes the grid).  Kinds:
