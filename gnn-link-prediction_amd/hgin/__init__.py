@@ -9,6 +9,7 @@ from . import data  # noqa: F401
 from ._lib import HginError, HginUnavailable, build  # noqa: F401
 from .conv import GINConv, GINLayer, HeteroConv, MessagePassing, reset  # noqa: F401
 from .models import HetroGAT, HetroGIN  # noqa: F401
+from .qt import QTBaseline  # noqa: F401
 
-__all__ = ["HetroGIN", "HetroGAT", "GINLayer", "GINConv", "HeteroConv", "MessagePassing", "reset", "build",
+__all__ = ["HetroGIN", "HetroGAT", "QTBaseline", "GINLayer", "GINConv", "HeteroConv", "MessagePassing", "reset", "build",
            "HginError", "HginUnavailable", "data"]
