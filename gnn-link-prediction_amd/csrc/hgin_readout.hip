@@ -12,6 +12,8 @@
 // forms g_out = (100 g / M) * sgn(q) / y per row (the autograd of mape's mul / mean / abs / div), writes
 // g_h = g_out w and accumulates g_w = sum g_out h, g_b = sum g_out as fixed-order block partials, then a
 // fixed-order final pass.  Deterministic; h may be fp32 or bf16 (cfg5), everything else fp32.
+// m_valid (device int32, optional): only rows < *m_valid are labelled — the loss is their mean and the
+// other rows get zero gradient (static-shape padded batches replayed from a hipGraph, hgin/graphs.py).
 #include "hgin_common.h"
 
 namespace hgin {
@@ -34,14 +36,21 @@ __device__ __forceinline__ float block_sum_tree(float v, float* red) {
 
 __device__ __forceinline__ float sgn(float x) { return x > 0.0f ? 1.0f : (x < 0.0f ? -1.0f : 0.0f); }
 
+__device__ __forceinline__ int64_t valid_rows(const int32_t* m_valid, int64_t M) {
+  if (!m_valid) return M;
+  const int64_t v = m_valid[0];
+  return v < M ? (v < 0 ? 0 : v) : M;
+}
+
 // thread per row: out[m] = sum_k h[m, k] w[k] (sequential fmaf) + b;  part[blk] = sum |(out - y) / y|
 template <typename T>
 __global__ __launch_bounds__(256) void k_head_fwd(const T* __restrict__ h, int64_t ldh, int64_t M, int K,
                                                   const float* __restrict__ w, const float* __restrict__ b,
-                                                  const float* __restrict__ y, float* __restrict__ out,
-                                                  float* __restrict__ part) {
+                                                  const float* __restrict__ y, const int32_t* __restrict__ m_valid,
+                                                  float* __restrict__ out, float* __restrict__ part) {
   __shared__ float red[256];
   const int64_t m = (int64_t)blockIdx.x * kHeadRows + threadIdx.x;
+  const int64_t mv = valid_rows(m_valid, M);
   float a = 0.0f;
   if (m < M) {
     float s = 0.0f;
@@ -49,7 +58,7 @@ __global__ __launch_bounds__(256) void k_head_fwd(const T* __restrict__ h, int64
     for (int k = 0; k < K; ++k) s = __fmaf_rn(Elem<T>::ld(row + k), w[k], s);
     const float o = __fadd_rn(s, b[0]);
     out[m] = o;
-    a = fabsf(__fdiv_rn(__fsub_rn(o, y[m]), y[m]));
+    if (m < mv) a = fabsf(__fdiv_rn(__fsub_rn(o, y[m]), y[m]));
   }
   const float tot = block_sum_tree(a, red);
   if (threadIdx.x == 0) part[blockIdx.x] = tot;
@@ -57,13 +66,14 @@ __global__ __launch_bounds__(256) void k_head_fwd(const T* __restrict__ h, int64
 
 // loss_value = 100 * (sum of the partials in block order) / M
 __global__ __launch_bounds__(256) void k_head_loss_final(const float* __restrict__ part, int64_t nblk, int64_t M,
+                                                         const int32_t* __restrict__ m_valid,
                                                          float* __restrict__ loss_value) {
   __shared__ float red[256];
   float s = 0.0f;
   for (int64_t i = threadIdx.x; i < nblk; i += 256) s = __fadd_rn(s, part[i]);
   const float tot = block_sum_tree(s, red);
   if (threadIdx.x == 0) {
-    loss_value[0] = __fmul_rn(100.0f, __fdiv_rn(tot, (float)M));
+    loss_value[0] = __fmul_rn(100.0f, __fdiv_rn(tot, (float)valid_rows(m_valid, M)));
   }
 }
 
@@ -74,8 +84,8 @@ template <typename T>
 __global__ __launch_bounds__(256) void k_head_bwd(const T* __restrict__ h, int64_t ldh, int64_t M, int K,
                                                   const float* __restrict__ w, const float* __restrict__ y,
                                                   const float* __restrict__ out, const float* __restrict__ g_loss,
-                                                  T* __restrict__ g_h, int64_t ldg, float* __restrict__ part_w,
-                                                  float* __restrict__ part_b) {
+                                                  const int32_t* __restrict__ m_valid, T* __restrict__ g_h, int64_t ldg,
+                                                  float* __restrict__ part_w, float* __restrict__ part_b) {
   __shared__ float gbuf[kHeadRows];
   __shared__ float red[256];
   const int t = threadIdx.x;
@@ -83,10 +93,11 @@ __global__ __launch_bounds__(256) void k_head_bwd(const T* __restrict__ h, int64
   const int64_t n = M - r0 < kHeadRows ? M - r0 : kHeadRows;
   {
     const int64_t m = r0 + t;
+    const int64_t mv = valid_rows(m_valid, M);
     float g = 0.0f;
-    if (t < n) {
+    if (m < mv) {
       const float q = __fdiv_rn(__fsub_rn(out[m], y[m]), y[m]);
-      const float gm = __fdiv_rn(__fmul_rn(100.0f, g_loss[0]), (float)M);   // d(100 * mean)
+      const float gm = __fdiv_rn(__fmul_rn(100.0f, g_loss[0]), (float)mv);  // d(100 * mean)
       g = __fdiv_rn(__fmul_rn(gm, sgn(q)), y[m]);                               // abs, then the / y
     }
     gbuf[t] = g;
@@ -135,7 +146,8 @@ __global__ __launch_bounds__(256) void k_head_bwd_final(const float* __restrict_
 
 template <typename T>
 int head_fwd(const char* what, const T* h, int64_t ldh, int64_t M, int64_t K, const float* w, const float* b,
-             const float* y, float* out, float* loss_value, void* ws, size_t ws_bytes, void* stream) {
+             const float* y, const int32_t* m_valid, float* out, float* loss_value, void* ws, size_t ws_bytes,
+             void* stream) {
   HGIN_ARG_CHECK(M > 0 && K > 0 && K <= 4096 && ldh >= K, "%s: bad sizes (M %lld, K %lld)", what, (long long)M,
                  (long long)K);
   HGIN_ARG_CHECK(h && w && b && y && out && loss_value, "%s: NULL operand", what);
@@ -148,15 +160,15 @@ int head_fwd(const char* what, const T* h, int64_t ldh, int64_t M, int64_t K, co
   hipStream_t s = as_stream(stream);
   const int64_t nblk = ceil_div(M, kHeadRows);
   float* part = static_cast<float*>(ws);
-  k_head_fwd<T><<<(unsigned)nblk, 256, 0, s>>>(h, ldh, M, (int)K, w, b, y, out, part);
-  k_head_loss_final<<<1, 256, 0, s>>>(part, nblk, M, loss_value);
+  k_head_fwd<T><<<(unsigned)nblk, 256, 0, s>>>(h, ldh, M, (int)K, w, b, y, m_valid, out, part);
+  k_head_loss_final<<<1, 256, 0, s>>>(part, nblk, M, m_valid, loss_value);
   return check_launch(what);
 }
 
 template <typename T>
 int head_bwd(const char* what, const T* h, int64_t ldh, int64_t M, int64_t K, const float* w, const float* y,
-             const float* out, const float* g_loss, T* g_h, int64_t ldg, float* g_w, float* g_b, void* ws,
-             size_t ws_bytes, void* stream) {
+             const float* out, const float* g_loss, const int32_t* m_valid, T* g_h, int64_t ldg, float* g_w,
+             float* g_b, void* ws, size_t ws_bytes, void* stream) {
   HGIN_ARG_CHECK(M > 0 && K > 0 && K <= 4096 && ldh >= K, "%s: bad sizes", what);
   HGIN_ARG_CHECK(h && w && y && out && g_loss && g_w && g_b, "%s: NULL operand", what);
   HGIN_ARG_CHECK(!g_h || ldg >= K, "%s: ldg < K", what);
@@ -170,7 +182,8 @@ int head_bwd(const char* what, const T* h, int64_t ldh, int64_t M, int64_t K, co
   const int64_t nblk = ceil_div(M, kHeadRows);
   float* part_w = static_cast<float*>(ws);
   float* part_b = part_w + nblk * K;
-  k_head_bwd<T><<<(unsigned)nblk, 256, 0, s>>>(h, ldh, M, (int)K, w, y, out, g_loss, g_h, ldg, part_w, part_b);
+  k_head_bwd<T><<<(unsigned)nblk, 256, 0, s>>>(h, ldh, M, (int)K, w, y, out, g_loss, m_valid, g_h, ldg, part_w,
+                                               part_b);
   k_head_bwd_final<<<(unsigned)(K + 1), 256, 0, s>>>(part_w, part_b, nblk, (int)K, g_w, g_b);
   return check_launch(what);
 }
@@ -188,29 +201,31 @@ extern "C" int hgin_head_mape_workspace_size(int64_t M, int64_t K, size_t* bytes
 }
 
 extern "C" int hgin_head_mape_fwd_f32(const float* h, int64_t ldh, int64_t M, int64_t K, const float* w,
-                                      const float* b, const float* y, float* out, float* loss_value, void* ws,
-                                      size_t ws_bytes, void* stream) {
-  return head_fwd<float>("hgin_head_mape_fwd_f32", h, ldh, M, K, w, b, y, out, loss_value, ws, ws_bytes, stream);
+                                      const float* b, const float* y, const int32_t* m_valid, float* out,
+                                      float* loss_value, void* ws, size_t ws_bytes, void* stream) {
+  return head_fwd<float>("hgin_head_mape_fwd_f32", h, ldh, M, K, w, b, y, m_valid, out, loss_value, ws, ws_bytes,
+                         stream);
 }
 
 extern "C" int hgin_head_mape_fwd_bf16(const uint16_t* h, int64_t ldh, int64_t M, int64_t K, const float* w,
-                                       const float* b, const float* y, float* out, float* loss_value, void* ws,
-                                       size_t ws_bytes, void* stream) {
-  return head_fwd<uint16_t>("hgin_head_mape_fwd_bf16", h, ldh, M, K, w, b, y, out, loss_value, ws, ws_bytes,
-                            stream);
+                                       const float* b, const float* y, const int32_t* m_valid, float* out,
+                                       float* loss_value, void* ws, size_t ws_bytes, void* stream) {
+  return head_fwd<uint16_t>("hgin_head_mape_fwd_bf16", h, ldh, M, K, w, b, y, m_valid, out, loss_value, ws,
+                            ws_bytes, stream);
 }
 
 extern "C" int hgin_head_mape_bwd_f32(const float* h, int64_t ldh, int64_t M, int64_t K, const float* w,
-                                      const float* y, const float* out, const float* g_loss, float* g_h, int64_t ldg,
-                                      float* g_w, float* g_b, void* ws, size_t ws_bytes, void* stream) {
-  return head_bwd<float>("hgin_head_mape_bwd_f32", h, ldh, M, K, w, y, out, g_loss, g_h, ldg, g_w, g_b, ws,
+                                      const float* y, const float* out, const float* g_loss, const int32_t* m_valid,
+                                      float* g_h, int64_t ldg, float* g_w, float* g_b, void* ws, size_t ws_bytes,
+                                      void* stream) {
+  return head_bwd<float>("hgin_head_mape_bwd_f32", h, ldh, M, K, w, y, out, g_loss, m_valid, g_h, ldg, g_w, g_b, ws,
                          ws_bytes, stream);
 }
 
 extern "C" int hgin_head_mape_bwd_bf16(const uint16_t* h, int64_t ldh, int64_t M, int64_t K, const float* w,
-                                       const float* y, const float* out, const float* g_loss, uint16_t* g_h,
-                                       int64_t ldg, float* g_w, float* g_b, void* ws, size_t ws_bytes,
-                                       void* stream) {
-  return head_bwd<uint16_t>("hgin_head_mape_bwd_bf16", h, ldh, M, K, w, y, out, g_loss, g_h, ldg, g_w, g_b, ws,
-                            ws_bytes, stream);
+                                       const float* y, const float* out, const float* g_loss,
+                                       const int32_t* m_valid, uint16_t* g_h, int64_t ldg, float* g_w, float* g_b,
+                                       void* ws, size_t ws_bytes, void* stream) {
+  return head_bwd<uint16_t>("hgin_head_mape_bwd_bf16", h, ldh, M, K, w, y, out, g_loss, m_valid, g_h, ldg, g_w, g_b,
+                            ws, ws_bytes, stream);
 }

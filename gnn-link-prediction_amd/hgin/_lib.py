@@ -109,10 +109,10 @@ _SIGS = {
     "hgin_prelu_bwd_bf16": ([_P, _I64, _P, _I64, _I64, _P, _P, _P, _P, _P, _SZ, _P], _I32),
     "hgin_combine_bwd_bf16": ([_P, _I64, _P, _I64, _I64, _I64, _P, _P, _I64, _P, _P, _SZ, _P], _I32),
     "hgin_head_mape_workspace_size": ([_I64, _I64, ctypes.POINTER(_SZ)], _I32),
-    "hgin_head_mape_fwd_f32": ([_P, _I64, _I64, _I64, _P, _P, _P, _P, _P, _P, _SZ, _P], _I32),
-    "hgin_head_mape_fwd_bf16": ([_P, _I64, _I64, _I64, _P, _P, _P, _P, _P, _P, _SZ, _P], _I32),
-    "hgin_head_mape_bwd_f32": ([_P, _I64, _I64, _I64, _P, _P, _P, _P, _P, _I64, _P, _P, _P, _SZ, _P], _I32),
-    "hgin_head_mape_bwd_bf16": ([_P, _I64, _I64, _I64, _P, _P, _P, _P, _P, _I64, _P, _P, _P, _SZ, _P], _I32),
+    "hgin_head_mape_fwd_f32": ([_P, _I64, _I64, _I64, _P, _P, _P, _P, _P, _P, _P, _SZ, _P], _I32),
+    "hgin_head_mape_fwd_bf16": ([_P, _I64, _I64, _I64, _P, _P, _P, _P, _P, _P, _P, _SZ, _P], _I32),
+    "hgin_head_mape_bwd_f32": ([_P, _I64, _I64, _I64, _P, _P, _P, _P, _P, _P, _I64, _P, _P, _P, _SZ, _P], _I32),
+    "hgin_head_mape_bwd_bf16": ([_P, _I64, _I64, _I64, _P, _P, _P, _P, _P, _P, _I64, _P, _P, _P, _SZ, _P], _I32),
     "hgin_qt_traffic": ([_P, _I64, _P, _P, _P, _P, _P, _P], _I32),
     "hgin_qt_link_sum": ([_P, _P, _P, _P, _I64, _P, _P], _I32),
     "hgin_qt_links": ([_P, _I64, _P, _P, _P, _I32, _P, _P, _P, _P, _P, _P], _I32),

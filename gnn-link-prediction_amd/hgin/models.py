@@ -123,18 +123,19 @@ class HetroGIN(torch.nn.Module):
         return dead
 
     def forward(self, x_dict, edge_index_dict, path_batch):
-        return self._run(x_dict, edge_index_dict, path_batch, None)
+        return self._run(x_dict, edge_index_dict, path_batch, None, None)
 
-    def forward_loss(self, x_dict, edge_index_dict, path_batch, y):
+    def forward_loss(self, x_dict, edge_index_dict, path_batch, y, m_valid=None):
         """(out, loss_value) with loss_value = train.py's mape(out, y.reshape(-1, 1)) (train.py:12-13, :38-40).
 
         When the head is the plain Linear(mlp_layers[-1], 1) (mlp_head_act None, the reference default), the
         head and the loss run as one fused pass forward and one backward (ops.head_mape):
         no per-element torch kernels and no host sync; ``out`` carries no gradient.  Otherwise the head
-        runs as usual and the loss is the torch expression."""
-        return self._run(x_dict, edge_index_dict, path_batch, y)
+        runs as usual and the loss is the torch expression.  ``m_valid`` (device int32 [1], fused head only):
+        the loss covers path rows < m_valid (padded static-shape batches, hgin/graphs.py)."""
+        return self._run(x_dict, edge_index_dict, path_batch, y, m_valid)
 
-    def _run(self, x_dict, edge_index_dict, path_batch, y):
+    def _run(self, x_dict, edge_index_dict, path_batch, y, m_valid):
         # models.py:333-342 feature slicing (assigns into the caller's dict, as the reference does)
         if not self.divided_features:
             x_dict["path"] = torch.cat([x_dict["path"][:, 0:3], x_dict["path"][:, 6].reshape(-1, 1)], axis=1)
@@ -179,7 +180,7 @@ class HetroGIN(torch.nn.Module):
             if (y is not None and i == n_ro - 1 and x2 is None and len(seq) == 1
                     and isinstance(seq[0], torch.nn.Linear) and seq[0].bias is not None
                     and seq[0].out_features == 1):
-                return ops.head_mape(x, seq[0].weight, seq[0].bias, y)     # F3: head + mape fused
+                return ops.head_mape(x, seq[0].weight, seq[0].bias, y, m_valid)   # F3: head + mape fused
             if _fusable_linear_prelu(seq):
                 x = ops.linear_prelu(x, seq[0].weight, seq[0].bias, seq[1].weight, x2=x2)
             elif len(seq) == 1 and isinstance(seq[0], torch.nn.Linear) and seq[0].bias is not None:
@@ -190,6 +191,8 @@ class HetroGIN(torch.nn.Module):
                 x = seq(x)
             x2 = None
         if y is not None:   # head with an activation / mlp_layers == []: unfused loss (train.py:12-13)
+            if m_valid is not None:
+                raise NotImplementedError("m_valid (padded batches) needs the fused Linear(k, 1) head")
             from .train import mape
             return x, mape(x, y.reshape(-1, 1))
         return x

@@ -481,7 +481,7 @@ class _HeadMapeFn(torch.autograd.Function):
     and carries no gradient (train.py back-propagates through the loss only)."""
 
     @staticmethod
-    def forward(ctx, h, weight, bias, y):
+    def forward(ctx, h, weight, bias, y, m_valid):
         M, K = h.shape
         dev = h.device
         out = torch.empty(M, 1, dtype=torch.float32, device=dev)
@@ -490,8 +490,9 @@ class _HeadMapeFn(torch.autograd.Function):
         nbytes = ctypes.c_size_t(0)
         _lib.check(_lib.lib().hgin_head_mape_workspace_size(M, K, ctypes.byref(nbytes)), "head_mape_workspace")
         ws = _workspace(nbytes.value, dev)
-        _lib.call(f"hgin_head_mape_fwd_{_sfx(h)}", _p(h), h.stride(0), M, K, _p(w), _p(bias), _p(y), _p(out),
-                  _p(lv), _p(ws), nbytes.value, _stream(h))
+        _lib.call(f"hgin_head_mape_fwd_{_sfx(h)}", _p(h), h.stride(0), M, K, _p(w), _p(bias), _p(y), _p(m_valid),
+                  _p(out), _p(lv), _p(ws), nbytes.value, _stream(h))
+        ctx.m_valid = m_valid
         ctx.save_for_backward(h, w, y, out)
         ctx.mark_non_differentiable(out)
         return out, lv
@@ -499,7 +500,7 @@ class _HeadMapeFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, g_out_unused, g_lv):
         h, w, y, out = ctx.saved_tensors
-        need_h, need_w, need_b, _ = ctx.needs_input_grad
+        need_h, need_w, need_b = ctx.needs_input_grad[:3]
         M, K = h.shape
         dev = h.device
         g_lv = g_lv.to(torch.float32).reshape(1).contiguous()
@@ -510,13 +511,15 @@ class _HeadMapeFn(torch.autograd.Function):
         _lib.check(_lib.lib().hgin_head_mape_workspace_size(M, K, ctypes.byref(nbytes)), "head_mape_workspace")
         ws = _workspace(nbytes.value, dev)
         _lib.call(f"hgin_head_mape_bwd_{_sfx(h)}", _p(h), h.stride(0), M, K, _p(w), _p(y), _p(out), _p(g_lv),
-                  _p(g_h), g_h.stride(0) if g_h is not None else K, _p(g_w), _p(g_b), _p(ws), nbytes.value,
-                  _stream(h))
-        return g_h, (g_w if need_w else None), (g_b if need_b else None), None
+                  _p(ctx.m_valid), _p(g_h), g_h.stride(0) if g_h is not None else K, _p(g_w), _p(g_b), _p(ws),
+                  nbytes.value, _stream(h))
+        return g_h, (g_w if need_w else None), (g_b if need_b else None), None, None
 
 
-def head_mape(h: Tensor, weight: Tensor, bias: Tensor, y: Tensor):
-    """(out [M, 1], loss_value) = (h @ W^T + b, 100 * mean(|(out - y) / y|)) on libhgin.so (F3)."""
+def head_mape(h: Tensor, weight: Tensor, bias: Tensor, y: Tensor, m_valid: Optional[Tensor] = None):
+    """(out [M, 1], loss_value) = (h @ W^T + b, 100 * mean(|(out - y) / y|)) on libhgin.so (F3).
+
+    ``m_valid``: optional device int32 [1]; only rows < m_valid are labelled (padded static batches)."""
     require_device(h, weight, bias, y, what="hgin.head_mape")
     h = _rowmajor(_f32(h, "h"))
     if weight.dim() != 2 or weight.size(0) != 1 or weight.size(1) != h.size(1):
@@ -526,4 +529,6 @@ def head_mape(h: Tensor, weight: Tensor, bias: Tensor, y: Tensor):
         raise RuntimeError(f"head_mape: {y.numel()} labels for {h.size(0)} rows")
     if y.dtype != torch.float32:
         raise TypeError(f"head_mape: labels must be float32, got {y.dtype}")
-    return _HeadMapeFn.apply(h, weight, bias.reshape(1).to(torch.float32).contiguous(), y.contiguous())
+    if m_valid is not None and (m_valid.dtype != torch.int32 or m_valid.numel() != 1):
+        raise TypeError("head_mape: m_valid must be a device int32 tensor with one element")
+    return _HeadMapeFn.apply(h, weight, bias.reshape(1).to(torch.float32).contiguous(), y.contiguous(), m_valid)

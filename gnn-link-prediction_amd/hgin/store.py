@@ -23,6 +23,7 @@ rebuild.  ``normalize=True`` applies the reference's always-on feature normalisa
 """
 from __future__ import annotations
 
+from dataclasses import dataclass
 from typing import Dict, List, Optional, Sequence
 
 import numpy as np
@@ -157,18 +158,77 @@ class GraphStore:
         return ids, nodes, edges, b_node, b_edge
 
     def collate(self, ids: Sequence[int]) -> HeteroGraph:
+        """A new exactly-sized batch of the graphs ``ids`` (in that order), CSR / CSC attached."""
         ids, nodes, edges, b_node, b_edge = self.plan(ids)
         dev = self.device
+        x_out = {t: torch.empty(int(b_node[t][-1]), self.x[t].shape[1], dtype=self.x[t].dtype, device=dev)
+                 for t in self.types}
+        batch_out = {t: torch.empty(int(b_node[t][-1]), dtype=torch.long, device=dev) for t in self.types}
+        y_out = torch.empty(int(b_node["path"][-1]), dtype=self.y.dtype, device=dev)
+        ei_out, csr_out, csc_out = {}, {}, {}
+        for r in self.relations:
+            s, _, d = r
+            E = int(b_edge[r][-1])
+            n_s, n_d = int(b_node[s][-1]), int(b_node[d][-1])
+            ei_out[r] = torch.empty(2, E, dtype=torch.long, device=dev)
+            csr_out[r] = ops.Csr(torch.empty(n_d + 1, dtype=torch.int32, device=dev),
+                                 torch.empty(E, dtype=torch.int32, device=dev),
+                                 torch.empty(E, dtype=torch.int32, device=dev), n_d, n_s)
+            csc_out[r] = ops.Csr(torch.empty(n_s + 1, dtype=torch.int32, device=dev),
+                                 torch.empty(E, dtype=torch.int32, device=dev),
+                                 torch.empty(E, dtype=torch.int32, device=dev), n_s, n_d)
+        self._launch(ids, nodes, edges, b_node, b_edge, x_out, batch_out, y_out, ei_out, csr_out, csc_out, None)
+        for r in self.relations:
+            s, _, d = r
+            ops.attach_relation_graph(ei_out[r], int(b_node[s][-1]), int(b_node[d][-1]), csr_out[r], csc_out[r])
+        return HeteroGraph(x_out, ei_out, y_out, batch_out)
+
+    # ------------------------------------------------------------------- static-shape padded batches
+    def padded_batch(self, batch_size: int) -> "PaddedBatch":
+        """Static buffers able to hold any ``batch_size`` graphs of this store (capacity = batch_size x the
+        largest graph, per node type and relation).  ``collate_into`` refills them in place, so a training
+        step over them can be captured once into a hipGraph and replayed (hgin/graphs.py)."""
+        dev = self.device
+        cap_n = {t: int(batch_size * np.diff(self.node_off[t]).max()) for t in self.types}
+        cap_e = {r: int(batch_size * np.diff(self.edge_off[r]).max()) for r in self.relations}
+        x = {t: torch.zeros(cap_n[t], self.x[t].shape[1], dtype=self.x[t].dtype, device=dev) for t in self.types}
+        batch = {t: torch.zeros(cap_n[t], dtype=torch.long, device=dev) for t in self.types}
+        y = torch.ones(cap_n["path"], dtype=self.y.dtype, device=dev)
+        ei, csr, csc = {}, {}, {}
+        for r in self.relations:
+            s, _, d = r
+            E = cap_e[r]
+            ei[r] = torch.zeros(2, E, dtype=torch.long, device=dev)
+            csr[r] = ops.Csr(torch.zeros(cap_n[d] + 1, dtype=torch.int32, device=dev),
+                             torch.zeros(E, dtype=torch.int32, device=dev),
+                             torch.zeros(E, dtype=torch.int32, device=dev), cap_n[d], cap_n[s])
+            csc[r] = ops.Csr(torch.zeros(cap_n[s] + 1, dtype=torch.int32, device=dev),
+                             torch.zeros(E, dtype=torch.int32, device=dev),
+                             torch.zeros(E, dtype=torch.int32, device=dev), cap_n[s], cap_n[d])
+            ops.attach_relation_graph(ei[r], cap_n[s], cap_n[d], csr[r], csc[r])
+        m_valid = torch.zeros(1, dtype=torch.int32, device=dev)
+        return PaddedBatch(x, ei, y, batch, m_valid, csr, csc, batch_size)
+
+    def collate_into(self, ids: Sequence[int], out: "PaddedBatch") -> "PaddedBatch":
+        """Refill ``out`` with the graphs ``ids``: valid rows first; the CSR / CSC rows past the batch get
+        empty ranges (padding vertices are isolated) and ``out.m_valid`` = the batch's path count, so the
+        fused loss covers exactly the batch.  One batched-copy launch, no allocation, no host sync."""
+        ids, nodes, edges, b_node, b_edge = self.plan(ids)
+        if len(ids) > out.batch_size:
+            raise ValueError(f"collate_into: {len(ids)} graphs > batch capacity {out.batch_size}")
+        self._launch(ids, nodes, edges, b_node, b_edge, out.x, out.batch, out.y, out.edge_index, out.csr, out.csc,
+                     out.m_valid)
+        return out
+
+    def _launch(self, ids, nodes, edges, b_node, b_edge, x_out, batch_out, y_out, ei_out, csr_out, csc_out,
+                m_valid) -> None:
         descs: List[tuple] = []
 
         def ptr(t: Tensor, elem_off: int) -> int:
             return t.data_ptr() + int(elem_off) * t.element_size()
 
-        x_out, batch_out = {}, {}
         for t in self.types:
             F = self.x[t].shape[1]
-            x_out[t] = torch.empty(int(b_node[t][-1]), F, dtype=self.x[t].dtype, device=dev)
-            batch_out[t] = torch.empty(int(b_node[t][-1]), dtype=torch.long, device=dev)
             for j, g in enumerate(ids):
                 n = int(nodes[t][j])
                 if n == 0:
@@ -177,24 +237,17 @@ class GraphStore:
                 descs.append((ptr(self.x[t], s_off * F), ptr(x_out[t], b_off * F), n * F, 0,
                               _COPY_KIND[self.x[t].element_size()]))
                 descs.append((0, ptr(batch_out[t], b_off), n, j, FILL_I64))
-        y_out = torch.empty(int(b_node["path"][-1]), dtype=self.y.dtype, device=dev)
         for j, g in enumerate(ids):
             n = int(nodes["path"][j])
             if n:
                 descs.append((ptr(self.y, self.node_off["path"][g]), ptr(y_out, b_node["path"][j]), n, 0, COPY_F32))
 
-        ei_out, csr_out, csc_out = {}, {}, {}
         for r in self.relations:
             s, _, d = r
             E = int(b_edge[r][-1])
             n_s, n_d = int(b_node[s][-1]), int(b_node[d][-1])
-            e = torch.empty(2, E, dtype=torch.long, device=dev)
-            cr = ops.Csr(torch.empty(n_d + 1, dtype=torch.int32, device=dev),
-                         torch.empty(E, dtype=torch.int32, device=dev),
-                         torch.empty(E, dtype=torch.int32, device=dev), n_d, n_s)
-            cc = ops.Csr(torch.empty(n_s + 1, dtype=torch.int32, device=dev),
-                         torch.empty(E, dtype=torch.int32, device=dev),
-                         torch.empty(E, dtype=torch.int32, device=dev), n_s, n_d)
+            e, cr, cc = ei_out[r], csr_out[r], csc_out[r]
+            e_cap = e.shape[1]                    # row stride of the [2, E] edge_index buffer
             se, sc, ss = self.edge_index[r], self.csr[r], self.csc[r]
             E_store = se.shape[1]
             for j, g in enumerate(ids):
@@ -205,7 +258,7 @@ class GraphStore:
                 nd, ns = int(nodes[d][j]), int(nodes[s][j])
                 if m:
                     descs.append((ptr(se, es), ptr(e, eb), m, db_s - ds_s, COPY_I64_ADD))              # src row
-                    descs.append((ptr(se, E_store + es), ptr(e, E + eb), m, db_d - ds_d, COPY_I64_ADD))  # dst row
+                    descs.append((ptr(se, E_store + es), ptr(e, e_cap + eb), m, db_d - ds_d, COPY_I64_ADD))  # dst
                     descs.append((ptr(sc.col, es), ptr(cr.col, eb), m, db_s - ds_s, COPY_I32_ADD))
                     descs.append((ptr(sc.perm, es), ptr(cr.perm, eb), m, eb - es, COPY_I32_ADD))
                     descs.append((ptr(ss.col, es), ptr(cc.col, eb), m, db_d - ds_d, COPY_I32_ADD))
@@ -214,18 +267,26 @@ class GraphStore:
                     descs.append((ptr(sc.rowptr, ds_d), ptr(cr.rowptr, db_d), nd, eb - es, COPY_I32_ADD))
                 if ns:
                     descs.append((ptr(ss.rowptr, ds_s), ptr(cc.rowptr, db_s), ns, eb - es, COPY_I32_ADD))
-            descs.append((0, ptr(cr.rowptr, n_d), 1, E, FILL_I32))
-            descs.append((0, ptr(cc.rowptr, n_s), 1, E, FILL_I32))
-            ei_out[r], csr_out[r], csc_out[r] = e, cr, cc
+            # rowptr[n .. capacity] = E: the last row's end, and empty rows for padding vertices
+            descs.append((0, ptr(cr.rowptr, n_d), cr.rowptr.numel() - n_d, E, FILL_I32))
+            descs.append((0, ptr(cc.rowptr, n_s), cc.rowptr.numel() - n_s, E, FILL_I32))
+        if m_valid is not None:
+            descs.append((0, ptr(m_valid, 0), 1, int(b_node["path"][-1]), FILL_I32))
 
         arr = np.zeros(len(descs), dtype=DESC_DTYPE)
         for i, (src, dst, cnt, add, kind) in enumerate(descs):
             arr[i] = (src, dst, cnt, add, kind, 0)
         host = torch.from_numpy(arr.view(np.uint8)).pin_memory()
-        dev_desc = host.to(dev, non_blocking=True)
+        dev_desc = host.to(self.device, non_blocking=True)
         max_count = int(arr["count"].max()) if len(arr) else 0
         _lib.call("hgin_batched_copy", ops._p(dev_desc), len(arr), max_count, ops._stream(dev_desc))
-        for r in self.relations:
-            s, _, d = r
-            ops.attach_relation_graph(ei_out[r], int(b_node[s][-1]), int(b_node[d][-1]), csr_out[r], csc_out[r])
-        return HeteroGraph(x_out, ei_out, y_out, batch_out)
+
+
+@dataclass
+class PaddedBatch(HeteroGraph):
+    """Static-capacity batch buffers (GraphStore.padded_batch): rows past the current batch are isolated
+    padding vertices; ``m_valid`` (device int32) holds the current batch's path count for the fused loss."""
+    m_valid: Tensor = None
+    csr: Dict[EdgeType, ops.Csr] = None
+    csc: Dict[EdgeType, ops.Csr] = None
+    batch_size: int = 0

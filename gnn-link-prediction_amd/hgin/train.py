@@ -43,7 +43,8 @@ def train_step(model, opt, graph, loss_func=mape, reducer: Optional[GradAllReduc
     opt.zero_grad()
     label = graph.y.reshape(-1, 1)
     if fused_loss and loss_func is mape and hasattr(model, "forward_loss"):
-        out, loss_value = model.forward_loss(graph.x_dict(), graph.edge_index_dict(), graph.batch["path"], graph.y)
+        out, loss_value = model.forward_loss(graph.x_dict(), graph.edge_index_dict(), graph.batch["path"], graph.y,
+                                             getattr(graph, "m_valid", None))
     else:
         out = model(graph.x_dict(), graph.edge_index_dict(), graph.batch["path"])
         loss_value = loss_func(out, label)

@@ -175,20 +175,23 @@ int hgin_combine_bwd_bf16(const uint16_t* g, int64_t ld_g, const uint16_t* x_dst
  *   g_out[m] = ((100 g_loss / M) * sgn(q[m])) / y[m],  q = (out - y) / y   (torch's autograd of mape)
  *   g_h[m, k] = g_out[m] w[k] (g_h may be NULL);  g_w[k] = sum_m g_out[m] h[m, k];  g_b[0] = sum_m g_out[m]
  * Fixed-order reductions (deterministic).  h: fp32 or bf16 [M, K] (ldh); w [K], b [1], y [M], out [M] fp32.
+ * m_valid: NULL, or a device int32 — only rows < *m_valid are labelled: the mean runs over them and the other
+ * rows get zero gradient (padded static-shape batches replayed from a hipGraph).
  * workspace: hgin_head_mape_workspace_size(M, K). */
 int hgin_head_mape_workspace_size(int64_t M, int64_t K, size_t* bytes);
 int hgin_head_mape_fwd_f32(const float* h, int64_t ldh, int64_t M, int64_t K, const float* w, const float* b,
-                           const float* y, float* out, float* loss_value, void* workspace, size_t workspace_bytes,
-                           void* stream);
+                           const float* y, const int32_t* m_valid, float* out, float* loss_value, void* workspace,
+                           size_t workspace_bytes, void* stream);
 int hgin_head_mape_fwd_bf16(const uint16_t* h, int64_t ldh, int64_t M, int64_t K, const float* w, const float* b,
-                            const float* y, float* out, float* loss_value, void* workspace, size_t workspace_bytes,
-                            void* stream);
+                            const float* y, const int32_t* m_valid, float* out, float* loss_value, void* workspace,
+                            size_t workspace_bytes, void* stream);
 int hgin_head_mape_bwd_f32(const float* h, int64_t ldh, int64_t M, int64_t K, const float* w, const float* y,
-                           const float* out, const float* g_loss, float* g_h, int64_t ldg, float* g_w, float* g_b,
-                           void* workspace, size_t workspace_bytes, void* stream);
+                           const float* out, const float* g_loss, const int32_t* m_valid, float* g_h, int64_t ldg,
+                           float* g_w, float* g_b, void* workspace, size_t workspace_bytes, void* stream);
 int hgin_head_mape_bwd_bf16(const uint16_t* h, int64_t ldh, int64_t M, int64_t K, const float* w, const float* y,
-                            const float* out, const float* g_loss, uint16_t* g_h, int64_t ldg, float* g_w,
-                            float* g_b, void* workspace, size_t workspace_bytes, void* stream);
+                            const float* out, const float* g_loss, const int32_t* m_valid, uint16_t* g_h,
+                            int64_t ldg, float* g_w, float* g_b, void* workspace, size_t workspace_bytes,
+                            void* stream);
 
 /* ---- F4: queueing-theory baseline (replaces QTBaseline.forward, models.py:54-158, run on the CPU) ----
  * Inputs prepared once per sample graph (hgin/qt.py): the path<->link edges (edge_type 0) as source runs
