@@ -392,7 +392,8 @@ int64_t tn_target_wgs() {
 int64_t tn_splits(int64_t M, int64_t N, int64_t K, int64_t stage_rows = kTnBM, int64_t target = 1024) {
   int64_t S;
   if (tn_is_small(N, K)) {
-    S = ceil_div(M, 2048);                                 // 2048 rows per workgroup
+    S = ceil_div(M, 128);          // >= 128 rows per workgroup: small graphs (the F1 batches) still get
+                                   // dozens of workgroups instead of a handful of long serial loops
     if (S > 1024) S = 1024;
   } else {
     const int64_t tiles = ceil_div(N, 128) * ceil_div(K, 128);

@@ -274,8 +274,10 @@ class GraphStore:
             descs.append((0, ptr(m_valid, 0), 1, int(b_node["path"][-1]), FILL_I32))
 
         arr = np.zeros(len(descs), dtype=DESC_DTYPE)
-        for i, (src, dst, cnt, add, kind) in enumerate(descs):
-            arr[i] = (src, dst, cnt, add, kind, 0)
+        if descs:
+            cols = list(zip(*descs))
+            for name, vals in zip(("src", "dst", "count", "add", "kind"), cols):
+                arr[name] = vals
         host = torch.from_numpy(arr.view(np.uint8)).pin_memory()
         dev_desc = host.to(self.device, non_blocking=True)
         max_count = int(arr["count"].max()) if len(arr) else 0
