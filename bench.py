@@ -169,8 +169,11 @@ def main():
             a = s.get("aggregate")
             if a:
                 achieved = a["avg_work"] / (a["avg_ms"] / 1e3) / 1e9
-                roofline = {"bound": "hbm", "kernel": "hgin_aggregate_bf16 (k_aggregate_bf16<8,G,8>)" if bf16 else
-                            "hgin_aggregate_f32 (k_aggregate<4,32,8>)",
+                # every launch of the aggregate entry point in the timed region: the concat (layer-0) aggregates
+                # run k_aggregate[_bf16], the add-mode and backward (CSC) aggregates the wide-lane k_agg_q
+                roofline = {"bound": "hbm", "kernel": ("hgin_aggregate_bf16 (k_aggregate_bf16 concat + k_agg_q "
+                                                       "add/backward)") if bf16 else
+                            "hgin_aggregate_f32 (k_aggregate concat + k_agg_q add/backward)",
                             "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                             "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
                             "bytes_per_launch": a["avg_work"], "avg_launch_ms": round(a["avg_ms"], 5),

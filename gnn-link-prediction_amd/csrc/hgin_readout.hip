@@ -64,6 +64,67 @@ __global__ __launch_bounds__(256) void k_head_fwd(const T* __restrict__ h, int64
   if (threadIdx.x == 0) part[blockIdx.x] = tot;
 }
 
+// Vector variant (K a multiple of the 16-B quad, aligned rows): 8 lanes per row, each lane a 16-B quad of
+// columns per pass, so one load instruction covers 8 full 128-B row segments (coalesced) instead of 64
+// scattered 4-B reads; the 8 lane partials are combined by a fixed xor butterfly.  A block still owns 256
+// rows (each 8-lane group walks 8 of them), so the partial-sum layout matches k_head_fwd.
+template <typename T>
+struct HQuad;
+template <>
+struct HQuad<float> {
+  static constexpr int E = 4;
+  static __device__ __forceinline__ float dot(const float* p, const float* w, float acc) {
+    const float4 v = *reinterpret_cast<const float4*>(p);
+    acc = __fmaf_rn(v.x, w[0], acc);
+    acc = __fmaf_rn(v.y, w[1], acc);
+    acc = __fmaf_rn(v.z, w[2], acc);
+    return __fmaf_rn(v.w, w[3], acc);
+  }
+};
+template <>
+struct HQuad<uint16_t> {
+  static constexpr int E = 8;
+  static __device__ __forceinline__ float dot(const uint16_t* p, const float* w, float acc) {
+    const uint4 v = *reinterpret_cast<const uint4*>(p);
+    const uint32_t q[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      acc = __fmaf_rn(bf_lo(q[i]), w[2 * i], acc);
+      acc = __fmaf_rn(bf_hi(q[i]), w[2 * i + 1], acc);
+    }
+    return acc;
+  }
+};
+
+template <typename T>
+__global__ __launch_bounds__(256) void k_head_fwd_vec(const T* __restrict__ h, int64_t ldh, int64_t M, int K,
+                                                      const float* __restrict__ w, const float* __restrict__ b,
+                                                      const float* __restrict__ y, const int32_t* __restrict__ m_valid,
+                                                      float* __restrict__ out, float* __restrict__ part) {
+  constexpr int E = HQuad<T>::E;
+  __shared__ float red[256];
+  const int t = threadIdx.x;
+  const int grp = t >> 3, gl = t & 7;
+  const int64_t mv = valid_rows(m_valid, M);
+  float a = 0.0f;
+  for (int i = 0; i < kHeadRows / 32; ++i) {
+    const int64_t m = (int64_t)blockIdx.x * kHeadRows + grp + 32 * i;
+    float s = 0.0f;
+    if (m < M)
+      for (int c = gl * E; c < K; c += 8 * E) s = HQuad<T>::dot(h + m * ldh + c, w + c, s);
+    s = __fadd_rn(s, __shfl_xor(s, 1, 8));
+    s = __fadd_rn(s, __shfl_xor(s, 2, 8));
+    s = __fadd_rn(s, __shfl_xor(s, 4, 8));
+    if (m < M && gl == 0) {
+      const float o = __fadd_rn(s, b[0]);
+      out[m] = o;
+      if (m < mv) a = __fadd_rn(a, fabsf(__fdiv_rn(__fsub_rn(o, y[m]), y[m])));
+    }
+  }
+  const float tot = block_sum_tree(a, red);
+  if (t == 0) part[blockIdx.x] = tot;
+}
+
 // loss_value = 100 * (sum of the partials in block order) / M
 __global__ __launch_bounds__(256) void k_head_loss_final(const float* __restrict__ part, int64_t nblk, int64_t M,
                                                          const int32_t* __restrict__ m_valid,
@@ -160,7 +221,11 @@ int head_fwd(const char* what, const T* h, int64_t ldh, int64_t M, int64_t K, co
   hipStream_t s = as_stream(stream);
   const int64_t nblk = ceil_div(M, kHeadRows);
   float* part = static_cast<float*>(ws);
-  k_head_fwd<T><<<(unsigned)nblk, 256, 0, s>>>(h, ldh, M, (int)K, w, b, y, m_valid, out, part);
+  constexpr int E = HQuad<T>::E;
+  if (K % E == 0 && ldh % E == 0 && aligned16(h))
+    k_head_fwd_vec<T><<<(unsigned)nblk, 256, 0, s>>>(h, ldh, M, (int)K, w, b, y, m_valid, out, part);
+  else
+    k_head_fwd<T><<<(unsigned)nblk, 256, 0, s>>>(h, ldh, M, (int)K, w, b, y, m_valid, out, part);
   k_head_loss_final<<<1, 256, 0, s>>>(part, nblk, M, m_valid, loss_value);
   return check_launch(what);
 }
