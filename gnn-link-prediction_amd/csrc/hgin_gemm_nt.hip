@@ -201,13 +201,13 @@ __device__ __forceinline__ void epilogue(const f32x16 (&acc)[2][TN], float* smem
   }
 }
 
-template <int EPI, bool kVec, int TN>
+template <int EPI, bool kVec, int TN, int WNv>
 __global__ __launch_bounds__(256, 3) void k_gemm_nt(Src2 A, Src2 B, int64_t M, int64_t N, int64_t K,
                                                     const float* __restrict__ bias, const float* __restrict__ prelu,
                                                     const float* __restrict__ accum, float* __restrict__ Z,
                                                     float* __restrict__ Y, int64_t ldc, bool vec_out,
                                                     int64_t n_tiles, bool xcd) {
-  constexpr int WN = TN == 2 ? 2 : 1;     // waves along N
+  constexpr int WN = WNv;                 // waves along N
   constexpr int WM = 4 / WN;              // waves along M
   constexpr int BM = WM * 64;             // rows per workgroup tile
   constexpr int BN = WN * TN * 32;        // columns per workgroup tile
@@ -282,20 +282,53 @@ __global__ __launch_bounds__(256, 3) void k_gemm_nt(Src2 A, Src2 B, int64_t M, i
                            vec_out);
 }
 
-template <int EPI, int TN>
+template <int EPI, int TN, int WN>
 void launch_nt_tn(bool vec, const Src2& a, const Src2& b, int64_t M, int64_t N, int64_t K, const float* bias,
                   const float* prelu, const float* accum, float* z, float* y, int64_t ldc, bool vec_out,
                   hipStream_t s) {
-  constexpr int BM = (TN == 2 ? 2 : 4) * 64;
-  constexpr int BN = (TN == 2 ? 2 : 1) * TN * 32;
+  constexpr int BM = (4 / WN) * 64;
+  constexpr int BN = WN * TN * 32;
   const int64_t tiles = ceil_div(N, BN) * ceil_div(M, BM);
   const bool xcd = xcd_remap_enabled();
   dim3 grid((unsigned)(xcd ? round_up8(tiles) : tiles));
   if (vec)
-    k_gemm_nt<EPI, true, TN><<<grid, 256, 0, s>>>(a, b, M, N, K, bias, prelu, accum, z, y, ldc, vec_out, tiles, xcd);
+    k_gemm_nt<EPI, true, TN, WN><<<grid, 256, 0, s>>>(a, b, M, N, K, bias, prelu, accum, z, y, ldc, vec_out, tiles,
+                                                      xcd);
   else
-    k_gemm_nt<EPI, false, TN><<<grid, 256, 0, s>>>(a, b, M, N, K, bias, prelu, accum, z, y, ldc, vec_out, tiles,
-                                                   xcd);
+    k_gemm_nt<EPI, false, TN, WN><<<grid, 256, 0, s>>>(a, b, M, N, K, bias, prelu, accum, z, y, ldc, vec_out, tiles,
+                                                       xcd);
+}
+
+// Resident workgroups of a kernel across the device (occupancy x CUs), queried once per kernel.
+template <typename F>
+int64_t resident_slots(F kernel) {
+  int per_cu = 0, dev = 0;
+  hipDeviceProp_t prop;
+  if (hipGetDevice(&dev) != hipSuccess || hipGetDeviceProperties(&prop, dev) != hipSuccess ||
+      hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, 256, 0) != hipSuccess || per_cu <= 0)
+    return 768;
+  return (int64_t)per_cu * prop.multiProcessorCount;
+}
+
+// Row-tile height for N > 32 (HGIN_NT_BM = 64 / 128 forces one).  A launch runs in "rounds" of resident
+// workgroups and its last round is usually partly empty (cfg2: 782 tiles of 128 rows on 768 slots = two
+// rounds for 1.02 rounds of work); 64-row tiles halve the granularity.  Pick the height with the smaller
+// estimated time = rounds x relative tile time (a 64-row tile measured at ~kRel64 of a 128-row one).
+template <int EPI>
+bool use_bm64(int64_t M, int64_t N) {
+  static const int env = [] {
+    const char* v = getenv("HGIN_NT_BM");
+    return v ? atoi(v) : 0;
+  }();
+  if (env == 64) return true;
+  if (env == 128) return false;
+  static const int64_t slots128 = resident_slots(k_gemm_nt<EPI, true, 2, 2>);
+  static const int64_t slots64 = resident_slots(k_gemm_nt<EPI, true, 1, 4>);
+  constexpr double kRel64 = 0.56;
+  const int64_t nt = ceil_div(N, 128);
+  const double t128 = (double)ceil_div(nt * ceil_div(M, 128), slots128);
+  const double t64 = (double)ceil_div(nt * ceil_div(M, 64), slots64) * kRel64;
+  return t64 < t128;
 }
 
 template <int EPI>
@@ -306,9 +339,11 @@ int launch_nt(const Src2& a, const Src2& b, int64_t M, int64_t N, int64_t K, con
   const bool vec_out = ldc % 4 == 0 && aligned16(y) && (z == nullptr || aligned16(z)) &&
                        (accum == nullptr || aligned16(accum));
   if (N <= 32)
-    launch_nt_tn<EPI, 1>(vec, a, b, M, N, K, bias, prelu, accum, z, y, ldc, vec_out, s);
+    launch_nt_tn<EPI, 1, 1>(vec, a, b, M, N, K, bias, prelu, accum, z, y, ldc, vec_out, s);
+  else if (use_bm64<EPI>(M, N))
+    launch_nt_tn<EPI, 1, 4>(vec, a, b, M, N, K, bias, prelu, accum, z, y, ldc, vec_out, s);
   else
-    launch_nt_tn<EPI, 2>(vec, a, b, M, N, K, bias, prelu, accum, z, y, ldc, vec_out, s);
+    launch_nt_tn<EPI, 2, 2>(vec, a, b, M, N, K, bias, prelu, accum, z, y, ldc, vec_out, s);
   return check_launch(what);
 }
 

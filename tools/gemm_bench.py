@@ -26,6 +26,9 @@ def timeit(fn, reps=20):
 def main():
     shapes = [(600_000, 256, 128), (600_000, 128, 128), (300_000, 256, 128), (6_000_000 // 4, 512, 256),
               (1_500_000, 256, 256)]
+    for a in sys.argv[1:]:
+        if a.startswith("--shapes="):     # e.g. --shapes=300000x256x128,294912x256x128  (M x K x N)
+            shapes = [tuple(int(v) for v in s.split("x")) for s in a.split("=", 1)[1].split(",")]
     for M, K, N in shapes:
         a = torch.randn(M, K, device="cuda")
         w = torch.randn(N, K, device="cuda") / K ** 0.5
