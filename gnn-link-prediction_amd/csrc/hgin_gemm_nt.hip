@@ -408,14 +408,14 @@ __device__ __forceinline__ void store_tile_h(uint16_t* __restrict__ dst, const u
     *reinterpret_cast<uint4*>(dst + ((tid >> 3) + 32 * i) * kLdsH + (tid & 7) * 8) = r[i];
 }
 
-template <int EPI, bool kVec, int TN, typename OutT>
+template <int EPI, bool kVec, int TN, int WNv, typename OutT>
 __global__ __launch_bounds__(256, 3) void k_gemm_nt_bf16(Src2h A, Src2h B, int64_t M, int64_t N, int64_t K,
                                                          const float* __restrict__ bias,
                                                          const float* __restrict__ prelu,
                                                          const OutT* __restrict__ accum, OutT* __restrict__ Z,
                                                          OutT* __restrict__ Y, int64_t ldc, bool vec_out,
                                                          int64_t n_tiles, bool xcd) {
-  constexpr int WN = TN == 2 ? 2 : 1;
+  constexpr int WN = WNv;
   constexpr int WM = 4 / WN;
   constexpr int BM = WM * 64;
   constexpr int BN = WN * TN * 32;
@@ -486,6 +486,23 @@ __global__ __launch_bounds__(256, 3) void k_gemm_nt_bf16(Src2h A, Src2h B, int64
 }
 
 template <int EPI, typename OutT>
+bool use_bm64_bf16(int64_t M, int64_t N) {
+  static const int env = [] {
+    const char* v = getenv("HGIN_NT_BM");
+    return v ? atoi(v) : 0;
+  }();
+  if (env == 64) return true;
+  if (env == 128) return false;
+  static const int64_t slots128 = resident_slots(k_gemm_nt_bf16<EPI, true, 2, 2, OutT>);
+  static const int64_t slots64 = resident_slots(k_gemm_nt_bf16<EPI, true, 1, 4, OutT>);
+  constexpr double kRel64 = 0.56;
+  const int64_t nt = ceil_div(N, 128);
+  const double t128 = (double)ceil_div(nt * ceil_div(M, 128), slots128);
+  const double t64 = (double)ceil_div(nt * ceil_div(M, 64), slots64) * kRel64;
+  return t64 < t128;
+}
+
+template <int EPI, typename OutT>
 int launch_nt_bf16(const Src2h& a, const Src2h& b, int64_t M, int64_t N, int64_t K, const float* bias,
                    const float* prelu, const OutT* accum, OutT* z, OutT* y, int64_t ldc, hipStream_t s,
                    const char* what) {
@@ -493,24 +510,26 @@ int launch_nt_bf16(const Src2h& a, const Src2h& b, int64_t M, int64_t N, int64_t
                    (a.k1 == K || (aligned16(a.p2) && a.ld2 % 8 == 0)) && aligned16(b.p1) && b.ld1 % 8 == 0;
   const bool vec_out = ldc % 4 == 0 && aligned16(y) && (z == nullptr || aligned16(z)) &&
                        (accum == nullptr || aligned16(accum));
-#define HGIN_NT_BF16(TNV)                                                                                     \
+#define HGIN_NT_BF16(TNV, WNV)                                                                                \
   {                                                                                                          \
-    constexpr int BM = (TNV == 2 ? 2 : 4) * 64;                                                              \
-    constexpr int BN = (TNV == 2 ? 2 : 1) * TNV * 32;                                                        \
+    constexpr int BM = (4 / WNV) * 64;                                                                       \
+    constexpr int BN = WNV * TNV * 32;                                                                       \
     const int64_t tiles = ceil_div(N, BN) * ceil_div(M, BM);                                                 \
     const bool xcd = xcd_remap_enabled();                                                                    \
     dim3 grid((unsigned)(xcd ? round_up8(tiles) : tiles));                                                   \
     if (vec)                                                                                                 \
-      k_gemm_nt_bf16<EPI, true, TNV, OutT><<<grid, 256, 0, s>>>(a, b, M, N, K, bias, prelu, accum, z, y, ldc, \
-                                                                vec_out, tiles, xcd);                        \
+      k_gemm_nt_bf16<EPI, true, TNV, WNV, OutT><<<grid, 256, 0, s>>>(a, b, M, N, K, bias, prelu, accum, z, y, \
+                                                                     ldc, vec_out, tiles, xcd);              \
     else                                                                                                     \
-      k_gemm_nt_bf16<EPI, false, TNV, OutT><<<grid, 256, 0, s>>>(a, b, M, N, K, bias, prelu, accum, z, y,    \
-                                                                 ldc, vec_out, tiles, xcd);                  \
+      k_gemm_nt_bf16<EPI, false, TNV, WNV, OutT><<<grid, 256, 0, s>>>(a, b, M, N, K, bias, prelu, accum, z,  \
+                                                                      y, ldc, vec_out, tiles, xcd);          \
   }
   if (N <= 32)
-    HGIN_NT_BF16(1)
+    HGIN_NT_BF16(1, 1)
+  else if (use_bm64_bf16<EPI, OutT>(M, N))
+    HGIN_NT_BF16(1, 4)
   else
-    HGIN_NT_BF16(2)
+    HGIN_NT_BF16(2, 2)
 #undef HGIN_NT_BF16
   return check_launch(what);
 }
