@@ -313,7 +313,9 @@ int64_t resident_slots(F kernel) {
 // Row-tile height for N > 32 (HGIN_NT_BM = 64 / 128 forces one).  A launch runs in "rounds" of resident
 // workgroups and its last round is usually partly empty (cfg2: 782 tiles of 128 rows on 768 slots = two
 // rounds for 1.02 rounds of work); 64-row tiles halve the granularity.  Pick the height with the smaller
-// estimated time = rounds x relative tile time (a 64-row tile measured at ~kRel64 of a 128-row one).
+// estimated time = rounds x relative tile time.  Measured (profiles/r01_gemm_bm64.txt): a 64-row tile costs
+// ~0.73 of a 128-row one (4 vs 3 resident per CU, half the rows, but 1.5x the B-tile and LDS traffic per
+// MFMA); kRel64 = 0.8 keeps 128 unless the round count drops clearly (M = 100k: 100.6 -> 90.3 us, -10 %).
 template <int EPI>
 bool use_bm64(int64_t M, int64_t N) {
   static const int env = [] {
@@ -324,7 +326,7 @@ bool use_bm64(int64_t M, int64_t N) {
   if (env == 128) return false;
   static const int64_t slots128 = resident_slots(k_gemm_nt<EPI, true, 2, 2>);
   static const int64_t slots64 = resident_slots(k_gemm_nt<EPI, true, 1, 4>);
-  constexpr double kRel64 = 0.56;
+  constexpr double kRel64 = 0.8;
   const int64_t nt = ceil_div(N, 128);
   const double t128 = (double)ceil_div(nt * ceil_div(M, 128), slots128);
   const double t64 = (double)ceil_div(nt * ceil_div(M, 64), slots64) * kRel64;
@@ -495,7 +497,7 @@ bool use_bm64_bf16(int64_t M, int64_t N) {
   if (env == 128) return false;
   static const int64_t slots128 = resident_slots(k_gemm_nt_bf16<EPI, true, 2, 2, OutT>);
   static const int64_t slots64 = resident_slots(k_gemm_nt_bf16<EPI, true, 1, 4, OutT>);
-  constexpr double kRel64 = 0.56;
+  constexpr double kRel64 = 0.8;
   const int64_t nt = ceil_div(N, 128);
   const double t128 = (double)ceil_div(nt * ceil_div(M, 128), slots128);
   const double t64 = (double)ceil_div(nt * ceil_div(M, 64), slots64) * kRel64;
