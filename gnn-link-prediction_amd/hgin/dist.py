@@ -14,7 +14,7 @@ exactly as it does single-device.
 """
 from __future__ import annotations
 
-from typing import Iterable, List, Optional
+from typing import Iterable, List
 
 import torch
 import torch.distributed as dist
