@@ -44,29 +44,45 @@ struct Src2 {
 
 // ROWS x 32 floats of [p1 | p2] starting at (row0, k0) -> ROWS/32 float4 per thread:
 // thread t owns column chunk q = t & 7 of rows (t >> 3) + 32 i.
-template <bool kVec, int ROWS>
+// kClean (K and k1 multiples of kBK, 16-B aligned rows): a K-tile lies wholly in p1 or p2 (a scalar choice)
+// and rows past the end are clamped to the last row instead of branched around — their products land in
+// output rows / columns that are never stored — so the loads are branch-free and the compiler keeps the
+// prefetch in flight under the MFMAs (a per-load branch made it wait at each join).  Otherwise every
+// element is bounds-checked.
+template <bool kClean, int ROWS>
 __device__ __forceinline__ void load_tile(float4 (&r)[ROWS / 32], const Src2& s, int64_t row0, int64_t rows,
                                           int64_t k0, int64_t K, int tid) {
-  const int64_t kk = k0 + (tid & 7) * 4;
+  if constexpr (kClean) {
+    // select between the loaded VALUES: a select between the two struct fields' addresses would make
+    // the compiler copy the by-value kernel argument into scratch
+    const bool first = k0 < s.k1;
+    const uintptr_t u1 = reinterpret_cast<uintptr_t>(s.p1), u2 = reinterpret_cast<uintptr_t>(s.p2);
+    const int64_t l1 = s.ld1, l2 = s.ld2;
+    const float* base = reinterpret_cast<const float*>(first ? u1 : u2);
+    const int64_t ld = first ? l1 : l2;
+    const int64_t kk = (first ? k0 : k0 - s.k1) + (tid & 7) * 4;
 #pragma unroll
-  for (int i = 0; i < ROWS / 32; ++i) {
-    const int64_t gr = row0 + (tid >> 3) + 32 * i;
-    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (gr < rows) {
-      if (kVec && kk + 3 < K && (kk + 3 < s.k1 || kk >= s.k1)) {
-        const float* p = kk < s.k1 ? s.p1 + gr * s.ld1 + kk : s.p2 + gr * s.ld2 + (kk - s.k1);
-        v = *reinterpret_cast<const float4*>(p);
-      } else {
-        float t[4];
+    for (int i = 0; i < ROWS / 32; ++i) {
+      int64_t gr = row0 + (tid >> 3) + 32 * i;
+      gr = gr < rows ? gr : rows - 1;
+      const float4 v = *reinterpret_cast<const float4*>(base + gr * ld + kk);
+      r[i] = v;
+    }
+  } else {
+    const int64_t kk = k0 + (tid & 7) * 4;
+#pragma unroll
+    for (int i = 0; i < ROWS / 32; ++i) {
+      const int64_t gr = row0 + (tid >> 3) + 32 * i;
+      float t[4] = {0.f, 0.f, 0.f, 0.f};
+      if (gr < rows) {
 #pragma unroll
         for (int c = 0; c < 4; ++c) {
           const int64_t k = kk + c;
           t[c] = k < K ? (k < s.k1 ? s.p1[gr * s.ld1 + k] : s.p2[gr * s.ld2 + (k - s.k1)]) : 0.0f;
         }
-        v = make_float4(t[0], t[1], t[2], t[3]);
       }
+      r[i] = make_float4(t[0], t[1], t[2], t[3]);
     }
-    r[i] = v;
   }
 }
 
@@ -201,7 +217,7 @@ __device__ __forceinline__ void epilogue(const f32x16 (&acc)[2][TN], float* smem
   }
 }
 
-template <int EPI, bool kVec, int TN, int WNv>
+template <int EPI, bool kClean, int TN, int WNv>
 __global__ __launch_bounds__(256, 3) void k_gemm_nt(Src2 A, Src2 B, int64_t M, int64_t N, int64_t K,
                                                     const float* __restrict__ bias, const float* __restrict__ prelu,
                                                     const float* __restrict__ accum, float* __restrict__ Z,
@@ -240,17 +256,18 @@ __global__ __launch_bounds__(256, 3) void k_gemm_nt(Src2 A, Src2 B, int64_t M, i
       for (int e = 0; e < 16; ++e) acc[a][b][e] = 0.0f;
 
   float4 ra[BM / 32], rb[BN >= 32 ? BN / 32 : 1];
-  load_tile<kVec, BM>(ra, A, m0, M, 0, K, tid);
-  load_tile<kVec, BN>(rb, B, n0, N, 0, K, tid);
+  load_tile<kClean, BM>(ra, A, m0, M, 0, K, tid);
+  load_tile<kClean, BN>(rb, B, n0, N, 0, K, tid);
   store_tile<BM>(As, ra, tid);
   store_tile<BN>(Bs, rb, tid);
   __syncthreads();
   for (int64_t k0 = 0; k0 < K; k0 += kBK) {
     const bool more = k0 + kBK < K;
     if (more) {   // next K-tile's global loads stay in flight under this K-tile's MFMAs
-      load_tile<kVec, BM>(ra, A, m0, M, k0 + kBK, K, tid);
-      load_tile<kVec, BN>(rb, B, n0, N, k0 + kBK, K, tid);
+      load_tile<kClean, BM>(ra, A, m0, M, k0 + kBK, K, tid);
+      load_tile<kClean, BN>(rb, B, n0, N, k0 + kBK, K, tid);
     }
+    __builtin_amdgcn_s_setprio(1);   // keep the MFMA cluster together (T5)
 #pragma unroll
     for (int c = 0; c < kBK / 8; ++c) {
       float4 fa[2], fb[TN];
@@ -270,6 +287,7 @@ __global__ __launch_bounds__(256, 3) void k_gemm_nt(Src2 A, Src2 B, int64_t M, i
           acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[tm].w, fb[tn].w, acc[tm][tn], 0, 0, 0);
         }
     }
+    __builtin_amdgcn_s_setprio(0);
     if (more) {
       __syncthreads();
       store_tile<BM>(As, ra, tid);
@@ -336,8 +354,8 @@ bool use_bm64(int64_t M, int64_t N) {
 template <int EPI>
 int launch_nt(const Src2& a, const Src2& b, int64_t M, int64_t N, int64_t K, const float* bias, const float* prelu,
               const float* accum, float* z, float* y, int64_t ldc, hipStream_t s, const char* what) {
-  const bool vec = aligned16(a.p1) && a.ld1 % 4 == 0 && a.k1 % 4 == 0 && (a.k1 == K || (aligned16(a.p2) &&
-                   a.ld2 % 4 == 0)) && aligned16(b.p1) && b.ld1 % 4 == 0;
+  const bool vec = K % kBK == 0 && a.k1 % kBK == 0 && aligned16(a.p1) && a.ld1 % 4 == 0 &&
+                   (a.k1 == K || (aligned16(a.p2) && a.ld2 % 4 == 0)) && aligned16(b.p1) && b.ld1 % 4 == 0;
   const bool vec_out = ldc % 4 == 0 && aligned16(y) && (z == nullptr || aligned16(z)) &&
                        (accum == nullptr || aligned16(accum));
   if (N <= 32)
@@ -377,29 +395,41 @@ struct Src2h {
   int64_t k1;
 };
 
-template <bool kVec, int ROWS>
+// bf16 twin of load_tile (8 elements = 16 B per thread and row; kClean as there, at kBKh granularity).
+template <bool kClean, int ROWS>
 __device__ __forceinline__ void load_tile_h(uint4 (&r)[ROWS / 32], const Src2h& s, int64_t row0, int64_t rows,
                                             int64_t k0, int64_t K, int tid) {
-  const int64_t kk = k0 + (tid & 7) * 8;
+  if constexpr (kClean) {
+    // select between the loaded VALUES: a select between the two struct fields' addresses would make
+    // the compiler copy the by-value kernel argument into scratch
+    const bool first = k0 < s.k1;
+    const uintptr_t u1 = reinterpret_cast<uintptr_t>(s.p1), u2 = reinterpret_cast<uintptr_t>(s.p2);
+    const int64_t l1 = s.ld1, l2 = s.ld2;
+    const uint16_t* base = reinterpret_cast<const uint16_t*>(first ? u1 : u2);
+    const int64_t ld = first ? l1 : l2;
+    const int64_t kk = (first ? k0 : k0 - s.k1) + (tid & 7) * 8;
 #pragma unroll
-  for (int i = 0; i < ROWS / 32; ++i) {
-    const int64_t gr = row0 + (tid >> 3) + 32 * i;
-    uint4 v = make_uint4(0u, 0u, 0u, 0u);
-    if (gr < rows) {
-      if (kVec && kk + 7 < K && (kk + 7 < s.k1 || kk >= s.k1)) {
-        const uint16_t* p = kk < s.k1 ? s.p1 + gr * s.ld1 + kk : s.p2 + gr * s.ld2 + (kk - s.k1);
-        v = *reinterpret_cast<const uint4*>(p);
-      } else {
-        uint32_t t[8];
+    for (int i = 0; i < ROWS / 32; ++i) {
+      int64_t gr = row0 + (tid >> 3) + 32 * i;
+      gr = gr < rows ? gr : rows - 1;
+      const uint4 v = *reinterpret_cast<const uint4*>(base + gr * ld + kk);
+      r[i] = v;
+    }
+  } else {
+    const int64_t kk = k0 + (tid & 7) * 8;
+#pragma unroll
+    for (int i = 0; i < ROWS / 32; ++i) {
+      const int64_t gr = row0 + (tid >> 3) + 32 * i;
+      uint32_t t[8] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
+      if (gr < rows) {
 #pragma unroll
         for (int c = 0; c < 8; ++c) {
           const int64_t k = kk + c;
           t[c] = k < K ? (k < s.k1 ? s.p1[gr * s.ld1 + k] : s.p2[gr * s.ld2 + (k - s.k1)]) : 0u;
         }
-        v = make_uint4(t[0] | (t[1] << 16), t[2] | (t[3] << 16), t[4] | (t[5] << 16), t[6] | (t[7] << 16));
       }
+      r[i] = make_uint4(t[0] | (t[1] << 16), t[2] | (t[3] << 16), t[4] | (t[5] << 16), t[6] | (t[7] << 16));
     }
-    r[i] = v;
   }
 }
 
@@ -410,7 +440,7 @@ __device__ __forceinline__ void store_tile_h(uint16_t* __restrict__ dst, const u
     *reinterpret_cast<uint4*>(dst + ((tid >> 3) + 32 * i) * kLdsH + (tid & 7) * 8) = r[i];
 }
 
-template <int EPI, bool kVec, int TN, int WNv, typename OutT>
+template <int EPI, bool kClean, int TN, int WNv, typename OutT>
 __global__ __launch_bounds__(256, 3) void k_gemm_nt_bf16(Src2h A, Src2h B, int64_t M, int64_t N, int64_t K,
                                                          const float* __restrict__ bias,
                                                          const float* __restrict__ prelu,
@@ -449,17 +479,18 @@ __global__ __launch_bounds__(256, 3) void k_gemm_nt_bf16(Src2h A, Src2h B, int64
       for (int e = 0; e < 16; ++e) acc[a][b][e] = 0.0f;
 
   uint4 ra[BM / 32], rb[BN >= 32 ? BN / 32 : 1];
-  load_tile_h<kVec, BM>(ra, A, m0, M, 0, K, tid);
-  load_tile_h<kVec, BN>(rb, B, n0, N, 0, K, tid);
+  load_tile_h<kClean, BM>(ra, A, m0, M, 0, K, tid);
+  load_tile_h<kClean, BN>(rb, B, n0, N, 0, K, tid);
   store_tile_h<BM>(As, ra, tid);
   store_tile_h<BN>(Bs, rb, tid);
   __syncthreads();
   for (int64_t k0 = 0; k0 < K; k0 += kBKh) {
     const bool more = k0 + kBKh < K;
     if (more) {
-      load_tile_h<kVec, BM>(ra, A, m0, M, k0 + kBKh, K, tid);
-      load_tile_h<kVec, BN>(rb, B, n0, N, k0 + kBKh, K, tid);
+      load_tile_h<kClean, BM>(ra, A, m0, M, k0 + kBKh, K, tid);
+      load_tile_h<kClean, BN>(rb, B, n0, N, k0 + kBKh, K, tid);
     }
+    __builtin_amdgcn_s_setprio(1);   // keep the MFMA cluster together (T5)
 #pragma unroll
     for (int c = 0; c < kBKh / 16; ++c) {
       bf16x8 fa[2], fb[TN];
@@ -475,6 +506,7 @@ __global__ __launch_bounds__(256, 3) void k_gemm_nt_bf16(Src2h A, Src2h B, int64
         for (int tn = 0; tn < TN; ++tn)
           acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[tm], fb[tn], acc[tm][tn], 0, 0, 0);
     }
+    __builtin_amdgcn_s_setprio(0);
     if (more) {
       __syncthreads();
       store_tile_h<BM>(As, ra, tid);
@@ -508,7 +540,7 @@ template <int EPI, typename OutT>
 int launch_nt_bf16(const Src2h& a, const Src2h& b, int64_t M, int64_t N, int64_t K, const float* bias,
                    const float* prelu, const OutT* accum, OutT* z, OutT* y, int64_t ldc, hipStream_t s,
                    const char* what) {
-  const bool vec = aligned16(a.p1) && a.ld1 % 8 == 0 && a.k1 % 8 == 0 &&
+  const bool vec = K % kBKh == 0 && a.k1 % kBKh == 0 && aligned16(a.p1) && a.ld1 % 8 == 0 &&
                    (a.k1 == K || (aligned16(a.p2) && a.ld2 % 8 == 0)) && aligned16(b.p1) && b.ld1 % 8 == 0;
   const bool vec_out = ldc % 4 == 0 && aligned16(y) && (z == nullptr || aligned16(z)) &&
                        (accum == nullptr || aligned16(accum));

@@ -128,6 +128,7 @@ __global__ __launch_bounds__(256, kOcc) void k_gemm_tn_partial(const float* __re
   for (int64_t m0 = mb; m0 < me; m0 += kTnBM) {
     const bool more = m0 + kTnBM < me;
     if (kPF && more) load_stage(m0 + kTnBM);
+    __builtin_amdgcn_s_setprio(1);   // keep the MFMA cluster together (T5)
 #pragma unroll
     for (int st = 0; st < kTnBM / 2; ++st) {
       const int row = 2 * st + lh;
@@ -143,6 +144,7 @@ __global__ __launch_bounds__(256, kOcc) void k_gemm_tn_partial(const float* __re
         for (int tn = 0; tn < 2; ++tn)
           acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[tm], fb[tn], acc[tm][tn], 0, 0, 0);
     }
+    __builtin_amdgcn_s_setprio(0);
     if (more) {
       __syncthreads();
       if (!kPF) load_stage(m0 + kTnBM);
@@ -340,6 +342,7 @@ __global__ __launch_bounds__(256, 2) void k_gemm_tn_bf16_partial(const uint16_t*
   for (int64_t m0 = mb; m0 < me; m0 += kTnBMh) {
     const bool more = m0 + kTnBMh < me;
     if (more) load_stage(m0 + kTnBMh);
+    __builtin_amdgcn_s_setprio(1);   // keep the MFMA cluster together (T5)
 #pragma unroll
     for (int st = 0; st < kTnBMh / 16; ++st) {
       bf16x8 fa[2], fb[2];
@@ -354,6 +357,7 @@ __global__ __launch_bounds__(256, 2) void k_gemm_tn_bf16_partial(const uint16_t*
         for (int tn = 0; tn < 2; ++tn)
           acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[tm], fb[tn], acc[tm][tn], 0, 0, 0);
     }
+    __builtin_amdgcn_s_setprio(0);
     if (more) {
       __syncthreads();
       store_stage();
