@@ -18,17 +18,21 @@ using f32x16 = __attribute__((ext_vector_type(16))) float;
 // The reduction runs over M (every node of a type: 1e5..1e7 rows) and the output is small (H x K), so
 // the M range is split over S workgroups per output tile (S chosen to fill the 256 CUs); each writes an
 // fp32 partial slab, and k_slab_reduce adds the slabs in split order — deterministic, no atomics.
-// Inner tile: 32 rows of M staged in LDS as [m][n] and [m][k] (row stride 132 floats); an MFMA k-step
-// takes rows 2s (lane half 0) and 2s+1 (half 1), lanes i = 0..31 read 32 consecutive floats of a row
-// (ds_read_b32, conflict-free).  The B operand is concatenated from two sources so [aggregate | x_dst]
-// needs no materialised copy.
+// Inner tile: 32 rows of M per stage.  A thread loads 4 consecutive rows x 4 columns of A (and of B):
+// read as row float4s (lanes 0-31 cover one row's 512 B, coalesced) and written transposed — the same 16
+// values regrouped as column float4s over the 4 rows, no shuffles — into [n][m] / [k][m] LDS images with
+// 36-float rows.  Lane half h owns rows m = 16h .. 16h+15 of the stage, so an MFMA k-step st pairs rows st
+// and 16 + st and a lane reads 4 k-steps of its operand with one ds_read_b128 (conflict-free: the 16 lanes
+// of a b128 group read 16 rows 144 B apart).  The B operand is concatenated from two sources so
+// [aggregate | x_dst] needs no materialised copy.
 constexpr int kTnBM = 32;       // rows of M per stage
-constexpr int kTnLd = 128 + 4;
+constexpr int kTnLd = kTnBM + 4;   // [col][m] image row stride (floats)
 
 // 1-D grid over (output tile, split) pairs, tiles of one split consecutive in the logical order, which is
 // XCD-contiguous (hgin_common.h): the workgroups reading the same rows of A / B share one XCD's L2.
 struct TnGrid {
-  int64_t tiles_n;   // 128-wide tiles along N
+  int64_t tile_n;    // output-tile rows along N (128, or 32 for N <= 32)
+  int64_t tiles_n;   // tiles along N
   int64_t tiles;     // tiles_n * tiles along K
   int64_t n_work;    // tiles * splits
   int xcd;
@@ -43,24 +47,30 @@ __device__ __forceinline__ TnWork tn_work(const TnGrid& g) {
   w.valid = q < g.n_work;
   const int64_t t = q % g.tiles;
   w.split = q / g.tiles;
-  w.n0 = (t % g.tiles_n) * 128;
+  w.n0 = (t % g.tiles_n) * g.tile_n;
   w.k0 = (t / g.tiles_n) * 128;
   return w;
 }
 
-template <bool kPF, int kOcc>
-__global__ __launch_bounds__(256, kOcc) void k_gemm_tn_partial(const float* __restrict__ A, int64_t lda,
+// TNR = output-tile rows along N: 128 (2 x 2 waves of 64 x 64) or 32 for narrow gradients such as the
+// readout's Linear(128, 32) (4 waves of 32 x 32 along K: no MFMA work on rows that do not exist; wave 0
+// alone stages the 32-column A block).
+template <bool kClean, int TNR>
+__global__ __launch_bounds__(256, 3) void k_gemm_tn_partial(const float* __restrict__ A, int64_t lda,
                                                             const float* __restrict__ B1, int64_t ldb1,
                                                             const float* __restrict__ B2, int64_t ldb2, int64_t K1,
                                                             int64_t M, int64_t N, int64_t K, int64_t rows_per_split,
                                                             bool vec, float* __restrict__ slab, TnGrid grid) {
-  __shared__ __attribute__((aligned(16))) float smem[2 * kTnBM * kTnLd];
-  float* As = smem;
-  float* Bs = smem + kTnBM * kTnLd;
+  constexpr int WGN = TNR == 128 ? 2 : 4;        // waves along K
+  constexpr int BMN = TNR == 128 ? 2 : 1;        // 32 x 32 MFMA blocks per wave along N
+  constexpr int BMK = TNR == 128 ? 2 : 1;        // ... and along K
+  __shared__ __attribute__((aligned(16))) float smem[(TNR + 128) * kTnLd];
+  float* At = smem;                  // [n][m]
+  float* Bt = smem + TNR * kTnLd;    // [k][m]
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = tid >> 6;
-  const int wm = wave >> 1, wn = wave & 1;
+  const int wm = wave / WGN, wn = wave % WGN;
   const int li = lane & 31, lh = lane >> 5;
   const TnWork work = tn_work(grid);
   if (!work.valid) return;
@@ -69,57 +79,101 @@ __global__ __launch_bounds__(256, kOcc) void k_gemm_tn_partial(const float* __re
   const int64_t mb = work.split * rows_per_split;
   const int64_t me = mb + rows_per_split < M ? mb + rows_per_split : M;
 
-  f32x16 acc[2][2];
+  f32x16 acc[BMN][BMK];
 #pragma unroll
-  for (int a = 0; a < 2; ++a)
+  for (int a = 0; a < BMN; ++a)
 #pragma unroll
-    for (int b = 0; b < 2; ++b)
+    for (int b = 0; b < BMK; ++b)
 #pragma unroll
       for (int e = 0; e < 16; ++e) acc[a][b][e] = 0.0f;
 
-  const int c4 = (tid & 31) * 4;   // column (x4) inside the 128-wide tile
+  const int c4 = (tid & 31) * 4;   // B: 4 columns inside the 128-wide tile
+  const int r4 = (tid >> 5) * 4;   // B: 4 rows inside the 32-row stage
+  // A: the same 4 x 4 blocks over TNR columns (TNR = 32: threads 0-63 only)
+  const int c4a = TNR == 128 ? c4 : (tid & 7) * 4;
+  const int r4a = TNR == 128 ? r4 : (tid >> 3) * 4;
+  const bool stage_a = TNR == 128 || tid < 64;   // wave-uniform
   float4 va[4], vb[4];
-  // one 32-row stage of A[:, n0:n0+128] and [B1|B2][:, k0:k0+128] into registers (4 + 4 float4 per thread)
+  // kClean (16-B rows; N, K and K1 multiples of 128, so every A tile lies inside N and every B tile wholly
+  // inside B1 or B2): the source pointers are fixed per workgroup and a stage is loaded without per-load
+  // branches (the selection below is between loaded values; a select between the two kernel arguments'
+  // addresses would put them in scratch).  A ragged last stage (the final split at M) loads clamped rows
+  // and zeroes them.  Otherwise every element is bounds-checked.
+  const bool from1 = k0 < K1;
+  const uintptr_t ub = from1 ? reinterpret_cast<uintptr_t>(B1 + k0) : reinterpret_cast<uintptr_t>(B2 + (k0 - K1));
+  const float* pb0 = reinterpret_cast<const float*>(ub);
+  const int64_t ldb = from1 ? ldb1 : ldb2;
+  const float* pa0 = A + n0;
+  const uint32_t oa = (uint32_t)(r4a * lda + c4a), ob = (uint32_t)(r4 * ldb + c4);
   auto load_stage = [&](int64_t m0) {
+    if constexpr (kClean) {
+      if (m0 + kTnBM <= me) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int64_t gm = m0 + (tid >> 5) + 8 * i;
-      va[i] = make_float4(0.f, 0.f, 0.f, 0.f);
-      vb[i] = va[i];
-      if (gm < me) {
-        const int64_t gn = n0 + c4;
-        const float* pa = A + gm * lda + gn;
-        if (vec && gn + 3 < N) {
-          va[i] = *reinterpret_cast<const float4*>(pa);
-        } else {
-          if (gn + 0 < N) va[i].x = pa[0];
-          if (gn + 1 < N) va[i].y = pa[1];
-          if (gn + 2 < N) va[i].z = pa[2];
-          if (gn + 3 < N) va[i].w = pa[3];
-        }
-        const int64_t gk = k0 + c4;
-        if (vec && gk + 3 < K && (gk + 3 < K1 || gk >= K1)) {
-          const float* pb = gk < K1 ? B1 + gm * ldb1 + gk : B2 + gm * ldb2 + (gk - K1);
-          vb[i] = *reinterpret_cast<const float4*>(pb);
-        } else {
-          float t[4];
-#pragma unroll
-          for (int c = 0; c < 4; ++c) {
-            const int64_t k = gk + c;
-            t[c] = k < K ? (k < K1 ? B1[gm * ldb1 + k] : B2[gm * ldb2 + (k - K1)]) : 0.0f;
+        for (int j = 0; j < 4; ++j) {
+          if (stage_a) {
+            const float4 a = *reinterpret_cast<const float4*>(pa0 + (m0 + j) * lda + oa);
+            va[j] = a;
           }
-          vb[i] = make_float4(t[0], t[1], t[2], t[3]);
+          const float4 b = *reinterpret_cast<const float4*>(pb0 + (m0 + j) * ldb + ob);
+          vb[j] = b;
         }
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          if (stage_a) {
+            const int64_t gm = m0 + r4a + j;
+            const bool ok = gm < me;
+            const float4 a = *reinterpret_cast<const float4*>(pa0 + (ok ? gm : me - 1) * lda + c4a);
+            va[j] = make_float4(ok ? a.x : 0.f, ok ? a.y : 0.f, ok ? a.z : 0.f, ok ? a.w : 0.f);
+          }
+          const int64_t gm = m0 + r4 + j;
+          const bool ok = gm < me;
+          const float4 b = *reinterpret_cast<const float4*>(pb0 + (ok ? gm : me - 1) * ldb + c4);
+          vb[j] = make_float4(ok ? b.x : 0.f, ok ? b.y : 0.f, ok ? b.z : 0.f, ok ? b.w : 0.f);
+        }
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        if (stage_a) {
+          const int64_t gm = m0 + r4a + j;
+          float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+          const int64_t gn = n0 + c4a;
+          if (gm < me) {
+            const float* pa = A + gm * lda + gn;
+            if (gn + 0 < N) a0 = pa[0];
+            if (gn + 1 < N) a1 = pa[1];
+            if (gn + 2 < N) a2 = pa[2];
+            if (gn + 3 < N) a3 = pa[3];
+          }
+          va[j] = make_float4(a0, a1, a2, a3);
+        }
+        const int64_t gm = m0 + r4 + j;
+        float b0 = 0.f, b1 = 0.f, b2 = 0.f, b3 = 0.f;
+        if (gm < me) {
+          const int64_t gk = k0 + c4;
+          auto bk = [&](int64_t k) { return k < K ? (k < K1 ? B1[gm * ldb1 + k] : B2[gm * ldb2 + (k - K1)]) : 0.0f; };
+          b0 = bk(gk);
+          b1 = bk(gk + 1);
+          b2 = bk(gk + 2);
+          b3 = bk(gk + 3);
+        }
+        vb[j] = make_float4(b0, b1, b2, b3);
       }
     }
   };
+  // the 4 x 4 block regrouped: column c4 + t gets (row r4 .. r4 + 3) as one float4
   auto store_stage = [&]() {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int r = (tid >> 5) + 8 * i;
-      *reinterpret_cast<float4*>(As + r * kTnLd + c4) = va[i];
-      *reinterpret_cast<float4*>(Bs + r * kTnLd + c4) = vb[i];
+    if (stage_a) {
+      *reinterpret_cast<float4*>(At + (c4a + 0) * kTnLd + r4a) = make_float4(va[0].x, va[1].x, va[2].x, va[3].x);
+      *reinterpret_cast<float4*>(At + (c4a + 1) * kTnLd + r4a) = make_float4(va[0].y, va[1].y, va[2].y, va[3].y);
+      *reinterpret_cast<float4*>(At + (c4a + 2) * kTnLd + r4a) = make_float4(va[0].z, va[1].z, va[2].z, va[3].z);
+      *reinterpret_cast<float4*>(At + (c4a + 3) * kTnLd + r4a) = make_float4(va[0].w, va[1].w, va[2].w, va[3].w);
     }
+    *reinterpret_cast<float4*>(Bt + (c4 + 0) * kTnLd + r4) = make_float4(vb[0].x, vb[1].x, vb[2].x, vb[3].x);
+    *reinterpret_cast<float4*>(Bt + (c4 + 1) * kTnLd + r4) = make_float4(vb[0].y, vb[1].y, vb[2].y, vb[3].y);
+    *reinterpret_cast<float4*>(Bt + (c4 + 2) * kTnLd + r4) = make_float4(vb[0].z, vb[1].z, vb[2].z, vb[3].z);
+    *reinterpret_cast<float4*>(Bt + (c4 + 3) * kTnLd + r4) = make_float4(vb[0].w, vb[1].w, vb[2].w, vb[3].w);
   };
   // Register-prefetch pipeline (as in hgin_gemm_nt.hip): stage s+1 is loaded under stage s's MFMAs.
   load_stage(mb);
@@ -127,41 +181,44 @@ __global__ __launch_bounds__(256, kOcc) void k_gemm_tn_partial(const float* __re
   __syncthreads();
   for (int64_t m0 = mb; m0 < me; m0 += kTnBM) {
     const bool more = m0 + kTnBM < me;
-    if (kPF && more) load_stage(m0 + kTnBM);
+    if (more) load_stage(m0 + kTnBM);
     __builtin_amdgcn_s_setprio(1);   // keep the MFMA cluster together (T5)
 #pragma unroll
-    for (int st = 0; st < kTnBM / 2; ++st) {
-      const int row = 2 * st + lh;
-      float fa[2], fb[2];
+    for (int q = 0; q < 4; ++q) {
+      float4 fa[BMN], fb[BMK];
 #pragma unroll
-      for (int t = 0; t < 2; ++t) {
-        fa[t] = As[row * kTnLd + wm * 64 + t * 32 + li];
-        fb[t] = Bs[row * kTnLd + wn * 64 + t * 32 + li];
-      }
+      for (int t = 0; t < BMN; ++t)
+        fa[t] = *reinterpret_cast<const float4*>(At + (wm * 32 * BMN + t * 32 + li) * kTnLd + lh * 16 + 4 * q);
 #pragma unroll
-      for (int tm = 0; tm < 2; ++tm)
+      for (int t = 0; t < BMK; ++t)
+        fb[t] = *reinterpret_cast<const float4*>(Bt + (wn * 32 * BMK + t * 32 + li) * kTnLd + lh * 16 + 4 * q);
 #pragma unroll
-        for (int tn = 0; tn < 2; ++tn)
-          acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[tm], fb[tn], acc[tm][tn], 0, 0, 0);
+      for (int tm = 0; tm < BMN; ++tm)
+#pragma unroll
+        for (int tn = 0; tn < BMK; ++tn) {
+          acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[tm].x, fb[tn].x, acc[tm][tn], 0, 0, 0);
+          acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[tm].y, fb[tn].y, acc[tm][tn], 0, 0, 0);
+          acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[tm].z, fb[tn].z, acc[tm][tn], 0, 0, 0);
+          acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[tm].w, fb[tn].w, acc[tm][tn], 0, 0, 0);
+        }
     }
     __builtin_amdgcn_s_setprio(0);
     if (more) {
       __syncthreads();
-      if (!kPF) load_stage(m0 + kTnBM);
       store_stage();
       __syncthreads();
     }
   }
   float* out = slab + work.split * N * K;
 #pragma unroll
-  for (int tm = 0; tm < 2; ++tm)
+  for (int tm = 0; tm < BMN; ++tm)
 #pragma unroll
-    for (int tn = 0; tn < 2; ++tn) {
-      const int64_t k = k0 + wn * 64 + tn * 32 + li;
+    for (int tn = 0; tn < BMK; ++tn) {
+      const int64_t k = k0 + wn * 32 * BMK + tn * 32 + li;
       if (k >= K) continue;
 #pragma unroll
       for (int e = 0; e < 16; ++e) {
-        const int64_t n = n0 + wm * 64 + tm * 32 + (e & 3) + 8 * (e >> 2) + 4 * lh;
+        const int64_t n = n0 + wm * 32 * BMN + tm * 32 + (e & 3) + 8 * (e >> 2) + 4 * lh;
         if (n < N) out[n * K + k] = acc[tm][tn][e];
       }
     }
@@ -455,21 +512,22 @@ extern "C" int hgin_gemm_tn_f32(const float* a, int64_t lda, const float* b1, in
   if (tn_is_small(N, K)) {
     k_tn_small<float><<<(unsigned)S_eff, 256, 0, s>>>(a, lda, b1, ldb1, b2, ldb2, k1, M, (int)N, (int)K, rows, slab);
   } else {
-    const int64_t tiles_n = ceil_div(N, 128);
-    const TnGrid tg{tiles_n, tiles_n * ceil_div(K, 128), tiles_n * ceil_div(K, 128) * S_eff, xcd_remap_enabled()};
+    const int64_t tile_n = N <= 32 ? 32 : 128;
+    const int64_t tiles_n = ceil_div(N, tile_n);
+    const TnGrid tg{tile_n, tiles_n, tiles_n * ceil_div(K, 128), tiles_n * ceil_div(K, 128) * S_eff,
+                    xcd_remap_enabled()};
     dim3 grid((unsigned)(tg.xcd ? round_up8(tg.n_work) : tg.n_work));
-    static const int variant = [] {
-      const char* v = getenv("HGIN_TN_VARIANT");
-      return v ? atoi(v) : 0;
-    }();
-    // Measured (profiles/r01_tn_variants.txt): register prefetch at 3 waves/SIMD is 12 % faster than the
-    // unpipelined loop and 3-5 % faster than prefetch at 2 waves.
-    if (variant == 1)
-      k_gemm_tn_partial<false, 2><<<grid, 256, 0, s>>>(a, lda, b1, ldb1, b2, ldb2, k1, M, N, K, rows, vec, slab, tg);
-    else if (variant == 2)
-      k_gemm_tn_partial<true, 2><<<grid, 256, 0, s>>>(a, lda, b1, ldb1, b2, ldb2, k1, M, N, K, rows, vec, slab, tg);
-    else
-      k_gemm_tn_partial<true, 3><<<grid, 256, 0, s>>>(a, lda, b1, ldb1, b2, ldb2, k1, M, N, K, rows, vec, slab, tg);
+    // register prefetch at 3 waves/SIMD (profiles/r01_tn_variants.txt: 12 % faster than the unpipelined
+    // loop, 3-5 % faster than prefetch at 2 waves)
+    const bool clean = vec && N % tile_n == 0 && K % 128 == 0 && k1 % 128 == 0;
+#define HGIN_TN_LAUNCH(CLEAN, TNR) \
+  k_gemm_tn_partial<CLEAN, TNR><<<grid, 256, 0, s>>>(a, lda, b1, ldb1, b2, ldb2, k1, M, N, K, rows, vec, slab, tg)
+    if (tile_n == 32) {
+      if (clean) HGIN_TN_LAUNCH(true, 32); else HGIN_TN_LAUNCH(false, 32);
+    } else {
+      if (clean) HGIN_TN_LAUNCH(true, 128); else HGIN_TN_LAUNCH(false, 128);
+    }
+#undef HGIN_TN_LAUNCH
   }
   const int64_t G = ceil_div(S_eff, kSlabGroup);
   dim3 g1((unsigned)ceil_div(ceil_div(NK, 4), 256), (unsigned)G);
@@ -517,7 +575,8 @@ extern "C" int hgin_gemm_tn_bf16(const uint16_t* a, int64_t lda, const uint16_t*
                                                           slab);
   } else {
     const int64_t tiles_n = ceil_div(N, 128);
-    const TnGrid tg{tiles_n, tiles_n * ceil_div(K, 128), tiles_n * ceil_div(K, 128) * S_eff, xcd_remap_enabled()};
+    const TnGrid tg{128, tiles_n, tiles_n * ceil_div(K, 128), tiles_n * ceil_div(K, 128) * S_eff,
+                    xcd_remap_enabled()};
     dim3 grid((unsigned)(tg.xcd ? round_up8(tg.n_work) : tg.n_work));
     if (vec)
       k_gemm_tn_bf16_partial<true><<<grid, 256, 0, s>>>(a, lda, b1, ldb1, b2, ldb2, k1, M, N, K, rows, slab, tg);

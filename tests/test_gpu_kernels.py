@@ -164,7 +164,8 @@ def test_gemm_layout_identity_asymmetric():
 
 
 @pytest.mark.parametrize("M,N,K1,K2", [(1, 1, 1, 0), (1000, 128, 256, 0), (600, 128, 128, 128), (777, 100, 6, 3),
-                                       (50000, 128, 256, 0), (33, 256, 64, 40), (0, 8, 4, 0)])
+                                       (50000, 128, 256, 0), (33, 256, 64, 40), (0, 8, 4, 0),
+                                       (20011, 32, 128, 0), (5000, 32, 128, 128), (3001, 17, 64, 64)])
 def test_gemm_tn(M, N, K1, K2):
     a = torch.randn(M, N, device=DEV)
     b1 = torch.randn(M, K1, device=DEV)
