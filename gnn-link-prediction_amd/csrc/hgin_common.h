@@ -67,6 +67,36 @@ __device__ __forceinline__ uint32_t f2bf(float f) {
 }
 __device__ __forceinline__ uint32_t pack_bf2(float lo, float hi) { return f2bf(lo) | (f2bf(hi) << 16); }
 
+// fp32 GEMMs on the bf16 matrix cores ("split" mode of hgin_gemm_nt / hgin_gemm_tn): each fp32 operand
+// a = a1 + a2 + a3 with a1 = bf16(a), a2 = bf16(a - a1), a3 = bf16(a - a1 - a2) (RNE; every residual is
+// exact in fp32, so a1 + a2 + a3 carries a's full 24-bit significand), and a product ab is formed from the
+// six bf16 MFMA terms a1b1, a1b2, a2b1, a1b3, a2b2, a3b1 with fp32 accumulation; the dropped terms are
+// below 2^-25 |ab|.  Measured error against fp64 is at or below the exact f32-MFMA kernel's
+// (tools/gemm_diag.hip: max 6.0e-7 vs 7.3e-7 of sum |ab| at K = 256) at 16x the matrix rate per term.
+// Out-of-range edge: |a| above the largest bf16 (3.39e38) rounds a1 to inf.
+// split4: 4 fp32 -> 3 planes of 4 packed bf16.
+__device__ __forceinline__ void split4(const float4 v, uint2 (&o)[3]) {
+  const float x[4] = {v.x, v.y, v.z, v.w};
+  uint32_t h[3][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const __bf16 b1 = (__bf16)x[i];
+    const float r1 = x[i] - (float)b1;
+    const __bf16 b2 = (__bf16)r1;
+    const float r2 = r1 - (float)b2;
+    const __bf16 b3 = (__bf16)r2;
+    h[0][i] = __builtin_bit_cast(uint16_t, b1);
+    h[1][i] = __builtin_bit_cast(uint16_t, b2);
+    h[2][i] = __builtin_bit_cast(uint16_t, b3);
+  }
+#pragma unroll
+  for (int p = 0; p < 3; ++p) o[p] = make_uint2(h[p][0] | (h[p][1] << 16), h[p][2] | (h[p][3] << 16));
+}
+// LDS row of a split operand: 3 planes x 32 bf16 (one 32-deep K-tile) + 16 B pad = 208 B = 13 x 16 B, so the
+// 16 rows of a ds_read_b128 lane group fall on 16 distinct 16-B bank slots (13 is odd).
+constexpr int kSplitRowWords = 52;
+bool gemm_split_enabled();   // HGIN_F32_GEMM=mfma32 selects the exact f32-MFMA kernels; default split
+
 // Element-type traits shared by the fp32 and bf16 instantiations of the memory-bound kernels.
 template <typename T>
 struct Elem;

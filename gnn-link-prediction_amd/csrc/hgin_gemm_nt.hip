@@ -93,6 +93,19 @@ __device__ __forceinline__ void store_tile(float* __restrict__ dst, const float4
     *reinterpret_cast<float4*>(dst + ((tid >> 3) + 32 * i) * kLds + (tid & 7) * 4) = r[i];
 }
 
+// Split mode (hgin_common.h): the same tile written as three bf16 planes per row.
+template <int ROWS>
+__device__ __forceinline__ void store_tile_split(uint32_t* __restrict__ dst, const float4 (&r)[ROWS / 32], int tid) {
+#pragma unroll
+  for (int i = 0; i < ROWS / 32; ++i) {
+    uint2 o[3];
+    split4(r[i], o);
+    uint32_t* row = dst + ((tid >> 3) + 32 * i) * kSplitRowWords + (tid & 7) * 2;
+#pragma unroll
+    for (int p = 0; p < 3; ++p) *reinterpret_cast<uint2*>(row + p * 16) = o[p];
+  }
+}
+
 // 4 consecutive output columns of one row: fp32 (16-B) or bf16 (8-B) accesses, scalar at the ragged edge.
 template <typename OutT>
 struct Out4;
@@ -217,7 +230,9 @@ __device__ __forceinline__ void epilogue(const f32x16 (&acc)[2][TN], float* smem
   }
 }
 
-template <int EPI, bool kClean, int TN, int WNv>
+using bf16x8 = __attribute__((ext_vector_type(8))) __bf16;
+
+template <int EPI, bool kClean, int TN, int WNv, bool kSplit>
 __global__ __launch_bounds__(256, 3) void k_gemm_nt(Src2 A, Src2 B, int64_t M, int64_t N, int64_t K,
                                                     const float* __restrict__ bias, const float* __restrict__ prelu,
                                                     const float* __restrict__ accum, float* __restrict__ Z,
@@ -228,9 +243,12 @@ __global__ __launch_bounds__(256, 3) void k_gemm_nt(Src2 A, Src2 B, int64_t M, i
   constexpr int BM = WM * 64;             // rows per workgroup tile
   constexpr int BN = WN * TN * 32;        // columns per workgroup tile
   constexpr int WCOLS = TN * 32;          // columns per wave
-  __shared__ __attribute__((aligned(16))) float smem[(BM + BN) * kLds];
+  constexpr int kRowW = kSplit ? kSplitRowWords : kLds;   // 4-B words per LDS row
+  __shared__ __attribute__((aligned(16))) float smem[(BM + BN) * kRowW];
   float* As = smem;
-  float* Bs = smem + BM * kLds;
+  float* Bs = smem + BM * kRowW;
+  uint32_t* Ash = reinterpret_cast<uint32_t*>(As);
+  uint32_t* Bsh = reinterpret_cast<uint32_t*>(Bs);
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = tid >> 6;
@@ -256,10 +274,18 @@ __global__ __launch_bounds__(256, 3) void k_gemm_nt(Src2 A, Src2 B, int64_t M, i
       for (int e = 0; e < 16; ++e) acc[a][b][e] = 0.0f;
 
   float4 ra[BM / 32], rb[BN >= 32 ? BN / 32 : 1];
+  auto stage = [&]() {
+    if constexpr (kSplit) {
+      store_tile_split<BM>(Ash, ra, tid);
+      store_tile_split<BN>(Bsh, rb, tid);
+    } else {
+      store_tile<BM>(As, ra, tid);
+      store_tile<BN>(Bs, rb, tid);
+    }
+  };
   load_tile<kClean, BM>(ra, A, m0, M, 0, K, tid);
   load_tile<kClean, BN>(rb, B, n0, N, 0, K, tid);
-  store_tile<BM>(As, ra, tid);
-  store_tile<BN>(Bs, rb, tid);
+  stage();
   __syncthreads();
   for (int64_t k0 = 0; k0 < K; k0 += kBK) {
     const bool more = k0 + kBK < K;
@@ -268,30 +294,60 @@ __global__ __launch_bounds__(256, 3) void k_gemm_nt(Src2 A, Src2 B, int64_t M, i
       load_tile<kClean, BN>(rb, B, n0, N, k0 + kBK, K, tid);
     }
     __builtin_amdgcn_s_setprio(1);   // keep the MFMA cluster together (T5)
+    if constexpr (kSplit) {
+      // two 16-deep k-blocks; lane (i, h) reads k = 16 kb + 8 h .. +7 of each plane (one ds_read_b128)
 #pragma unroll
-    for (int c = 0; c < kBK / 8; ++c) {
-      float4 fa[2], fb[TN];
+      for (int kb = 0; kb < 2; ++kb) {
+        bf16x8 fa[2][3], fb[TN][3];
 #pragma unroll
-      for (int t = 0; t < 2; ++t)
-        fa[t] = *reinterpret_cast<const float4*>(As + (wm * 64 + t * 32 + li) * kLds + c * 8 + lh * 4);
+        for (int t = 0; t < 2; ++t)
 #pragma unroll
-      for (int t = 0; t < TN; ++t)
-        fb[t] = *reinterpret_cast<const float4*>(Bs + (wn * WCOLS + t * 32 + li) * kLds + c * 8 + lh * 4);
+          for (int p = 0; p < 3; ++p)
+            fa[t][p] = *reinterpret_cast<const bf16x8*>(Ash + (wm * 64 + t * 32 + li) * kSplitRowWords + p * 16 +
+                                                        kb * 8 + lh * 4);
 #pragma unroll
-      for (int tm = 0; tm < 2; ++tm)
+        for (int t = 0; t < TN; ++t)
 #pragma unroll
-        for (int tn = 0; tn < TN; ++tn) {
-          acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[tm].x, fb[tn].x, acc[tm][tn], 0, 0, 0);
-          acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[tm].y, fb[tn].y, acc[tm][tn], 0, 0, 0);
-          acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[tm].z, fb[tn].z, acc[tm][tn], 0, 0, 0);
-          acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[tm].w, fb[tn].w, acc[tm][tn], 0, 0, 0);
-        }
+          for (int p = 0; p < 3; ++p)
+            fb[t][p] = *reinterpret_cast<const bf16x8*>(Bsh + (wn * WCOLS + t * 32 + li) * kSplitRowWords + p * 16 +
+                                                        kb * 8 + lh * 4);
+#pragma unroll
+        for (int tm = 0; tm < 2; ++tm)
+#pragma unroll
+          for (int tn = 0; tn < TN; ++tn) {   // smallest terms first
+            acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[tm][2], fb[tn][0], acc[tm][tn], 0, 0, 0);
+            acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[tm][1], fb[tn][1], acc[tm][tn], 0, 0, 0);
+            acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[tm][0], fb[tn][2], acc[tm][tn], 0, 0, 0);
+            acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[tm][1], fb[tn][0], acc[tm][tn], 0, 0, 0);
+            acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[tm][0], fb[tn][1], acc[tm][tn], 0, 0, 0);
+            acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[tm][0], fb[tn][0], acc[tm][tn], 0, 0, 0);
+          }
+      }
+    } else {
+#pragma unroll
+      for (int c = 0; c < kBK / 8; ++c) {
+        float4 fa[2], fb[TN];
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+          fa[t] = *reinterpret_cast<const float4*>(As + (wm * 64 + t * 32 + li) * kLds + c * 8 + lh * 4);
+#pragma unroll
+        for (int t = 0; t < TN; ++t)
+          fb[t] = *reinterpret_cast<const float4*>(Bs + (wn * WCOLS + t * 32 + li) * kLds + c * 8 + lh * 4);
+#pragma unroll
+        for (int tm = 0; tm < 2; ++tm)
+#pragma unroll
+          for (int tn = 0; tn < TN; ++tn) {
+            acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[tm].x, fb[tn].x, acc[tm][tn], 0, 0, 0);
+            acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[tm].y, fb[tn].y, acc[tm][tn], 0, 0, 0);
+            acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[tm].z, fb[tn].z, acc[tm][tn], 0, 0, 0);
+            acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[tm].w, fb[tn].w, acc[tm][tn], 0, 0, 0);
+          }
+      }
     }
     __builtin_amdgcn_s_setprio(0);
     if (more) {
       __syncthreads();
-      store_tile<BM>(As, ra, tid);
-      store_tile<BN>(Bs, rb, tid);
+      stage();
       __syncthreads();
     }
   }
@@ -309,12 +365,15 @@ void launch_nt_tn(bool vec, const Src2& a, const Src2& b, int64_t M, int64_t N, 
   const int64_t tiles = ceil_div(N, BN) * ceil_div(M, BM);
   const bool xcd = xcd_remap_enabled();
   dim3 grid((unsigned)(xcd ? round_up8(tiles) : tiles));
-  if (vec)
-    k_gemm_nt<EPI, true, TN, WN><<<grid, 256, 0, s>>>(a, b, M, N, K, bias, prelu, accum, z, y, ldc, vec_out, tiles,
-                                                      xcd);
-  else
-    k_gemm_nt<EPI, false, TN, WN><<<grid, 256, 0, s>>>(a, b, M, N, K, bias, prelu, accum, z, y, ldc, vec_out, tiles,
-                                                       xcd);
+#define HGIN_NT_F32(CLEAN, SPLIT)                                                                           \
+  k_gemm_nt<EPI, CLEAN, TN, WN, SPLIT><<<grid, 256, 0, s>>>(a, b, M, N, K, bias, prelu, accum, z, y, ldc, vec_out, \
+                                                            tiles, xcd)
+  if (gemm_split_enabled()) {
+    if (vec) HGIN_NT_F32(true, true); else HGIN_NT_F32(false, true);
+  } else {
+    if (vec) HGIN_NT_F32(true, false); else HGIN_NT_F32(false, false);
+  }
+#undef HGIN_NT_F32
 }
 
 // Resident workgroups of a kernel across the device (occupancy x CUs), queried once per kernel.
@@ -342,8 +401,10 @@ bool use_bm64(int64_t M, int64_t N) {
   }();
   if (env == 64) return true;
   if (env == 128) return false;
-  static const int64_t slots128 = resident_slots(k_gemm_nt<EPI, true, 2, 2>);
-  static const int64_t slots64 = resident_slots(k_gemm_nt<EPI, true, 1, 4>);
+  static const int64_t slots128 = gemm_split_enabled() ? resident_slots(k_gemm_nt<EPI, true, 2, 2, true>)
+                                                       : resident_slots(k_gemm_nt<EPI, true, 2, 2, false>);
+  static const int64_t slots64 = gemm_split_enabled() ? resident_slots(k_gemm_nt<EPI, true, 1, 4, true>)
+                                                      : resident_slots(k_gemm_nt<EPI, true, 1, 4, false>);
   constexpr double kRel64 = 0.8;
   const int64_t nt = ceil_div(N, 128);
   const double t128 = (double)ceil_div(nt * ceil_div(M, 128), slots128);
@@ -383,7 +444,6 @@ int check_a(const char* what, const float* a1, int64_t lda1, int64_t k1, const f
 // At the GIN shapes (K = 128..512, N = 128..256) these GEMMs are HBM-bound (A read once, Y/Z written
 // once: ~43 flop/B at K = 256, N = 128, far below the bf16 MFMA ridge), so the tile keeps the whole of N
 // per workgroup where it can and the epilogue writes 8-B bf16 quads.
-using bf16x8 = __attribute__((ext_vector_type(8))) __bf16;
 constexpr int kBKh = 64;
 constexpr int kLdsH = kBKh + 8;
 

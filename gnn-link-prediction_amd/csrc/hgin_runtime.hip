@@ -24,6 +24,14 @@ bool xcd_remap_enabled() {
   return on;
 }
 
+bool gemm_split_enabled() {
+  static const bool on = [] {
+    const char* v = getenv("HGIN_F32_GEMM");
+    return !(v && std::string(v) == "mfma32");
+  }();
+  return on;
+}
+
 }  // namespace hgin
 
 extern "C" int hgin_abi_version(void) { return HGIN_ABI_VERSION; }
