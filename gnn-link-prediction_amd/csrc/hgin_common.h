@@ -75,22 +75,23 @@ __device__ __forceinline__ uint32_t pack_bf2(float lo, float hi) { return f2bf(l
 // (tools/gemm_diag.hip: max 6.0e-7 vs 7.3e-7 of sum |ab| at K = 256) at 16x the matrix rate per term.
 // Out-of-range edge: |a| above the largest bf16 (3.39e38) rounds a1 to inf.
 // split4: 4 fp32 -> 3 planes of 4 packed bf16.
+// Pairs go through one v_cvt_pk_bf16_f32 per plane (the packed pair IS the plane's dword) and are widened
+// back with a shift / mask: 5.5 VALU ops per element.
+using f32x2_t = __attribute__((ext_vector_type(2))) float;
+using bf16x2_t = __attribute__((ext_vector_type(2))) __bf16;
+__device__ __forceinline__ uint32_t cvt_pk_bf16(float lo, float hi) {
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2_t{lo, hi}, bf16x2_t));
+}
+__device__ __forceinline__ void split2(float x0, float x1, uint32_t& p1, uint32_t& p2, uint32_t& p3) {
+  p1 = cvt_pk_bf16(x0, x1);
+  const float r0 = x0 - bf_lo(p1), r1 = x1 - bf_hi(p1);
+  p2 = cvt_pk_bf16(r0, r1);
+  const float s0 = r0 - bf_lo(p2), s1 = r1 - bf_hi(p2);
+  p3 = cvt_pk_bf16(s0, s1);
+}
 __device__ __forceinline__ void split4(const float4 v, uint2 (&o)[3]) {
-  const float x[4] = {v.x, v.y, v.z, v.w};
-  uint32_t h[3][4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const __bf16 b1 = (__bf16)x[i];
-    const float r1 = x[i] - (float)b1;
-    const __bf16 b2 = (__bf16)r1;
-    const float r2 = r1 - (float)b2;
-    const __bf16 b3 = (__bf16)r2;
-    h[0][i] = __builtin_bit_cast(uint16_t, b1);
-    h[1][i] = __builtin_bit_cast(uint16_t, b2);
-    h[2][i] = __builtin_bit_cast(uint16_t, b3);
-  }
-#pragma unroll
-  for (int p = 0; p < 3; ++p) o[p] = make_uint2(h[p][0] | (h[p][1] << 16), h[p][2] | (h[p][3] << 16));
+  split2(v.x, v.y, o[0].x, o[1].x, o[2].x);
+  split2(v.z, v.w, o[0].y, o[1].y, o[2].y);
 }
 // LDS row of a split operand: 3 planes x 32 bf16 (one 32-deep K-tile) + 16 B pad = 208 B = 13 x 16 B, so the
 // 16 rows of a ds_read_b128 lane group fall on 16 distinct 16-B bank slots (13 is odd).

@@ -55,7 +55,12 @@ __device__ __forceinline__ TnWork tn_work(const TnGrid& g) {
 // TNR = output-tile rows along N: 128 (2 x 2 waves of 64 x 64) or 32 for narrow gradients such as the
 // readout's Linear(128, 32) (4 waves of 32 x 32 along K: no MFMA work on rows that do not exist; wave 0
 // alone stages the 32-column A block).
-template <bool kClean, int TNR>
+using bf16x8 = __attribute__((ext_vector_type(8))) __bf16;
+
+// kSplit: fp32 operands on the bf16 matrix cores (hgin_common.h split4): the transposed column runs of 4 m
+// are written as three bf16 planes ([col][3 x 32 m + pad] rows of kSplitRowWords words) and a lane reads
+// 8 consecutive m of a plane (one 16-deep k-block) per ds_read_b128.
+template <bool kClean, int TNR, bool kSplit>
 __global__ __launch_bounds__(256, 3) void k_gemm_tn_partial(const float* __restrict__ A, int64_t lda,
                                                             const float* __restrict__ B1, int64_t ldb1,
                                                             const float* __restrict__ B2, int64_t ldb2, int64_t K1,
@@ -64,9 +69,12 @@ __global__ __launch_bounds__(256, 3) void k_gemm_tn_partial(const float* __restr
   constexpr int WGN = TNR == 128 ? 2 : 4;        // waves along K
   constexpr int BMN = TNR == 128 ? 2 : 1;        // 32 x 32 MFMA blocks per wave along N
   constexpr int BMK = TNR == 128 ? 2 : 1;        // ... and along K
-  __shared__ __attribute__((aligned(16))) float smem[(TNR + 128) * kTnLd];
+  constexpr int kRowW = kSplit ? kSplitRowWords : kTnLd;
+  __shared__ __attribute__((aligned(16))) float smem[(TNR + 128) * kRowW];
   float* At = smem;                  // [n][m]
-  float* Bt = smem + TNR * kTnLd;    // [k][m]
+  float* Bt = smem + TNR * kRowW;    // [k][m]
+  uint32_t* Ath = reinterpret_cast<uint32_t*>(At);
+  uint32_t* Bth = reinterpret_cast<uint32_t*>(Bt);
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = tid >> 6;
@@ -164,6 +172,26 @@ __global__ __launch_bounds__(256, 3) void k_gemm_tn_partial(const float* __restr
   };
   // the 4 x 4 block regrouped: column c4 + t gets (row r4 .. r4 + 3) as one float4
   auto store_stage = [&]() {
+    if constexpr (kSplit) {
+      auto put = [&](uint32_t* img, int col, int r, const float4 v) {
+        uint2 o[3];
+        split4(v, o);
+        uint32_t* row = img + col * kSplitRowWords + (r >> 1);
+#pragma unroll
+        for (int p = 0; p < 3; ++p) *reinterpret_cast<uint2*>(row + p * 16) = o[p];
+      };
+      if (stage_a) {
+        put(Ath, c4a + 0, r4a, make_float4(va[0].x, va[1].x, va[2].x, va[3].x));
+        put(Ath, c4a + 1, r4a, make_float4(va[0].y, va[1].y, va[2].y, va[3].y));
+        put(Ath, c4a + 2, r4a, make_float4(va[0].z, va[1].z, va[2].z, va[3].z));
+        put(Ath, c4a + 3, r4a, make_float4(va[0].w, va[1].w, va[2].w, va[3].w));
+      }
+      put(Bth, c4 + 0, r4, make_float4(vb[0].x, vb[1].x, vb[2].x, vb[3].x));
+      put(Bth, c4 + 1, r4, make_float4(vb[0].y, vb[1].y, vb[2].y, vb[3].y));
+      put(Bth, c4 + 2, r4, make_float4(vb[0].z, vb[1].z, vb[2].z, vb[3].z));
+      put(Bth, c4 + 3, r4, make_float4(vb[0].w, vb[1].w, vb[2].w, vb[3].w));
+      return;
+    }
     if (stage_a) {
       *reinterpret_cast<float4*>(At + (c4a + 0) * kTnLd + r4a) = make_float4(va[0].x, va[1].x, va[2].x, va[3].x);
       *reinterpret_cast<float4*>(At + (c4a + 1) * kTnLd + r4a) = make_float4(va[0].y, va[1].y, va[2].y, va[3].y);
@@ -183,24 +211,54 @@ __global__ __launch_bounds__(256, 3) void k_gemm_tn_partial(const float* __restr
     const bool more = m0 + kTnBM < me;
     if (more) load_stage(m0 + kTnBM);
     __builtin_amdgcn_s_setprio(1);   // keep the MFMA cluster together (T5)
+    if constexpr (kSplit) {
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      float4 fa[BMN], fb[BMK];
+      for (int kb = 0; kb < 2; ++kb) {
+        bf16x8 fa[BMN][3], fb[BMK][3];
 #pragma unroll
-      for (int t = 0; t < BMN; ++t)
-        fa[t] = *reinterpret_cast<const float4*>(At + (wm * 32 * BMN + t * 32 + li) * kTnLd + lh * 16 + 4 * q);
+        for (int t = 0; t < BMN; ++t)
 #pragma unroll
-      for (int t = 0; t < BMK; ++t)
-        fb[t] = *reinterpret_cast<const float4*>(Bt + (wn * 32 * BMK + t * 32 + li) * kTnLd + lh * 16 + 4 * q);
+          for (int p = 0; p < 3; ++p)
+            fa[t][p] = *reinterpret_cast<const bf16x8*>(Ath + (wm * 32 * BMN + t * 32 + li) * kSplitRowWords + p * 16 +
+                                                        kb * 8 + lh * 4);
 #pragma unroll
-      for (int tm = 0; tm < BMN; ++tm)
+        for (int t = 0; t < BMK; ++t)
 #pragma unroll
-        for (int tn = 0; tn < BMK; ++tn) {
-          acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[tm].x, fb[tn].x, acc[tm][tn], 0, 0, 0);
-          acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[tm].y, fb[tn].y, acc[tm][tn], 0, 0, 0);
-          acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[tm].z, fb[tn].z, acc[tm][tn], 0, 0, 0);
-          acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[tm].w, fb[tn].w, acc[tm][tn], 0, 0, 0);
-        }
+          for (int p = 0; p < 3; ++p)
+            fb[t][p] = *reinterpret_cast<const bf16x8*>(Bth + (wn * 32 * BMK + t * 32 + li) * kSplitRowWords + p * 16 +
+                                                        kb * 8 + lh * 4);
+#pragma unroll
+        for (int tm = 0; tm < BMN; ++tm)
+#pragma unroll
+          for (int tn = 0; tn < BMK; ++tn) {   // smallest terms first
+            acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[tm][2], fb[tn][0], acc[tm][tn], 0, 0, 0);
+            acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[tm][1], fb[tn][1], acc[tm][tn], 0, 0, 0);
+            acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[tm][0], fb[tn][2], acc[tm][tn], 0, 0, 0);
+            acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[tm][1], fb[tn][0], acc[tm][tn], 0, 0, 0);
+            acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[tm][0], fb[tn][1], acc[tm][tn], 0, 0, 0);
+            acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[tm][0], fb[tn][0], acc[tm][tn], 0, 0, 0);
+          }
+      }
+    } else {
+  #pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        float4 fa[BMN], fb[BMK];
+  #pragma unroll
+        for (int t = 0; t < BMN; ++t)
+          fa[t] = *reinterpret_cast<const float4*>(At + (wm * 32 * BMN + t * 32 + li) * kTnLd + lh * 16 + 4 * q);
+  #pragma unroll
+        for (int t = 0; t < BMK; ++t)
+          fb[t] = *reinterpret_cast<const float4*>(Bt + (wn * 32 * BMK + t * 32 + li) * kTnLd + lh * 16 + 4 * q);
+  #pragma unroll
+        for (int tm = 0; tm < BMN; ++tm)
+  #pragma unroll
+          for (int tn = 0; tn < BMK; ++tn) {
+            acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[tm].x, fb[tn].x, acc[tm][tn], 0, 0, 0);
+            acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[tm].y, fb[tn].y, acc[tm][tn], 0, 0, 0);
+            acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[tm].z, fb[tn].z, acc[tm][tn], 0, 0, 0);
+            acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[tm].w, fb[tn].w, acc[tm][tn], 0, 0, 0);
+          }
+      }
     }
     __builtin_amdgcn_s_setprio(0);
     if (more) {
@@ -306,7 +364,6 @@ __global__ __launch_bounds__(256) void k_slab_reduce2(const float* __restrict__ 
 // stage A, waves 2-3 stage B.  64 rows of M per stage, register prefetch of the next stage.
 constexpr int kTnBMh = 64;
 constexpr int kTnLdH = kTnBMh + 8;
-using bf16x8 = __attribute__((ext_vector_type(8))) __bf16;
 
 template <bool kVec>
 __global__ __launch_bounds__(256, 2) void k_gemm_tn_bf16_partial(const uint16_t* __restrict__ A, int64_t lda,
@@ -520,13 +577,18 @@ extern "C" int hgin_gemm_tn_f32(const float* a, int64_t lda, const float* b1, in
     // register prefetch at 3 waves/SIMD (profiles/r01_tn_variants.txt: 12 % faster than the unpipelined
     // loop, 3-5 % faster than prefetch at 2 waves)
     const bool clean = vec && N % tile_n == 0 && K % 128 == 0 && k1 % 128 == 0;
-#define HGIN_TN_LAUNCH(CLEAN, TNR) \
-  k_gemm_tn_partial<CLEAN, TNR><<<grid, 256, 0, s>>>(a, lda, b1, ldb1, b2, ldb2, k1, M, N, K, rows, vec, slab, tg)
+#define HGIN_TN_LAUNCH(CLEAN, TNR, SPLIT)                                                             \
+  k_gemm_tn_partial<CLEAN, TNR, SPLIT><<<grid, 256, 0, s>>>(a, lda, b1, ldb1, b2, ldb2, k1, M, N, K, rows, vec, \
+                                                             slab, tg)
+#define HGIN_TN_CLEAN(TNR, SPLIT) \
+  if (clean) HGIN_TN_LAUNCH(true, TNR, SPLIT); else HGIN_TN_LAUNCH(false, TNR, SPLIT);
+    const bool split = gemm_split_enabled();
     if (tile_n == 32) {
-      if (clean) HGIN_TN_LAUNCH(true, 32); else HGIN_TN_LAUNCH(false, 32);
+      if (split) { HGIN_TN_CLEAN(32, true) } else { HGIN_TN_CLEAN(32, false) }
     } else {
-      if (clean) HGIN_TN_LAUNCH(true, 128); else HGIN_TN_LAUNCH(false, 128);
+      if (split) { HGIN_TN_CLEAN(128, true) } else { HGIN_TN_CLEAN(128, false) }
     }
+#undef HGIN_TN_CLEAN
 #undef HGIN_TN_LAUNCH
   }
   const int64_t G = ceil_div(S_eff, kSlabGroup);
