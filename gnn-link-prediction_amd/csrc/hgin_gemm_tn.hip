@@ -52,6 +52,52 @@ __device__ __forceinline__ TnWork tn_work(const TnGrid& g) {
   return w;
 }
 
+// Fused PReLU-backward prologue (hgin_gin_mlp_bwd_w_*): the A operand is formed on its way into LDS as
+// g_z = z > 0 ? g_y : slope * g_y from the g_y / z streams (the g_z stream of a separate PReLU-backward pass
+// is never written and re-read), and the workgroups of the first K tile also produce the bias / slope
+// gradients as per-split partials (column sums of g_z; sum of z * g_y over z <= 0), summed afterwards in a
+// fixed order.  (g_z is never written: the dX GEMM applies the same prologue to its A operand.)  Reference: autograd of PReLU + Linear bias
+// (models.py:237-238) reached from train.py:43.
+struct TnPro {
+  const void* z;        // [M, N] pre-activation, row stride ldz (A's element type)
+  int64_t ldz;
+  const float* slope;   // device float[1]
+  float* pcol;          // [N][S] column-sum partials
+  float* ps;            // [N tiles][S] slope-sum partials
+  int64_t S;
+};
+
+// Fixed-order combine of the per-thread prologue partials of one workgroup: 8 row groups of csum per
+// column (in group order) and a fixed tree over 256 slope partials.  red: >= 8 * cols + 256 floats.
+template <int CPT>
+__device__ __forceinline__ void pro_partials(const TnPro& pro, float* red, int cols, int rg, int c0, bool active,
+                                             const float (&csum)[CPT], const float (&ssc)[CPT], int64_t n0,
+                                             int64_t N, int64_t split) {
+  const int tid = threadIdx.x;
+  float ssum = 0.0f;
+#pragma unroll
+  for (int q = 0; q < CPT; ++q) ssum = __fadd_rn(ssum, ssc[q]);
+  __syncthreads();   // the LDS operand images are no longer read
+  if (active) {
+#pragma unroll
+    for (int q = 0; q < CPT; ++q) red[rg * cols + c0 + q] = csum[q];
+  }
+  float* rs = red + 8 * cols;
+  rs[tid] = active ? ssum : 0.0f;
+  __syncthreads();
+  if (tid < cols && n0 + tid < N) {
+    float s = 0.0f;
+#pragma unroll
+    for (int g = 0; g < 8; ++g) s = __fadd_rn(s, red[g * cols + tid]);
+    pro.pcol[(n0 + tid) * pro.S + split] = s;
+  }
+  for (int off = 128; off > 0; off >>= 1) {
+    if (tid < off) rs[tid] = __fadd_rn(rs[tid], rs[tid + off]);
+    __syncthreads();
+  }
+  if (tid == 0) pro.ps[(n0 / cols) * pro.S + split] = rs[0];   // [N tile][S]
+}
+
 // TNR = output-tile rows along N: 128 (2 x 2 waves of 64 x 64) or 32 for narrow gradients such as the
 // readout's Linear(128, 32) (4 waves of 32 x 32 along K: no MFMA work on rows that do not exist; wave 0
 // alone stages the 32-column A block).
@@ -60,12 +106,15 @@ using bf16x8 = __attribute__((ext_vector_type(8))) __bf16;
 // kSplit: fp32 operands on the bf16 matrix cores (hgin_common.h split4): the transposed column runs of 4 m
 // are written as three bf16 planes ([col][3 x 32 m + pad] rows of kSplitRowWords words) and a lane reads
 // 8 consecutive m of a plane (one 16-deep k-block) per ds_read_b128.
-template <bool kClean, int TNR, bool kSplit>
-__global__ __launch_bounds__(256, 3) void k_gemm_tn_partial(const float* __restrict__ A, int64_t lda,
+// kPro: A = g_y and the PReLU-backward prologue above (TnPro).  kLateZ: z is loaded when the stage is
+// written to LDS instead of with the register prefetch (16 fewer VGPRs live across the MFMA cluster).
+template <bool kClean, int TNR, bool kSplit, bool kPro, bool kLateZ = false>
+__global__ __launch_bounds__(256, (kPro && !kLateZ) ? 2 : 3) void k_gemm_tn_partial(const float* __restrict__ A, int64_t lda,
                                                             const float* __restrict__ B1, int64_t ldb1,
                                                             const float* __restrict__ B2, int64_t ldb2, int64_t K1,
                                                             int64_t M, int64_t N, int64_t K, int64_t rows_per_split,
-                                                            bool vec, float* __restrict__ slab, TnGrid grid) {
+                                                            bool vec, float* __restrict__ slab, TnGrid grid,
+                                                            TnPro pro) {
   constexpr int WGN = TNR == 128 ? 2 : 4;        // waves along K
   constexpr int BMN = TNR == 128 ? 2 : 1;        // 32 x 32 MFMA blocks per wave along N
   constexpr int BMK = TNR == 128 ? 2 : 1;        // ... and along K
@@ -102,6 +151,9 @@ __global__ __launch_bounds__(256, 3) void k_gemm_tn_partial(const float* __restr
   const int r4a = TNR == 128 ? r4 : (tid >> 3) * 4;
   const bool stage_a = TNR == 128 || tid < 64;   // wave-uniform
   float4 va[4], vb[4];
+  float4 vz[4];                                  // kPro: z of the A block
+  const float* Z = static_cast<const float*>(pro.z);
+  const int64_t ldz = pro.ldz;
   // kClean (16-B rows; N, K and K1 multiples of 128, so every A tile lies inside N and every B tile wholly
   // inside B1 or B2): the source pointers are fixed per workgroup and a stage is loaded without per-load
   // branches (the selection below is between loaded values; a select between the two kernel arguments'
@@ -113,7 +165,34 @@ __global__ __launch_bounds__(256, 3) void k_gemm_tn_partial(const float* __restr
   const int64_t ldb = from1 ? ldb1 : ldb2;
   const float* pa0 = A + n0;
   const uint32_t oa = (uint32_t)(r4a * lda + c4a), ob = (uint32_t)(r4 * ldb + c4);
+  const float* pz0 = kPro ? Z + n0 : nullptr;
+  const uint32_t oz = kPro ? (uint32_t)(r4a * ldz + c4a) : 0u;
+  int64_t m_ld = mb;   // first row of the stage held in va / vb
+  // kPro: z of the A block, rows m0 + r4a .. + 3 (zero past me, as the A loads)
+  auto load_z = [&](int64_t m0) {
+    if (!stage_a) return;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int64_t gm = m0 + r4a + j;
+      const bool ok = gm < me;
+      if (kClean) {
+        const float4 zz = *reinterpret_cast<const float4*>(pz0 + (ok ? gm : me - 1) * ldz + c4a);
+        vz[j] = make_float4(ok ? zz.x : 0.f, ok ? zz.y : 0.f, ok ? zz.z : 0.f, ok ? zz.w : 0.f);
+      } else {
+        const int64_t gn = n0 + c4a;
+        float z4[4] = {0.f, 0.f, 0.f, 0.f};
+        if (ok) {
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+            if (gn + q < N) z4[q] = Z[gm * ldz + gn + q];
+        }
+        vz[j] = make_float4(z4[0], z4[1], z4[2], z4[3]);
+      }
+    }
+  };
   auto load_stage = [&](int64_t m0) {
+    m_ld = m0;
+    if constexpr (kPro && !kLateZ) load_z(m0);
     if constexpr (kClean) {
       if (m0 + kTnBM <= me) {
 #pragma unroll
@@ -170,8 +249,31 @@ __global__ __launch_bounds__(256, 3) void k_gemm_tn_partial(const float* __restr
       }
     }
   };
+  // kPro: g_z of the loaded A block (zero rows stay zero), its partial sums, and the optional g_z stream
+  float csum[4] = {0.f, 0.f, 0.f, 0.f};   // per-column fixed-order chains, branch-free (see the bf16 kernel)
+  float ssc[4] = {0.f, 0.f, 0.f, 0.f};
+  const float slope = kPro ? pro.slope[0] : 0.0f;
+  auto prologue = [&]() {
+    if (!stage_a) return;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {   // branch-free (a data-dependent branch per element splits the block and
+                                    // the scheduler then keeps every loaded value alive: heavy spilling)
+      float g[4] = {va[j].x, va[j].y, va[j].z, va[j].w};
+      const float zz[4] = {vz[j].x, vz[j].y, vz[j].z, vz[j].w};
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const bool pos = zz[q] > 0.0f;
+        ssc[q] = __fadd_rn(ssc[q], pos ? 0.0f : __fmul_rn(zz[q], g[q]));
+        g[q] = pos ? g[q] : __fmul_rn(slope, g[q]);
+        csum[q] = __fadd_rn(csum[q], g[q]);
+      }
+      va[j] = make_float4(g[0], g[1], g[2], g[3]);
+    }
+  };
   // the 4 x 4 block regrouped: column c4 + t gets (row r4 .. r4 + 3) as one float4
   auto store_stage = [&]() {
+    if constexpr (kPro && kLateZ) load_z(m_ld);
+    if constexpr (kPro) prologue();
     if constexpr (kSplit) {
       auto put = [&](uint32_t* img, int col, int r, const float4 v) {
         uint2 o[3];
@@ -266,6 +368,10 @@ __global__ __launch_bounds__(256, 3) void k_gemm_tn_partial(const float* __restr
       store_stage();
       __syncthreads();
     }
+  }
+  if constexpr (kPro) {
+    if (work.k0 == 0)   // workgroup-uniform
+      pro_partials<4>(pro, smem, TNR, r4a >> 2, c4a, stage_a, csum, ssc, n0, N, work.split);
   }
   float* out = slab + work.split * N * K;
 #pragma unroll
@@ -507,6 +613,16 @@ int64_t tn_target_wgs() {
   return t;
 }
 
+// Fused PReLU-backward prologue: z loaded with the register prefetch (2 waves / SIMD, the extra 16-32 live
+// VGPRs) or at LDS-store time (3 waves / SIMD for fp32).  HGIN_TN_LATEZ=0/1.
+bool tn_late_z() {
+  static const bool v = [] {
+    const char* e = getenv("HGIN_TN_LATEZ");
+    return e ? atoi(e) != 0 : true;
+  }();
+  return v;
+}
+
 int64_t tn_splits(int64_t M, int64_t N, int64_t K, int64_t stage_rows = kTnBM, int64_t target = 1024) {
   int64_t S;
   if (tn_is_small(N, K)) {
@@ -522,109 +638,71 @@ int64_t tn_splits(int64_t M, int64_t N, int64_t K, int64_t stage_rows = kTnBM, i
   return S < 1 ? 1 : S;
 }
 
-}  // namespace
-}  // namespace hgin
-
-using namespace hgin;
-
-extern "C" int hgin_gemm_tn_workspace_size(int64_t M, int64_t N, int64_t K, size_t* bytes) {
-  HGIN_ARG_CHECK(bytes && M >= 0 && N >= 0 && K >= 0, "hgin_gemm_tn_workspace_size: bad args");
+size_t tn_ws_bytes(int64_t M, int64_t N, int64_t K) {
   const int64_t S = tn_splits(M, N, K);
-  *bytes = align_up(sizeof(float) * (size_t)(S * N * K), 256) +
-           sizeof(float) * (size_t)(ceil_div(S, kSlabGroup) * N * K) + 256;
-  return HGIN_OK;
+  return align_up(sizeof(float) * (size_t)(S * N * K), 256) + align_up(sizeof(float) * (size_t)(ceil_div(S, kSlabGroup) * N * K), 256);
 }
 
-extern "C" int hgin_gemm_tn_f32(const float* a, int64_t lda, const float* b1, int64_t ldb1, int64_t k1,
-                                const float* b2, int64_t ldb2, int64_t M, int64_t N, int64_t K, float* out,
-                                int64_t ldo, void* workspace, size_t workspace_bytes, void* stream) {
-  HGIN_ARG_CHECK(M >= 0 && N >= 0 && K >= 0 && k1 >= 0 && k1 <= K, "hgin_gemm_tn_f32: bad sizes");
-  HGIN_ARG_CHECK(N <= 65535 * 128 && K <= 65535 * 128, "hgin_gemm_tn_f32: N/K too large");
-  if (N == 0 || K == 0) return HGIN_OK;
-  HGIN_ARG_CHECK(out && ldo >= K, "hgin_gemm_tn_f32: bad output");
-  size_t need = 0;
-  hgin_gemm_tn_workspace_size(M, N, K, &need);
-  if (workspace_bytes < need || !workspace) {
-    set_error("hgin_gemm_tn_f32: workspace %zu < %zu", workspace_bytes, need);
+// Prologue partials of hgin_gin_mlp_bwd_w_*: [N][S] column sums + [N tiles][S] slope sums.
+size_t pro_ws_bytes(int64_t M, int64_t N, int64_t K) {
+  const int64_t S = tn_splits(M, N, K);
+  return align_up(sizeof(float) * (size_t)(N * S), 256) + align_up(sizeof(float) * (size_t)(ceil_div(N, 32) * S), 256);
+}
+
+// Final fixed-order sums of the prologue partials (one workgroup per column; one for the slope).
+__global__ __launch_bounds__(256) void k_pro_final(const float* __restrict__ pcol, const float* __restrict__ ps,
+                                                   int64_t S, int64_t n_ps, float* __restrict__ g_bias,
+                                                   float* __restrict__ g_prelu) {
+  __shared__ float red[256];
+  const int c = blockIdx.x;
+  const int64_t n = c < (int)gridDim.x - 1 ? S : n_ps;
+  const float* p = c < (int)gridDim.x - 1 ? pcol + (int64_t)c * S : ps;
+  float s = 0.0f;
+  for (int64_t b = threadIdx.x; b < n; b += 256) s = __fadd_rn(s, p[b]);
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int off = 128; off > 0; off >>= 1) {
+    if ((int)threadIdx.x < off) red[threadIdx.x] = __fadd_rn(red[threadIdx.x], red[threadIdx.x + off]);
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    if (c < (int)gridDim.x - 1) g_bias[c] = red[0];
+    else g_prelu[0] = red[0];
+  }
+}
+
+// Shared host path of hgin_gemm_tn_* (pro == NULL) and hgin_gin_mlp_bwd_w_* (pro: A = g_y, z, slope, ...).
+template <typename T>
+int gemm_tn_impl(const char* what, const T* a, int64_t lda, const T* b1, int64_t ldb1, int64_t k1, const T* b2,
+                 int64_t ldb2, int64_t M, int64_t N, int64_t K, float* out, int64_t ldo, void* workspace,
+                 size_t workspace_bytes, hipStream_t s, const TnPro* pro_in, float* g_bias, float* g_prelu) {
+  constexpr bool kHalf = sizeof(T) == 2;
+  const size_t need = tn_ws_bytes(M, N, K);
+  const size_t need_pro = pro_in ? pro_ws_bytes(M, N, K) : 0;
+  if (workspace_bytes < need + need_pro || !workspace) {
+    set_error("%s: workspace %zu < %zu", what, workspace_bytes, need + need_pro);
     return HGIN_E_WORKSPACE;
   }
-  hipStream_t s = as_stream(stream);
   if (M == 0) {
     for (int64_t n = 0; n < N; ++n) {
-      int rc = memset_async(out + n * ldo, 0, sizeof(float) * (size_t)K, s, "hgin_gemm_tn_f32");
+      int rc = memset_async(out + n * ldo, 0, sizeof(float) * (size_t)K, s, what);
       if (rc) return rc;
+    }
+    if (pro_in) {
+      int rc = memset_async(g_bias, 0, sizeof(float) * (size_t)N, s, what);
+      if (rc == HGIN_OK) rc = memset_async(g_prelu, 0, sizeof(float), s, what);
+      return rc;
     }
     return HGIN_OK;
   }
   HGIN_ARG_CHECK(a && lda >= N && (k1 == 0 || (b1 && ldb1 >= k1)) && (k1 == K || (b2 && ldb2 >= K - k1)),
-                 "hgin_gemm_tn_f32: bad operand");
-  const bool vec = aligned16(a) && lda % 4 == 0 && (k1 == 0 || (aligned16(b1) && ldb1 % 4 == 0)) &&
-                   (k1 == K || (aligned16(b2) && ldb2 % 4 == 0)) && k1 % 4 == 0;
-  const int64_t S = tn_splits(M, N, K, kTnBM, tn_target_wgs());
-  const int64_t rows = ceil_div(ceil_div(M, S), kTnBM) * kTnBM;
-  const int64_t S_eff = ceil_div(M, rows);
-  const int64_t NK = N * K;
-  float* slab = static_cast<float*>(workspace);
-  float* part = reinterpret_cast<float*>(static_cast<char*>(workspace) + align_up(sizeof(float) * (size_t)(S * NK), 256));
-  if (tn_is_small(N, K)) {
-    k_tn_small<float><<<(unsigned)S_eff, 256, 0, s>>>(a, lda, b1, ldb1, b2, ldb2, k1, M, (int)N, (int)K, rows, slab);
-  } else {
-    const int64_t tile_n = N <= 32 ? 32 : 128;
-    const int64_t tiles_n = ceil_div(N, tile_n);
-    const TnGrid tg{tile_n, tiles_n, tiles_n * ceil_div(K, 128), tiles_n * ceil_div(K, 128) * S_eff,
-                    xcd_remap_enabled()};
-    dim3 grid((unsigned)(tg.xcd ? round_up8(tg.n_work) : tg.n_work));
-    // register prefetch at 3 waves/SIMD (profiles/r01_tn_variants.txt: 12 % faster than the unpipelined
-    // loop, 3-5 % faster than prefetch at 2 waves)
-    const bool clean = vec && N % tile_n == 0 && K % 128 == 0 && k1 % 128 == 0;
-#define HGIN_TN_LAUNCH(CLEAN, TNR, SPLIT)                                                             \
-  k_gemm_tn_partial<CLEAN, TNR, SPLIT><<<grid, 256, 0, s>>>(a, lda, b1, ldb1, b2, ldb2, k1, M, N, K, rows, vec, \
-                                                             slab, tg)
-#define HGIN_TN_CLEAN(TNR, SPLIT) \
-  if (clean) HGIN_TN_LAUNCH(true, TNR, SPLIT); else HGIN_TN_LAUNCH(false, TNR, SPLIT);
-    const bool split = gemm_split_enabled();
-    if (tile_n == 32) {
-      if (split) { HGIN_TN_CLEAN(32, true) } else { HGIN_TN_CLEAN(32, false) }
-    } else {
-      if (split) { HGIN_TN_CLEAN(128, true) } else { HGIN_TN_CLEAN(128, false) }
-    }
-#undef HGIN_TN_CLEAN
-#undef HGIN_TN_LAUNCH
-  }
-  const int64_t G = ceil_div(S_eff, kSlabGroup);
-  dim3 g1((unsigned)ceil_div(ceil_div(NK, 4), 256), (unsigned)G);
-  k_slab_reduce1<<<g1, 256, 0, s>>>(slab, S_eff, NK, part);
-  k_slab_reduce2<<<(unsigned)ceil_div(NK, 256), 256, 0, s>>>(part, G, NK, out, K, ldo);
-  return check_launch("hgin_gemm_tn_f32");
-}
-
-extern "C" int hgin_gemm_tn_bf16(const uint16_t* a, int64_t lda, const uint16_t* b1, int64_t ldb1, int64_t k1,
-                                 const uint16_t* b2, int64_t ldb2, int64_t M, int64_t N, int64_t K, float* out,
-                                 int64_t ldo, void* workspace, size_t workspace_bytes, void* stream) {
-  HGIN_ARG_CHECK(M >= 0 && N >= 0 && K >= 0 && k1 >= 0 && k1 <= K, "hgin_gemm_tn_bf16: bad sizes");
-  HGIN_ARG_CHECK(N <= 65535 * 128 && K <= 65535 * 128, "hgin_gemm_tn_bf16: N/K too large");
-  if (N == 0 || K == 0) return HGIN_OK;
-  HGIN_ARG_CHECK(out && ldo >= K, "hgin_gemm_tn_bf16: bad output");
-  size_t need = 0;
-  hgin_gemm_tn_workspace_size(M, N, K, &need);
-  if (workspace_bytes < need || !workspace) {
-    set_error("hgin_gemm_tn_bf16: workspace %zu < %zu", workspace_bytes, need);
-    return HGIN_E_WORKSPACE;
-  }
-  hipStream_t s = as_stream(stream);
-  if (M == 0) {
-    for (int64_t n = 0; n < N; ++n) {
-      int rc = memset_async(out + n * ldo, 0, sizeof(float) * (size_t)K, s, "hgin_gemm_tn_bf16");
-      if (rc) return rc;
-    }
-    return HGIN_OK;
-  }
-  HGIN_ARG_CHECK(a && lda >= N && (k1 == 0 || (b1 && ldb1 >= k1)) && (k1 == K || (b2 && ldb2 >= K - k1)),
-                 "hgin_gemm_tn_bf16: bad operand");
-  const bool vec = aligned16(a) && lda % 8 == 0 && (k1 == 0 || (aligned16(b1) && ldb1 % 8 == 0)) &&
-                   (k1 == K || (aligned16(b2) && ldb2 % 8 == 0)) && k1 % 8 == 0;
+                 "%s: bad operand", what);
+  constexpr int64_t vw = kHalf ? 8 : 4;   // elements per 16 B
+  bool vec = aligned16(a) && lda % vw == 0 && (k1 == 0 || (aligned16(b1) && ldb1 % vw == 0)) &&
+             (k1 == K || (aligned16(b2) && ldb2 % vw == 0)) && k1 % vw == 0;
+  if (pro_in) vec = vec && aligned16(pro_in->z) && pro_in->ldz % vw == 0;
   const bool small = tn_is_small(N, K);
-  const int64_t stage = small ? kTnBM : kTnBMh;
+  const int64_t stage = (kHalf && !small) ? kTnBMh : kTnBM;
   const int64_t S = tn_splits(M, N, K, stage, tn_target_wgs());   // <= the workspace's split count
   const int64_t rows = ceil_div(ceil_div(M, S), stage) * stage;
   const int64_t S_eff = ceil_div(M, rows);
@@ -632,22 +710,179 @@ extern "C" int hgin_gemm_tn_bf16(const uint16_t* a, int64_t lda, const uint16_t*
   float* slab = static_cast<float*>(workspace);
   float* part = reinterpret_cast<float*>(static_cast<char*>(workspace) +
                                          align_up(sizeof(float) * (size_t)(tn_splits(M, N, K) * NK), 256));
+  TnPro pro{};
+  if (pro_in) {
+    pro = *pro_in;
+    pro.pcol = reinterpret_cast<float*>(static_cast<char*>(workspace) + need);
+    pro.ps = reinterpret_cast<float*>(static_cast<char*>(workspace) + need +
+                                      align_up(sizeof(float) * (size_t)(N * tn_splits(M, N, K)), 256));
+    pro.S = S_eff;
+  }
+  const bool late = tn_late_z();
+  int64_t tile_n = 128;
   if (small) {
-    k_tn_small<uint16_t><<<(unsigned)S_eff, 256, 0, s>>>(a, lda, b1, ldb1, b2, ldb2, k1, M, (int)N, (int)K, rows,
-                                                          slab);
-  } else {
+    HGIN_ARG_CHECK(!pro_in, "%s: no fused prologue for N or K < 16", what);
+    k_tn_small<T><<<(unsigned)S_eff, 256, 0, s>>>(a, lda, b1, ldb1, b2, ldb2, k1, M, (int)N, (int)K, rows, slab);
+  } else if constexpr (kHalf) {
     const int64_t tiles_n = ceil_div(N, 128);
-    const TnGrid tg{128, tiles_n, tiles_n * ceil_div(K, 128), tiles_n * ceil_div(K, 128) * S_eff,
-                    xcd_remap_enabled()};
+    const TnGrid tg{128, tiles_n, tiles_n * ceil_div(K, 128), tiles_n * ceil_div(K, 128) * S_eff, xcd_remap_enabled()};
     dim3 grid((unsigned)(tg.xcd ? round_up8(tg.n_work) : tg.n_work));
+    HGIN_ARG_CHECK(!pro_in, "%s: no fused prologue for bf16", what);
     if (vec)
       k_gemm_tn_bf16_partial<true><<<grid, 256, 0, s>>>(a, lda, b1, ldb1, b2, ldb2, k1, M, N, K, rows, slab, tg);
     else
       k_gemm_tn_bf16_partial<false><<<grid, 256, 0, s>>>(a, lda, b1, ldb1, b2, ldb2, k1, M, N, K, rows, slab, tg);
+  } else {
+    tile_n = N <= 32 ? 32 : 128;
+    const int64_t tiles_n = ceil_div(N, tile_n);
+    const TnGrid tg{tile_n, tiles_n, tiles_n * ceil_div(K, 128), tiles_n * ceil_div(K, 128) * S_eff,
+                    xcd_remap_enabled()};
+    dim3 grid((unsigned)(tg.xcd ? round_up8(tg.n_work) : tg.n_work));
+    // register prefetch at 3 waves/SIMD (profiles/r01_tn_variants.txt: 12 % faster than the unpipelined
+    // loop, 3-5 % faster than prefetch at 2 waves)
+    const bool clean = vec && N % tile_n == 0 && K % 128 == 0 && k1 % 128 == 0;
+    const bool split = gemm_split_enabled();
+#define HGIN_TN_LAUNCH(CLEAN, TNR, SPLIT, PRO, LATE)                                                          \
+  k_gemm_tn_partial<CLEAN, TNR, SPLIT, PRO, LATE><<<grid, 256, 0, s>>>(a, lda, b1, ldb1, b2, ldb2, k1, M, N, K, \
+                                                                        rows, vec, slab, tg, pro)
+#define HGIN_TN_PRO(CLEAN, TNR, SPLIT)                                          \
+  if (!pro_in) HGIN_TN_LAUNCH(CLEAN, TNR, SPLIT, false, false);                 \
+  else if (late) HGIN_TN_LAUNCH(CLEAN, TNR, SPLIT, true, true);                 \
+  else HGIN_TN_LAUNCH(CLEAN, TNR, SPLIT, true, false);
+#define HGIN_TN_CLEAN(TNR, SPLIT) \
+  if (clean) { HGIN_TN_PRO(true, TNR, SPLIT) } else { HGIN_TN_PRO(false, TNR, SPLIT) }
+    if (tile_n == 32) {
+      if (split) { HGIN_TN_CLEAN(32, true) } else { HGIN_TN_CLEAN(32, false) }
+    } else {
+      if (split) { HGIN_TN_CLEAN(128, true) } else { HGIN_TN_CLEAN(128, false) }
+    }
+#undef HGIN_TN_CLEAN
+#undef HGIN_TN_PRO
+#undef HGIN_TN_LAUNCH
   }
   const int64_t G = ceil_div(S_eff, kSlabGroup);
   dim3 g1((unsigned)ceil_div(ceil_div(NK, 4), 256), (unsigned)G);
   k_slab_reduce1<<<g1, 256, 0, s>>>(slab, S_eff, NK, part);
   k_slab_reduce2<<<(unsigned)ceil_div(NK, 256), 256, 0, s>>>(part, G, NK, out, K, ldo);
-  return check_launch("hgin_gemm_tn_bf16");
+  if (pro_in)
+    k_pro_final<<<(unsigned)(N + 1), 256, 0, s>>>(pro.pcol, pro.ps, S_eff, ceil_div(N, tile_n) * S_eff, g_bias, g_prelu);
+  return check_launch(what);
+}
+
+template <typename T>
+int gemm_tn_entry(const char* what, const T* a, int64_t lda, const T* b1, int64_t ldb1, int64_t k1, const T* b2,
+                  int64_t ldb2, int64_t M, int64_t N, int64_t K, float* out, int64_t ldo, void* workspace,
+                  size_t workspace_bytes, void* stream) {
+  HGIN_ARG_CHECK(M >= 0 && N >= 0 && K >= 0 && k1 >= 0 && k1 <= K, "%s: bad sizes", what);
+  HGIN_ARG_CHECK(N <= 65535 * 128 && K <= 65535 * 128, "%s: N/K too large", what);
+  if (N == 0 || K == 0) return HGIN_OK;
+  HGIN_ARG_CHECK(out && ldo >= K, "%s: bad output", what);
+  return gemm_tn_impl<T>(what, a, lda, b1, ldb1, k1, b2, ldb2, M, N, K, out, ldo, workspace, workspace_bytes,
+                         as_stream(stream), nullptr, nullptr, nullptr);
+}
+
+// hgin_gin_mlp_bwd_w_*: fp32 with an MFMA tile and no g_z requested -> the fused prologue; otherwise the
+// PReLU backward into g_z (the caller's buffer, or workspace scratch) followed by the plain TN GEMM.
+bool mlp_bwd_w_fused(int64_t N, int64_t K, size_t elem) { return elem == 4 && !tn_is_small(N, K); }
+
+size_t mlp_bwd_w_ws_bytes(int64_t M, int64_t N, int64_t K, size_t elem, bool have_gz) {
+  if (mlp_bwd_w_fused(N, K, elem) && !have_gz) return tn_ws_bytes(M, N, K) + pro_ws_bytes(M, N, K);
+  size_t pw = 0;
+  hgin_prelu_bwd_workspace_size(M, N, &pw);
+  return align_up(pw, 256) + tn_ws_bytes(M, N, K) + (have_gz ? 0 : align_up(elem * (size_t)(M * N), 256));
+}
+
+template <typename T>
+int mlp_bwd_w_entry(const char* what, const T* g_y, int64_t ld_gy, const T* z, int64_t ldz, const float* prelu,
+                    const T* b1, int64_t ldb1, int64_t k1, const T* b2, int64_t ldb2, int64_t M, int64_t N, int64_t K,
+                    float* g_w, int64_t ldw, float* g_prelu, float* g_bias, T* g_z, int64_t ld_gz, void* workspace,
+                    size_t workspace_bytes, void* stream) {
+  HGIN_ARG_CHECK(M >= 0 && N >= 0 && K >= 0 && k1 >= 0 && k1 <= K, "%s: bad sizes", what);
+  HGIN_ARG_CHECK(N >= 1 && N <= 65535 * 128 && K >= 1 && K <= 65535 * 128, "%s: N/K out of range", what);
+  HGIN_ARG_CHECK(prelu && g_prelu && g_bias && g_w && ldw >= K, "%s: NULL output / bad ldw", what);
+  HGIN_ARG_CHECK(M == 0 || (g_y && ld_gy >= N && z && ldz >= N), "%s: bad g_y / z", what);
+  HGIN_ARG_CHECK(!g_z || ld_gz >= N, "%s: ld_gz < N", what);
+  const size_t need = mlp_bwd_w_ws_bytes(M, N, K, sizeof(T), g_z != nullptr);
+  if (workspace_bytes < need || !workspace) {
+    set_error("%s: workspace %zu < %zu", what, workspace_bytes, need);
+    return HGIN_E_WORKSPACE;
+  }
+  hipStream_t s = as_stream(stream);
+  if (mlp_bwd_w_fused(N, K, sizeof(T)) && !g_z) {
+    TnPro pro{z, ldz, prelu, nullptr, nullptr, 0};
+    return gemm_tn_impl<T>(what, g_y, ld_gy, b1, ldb1, k1, b2, ldb2, M, N, K, g_w, ldw, workspace, workspace_bytes,
+                           s, &pro, g_bias, g_prelu);
+  }
+  size_t pw = 0;
+  hgin_prelu_bwd_workspace_size(M, N, &pw);
+  char* ws = static_cast<char*>(workspace);
+  const size_t tw = tn_ws_bytes(M, N, K);
+  T* gz = g_z;
+  int64_t ldg = ld_gz;
+  if (!gz) {
+    gz = reinterpret_cast<T*>(ws + align_up(pw, 256) + tw);
+    ldg = N;
+  }
+  int rc;
+  if constexpr (sizeof(T) == 2) {
+    HGIN_ARG_CHECK(ldg == N, "%s: bf16 g_z must be dense (ld_gz == N)", what);
+    rc = hgin_prelu_bwd_bf16(g_y, ld_gy, z, M, N, prelu, gz, g_prelu, g_bias, ws, pw, stream);
+  } else {
+    HGIN_ARG_CHECK(ldg == N, "%s: g_z must be dense (ld_gz == N)", what);
+    rc = hgin_prelu_bwd_f32(g_y, ld_gy, z, M, N, prelu, gz, g_prelu, g_bias, ws, pw, stream);
+  }
+  if (rc) return rc;
+  return gemm_tn_impl<T>(what, gz, ldg, b1, ldb1, k1, b2, ldb2, M, N, K, g_w, ldw, ws + align_up(pw, 256), tw, s,
+                         nullptr, nullptr, nullptr);
+}
+
+}  // namespace
+}  // namespace hgin
+
+using namespace hgin;
+
+extern "C" int hgin_gemm_tn_workspace_size(int64_t M, int64_t N, int64_t K, size_t* bytes) {
+  HGIN_ARG_CHECK(bytes && M >= 0 && N >= 0 && K >= 0, "hgin_gemm_tn_workspace_size: bad args");
+  *bytes = tn_ws_bytes(M, N, K);
+  return HGIN_OK;
+}
+
+extern "C" int hgin_gemm_tn_f32(const float* a, int64_t lda, const float* b1, int64_t ldb1, int64_t k1,
+                                const float* b2, int64_t ldb2, int64_t M, int64_t N, int64_t K, float* out,
+                                int64_t ldo, void* workspace, size_t workspace_bytes, void* stream) {
+  return gemm_tn_entry<float>("hgin_gemm_tn_f32", a, lda, b1, ldb1, k1, b2, ldb2, M, N, K, out, ldo, workspace,
+                              workspace_bytes, stream);
+}
+
+extern "C" int hgin_gemm_tn_bf16(const uint16_t* a, int64_t lda, const uint16_t* b1, int64_t ldb1, int64_t k1,
+                                 const uint16_t* b2, int64_t ldb2, int64_t M, int64_t N, int64_t K, float* out,
+                                 int64_t ldo, void* workspace, size_t workspace_bytes, void* stream) {
+  return gemm_tn_entry<uint16_t>("hgin_gemm_tn_bf16", a, lda, b1, ldb1, k1, b2, ldb2, M, N, K, out, ldo, workspace,
+                                 workspace_bytes, stream);
+}
+
+extern "C" int hgin_gin_mlp_bwd_w_workspace_size(int64_t M, int64_t N, int64_t K, int elem_bytes, int have_gz,
+                                                 size_t* bytes) {
+  HGIN_ARG_CHECK(bytes && M >= 0 && N >= 0 && K >= 0 && (elem_bytes == 2 || elem_bytes == 4),
+                 "hgin_gin_mlp_bwd_w_workspace_size: bad args");
+  *bytes = mlp_bwd_w_ws_bytes(M, N, K, (size_t)elem_bytes, have_gz != 0);
+  return HGIN_OK;
+}
+
+extern "C" int hgin_gin_mlp_bwd_w_f32(const float* g_y, int64_t ld_gy, const float* z, int64_t ldz, const float* prelu,
+                                      const float* b1, int64_t ldb1, int64_t k1, const float* b2, int64_t ldb2,
+                                      int64_t M, int64_t N, int64_t K, float* g_w, int64_t ldw, float* g_prelu,
+                                      float* g_bias, float* g_z, int64_t ld_gz, void* workspace,
+                                      size_t workspace_bytes, void* stream) {
+  return mlp_bwd_w_entry<float>("hgin_gin_mlp_bwd_w_f32", g_y, ld_gy, z, ldz, prelu, b1, ldb1, k1, b2, ldb2, M, N, K,
+                                g_w, ldw, g_prelu, g_bias, g_z, ld_gz, workspace, workspace_bytes, stream);
+}
+
+extern "C" int hgin_gin_mlp_bwd_w_bf16(const uint16_t* g_y, int64_t ld_gy, const uint16_t* z, int64_t ldz,
+                                       const float* prelu, const uint16_t* b1, int64_t ldb1, int64_t k1,
+                                       const uint16_t* b2, int64_t ldb2, int64_t M, int64_t N, int64_t K, float* g_w,
+                                       int64_t ldw, float* g_prelu, float* g_bias, uint16_t* g_z, int64_t ld_gz,
+                                       void* workspace, size_t workspace_bytes, void* stream) {
+  return mlp_bwd_w_entry<uint16_t>("hgin_gin_mlp_bwd_w_bf16", g_y, ld_gy, z, ldz, prelu, b1, ldb1, k1, b2, ldb2, M, N,
+                                   K, g_w, ldw, g_prelu, g_bias, g_z, ld_gz, workspace, workspace_bytes, stream);
 }

@@ -107,6 +107,11 @@ _SIGS = {
     "hgin_gemm_nt_bf16": ([_P, _I64, _P, _I64, _P, _I64, _I64, _I64, _I64, _P], _I32),
     "hgin_gemm_tn_bf16": ([_P, _I64, _P, _I64, _I64, _P, _I64, _I64, _I64, _I64, _P, _I64, _P, _SZ, _P], _I32),
     "hgin_prelu_bwd_bf16": ([_P, _I64, _P, _I64, _I64, _P, _P, _P, _P, _P, _SZ, _P], _I32),
+    "hgin_gin_mlp_bwd_w_workspace_size": ([_I64, _I64, _I64, _I32, _I32, ctypes.POINTER(_SZ)], _I32),
+    "hgin_gin_mlp_bwd_w_f32": ([_P, _I64, _P, _I64, _P, _P, _I64, _I64, _P, _I64, _I64, _I64, _I64, _P, _I64, _P, _P,
+                                _P, _I64, _P, _SZ, _P], _I32),
+    "hgin_gin_mlp_bwd_w_bf16": ([_P, _I64, _P, _I64, _P, _P, _I64, _I64, _P, _I64, _I64, _I64, _I64, _P, _I64, _P, _P,
+                                 _P, _I64, _P, _SZ, _P], _I32),
     "hgin_combine_bwd_bf16": ([_P, _I64, _P, _I64, _I64, _I64, _P, _P, _I64, _P, _P, _SZ, _P], _I32),
     "hgin_head_mape_workspace_size": ([_I64, _I64, ctypes.POINTER(_SZ)], _I32),
     "hgin_head_mape_fwd_f32": ([_P, _I64, _I64, _I64, _P, _P, _P, _P, _P, _P, _P, _SZ, _P], _I32),

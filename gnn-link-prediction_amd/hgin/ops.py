@@ -261,6 +261,40 @@ def gemm_tn(a: Tensor, b1: Tensor, b2: Optional[Tensor] = None) -> Tensor:
     return out
 
 
+def mlp_bwd_fused(z: Tensor, n: int, k: int) -> bool:
+    """True where libhgin runs the PReLU backward inside the dW GEMM (fp32, N and K >= 16)."""
+    return z.dtype == torch.float32 and n >= 16 and k >= 16
+
+
+def mlp_bwd_w(g_y: Tensor, z: Tensor, prelu: Tensor, b1: Tensor, b2: Optional[Tensor] = None,
+              want_gz: bool = False):
+    """Backward of prelu([b1 | b2] @ W^T + b) up to the weights: (g_w [N, K] fp32, g_a [1], g_b [N], g_z).
+
+    g_z = z > 0 ? g_y : a * g_y is formed inside the weight-gradient GEMM where fused (mlp_bwd_fused) and
+    then returned as None unless ``want_gz``; otherwise (bf16, narrow layers) it is materialised."""
+    g_y, b1 = _rowmajor(g_y), _rowmajor(b1)
+    if b2 is not None:
+        b2 = _rowmajor(b2)
+    _same_dtype("mlp_bwd_w", g_y, z, b1, b2)
+    M, N = z.shape
+    k1 = b1.shape[1]
+    K = k1 + (b2.shape[1] if b2 is not None else 0)
+    dev = z.device
+    fused = mlp_bwd_fused(z, N, K)
+    g_z = torch.empty_like(z) if (want_gz or not fused) else None
+    g_w = torch.empty(N, K, dtype=torch.float32, device=dev)
+    g_a = torch.empty(1, dtype=torch.float32, device=dev)
+    g_b = torch.empty(N, dtype=torch.float32, device=dev)
+    nbytes = ctypes.c_size_t(0)
+    _lib.check(_lib.lib().hgin_gin_mlp_bwd_w_workspace_size(M, N, K, z.element_size(), int(g_z is not None),
+                                                            ctypes.byref(nbytes)), "gin_mlp_bwd_w_workspace_size")
+    ws = _workspace(nbytes.value, dev)
+    _lib.call(f"hgin_gin_mlp_bwd_w_{_sfx(z)}", _p(g_y), g_y.stride(0), _p(z), z.stride(0), _p(prelu), _p(b1),
+              b1.stride(0), k1, _p(b2), b2.stride(0) if b2 is not None else 0, M, N, K, _p(g_w), g_w.stride(0),
+              _p(g_a), _p(g_b), _p(g_z), N, _p(ws), nbytes.value, _stream(z))
+    return g_w, g_a, g_b, g_z
+
+
 def gin_mlp_fwd(comb: Tensor, weight: Tensor, bias: Tensor, prelu: Optional[Tensor], accum: Optional[Tensor],
                 save_z: bool = True, comb2: Optional[Tensor] = None):
     """y = prelu([comb | comb2] @ W^T + b) [+ accum]  (prelu None: plain Linear, y = z, nothing saved).
@@ -330,70 +364,6 @@ class _AggregateFn(torch.autograd.Function):
         return g_src, g_dst, (g_eps.view_as(eps) if need_eps and g_eps is not None else None), None, None
 
 
-class _SideStream:
-    """Run part of a backward on a second HIP stream of the same device (HGIN_STREAMS=1 enables).
-
-    Off by default: measured on cfg2 / cfg2bf, overlapping dW with the dX GEMM + CSC aggregate was 1 %
-    slower (7.55 vs 7.49 ms, 4.10 vs 4.07 ms) — each of these kernels already fills the 256 CUs, so the
-    second stream only adds contention.
-
-    ``begin`` makes the side stream wait for everything queued so far on the current stream; work inside
-    ``with side:`` is issued there; ``keep`` marks current-stream tensors the side work reads (so the
-    caching allocator does not recycle them early); ``join`` makes the current stream wait for the side work
-    and marks its outputs as used on the current stream.  Everything is joined before the autograd function
-    returns, so callers (AccumulateGrad, the optimizer) see ordinary current-stream tensors."""
-
-    _streams: dict = {}
-    _enabled = None
-
-    def __init__(self, dev, main, stream):
-        self.dev, self.main, self.stream, self._ctx = dev, main, stream, None
-
-    @classmethod
-    def enabled(cls) -> bool:
-        if cls._enabled is None:
-            import os
-            cls._enabled = os.environ.get("HGIN_STREAMS", "0") == "1"
-        return cls._enabled
-
-    @classmethod
-    def begin(cls, like: Tensor) -> "_SideStream":
-        dev = like.device
-        main = torch.cuda.current_stream(dev)
-        if not cls.enabled() or torch.cuda.is_current_stream_capturing():
-            return _SideStream(dev, main, None)
-        s = cls._streams.get(dev)
-        if s is None:
-            s = cls._streams[dev] = torch.cuda.Stream(device=dev)
-        s.wait_stream(main)
-        return _SideStream(dev, main, s)
-
-    def __enter__(self):
-        if self.stream is not None:
-            self._ctx = torch.cuda.stream(self.stream)
-            self._ctx.__enter__()
-        return self
-
-    def __exit__(self, *exc):
-        if self._ctx is not None:
-            self._ctx.__exit__(*exc)
-            self._ctx = None
-        return False
-
-    def keep(self, *tensors) -> None:
-        if self.stream is not None:
-            for t in tensors:
-                if t is not None:
-                    t.record_stream(self.stream)
-
-    def join(self, *outputs) -> None:
-        if self.stream is not None:
-            self.main.wait_stream(self.stream)
-            for t in outputs:
-                if t is not None:
-                    t.record_stream(self.main)
-
-
 class _GINConvFn(torch.autograd.Function):
     """Fused GINConv + GINLayer MLP: y = prelu(comb @ W^T + b) [+ accum], comb = aggregate + self term."""
 
@@ -415,44 +385,37 @@ class _GINConvFn(torch.autograd.Function):
         need = ctx.needs_input_grad
         need_src, need_dst, need_eps, need_w, need_b, need_a, need_acc = need[:7]
         g_y = _rowmajor(g_y)
-        g_z, g_a, g_b = prelu_bwd(g_y, z, prelu)
         g_w = g_src = g_dst = g_eps = None
         f_src, mode = ctx.f_src, ctx.mode
         if need_src or need_dst:
-            side = None
-            if need_w:
-                # dW = g_z^T comb (MFMA-bound) on a side stream, overlapping the dX GEMM and the HBM-bound
-                # CSC aggregate / combine backward below; joined before returning (see _SideStream)
-                side = _SideStream.begin(g_z)
-                with side:
-                    g_w = gemm_tn(g_z, comb)
-                side.keep(g_z, comb)
+            # (a side stream overlapping dW with the dX GEMM + CSC aggregate measured 1 % slower on cfg2 / cfg2bf:
+            # each of these kernels already fills the 256 CUs)
+            g_w, g_a, g_b, g_z = mlp_bwd_w(g_y, z, prelu, comb, want_gz=True)
             g_comb = gemm_nt(g_z, weight.t().contiguous())      # dX = g_z W   [N_dst, K]
             if need_src:
                 g_src = _backward_aggregate(ctx.graph, g_comb[:, :f_src])
             if mode != COMBINE_NONE:
                 gs = g_comb[:, f_src:] if mode == COMBINE_CONCAT else g_comb
                 g_dst, g_eps = combine_bwd(gs, x_dst, eps, need_dst)
-            if side is not None:
-                side.join(g_w)
         elif need_eps and mode != COMBINE_NONE:
             # Only parameters need gradients (the first layer, whose inputs are data):
             # sum(g_comb[:, self] * x_dst) = sum(W_self * (g_z^T x_dst)), so one TN pass over
             # [aggregate | x_dst] yields dW and the eps gradient and the [N_dst, K] dX GEMM is skipped.
             if mode == COMBINE_CONCAT:
-                G = gemm_tn(g_z, comb[:, :f_src], x_dst)
+                G, g_a, g_b, _ = mlp_bwd_w(g_y, z, prelu, comb[:, :f_src], x_dst)
                 gx = G[:, f_src:]
                 g_w = torch.cat((G[:, :f_src], (1 + eps) * gx), 1) if need_w else None
                 g_eps = (weight[:, f_src:] * gx).sum().reshape(1)
             else:
-                G = gemm_tn(g_z, comb, x_dst)
+                G, g_a, g_b, _ = mlp_bwd_w(g_y, z, prelu, comb, x_dst)
                 g_w = G[:, :f_src].contiguous() if need_w else None
                 g_eps = (weight * G[:, f_src:]).sum().reshape(1)
-        elif need_w:
-            g_w = gemm_tn(g_z, comb)
+        else:
+            g_w, g_a, g_b, _ = mlp_bwd_w(g_y, z, prelu, comb)
         g_acc = g_y if need_acc else None
-        return (g_src, g_dst, (g_eps.view_as(eps) if (need_eps and g_eps is not None) else None), g_w,
-                g_b if need_b else None, (g_a.view_as(prelu) if need_a else None), g_acc, None, None)
+        return (g_src, g_dst, (g_eps.view_as(eps) if (need_eps and g_eps is not None) else None),
+                g_w if need_w else None, g_b if need_b else None, (g_a.view_as(prelu) if need_a else None), g_acc,
+                None, None)
 
 
 _ONE = {}
@@ -482,27 +445,19 @@ class _LinearPReLUFn(torch.autograd.Function):
         x1, x2, weight, prelu, z = ctx.saved_tensors
         need_x1, need_x2, need_w, need_b, need_a = ctx.needs_input_grad
         g_y = _rowmajor(g_y)
+        k1 = x1.size(1)
         if prelu is None:   # g_z = g_y; the PReLU-backward kernel with slope 1 yields the bias column sums
             g_z, _, g_b = prelu_bwd(g_y, g_y, _one(g_y.device))
             g_a = None
             g_z = g_z.to(x1.dtype)     # bf16 path: the head's output (and g_y) are fp32, its operands bf16
+            g_w = gemm_tn(g_z, x1, x2) if need_w else None
+            g_x1 = gemm_nt(g_z, weight[:, :k1].t().contiguous()) if need_x1 else None
+            g_x2 = gemm_nt(g_z, weight[:, k1:].t().contiguous()) if (need_x2 and x2 is not None) else None
         else:
-            g_z, g_a, g_b = prelu_bwd(g_y, z, prelu)
-        k1 = x1.size(1)
-        g_w, side = None, None
-        if need_w:
-            side = _SideStream.begin(g_z) if need_x1 else None      # dW overlaps the dX GEMM
-            if side is not None:
-                with side:
-                    g_w = gemm_tn(g_z, x1, x2)
-                side.keep(g_z, x1, x2)
-            else:
-                g_w = gemm_tn(g_z, x1, x2)
-        g_x1 = gemm_nt(g_z, weight[:, :k1].t().contiguous()) if need_x1 else None
-        g_x2 = gemm_nt(g_z, weight[:, k1:].t().contiguous()) if (need_x2 and x2 is not None) else None
-        if side is not None:
-            side.join(g_w)
-        return (g_x1, g_x2, g_w, (g_b if need_b else None),
+            g_w, g_a, g_b, g_z = mlp_bwd_w(g_y, z, prelu, x1, x2, want_gz=need_x1 or (need_x2 and x2 is not None))
+            g_x1 = gemm_nt(g_z, weight[:, :k1].t().contiguous()) if need_x1 else None
+            g_x2 = gemm_nt(g_z, weight[:, k1:].t().contiguous()) if (need_x2 and x2 is not None) else None
+        return (g_x1, g_x2, g_w if need_w else None, (g_b if need_b else None),
                 (g_a.view_as(prelu) if (need_a and g_a is not None) else None))
 
 

@@ -133,6 +133,25 @@ int hgin_gemm_tn_f32(const float* a, int64_t lda, const float* b1, int64_t ldb1,
                      int64_t ldb2, int64_t M, int64_t N, int64_t K, float* out, int64_t ldo, void* workspace,
                      size_t workspace_bytes, void* stream);
 
+/* ---- A9 fused: PReLU + bias backward folded into the weight-gradient GEMM ------------------------------
+ * Replaces autograd of GINLayer.mlp = Sequential(Linear, PReLU) (models.py:236-239) and of the readout's
+ * Linear + PReLU (models.py:300-330) at train.py:43 — hgin_prelu_bwd_* followed by hgin_gemm_tn_*:
+ *   g_z = z > 0 ? g_y : prelu[0] * g_y
+ *   g_w[N, K] = g_z^T @ [b1 | b2]                          (operand conventions of hgin_gemm_tn_f32)
+ *   g_bias[n] = sum_m g_z[m, n];  g_prelu[0] = sum (z > 0 ? 0 : z * g_y)
+ * fp32 with N, K >= 16 and g_z == NULL: one pass — g_z is formed while the A operand is staged and never
+ * stored; bias / slope gradients come from per-split partials.  Otherwise (bf16, narrow shapes, or g_z
+ * requested: g_z != NULL, dense, ld_gz == N) the two passes run, g_z in the caller's buffer or workspace.
+ * Deterministic.  workspace: hgin_gin_mlp_bwd_w_workspace_size(M, N, K, element bytes 4 | 2, g_z != NULL).
+ *
+ * (A dX GEMM applying the same prologue to its A operand measured slower than the separate passes — the
+ * z stream under the dX tile costs more than the g_z stream it saves — so dX reads a materialised g_z.) */
+int hgin_gin_mlp_bwd_w_workspace_size(int64_t M, int64_t N, int64_t K, int elem_bytes, int have_gz, size_t* bytes);
+int hgin_gin_mlp_bwd_w_f32(const float* g_y, int64_t ld_gy, const float* z, int64_t ldz, const float* prelu,
+                           const float* b1, int64_t ldb1, int64_t k1, const float* b2, int64_t ldb2,
+                           int64_t M, int64_t N, int64_t K, float* g_w, int64_t ldw, float* g_prelu, float* g_bias,
+                           float* g_z, int64_t ld_gz, void* workspace, size_t workspace_bytes, void* stream);
+
 /* ---- cfg5: bf16 storage + bf16 MFMA, fp32 accumulate (BASELINE.json configs[4]) ---------------------
  * Same operations and operand conventions as the fp32 entry points above; `uint16_t` = a bfloat16 bit
  * pattern.  Every sum / product is formed in fp32 and each stored bf16 value is rounded once
@@ -164,6 +183,11 @@ int hgin_gemm_tn_bf16(const uint16_t* a, int64_t lda, const uint16_t* b1, int64_
 int hgin_prelu_bwd_bf16(const uint16_t* g_y, int64_t ld_gy, const uint16_t* z, int64_t M, int64_t N,
                         const float* prelu, uint16_t* g_z, float* g_prelu, float* g_bias, void* workspace,
                         size_t workspace_bytes, void* stream);
+int hgin_gin_mlp_bwd_w_bf16(const uint16_t* g_y, int64_t ld_gy, const uint16_t* z, int64_t ldz, const float* prelu,
+                            const uint16_t* b1, int64_t ldb1, int64_t k1, const uint16_t* b2, int64_t ldb2,
+                            int64_t M, int64_t N, int64_t K, float* g_w, int64_t ldw, float* g_prelu,
+                            float* g_bias, uint16_t* g_z, int64_t ld_gz, void* workspace, size_t workspace_bytes,
+                            void* stream);
 int hgin_combine_bwd_bf16(const uint16_t* g, int64_t ld_g, const uint16_t* x_dst, int64_t ld_dst,
                           int64_t n_rows, int64_t f_dst, const float* eps, uint16_t* g_x_dst, int64_t ld_gx,
                           float* g_eps, void* workspace, size_t workspace_bytes, void* stream);

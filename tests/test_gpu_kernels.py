@@ -234,6 +234,39 @@ def test_prelu_bwd_strided_grad():
     assert torch.equal(g_z, torch.where(z > 0, gy, a * gy))
 
 
+@pytest.mark.parametrize("M,N,K1,K2", [(1000, 128, 256, 0), (600, 128, 128, 128), (50000, 128, 128, 128),
+                                       (20011, 32, 128, 0), (3001, 17, 64, 64), (777, 100, 6, 3), (5, 8, 4, 4),
+                                       (129, 256, 100, 28), (0, 64, 64, 0)])
+@pytest.mark.parametrize("want_gz", [False, True])
+def test_mlp_bwd_fused(M, N, K1, K2, want_gz):
+    """A9 fused: PReLU + bias backward inside the dW GEMM against a float64 evaluation (the fallback shapes
+    and want_gz run the separate passes and return g_z)."""
+    big = torch.randn(M, N + 5, device=DEV)
+    gy = big[:, 3:3 + N]                                # strided incoming gradient (a column slice)
+    z = torch.randn(M, N, device=DEV)
+    if M:
+        z[0, 0] = 0.0
+    a = torch.tensor([0.3], device=DEV)
+    b1 = torch.randn(M, K1, device=DEV)
+    b2 = torch.randn(M, K2, device=DEV) if K2 else None
+    g_w, g_a, g_b, g_z = ops.mlp_bwd_w(gy, z, a, b1, b2, want_gz=want_gz)
+    gz_ref = torch.where(z > 0, gy, a * gy)
+    if want_gz or not ops.mlp_bwd_fused(z, N, K1 + K2):
+        assert torch.equal(g_z, gz_ref)
+    else:
+        assert g_z is None
+    b = b1 if b2 is None else torch.cat((b1, b2), 1)
+    gzd = gz_ref.double()
+    ref_w = gzd.t() @ b.double()
+    assert ((g_w.double() - ref_w).abs() <= 1e-5 * (gzd.abs().t() @ b.double().abs() + 1)).all()
+    assert ((g_b.double() - gzd.sum(0)).abs() <= 1e-5 * gzd.abs().sum(0) + 1e-6).all()
+    zr = z.double()
+    ga_ref = (torch.where(zr > 0, torch.zeros_like(zr), zr) * gy.double()).sum()
+    assert abs(float(g_a) - float(ga_ref)) <= 1e-5 * (float((zr * gy.double()).abs().sum()) + 1)
+    again = ops.mlp_bwd_w(gy, z, a, b1, b2, want_gz=want_gz)
+    assert all(torch.equal(p, q) for p, q in zip(again[:3], (g_w, g_a, g_b)))    # deterministic
+
+
 def test_combine_bwd():
     g = torch.randn(900, 130, device=DEV)
     x = torch.randn(900, 64, device=DEV)
