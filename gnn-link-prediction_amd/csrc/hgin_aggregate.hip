@@ -20,6 +20,27 @@
 namespace hgin {
 namespace {
 
+// Batched tail (HGIN_AGG_TAIL = 0 / 1): GIN rows are short (uniform random graphs: mean degree 5-10), so
+// with full-batch-then-one-at-a-time walking most neighbours of most rows were fetched one dependent round
+// trip at a time.  Batched: every batch of up to U neighbour rows is in flight together (lanes past the
+// row's end issue nothing); the adds stay sequential in edge order (bit-identical).
+bool agg_tail_batched() {
+  static const bool v = [] {
+    const char* e = getenv("HGIN_AGG_TAIL");
+    return e ? atoi(e) != 0 : true;
+  }();
+  return v;
+}
+
+// Neighbour rows in flight per lane group (HGIN_AGG_U = 8 / 16; 16 only with the batched tail).
+int agg_u() {
+  static const int v = [] {
+    const char* e = getenv("HGIN_AGG_U");
+    return e && atoi(e) == 16 ? 16 : 8;
+  }();
+  return v;
+}
+
 template <int VEC>
 struct Vec;
 // NT = true: streamed-once data (the self-term rows and the output) use non-temporal loads / stores so they
@@ -65,7 +86,9 @@ struct Vec<4> {
   }
 };
 
-template <int VEC, int G, int U, bool NT>
+// kTail: the neighbour walk issues every batch's loads together, the last partial batch included (see
+// agg_tail_batched); otherwise full batches of U, then the remainder one neighbour at a time.
+template <int VEC, int G, int U, bool NT, bool kTail>
 __global__ __launch_bounds__(256) void k_aggregate(const int32_t* __restrict__ rowptr, const int32_t* __restrict__ col,
                                                    int64_t n_rows, const float* __restrict__ x_src, int64_t ld_src,
                                                    int f_src, const float* __restrict__ x_dst, int64_t ld_dst,
@@ -90,23 +113,44 @@ __global__ __launch_bounds__(256) void k_aggregate(const int32_t* __restrict__ r
 #pragma unroll
     for (int c = 0; c < VEC; ++c) acc[c] = 0.0f;
     int k = beg;
-    for (; k + U <= end; k += U) {
-      int idx[U];
+    if constexpr (kTail) {
+      // every batch, including a row's last partial one, issues its (up to U) neighbour loads together;
+      // lanes past the row's end load nothing and add nothing (rows are mostly shorter than U)
+      for (; k < end; k += U) {
+        const int n = end - k;
+        T v[U];
 #pragma unroll
-      for (int u = 0; u < U; ++u) idx[u] = col[k + u];
-      T v[U];
+        for (int u = 0; u < U; ++u) {
+          v[u] = T{};
+          if (u < n) v[u] = V::load(x_src + (int64_t)col[k + u] * ld_src + f0);
+        }
 #pragma unroll
-      for (int u = 0; u < U; ++u) v[u] = V::load(x_src + (int64_t)idx[u] * ld_src + f0);
+        for (int u = 0; u < U; ++u) {
+          if (u < n) {
 #pragma unroll
-      for (int u = 0; u < U; ++u) {
-#pragma unroll
-        for (int c = 0; c < VEC; ++c) acc[c] = __fadd_rn(acc[c], V::get(v[u], c));
+            for (int c = 0; c < VEC; ++c) acc[c] = __fadd_rn(acc[c], V::get(v[u], c));
+          }
+        }
       }
-    }
-    for (; k < end; ++k) {
-      const T v = V::load(x_src + (int64_t)col[k] * ld_src + f0);
+    } else {
+      for (; k + U <= end; k += U) {
+        int idx[U];
 #pragma unroll
-      for (int c = 0; c < VEC; ++c) acc[c] = __fadd_rn(acc[c], V::get(v, c));
+        for (int u = 0; u < U; ++u) idx[u] = col[k + u];
+        T v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) v[u] = V::load(x_src + (int64_t)idx[u] * ld_src + f0);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+#pragma unroll
+          for (int c = 0; c < VEC; ++c) acc[c] = __fadd_rn(acc[c], V::get(v[u], c));
+        }
+      }
+      for (; k < end; ++k) {
+        const T v = V::load(x_src + (int64_t)col[k] * ld_src + f0);
+#pragma unroll
+        for (int c = 0; c < VEC; ++c) acc[c] = __fadd_rn(acc[c], V::get(v, c));
+      }
     }
     T o;
     if (combine == HGIN_COMBINE_ADD) {
@@ -135,7 +179,6 @@ int launch_aggregate(const int32_t* rowptr, const int32_t* col, int64_t n_rows, 
                      int f_src, const float* x_dst, int64_t ld_dst, int f_dst, const float* eps, int combine,
                      float* out, int64_t ld_out, hipStream_t s) {
   constexpr int kRowsPerWave = kWave / G;
-  constexpr int kU = 8;
   const int64_t waves = ceil_div(n_rows, kRowsPerWave);
   const int64_t blocks = ceil_div(waves, 256 / kWave);
   // Non-temporal self-term loads / output stores: measured (profiles/r01_agg_nt.txt) 3-9 % faster for the
@@ -145,13 +188,15 @@ int launch_aggregate(const int32_t* rowptr, const int32_t* col, int64_t n_rows, 
     return v ? atoi(v) : -1;
   }();
   const bool nt = nt_env >= 0 ? nt_env != 0 : combine == HGIN_COMBINE_CONCAT;
-  if (nt)
-    k_aggregate<VEC, G, kU, true><<<dim3((unsigned)blocks), 256, 0, s>>>(rowptr, col, n_rows, x_src, ld_src, f_src,
-                                                                         x_dst, ld_dst, f_dst, eps, combine, out, ld_out);
-  else
-    k_aggregate<VEC, G, kU, false><<<dim3((unsigned)blocks), 256, 0, s>>>(rowptr, col, n_rows, x_src, ld_src, f_src,
-                                                                          x_dst, ld_dst, f_dst, eps, combine, out,
-                                                                          ld_out);
+#define HGIN_AGG_L(UV, NTV, TAIL)                                                                           \
+  k_aggregate<VEC, G, UV, NTV, TAIL><<<dim3((unsigned)blocks), 256, 0, s>>>(rowptr, col, n_rows, x_src, ld_src, \
+                                                                           f_src, x_dst, ld_dst, f_dst, eps,     \
+                                                                           combine, out, ld_out)
+  const bool tail = agg_tail_batched();
+  if (agg_u() == 16 && tail) { if (nt) HGIN_AGG_L(16, true, true); else HGIN_AGG_L(16, false, true); }
+  else if (nt) { if (tail) HGIN_AGG_L(8, true, true); else HGIN_AGG_L(8, true, false); }
+  else { if (tail) HGIN_AGG_L(8, false, true); else HGIN_AGG_L(8, false, false); }
+#undef HGIN_AGG_L
   return check_launch("hgin_aggregate_f32");
 }
 
@@ -211,7 +256,7 @@ struct BVec<8> {
   }
 };
 
-template <int VEC, int G, int U, bool NT>
+template <int VEC, int G, int U, bool NT, bool kTail>
 __global__ __launch_bounds__(256) void k_aggregate_bf16(const int32_t* __restrict__ rowptr,
                                                         const int32_t* __restrict__ col, int64_t n_rows,
                                                         const uint16_t* __restrict__ x_src, int64_t ld_src, int f_src,
@@ -237,26 +282,47 @@ __global__ __launch_bounds__(256) void k_aggregate_bf16(const int32_t* __restric
 #pragma unroll
     for (int c = 0; c < VEC; ++c) acc[c] = 0.0f;
     int k = beg;
-    for (; k + U <= end; k += U) {
-      int idx[U];
+    if constexpr (kTail) {
+      for (; k < end; k += U) {   // batched tail, as k_aggregate
+        const int n = end - k;
+        T v[U];
 #pragma unroll
-      for (int u = 0; u < U; ++u) idx[u] = col[k + u];
-      T v[U];
+        for (int u = 0; u < U; ++u) {
+          v[u] = T{};
+          if (u < n) v[u] = V::load(x_src + (int64_t)col[k + u] * ld_src + f0);
+        }
 #pragma unroll
-      for (int u = 0; u < U; ++u) v[u] = V::load(x_src + (int64_t)idx[u] * ld_src + f0);
+        for (int u = 0; u < U; ++u) {
+          if (u < n) {
+            float f[VEC];
+            V::unpack(v[u], f);
 #pragma unroll
-      for (int u = 0; u < U; ++u) {
+            for (int c = 0; c < VEC; ++c) acc[c] = __fadd_rn(acc[c], f[c]);
+          }
+        }
+      }
+    } else {
+      for (; k + U <= end; k += U) {
+        int idx[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) idx[u] = col[k + u];
+        T v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) v[u] = V::load(x_src + (int64_t)idx[u] * ld_src + f0);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          float f[VEC];
+          V::unpack(v[u], f);
+#pragma unroll
+          for (int c = 0; c < VEC; ++c) acc[c] = __fadd_rn(acc[c], f[c]);
+        }
+      }
+      for (; k < end; ++k) {
         float f[VEC];
-        V::unpack(v[u], f);
+        V::unpack(V::load(x_src + (int64_t)col[k] * ld_src + f0), f);
 #pragma unroll
         for (int c = 0; c < VEC; ++c) acc[c] = __fadd_rn(acc[c], f[c]);
       }
-    }
-    for (; k < end; ++k) {
-      float f[VEC];
-      V::unpack(V::load(x_src + (int64_t)col[k] * ld_src + f0), f);
-#pragma unroll
-      for (int c = 0; c < VEC; ++c) acc[c] = __fadd_rn(acc[c], f[c]);
     }
     if (combine == HGIN_COMBINE_ADD) {
       float xd[VEC];
@@ -283,12 +349,15 @@ int launch_aggregate_bf16(const int32_t* rowptr, const int32_t* col, int64_t n_r
                           int combine, uint16_t* out, int64_t ld_out, hipStream_t s) {
   constexpr int kRowsPerWave = kWave / G;
   const int64_t blocks = ceil_div(ceil_div(n_rows, kRowsPerWave), 256 / kWave);
-  if (combine == HGIN_COMBINE_CONCAT)
-    k_aggregate_bf16<VEC, G, 8, true><<<dim3((unsigned)blocks), 256, 0, s>>>(
-        rowptr, col, n_rows, x_src, ld_src, f_src, x_dst, ld_dst, f_dst, eps, combine, out, ld_out);
-  else
-    k_aggregate_bf16<VEC, G, 8, false><<<dim3((unsigned)blocks), 256, 0, s>>>(
-        rowptr, col, n_rows, x_src, ld_src, f_src, x_dst, ld_dst, f_dst, eps, combine, out, ld_out);
+#define HGIN_AGGB_L(UV, NTV, TAIL)                                    \
+  k_aggregate_bf16<VEC, G, UV, NTV, TAIL><<<dim3((unsigned)blocks), 256, 0, s>>>( \
+      rowptr, col, n_rows, x_src, ld_src, f_src, x_dst, ld_dst, f_dst, eps, combine, out, ld_out)
+  const bool tail = agg_tail_batched();
+  const bool nt = combine == HGIN_COMBINE_CONCAT;
+  if (agg_u() == 16 && tail) { if (nt) HGIN_AGGB_L(16, true, true); else HGIN_AGGB_L(16, false, true); }
+  else if (nt) { if (tail) HGIN_AGGB_L(8, true, true); else HGIN_AGGB_L(8, true, false); }
+  else { if (tail) HGIN_AGGB_L(8, false, true); else HGIN_AGGB_L(8, false, false); }
+#undef HGIN_AGGB_L
   return check_launch("hgin_aggregate_bf16");
 }
 
@@ -351,7 +420,7 @@ __device__ __forceinline__ void st_quad(void* p, const uint4& v) {
   else *reinterpret_cast<u4v*>(p) = t;
 }
 
-template <typename T, int NQ, int G, int U, bool NT>
+template <typename T, int NQ, int G, int U, bool NT, bool kTail>
 __global__ __launch_bounds__(256) void k_agg_q(const int32_t* __restrict__ rowptr, const int32_t* __restrict__ col,
                                                int64_t n_rows, const T* __restrict__ x_src, int64_t ld_src, int f_src,
                                                const T* __restrict__ x_dst, int64_t ld_dst, int f_dst,
@@ -375,7 +444,35 @@ __global__ __launch_bounds__(256) void k_agg_q(const int32_t* __restrict__ rowpt
 #pragma unroll
     for (int c = 0; c < VEC; ++c) acc[c] = 0.0f;
     int k = beg;
-    for (; k + U <= end; k += U) {
+    if constexpr (kTail) {
+      for (; k < end; k += U) {   // batched tail, as k_aggregate
+        const int n = end - k;
+        uint4 v[U][NQ];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+#pragma unroll
+          for (int q = 0; q < NQ; ++q) v[u][q] = make_uint4(0u, 0u, 0u, 0u);
+          if (u < n) {
+            const T* p = x_src + (int64_t)col[k + u] * ld_src + f0;
+#pragma unroll
+            for (int q = 0; q < NQ; ++q) v[u][q] = ld_quad<false>(p + q * E);
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          if (u < n) {
+#pragma unroll
+            for (int q = 0; q < NQ; ++q) {
+              float f[E];
+              Quad<T>::unpack(v[u][q], f);
+#pragma unroll
+              for (int c = 0; c < E; ++c) acc[q * E + c] = __fadd_rn(acc[q * E + c], f[c]);
+            }
+          }
+        }
+      }
+    }
+    for (; !kTail && k + U <= end; k += U) {
       int idx[U];
 #pragma unroll
       for (int u = 0; u < U; ++u) idx[u] = col[k + u];
@@ -394,7 +491,7 @@ __global__ __launch_bounds__(256) void k_agg_q(const int32_t* __restrict__ rowpt
           for (int c = 0; c < E; ++c) acc[q * E + c] = __fadd_rn(acc[q * E + c], f[c]);
         }
     }
-    for (; k < end; ++k) {
+    for (; !kTail && k < end; ++k) {
       const T* p = x_src + (int64_t)col[k] * ld_src + f0;
       uint4 v[NQ];
 #pragma unroll
@@ -448,6 +545,9 @@ int agg_nq_env() {
 int agg_nq(int combine) {
   const int env = agg_nq_env();
   if (env) return env;
+  // with the batched tail the 1-quad kernels are as fast or faster for every mode (profiles/r01_agg_tail.txt):
+  // the wide lanes only paid off while short rows were walked one neighbour at a time
+  if (agg_tail_batched()) return 1;
   return combine == HGIN_COMBINE_CONCAT ? 1 : 4;
 }
 
@@ -457,35 +557,26 @@ int launch_agg_q(int lanes_needed, const int32_t* rowptr, const int32_t* col, in
                  T* out, int64_t ld_out, hipStream_t s, const char* what) {
   constexpr int kU = NQ >= 4 ? 4 : 8;
   const bool nt = combine == HGIN_COMBINE_CONCAT;
-#define HGIN_AGGQ_CASE(GV)                                                                                       \
-  if (lanes_needed <= GV) {                                                                                     \
-    const int64_t blocks = ceil_div(ceil_div(n_rows, kWave / GV), 256 / kWave);                                 \
-    if (nt)                                                                                                     \
-      k_agg_q<T, NQ, GV, kU, true><<<dim3((unsigned)blocks), 256, 0, s>>>(rowptr, col, n_rows, x_src, ld_src,   \
-                                                                         f_src, x_dst, ld_dst, f_dst, eps,      \
-                                                                         combine, out, ld_out);                 \
-    else                                                                                                        \
-      k_agg_q<T, NQ, GV, kU, false><<<dim3((unsigned)blocks), 256, 0, s>>>(rowptr, col, n_rows, x_src, ld_src,  \
-                                                                          f_src, x_dst, ld_dst, f_dst, eps,     \
-                                                                          combine, out, ld_out);                \
-    return check_launch(what);                                                                                  \
+  const bool tail = agg_tail_batched();
+#define HGIN_AGGQ_L(GV, NTV, TAIL, BLOCKS)                                                                      \
+  k_agg_q<T, NQ, GV, kU, NTV, TAIL><<<dim3((unsigned)(BLOCKS)), 256, 0, s>>>(rowptr, col, n_rows, x_src, ld_src, \
+                                                                            f_src, x_dst, ld_dst, f_dst, eps,   \
+                                                                            combine, out, ld_out)
+#define HGIN_AGGQ_G(GV)                                                                 \
+  {                                                                                     \
+    const int64_t blocks = ceil_div(ceil_div(n_rows, kWave / GV), 256 / kWave);         \
+    if (nt) { if (tail) HGIN_AGGQ_L(GV, true, true, blocks); else HGIN_AGGQ_L(GV, true, false, blocks); } \
+    else { if (tail) HGIN_AGGQ_L(GV, false, true, blocks); else HGIN_AGGQ_L(GV, false, false, blocks); } \
+    return check_launch(what);                                                          \
   }
-  HGIN_AGGQ_CASE(2)
-  HGIN_AGGQ_CASE(4)
-  HGIN_AGGQ_CASE(8)
-  HGIN_AGGQ_CASE(16)
-  HGIN_AGGQ_CASE(32)
-#undef HGIN_AGGQ_CASE
-  const int64_t blocks = ceil_div(n_rows, 256 / kWave);
-  if (nt)
-    k_agg_q<T, NQ, 64, kU, true><<<dim3((unsigned)blocks), 256, 0, s>>>(rowptr, col, n_rows, x_src, ld_src, f_src,
-                                                                        x_dst, ld_dst, f_dst, eps, combine, out,
-                                                                        ld_out);
-  else
-    k_agg_q<T, NQ, 64, kU, false><<<dim3((unsigned)blocks), 256, 0, s>>>(rowptr, col, n_rows, x_src, ld_src, f_src,
-                                                                         x_dst, ld_dst, f_dst, eps, combine, out,
-                                                                         ld_out);
-  return check_launch(what);
+  if (lanes_needed <= 2) HGIN_AGGQ_G(2)
+  if (lanes_needed <= 4) HGIN_AGGQ_G(4)
+  if (lanes_needed <= 8) HGIN_AGGQ_G(8)
+  if (lanes_needed <= 16) HGIN_AGGQ_G(16)
+  if (lanes_needed <= 32) HGIN_AGGQ_G(32)
+  HGIN_AGGQ_G(64)
+#undef HGIN_AGGQ_G
+#undef HGIN_AGGQ_L
 }
 
 // Try the wide-lane kernel with nq quads per lane; returns -1000 when the shapes do not allow it.
