@@ -19,7 +19,7 @@ using f32x16 = __attribute__((ext_vector_type(16))) float;
 // the M range is split over S workgroups per output tile (S chosen to fill the 256 CUs); each writes an
 // fp32 partial slab, and k_slab_reduce adds the slabs in split order — deterministic, no atomics.
 // Inner tile: 32 rows of M per stage.  A thread loads 4 consecutive rows x 4 columns of A (and of B):
-// read as row float4s (lanes 0-31 cover one row's 512 B, coalesced) and written transposed — the same 16
+// read as row float4s (8 lanes cover a 128-B segment of a row) and written transposed — the same 16
 // values regrouped as column float4s over the 4 rows, no shuffles — into [n][m] / [k][m] LDS images with
 // 36-float rows.  Lane half h owns rows m = 16h .. 16h+15 of the stage, so an MFMA k-step st pairs rows st
 // and 16 + st and a lane reads 4 k-steps of its operand with one ds_read_b128 (conflict-free: the 16 lanes
@@ -144,11 +144,15 @@ __global__ __launch_bounds__(256, (kPro && !kLateZ) ? 2 : 3) void k_gemm_tn_part
 #pragma unroll
       for (int e = 0; e < 16; ++e) acc[a][b][e] = 0.0f;
 
-  const int c4 = (tid & 31) * 4;   // B: 4 columns inside the 128-wide tile
-  const int r4 = (tid >> 5) * 4;   // B: 4 rows inside the 32-row stage
+  // Row quads vary fastest across lanes: the 8 lanes of one column quad cover the stage's 32 rows, so each
+  // 16-lane store group writes two column runs of 16 words each (conflict-free banks; with columns varying
+  // fastest all 16 lanes hit the same in-row offset of rows 4 apart: 8-way conflicts, SQ_LDS_BANK_CONFLICT
+  // 3.8x the LDS-active cycles).  Global loads stay full 128-B row segments (8 column quads per row).
+  const int c4 = (tid >> 3) * 4;   // B: 4 columns inside the 128-wide tile
+  const int r4 = (tid & 7) * 4;    // B: 4 rows inside the 32-row stage
   // A: the same 4 x 4 blocks over TNR columns (TNR = 32: threads 0-63 only)
-  const int c4a = TNR == 128 ? c4 : (tid & 7) * 4;
-  const int r4a = TNR == 128 ? r4 : (tid >> 3) * 4;
+  const int c4a = TNR == 128 ? c4 : (tid >> 3) * 4;
+  const int r4a = TNR == 128 ? r4 : (tid & 7) * 4;
   const bool stage_a = TNR == 128 || tid < 64;   // wave-uniform
   float4 va[4], vb[4];
   float4 vz[4];                                  // kPro: z of the A block
