@@ -468,7 +468,7 @@ __global__ __launch_bounds__(256) void k_slab_reduce2(const float* __restrict__ 
 // bf16 operands (cfg5): out[N, K] (fp32) = A^T [B1 | B2] on v_mfma_f32_32x32x16_bf16.  A bf16 fragment
 // holds 8 consecutive k (= 8 consecutive rows m here) of one column, but both operands are stored
 // m-major, so each stage is transposed on its way into LDS: a thread loads an 8 x 8 block (8 rows m x
-// 16 B of columns; 16 lanes cover a 256-B row segment, coalesced), transposes it in registers (16-bit
+// 16 B of columns; a wave-load covers 8 rows x 128-B segments), transposes it in registers (16-bit
 // lane shuffles of 32 words) and writes 8 column-runs of 8 m as 16-B stores into [col][m] images with
 // 144-B rows, from which every fragment is one conflict-free ds_read_b128 as in the NT kernel.  Waves 0-1
 // stage A, waves 2-3 stage B.  64 rows of M per stage, register prefetch of the next stage.
@@ -497,8 +497,11 @@ __global__ __launch_bounds__(256, 2) void k_gemm_tn_bf16_partial(const uint16_t*
   const int64_t mb = work.split * rows_per_split;
   const int64_t me = mb + rows_per_split < M ? mb + rows_per_split : M;
   const bool isB = tid >= 128;
-  const int cq = tid & 15;          // 8-column chunk of the 128-wide tile
-  const int rb = (tid & 127) >> 4;  // 8-row block of the 64-row stage
+  // row blocks vary fastest across lanes: a ds_write_b128 lane group (8 lanes) then writes one column run
+  // of 8 x 16 B (conflict-free); with the column chunks fastest its 8 lanes hit rows 8 apart = 288 words,
+  // one bank group: 8-way conflicts (SQ_LDS_BANK_CONFLICT 6.5x the LDS-active cycles)
+  const int rb = tid & 7;           // 8-row block of the 64-row stage
+  const int cq = (tid & 127) >> 3;  // 8-column chunk of the 128-wide tile
   uint16_t* T = isB ? Bt : At;
 
   f32x16 acc[2][2];
