@@ -606,7 +606,160 @@ __global__ __launch_bounds__(256, 2) void k_gemm_tn_bf16_partial(const uint16_t*
     }
 }
 
+
+// bf16 TN with hardware-transposed fragment reads (gfx950 ds_read_b64_tr_b16): the 64-row stages of A [m][n]
+// and B [m][k] go to LDS exactly as loaded (16-B chunks, m-major rows of 128 bf16 = 256 B, no register
+// transpose), and each MFMA fragment — 8 consecutive m of one column — is gathered by two transposed reads
+// (4 rows x 16 columns per 16-lane group each).  Image layout (b) of cdna_hip_programming.md T10: chunk ch of
+// row r at 256 r + 16 (ch ^ (((r & 3) << 2) | ((r >> 2) & 3))): the 16-B stores and both transposed reads
+// are bank-conflict-free (checked by enumeration).  Waves 0-1 stage A, waves 2-3 B; register prefetch of the
+// next stage under the MFMAs; 2 x 2 waves of 64 x 64 outputs.
+using bf16x4 = __attribute__((ext_vector_type(4))) __bf16;
+typedef bf16x4 __attribute__((address_space(3))) lds_bf16x4;
+
+__device__ __forceinline__ int tr_img_off(int row, int ch) {   // byte offset in a [64][256 B] image
+  return 256 * row + 16 * (ch ^ (((row & 3) << 2) | ((row >> 2) & 3)));
+}
+
+template <bool kVec>
+__global__ __launch_bounds__(256, 2) void k_gemm_tn_bf16_tr(const uint16_t* __restrict__ A, int64_t lda,
+                                                            const uint16_t* __restrict__ B1, int64_t ldb1,
+                                                            const uint16_t* __restrict__ B2, int64_t ldb2, int64_t K1,
+                                                            int64_t M, int64_t N, int64_t K, int64_t rows_per_split,
+                                                            float* __restrict__ slab, TnGrid grid) {
+  __shared__ __attribute__((aligned(16))) uint16_t smem[2 * 64 * 128];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const TnWork work = tn_work(grid);
+  if (!work.valid) return;
+  const int64_t n0 = work.n0;
+  const int64_t k0 = work.k0;
+  const int64_t mb = work.split * rows_per_split;
+  const int64_t me = mb + rows_per_split < M ? mb + rows_per_split : M;
+  const bool isB = tid >= 128;
+  const int ch = tid & 15;            // 16-B chunk (8 columns) of a 256-B row
+  const int r0 = (tid & 127) >> 4;    // rows r0 + 8 i of the 64-row stage
+  char* const img = reinterpret_cast<char*>(smem) + (isB ? 64 * 256 : 0);
+
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[a][b][e] = 0.0f;
+
+  uint4 v[8];
+  const int64_t c0 = (isB ? k0 : n0) + 8 * ch;
+  const int64_t lim = isB ? K : N;
+  const uint16_t* vbase = !isB ? A + c0 : (c0 < K1 ? B1 + c0 : B2 + (c0 - K1));
+  const int64_t vld = !isB ? lda : (c0 < K1 ? ldb1 : ldb2);
+  // kVec (16-B aligned rows, N, K, K1 multiples of 8): a chunk lies wholly inside or outside its matrix
+  auto load_stage = [&](int64_t m0) {
+    if constexpr (kVec) {
+      const bool cin = c0 < lim;
+      const uint16_t* p = vbase + (m0 + r0) * vld;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const bool ok = cin && m0 + r0 + 8 * i < me;
+        v[i] = ok ? *reinterpret_cast<const uint4*>(p + 8 * i * vld) : make_uint4(0u, 0u, 0u, 0u);
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int64_t gm = m0 + r0 + 8 * i;
+        uint32_t t[8];
+#pragma unroll
+        for (int c = 0; c < 8; ++c) {
+          const int64_t k = c0 + c;
+          t[c] = 0u;
+          if (gm < me && k < lim)
+            t[c] = !isB ? A[gm * lda + k] : (k < K1 ? B1[gm * ldb1 + k] : B2[gm * ldb2 + (k - K1)]);
+        }
+        v[i] = make_uint4(t[0] | (t[1] << 16), t[2] | (t[3] << 16), t[4] | (t[5] << 16), t[6] | (t[7] << 16));
+      }
+    }
+  };
+  auto store_stage = [&]() {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) *reinterpret_cast<uint4*>(img + tr_img_off(r0 + 8 * i, ch)) = v[i];
+  };
+  // per-lane byte offsets of the two transposed reads of each fragment (kb adds 16 rows = 4096 B):
+  // lane 4q + p of 16-lane group g reads rows 8 (g >> 1) + 4 half + q, columns cb + 16 (g & 1) + 4p .. + 3
+  const int g = lane >> 4, q = (lane >> 2) & 3, pp = lane & 3;
+  int ra[2][2], rbo[2][2];   // [tile][half]
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int row = 8 * (g >> 1) + 4 * h + q;
+      const int ca = wm * 64 + t * 32 + 16 * (g & 1);
+      const int cb = wn * 64 + t * 32 + 16 * (g & 1);
+      ra[t][h] = tr_img_off(row, ca / 8 + (pp >> 1)) + 8 * (pp & 1);
+      rbo[t][h] = 64 * 256 + tr_img_off(row, cb / 8 + (pp >> 1)) + 8 * (pp & 1);
+    }
+  const char* lds = reinterpret_cast<const char*>(smem);
+  auto tr = [&](int off) {
+    return __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(lds + off));
+  };
+  load_stage(mb);
+  store_stage();
+  __syncthreads();
+  for (int64_t m0 = mb; m0 < me; m0 += kTnBMh) {
+    const bool more = m0 + kTnBMh < me;
+    if (more) load_stage(m0 + kTnBMh);
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int kb = 0; kb < kTnBMh / 16; ++kb) {
+      bf16x8 fa[2], fb[2];
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        const bf16x4 a0 = tr(ra[t][0] + kb * 4096), a1 = tr(ra[t][1] + kb * 4096);
+        const bf16x4 b0 = tr(rbo[t][0] + kb * 4096), b1 = tr(rbo[t][1] + kb * 4096);
+        fa[t] = __builtin_shufflevector(a0, a1, 0, 1, 2, 3, 4, 5, 6, 7);
+        fb[t] = __builtin_shufflevector(b0, b1, 0, 1, 2, 3, 4, 5, 6, 7);
+      }
+#pragma unroll
+      for (int tm = 0; tm < 2; ++tm)
+#pragma unroll
+        for (int tn = 0; tn < 2; ++tn)
+          acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[tm], fb[tn], acc[tm][tn], 0, 0, 0);
+    }
+    __builtin_amdgcn_s_setprio(0);
+    if (more) {
+      __syncthreads();
+      store_stage();
+      __syncthreads();
+    }
+  }
+  float* out = slab + work.split * N * K;
+  const int li = lane & 31, lh = lane >> 5;
+#pragma unroll
+  for (int tm = 0; tm < 2; ++tm)
+#pragma unroll
+    for (int tn = 0; tn < 2; ++tn) {
+      const int64_t k = k0 + wn * 64 + tn * 32 + li;
+      if (k >= K) continue;
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int64_t n = n0 + wm * 64 + tm * 32 + (e & 3) + 8 * (e >> 2) + 4 * lh;
+        if (n < N) out[n * K + k] = acc[tm][tn][e];
+      }
+    }
+}
+
 bool tn_is_small(int64_t N, int64_t K) { return N < 16 || K < 16; }
+
+// bf16 dW kernel: transposed LDS reads (default) or the register-transposing kernel (HGIN_TN_BF16=regt).
+bool tn_bf16_tr() {
+  static const bool v = [] {
+    const char* e = getenv("HGIN_TN_BF16");
+    return !(e && std::string(e) == "regt");
+  }();
+  return v;
+}
 
 // Workgroups a split-M launch aims for (HGIN_TN_WGS, <= 1024 = the workspace sizing target).  768 = one
 // resident round at 3 workgroups per CU: measured (profiles/r01_gemm_variants_*.txt) 1.35x faster than 1024
@@ -735,10 +888,16 @@ int gemm_tn_impl(const char* what, const T* a, int64_t lda, const T* b1, int64_t
     const TnGrid tg{128, tiles_n, tiles_n * ceil_div(K, 128), tiles_n * ceil_div(K, 128) * S_eff, xcd_remap_enabled()};
     dim3 grid((unsigned)(tg.xcd ? round_up8(tg.n_work) : tg.n_work));
     HGIN_ARG_CHECK(!pro_in, "%s: no fused prologue for bf16", what);
-    if (vec)
+    if (tn_bf16_tr()) {
+      if (vec && N % 8 == 0 && K % 8 == 0)
+        k_gemm_tn_bf16_tr<true><<<grid, 256, 0, s>>>(a, lda, b1, ldb1, b2, ldb2, k1, M, N, K, rows, slab, tg);
+      else
+        k_gemm_tn_bf16_tr<false><<<grid, 256, 0, s>>>(a, lda, b1, ldb1, b2, ldb2, k1, M, N, K, rows, slab, tg);
+    } else if (vec) {
       k_gemm_tn_bf16_partial<true><<<grid, 256, 0, s>>>(a, lda, b1, ldb1, b2, ldb2, k1, M, N, K, rows, slab, tg);
-    else
+    } else {
       k_gemm_tn_bf16_partial<false><<<grid, 256, 0, s>>>(a, lda, b1, ldb1, b2, ldb2, k1, M, N, K, rows, slab, tg);
+    }
   } else {
     tile_n = N <= 32 ? 32 : 128;
     const int64_t tiles_n = ceil_div(N, tile_n);
