@@ -598,6 +598,166 @@ int try_agg_wide(int nq, const int32_t* rowptr, const int32_t* col, int64_t n_ro
   return -1000;
 }
 
+// ---------------------------------------------------------------------------------------------------
+// Software-pipelined persistent walk (HGIN_AGG_PIPE = 1, the default; 0 selects the kernels above).
+// The kernels above pay up to four dependent memory round trips per destination row — rowptr, then the
+// row's col entries, then the neighbour rows, then the self-term row — and a wave exits after one row per
+// lane group.  Here every wave loops over rows r, r + S, r + 2S, ... (S = resident lane groups of the
+// grid) and, in the iteration that gathers row r, also issues rowptr of row r + 2S, the first col chunk of
+// row r + S (one coalesced G-lane load; lane j holds col[beg + j], broadcast to the group by ds_bpermute)
+// and row r's self-term quad: one round trip per row.  Per-feature sums stay sequential in edge order
+// (bit-identical to the kernels above and to CPU scatter_add_).  One 16-B quad per lane: f_src, f_dst <=
+// G * E elements (E = 4 fp32 / 8 bf16).  The walk's trip count is the wave's largest row (wave-uniform,
+// so every lane reaches the broadcasts); lanes past their row's end load nothing.
+// Measured (tools/agg_bench.py, profiles/r01_agg_pipe.txt): bf16 1.7-1.9 % faster over the cfg2 / cfg3 relation
+// shapes (cfg3 backward +7.8 %), fp32 6-9 % slower (fewer resident waves: 5-6 per SIMD against the one-row
+// kernels' short-lived 8), so the default is the pipelined walk for bf16 and the batched-tail kernel for fp32.
+// HGIN_AGG_PIPE = 0 / 1 forces one choice for both element types.
+template <typename T>
+bool agg_pipe_enabled() {
+  static const int v = [] {
+    const char* e = getenv("HGIN_AGG_PIPE");
+    return e ? atoi(e) : -1;
+  }();
+  return v >= 0 ? v != 0 : sizeof(T) == 2;
+}
+
+template <int G>
+__device__ __forceinline__ int wave_max_over_groups(int v) {
+#pragma unroll
+  for (int off = G; off < kWave; off <<= 1) v = max(v, __shfl_xor(v, off));
+  return v;
+}
+
+template <typename T, int G, int U, bool NT>
+__global__ __launch_bounds__(256) void k_agg_pipe(const int32_t* __restrict__ rowptr, const int32_t* __restrict__ col,
+                                                  int64_t n_rows, const T* __restrict__ x_src, int64_t ld_src,
+                                                  int f_src, const T* __restrict__ x_dst, int64_t ld_dst, int f_dst,
+                                                  const float* __restrict__ eps, int combine, T* __restrict__ out,
+                                                  int64_t ld_out) {
+  static_assert(G % U == 0, "a col chunk must hold whole batches");
+  constexpr int E = Quad<T>::E;
+  constexpr int kRowsPerWave = kWave / G;
+  const int lane = threadIdx.x & (kWave - 1);
+  const int grp = lane / G;
+  const int gl = lane % G;
+  const int64_t S = (int64_t)gridDim.x * (blockDim.x / kWave) * kRowsPerWave;
+  int64_t r0 = ((int64_t)blockIdx.x * (blockDim.x / kWave) + threadIdx.x / kWave) * kRowsPerWave;
+  int64_t r = r0 + grp;
+  const int f0 = gl * E;
+  const bool src_lane = f0 < f_src;
+  const bool self_lane = combine != HGIN_COMBINE_NONE && f0 < f_dst;
+  const float s = combine != HGIN_COMBINE_NONE ? __fadd_rn(1.0f, eps[0]) : 1.0f;
+
+  int beg = 0, end = 0, begn = 0, endn = 0;
+  if (r < n_rows) { beg = rowptr[r]; end = rowptr[r + 1]; }
+  if (r + S < n_rows) { begn = rowptr[r + S]; endn = rowptr[r + S + 1]; }
+  int cur = gl < end - beg ? col[beg + gl] : 0;
+  for (; r0 < n_rows; r0 += S, r += S) {
+    // prefetches for the next two rows of this lane group, issued with this row's loads
+    int begnn = 0, endnn = 0;
+    if (r + 2 * S < n_rows) { begnn = rowptr[r + 2 * S]; endnn = rowptr[r + 2 * S + 1]; }
+    const int curn = gl < endn - begn ? col[begn + gl] : 0;
+    const bool valid = r < n_rows;
+    uint4 xd = make_uint4(0u, 0u, 0u, 0u);
+    if (valid && self_lane) xd = ld_quad<NT>(x_dst + r * ld_dst + f0);
+
+    const int n = end - beg;     // 0 past the last row
+    const int n_wave = wave_max_over_groups<G>(n);
+    float acc[E];
+#pragma unroll
+    for (int c = 0; c < E; ++c) acc[c] = 0.0f;
+    for (int k = 0; k < n_wave; k += U) {
+      if (k != 0 && (k & (G - 1)) == 0) cur = k + gl < n ? col[beg + k + gl] : 0;   // rows longer than G
+      uint4 v[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int idx = __shfl(cur, grp * G + ((k + u) & (G - 1)));
+        v[u] = make_uint4(0u, 0u, 0u, 0u);
+        if (k + u < n && src_lane) v[u] = ld_quad<false>(x_src + (int64_t)idx * ld_src + f0);
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        if (k + u < n) {
+          float f[E];
+          Quad<T>::unpack(v[u], f);
+#pragma unroll
+          for (int c = 0; c < E; ++c) acc[c] = __fadd_rn(acc[c], f[c]);
+        }
+      }
+    }
+    if (valid) {
+      T* __restrict__ orow = out + r * ld_out;
+      float xs[E];
+      Quad<T>::unpack(xd, xs);
+      if (combine == HGIN_COMBINE_ADD) {
+#pragma unroll
+        for (int c = 0; c < E; ++c) acc[c] = __fadd_rn(acc[c], __fmul_rn(s, xs[c]));
+      }
+      if (src_lane) st_quad<NT>(orow + f0, Quad<T>::pack(acc));
+      if (combine == HGIN_COMBINE_CONCAT && self_lane) {
+#pragma unroll
+        for (int c = 0; c < E; ++c) xs[c] = __fmul_rn(s, xs[c]);
+        st_quad<NT>(orow + f_src + f0, Quad<T>::pack(xs));
+      }
+    }
+    beg = begn; end = endn; begn = begnn; endn = endnn; cur = curn;
+  }
+}
+
+template <typename F>
+int64_t agg_resident_blocks(F kernel) {
+  int per_cu = 0, dev = 0, cus = 256;
+  hipDeviceProp_t prop;
+  if (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&prop, dev) == hipSuccess)
+    cus = prop.multiProcessorCount;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, 256, 0) != hipSuccess || per_cu <= 0) per_cu = 4;
+  return (int64_t)per_cu * cus;
+}
+
+template <typename T, int G, int U, bool NT>
+int launch_agg_pipe_g(const int32_t* rowptr, const int32_t* col, int64_t n_rows, const T* x_src, int64_t ld_src,
+                      int f_src, const T* x_dst, int64_t ld_dst, int f_dst, const float* eps, int combine, T* out,
+                      int64_t ld_out, hipStream_t s) {
+  static const int64_t slots = agg_resident_blocks(k_agg_pipe<T, G, U, NT>);
+  const int64_t need = ceil_div(n_rows, (int64_t)(256 / G));
+  const int64_t blocks = need < slots ? need : slots;
+  k_agg_pipe<T, G, U, NT><<<dim3((unsigned)blocks), 256, 0, s>>>(rowptr, col, n_rows, x_src, ld_src, f_src, x_dst,
+                                                                  ld_dst, f_dst, eps, combine, out, ld_out);
+  return HGIN_OK;
+}
+
+// Returns -1000 when the shapes do not fit the pipelined kernel (one aligned quad per lane, <= 64 lanes).
+template <typename T>
+int try_agg_pipe(const int32_t* rowptr, const int32_t* col, int64_t n_rows, const T* x_src, int64_t ld_src, int f_src,
+                 const T* x_dst, int64_t ld_dst, int f_dst, const float* eps, int combine, T* out, int64_t ld_out,
+                 hipStream_t s, const char* what) {
+  constexpr int E = Quad<T>::E;
+  const int fd = combine == HGIN_COMBINE_NONE ? 0 : f_dst;
+  if (!agg_pipe_enabled<T>() || f_src % E || fd % E || !aligned16(x_src) || ld_src % E || !aligned16(out) ||
+      ld_out % E)
+    return -1000;
+  if (fd && (!aligned16(x_dst) || ld_dst % E)) return -1000;
+  const int widest = f_src > fd ? f_src : fd;
+  const int lanes = (widest + E - 1) / E;
+  if (lanes < 1 || lanes > kWave) return -1000;
+  const bool nt = combine == HGIN_COMBINE_CONCAT;
+  int rc;
+#define HGIN_PIPE_G(GV, UV)                                                                                      \
+  rc = nt ? launch_agg_pipe_g<T, GV, UV, true>(rowptr, col, n_rows, x_src, ld_src, f_src, x_dst, ld_dst, f_dst, eps, \
+                                               combine, out, ld_out, s)                                         \
+          : launch_agg_pipe_g<T, GV, UV, false>(rowptr, col, n_rows, x_src, ld_src, f_src, x_dst, ld_dst, f_dst, eps, \
+                                                combine, out, ld_out, s);
+  if (lanes <= 4) { HGIN_PIPE_G(4, 4) }
+  else if (lanes <= 8) { HGIN_PIPE_G(8, 8) }
+  else if (lanes <= 16) { HGIN_PIPE_G(16, 8) }
+  else if (lanes <= 32) { HGIN_PIPE_G(32, 8) }
+  else { HGIN_PIPE_G(64, 8) }
+#undef HGIN_PIPE_G
+  if (rc) return rc;
+  return check_launch(what);
+}
+
 int check_aggregate_args(const char* what, const int32_t* rowptr, int64_t n_rows, int64_t ld_src, int64_t f_src,
                          const void* x_dst, int64_t ld_dst, int64_t f_dst, const float* eps, int combine,
                          const void* out, int64_t ld_out) {
@@ -638,6 +798,11 @@ extern "C" int hgin_aggregate_bf16(const int32_t* rowptr, const int32_t* col, in
                     dst_ok && (f_src > 0 || f_dst > 0);
   const int fd = combine == HGIN_COMBINE_CONCAT ? (int)f_dst : 0;
   const int64_t widest = f_src > fd ? f_src : fd;
+  {
+    const int rc = try_agg_pipe<uint16_t>(rowptr, col, n_rows, x_src, ld_src, (int)f_src, x_dst, ld_dst, (int)f_dst,
+                                          eps, combine, out, ld_out, s, "hgin_aggregate_bf16");
+    if (rc != -1000) return rc;
+  }
   if (vec8 && agg_nq(combine) > 1) {
     const int rc = try_agg_wide<uint16_t>(agg_nq(combine), rowptr, col, n_rows, x_src, ld_src, (int)f_src, x_dst, ld_dst,
                                           (int)f_dst, eps, combine, out, ld_out, s, "hgin_aggregate_bf16");
@@ -662,6 +827,11 @@ extern "C" int hgin_aggregate_f32(const int32_t* rowptr, const int32_t* col, int
   const bool vec4 = f_src % 4 == 0 && aligned16(x_src) && ld_src % 4 == 0 && aligned16(out) && ld_out % 4 == 0 &&
                     dst_ok && (f_src > 0 || f_dst > 0);
   const int fd = combine == HGIN_COMBINE_CONCAT ? (int)f_dst : 0;
+  {
+    const int rc = try_agg_pipe<float>(rowptr, col, n_rows, x_src, ld_src, (int)f_src, x_dst, ld_dst, (int)f_dst, eps,
+                                       combine, out, ld_out, s, "hgin_aggregate_f32");
+    if (rc != -1000) return rc;
+  }
   if (vec4 && agg_nq(combine) > 1) {
     const int rc = try_agg_wide<float>(agg_nq(combine), rowptr, col, n_rows, x_src, ld_src, (int)f_src, x_dst, ld_dst,
                                        (int)f_dst, eps, combine, out, ld_out, s, "hgin_aggregate_f32");

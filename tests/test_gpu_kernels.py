@@ -96,6 +96,35 @@ def test_aggregate_bit_exact(F_src, F_dst, mode):
     assert np.array_equal(out.cpu().numpy(), ref)
 
 
+@pytest.mark.parametrize("F,dtype", [(128, torch.float32), (16, torch.float32), (256, torch.float32),
+                                     (256, torch.bfloat16), (64, torch.bfloat16)])
+@pytest.mark.parametrize("mode", [0, 1, 2])
+def test_aggregate_bit_exact_skewed_rows(F, dtype, mode):
+    """Zipf(1.1) destinations (rows of 0 .. thousands of edges: col chunks reloaded past one lane group,
+    long runs of empty rows) and a uniform tail; more rows than one persistent round of lane groups."""
+    n_src, n_dst = 3000, 40000
+    zipf = _rand_graph(60000, n_src, n_dst, seed=F + mode, zipf=True)
+    unif = _rand_graph(60000, n_src, n_dst, seed=F * 3 + mode)
+    ei = np.concatenate([zipf, unif], 1)
+    g = torch.Generator().manual_seed(F + 7 * mode)
+    x = torch.randn(n_src, F, generator=g).to(dtype)
+    xd = torch.randn(n_dst, F, generator=g).to(dtype)
+    eps = np.float32(0.3125)
+    rowptr, col, _, _ = co.csr_build(ei, 1, n_dst, n_src)
+    assert int(np.diff(rowptr).max()) > 1000
+    ref = torch.from_numpy(co.aggregate(rowptr, col, x.float().numpy(), xd.float().numpy() if mode else None,
+                                        float(eps), mode)).to(dtype)
+    csr = ops.build_csr(torch.from_numpy(ei).to(DEV), 1, n_dst, n_src)
+    out = torch.full((n_dst, F * (2 if mode == 2 else 1)), float("nan"), device=DEV).to(dtype)
+    ops.aggregate_into(csr, x.to(DEV), xd.to(DEV) if mode else None,
+                       torch.tensor([eps], device=DEV) if mode else None, mode, out)
+    got = out.cpu()
+    if dtype == torch.bfloat16:
+        assert torch.equal(got.view(torch.int16), ref.view(torch.int16))
+    else:
+        assert torch.equal(got, ref)
+
+
 def test_aggregate_matches_reference_cpu_op():
     """Against PyG's CPU path itself (index_select + scatter_add_ + cat), bit for bit."""
     g = torch.Generator().manual_seed(5)

@@ -43,7 +43,7 @@ def main():
         out = torch.empty(n_dst, F * (2 if mode == 2 else 1), device="cuda", dtype=dt)
         t = sorted(timeit(lambda: ops.aggregate_into(graph.csr, x, xd, eps, mode, out)) for _ in range(3))[1]
         b = profiling.aggregate_bytes(E, n_dst, F, F if mode else 0, mode, x.element_size())
-        print(f"{os.environ.get('HGIN_AGG_NQ', '-')} {str(dt)[6:]:8s} {name:18s} {t * 1e3:8.1f} us  {b / 1e9:6.2f} GB  {b / (t / 1e3) / 1e9:7.0f} GB/s")
+        print(f"{os.environ.get('HGIN_AGG_PIPE', '-')} {str(dt)[6:]:8s} {name:18s} {t * 1e3:8.1f} us  {b / 1e9:6.2f} GB  {b / (t / 1e3) / 1e9:7.0f} GB/s")
         del ei, graph, x, xd, out
         torch.cuda.empty_cache()
 
