@@ -13,12 +13,12 @@ gradient.  The optimizer must be capturable (``torch.optim.Adam(..., capturable=
 """
 from __future__ import annotations
 
-from typing import Sequence
+from typing import Optional, Sequence
 
 import torch
 
 from .store import GraphStore, PaddedBatch
-from .train import train_step
+from .train import mape, train_step
 
 
 class CapturedTrainStep:
@@ -47,4 +47,62 @@ class CapturedTrainStep:
         """One training step on the graphs ``ids``; returns the device loss_value (no host sync)."""
         self.store.collate_into(ids, self.batch)
         self.graph.replay()
+        return self.loss
+
+
+def _forward_backward(model: torch.nn.Module, graph) -> torch.Tensor:
+    """train.py:33-43 without zero_grad / opt.step: forward (fused head + MAPE, §8 F3), sqrt, backward."""
+    if hasattr(model, "forward_loss"):
+        _, loss_value = model.forward_loss(graph.x_dict(), graph.edge_index_dict(), graph.batch["path"], graph.y,
+                                           getattr(graph, "m_valid", None))
+    else:
+        loss_value = mape(model(graph.x_dict(), graph.edge_index_dict(), graph.batch["path"]), graph.y.reshape(-1, 1))
+    torch.sqrt(loss_value).backward()
+    return loss_value.detach()
+
+
+class CapturedStaticStep:
+    """hipGraph replay of train.py's step on a resident graph whose tensors never move (cfg2-cfg5: one large
+    static graph per rank, the bench workload).
+
+    An eager step issues ~90 launches from Python (autograd, ctypes); a replay issues them as one graph.  At
+    the bench sizes the two measure the same (cfg2 5.76 vs 5.74 ms, cfg5 101.4 vs 101.5 ms: the host runs
+    ahead of a GPU-bound step, and the ~0.2 ms of kernel-to-kernel gaps per cfg2 step remain in a replay),
+    so bench.py uses it only with ``--graph``.  Capture protocol (the standard whole-step one): a few eager warm-up steps on a side stream
+    (CSR / CSC caches, allocator pools, optimizer state), gradients set to None, then forward + loss +
+    backward captured — the captured backward (re)writes every .grad in place on each replay — followed by
+    the optimizer step.  With a ``reducer`` (N > 1) the RCCL gradient all-reduce runs eagerly between two
+    replays (forward/backward, then the optimizer), so no collective is captured.  The optimizer must be
+    capturable (``torch.optim.Adam(..., capturable=True)``).  Every kernel is the eager step's, in the same
+    order, so a replay equals an eager step with the same optimizer bit for bit (tests/test_gpu_model.py)."""
+
+    def __init__(self, model: torch.nn.Module, opt: torch.optim.Optimizer, graph, reducer=None, warmup: int = 2):
+        if not all(g.get("capturable", False) for g in opt.param_groups):
+            raise ValueError("CapturedStaticStep needs a capturable optimizer (e.g. Adam(..., capturable=True))")
+        self.model, self.opt, self.graph, self.reducer = model, opt, graph, reducer
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            for _ in range(max(int(warmup), 1)):
+                train_step(model, opt, graph, reducer=reducer)
+        torch.cuda.current_stream().wait_stream(side)
+        torch.cuda.synchronize()
+        opt.zero_grad(set_to_none=True)
+        self.fwd_bwd = torch.cuda.CUDAGraph()
+        self.opt_graph: Optional[torch.cuda.CUDAGraph] = None
+        with torch.cuda.graph(self.fwd_bwd):
+            self.loss = _forward_backward(model, graph)
+            if reducer is None:
+                opt.step()
+        if reducer is not None:
+            self.opt_graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(self.opt_graph, pool=self.fwd_bwd.pool()):
+                opt.step()
+
+    def step(self) -> torch.Tensor:
+        """One training step; returns the device loss_value (no host sync)."""
+        self.fwd_bwd.replay()
+        if self.opt_graph is not None:
+            self.reducer.sync()
+            self.opt_graph.replay()
         return self.loss

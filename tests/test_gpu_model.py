@@ -177,3 +177,32 @@ def test_full_size_cfg2_step():
     ref = torch.zeros(cfg.n_link, 128, device=DEV).index_add_(0, e[1], x[e[0]])
     agg = ops.aggregate(x, None, None, graph, ops.COMBINE_NONE)
     assert torch.allclose(agg, ref, rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("feat", ["f32", "bf16"])
+def test_captured_static_step_equals_eager(feat):
+    """bench.py's default mode: a hipGraph replay of the whole step (forward, fused head + loss, backward,
+    capturable Adam) runs the eager step's kernels in the same order -> bitwise the same trajectory."""
+    import dataclasses
+
+    from hgin.data import CONFIGS, scaled_config, synthetic_graph
+    from hgin.graphs import CapturedStaticStep
+    from hgin.train import train_step as hip_step
+    cfg = dataclasses.replace(scaled_config(CONFIGS["cfg2"], 0.02, name="cfg2-small"), feat_dtype=feat)
+    g = synthetic_graph(cfg, seed=0, device=DEV)
+    runs = []
+    for mode in ("eager", "graph"):
+        torch.manual_seed(1997)
+        model = HetroGIN(**cfg.model_kwargs({"link": cfg.f_link, "path": cfg.f_path, "node": cfg.f_node})).to(DEV)
+        opt = torch.optim.Adam(lr=1e-3, params=model.parameters(), capturable=True)
+        if mode == "eager":
+            losses = [hip_step(model, opt, g).clone() for _ in range(3)]
+        else:
+            st = CapturedStaticStep(model, opt, g, warmup=1)
+            losses = [torch.zeros(())] + [st.step().clone() for _ in range(2)]
+        torch.cuda.synchronize()
+        runs.append((losses, [p.detach().clone() for p in model.parameters()]))
+    (l_e, p_e), (l_g, p_g) = runs
+    assert torch.equal(l_e[2], l_g[2]) and torch.equal(l_e[1], l_g[1])
+    for a, b in zip(p_e, p_g):
+        assert torch.equal(a, b)
