@@ -263,10 +263,71 @@ int combine_bwd(const char* what, const T* g, int64_t ld_g, const T* x_dst, int6
   return check_launch(what);
 }
 
+// Self-term weight gradient of a GINConv whose inputs are data (ops._GINConvFn's one-TN-pass form, first
+// layer; models.py:210-217 reached from train.py:43): G [N, KG] = g_z^T [aggregate | x_dst] from the dW GEMM.
+//   g_w[:, :f] = G[:, :f];   concat: g_w[:, f:] = (1 + eps) G[:, f:]   (add: g_w is G[:, :f] only)
+//   g_eps = sum_{n, j < KG - f} W[n, w0 + j] G[n, f + j]          (concat: w0 = f; add: w0 = 0)
+// Element i of the flattened G goes to thread i % (blocks * 256) in a fixed order; per-block fixed trees,
+// then k_final_scalar over the block partials.  Replaces 3-5 torch launches (scale, cat, product, sum).
+constexpr int kSelfPerThread = 8;
+
+int64_t self_wgrad_blocks(int64_t N, int64_t KG) {
+  const int64_t b = ceil_div(N * KG > 0 ? N * KG : 1, (int64_t)256 * kSelfPerThread);
+  return b < 512 ? b : 512;
+}
+
+__global__ __launch_bounds__(256) void k_self_wgrad(const float* __restrict__ G, int64_t ldg,
+                                                    const float* __restrict__ W, int64_t ldw, int64_t N, int64_t KG,
+                                                    int64_t f, int64_t w0, int concat, const float* __restrict__ eps,
+                                                    float* __restrict__ gw, int64_t ldgw, float* __restrict__ part) {
+  __shared__ float red[256];
+  const float sc = __fadd_rn(1.0f, eps[0]);
+  const int64_t total = N * KG;
+  const int64_t stride = (int64_t)gridDim.x * 256;
+  float s = 0.0f;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < total; i += stride) {
+    const int64_t n = i / KG, k = i - n * KG;
+    const float v = G[n * ldg + k];
+    if (k < f) {
+      gw[n * ldgw + k] = v;
+    } else {
+      s = __fadd_rn(s, __fmul_rn(W[n * ldw + w0 + (k - f)], v));
+      if (concat) gw[n * ldgw + k] = __fmul_rn(sc, v);
+    }
+  }
+  const float bs = block_sum_fixed(s, red);
+  if (threadIdx.x == 0) part[blockIdx.x] = bs;
+}
+
 }  // namespace
 }  // namespace hgin
 
 using namespace hgin;
+
+extern "C" int hgin_self_wgrad_workspace_size(int64_t N, int64_t KG, size_t* bytes) {
+  HGIN_ARG_CHECK(bytes && N >= 0 && KG >= 0, "hgin_self_wgrad_workspace_size: bad args");
+  *bytes = align_up(sizeof(float) * (size_t)self_wgrad_blocks(N, KG), 256);
+  return HGIN_OK;
+}
+
+extern "C" int hgin_self_wgrad_f32(const float* G, int64_t ldg, const float* W, int64_t ldw, int64_t N, int64_t KG,
+                                   int64_t f, int concat, const float* eps, float* g_w, int64_t ld_gw, float* g_eps,
+                                   void* workspace, size_t workspace_bytes, void* stream) {
+  HGIN_ARG_CHECK(N >= 0 && KG >= 0 && f >= 0 && f <= KG, "hgin_self_wgrad_f32: bad sizes");
+  HGIN_ARG_CHECK(G && W && eps && g_w && g_eps, "hgin_self_wgrad_f32: NULL operand");
+  HGIN_ARG_CHECK(ldg >= KG && ld_gw >= (concat ? KG : f), "hgin_self_wgrad_f32: leading dimension too small");
+  HGIN_ARG_CHECK(ldw >= (concat ? KG : KG - f), "hgin_self_wgrad_f32: W narrower than the self block");
+  const int64_t nblk = self_wgrad_blocks(N, KG);
+  if (!workspace || workspace_bytes < sizeof(float) * (size_t)nblk) {
+    set_error("hgin_self_wgrad_f32: workspace %zu < %zu", workspace_bytes, sizeof(float) * (size_t)nblk);
+    return HGIN_E_WORKSPACE;
+  }
+  hipStream_t s = as_stream(stream);
+  float* part = static_cast<float*>(workspace);
+  k_self_wgrad<<<(unsigned)nblk, 256, 0, s>>>(G, ldg, W, ldw, N, KG, f, concat ? f : 0, concat, eps, g_w, ld_gw, part);
+  k_final_scalar<<<1, 256, 0, s>>>(part, nblk, g_eps);
+  return check_launch("hgin_self_wgrad_f32");
+}
 
 extern "C" int hgin_prelu_bwd_workspace_size(int64_t M, int64_t N, size_t* bytes) {
   HGIN_ARG_CHECK(bytes && M >= 0 && N >= 0, "hgin_prelu_bwd_workspace_size: bad args");

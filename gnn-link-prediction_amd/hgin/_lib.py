@@ -112,6 +112,8 @@ _SIGS = {
                                 _P, _I64, _P, _SZ, _P], _I32),
     "hgin_gin_mlp_bwd_w_bf16": ([_P, _I64, _P, _I64, _P, _P, _I64, _I64, _P, _I64, _I64, _I64, _I64, _P, _I64, _P, _P,
                                  _P, _I64, _P, _SZ, _P], _I32),
+    "hgin_self_wgrad_workspace_size": ([_I64, _I64, ctypes.POINTER(_SZ)], _I32),
+    "hgin_self_wgrad_f32": ([_P, _I64, _P, _I64, _I64, _I64, _I64, _I32, _P, _P, _I64, _P, _P, _SZ, _P], _I32),
     "hgin_combine_bwd_bf16": ([_P, _I64, _P, _I64, _I64, _I64, _P, _P, _I64, _P, _P, _SZ, _P], _I32),
     "hgin_head_mape_workspace_size": ([_I64, _I64, ctypes.POINTER(_SZ)], _I32),
     "hgin_head_mape_fwd_f32": ([_P, _I64, _I64, _I64, _P, _P, _P, _P, _P, _P, _P, _SZ, _P], _I32),

@@ -295,6 +295,21 @@ def mlp_bwd_w(g_y: Tensor, z: Tensor, prelu: Tensor, b1: Tensor, b2: Optional[Te
     return g_w, g_a, g_b, g_z
 
 
+def self_wgrad(G: Tensor, weight: Tensor, f: int, concat: bool, eps: Tensor):
+    """(g_w, g_eps) of a first-layer GINConv from G = g_z^T [aggregate | x_dst] (hgin_self_wgrad_f32):
+    g_w = [G[:, :f] | (1 + eps) G[:, f:]] (concat) or G[:, :f] (add); g_eps = sum(W_self * G[:, f:])."""
+    N, KG = G.shape
+    w = weight if weight.dtype == torch.float32 else weight.float()   # bf16 path: the GEMM's operand copy
+    g_w = torch.empty(N, KG if concat else f, dtype=torch.float32, device=G.device)
+    g_eps = torch.empty(1, dtype=torch.float32, device=G.device)
+    nbytes = ctypes.c_size_t(0)
+    _lib.check(_lib.lib().hgin_self_wgrad_workspace_size(N, KG, ctypes.byref(nbytes)), "self_wgrad_workspace_size")
+    ws = _workspace(nbytes.value, G.device)
+    _lib.call("hgin_self_wgrad_f32", _p(G), G.stride(0), _p(w), w.stride(0), N, KG, f, int(concat), _p(eps), _p(g_w),
+              g_w.stride(0), _p(g_eps), _p(ws), nbytes.value, _stream(G))
+    return g_w, g_eps
+
+
 def gin_mlp_fwd(comb: Tensor, weight: Tensor, bias: Tensor, prelu: Optional[Tensor], accum: Optional[Tensor],
                 save_z: bool = True, comb2: Optional[Tensor] = None):
     """y = prelu([comb | comb2] @ W^T + b) [+ accum]  (prelu None: plain Linear, y = z, nothing saved).
@@ -403,13 +418,10 @@ class _GINConvFn(torch.autograd.Function):
             # [aggregate | x_dst] yields dW and the eps gradient and the [N_dst, K] dX GEMM is skipped.
             if mode == COMBINE_CONCAT:
                 G, g_a, g_b, _ = mlp_bwd_w(g_y, z, prelu, comb[:, :f_src], x_dst)
-                gx = G[:, f_src:]
-                g_w = torch.cat((G[:, :f_src], (1 + eps) * gx), 1) if need_w else None
-                g_eps = (weight[:, f_src:] * gx).sum().reshape(1)
             else:
                 G, g_a, g_b, _ = mlp_bwd_w(g_y, z, prelu, comb, x_dst)
-                g_w = G[:, :f_src].contiguous() if need_w else None
-                g_eps = (weight * G[:, f_src:]).sum().reshape(1)
+            g_w, g_eps = self_wgrad(G, weight, f_src, mode == COMBINE_CONCAT, eps)
+            g_w = g_w if need_w else None
         else:
             g_w, g_a, g_b, _ = mlp_bwd_w(g_y, z, prelu, comb)
         g_acc = g_y if need_acc else None

@@ -152,6 +152,18 @@ int hgin_gin_mlp_bwd_w_f32(const float* g_y, int64_t ld_gy, const float* z, int6
                            int64_t M, int64_t N, int64_t K, float* g_w, int64_t ldw, float* g_prelu, float* g_bias,
                            float* g_z, int64_t ld_gz, void* workspace, size_t workspace_bytes, void* stream);
 
+/* ---- A9: self-term weight gradient of a first-layer GINConv (inputs are data) ---------------------------
+ * Given G[N, KG] = g_z^T [aggregate | x_dst] (hgin_gin_mlp_bwd_w_* over both blocks; f = aggregate width):
+ *   g_w[:, :f] = G[:, :f];  concat != 0: g_w[:, f:KG] = (1 + eps[0]) G[:, f:KG]
+ *   g_eps[0] = sum_{n, j < KG - f} W[n, w0 + j] G[n, f + j]    (w0 = f for concat, 0 for add; W = the Linear weight)
+ * i.e. d loss / d W and d loss / d eps of (1 + eps) * x_dst (models.py:210-215) without forming the [N_dst, K]
+ * input gradient.  Replaces torch's scale / cat / product / sum (3-5 launches) with two.  Deterministic.
+ * workspace: hgin_self_wgrad_workspace_size. */
+int hgin_self_wgrad_workspace_size(int64_t N, int64_t KG, size_t* bytes);
+int hgin_self_wgrad_f32(const float* G, int64_t ldg, const float* W, int64_t ldw, int64_t N, int64_t KG, int64_t f,
+                        int concat, const float* eps, float* g_w, int64_t ld_gw, float* g_eps, void* workspace,
+                        size_t workspace_bytes, void* stream);
+
 /* ---- cfg5: bf16 storage + bf16 MFMA, fp32 accumulate (BASELINE.json configs[4]) ---------------------
  * Same operations and operand conventions as the fp32 entry points above; `uint16_t` = a bfloat16 bit
  * pattern.  Every sum / product is formed in fp32 and each stored bf16 value is rounded once

@@ -375,3 +375,28 @@ def test_linear_two_source_autograd(M, K1, K2, N, act):
         pairs.append((a.weight.grad, ar.grad))
     for got, want in pairs:
         assert float((got.double() - want).norm()) <= 1e-5 * float(want.norm()) + 1e-6
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("concat", [True, False])
+@pytest.mark.parametrize("shape", [(128, 128), (32, 7), (256, 256)])
+def test_self_wgrad(concat, shape):
+    """hgin_self_wgrad_f32: the first-layer GINConv's self-term weight gradient and eps gradient."""
+    from hgin import ops
+    N, f = shape
+    dev = "cuda"
+    gen = torch.Generator().manual_seed(N + f)
+    G = torch.randn(N, 2 * f, generator=gen).to(dev)
+    W = torch.randn(N, 2 * f if concat else f, generator=gen).to(dev)
+    eps = torch.tensor([0.3], device=dev)
+    g_w, g_eps = ops.self_wgrad(G, W, f, concat, eps)
+    if concat:
+        want_w = torch.cat((G[:, :f], (1 + eps) * G[:, f:]), 1)
+        want_eps = (W[:, f:].double() * G[:, f:].double()).sum()
+    else:
+        want_w = G[:, :f]
+        want_eps = (W.double() * G[:, f:].double()).sum()
+    assert torch.equal(g_w, want_w)
+    assert abs(float(g_eps) - float(want_eps)) <= 1e-5 * float((W.abs().double().sum() * G.abs().max()))
+    g_w2, g_eps2 = ops.self_wgrad(G, W, f, concat, eps)
+    assert torch.equal(g_eps, g_eps2) and torch.equal(g_w, g_w2)
