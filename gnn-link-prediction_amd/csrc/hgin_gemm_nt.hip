@@ -40,6 +40,9 @@ struct Src2 {
   const float* p2;
   int64_t ld2;
   int64_t k1;
+  // optional: columns from p2 are (1 + eps2[0]) * p2 (the GIN self term of a concat GINConv, models.py:212-213,
+  // applied as the tile is loaded instead of materialised by the aggregate; same fp32 product, one rounding)
+  const float* eps2 = nullptr;
 };
 
 // ROWS x 32 floats of [p1 | p2] starting at (row0, k0) -> ROWS/32 float4 per thread:
@@ -49,9 +52,11 @@ struct Src2 {
 // output rows / columns that are never stored — so the loads are branch-free and the compiler keeps the
 // prefetch in flight under the MFMAs (a per-load branch made it wait at each join).  Otherwise every
 // element is bounds-checked.
+__device__ __forceinline__ float self_scale(const float* eps2) { return eps2 ? __fadd_rn(1.0f, eps2[0]) : 1.0f; }
+
 template <bool kClean, int ROWS>
 __device__ __forceinline__ void load_tile(float4 (&r)[ROWS / 32], const Src2& s, int64_t row0, int64_t rows,
-                                          int64_t k0, int64_t K, int tid) {
+                                          int64_t k0, int64_t K, int tid, float sc2 = 1.0f) {
   if constexpr (kClean) {
     // select between the loaded VALUES: a select between the two struct fields' addresses would make
     // the compiler copy the by-value kernel argument into scratch
@@ -68,6 +73,7 @@ __device__ __forceinline__ void load_tile(float4 (&r)[ROWS / 32], const Src2& s,
       const float4 v = *reinterpret_cast<const float4*>(base + gr * ld + kk);
       r[i] = v;
     }
+    // (eps2 scaling of a clean p2 tile is applied when the tile is staged: scale_tile)
   } else {
     const int64_t kk = k0 + (tid & 7) * 4;
 #pragma unroll
@@ -78,12 +84,21 @@ __device__ __forceinline__ void load_tile(float4 (&r)[ROWS / 32], const Src2& s,
 #pragma unroll
         for (int c = 0; c < 4; ++c) {
           const int64_t k = kk + c;
-          t[c] = k < K ? (k < s.k1 ? s.p1[gr * s.ld1 + k] : s.p2[gr * s.ld2 + (k - s.k1)]) : 0.0f;
+          t[c] = k < K ? (k < s.k1 ? s.p1[gr * s.ld1 + k] : __fmul_rn(sc2, s.p2[gr * s.ld2 + (k - s.k1)])) : 0.0f;
         }
       }
       r[i] = make_float4(t[0], t[1], t[2], t[3]);
     }
   }
+}
+
+// The eps2 scale of a clean p2 tile, applied at staging time (after the MFMAs the prefetch hides under):
+// scaling inside load_tile would consume the loaded values at once and make the loads wait there.
+template <int ROWS>
+__device__ __forceinline__ void scale_tile(float4 (&r)[ROWS / 32], float sc) {
+#pragma unroll
+  for (int i = 0; i < ROWS / 32; ++i)
+    r[i] = make_float4(__fmul_rn(sc, r[i].x), __fmul_rn(sc, r[i].y), __fmul_rn(sc, r[i].z), __fmul_rn(sc, r[i].w));
 }
 
 template <int ROWS>
@@ -274,7 +289,14 @@ __global__ __launch_bounds__(256, 3) void k_gemm_nt(Src2 A, Src2 B, int64_t M, i
       for (int e = 0; e < 16; ++e) acc[a][b][e] = 0.0f;
 
   float4 ra[BM / 32], rb[BN >= 32 ? BN / 32 : 1];
+  const float sc2 = self_scale(A.eps2);
+  bool scale_a = false;   // ra holds a clean p2 tile still to be scaled by sc2
+  auto load_a = [&](int64_t k0) {
+    load_tile<kClean, BM>(ra, A, m0, M, k0, K, tid, sc2);
+    scale_a = kClean && A.eps2 != nullptr && k0 >= A.k1;
+  };
   auto stage = [&]() {
+    if (scale_a) scale_tile<BM>(ra, sc2);
     if constexpr (kSplit) {
       store_tile_split<BM>(Ash, ra, tid);
       store_tile_split<BN>(Bsh, rb, tid);
@@ -283,14 +305,14 @@ __global__ __launch_bounds__(256, 3) void k_gemm_nt(Src2 A, Src2 B, int64_t M, i
       store_tile<BN>(Bs, rb, tid);
     }
   };
-  load_tile<kClean, BM>(ra, A, m0, M, 0, K, tid);
+  load_a(0);
   load_tile<kClean, BN>(rb, B, n0, N, 0, K, tid);
   stage();
   __syncthreads();
   for (int64_t k0 = 0; k0 < K; k0 += kBK) {
     const bool more = k0 + kBK < K;
     if (more) {   // next K-tile's global loads stay in flight under this K-tile's MFMAs
-      load_tile<kClean, BM>(ra, A, m0, M, k0 + kBK, K, tid);
+      load_a(k0 + kBK);
       load_tile<kClean, BN>(rb, B, n0, N, k0 + kBK, K, tid);
     }
     __builtin_amdgcn_s_setprio(1);   // keep the MFMA cluster together (T5)
@@ -453,12 +475,17 @@ struct Src2h {
   const uint16_t* p2;
   int64_t ld2;
   int64_t k1;
+  const float* eps2 = nullptr;   // as Src2::eps2 (fp32 product of the bf16 value, rounded once to bf16)
 };
 
 // bf16 twin of load_tile (8 elements = 16 B per thread and row; kClean as there, at kBKh granularity).
+__device__ __forceinline__ uint32_t scale_bf2(uint32_t w, float sc) {
+  return pack_bf2(__fmul_rn(sc, bf_lo(w)), __fmul_rn(sc, bf_hi(w)));
+}
+
 template <bool kClean, int ROWS>
 __device__ __forceinline__ void load_tile_h(uint4 (&r)[ROWS / 32], const Src2h& s, int64_t row0, int64_t rows,
-                                            int64_t k0, int64_t K, int tid) {
+                                            int64_t k0, int64_t K, int tid, float sc2 = 1.0f) {
   if constexpr (kClean) {
     // select between the loaded VALUES: a select between the two struct fields' addresses would make
     // the compiler copy the by-value kernel argument into scratch
@@ -475,6 +502,7 @@ __device__ __forceinline__ void load_tile_h(uint4 (&r)[ROWS / 32], const Src2h& 
       const uint4 v = *reinterpret_cast<const uint4*>(base + gr * ld + kk);
       r[i] = v;
     }
+    // (eps2 scaling of a clean p2 tile is applied when the tile is staged: scale_tile_h)
   } else {
     const int64_t kk = k0 + (tid & 7) * 8;
 #pragma unroll
@@ -485,7 +513,10 @@ __device__ __forceinline__ void load_tile_h(uint4 (&r)[ROWS / 32], const Src2h& 
 #pragma unroll
         for (int c = 0; c < 8; ++c) {
           const int64_t k = kk + c;
-          t[c] = k < K ? (k < s.k1 ? s.p1[gr * s.ld1 + k] : s.p2[gr * s.ld2 + (k - s.k1)]) : 0u;
+          t[c] = k < K ? (k < s.k1 ? s.p1[gr * s.ld1 + k]
+                                   : (s.eps2 ? f2bf(__fmul_rn(sc2, bf2f(s.p2[gr * s.ld2 + (k - s.k1)])))
+                                             : (uint32_t)s.p2[gr * s.ld2 + (k - s.k1)]))
+                       : 0u;
         }
       }
       r[i] = make_uint4(t[0] | (t[1] << 16), t[2] | (t[3] << 16), t[4] | (t[5] << 16), t[6] | (t[7] << 16));
@@ -539,15 +570,30 @@ __global__ __launch_bounds__(256, 3) void k_gemm_nt_bf16(Src2h A, Src2h B, int64
       for (int e = 0; e < 16; ++e) acc[a][b][e] = 0.0f;
 
   uint4 ra[BM / 32], rb[BN >= 32 ? BN / 32 : 1];
-  load_tile_h<kClean, BM>(ra, A, m0, M, 0, K, tid);
+  const float sc2 = self_scale(A.eps2);
+  bool scale_a = false;   // ra holds a clean p2 tile still to be scaled (at staging time, as the fp32 kernel)
+  auto load_a = [&](int64_t k0) {
+    load_tile_h<kClean, BM>(ra, A, m0, M, k0, K, tid, sc2);
+    scale_a = kClean && A.eps2 != nullptr && k0 >= A.k1;
+  };
+  auto scale_a_tile = [&]() {
+    if (scale_a) {
+#pragma unroll
+      for (int i = 0; i < BM / 32; ++i)
+        ra[i] = make_uint4(scale_bf2(ra[i].x, sc2), scale_bf2(ra[i].y, sc2), scale_bf2(ra[i].z, sc2),
+                           scale_bf2(ra[i].w, sc2));
+    }
+  };
+  load_a(0);
   load_tile_h<kClean, BN>(rb, B, n0, N, 0, K, tid);
+  scale_a_tile();
   store_tile_h<BM>(As, ra, tid);
   store_tile_h<BN>(Bs, rb, tid);
   __syncthreads();
   for (int64_t k0 = 0; k0 < K; k0 += kBKh) {
     const bool more = k0 + kBKh < K;
     if (more) {
-      load_tile_h<kClean, BM>(ra, A, m0, M, k0 + kBKh, K, tid);
+      load_a(k0 + kBKh);
       load_tile_h<kClean, BN>(rb, B, n0, N, k0 + kBKh, K, tid);
     }
     __builtin_amdgcn_s_setprio(1);   // keep the MFMA cluster together (T5)
@@ -569,6 +615,7 @@ __global__ __launch_bounds__(256, 3) void k_gemm_nt_bf16(Src2h A, Src2h B, int64
     __builtin_amdgcn_s_setprio(0);
     if (more) {
       __syncthreads();
+      scale_a_tile();
       store_tile_h<BM>(As, ra, tid);
       store_tile_h<BN>(Bs, rb, tid);
       __syncthreads();
@@ -642,14 +689,15 @@ int check_a_h(const char* what, const uint16_t* a1, int64_t lda1, int64_t k1, co
 using namespace hgin;
 
 extern "C" int hgin_gin_mlp_fwd_bf16(const uint16_t* a1, int64_t lda1, int64_t k1, const uint16_t* a2, int64_t lda2,
-                                     const uint16_t* w, const float* bias, const float* prelu, const uint16_t* accum,
-                                     uint16_t* z, uint16_t* y, int64_t M, int64_t N, int64_t K, void* stream) {
+                                     const float* a2_eps, const uint16_t* w, const float* bias, const float* prelu,
+                                     const uint16_t* accum, uint16_t* z, uint16_t* y, int64_t M, int64_t N, int64_t K,
+                                     void* stream) {
   HGIN_ARG_CHECK(M >= 0 && N >= 0 && K >= 0, "hgin_gin_mlp_fwd_bf16: negative size");
   HGIN_ARG_CHECK(M < (int64_t(1) << 31) && N <= 65535 * 128, "hgin_gin_mlp_fwd_bf16: size too large");
   if (M == 0 || N == 0) return HGIN_OK;
   HGIN_ARG_CHECK(w && bias && prelu && y, "hgin_gin_mlp_fwd_bf16: NULL operand");
   if (int rc = check_a_h("hgin_gin_mlp_fwd_bf16", a1, lda1, k1, a2, lda2, K)) return rc;
-  return launch_nt_bf16<1, uint16_t>(Src2h{a1, lda1, a2, lda2, k1}, Src2h{w, K, nullptr, 0, K}, M, N, K, bias, prelu,
+  return launch_nt_bf16<1, uint16_t>(Src2h{a1, lda1, a2, lda2, k1, a2_eps}, Src2h{w, K, nullptr, 0, K}, M, N, K, bias, prelu,
                                      accum, z, y, N, as_stream(stream), "hgin_gin_mlp_fwd_bf16");
 }
 
@@ -677,14 +725,15 @@ extern "C" int hgin_gemm_nt_bf16(const uint16_t* a, int64_t lda, const uint16_t*
 }
 
 extern "C" int hgin_gin_mlp_fwd_f32(const float* a1, int64_t lda1, int64_t k1, const float* a2, int64_t lda2,
-                                    const float* w, const float* bias, const float* prelu, const float* accum, float* z,
-                                    float* y, int64_t M, int64_t N, int64_t K, void* stream) {
+                                    const float* a2_eps, const float* w, const float* bias, const float* prelu,
+                                    const float* accum, float* z, float* y, int64_t M, int64_t N, int64_t K,
+                                    void* stream) {
   HGIN_ARG_CHECK(M >= 0 && N >= 0 && K >= 0, "hgin_gin_mlp_fwd_f32: negative size");
   HGIN_ARG_CHECK(M < (int64_t(1) << 31) && N <= 65535 * 128, "hgin_gin_mlp_fwd_f32: size too large");
   if (M == 0 || N == 0) return HGIN_OK;
   HGIN_ARG_CHECK(w && bias && prelu && y, "hgin_gin_mlp_fwd_f32: NULL operand");
   if (int rc = check_a("hgin_gin_mlp_fwd_f32", a1, lda1, k1, a2, lda2, K)) return rc;
-  return launch_nt<1>(Src2{a1, lda1, a2, lda2, k1}, Src2{w, K, nullptr, 0, K}, M, N, K, bias, prelu, accum, z, y,
+  return launch_nt<1>(Src2{a1, lda1, a2, lda2, k1, a2_eps}, Src2{w, K, nullptr, 0, K}, M, N, K, bias, prelu, accum, z, y,
                       N, as_stream(stream), "hgin_gin_mlp_fwd_f32");
 }
 

@@ -94,7 +94,7 @@ _SIGS = {
     "hgin_aggregate_f32": ([_P, _P, _I64, _P, _I64, _I64, _P, _I64, _I64, _P, _I32, _P, _I64, _P], _I32),
     "hgin_combine_bwd_workspace_size": ([_I64, ctypes.POINTER(_SZ)], _I32),
     "hgin_combine_bwd_f32": ([_P, _I64, _P, _I64, _I64, _I64, _P, _P, _I64, _P, _P, _SZ, _P], _I32),
-    "hgin_gin_mlp_fwd_f32": ([_P, _I64, _I64, _P, _I64, _P, _P, _P, _P, _P, _P, _I64, _I64, _I64, _P], _I32),
+    "hgin_gin_mlp_fwd_f32": ([_P, _I64, _I64, _P, _I64, _P, _P, _P, _P, _P, _P, _P, _I64, _I64, _I64, _P], _I32),
     "hgin_linear_fwd_f32": ([_P, _I64, _I64, _P, _I64, _P, _P, _P, _I64, _I64, _I64, _P], _I32),
     "hgin_prelu_bwd_workspace_size": ([_I64, _I64, ctypes.POINTER(_SZ)], _I32),
     "hgin_prelu_bwd_f32": ([_P, _I64, _P, _I64, _I64, _P, _P, _P, _P, _P, _SZ, _P], _I32),
@@ -102,7 +102,7 @@ _SIGS = {
     "hgin_gemm_tn_workspace_size": ([_I64, _I64, _I64, ctypes.POINTER(_SZ)], _I32),
     "hgin_gemm_tn_f32": ([_P, _I64, _P, _I64, _I64, _P, _I64, _I64, _I64, _I64, _P, _I64, _P, _SZ, _P], _I32),
     "hgin_aggregate_bf16": ([_P, _P, _I64, _P, _I64, _I64, _P, _I64, _I64, _P, _I32, _P, _I64, _P], _I32),
-    "hgin_gin_mlp_fwd_bf16": ([_P, _I64, _I64, _P, _I64, _P, _P, _P, _P, _P, _P, _I64, _I64, _I64, _P], _I32),
+    "hgin_gin_mlp_fwd_bf16": ([_P, _I64, _I64, _P, _I64, _P, _P, _P, _P, _P, _P, _P, _I64, _I64, _I64, _P], _I32),
     "hgin_linear_fwd_bf16": ([_P, _I64, _I64, _P, _I64, _P, _P, _P, _I64, _I64, _I64, _P], _I32),
     "hgin_gemm_nt_bf16": ([_P, _I64, _P, _I64, _P, _I64, _I64, _I64, _I64, _P], _I32),
     "hgin_gemm_tn_bf16": ([_P, _I64, _P, _I64, _I64, _P, _I64, _I64, _I64, _I64, _P, _I64, _P, _SZ, _P], _I32),

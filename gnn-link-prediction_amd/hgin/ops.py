@@ -311,8 +311,9 @@ def self_wgrad(G: Tensor, weight: Tensor, f: int, concat: bool, eps: Tensor):
 
 
 def gin_mlp_fwd(comb: Tensor, weight: Tensor, bias: Tensor, prelu: Optional[Tensor], accum: Optional[Tensor],
-                save_z: bool = True, comb2: Optional[Tensor] = None):
-    """y = prelu([comb | comb2] @ W^T + b) [+ accum]  (prelu None: plain Linear, y = z, nothing saved).
+                save_z: bool = True, comb2: Optional[Tensor] = None, eps2: Optional[Tensor] = None):
+    """y = prelu([comb | s * comb2] @ W^T + b) [+ accum]  (prelu None: plain Linear, y = z, nothing saved);
+    s = 1 + eps2[0] when ``eps2`` is given (the concat GINConv's self term formed in the GEMM's loads), else 1.
 
     fp32 storage: everything fp32.  bf16 storage (cfg5): comb / comb2 / weight / accum / z / y bf16, bias and
     prelu fp32; the plain Linear (the readout head) returns fp32."""
@@ -331,7 +332,7 @@ def gin_mlp_fwd(comb: Tensor, weight: Tensor, bias: Tensor, prelu: Optional[Tens
             _lib.call(f"hgin_linear_fwd_{sfx}", _p(comb), comb.stride(0), k1, _p(comb2), ld2, _p(weight), _p(bias),
                       _p(y), M, N, K, _stream(comb))
         else:
-            _lib.call(f"hgin_gin_mlp_fwd_{sfx}", _p(comb), comb.stride(0), k1, _p(comb2), ld2, _p(weight),
+            _lib.call(f"hgin_gin_mlp_fwd_{sfx}", _p(comb), comb.stride(0), k1, _p(comb2), ld2, _p(eps2), _p(weight),
                       _p(bias), _p(prelu), _p(accum), _p(z), _p(y), M, N, K, _stream(comb))
 
     probe = profiling.active()
@@ -385,11 +386,19 @@ class _GINConvFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x_src, x_dst, eps, weight, bias, prelu, accum, graph: RelationGraph, mode: int):
         f_src = x_src.size(1)
-        width = f_src + (x_dst.size(1) if mode == COMBINE_CONCAT else 0)
-        comb = torch.empty(graph.n_dst, width, dtype=x_src.dtype, device=x_src.device)
-        aggregate_into(graph.csr, x_src, x_dst, eps, mode, comb)
         w_op = _as(weight, x_src.dtype)          # bf16 path: the GEMM reads a bf16 copy of the fp32 master
-        z, y = gin_mlp_fwd(comb, w_op, bias, prelu, accum)
+        if mode == COMBINE_CONCAT and not (ctx.needs_input_grad[0] or ctx.needs_input_grad[1]):
+            # inputs are data (the first layer): the backward never needs the concat, so the self half
+            # (1 + eps) x_dst is formed in the GEMM's tile loads instead of being written by the aggregate and
+            # read back (2 * N_dst * F_dst * s bytes less per relation); comb holds the aggregate only
+            comb = torch.empty(graph.n_dst, f_src, dtype=x_src.dtype, device=x_src.device)
+            aggregate_into(graph.csr, x_src, None, None, COMBINE_NONE, comb)
+            z, y = gin_mlp_fwd(comb, w_op, bias, prelu, accum, comb2=x_dst, eps2=eps)
+        else:
+            width = f_src + (x_dst.size(1) if mode == COMBINE_CONCAT else 0)
+            comb = torch.empty(graph.n_dst, width, dtype=x_src.dtype, device=x_src.device)
+            aggregate_into(graph.csr, x_src, x_dst, eps, mode, comb)
+            z, y = gin_mlp_fwd(comb, w_op, bias, prelu, accum)
         ctx.graph, ctx.mode, ctx.f_src = graph, mode, f_src
         ctx.save_for_backward(x_dst, eps, w_op, prelu, comb, z)
         return y
@@ -422,6 +431,10 @@ class _GINConvFn(torch.autograd.Function):
                 G, g_a, g_b, _ = mlp_bwd_w(g_y, z, prelu, comb, x_dst)
             g_w, g_eps = self_wgrad(G, weight, f_src, mode == COMBINE_CONCAT, eps)
             g_w = g_w if need_w else None
+        elif mode == COMBINE_CONCAT and comb.size(1) == f_src:
+            # the forward kept only the aggregate (inputs are data): dW of the self block = (1 + eps) g_z^T x_dst
+            G, g_a, g_b, _ = mlp_bwd_w(g_y, z, prelu, comb, x_dst)
+            g_w = self_wgrad(G, weight, f_src, True, eps)[0] if need_w else None
         else:
             g_w, g_a, g_b, _ = mlp_bwd_w(g_y, z, prelu, comb)
         g_acc = g_y if need_acc else None

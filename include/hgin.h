@@ -99,11 +99,16 @@ int hgin_combine_bwd_f32(const float* g, int64_t ld_g, const float* x_dst, int64
  *   z = [a1 | a2] @ w^T + bias;  y = (z > 0 ? z : prelu[0] * z) [+ accum]
  * The A operand is the column concatenation of a1 ([M, k1], lda1) and a2 ([M, K - k1], lda2; NULL when
  * k1 == K), which also replaces the readout's torch.cat((x_path, raw path features)) (models.py:362-371).
+ * a2_eps (device float[1], may be NULL): the a2 columns enter as (1 + a2_eps[0]) * a2 — the concat GINConv's
+ * self term cat(aggregate, (1 + eps) * x_dst) (models.py:212-213) formed as the tile is loaded (the same
+ * single-rounded fp32 product the aggregate's epilogue would store), so the [N_dst, F_src + F_dst] concat
+ * need not be materialised.
  * w: [N, K] row-major (torch Linear.weight), bias: [N], prelu: device float[1].  Output rows are N wide.
- * z (pre-activation, saved for backward) may be NULL.  fp32 in, fp32 MFMA (v_mfma_f32_32x32x2_f32). */
+ * z (pre-activation, saved for backward) may be NULL.  fp32 in, fp32 results (hgin_gemm_nt.hip: f32 MFMA
+ * or the exact bf16 3-way operand split). */
 int hgin_gin_mlp_fwd_f32(const float* a1, int64_t lda1, int64_t k1, const float* a2, int64_t lda2,
-                         const float* w, const float* bias, const float* prelu, const float* accum,
-                         float* z, float* y, int64_t M, int64_t N, int64_t K, void* stream);
+                         const float* a2_eps, const float* w, const float* bias, const float* prelu,
+                         const float* accum, float* z, float* y, int64_t M, int64_t N, int64_t K, void* stream);
 
 /* ---- readout Linear without activation (models.py:326-330, the head Linear(mlp_layers[-1], 1)) ------
  *   y = [a1 | a2] @ w^T + bias     (same operand conventions as hgin_gin_mlp_fwd_f32) */
@@ -182,8 +187,9 @@ int hgin_aggregate_bf16(const int32_t* rowptr, const int32_t* col, int64_t n_row
                         const uint16_t* x_dst, int64_t ld_dst, int64_t f_dst,
                         const float* eps, int combine, uint16_t* out, int64_t ld_out, void* stream);
 int hgin_gin_mlp_fwd_bf16(const uint16_t* a1, int64_t lda1, int64_t k1, const uint16_t* a2, int64_t lda2,
-                          const uint16_t* w, const float* bias, const float* prelu, const uint16_t* accum,
-                          uint16_t* z, uint16_t* y, int64_t M, int64_t N, int64_t K, void* stream);
+                          const float* a2_eps, const uint16_t* w, const float* bias, const float* prelu,
+                          const uint16_t* accum, uint16_t* z, uint16_t* y, int64_t M, int64_t N, int64_t K,
+                          void* stream);
 int hgin_linear_fwd_bf16(const uint16_t* a1, int64_t lda1, int64_t k1, const uint16_t* a2, int64_t lda2,
                          const uint16_t* w, const float* bias, float* y, int64_t M, int64_t N, int64_t K,
                          void* stream);

@@ -400,3 +400,25 @@ def test_self_wgrad(concat, shape):
     assert abs(float(g_eps) - float(want_eps)) <= 1e-5 * float((W.abs().double().sum() * G.abs().max()))
     g_w2, g_eps2 = ops.self_wgrad(G, W, f, concat, eps)
     assert torch.equal(g_eps, g_eps2) and torch.equal(g_w, g_w2)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("M,F,N", [(1000, 128, 128), (777, 48, 40), (5000, 256, 256)])
+def test_mlp_fwd_self_term_in_loads(dtype, M, F, N):
+    """The concat GINConv forward without the materialised concat: [agg | (1+eps) x_dst] formed in the GEMM's
+    tile loads gives bit-for-bit the z / y of the GEMM over the aggregate kernel's concat output."""
+    from hgin import ops
+    dev = "cuda"
+    gen = torch.Generator().manual_seed(M + F + N)
+    agg = torch.randn(M, F, generator=gen).to(dev, dtype)
+    xd = torch.randn(M, F, generator=gen).to(dev, dtype)
+    w = (torch.randn(N, 2 * F, generator=gen) / (2 * F) ** 0.5).to(dev, dtype)
+    b = torch.randn(N, generator=gen).to(dev)
+    a = torch.tensor([0.25], device=dev)
+    eps = torch.tensor([0.37], device=dev)
+    self_half = (xd.float() * (1 + eps)).to(dtype)       # the aggregate epilogue's (1+eps)*x_dst, one rounding
+    comb = torch.cat((agg, self_half), 1)
+    z0, y0 = ops.gin_mlp_fwd(comb, w, b, a, None)
+    z1, y1 = ops.gin_mlp_fwd(agg, w, b, a, None, comb2=xd, eps2=eps)
+    assert torch.equal(z0, z1) and torch.equal(y0, y1)
