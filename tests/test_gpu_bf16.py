@@ -245,3 +245,28 @@ def test_model_bf16_full_cfg2_step_runs():
     for n, p in model.named_parameters():
         if p.grad is not None:
             assert torch.isfinite(p.grad).all(), n
+
+
+@pytest.mark.parametrize("M,N,K1,K2", [(3000, 128, 128, 128), (20000, 256, 256, 256), (1001, 64, 40, 24),
+                                       (777, 24, 16, 0), (500, 20, 16, 3), (0, 64, 64, 0)])
+def test_mlp_bwd_fused_bf16(M, N, K1, K2):
+    """hgin_gin_mlp_bwd_w_bf16: g_w bit-identical to hgin_prelu_bwd_bf16's rounded g_z -> hgin_gemm_tn_bf16;
+    bias / slope gradients (fixed-order sums of the unrounded fp32 g_z) against float64; deterministic.
+    (A variant forming g_z in the transposed-read dW kernel's staging passed this test but ran 1.6x slower
+    than the two passes: profiles/r01/s4/mlp_bwd_bf16_fused.txt.)"""
+    gen = torch.Generator().manual_seed(M + N + K1)
+    gy = torch.randn(M, N, generator=gen).to(DEV, BF)
+    z = torch.randn(M, N, generator=gen).to(DEV, BF)
+    a = torch.tensor([0.3], device=DEV)
+    b1 = torch.randn(M, K1, generator=gen).to(DEV, BF)
+    b2 = torch.randn(M, K2, generator=gen).to(DEV, BF) if K2 else None
+    g_w, g_a, g_b, _ = ops.mlp_bwd_w(gy, z, a, b1, b2)
+    gz2, _, _ = ops.prelu_bwd(gy, z, a)
+    assert torch.equal(g_w, ops.gemm_tn(gz2, b1, b2))
+    gzd = torch.where(z.double() > 0, gy.double(), gy.double() * 0.3)
+    assert ((g_b.double() - gzd.sum(0)).abs() <= 1e-5 * gzd.abs().sum(0) + 1e-6).all()
+    zr = z.double()
+    ga_ref = (torch.where(zr > 0, torch.zeros_like(zr), zr) * gy.double()).sum()
+    assert abs(float(g_a) - float(ga_ref)) <= 1e-5 * (float((zr * gy.double()).abs().sum()) + 1)
+    again = ops.mlp_bwd_w(gy, z, a, b1, b2)
+    assert all(torch.equal(p, q) for p, q in zip(again[:3], (g_w, g_a, g_b)))

@@ -27,6 +27,8 @@ def timeit(fn, reps=20):
 
 def main():
     shapes = [(600_000, 128, 256), (300_000, 128, 256), (600_000, 128, 128), (1_500_000, 256, 512)]
+    if "--cfg5" in sys.argv:   # the first-layer dW-only shapes of a cfg5 step (N = H = 256, K = 2 x 256)
+        shapes = [(6_000_000, 256, 512), (3_000_000, 256, 512), (1_000_000, 256, 512)]
     dt = torch.bfloat16 if "--bf16" in sys.argv else torch.float32
     for M, N, K in shapes:
         gy = torch.randn(M, N, device="cuda").to(dt)
