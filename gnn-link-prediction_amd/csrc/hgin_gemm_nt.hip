@@ -127,6 +127,7 @@ struct Out4;
 template <>
 struct Out4<float> {
   using raw = float4;   // a prefetched group in its storage form (4 VGPRs)
+  static __device__ __forceinline__ float rt(float v) { return v; }   // the value a store keeps
   static __device__ __forceinline__ raw ld_raw(const float* p, bool full, int nv) {
     if (full) return *reinterpret_cast<const float4*>(p);
     float t[4] = {0.f, 0.f, 0.f, 0.f};
@@ -152,6 +153,7 @@ struct Out4<float> {
 template <>
 struct Out4<uint16_t> {
   using raw = uint2;    // 4 packed bf16 (2 VGPRs)
+  static __device__ __forceinline__ float rt(float v) { return bf2f(f2bf(v)); }
   static __device__ __forceinline__ raw ld_raw(const uint16_t* p, bool full, int nv) {
     if (full) return *reinterpret_cast<const uint2*>(p);
     uint32_t t[4] = {0u, 0u, 0u, 0u};
@@ -175,6 +177,22 @@ struct Out4<uint16_t> {
   }
 };
 
+// EPI 4 — the dX GEMM of a GINConv backward with the self term's backward fused (models.py:210-215 reached
+// from train.py:43; replaces hgin_combine_bwd_* after the GEMM): C = g_comb = g_z W is stored as usual and,
+// for the self columns [cs, N) (cs = F_src for concat, 0 for add), g_x_dst[:, c - cs] = (1 + eps) C[:, c]
+// (optional) and a per-workgroup partial of sum(C[:, c] * x_dst[:, c - cs]) (the eps gradient; fixed order,
+// summed over workgroups by k_final_scalar).  C is used as stored (bf16: after its rounding), as the separate
+// combine backward would read it.
+struct CombEpi {
+  const void* xd;     // x_dst [M, N - cs], row stride ldxd (C's element type)
+  int64_t ldxd;
+  void* gd;           // g_x_dst [M, N - cs] or NULL, row stride ldgd
+  int64_t ldgd;
+  int64_t cs;         // first self column of C (a multiple of 4)
+  const float* eps;   // device float[1]
+  float* part;        // [workgroup tiles] eps-gradient partials
+};
+
 // Epilogue shared by the fp32 and bf16 kernels.  Per 32-row half (tm) each wave parks its 32 x WCOLS
 // results in LDS, then writes row-contiguous 4-column groups (bias, PReLU, accum applied on the way out).
 // A lane always owns the same 4 columns, so its bias values are loaded once, and the accum rows it will
@@ -184,7 +202,8 @@ __device__ __forceinline__ void epilogue(const f32x16 (&acc)[2][TN], float* smem
                                          int li, int lh, int64_t m0, int64_t n0, int64_t M, int64_t N,
                                          const float* __restrict__ bias, const float* __restrict__ prelu,
                                          const OutT* __restrict__ accum, OutT* __restrict__ Z, OutT* __restrict__ Y,
-                                         int64_t ldc, bool vec_out) {
+                                         int64_t ldc, bool vec_out, const CombEpi& ce = CombEpi{},
+                                         float* ep_out = nullptr) {
   constexpr int WCOLS = TN * 32;
   constexpr int kLc = WCOLS + 4;
   constexpr int kQ = WCOLS / 4;     // 4-column groups per row
@@ -198,7 +217,12 @@ __device__ __forceinline__ void epilogue(const f32x16 (&acc)[2][TN], float* smem
   const int nv = col < N ? (N - col < 4 ? (int)(N - col) : 4) : 0;
   const bool full = vec_out && nv == 4;
   float bcol[4] = {0.f, 0.f, 0.f, 0.f};
-  if (EPI >= 1) {
+  float ep = 0.0f;                                   // EPI 4: this lane's eps-gradient partial
+  const float sc_self = EPI == 4 ? __fadd_rn(1.0f, ce.eps[0]) : 0.0f;
+  const bool self_cols = EPI == 4 && col >= ce.cs && nv > 0;   // col, cs multiples of 4: whole group
+  const OutT* xd = static_cast<const OutT*>(ce.xd);
+  OutT* gd = static_cast<OutT*>(ce.gd);
+  if (EPI == 1 || EPI == 2) {
 #pragma unroll
     for (int t = 0; t < 4; ++t)
       if (t < nv) bcol[t] = bias[col + t];
@@ -208,10 +232,11 @@ __device__ __forceinline__ void epilogue(const f32x16 (&acc)[2][TN], float* smem
   for (int tm = 0; tm < 2; ++tm) {
     typename Out4<OutT>::raw acc_raw[kJ];
 #pragma unroll
-    for (int j = 0; j < kJ; ++j) {
+    for (int j = 0; j < kJ; ++j) {   // accum (EPI 1) / x_dst (EPI 4) rows: loaded before the LDS round trip
       acc_raw[j] = {};
       const int64_t row = m0 + wm * 64 + tm * 32 + r0 + kRS * j;
       if (EPI == 1 && accum && row < M && nv) acc_raw[j] = Out4<OutT>::ld_raw(accum + row * ldc + col, full, nv);
+      if (EPI == 4 && self_cols && row < M) acc_raw[j] = Out4<OutT>::ld_raw(xd + row * ce.ldxd + (col - ce.cs), full, nv);
     }
 #pragma unroll
     for (int tn = 0; tn < TN; ++tn)
@@ -240,19 +265,46 @@ __device__ __forceinline__ void epilogue(const f32x16 (&acc)[2][TN], float* smem
       }
       Out4<OutT>::st(Y + row * ldc + col, o, full, nv);
       if (EPI == 1 && Z) Out4<OutT>::st(Z + row * ldc + col, zz, full, nv);
+      if (EPI == 4 && self_cols) {
+        float c4[4], x4[4], g4[4];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) c4[t] = Out4<OutT>::rt(o[t]);   // C as stored
+        const int64_t sc = col - ce.cs;
+        Out4<OutT>::unpack(acc_raw[j], x4);
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          if (t < nv) ep = __fadd_rn(ep, __fmul_rn(c4[t], x4[t]));
+          g4[t] = __fmul_rn(sc_self, c4[t]);
+        }
+        if (gd) Out4<OutT>::st(gd + row * ce.ldgd + sc, g4, full, nv);
+      }
     }
     if (tm == 0) __syncthreads();
   }
+  if (EPI == 4) *ep_out = ep;
 }
 
 using bf16x8 = __attribute__((ext_vector_type(8))) __bf16;
+
+// EPI 4: the workgroup's eps-gradient partial, a fixed tree over its 256 lanes -> part[tile]
+__device__ __forceinline__ void tile_partial(float* smem, float ep, float* part, int64_t q) {
+  __syncthreads();   // the epilogue's LDS staging is done
+  const int t = threadIdx.x;
+  smem[t] = ep;
+  __syncthreads();
+  for (int off = 128; off > 0; off >>= 1) {
+    if (t < off) smem[t] = __fadd_rn(smem[t], smem[t + off]);
+    __syncthreads();
+  }
+  if (t == 0) part[q] = smem[0];
+}
 
 template <int EPI, bool kClean, int TN, int WNv, bool kSplit>
 __global__ __launch_bounds__(256, 3) void k_gemm_nt(Src2 A, Src2 B, int64_t M, int64_t N, int64_t K,
                                                     const float* __restrict__ bias, const float* __restrict__ prelu,
                                                     const float* __restrict__ accum, float* __restrict__ Z,
                                                     float* __restrict__ Y, int64_t ldc, bool vec_out,
-                                                    int64_t n_tiles, bool xcd) {
+                                                    int64_t n_tiles, bool xcd, CombEpi ce) {
   constexpr int WN = WNv;                 // waves along N
   constexpr int WM = 4 / WN;              // waves along M
   constexpr int BM = WM * 64;             // rows per workgroup tile
@@ -374,14 +426,16 @@ __global__ __launch_bounds__(256, 3) void k_gemm_nt(Src2 A, Src2 B, int64_t M, i
     }
   }
 
+  float ep = 0.0f;
   epilogue<EPI, TN, float>(acc, smem, wave, wm, wn, lane, li, lh, m0, n0, M, N, bias, prelu, accum, Z, Y, ldc,
-                           vec_out);
+                           vec_out, ce, &ep);
+  if constexpr (EPI == 4) tile_partial(smem, ep, ce.part, q);
 }
 
 template <int EPI, int TN, int WN>
-void launch_nt_tn(bool vec, const Src2& a, const Src2& b, int64_t M, int64_t N, int64_t K, const float* bias,
-                  const float* prelu, const float* accum, float* z, float* y, int64_t ldc, bool vec_out,
-                  hipStream_t s) {
+int64_t launch_nt_tn(bool vec, const Src2& a, const Src2& b, int64_t M, int64_t N, int64_t K, const float* bias,
+                     const float* prelu, const float* accum, float* z, float* y, int64_t ldc, bool vec_out,
+                     hipStream_t s, const CombEpi& ce) {
   constexpr int BM = (4 / WN) * 64;
   constexpr int BN = WN * TN * 32;
   const int64_t tiles = ceil_div(N, BN) * ceil_div(M, BM);
@@ -389,13 +443,14 @@ void launch_nt_tn(bool vec, const Src2& a, const Src2& b, int64_t M, int64_t N, 
   dim3 grid((unsigned)(xcd ? round_up8(tiles) : tiles));
 #define HGIN_NT_F32(CLEAN, SPLIT)                                                                           \
   k_gemm_nt<EPI, CLEAN, TN, WN, SPLIT><<<grid, 256, 0, s>>>(a, b, M, N, K, bias, prelu, accum, z, y, ldc, vec_out, \
-                                                            tiles, xcd)
+                                                            tiles, xcd, ce)
   if (gemm_split_enabled()) {
     if (vec) HGIN_NT_F32(true, true); else HGIN_NT_F32(false, true);
   } else {
     if (vec) HGIN_NT_F32(true, false); else HGIN_NT_F32(false, false);
   }
 #undef HGIN_NT_F32
+  return tiles;
 }
 
 // Resident workgroups of a kernel across the device (occupancy x CUs), queried once per kernel.
@@ -436,17 +491,22 @@ bool use_bm64(int64_t M, int64_t N) {
 
 template <int EPI>
 int launch_nt(const Src2& a, const Src2& b, int64_t M, int64_t N, int64_t K, const float* bias, const float* prelu,
-              const float* accum, float* z, float* y, int64_t ldc, hipStream_t s, const char* what) {
+              const float* accum, float* z, float* y, int64_t ldc, hipStream_t s, const char* what,
+              const CombEpi& ce = CombEpi{}, int64_t* tiles_out = nullptr) {
   const bool vec = K % kBK == 0 && a.k1 % kBK == 0 && aligned16(a.p1) && a.ld1 % 4 == 0 &&
                    (a.k1 == K || (aligned16(a.p2) && a.ld2 % 4 == 0)) && aligned16(b.p1) && b.ld1 % 4 == 0;
   const bool vec_out = ldc % 4 == 0 && aligned16(y) && (z == nullptr || aligned16(z)) &&
-                       (accum == nullptr || aligned16(accum));
+                       (accum == nullptr || aligned16(accum)) &&
+                       (EPI != 4 || (aligned16(ce.xd) && ce.ldxd % 4 == 0 &&
+                                     (ce.gd == nullptr || (aligned16(ce.gd) && ce.ldgd % 4 == 0))));
+  int64_t tiles;
   if (N <= 32)
-    launch_nt_tn<EPI, 1, 1>(vec, a, b, M, N, K, bias, prelu, accum, z, y, ldc, vec_out, s);
-  else if (use_bm64<EPI>(M, N))
-    launch_nt_tn<EPI, 1, 4>(vec, a, b, M, N, K, bias, prelu, accum, z, y, ldc, vec_out, s);
+    tiles = launch_nt_tn<EPI, 1, 1>(vec, a, b, M, N, K, bias, prelu, accum, z, y, ldc, vec_out, s, ce);
+  else if (use_bm64<EPI == 4 ? 0 : EPI>(M, N))
+    tiles = launch_nt_tn<EPI, 1, 4>(vec, a, b, M, N, K, bias, prelu, accum, z, y, ldc, vec_out, s, ce);
   else
-    launch_nt_tn<EPI, 2, 2>(vec, a, b, M, N, K, bias, prelu, accum, z, y, ldc, vec_out, s);
+    tiles = launch_nt_tn<EPI, 2, 2>(vec, a, b, M, N, K, bias, prelu, accum, z, y, ldc, vec_out, s, ce);
+  if (tiles_out) *tiles_out = tiles;
   return check_launch(what);
 }
 
@@ -537,7 +597,7 @@ __global__ __launch_bounds__(256, 3) void k_gemm_nt_bf16(Src2h A, Src2h B, int64
                                                          const float* __restrict__ prelu,
                                                          const OutT* __restrict__ accum, OutT* __restrict__ Z,
                                                          OutT* __restrict__ Y, int64_t ldc, bool vec_out,
-                                                         int64_t n_tiles, bool xcd) {
+                                                         int64_t n_tiles, bool xcd, CombEpi ce) {
   constexpr int WN = WNv;
   constexpr int WM = 4 / WN;
   constexpr int BM = WM * 64;
@@ -622,8 +682,10 @@ __global__ __launch_bounds__(256, 3) void k_gemm_nt_bf16(Src2h A, Src2h B, int64
     }
   }
 
+  float ep = 0.0f;
   epilogue<EPI, TN, OutT>(acc, smem, wave, wm, wn, lane, li, lh, m0, n0, M, N, bias, prelu, accum, Z, Y, ldc,
-                          vec_out);
+                          vec_out, ce, &ep);
+  if constexpr (EPI == 4) tile_partial(smem, ep, ce.part, q);
 }
 
 template <int EPI, typename OutT>
@@ -646,11 +708,13 @@ bool use_bm64_bf16(int64_t M, int64_t N) {
 template <int EPI, typename OutT>
 int launch_nt_bf16(const Src2h& a, const Src2h& b, int64_t M, int64_t N, int64_t K, const float* bias,
                    const float* prelu, const OutT* accum, OutT* z, OutT* y, int64_t ldc, hipStream_t s,
-                   const char* what) {
+                   const char* what, const CombEpi& ce = CombEpi{}, int64_t* tiles_out = nullptr) {
   const bool vec = K % kBKh == 0 && a.k1 % kBKh == 0 && aligned16(a.p1) && a.ld1 % 8 == 0 &&
                    (a.k1 == K || (aligned16(a.p2) && a.ld2 % 8 == 0)) && aligned16(b.p1) && b.ld1 % 8 == 0;
   const bool vec_out = ldc % 4 == 0 && aligned16(y) && (z == nullptr || aligned16(z)) &&
-                       (accum == nullptr || aligned16(accum));
+                       (accum == nullptr || aligned16(accum)) &&
+                       (EPI != 4 || (aligned16(ce.xd) && ce.ldxd % 4 == 0 &&
+                                     (ce.gd == nullptr || (aligned16(ce.gd) && ce.ldgd % 4 == 0))));
 #define HGIN_NT_BF16(TNV, WNV)                                                                                \
   {                                                                                                          \
     constexpr int BM = (4 / WNV) * 64;                                                                       \
@@ -660,14 +724,15 @@ int launch_nt_bf16(const Src2h& a, const Src2h& b, int64_t M, int64_t N, int64_t
     dim3 grid((unsigned)(xcd ? round_up8(tiles) : tiles));                                                   \
     if (vec)                                                                                                 \
       k_gemm_nt_bf16<EPI, true, TNV, WNV, OutT><<<grid, 256, 0, s>>>(a, b, M, N, K, bias, prelu, accum, z, y, \
-                                                                     ldc, vec_out, tiles, xcd);              \
+                                                                     ldc, vec_out, tiles, xcd, ce);          \
     else                                                                                                     \
       k_gemm_nt_bf16<EPI, false, TNV, WNV, OutT><<<grid, 256, 0, s>>>(a, b, M, N, K, bias, prelu, accum, z,  \
-                                                                      y, ldc, vec_out, tiles, xcd);          \
+                                                                      y, ldc, vec_out, tiles, xcd, ce);      \
+    if (tiles_out) *tiles_out = tiles;                                                                       \
   }
   if (N <= 32)
     HGIN_NT_BF16(1, 1)
-  else if (use_bm64_bf16<EPI, OutT>(M, N))
+  else if (use_bm64_bf16<EPI == 4 ? 0 : EPI, OutT>(M, N))
     HGIN_NT_BF16(1, 4)
   else
     HGIN_NT_BF16(2, 2)
@@ -683,10 +748,102 @@ int check_a_h(const char* what, const uint16_t* a1, int64_t lda1, int64_t k1, co
   return HGIN_OK;
 }
 
+// Fixed-order sum of the EPI 4 tile partials: level 1 (k_part_sum over kPartChunk-long chunks, one workgroup
+// each), level 2 (one workgroup over the level-1 sums).  cfg5 launches ~94k tiles: one workgroup alone took 0.1 ms.
+constexpr int64_t kPartChunk = 4096;
+
+__global__ __launch_bounds__(256) void k_part_sum(const float* __restrict__ part, int64_t n, float* __restrict__ out) {
+  __shared__ float red[256];
+  const int t = threadIdx.x;
+  const int64_t b0 = (int64_t)blockIdx.x * kPartChunk;
+  const int64_t b1 = b0 + kPartChunk < n ? b0 + kPartChunk : n;
+  float s = 0.0f;
+  for (int64_t i = b0 + t; i < b1; i += 256) s = __fadd_rn(s, part[i]);
+  red[t] = s;
+  __syncthreads();
+  for (int off = 128; off > 0; off >>= 1) {
+    if (t < off) red[t] = __fadd_rn(red[t], red[t + off]);
+    __syncthreads();
+  }
+  if (t == 0) out[blockIdx.x] = red[0];
+}
+
+int64_t combine_max_tiles(int64_t M, int64_t N) {   // the most tiles any tile shape launches (64-row x 32-col)
+  return ceil_div(M > 0 ? M : 1, 64) * ceil_div(N > 0 ? N : 1, 32);
+}
+
+size_t combine_ws_bytes(int64_t M, int64_t N) {
+  const int64_t t = combine_max_tiles(M, N);
+  return align_up(sizeof(float) * (size_t)t, 256) + align_up(sizeof(float) * (size_t)ceil_div(t, kPartChunk), 256);
+}
+
+template <typename T>
+int gemm_nt_combine(const char* what, const T* a, int64_t lda, const T* b, int64_t ldb, T* c, int64_t ldc, int64_t M,
+                    int64_t N, int64_t K, const T* x_dst, int64_t ld_xd, T* g_dst, int64_t ld_gd, int64_t cs,
+                    const float* eps, float* g_eps, void* workspace, size_t workspace_bytes, void* stream) {
+  HGIN_ARG_CHECK(M >= 0 && N >= 0 && K >= 0 && cs >= 0 && cs <= N, "%s: bad sizes", what);
+  HGIN_ARG_CHECK(N <= 65535 * 128 && M < (int64_t(1) << 31), "%s: size too large", what);
+  HGIN_ARG_CHECK(cs % 4 == 0, "%s: the self columns must start at a multiple of 4", what);
+  HGIN_ARG_CHECK(eps && g_eps, "%s: NULL eps / g_eps", what);
+  hipStream_t s = as_stream(stream);
+  if (M == 0 || N == cs) return memset_async(g_eps, 0, sizeof(float), s, what);
+  HGIN_ARG_CHECK(a && b && c && x_dst, "%s: NULL operand", what);
+  HGIN_ARG_CHECK(lda >= K && ldb >= K && ldc >= N && ld_xd >= N - cs && (!g_dst || ld_gd >= N - cs),
+                 "%s: leading dimension too small", what);
+  const size_t need = combine_ws_bytes(M, N);
+  if (!workspace || workspace_bytes < need) {
+    set_error("%s: workspace %zu < %zu", what, workspace_bytes, need);
+    return HGIN_E_WORKSPACE;
+  }
+  float* part = static_cast<float*>(workspace);
+  const CombEpi ce{x_dst, ld_xd, g_dst, ld_gd, cs, eps, part};
+  int64_t tiles = 0;
+  int rc;
+  if constexpr (sizeof(T) == 2)
+    rc = launch_nt_bf16<4, uint16_t>(Src2h{a, lda, nullptr, 0, K}, Src2h{b, ldb, nullptr, 0, K}, M, N, K, nullptr,
+                                     nullptr, nullptr, nullptr, c, ldc, s, what, ce, &tiles);
+  else
+    rc = launch_nt<4>(Src2{a, lda, nullptr, 0, K}, Src2{b, ldb, nullptr, 0, K}, M, N, K, nullptr, nullptr, nullptr,
+                      nullptr, c, ldc, s, what, ce, &tiles);
+  if (rc) return rc;
+  const int64_t nb = ceil_div(tiles, kPartChunk);
+  if (nb == 1) {
+    k_part_sum<<<1, 256, 0, s>>>(part, tiles, g_eps);
+  } else {
+    float* part2 = reinterpret_cast<float*>(static_cast<char*>(workspace) +
+                                            align_up(sizeof(float) * (size_t)combine_max_tiles(M, N), 256));
+    k_part_sum<<<(unsigned)nb, 256, 0, s>>>(part, tiles, part2);
+    k_part_sum<<<1, 256, 0, s>>>(part2, nb, g_eps);   // nb <= kPartChunk for any M < 2^31
+  }
+  return check_launch(what);
+}
+
 }  // namespace
 }  // namespace hgin
 
 using namespace hgin;
+
+extern "C" int hgin_gemm_nt_combine_workspace_size(int64_t M, int64_t N, size_t* bytes) {
+  HGIN_ARG_CHECK(bytes && M >= 0 && N >= 0, "hgin_gemm_nt_combine_workspace_size: bad args");
+  *bytes = combine_ws_bytes(M, N);
+  return HGIN_OK;
+}
+
+extern "C" int hgin_gemm_nt_combine_f32(const float* a, int64_t lda, const float* b, int64_t ldb, float* c,
+                                        int64_t ldc, int64_t M, int64_t N, int64_t K, const float* x_dst,
+                                        int64_t ld_xd, float* g_dst, int64_t ld_gd, int64_t cs, const float* eps,
+                                        float* g_eps, void* workspace, size_t workspace_bytes, void* stream) {
+  return gemm_nt_combine<float>("hgin_gemm_nt_combine_f32", a, lda, b, ldb, c, ldc, M, N, K, x_dst, ld_xd, g_dst,
+                                ld_gd, cs, eps, g_eps, workspace, workspace_bytes, stream);
+}
+
+extern "C" int hgin_gemm_nt_combine_bf16(const uint16_t* a, int64_t lda, const uint16_t* b, int64_t ldb, uint16_t* c,
+                                         int64_t ldc, int64_t M, int64_t N, int64_t K, const uint16_t* x_dst,
+                                         int64_t ld_xd, uint16_t* g_dst, int64_t ld_gd, int64_t cs, const float* eps,
+                                         float* g_eps, void* workspace, size_t workspace_bytes, void* stream) {
+  return gemm_nt_combine<uint16_t>("hgin_gemm_nt_combine_bf16", a, lda, b, ldb, c, ldc, M, N, K, x_dst, ld_xd, g_dst,
+                                   ld_gd, cs, eps, g_eps, workspace, workspace_bytes, stream);
+}
 
 extern "C" int hgin_gin_mlp_fwd_bf16(const uint16_t* a1, int64_t lda1, int64_t k1, const uint16_t* a2, int64_t lda2,
                                      const float* a2_eps, const uint16_t* w, const float* bias, const float* prelu,

@@ -242,6 +242,26 @@ def gemm_nt(a: Tensor, b: Tensor) -> Tensor:
     return c
 
 
+def gemm_nt_combine(a: Tensor, b: Tensor, x_dst: Tensor, eps: Tensor, cs: int, want_gx: bool):
+    """(c, g_x_dst, g_eps): c = a @ b^T, g_x_dst = (1 + eps) c[:, cs:], g_eps = sum(c[:, cs:] * x_dst) in one
+    GEMM launch + a final sum (hgin_gemm_nt_combine_*): the dX GEMM of a GINConv backward with the self
+    term's backward in its epilogue."""
+    a, b = _rowmajor(a), _rowmajor(b)
+    _same_dtype("gemm_nt_combine", a, b, x_dst)
+    M, K = a.shape
+    N = b.shape[0]
+    c = torch.empty(M, N, dtype=a.dtype, device=a.device)
+    gx = torch.empty(M, N - cs, dtype=a.dtype, device=a.device) if want_gx else None
+    g_eps = torch.empty(1, dtype=torch.float32, device=a.device)
+    nbytes = ctypes.c_size_t(0)
+    _lib.check(_lib.lib().hgin_gemm_nt_combine_workspace_size(M, N, ctypes.byref(nbytes)), "nt_combine_workspace")
+    ws = _workspace(nbytes.value, a.device)
+    _lib.call(f"hgin_gemm_nt_combine_{_sfx(a)}", _p(a), a.stride(0), _p(b), b.stride(0), _p(c), c.stride(0), M, N, K,
+              _p(x_dst), x_dst.stride(0), _p(gx), gx.stride(0) if gx is not None else 0, cs, _p(eps), _p(g_eps),
+              _p(ws), nbytes.value, _stream(a))
+    return c, gx, g_eps
+
+
 def gemm_tn(a: Tensor, b1: Tensor, b2: Optional[Tensor] = None) -> Tensor:
     """out[N, K] (fp32) = a[M, N]^T @ [b1 | b2] (weight gradients), split-M MFMA + deterministic slab reduce."""
     a, b1 = _rowmajor(a), _rowmajor(b1)
@@ -415,12 +435,16 @@ class _GINConvFn(torch.autograd.Function):
             # (a side stream overlapping dW with the dX GEMM + CSC aggregate measured 1 % slower on cfg2 / cfg2bf:
             # each of these kernels already fills the 256 CUs)
             g_w, g_a, g_b, g_z = mlp_bwd_w(g_y, z, prelu, comb, want_gz=True)
-            g_comb = gemm_nt(g_z, weight.t().contiguous())      # dX = g_z W   [N_dst, K]
+            cs = f_src if mode == COMBINE_CONCAT else 0
+            if mode != COMBINE_NONE and cs % 4 == 0 and x_dst.stride(1) == 1:
+                # dX = g_z W [N_dst, K] with the self term's backward in the GEMM epilogue
+                g_comb, g_dst, g_eps = gemm_nt_combine(g_z, weight.t().contiguous(), x_dst, eps, cs, need_dst)
+            else:
+                g_comb = gemm_nt(g_z, weight.t().contiguous())      # dX = g_z W   [N_dst, K]
+                if mode != COMBINE_NONE:
+                    g_dst, g_eps = combine_bwd(g_comb[:, cs:], x_dst, eps, need_dst)
             if need_src:
                 g_src = _backward_aggregate(ctx.graph, g_comb[:, :f_src])
-            if mode != COMBINE_NONE:
-                gs = g_comb[:, f_src:] if mode == COMBINE_CONCAT else g_comb
-                g_dst, g_eps = combine_bwd(gs, x_dst, eps, need_dst)
         elif need_eps and mode != COMBINE_NONE:
             # Only parameters need gradients (the first layer, whose inputs are data):
             # sum(g_comb[:, self] * x_dst) = sum(W_self * (g_z^T x_dst)), so one TN pass over

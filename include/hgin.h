@@ -129,6 +129,23 @@ int hgin_prelu_bwd_f32(const float* g_y, int64_t ld_gy, const float* z, int64_t 
 int hgin_gemm_nt_f32(const float* a, int64_t lda, const float* b, int64_t ldb, float* c, int64_t ldc,
                      int64_t M, int64_t N, int64_t K, void* stream);
 
+/* ---- A9: dX GEMM with the self term's backward fused --------------------------------------------------
+ * Replaces hgin_gemm_nt_* followed by hgin_combine_bwd_* in a GINConv backward (models.py:210-217 reached
+ * from train.py:43): c[M, N] = a[M, K] @ b[N, K]^T (= g_comb = g_z W) and, over the self columns [cs, N)
+ * (cs = F_src for concat, 0 for add; a multiple of 4), with C as stored:
+ *   g_dst[m, j] = (1 + eps[0]) * c[m, cs + j]   (g_dst may be NULL)
+ *   g_eps[0]    = sum_{m, j} c[m, cs + j] * x_dst[m, j]      (fixed-order per-workgroup partials + final)
+ * so g_comb is not read back.  workspace: hgin_gemm_nt_combine_workspace_size.  Deterministic. */
+int hgin_gemm_nt_combine_workspace_size(int64_t M, int64_t N, size_t* bytes);
+int hgin_gemm_nt_combine_f32(const float* a, int64_t lda, const float* b, int64_t ldb, float* c, int64_t ldc,
+                             int64_t M, int64_t N, int64_t K, const float* x_dst, int64_t ld_xd, float* g_dst,
+                             int64_t ld_gd, int64_t cs, const float* eps, float* g_eps, void* workspace,
+                             size_t workspace_bytes, void* stream);
+int hgin_gemm_nt_combine_bf16(const uint16_t* a, int64_t lda, const uint16_t* b, int64_t ldb, uint16_t* c,
+                              int64_t ldc, int64_t M, int64_t N, int64_t K, const uint16_t* x_dst, int64_t ld_xd,
+                              uint16_t* g_dst, int64_t ld_gd, int64_t cs, const float* eps, float* g_eps,
+                              void* workspace, size_t workspace_bytes, void* stream);
+
 /* ---- weight-gradient GEMM (backward of Linear: dW = g_z^T X) ----------------------------------------
  * out[N, K] = a[M, N]^T @ [b1 | b2],  b1 = columns [0, k1) ([M, k1], ldb1), b2 = columns [k1, K) ([M, K-k1],
  * ldb2; may be NULL when k1 == K).  Reduction over M split across workgroups into fp32 slabs summed in a

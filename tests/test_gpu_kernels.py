@@ -422,3 +422,32 @@ def test_mlp_fwd_self_term_in_loads(dtype, M, F, N):
     z0, y0 = ops.gin_mlp_fwd(comb, w, b, a, None)
     z1, y1 = ops.gin_mlp_fwd(agg, w, b, a, None, comb2=xd, eps2=eps)
     assert torch.equal(z0, z1) and torch.equal(y0, y1)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("M,K,F_src,F_dst", [(1000, 128, 0, 128), (777, 64, 48, 40), (30000, 128, 128, 128),
+                                             (5, 32, 8, 20), (200, 16, 0, 30)])
+@pytest.mark.parametrize("want_gx", [True, False])
+def test_gemm_nt_combine(dtype, M, K, F_src, F_dst, want_gx):
+    """dX GEMM with the fused self-term backward: c equals the plain NT GEMM bit for bit; g_x_dst equals
+    hgin_combine_bwd_* on that c bit for bit; g_eps within fp32 reduction-order tolerance."""
+    from hgin import ops
+    dev = "cuda"
+    gen = torch.Generator().manual_seed(M + K + F_dst)
+    N = F_src + F_dst
+    a = torch.randn(M, K, generator=gen).to(dev, dtype)
+    b = torch.randn(N, K, generator=gen).to(dev, dtype)
+    xd = torch.randn(M, F_dst, generator=gen).to(dev, dtype)
+    eps = torch.tensor([0.2], device=dev)
+    c, gx, ge = ops.gemm_nt_combine(a, b, xd, eps, F_src, want_gx)
+    c0 = ops.gemm_nt(a, b)
+    assert torch.equal(c, c0)
+    gx0, ge0 = ops.combine_bwd(c0[:, F_src:], xd, eps, True)
+    if want_gx:
+        assert torch.equal(gx, gx0)
+    else:
+        assert gx is None
+    ref = (c0[:, F_src:].double() * xd.double()).sum()
+    bound = 1e-5 * float((c0[:, F_src:].double() * xd.double()).abs().sum()) + 1e-6
+    assert abs(float(ge) - float(ref)) <= bound and abs(float(ge0) - float(ref)) <= bound
