@@ -52,6 +52,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-steps", type=int, default=2)
     ap.add_argument("--no-probe", action="store_true", help="no per-kernel events in the timed region")
+    ap.add_argument("--adam", choices=("foreach", "fused"), default="foreach",
+                    help="torch.optim.Adam implementation (train.py's optimizer, same update rule)")
     ap.add_argument("--graph", action="store_true",
                     help="one hipGraph replay per step (default: the step issued from Python; measured equal on cfg2 "
                          "and cfg5 — the step is GPU-bound, the host runs ahead)")
@@ -142,7 +144,8 @@ def main():
     if args.prune_dead:
         model.prune_dead(True)
     # capturable Adam: the optimizer step is part of the replayed graph (same update rule and arithmetic)
-    opt = torch.optim.Adam(lr=1e-3, params=model.parameters(), weight_decay=0, capturable=args.graph)
+    opt = torch.optim.Adam(lr=1e-3, params=model.parameters(), weight_decay=0, capturable=args.graph,
+                           **({"fused": True} if args.adam == "fused" else {}))
     reducer = GradAllReducer(model.parameters()) if world > 1 else None
 
     def barrier():
@@ -234,7 +237,8 @@ def main():
                           "global_batch": world, "parallelism": f"dp{world} (graph component per rank, RCCL "
                                                                 f"gradient all-reduce)",
                           "prune_dead": bool(args.prune_dead),
-                          "execution": "hipgraph (one replay per step)" if args.graph else "eager"},
+                          "execution": "hipgraph (one replay per step)" if args.graph else "eager",
+                          "optimizer": f"torch.optim.Adam(lr=1e-3), {args.adam}"},
                "roofline": roofline, "mfma": mfma, "final_loss": final_loss}
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(cfg, args.cpu_steps)
