@@ -464,6 +464,78 @@ __global__ __launch_bounds__(256) void k_slab_reduce2(const float* __restrict__ 
   out[(i / K) * ldo + (i % K)] = s;
 }
 
+// Both levels of the slab sum in ONE launch, with the same arithmetic (bit-identical to k_slab_reduce1 +
+// k_slab_reduce2): a workgroup owns 64 consecutive outputs; its 16 thread rows x 16 float4 lanes form the
+// group sums (group g by row g mod 16) into LDS, then 64 threads add the group sums in group order.  The
+// level-2 pass no longer re-reads G x NK partials from HBM, and a launch + kernel boundary goes per call.
+// With `pro` the last N + 1 workgroups are k_pro_final's (independent work, uniform per workgroup).
+constexpr int kSlabMaxG = 64;   // S <= 1024 (tn_splits) -> G = ceil(S / kSlabGroup) <= 64
+constexpr int kSlabCols = 64;
+
+__global__ __launch_bounds__(256) void k_slab_reduce(const float* __restrict__ slab, int64_t S, int64_t NK,
+                                                     float* __restrict__ out, int64_t K, int64_t ldo,
+                                                     int64_t n_red, const float* __restrict__ pcol,
+                                                     const float* __restrict__ ps, int64_t n_ps,
+                                                     float* __restrict__ g_bias, float* __restrict__ g_prelu) {
+  __shared__ float part[kSlabMaxG * kSlabCols];
+  const int t = threadIdx.x;
+  if ((int64_t)blockIdx.x >= n_red) {   // k_pro_final workgroups
+    float* red = part;
+    const int64_t c = (int64_t)blockIdx.x - n_red;
+    const bool slope = c == (int64_t)gridDim.x - n_red - 1;
+    const int64_t n = slope ? n_ps : S;
+    const float* p = slope ? ps : pcol + c * S;
+    float s = 0.0f;
+    for (int64_t b = t; b < n; b += 256) s = __fadd_rn(s, p[b]);
+    red[t] = s;
+    __syncthreads();
+    for (int off = 128; off > 0; off >>= 1) {
+      if (t < off) red[t] = __fadd_rn(red[t], red[t + off]);
+      __syncthreads();
+    }
+    if (t == 0) {
+      if (slope) g_prelu[0] = red[0];
+      else g_bias[c] = red[0];
+    }
+    return;
+  }
+  const int q = t & 15, r = t >> 4;
+  const int64_t base = (int64_t)blockIdx.x * kSlabCols;
+  const int64_t i4 = base + q * 4;
+  const int64_t G = (S + kSlabGroup - 1) / kSlabGroup;
+  const bool full = i4 + 3 < NK && (NK & 3) == 0;
+  for (int64_t g = r; g < G; g += 16) {
+    const int64_t s0 = g * kSlabGroup;
+    const int64_t s1 = s0 + kSlabGroup < S ? s0 + kSlabGroup : S;
+    float a[4] = {0.f, 0.f, 0.f, 0.f};
+    if (full) {
+      for (int64_t j = s0; j < s1; ++j) {
+        const float4 v = *reinterpret_cast<const float4*>(slab + j * NK + i4);
+        a[0] = __fadd_rn(a[0], v.x); a[1] = __fadd_rn(a[1], v.y); a[2] = __fadd_rn(a[2], v.z); a[3] = __fadd_rn(a[3], v.w);
+      }
+    } else {
+      for (int64_t j = s0; j < s1; ++j)
+        for (int c = 0; c < 4 && i4 + c < NK; ++c) a[c] = __fadd_rn(a[c], slab[j * NK + i4 + c]);
+    }
+    for (int c = 0; c < 4; ++c) part[g * kSlabCols + q * 4 + c] = a[c];
+  }
+  __syncthreads();
+  if (t < kSlabCols && base + t < NK) {
+    float s = 0.0f;
+    for (int64_t g = 0; g < G; ++g) s = __fadd_rn(s, part[g * kSlabCols + t]);
+    const int64_t i = base + t;
+    out[(i / K) * ldo + (i % K)] = s;
+  }
+}
+
+bool slab_fused_enabled() {
+  static const bool on = [] {
+    const char* e = getenv("HGIN_SLAB_REDUCE");
+    return !(e && std::string(e) == "2pass");
+  }();
+  return on;
+}
+
 // ---------------------------------------------------------------------------------------------------
 // bf16 operands (cfg5): out[N, K] (fp32) = A^T [B1 | B2] on v_mfma_f32_32x32x16_bf16.  A bf16 fragment
 // holds 8 consecutive k (= 8 consecutive rows m here) of one column, but both operands are stored
@@ -927,6 +999,13 @@ int gemm_tn_impl(const char* what, const T* a, int64_t lda, const T* b1, int64_t
 #undef HGIN_TN_LAUNCH
   }
   const int64_t G = ceil_div(S_eff, kSlabGroup);
+  if (slab_fused_enabled() && G <= kSlabMaxG) {
+    const int64_t n_red = ceil_div(NK, kSlabCols);
+    const int64_t n_pro = pro_in ? N + 1 : 0;
+    k_slab_reduce<<<(unsigned)(n_red + n_pro), 256, 0, s>>>(slab, S_eff, NK, out, K, ldo, n_red, pro.pcol, pro.ps,
+                                                           ceil_div(N, tile_n) * S_eff, g_bias, g_prelu);
+    return check_launch(what);
+  }
   dim3 g1((unsigned)ceil_div(ceil_div(NK, 4), 256), (unsigned)G);
   k_slab_reduce1<<<g1, 256, 0, s>>>(slab, S_eff, NK, part);
   k_slab_reduce2<<<(unsigned)ceil_div(NK, 256), 256, 0, s>>>(part, G, NK, out, K, ldo);
