@@ -20,12 +20,14 @@ constexpr int kMinRowsPerBlock = 64;   // workspace sizing: the most blocks any 
 struct RowsCfg {
   int rpb = 256;
   int u = 0;
+  int nt = -1;   // -1: fp32 on, bf16 off (measured); 0 / 1 forced
 };
 const RowsCfg& rows_cfg() {
   static const RowsCfg c = [] {
     RowsCfg r;
     if (const char* v = getenv("HGIN_ROWS_RPB")) r.rpb = atoi(v);
     if (const char* v = getenv("HGIN_ROWS_U")) r.u = atoi(v);
+    if (const char* v = getenv("HGIN_ROWS_NT")) r.nt = atoi(v) != 0;
     if (r.rpb != 64 && r.rpb != 128 && r.rpb != 256) r.rpb = 256;
     if (r.u != 0 && r.u != 1 && r.u != 4) r.u = 0;
     return r;
@@ -81,11 +83,29 @@ struct RowVec<4, uint16_t> {
   }
 };
 
+// Read-once operand streams (g_y / z, g / x_dst) loaded non-temporally so they do not displace the output,
+// which the dW / dX GEMMs read next.  fp32: row kernel 5-15 % faster, cfg2 step -0.8 %; bf16: mixed in
+// isolation, cfg5 step equal, so off (HGIN_ROWS_NT=0/1 forces; profiles/r01/s6/rows_nt.txt).
+typedef float rows_f4v __attribute__((ext_vector_type(4)));
+typedef unsigned rows_u2v __attribute__((ext_vector_type(2)));
+template <bool NT, int VEC, typename T>
+__device__ __forceinline__ void rows_load(const T* p, float (&v)[VEC]) {
+  if constexpr (NT && VEC == 4 && sizeof(T) == 4) {
+    const rows_f4v t = __builtin_nontemporal_load(reinterpret_cast<const rows_f4v*>(p));
+    v[0] = t.x; v[1] = t.y; v[2] = t.z; v[3] = t.w;
+  } else if constexpr (NT && VEC == 4 && sizeof(T) == 2) {
+    const rows_u2v t = __builtin_nontemporal_load(reinterpret_cast<const rows_u2v*>(p));
+    v[0] = bf_lo(t.x); v[1] = bf_hi(t.x); v[2] = bf_lo(t.y); v[3] = bf_hi(t.y);
+  } else {
+    RowVec<VEC, T>::load(p, v);
+  }
+}
+
 // MODE 0: PReLU backward.  in0 = g_y, in1 = z; out = g_z; colsum(g_z) -> part_col; sum(z<=0 ? z*g : 0) -> part_s
 //         (the column sums and the slope sum use the fp32 g_z before any bf16 rounding of the output)
 // MODE 1: combine backward.  in0 = g (self-term columns), in1 = x_dst; out = s*g (optional);
 //         part_s = sum(g * x_dst); no column sums.
-template <int MODE, int VEC, typename T, int kU>
+template <int MODE, int VEC, typename T, int kU, bool NT = false>
 __global__ __launch_bounds__(256) void k_rows_bwd(const T* __restrict__ in0, int64_t ld0, const T* __restrict__ in1,
                                                   int64_t ld1, int64_t M, int N, const float* __restrict__ scalar,
                                                   T* __restrict__ out, int64_t ldo, float* __restrict__ part_col,
@@ -133,16 +153,16 @@ __global__ __launch_bounds__(256) void k_rows_bwd(const T* __restrict__ in0, int
         float g[kU][VEC], x[kU][VEC];
 #pragma unroll
         for (int u = 0; u < kU; ++u) {
-          RowVec<VEC, T>::load(in0 + (r + u * RL) * ld0 + c, g[u]);
-          RowVec<VEC, T>::load(in1 + (r + u * RL) * ld1 + c, x[u]);
+          rows_load<NT, VEC, T>(in0 + (r + u * RL) * ld0 + c, g[u]);
+          rows_load<NT, VEC, T>(in1 + (r + u * RL) * ld1 + c, x[u]);
         }
 #pragma unroll
         for (int u = 0; u < kU; ++u) row(r + u * RL, g[u], x[u]);
       }
       for (; r < r1; r += RL) {
         float g[VEC], x[VEC];
-        RowVec<VEC, T>::load(in0 + r * ld0 + c, g);
-        RowVec<VEC, T>::load(in1 + r * ld1 + c, x);
+        rows_load<NT, VEC, T>(in0 + r * ld0 + c, g);
+        rows_load<NT, VEC, T>(in1 + r * ld1 + c, x);
         row(r, g, x);
       }
     }
@@ -170,7 +190,13 @@ void launch_rows_bwd(bool vec, unsigned nblk, int rpb, hipStream_t s, const T* i
                      int64_t ld1, int64_t M, int N, const float* scalar, T* out, int64_t ldo, float* part_col,
                      float* part_s) {
   const bool u4 = rows_cfg().u == 4 || (rows_cfg().u == 0 && sizeof(T) == 4);
-  if (vec && u4)
+  const bool nt = rows_cfg().nt < 0 ? sizeof(T) == 4 : rows_cfg().nt == 1;
+  if (vec && nt) {
+    if (u4)
+      k_rows_bwd<MODE, 4, T, 4, true><<<nblk, 256, 0, s>>>(in0, ld0, in1, ld1, M, N, scalar, out, ldo, part_col, part_s, rpb);
+    else
+      k_rows_bwd<MODE, 4, T, 1, true><<<nblk, 256, 0, s>>>(in0, ld0, in1, ld1, M, N, scalar, out, ldo, part_col, part_s, rpb);
+  } else if (vec && u4)
     k_rows_bwd<MODE, 4, T, 4><<<nblk, 256, 0, s>>>(in0, ld0, in1, ld1, M, N, scalar, out, ldo, part_col, part_s, rpb);
   else if (vec)
     k_rows_bwd<MODE, 4, T, 1><<<nblk, 256, 0, s>>>(in0, ld0, in1, ld1, M, N, scalar, out, ldo, part_col, part_s, rpb);
@@ -185,18 +211,7 @@ bool rows_vec_ok(int64_t N, const T* a, int64_t lda, const T* b, int64_t ldb, co
   return N % 4 == 0 && ok(a) && lda % 4 == 0 && ok(b) && ldb % 4 == 0 && (c == nullptr || (ok(c) && ldc % 4 == 0));
 }
 
-// Sum block partials in a fixed order: one workgroup per column, strided per-thread sums + fixed tree.
-__global__ __launch_bounds__(256) void k_final_cols(const float* __restrict__ part, int64_t nblk, int N,
-                                                    float* __restrict__ out) {
-  __shared__ float red[256];
-  const int c = blockIdx.x;
-  const float* p = part + (int64_t)c * nblk;
-  float s = 0.0f;
-  for (int64_t b = threadIdx.x; b < nblk; b += 256) s = __fadd_rn(s, p[b]);
-  const float tot = block_sum_fixed(s, red);
-  if (threadIdx.x == 0) out[c] = tot;
-}
-
+// Sum block partials in a fixed order (one workgroup): strided per-thread sums + fixed tree.
 __global__ __launch_bounds__(256) void k_final_scalar(const float* __restrict__ part, int64_t nblk,
                                                       float* __restrict__ out) {
   __shared__ float red[256];
@@ -204,6 +219,23 @@ __global__ __launch_bounds__(256) void k_final_scalar(const float* __restrict__ 
   for (int64_t b = threadIdx.x; b < nblk; b += 256) s = __fadd_rn(s, part[b]);
   const float tot = block_sum_fixed(s, red);
   if (threadIdx.x == 0) out[0] = tot;
+}
+
+// Per-column sums (workgroups 0..N-1, one per column) and the slope sum (workgroup N) of the block partials in
+// one launch: strided per-thread sums + the fixed tree, so the order is fixed.
+__global__ __launch_bounds__(256) void k_final_cols_scalar(const float* __restrict__ part_col,
+                                                           const float* __restrict__ part_s, int64_t nblk, int N,
+                                                           float* __restrict__ out_col, float* __restrict__ out_s) {
+  __shared__ float red[256];
+  const int c = blockIdx.x;
+  const float* p = c < N ? part_col + (int64_t)c * nblk : part_s;
+  float s = 0.0f;
+  for (int64_t b = threadIdx.x; b < nblk; b += 256) s = __fadd_rn(s, p[b]);
+  const float tot = block_sum_fixed(s, red);
+  if (threadIdx.x == 0) {
+    if (c < N) out_col[c] = tot;
+    else out_s[0] = tot;
+  }
 }
 
 size_t prelu_ws_bytes(int64_t M, int64_t N) {
@@ -235,8 +267,7 @@ int prelu_bwd(const char* what, const T* g_y, int64_t ld_gy, const T* z, int64_t
                                            align_up(sizeof(float) * (size_t)(nblk * N), 256));
   launch_rows_bwd<0, T>(rows_vec_ok<T>(N, g_y, ld_gy, z, N, g_z, N), (unsigned)nblk, rpb, s, g_y, ld_gy, z, N, M, (int)N,
                         prelu, g_z, N, part_col, part_s);
-  k_final_cols<<<(unsigned)N, 256, 0, s>>>(part_col, nblk, (int)N, g_bias);
-  k_final_scalar<<<1, 256, 0, s>>>(part_s, nblk, g_prelu);
+  k_final_cols_scalar<<<(unsigned)N + 1, 256, 0, s>>>(part_col, part_s, nblk, (int)N, g_bias, g_prelu);
   return check_launch(what);
 }
 
