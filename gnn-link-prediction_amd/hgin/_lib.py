@@ -63,20 +63,54 @@ def is_stale() -> bool:
     return any(os.path.getmtime(p) > t for p in _deps())
 
 
+def _object(src: str) -> str:
+    return os.path.join(BUILD_DIR, os.path.basename(src)[:-4] + ".o")
+
+
+def _compile(src: str, verbose: bool) -> None:
+    """One translation unit -> an object carrying its own gfx950 code object (no -fgpu-rdc: kernels never
+    call across files), rebuilt only when it or a header changed."""
+    obj = _object(src)
+    headers = sorted(glob.glob(os.path.join(CSRC, "*.h"))) + [os.path.join(INCLUDE, "hgin.h")]
+    if os.path.exists(obj) and all(os.path.getmtime(p) <= os.path.getmtime(obj) for p in [src] + headers):
+        return
+    tmp = obj + f".{os.getpid()}.tmp"
+    cmd = [_hipcc()] + [f for f in HIPCC_FLAGS if f != "-shared"] + ["-I", INCLUDE, "-c", "-o", tmp, src]
+    if verbose:
+        print(" ".join(cmd))
+    res = subprocess.run(cmd, capture_output=True, text=True)
+    if res.returncode != 0:
+        if os.path.exists(tmp):
+            os.unlink(tmp)
+        raise HginUnavailable(f"hipcc failed on {os.path.basename(src)} ({res.returncode}):\n{res.stderr[-4000:]}")
+    os.replace(tmp, obj)
+
+
 def build(force: bool = False, verbose: bool = False) -> str:
-    """Compile every HIP source into libhgin.so for gfx950 (atomic replace).  Returns the path."""
+    """Compile every HIP source for gfx950 (one object per file, in parallel) and link libhgin.so (atomic
+    replace).  Returns the path."""
     if not force and not is_stale():
         return LIB_PATH
+    from concurrent.futures import ThreadPoolExecutor
     os.makedirs(BUILD_DIR, exist_ok=True)
+    srcs = sources()
+    if force:
+        for s in srcs:
+            if os.path.exists(_object(s)):
+                os.unlink(_object(s))
+    jobs = max(1, min(len(srcs), int(os.environ.get("MAX_JOBS", "0") or 0) or (os.cpu_count() or 4), 16))
+    with ThreadPoolExecutor(jobs) as ex:
+        for f in [ex.submit(_compile, s, verbose) for s in srcs]:
+            f.result()
     fd, tmp = tempfile.mkstemp(prefix=".libhgin.", suffix=".so", dir=BUILD_DIR)
     os.close(fd)
-    cmd = [_hipcc()] + HIPCC_FLAGS + ["-I", INCLUDE, "-o", tmp] + sources()
+    cmd = [_hipcc(), "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", tmp] + [_object(s) for s in srcs]
     if verbose:
         print(" ".join(cmd))
     try:
         res = subprocess.run(cmd, capture_output=True, text=True)
         if res.returncode != 0:
-            raise HginUnavailable(f"hipcc failed ({res.returncode}):\n{res.stderr[-4000:]}")
+            raise HginUnavailable(f"hipcc link failed ({res.returncode}):\n{res.stderr[-4000:]}")
         os.replace(tmp, LIB_PATH)
     finally:
         if os.path.exists(tmp):

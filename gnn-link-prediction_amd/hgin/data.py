@@ -63,6 +63,7 @@ class GraphConfig:
     global_feats: bool = False       # config.json:25
     mlp_layers: List[int] = field(default_factory=lambda: [128, 32])   # config.json:26
     feat_dtype: str = "f32"          # "bf16": cfg5 storage (features, activations, gradients); fp32 params
+    components: int = 1              # > 1: generated as this many independent, equal components (cfg4)
 
     @property
     def graph_edges(self) -> int:
@@ -99,6 +100,9 @@ CONFIGS: Dict[str, GraphConfig] = {
     # cfg4 component: one eighth of cfg3 (one per GPU of the 8-GPU node)
     "cfg4c": GraphConfig("cfg4c", 750_000, 375_000, 125_000, 3_750_000, 625_000, 3_750_000,
                          256, 256, 256, 256, 3),
+    # configs[3]: cfg3's 100M edges generated as 8 independent components; N GPUs take 8/N each
+    "cfg4": GraphConfig("cfg4", 6_000_000, 3_000_000, 1_000_000, 30_000_000, 5_000_000, 30_000_000,
+                        256, 256, 256, 256, 3, components=8),
     # configs[4]: cfg3 with bf16 node features + bf16 MFMA update (fp32 accumulate, fp32 master weights)
     "cfg5": GraphConfig("cfg5", 6_000_000, 3_000_000, 1_000_000, 30_000_000, 5_000_000, 30_000_000,
                         256, 256, 256, 256, 3, feat_dtype="bf16"),
@@ -201,3 +205,19 @@ def component_graph(cfg: GraphConfig, n_components: int, seed: int = 0, device="
     """cfg split into ``n_components`` independent graphs, collated."""
     part = scaled_config(cfg, 1.0 / n_components, name=f"{cfg.name}/{n_components}")
     return collate([synthetic_graph(part, seed=seed + i, device=device) for i in range(n_components)])
+
+
+def rank_components(cfg: GraphConfig, rank: int, world: int, device="cpu", n_components: Optional[int] = None
+                    ) -> Tuple[HeteroGraph, List[int]]:
+    """The components of ``cfg`` (generated as ``n_components`` equal independent graphs, default
+    ``cfg.components``) that rank ``rank`` of ``world`` owns — a contiguous block of n / world components,
+    component c always drawn from seed 1000 + c — collated into one batch.  The union over the ranks is the
+    same graph for every world size, so N GPUs split ONE fixed workload (strong scaling)."""
+    n = int(n_components or cfg.components)
+    if n < 1 or n % world:
+        raise ValueError(f"{n} components cannot be split evenly over {world} ranks")
+    per = n // world
+    ids = list(range(rank * per, (rank + 1) * per))
+    import dataclasses
+    part = dataclasses.replace(scaled_config(cfg, 1.0 / n, name=f"{cfg.name}/{n}"), components=1)
+    return collate([synthetic_graph(part, seed=1000 + c, device=device) for c in ids]), ids

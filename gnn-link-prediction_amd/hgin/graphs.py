@@ -7,7 +7,8 @@ launches (Python, autograd, ctypes).  HIP graphs remove that: the step runs on s
 fused loss limited to the batch's paths through a device-side count), is captured once after a short
 warm-up, and each iteration is one batched-copy launch (``GraphStore.collate_into``) + one graph replay.
 
-Numerically the padded step is the unpadded step: padding rows have no edges, so they never feed a real
+Numerically the padded step is the unpadded step for row-independent readouts (no BatchNorm, no global
+pooling, no dropout — refused by ``_check_row_independent``): padding rows have no edges, so they never feed a real
 row; their loss rows are masked, so their gradients are exactly zero and add nothing to any parameter
 gradient.  The optimizer must be capturable (``torch.optim.Adam(..., capturable=True)``).
 """
@@ -21,6 +22,21 @@ from .store import GraphStore, PaddedBatch
 from .train import mape, train_step
 
 
+def _check_row_independent(model: torch.nn.Module) -> None:
+    """A padded batch equals the exact batch only when nothing mixes rows across the batch outside the
+    graph's edges: padding path rows carry stale data and still pass through the readout.  BatchNorm
+    (MLP_BN) takes batch statistics over them, global pooling (GLOBAL_FEATS) pools them (and syncs the host
+    during capture), dropout > 0 draws fresh randomness per replay — all three are refused."""
+    if any(isinstance(m, torch.nn.modules.batchnorm._BatchNorm) for m in model.modules()):
+        raise ValueError("CapturedTrainStep: BatchNorm in the model (mlp_bn=True) would take batch statistics over "
+                         "padding rows; use the eager train_step")
+    if getattr(model, "global_feats", False):
+        raise ValueError("CapturedTrainStep: global_feats pools over padding rows (and syncs the host during "
+                         "capture); use the eager train_step")
+    if getattr(model, "dropout", 0.0) > 0.0:
+        raise ValueError("CapturedTrainStep: dropout > 0 is not replayable; use the eager train_step")
+
+
 class CapturedTrainStep:
     def __init__(self, model: torch.nn.Module, opt: torch.optim.Optimizer, store: GraphStore, batch_size: int,
                  warmup_ids: Sequence[Sequence[int]], warmup: int = 3):
@@ -28,6 +44,7 @@ class CapturedTrainStep:
             raise ValueError("CapturedTrainStep needs a capturable optimizer (e.g. Adam(..., capturable=True))")
         if not warmup_ids:
             raise ValueError("CapturedTrainStep needs at least one warm-up batch")
+        _check_row_independent(model)
         self.model, self.opt, self.store = model, opt, store
         self.batch: PaddedBatch = store.padded_batch(batch_size)
         # warm-up on a side stream (allocator pools, lazily created constants, the optimizer state)
@@ -50,15 +67,25 @@ class CapturedTrainStep:
         return self.loss
 
 
-def _forward_backward(model: torch.nn.Module, graph) -> torch.Tensor:
-    """train.py:33-43 without zero_grad / opt.step: forward (fused head + MAPE, §8 F3), sqrt, backward."""
+def _forward_backward(model: torch.nn.Module, graph, distributed: bool = False):
+    """train.py:33-43 without zero_grad / opt.step: forward (fused head + MAPE, §8 F3), sqrt, backward.
+
+    ``distributed``: back-propagate the rank's path sum S_r = m_r * mape_r instead (hgin/dist.py) and return
+    (S_r, m_r) for ``GradAllReducer.sync_sqrt_mean``."""
     if hasattr(model, "forward_loss"):
         _, loss_value = model.forward_loss(graph.x_dict(), graph.edge_index_dict(), graph.batch["path"], graph.y,
                                            getattr(graph, "m_valid", None))
     else:
         loss_value = mape(model(graph.x_dict(), graph.edge_index_dict(), graph.batch["path"]), graph.y.reshape(-1, 1))
-    torch.sqrt(loss_value).backward()
-    return loss_value.detach()
+    if not distributed:
+        torch.sqrt(loss_value).backward()
+        return loss_value.detach()
+    m_valid = getattr(graph, "m_valid", None)
+    m_local = (m_valid.to(torch.float32) if m_valid is not None
+               else torch.full((), float(graph.y.numel()), dtype=torch.float32, device=loss_value.device))
+    s_local = loss_value * m_local
+    s_local.backward()
+    return s_local.detach(), m_local
 
 
 class CapturedStaticStep:
@@ -71,8 +98,9 @@ class CapturedStaticStep:
     so bench.py uses it only with ``--graph``.  Capture protocol (the standard whole-step one): a few eager warm-up steps on a side stream
     (CSR / CSC caches, allocator pools, optimizer state), gradients set to None, then forward + loss +
     backward captured — the captured backward (re)writes every .grad in place on each replay — followed by
-    the optimizer step.  With a ``reducer`` (N > 1) the RCCL gradient all-reduce runs eagerly between two
-    replays (forward/backward, then the optimizer), so no collective is captured.  The optimizer must be
+    the optimizer step.  With a ``reducer`` (N > 1) the captured backward is that of the rank's path sum and the
+    RCCL gradient all-reduce (+ the sqrt-loss scaling, hgin/dist.py) runs eagerly between two replays
+    (forward/backward, then the optimizer), so no collective is captured.  The optimizer must be
     capturable (``torch.optim.Adam(..., capturable=True)``).  Every kernel is the eager step's, in the same
     order, so a replay equals an eager step with the same optimizer bit for bit (tests/test_gpu_model.py)."""
 
@@ -91,7 +119,7 @@ class CapturedStaticStep:
         self.fwd_bwd = torch.cuda.CUDAGraph()
         self.opt_graph: Optional[torch.cuda.CUDAGraph] = None
         with torch.cuda.graph(self.fwd_bwd):
-            self.loss = _forward_backward(model, graph)
+            self.loss = _forward_backward(model, graph, distributed=reducer is not None)
             if reducer is None:
                 opt.step()
         if reducer is not None:
@@ -102,7 +130,8 @@ class CapturedStaticStep:
     def step(self) -> torch.Tensor:
         """One training step; returns the device loss_value (no host sync)."""
         self.fwd_bwd.replay()
-        if self.opt_graph is not None:
-            self.reducer.sync()
-            self.opt_graph.replay()
-        return self.loss
+        if self.opt_graph is None:
+            return self.loss
+        loss_value = self.reducer.sync_sqrt_mean(*self.loss)
+        self.opt_graph.replay()
+        return loss_value

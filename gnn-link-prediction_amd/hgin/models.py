@@ -42,6 +42,51 @@ def _global_pool(x: torch.Tensor, batch: torch.Tensor, reduce: str) -> torch.Ten
         0, idx, x, reduce=reduce, include_self=False)
 
 
+def _host_call_device(model: torch.nn.Module, x_dict, edge_index_dict, path_batch):
+    """The HIP device to run a host-resident call on, or None when inputs and parameters are already on it.
+
+    ``train.py:322-348`` (``evaluate``) builds the model and the batches on the CPU and never calls
+    ``.cuda()``; there the call runs on the MI355X (there is no CPU fallback) and the result comes back to
+    the CPU.  Without a HIP device it raises."""
+    tensors = list(x_dict.values()) + list(edge_index_dict.values()) + [path_batch]
+    tensors += [p for p in model.parameters()]
+    if all(t is None or t.is_cuda for t in tensors):
+        return None
+    if any(t is not None and t.is_cuda for t in tensors):
+        devs = sorted({str(t.device) for t in tensors if t is not None})
+        raise RuntimeError(f"HetroGIN: inputs and parameters on different devices {devs}")
+    from ._lib import HginUnavailable
+    if not torch.cuda.is_available():
+        raise HginUnavailable("HetroGIN: the MI355X path has no CPU fallback and no HIP device is visible")
+    return torch.device("cuda", torch.cuda.current_device())
+
+
+class _DeviceCall(torch.nn.Module):
+    def __init__(self, model):
+        super().__init__()
+        self.m = model
+
+    def forward(self, x_dict, edge_index_dict, path_batch):
+        return self.m._run(x_dict, edge_index_dict, path_batch, None, None)
+
+
+def _host_call(model: torch.nn.Module, dev, x_dict, edge_index_dict, path_batch):
+    """Run ``model`` on ``dev`` with device copies of its (host) parameters and inputs, through
+    ``torch.func.functional_call``: gradients flow back to the host parameters, the output returns to the
+    host.  The host copies of the inputs are not modified (PyG's ``x_dict`` is a fresh dict per access)."""
+    if model.training and any(isinstance(m, torch.nn.modules.batchnorm._BatchNorm) for m in model.modules()):
+        raise RuntimeError("HetroGIN: a training-mode host-resident call would lose BatchNorm running-stat "
+                           "updates; move the model to the device (model.cuda(), train.py:177)")
+    host = next(iter(x_dict.values())).device
+    state = {"m." + n: t.to(dev) for n, t in model.named_parameters()}
+    state.update({"m." + n: t.to(dev) for n, t in model.named_buffers()})
+    xd = {k: v.to(dev) for k, v in x_dict.items()}
+    ed = {k: v.to(dev) for k, v in edge_index_dict.items()}
+    pb = path_batch.to(dev) if path_batch is not None else None
+    out = torch.func.functional_call(_DeviceCall(model), state, (xd, ed, pb))
+    return out.to(host)
+
+
 class HetroGIN(torch.nn.Module):
     def __init__(self, input_channels: dict, node_embedding_size: int, message_passing_layers: int, dropout: float,
                  concat_path: bool, bl_features: bool, divided_features: bool, global_feats: bool,
@@ -123,6 +168,9 @@ class HetroGIN(torch.nn.Module):
         return dead
 
     def forward(self, x_dict, edge_index_dict, path_batch):
+        dev = _host_call_device(self, x_dict, edge_index_dict, path_batch)
+        if dev is not None:
+            return _host_call(self, dev, x_dict, edge_index_dict, path_batch)
         return self._run(x_dict, edge_index_dict, path_batch, None, None)
 
     def forward_loss(self, x_dict, edge_index_dict, path_batch, y, m_valid=None):

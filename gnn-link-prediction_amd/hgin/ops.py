@@ -359,7 +359,8 @@ def gin_mlp_fwd(comb: Tensor, weight: Tensor, bias: Tensor, prelu: Optional[Tens
     if probe is None:
         launch()
     else:
-        probe.around("gin_mlp", 2.0 * M * N * K, launch)
+        probe.around("gin_mlp" if prelu is not None else "linear", 2.0 * M * N * K, launch,
+                     profiling.gemm_bytes(M, N, K, comb.element_size(), z is not None, accum is not None))
     return z, y
 
 

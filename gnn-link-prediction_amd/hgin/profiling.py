@@ -16,24 +16,28 @@ _probe: Optional["KernelProbe"] = None
 
 class KernelProbe:
     def __init__(self):
-        self.records: Dict[str, List[Tuple[torch.cuda.Event, torch.cuda.Event, float]]] = {}
+        self.records: Dict[str, List[Tuple[torch.cuda.Event, torch.cuda.Event, float, float]]] = {}
 
-    def around(self, kind: str, work: float, launch: Callable[[], None]) -> None:
+    def around(self, kind: str, work: float, launch: Callable[[], None], nbytes: float = 0.0) -> None:
+        """Time ``launch`` with events on the current stream; ``work`` is its algorithmic work (bytes for an
+        HBM-bound kernel, FLOPs for a GEMM), ``nbytes`` a GEMM's algorithmic HBM bytes."""
         s = torch.cuda.Event(enable_timing=True)
         e = torch.cuda.Event(enable_timing=True)
         s.record()
         launch()
         e.record()
-        self.records.setdefault(kind, []).append((s, e, float(work)))
+        self.records.setdefault(kind, []).append((s, e, float(work), float(nbytes)))
 
     def summary(self) -> Dict[str, dict]:
         torch.cuda.synchronize()
         out = {}
         for kind, recs in self.records.items():
-            ms = sum(s.elapsed_time(e) for s, e, _ in recs)
-            work = sum(w for _, _, w in recs)
-            out[kind] = {"launches": len(recs), "total_ms": ms, "avg_ms": ms / max(len(recs), 1),
-                         "work": work, "avg_work": work / max(len(recs), 1),
+            ms = sum(s.elapsed_time(e) for s, e, _, _ in recs)
+            work = sum(w for _, _, w, _ in recs)
+            nb = sum(b for _, _, _, b in recs)
+            n = max(len(recs), 1)
+            out[kind] = {"launches": len(recs), "total_ms": ms, "avg_ms": ms / n,
+                         "work": work, "avg_work": work / n, "avg_bytes": nb / n,
                          "rate_per_s": work / (ms / 1e3) if ms > 0 else 0.0}
         return out
 
@@ -52,6 +56,12 @@ def stop() -> Optional[KernelProbe]:
 
 def active() -> Optional[KernelProbe]:
     return _probe
+
+
+def gemm_bytes(M: int, N: int, K: int, s: int, z: bool, accum: bool) -> int:
+    """Algorithmic HBM bytes of the forward MLP GEMM y = prelu(A W^T + b) [+ accum]: A read once, W once,
+    y written, z written (saved for the backward) and accum read when present (s = element bytes)."""
+    return s * (M * K + N * K + M * N * (1 + int(z) + int(accum)))
 
 
 def aggregate_bytes(n_edges: int, n_rows: int, f_src: int, f_dst: int, mode: int, s: int = 4) -> int:

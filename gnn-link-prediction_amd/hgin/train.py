@@ -48,10 +48,18 @@ def train_step(model, opt, graph, loss_func=mape, reducer: Optional[GradAllReduc
     else:
         out = model(graph.x_dict(), graph.edge_index_dict(), graph.batch["path"])
         loss_value = loss_func(out, label)
-    loss = torch.sqrt(loss_value)
-    loss.backward()
-    if reducer is not None:
-        reducer.sync()
+    if reducer is None:
+        loss = torch.sqrt(loss_value)
+        loss.backward()
+    else:
+        # N ranks = one batch (hgin/dist.py): back-propagate this rank's path sum S_r = m_r * mape_r, then one
+        # all-reduce turns the gradients into those of sqrt(batch mape) and returns the batch loss value
+        m_valid = getattr(graph, "m_valid", None)
+        m_local = (m_valid.to(torch.float32) if m_valid is not None
+                   else torch.full((), float(label.numel()), dtype=torch.float32, device=loss_value.device))
+        s_local = loss_value * m_local
+        s_local.backward()
+        loss_value = reducer.sync_sqrt_mean(s_local, m_local)
     opt.step()
     if sync_metric:
         return float(mape(out, label).item())

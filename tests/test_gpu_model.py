@@ -206,3 +206,32 @@ def test_captured_static_step_equals_eager(feat):
     assert torch.equal(l_e[2], l_g[2]) and torch.equal(l_e[1], l_g[1])
     for a, b in zip(p_e, p_g):
         assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("case", ["cfg1_L2", "collate2_global_bn"])
+def test_evaluate_host_resident_call(case):
+    """train.py:322-348 unchanged: load_model on the CPU -> load_state_dict -> eval -> model(cpu batch) under
+    set_grad_enabled(False).  The call runs on the MI355X and returns the output on the CPU, within 1e-5 of
+    the reference's; a host-resident training call back-propagates into the host parameters."""
+    fx = load_fixture(case)
+    model = HetroGIN(**fixture_model_kwargs(fx))
+    model.load_state_dict({k[3:]: v for k, v in fx.items() if k.startswith("sd.")})
+    model.eval()
+    x, ei, batch, y = fixture_inputs(fx)
+    with torch.set_grad_enabled(False):
+        out = model(dict(x), ei, batch)
+    assert out.device.type == "cpu"
+    if not fx["meta"]["mlp_bn"]:        # training-mode BatchNorm: the fixture output is the train-mode one
+        assert _close(out, fx["out"])
+    if fx["meta"]["mlp_bn"]:
+        return
+    model.train()
+    out = model(dict(x), ei, batch)
+    torch.sqrt(mape(out, y.reshape(-1, 1))).backward()
+    no_grad = set(fx["meta"]["no_grad_params"])
+    for n, p in model.named_parameters():
+        if n in no_grad:
+            continue
+        ref = fx["grad." + n].double()
+        assert p.grad is not None and p.grad.device.type == "cpu", n
+        assert float((p.grad.double() - ref).norm()) <= 1e-4 * float(ref.norm()) + 1e-9, n

@@ -1,0 +1,63 @@
+"""libhgin.so's process-static kernel switches, each exercised in a fresh child process on the reference
+fixtures (tests/variant_child.py), so the non-default paths pytest's own process never selects are covered:
+
+  * HGIN_F32_GEMM=mfma32    — the exact-f32 MFMA GEMM (v_mfma_f32_32x32x2_f32) instead of the 3-way bf16 split:
+                              fixture tolerances (1e-5 outputs, 1e-4 gradients);
+  * HGIN_SLAB_REDUCE=2pass  — the two-launch weight-gradient slab sum: bit-identical to the one-launch default;
+  * HGIN_AGG_NQ=2 / HGIN_AGG_PIPE=1 / HGIN_AGG_TAIL=0 — aggregate lane-width / pipelined / tail variants:
+                              bit-identical to the default (every variant sums each row in edge order);
+  * HGIN_XCD=0              — GEMM tiles in plain order instead of XCD-contiguous: bit-identical.
+
+Each child is a separate interpreter started with subprocess (never an exec of this process).
+"""
+import os
+import subprocess
+import sys
+import tempfile
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+VARIANTS = {
+    "default": {},
+    "mfma32": {"HGIN_F32_GEMM": "mfma32"},
+    "slab2pass": {"HGIN_SLAB_REDUCE": "2pass"},
+    "agg_nq2": {"HGIN_AGG_NQ": "2"},
+    "agg_pipe": {"HGIN_AGG_PIPE": "1"},
+    "agg_notail": {"HGIN_AGG_TAIL": "0"},
+    "xcd_off": {"HGIN_XCD": "0"},
+}
+BITWISE_EQUAL_TO_DEFAULT = ("slab2pass", "agg_nq2", "agg_pipe", "agg_notail", "xcd_off")
+
+_results = {}
+
+
+def _run(name):
+    if name in _results:
+        return _results[name]
+    env = {k: v for k, v in os.environ.items() if not k.startswith("HGIN_")}
+    env.update(VARIANTS[name])
+    with tempfile.TemporaryDirectory() as d:
+        out = os.path.join(d, "res.pt")
+        p = subprocess.run([sys.executable, os.path.join(HERE, "variant_child.py"), out], env=env,
+                           capture_output=True, text=True, timeout=300)
+        assert p.returncode == 0, f"{name}: child failed ({p.returncode})\n{p.stdout[-2000:]}\n{p.stderr[-4000:]}"
+        _results[name] = torch.load(out, weights_only=True)
+    return _results[name]
+
+
+@pytest.mark.parametrize("name", sorted(VARIANTS))
+def test_variant_meets_fixture_tolerances(name):
+    _run(name)        # the child asserts the fixture tolerances itself
+
+
+@pytest.mark.parametrize("name", BITWISE_EQUAL_TO_DEFAULT)
+def test_variant_bitwise_equal_default(name):
+    ref, got = _run("default"), _run(name)
+    for case in ref:
+        assert ref[case].keys() == got[case].keys()
+        for k in ref[case]:
+            assert torch.equal(ref[case][k], got[case][k]), (name, case, k)

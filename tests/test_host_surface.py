@@ -36,6 +36,10 @@ def test_init_and_state_dict_match_reference(case):
 
 
 def test_forward_refuses_cpu_tensors():
+    """Host-resident call (train.py:322-348 evaluate) without a HIP device: raises, never a CPU fallback.
+    With a device the call runs there (tests/test_gpu_model.py::test_evaluate_host_resident_call)."""
+    if torch.cuda.is_available():
+        pytest.skip("a HIP device is visible: host-resident calls run on it")
     fx = load_fixture("cfg1_L2")
     model = HetroGIN(**fixture_model_kwargs(fx))
     x = {t: fx[f"in.x.{t}"] for t in ("path", "link", "node")}
