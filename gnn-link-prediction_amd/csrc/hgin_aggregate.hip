@@ -780,6 +780,132 @@ int check_aggregate_args(const char* what, const int32_t* rowptr, int64_t n_rows
   return HGIN_OK;
 }
 
+// ---------------------------------------------------------------------------------------------------
+// Long rows (degree skew; SURVEY.md §7 "Hard parts", §8.D skew variant).  The row-per-lane-group walk above
+// is serial in a row's edges, so one destination with millions of in-edges (Zipf(1.1) destinations: the top
+// link of cfg3 gets ~9 % of a relation's 30M edges) stalls the whole launch.  The host splits such rows out
+// of the CSR (ops.py: rows with more than HGIN_LONG_ROW edges are emptied in a compacted copy the main
+// kernel runs on — so it writes their self term, and zeros for the neighbour sum) and hands them here as
+// chunks of consecutive edges (items: [row-local chunk start, end) pairs, in edge order):
+//   k_long_partial: one wave per chunk, lanes across the features, the chunk's edges summed in edge order
+//                   (fp32) -> partial[chunk][F];
+//   k_long_combine: one wave per long row, its chunk partials added in chunk order, then the self term
+//                   ((1 + eps) x_dst for ADD, one rounding as the main kernel), stored over columns [0, F).
+// Fixed chunking and fixed combine order: bitwise reproducible run to run, but re-associated against the
+// CPU's sequential edge-order sum (a tolerance, not bit-exact; tests/test_gpu_kernels.py).
+template <typename T>
+struct LongElem;
+template <>
+struct LongElem<float> {
+  static __device__ __forceinline__ void load4(const float* p, float (&f)[4]) {
+    const float4 v = *reinterpret_cast<const float4*>(p);
+    f[0] = v.x; f[1] = v.y; f[2] = v.z; f[3] = v.w;
+  }
+  static __device__ __forceinline__ void store4(float* p, const float (&f)[4]) {
+    *reinterpret_cast<float4*>(p) = make_float4(f[0], f[1], f[2], f[3]);
+  }
+};
+template <>
+struct LongElem<uint16_t> {
+  static __device__ __forceinline__ void load4(const uint16_t* p, float (&f)[4]) {
+    const uint2 v = *reinterpret_cast<const uint2*>(p);
+    f[0] = bf_lo(v.x); f[1] = bf_hi(v.x); f[2] = bf_lo(v.y); f[3] = bf_hi(v.y);
+  }
+  static __device__ __forceinline__ void store4(uint16_t* p, const float (&f)[4]) {
+    *reinterpret_cast<uint2*>(p) = make_uint2(pack_bf2(f[0], f[1]), pack_bf2(f[2], f[3]));
+  }
+};
+
+template <typename T, int U>
+__global__ __launch_bounds__(256) void k_long_partial(const int32_t* __restrict__ col, const int32_t* __restrict__ items,
+                                                      int64_t n_items, const T* __restrict__ x_src, int64_t ld_src,
+                                                      int f_src, float* __restrict__ partial) {
+  const int lane = threadIdx.x & (kWave - 1);
+  const int64_t item = (int64_t)blockIdx.x * (blockDim.x / kWave) + (threadIdx.x / kWave);
+  if (item >= n_items) return;
+  const int beg = items[2 * item];
+  const int end = items[2 * item + 1];
+  float* prow = partial + item * f_src;
+  for (int f0 = lane * 4; f0 < f_src; f0 += kWave * 4) {
+    float acc[4] = {0.f, 0.f, 0.f, 0.f};
+    for (int k = beg; k < end; k += U) {
+      const int n = end - k;
+      float v[U][4];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        v[u][0] = v[u][1] = v[u][2] = v[u][3] = 0.f;
+        if (u < n) LongElem<T>::load4(x_src + (int64_t)col[k + u] * ld_src + f0, v[u]);
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        if (u < n)
+#pragma unroll
+          for (int c = 0; c < 4; ++c) acc[c] = __fadd_rn(acc[c], v[u][c]);
+    }
+    *reinterpret_cast<float4*>(prow + f0) = make_float4(acc[0], acc[1], acc[2], acc[3]);
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void k_long_combine(const int32_t* __restrict__ long_rows,
+                                                      const int32_t* __restrict__ item_ptr, int64_t n_long,
+                                                      const float* __restrict__ partial, int f_src,
+                                                      const T* __restrict__ x_dst, int64_t ld_dst,
+                                                      const float* __restrict__ eps, int combine, T* __restrict__ out,
+                                                      int64_t ld_out) {
+  const int lane = threadIdx.x & (kWave - 1);
+  const int64_t j = (int64_t)blockIdx.x * (blockDim.x / kWave) + (threadIdx.x / kWave);
+  if (j >= n_long) return;
+  const int64_t r = long_rows[j];
+  const int i0 = item_ptr[j], i1 = item_ptr[j + 1];
+  const float s = combine != HGIN_COMBINE_NONE ? __fadd_rn(1.0f, eps[0]) : 1.0f;
+  for (int f0 = lane * 4; f0 < f_src; f0 += kWave * 4) {
+    float acc[4];
+    {
+      const float4 p = *reinterpret_cast<const float4*>(partial + (int64_t)i0 * f_src + f0);
+      acc[0] = p.x; acc[1] = p.y; acc[2] = p.z; acc[3] = p.w;
+    }
+    for (int i = i0 + 1; i < i1; ++i) {
+      const float4 p = *reinterpret_cast<const float4*>(partial + (int64_t)i * f_src + f0);
+      acc[0] = __fadd_rn(acc[0], p.x); acc[1] = __fadd_rn(acc[1], p.y);
+      acc[2] = __fadd_rn(acc[2], p.z); acc[3] = __fadd_rn(acc[3], p.w);
+    }
+    if (combine == HGIN_COMBINE_ADD) {
+      float xd[4];
+      LongElem<T>::load4(x_dst + r * ld_dst + f0, xd);
+#pragma unroll
+      for (int c = 0; c < 4; ++c) acc[c] = __fadd_rn(acc[c], __fmul_rn(s, xd[c]));
+    }
+    LongElem<T>::store4(out + r * ld_out + f0, acc);
+  }
+}
+
+template <typename T>
+int aggregate_long(const char* what, const int32_t* col, const int32_t* items, int64_t n_items,
+                   const int32_t* long_rows, const int32_t* item_ptr, int64_t n_long, const T* x_src, int64_t ld_src,
+                   int64_t f_src, const T* x_dst, int64_t ld_dst, int64_t f_dst, const float* eps, int combine, T* out,
+                   int64_t ld_out, float* partial, size_t partial_bytes, void* stream) {
+  HGIN_ARG_CHECK(combine == HGIN_COMBINE_NONE || combine == HGIN_COMBINE_ADD || combine == HGIN_COMBINE_CONCAT,
+                 "%s: bad combine", what);
+  HGIN_ARG_CHECK(n_items >= 0 && n_long >= 0 && f_src >= 0, "%s: bad sizes", what);
+  if (n_long == 0 || f_src == 0) return HGIN_OK;
+  constexpr int E4 = 4;
+  HGIN_ARG_CHECK(col && items && long_rows && item_ptr && x_src && out && partial, "%s: NULL argument", what);
+  HGIN_ARG_CHECK(f_src % E4 == 0 && ld_src % E4 == 0 && ld_out % E4 == 0, "%s: f_src / ld must be multiples of 4", what);
+  HGIN_ARG_CHECK(combine != HGIN_COMBINE_ADD || (x_dst && eps && f_dst == f_src && ld_dst % E4 == 0),
+                 "%s: ADD needs x_dst / eps with f_dst == f_src", what);
+  HGIN_ARG_CHECK(combine == HGIN_COMBINE_NONE || eps, "%s: combine needs eps", what);
+  HGIN_ARG_CHECK(partial_bytes >= (size_t)n_items * (size_t)f_src * sizeof(float), "%s: partial workspace too small",
+                 what);
+  hipStream_t s = as_stream(stream);
+  const unsigned pb = (unsigned)ceil_div(n_items, 4);
+  k_long_partial<T, 8><<<pb, 256, 0, s>>>(col, items, n_items, x_src, ld_src, (int)f_src, partial);
+  const unsigned cb = (unsigned)ceil_div(n_long, 4);
+  k_long_combine<T><<<cb, 256, 0, s>>>(long_rows, item_ptr, n_long, partial, (int)f_src, x_dst, ld_dst, eps, combine,
+                                       out, ld_out);
+  return check_launch(what);
+}
+
 }  // namespace
 }  // namespace hgin
 
@@ -845,4 +971,25 @@ extern "C" int hgin_aggregate_f32(const int32_t* rowptr, const int32_t* col, int
   const int64_t widest = f_src > fd ? f_src : fd;
   return dispatch_g<1>((int)widest, rowptr, col, n_rows, x_src, ld_src, (int)f_src, x_dst, ld_dst, (int)f_dst, eps,
                        combine, out, ld_out, s);
+}
+
+
+extern "C" int hgin_aggregate_long_f32(const int32_t* col, const int32_t* items, int64_t n_items,
+                                       const int32_t* long_rows, const int32_t* item_ptr, int64_t n_long,
+                                       const float* x_src, int64_t ld_src, int64_t f_src, const float* x_dst,
+                                       int64_t ld_dst, int64_t f_dst, const float* eps, int combine, float* out,
+                                       int64_t ld_out, float* partial, size_t partial_bytes, void* stream) {
+  return aggregate_long<float>("hgin_aggregate_long_f32", col, items, n_items, long_rows, item_ptr, n_long, x_src,
+                               ld_src, f_src, x_dst, ld_dst, f_dst, eps, combine, out, ld_out, partial, partial_bytes,
+                               stream);
+}
+
+extern "C" int hgin_aggregate_long_bf16(const int32_t* col, const int32_t* items, int64_t n_items,
+                                        const int32_t* long_rows, const int32_t* item_ptr, int64_t n_long,
+                                        const uint16_t* x_src, int64_t ld_src, int64_t f_src, const uint16_t* x_dst,
+                                        int64_t ld_dst, int64_t f_dst, const float* eps, int combine, uint16_t* out,
+                                        int64_t ld_out, float* partial, size_t partial_bytes, void* stream) {
+  return aggregate_long<uint16_t>("hgin_aggregate_long_bf16", col, items, n_items, long_rows, item_ptr, n_long, x_src,
+                                  ld_src, f_src, x_dst, ld_dst, f_dst, eps, combine, out, ld_out, partial,
+                                  partial_bytes, stream);
 }

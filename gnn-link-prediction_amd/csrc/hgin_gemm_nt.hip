@@ -6,7 +6,9 @@
 // relation into a node type (models.py:286-298), and the readout Sequential(Linear, PReLU) layers applied
 // to cat(x_path, raw path features) (models.py:300-330, :362-374).  One kernel computes
 //     z = [A1 | A2] W^T + b ;  y = prelu(z) [+ accum]          (EPI 1; EPI 2: y = z; EPI 0: no bias)
-// with fp32 operands on the f32 matrix cores (v_mfma_f32_32x32x2_f32: exact f32, 157 TF/s chip peak).
+// with fp32 operands on the bf16 matrix cores by default: each operand is split into three bf16 planes at
+// staging time and every product is formed from six v_mfma_f32_32x32x16_bf16 terms (hgin_common.h, "split"
+// mode); HGIN_F32_GEMM=mfma32 selects the exact f32 matrix-core path (v_mfma_f32_32x32x2_f32, 157 TF/s peak).
 // The two A sources remove the readout's torch.cat: columns [0, K1) come from A1, [K1, K) from A2.
 //
 // Tiling: 256 threads = 4 waves.  Each wave owns 2 x TN MFMA tiles of 32 x 32 (64 rows x 32*TN columns);
@@ -748,6 +750,330 @@ int check_a_h(const char* what, const uint16_t* a1, int64_t lda1, int64_t k1, co
   return HGIN_OK;
 }
 
+// ---------------------------------------------------------------------------------------------------
+// k_nt2 — the same NT GEMM (fp32 split / bf16) and the same epilogues, restructured around LDS-DMA staging
+// (cdna_hip_programming.md §5 "Async global->LDS copy", "Pipelining across barriers"): the 128-row A stage
+// and the B stage go global -> LDS with global_load_lds_dwordx4 into an NST-deep ring of LDS buffers, with a
+// counted vmcnt and ONE raw s_barrier per stage (the 2-barrier register-staged loop above sits at that
+// structure's ceiling, ~40 % of the matrix-core rate at the cfg3 shapes).
+//   * B is pre-converted once per call (k_nt_planes, hgin_nt_planes): fp32 -> the three bf16 split planes
+//     (bf16: one plane), laid out per K-stage exactly as the LDS image ([stage][plane][N][stage k], XOR-
+//     swizzled 16-B chunks), so a stage is a plain contiguous copy and no workgroup re-splits W.
+//   * A stays fp32 in LDS (128-B rows of 32 k; bf16: 64 k) and each wave splits its own fragments after the
+//     ds_read (the two N-waves of a row split it twice: 88 VALU per 48 MFMA, issued between MFMAs).
+//   * Workgroup tile 128 x BN (BN = 256 or 128, the whole of N for the GIN layers, so A streams from HBM
+//     once), 2 x 2 waves of 64 x BN/2; per k16 the MFMAs run in the order of k_gemm_nt, so the result is
+//     bit-identical to it (same products, same per-accumulator order).
+// LDS image swizzles (16-B chunks; a ds_read_b128 lane group of 16 rows / columns hits 16 distinct slots):
+//   A (128-B rows):     chunk c of row r at slot c ^ ((r >> 1) & 7)
+//   B fp32 planes (64-B rows of 32 k): chunk c of column n at c ^ ((n >> 2) & 3)
+//   B bf16 (128-B rows of 64 k):       chunk c of column n at c ^ ((n >> 1) & 7)
+typedef __attribute__((address_space(3))) void lds_void_t;
+typedef __attribute__((address_space(1))) void glb_void_t;
+
+__device__ __forceinline__ void glds16(const void* g, void* lds_wave_base) {
+  __builtin_amdgcn_global_load_lds((glb_void_t*)g, (lds_void_t*)lds_wave_base, 16, 0, 0);
+}
+
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+template <typename T>
+struct Nt2 {
+  static constexpr bool kF32 = sizeof(T) == 4;
+  static constexpr int KS = kF32 ? 32 : 64;       // K elements per stage
+  static constexpr int KB = KS / 16;              // 16-deep MFMA k-blocks per stage
+  static constexpr int NP = kF32 ? 3 : 1;         // B planes
+  static constexpr int BROW = kF32 ? 64 : 128;    // bytes of one B plane row per stage
+  static constexpr int A_BYTES = 128 * 128;       // 128 rows x 128 B
+};
+
+// B planes, global layout [K / KS][NP][N][KS] (2-B elements), chunks swizzled as in the LDS image.
+template <typename T>
+__global__ __launch_bounds__(256) void k_nt_planes(const T* __restrict__ b, int64_t ldb, int64_t N, int64_t K,
+                                                   uint16_t* __restrict__ out) {
+  using P = Nt2<T>;
+  constexpr int CH = P::BROW / 16;                     // 16-B chunks per plane row
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;   // (stage, n, chunk)
+  const int64_t stages = K / P::KS;
+  if (i >= stages * N * CH) return;
+  const int q = (int)(i % CH);
+  const int64_t n = (i / CH) % N;
+  const int64_t s = i / (CH * N);
+  const int c = P::kF32 ? (q ^ (int)((n >> 2) & 3)) : (q ^ (int)((n >> 1) & 7));   // logical chunk at slot q
+  const int64_t k0 = s * P::KS + c * 8;
+  uint4 o[P::NP];
+  if constexpr (P::kF32) {
+    const float* src = reinterpret_cast<const float*>(b) + n * ldb + k0;
+    const float4 v0 = *reinterpret_cast<const float4*>(src);
+    const float4 v1 = *reinterpret_cast<const float4*>(src + 4);
+    uint2 a[3], bb[3];
+    split4(v0, a);
+    split4(v1, bb);
+#pragma unroll
+    for (int p = 0; p < 3; ++p) o[p] = make_uint4(a[p].x, a[p].y, bb[p].x, bb[p].y);
+  } else {
+    o[0] = *reinterpret_cast<const uint4*>(reinterpret_cast<const uint16_t*>(b) + n * ldb + k0);
+  }
+#pragma unroll
+  for (int p = 0; p < P::NP; ++p)
+    *reinterpret_cast<uint4*>(out + (((s * P::NP + p) * N + n) * P::BROW + q * 16) / 2) = o[p];
+}
+
+// One NT GEMM on the LDS-DMA structure.  A: [M, K] as [p1 (columns < k1) | eps-scaled p2], element type T;
+// Bp: planes of B [N, K] (k_nt_planes).  Requirements (checked by nt2_eligible): K, k1 multiples of KS, A
+// rows 16-B aligned, N a multiple of BN.
+template <typename T, int EPI, int BN, int NST, typename OutT>
+__global__ __launch_bounds__(256, 1) void k_nt2(const T* __restrict__ a1, int64_t lda1, const T* __restrict__ a2,
+                                                int64_t lda2, int64_t k1, const float* __restrict__ eps2,
+                                                const uint16_t* __restrict__ Bp, int64_t M, int64_t N, int64_t K,
+                                                const float* __restrict__ bias, const float* __restrict__ prelu,
+                                                const OutT* __restrict__ accum, OutT* __restrict__ Z,
+                                                OutT* __restrict__ Y, int64_t ldc, bool vec_out, int64_t n_tiles,
+                                                bool xcd, CombEpi ce) {
+  using P = Nt2<T>;
+  constexpr int TN = BN / 64;                            // 32-col MFMA tiles per wave (wave tile 64 x BN/2)
+  constexpr int WC = BN / 2;
+  constexpr int B_BYTES = P::NP * BN * P::BROW;
+  constexpr int STAGE = P::A_BYTES + B_BYTES;
+  constexpr int A_INS = P::A_BYTES / 1024 / 4;           // glds per wave per stage
+  constexpr int BP_INS = BN * P::BROW / 1024 / 4;        // per plane
+  constexpr int G = A_INS + P::NP * BP_INS;
+  extern __shared__ __attribute__((aligned(16))) char nt2_smem[];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wm = wave >> 1;
+  const int wn = wave & 1;
+  const int li = lane & 31;
+  const int lh = lane >> 5;
+  const int64_t n_tiles_n = N / BN;
+  const int64_t q = xcd ? xcd_logical(blockIdx.x, gridDim.x) : (int64_t)blockIdx.x;
+  if (q >= n_tiles) return;
+  const int64_t m0 = (q / n_tiles_n) * 128;
+  const int64_t n0 = (q % n_tiles_n) * BN;
+  const int64_t S = K / P::KS;
+  const float sc2 = eps2 ? __fadd_rn(1.0f, eps2[0]) : 1.0f;
+
+  // per-lane A source rows of this wave's glds instructions (rows past M clamp to M - 1; their products
+  // land in rows that are never stored)
+  int64_t a_row_off1[A_INS], a_row_off2[A_INS];
+  int a_chunk[A_INS];
+#pragma unroll
+  for (int i = 0; i < A_INS; ++i) {
+    const int r = (wave * A_INS + i) * 8 + (lane >> 3);
+    int64_t gr = m0 + r;
+    gr = gr < M ? gr : M - 1;
+    a_row_off1[i] = gr * lda1;
+    a_row_off2[i] = gr * lda2;
+    a_chunk[i] = ((lane & 7) ^ ((r >> 1) & 7)) * (16 / (int)sizeof(T));
+  }
+  const uintptr_t u1 = reinterpret_cast<uintptr_t>(a1), u2 = reinterpret_cast<uintptr_t>(a2);
+  auto issue = [&](int64_t s, int buf) {
+    char* base = nt2_smem + buf * STAGE;
+    const int64_t k0 = s * P::KS;
+    const bool first = k0 < k1;
+    const T* src = reinterpret_cast<const T*>(first ? u1 : u2);
+    const int64_t kk = first ? k0 : k0 - k1;
+#pragma unroll
+    for (int i = 0; i < A_INS; ++i)
+      glds16(src + (first ? a_row_off1[i] : a_row_off2[i]) + kk + a_chunk[i], base + (wave * A_INS + i) * 1024);
+    const char* bsrc = reinterpret_cast<const char*>(Bp) + ((s * P::NP) * N + n0) * P::BROW;
+#pragma unroll
+    for (int p = 0; p < P::NP; ++p)
+#pragma unroll
+      for (int j = 0; j < BP_INS; ++j) {
+        const int off = (wave * BP_INS + j) * 1024;
+        glds16(bsrc + (int64_t)p * N * P::BROW + off + lane * 16, base + P::A_BYTES + p * BN * P::BROW + off);
+      }
+  };
+
+  f32x16 acc[2][TN];
+#pragma unroll
+  for (int x = 0; x < 2; ++x)
+#pragma unroll
+    for (int y = 0; y < TN; ++y)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[x][y][e] = 0.0f;
+
+#pragma unroll
+  for (int s = 0; s < NST - 1; ++s)
+    if (s < S) issue(s, s);
+
+  for (int64_t s = 0; s < S; ++s) {
+    // stage s landed for this wave's DMAs: everything issued after it may stay in flight
+    const int64_t ahead = (S - 1 < s + NST - 2 ? S - 1 : s + NST - 2) - s;
+    if constexpr (NST >= 3) {
+      if (ahead >= 1) wait_vm<G>(); else wait_vm<0>();
+    } else {
+      wait_vm<0>();
+    }
+    __builtin_amdgcn_s_barrier();      // every wave's stage-s DMAs landed; every wave is done with stage s-1
+    asm volatile("" ::: "memory");
+    if (s + NST - 1 < S) issue(s + NST - 1, (int)((s + NST - 1) % NST));
+    const char* base = nt2_smem + (s % NST) * STAGE;
+    const bool scale = eps2 != nullptr && s * P::KS >= k1;
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int kb = 0; kb < P::KB; ++kb) {
+      bf16x8 fa[2][P::NP], fb[TN][P::NP];
+#pragma unroll
+      for (int tm = 0; tm < 2; ++tm) {
+        const int r = wm * 64 + tm * 32 + li;
+        const char* row = base + r * 128;
+        const int sw = (r >> 1) & 7;
+        if constexpr (P::kF32) {
+          const int c0 = kb * 4 + lh * 2;
+          float4 v0 = *reinterpret_cast<const float4*>(row + ((c0 ^ sw) << 4));
+          float4 v1 = *reinterpret_cast<const float4*>(row + (((c0 + 1) ^ sw) << 4));
+          if (scale) {
+            v0 = make_float4(__fmul_rn(sc2, v0.x), __fmul_rn(sc2, v0.y), __fmul_rn(sc2, v0.z), __fmul_rn(sc2, v0.w));
+            v1 = make_float4(__fmul_rn(sc2, v1.x), __fmul_rn(sc2, v1.y), __fmul_rn(sc2, v1.z), __fmul_rn(sc2, v1.w));
+          }
+          uint2 o0[3], o1[3];
+          split4(v0, o0);
+          split4(v1, o1);
+#pragma unroll
+          for (int p = 0; p < 3; ++p) {
+            const uint4 u = make_uint4(o0[p].x, o0[p].y, o1[p].x, o1[p].y);
+            fa[tm][p] = __builtin_bit_cast(bf16x8, u);
+          }
+        } else {
+          const int c = kb * 2 + lh;
+          uint4 u = *reinterpret_cast<const uint4*>(row + ((c ^ sw) << 4));
+          if (scale) u = make_uint4(scale_bf2(u.x, sc2), scale_bf2(u.y, sc2), scale_bf2(u.z, sc2), scale_bf2(u.w, sc2));
+          fa[tm][0] = __builtin_bit_cast(bf16x8, u);
+        }
+      }
+#pragma unroll
+      for (int tn = 0; tn < TN; ++tn) {
+        const int n = wn * WC + tn * 32 + li;
+        const int c = kb * 2 + lh;
+        const int slot = P::kF32 ? (c ^ ((n >> 2) & 3)) : (c ^ ((n >> 1) & 7));
+#pragma unroll
+        for (int p = 0; p < P::NP; ++p)
+          fb[tn][p] = *reinterpret_cast<const bf16x8*>(base + P::A_BYTES + p * BN * P::BROW + n * P::BROW + (slot << 4));
+      }
+#pragma unroll
+      for (int tm = 0; tm < 2; ++tm)
+#pragma unroll
+        for (int tn = 0; tn < TN; ++tn) {
+          if constexpr (P::kF32) {   // k_gemm_nt's order: smallest terms first
+            acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[tm][2], fb[tn][0], acc[tm][tn], 0, 0, 0);
+            acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[tm][1], fb[tn][1], acc[tm][tn], 0, 0, 0);
+            acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[tm][0], fb[tn][2], acc[tm][tn], 0, 0, 0);
+            acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[tm][1], fb[tn][0], acc[tm][tn], 0, 0, 0);
+            acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[tm][0], fb[tn][1], acc[tm][tn], 0, 0, 0);
+            acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[tm][0], fb[tn][0], acc[tm][tn], 0, 0, 0);
+          } else {
+            acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[tm][0], fb[tn][0], acc[tm][tn], 0, 0, 0);
+          }
+        }
+    }
+    __builtin_amdgcn_s_setprio(0);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // this wave's reads of the buffer are done
+  }
+
+  float ep = 0.0f;
+  float* smem = reinterpret_cast<float*>(nt2_smem);
+  epilogue<EPI, TN, OutT>(acc, smem, wave, wm, wn, lane, li, lh, m0, n0, M, N, bias, prelu, accum, Z, Y, ldc,
+                          vec_out, ce, &ep);
+  if constexpr (EPI == 4) tile_partial(smem, ep, ce.part, q);
+}
+
+template <typename T, int BN>
+constexpr size_t nt2_lds_bytes() {
+  using P = Nt2<T>;
+  constexpr size_t stage = P::A_BYTES + (size_t)P::NP * BN * P::BROW;
+  constexpr size_t ring = stage * (P::kF32 ? 2 : 3);
+  constexpr size_t epi = 4 * 32 * (BN / 2 + 4) * 4;
+  return ring > epi ? ring : epi;
+}
+
+// Measured (profiles/r02/nt2_not_adopted_*.txt, cfg3 / cfg5 shapes): bit-identical, but 5-16 % slower than
+// k_gemm_nt in fp32 and 1.5-1.7x slower in bf16 — at one 128 x 256 workgroup per CU the three B planes fill
+// the LDS ring and only one 16-KB A stage is in flight per CU, against three register-prefetched tiles in
+// k_gemm_nt.  So it is off by default; HGIN_NT2=1 selects it where planes are passed.
+bool nt2_enabled() {
+  static const bool on = [] {
+    const char* v = getenv("HGIN_NT2");
+    return v && v[0] == '1';
+  }();
+  return on;
+}
+
+template <typename T>
+int nt2_bn(int64_t N) {
+  return N % 256 == 0 ? 256 : (N % 128 == 0 ? 128 : 0);
+}
+
+template <typename T>
+bool nt2_eligible(const T* a1, int64_t lda1, int64_t k1, const T* a2, int64_t lda2, const void* planes, int64_t N,
+                  int64_t K, bool split_mode) {
+  using P = Nt2<T>;
+  constexpr int EPR = 16 / (int)sizeof(T);   // elements per 16 B
+  if (!planes || !nt2_enabled()) return false;
+  if (P::kF32 && !split_mode) return false;   // the exact-f32 MFMA mode keeps k_gemm_nt
+  if (K % P::KS || k1 % P::KS || nt2_bn<T>(N) == 0) return false;
+  if (k1 > 0 && (!aligned16(a1) || lda1 % EPR)) return false;
+  if (k1 < K && (!aligned16(a2) || lda2 % EPR)) return false;
+  return true;
+}
+
+template <typename T, int EPI, typename OutT>
+int launch_nt2(const T* a1, int64_t lda1, int64_t k1, const T* a2, int64_t lda2, const float* eps2,
+               const void* planes, int64_t M, int64_t N, int64_t K, const float* bias, const float* prelu,
+               const OutT* accum, OutT* z, OutT* y, int64_t ldc, hipStream_t s, const char* what,
+               const CombEpi& ce = CombEpi{}, int64_t* tiles_out = nullptr) {
+  const bool vec_out = ldc % 4 == 0 && aligned16(y) && (z == nullptr || aligned16(z)) &&
+                       (accum == nullptr || aligned16(accum)) &&
+                       (EPI != 4 || (aligned16(ce.xd) && ce.ldxd % 4 == 0 &&
+                                     (ce.gd == nullptr || (aligned16(ce.gd) && ce.ldgd % 4 == 0))));
+  const bool xcd = xcd_remap_enabled();
+  const uint16_t* bp = static_cast<const uint16_t*>(planes);
+#define HGIN_NT2_LAUNCH(BNV)                                                                                   \
+  {                                                                                                            \
+    constexpr int NSTV = Nt2<T>::kF32 ? 2 : 3;                                                                 \
+    constexpr size_t lds = nt2_lds_bytes<T, BNV>();                                                            \
+    auto kern = k_nt2<T, EPI, BNV, NSTV, OutT>;                                                                \
+    static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),                    \
+                                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds); \
+    if (attr != hipSuccess) {                                                                                  \
+      set_error("%s: hipFuncSetAttribute failed: %s", what, hipGetErrorString(attr));                         \
+      return (int)attr;                                                                                        \
+    }                                                                                                          \
+    const int64_t tiles = ceil_div(M, 128) * (N / BNV);                                                        \
+    dim3 grid((unsigned)(xcd ? round_up8(tiles) : tiles));                                                     \
+    kern<<<grid, 256, lds, s>>>(a1, lda1, a2, lda2, k1, eps2, bp, M, N, K, bias, prelu, accum, z, y, ldc,      \
+                                vec_out, tiles, xcd, ce);                                                      \
+    if (tiles_out) *tiles_out = tiles;                                                                         \
+  }
+  if (N % 256 == 0)
+    HGIN_NT2_LAUNCH(256)
+  else
+    HGIN_NT2_LAUNCH(128)
+#undef HGIN_NT2_LAUNCH
+  return check_launch(what);
+}
+
+template <typename T>
+size_t nt_planes_bytes(int64_t N, int64_t K) {
+  return (size_t)N * (size_t)K * Nt2<T>::NP * 2;
+}
+
+template <typename T>
+int nt_planes(const T* b, int64_t ldb, int64_t N, int64_t K, void* out, hipStream_t s, const char* what) {
+  using P = Nt2<T>;
+  HGIN_ARG_CHECK(N > 0 && K > 0 && K % P::KS == 0, "%s: K must be a positive multiple of %d", what, P::KS);
+  HGIN_ARG_CHECK(b && out && ldb >= K && aligned16(b) && ldb % (16 / (int)sizeof(T)) == 0 && aligned16(out),
+                 "%s: bad operand / alignment", what);
+  const int64_t work = (K / P::KS) * N * (P::BROW / 16);
+  k_nt_planes<T><<<(unsigned)ceil_div(work, 256), 256, 0, s>>>(b, ldb, N, K, static_cast<uint16_t*>(out));
+  return check_launch(what);
+}
+
 // Fixed-order sum of the EPI 4 tile partials: level 1 (k_part_sum over kPartChunk-long chunks, one workgroup
 // each), level 2 (one workgroup over the level-1 sums).  cfg5 launches ~94k tiles: one workgroup alone took 0.1 ms.
 constexpr int64_t kPartChunk = 4096;
@@ -780,7 +1106,8 @@ size_t combine_ws_bytes(int64_t M, int64_t N) {
 template <typename T>
 int gemm_nt_combine(const char* what, const T* a, int64_t lda, const T* b, int64_t ldb, T* c, int64_t ldc, int64_t M,
                     int64_t N, int64_t K, const T* x_dst, int64_t ld_xd, T* g_dst, int64_t ld_gd, int64_t cs,
-                    const float* eps, float* g_eps, void* workspace, size_t workspace_bytes, void* stream) {
+                    const float* eps, float* g_eps, void* workspace, size_t workspace_bytes, const void* b_planes,
+                    void* stream) {
   HGIN_ARG_CHECK(M >= 0 && N >= 0 && K >= 0 && cs >= 0 && cs <= N, "%s: bad sizes", what);
   HGIN_ARG_CHECK(N <= 65535 * 128 && M < (int64_t(1) << 31), "%s: size too large", what);
   HGIN_ARG_CHECK(cs % 4 == 0, "%s: the self columns must start at a multiple of 4", what);
@@ -799,7 +1126,10 @@ int gemm_nt_combine(const char* what, const T* a, int64_t lda, const T* b, int64
   const CombEpi ce{x_dst, ld_xd, g_dst, ld_gd, cs, eps, part};
   int64_t tiles = 0;
   int rc;
-  if constexpr (sizeof(T) == 2)
+  if (nt2_eligible<T>(a, lda, K, nullptr, 0, b_planes, N, K, gemm_split_enabled()))
+    rc = launch_nt2<T, 4, T>(a, lda, K, nullptr, 0, nullptr, b_planes, M, N, K, nullptr, nullptr, nullptr, nullptr, c,
+                             ldc, s, what, ce, &tiles);
+  else if constexpr (sizeof(T) == 2)
     rc = launch_nt_bf16<4, uint16_t>(Src2h{a, lda, nullptr, 0, K}, Src2h{b, ldb, nullptr, 0, K}, M, N, K, nullptr,
                                      nullptr, nullptr, nullptr, c, ldc, s, what, ce, &tiles);
   else
@@ -832,51 +1162,62 @@ extern "C" int hgin_gemm_nt_combine_workspace_size(int64_t M, int64_t N, size_t*
 extern "C" int hgin_gemm_nt_combine_f32(const float* a, int64_t lda, const float* b, int64_t ldb, float* c,
                                         int64_t ldc, int64_t M, int64_t N, int64_t K, const float* x_dst,
                                         int64_t ld_xd, float* g_dst, int64_t ld_gd, int64_t cs, const float* eps,
-                                        float* g_eps, void* workspace, size_t workspace_bytes, void* stream) {
+                                        float* g_eps, void* workspace, size_t workspace_bytes, const void* b_planes,
+                                        void* stream) {
   return gemm_nt_combine<float>("hgin_gemm_nt_combine_f32", a, lda, b, ldb, c, ldc, M, N, K, x_dst, ld_xd, g_dst,
-                                ld_gd, cs, eps, g_eps, workspace, workspace_bytes, stream);
+                                ld_gd, cs, eps, g_eps, workspace, workspace_bytes, b_planes, stream);
 }
 
 extern "C" int hgin_gemm_nt_combine_bf16(const uint16_t* a, int64_t lda, const uint16_t* b, int64_t ldb, uint16_t* c,
                                          int64_t ldc, int64_t M, int64_t N, int64_t K, const uint16_t* x_dst,
                                          int64_t ld_xd, uint16_t* g_dst, int64_t ld_gd, int64_t cs, const float* eps,
-                                         float* g_eps, void* workspace, size_t workspace_bytes, void* stream) {
+                                         float* g_eps, void* workspace, size_t workspace_bytes, const void* b_planes,
+                                         void* stream) {
   return gemm_nt_combine<uint16_t>("hgin_gemm_nt_combine_bf16", a, lda, b, ldb, c, ldc, M, N, K, x_dst, ld_xd, g_dst,
-                                   ld_gd, cs, eps, g_eps, workspace, workspace_bytes, stream);
+                                   ld_gd, cs, eps, g_eps, workspace, workspace_bytes, b_planes, stream);
 }
 
 extern "C" int hgin_gin_mlp_fwd_bf16(const uint16_t* a1, int64_t lda1, int64_t k1, const uint16_t* a2, int64_t lda2,
                                      const float* a2_eps, const uint16_t* w, const float* bias, const float* prelu,
                                      const uint16_t* accum, uint16_t* z, uint16_t* y, int64_t M, int64_t N, int64_t K,
-                                     void* stream) {
+                                     const void* w_planes, void* stream) {
   HGIN_ARG_CHECK(M >= 0 && N >= 0 && K >= 0, "hgin_gin_mlp_fwd_bf16: negative size");
   HGIN_ARG_CHECK(M < (int64_t(1) << 31) && N <= 65535 * 128, "hgin_gin_mlp_fwd_bf16: size too large");
   if (M == 0 || N == 0) return HGIN_OK;
   HGIN_ARG_CHECK(w && bias && prelu && y, "hgin_gin_mlp_fwd_bf16: NULL operand");
   if (int rc = check_a_h("hgin_gin_mlp_fwd_bf16", a1, lda1, k1, a2, lda2, K)) return rc;
+  if (nt2_eligible<uint16_t>(a1, lda1, k1, a2, lda2, w_planes, N, K, true))
+    return launch_nt2<uint16_t, 1, uint16_t>(a1, lda1, k1, a2, lda2, a2_eps, w_planes, M, N, K, bias, prelu, accum, z, y,
+                                             N, as_stream(stream), "hgin_gin_mlp_fwd_bf16");
   return launch_nt_bf16<1, uint16_t>(Src2h{a1, lda1, a2, lda2, k1, a2_eps}, Src2h{w, K, nullptr, 0, K}, M, N, K, bias, prelu,
                                      accum, z, y, N, as_stream(stream), "hgin_gin_mlp_fwd_bf16");
 }
 
 extern "C" int hgin_linear_fwd_bf16(const uint16_t* a1, int64_t lda1, int64_t k1, const uint16_t* a2, int64_t lda2,
                                     const uint16_t* w, const float* bias, float* y, int64_t M, int64_t N, int64_t K,
-                                    void* stream) {
+                                    const void* w_planes, void* stream) {
   HGIN_ARG_CHECK(M >= 0 && N >= 0 && K >= 0, "hgin_linear_fwd_bf16: negative size");
   HGIN_ARG_CHECK(M < (int64_t(1) << 31) && N <= 65535 * 128, "hgin_linear_fwd_bf16: size too large");
   if (M == 0 || N == 0) return HGIN_OK;
   HGIN_ARG_CHECK(w && bias && y, "hgin_linear_fwd_bf16: NULL operand");
   if (int rc = check_a_h("hgin_linear_fwd_bf16", a1, lda1, k1, a2, lda2, K)) return rc;
+  if (nt2_eligible<uint16_t>(a1, lda1, k1, a2, lda2, w_planes, N, K, true))
+    return launch_nt2<uint16_t, 2, float>(a1, lda1, k1, a2, lda2, nullptr, w_planes, M, N, K, bias, nullptr, nullptr,
+                                          nullptr, y, N, as_stream(stream), "hgin_linear_fwd_bf16");
   return launch_nt_bf16<2, float>(Src2h{a1, lda1, a2, lda2, k1}, Src2h{w, K, nullptr, 0, K}, M, N, K, bias, nullptr,
                                   nullptr, nullptr, y, N, as_stream(stream), "hgin_linear_fwd_bf16");
 }
 
 extern "C" int hgin_gemm_nt_bf16(const uint16_t* a, int64_t lda, const uint16_t* b, int64_t ldb, uint16_t* c,
-                                 int64_t ldc, int64_t M, int64_t N, int64_t K, void* stream) {
+                                 int64_t ldc, int64_t M, int64_t N, int64_t K, const void* b_planes, void* stream) {
   HGIN_ARG_CHECK(M >= 0 && N >= 0 && K >= 0, "hgin_gemm_nt_bf16: negative size");
   HGIN_ARG_CHECK(N <= 65535 * 128, "hgin_gemm_nt_bf16: N too large");
   if (M == 0 || N == 0) return HGIN_OK;
   HGIN_ARG_CHECK(a && b && c, "hgin_gemm_nt_bf16: NULL operand");
   HGIN_ARG_CHECK(lda >= K && ldb >= K && ldc >= N, "hgin_gemm_nt_bf16: leading dimension too small");
+  if (nt2_eligible<uint16_t>(a, lda, K, nullptr, 0, b_planes, N, K, true))
+    return launch_nt2<uint16_t, 0, uint16_t>(a, lda, K, nullptr, 0, nullptr, b_planes, M, N, K, nullptr, nullptr,
+                                             nullptr, nullptr, c, ldc, as_stream(stream), "hgin_gemm_nt_bf16");
   return launch_nt_bf16<0, uint16_t>(Src2h{a, lda, nullptr, 0, K}, Src2h{b, ldb, nullptr, 0, K}, M, N, K, nullptr,
                                      nullptr, nullptr, nullptr, c, ldc, as_stream(stream), "hgin_gemm_nt_bf16");
 }
@@ -884,35 +1225,58 @@ extern "C" int hgin_gemm_nt_bf16(const uint16_t* a, int64_t lda, const uint16_t*
 extern "C" int hgin_gin_mlp_fwd_f32(const float* a1, int64_t lda1, int64_t k1, const float* a2, int64_t lda2,
                                     const float* a2_eps, const float* w, const float* bias, const float* prelu,
                                     const float* accum, float* z, float* y, int64_t M, int64_t N, int64_t K,
-                                    void* stream) {
+                                    const void* w_planes, void* stream) {
   HGIN_ARG_CHECK(M >= 0 && N >= 0 && K >= 0, "hgin_gin_mlp_fwd_f32: negative size");
   HGIN_ARG_CHECK(M < (int64_t(1) << 31) && N <= 65535 * 128, "hgin_gin_mlp_fwd_f32: size too large");
   if (M == 0 || N == 0) return HGIN_OK;
   HGIN_ARG_CHECK(w && bias && prelu && y, "hgin_gin_mlp_fwd_f32: NULL operand");
   if (int rc = check_a("hgin_gin_mlp_fwd_f32", a1, lda1, k1, a2, lda2, K)) return rc;
+  if (nt2_eligible<float>(a1, lda1, k1, a2, lda2, w_planes, N, K, gemm_split_enabled()))
+    return launch_nt2<float, 1, float>(a1, lda1, k1, a2, lda2, a2_eps, w_planes, M, N, K, bias, prelu, accum, z, y, N,
+                                       as_stream(stream), "hgin_gin_mlp_fwd_f32");
   return launch_nt<1>(Src2{a1, lda1, a2, lda2, k1, a2_eps}, Src2{w, K, nullptr, 0, K}, M, N, K, bias, prelu, accum, z, y,
                       N, as_stream(stream), "hgin_gin_mlp_fwd_f32");
 }
 
 extern "C" int hgin_linear_fwd_f32(const float* a1, int64_t lda1, int64_t k1, const float* a2, int64_t lda2,
                                    const float* w, const float* bias, float* y, int64_t M, int64_t N, int64_t K,
-                                   void* stream) {
+                                   const void* w_planes, void* stream) {
   HGIN_ARG_CHECK(M >= 0 && N >= 0 && K >= 0, "hgin_linear_fwd_f32: negative size");
   HGIN_ARG_CHECK(M < (int64_t(1) << 31) && N <= 65535 * 128, "hgin_linear_fwd_f32: size too large");
   if (M == 0 || N == 0) return HGIN_OK;
   HGIN_ARG_CHECK(w && bias && y, "hgin_linear_fwd_f32: NULL operand");
   if (int rc = check_a("hgin_linear_fwd_f32", a1, lda1, k1, a2, lda2, K)) return rc;
+  if (nt2_eligible<float>(a1, lda1, k1, a2, lda2, w_planes, N, K, gemm_split_enabled()))
+    return launch_nt2<float, 2, float>(a1, lda1, k1, a2, lda2, nullptr, w_planes, M, N, K, bias, nullptr, nullptr,
+                                       nullptr, y, N, as_stream(stream), "hgin_linear_fwd_f32");
   return launch_nt<2>(Src2{a1, lda1, a2, lda2, k1}, Src2{w, K, nullptr, 0, K}, M, N, K, bias, nullptr, nullptr,
                       nullptr, y, N, as_stream(stream), "hgin_linear_fwd_f32");
 }
 
 extern "C" int hgin_gemm_nt_f32(const float* a, int64_t lda, const float* b, int64_t ldb, float* c, int64_t ldc,
-                                int64_t M, int64_t N, int64_t K, void* stream) {
+                                int64_t M, int64_t N, int64_t K, const void* b_planes, void* stream) {
   HGIN_ARG_CHECK(M >= 0 && N >= 0 && K >= 0, "hgin_gemm_nt_f32: negative size");
   HGIN_ARG_CHECK(N <= 65535 * 128, "hgin_gemm_nt_f32: N too large");
   if (M == 0 || N == 0) return HGIN_OK;
   HGIN_ARG_CHECK(a && b && c, "hgin_gemm_nt_f32: NULL operand");
   HGIN_ARG_CHECK(lda >= K && ldb >= K && ldc >= N, "hgin_gemm_nt_f32: leading dimension too small");
+  if (nt2_eligible<float>(a, lda, K, nullptr, 0, b_planes, N, K, gemm_split_enabled()))
+    return launch_nt2<float, 0, float>(a, lda, K, nullptr, 0, nullptr, b_planes, M, N, K, nullptr, nullptr, nullptr,
+                                       nullptr, c, ldc, as_stream(stream), "hgin_gemm_nt_f32");
   return launch_nt<0>(Src2{a, lda, nullptr, 0, K}, Src2{b, ldb, nullptr, 0, K}, M, N, K, nullptr, nullptr, nullptr,
                       nullptr, c, ldc, as_stream(stream), "hgin_gemm_nt_f32");
+}
+
+extern "C" int hgin_nt_planes_size(int64_t N, int64_t K, int elem_bytes, size_t* bytes) {
+  HGIN_ARG_CHECK(bytes && N >= 0 && K >= 0 && (elem_bytes == 4 || elem_bytes == 2), "hgin_nt_planes_size: bad args");
+  *bytes = elem_bytes == 4 ? nt_planes_bytes<float>(N, K) : nt_planes_bytes<uint16_t>(N, K);
+  return HGIN_OK;
+}
+
+extern "C" int hgin_nt_planes_f32(const float* b, int64_t ldb, int64_t N, int64_t K, void* out, void* stream) {
+  return nt_planes<float>(b, ldb, N, K, out, as_stream(stream), "hgin_nt_planes_f32");
+}
+
+extern "C" int hgin_nt_planes_bf16(const uint16_t* b, int64_t ldb, int64_t N, int64_t K, void* out, void* stream) {
+  return nt_planes<uint16_t>(b, ldb, N, K, out, as_stream(stream), "hgin_nt_planes_bf16");
 }

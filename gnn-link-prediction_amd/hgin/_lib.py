@@ -128,22 +128,22 @@ _SIGS = {
     "hgin_aggregate_f32": ([_P, _P, _I64, _P, _I64, _I64, _P, _I64, _I64, _P, _I32, _P, _I64, _P], _I32),
     "hgin_combine_bwd_workspace_size": ([_I64, ctypes.POINTER(_SZ)], _I32),
     "hgin_combine_bwd_f32": ([_P, _I64, _P, _I64, _I64, _I64, _P, _P, _I64, _P, _P, _SZ, _P], _I32),
-    "hgin_gin_mlp_fwd_f32": ([_P, _I64, _I64, _P, _I64, _P, _P, _P, _P, _P, _P, _P, _I64, _I64, _I64, _P], _I32),
-    "hgin_linear_fwd_f32": ([_P, _I64, _I64, _P, _I64, _P, _P, _P, _I64, _I64, _I64, _P], _I32),
+    "hgin_gin_mlp_fwd_f32": ([_P, _I64, _I64, _P, _I64, _P, _P, _P, _P, _P, _P, _P, _I64, _I64, _I64, _P, _P], _I32),
+    "hgin_linear_fwd_f32": ([_P, _I64, _I64, _P, _I64, _P, _P, _P, _I64, _I64, _I64, _P, _P], _I32),
     "hgin_prelu_bwd_workspace_size": ([_I64, _I64, ctypes.POINTER(_SZ)], _I32),
     "hgin_prelu_bwd_f32": ([_P, _I64, _P, _I64, _I64, _P, _P, _P, _P, _P, _SZ, _P], _I32),
-    "hgin_gemm_nt_f32": ([_P, _I64, _P, _I64, _P, _I64, _I64, _I64, _I64, _P], _I32),
+    "hgin_gemm_nt_f32": ([_P, _I64, _P, _I64, _P, _I64, _I64, _I64, _I64, _P, _P], _I32),
     "hgin_gemm_nt_combine_workspace_size": ([_I64, _I64, ctypes.POINTER(_SZ)], _I32),
     "hgin_gemm_nt_combine_f32": ([_P, _I64, _P, _I64, _P, _I64, _I64, _I64, _I64, _P, _I64, _P, _I64, _I64, _P, _P,
-                                  _P, _SZ, _P], _I32),
+                                  _P, _SZ, _P, _P], _I32),
     "hgin_gemm_nt_combine_bf16": ([_P, _I64, _P, _I64, _P, _I64, _I64, _I64, _I64, _P, _I64, _P, _I64, _I64, _P, _P,
-                                   _P, _SZ, _P], _I32),
+                                   _P, _SZ, _P, _P], _I32),
     "hgin_gemm_tn_workspace_size": ([_I64, _I64, _I64, ctypes.POINTER(_SZ)], _I32),
     "hgin_gemm_tn_f32": ([_P, _I64, _P, _I64, _I64, _P, _I64, _I64, _I64, _I64, _P, _I64, _P, _SZ, _P], _I32),
     "hgin_aggregate_bf16": ([_P, _P, _I64, _P, _I64, _I64, _P, _I64, _I64, _P, _I32, _P, _I64, _P], _I32),
-    "hgin_gin_mlp_fwd_bf16": ([_P, _I64, _I64, _P, _I64, _P, _P, _P, _P, _P, _P, _P, _I64, _I64, _I64, _P], _I32),
-    "hgin_linear_fwd_bf16": ([_P, _I64, _I64, _P, _I64, _P, _P, _P, _I64, _I64, _I64, _P], _I32),
-    "hgin_gemm_nt_bf16": ([_P, _I64, _P, _I64, _P, _I64, _I64, _I64, _I64, _P], _I32),
+    "hgin_gin_mlp_fwd_bf16": ([_P, _I64, _I64, _P, _I64, _P, _P, _P, _P, _P, _P, _P, _I64, _I64, _I64, _P, _P], _I32),
+    "hgin_linear_fwd_bf16": ([_P, _I64, _I64, _P, _I64, _P, _P, _P, _I64, _I64, _I64, _P, _P], _I32),
+    "hgin_gemm_nt_bf16": ([_P, _I64, _P, _I64, _P, _I64, _I64, _I64, _I64, _P, _P], _I32),
     "hgin_gemm_tn_bf16": ([_P, _I64, _P, _I64, _I64, _P, _I64, _I64, _I64, _I64, _P, _I64, _P, _SZ, _P], _I32),
     "hgin_prelu_bwd_bf16": ([_P, _I64, _P, _I64, _I64, _P, _P, _P, _P, _P, _SZ, _P], _I32),
     "hgin_gin_mlp_bwd_w_workspace_size": ([_I64, _I64, _I64, _I32, _I32, ctypes.POINTER(_SZ)], _I32),
@@ -167,8 +167,15 @@ _SIGS = {
     "hgin_neg_sample": ([_U64, _U64, _I64, _I64, _P, _P], _I32),
     "hgin_dot_decode_fwd_f32": ([_P, _P, _I64, _P, _I64, _P, _I64, _I64, _P, _P], _I32),
     "hgin_dot_decode_bwd_f32": ([_P, _P, _P, _I64, _P, _P, _I64, _I64, _P, _I64, _P], _I32),
+    "hgin_aggregate_long_f32": ([_P, _P, _I64, _P, _P, _I64, _P, _I64, _I64, _P, _I64, _I64, _P, _I32, _P, _I64, _P,
+                                 _SZ, _P], _I32),
+    "hgin_aggregate_long_bf16": ([_P, _P, _I64, _P, _P, _I64, _P, _I64, _I64, _P, _I64, _I64, _P, _I32, _P, _I64, _P,
+                                  _SZ, _P], _I32),
+    "hgin_nt_planes_size": ([_I64, _I64, _I32, ctypes.POINTER(_SZ)], _I32),
+    "hgin_nt_planes_f32": ([_P, _I64, _I64, _I64, _P, _P], _I32),
+    "hgin_nt_planes_bf16": ([_P, _I64, _I64, _I64, _P, _P], _I32),
 }
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 
 def lib() -> ctypes.CDLL:

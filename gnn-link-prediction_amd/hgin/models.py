@@ -61,30 +61,35 @@ def _host_call_device(model: torch.nn.Module, x_dict, edge_index_dict, path_batc
     return torch.device("cuda", torch.cuda.current_device())
 
 
-class _DeviceCall(torch.nn.Module):
-    def __init__(self, model):
-        super().__init__()
-        self.m = model
-
-    def forward(self, x_dict, edge_index_dict, path_batch):
-        return self.m._run(x_dict, edge_index_dict, path_batch, None, None)
-
-
 def _host_call(model: torch.nn.Module, dev, x_dict, edge_index_dict, path_batch):
-    """Run ``model`` on ``dev`` with device copies of its (host) parameters and inputs, through
-    ``torch.func.functional_call``: gradients flow back to the host parameters, the output returns to the
-    host.  The host copies of the inputs are not modified (PyG's ``x_dict`` is a fresh dict per access)."""
-    if model.training and any(isinstance(m, torch.nn.modules.batchnorm._BatchNorm) for m in model.modules()):
-        raise RuntimeError("HetroGIN: a training-mode host-resident call would lose BatchNorm running-stat "
-                           "updates; move the model to the device (model.cuda(), train.py:177)")
+    """Run ``model`` on ``dev`` for a host-resident inference call (``evaluate``, train.py:331-335 runs it under
+    ``torch.set_grad_enabled(False)``): parameters and buffers are lent to the device for the call and restored
+    afterwards (same Parameter objects), inputs are copied over, the output returns to the host.  The host
+    copies of the inputs are not modified (PyG's ``x_dict`` is a fresh dict per access).  A gradient-recording
+    host call raises: training moves the model to the device first (``model.cuda()``, train.py:177)."""
+    if torch.is_grad_enabled() and any(p.requires_grad for p in model.parameters()):
+        raise RuntimeError("HetroGIN: a host-resident call with gradients enabled; move the model to the HIP "
+                           "device for training (model.cuda(), train.py:177) or call it under torch.no_grad() / "
+                           "torch.set_grad_enabled(False) as train.py's evaluate() does")
     host = next(iter(x_dict.values())).device
-    state = {"m." + n: t.to(dev) for n, t in model.named_parameters()}
-    state.update({"m." + n: t.to(dev) for n, t in model.named_buffers()})
-    xd = {k: v.to(dev) for k, v in x_dict.items()}
-    ed = {k: v.to(dev) for k, v in edge_index_dict.items()}
-    pb = path_batch.to(dev) if path_batch is not None else None
-    out = torch.func.functional_call(_DeviceCall(model), state, (xd, ed, pb))
-    return out.to(host)
+    lent = []
+    seen = set()
+    for t in list(model.parameters()) + list(model.buffers()):
+        if id(t) not in seen:
+            seen.add(id(t))
+            lent.append((t, t.data))
+    try:
+        for t, d in lent:
+            t.data = d.to(dev)
+        xd = {k: v.to(dev) for k, v in x_dict.items()}
+        ed = {k: v.to(dev) for k, v in edge_index_dict.items()}
+        pb = path_batch.to(dev) if path_batch is not None else None
+        out = model._run(xd, ed, pb, None, None)
+        res = out.to(host)
+    finally:
+        for t, d in lent:
+            t.data = d
+    return res
 
 
 class HetroGIN(torch.nn.Module):

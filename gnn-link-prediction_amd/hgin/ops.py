@@ -17,6 +17,7 @@ Ops:
 from __future__ import annotations
 
 import ctypes
+import os
 from dataclasses import dataclass
 from typing import Optional
 
@@ -74,6 +75,27 @@ def _workspace(nbytes: int, device) -> Tensor:
 # ---------------------------------------------------------------------------------------------------
 # A12: CSR / CSC
 # ---------------------------------------------------------------------------------------------------
+# Degree skew (SURVEY.md §8.D Zipf variant): rows with more than LONG_ROW_MIN edges leave the row-per-lane-group
+# walk (serial in a row's edges) for the chunked long-row kernels (hgin_aggregate_long_*, LONG_CHUNK edges per
+# wave, chunk sums added in a fixed order: deterministic, re-associated).  Uniform GIN graphs (max in-degree
+# ~40 at cfg3) never reach it, so their aggregates stay bit-exact.  HGIN_LONG_ROW=0 keeps every row sequential.
+LONG_ROW_MIN = int(os.environ.get("HGIN_LONG_ROW", "2048"))
+# The LDS-DMA NT GEMM (hgin_gemm_nt.hip k_nt2) is measured slower than the register-staged one and off by
+# default; HGIN_NT2=1 selects it (the C side reads the same switch).
+NT2 = os.environ.get("HGIN_NT2", "0") == "1"
+LONG_CHUNK = 1024
+
+
+@dataclass
+class LongRows:
+    rowptr_short: Tensor   # int32 [n_rows + 1]: the CSR with the long rows emptied
+    col_short: Tensor      # int32 [E - long edges]
+    long_rows: Tensor      # int32 [n_long]
+    item_ptr: Tensor       # int32 [n_long + 1]
+    items: Tensor          # int32 [2 * n_items]: (begin, end) edge ranges into the full col, per row in edge order
+    n_items: int
+
+
 @dataclass
 class Csr:
     rowptr: Tensor   # int32 [n_rows + 1]
@@ -81,10 +103,41 @@ class Csr:
     perm: Tensor     # int32 [E]   original edge id of each sorted position
     n_rows: int
     n_cols: int
+    long: Optional[LongRows] = None
 
     @property
     def n_edges(self) -> int:
         return int(self.col.numel())
+
+
+def split_long_rows(csr: Csr, min_deg: int = None, chunk: int = None) -> Csr:
+    """Attach the long-row split of ``csr`` (rows with more than ``min_deg`` edges), if it has any."""
+    min_deg = LONG_ROW_MIN if min_deg is None else int(min_deg)
+    chunk = LONG_CHUNK if chunk is None else int(chunk)
+    csr.long = None
+    if min_deg <= 0 or csr.n_edges == 0 or csr.n_rows == 0:
+        return csr
+    rp = csr.rowptr.long()
+    deg = rp[1:] - rp[:-1]
+    if int(deg.max()) <= min_deg:          # one host sync per CSR build (cached with the graph)
+        return csr
+    is_long = deg > min_deg
+    long_rows = torch.nonzero(is_long).flatten()
+    d = deg[long_rows]
+    nch = (d + chunk - 1) // chunk
+    item_ptr = torch.cat([torch.zeros(1, dtype=torch.long, device=d.device), torch.cumsum(nch, 0)])
+    n_items = int(item_ptr[-1])
+    row_of_item = torch.repeat_interleave(torch.arange(long_rows.numel(), device=d.device), nch)
+    local = torch.arange(n_items, device=d.device) - item_ptr[row_of_item]
+    beg = rp[long_rows][row_of_item] + local * chunk
+    end = torch.minimum(beg + chunk, rp[long_rows + 1][row_of_item])
+    deg_short = torch.where(is_long, torch.zeros_like(deg), deg)
+    rowptr_short = torch.cat([torch.zeros(1, dtype=torch.long, device=d.device), torch.cumsum(deg_short, 0)])
+    keep = torch.repeat_interleave(~is_long, deg)
+    csr.long = LongRows(rowptr_short.to(torch.int32), csr.col[keep].contiguous(), long_rows.to(torch.int32),
+                        item_ptr.to(torch.int32), torch.stack([beg, end], 1).to(torch.int32).reshape(-1).contiguous(),
+                        n_items)
+    return csr
 
 
 def build_csr(edge_index: Tensor, key_row: int, n_rows: int, n_cols: int, validate: bool = True) -> Csr:
@@ -112,7 +165,7 @@ def build_csr(edge_index: Tensor, key_row: int, n_rows: int, n_cols: int, valida
             if st & STATUS_COL_OOR:
                 which.append(f"{'src' if key_row == 1 else 'dst'} index out of range [0, {n_cols})")
             raise IndexError("edge_index: " + "; ".join(which))
-    return Csr(rowptr, col, perm, n_rows, n_cols)
+    return split_long_rows(Csr(rowptr, col, perm, n_rows, n_cols))
 
 
 def check_edge_index(edge_index: Tensor) -> None:
@@ -180,15 +233,35 @@ def relation_graph(edge_index: Tensor, n_src: int, n_dst: int) -> RelationGraph:
 # ---------------------------------------------------------------------------------------------------
 # raw launches
 # ---------------------------------------------------------------------------------------------------
+def _long_ok(lr: Optional[LongRows], x_src: Tensor, x_dst: Optional[Tensor], out: Tensor, mode: int) -> bool:
+    """Whether the long-row kernels take these operands (4-wide rows; otherwise every row walks serially)."""
+    if lr is None:
+        return False
+    f = int(x_src.size(1))
+    ok = f % 4 == 0 and x_src.stride(0) % 4 == 0 and out.stride(0) % 4 == 0
+    ok = ok and x_src.data_ptr() % (4 * x_src.element_size()) == 0 and out.data_ptr() % (4 * out.element_size()) == 0
+    if mode == COMBINE_ADD:
+        ok = ok and x_dst.stride(0) % 4 == 0 and x_dst.data_ptr() % (4 * x_dst.element_size()) == 0
+    return ok
+
+
 def aggregate_into(csr: Csr, x_src: Tensor, x_dst: Optional[Tensor], eps: Optional[Tensor], mode: int,
                    out: Tensor) -> Tensor:
     f_src = int(x_src.size(1))
     f_dst = int(x_dst.size(1)) if x_dst is not None else 0
+    lr = csr.long if _long_ok(csr.long, x_src, x_dst, out, mode) else None
 
     def launch():
-        _lib.call(f"hgin_aggregate_{_sfx(x_src)}", _p(csr.rowptr), _p(csr.col), csr.n_rows, _p(x_src),
+        rowptr, col = (lr.rowptr_short, lr.col_short) if lr is not None else (csr.rowptr, csr.col)
+        _lib.call(f"hgin_aggregate_{_sfx(x_src)}", _p(rowptr), _p(col), csr.n_rows, _p(x_src),
                   x_src.stride(0), f_src, _p(x_dst), x_dst.stride(0) if x_dst is not None else 0, f_dst, _p(eps),
                   mode, _p(out), out.stride(0), _stream(out))
+        if lr is not None:
+            part = torch.empty(lr.n_items * f_src, dtype=torch.float32, device=out.device)
+            _lib.call(f"hgin_aggregate_long_{_sfx(x_src)}", _p(csr.col), _p(lr.items), lr.n_items, _p(lr.long_rows),
+                      _p(lr.item_ptr), lr.long_rows.numel(), _p(x_src), x_src.stride(0), f_src, _p(x_dst),
+                      x_dst.stride(0) if x_dst is not None else 0, f_dst, _p(eps), mode, _p(out), out.stride(0),
+                      _p(part), part.numel() * 4, _stream(out))
 
     probe = profiling.active()
     if probe is None:
@@ -230,6 +303,23 @@ def combine_bwd(g: Tensor, x_dst: Tensor, eps: Tensor, want_gx: bool):
     return gx, g_eps
 
 
+def nt_planes(b: Tensor) -> Optional[Tensor]:
+    """The B operand [N, K] of an NT GEMM pre-converted for the LDS-DMA kernel (hgin_nt_planes_*: fp32 -> its
+    three bf16 split planes, bf16 -> a swizzled copy; N * K * 6 or N * K * 2 bytes), or None where that kernel
+    does not take the shape (the register-staged kernel runs; the result is bit-identical either way)."""
+    if not NT2:
+        return None
+    N, K = b.shape
+    ks = 32 if b.dtype == torch.float32 else 64
+    if N == 0 or K == 0 or K % ks or N % 128 or b.stride(1) != 1 or b.data_ptr() % 16 or b.stride(0) % (16 // b.element_size()):
+        return None
+    nbytes = ctypes.c_size_t(0)
+    _lib.check(_lib.lib().hgin_nt_planes_size(N, K, b.element_size(), ctypes.byref(nbytes)), "hgin_nt_planes_size")
+    out = torch.empty(nbytes.value, dtype=torch.uint8, device=b.device)
+    _lib.call(f"hgin_nt_planes_{_sfx(b)}", _p(b), b.stride(0), N, K, _p(out), _stream(b))
+    return out
+
+
 def gemm_nt(a: Tensor, b: Tensor) -> Tensor:
     """c = a @ b^T on the matrix cores (a [M,K], b [N,K], both K-contiguous; c in the operands' dtype)."""
     a, b = _rowmajor(a), _rowmajor(b)
@@ -238,7 +328,7 @@ def gemm_nt(a: Tensor, b: Tensor) -> Tensor:
     N = b.shape[0]
     c = torch.empty(M, N, dtype=a.dtype, device=a.device)
     _lib.call(f"hgin_gemm_nt_{_sfx(a)}", _p(a), a.stride(0), _p(b), b.stride(0), _p(c), c.stride(0), M, N, K,
-              _stream(a))
+              _p(nt_planes(b)), _stream(a))
     return c
 
 
@@ -258,7 +348,7 @@ def gemm_nt_combine(a: Tensor, b: Tensor, x_dst: Tensor, eps: Tensor, cs: int, w
     ws = _workspace(nbytes.value, a.device)
     _lib.call(f"hgin_gemm_nt_combine_{_sfx(a)}", _p(a), a.stride(0), _p(b), b.stride(0), _p(c), c.stride(0), M, N, K,
               _p(x_dst), x_dst.stride(0), _p(gx), gx.stride(0) if gx is not None else 0, cs, _p(eps), _p(g_eps),
-              _p(ws), nbytes.value, _stream(a))
+              _p(ws), nbytes.value, _p(nt_planes(b)), _stream(a))
     return c, gx, g_eps
 
 
@@ -346,14 +436,15 @@ def gin_mlp_fwd(comb: Tensor, weight: Tensor, bias: Tensor, prelu: Optional[Tens
     z = torch.empty(M, N, dtype=dt, device=comb.device) if (save_z and prelu is not None) else None
     y = torch.empty(M, N, dtype=dt if prelu is not None else torch.float32, device=comb.device)
     ld2 = comb2.stride(0) if comb2 is not None else 0
+    planes = nt_planes(weight) if weight.stride(1) == 1 else None
 
     def launch():
         if prelu is None:
             _lib.call(f"hgin_linear_fwd_{sfx}", _p(comb), comb.stride(0), k1, _p(comb2), ld2, _p(weight), _p(bias),
-                      _p(y), M, N, K, _stream(comb))
+                      _p(y), M, N, K, _p(planes), _stream(comb))
         else:
             _lib.call(f"hgin_gin_mlp_fwd_{sfx}", _p(comb), comb.stride(0), k1, _p(comb2), ld2, _p(eps2), _p(weight),
-                      _p(bias), _p(prelu), _p(accum), _p(z), _p(y), M, N, K, _stream(comb))
+                      _p(bias), _p(prelu), _p(accum), _p(z), _p(y), M, N, K, _p(planes), _stream(comb))
 
     probe = profiling.active()
     if probe is None:

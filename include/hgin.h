@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define HGIN_ABI_VERSION 1
+#define HGIN_ABI_VERSION 2
 
 #define HGIN_OK 0
 #define HGIN_E_ARG (-1)        /* bad size / null pointer / unsupported combination */
@@ -108,13 +108,34 @@ int hgin_combine_bwd_f32(const float* g, int64_t ld_g, const float* x_dst, int64
  * or the exact bf16 3-way operand split). */
 int hgin_gin_mlp_fwd_f32(const float* a1, int64_t lda1, int64_t k1, const float* a2, int64_t lda2,
                          const float* a2_eps, const float* w, const float* bias, const float* prelu,
-                         const float* accum, float* z, float* y, int64_t M, int64_t N, int64_t K, void* stream);
+                         const float* accum, float* z, float* y, int64_t M, int64_t N, int64_t K,
+                         const void* w_planes, void* stream);
 
 /* ---- readout Linear without activation (models.py:326-330, the head Linear(mlp_layers[-1], 1)) ------
  *   y = [a1 | a2] @ w^T + bias     (same operand conventions as hgin_gin_mlp_fwd_f32) */
 int hgin_linear_fwd_f32(const float* a1, int64_t lda1, int64_t k1, const float* a2, int64_t lda2,
                         const float* w, const float* bias, float* y, int64_t M, int64_t N, int64_t K,
-                        void* stream);
+                        const void* w_planes, void* stream);
+
+/* ---- A3 / A9: long rows (degree skew) ------------------------------------------------------------------
+ * The neighbour sums of rows too long for the row-per-lane-group walk of hgin_aggregate_* (whose CSR the
+ * caller passes with these rows emptied, so it writes their self term and zeros for the sum): items holds
+ * n_items chunks of consecutive edges as (begin, end) pairs into `col`, grouped by row in edge order; row j
+ * of `long_rows` owns items [item_ptr[j], item_ptr[j + 1]).  Each chunk is summed in edge order (fp32), the
+ * chunk sums of a row are added in chunk order, then (ADD) the self term (1 + eps[0]) * x_dst; the result
+ * overwrites out[row, 0:f_src] (CONCAT's self columns stay as hgin_aggregate_* wrote them).  Deterministic
+ * run to run; re-associated against the sequential sum (tolerance).  partial: n_items * f_src floats.
+ * f_src, ld_src, ld_out multiples of 4. */
+int hgin_aggregate_long_f32(const int32_t* col, const int32_t* items, int64_t n_items, const int32_t* long_rows,
+                            const int32_t* item_ptr, int64_t n_long, const float* x_src, int64_t ld_src,
+                            int64_t f_src, const float* x_dst, int64_t ld_dst, int64_t f_dst, const float* eps,
+                            int combine, float* out, int64_t ld_out, float* partial, size_t partial_bytes,
+                            void* stream);
+int hgin_aggregate_long_bf16(const int32_t* col, const int32_t* items, int64_t n_items, const int32_t* long_rows,
+                             const int32_t* item_ptr, int64_t n_long, const uint16_t* x_src, int64_t ld_src,
+                             int64_t f_src, const uint16_t* x_dst, int64_t ld_dst, int64_t f_dst, const float* eps,
+                             int combine, uint16_t* out, int64_t ld_out, float* partial, size_t partial_bytes,
+                             void* stream);
 
 /* ---- A9: PReLU + bias backward -------------------------------------------------------------------
  *   g_z = z > 0 ? g_y : prelu[0] * g_y;  g_prelu[0] = sum (z > 0 ? 0 : z * g_y);  g_bias[n] = sum_m g_z[m, n]
@@ -127,7 +148,19 @@ int hgin_prelu_bwd_f32(const float* g_y, int64_t ld_gy, const float* z, int64_t 
 /* ---- plain GEMM on MFMA (backward of Linear) --------------------------------------------------------
  * c[M, N] = a[M, K] @ b[N, K]^T   ("NT", both operands K-contiguous), fp32 MFMA. */
 int hgin_gemm_nt_f32(const float* a, int64_t lda, const float* b, int64_t ldb, float* c, int64_t ldc,
-                     int64_t M, int64_t N, int64_t K, void* stream);
+                     int64_t M, int64_t N, int64_t K, const void* b_planes, void* stream);
+
+/* ---- NT GEMM operand planes (ABI 2) --------------------------------------------------------------------
+ * Every NT GEMM entry point (hgin_gin_mlp_fwd_*, hgin_linear_fwd_*, hgin_gemm_nt_*, hgin_gemm_nt_combine_*)
+ * takes `w_planes` / `b_planes`: NULL, or the B operand ([N, K], the weight) pre-converted by
+ * hgin_nt_planes_* — fp32: its three bf16 split planes, bf16: a copy — in the per-K-stage, XOR-swizzled
+ * layout of the LDS-DMA GEMM kernel (k_nt2 in hgin_gemm_nt.hip).  With planes, shapes the kernel takes
+ * (K and the A split column multiples of 32 (fp32) / 64 (bf16), 16-B aligned A rows, N a multiple of 128) run
+ * on it; everything else runs on the register-staged kernel.  Results are bit-identical either way.
+ * Size: hgin_nt_planes_size (elem_bytes 4 or 2) = N * K * 6 (fp32) or N * K * 2 (bf16) bytes. */
+int hgin_nt_planes_size(int64_t N, int64_t K, int elem_bytes, size_t* bytes);
+int hgin_nt_planes_f32(const float* b, int64_t ldb, int64_t N, int64_t K, void* out, void* stream);
+int hgin_nt_planes_bf16(const uint16_t* b, int64_t ldb, int64_t N, int64_t K, void* out, void* stream);
 
 /* ---- A9: dX GEMM with the self term's backward fused --------------------------------------------------
  * Replaces hgin_gemm_nt_* followed by hgin_combine_bwd_* in a GINConv backward (models.py:210-217 reached
@@ -140,11 +173,11 @@ int hgin_gemm_nt_combine_workspace_size(int64_t M, int64_t N, size_t* bytes);
 int hgin_gemm_nt_combine_f32(const float* a, int64_t lda, const float* b, int64_t ldb, float* c, int64_t ldc,
                              int64_t M, int64_t N, int64_t K, const float* x_dst, int64_t ld_xd, float* g_dst,
                              int64_t ld_gd, int64_t cs, const float* eps, float* g_eps, void* workspace,
-                             size_t workspace_bytes, void* stream);
+                             size_t workspace_bytes, const void* b_planes, void* stream);
 int hgin_gemm_nt_combine_bf16(const uint16_t* a, int64_t lda, const uint16_t* b, int64_t ldb, uint16_t* c,
                               int64_t ldc, int64_t M, int64_t N, int64_t K, const uint16_t* x_dst, int64_t ld_xd,
                               uint16_t* g_dst, int64_t ld_gd, int64_t cs, const float* eps, float* g_eps,
-                              void* workspace, size_t workspace_bytes, void* stream);
+                              void* workspace, size_t workspace_bytes, const void* b_planes, void* stream);
 
 /* ---- weight-gradient GEMM (backward of Linear: dW = g_z^T X) ----------------------------------------
  * out[N, K] = a[M, N]^T @ [b1 | b2],  b1 = columns [0, k1) ([M, k1], ldb1), b2 = columns [k1, K) ([M, K-k1],
@@ -206,12 +239,12 @@ int hgin_aggregate_bf16(const int32_t* rowptr, const int32_t* col, int64_t n_row
 int hgin_gin_mlp_fwd_bf16(const uint16_t* a1, int64_t lda1, int64_t k1, const uint16_t* a2, int64_t lda2,
                           const float* a2_eps, const uint16_t* w, const float* bias, const float* prelu,
                           const uint16_t* accum, uint16_t* z, uint16_t* y, int64_t M, int64_t N, int64_t K,
-                          void* stream);
+                          const void* w_planes, void* stream);
 int hgin_linear_fwd_bf16(const uint16_t* a1, int64_t lda1, int64_t k1, const uint16_t* a2, int64_t lda2,
                          const uint16_t* w, const float* bias, float* y, int64_t M, int64_t N, int64_t K,
-                         void* stream);
+                         const void* w_planes, void* stream);
 int hgin_gemm_nt_bf16(const uint16_t* a, int64_t lda, const uint16_t* b, int64_t ldb, uint16_t* c, int64_t ldc,
-                      int64_t M, int64_t N, int64_t K, void* stream);
+                      int64_t M, int64_t N, int64_t K, const void* b_planes, void* stream);
 int hgin_gemm_tn_bf16(const uint16_t* a, int64_t lda, const uint16_t* b1, int64_t ldb1, int64_t k1,
                       const uint16_t* b2, int64_t ldb2, int64_t M, int64_t N, int64_t K, float* out, int64_t ldo,
                       void* workspace, size_t workspace_bytes, void* stream);

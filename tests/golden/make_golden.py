@@ -35,10 +35,20 @@ REFERENCE_MODELS = "/root/reference/models.py"
 
 sys.path.insert(0, os.path.join(HERE, "pyg_shim"))
 sys.path.insert(0, os.path.join(REPO, "gnn-link-prediction_amd"))
+sys.path.insert(0, REPO)
 
 import torch  # noqa: E402
 
-from hgin.data import CONFIGS, GraphConfig, collate, scaled_config, synthetic_graph  # noqa: E402
+from hgin.data import CONFIGS, GraphConfig, HeteroGraph, scaled_config, synthetic_graph  # noqa: E402
+from oracle import collate_np  # noqa: E402
+
+
+def collate(graphs):
+    """PyG Batch.from_data_list, as restated independently in oracle/collate_np.py."""
+    c = collate_np.collate([collate_np.from_graph(g) for g in graphs])
+    return HeteroGraph({t: torch.from_numpy(v) for t, v in c["x"].items()},
+                       {r: torch.from_numpy(e) for r, e in c["edge_index"].items()}, torch.from_numpy(c["y"]),
+                       {t: torch.from_numpy(b) for t, b in c["batch"].items()})
 
 
 def load_reference_models():

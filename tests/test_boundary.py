@@ -45,7 +45,7 @@ def test_argument_errors_do_not_touch_the_device():
     assert rc == -1
     rc = lib.hgin_neg_sample(0, 0, 10, 0, None, None)
     assert rc == -1 and b"n_dst" in lib.hgin_last_error()
-    rc = lib.hgin_gemm_nt_f32(None, 2, None, 2, None, 2, 4, 4, 4, None)
+    rc = lib.hgin_gemm_nt_f32(None, 2, None, 2, None, 2, 4, 4, 4, None, None)
     assert rc == -1
     sz = ctypes.c_size_t(0)
     assert lib.hgin_csr_workspace_size(1000, 10, ctypes.byref(sz)) == 0 and sz.value >= 16000

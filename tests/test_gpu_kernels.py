@@ -114,7 +114,9 @@ def test_aggregate_bit_exact_skewed_rows(F, dtype, mode):
     assert int(np.diff(rowptr).max()) > 1000
     ref = torch.from_numpy(co.aggregate(rowptr, col, x.float().numpy(), xd.float().numpy() if mode else None,
                                         float(eps), mode)).to(dtype)
-    csr = ops.build_csr(torch.from_numpy(ei).to(DEV), 1, n_dst, n_src)
+    # the sequential walk for every row (the long-row split off): bit-exact
+    csr = ops.split_long_rows(ops.build_csr(torch.from_numpy(ei).to(DEV), 1, n_dst, n_src), 0)
+    assert csr.long is None
     out = torch.full((n_dst, F * (2 if mode == 2 else 1)), float("nan"), device=DEV).to(dtype)
     ops.aggregate_into(csr, x.to(DEV), xd.to(DEV) if mode else None,
                        torch.tensor([eps], device=DEV) if mode else None, mode, out)
@@ -123,6 +125,56 @@ def test_aggregate_bit_exact_skewed_rows(F, dtype, mode):
         assert torch.equal(got.view(torch.int16), ref.view(torch.int16))
     else:
         assert torch.equal(got, ref)
+
+
+@pytest.mark.parametrize("F,dtype", [(256, torch.float32), (128, torch.float32), (256, torch.bfloat16)])
+@pytest.mark.parametrize("mode", [0, 1, 2])
+def test_aggregate_long_row_split(F, dtype, mode):
+    """Zipf(1.1) destinations with the long-row split on (rows above 256 edges, 128-edge chunks): rows at or
+    below the threshold stay bit-exact against the C oracle; split rows are the chunked, re-associated sum —
+    within 1e-6 of sum |x| of a float64 evaluation (fp32: chunk and combine adds, ~40 per output) and
+    bitwise reproducible; CONCAT's self columns are exact everywhere."""
+    n_src, n_dst = 3000, 40000
+    ei = np.concatenate([_rand_graph(60000, n_src, n_dst, seed=F + mode, zipf=True),
+                         _rand_graph(60000, n_src, n_dst, seed=F * 3 + mode)], 1)
+    g = torch.Generator().manual_seed(F + 7 * mode)
+    x = torch.randn(n_src, F, generator=g).to(dtype)
+    xd = torch.randn(n_dst, F, generator=g).to(dtype)
+    eps = np.float32(0.3125)
+    rowptr, col, _, _ = co.csr_build(ei, 1, n_dst, n_src)
+    deg = np.diff(rowptr)
+    ref = torch.from_numpy(co.aggregate(rowptr, col, x.float().numpy(), xd.float().numpy() if mode else None,
+                                        float(eps), mode)).to(dtype)
+    csr = ops.split_long_rows(ops.build_csr(torch.from_numpy(ei).to(DEV), 1, n_dst, n_src), 256, 128)
+    assert csr.long is not None and csr.long.long_rows.numel() == int((deg > 256).sum()) > 3
+    outs = []
+    for _ in range(2):
+        out = torch.full((n_dst, F * (2 if mode == 2 else 1)), float("nan"), device=DEV).to(dtype)
+        ops.aggregate_into(csr, x.to(DEV), xd.to(DEV) if mode else None,
+                           torch.tensor([eps], device=DEV) if mode else None, mode, out)
+        outs.append(out.cpu())
+    assert torch.equal(outs[0].view(torch.int16) if dtype == torch.bfloat16 else outs[0],
+                       outs[1].view(torch.int16) if dtype == torch.bfloat16 else outs[1])
+    got = outs[0]
+    short = torch.from_numpy(deg <= 256)
+    if dtype == torch.bfloat16:
+        assert torch.equal(got[short].view(torch.int16), ref[short].view(torch.int16))
+    else:
+        assert torch.equal(got[short], ref[short])
+    if mode == 2:
+        assert torch.equal(got[:, F:].float(), ref[:, F:].float())
+    # split rows against float64
+    lrows = np.nonzero(deg > 256)[0]
+    x64 = x.double().numpy()
+    for r in lrows:
+        nb = col[rowptr[r]:rowptr[r + 1]]
+        want = x64[nb].sum(0)
+        if mode == 1:
+            want = want + (1.0 + float(eps)) * xd[r].double().numpy()
+        scale = np.abs(x64[nb]).sum(0) + (np.abs(xd[r].double().numpy()) * 2 if mode == 1 else 0)
+        err = np.abs(got[r, :F].double().numpy() - want)
+        tol = (1e-6 * scale + 1e-6) if dtype == torch.float32 else (np.abs(want) * 2 ** -8 + 1e-6 * scale + 1e-6)
+        assert (err <= tol).all(), (r, float(err.max()))
 
 
 def test_aggregate_matches_reference_cpu_op():

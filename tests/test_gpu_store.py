@@ -1,8 +1,9 @@
 """§8 F1/F2 on the GPU: device batch collation out of an HBM-resident GraphStore.
 
-The checker is hgin.data.collate (the PyG Batch.from_data_list restatement, dataset.py:239-244) on the host
-plus the C oracle's stable CSR build (oracle/hgin_oracle.c) of the collated edge_index — every collated array
-must be bit-identical, including the CSR / CSC the store assembles without sorting.
+The checker is oracle/collate_np.py (an independent numpy restatement of PyG's Batch.from_data_list,
+dataset.py:239-244) on the host plus the C oracle's stable CSR build (oracle/hgin_oracle.c) of the collated
+edge_index — every collated array must be bit-identical, including the CSR / CSC the store assembles without
+sorting.
 """
 import dataclasses
 
@@ -11,9 +12,17 @@ import pytest
 import torch
 
 from hgin import HetroGIN, ops
-from hgin.data import CONFIGS, REL_PN, HeteroGraph, collate, scaled_config, synthetic_graph
+from hgin.data import CONFIGS, REL_PN, HeteroGraph, scaled_config, synthetic_graph
 from hgin.store import GraphStore, normalize_reference
 from oracle import c_oracle as co
+from oracle import collate_np
+
+
+def oracle_collate(graphs) -> HeteroGraph:
+    c = collate_np.collate([collate_np.from_graph(g) for g in graphs])
+    return HeteroGraph({t: torch.from_numpy(v) for t, v in c["x"].items()},
+                       {r: torch.from_numpy(e) for r, e in c["edge_index"].items()}, torch.from_numpy(c["y"]),
+                       {t: torch.from_numpy(b) for t, b in c["batch"].items()})
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
@@ -57,13 +66,13 @@ def test_collate_bit_exact(ids):
     store = GraphStore.build(graphs, device=DEV)
     b = store.collate(ids)
     torch.cuda.synchronize()
-    _check_batch(b, collate([graphs[i] for i in ids]))
+    _check_batch(b, oracle_collate([graphs[i] for i in ids]))
 
 
 def test_collate_store_csr_matches_fresh_build():
     graphs = _graphs(6, seed=2)
     store = GraphStore.build(graphs, device=DEV)
-    big = collate(graphs)
+    big = oracle_collate(graphs)
     for r, e in big.edge_index.items():
         n_s, n_d = big.x[r[0]].shape[0], big.x[r[2]].shape[0]
         rp, col, perm, _ = co.csr_build(e.numpy(), 1, n_d, n_s)
@@ -79,7 +88,7 @@ def test_collate_model_output_identical():
     model = HetroGIN(**cfg.model_kwargs({"link": 7, "path": 7, "node": 3})).to(DEV)
     ids = [7, 2, 9, 0, 4, 4, 1, 8]
     b = store.collate(ids)
-    ref = collate([graphs[i] for i in ids]).to(DEV)     # fresh tensors -> CSR / CSC built by sorting
+    ref = oracle_collate([graphs[i] for i in ids]).to(DEV)     # fresh tensors -> CSR / CSC built by sorting
     out_b = model(b.x_dict(), b.edge_index_dict(), b.batch["path"])
     out_r = model(ref.x_dict(), ref.edge_index_dict(), ref.batch["path"])
     assert torch.equal(out_b, out_r)
@@ -105,7 +114,7 @@ def test_save_load_roundtrip(tmp_path):
     for r in a.edge_index:
         assert torch.equal(a.edge_index[r], b.edge_index[r])
     # normalisation applied once at build, exactly as dataset.py:33-58 does per sample
-    ref = collate([HeteroGraph(normalize_reference(g.x), g.edge_index, g.y, g.batch) for g in [graphs[i] for i in ids]])
+    ref = oracle_collate([HeteroGraph(normalize_reference(g.x), g.edge_index, g.y, g.batch) for g in [graphs[i] for i in ids]])
     _check_batch(b, ref)
 
 

@@ -6,7 +6,8 @@ fixtures (tests/variant_child.py), so the non-default paths pytest's own process
   * HGIN_SLAB_REDUCE=2pass  — the two-launch weight-gradient slab sum: bit-identical to the one-launch default;
   * HGIN_AGG_NQ=2 / HGIN_AGG_PIPE=1 / HGIN_AGG_TAIL=0 — aggregate lane-width / pipelined / tail variants:
                               bit-identical to the default (every variant sums each row in edge order);
-  * HGIN_XCD=0              — GEMM tiles in plain order instead of XCD-contiguous: bit-identical.
+  * HGIN_XCD=0              — GEMM tiles in plain order instead of XCD-contiguous: bit-identical;
+  * HGIN_NT2=1              — the LDS-DMA NT GEMM (k_nt2) instead of the register-staged one: bit-identical.
 
 Each child is a separate interpreter started with subprocess (never an exec of this process).
 """
@@ -29,8 +30,9 @@ VARIANTS = {
     "agg_pipe": {"HGIN_AGG_PIPE": "1"},
     "agg_notail": {"HGIN_AGG_TAIL": "0"},
     "xcd_off": {"HGIN_XCD": "0"},
+    "nt2_on": {"HGIN_NT2": "1"},
 }
-BITWISE_EQUAL_TO_DEFAULT = ("slab2pass", "agg_nq2", "agg_pipe", "agg_notail", "xcd_off")
+BITWISE_EQUAL_TO_DEFAULT = ("slab2pass", "agg_nq2", "agg_pipe", "agg_notail", "xcd_off", "nt2_on")
 
 _results = {}
 
