@@ -110,14 +110,25 @@ __device__ __forceinline__ void store_tile(float* __restrict__ dst, const float4
     *reinterpret_cast<float4*>(dst + ((tid >> 3) + 32 * i) * kLds + (tid & 7) * 4) = r[i];
 }
 
-// Split mode (hgin_common.h): the same tile written as three bf16 planes per row.
+// Split mode (hgin_common.h): the same tile written as three bf16 planes per row.  NT image: 48-word rows
+// (3 planes x 16 words, no pad) with the 4-word chunks of a plane XOR-swizzled by (row >> 2) & 3.  Row bases
+// 48 r mod 64 = 16 (3 r mod 4), so the split stores (8 lanes x 2 words per row, 4 rows per 32 lanes) cover
+// 4 disjoint 16-word bank blocks and a ds_read_b128 lane group (16 rows, one logical chunk) hits 4 bases x 4
+// swizzled chunks = 16 distinct slots: both conflict-free.  (The 52-word rows of hgin_common.h kept the reads
+// conflict-free but made the stores 2-way: SQ_LDS_BANK_CONFLICT ~0.9 of the LDS-active cycles, PMC at
+// M = 3M, K = 512, N = 256, profiles/r02/gemm_pmc_cfg3.txt.)
+constexpr int kSplitRowWordsNT = 48;
+__device__ __forceinline__ int nt_chunk(int row, int c) { return (c ^ ((row >> 2) & 3)) << 2; }
+
 template <int ROWS>
 __device__ __forceinline__ void store_tile_split(uint32_t* __restrict__ dst, const float4 (&r)[ROWS / 32], int tid) {
 #pragma unroll
   for (int i = 0; i < ROWS / 32; ++i) {
     uint2 o[3];
     split4(r[i], o);
-    uint32_t* row = dst + ((tid >> 3) + 32 * i) * kSplitRowWords + (tid & 7) * 2;
+    const int rr = (tid >> 3) + 32 * i;
+    const int q = tid & 7;                        // float4 quad q = chunk q >> 1, half q & 1
+    uint32_t* row = dst + rr * kSplitRowWordsNT + nt_chunk(rr, q >> 1) + (q & 1) * 2;
 #pragma unroll
     for (int p = 0; p < 3; ++p) *reinterpret_cast<uint2*>(row + p * 16) = o[p];
   }
@@ -193,6 +204,8 @@ struct CombEpi {
   int64_t cs;         // first self column of C (a multiple of 4)
   const float* eps;   // device float[1]
   float* part;        // [workgroup tiles] eps-gradient partials
+  const void* gp = nullptr;   // optional: a gradient g_x_dst accumulates onto (may alias gd), row stride ldgp
+  int64_t ldgp = 0;
 };
 
 // Epilogue shared by the fp32 and bf16 kernels.  Per 32-row half (tm) each wave parks its 32 x WCOLS
@@ -224,6 +237,7 @@ __device__ __forceinline__ void epilogue(const f32x16 (&acc)[2][TN], float* smem
   const bool self_cols = EPI == 4 && col >= ce.cs && nv > 0;   // col, cs multiples of 4: whole group
   const OutT* xd = static_cast<const OutT*>(ce.xd);
   OutT* gd = static_cast<OutT*>(ce.gd);
+  const OutT* gp = static_cast<const OutT*>(ce.gp);
   if (EPI == 1 || EPI == 2) {
 #pragma unroll
     for (int t = 0; t < 4; ++t)
@@ -233,12 +247,17 @@ __device__ __forceinline__ void epilogue(const f32x16 (&acc)[2][TN], float* smem
 #pragma unroll
   for (int tm = 0; tm < 2; ++tm) {
     typename Out4<OutT>::raw acc_raw[kJ];
+    typename Out4<OutT>::raw prev_raw[EPI == 4 ? kJ : 1];
 #pragma unroll
-    for (int j = 0; j < kJ; ++j) {   // accum (EPI 1) / x_dst (EPI 4) rows: loaded before the LDS round trip
+    for (int j = 0; j < kJ; ++j) {   // accum (EPI 1) / x_dst, g_prev (EPI 4) rows: loaded before the LDS round trip
       acc_raw[j] = {};
       const int64_t row = m0 + wm * 64 + tm * 32 + r0 + kRS * j;
       if (EPI == 1 && accum && row < M && nv) acc_raw[j] = Out4<OutT>::ld_raw(accum + row * ldc + col, full, nv);
       if (EPI == 4 && self_cols && row < M) acc_raw[j] = Out4<OutT>::ld_raw(xd + row * ce.ldxd + (col - ce.cs), full, nv);
+      if constexpr (EPI == 4) {
+        prev_raw[j] = {};
+        if (gp && gd && self_cols && row < M) prev_raw[j] = Out4<OutT>::ld_raw(gp + row * ce.ldgp + (col - ce.cs), full, nv);
+      }
     }
 #pragma unroll
     for (int tn = 0; tn < TN; ++tn)
@@ -268,15 +287,19 @@ __device__ __forceinline__ void epilogue(const f32x16 (&acc)[2][TN], float* smem
       Out4<OutT>::st(Y + row * ldc + col, o, full, nv);
       if (EPI == 1 && Z) Out4<OutT>::st(Z + row * ldc + col, zz, full, nv);
       if (EPI == 4 && self_cols) {
-        float c4[4], x4[4], g4[4];
+        float c4[4], x4[4], g4[4], p4[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int t = 0; t < 4; ++t) c4[t] = Out4<OutT>::rt(o[t]);   // C as stored
         const int64_t sc = col - ce.cs;
         Out4<OutT>::unpack(acc_raw[j], x4);
+        if constexpr (EPI == 4) {
+          if (gp) Out4<OutT>::unpack(prev_raw[j], p4);
+        }
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
           if (t < nv) ep = __fadd_rn(ep, __fmul_rn(c4[t], x4[t]));
           g4[t] = __fmul_rn(sc_self, c4[t]);
+          if (gp) g4[t] = __fadd_rn(p4[t], g4[t]);   // accumulate onto another relation's g_x_dst
         }
         if (gd) Out4<OutT>::st(gd + row * ce.ldgd + sc, g4, full, nv);
       }
@@ -312,7 +335,7 @@ __global__ __launch_bounds__(256, 3) void k_gemm_nt(Src2 A, Src2 B, int64_t M, i
   constexpr int BM = WM * 64;             // rows per workgroup tile
   constexpr int BN = WN * TN * 32;        // columns per workgroup tile
   constexpr int WCOLS = TN * 32;          // columns per wave
-  constexpr int kRowW = kSplit ? kSplitRowWords : kLds;   // 4-B words per LDS row
+  constexpr int kRowW = kSplit ? kSplitRowWordsNT : kLds;   // 4-B words per LDS row
   __shared__ __attribute__((aligned(16))) float smem[(BM + BN) * kRowW];
   float* As = smem;
   float* Bs = smem + BM * kRowW;
@@ -379,14 +402,14 @@ __global__ __launch_bounds__(256, 3) void k_gemm_nt(Src2 A, Src2 B, int64_t M, i
         for (int t = 0; t < 2; ++t)
 #pragma unroll
           for (int p = 0; p < 3; ++p)
-            fa[t][p] = *reinterpret_cast<const bf16x8*>(Ash + (wm * 64 + t * 32 + li) * kSplitRowWords + p * 16 +
-                                                        kb * 8 + lh * 4);
+            fa[t][p] = *reinterpret_cast<const bf16x8*>(Ash + (wm * 64 + t * 32 + li) * kSplitRowWordsNT + p * 16 +
+                                                        nt_chunk(li, kb * 2 + lh));
 #pragma unroll
         for (int t = 0; t < TN; ++t)
 #pragma unroll
           for (int p = 0; p < 3; ++p)
-            fb[t][p] = *reinterpret_cast<const bf16x8*>(Bsh + (wn * WCOLS + t * 32 + li) * kSplitRowWords + p * 16 +
-                                                        kb * 8 + lh * 4);
+            fb[t][p] = *reinterpret_cast<const bf16x8*>(Bsh + (wn * WCOLS + t * 32 + li) * kSplitRowWordsNT + p * 16 +
+                                                        nt_chunk(li, kb * 2 + lh));
 #pragma unroll
         for (int tm = 0; tm < 2; ++tm)
 #pragma unroll
@@ -905,7 +928,9 @@ __global__ __launch_bounds__(256, 1) void k_nt2(const T* __restrict__ a1, int64_
   for (int64_t s = 0; s < S; ++s) {
     // stage s landed for this wave's DMAs: everything issued after it may stay in flight
     const int64_t ahead = (S - 1 < s + NST - 2 ? S - 1 : s + NST - 2) - s;
-    if constexpr (NST >= 3) {
+    if constexpr (NST >= 4) {
+      if (ahead >= 2) wait_vm<2 * G>(); else if (ahead == 1) wait_vm<G>(); else wait_vm<0>();
+    } else if constexpr (NST == 3) {
       if (ahead >= 1) wait_vm<G>(); else wait_vm<0>();
     } else {
       wait_vm<0>();
@@ -983,13 +1008,23 @@ __global__ __launch_bounds__(256, 1) void k_nt2(const T* __restrict__ a1, int64_
   if constexpr (EPI == 4) tile_partial(smem, ep, ce.part, q);
 }
 
-template <typename T, int BN>
+template <typename T, int BN, int NST>
 constexpr size_t nt2_lds_bytes() {
   using P = Nt2<T>;
   constexpr size_t stage = P::A_BYTES + (size_t)P::NP * BN * P::BROW;
-  constexpr size_t ring = stage * (P::kF32 ? 2 : 3);
+  constexpr size_t ring = stage * NST;
   constexpr size_t epi = 4 * 32 * (BN / 2 + 4) * 4;
   return ring > epi ? ring : epi;
+}
+
+// Tile / ring-depth variants of k_nt2 (HGIN_NT2_TILE: 0 = BN 256 with the default depth (fp32 2, bf16 3 stages);
+// 1 = BN 128, deeper ring (fp32 3, bf16 4 stages): more A bytes in flight per CU, A read by two tiles).
+int nt2_tile() {
+  static const int v = [] {
+    const char* e = getenv("HGIN_NT2_TILE");
+    return e ? atoi(e) : 0;
+  }();
+  return v;
 }
 
 // Measured (profiles/r02/nt2_not_adopted_*.txt, cfg3 / cfg5 shapes): bit-identical, but 5-16 % slower than
@@ -1033,10 +1068,9 @@ int launch_nt2(const T* a1, int64_t lda1, int64_t k1, const T* a2, int64_t lda2,
                                      (ce.gd == nullptr || (aligned16(ce.gd) && ce.ldgd % 4 == 0))));
   const bool xcd = xcd_remap_enabled();
   const uint16_t* bp = static_cast<const uint16_t*>(planes);
-#define HGIN_NT2_LAUNCH(BNV)                                                                                   \
+#define HGIN_NT2_LAUNCH(BNV, NSTV)                                                                             \
   {                                                                                                            \
-    constexpr int NSTV = Nt2<T>::kF32 ? 2 : 3;                                                                 \
-    constexpr size_t lds = nt2_lds_bytes<T, BNV>();                                                            \
+    constexpr size_t lds = nt2_lds_bytes<T, BNV, NSTV>();                                                      \
     auto kern = k_nt2<T, EPI, BNV, NSTV, OutT>;                                                                \
     static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),                    \
                                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds); \
@@ -1050,10 +1084,11 @@ int launch_nt2(const T* a1, int64_t lda1, int64_t k1, const T* a2, int64_t lda2,
                                 vec_out, tiles, xcd, ce);                                                      \
     if (tiles_out) *tiles_out = tiles;                                                                         \
   }
-  if (N % 256 == 0)
-    HGIN_NT2_LAUNCH(256)
+  constexpr bool F32 = Nt2<T>::kF32;
+  if (N % 256 == 0 && nt2_tile() == 0)
+    HGIN_NT2_LAUNCH(256, (F32 ? 2 : 3))
   else
-    HGIN_NT2_LAUNCH(128)
+    HGIN_NT2_LAUNCH(128, (F32 ? 3 : 4))
 #undef HGIN_NT2_LAUNCH
   return check_launch(what);
 }
@@ -1105,7 +1140,8 @@ size_t combine_ws_bytes(int64_t M, int64_t N) {
 
 template <typename T>
 int gemm_nt_combine(const char* what, const T* a, int64_t lda, const T* b, int64_t ldb, T* c, int64_t ldc, int64_t M,
-                    int64_t N, int64_t K, const T* x_dst, int64_t ld_xd, T* g_dst, int64_t ld_gd, int64_t cs,
+                    int64_t N, int64_t K, const T* x_dst, int64_t ld_xd, T* g_dst, int64_t ld_gd, const T* g_prev,
+                    int64_t ld_gp, int64_t cs,
                     const float* eps, float* g_eps, void* workspace, size_t workspace_bytes, const void* b_planes,
                     void* stream) {
   HGIN_ARG_CHECK(M >= 0 && N >= 0 && K >= 0 && cs >= 0 && cs <= N, "%s: bad sizes", what);
@@ -1123,7 +1159,12 @@ int gemm_nt_combine(const char* what, const T* a, int64_t lda, const T* b, int64
     return HGIN_E_WORKSPACE;
   }
   float* part = static_cast<float*>(workspace);
-  const CombEpi ce{x_dst, ld_xd, g_dst, ld_gd, cs, eps, part};
+  HGIN_ARG_CHECK(!g_prev || (g_dst && ld_gp >= N - cs && aligned16(g_prev) == aligned16(g_dst) &&
+                              (ld_gp % 4 == 0) == (ld_gd % 4 == 0)),
+                 "%s: g_prev needs g_dst and a matching layout", what);
+  CombEpi ce{x_dst, ld_xd, g_dst, ld_gd, cs, eps, part};
+  ce.gp = g_prev;
+  ce.ldgp = ld_gp;
   int64_t tiles = 0;
   int rc;
   if (nt2_eligible<T>(a, lda, K, nullptr, 0, b_planes, N, K, gemm_split_enabled()))
@@ -1161,20 +1202,20 @@ extern "C" int hgin_gemm_nt_combine_workspace_size(int64_t M, int64_t N, size_t*
 
 extern "C" int hgin_gemm_nt_combine_f32(const float* a, int64_t lda, const float* b, int64_t ldb, float* c,
                                         int64_t ldc, int64_t M, int64_t N, int64_t K, const float* x_dst,
-                                        int64_t ld_xd, float* g_dst, int64_t ld_gd, int64_t cs, const float* eps,
-                                        float* g_eps, void* workspace, size_t workspace_bytes, const void* b_planes,
-                                        void* stream) {
+                                        int64_t ld_xd, float* g_dst, int64_t ld_gd, const float* g_prev,
+                                        int64_t ld_gp, int64_t cs, const float* eps, float* g_eps, void* workspace,
+                                        size_t workspace_bytes, const void* b_planes, void* stream) {
   return gemm_nt_combine<float>("hgin_gemm_nt_combine_f32", a, lda, b, ldb, c, ldc, M, N, K, x_dst, ld_xd, g_dst,
-                                ld_gd, cs, eps, g_eps, workspace, workspace_bytes, b_planes, stream);
+                                ld_gd, g_prev, ld_gp, cs, eps, g_eps, workspace, workspace_bytes, b_planes, stream);
 }
 
 extern "C" int hgin_gemm_nt_combine_bf16(const uint16_t* a, int64_t lda, const uint16_t* b, int64_t ldb, uint16_t* c,
                                          int64_t ldc, int64_t M, int64_t N, int64_t K, const uint16_t* x_dst,
-                                         int64_t ld_xd, uint16_t* g_dst, int64_t ld_gd, int64_t cs, const float* eps,
-                                         float* g_eps, void* workspace, size_t workspace_bytes, const void* b_planes,
-                                         void* stream) {
+                                         int64_t ld_xd, uint16_t* g_dst, int64_t ld_gd, const uint16_t* g_prev,
+                                         int64_t ld_gp, int64_t cs, const float* eps, float* g_eps, void* workspace,
+                                         size_t workspace_bytes, const void* b_planes, void* stream) {
   return gemm_nt_combine<uint16_t>("hgin_gemm_nt_combine_bf16", a, lda, b, ldb, c, ldc, M, N, K, x_dst, ld_xd, g_dst,
-                                   ld_gd, cs, eps, g_eps, workspace, workspace_bytes, b_planes, stream);
+                                   ld_gd, g_prev, ld_gp, cs, eps, g_eps, workspace, workspace_bytes, b_planes, stream);
 }
 
 extern "C" int hgin_gin_mlp_fwd_bf16(const uint16_t* a1, int64_t lda1, int64_t k1, const uint16_t* a2, int64_t lda2,

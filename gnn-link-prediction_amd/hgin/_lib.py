@@ -134,10 +134,10 @@ _SIGS = {
     "hgin_prelu_bwd_f32": ([_P, _I64, _P, _I64, _I64, _P, _P, _P, _P, _P, _SZ, _P], _I32),
     "hgin_gemm_nt_f32": ([_P, _I64, _P, _I64, _P, _I64, _I64, _I64, _I64, _P, _P], _I32),
     "hgin_gemm_nt_combine_workspace_size": ([_I64, _I64, ctypes.POINTER(_SZ)], _I32),
-    "hgin_gemm_nt_combine_f32": ([_P, _I64, _P, _I64, _P, _I64, _I64, _I64, _I64, _P, _I64, _P, _I64, _I64, _P, _P,
-                                  _P, _SZ, _P, _P], _I32),
-    "hgin_gemm_nt_combine_bf16": ([_P, _I64, _P, _I64, _P, _I64, _I64, _I64, _I64, _P, _I64, _P, _I64, _I64, _P, _P,
-                                   _P, _SZ, _P, _P], _I32),
+    "hgin_gemm_nt_combine_f32": ([_P, _I64, _P, _I64, _P, _I64, _I64, _I64, _I64, _P, _I64, _P, _I64, _P, _I64, _I64,
+                                  _P, _P, _P, _SZ, _P, _P], _I32),
+    "hgin_gemm_nt_combine_bf16": ([_P, _I64, _P, _I64, _P, _I64, _I64, _I64, _I64, _P, _I64, _P, _I64, _P, _I64, _I64,
+                                   _P, _P, _P, _SZ, _P, _P], _I32),
     "hgin_gemm_tn_workspace_size": ([_I64, _I64, _I64, ctypes.POINTER(_SZ)], _I32),
     "hgin_gemm_tn_f32": ([_P, _I64, _P, _I64, _I64, _P, _I64, _I64, _I64, _I64, _P, _I64, _P, _SZ, _P], _I32),
     "hgin_aggregate_bf16": ([_P, _P, _I64, _P, _I64, _I64, _P, _I64, _I64, _P, _I32, _P, _I64, _P], _I32),

@@ -20,6 +20,7 @@ relations ``a + b``, bit-identical).  Everything runs on the device; CPU tensors
 """
 from __future__ import annotations
 
+import os
 from typing import Any, Callable, Dict, Optional, Tuple, Union
 
 import torch
@@ -28,6 +29,10 @@ from torch import Tensor
 from . import ops
 
 EdgeType = Tuple[str, str, str]
+
+# HeteroConv layers of GINLayers run as one autograd node (ops.hetero_gin_layer); HGIN_LAYER_FN=0 (or setting
+# this to False) keeps one autograd node per relation, whose shared-node-type gradients autograd adds itself.
+LAYER_FN = os.environ.get("HGIN_LAYER_FN", "1") != "0"
 
 
 def reset(value: Any) -> None:
@@ -150,7 +155,49 @@ class HeteroConv(torch.nn.Module):
         for conv in self.convs.values():
             conv.reset_parameters()
 
+    def _layer_specs(self, x_dict, edge_index_dict):
+        """The relations of this call for the one-node layer path (ops.hetero_gin_layer), or None when it does not
+        apply: every live relation a GINLayer-style GINConv (Linear + PReLU, trainable-or-buffer eps) between two
+        different node types, device inputs, aggr='sum'."""
+        if self.aggr != "sum" or not LAYER_FN:
+            return None
+        types, specs, params = [], [], []
+        for edge_type, edge_index in edge_index_dict.items():
+            src, _, dst = edge_type
+            key = "__".join(edge_type)
+            if key not in self.convs or key in self.skip:
+                continue
+            conv = self.convs[key]
+            conv = getattr(conv, "conv", conv)
+            if not isinstance(conv, GINConv) or not _fusable_mlp(conv.nn) or src == dst:
+                return None
+            for t in (src, dst):
+                if t not in types:
+                    types.append(t)
+            x_src, x_dst = x_dict[src], x_dict[dst]
+            if not (x_src.is_cuda and x_dst.is_cuda):
+                return None
+            graph = conv._graph(edge_index, x_src, x_dst, None)
+            mode = ops.COMBINE_CONCAT if conv.concat else ops.COMBINE_ADD
+            specs.append(ops.RelSpec(types.index(src), types.index(dst), graph, mode))
+            lin, act = conv.nn[0], conv.nn[1]
+            params.append((conv.eps, lin.weight, lin.bias, act.weight))
+        if not specs:
+            return None
+        return types, specs, params
+
     def forward(self, x_dict: Dict[str, Tensor], edge_index_dict: Dict[EdgeType, Tensor]) -> Dict[str, Tensor]:
+        plan = self._layer_specs(x_dict, edge_index_dict)
+        if plan is not None:
+            # one autograd node for the layer: the gradient sums over relations sharing a node type happen inside
+            # the backward kernels (ops._HeteroGINLayerFn); same forward arithmetic as the loop below
+            types, specs, params = plan
+            ys = ops.hetero_gin_layer([x_dict[t] for t in types], specs, params)
+            dst_order = []
+            for sp in specs:
+                if types[sp.dst] not in dst_order:
+                    dst_order.append(types[sp.dst])
+            return dict(zip(dst_order, ys))
         outs: Dict[str, list] = {}
         for edge_type, edge_index in edge_index_dict.items():
             src, _, dst = edge_type

@@ -332,22 +332,28 @@ def gemm_nt(a: Tensor, b: Tensor) -> Tensor:
     return c
 
 
-def gemm_nt_combine(a: Tensor, b: Tensor, x_dst: Tensor, eps: Tensor, cs: int, want_gx: bool):
-    """(c, g_x_dst, g_eps): c = a @ b^T, g_x_dst = (1 + eps) c[:, cs:], g_eps = sum(c[:, cs:] * x_dst) in one
-    GEMM launch + a final sum (hgin_gemm_nt_combine_*): the dX GEMM of a GINConv backward with the self
-    term's backward in its epilogue."""
+def gemm_nt_combine(a: Tensor, b: Tensor, x_dst: Tensor, eps: Tensor, cs: int, want_gx: bool,
+                    g_prev: Optional[Tensor] = None):
+    """(c, g_x_dst, g_eps): c = a @ b^T, g_x_dst = (1 + eps) c[:, cs:] [+ g_prev, in place], g_eps =
+    sum(c[:, cs:] * x_dst) in one GEMM launch + a final sum (hgin_gemm_nt_combine_*): the dX GEMM of a GINConv
+    backward with the self term's backward in its epilogue."""
     a, b = _rowmajor(a), _rowmajor(b)
-    _same_dtype("gemm_nt_combine", a, b, x_dst)
+    _same_dtype("gemm_nt_combine", a, b, x_dst, g_prev)
     M, K = a.shape
     N = b.shape[0]
     c = torch.empty(M, N, dtype=a.dtype, device=a.device)
-    gx = torch.empty(M, N - cs, dtype=a.dtype, device=a.device) if want_gx else None
+    if g_prev is not None:
+        assert want_gx and g_prev.shape == (M, N - cs) and g_prev.stride(1) == 1
+        gx = g_prev                      # accumulated in place
+    else:
+        gx = torch.empty(M, N - cs, dtype=a.dtype, device=a.device) if want_gx else None
     g_eps = torch.empty(1, dtype=torch.float32, device=a.device)
     nbytes = ctypes.c_size_t(0)
     _lib.check(_lib.lib().hgin_gemm_nt_combine_workspace_size(M, N, ctypes.byref(nbytes)), "nt_combine_workspace")
     ws = _workspace(nbytes.value, a.device)
     _lib.call(f"hgin_gemm_nt_combine_{_sfx(a)}", _p(a), a.stride(0), _p(b), b.stride(0), _p(c), c.stride(0), M, N, K,
-              _p(x_dst), x_dst.stride(0), _p(gx), gx.stride(0) if gx is not None else 0, cs, _p(eps), _p(g_eps),
+              _p(x_dst), x_dst.stride(0), _p(gx), gx.stride(0) if gx is not None else 0, _p(g_prev),
+              g_prev.stride(0) if g_prev is not None else 0, cs, _p(eps), _p(g_eps),
               _p(ws), nbytes.value, _p(nt_planes(b)), _stream(a))
     return c, gx, g_eps
 
@@ -458,9 +464,22 @@ def gin_mlp_fwd(comb: Tensor, weight: Tensor, bias: Tensor, prelu: Optional[Tens
 # ---------------------------------------------------------------------------------------------------
 # autograd
 # ---------------------------------------------------------------------------------------------------
-def _backward_aggregate(graph: RelationGraph, g_agg: Tensor) -> Tensor:
-    """d x_src = index_add over the reversed relation = the A3 kernel on the CSC (edge order kept)."""
+_ZERO = {}
+
+
+def _zero(device) -> Tensor:
+    t = _ZERO.get(device)
+    if t is None:
+        t = _ZERO[device] = torch.zeros(1, dtype=torch.float32, device=device)
+    return t
+
+
+def _backward_aggregate(graph: RelationGraph, g_agg: Tensor, prev: Optional[Tensor] = None) -> Tensor:
+    """d x_src = index_add over the reversed relation = the A3 kernel on the CSC (edge order kept).  ``prev``:
+    a running gradient of the source type, accumulated onto in place (ADD self term with eps 0: prev + sum)."""
     csc = graph.csc
+    if prev is not None:
+        return aggregate_into(csc, g_agg, prev, _zero(g_agg.device), COMBINE_ADD, prev)
     g = torch.empty(graph.n_src, g_agg.size(1), dtype=g_agg.dtype, device=g_agg.device)
     return aggregate_into(csc, g_agg, None, None, COMBINE_NONE, g)
 
@@ -492,71 +511,187 @@ class _AggregateFn(torch.autograd.Function):
         return g_src, g_dst, (g_eps.view_as(eps) if need_eps and g_eps is not None else None), None, None
 
 
+def _gin_forward(x_src, x_dst, eps, weight, bias, prelu, accum, graph: RelationGraph, mode: int, data_inputs: bool):
+    """One GINConv + GINLayer MLP forward: y = prelu(comb @ W^T + b) [+ accum], comb = aggregate + self term.
+    Returns (y, w_op, comb, z) — what the backward needs besides x_dst / eps / prelu."""
+    f_src = x_src.size(1)
+    w_op = _as(weight, x_src.dtype)          # bf16 path: the GEMM reads a bf16 copy of the fp32 master
+    if mode == COMBINE_CONCAT and data_inputs:
+        # inputs are data (the first layer): the backward never needs the concat, so the self half
+        # (1 + eps) x_dst is formed in the GEMM's tile loads instead of being written by the aggregate and
+        # read back (2 * N_dst * F_dst * s bytes less per relation); comb holds the aggregate only
+        comb = torch.empty(graph.n_dst, f_src, dtype=x_src.dtype, device=x_src.device)
+        aggregate_into(graph.csr, x_src, None, None, COMBINE_NONE, comb)
+        z, y = gin_mlp_fwd(comb, w_op, bias, prelu, accum, comb2=x_dst, eps2=eps)
+    else:
+        width = f_src + (x_dst.size(1) if mode == COMBINE_CONCAT else 0)
+        comb = torch.empty(graph.n_dst, width, dtype=x_src.dtype, device=x_src.device)
+        aggregate_into(graph.csr, x_src, x_dst, eps, mode, comb)
+        z, y = gin_mlp_fwd(comb, w_op, bias, prelu, accum)
+    return y, w_op, comb, z
+
+
+def _gin_backward(g_y, x_dst, eps, weight, prelu, comb, z, graph: RelationGraph, mode: int, f_src: int,
+                  need_src: bool, need_dst: bool, need_eps: bool, need_w: bool,
+                  g_src_prev: Optional[Tensor] = None, g_dst_prev: Optional[Tensor] = None):
+    """Backward of _gin_forward: (g_src, g_dst, g_eps, g_w, g_b, g_a).  ``g_src_prev`` / ``g_dst_prev``: running
+    gradients of the source / destination node type from other relations, which g_src / g_dst accumulate onto
+    in place inside the CSC aggregate (ADD mode, eps 0) and the dX GEMM's epilogue — autograd's sum over the
+    relations sharing a node type without separate add kernels (the returned tensors are then those buffers)."""
+    g_y = _rowmajor(g_y)
+    g_w = g_src = g_dst = g_eps = None
+    if need_src or need_dst:
+        # (a side stream overlapping dW with the dX GEMM + CSC aggregate measured 1 % slower on cfg2 / cfg2bf:
+        # each of these kernels already fills the 256 CUs)
+        g_w, g_a, g_b, g_z = mlp_bwd_w(g_y, z, prelu, comb, want_gz=True)
+        cs = f_src if mode == COMBINE_CONCAT else 0
+        if mode != COMBINE_NONE and cs % 4 == 0 and x_dst.stride(1) == 1:
+            # dX = g_z W [N_dst, K] with the self term's backward in the GEMM epilogue
+            g_comb, g_dst, g_eps = gemm_nt_combine(g_z, weight.t().contiguous(), x_dst, eps, cs, need_dst,
+                                                   g_prev=g_dst_prev if need_dst else None)
+        else:
+            g_comb = gemm_nt(g_z, weight.t().contiguous())      # dX = g_z W   [N_dst, K]
+            if mode != COMBINE_NONE:
+                g_dst, g_eps = combine_bwd(g_comb[:, cs:], x_dst, eps, need_dst)
+                if g_dst is not None and g_dst_prev is not None:
+                    g_dst = g_dst_prev.add_(g_dst)
+        if need_src:
+            g_src = _backward_aggregate(graph, g_comb[:, :f_src], g_src_prev)
+    elif need_eps and mode != COMBINE_NONE:
+        # Only parameters need gradients (the first layer, whose inputs are data):
+        # sum(g_comb[:, self] * x_dst) = sum(W_self * (g_z^T x_dst)), so one TN pass over
+        # [aggregate | x_dst] yields dW and the eps gradient and the [N_dst, K] dX GEMM is skipped.
+        if mode == COMBINE_CONCAT:
+            G, g_a, g_b, _ = mlp_bwd_w(g_y, z, prelu, comb[:, :f_src], x_dst)
+        else:
+            G, g_a, g_b, _ = mlp_bwd_w(g_y, z, prelu, comb, x_dst)
+        g_w, g_eps = self_wgrad(G, weight, f_src, mode == COMBINE_CONCAT, eps)
+        g_w = g_w if need_w else None
+    elif mode == COMBINE_CONCAT and comb.size(1) == f_src:
+        # the forward kept only the aggregate (inputs are data): dW of the self block = (1 + eps) g_z^T x_dst
+        G, g_a, g_b, _ = mlp_bwd_w(g_y, z, prelu, comb, x_dst)
+        g_w = self_wgrad(G, weight, f_src, True, eps)[0] if need_w else None
+    else:
+        g_w, g_a, g_b, _ = mlp_bwd_w(g_y, z, prelu, comb)
+    return g_src, g_dst, g_eps, g_w, g_b, g_a
+
+
 class _GINConvFn(torch.autograd.Function):
     """Fused GINConv + GINLayer MLP: y = prelu(comb @ W^T + b) [+ accum], comb = aggregate + self term."""
 
     @staticmethod
     def forward(ctx, x_src, x_dst, eps, weight, bias, prelu, accum, graph: RelationGraph, mode: int):
-        f_src = x_src.size(1)
-        w_op = _as(weight, x_src.dtype)          # bf16 path: the GEMM reads a bf16 copy of the fp32 master
-        if mode == COMBINE_CONCAT and not (ctx.needs_input_grad[0] or ctx.needs_input_grad[1]):
-            # inputs are data (the first layer): the backward never needs the concat, so the self half
-            # (1 + eps) x_dst is formed in the GEMM's tile loads instead of being written by the aggregate and
-            # read back (2 * N_dst * F_dst * s bytes less per relation); comb holds the aggregate only
-            comb = torch.empty(graph.n_dst, f_src, dtype=x_src.dtype, device=x_src.device)
-            aggregate_into(graph.csr, x_src, None, None, COMBINE_NONE, comb)
-            z, y = gin_mlp_fwd(comb, w_op, bias, prelu, accum, comb2=x_dst, eps2=eps)
-        else:
-            width = f_src + (x_dst.size(1) if mode == COMBINE_CONCAT else 0)
-            comb = torch.empty(graph.n_dst, width, dtype=x_src.dtype, device=x_src.device)
-            aggregate_into(graph.csr, x_src, x_dst, eps, mode, comb)
-            z, y = gin_mlp_fwd(comb, w_op, bias, prelu, accum)
-        ctx.graph, ctx.mode, ctx.f_src = graph, mode, f_src
+        data_inputs = not (ctx.needs_input_grad[0] or ctx.needs_input_grad[1])
+        y, w_op, comb, z = _gin_forward(x_src, x_dst, eps, weight, bias, prelu, accum, graph, mode, data_inputs)
+        ctx.graph, ctx.mode, ctx.f_src = graph, mode, x_src.size(1)
         ctx.save_for_backward(x_dst, eps, w_op, prelu, comb, z)
         return y
 
     @staticmethod
     def backward(ctx, g_y):
         x_dst, eps, weight, prelu, comb, z = ctx.saved_tensors   # weight: the operand copy the forward used
-        need = ctx.needs_input_grad
-        need_src, need_dst, need_eps, need_w, need_b, need_a, need_acc = need[:7]
-        g_y = _rowmajor(g_y)
-        g_w = g_src = g_dst = g_eps = None
-        f_src, mode = ctx.f_src, ctx.mode
-        if need_src or need_dst:
-            # (a side stream overlapping dW with the dX GEMM + CSC aggregate measured 1 % slower on cfg2 / cfg2bf:
-            # each of these kernels already fills the 256 CUs)
-            g_w, g_a, g_b, g_z = mlp_bwd_w(g_y, z, prelu, comb, want_gz=True)
-            cs = f_src if mode == COMBINE_CONCAT else 0
-            if mode != COMBINE_NONE and cs % 4 == 0 and x_dst.stride(1) == 1:
-                # dX = g_z W [N_dst, K] with the self term's backward in the GEMM epilogue
-                g_comb, g_dst, g_eps = gemm_nt_combine(g_z, weight.t().contiguous(), x_dst, eps, cs, need_dst)
-            else:
-                g_comb = gemm_nt(g_z, weight.t().contiguous())      # dX = g_z W   [N_dst, K]
-                if mode != COMBINE_NONE:
-                    g_dst, g_eps = combine_bwd(g_comb[:, cs:], x_dst, eps, need_dst)
-            if need_src:
-                g_src = _backward_aggregate(ctx.graph, g_comb[:, :f_src])
-        elif need_eps and mode != COMBINE_NONE:
-            # Only parameters need gradients (the first layer, whose inputs are data):
-            # sum(g_comb[:, self] * x_dst) = sum(W_self * (g_z^T x_dst)), so one TN pass over
-            # [aggregate | x_dst] yields dW and the eps gradient and the [N_dst, K] dX GEMM is skipped.
-            if mode == COMBINE_CONCAT:
-                G, g_a, g_b, _ = mlp_bwd_w(g_y, z, prelu, comb[:, :f_src], x_dst)
-            else:
-                G, g_a, g_b, _ = mlp_bwd_w(g_y, z, prelu, comb, x_dst)
-            g_w, g_eps = self_wgrad(G, weight, f_src, mode == COMBINE_CONCAT, eps)
-            g_w = g_w if need_w else None
-        elif mode == COMBINE_CONCAT and comb.size(1) == f_src:
-            # the forward kept only the aggregate (inputs are data): dW of the self block = (1 + eps) g_z^T x_dst
-            G, g_a, g_b, _ = mlp_bwd_w(g_y, z, prelu, comb, x_dst)
-            g_w = self_wgrad(G, weight, f_src, True, eps)[0] if need_w else None
-        else:
-            g_w, g_a, g_b, _ = mlp_bwd_w(g_y, z, prelu, comb)
+        need_src, need_dst, need_eps, need_w, need_b, need_a, need_acc = ctx.needs_input_grad[:7]
+        g_src, g_dst, g_eps, g_w, g_b, g_a = _gin_backward(g_y, x_dst, eps, weight, prelu, comb, z, ctx.graph,
+                                                           ctx.mode, ctx.f_src, need_src, need_dst, need_eps, need_w)
         g_acc = g_y if need_acc else None
         return (g_src, g_dst, (g_eps.view_as(eps) if (need_eps and g_eps is not None) else None),
                 g_w if need_w else None, g_b if need_b else None, (g_a.view_as(prelu) if need_a else None), g_acc,
                 None, None)
+
+
+@dataclass
+class RelSpec:
+    """One relation of a HeteroConv layer for the layer-level path: node-type indices, graph, combine mode."""
+    src: int
+    dst: int
+    graph: RelationGraph
+    mode: int
+
+
+class _HeteroGINLayerFn(torch.autograd.Function):
+    """A whole HeteroConv(aggr='sum') layer of GINLayers (models.py:286-298) as ONE autograd node, so the
+    backward controls how the gradients of a node type consumed by several relations are summed (autograd would
+    add them with separate elementwise kernels: 3.1 ms / step at cfg5, 6.2 ms at cfg3): every contribution after
+    the first accumulates in place inside the kernel that produces it (the CSC aggregate's ADD self term with
+    eps 0, the dX GEMM's combine epilogue).  Relations run in forward order (the second relation into a type adds
+    the first's output in its epilogue, as conv.HeteroConv does); the backward visits them in reverse (autograd's
+    order) and skips relations whose output gradient is None (dead relations).
+
+    Inputs: (specs, n_types, *tensors) with tensors = node features per type, then (eps, weight, bias, prelu) per
+    relation.  Outputs: one tensor per destination type, in order of first appearance."""
+
+    @staticmethod
+    def forward(ctx, specs, n_types, *tensors):
+        xs = tensors[:n_types]
+        need = ctx.needs_input_grad[2:]
+        outs = {}
+        saved = []
+        for i, sp in enumerate(specs):
+            eps, w, b, a = tensors[n_types + 4 * i: n_types + 4 * i + 4]
+            data_inputs = not (need[sp.src] or need[sp.dst])
+            y, w_op, comb, z = _gin_forward(xs[sp.src], xs[sp.dst], eps, w, b, a, outs.get(sp.dst), sp.graph,
+                                            sp.mode, data_inputs)
+            outs[sp.dst] = y
+            saved += [w_op, comb, z]
+        ctx.specs, ctx.n_types = specs, n_types
+        ctx.out_types = list(outs)
+        ctx.f_src = [xs[sp.src].size(1) for sp in specs]
+        ctx.set_materialize_grads(False)
+        ctx.save_for_backward(*tensors, *saved)
+        return tuple(outs[t] for t in ctx.out_types)
+
+    @staticmethod
+    def backward(ctx, *g_outs):
+        specs, nt = ctx.specs, ctx.n_types
+        st = ctx.saved_tensors
+        xs = st[:nt]
+        npar = 4 * len(specs)
+        params = st[nt:nt + npar]
+        saved = st[nt + npar:]
+        need = ctx.needs_input_grad[2:]
+        g_of = dict(zip(ctx.out_types, g_outs))
+        gx = [None] * nt
+        gp = [None] * npar
+        for i in reversed(range(len(specs))):
+            sp = specs[i]
+            g_y = g_of.get(sp.dst)
+            if g_y is None:
+                continue
+            eps, _, _, prelu = params[4 * i: 4 * i + 4]
+            w_op, comb, z = saved[3 * i: 3 * i + 3]
+            pn = need[nt + 4 * i: nt + 4 * i + 4]
+            g_src, g_dst, g_eps, g_w, g_b, g_a = _gin_backward(
+                g_y, xs[sp.dst], eps, w_op, prelu, comb, z, sp.graph, sp.mode, ctx.f_src[i], need[sp.src],
+                need[sp.dst], pn[0], pn[1], g_src_prev=gx[sp.src], g_dst_prev=gx[sp.dst])
+            if need[sp.src]:
+                gx[sp.src] = g_src
+            if need[sp.dst]:
+                gx[sp.dst] = g_dst
+            gp[4 * i] = g_eps.view_as(eps) if (pn[0] and g_eps is not None) else None
+            gp[4 * i + 1] = g_w if pn[1] else None
+            gp[4 * i + 2] = g_b if pn[2] else None
+            gp[4 * i + 3] = g_a.view_as(prelu) if (pn[3] and g_a is not None) else None
+        return (None, None, *gx, *gp)
+
+
+def hetero_gin_layer(xs, specs, params):
+    """Outputs (one per destination type, in order of first appearance) of a HeteroConv layer of GINLayers run as
+    one autograd node (_HeteroGINLayerFn).  ``xs``: node features per type index; ``params``: (eps, weight,
+    bias, prelu) per relation."""
+    require_device(*xs, what="hgin.hetero_gin_layer")
+    xs = [_rowmajor(_f32(x, "x")) for x in xs]
+    _same_dtype("hgin.hetero_gin_layer", *xs)
+    flat = []
+    for sp, (eps, w, b, a) in zip(specs, params):
+        f_src = xs[sp.src].size(1)
+        width = f_src + (xs[sp.dst].size(1) if sp.mode == COMBINE_CONCAT else 0)
+        if sp.mode == COMBINE_ADD and xs[sp.dst].size(1) != f_src:
+            raise RuntimeError(f"GINConv add: feature sizes differ ({f_src} vs {xs[sp.dst].size(1)})")
+        if w.size(1) != width:
+            raise RuntimeError(f"mat1 and mat2 shapes cannot be multiplied ({sp.graph.n_dst}x{width} and "
+                               f"{w.size(1)}x{w.size(0)})")
+        flat += [eps, _rowmajor(w), b.contiguous(), a]
+    return _HeteroGINLayerFn.apply(specs, len(xs), *xs, *flat)
 
 
 _ONE = {}

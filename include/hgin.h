@@ -168,16 +168,21 @@ int hgin_nt_planes_bf16(const uint16_t* b, int64_t ldb, int64_t N, int64_t K, vo
  * (cs = F_src for concat, 0 for add; a multiple of 4), with C as stored:
  *   g_dst[m, j] = (1 + eps[0]) * c[m, cs + j]   (g_dst may be NULL)
  *   g_eps[0]    = sum_{m, j} c[m, cs + j] * x_dst[m, j]      (fixed-order per-workgroup partials + final)
- * so g_comb is not read back.  workspace: hgin_gemm_nt_combine_workspace_size.  Deterministic. */
+ * so g_comb is not read back.  g_prev (may be NULL; may alias g_dst; row stride ld_gp): another relation's
+ * gradient of the same node type, which g_dst accumulates onto (g_dst = g_prev + (1 + eps) c, one rounding
+ * more) — autograd's gradient sum over the relations sharing x_dst, fused (hgin/ops.py hetero layer).
+ * workspace: hgin_gemm_nt_combine_workspace_size.  Deterministic. */
 int hgin_gemm_nt_combine_workspace_size(int64_t M, int64_t N, size_t* bytes);
 int hgin_gemm_nt_combine_f32(const float* a, int64_t lda, const float* b, int64_t ldb, float* c, int64_t ldc,
                              int64_t M, int64_t N, int64_t K, const float* x_dst, int64_t ld_xd, float* g_dst,
-                             int64_t ld_gd, int64_t cs, const float* eps, float* g_eps, void* workspace,
-                             size_t workspace_bytes, const void* b_planes, void* stream);
+                             int64_t ld_gd, const float* g_prev, int64_t ld_gp, int64_t cs, const float* eps,
+                             float* g_eps, void* workspace, size_t workspace_bytes, const void* b_planes,
+                             void* stream);
 int hgin_gemm_nt_combine_bf16(const uint16_t* a, int64_t lda, const uint16_t* b, int64_t ldb, uint16_t* c,
                               int64_t ldc, int64_t M, int64_t N, int64_t K, const uint16_t* x_dst, int64_t ld_xd,
-                              uint16_t* g_dst, int64_t ld_gd, int64_t cs, const float* eps, float* g_eps,
-                              void* workspace, size_t workspace_bytes, const void* b_planes, void* stream);
+                              uint16_t* g_dst, int64_t ld_gd, const uint16_t* g_prev, int64_t ld_gp, int64_t cs,
+                              const float* eps, float* g_eps, void* workspace, size_t workspace_bytes,
+                              const void* b_planes, void* stream);
 
 /* ---- weight-gradient GEMM (backward of Linear: dW = g_z^T X) ----------------------------------------
  * out[N, K] = a[M, N]^T @ [b1 | b2],  b1 = columns [0, k1) ([M, k1], ldb1), b2 = columns [k1, K) ([M, K-k1],

@@ -240,3 +240,38 @@ def test_evaluate_host_resident_call(case):
     model.train()
     with pytest.raises(RuntimeError, match="gradients enabled"):
         model(dict(x), ei, batch)
+
+
+@pytest.mark.parametrize("feat", ["f32", "bf16"])
+def test_layer_fn_equals_per_relation_autograd(feat):
+    """The one-node-per-layer backward (conv.LAYER_FN, ops._HeteroGINLayerFn: shared-node-type gradient sums
+    inside the CSC aggregate / dX epilogue) against one autograd node per relation (autograd adds them):
+    the same contributions summed in another order (autograd's input-buffer order is not the relations' reverse
+    order everywhere): fp32 within 1e-6 relative L2; bf16 within 1e-2 (the fused sum also rounds once instead of
+    twice, and later bf16 GEMMs amplify the one-ulp differences)."""
+    import dataclasses
+
+    from hgin import conv as conv_mod
+    from hgin.data import CONFIGS, scaled_config, synthetic_graph
+    cfg = dataclasses.replace(scaled_config(CONFIGS["cfg3"], 0.003, name="cfg3-small"), feat_dtype=feat)
+    g = synthetic_graph(cfg, seed=0, device=DEV)
+    res = []
+    for on in (True, False):
+        conv_mod.LAYER_FN = on
+        try:
+            torch.manual_seed(1997)
+            model = HetroGIN(**cfg.model_kwargs({"link": cfg.f_link, "path": cfg.f_path, "node": cfg.f_node})).to(DEV)
+            # gradient-carrying inputs, so every layer's input gradients (the summed ones) are exercised
+            x = {t: v.clone().requires_grad_(True) for t, v in g.x.items()}
+            _, lv = model.forward_loss(dict(x), g.edge_index_dict(), g.batch["path"], g.y)
+            torch.sqrt(lv).backward()
+            res.append([lv.detach()] + [x[t].grad for t in ("path", "link", "node")] +
+                       [p.grad for p in model.parameters()])
+        finally:
+            conv_mod.LAYER_FN = True
+    for a, b in zip(*res):
+        assert (a is None) == (b is None)
+        if a is None:
+            continue
+        rel = float((a.double() - b.double()).norm() / (b.double().norm() + 1e-30))
+        assert rel <= (1e-6 if feat == "f32" else 1e-2), rel

@@ -1,5 +1,5 @@
 #!/bin/bash
-# SQ counters for the split-mode fp32 GEMMs at the cfg2 l->p shape (one rocprofv3 --pmc pass per group).
+# SQ counters for the split-mode fp32 GEMMs (SHAPE=MxKxN, default the cfg2 l->p shape) (one rocprofv3 --pmc pass per group).
 set -u
 cd "$(dirname "$0")/.."
 OUT=gpurun_out/${TAG:-gemm_pmc}; mkdir -p $OUT; export TMPDIR=/tmp
@@ -9,6 +9,6 @@ for C in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ
          "GRBM_GUI_ACTIVE GRBM_COUNT"; do
   i=$((i+1))
   timeout -s KILL 120 rocprofv3 --pmc $C --kernel-include-regex "k_gemm" --output-format csv -d $OUT/p$i -o run -- \
-    python3 tools/gemm_bench.py --quick --shapes=600000x256x128 > $OUT/p$i.log 2>&1 || { echo "FAIL pass $i"; tail -5 $OUT/p$i.log; exit 1; }
+    python3 tools/gemm_bench.py --quick --shapes=${SHAPE:-600000x256x128} > $OUT/p$i.log 2>&1 || { echo "FAIL pass $i"; tail -5 $OUT/p$i.log; exit 1; }
 done
 echo done > $OUT/status.txt
