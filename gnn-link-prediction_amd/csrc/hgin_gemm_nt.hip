@@ -56,9 +56,10 @@ struct Src2 {
 // element is bounds-checked.
 __device__ __forceinline__ float self_scale(const float* eps2) { return eps2 ? __fadd_rn(1.0f, eps2[0]) : 1.0f; }
 
-template <bool kClean, int ROWS>
-__device__ __forceinline__ void load_tile(float4 (&r)[ROWS / 32], const Src2& s, int64_t row0, int64_t rows,
+template <bool kClean, int ROWS, int NT = 256>
+__device__ __forceinline__ void load_tile(float4 (&r)[ROWS / (NT / 8)], const Src2& s, int64_t row0, int64_t rows,
                                           int64_t k0, int64_t K, int tid, float sc2 = 1.0f) {
+  constexpr int RP = NT / 8;   // rows per pass of the workgroup's threads
   if constexpr (kClean) {
     // select between the loaded VALUES: a select between the two struct fields' addresses would make
     // the compiler copy the by-value kernel argument into scratch
@@ -69,8 +70,8 @@ __device__ __forceinline__ void load_tile(float4 (&r)[ROWS / 32], const Src2& s,
     const int64_t ld = first ? l1 : l2;
     const int64_t kk = (first ? k0 : k0 - s.k1) + (tid & 7) * 4;
 #pragma unroll
-    for (int i = 0; i < ROWS / 32; ++i) {
-      int64_t gr = row0 + (tid >> 3) + 32 * i;
+    for (int i = 0; i < ROWS / RP; ++i) {
+      int64_t gr = row0 + (tid >> 3) + RP * i;
       gr = gr < rows ? gr : rows - 1;
       const float4 v = *reinterpret_cast<const float4*>(base + gr * ld + kk);
       r[i] = v;
@@ -79,8 +80,8 @@ __device__ __forceinline__ void load_tile(float4 (&r)[ROWS / 32], const Src2& s,
   } else {
     const int64_t kk = k0 + (tid & 7) * 4;
 #pragma unroll
-    for (int i = 0; i < ROWS / 32; ++i) {
-      const int64_t gr = row0 + (tid >> 3) + 32 * i;
+    for (int i = 0; i < ROWS / RP; ++i) {
+      const int64_t gr = row0 + (tid >> 3) + RP * i;
       float t[4] = {0.f, 0.f, 0.f, 0.f};
       if (gr < rows) {
 #pragma unroll
@@ -96,18 +97,18 @@ __device__ __forceinline__ void load_tile(float4 (&r)[ROWS / 32], const Src2& s,
 
 // The eps2 scale of a clean p2 tile, applied at staging time (after the MFMAs the prefetch hides under):
 // scaling inside load_tile would consume the loaded values at once and make the loads wait there.
-template <int ROWS>
-__device__ __forceinline__ void scale_tile(float4 (&r)[ROWS / 32], float sc) {
+template <int ROWS, int NT = 256>
+__device__ __forceinline__ void scale_tile(float4 (&r)[ROWS / (NT / 8)], float sc) {
 #pragma unroll
-  for (int i = 0; i < ROWS / 32; ++i)
+  for (int i = 0; i < ROWS / (NT / 8); ++i)
     r[i] = make_float4(__fmul_rn(sc, r[i].x), __fmul_rn(sc, r[i].y), __fmul_rn(sc, r[i].z), __fmul_rn(sc, r[i].w));
 }
 
-template <int ROWS>
-__device__ __forceinline__ void store_tile(float* __restrict__ dst, const float4 (&r)[ROWS / 32], int tid) {
+template <int ROWS, int NT = 256>
+__device__ __forceinline__ void store_tile(float* __restrict__ dst, const float4 (&r)[ROWS / (NT / 8)], int tid) {
 #pragma unroll
-  for (int i = 0; i < ROWS / 32; ++i)
-    *reinterpret_cast<float4*>(dst + ((tid >> 3) + 32 * i) * kLds + (tid & 7) * 4) = r[i];
+  for (int i = 0; i < ROWS / (NT / 8); ++i)
+    *reinterpret_cast<float4*>(dst + ((tid >> 3) + (NT / 8) * i) * kLds + (tid & 7) * 4) = r[i];
 }
 
 // Split mode (hgin_common.h): the same tile written as three bf16 planes per row.  NT image: 48-word rows
@@ -120,13 +121,14 @@ __device__ __forceinline__ void store_tile(float* __restrict__ dst, const float4
 constexpr int kSplitRowWordsNT = 48;
 __device__ __forceinline__ int nt_chunk(int row, int c) { return (c ^ ((row >> 2) & 3)) << 2; }
 
-template <int ROWS>
-__device__ __forceinline__ void store_tile_split(uint32_t* __restrict__ dst, const float4 (&r)[ROWS / 32], int tid) {
+template <int ROWS, int NT = 256>
+__device__ __forceinline__ void store_tile_split(uint32_t* __restrict__ dst, const float4 (&r)[ROWS / (NT / 8)],
+                                                 int tid) {
 #pragma unroll
-  for (int i = 0; i < ROWS / 32; ++i) {
+  for (int i = 0; i < ROWS / (NT / 8); ++i) {
     uint2 o[3];
     split4(r[i], o);
-    const int rr = (tid >> 3) + 32 * i;
+    const int rr = (tid >> 3) + (NT / 8) * i;
     const int q = tid & 7;                        // float4 quad q = chunk q >> 1, half q & 1
     uint32_t* row = dst + rr * kSplitRowWordsNT + nt_chunk(rr, q >> 1) + (q & 1) * 2;
 #pragma unroll
@@ -317,21 +319,22 @@ __device__ __forceinline__ void tile_partial(float* smem, float ep, float* part,
   const int t = threadIdx.x;
   smem[t] = ep;
   __syncthreads();
-  for (int off = 128; off > 0; off >>= 1) {
+  for (int off = (int)blockDim.x / 2; off > 0; off >>= 1) {
     if (t < off) smem[t] = __fadd_rn(smem[t], smem[t + off]);
     __syncthreads();
   }
   if (t == 0) part[q] = smem[0];
 }
 
-template <int EPI, bool kClean, int TN, int WNv, bool kSplit>
-__global__ __launch_bounds__(256, 3) void k_gemm_nt(Src2 A, Src2 B, int64_t M, int64_t N, int64_t K,
+template <int EPI, bool kClean, int TN, int WNv, bool kSplit, int NW = 4>
+__global__ __launch_bounds__(NW * 64, NW == 8 ? 2 : 3) void k_gemm_nt(Src2 A, Src2 B, int64_t M, int64_t N, int64_t K,
                                                     const float* __restrict__ bias, const float* __restrict__ prelu,
                                                     const float* __restrict__ accum, float* __restrict__ Z,
                                                     float* __restrict__ Y, int64_t ldc, bool vec_out,
                                                     int64_t n_tiles, bool xcd, CombEpi ce) {
+  constexpr int NT = NW * 64;             // threads
   constexpr int WN = WNv;                 // waves along N
-  constexpr int WM = 4 / WN;              // waves along M
+  constexpr int WM = NW / WN;             // waves along M
   constexpr int BM = WM * 64;             // rows per workgroup tile
   constexpr int BN = WN * TN * 32;        // columns per workgroup tile
   constexpr int WCOLS = TN * 32;          // columns per wave
@@ -365,32 +368,32 @@ __global__ __launch_bounds__(256, 3) void k_gemm_nt(Src2 A, Src2 B, int64_t M, i
 #pragma unroll
       for (int e = 0; e < 16; ++e) acc[a][b][e] = 0.0f;
 
-  float4 ra[BM / 32], rb[BN >= 32 ? BN / 32 : 1];
+  float4 ra[BM / (NT / 8)], rb[BN >= NT / 8 ? BN / (NT / 8) : 1];
   const float sc2 = self_scale(A.eps2);
   bool scale_a = false;   // ra holds a clean p2 tile still to be scaled by sc2
   auto load_a = [&](int64_t k0) {
-    load_tile<kClean, BM>(ra, A, m0, M, k0, K, tid, sc2);
+    load_tile<kClean, BM, NT>(ra, A, m0, M, k0, K, tid, sc2);
     scale_a = kClean && A.eps2 != nullptr && k0 >= A.k1;
   };
   auto stage = [&]() {
-    if (scale_a) scale_tile<BM>(ra, sc2);
+    if (scale_a) scale_tile<BM, NT>(ra, sc2);
     if constexpr (kSplit) {
-      store_tile_split<BM>(Ash, ra, tid);
-      store_tile_split<BN>(Bsh, rb, tid);
+      store_tile_split<BM, NT>(Ash, ra, tid);
+      store_tile_split<BN, NT>(Bsh, rb, tid);
     } else {
-      store_tile<BM>(As, ra, tid);
-      store_tile<BN>(Bs, rb, tid);
+      store_tile<BM, NT>(As, ra, tid);
+      store_tile<BN, NT>(Bs, rb, tid);
     }
   };
   load_a(0);
-  load_tile<kClean, BN>(rb, B, n0, N, 0, K, tid);
+  load_tile<kClean, BN, NT>(rb, B, n0, N, 0, K, tid);
   stage();
   __syncthreads();
   for (int64_t k0 = 0; k0 < K; k0 += kBK) {
     const bool more = k0 + kBK < K;
     if (more) {   // next K-tile's global loads stay in flight under this K-tile's MFMAs
       load_a(k0 + kBK);
-      load_tile<kClean, BN>(rb, B, n0, N, k0 + kBK, K, tid);
+      load_tile<kClean, BN, NT>(rb, B, n0, N, k0 + kBK, K, tid);
     }
     __builtin_amdgcn_s_setprio(1);   // keep the MFMA cluster together (T5)
     if constexpr (kSplit) {
@@ -457,18 +460,18 @@ __global__ __launch_bounds__(256, 3) void k_gemm_nt(Src2 A, Src2 B, int64_t M, i
   if constexpr (EPI == 4) tile_partial(smem, ep, ce.part, q);
 }
 
-template <int EPI, int TN, int WN>
+template <int EPI, int TN, int WN, int NW = 4>
 int64_t launch_nt_tn(bool vec, const Src2& a, const Src2& b, int64_t M, int64_t N, int64_t K, const float* bias,
                      const float* prelu, const float* accum, float* z, float* y, int64_t ldc, bool vec_out,
                      hipStream_t s, const CombEpi& ce) {
-  constexpr int BM = (4 / WN) * 64;
+  constexpr int BM = (NW / WN) * 64;
   constexpr int BN = WN * TN * 32;
   const int64_t tiles = ceil_div(N, BN) * ceil_div(M, BM);
   const bool xcd = xcd_remap_enabled();
   dim3 grid((unsigned)(xcd ? round_up8(tiles) : tiles));
 #define HGIN_NT_F32(CLEAN, SPLIT)                                                                           \
-  k_gemm_nt<EPI, CLEAN, TN, WN, SPLIT><<<grid, 256, 0, s>>>(a, b, M, N, K, bias, prelu, accum, z, y, ldc, vec_out, \
-                                                            tiles, xcd, ce)
+  k_gemm_nt<EPI, CLEAN, TN, WN, SPLIT, NW><<<grid, NW * 64, 0, s>>>(a, b, M, N, K, bias, prelu, accum, z, y, ldc, \
+                                                                    vec_out, tiles, xcd, ce)
   if (gemm_split_enabled()) {
     if (vec) HGIN_NT_F32(true, true); else HGIN_NT_F32(false, true);
   } else {
@@ -525,6 +528,8 @@ int launch_nt(const Src2& a, const Src2& b, int64_t M, int64_t N, int64_t K, con
                        (EPI != 4 || (aligned16(ce.xd) && ce.ldxd % 4 == 0 &&
                                      (ce.gd == nullptr || (aligned16(ce.gd) && ce.ldgd % 4 == 0))));
   int64_t tiles;
+  // (an 8-wave 128 x 128 tile, 64 x 32 per wave at 4 waves / SIMD — launch_nt_tn<EPI, 1, 4, 8> — measured 5 %
+  // slower than this 4-wave tile at the cfg3 shapes: profiles/r02/gemm_pmc_cfg3.txt)
   if (N <= 32)
     tiles = launch_nt_tn<EPI, 1, 1>(vec, a, b, M, N, K, bias, prelu, accum, z, y, ldc, vec_out, s, ce);
   else if (use_bm64<EPI == 4 ? 0 : EPI>(M, N))
