@@ -41,6 +41,21 @@ int agg_u() {
   return v;
 }
 
+// Non-temporal self-term loads / output stores (the streamed-once data) so they do not evict the gathered source
+// table from L2 / the Infinity Cache.  Measured: 3-9 % faster for the concat layer at every size
+// (profiles/r01_agg_nt.txt); for the other modes 1-2 % slower at cfg2, whose tables fit in the 256 MiB Infinity
+// Cache, and 4-5 % faster at cfg3, whose tables do not (aggregate 5.48-5.57 -> 5.77 TB/s, step 212-214 -> 209.6
+// ms: profiles/r02/agg_variants_cfg3.txt).  So: concat always, the other modes once the output stream alone
+// exceeds 512 MiB (cfg2's largest is 307 MB).  HGIN_AGG_NT = 0 / 1 forces one choice.
+bool agg_nt(int combine, int64_t n_rows, int64_t out_row_bytes) {
+  static const int env = [] {
+    const char* v = getenv("HGIN_AGG_NT");
+    return v ? atoi(v) : -1;
+  }();
+  if (env >= 0) return env != 0;
+  return combine == HGIN_COMBINE_CONCAT || n_rows * out_row_bytes > (int64_t(512) << 20);
+}
+
 template <int VEC>
 struct Vec;
 // NT = true: streamed-once data (the self-term rows and the output) use non-temporal loads / stores so they
@@ -181,13 +196,7 @@ int launch_aggregate(const int32_t* rowptr, const int32_t* col, int64_t n_rows, 
   constexpr int kRowsPerWave = kWave / G;
   const int64_t waves = ceil_div(n_rows, kRowsPerWave);
   const int64_t blocks = ceil_div(waves, 256 / kWave);
-  // Non-temporal self-term loads / output stores: measured (profiles/r01_agg_nt.txt) 3-9 % faster for the
-  // concat layer, whose [N, F_src + F_dst] output is the largest stream, and 1-2 % slower otherwise.
-  static const int nt_env = [] {
-    const char* v = getenv("HGIN_AGG_NT");
-    return v ? atoi(v) : -1;
-  }();
-  const bool nt = nt_env >= 0 ? nt_env != 0 : combine == HGIN_COMBINE_CONCAT;
+  const bool nt = agg_nt(combine, n_rows, (int64_t)(f_src + (combine == HGIN_COMBINE_CONCAT ? f_dst : 0)) * 4);
 #define HGIN_AGG_L(UV, NTV, TAIL)                                                                           \
   k_aggregate<VEC, G, UV, NTV, TAIL><<<dim3((unsigned)blocks), 256, 0, s>>>(rowptr, col, n_rows, x_src, ld_src, \
                                                                            f_src, x_dst, ld_dst, f_dst, eps,     \
@@ -353,7 +362,7 @@ int launch_aggregate_bf16(const int32_t* rowptr, const int32_t* col, int64_t n_r
   k_aggregate_bf16<VEC, G, UV, NTV, TAIL><<<dim3((unsigned)blocks), 256, 0, s>>>( \
       rowptr, col, n_rows, x_src, ld_src, f_src, x_dst, ld_dst, f_dst, eps, combine, out, ld_out)
   const bool tail = agg_tail_batched();
-  const bool nt = combine == HGIN_COMBINE_CONCAT;
+  const bool nt = agg_nt(combine, n_rows, (int64_t)(f_src + (combine == HGIN_COMBINE_CONCAT ? f_dst : 0)) * 2);
   if (agg_u() == 16 && tail) { if (nt) HGIN_AGGB_L(16, true, true); else HGIN_AGGB_L(16, false, true); }
   else if (nt) { if (tail) HGIN_AGGB_L(8, true, true); else HGIN_AGGB_L(8, true, false); }
   else { if (tail) HGIN_AGGB_L(8, false, true); else HGIN_AGGB_L(8, false, false); }
@@ -556,7 +565,7 @@ int launch_agg_q(int lanes_needed, const int32_t* rowptr, const int32_t* col, in
                  int64_t ld_src, int f_src, const T* x_dst, int64_t ld_dst, int f_dst, const float* eps, int combine,
                  T* out, int64_t ld_out, hipStream_t s, const char* what) {
   constexpr int kU = NQ >= 4 ? 4 : 8;
-  const bool nt = combine == HGIN_COMBINE_CONCAT;
+  const bool nt = agg_nt(combine, n_rows, (int64_t)(f_src + (combine == HGIN_COMBINE_CONCAT ? f_dst : 0)) * (int64_t)sizeof(T));
   const bool tail = agg_tail_batched();
 #define HGIN_AGGQ_L(GV, NTV, TAIL, BLOCKS)                                                                      \
   k_agg_q<T, NQ, GV, kU, NTV, TAIL><<<dim3((unsigned)(BLOCKS)), 256, 0, s>>>(rowptr, col, n_rows, x_src, ld_src, \
@@ -741,7 +750,7 @@ int try_agg_pipe(const int32_t* rowptr, const int32_t* col, int64_t n_rows, cons
   const int widest = f_src > fd ? f_src : fd;
   const int lanes = (widest + E - 1) / E;
   if (lanes < 1 || lanes > kWave) return -1000;
-  const bool nt = combine == HGIN_COMBINE_CONCAT;
+  const bool nt = agg_nt(combine, n_rows, (int64_t)(f_src + (combine == HGIN_COMBINE_CONCAT ? f_dst : 0)) * (int64_t)sizeof(T));
   int rc;
 #define HGIN_PIPE_G(GV, UV)                                                                                      \
   rc = nt ? launch_agg_pipe_g<T, GV, UV, true>(rowptr, col, n_rows, x_src, ld_src, f_src, x_dst, ld_dst, f_dst, eps, \

@@ -4,7 +4,8 @@ fixtures (tests/variant_child.py), so the non-default paths pytest's own process
   * HGIN_F32_GEMM=mfma32    — the exact-f32 MFMA GEMM (v_mfma_f32_32x32x2_f32) instead of the 3-way bf16 split:
                               fixture tolerances (1e-5 outputs, 1e-4 gradients);
   * HGIN_SLAB_REDUCE=2pass  — the two-launch weight-gradient slab sum: bit-identical to the one-launch default;
-  * HGIN_AGG_NQ=2 / HGIN_AGG_PIPE=1 / HGIN_AGG_TAIL=0 — aggregate lane-width / pipelined / tail variants:
+  * HGIN_AGG_NQ=2 / HGIN_AGG_PIPE=1 / HGIN_AGG_TAIL=0 / HGIN_AGG_NT=1 — aggregate lane-width / pipelined / tail /
+                              non-temporal-stream variants:
                               bit-identical to the default (every variant sums each row in edge order);
   * HGIN_XCD=0              — GEMM tiles in plain order instead of XCD-contiguous: bit-identical;
   * HGIN_NT2=1              — the LDS-DMA NT GEMM (k_nt2) instead of the register-staged one: bit-identical.
@@ -31,8 +32,9 @@ VARIANTS = {
     "agg_notail": {"HGIN_AGG_TAIL": "0"},
     "xcd_off": {"HGIN_XCD": "0"},
     "nt2_on": {"HGIN_NT2": "1"},
+    "agg_nt_all": {"HGIN_AGG_NT": "1"},
 }
-BITWISE_EQUAL_TO_DEFAULT = ("slab2pass", "agg_nq2", "agg_pipe", "agg_notail", "xcd_off", "nt2_on")
+BITWISE_EQUAL_TO_DEFAULT = ("slab2pass", "agg_nq2", "agg_pipe", "agg_notail", "xcd_off", "nt2_on", "agg_nt_all")
 
 _results = {}
 
