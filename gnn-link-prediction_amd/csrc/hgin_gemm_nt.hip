@@ -156,6 +156,18 @@ struct Out4<float> {
     if (full) *reinterpret_cast<float4*>(p) = make_float4(o[0], o[1], o[2], o[3]);
     else for (int t = 0; t < nv; ++t) p[t] = o[t];
   }
+  // non-temporal forms (streamed-once outputs / epilogue inputs)
+  static __device__ __forceinline__ void st_nt(float* p, const float (&o)[4], bool full, int nv) {
+    using f4v = __attribute__((ext_vector_type(4))) float;
+    if (full) __builtin_nontemporal_store(f4v{o[0], o[1], o[2], o[3]}, reinterpret_cast<f4v*>(p));
+    else for (int t = 0; t < nv; ++t) __builtin_nontemporal_store(o[t], p + t);
+  }
+  static __device__ __forceinline__ raw ld_raw_nt(const float* p, bool full, int nv) {
+    using f4v = __attribute__((ext_vector_type(4))) float;
+    if (!full) return ld_raw(p, full, nv);
+    const f4v v = __builtin_nontemporal_load(reinterpret_cast<const f4v*>(p));
+    return make_float4(v.x, v.y, v.z, v.w);
+  }
   static __device__ __forceinline__ void ld(const float* p, float (&o)[4], bool full, int nv) {
     if (full) {
       const float4 v = *reinterpret_cast<const float4*>(p);
@@ -181,6 +193,17 @@ struct Out4<uint16_t> {
   static __device__ __forceinline__ void st(uint16_t* p, const float (&o)[4], bool full, int nv) {
     if (full) *reinterpret_cast<uint2*>(p) = make_uint2(pack_bf2(o[0], o[1]), pack_bf2(o[2], o[3]));
     else for (int t = 0; t < nv; ++t) p[t] = (uint16_t)f2bf(o[t]);
+  }
+  static __device__ __forceinline__ void st_nt(uint16_t* p, const float (&o)[4], bool full, int nv) {
+    using u2v = __attribute__((ext_vector_type(2))) unsigned int;
+    if (full) __builtin_nontemporal_store(u2v{pack_bf2(o[0], o[1]), pack_bf2(o[2], o[3])}, reinterpret_cast<u2v*>(p));
+    else st(p, o, full, nv);
+  }
+  static __device__ __forceinline__ raw ld_raw_nt(const uint16_t* p, bool full, int nv) {
+    using u2v = __attribute__((ext_vector_type(2))) unsigned int;
+    if (!full) return ld_raw(p, full, nv);
+    const u2v v = __builtin_nontemporal_load(reinterpret_cast<const u2v*>(p));
+    return make_uint2(v.x, v.y);
   }
   static __device__ __forceinline__ void ld(const uint16_t* p, float (&o)[4], bool full, int nv) {
     if (full) {
@@ -208,6 +231,7 @@ struct CombEpi {
   float* part;        // [workgroup tiles] eps-gradient partials
   const void* gp = nullptr;   // optional: a gradient g_x_dst accumulates onto (may alias gd), row stride ldgp
   int64_t ldgp = 0;
+  bool nt_io = false;         // non-temporal epilogue streams (outputs, accum / x_dst / g_prev rows)
 };
 
 // Epilogue shared by the fp32 and bf16 kernels.  Per 32-row half (tm) each wave parks its 32 x WCOLS
@@ -254,11 +278,17 @@ __device__ __forceinline__ void epilogue(const f32x16 (&acc)[2][TN], float* smem
     for (int j = 0; j < kJ; ++j) {   // accum (EPI 1) / x_dst, g_prev (EPI 4) rows: loaded before the LDS round trip
       acc_raw[j] = {};
       const int64_t row = m0 + wm * 64 + tm * 32 + r0 + kRS * j;
-      if (EPI == 1 && accum && row < M && nv) acc_raw[j] = Out4<OutT>::ld_raw(accum + row * ldc + col, full, nv);
-      if (EPI == 4 && self_cols && row < M) acc_raw[j] = Out4<OutT>::ld_raw(xd + row * ce.ldxd + (col - ce.cs), full, nv);
+      if (EPI == 1 && accum && row < M && nv)
+        acc_raw[j] = ce.nt_io ? Out4<OutT>::ld_raw_nt(accum + row * ldc + col, full, nv)
+                              : Out4<OutT>::ld_raw(accum + row * ldc + col, full, nv);
+      if (EPI == 4 && self_cols && row < M)
+        acc_raw[j] = ce.nt_io ? Out4<OutT>::ld_raw_nt(xd + row * ce.ldxd + (col - ce.cs), full, nv)
+                              : Out4<OutT>::ld_raw(xd + row * ce.ldxd + (col - ce.cs), full, nv);
       if constexpr (EPI == 4) {
         prev_raw[j] = {};
-        if (gp && gd && self_cols && row < M) prev_raw[j] = Out4<OutT>::ld_raw(gp + row * ce.ldgp + (col - ce.cs), full, nv);
+        if (gp && gd && self_cols && row < M)
+          prev_raw[j] = ce.nt_io ? Out4<OutT>::ld_raw_nt(gp + row * ce.ldgp + (col - ce.cs), full, nv)
+                                 : Out4<OutT>::ld_raw(gp + row * ce.ldgp + (col - ce.cs), full, nv);
       }
     }
 #pragma unroll
@@ -286,8 +316,13 @@ __device__ __forceinline__ void epilogue(const f32x16 (&acc)[2][TN], float* smem
           o[t] = accum ? __fadd_rn(acc_in[t], y) : y;
         }
       }
-      Out4<OutT>::st(Y + row * ldc + col, o, full, nv);
-      if (EPI == 1 && Z) Out4<OutT>::st(Z + row * ldc + col, zz, full, nv);
+      if (ce.nt_io) {
+        Out4<OutT>::st_nt(Y + row * ldc + col, o, full, nv);
+        if (EPI == 1 && Z) Out4<OutT>::st_nt(Z + row * ldc + col, zz, full, nv);
+      } else {
+        Out4<OutT>::st(Y + row * ldc + col, o, full, nv);
+        if (EPI == 1 && Z) Out4<OutT>::st(Z + row * ldc + col, zz, full, nv);
+      }
       if (EPI == 4 && self_cols) {
         float c4[4], x4[4], g4[4], p4[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -303,7 +338,10 @@ __device__ __forceinline__ void epilogue(const f32x16 (&acc)[2][TN], float* smem
           g4[t] = __fmul_rn(sc_self, c4[t]);
           if (gp) g4[t] = __fadd_rn(p4[t], g4[t]);   // accumulate onto another relation's g_x_dst
         }
-        if (gd) Out4<OutT>::st(gd + row * ce.ldgd + sc, g4, full, nv);
+        if (gd) {
+          if (ce.nt_io) Out4<OutT>::st_nt(gd + row * ce.ldgd + sc, g4, full, nv);
+          else Out4<OutT>::st(gd + row * ce.ldgd + sc, g4, full, nv);
+        }
       }
     }
     if (tm == 0) __syncthreads();
@@ -517,10 +555,23 @@ bool use_bm64(int64_t M, int64_t N) {
   return t64 < t128;
 }
 
+// Non-temporal epilogue streams (HGIN_GEMM_NT_IO = 0 / 1 forces; default: once the output stream exceeds
+// 512 MiB, as the aggregate's streams — outputs read back only by later kernels, far beyond the caches).
+bool gemm_nt_io(int64_t M, int64_t N, int64_t elem) {
+  static const int env = [] {
+    const char* v = getenv("HGIN_GEMM_NT_IO");
+    return v ? atoi(v) : -1;
+  }();
+  if (env >= 0) return env != 0;
+  return M * N * elem > (int64_t(512) << 20);
+}
+
 template <int EPI>
 int launch_nt(const Src2& a, const Src2& b, int64_t M, int64_t N, int64_t K, const float* bias, const float* prelu,
               const float* accum, float* z, float* y, int64_t ldc, hipStream_t s, const char* what,
-              const CombEpi& ce = CombEpi{}, int64_t* tiles_out = nullptr) {
+              const CombEpi& ce_in = CombEpi{}, int64_t* tiles_out = nullptr) {
+  CombEpi ce = ce_in;
+  ce.nt_io = gemm_nt_io(M, N, 4);
   const bool vec = K % kBK == 0 && a.k1 % kBK == 0 && aligned16(a.p1) && a.ld1 % 4 == 0 &&
                    (a.k1 == K || (aligned16(a.p2) && a.ld2 % 4 == 0)) && aligned16(b.p1) && b.ld1 % 4 == 0;
   const bool vec_out = ldc % 4 == 0 && aligned16(y) && (z == nullptr || aligned16(z)) &&
@@ -738,7 +789,9 @@ bool use_bm64_bf16(int64_t M, int64_t N) {
 template <int EPI, typename OutT>
 int launch_nt_bf16(const Src2h& a, const Src2h& b, int64_t M, int64_t N, int64_t K, const float* bias,
                    const float* prelu, const OutT* accum, OutT* z, OutT* y, int64_t ldc, hipStream_t s,
-                   const char* what, const CombEpi& ce = CombEpi{}, int64_t* tiles_out = nullptr) {
+                   const char* what, const CombEpi& ce_in = CombEpi{}, int64_t* tiles_out = nullptr) {
+  CombEpi ce = ce_in;
+  ce.nt_io = gemm_nt_io(M, N, (int64_t)sizeof(OutT));
   const bool vec = K % kBKh == 0 && a.k1 % kBKh == 0 && aligned16(a.p1) && a.ld1 % 8 == 0 &&
                    (a.k1 == K || (aligned16(a.p2) && a.ld2 % 8 == 0)) && aligned16(b.p1) && b.ld1 % 8 == 0;
   const bool vec_out = ldc % 4 == 0 && aligned16(y) && (z == nullptr || aligned16(z)) &&

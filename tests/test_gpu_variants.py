@@ -8,7 +8,8 @@ fixtures (tests/variant_child.py), so the non-default paths pytest's own process
                               non-temporal-stream variants:
                               bit-identical to the default (every variant sums each row in edge order);
   * HGIN_XCD=0              — GEMM tiles in plain order instead of XCD-contiguous: bit-identical;
-  * HGIN_NT2=1              — the LDS-DMA NT GEMM (k_nt2) instead of the register-staged one: bit-identical.
+  * HGIN_NT2=1              — the LDS-DMA NT GEMM (k_nt2) instead of the register-staged one: bit-identical;
+  * HGIN_GEMM_NT_IO=1       — non-temporal GEMM epilogue streams at every size (default: > 512 MiB): bit-identical.
 
 Each child is a separate interpreter started with subprocess (never an exec of this process).
 """
@@ -33,8 +34,9 @@ VARIANTS = {
     "xcd_off": {"HGIN_XCD": "0"},
     "nt2_on": {"HGIN_NT2": "1"},
     "agg_nt_all": {"HGIN_AGG_NT": "1"},
+    "gemm_nt_io": {"HGIN_GEMM_NT_IO": "1"},
 }
-BITWISE_EQUAL_TO_DEFAULT = ("slab2pass", "agg_nq2", "agg_pipe", "agg_notail", "xcd_off", "nt2_on", "agg_nt_all")
+BITWISE_EQUAL_TO_DEFAULT = ("slab2pass", "agg_nq2", "agg_pipe", "agg_notail", "xcd_off", "nt2_on", "agg_nt_all", "gemm_nt_io")
 
 _results = {}
 
