@@ -28,6 +28,8 @@
 // persistent grid with cross-tile prefetch was 5 % slower (it needs 2 waves/SIMD).
 #include "hgin_common.h"
 
+#include <type_traits>
+
 namespace hgin {
 namespace {
 
@@ -607,8 +609,33 @@ int check_a(const char* what, const float* a1, int64_t lda1, int64_t k1, const f
 // At the GIN shapes (K = 128..512, N = 128..256) these GEMMs are HBM-bound (A read once, Y/Z written
 // once: ~43 flop/B at K = 256, N = 128, far below the bf16 MFMA ridge), so the tile keeps the whole of N
 // per workgroup where it can and the epilogue writes 8-B bf16 quads.
+// LDS-DMA (global_load_lds_dwordx4: 64 lanes x 16 B into 1 KiB at a wave-uniform LDS address) and counted
+// vector-memory waits, shared by k_ws_bf16 and k_nt2.
+typedef __attribute__((address_space(3))) void lds_void_t;
+typedef __attribute__((address_space(1))) void glb_void_t;
+
+__device__ __forceinline__ void glds16(const void* g, void* lds_wave_base) {
+  __builtin_amdgcn_global_load_lds((glb_void_t*)g, (lds_void_t*)lds_wave_base, 16, 0, 0);
+}
+
+// The same DMA issued from inline asm: the compiler does not see it, so it does not guard the kernel's later
+// LDS reads with a vmcnt(0) of its own (which would drain the whole ring); the kernel's counted waits do.
+template <bool kNt = false>
+__device__ __forceinline__ void glds16_asm(const void* g, void* lds_wave_base) {
+  const uint32_t m0 = __builtin_amdgcn_readfirstlane(
+      (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)(lds_wave_base));
+  if constexpr (kNt)
+    asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off nt" ::"v"(g), "s"(m0) : "memory", "m0");
+  else
+    asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(g), "s"(m0) : "memory", "m0");
+}
+
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
 constexpr int kBKh = 64;
-constexpr int kLdsH = kBKh + 8;
 
 struct Src2h {
   const uint16_t* p1;
@@ -624,9 +651,18 @@ __device__ __forceinline__ uint32_t scale_bf2(uint32_t w, float sc) {
   return pack_bf2(__fmul_rn(sc, bf_lo(w)), __fmul_rn(sc, bf_hi(w)));
 }
 
-template <bool kClean, int ROWS>
-__device__ __forceinline__ void load_tile_h(uint4 (&r)[ROWS / 32], const Src2h& s, int64_t row0, int64_t rows,
-                                            int64_t k0, int64_t K, int tid, float sc2 = 1.0f) {
+// A K-tile of BKH bf16 per row: BKH / 8 threads per row (16 B each), 256 / (BKH / 8) rows per pass.
+template <int BKH>
+struct TileH {
+  static constexpr int kTpr = BKH / 8;        // threads per row
+  static constexpr int kRp = 256 / kTpr;      // rows per pass
+  static constexpr int kLd = BKH + 8;         // LDS row stride (bf16): 144 B / 272 B, both conflict-free
+};
+
+template <bool kClean, int ROWS, int BKH = kBKh>
+__device__ __forceinline__ void load_tile_h(uint4 (&r)[ROWS / TileH<BKH>::kRp], const Src2h& s, int64_t row0,
+                                            int64_t rows, int64_t k0, int64_t K, int tid, float sc2 = 1.0f) {
+  constexpr int TPR = TileH<BKH>::kTpr, RP = TileH<BKH>::kRp;
   if constexpr (kClean) {
     // select between the loaded VALUES: a select between the two struct fields' addresses would make
     // the compiler copy the by-value kernel argument into scratch
@@ -635,20 +671,20 @@ __device__ __forceinline__ void load_tile_h(uint4 (&r)[ROWS / 32], const Src2h& 
     const int64_t l1 = s.ld1, l2 = s.ld2;
     const uint16_t* base = reinterpret_cast<const uint16_t*>(first ? u1 : u2);
     const int64_t ld = first ? l1 : l2;
-    const int64_t kk = (first ? k0 : k0 - s.k1) + (tid & 7) * 8;
+    const int64_t kk = (first ? k0 : k0 - s.k1) + (tid % TPR) * 8;
 #pragma unroll
-    for (int i = 0; i < ROWS / 32; ++i) {
-      int64_t gr = row0 + (tid >> 3) + 32 * i;
+    for (int i = 0; i < ROWS / RP; ++i) {
+      int64_t gr = row0 + (tid / TPR) + RP * i;
       gr = gr < rows ? gr : rows - 1;
       const uint4 v = *reinterpret_cast<const uint4*>(base + gr * ld + kk);
       r[i] = v;
     }
     // (eps2 scaling of a clean p2 tile is applied when the tile is staged: scale_tile_h)
   } else {
-    const int64_t kk = k0 + (tid & 7) * 8;
+    const int64_t kk = k0 + (tid % TPR) * 8;
 #pragma unroll
-    for (int i = 0; i < ROWS / 32; ++i) {
-      const int64_t gr = row0 + (tid >> 3) + 32 * i;
+    for (int i = 0; i < ROWS / RP; ++i) {
+      const int64_t gr = row0 + (tid / TPR) + RP * i;
       uint32_t t[8] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
       if (gr < rows) {
 #pragma unroll
@@ -665,15 +701,17 @@ __device__ __forceinline__ void load_tile_h(uint4 (&r)[ROWS / 32], const Src2h& 
   }
 }
 
-template <int ROWS>
-__device__ __forceinline__ void store_tile_h(uint16_t* __restrict__ dst, const uint4 (&r)[ROWS / 32], int tid) {
+template <int ROWS, int BKH = kBKh>
+__device__ __forceinline__ void store_tile_h(uint16_t* __restrict__ dst, const uint4 (&r)[ROWS / TileH<BKH>::kRp],
+                                             int tid) {
+  constexpr int TPR = TileH<BKH>::kTpr, RP = TileH<BKH>::kRp, LD = TileH<BKH>::kLd;
 #pragma unroll
-  for (int i = 0; i < ROWS / 32; ++i)
-    *reinterpret_cast<uint4*>(dst + ((tid >> 3) + 32 * i) * kLdsH + (tid & 7) * 8) = r[i];
+  for (int i = 0; i < ROWS / RP; ++i)
+    *reinterpret_cast<uint4*>(dst + ((tid / TPR) + RP * i) * LD + (tid % TPR) * 8) = r[i];
 }
 
-template <int EPI, bool kClean, int TN, int WNv, typename OutT>
-__global__ __launch_bounds__(256, 3) void k_gemm_nt_bf16(Src2h A, Src2h B, int64_t M, int64_t N, int64_t K,
+template <int EPI, bool kClean, int TN, int WNv, typename OutT, int BKH = kBKh>
+__global__ __launch_bounds__(256, BKH == 64 ? 3 : 2) void k_gemm_nt_bf16(Src2h A, Src2h B, int64_t M, int64_t N, int64_t K,
                                                          const float* __restrict__ bias,
                                                          const float* __restrict__ prelu,
                                                          const OutT* __restrict__ accum, OutT* __restrict__ Z,
@@ -684,11 +722,13 @@ __global__ __launch_bounds__(256, 3) void k_gemm_nt_bf16(Src2h A, Src2h B, int64
   constexpr int BM = WM * 64;
   constexpr int BN = WN * TN * 32;
   constexpr int WCOLS = TN * 32;
-  constexpr int kTileBytes = (BM + BN) * kLdsH * 2;
+  constexpr int LDH = TileH<BKH>::kLd;
+  constexpr int RPH = TileH<BKH>::kRp;
+  constexpr int kTileBytes = (BM + BN) * LDH * 2;
   constexpr int kEpiBytes = 4 * 32 * (WCOLS + 4) * 4;
   __shared__ __attribute__((aligned(16))) float smem[(kTileBytes > kEpiBytes ? kTileBytes : kEpiBytes) / 4];
   uint16_t* As = reinterpret_cast<uint16_t*>(smem);
-  uint16_t* Bs = As + BM * kLdsH;
+  uint16_t* Bs = As + BM * LDH;
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = tid >> 6;
@@ -710,43 +750,43 @@ __global__ __launch_bounds__(256, 3) void k_gemm_nt_bf16(Src2h A, Src2h B, int64
 #pragma unroll
       for (int e = 0; e < 16; ++e) acc[a][b][e] = 0.0f;
 
-  uint4 ra[BM / 32], rb[BN >= 32 ? BN / 32 : 1];
+  uint4 ra[BM / RPH], rb[BN >= RPH ? BN / RPH : 1];
   const float sc2 = self_scale(A.eps2);
   bool scale_a = false;   // ra holds a clean p2 tile still to be scaled (at staging time, as the fp32 kernel)
   auto load_a = [&](int64_t k0) {
-    load_tile_h<kClean, BM>(ra, A, m0, M, k0, K, tid, sc2);
+    load_tile_h<kClean, BM, BKH>(ra, A, m0, M, k0, K, tid, sc2);
     scale_a = kClean && A.eps2 != nullptr && k0 >= A.k1;
   };
   auto scale_a_tile = [&]() {
     if (scale_a) {
 #pragma unroll
-      for (int i = 0; i < BM / 32; ++i)
+      for (int i = 0; i < BM / RPH; ++i)
         ra[i] = make_uint4(scale_bf2(ra[i].x, sc2), scale_bf2(ra[i].y, sc2), scale_bf2(ra[i].z, sc2),
                            scale_bf2(ra[i].w, sc2));
     }
   };
   load_a(0);
-  load_tile_h<kClean, BN>(rb, B, n0, N, 0, K, tid);
+  load_tile_h<kClean, BN, BKH>(rb, B, n0, N, 0, K, tid);
   scale_a_tile();
-  store_tile_h<BM>(As, ra, tid);
-  store_tile_h<BN>(Bs, rb, tid);
+  store_tile_h<BM, BKH>(As, ra, tid);
+  store_tile_h<BN, BKH>(Bs, rb, tid);
   __syncthreads();
-  for (int64_t k0 = 0; k0 < K; k0 += kBKh) {
-    const bool more = k0 + kBKh < K;
+  for (int64_t k0 = 0; k0 < K; k0 += BKH) {
+    const bool more = k0 + BKH < K;
     if (more) {
-      load_a(k0 + kBKh);
-      load_tile_h<kClean, BN>(rb, B, n0, N, k0 + kBKh, K, tid);
+      load_a(k0 + BKH);
+      load_tile_h<kClean, BN, BKH>(rb, B, n0, N, k0 + BKH, K, tid);
     }
     __builtin_amdgcn_s_setprio(1);   // keep the MFMA cluster together (T5)
 #pragma unroll
-    for (int c = 0; c < kBKh / 16; ++c) {
+    for (int c = 0; c < BKH / 16; ++c) {
       bf16x8 fa[2], fb[TN];
 #pragma unroll
       for (int t = 0; t < 2; ++t)
-        fa[t] = *reinterpret_cast<const bf16x8*>(As + (wm * 64 + t * 32 + li) * kLdsH + c * 16 + lh * 8);
+        fa[t] = *reinterpret_cast<const bf16x8*>(As + (wm * 64 + t * 32 + li) * LDH + c * 16 + lh * 8);
 #pragma unroll
       for (int t = 0; t < TN; ++t)
-        fb[t] = *reinterpret_cast<const bf16x8*>(Bs + (wn * WCOLS + t * 32 + li) * kLdsH + c * 16 + lh * 8);
+        fb[t] = *reinterpret_cast<const bf16x8*>(Bs + (wn * WCOLS + t * 32 + li) * LDH + c * 16 + lh * 8);
 #pragma unroll
       for (int tm = 0; tm < 2; ++tm)
 #pragma unroll
@@ -757,8 +797,8 @@ __global__ __launch_bounds__(256, 3) void k_gemm_nt_bf16(Src2h A, Src2h B, int64
     if (more) {
       __syncthreads();
       scale_a_tile();
-      store_tile_h<BM>(As, ra, tid);
-      store_tile_h<BN>(Bs, rb, tid);
+      store_tile_h<BM, BKH>(As, ra, tid);
+      store_tile_h<BN, BKH>(Bs, rb, tid);
       __syncthreads();
     }
   }
@@ -786,18 +826,333 @@ bool use_bm64_bf16(int64_t M, int64_t N) {
   return t64 < t128;
 }
 
+// ---------------------------------------------------------------------------------------------------
+// k_ws_bf16 — weight-stationary streaming form of the bf16 NT GEMM for the GIN MLP shapes (K = 128 / 256 /
+// 512, N = 128 / 256: the layer GEMMs of cfg5).  These GEMMs are HBM-bound (A read once, z / y written,
+// accum read: ~200 flop/B at K = 512), and the tiled kernel above streams A twice per row block (two 128-col
+// tiles, the second from L2) with one register-staged K-tile in flight per workgroup: ~4 TB/s.  Here:
+//   * one persistent workgroup per CU, N / 32 waves; wave w keeps W[32 w .. 32 w + 31][0 .. K) in registers
+//     as its MFMA B fragments for the whole launch (K / 16 x 16 B per lane: 128 VGPRs at K = 512), so W is
+//     read once per CU and A exactly once from HBM;
+//   * the A rows of a 32-row block (64 at K = 128) and the block's accum rows stream HBM -> LDS with
+//     global_load_lds_dwordx4 into an NST-deep ring (NST - 1 blocks in flight while one is computed), with
+//     counted vmcnt waits and raw s_barriers: the loop has no VGPR-destination global load, so nothing in it
+//     makes the compiler drain the ring (cdna_hip_programming.md §5, "Pipelining across barriers");
+//   * every wave multiplies the whole block by its W slice (v_mfma_f32_32x32x16_bf16, the per-accumulator
+//     k order of k_gemm_nt_bf16: bit-identical results), then the fp32 results are staged 16 rows at a time
+//     through the block's dead A image and written as row-contiguous 8-B bf16 quads (bias, PReLU, accum from
+//     the LDS copy), the same epilogue arithmetic as epilogue<1 / 2>.
+// LDS images (16-B chunks): A row r of the block at r * 2K bytes, logical chunk c stored at slot c ^ (r & 15)
+// (the DMA lanes fetch pre-swizzled sources; a ds_read_b128 group of 16 rows hits 16 distinct bank slots);
+// accum rows linear; fp32 staging [16][N] with column bit 5 flipped on rows with bit 2 set (the two lane halves
+// of an accumulator store hit opposite bank halves).
+template <int K, int N>
+struct WsCfg {
+  static constexpr int NW = N / 32;                     // waves (one 32-column W slice each)
+  static constexpr int NT = NW * 64;
+  static constexpr int KS = K / 16;                     // MFMA k-steps
+  static constexpr int BM = K >= 256 ? 32 : 64;         // rows per block (A image >= 16 KB: the staging area)
+  static constexpr int TM = BM / 32;
+  static constexpr int ROWB = K * 2;
+  static constexpr int A_BYTES = BM * ROWB;
+  static constexpr int C_BYTES = BM * N * 2;
+  static constexpr int SLOT_A = A_BYTES;                // accum image follows the A image in a slot
+  static constexpr int PA = A_BYTES / 1024 / NW;        // DMA pieces per wave per block
+  static constexpr int PC = C_BYTES / 1024 / NW;
+  static_assert(A_BYTES % (1024 * NW) == 0 && C_BYTES % (1024 * NW) == 0, "DMA pieces");
+  static_assert(16 * N * 4 <= A_BYTES, "staging fits the A image");
+};
+
+template <int K, int N, bool kAcc>
+struct WsRing {
+  static constexpr int SLOT = WsCfg<K, N>::A_BYTES + (kAcc ? WsCfg<K, N>::C_BYTES : 0);
+  static constexpr int NST = SLOT * 4 <= 147456 ? 4 : 3;
+  static constexpr int BYTES = SLOT * NST;
+};
+
+template <int K, int N, int EPI, bool kAcc, bool kZ>
+__global__ __launch_bounds__((WsCfg<K, N>::NT), 1) void k_ws_bf16(
+    const uint16_t* __restrict__ a1, int64_t lda1, const uint16_t* __restrict__ a2, int64_t lda2, int64_t k1,
+    const uint16_t* __restrict__ W, const float* __restrict__ bias,
+    const float* __restrict__ prelu, const uint16_t* __restrict__ accum, uint16_t* __restrict__ Z,
+    uint16_t* __restrict__ Y, int64_t M, bool nt_io, bool nt_in) {
+  using C = WsCfg<K, N>;
+  using R = WsRing<K, N, kAcc>;
+  constexpr int NST = R::NST;
+  constexpr int P = C::PA + (kAcc ? C::PC : 0);                  // DMA instructions per wave per block
+  constexpr int S = C::TM * 4 * (kZ ? 2 : 1);                    // stores per lane per block
+  constexpr int QPR = N / 4;                                     // 4-column groups per row
+  constexpr int kWaitSteady = (NST - 2) * P + (NST - 1) * S < 63 ? (NST - 2) * P + (NST - 1) * S : 63;
+  constexpr int kWaitEarly = (NST - 2) * P < 63 ? (NST - 2) * P : 63;
+  extern __shared__ __attribute__((aligned(16))) char ws_smem[];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int li = lane & 31;
+  const int lh = lane >> 5;
+  const int64_t nblk = (M + C::BM - 1) / C::BM;
+  const int64_t G = gridDim.x;
+  if ((int64_t)blockIdx.x >= nblk) return;
+  const int64_t my = (nblk - 1 - blockIdx.x) / G + 1;             // blocks blockIdx.x + i G, i < my
+
+  // this wave's W slice as B fragments: lane (li, lh) holds W[32 wave + li][16 t + 8 lh .. + 7]
+  uint4 wf[C::KS];
+  {
+    const uint16_t* wr = W + (int64_t)(wave * 32 + li) * K + lh * 8;
+#pragma unroll
+    for (int t = 0; t < C::KS; ++t) wf[t] = *reinterpret_cast<const uint4*>(wr + t * 16);
+  }
+  // row-pass columns of this thread (fixed), bias, PReLU slope, eps scale
+  const int cq = (tid % QPR) * 4;
+  const int rq = tid / QPR;                                      // row within an 8-row pass
+  float bcol[4] = {0.f, 0.f, 0.f, 0.f};
+  if (EPI == 1 || EPI == 2) {
+#pragma unroll
+    for (int t = 0; t < 4; ++t) bcol[t] = bias[cq + t];
+  }
+  const float a_slope = EPI == 1 ? prelu[0] : 0.0f;
+  // consume the prologue loads here, so that the compiler's own wait for them sits before the ring starts and
+  // not inside the loop (where it would count the ring's DMAs)
+#pragma unroll
+  for (int t = 0; t < C::KS; ++t) asm volatile("" ::"v"(wf[t].x), "v"(wf[t].y), "v"(wf[t].z), "v"(wf[t].w));
+#pragma unroll
+  for (int t = 0; t < 4; ++t) asm volatile("" ::"v"(bcol[t]));
+
+  auto issue = [&](int64_t i) {
+    char* base = ws_smem + (int)(i % NST) * R::SLOT;
+    const int64_t r0 = ((int64_t)blockIdx.x + i * G) * C::BM;
+#pragma unroll
+    for (int p = 0; p < C::PA; ++p) {
+      const int piece = wave * C::PA + p;
+      const int off = piece * 1024 + lane * 16;
+      const int r = off / C::ROWB;
+      const int c = ((off % C::ROWB) >> 4) ^ (r & 15);           // logical chunk stored at this slot
+      int64_t gr = r0 + r;
+      gr = gr < M ? gr : M - 1;                                   // clamped rows are never stored
+      const int64_t k = (int64_t)c * 8;
+      const uint16_t* src = k < k1 ? a1 + gr * lda1 + k : a2 + gr * lda2 + (k - k1);
+      if (nt_in) glds16_asm<true>(src, base + piece * 1024); else glds16_asm(src, base + piece * 1024);
+    }
+    if constexpr (kAcc) {
+#pragma unroll
+      for (int p = 0; p < C::PC; ++p) {
+        const int piece = wave * C::PC + p;
+        const int off = piece * 1024 + lane * 16;
+        int64_t gr = r0 + off / (N * 2);
+        gr = gr < M ? gr : M - 1;
+        const uint16_t* src = accum + gr * N + (off % (N * 2)) / 2;
+        if (nt_in) glds16_asm<true>(src, base + C::SLOT_A + piece * 1024); else glds16_asm(src, base + C::SLOT_A + piece * 1024);
+      }
+    }
+  };
+
+#pragma unroll
+  for (int i = 0; i < NST - 1; ++i)
+    if (i < my) issue(i);
+
+  for (int64_t i = 0; i < my; ++i) {
+    // this wave's pieces of block i have landed: every younger vector-memory op may stay in flight (the
+    // counts are exact for full blocks; only a workgroup's last blocks can be partial, and those wait for all)
+    // (issue order: DMA(i) at the top of iteration i - NST + 1, then that iteration's stores, then NST - 2 more
+    // iterations of DMA + stores; early iterations and a workgroup's last blocks wait for more, never less)
+    if (i + NST - 2 < my) {
+      if (i >= NST - 1) wait_vm<kWaitSteady>(); else wait_vm<kWaitEarly>();
+    } else {
+      wait_vm<0>();
+    }
+    __builtin_amdgcn_s_barrier();                 // every wave's pieces landed; the slot of block i-1 is free
+    asm volatile("" ::: "memory");
+    if (i + NST - 1 < my) issue(i + NST - 1);
+    const char* abase = ws_smem + (int)(i % NST) * R::SLOT;
+    const int64_t r0 = ((int64_t)blockIdx.x + i * G) * C::BM;
+
+    f32x16 acc[C::TM];
+#pragma unroll
+    for (int tm = 0; tm < C::TM; ++tm)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[tm][e] = 0.0f;
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int t = 0; t < C::KS; ++t) {
+#pragma unroll
+      for (int tm = 0; tm < C::TM; ++tm) {
+        const int r = tm * 32 + li;
+        const uint4 u = *reinterpret_cast<const uint4*>(abase + r * C::ROWB + (((2 * t + lh) ^ (r & 15)) << 4));
+        acc[tm] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, u),
+                                                          __builtin_bit_cast(bf16x8, wf[t]), acc[tm], 0, 0, 0);
+      }
+    }
+    __builtin_amdgcn_s_setprio(0);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+
+    float* stg = reinterpret_cast<float*>(ws_smem + (int)(i % NST) * R::SLOT);   // the dead A image
+    const uint16_t* cimg = reinterpret_cast<const uint16_t*>(abase + C::SLOT_A);
+#pragma unroll
+    for (int tm = 0; tm < C::TM; ++tm) {
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        __builtin_amdgcn_s_barrier();             // A image reads / the previous half's staging reads are done
+        asm volatile("" ::: "memory");
+#pragma unroll
+        for (int e8 = 0; e8 < 8; ++e8) {
+          const int e = 8 * h + e8;
+          const int row = (e & 3) + 8 * ((e >> 2) & 1) + 4 * lh;          // row within the 16-row half
+          stg[row * N + ((wave * 32 + li) ^ (((row >> 2) & 1) << 5))] = acc[tm][e];
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+#pragma unroll
+        for (int pass = 0; pass < 2; ++pass) {
+          const int row = pass * 8 + rq;
+          const int brow = tm * 32 + h * 16 + row;                        // row within the block
+          const int64_t grow = r0 + brow;
+          const float4 v4 = *reinterpret_cast<const float4*>(stg + row * N + (cq ^ (((row >> 2) & 1) << 5)));
+          float o[4] = {v4.x, v4.y, v4.z, v4.w};
+          float zz[4] = {0.f, 0.f, 0.f, 0.f};
+          float acc_in[4] = {0.f, 0.f, 0.f, 0.f};
+          if constexpr (kAcc) Out4<uint16_t>::unpack(*reinterpret_cast<const uint2*>(cimg + brow * N + cq), acc_in);
+#pragma unroll
+          for (int t = 0; t < 4; ++t) {
+            if (EPI == 2) {
+              o[t] = __fadd_rn(o[t], bcol[t]);
+            } else if (EPI == 1) {
+              zz[t] = __fadd_rn(o[t], bcol[t]);
+              const float y = zz[t] > 0.0f ? zz[t] : __fmul_rn(a_slope, zz[t]);
+              o[t] = kAcc ? __fadd_rn(acc_in[t], y) : y;
+            }
+          }
+          if (grow < M) {
+            if (nt_io) {
+              Out4<uint16_t>::st_nt(Y + grow * N + cq, o, true, 4);
+              if constexpr (kZ) Out4<uint16_t>::st_nt(Z + grow * N + cq, zz, true, 4);
+            } else {
+              Out4<uint16_t>::st(Y + grow * N + cq, o, true, 4);
+              if constexpr (kZ) Out4<uint16_t>::st(Z + grow * N + cq, zz, true, 4);
+            }
+          }
+        }
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // this wave's LDS reads of the slot are done
+  }
+}
+
+// Weight-stationary launch (HGIN_NT_WS = 0 / 1; default on) when the shape and operands allow it: N 128 / 256,
+// K 128 / 256 / 512, k1 a multiple of 8, no eps-scaled second source (the first layer's data inputs keep the
+// tiled kernel), 16-B aligned rows everywhere, W packed [N, K], outputs [M, N] packed.
+bool ws_enabled() {
+  static const bool on = [] {
+    const char* v = getenv("HGIN_NT_WS");
+    return !(v && v[0] == '0');
+  }();
+  return on;
+}
+
+// Non-temporal DMA of the streamed A / accum rows (HGIN_WS_NT = 0 / 1; default on: 1-3 % faster at the cfg5
+// shapes, profiles/r02/gemm_ws_bf16.txt).
+bool ws_nt_in() {
+  static const bool on = [] {
+    const char* v = getenv("HGIN_WS_NT");
+    return !(v && v[0] == '0');
+  }();
+  return on;
+}
+
+int ws_grid() {
+  static const int g = [] {
+    int dev = 0;
+    hipDeviceProp_t prop;
+    if (hipGetDevice(&dev) != hipSuccess || hipGetDeviceProperties(&prop, dev) != hipSuccess) return 256;
+    return prop.multiProcessorCount;
+  }();
+  return g;
+}
+
+template <int K, int N, int EPI, bool kAcc, bool kZ>
+int launch_ws_kn(const Src2h& a, const uint16_t* w, const float* bias, const float* prelu, const uint16_t* accum,
+                 uint16_t* z, uint16_t* y, int64_t M, bool nt_io, hipStream_t s, const char* what) {
+  constexpr int lds = WsRing<K, N, kAcc>::BYTES;
+  auto kern = k_ws_bf16<K, N, EPI, kAcc, kZ>;
+  static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                                                     hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+  if (attr != hipSuccess) {
+    set_error("%s: hipFuncSetAttribute failed: %s", what, hipGetErrorString(attr));
+    return (int)attr;
+  }
+  const int64_t nblk = ceil_div(M, (int64_t)WsCfg<K, N>::BM);
+  const int64_t grid = nblk < ws_grid() ? nblk : ws_grid();
+  kern<<<(unsigned)grid, WsCfg<K, N>::NT, lds, s>>>(a.p1, a.ld1, a.p2, a.ld2, a.k1, w, bias, prelu, accum,
+                                                     z, y, M, nt_io, ws_nt_in());
+  return check_launch(what);
+}
+
+template <int EPI, int K, int N>
+int launch_ws_epi(const Src2h& a, const uint16_t* w, const float* bias, const float* prelu, const uint16_t* accum,
+                  uint16_t* z, uint16_t* y, int64_t M, bool nt_io, hipStream_t s, const char* what) {
+  if constexpr (EPI == 1) {
+    if (accum && z) return launch_ws_kn<K, N, 1, true, true>(a, w, bias, prelu, accum, z, y, M, nt_io, s, what);
+    if (accum) return launch_ws_kn<K, N, 1, true, false>(a, w, bias, prelu, accum, z, y, M, nt_io, s, what);
+    if (z) return launch_ws_kn<K, N, 1, false, true>(a, w, bias, prelu, accum, z, y, M, nt_io, s, what);
+    return launch_ws_kn<K, N, 1, false, false>(a, w, bias, prelu, accum, z, y, M, nt_io, s, what);
+  } else {
+    return launch_ws_kn<K, N, EPI, false, false>(a, w, bias, prelu, nullptr, nullptr, y, M, nt_io, s, what);
+  }
+}
+
+// Returns -1 when the weight-stationary form does not apply (the caller launches the tiled kernel).
+template <int EPI, typename OutT>
+int try_ws_bf16(const Src2h& a, const Src2h& b, int64_t M, int64_t N, int64_t K, const float* bias,
+                const float* prelu, const OutT* accum, OutT* z, OutT* y, int64_t ldc, bool nt_io, hipStream_t s,
+                const char* what) {
+  if constexpr (!std::is_same<OutT, uint16_t>::value || !(EPI == 1 || EPI == 2)) {
+    return -1;
+  } else {
+    if (!ws_enabled() || M < 1 || ldc != N || (N != 128 && N != 256) || (K != 128 && K != 256 && K != 512))
+      return -1;
+    if (a.eps2 || a.k1 % 8 || b.ld1 != K || !aligned16(b.p1) || !aligned16(y) || (z && !aligned16(z)) ||
+        (accum && !aligned16(accum)))
+      return -1;
+    if (a.k1 > 0 && (!aligned16(a.p1) || a.ld1 % 8)) return -1;
+    if (a.k1 < K && (!aligned16(a.p2) || a.ld2 % 8)) return -1;
+#define HGIN_WS(KV, NV) \
+  if (K == KV && N == NV) return launch_ws_epi<EPI, KV, NV>(a, b.p1, bias, prelu, accum, z, y, M, nt_io, s, what);
+    HGIN_WS(512, 256) HGIN_WS(256, 256) HGIN_WS(128, 256) HGIN_WS(512, 128) HGIN_WS(256, 128) HGIN_WS(128, 128)
+#undef HGIN_WS
+    return -1;
+  }
+}
+
+// K-tile depth of the bf16 NT kernel (HGIN_NT_BKH = 64 / 128).  128: twice the A bytes per prefetch (32 KB
+// per workgroup) at 2 workgroups / CU instead of 3 — more of the A stream in flight per CU, half the barriers.
+bool bf16_bk128(int64_t K, int64_t k1) {
+  static const int env = [] {
+    const char* v = getenv("HGIN_NT_BKH");
+    return v ? atoi(v) : 64;
+  }();
+  return env == 128 && K % 128 == 0 && k1 % 128 == 0;
+}
+
 template <int EPI, typename OutT>
 int launch_nt_bf16(const Src2h& a, const Src2h& b, int64_t M, int64_t N, int64_t K, const float* bias,
                    const float* prelu, const OutT* accum, OutT* z, OutT* y, int64_t ldc, hipStream_t s,
                    const char* what, const CombEpi& ce_in = CombEpi{}, int64_t* tiles_out = nullptr) {
   CombEpi ce = ce_in;
   ce.nt_io = gemm_nt_io(M, N, (int64_t)sizeof(OutT));
+  {
+    const int rc = try_ws_bf16<EPI, OutT>(a, b, M, N, K, bias, prelu, accum, z, y, ldc, ce.nt_io, s, what);
+    if (rc >= 0) {
+      if (tiles_out) *tiles_out = 0;
+      return rc;
+    }
+  }
   const bool vec = K % kBKh == 0 && a.k1 % kBKh == 0 && aligned16(a.p1) && a.ld1 % 8 == 0 &&
                    (a.k1 == K || (aligned16(a.p2) && a.ld2 % 8 == 0)) && aligned16(b.p1) && b.ld1 % 8 == 0;
   const bool vec_out = ldc % 4 == 0 && aligned16(y) && (z == nullptr || aligned16(z)) &&
                        (accum == nullptr || aligned16(accum)) &&
                        (EPI != 4 || (aligned16(ce.xd) && ce.ldxd % 4 == 0 &&
                                      (ce.gd == nullptr || (aligned16(ce.gd) && ce.ldgd % 4 == 0))));
+  const bool deep = vec && bf16_bk128(K, a.k1);
 #define HGIN_NT_BF16(TNV, WNV)                                                                                \
   {                                                                                                          \
     constexpr int BM = (4 / WNV) * 64;                                                                       \
@@ -805,7 +1160,10 @@ int launch_nt_bf16(const Src2h& a, const Src2h& b, int64_t M, int64_t N, int64_t
     const int64_t tiles = ceil_div(N, BN) * ceil_div(M, BM);                                                 \
     const bool xcd = xcd_remap_enabled();                                                                    \
     dim3 grid((unsigned)(xcd ? round_up8(tiles) : tiles));                                                   \
-    if (vec)                                                                                                 \
+    if (deep)                                                                                                \
+      k_gemm_nt_bf16<EPI, true, TNV, WNV, OutT, 128><<<grid, 256, 0, s>>>(a, b, M, N, K, bias, prelu, accum, \
+                                                                          z, y, ldc, vec_out, tiles, xcd, ce); \
+    else if (vec)                                                                                            \
       k_gemm_nt_bf16<EPI, true, TNV, WNV, OutT><<<grid, 256, 0, s>>>(a, b, M, N, K, bias, prelu, accum, z, y, \
                                                                      ldc, vec_out, tiles, xcd, ce);          \
     else                                                                                                     \
@@ -849,18 +1207,6 @@ int check_a_h(const char* what, const uint16_t* a1, int64_t lda1, int64_t k1, co
 //   A (128-B rows):     chunk c of row r at slot c ^ ((r >> 1) & 7)
 //   B fp32 planes (64-B rows of 32 k): chunk c of column n at c ^ ((n >> 2) & 3)
 //   B bf16 (128-B rows of 64 k):       chunk c of column n at c ^ ((n >> 1) & 7)
-typedef __attribute__((address_space(3))) void lds_void_t;
-typedef __attribute__((address_space(1))) void glb_void_t;
-
-__device__ __forceinline__ void glds16(const void* g, void* lds_wave_base) {
-  __builtin_amdgcn_global_load_lds((glb_void_t*)g, (lds_void_t*)lds_wave_base, 16, 0, 0);
-}
-
-template <int N>
-__device__ __forceinline__ void wait_vm() {
-  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
-}
-
 template <typename T>
 struct Nt2 {
   static constexpr bool kF32 = sizeof(T) == 4;

@@ -1,0 +1,50 @@
+"""The bf16 GIN MLP GEMM under its process-static kernel switches, each in a fresh child process
+(tests/gemm_child.py; a separate interpreter started with subprocess, never an exec of this process):
+
+  * default                 — the weight-stationary streaming kernel (k_ws_bf16) at K 128 / 256 / 512, N 128 / 256;
+  * HGIN_NT_WS=0            — the tiled register-staged kernel (k_gemm_nt_bf16) for every shape;
+  * HGIN_NT_BKH=128         — the tiled kernel with 128-deep K-tiles (with the weight-stationary form off).
+
+Every child checks its outputs against an fp32 evaluation of the same bf16 operands; the three settings must
+agree bit for bit (same products, same per-accumulator k order, same epilogue arithmetic)."""
+import os
+import subprocess
+import sys
+import tempfile
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+SWITCHES = {"default": {}, "tiled": {"HGIN_NT_WS": "0"}, "tiled_bk128": {"HGIN_NT_WS": "0", "HGIN_NT_BKH": "128"}}
+_results = {}
+
+
+def _run(name):
+    if name in _results:
+        return _results[name]
+    env = {k: v for k, v in os.environ.items() if not k.startswith("HGIN_")}
+    env.update(SWITCHES[name])
+    with tempfile.TemporaryDirectory() as d:
+        out = os.path.join(d, "res.pt")
+        p = subprocess.run([sys.executable, os.path.join(HERE, "gemm_child.py"), out], env=env,
+                           capture_output=True, text=True, timeout=300)
+        assert p.returncode == 0, f"{name}: child failed ({p.returncode})\n{p.stdout[-2000:]}\n{p.stderr[-4000:]}"
+        _results[name] = torch.load(out, weights_only=True)
+    return _results[name]
+
+
+@pytest.mark.parametrize("name", sorted(SWITCHES))
+def test_switch_within_tolerance(name):
+    _run(name)        # the child checks against fp32 itself
+
+
+@pytest.mark.parametrize("name", ["tiled", "tiled_bk128"])
+def test_switch_bitwise_equal_default(name):
+    ref, got = _run("default"), _run(name)
+    assert ref.keys() == got.keys()
+    for case in ref:
+        for k in ref[case]:
+            assert torch.equal(ref[case][k], got[case][k]), (name, case, k)
