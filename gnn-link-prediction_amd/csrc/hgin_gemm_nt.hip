@@ -841,7 +841,9 @@ bool use_bm64_bf16(int64_t M, int64_t N) {
 //   * every wave multiplies the whole block by its W slice (v_mfma_f32_32x32x16_bf16, the per-accumulator
 //     k order of k_gemm_nt_bf16: bit-identical results), then the fp32 results are staged 16 rows at a time
 //     through the block's dead A image and written as row-contiguous 8-B bf16 quads (bias, PReLU, accum from
-//     the LDS copy), the same epilogue arithmetic as epilogue<1 / 2>.
+//     the LDS copy), the same epilogue arithmetic as epilogue<1 / 2>;
+//   * an eps-scaled second source (the first layer's concat self term, Src2h::eps2) is scaled in the block's
+//     LDS image once, before the MFMAs (bf16(s * v), the tiled kernel's staging arithmetic).
 // LDS images (16-B chunks): A row r of the block at r * 2K bytes, logical chunk c stored at slot c ^ (r & 15)
 // (the DMA lanes fetch pre-swizzled sources; a ds_read_b128 group of 16 rows hits 16 distinct bank slots);
 // accum rows linear; fp32 staging [16][N] with column bit 5 flipped on rows with bit 2 set (the two lane halves
@@ -861,25 +863,52 @@ struct WsCfg {
   static constexpr int PC = C_BYTES / 1024 / NW;
   static_assert(A_BYTES % (1024 * NW) == 0 && C_BYTES % (1024 * NW) == 0, "DMA pieces");
   static_assert(16 * N * 4 <= A_BYTES, "staging fits the A image");
+  static_assert((A_BYTES / 16) % NT == 0, "eps-scaling pass");
 };
 
-template <int K, int N, bool kAcc>
+template <int K, int N, int NIMG>
 struct WsRing {
-  static constexpr int SLOT = WsCfg<K, N>::A_BYTES + (kAcc ? WsCfg<K, N>::C_BYTES : 0);
-  static constexpr int NST = SLOT * 4 <= 147456 ? 4 : 3;
-  static constexpr int BYTES = SLOT * NST;
+  static constexpr int SLOT = WsCfg<K, N>::A_BYTES + NIMG * WsCfg<K, N>::C_BYTES;
+  // ring depth: as deep as 144 KB of LDS allows, up to 4 (0: does not fit, the tiled kernel is used)
+  static constexpr int NST = SLOT * 4 <= 147456 ? 4 : SLOT * 3 <= 147456 ? 3 : SLOT * 2 <= 147456 ? 2 : 0;
+  static constexpr int BYTES = SLOT * (NST > 0 ? NST : 1);
 };
 
-template <int K, int N, int EPI, bool kAcc, bool kZ>
-__global__ __launch_bounds__((WsCfg<K, N>::NT), 1) void k_ws_bf16(
-    const uint16_t* __restrict__ a1, int64_t lda1, const uint16_t* __restrict__ a2, int64_t lda2, int64_t k1,
-    const uint16_t* __restrict__ W, const float* __restrict__ bias,
-    const float* __restrict__ prelu, const uint16_t* __restrict__ accum, uint16_t* __restrict__ Z,
-    uint16_t* __restrict__ Y, int64_t M, bool nt_io, bool nt_in) {
+// Operands of one weight-stationary launch.  Row images (bf16 [M, N] rows streamed beside A, read by the
+// epilogue from LDS): r1 = accum (EPI 1) / x_dst (EPI 4); r2 = g_prev (EPI 4).  Outputs: Y = y (EPI 1) / C (EPI 0,
+// 4); Z = z (EPI 1) / g_x_dst (EPI 4).
+struct WsArgs {
+  const uint16_t* a1;
+  int64_t lda1;
+  const uint16_t* a2;
+  int64_t lda2;
+  int64_t k1;
+  const float* eps2;
+  const uint16_t* w;
+  const float* bias;
+  const float* prelu;
+  const uint16_t* r1;
+  int64_t ldr1;
+  const uint16_t* r2;
+  int64_t ldr2;
+  uint16_t* y;
+  int64_t ldy;
+  uint16_t* z;
+  int64_t ldz;
+  const float* eps;   // EPI 4: the GIN eps (self term scale 1 + eps)
+  float* part;        // EPI 4: one eps-gradient partial per workgroup
+  int64_t M;
+  bool nt_io;
+  bool nt_in;
+};
+
+template <int K, int N, int EPI, bool kR1, bool kZ, bool kR2>
+__global__ __launch_bounds__((WsCfg<K, N>::NT), 1) void k_ws_bf16(WsArgs g) {
   using C = WsCfg<K, N>;
-  using R = WsRing<K, N, kAcc>;
+  constexpr int NIMG = (kR1 ? 1 : 0) + (kR2 ? 1 : 0);
+  using R = WsRing<K, N, NIMG>;
   constexpr int NST = R::NST;
-  constexpr int P = C::PA + (kAcc ? C::PC : 0);                  // DMA instructions per wave per block
+  constexpr int P = C::PA + NIMG * C::PC;                        // DMA instructions per wave per block
   constexpr int S = C::TM * 4 * (kZ ? 2 : 1);                    // stores per lane per block
   constexpr int QPR = N / 4;                                     // 4-column groups per row
   constexpr int kWaitSteady = (NST - 2) * P + (NST - 1) * S < 63 ? (NST - 2) * P + (NST - 1) * S : 63;
@@ -890,6 +919,7 @@ __global__ __launch_bounds__((WsCfg<K, N>::NT), 1) void k_ws_bf16(
   const int wave = tid >> 6;
   const int li = lane & 31;
   const int lh = lane >> 5;
+  const int64_t M = g.M;
   const int64_t nblk = (M + C::BM - 1) / C::BM;
   const int64_t G = gridDim.x;
   if ((int64_t)blockIdx.x >= nblk) return;
@@ -898,19 +928,25 @@ __global__ __launch_bounds__((WsCfg<K, N>::NT), 1) void k_ws_bf16(
   // this wave's W slice as B fragments: lane (li, lh) holds W[32 wave + li][16 t + 8 lh .. + 7]
   uint4 wf[C::KS];
   {
-    const uint16_t* wr = W + (int64_t)(wave * 32 + li) * K + lh * 8;
+    const uint16_t* wr = g.w + (int64_t)(wave * 32 + li) * K + lh * 8;
 #pragma unroll
     for (int t = 0; t < C::KS; ++t) wf[t] = *reinterpret_cast<const uint4*>(wr + t * 16);
   }
-  // row-pass columns of this thread (fixed), bias, PReLU slope, eps scale
+  // row-pass columns of this thread (fixed), bias, PReLU slope, eps scales
   const int cq = (tid % QPR) * 4;
   const int rq = tid / QPR;                                      // row within an 8-row pass
   float bcol[4] = {0.f, 0.f, 0.f, 0.f};
   if (EPI == 1 || EPI == 2) {
 #pragma unroll
-    for (int t = 0; t < 4; ++t) bcol[t] = bias[cq + t];
+    for (int t = 0; t < 4; ++t) bcol[t] = g.bias[cq + t];
   }
-  const float a_slope = EPI == 1 ? prelu[0] : 0.0f;
+  const float a_slope = EPI == 1 ? g.prelu[0] : 0.0f;
+  const float sc_self = EPI == 4 ? __fadd_rn(1.0f, g.eps[0]) : 0.0f;
+  // eps-scaled second source (the first layer's concat self term): the A image's chunks with k >= k1 are
+  // scaled in LDS once per block (bf16(s * v), the tiled kernel's staging arithmetic)
+  const int64_t k1 = g.k1;
+  const bool scale_any = g.eps2 != nullptr && k1 < K;
+  const float sc2 = g.eps2 ? __fadd_rn(1.0f, g.eps2[0]) : 1.0f;
   // consume the prologue loads here, so that the compiler's own wait for them sits before the ring starts and
   // not inside the loop (where it would count the ring's DMAs)
 #pragma unroll
@@ -918,43 +954,62 @@ __global__ __launch_bounds__((WsCfg<K, N>::NT), 1) void k_ws_bf16(
 #pragma unroll
   for (int t = 0; t < 4; ++t) asm volatile("" ::"v"(bcol[t]));
 
+  auto dma = [&](const void* src, void* dst) {
+    if (g.nt_in) glds16_asm<true>(src, dst); else glds16_asm(src, dst);
+  };
+  // addresses: a block-uniform 64-bit base (row r0) plus a 32-bit per-lane offset (rows past M clamp to M - 1:
+  // their products land in rows that are never stored)
+  const int ki = (int)k1;
+  // the thread index as an opaque value, re-read where used inside the loop: the per-lane DMA / scaling offsets
+  // derived from it are then recomputed per block instead of being hoisted out of the loop into registers
+  // (which spills the K = 512 kernels, whose W slice alone holds 128 VGPRs)
+  auto tid_o = [&]() {
+    int t;
+    asm volatile("v_mov_b32 %0, %1" : "=v"(t) : "v"(tid));
+    return t;
+  };
+  auto issue_rows = [&](const uint16_t* p, int64_t ld, char* img, int64_t r0, int rmax) {
+    const uint16_t* pb = p + r0 * ld;
+    const int lane = tid_o() & 63;
+#pragma unroll
+    for (int q = 0; q < C::PC; ++q) {
+      const int piece = wave * C::PC + q;
+      const int off = piece * 1024 + lane * 16;
+      const int r = off / (N * 2);
+      dma(pb + ((r < rmax ? r : rmax) * (int)ld + (off % (N * 2)) / 2), img + piece * 1024);
+    }
+  };
   auto issue = [&](int64_t i) {
     char* base = ws_smem + (int)(i % NST) * R::SLOT;
     const int64_t r0 = ((int64_t)blockIdx.x + i * G) * C::BM;
+    const int rmax = (int)(M - 1 - r0 < C::BM ? M - 1 - r0 : C::BM - 1);
+    const uint16_t* b1 = g.a1 + r0 * g.lda1;
+    const uint16_t* b2 = g.a2 + r0 * g.lda2;
+    const int lane = tid_o() & 63;
 #pragma unroll
-    for (int p = 0; p < C::PA; ++p) {
-      const int piece = wave * C::PA + p;
+    for (int q = 0; q < C::PA; ++q) {
+      const int piece = wave * C::PA + q;
       const int off = piece * 1024 + lane * 16;
-      const int r = off / C::ROWB;
+      int r = off / C::ROWB;
       const int c = ((off % C::ROWB) >> 4) ^ (r & 15);           // logical chunk stored at this slot
-      int64_t gr = r0 + r;
-      gr = gr < M ? gr : M - 1;                                   // clamped rows are never stored
-      const int64_t k = (int64_t)c * 8;
-      const uint16_t* src = k < k1 ? a1 + gr * lda1 + k : a2 + gr * lda2 + (k - k1);
-      if (nt_in) glds16_asm<true>(src, base + piece * 1024); else glds16_asm(src, base + piece * 1024);
+      r = r < rmax ? r : rmax;
+      const int k = c * 8;
+      dma(k < ki ? b1 + (r * (int)g.lda1 + k) : b2 + (r * (int)g.lda2 + (k - ki)), base + piece * 1024);
     }
-    if constexpr (kAcc) {
-#pragma unroll
-      for (int p = 0; p < C::PC; ++p) {
-        const int piece = wave * C::PC + p;
-        const int off = piece * 1024 + lane * 16;
-        int64_t gr = r0 + off / (N * 2);
-        gr = gr < M ? gr : M - 1;
-        const uint16_t* src = accum + gr * N + (off % (N * 2)) / 2;
-        if (nt_in) glds16_asm<true>(src, base + C::SLOT_A + piece * 1024); else glds16_asm(src, base + C::SLOT_A + piece * 1024);
-      }
-    }
+    if constexpr (kR1) issue_rows(g.r1, g.ldr1, base + C::A_BYTES, r0, rmax);
+    if constexpr (kR2) issue_rows(g.r2, g.ldr2, base + C::A_BYTES + (kR1 ? C::C_BYTES : 0), r0, rmax);
   };
 
 #pragma unroll
   for (int i = 0; i < NST - 1; ++i)
     if (i < my) issue(i);
 
+  float ep = 0.0f;                                               // EPI 4: this thread's eps-gradient partial
   for (int64_t i = 0; i < my; ++i) {
-    // this wave's pieces of block i have landed: every younger vector-memory op may stay in flight (the
-    // counts are exact for full blocks; only a workgroup's last blocks can be partial, and those wait for all)
-    // (issue order: DMA(i) at the top of iteration i - NST + 1, then that iteration's stores, then NST - 2 more
-    // iterations of DMA + stores; early iterations and a workgroup's last blocks wait for more, never less)
+    // this wave's pieces of block i have landed: every younger vector-memory op may stay in flight.  Issue
+    // order: DMA(i) at the top of iteration i - NST + 1, then that iteration's stores, then NST - 2 more
+    // iterations of DMA + stores.  The counts are exact for full blocks; early iterations and a workgroup's
+    // last blocks (the only partial block is the last) wait for more, never less.
     if (i + NST - 2 < my) {
       if (i >= NST - 1) wait_vm<kWaitSteady>(); else wait_vm<kWaitEarly>();
     } else {
@@ -963,8 +1018,29 @@ __global__ __launch_bounds__((WsCfg<K, N>::NT), 1) void k_ws_bf16(
     __builtin_amdgcn_s_barrier();                 // every wave's pieces landed; the slot of block i-1 is free
     asm volatile("" ::: "memory");
     if (i + NST - 1 < my) issue(i + NST - 1);
-    const char* abase = ws_smem + (int)(i % NST) * R::SLOT;
+    char* abase = ws_smem + (int)(i % NST) * R::SLOT;
+    if (scale_any) {
+      constexpr int CH = C::A_BYTES / 16;                        // 16-B chunks of the A image
+      const int tq = tid_o();
+#pragma unroll
+      for (int q = 0; q < CH / C::NT; ++q) {
+        const int ch = q * C::NT + tq;
+        const int r = ch / (C::ROWB / 16);
+        const int c = (ch % (C::ROWB / 16)) ^ (r & 15);          // logical chunk at this slot
+        if (c * 8 >= k1) {
+          uint4* pu = reinterpret_cast<uint4*>(abase + ch * 16);
+          const uint4 u = *pu;
+          *pu = make_uint4(scale_bf2(u.x, sc2), scale_bf2(u.y, sc2), scale_bf2(u.z, sc2), scale_bf2(u.w, sc2));
+        }
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+    }
     const int64_t r0 = ((int64_t)blockIdx.x + i * G) * C::BM;
+    const int64_t ldy = EPI == 1 ? N : g.ldy, ldz = EPI == 1 ? N : g.ldz;
+    uint16_t* yb = g.y + r0 * ldy;                                // block-uniform output bases
+    uint16_t* zb = kZ ? g.z + r0 * ldz : nullptr;
 
     f32x16 acc[C::TM];
 #pragma unroll
@@ -985,8 +1061,9 @@ __global__ __launch_bounds__((WsCfg<K, N>::NT), 1) void k_ws_bf16(
     __builtin_amdgcn_s_setprio(0);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 
-    float* stg = reinterpret_cast<float*>(ws_smem + (int)(i % NST) * R::SLOT);   // the dead A image
-    const uint16_t* cimg = reinterpret_cast<const uint16_t*>(abase + C::SLOT_A);
+    float* stg = reinterpret_cast<float*>(abase);                // the dead A image
+    const uint16_t* img1 = reinterpret_cast<const uint16_t*>(abase + C::A_BYTES);
+    const uint16_t* img2 = reinterpret_cast<const uint16_t*>(abase + C::A_BYTES + (kR1 ? C::C_BYTES : 0));
 #pragma unroll
     for (int tm = 0; tm < C::TM; ++tm) {
 #pragma unroll
@@ -1010,8 +1087,9 @@ __global__ __launch_bounds__((WsCfg<K, N>::NT), 1) void k_ws_bf16(
           const float4 v4 = *reinterpret_cast<const float4*>(stg + row * N + (cq ^ (((row >> 2) & 1) << 5)));
           float o[4] = {v4.x, v4.y, v4.z, v4.w};
           float zz[4] = {0.f, 0.f, 0.f, 0.f};
-          float acc_in[4] = {0.f, 0.f, 0.f, 0.f};
-          if constexpr (kAcc) Out4<uint16_t>::unpack(*reinterpret_cast<const uint2*>(cimg + brow * N + cq), acc_in);
+          float in1[4] = {0.f, 0.f, 0.f, 0.f}, in2[4] = {0.f, 0.f, 0.f, 0.f};
+          if constexpr (kR1) Out4<uint16_t>::unpack(*reinterpret_cast<const uint2*>(img1 + brow * N + cq), in1);
+          if constexpr (kR2) Out4<uint16_t>::unpack(*reinterpret_cast<const uint2*>(img2 + brow * N + cq), in2);
 #pragma unroll
           for (int t = 0; t < 4; ++t) {
             if (EPI == 2) {
@@ -1019,16 +1097,26 @@ __global__ __launch_bounds__((WsCfg<K, N>::NT), 1) void k_ws_bf16(
             } else if (EPI == 1) {
               zz[t] = __fadd_rn(o[t], bcol[t]);
               const float y = zz[t] > 0.0f ? zz[t] : __fmul_rn(a_slope, zz[t]);
-              o[t] = kAcc ? __fadd_rn(acc_in[t], y) : y;
+              o[t] = kR1 ? __fadd_rn(in1[t], y) : y;
             }
           }
           if (grow < M) {
-            if (nt_io) {
-              Out4<uint16_t>::st_nt(Y + grow * N + cq, o, true, 4);
-              if constexpr (kZ) Out4<uint16_t>::st_nt(Z + grow * N + cq, zz, true, 4);
+            if constexpr (EPI == 4) {   // epilogue<4>'s self-term backward on C as stored (bf16-rounded)
+#pragma unroll
+              for (int t = 0; t < 4; ++t) {
+                const float c4 = Out4<uint16_t>::rt(o[t]);
+                ep = __fadd_rn(ep, __fmul_rn(c4, in1[t]));
+                zz[t] = __fmul_rn(sc_self, c4);
+                if (kR2) zz[t] = __fadd_rn(in2[t], zz[t]);
+              }
+            }
+            const int oy = brow * (int)ldy + cq, oz = brow * (int)ldz + cq;
+            if (g.nt_io) {
+              Out4<uint16_t>::st_nt(yb + oy, o, true, 4);
+              if constexpr (kZ) Out4<uint16_t>::st_nt(zb + oz, zz, true, 4);
             } else {
-              Out4<uint16_t>::st(Y + grow * N + cq, o, true, 4);
-              if constexpr (kZ) Out4<uint16_t>::st(Z + grow * N + cq, zz, true, 4);
+              Out4<uint16_t>::st(yb + oy, o, true, 4);
+              if constexpr (kZ) Out4<uint16_t>::st(zb + oz, zz, true, 4);
             }
           }
         }
@@ -1036,11 +1124,12 @@ __global__ __launch_bounds__((WsCfg<K, N>::NT), 1) void k_ws_bf16(
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // this wave's LDS reads of the slot are done
   }
+  if constexpr (EPI == 4) tile_partial(reinterpret_cast<float*>(ws_smem), ep, g.part, blockIdx.x);
 }
 
 // Weight-stationary launch (HGIN_NT_WS = 0 / 1; default on) when the shape and operands allow it: N 128 / 256,
-// K 128 / 256 / 512, k1 a multiple of 8, no eps-scaled second source (the first layer's data inputs keep the
-// tiled kernel), 16-B aligned rows everywhere, W packed [N, K], outputs [M, N] packed.
+// K 128 / 256 / 512, k1 a multiple of 8, 16-B aligned rows everywhere (leading dimensions multiples of 8), W
+// packed [N, K]; EPI 1 (forward MLP), EPI 0 (plain dX) and EPI 4 with the self term on every column (cs = 0).
 bool ws_enabled() {
   static const bool on = [] {
     const char* v = getenv("HGIN_NT_WS");
@@ -1049,8 +1138,8 @@ bool ws_enabled() {
   return on;
 }
 
-// Non-temporal DMA of the streamed A / accum rows (HGIN_WS_NT = 0 / 1; default on: 1-3 % faster at the cfg5
-// shapes, profiles/r02/gemm_ws_bf16.txt).
+// Non-temporal DMA of the streamed A / row-image rows (HGIN_WS_NT = 0 / 1; default on: 1-3 % faster at the
+// cfg5 shapes, profiles/r02/gemm_ws_bf16.txt).
 bool ws_nt_in() {
   static const bool on = [] {
     const char* v = getenv("HGIN_WS_NT");
@@ -1069,54 +1158,85 @@ int ws_grid() {
   return g;
 }
 
-template <int K, int N, int EPI, bool kAcc, bool kZ>
-int launch_ws_kn(const Src2h& a, const uint16_t* w, const float* bias, const float* prelu, const uint16_t* accum,
-                 uint16_t* z, uint16_t* y, int64_t M, bool nt_io, hipStream_t s, const char* what) {
-  constexpr int lds = WsRing<K, N, kAcc>::BYTES;
-  auto kern = k_ws_bf16<K, N, EPI, kAcc, kZ>;
-  static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
-                                                     hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-  if (attr != hipSuccess) {
-    set_error("%s: hipFuncSetAttribute failed: %s", what, hipGetErrorString(attr));
-    return (int)attr;
+template <int K, int N, int EPI, bool kR1, bool kZ, bool kR2>
+int launch_ws_kn(const WsArgs& a, hipStream_t s, const char* what, int64_t* grid_out) {
+  using Ring = WsRing<K, N, (kR1 ? 1 : 0) + (kR2 ? 1 : 0)>;
+  if constexpr (Ring::NST < 2) {
+    return -1;
+  } else {
+    constexpr int lds = Ring::BYTES;
+    auto kern = k_ws_bf16<K, N, EPI, kR1, kZ, kR2>;
+    static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                                                       hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    if (attr != hipSuccess) {
+      set_error("%s: hipFuncSetAttribute failed: %s", what, hipGetErrorString(attr));
+      return (int)attr;
+    }
+    const int64_t nblk = ceil_div(a.M, (int64_t)WsCfg<K, N>::BM);
+    const int64_t grid = nblk < ws_grid() ? nblk : ws_grid();
+    kern<<<(unsigned)grid, WsCfg<K, N>::NT, lds, s>>>(a);
+    if (grid_out) *grid_out = grid;
+    return check_launch(what);
   }
-  const int64_t nblk = ceil_div(M, (int64_t)WsCfg<K, N>::BM);
-  const int64_t grid = nblk < ws_grid() ? nblk : ws_grid();
-  kern<<<(unsigned)grid, WsCfg<K, N>::NT, lds, s>>>(a.p1, a.ld1, a.p2, a.ld2, a.k1, w, bias, prelu, accum,
-                                                     z, y, M, nt_io, ws_nt_in());
-  return check_launch(what);
 }
 
 template <int EPI, int K, int N>
-int launch_ws_epi(const Src2h& a, const uint16_t* w, const float* bias, const float* prelu, const uint16_t* accum,
-                  uint16_t* z, uint16_t* y, int64_t M, bool nt_io, hipStream_t s, const char* what) {
+int launch_ws_epi(const WsArgs& a, hipStream_t s, const char* what, int64_t* grid_out) {
+  const bool r1 = a.r1 != nullptr, z = a.z != nullptr, r2 = a.r2 != nullptr;
   if constexpr (EPI == 1) {
-    if (accum && z) return launch_ws_kn<K, N, 1, true, true>(a, w, bias, prelu, accum, z, y, M, nt_io, s, what);
-    if (accum) return launch_ws_kn<K, N, 1, true, false>(a, w, bias, prelu, accum, z, y, M, nt_io, s, what);
-    if (z) return launch_ws_kn<K, N, 1, false, true>(a, w, bias, prelu, accum, z, y, M, nt_io, s, what);
-    return launch_ws_kn<K, N, 1, false, false>(a, w, bias, prelu, accum, z, y, M, nt_io, s, what);
+    if (r1 && z) return launch_ws_kn<K, N, 1, true, true, false>(a, s, what, grid_out);
+    if (r1) return launch_ws_kn<K, N, 1, true, false, false>(a, s, what, grid_out);
+    if (z) return launch_ws_kn<K, N, 1, false, true, false>(a, s, what, grid_out);
+    return launch_ws_kn<K, N, 1, false, false, false>(a, s, what, grid_out);
+  } else if constexpr (EPI == 4) {
+    if (z && r2) return launch_ws_kn<K, N, 4, true, true, true>(a, s, what, grid_out);
+    if (z) return launch_ws_kn<K, N, 4, true, true, false>(a, s, what, grid_out);
+    return launch_ws_kn<K, N, 4, true, false, false>(a, s, what, grid_out);
   } else {
-    return launch_ws_kn<K, N, EPI, false, false>(a, w, bias, prelu, nullptr, nullptr, y, M, nt_io, s, what);
+    return launch_ws_kn<K, N, EPI, false, false, false>(a, s, what, grid_out);
   }
 }
 
 // Returns -1 when the weight-stationary form does not apply (the caller launches the tiled kernel).
 template <int EPI, typename OutT>
 int try_ws_bf16(const Src2h& a, const Src2h& b, int64_t M, int64_t N, int64_t K, const float* bias,
-                const float* prelu, const OutT* accum, OutT* z, OutT* y, int64_t ldc, bool nt_io, hipStream_t s,
-                const char* what) {
-  if constexpr (!std::is_same<OutT, uint16_t>::value || !(EPI == 1 || EPI == 2)) {
+                const float* prelu, const OutT* accum, OutT* z, OutT* y, int64_t ldc, const CombEpi& ce,
+                hipStream_t s, const char* what, int64_t* grid_out) {
+  if constexpr (!std::is_same<OutT, uint16_t>::value || !(EPI == 0 || EPI == 1 || EPI == 4)) {
     return -1;
   } else {
-    if (!ws_enabled() || M < 1 || ldc != N || (N != 128 && N != 256) || (K != 128 && K != 256 && K != 512))
-      return -1;
-    if (a.eps2 || a.k1 % 8 || b.ld1 != K || !aligned16(b.p1) || !aligned16(y) || (z && !aligned16(z)) ||
-        (accum && !aligned16(accum)))
-      return -1;
-    if (a.k1 > 0 && (!aligned16(a.p1) || a.ld1 % 8)) return -1;
-    if (a.k1 < K && (!aligned16(a.p2) || a.ld2 % 8)) return -1;
+    if (!ws_enabled() || M < 1 || (N != 128 && N != 256) || (K != 128 && K != 256 && K != 512)) return -1;
+    // (16-B aligned rows; ld < 2^24 keeps the kernel's per-lane 32-bit offsets in range within a block)
+    auto ok = [](const void* p, int64_t ld) {
+      return p == nullptr || (aligned16(p) && ld % 8 == 0 && ld < (int64_t(1) << 24));
+    };
+    if (a.k1 % 8 || b.ld1 != K || !aligned16(b.p1) || !ok(y, ldc)) return -1;
+    if (a.k1 > 0 && !ok(a.p1, a.ld1)) return -1;
+    if (a.k1 < K && !ok(a.p2, a.ld2)) return -1;
+    WsArgs w{a.p1, a.ld1, a.p2, a.ld2, a.k1, a.eps2, b.p1, bias, prelu,
+             nullptr, 0, nullptr, 0, y, ldc, nullptr, 0, nullptr, nullptr, M, ce.nt_io, ws_nt_in()};
+    if constexpr (EPI == 1) {
+      if (ldc != N || !ok(z, N) || !ok(accum, N)) return -1;
+      w.r1 = accum;
+      w.ldr1 = N;
+      w.z = z;
+      w.ldz = N;
+    } else if constexpr (EPI == 4) {
+      const uint16_t* xd = static_cast<const uint16_t*>(ce.xd);
+      uint16_t* gd = static_cast<uint16_t*>(ce.gd);
+      const uint16_t* gp = static_cast<const uint16_t*>(ce.gp);
+      if (ce.cs != 0 || !xd || !ok(xd, ce.ldxd) || !ok(gd, ce.ldgd) || !ok(gp, ce.ldgp)) return -1;
+      w.r1 = xd;
+      w.ldr1 = ce.ldxd;
+      w.z = gd;
+      w.ldz = ce.ldgd;
+      w.r2 = gd ? gp : nullptr;
+      w.ldr2 = ce.ldgp;
+      w.eps = ce.eps;
+      w.part = ce.part;
+    }
 #define HGIN_WS(KV, NV) \
-  if (K == KV && N == NV) return launch_ws_epi<EPI, KV, NV>(a, b.p1, bias, prelu, accum, z, y, M, nt_io, s, what);
+  if (K == KV && N == NV) return launch_ws_epi<EPI, KV, NV>(w, s, what, grid_out);
     HGIN_WS(512, 256) HGIN_WS(256, 256) HGIN_WS(128, 256) HGIN_WS(512, 128) HGIN_WS(256, 128) HGIN_WS(128, 128)
 #undef HGIN_WS
     return -1;
@@ -1140,11 +1260,8 @@ int launch_nt_bf16(const Src2h& a, const Src2h& b, int64_t M, int64_t N, int64_t
   CombEpi ce = ce_in;
   ce.nt_io = gemm_nt_io(M, N, (int64_t)sizeof(OutT));
   {
-    const int rc = try_ws_bf16<EPI, OutT>(a, b, M, N, K, bias, prelu, accum, z, y, ldc, ce.nt_io, s, what);
-    if (rc >= 0) {
-      if (tiles_out) *tiles_out = 0;
-      return rc;
-    }
+    const int rc = try_ws_bf16<EPI, OutT>(a, b, M, N, K, bias, prelu, accum, z, y, ldc, ce, s, what, tiles_out);
+    if (rc >= 0) return rc;   // (EPI 4: *tiles_out = the grid, one eps-gradient partial per workgroup)
   }
   const bool vec = K % kBKh == 0 && a.k1 % kBKh == 0 && aligned16(a.p1) && a.ld1 % 8 == 0 &&
                    (a.k1 == K || (aligned16(a.p2) && a.ld2 % 8 == 0)) && aligned16(b.p1) && b.ld1 % 8 == 0;

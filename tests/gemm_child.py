@@ -20,15 +20,16 @@ import torch  # noqa: E402
 from hgin import ops  # noqa: E402
 
 BF = torch.bfloat16
-CASES = [  # (M, K, N, accum, save_z, k1 of a two-source A or 0)
+CASES = [  # (M, K, N, accum, save_z, k1 of a two-source A or 0, eps of the second source or None)
     (300_007, 512, 256, True, True, 0), (1, 512, 256, True, True, 0), (31, 256, 256, False, True, 0),
     (70_001, 256, 256, True, False, 0), (50_000, 128, 256, True, True, 0), (65, 128, 256, False, False, 0),
     (100_003, 512, 128, True, True, 0), (20_000, 256, 128, True, True, 0), (9_999, 128, 128, True, True, 0),
     (40_000, 512, 256, True, True, 256), (12_345, 256, 128, False, True, 128),
+    (60_001, 512, 256, True, True, 256, 0.37), (5_000, 256, 256, False, True, 64, -0.2),
 ]
 
 
-def run(M, K, N, with_acc, save_z, k1, g):
+def run(M, K, N, with_acc, save_z, k1, eps=None, *, g):
     a = torch.randn(M, K, device="cuda", generator=g).to(BF)
     w = (torch.randn(N, K, device="cuda", generator=g) / K ** 0.5).to(BF)
     b = torch.randn(N, device="cuda", generator=g)
@@ -36,7 +37,10 @@ def run(M, K, N, with_acc, save_z, k1, g):
     acc = torch.randn(M, N, device="cuda", generator=g).to(BF) if with_acc else None
     if k1:
         a1, a2 = a[:, :k1].contiguous(), a[:, k1:].contiguous()
-        z, y = ops.gin_mlp_fwd(a1, w, b, s, acc, save_z=save_z, comb2=a2)
+        e2 = torch.tensor([eps], device="cuda") if eps is not None else None
+        z, y = ops.gin_mlp_fwd(a1, w, b, s, acc, save_z=save_z, comb2=a2, eps2=e2)
+        if eps is not None:   # the kernels' self term: bf16(fp32(1 + eps) * a2), rounded once
+            a = torch.cat([a1, (a2.float() * (1.0 + torch.tensor(eps, dtype=torch.float32))).to(BF)], 1)
     else:
         z, y = ops.gin_mlp_fwd(a, w, b, s, acc, save_z=save_z)
     zr = a.float() @ w.float().t() + b
@@ -51,10 +55,48 @@ def run(M, K, N, with_acc, save_z, k1, g):
     return out
 
 
+DX_CASES = [  # (M, K, N, combine: None | (want_gx, with g_prev))  — the backward dX GEMMs (EPI 0 / 4)
+    (200_003, 256, 256, None), (31, 512, 256, None), (70_000, 256, 128, None),
+    (150_001, 256, 256, (True, True)), (99_999, 256, 256, (True, False)), (40_000, 256, 256, (False, False)),
+    (33, 256, 128, (True, True)),
+]
+
+
+def run_dx(M, K, N, comb, *, g):
+    """c = a @ b^T (ops.gemm_nt) or the combine form (ops.gemm_nt_combine, self term on every column)."""
+    a = torch.randn(M, K, device="cuda", generator=g).to(BF)
+    b = (torch.randn(N, K, device="cuda", generator=g) / K ** 0.5).to(BF)
+    cr = a.float() @ b.float().t()
+    bound = 2 ** -8 * cr.abs() + 1e-3 * (a.float().abs() @ b.float().abs().t() + 1)
+    if comb is None:
+        c = ops.gemm_nt(a, b)
+        assert bool(((c.float() - cr).abs() <= bound).all()), (M, K, N)
+        return {"c": c.cpu()}
+    want_gx, with_prev = comb
+    xd = torch.randn(M, N, device="cuda", generator=g).to(BF)
+    eps = torch.tensor([0.3], device="cuda")
+    prev = torch.randn(M, N, device="cuda", generator=g).to(BF) if with_prev else None
+    prev0 = prev.clone() if with_prev else None
+    c, gx, ge = ops.gemm_nt_combine(a, b, xd, eps, 0, want_gx, g_prev=prev)
+    assert bool(((c.float() - cr).abs() <= bound).all()), (M, K, N, "c")
+    c32 = c.float()
+    ge_ref = float((c32.double() * xd.double()).sum())
+    assert abs(float(ge) - ge_ref) <= 1e-5 * float((c32.double() * xd.double()).abs().sum()), (M, float(ge), ge_ref)
+    out = {"c": c.cpu(), "tol_g_eps": ge.detach().reshape(1).cpu()}
+    if want_gx:
+        gr = (torch.tensor(1.3, dtype=torch.float32) * c32).to(BF).float()   # fp32 (1 + eps) * c, rounded once
+        if with_prev:
+            gr = (prev0.float() + (1.3 * c32)).to(BF).float()
+        assert bool(((gx.float() - gr).abs() <= 2 ** -7 * gr.abs() + 1e-6).all()), (M, "g_x_dst")
+        out["gx"] = gx.cpu()
+    return out
+
+
 def main():
     torch.cuda.init()
     g = torch.Generator(device="cuda").manual_seed(7)
-    res = {f"{c}": run(*c, g) for c in CASES}
+    res = {f"{c}": run(*c, g=g) for c in CASES}
+    res.update({f"dx{c}": run_dx(*c, g=g) for c in DX_CASES})
     torch.save(res, sys.argv[1])
     print("gemm child ok", {k: v for k, v in os.environ.items() if k.startswith("HGIN_")}, flush=True)
 

@@ -1,12 +1,15 @@
 """The bf16 GIN MLP GEMM under its process-static kernel switches, each in a fresh child process
 (tests/gemm_child.py; a separate interpreter started with subprocess, never an exec of this process):
 
-  * default                 — the weight-stationary streaming kernel (k_ws_bf16) at K 128 / 256 / 512, N 128 / 256;
+  * default                 — the weight-stationary streaming kernel (k_ws_bf16) at K 128 / 256 / 512, N 128 / 256:
+                              the forward MLP GEMM (EPI 1), the plain dX GEMM (EPI 0) and the dX GEMM with the
+                              self-term backward in its epilogue (EPI 4, combine);
   * HGIN_NT_WS=0            — the tiled register-staged kernel (k_gemm_nt_bf16) for every shape;
   * HGIN_NT_BKH=128         — the tiled kernel with 128-deep K-tiles (with the weight-stationary form off).
 
 Every child checks its outputs against an fp32 evaluation of the same bf16 operands; the three settings must
-agree bit for bit (same products, same per-accumulator k order, same epilogue arithmetic)."""
+agree bit for bit (same products, same per-accumulator k order, same epilogue arithmetic), except the combine's
+eps gradient, a sum over per-workgroup partials whose grouping follows the launch (within 1e-5 relative)."""
 import os
 import subprocess
 import sys
@@ -47,4 +50,8 @@ def test_switch_bitwise_equal_default(name):
     assert ref.keys() == got.keys()
     for case in ref:
         for k in ref[case]:
-            assert torch.equal(ref[case][k], got[case][k]), (name, case, k)
+            if k.startswith("tol_"):
+                r, x = float(ref[case][k][0]), float(got[case][k][0])
+                assert abs(r - x) <= 1e-5 * abs(r) + 1e-6, (name, case, k, r, x)
+            else:
+                assert torch.equal(ref[case][k], got[case][k]), (name, case, k)
