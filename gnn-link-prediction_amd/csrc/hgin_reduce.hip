@@ -21,6 +21,7 @@ struct RowsCfg {
   int rpb = 256;
   int u = 0;
   int nt = -1;   // -1: fp32 on, bf16 off (measured); 0 / 1 forced
+  int nt_out = -1;   // -1: by output size; 0 / 1 forced
 };
 const RowsCfg& rows_cfg() {
   static const RowsCfg c = [] {
@@ -28,6 +29,7 @@ const RowsCfg& rows_cfg() {
     if (const char* v = getenv("HGIN_ROWS_RPB")) r.rpb = atoi(v);
     if (const char* v = getenv("HGIN_ROWS_U")) r.u = atoi(v);
     if (const char* v = getenv("HGIN_ROWS_NT")) r.nt = atoi(v) != 0;
+    if (const char* v = getenv("HGIN_ROWS_NT_OUT")) r.nt_out = atoi(v) != 0;
     if (r.rpb != 64 && r.rpb != 128 && r.rpb != 256) r.rpb = 256;
     if (r.u != 0 && r.u != 1 && r.u != 4) r.u = 0;
     return r;
@@ -105,11 +107,28 @@ __device__ __forceinline__ void rows_load(const T* p, float (&v)[VEC]) {
 //         (the column sums and the slope sum use the fp32 g_z before any bf16 rounding of the output)
 // MODE 1: combine backward.  in0 = g (self-term columns), in1 = x_dst; out = s*g (optional);
 //         part_s = sum(g * x_dst); no column sums.
+// Non-temporal store of one output group (nt_out: outputs far beyond the caches, read back by a later kernel).
+template <int VEC, typename T>
+__device__ __forceinline__ void rows_store(T* p, const float (&v)[VEC], bool nt) {
+  if constexpr (VEC == 4 && sizeof(T) == 4) {
+    if (nt) {
+      __builtin_nontemporal_store(rows_f4v{v[0], v[1], v[2], v[3]}, reinterpret_cast<rows_f4v*>(p));
+      return;
+    }
+  } else if constexpr (VEC == 4 && sizeof(T) == 2) {
+    if (nt) {
+      __builtin_nontemporal_store(rows_u2v{pack_bf2(v[0], v[1]), pack_bf2(v[2], v[3])}, reinterpret_cast<rows_u2v*>(p));
+      return;
+    }
+  }
+  RowVec<VEC, T>::store(p, v);
+}
+
 template <int MODE, int VEC, typename T, int kU, bool NT = false>
 __global__ __launch_bounds__(256) void k_rows_bwd(const T* __restrict__ in0, int64_t ld0, const T* __restrict__ in1,
                                                   int64_t ld1, int64_t M, int N, const float* __restrict__ scalar,
                                                   T* __restrict__ out, int64_t ldo, float* __restrict__ part_col,
-                                                  float* __restrict__ part_s, int rows_per_block) {
+                                                  float* __restrict__ part_s, int rows_per_block, bool nt_out) {
   __shared__ float red[256 * VEC];
   const int t = threadIdx.x;
   const int NU = N / VEC;                 // column units
@@ -146,7 +165,7 @@ __global__ __launch_bounds__(256) void k_rows_bwd(const T* __restrict__ in0, int
             ssum = __fadd_rn(ssum, __fmul_rn(g[q], x[q]));
           }
         }
-        if (MODE == 0 || out) RowVec<VEC, T>::store(out + r * ldo + c, o);
+        if (MODE == 0 || out) rows_store<VEC, T>(out + r * ldo + c, o, nt_out);
       };
       int64_t r = r0 + rl;     // kU rows' loads in flight together
       for (; r + (kU - 1) * RL < r1; r += kU * RL) {
@@ -191,17 +210,19 @@ void launch_rows_bwd(bool vec, unsigned nblk, int rpb, hipStream_t s, const T* i
                      float* part_s) {
   const bool u4 = rows_cfg().u == 4 || (rows_cfg().u == 0 && sizeof(T) == 4);
   const bool nt = rows_cfg().nt < 0 ? sizeof(T) == 4 : rows_cfg().nt == 1;
+  // non-temporal output stores once the output exceeds 512 MiB (HGIN_ROWS_NT_OUT = 0 / 1 forces)
+  const bool nt_out = rows_cfg().nt_out < 0 ? M * N * (int64_t)sizeof(T) > (int64_t(512) << 20) : rows_cfg().nt_out == 1;
   if (vec && nt) {
     if (u4)
-      k_rows_bwd<MODE, 4, T, 4, true><<<nblk, 256, 0, s>>>(in0, ld0, in1, ld1, M, N, scalar, out, ldo, part_col, part_s, rpb);
+      k_rows_bwd<MODE, 4, T, 4, true><<<nblk, 256, 0, s>>>(in0, ld0, in1, ld1, M, N, scalar, out, ldo, part_col, part_s, rpb, nt_out);
     else
-      k_rows_bwd<MODE, 4, T, 1, true><<<nblk, 256, 0, s>>>(in0, ld0, in1, ld1, M, N, scalar, out, ldo, part_col, part_s, rpb);
+      k_rows_bwd<MODE, 4, T, 1, true><<<nblk, 256, 0, s>>>(in0, ld0, in1, ld1, M, N, scalar, out, ldo, part_col, part_s, rpb, nt_out);
   } else if (vec && u4)
-    k_rows_bwd<MODE, 4, T, 4><<<nblk, 256, 0, s>>>(in0, ld0, in1, ld1, M, N, scalar, out, ldo, part_col, part_s, rpb);
+    k_rows_bwd<MODE, 4, T, 4><<<nblk, 256, 0, s>>>(in0, ld0, in1, ld1, M, N, scalar, out, ldo, part_col, part_s, rpb, nt_out);
   else if (vec)
-    k_rows_bwd<MODE, 4, T, 1><<<nblk, 256, 0, s>>>(in0, ld0, in1, ld1, M, N, scalar, out, ldo, part_col, part_s, rpb);
+    k_rows_bwd<MODE, 4, T, 1><<<nblk, 256, 0, s>>>(in0, ld0, in1, ld1, M, N, scalar, out, ldo, part_col, part_s, rpb, nt_out);
   else
-    k_rows_bwd<MODE, 1, T, 1><<<nblk, 256, 0, s>>>(in0, ld0, in1, ld1, M, N, scalar, out, ldo, part_col, part_s, rpb);
+    k_rows_bwd<MODE, 1, T, 1><<<nblk, 256, 0, s>>>(in0, ld0, in1, ld1, M, N, scalar, out, ldo, part_col, part_s, rpb, nt_out);
 }
 
 template <typename T>
