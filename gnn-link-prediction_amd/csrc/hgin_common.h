@@ -98,6 +98,26 @@ __device__ __forceinline__ void split4(const float4 v, uint2 (&o)[3]) {
 constexpr int kSplitRowWords = 52;
 bool gemm_split_enabled();   // HGIN_F32_GEMM=mfma32 selects the exact f32-MFMA kernels; default split
 
+// LDS-DMA (global_load_lds_dwordx4: 64 lanes x 16 B into 1 KiB at a wave-uniform LDS address) issued from
+// inline asm: the compiler does not see it, so it does not guard the kernel's later LDS reads with a vmcnt(0)
+// of its own (which would drain a DMA ring); kernels that use it count their vector-memory ops and wait with
+// wait_vm<N>() (loads, stores and LDS-DMA retire in issue order for vmcnt).  Used by the weight-stationary
+// GEMMs (hgin_gemm_nt.hip k_ws_bf16, hgin_gemm_tn.hip k_wsd_bf16).
+template <bool kNt = false>
+__device__ __forceinline__ void glds16_asm(const void* g, void* lds_wave_base) {
+  const uint32_t m0 = __builtin_amdgcn_readfirstlane(
+      (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)(lds_wave_base));
+  if constexpr (kNt)
+    asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off nt" ::"v"(g), "s"(m0) : "memory", "m0");
+  else
+    asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(g), "s"(m0) : "memory", "m0");
+}
+
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
 // Element-type traits shared by the fp32 and bf16 instantiations of the memory-bound kernels.
 template <typename T>
 struct Elem;

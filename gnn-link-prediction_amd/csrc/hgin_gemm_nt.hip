@@ -618,22 +618,6 @@ __device__ __forceinline__ void glds16(const void* g, void* lds_wave_base) {
   __builtin_amdgcn_global_load_lds((glb_void_t*)g, (lds_void_t*)lds_wave_base, 16, 0, 0);
 }
 
-// The same DMA issued from inline asm: the compiler does not see it, so it does not guard the kernel's later
-// LDS reads with a vmcnt(0) of its own (which would drain the whole ring); the kernel's counted waits do.
-template <bool kNt = false>
-__device__ __forceinline__ void glds16_asm(const void* g, void* lds_wave_base) {
-  const uint32_t m0 = __builtin_amdgcn_readfirstlane(
-      (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)(lds_wave_base));
-  if constexpr (kNt)
-    asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off nt" ::"v"(g), "s"(m0) : "memory", "m0");
-  else
-    asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(g), "s"(m0) : "memory", "m0");
-}
-
-template <int N>
-__device__ __forceinline__ void wait_vm() {
-  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
-}
 
 constexpr int kBKh = 64;
 

@@ -822,6 +822,253 @@ __global__ __launch_bounds__(256, 2) void k_gemm_tn_bf16_tr(const uint16_t* __re
     }
 }
 
+
+// ---------------------------------------------------------------------------------------------------
+// k_wsd_bf16 — weight-gradient (dW = A^T B, A = g_z [M, N], B = comb [M, K]) in the streaming form of
+// k_ws_bf16 (hgin_gemm_nt.hip) for N, K in {128, 256}: one persistent workgroup per CU of 8 waves holds the
+// WHOLE N x K output in registers (each wave 64 n x K/WK k; 128 accumulator VGPRs at N = K = 256), so A and B are
+// each read exactly once from HBM (the tiled kernel reads every row twice: two 128-column output tiles each).
+// 32-row m-blocks of A and B stream HBM -> LDS by inline-asm LDS-DMA into a 4-deep ring with counted vmcnt
+// waits (nothing else touches vector memory inside the loop); the images are m-major rows with image (b) of
+// k_gemm_tn_bf16_tr (16-B chunk ch of row r at ch ^ (((r & 3) << 2) | ((r >> 2) & 3))), the DMA lanes fetching
+// pre-swizzled sources, and every MFMA fragment is gathered by two ds_read_b64_tr_b16 reads.  Rows past M in
+// the last block are zeroed in LDS before use.  Each workgroup's N x K partial goes to its fp32 slab; the slabs
+// are added by k_slab_reduce in fixed order: deterministic (a different M partition from the tiled kernel,
+// so equal within fp32 reassociation, not bitwise).
+template <int N, int K>
+struct WsdCfg {
+  static constexpr int NT = 512;
+  static constexpr int WM = N / 64;                  // waves along n (64 rows each)
+  static constexpr int WK = 8 / WM;                  // waves along k
+  static constexpr int TK = K / WK / 32;             // 32-col MFMA tiles per wave along k
+  static constexpr int BM = 32;                      // m rows per block
+  static constexpr int RA = N * 2, RB = K * 2;       // image row bytes
+  static constexpr int A_BYTES = BM * RA, B_BYTES = BM * RB;
+  static constexpr int SLOT = A_BYTES + B_BYTES;
+  static constexpr int NST = 4;
+  static constexpr int PA = A_BYTES / 1024 / 8, PB = B_BYTES / 1024 / 8;   // DMA pieces per wave per block
+  static constexpr int P = PA + PB;
+  static_assert(TK >= 1 && A_BYTES % 8192 == 0 && B_BYTES % 8192 == 0 && SLOT * NST <= 147456, "shape");
+};
+
+__device__ __forceinline__ int wsd_swz(int row) { return ((row & 3) << 2) | ((row >> 2) & 3); }
+
+template <int N, int K>
+__global__ __launch_bounds__(512, 1) void k_wsd_bf16(const uint16_t* __restrict__ A, int64_t lda,
+                                                     const uint16_t* __restrict__ B1, int64_t ldb1,
+                                                     const uint16_t* __restrict__ B2, int64_t ldb2, int64_t K1,
+                                                     int64_t M, float* __restrict__ slab, int64_t ld_slab,
+                                                     bool nt_in) {
+  using C = WsdCfg<N, K>;
+  constexpr int NST = C::NST;
+  extern __shared__ __attribute__((aligned(16))) char wsd_smem[];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wm = wave % C::WM, wk = wave / C::WM;
+  const int64_t nblk = (M + C::BM - 1) / C::BM;
+  const int64_t G = gridDim.x;
+  if ((int64_t)blockIdx.x >= nblk) return;
+  const int64_t my = (nblk - 1 - blockIdx.x) / G + 1;
+
+  auto tid_o = [&]() {   // opaque: keeps the per-lane DMA offsets from being hoisted into registers
+    int t;
+    asm volatile("v_mov_b32 %0, %1" : "=v"(t) : "v"(tid));
+    return t;
+  };
+  auto dma = [&](const void* src, void* dst) {
+    if (nt_in) glds16_asm<true>(src, dst); else glds16_asm(src, dst);
+  };
+  const int k1 = (int)K1;
+  auto issue = [&](int64_t i) {
+    char* base = wsd_smem + (int)(i % NST) * C::SLOT;
+    const int64_t r0 = ((int64_t)blockIdx.x + i * G) * C::BM;
+    const int rmax = (int)(M - 1 - r0 < C::BM ? M - 1 - r0 : C::BM - 1);
+    const int ln = tid_o() & 63;
+    const uint16_t* ab = A + r0 * lda;
+    const uint16_t* b1 = B1 + r0 * ldb1;
+    const uint16_t* b2 = B2 + r0 * ldb2;
+#pragma unroll
+    for (int q = 0; q < C::PA; ++q) {
+      const int piece = wave * C::PA + q;
+      const int off = piece * 1024 + ln * 16;
+      int r = off / C::RA;
+      const int c = ((off % C::RA) >> 4) ^ wsd_swz(r);
+      r = r < rmax ? r : rmax;                       // (rows past M are zeroed in LDS before use)
+      dma(ab + (r * (int)lda + c * 8), base + piece * 1024);
+    }
+#pragma unroll
+    for (int q = 0; q < C::PB; ++q) {
+      const int piece = wave * C::PB + q;
+      const int off = piece * 1024 + ln * 16;
+      int r = off / C::RB;
+      const int c = ((off % C::RB) >> 4) ^ wsd_swz(r);
+      r = r < rmax ? r : rmax;
+      const int k = c * 8;
+      dma(k < k1 ? b1 + (r * (int)ldb1 + k) : b2 + (r * (int)ldb2 + (k - k1)), base + C::A_BYTES + piece * 1024);
+    }
+  };
+
+  f32x16 acc[2][C::TK];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < C::TK; ++b)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[a][b][e] = 0.0f;
+
+  // per-lane byte offsets of the two transposed reads of each fragment (k-step kb adds 16 rows):
+  // lane 4q + p of 16-lane group g reads rows 8 (g >> 1) + 4 half + q, columns cb + 16 (g & 1) + 4p .. + 3
+  const int g = lane >> 4, q4 = (lane >> 2) & 3, pp = lane & 3;
+  auto tr_off = [&](int rowbytes, int row, int col) {   // col: first of 4 bf16 read by the lane
+    return rowbytes * row + 16 * ((col >> 3) ^ wsd_swz(row)) + 2 * (col & 7);
+  };
+  const char* lds = wsd_smem;
+  auto tr = [&](int off) { return __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(lds + off)); };
+
+#pragma unroll
+  for (int i = 0; i < NST - 1; ++i)
+    if (i < my) issue(i);
+
+  for (int64_t i = 0; i < my; ++i) {
+    if (i + NST - 2 < my) wait_vm<(NST - 2) * C::P>(); else wait_vm<0>();
+    __builtin_amdgcn_s_barrier();                  // block i landed for every wave; slot of block i-1 is free
+    asm volatile("" ::: "memory");
+    if (i + NST - 1 < my) issue(i + NST - 1);
+    const int sbase = (int)(i % NST) * C::SLOT;
+    const int64_t r0 = ((int64_t)blockIdx.x + i * G) * C::BM;
+    if (r0 + C::BM > M) {                          // the partial last block: zero its rows past M
+      const int valid = (int)(M - r0);
+      uint4* p = reinterpret_cast<uint4*>(wsd_smem + sbase);
+      for (int ch = tid; ch < C::SLOT / 16; ch += C::NT) {
+        const int inb = ch * 16 >= C::A_BYTES;
+        const int row = inb ? (ch * 16 - C::A_BYTES) / C::RB : (ch * 16) / C::RA;
+        if (row >= valid) p[ch] = make_uint4(0u, 0u, 0u, 0u);
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+    }
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int kb = 0; kb < C::BM / 16; ++kb) {
+      bf16x8 fa[2], fb[C::TK];
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        const int col = wm * 64 + t * 32 + 16 * (g & 1) + 4 * pp;
+        const int row = 16 * kb + 8 * (g >> 1) + q4;
+        const bf16x4 a0 = tr(sbase + tr_off(C::RA, row, col)), a1 = tr(sbase + tr_off(C::RA, row + 4, col));
+        fa[t] = __builtin_shufflevector(a0, a1, 0, 1, 2, 3, 4, 5, 6, 7);
+      }
+#pragma unroll
+      for (int t = 0; t < C::TK; ++t) {
+        const int col = wk * (C::TK * 32) + t * 32 + 16 * (g & 1) + 4 * pp;
+        const int row = 16 * kb + 8 * (g >> 1) + q4;
+        const int bb = sbase + C::A_BYTES;
+        const bf16x4 b0 = tr(bb + tr_off(C::RB, row, col)), b1 = tr(bb + tr_off(C::RB, row + 4, col));
+        fb[t] = __builtin_shufflevector(b0, b1, 0, 1, 2, 3, 4, 5, 6, 7);
+      }
+#pragma unroll
+      for (int tm = 0; tm < 2; ++tm)
+#pragma unroll
+        for (int tn = 0; tn < C::TK; ++tn)
+          acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[tm], fb[tn], acc[tm][tn], 0, 0, 0);
+    }
+    __builtin_amdgcn_s_setprio(0);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // this wave's reads of the slot are done
+  }
+  // this workgroup's slab [N][ld_slab] (the caller offsets slab to its column block)
+  float* out = slab + (int64_t)blockIdx.x * N * ld_slab;
+  const int li = lane & 31, lh = lane >> 5;
+#pragma unroll
+  for (int tm = 0; tm < 2; ++tm)
+#pragma unroll
+    for (int tn = 0; tn < C::TK; ++tn) {
+      const int k = wk * (C::TK * 32) + tn * 32 + li;
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int n = wm * 64 + tm * 32 + (e & 3) + 8 * (e >> 2) + 4 * lh;
+        out[n * ld_slab + k] = acc[tm][tn][e];
+      }
+    }
+}
+
+// Weight-stationary dW launch (HGIN_TN_WS = 0 / 1; default on): bf16, N in {128, 256}, K in {128, 256, 512},
+// k1 a multiple of 8, 16-B aligned rows (leading dimensions multiples of 8, below 2^24).  Returns the slab
+// count, or 0 when it does not apply.
+bool wsd_enabled() {
+  static const bool on = [] {
+    const char* v = getenv("HGIN_TN_WS");
+    return !(v && v[0] == '0');
+  }();
+  return on;
+}
+
+int64_t wsd_cus() {
+  static const int64_t g = [] {
+    int dev = 0;
+    hipDeviceProp_t prop;
+    if (hipGetDevice(&dev) != hipSuccess || hipGetDeviceProperties(&prop, dev) != hipSuccess) return int64_t(256);
+    return (int64_t)prop.multiProcessorCount;
+  }();
+  return g;
+}
+
+template <int NV, int KV>
+int64_t launch_wsd(const uint16_t* a, int64_t lda, const uint16_t* b1, int64_t ldb1, const uint16_t* b2,
+                   int64_t ldb2, int64_t k1, int64_t M, float* slab, int64_t ld_slab, int64_t grid, hipStream_t s) {
+  constexpr int lds = WsdCfg<NV, KV>::SLOT * WsdCfg<NV, KV>::NST;
+  auto kern = k_wsd_bf16<NV, KV>;
+  static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                                                     hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+  if (attr != hipSuccess) return 0;
+  static const bool nt = [] {
+    const char* v = getenv("HGIN_WS_NT");
+    return !(v && v[0] == '0');
+  }();
+  kern<<<(unsigned)grid, 512, lds, s>>>(a, lda, b1, ldb1, b2, ldb2, k1, M, slab, ld_slab, nt);
+  return grid;
+}
+
+// One weight-stationary pass over output columns [c0, c0 + KV) of B = [b1 (k1 columns) | b2].
+template <int NV, int KV>
+int64_t wsd_cols(const uint16_t* a, int64_t lda, const uint16_t* b1, int64_t ldb1, int64_t k1, const uint16_t* b2,
+                 int64_t ldb2, int64_t c0, int64_t M, float* slab, int64_t ld_slab, int64_t grid, hipStream_t s) {
+  // the column block's two sources: [c0, k1) from b1, [max(c0, k1), c0 + KV) from b2
+  const int64_t kk1 = k1 > c0 ? (k1 - c0 < KV ? k1 - c0 : KV) : 0;
+  const uint16_t* p1 = kk1 > 0 ? b1 + c0 : b2;
+  const int64_t l1 = kk1 > 0 ? ldb1 : ldb2;
+  const uint16_t* p2 = kk1 < KV ? b2 + (c0 + kk1 - k1) : p1;
+  const int64_t l2 = kk1 < KV ? ldb2 : l1;
+  return launch_wsd<NV, KV>(a, lda, p1, l1, p2, l2, kk1, M, slab + c0, ld_slab, grid, s);
+}
+
+int64_t try_wsd_bf16(const uint16_t* a, int64_t lda, const uint16_t* b1, int64_t ldb1, int64_t k1,
+                     const uint16_t* b2, int64_t ldb2, int64_t M, int64_t N, int64_t K, float* slab,
+                     int64_t max_slabs, hipStream_t s) {
+  if (!wsd_enabled() || M < 1 || (N != 128 && N != 256) || (K != 128 && K != 256 && K != 512) || k1 % 8) return 0;
+  auto ok = [](const void* p, int64_t ld) { return aligned16(p) && ld % 8 == 0 && ld < (int64_t(1) << 24); };
+  if (!ok(a, lda) || (k1 > 0 && !ok(b1, ldb1)) || (k1 < K && !ok(b2, ldb2))) return 0;
+  const int64_t nblk = ceil_div(M, (int64_t)32);
+  int64_t grid = wsd_cus();
+  if (grid > nblk) grid = nblk;
+  if (grid > max_slabs) grid = max_slabs;
+  // K = 512 (the first layer's [aggregate | x_dst]): two 256-column passes into the same slabs (A read twice,
+  // B once; the tiled kernel reads both twice)
+  if (K == 512) {
+    if (N == 256) {
+      if (!wsd_cols<256, 256>(a, lda, b1, ldb1, k1, b2, ldb2, 0, M, slab, K, grid, s)) return 0;
+      return wsd_cols<256, 256>(a, lda, b1, ldb1, k1, b2, ldb2, 256, M, slab, K, grid, s);
+    }
+    if (!wsd_cols<128, 256>(a, lda, b1, ldb1, k1, b2, ldb2, 0, M, slab, K, grid, s)) return 0;
+    return wsd_cols<128, 256>(a, lda, b1, ldb1, k1, b2, ldb2, 256, M, slab, K, grid, s);
+  }
+  if (N == 256 && K == 256) return wsd_cols<256, 256>(a, lda, b1, ldb1, k1, b2, ldb2, 0, M, slab, K, grid, s);
+  if (N == 256 && K == 128) return wsd_cols<256, 128>(a, lda, b1, ldb1, k1, b2, ldb2, 0, M, slab, K, grid, s);
+  if (N == 128 && K == 256) return wsd_cols<128, 256>(a, lda, b1, ldb1, k1, b2, ldb2, 0, M, slab, K, grid, s);
+  return wsd_cols<128, 128>(a, lda, b1, ldb1, k1, b2, ldb2, 0, M, slab, K, grid, s);
+}
+
 bool tn_is_small(int64_t N, int64_t K) { return N < 16 || K < 16; }
 
 // bf16 dW kernel: transposed LDS reads (default) or the register-transposing kernel (HGIN_TN_BF16=regt).
@@ -870,8 +1117,16 @@ int64_t tn_splits(int64_t M, int64_t N, int64_t K, int64_t stage_rows = kTnBM, i
   return S < 1 ? 1 : S;
 }
 
-size_t tn_ws_bytes(int64_t M, int64_t N, int64_t K) {
+// Slabs the workspace holds: the split count, or one per CU (up to 256) for the weight-stationary bf16 dW.
+int64_t tn_ws_slabs(int64_t M, int64_t N, int64_t K) {
   const int64_t S = tn_splits(M, N, K);
+  if (tn_is_small(N, K) || N > 256 || K > 512) return S;
+  const int64_t w = ceil_div(M > 0 ? M : 1, 32) < 256 ? ceil_div(M > 0 ? M : 1, 32) : 256;
+  return S > w ? S : w;
+}
+
+size_t tn_ws_bytes(int64_t M, int64_t N, int64_t K) {
+  const int64_t S = tn_ws_slabs(M, N, K);
   return align_up(sizeof(float) * (size_t)(S * N * K), 256) + align_up(sizeof(float) * (size_t)(ceil_div(S, kSlabGroup) * N * K), 256);
 }
 
@@ -937,11 +1192,11 @@ int gemm_tn_impl(const char* what, const T* a, int64_t lda, const T* b1, int64_t
   const int64_t stage = (kHalf && !small) ? kTnBMh : kTnBM;
   const int64_t S = tn_splits(M, N, K, stage, tn_target_wgs());   // <= the workspace's split count
   const int64_t rows = ceil_div(ceil_div(M, S), stage) * stage;
-  const int64_t S_eff = ceil_div(M, rows);
+  int64_t S_eff = ceil_div(M, rows);
   const int64_t NK = N * K;
   float* slab = static_cast<float*>(workspace);
   float* part = reinterpret_cast<float*>(static_cast<char*>(workspace) +
-                                         align_up(sizeof(float) * (size_t)(tn_splits(M, N, K) * NK), 256));
+                                         align_up(sizeof(float) * (size_t)(tn_ws_slabs(M, N, K) * NK), 256));
   TnPro pro{};
   if (pro_in) {
     pro = *pro_in;
@@ -955,6 +1210,13 @@ int gemm_tn_impl(const char* what, const T* a, int64_t lda, const T* b1, int64_t
   if (small) {
     HGIN_ARG_CHECK(!pro_in, "%s: no fused prologue for N or K < 16", what);
     k_tn_small<T><<<(unsigned)S_eff, 256, 0, s>>>(a, lda, b1, ldb1, b2, ldb2, k1, M, (int)N, (int)K, rows, slab);
+  } else if (int64_t g = (kHalf && !pro_in && vec)
+                             ? try_wsd_bf16(reinterpret_cast<const uint16_t*>(a), lda,
+                                            reinterpret_cast<const uint16_t*>(b1), ldb1, k1,
+                                            reinterpret_cast<const uint16_t*>(b2), ldb2, M, N, K, slab,
+                                            tn_ws_slabs(M, N, K), s)
+                             : 0) {
+    S_eff = g;   // one slab per weight-stationary workgroup
   } else if constexpr (kHalf) {
     const int64_t tiles_n = ceil_div(N, 128);
     const TnGrid tg{128, tiles_n, tiles_n * ceil_div(K, 128), tiles_n * ceil_div(K, 128) * S_eff, xcd_remap_enabled()};

@@ -1,8 +1,8 @@
 """Child process of tests/test_gpu_gemm_switch.py: the bf16 GIN MLP GEMM (hgin_gin_mlp_fwd_bf16) at the shapes
 of the weight-stationary kernel (K 128 / 256 / 512, N 128 / 256; ragged M, M below one block, many blocks
 per workgroup; accum / z present or not; a two-source A) under the process-static HGIN_* switches its parent
-set.  Checks every output against an fp32 evaluation of the same bf16 operands and saves them, so the parent
-can compare switch settings bit for bit.
+set.  Also the dX GEMMs (plain and combine) and the bf16 weight-gradient GEMM.  Checks every output against an
+fp32 / fp64 evaluation of the same bf16 operands and saves them, so the parent can compare switch settings.
 
     python tests/gemm_child.py OUT.pt
 """
@@ -92,11 +92,28 @@ def run_dx(M, K, N, comb, *, g):
     return out
 
 
+DW_CASES = [  # (M, N, K, k1 of a two-source B or 0) — the bf16 weight-gradient GEMM (ops.gemm_tn)
+    (300_007, 256, 256, 0), (1, 256, 256, 0), (45, 256, 128, 0), (100_000, 128, 256, 128), (77_777, 128, 128, 0),
+    (64_001, 256, 256, 256), (200_003, 256, 512, 256), (9_000, 128, 512, 200), (5, 256, 512, 0),
+]
+
+
+def run_dw(M, N, K, k1, *, g):
+    a = torch.randn(M, N, device="cuda", generator=g).to(BF)
+    b = torch.randn(M, K, device="cuda", generator=g).to(BF)
+    out = ops.gemm_tn(a, b[:, :k1].contiguous(), b[:, k1:].contiguous()) if k1 else ops.gemm_tn(a, b)
+    ref = a.double().t() @ b.double()
+    bound = 1e-5 * (a.double().abs().t() @ b.double().abs()) + 1e-6
+    assert bool(((out.double() - ref).abs() <= bound).all()), (M, N, K)
+    return {"tol_dw": out.cpu()}
+
+
 def main():
     torch.cuda.init()
     g = torch.Generator(device="cuda").manual_seed(7)
     res = {f"{c}": run(*c, g=g) for c in CASES}
     res.update({f"dx{c}": run_dx(*c, g=g) for c in DX_CASES})
+    res.update({f"dw{c}": run_dw(*c, g=g) for c in DW_CASES})
     torch.save(res, sys.argv[1])
     print("gemm child ok", {k: v for k, v in os.environ.items() if k.startswith("HGIN_")}, flush=True)
 

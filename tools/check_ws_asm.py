@@ -1,4 +1,5 @@
-"""Static check of the weight-stationary kernels (k_ws_bf16) in the gfx950 assembly of hgin_gemm_nt.hip: the
+"""Static check of the weight-stationary kernels (k_ws_bf16 in hgin_gemm_nt.hip, k_wsd_bf16 in hgin_gemm_tn.hip)
+in their gfx950 assembly: the
 counted-vmcnt ring is only correct when the loop holds no compiler-visible vector-memory load (the compiler's
 own waits would not count the inline-asm DMAs), so every instantiation must have no scratch (spill) traffic,
 and its only global loads must be the W-slice / bias loads of the prologue.
@@ -12,24 +13,26 @@ import sys
 import tempfile
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-SRC = os.path.join(ROOT, "gnn-link-prediction_amd", "csrc", "hgin_gemm_nt.hip")
+SRCS = [os.path.join(ROOT, "gnn-link-prediction_amd", "csrc", f) for f in ("hgin_gemm_nt.hip", "hgin_gemm_tn.hip")]
 
 
 def main():
+    s = ""
     with tempfile.TemporaryDirectory() as d:
-        out = os.path.join(d, "nt.s")
-        cmd = ["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "-ffp-contract=off", "--offload-arch=gfx950",
-               "--offload-device-only", "-S", "-I", os.path.join(ROOT, "include"), "-o", out, SRC]
-        subprocess.run(cmd, check=True, capture_output=True)
-        s = open(out).read()
+        for i, src in enumerate(SRCS):
+            out = os.path.join(d, f"k{i}.s")
+            cmd = ["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "-ffp-contract=off", "--offload-arch=gfx950",
+                   "--offload-device-only", "-S", "-I", os.path.join(ROOT, "include"), "-o", out, src]
+            subprocess.run(cmd, check=True, capture_output=True)
+            s += open(out).read()
     bad = 0
-    for m in re.finditer(r"^(_ZN4hgin12_GLOBAL__N_19k_ws_bf16\S*):", s, re.M):
+    for m in re.finditer(r"^(_ZN4hgin12_GLOBAL__N_1\d+k_wsd?_bf16\S*):", s, re.M):
         body = s[m.end():s.index(".Lfunc_end", m.end())]
         loop = body[body.find("Loop Header"):] if "Loop Header" in body else body
         scratch = len(re.findall(r"\bscratch_(load|store)|buffer_(load|store)_dword\S* \S+, off, s\[0:3\]", body))
         loads_in_loop = len(re.findall(r"\bglobal_load_(?!lds)\w+", loop))
         waits = sorted(set(int(x) for x in re.findall(r"s_waitcnt vmcnt\((\d+)\)", loop)))
-        name = re.search(r"bf16(I.*)EEEv", m.group(1)).group(1)
+        name = re.search(r"(k_wsd?_bf16I.*?)EEEv", m.group(1)).group(1)
         ok = scratch == 0 and loads_in_loop == 0
         bad += not ok
         print(f"{'ok ' if ok else 'BAD'} {name}: scratch ops {scratch}, VGPR-destination global loads in the loop "
