@@ -993,6 +993,189 @@ __global__ __launch_bounds__(512, 1) void k_wsd_bf16(const uint16_t* __restrict_
     }
 }
 
+// k_wsd_f32 — the fp32 weight gradient in the same streaming form (split mode: six bf16 products per pair, the
+// k_gemm_tn_partial arithmetic).  16-row m-blocks of A and B (fp32, linear images) stream HBM -> LDS by DMA into
+// a 3-deep ring; per block one pass splits both into three bf16 planes (each element once per CU, into
+// swizzled m-major plane images read by ds_read_b64_tr_b16), then each wave runs its 2 x TK tiles x 6 products.
+template <int N, int K>
+struct WsdF32Cfg {
+  static constexpr int NT = 512;
+  static constexpr int WM = N / 64, WK = 8 / WM, TK = K / WK / 32;
+  static constexpr int BM = 16;                              // one 16-deep MFMA k-step per block
+  static constexpr int A_BYTES = BM * N * 4, B_BYTES = BM * K * 4;
+  static constexpr int SLOT = A_BYTES + B_BYTES;
+  static constexpr int NST = 3;
+  static constexpr int PA_ROW = N * 2, PB_ROW = K * 2;       // plane image row bytes (bf16)
+  static constexpr int PA_BYTES = BM * PA_ROW, PB_BYTES = BM * PB_ROW;   // one plane
+  static constexpr int PLANES = 3 * (PA_BYTES + PB_BYTES);
+  static constexpr int LDS = SLOT * NST + PLANES;
+  static constexpr int PA = A_BYTES / 1024 / 8, PB = B_BYTES / 1024 / 8;
+  static constexpr int P = PA + PB;
+  static_assert(TK >= 1 && A_BYTES % 8192 == 0 && B_BYTES % 8192 == 0 && LDS <= 147456, "shape");
+};
+
+template <int N, int K>
+__global__ __launch_bounds__(512, 1) void k_wsd_f32(const float* __restrict__ A, int64_t lda,
+                                                    const float* __restrict__ B1, int64_t ldb1,
+                                                    const float* __restrict__ B2, int64_t ldb2, int64_t K1, int64_t M,
+                                                    float* __restrict__ slab, int64_t ld_slab, bool nt_in) {
+  using C = WsdF32Cfg<N, K>;
+  constexpr int NST = C::NST;
+  extern __shared__ __attribute__((aligned(16))) char wsdf_smem[];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wm = wave % C::WM, wk = wave / C::WM;
+  const int64_t nblk = (M + C::BM - 1) / C::BM;
+  const int64_t G = gridDim.x;
+  if ((int64_t)blockIdx.x >= nblk) return;
+  const int64_t my = (nblk - 1 - blockIdx.x) / G + 1;
+  char* const planes = wsdf_smem + C::SLOT * NST;
+
+  auto tid_o = [&]() {
+    int t;
+    asm volatile("v_mov_b32 %0, %1" : "=v"(t) : "v"(tid));
+    return t;
+  };
+  auto dma = [&](const void* src, void* dst) {
+    if (nt_in) glds16_asm<true>(src, dst); else glds16_asm(src, dst);
+  };
+  const int k1 = (int)K1;
+  auto issue = [&](int64_t i) {
+    char* base = wsdf_smem + (int)(i % NST) * C::SLOT;
+    const int64_t r0 = ((int64_t)blockIdx.x + i * G) * C::BM;
+    const int rmax = (int)(M - 1 - r0 < C::BM ? M - 1 - r0 : C::BM - 1);
+    const int ln = tid_o() & 63;
+    const float* ab = A + r0 * lda;
+    const float* b1 = B1 + r0 * ldb1;
+    const float* b2 = B2 + r0 * ldb2;
+#pragma unroll
+    for (int q = 0; q < C::PA; ++q) {
+      const int piece = wave * C::PA + q;
+      const int off = piece * 1024 + ln * 16;
+      int r = off / (N * 4);
+      r = r < rmax ? r : rmax;                       // (rows past M are zeroed at the split)
+      dma(ab + (r * (int)lda + (off % (N * 4)) / 4), base + piece * 1024);
+    }
+#pragma unroll
+    for (int q = 0; q < C::PB; ++q) {
+      const int piece = wave * C::PB + q;
+      const int off = piece * 1024 + ln * 16;
+      int r = off / (K * 4);
+      r = r < rmax ? r : rmax;
+      const int k = (off % (K * 4)) / 4;
+      dma(k < k1 ? b1 + (r * (int)ldb1 + k) : b2 + (r * (int)ldb2 + (k - k1)), base + C::A_BYTES + piece * 1024);
+    }
+  };
+
+  f32x16 acc[2][C::TK];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < C::TK; ++b)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[a][b][e] = 0.0f;
+
+  const int g = lane >> 4, q4 = (lane >> 2) & 3, pp = lane & 3;
+  auto tr_off = [&](int rowbytes, int row, int col) {
+    return rowbytes * row + 16 * ((col >> 3) ^ wsd_swz(row)) + 2 * (col & 7);
+  };
+  auto tr = [&](int off) { return __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(wsdf_smem + off)); };
+
+#pragma unroll
+  for (int i = 0; i < NST - 1; ++i)
+    if (i < my) issue(i);
+
+  for (int64_t i = 0; i < my; ++i) {
+    if (i + NST - 2 < my) wait_vm<(NST - 2) * C::P>(); else wait_vm<0>();
+    __builtin_amdgcn_s_barrier();   // block i landed for every wave; slot i-1 and the plane images are free
+    asm volatile("" ::: "memory");
+    if (i + NST - 1 < my) issue(i + NST - 1);
+    const char* fbase = wsdf_smem + (int)(i % NST) * C::SLOT;
+    const int64_t r0 = ((int64_t)blockIdx.x + i * G) * C::BM;
+    const int valid = M - r0 < C::BM ? (int)(M - r0) : C::BM;
+    {   // split both fp32 images into three bf16 planes (8 consecutive columns = one 16-B chunk per plane)
+      const int t = tid_o();
+      constexpr int CA = C::BM * N / 8, CT = C::BM * (N + K) / 8;   // 8-element groups
+#pragma unroll
+      for (int q = 0; q < (CT + C::NT - 1) / C::NT; ++q) {
+        const int grp = q * C::NT + t;
+        if (CT % C::NT != 0 && grp >= CT) break;
+        const bool isA = grp < CA;
+        const int cols = isA ? N : K;
+        const int e0 = (isA ? grp : grp - CA) * 8;
+        const int row = e0 / cols, col = e0 % cols;
+        const float* src = reinterpret_cast<const float*>(fbase + (isA ? 0 : C::A_BYTES)) + e0;
+        float4 v0 = *reinterpret_cast<const float4*>(src), v1 = *reinterpret_cast<const float4*>(src + 4);
+        if (row >= valid) v0 = v1 = make_float4(0.f, 0.f, 0.f, 0.f);
+        uint2 o0[3], o1[3];
+        split4(v0, o0);
+        split4(v1, o1);
+        const int prow = isA ? C::PA_ROW : C::PB_ROW;
+        char* pl = planes + (isA ? 0 : 3 * C::PA_BYTES);
+        const int pbytes = isA ? C::PA_BYTES : C::PB_BYTES;
+        const int off = prow * row + 16 * ((col >> 3) ^ wsd_swz(row));
+#pragma unroll
+        for (int p = 0; p < 3; ++p)
+          *reinterpret_cast<uint4*>(pl + p * pbytes + off) = make_uint4(o0[p].x, o0[p].y, o1[p].x, o1[p].y);
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    const int pa0 = C::SLOT * NST, pb0 = pa0 + 3 * C::PA_BYTES;
+    bf16x8 fa[2][3];
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const int col = wm * 64 + t * 32 + 16 * (g & 1) + 4 * pp;
+      const int row = 8 * (g >> 1) + q4;
+#pragma unroll
+      for (int p = 0; p < 3; ++p) {
+        const int o = pa0 + p * C::PA_BYTES;
+        const bf16x4 a0 = tr(o + tr_off(C::PA_ROW, row, col)), a1 = tr(o + tr_off(C::PA_ROW, row + 4, col));
+        fa[t][p] = __builtin_shufflevector(a0, a1, 0, 1, 2, 3, 4, 5, 6, 7);
+      }
+    }
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int tn = 0; tn < C::TK; ++tn) {
+      bf16x8 fb[3];
+      const int col = wk * (C::TK * 32) + tn * 32 + 16 * (g & 1) + 4 * pp;
+      const int row = 8 * (g >> 1) + q4;
+#pragma unroll
+      for (int p = 0; p < 3; ++p) {
+        const int o = pb0 + p * C::PB_BYTES;
+        const bf16x4 b0 = tr(o + tr_off(C::PB_ROW, row, col)), b1 = tr(o + tr_off(C::PB_ROW, row + 4, col));
+        fb[p] = __builtin_shufflevector(b0, b1, 0, 1, 2, 3, 4, 5, 6, 7);
+      }
+#pragma unroll
+      for (int tm = 0; tm < 2; ++tm) {   // k_gemm_tn_partial's order: smallest terms first
+        acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[tm][2], fb[0], acc[tm][tn], 0, 0, 0);
+        acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[tm][1], fb[1], acc[tm][tn], 0, 0, 0);
+        acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[tm][0], fb[2], acc[tm][tn], 0, 0, 0);
+        acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[tm][1], fb[0], acc[tm][tn], 0, 0, 0);
+        acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[tm][0], fb[1], acc[tm][tn], 0, 0, 0);
+        acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[tm][0], fb[0], acc[tm][tn], 0, 0, 0);
+      }
+    }
+    __builtin_amdgcn_s_setprio(0);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  }
+  float* out = slab + (int64_t)blockIdx.x * N * ld_slab;
+  const int li = lane & 31, lh = lane >> 5;
+#pragma unroll
+  for (int tm = 0; tm < 2; ++tm)
+#pragma unroll
+    for (int tn = 0; tn < C::TK; ++tn) {
+      const int k = wk * (C::TK * 32) + tn * 32 + li;
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int n = wm * 64 + tm * 32 + (e & 3) + 8 * (e >> 2) + 4 * lh;
+        out[n * ld_slab + k] = acc[tm][tn][e];
+      }
+    }
+}
+
 // Weight-stationary dW launch (HGIN_TN_WS = 0 / 1; default on): bf16, N in {128, 256}, K in {128, 256, 512},
 // k1 a multiple of 8, 16-B aligned rows (leading dimensions multiples of 8, below 2^24).  Returns the slab
 // count, or 0 when it does not apply.
@@ -1030,26 +1213,44 @@ int64_t launch_wsd(const uint16_t* a, int64_t lda, const uint16_t* b1, int64_t l
   return grid;
 }
 
-// One weight-stationary pass over output columns [c0, c0 + KV) of B = [b1 (k1 columns) | b2].
 template <int NV, int KV>
-int64_t wsd_cols(const uint16_t* a, int64_t lda, const uint16_t* b1, int64_t ldb1, int64_t k1, const uint16_t* b2,
+int64_t launch_wsd(const float* a, int64_t lda, const float* b1, int64_t ldb1, const float* b2, int64_t ldb2,
+                   int64_t k1, int64_t M, float* slab, int64_t ld_slab, int64_t grid, hipStream_t s) {
+  constexpr int lds = WsdF32Cfg<NV, KV>::LDS;
+  auto kern = k_wsd_f32<NV, KV>;
+  static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                                                     hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+  if (attr != hipSuccess) return 0;
+  static const bool nt = [] {
+    const char* v = getenv("HGIN_WS_NT");
+    return !(v && v[0] == '0');
+  }();
+  kern<<<(unsigned)grid, 512, lds, s>>>(a, lda, b1, ldb1, b2, ldb2, k1, M, slab, ld_slab, nt);
+  return grid;
+}
+
+// One weight-stationary pass over output columns [c0, c0 + KV) of B = [b1 (k1 columns) | b2].
+template <int NV, int KV, typename T>
+int64_t wsd_cols(const T* a, int64_t lda, const T* b1, int64_t ldb1, int64_t k1, const T* b2,
                  int64_t ldb2, int64_t c0, int64_t M, float* slab, int64_t ld_slab, int64_t grid, hipStream_t s) {
   // the column block's two sources: [c0, k1) from b1, [max(c0, k1), c0 + KV) from b2
   const int64_t kk1 = k1 > c0 ? (k1 - c0 < KV ? k1 - c0 : KV) : 0;
-  const uint16_t* p1 = kk1 > 0 ? b1 + c0 : b2;
+  const T* p1 = kk1 > 0 ? b1 + c0 : b2;
   const int64_t l1 = kk1 > 0 ? ldb1 : ldb2;
-  const uint16_t* p2 = kk1 < KV ? b2 + (c0 + kk1 - k1) : p1;
+  const T* p2 = kk1 < KV ? b2 + (c0 + kk1 - k1) : p1;
   const int64_t l2 = kk1 < KV ? ldb2 : l1;
   return launch_wsd<NV, KV>(a, lda, p1, l1, p2, l2, kk1, M, slab + c0, ld_slab, grid, s);
 }
 
-int64_t try_wsd_bf16(const uint16_t* a, int64_t lda, const uint16_t* b1, int64_t ldb1, int64_t k1,
-                     const uint16_t* b2, int64_t ldb2, int64_t M, int64_t N, int64_t K, float* slab,
-                     int64_t max_slabs, hipStream_t s) {
-  if (!wsd_enabled() || M < 1 || (N != 128 && N != 256) || (K != 128 && K != 256 && K != 512) || k1 % 8) return 0;
-  auto ok = [](const void* p, int64_t ld) { return aligned16(p) && ld % 8 == 0 && ld < (int64_t(1) << 24); };
+template <typename T>
+int64_t try_wsd(const T* a, int64_t lda, const T* b1, int64_t ldb1, int64_t k1, const T* b2, int64_t ldb2,
+                int64_t M, int64_t N, int64_t K, float* slab, int64_t max_slabs, hipStream_t s) {
+  constexpr int64_t vw = 16 / sizeof(T);   // elements per 16-B chunk
+  if (!wsd_enabled() || M < 1 || (N != 128 && N != 256) || (K != 128 && K != 256 && K != 512) || k1 % vw) return 0;
+  if (sizeof(T) == 4 && !gemm_split_enabled()) return 0;   // the exact-f32 MFMA mode keeps the tiled kernel
+  auto ok = [](const void* p, int64_t ld) { return aligned16(p) && ld % vw == 0 && ld < (int64_t(1) << 24); };
   if (!ok(a, lda) || (k1 > 0 && !ok(b1, ldb1)) || (k1 < K && !ok(b2, ldb2))) return 0;
-  const int64_t nblk = ceil_div(M, (int64_t)32);
+  const int64_t nblk = ceil_div(M, (int64_t)(sizeof(T) == 2 ? 32 : 16));
   int64_t grid = wsd_cus();
   if (grid > nblk) grid = nblk;
   if (grid > max_slabs) grid = max_slabs;
@@ -1210,12 +1411,9 @@ int gemm_tn_impl(const char* what, const T* a, int64_t lda, const T* b1, int64_t
   if (small) {
     HGIN_ARG_CHECK(!pro_in, "%s: no fused prologue for N or K < 16", what);
     k_tn_small<T><<<(unsigned)S_eff, 256, 0, s>>>(a, lda, b1, ldb1, b2, ldb2, k1, M, (int)N, (int)K, rows, slab);
-  } else if (int64_t g = (kHalf && !pro_in && vec)
-                             ? try_wsd_bf16(reinterpret_cast<const uint16_t*>(a), lda,
-                                            reinterpret_cast<const uint16_t*>(b1), ldb1, k1,
-                                            reinterpret_cast<const uint16_t*>(b2), ldb2, M, N, K, slab,
-                                            tn_ws_slabs(M, N, K), s)
-                             : 0) {
+  } else if (int64_t g = (!pro_in && vec) ? try_wsd<T>(a, lda, b1, ldb1, k1, b2, ldb2, M, N, K, slab,
+                                                        tn_ws_slabs(M, N, K), s)
+                                          : 0) {
     S_eff = g;   // one slab per weight-stationary workgroup
   } else if constexpr (kHalf) {
     const int64_t tiles_n = ceil_div(N, 128);

@@ -95,12 +95,15 @@ def run_dx(M, K, N, comb, *, g):
 DW_CASES = [  # (M, N, K, k1 of a two-source B or 0) — the bf16 weight-gradient GEMM (ops.gemm_tn)
     (300_007, 256, 256, 0), (1, 256, 256, 0), (45, 256, 128, 0), (100_000, 128, 256, 128), (77_777, 128, 128, 0),
     (64_001, 256, 256, 256), (200_003, 256, 512, 256), (9_000, 128, 512, 200), (5, 256, 512, 0),
+    # fp32 (split mode: k_wsd_f32 by default)
+    (300_001, 256, 256, 0, torch.float32), (17, 256, 128, 0, torch.float32), (80_000, 128, 256, 128, torch.float32),
+    (60_000, 256, 512, 256, torch.float32), (4_001, 128, 128, 0, torch.float32),
 ]
 
 
-def run_dw(M, N, K, k1, *, g):
-    a = torch.randn(M, N, device="cuda", generator=g).to(BF)
-    b = torch.randn(M, K, device="cuda", generator=g).to(BF)
+def run_dw(M, N, K, k1, dt=BF, *, g):
+    a = torch.randn(M, N, device="cuda", generator=g).to(dt)
+    b = torch.randn(M, K, device="cuda", generator=g).to(dt)
     out = ops.gemm_tn(a, b[:, :k1].contiguous(), b[:, k1:].contiguous()) if k1 else ops.gemm_tn(a, b)
     ref = a.double().t() @ b.double()
     bound = 1e-5 * (a.double().abs().t() @ b.double().abs()) + 1e-6
