@@ -16,6 +16,9 @@ fp32 — the graph the north star's >= 60 %-of-HBM aggregate target is stated on
     that of sqrt(mape) over all paths).  Total work is fixed as N grows: "strong" scaling.
   ``--config cfg4`` runs the 8-component graph at N = 1 too (the 1-GPU point of the cfg4 curve); ``cfg5`` is
   cfg3 in bf16 (configs[4]); ``cfg2`` is configs[1].
+  ``--partition dst-range`` (reported, not the headline): the connected graph itself over N ranks, each owning
+  1/N of every node type's rows and the edges into them; per layer the source embeddings are all-gathered and
+  their gradients reduce-scattered over RCCL (hgin/partition.py).
 
 value = E_conv(total) / t_step, E_conv = edges of the four convolved relations (p->l, l->p, l->n, n->l),
 counted once per step.  t_step = max over ranks of (barrier + hipDeviceSynchronize
@@ -58,9 +61,10 @@ def parse():
     ap.add_argument("--config", default="cfg3",
                     help="cfg3 (default, BASELINE configs[2]; N > 1: cfg4's 8-component split), cfg4, cfg5 (bf16), "
                          "cfg2, cfg2bf (bf16 at cfg2 size)")
-    ap.add_argument("--partition", choices=("auto", "connected", "components"), default="auto",
+    ap.add_argument("--partition", choices=("auto", "connected", "components", "dst-range"), default="auto",
                     help="auto: connected graph at N = 1 (cfg4: components), 8 components split over the ranks "
-                         "at N > 1")
+                         "at N > 1; dst-range: the connected graph with destination rows split over the ranks "
+                         "(SURVEY.md §8.E connected-graph variant: per-layer all-gather / reduce-scatter)")
     ap.add_argument("--skew", choices=("uniform", "zipf"), default="uniform",
                     help="zipf: destination ids ~ Zipf(1.1) (SURVEY.md §8.D skew variant)")
     ap.add_argument("--prune-dead", action="store_true", help="skip dead relations (reported separately)")
@@ -234,6 +238,8 @@ def main():
     from hgin.data import CONFIGS, rank_components, synthetic_graph
     from hgin.dist import GradAllReducer
     from hgin.graphs import CapturedStaticStep
+    from hgin.partition import DstRangePartition
+    from hgin.partition import train_step as partition_step
     from hgin.train import train_step
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -266,16 +272,35 @@ def main():
         scaling = "strong"
         part_desc = (f"{n_comp} independent components of {cfg.name}'s totals ({cfg.conv_edges // n_comp} convolved "
                      f"edges each), {len(comp_ids)} per rank")
+    elif partition == "dst-range":
+        full = synthetic_graph(cfg, seed=0, device=dev)
+        if args.skew == "zipf":
+            full = zipf_dst(cfg, full, dev)
+        dst_part = DstRangePartition({t: full.num_nodes(t) for t in full.x})
+        graph = dst_part.local_graph(full)
+        del full
+        comp_ids = [0]
+        total_conv_edges = cfg.conv_edges
+        scaling = "strong"
+        elem = 2 if cfg.feat_dtype == "bf16" else 4
+        widths0 = {"path": cfg.f_path, "link": cfg.f_link, "node": cfg.f_node}
+        widths = {t: cfg.hidden for t in widths0}
+        # forward: one all-gather per layer; backward: one reduce-scatter per layer above the first (the raw
+        # features need no gradient)
+        xchg = dst_part.exchange_bytes(widths0, elem) + (2 * cfg.layers - 1) * dst_part.exchange_bytes(widths, elem)
+        part_desc = (f"one connected graph, destination rows of every node type split over {world} rank(s) "
+                     f"(per-layer all-gather of source embeddings / reduce-scatter of their gradients, "
+                     f"{xchg / 1e9:.2f} GB received per rank per step)")
     else:
         if world > 1:
             raise SystemExit("--partition connected: one connected graph per rank is not a data-parallel split of "
-                             "one workload; use components")
+                             "one workload; use components or dst-range")
         graph = synthetic_graph(cfg, seed=0, device=dev)
         comp_ids = [0]
         total_conv_edges = cfg.conv_edges
         scaling = "strong"
         part_desc = "one connected graph"
-    if args.skew == "zipf":
+    if args.skew == "zipf" and partition != "dst-range":
         graph = zipf_dst(cfg, graph, dev)
     torch.manual_seed(1997)
     model = HetroGIN(**cfg.model_kwargs({"link": cfg.f_link, "path": cfg.f_path, "node": cfg.f_node})).to(dev)
@@ -284,17 +309,24 @@ def main():
     # capturable Adam: the optimizer step is part of the replayed graph (same update rule and arithmetic)
     opt = torch.optim.Adam(lr=1e-3, params=model.parameters(), weight_decay=0, capturable=args.graph,
                            **({"fused": True} if args.adam == "fused" else {}))
-    reducer = GradAllReducer(model.parameters()) if world > 1 else None
+    reducer = GradAllReducer(model.parameters()) if (world > 1 or partition == "dst-range") else None
 
     def barrier():
         if world > 1:
             dist.barrier(device_ids=[dev.index]) if backend == "nccl" else dist.barrier()
 
+    # the dst-range graph is a rank's share (local destination ids, global source ids): no standalone extras
+    no_extras = args.no_extras or partition == "dst-range"
     csr_ms = None
-    if rank == 0 and not args.no_extras:
+    if rank == 0 and not no_extras:
         csr_ms = csr_build_ms(graph, dev)     # separate cold builds; the model builds its own cached copies
 
-    eager_step = lambda: train_step(model, opt, graph, reducer=reducer)  # noqa: E731
+    if partition == "dst-range":
+        if args.graph:
+            raise SystemExit("--graph: the dst-range partition's collectives run eagerly")
+        eager_step = lambda: partition_step(model, opt, dst_part, graph, reducer=reducer)  # noqa: E731
+    else:
+        eager_step = lambda: train_step(model, opt, graph, reducer=reducer)  # noqa: E731
     if not args.graph:
         for _ in range(args.warmup):
             eager_step()
@@ -332,7 +364,7 @@ def main():
         profiling.stop()
 
     extra = None
-    if rank == 0 and not args.no_extras:
+    if rank == 0 and not no_extras:
         extra = extras(graph, dev)
 
     out = None
@@ -387,8 +419,12 @@ def main():
                           "conv_edges": total_conv_edges, "hidden": cfg.hidden, "layers": cfg.layers,
                           "partition": partition, "components_per_rank": len(comp_ids),
                           "global_batch": len(comp_ids) * world,
-                          "parallelism": (f"dp{world} over graph components, one RCCL all-reduce per step "
-                                          f"(gradients + loss sums)" if world > 1 else "single GPU"),
+                          "parallelism": ("single GPU" if world == 1 else
+                                          f"dst-range partition over {world} ranks: per-layer all-gather / "
+                                          f"reduce-scatter of node embeddings + one all-reduce of gradients and "
+                                          f"loss sums" if partition == "dst-range" else
+                                          f"dp{world} over graph components, one RCCL all-reduce per step "
+                                          f"(gradients + loss sums)"),
                           "world_size": world, "backend": (f"{backend} ({'RCCL' if backend == 'nccl' else backend})"
                                                            if world > 1 else None),
                           "skew": args.skew, "prune_dead": bool(args.prune_dead),

@@ -189,20 +189,10 @@ class HetroGIN(torch.nn.Module):
         return self._run(x_dict, edge_index_dict, path_batch, y, m_valid)
 
     def _run(self, x_dict, edge_index_dict, path_batch, y, m_valid):
-        # models.py:333-342 feature slicing (assigns into the caller's dict, as the reference does)
-        if not self.divided_features:
-            x_dict["path"] = torch.cat([x_dict["path"][:, 0:3], x_dict["path"][:, 6].reshape(-1, 1)], axis=1)
-            x_dict["link"] = torch.cat([x_dict["link"][:, 0:3], x_dict["link"][:, 4:7]], axis=1)
-            if not self.bl_features:
-                x_dict["path"] = x_dict["path"][:, 0:3]
-                x_dict["link"] = x_dict["link"][:, 0:3]
-        else:
-            if not self.bl_features:
-                x_dict["path"] = x_dict["path"][:, 0:6]
-                x_dict["link"] = x_dict["link"][:, 0:3]
-
+        self._select_features(x_dict)
         origin_input = x_dict.copy()
 
+        mean_f = max_f = None
         if self.global_feats:   # models.py:347-352
             mean_f = _global_pool(origin_input["path"], path_batch, "mean")
             max_f = _global_pool(origin_input["path"], path_batch, "amax")
@@ -214,18 +204,34 @@ class HetroGIN(torch.nn.Module):
             if self.dropout > 0.0 and self.training:
                 for k in list(x_dict.keys()):
                     x_dict[k] = torch.nn.functional.dropout(x_dict[k], p=self.dropout, training=True)
+        return self._readout(x_dict["path"], origin_input["path"], mean_f, max_f, y, m_valid)
 
+    def _select_features(self, x_dict):
+        """models.py:333-342 feature slicing (assigns into the caller's dict, as the reference does)."""
+        if not self.divided_features:
+            x_dict["path"] = torch.cat([x_dict["path"][:, 0:3], x_dict["path"][:, 6].reshape(-1, 1)], axis=1)
+            x_dict["link"] = torch.cat([x_dict["link"][:, 0:3], x_dict["link"][:, 4:7]], axis=1)
+            if not self.bl_features:
+                x_dict["path"] = x_dict["path"][:, 0:3]
+                x_dict["link"] = x_dict["link"][:, 0:3]
+        else:
+            if not self.bl_features:
+                x_dict["path"] = x_dict["path"][:, 0:6]
+                x_dict["link"] = x_dict["link"][:, 0:3]
+
+    def _readout(self, x_path, origin_path, mean_f, max_f, y, m_valid):
+        """models.py:362-376 on the final path embeddings (+ F3's fused head + loss when ``y`` is given)."""
         x2 = None   # second column block of the readout input, read in place instead of torch.cat
         if self.concat_path:   # models.py:362-371
             if self.global_feats:
-                x = torch.cat((x_dict["path"], origin_input["path"], mean_f, max_f), 1)
+                x = torch.cat((x_path, origin_path, mean_f, max_f), 1)
             else:
-                x, x2 = x_dict["path"], origin_input["path"]
+                x, x2 = x_path, origin_path
         else:
             if self.global_feats:
-                x = torch.cat((x_dict["path"], mean_f, max_f), 1)
+                x = torch.cat((x_path, mean_f, max_f), 1)
             else:
-                x = x_dict["path"]
+                x = x_path
 
         n_ro = len(self.mlp_layers) + 1
         for i in range(n_ro):   # models.py:373-374

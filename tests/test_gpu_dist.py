@@ -5,6 +5,9 @@ step's arithmetic is the RCCL run's.  Each rank holds half the components of a c
 (hgin.data.rank_components); after one step both ranks must hold the single-device gradient of the union
 and its loss value (hgin/dist.py), within fp32 summation-order tolerance (the GEMM weight-gradient
 reductions run over different row counts).
+
+The connected-graph variant (hgin/partition.py: destination-range rows per rank, per-layer all-gather of
+source embeddings, reduce-scatter of their gradients) runs the same check on one connected graph.
 """
 import os
 import socket
@@ -89,6 +92,67 @@ def test_two_ranks_equal_single_device(feat):
     g_scale = max(float(p.grad.double().norm()) for p in model.parameters() if p.grad is not None)
     for n, p in model.named_parameters():
         g0, g1 = r0["grads"][n], r1["grads"][n]
+        assert (g0 is None) == (p.grad is None), n
+        if g0 is None:
+            continue
+        assert torch.equal(g0, g1), n
+        err = float((g0.double() - p.grad.double().cpu()).norm())
+        assert err <= tol * float(p.grad.double().norm()) + 1e-6 * g_scale, (n, err)
+
+
+def _part_worker(rank, world, port, outdir, feat):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from hgin.data import synthetic_graph
+    from hgin.partition import DstRangePartition, forward_loss, train_step
+    cfg = _cfg(feat)
+    g = synthetic_graph(cfg, seed=3, device="cuda")
+    part = DstRangePartition({t: g.num_nodes(t) for t in g.x})
+    local = part.local_graph(g)
+    model = _model(cfg)
+    with torch.no_grad():
+        out, _ = forward_loss(model, part, local)
+    lv = train_step(model, torch.optim.SGD(model.parameters(), lr=0.0), part, local)
+    torch.save({"loss": lv.cpu(), "out": out.float().cpu(), "rows": part.rows("path"),
+                "grads": {n: (p.grad.cpu() if p.grad is not None else None) for n, p in model.named_parameters()}},
+               os.path.join(outdir, f"rank{rank}.pt"))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("feat", ["f32", "bf16"])
+def test_dst_range_partition_equals_single_device(feat):
+    """Two ranks each own half of every node type of ONE connected graph: the forward output rows are
+    bit-identical to the single-device forward (same edges per destination row, same order), the loss and the
+    gradients equal the single-device ones within fp32 summation-order tolerance."""
+    from hgin.data import synthetic_graph
+    cfg = _cfg(feat)
+    with tempfile.TemporaryDirectory() as d:
+        ctx = mp.get_context("spawn")
+        port = _free_port()
+        procs = [ctx.Process(target=_part_worker, args=(r, 2, port, d, feat)) for r in range(2)]
+        for p in procs:
+            p.start()
+        for p in procs:
+            p.join(timeout=240)
+            assert p.exitcode == 0, p.exitcode
+        rs = [torch.load(os.path.join(d, f"rank{r}.pt"), weights_only=True) for r in range(2)]
+    g = synthetic_graph(cfg, seed=3, device="cuda")
+    model = _model(cfg)
+    out, lv = model.forward_loss(g.x_dict(), g.edge_index_dict(), g.batch["path"], g.y)
+    torch.sqrt(lv).backward()
+    lv = float(lv)
+    full_out = out.detach().float().cpu()
+    for r in rs:
+        lo, hi = r["rows"]
+        assert torch.equal(r["out"], full_out[lo:hi])
+    assert torch.equal(rs[0]["loss"], rs[1]["loss"])
+    assert abs(float(rs[0]["loss"]) - lv) <= 1e-5 * lv
+    tol = 1e-4 if feat == "f32" else 5e-3
+    g_scale = max(float(p.grad.double().norm()) for p in model.parameters() if p.grad is not None)
+    for n, p in model.named_parameters():
+        g0, g1 = rs[0]["grads"][n], rs[1]["grads"][n]
         assert (g0 is None) == (p.grad is None), n
         if g0 is None:
             continue
