@@ -23,7 +23,9 @@ fp32 — the graph the north star's >= 60 %-of-HBM aggregate target is stated on
 value = E_conv(total) / t_step, E_conv = edges of the four convolved relations (p->l, l->p, l->n, n->l),
 counted once per step.  t_step = max over ranks of (barrier + hipDeviceSynchronize
 bracketed K steps) / K (the bench contract); the median of the K per-step durations (HIP events between
-steps on the step's stream) is reported beside it.  The timed region runs no probes: the
+steps on the step's stream) is reported beside it.  N > 1 (components): after the timed region
+rank 0 alone also trains all the components the ranks split (2 warm-up + median of 5) and reports
+``scaling_vs_1gpu`` = that step time / this run's median step (ideal N).  The timed region runs no probes: the
 per-kernel HIP-event figures (``roofline``, ``gemm``) come from a separate untimed pass over the same step.
 
 Rank 0 prints one JSON line.
@@ -71,6 +73,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-probe", action="store_true", help="skip the untimed per-kernel event pass")
     ap.add_argument("--no-extras", action="store_true", help="skip the sampler / decoder / CSR-build lines")
+    ap.add_argument("--no-ref1", action="store_true",
+                    help="N > 1 components split: skip rank 0's single-GPU run of all the components (scaling_vs_1gpu)")
     ap.add_argument("--adam", choices=("foreach", "fused"), default="foreach",
                     help="torch.optim.Adam implementation (train.py's optimizer, same update rule)")
     ap.add_argument("--graph", action="store_true",
@@ -185,6 +189,33 @@ def csr_build_ms(graph, dev) -> dict:
                                "csc_ms": round(m.elapsed_time(t), 3)}
         del csr, csc
     return out
+
+
+def one_gpu_reference(cfg, n_comp: int, dev, adam: str, warmup: int = 2, steps: int = 5) -> dict:
+    """The 1-GPU point of the strong-scaling curve measured inside an N > 1 run: rank 0 alone trains ALL n_comp
+    components (the graph the N ranks split) on its GPU, a fresh model from the same seed, 2 warm-up steps +
+    the median of 5 HIP-event-timed steps; the other ranks wait at a barrier."""
+    from hgin import HetroGIN
+    from hgin.data import rank_components
+    from hgin.train import train_step
+    graph, _ = rank_components(cfg, 0, 1, device=dev, n_components=n_comp)
+    torch.manual_seed(1997)
+    model = HetroGIN(**cfg.model_kwargs({"link": cfg.f_link, "path": cfg.f_path, "node": cfg.f_node})).to(dev)
+    opt = torch.optim.Adam(lr=1e-3, params=model.parameters(), **({"fused": True} if adam == "fused" else {}))
+    for _ in range(warmup):
+        train_step(model, opt, graph)
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(steps + 1)]
+    torch.cuda.synchronize()
+    ev[0].record()
+    for i in range(steps):
+        train_step(model, opt, graph)
+        ev[i + 1].record()
+    torch.cuda.synchronize()
+    ms = statistics.median(ev[i].elapsed_time(ev[i + 1]) for i in range(steps))
+    del graph, model, opt
+    torch.cuda.empty_cache()
+    return {"ms_per_step_median": round(ms, 4), "components": n_comp, "warmup": warmup, "steps": steps,
+            "what": "rank 0 alone, all components of the split graph, after the timed region"}
 
 
 def extras(graph, dev) -> dict:
@@ -363,6 +394,12 @@ def main():
             eager_step()
         profiling.stop()
 
+    ref1 = None
+    if world > 1 and partition == "components" and args.skew == "uniform" and not (args.no_ref1 or args.prune_dead):
+        if rank == 0:
+            ref1 = one_gpu_reference(cfg, n_comp, dev, args.adam)
+        barrier()
+
     extra = None
     if rank == 0 and not no_extras:
         extra = extras(graph, dev)
@@ -431,6 +468,10 @@ def main():
                           "execution": "hipgraph (one replay per step)" if args.graph else "eager",
                           "optimizer": f"torch.optim.Adam(lr=1e-3), {args.adam}"},
                "roofline": roofline, "gemm": gemm, "csr_build": csr_ms, "extras": extra, "final_loss": final_loss}
+        if ref1 is not None:
+            # strong scaling against the same graph on one GPU: t_1gpu / t_step (ideal: N)
+            out["one_gpu_reference"] = ref1
+            out["scaling_vs_1gpu"] = round(ref1["ms_per_step_median"] / (t_med * 1e3), 3)
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(cfg)
         else:
