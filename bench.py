@@ -433,8 +433,9 @@ def main():
                 tfs = m["avg_work"] / (m["avg_ms"] / 1e3) / 1e12
                 # the GIN / readout MLP GEMMs are HBM-bound at these shapes (K <= 512, N <= 256: far below the
                 # MFMA ridge), so they are reported against HBM; the FLOP rate is given beside it
-                gemm = {"bound": "hbm", "kernel": f"hgin_gin_mlp_fwd_{'bf16' if bf16 else 'f32'} (k_gemm_nt"
-                                                  f"{'_bf16' if bf16 else ''} + bias/PReLU/accum epilogue)",
+                gemm = {"bound": "hbm", "kernel": (f"hgin_gin_mlp_fwd_{'bf16' if bf16 else 'f32'} ("
+                                                   f"{'k_ws_bf16 / k_gemm_nt_bf16' if bf16 else 'k_ws_f32 / k_gemm_nt'}"
+                                                   f" + bias/PReLU/accum epilogue)"),
                         "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                         "frac": round(gbs / HBM_PEAK_GBS, 4), "bytes_per_launch": m["avg_bytes"],
                         "tflops": round(tfs, 2),

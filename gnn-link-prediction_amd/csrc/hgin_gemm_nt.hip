@@ -886,6 +886,21 @@ struct WsArgs {
   bool nt_in;
 };
 
+// Operands of one fp32 weight-stationary forward launch (k_ws_f32, below).
+struct WsArgs32 {
+  const float* a;
+  int64_t lda;
+  const float* w;
+  const float* bias;
+  const float* prelu;
+  const float* accum;
+  float* z;
+  float* y;
+  int64_t M;
+  bool nt_io;
+  bool nt_in;
+};
+
 template <int K, int N, int EPI, bool kR1, bool kZ, bool kR2>
 __global__ __launch_bounds__((WsCfg<K, N>::NT), 1) void k_ws_bf16(WsArgs g) {
   using C = WsCfg<K, N>;
@@ -1225,6 +1240,325 @@ int try_ws_bf16(const Src2h& a, const Src2h& b, int64_t M, int64_t N, int64_t K,
 #undef HGIN_WS
     return -1;
   }
+}
+
+// ---------------------------------------------------------------------------------------------------
+// k_ws_f32 — the fp32 forward MLP GEMM (EPI 1, split mode) in the weight-stationary streaming form, for the
+// square layers K = N = 256 (cfg3's layers above the first; an instantiation at K = N = 128 measured slower than
+// the tiled kernel, 600k rows: 0.279 vs 0.243 ms, so there is none):
+//   * N/32 waves; wave w holds the three bf16 planes of W[32 w .. 32 w + 31][0, K) in registers as its MFMA B
+//     fragments (3K/4 VGPRs: 192 at K = 256), split once per launch;
+//   * 32-row blocks of A (fp32) stream HBM -> LDS by DMA into a 3-slot ring (two blocks in flight while one is
+//     computed); the block's accum rows are DMA'd into a single buffer at the top of its own iteration (they are
+//     read only by its epilogue, after the split pass and the MFMAs); counted vmcnt waits as in k_ws_bf16;
+//   * one split pass per block turns the fp32 A image into three bf16 planes (each element split once per CU):
+//     the pass reads the whole image into registers, then — after a barrier — writes planes 0 and 1 over the
+//     dead fp32 image and plane 2 into its own buffer (so the ring needs no plane space of its own); plane rows
+//     are 2K bytes of 16-B chunks, chunk c of row r stored at c ^ (r & SW) (conflict-free fragment reads);
+//   * per 16-wide k-step six v_mfma_f32_32x32x16_bf16 products in k_gemm_nt's order (smallest terms first), k
+//     ascending, one accumulator per wave — the tiled kernel's per-output arithmetic, so the results are
+//     bit-identical to it (tests/test_gpu_gemm_switch.py);
+//   * epilogue as k_ws_bf16 (16 rows at a time staged in the block's dead plane image, row-contiguous float4
+//     stores of z and y, bias / PReLU / accum as epilogue<1>).
+template <int K, int N>
+struct Ws32Cfg {
+  static constexpr int NW = N / 32;
+  static constexpr int NT = NW * 64;
+  static constexpr int KS = K / 16;
+  static constexpr int BM = 32;
+  static constexpr int A_BYTES = BM * K * 4;          // fp32 image; later planes 0 and 1 (BM * K * 2 each)
+  static constexpr int C_BYTES = BM * N * 4;          // accum image
+  static constexpr int PL = BM * K * 2;               // one bf16 plane
+  static constexpr int PROW = K * 2;                  // plane row bytes
+  static constexpr int SW = (PROW / 16 < 32 ? PROW / 16 : 32) - 1;
+  static constexpr int PA = A_BYTES / 1024 / NW, PC = C_BYTES / 1024 / NW;
+  static constexpr int G4 = BM * K / 4 / NT;          // float4 groups per thread in the split pass
+  static_assert(K == N && A_BYTES % (1024 * NW) == 0 && C_BYTES % (1024 * NW) == 0, "shape");
+  static_assert(16 * N * 4 <= A_BYTES && G4 * NT * 4 == BM * K, "staging / split pass");
+};
+
+template <int K, int N, bool kR1>
+struct Ws32Ring {
+  static constexpr int NST = 3;                                          // A ring depth
+  static constexpr int ACC = NST * Ws32Cfg<K, N>::A_BYTES;               // accum buffer
+  static constexpr int P2 = ACC + (kR1 ? Ws32Cfg<K, N>::C_BYTES : 0);    // plane 2
+  static constexpr int BIAS = P2 + Ws32Cfg<K, N>::PL;                    // the bias row
+  static constexpr int BYTES = BIAS + N * 4;
+};
+
+template <int K, int N, bool kR1, bool kZ>
+__global__ __launch_bounds__((Ws32Cfg<K, N>::NT), 1) void k_ws_f32(WsArgs32 g) {
+  using C = Ws32Cfg<K, N>;
+  using R = Ws32Ring<K, N, kR1>;
+  constexpr int PA = C::PA, PC = kR1 ? C::PC : 0;              // DMA instructions per wave per block (A, accum)
+  constexpr int S = 4 * (kZ ? 2 : 1);                            // stores per lane per block
+  constexpr int QPR = N / 4;
+  extern __shared__ __attribute__((aligned(16))) char ws32_smem[];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int li = lane & 31;
+  const int lh = lane >> 5;
+  const int64_t M = g.M;
+  const int64_t nblk = (M + C::BM - 1) / C::BM;
+  const int64_t G = gridDim.x;
+  if ((int64_t)blockIdx.x >= nblk) return;
+  const int64_t my = (nblk - 1 - blockIdx.x) / G + 1;
+  char* const plane2 = ws32_smem + R::P2;
+
+  // this wave's W slice as split B fragments: lane (li, lh) holds W[32 wave + li][16 t + 8 lh .. + 7]
+  uint4 wf[C::KS][3];
+  {
+    const float* wr = g.w + (int64_t)(wave * 32 + li) * K + lh * 8;
+#pragma unroll
+    for (int t = 0; t < C::KS; ++t) {
+      const float4 v0 = *reinterpret_cast<const float4*>(wr + t * 16);
+      const float4 v1 = *reinterpret_cast<const float4*>(wr + t * 16 + 4);
+      uint2 o0[3], o1[3];
+      split4(v0, o0);
+      split4(v1, o1);
+#pragma unroll
+      for (int p = 0; p < 3; ++p) wf[t][p] = make_uint4(o0[p].x, o0[p].y, o1[p].x, o1[p].y);
+    }
+  }
+  // the bias row goes to LDS once (read per row pass: no VGPRs held across the loop); the PReLU slope is uniform
+  float* const bias_lds = reinterpret_cast<float*>(ws32_smem + R::BIAS);
+  if (tid < N / 4) {
+    const float4 b4 = *reinterpret_cast<const float4*>(g.bias + tid * 4);
+    asm volatile("" ::"v"(b4.x), "v"(b4.y), "v"(b4.z), "v"(b4.w));
+    *reinterpret_cast<float4*>(bias_lds + tid * 4) = b4;
+  }
+  const float a_slope = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(g.prelu[0])));
+#pragma unroll
+  for (int t = 0; t < C::KS; ++t)
+#pragma unroll
+    for (int p = 0; p < 3; ++p) asm volatile("" ::"v"(wf[t][p].x), "v"(wf[t][p].y), "v"(wf[t][p].z), "v"(wf[t][p].w));
+
+  auto dma = [&](const void* src, void* dst) {
+    if (g.nt_in) glds16_asm<true>(src, dst); else glds16_asm(src, dst);
+  };
+  auto tid_o = [&]() {
+    int t;
+    asm volatile("v_mov_b32 %0, %1" : "=v"(t) : "v"(tid));
+    return t;
+  };
+  auto rows_of = [&](int64_t i, int64_t& r0, int& rmax) {
+    r0 = ((int64_t)blockIdx.x + i * G) * C::BM;
+    rmax = (int)(M - 1 - r0 < C::BM ? M - 1 - r0 : C::BM - 1);
+  };
+  auto issue_a = [&](int64_t i) {
+    char* base = ws32_smem + (int)(i % R::NST) * C::A_BYTES;
+    int64_t r0;
+    int rmax;
+    rows_of(i, r0, rmax);
+    const float* ab = g.a + r0 * g.lda;
+    const int ln = tid_o() & 63;
+#pragma unroll
+    for (int q = 0; q < C::PA; ++q) {
+      const int piece = wave * C::PA + q;
+      const int off = piece * 1024 + ln * 16;
+      int r = off / (K * 4);
+      r = r < rmax ? r : rmax;
+      dma(ab + (r * (int)g.lda + (off % (K * 4)) / 4), base + piece * 1024);
+    }
+  };
+  auto issue_c = [&](int64_t i) {
+    int64_t r0;
+    int rmax;
+    rows_of(i, r0, rmax);
+    const float* cb = g.accum + r0 * N;
+    const int ln = tid_o() & 63;
+#pragma unroll
+    for (int q = 0; q < C::PC; ++q) {
+      const int piece = wave * C::PC + q;
+      const int off = piece * 1024 + ln * 16;
+      int r = off / (N * 4);
+      r = r < rmax ? r : rmax;
+      dma(cb + (r * N + (off % (N * 4)) / 4), ws32_smem + R::ACC + piece * 1024);
+    }
+  };
+
+  issue_a(0);
+  if (1 < my) issue_a(1);
+  for (int64_t i = 0; i < my; ++i) {
+    // wait for A(i).  Issue order: A(0), A(1); then per iteration j: accum(j), A(j + 2), the stores of j.  The
+    // counts below are exact when every block is full (only a grid's last block is partial, and it is the last
+    // iteration of its workgroup) and count only the ops actually issued after A(i).
+    static_assert(2 * S + PC + PA <= 63, "vmcnt range");
+    if (i >= 2) {
+      if (i + 1 < my) wait_vm<2 * S + PC + PA>(); else wait_vm<2 * S + PC>();
+    } else if (i == 1) {
+      if (2 < my) wait_vm<PC + S + PA>(); else wait_vm<PC + S>();
+    } else {
+      if (1 < my) wait_vm<PA>(); else wait_vm<0>();
+    }
+    __builtin_amdgcn_s_barrier();   // A(i) landed for every wave; the slot of A(i - 1) and the accum buffer are free
+    asm volatile("" ::: "memory");
+    if constexpr (kR1) issue_c(i);
+    if (i + 2 < my) issue_a(i + 2);
+    char* abase = ws32_smem + (int)(i % R::NST) * C::A_BYTES;
+    {   // split pass: the fp32 image -> planes 0 / 1 (in place) and 2 (own buffer)
+      const int t = tid_o();
+      float4 v[C::G4];
+#pragma unroll
+      for (int j = 0; j < C::G4; ++j) v[j] = *reinterpret_cast<const float4*>(abase + (j * C::NT + t) * 16);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();               // every thread holds its groups: the image may be overwritten
+      asm volatile("" ::: "memory");
+#pragma unroll
+      for (int j = 0; j < C::G4; ++j) {
+        const int grp = j * C::NT + t;
+        const int r = grp / (K / 4), k = (grp % (K / 4)) * 4;
+        uint2 o[3];
+        split4(v[j], o);
+        const int off = r * C::PROW + 16 * ((k >> 3) ^ (r & C::SW)) + 8 * ((k >> 2) & 1);
+        *reinterpret_cast<uint2*>(abase + off) = o[0];
+        *reinterpret_cast<uint2*>(abase + C::PL + off) = o[1];
+        *reinterpret_cast<uint2*>(plane2 + off) = o[2];
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+    }
+    const int64_t r0 = ((int64_t)blockIdx.x + i * G) * C::BM;
+    f32x16 acc;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) acc[e] = 0.0f;
+    // A fragments double-buffered one k-step ahead; the scheduling fences keep the compiler from hoisting every
+    // k-step's fragment reads to the top of the block (3 x 4 x KS VGPRs on top of the W slice)
+    const int fl = tid_o() & 63;
+    const int frow = (fl & 31) * C::PROW;
+    const int fsw = ((fl >> 5) ^ (fl & 31)) & C::SW;          // (2t + lh) ^ (li & SW) = 2t ^ fsw for 2t even
+    auto frag = [&](int t, uint4 (&f)[3]) {
+      const int off = frow + ((2 * t ^ fsw) << 4);
+      f[0] = *reinterpret_cast<const uint4*>(abase + off);
+      f[1] = *reinterpret_cast<const uint4*>(abase + C::PL + off);
+      f[2] = *reinterpret_cast<const uint4*>(plane2 + off);
+    };
+    uint4 fa[2][3];
+    frag(0, fa[0]);
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int t = 0; t < C::KS; ++t) {
+      if (t + 1 < C::KS) frag(t + 1, fa[(t + 1) & 1]);
+      const uint4(&f)[3] = fa[t & 1];
+      const bf16x8 a0 = __builtin_bit_cast(bf16x8, f[0]), a1 = __builtin_bit_cast(bf16x8, f[1]),
+                   a2 = __builtin_bit_cast(bf16x8, f[2]);
+      const bf16x8 b0 = __builtin_bit_cast(bf16x8, wf[t][0]), b1 = __builtin_bit_cast(bf16x8, wf[t][1]),
+                   b2 = __builtin_bit_cast(bf16x8, wf[t][2]);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a2, b0, acc, 0, 0, 0);   // k_gemm_nt's order
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b1, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b2, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b0, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b1, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b0, acc, 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    __builtin_amdgcn_s_setprio(0);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+
+    // accum(i) landed (A(i + 2) may stay in flight); every wave's share, so a barrier follows below
+    if constexpr (kR1) {
+      if (i + 2 < my) wait_vm<PA>(); else wait_vm<0>();
+    }
+    float* stg = reinterpret_cast<float*>(abase);                // the dead plane images
+    const float* img1 = reinterpret_cast<const float*>(ws32_smem + R::ACC);
+    float* yb = g.y + r0 * N;
+    float* zb = kZ ? g.z + r0 * N : nullptr;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      __builtin_amdgcn_s_barrier();               // plane reads / the previous half's staging reads are done
+      asm volatile("" ::: "memory");
+#pragma unroll
+      for (int e8 = 0; e8 < 8; ++e8) {
+        const int e = 8 * h + e8;
+        const int row = (e & 3) + 8 * ((e >> 2) & 1) + 4 * lh;
+        stg[row * N + ((wave * 32 + li) ^ (((row >> 2) & 1) << 5))] = acc[e];
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+#pragma unroll
+      for (int pass = 0; pass < 2; ++pass) {
+        const int tq = tid_o();
+        const int cq = (tq % QPR) * 4;
+        const int row = pass * 8 + tq / QPR;
+        const int brow = h * 16 + row;
+        const int64_t grow = r0 + brow;
+        const float4 v4 = *reinterpret_cast<const float4*>(stg + row * N + (cq ^ (((row >> 2) & 1) << 5)));
+        const float4 b4 = *reinterpret_cast<const float4*>(bias_lds + cq);
+        const float bcol[4] = {b4.x, b4.y, b4.z, b4.w};
+        float o[4] = {v4.x, v4.y, v4.z, v4.w};
+        float zz[4];
+        float in1[4] = {0.f, 0.f, 0.f, 0.f};
+        if constexpr (kR1) {
+          const float4 c4 = *reinterpret_cast<const float4*>(img1 + brow * N + cq);
+          in1[0] = c4.x; in1[1] = c4.y; in1[2] = c4.z; in1[3] = c4.w;
+        }
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          zz[t] = __fadd_rn(o[t], bcol[t]);
+          const float y = zz[t] > 0.0f ? zz[t] : __fmul_rn(a_slope, zz[t]);
+          o[t] = kR1 ? __fadd_rn(in1[t], y) : y;
+        }
+        if (grow < M) {
+          const int oo = brow * N + cq;
+          if (g.nt_io) {
+            Out4<float>::st_nt(yb + oo, o, true, 4);
+            if constexpr (kZ) Out4<float>::st_nt(zb + oo, zz, true, 4);
+          } else {
+            Out4<float>::st(yb + oo, o, true, 4);
+            if constexpr (kZ) Out4<float>::st(zb + oo, zz, true, 4);
+          }
+        }
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  }
+}
+
+// HGIN_NT_WS32 = 0 keeps the tiled kernel for the fp32 forward GEMM.
+bool ws32_enabled() {
+  static const bool on = [] {
+    const char* v = getenv("HGIN_NT_WS32");
+    return !(v && v[0] == '0');
+  }();
+  return on;
+}
+
+template <int K, int N, bool kR1, bool kZ>
+int launch_ws32(const WsArgs32& a, hipStream_t s, const char* what) {
+  constexpr int lds = Ws32Ring<K, N, kR1>::BYTES;
+  static_assert(lds <= 160 * 1024, "LDS");
+  auto kern = k_ws_f32<K, N, kR1, kZ>;
+  static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                                                     hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+  if (attr != hipSuccess) {
+    set_error("%s: hipFuncSetAttribute failed: %s", what, hipGetErrorString(attr));
+    return (int)attr;
+  }
+  const int64_t nblk = ceil_div(a.M, (int64_t)Ws32Cfg<K, N>::BM);
+  const int64_t grid = nblk < ws_grid() ? nblk : ws_grid();
+  kern<<<(unsigned)grid, Ws32Cfg<K, N>::NT, lds, s>>>(a);
+  return check_launch(what);
+}
+
+// Returns -1 when the fp32 weight-stationary form does not apply (the caller launches the tiled kernel): split
+// mode, one A source (no eps-scaled second half), K = N = 256, 16-B aligned rows, packed W / z / y / accum.
+int try_ws_f32(const float* a1, int64_t lda1, int64_t k1, const float* a2_eps, const float* w, const float* bias,
+               const float* prelu, const float* accum, float* z, float* y, int64_t M, int64_t N, int64_t K,
+               hipStream_t s, const char* what) {
+  // (profiles/r02/gemm_ws_f32_fwd.txt)
+  if (!ws32_enabled() || !gemm_split_enabled() || M < 1 || K != N || K != 256 || k1 != K || a2_eps != nullptr)
+    return -1;
+  if (!aligned16(a1) || lda1 % 4 || lda1 >= (int64_t(1) << 24) || !aligned16(w) || !aligned16(y) ||
+      (z && !aligned16(z)) || (accum && !aligned16(accum)))
+    return -1;
+  WsArgs32 g{a1, lda1, w, bias, prelu, accum, z, y, M, gemm_nt_io(M, N, 4), ws_nt_in()};
+  if (accum && z) return launch_ws32<256, 256, true, true>(g, s, what);
+  if (accum) return launch_ws32<256, 256, true, false>(g, s, what);
+  if (z) return launch_ws32<256, 256, false, true>(g, s, what);
+  return launch_ws32<256, 256, false, false>(g, s, what);
 }
 
 // K-tile depth of the bf16 NT kernel (HGIN_NT_BKH = 64 / 128).  128: twice the A bytes per prefetch (32 KB
@@ -1780,6 +2114,11 @@ extern "C" int hgin_gin_mlp_fwd_f32(const float* a1, int64_t lda1, int64_t k1, c
   if (nt2_eligible<float>(a1, lda1, k1, a2, lda2, w_planes, N, K, gemm_split_enabled()))
     return launch_nt2<float, 1, float>(a1, lda1, k1, a2, lda2, a2_eps, w_planes, M, N, K, bias, prelu, accum, z, y, N,
                                        as_stream(stream), "hgin_gin_mlp_fwd_f32");
+  {
+    const int rc = try_ws_f32(a1, lda1, k1, a2_eps, w, bias, prelu, accum, z, y, M, N, K, as_stream(stream),
+                              "hgin_gin_mlp_fwd_f32");
+    if (rc >= 0) return rc;
+  }
   return launch_nt<1>(Src2{a1, lda1, a2, lda2, k1, a2_eps}, Src2{w, K, nullptr, 0, K}, M, N, K, bias, prelu, accum, z, y,
                       N, as_stream(stream), "hgin_gin_mlp_fwd_f32");
 }

@@ -1,8 +1,9 @@
 """Child process of tests/test_gpu_gemm_switch.py: the bf16 GIN MLP GEMM (hgin_gin_mlp_fwd_bf16) at the shapes
 of the weight-stationary kernel (K 128 / 256 / 512, N 128 / 256; ragged M, M below one block, many blocks
 per workgroup; accum / z present or not; a two-source A) under the process-static HGIN_* switches its parent
-set.  Also the dX GEMMs (plain and combine) and the bf16 weight-gradient GEMM.  Checks every output against an
-fp32 / fp64 evaluation of the same bf16 operands and saves them, so the parent can compare switch settings.
+set, and the fp32 forward GEMM at the shapes of its weight-stationary kernel (k_ws_f32).  Also the dX GEMMs (plain
+and combine) and the weight-gradient GEMMs.  Checks every output against an fp32 / fp64 evaluation of the same
+operands and saves them, so the parent can compare switch settings.
 
     python tests/gemm_child.py OUT.pt
 """
@@ -51,6 +52,31 @@ def run(M, K, N, with_acc, save_z, k1, eps=None, *, g):
         assert bool(((z.float() - zr).abs() <= tol(zr)).all()), (M, K, N, "z")
     out = {"y": y.cpu()}
     if save_z:
+        out["z"] = z.cpu()
+    return out
+
+
+F32_CASES = [  # (M, K, N, accum, save_z) — fp32 forward (split mode: k_ws_f32 at K = N = 256 by default)
+    (300_007, 256, 256, True, True), (1, 256, 256, True, True), (31, 256, 256, False, True),
+    (70_001, 256, 256, True, False), (65, 128, 128, False, False), (20_000, 128, 128, True, True),
+    (40_000, 512, 256, True, True),
+]
+
+
+def run_f32(M, K, N, with_acc, save_z, *, g):
+    a = torch.randn(M, K, device="cuda", generator=g)
+    w = torch.randn(N, K, device="cuda", generator=g) / K ** 0.5
+    b = torch.randn(N, device="cuda", generator=g)
+    s = torch.tensor([0.25], device="cuda")
+    acc = torch.randn(M, N, device="cuda", generator=g) if with_acc else None
+    z, y = ops.gin_mlp_fwd(a, w, b, s, acc, save_z=save_z)
+    zr = a.double() @ w.double().t() + b.double()
+    yr = torch.where(zr > 0, zr, 0.25 * zr) + (acc.double() if with_acc else 0.0)
+    tol = lambda r: 1e-6 * r.abs() + 1e-5 * (a.double().abs() @ w.double().abs().t() + 1)   # noqa: E731
+    assert bool(((y.double() - yr).abs() <= tol(yr)).all()), (M, K, N, "y")
+    out = {"y": y.cpu()}
+    if save_z:
+        assert bool(((z.double() - zr).abs() <= tol(zr)).all()), (M, K, N, "z")
         out["z"] = z.cpu()
     return out
 
@@ -115,6 +141,7 @@ def main():
     torch.cuda.init()
     g = torch.Generator(device="cuda").manual_seed(7)
     res = {f"{c}": run(*c, g=g) for c in CASES}
+    res.update({f"f32{c}": run_f32(*c, g=g) for c in F32_CASES})
     res.update({f"dx{c}": run_dx(*c, g=g) for c in DX_CASES})
     res.update({f"dw{c}": run_dw(*c, g=g) for c in DW_CASES})
     torch.save(res, sys.argv[1])

@@ -4,8 +4,10 @@
   * default                 — the weight-stationary streaming kernel (k_ws_bf16) at K 128 / 256 / 512, N 128 / 256:
                               the forward MLP GEMM (EPI 1), the plain dX GEMM (EPI 0) and the dX GEMM with the
                               self-term backward in its epilogue (EPI 4, combine);
-  * HGIN_NT_WS=0 HGIN_TN_WS=0 — the tiled register-staged kernels (k_gemm_nt_bf16, k_gemm_tn_bf16_tr) for every
-                              shape (the weight-stationary dW kernel k_wsd_bf16 is the default at N, K in {128, 256});
+  * HGIN_NT_WS=0 HGIN_TN_WS=0 HGIN_NT_WS32=0 — the tiled register-staged kernels (k_gemm_nt_bf16,
+                              k_gemm_tn_bf16_tr, and k_gemm_nt for the fp32 forward GEMM, whose default at K = N = 256
+                              is k_ws_f32) for every shape (the weight-stationary dW kernel k_wsd_bf16 is
+                              the default at N, K in {128, 256});
   * HGIN_NT_BKH=128         — the tiled kernel with 128-deep K-tiles (with the weight-stationary form off).
 
 Every child checks its outputs against an fp32 evaluation of the same bf16 operands; the three settings must
@@ -23,8 +25,8 @@ import torch
 pytestmark = pytest.mark.gpu
 HERE = os.path.dirname(os.path.abspath(__file__))
 
-SWITCHES = {"default": {}, "tiled": {"HGIN_NT_WS": "0", "HGIN_TN_WS": "0"},
-            "tiled_bk128": {"HGIN_NT_WS": "0", "HGIN_NT_BKH": "128", "HGIN_TN_WS": "0"}}
+SWITCHES = {"default": {}, "tiled": {"HGIN_NT_WS": "0", "HGIN_TN_WS": "0", "HGIN_NT_WS32": "0"},
+            "tiled_bk128": {"HGIN_NT_WS": "0", "HGIN_NT_BKH": "128", "HGIN_TN_WS": "0", "HGIN_NT_WS32": "0"}}
 _results = {}
 
 
