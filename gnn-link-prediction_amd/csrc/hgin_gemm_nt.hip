@@ -1248,18 +1248,18 @@ int try_ws_bf16(const Src2h& a, const Src2h& b, int64_t M, int64_t N, int64_t K,
 // the tiled kernel, 600k rows: 0.279 vs 0.243 ms, so there is none):
 //   * N/32 waves; wave w holds the three bf16 planes of W[32 w .. 32 w + 31][0, K) in registers as its MFMA B
 //     fragments (3K/4 VGPRs: 192 at K = 256), split once per launch;
-//   * 32-row blocks of A (fp32) stream HBM -> LDS by DMA into a 3-slot ring (two blocks in flight while one is
-//     computed); the block's accum rows are DMA'd into a single buffer at the top of its own iteration (they are
-//     read only by its epilogue, after the split pass and the MFMAs); counted vmcnt waits as in k_ws_bf16;
-//   * one split pass per block turns the fp32 A image into three bf16 planes (each element split once per CU):
-//     the pass reads the whole image into registers, then — after a barrier — writes planes 0 and 1 over the
-//     dead fp32 image and plane 2 into its own buffer (so the ring needs no plane space of its own); plane rows
-//     are 2K bytes of 16-B chunks, chunk c of row r stored at c ^ (r & SW) (conflict-free fragment reads);
+//   * 32-row blocks of A (fp32) stream HBM -> LDS by DMA into a 2-slot ring (one block in flight while one is
+//     computed; 3 slots measured equal); the block's accum rows are DMA'd into a single buffer at the top of its
+//     own iteration (read only by its epilogue, after the split pass and the MFMAs); counted vmcnt waits as in
+//     k_ws_bf16;
+//   * one split pass per block turns the fp32 A image into three bf16 plane images (each element split once per
+//     CU, one barrier); plane rows are 2K bytes of 16-B chunks, chunk c of row r stored at c ^ (r & SW)
+//     (conflict-free fragment reads);
 //   * per 16-wide k-step six v_mfma_f32_32x32x16_bf16 products in k_gemm_nt's order (smallest terms first), k
 //     ascending, one accumulator per wave — the tiled kernel's per-output arithmetic, so the results are
 //     bit-identical to it (tests/test_gpu_gemm_switch.py);
-//   * epilogue as k_ws_bf16 (16 rows at a time staged in the block's dead plane image, row-contiguous float4
-//     stores of z and y, bias / PReLU / accum as epilogue<1>).
+//   * epilogue: the 32 x N results staged at once in the dead plane images, then row-contiguous float4 stores of
+//     z and y with epilogue<1>'s bias / PReLU / accum arithmetic (four barriers per block in all).
 template <int K, int N>
 struct Ws32Cfg {
   static constexpr int NW = N / 32;
@@ -1279,11 +1279,12 @@ struct Ws32Cfg {
 
 template <int K, int N, bool kR1>
 struct Ws32Ring {
-  static constexpr int NST = 3;                                          // A ring depth
+  static constexpr int NST = 2;                                          // A ring depth
   static constexpr int ACC = NST * Ws32Cfg<K, N>::A_BYTES;               // accum buffer
-  static constexpr int P2 = ACC + (kR1 ? Ws32Cfg<K, N>::C_BYTES : 0);    // plane 2
-  static constexpr int BIAS = P2 + Ws32Cfg<K, N>::PL;                    // the bias row
+  static constexpr int PLANES = ACC + (kR1 ? Ws32Cfg<K, N>::C_BYTES : 0);  // the three bf16 planes
+  static constexpr int BIAS = PLANES + 3 * Ws32Cfg<K, N>::PL;            // the bias row
   static constexpr int BYTES = BIAS + N * 4;
+  static_assert(32 * N * 4 <= 3 * Ws32Cfg<K, N>::PL, "the 32-row staging fits the plane images");
 };
 
 template <int K, int N, bool kR1, bool kZ>
@@ -1304,7 +1305,7 @@ __global__ __launch_bounds__((Ws32Cfg<K, N>::NT), 1) void k_ws_f32(WsArgs32 g) {
   const int64_t G = gridDim.x;
   if ((int64_t)blockIdx.x >= nblk) return;
   const int64_t my = (nblk - 1 - blockIdx.x) / G + 1;
-  char* const plane2 = ws32_smem + R::P2;
+  char* const planes = ws32_smem + R::PLANES;
 
   // this wave's W slice as split B fragments: lane (li, lh) holds W[32 wave + li][16 t + 8 lh .. + 7]
   uint4 wf[C::KS][3];
@@ -1379,42 +1380,27 @@ __global__ __launch_bounds__((Ws32Cfg<K, N>::NT), 1) void k_ws_f32(WsArgs32 g) {
   };
 
   issue_a(0);
-  if (1 < my) issue_a(1);
   for (int64_t i = 0; i < my; ++i) {
-    // wait for A(i).  Issue order: A(0), A(1); then per iteration j: accum(j), A(j + 2), the stores of j.  The
-    // counts below are exact when every block is full (only a grid's last block is partial, and it is the last
-    // iteration of its workgroup) and count only the ops actually issued after A(i).
-    static_assert(2 * S + PC + PA <= 63, "vmcnt range");
-    if (i >= 2) {
-      if (i + 1 < my) wait_vm<2 * S + PC + PA>(); else wait_vm<2 * S + PC>();
-    } else if (i == 1) {
-      if (2 < my) wait_vm<PC + S + PA>(); else wait_vm<PC + S>();
-    } else {
-      if (1 < my) wait_vm<PA>(); else wait_vm<0>();
-    }
-    __builtin_amdgcn_s_barrier();   // A(i) landed for every wave; the slot of A(i - 1) and the accum buffer are free
+    // wait for A(i).  Issue order: A(0); then per iteration j: accum(j), A(j + 1), the stores of j.  Exact when
+    // every block is full (only a grid's last block is partial, and it is the last iteration of its workgroup).
+    if (i > 0) wait_vm<S>(); else wait_vm<0>();
+    __builtin_amdgcn_s_barrier();   // A(i) landed for every wave; the slot of A(i - 1), accum and planes are free
     asm volatile("" ::: "memory");
     if constexpr (kR1) issue_c(i);
-    if (i + 2 < my) issue_a(i + 2);
-    char* abase = ws32_smem + (int)(i % R::NST) * C::A_BYTES;
-    {   // split pass: the fp32 image -> planes 0 / 1 (in place) and 2 (own buffer)
+    if (i + 1 < my) issue_a(i + 1);
+    const char* abase = ws32_smem + (int)(i % R::NST) * C::A_BYTES;
+    {   // split pass: the fp32 image -> the three plane images
       const int t = tid_o();
-      float4 v[C::G4];
-#pragma unroll
-      for (int j = 0; j < C::G4; ++j) v[j] = *reinterpret_cast<const float4*>(abase + (j * C::NT + t) * 16);
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();               // every thread holds its groups: the image may be overwritten
-      asm volatile("" ::: "memory");
 #pragma unroll
       for (int j = 0; j < C::G4; ++j) {
         const int grp = j * C::NT + t;
+        const float4 v = *reinterpret_cast<const float4*>(abase + grp * 16);
         const int r = grp / (K / 4), k = (grp % (K / 4)) * 4;
         uint2 o[3];
-        split4(v[j], o);
+        split4(v, o);
         const int off = r * C::PROW + 16 * ((k >> 3) ^ (r & C::SW)) + 8 * ((k >> 2) & 1);
-        *reinterpret_cast<uint2*>(abase + off) = o[0];
-        *reinterpret_cast<uint2*>(abase + C::PL + off) = o[1];
-        *reinterpret_cast<uint2*>(plane2 + off) = o[2];
+#pragma unroll
+        for (int p = 0; p < 3; ++p) *reinterpret_cast<uint2*>(planes + p * C::PL + off) = o[p];
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
@@ -1431,9 +1417,9 @@ __global__ __launch_bounds__((Ws32Cfg<K, N>::NT), 1) void k_ws_f32(WsArgs32 g) {
     const int fsw = ((fl >> 5) ^ (fl & 31)) & C::SW;          // (2t + lh) ^ (li & SW) = 2t ^ fsw for 2t even
     auto frag = [&](int t, uint4 (&f)[3]) {
       const int off = frow + ((2 * t ^ fsw) << 4);
-      f[0] = *reinterpret_cast<const uint4*>(abase + off);
-      f[1] = *reinterpret_cast<const uint4*>(abase + C::PL + off);
-      f[2] = *reinterpret_cast<const uint4*>(plane2 + off);
+      f[0] = *reinterpret_cast<const uint4*>(planes + off);
+      f[1] = *reinterpret_cast<const uint4*>(planes + C::PL + off);
+      f[2] = *reinterpret_cast<const uint4*>(planes + 2 * C::PL + off);
     };
     uint4 fa[2][3];
     frag(0, fa[0]);
@@ -1457,59 +1443,54 @@ __global__ __launch_bounds__((Ws32Cfg<K, N>::NT), 1) void k_ws_f32(WsArgs32 g) {
     __builtin_amdgcn_s_setprio(0);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 
-    // accum(i) landed (A(i + 2) may stay in flight); every wave's share, so a barrier follows below
+    // accum(i) landed (A(i + 1) may stay in flight); every wave's share, so a barrier follows below
     if constexpr (kR1) {
-      if (i + 2 < my) wait_vm<PA>(); else wait_vm<0>();
+      if (i + 1 < my) wait_vm<PA>(); else wait_vm<0>();
     }
-    float* stg = reinterpret_cast<float*>(abase);                // the dead plane images
+    float* stg = reinterpret_cast<float*>(planes);               // the dead plane images: all 32 rows at once
     const float* img1 = reinterpret_cast<const float*>(ws32_smem + R::ACC);
     float* yb = g.y + r0 * N;
     float* zb = kZ ? g.z + r0 * N : nullptr;
+    __builtin_amdgcn_s_barrier();                 // every wave's plane reads are done (and its accum pieces landed)
+    asm volatile("" ::: "memory");
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      __builtin_amdgcn_s_barrier();               // plane reads / the previous half's staging reads are done
-      asm volatile("" ::: "memory");
+    for (int e = 0; e < 16; ++e) {
+      const int row = (e & 3) + 8 * (e >> 2) + 4 * lh;
+      stg[row * N + ((wave * 32 + li) ^ (((row >> 2) & 1) << 5))] = acc[e];
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
 #pragma unroll
-      for (int e8 = 0; e8 < 8; ++e8) {
-        const int e = 8 * h + e8;
-        const int row = (e & 3) + 8 * ((e >> 2) & 1) + 4 * lh;
-        stg[row * N + ((wave * 32 + li) ^ (((row >> 2) & 1) << 5))] = acc[e];
+    for (int pass = 0; pass < 4; ++pass) {
+      const int tq = tid_o();
+      const int cq = (tq % QPR) * 4;
+      const int brow = pass * 8 + tq / QPR;
+      const int64_t grow = r0 + brow;
+      const float4 v4 = *reinterpret_cast<const float4*>(stg + brow * N + (cq ^ (((brow >> 2) & 1) << 5)));
+      const float4 b4 = *reinterpret_cast<const float4*>(bias_lds + cq);
+      const float bcol[4] = {b4.x, b4.y, b4.z, b4.w};
+      float o[4] = {v4.x, v4.y, v4.z, v4.w};
+      float zz[4];
+      float in1[4] = {0.f, 0.f, 0.f, 0.f};
+      if constexpr (kR1) {
+        const float4 c4 = *reinterpret_cast<const float4*>(img1 + brow * N + cq);
+        in1[0] = c4.x; in1[1] = c4.y; in1[2] = c4.z; in1[3] = c4.w;
       }
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-      asm volatile("" ::: "memory");
 #pragma unroll
-      for (int pass = 0; pass < 2; ++pass) {
-        const int tq = tid_o();
-        const int cq = (tq % QPR) * 4;
-        const int row = pass * 8 + tq / QPR;
-        const int brow = h * 16 + row;
-        const int64_t grow = r0 + brow;
-        const float4 v4 = *reinterpret_cast<const float4*>(stg + row * N + (cq ^ (((row >> 2) & 1) << 5)));
-        const float4 b4 = *reinterpret_cast<const float4*>(bias_lds + cq);
-        const float bcol[4] = {b4.x, b4.y, b4.z, b4.w};
-        float o[4] = {v4.x, v4.y, v4.z, v4.w};
-        float zz[4];
-        float in1[4] = {0.f, 0.f, 0.f, 0.f};
-        if constexpr (kR1) {
-          const float4 c4 = *reinterpret_cast<const float4*>(img1 + brow * N + cq);
-          in1[0] = c4.x; in1[1] = c4.y; in1[2] = c4.z; in1[3] = c4.w;
-        }
-#pragma unroll
-        for (int t = 0; t < 4; ++t) {
-          zz[t] = __fadd_rn(o[t], bcol[t]);
-          const float y = zz[t] > 0.0f ? zz[t] : __fmul_rn(a_slope, zz[t]);
-          o[t] = kR1 ? __fadd_rn(in1[t], y) : y;
-        }
-        if (grow < M) {
-          const int oo = brow * N + cq;
-          if (g.nt_io) {
-            Out4<float>::st_nt(yb + oo, o, true, 4);
-            if constexpr (kZ) Out4<float>::st_nt(zb + oo, zz, true, 4);
-          } else {
-            Out4<float>::st(yb + oo, o, true, 4);
-            if constexpr (kZ) Out4<float>::st(zb + oo, zz, true, 4);
-          }
+      for (int t = 0; t < 4; ++t) {
+        zz[t] = __fadd_rn(o[t], bcol[t]);
+        const float y = zz[t] > 0.0f ? zz[t] : __fmul_rn(a_slope, zz[t]);
+        o[t] = kR1 ? __fadd_rn(in1[t], y) : y;
+      }
+      if (grow < M) {
+        const int oo = brow * N + cq;
+        if (g.nt_io) {
+          Out4<float>::st_nt(yb + oo, o, true, 4);
+          if constexpr (kZ) Out4<float>::st_nt(zb + oo, zz, true, 4);
+        } else {
+          Out4<float>::st(yb + oo, o, true, 4);
+          if constexpr (kZ) Out4<float>::st(zb + oo, zz, true, 4);
         }
       }
     }
