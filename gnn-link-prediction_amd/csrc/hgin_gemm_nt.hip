@@ -893,9 +893,16 @@ struct WsArgs32 {
   const float* w;
   const float* bias;
   const float* prelu;
-  const float* accum;
-  float* z;
-  float* y;
+  const float* r1;     // EPI 1: accum (row stride N); EPI 4: x_dst
+  int64_t ldr1;
+  const float* r2;     // EPI 4: g_prev (DMA'd into the block's dead A slot)
+  int64_t ldr2;
+  float* z;            // EPI 1: z; EPI 4: g_x_dst
+  int64_t ldz;
+  float* y;            // EPI 1: y; EPI 4: C = g_comb
+  int64_t ldy;
+  const float* eps;    // EPI 4: the GIN eps
+  float* part;         // EPI 4: one eps-gradient partial per workgroup
   int64_t M;
   bool nt_io;
   bool nt_in;
@@ -1243,9 +1250,11 @@ int try_ws_bf16(const Src2h& a, const Src2h& b, int64_t M, int64_t N, int64_t K,
 }
 
 // ---------------------------------------------------------------------------------------------------
-// k_ws_f32 — the fp32 forward MLP GEMM (EPI 1, split mode) in the weight-stationary streaming form, for the
-// square layers K = N = 256 (cfg3's layers above the first; an instantiation at K = N = 128 measured slower than
-// the tiled kernel, 600k rows: 0.279 vs 0.243 ms, so there is none):
+// k_ws_f32 — the fp32 forward MLP GEMM (EPI 1) and the dX GEMM with the self-term backward (EPI 4: x_dst rows in
+// the r1 buffer, g_prev rows DMA'd into the block's A slot once the split pass has consumed it), split mode, in the
+// weight-stationary streaming form, for the square layers K = N = 256 (cfg3's layers above the first; an
+// instantiation at K = N = 128 measured slower than the tiled kernel, 600k rows: 0.279 vs 0.243 ms, so there is
+// none):
 //   * N/32 waves; wave w holds the three bf16 planes of W[32 w .. 32 w + 31][0, K) in registers as its MFMA B
 //     fragments (3K/4 VGPRs: 192 at K = 256), split once per launch;
 //   * 32-row blocks of A (fp32) stream HBM -> LDS by DMA into a 2-slot ring (one block in flight while one is
@@ -1287,11 +1296,13 @@ struct Ws32Ring {
   static_assert(32 * N * 4 <= 3 * Ws32Cfg<K, N>::PL, "the 32-row staging fits the plane images");
 };
 
-template <int K, int N, bool kR1, bool kZ>
+template <int K, int N, int EPI, bool kR1, bool kZ, bool kR2>
 __global__ __launch_bounds__((Ws32Cfg<K, N>::NT), 1) void k_ws_f32(WsArgs32 g) {
   using C = Ws32Cfg<K, N>;
   using R = Ws32Ring<K, N, kR1>;
-  constexpr int PA = C::PA, PC = kR1 ? C::PC : 0;              // DMA instructions per wave per block (A, accum)
+  static_assert((EPI == 1 && !kR2) || (EPI == 4 && kR1 && (kZ || !kR2)), "epilogue operands");
+  constexpr int PA = C::PA, PC = kR1 ? C::PC : 0;              // DMA instructions per wave per block (A, r1)
+  constexpr int PR2 = kR2 ? C::PC : 0;                           // (r2)
   constexpr int S = 4 * (kZ ? 2 : 1);                            // stores per lane per block
   constexpr int QPR = N / 4;
   extern __shared__ __attribute__((aligned(16))) char ws32_smem[];
@@ -1324,12 +1335,15 @@ __global__ __launch_bounds__((Ws32Cfg<K, N>::NT), 1) void k_ws_f32(WsArgs32 g) {
   }
   // the bias row goes to LDS once (read per row pass: no VGPRs held across the loop); the PReLU slope is uniform
   float* const bias_lds = reinterpret_cast<float*>(ws32_smem + R::BIAS);
-  if (tid < N / 4) {
+  if (EPI == 1 && tid < N / 4) {
     const float4 b4 = *reinterpret_cast<const float4*>(g.bias + tid * 4);
     asm volatile("" ::"v"(b4.x), "v"(b4.y), "v"(b4.z), "v"(b4.w));
     *reinterpret_cast<float4*>(bias_lds + tid * 4) = b4;
   }
-  const float a_slope = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(g.prelu[0])));
+  const float a_slope = EPI == 1 ? __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(g.prelu[0]))) : 0.0f;
+  const float sc_self = EPI == 4 ? __fadd_rn(1.0f, __int_as_float(__builtin_amdgcn_readfirstlane(
+                                                        __float_as_int(g.eps[0])))) : 0.0f;
+  float ep = 0.0f;                                               // EPI 4: this thread's eps-gradient partial
 #pragma unroll
   for (int t = 0; t < C::KS; ++t)
 #pragma unroll
@@ -1363,11 +1377,11 @@ __global__ __launch_bounds__((Ws32Cfg<K, N>::NT), 1) void k_ws_f32(WsArgs32 g) {
       dma(ab + (r * (int)g.lda + (off % (K * 4)) / 4), base + piece * 1024);
     }
   };
-  auto issue_c = [&](int64_t i) {
+  auto issue_rows = [&](int64_t i, const float* src, int64_t ld, char* img) {   // N-wide rows of block i
     int64_t r0;
     int rmax;
     rows_of(i, r0, rmax);
-    const float* cb = g.accum + r0 * N;
+    const float* cb = src + r0 * ld;
     const int ln = tid_o() & 63;
 #pragma unroll
     for (int q = 0; q < C::PC; ++q) {
@@ -1375,18 +1389,19 @@ __global__ __launch_bounds__((Ws32Cfg<K, N>::NT), 1) void k_ws_f32(WsArgs32 g) {
       const int off = piece * 1024 + ln * 16;
       int r = off / (N * 4);
       r = r < rmax ? r : rmax;
-      dma(cb + (r * N + (off % (N * 4)) / 4), ws32_smem + R::ACC + piece * 1024);
+      dma(cb + (r * (int)ld + (off % (N * 4)) / 4), img + piece * 1024);
     }
   };
 
   issue_a(0);
   for (int64_t i = 0; i < my; ++i) {
-    // wait for A(i).  Issue order: A(0); then per iteration j: accum(j), A(j + 1), the stores of j.  Exact when
-    // every block is full (only a grid's last block is partial, and it is the last iteration of its workgroup).
-    if (i > 0) wait_vm<S>(); else wait_vm<0>();
-    __builtin_amdgcn_s_barrier();   // A(i) landed for every wave; the slot of A(i - 1), accum and planes are free
+    // wait for A(i).  Issue order: A(0); then per iteration j: r1(j), A(j + 1), [r2(j) after the split pass], the
+    // stores of j.  Exact when every block is full (only a grid's last block is partial, and it is the last
+    // iteration of its workgroup).
+    if (i > 0) wait_vm<S + PR2>(); else wait_vm<0>();
+    __builtin_amdgcn_s_barrier();   // A(i) landed for every wave; the slot of A(i - 1), r1 and planes are free
     asm volatile("" ::: "memory");
-    if constexpr (kR1) issue_c(i);
+    if constexpr (kR1) issue_rows(i, g.r1, g.ldr1, ws32_smem + R::ACC);
     if (i + 1 < my) issue_a(i + 1);
     const char* abase = ws32_smem + (int)(i % R::NST) * C::A_BYTES;
     {   // split pass: the fp32 image -> the three plane images
@@ -1406,6 +1421,9 @@ __global__ __launch_bounds__((Ws32Cfg<K, N>::NT), 1) void k_ws_f32(WsArgs32 g) {
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
     }
+    // g_prev rows into the block's A slot, dead after the split pass (refilled by A(i + 2) only after the next
+    // iteration's barrier)
+    if constexpr (kR2) issue_rows(i, g.r2, g.ldr2, ws32_smem + (int)(i % R::NST) * C::A_BYTES);
     const int64_t r0 = ((int64_t)blockIdx.x + i * G) * C::BM;
     f32x16 acc;
 #pragma unroll
@@ -1443,14 +1461,19 @@ __global__ __launch_bounds__((Ws32Cfg<K, N>::NT), 1) void k_ws_f32(WsArgs32 g) {
     __builtin_amdgcn_s_setprio(0);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 
-    // accum(i) landed (A(i + 1) may stay in flight); every wave's share, so a barrier follows below
-    if constexpr (kR1) {
+    // r1(i) [and r2(i)] landed (A(i + 1) may stay in flight unless r2 was issued after it); every wave's share, so a
+    // barrier follows below
+    if constexpr (kR2) {
+      wait_vm<0>();
+    } else if constexpr (kR1) {
       if (i + 1 < my) wait_vm<PA>(); else wait_vm<0>();
     }
     float* stg = reinterpret_cast<float*>(planes);               // the dead plane images: all 32 rows at once
     const float* img1 = reinterpret_cast<const float*>(ws32_smem + R::ACC);
-    float* yb = g.y + r0 * N;
-    float* zb = kZ ? g.z + r0 * N : nullptr;
+    const float* img2 = reinterpret_cast<const float*>(ws32_smem + (int)(i % R::NST) * C::A_BYTES);
+    const int ldy = EPI == 1 ? N : (int)g.ldy, ldz = EPI == 1 ? N : (int)g.ldz;
+    float* yb = g.y + r0 * ldy;
+    float* zb = kZ ? g.z + r0 * ldz : nullptr;
     __builtin_amdgcn_s_barrier();                 // every wave's plane reads are done (and its accum pieces landed)
     asm volatile("" ::: "memory");
 #pragma unroll
@@ -1468,34 +1491,50 @@ __global__ __launch_bounds__((Ws32Cfg<K, N>::NT), 1) void k_ws_f32(WsArgs32 g) {
       const int brow = pass * 8 + tq / QPR;
       const int64_t grow = r0 + brow;
       const float4 v4 = *reinterpret_cast<const float4*>(stg + brow * N + (cq ^ (((brow >> 2) & 1) << 5)));
-      const float4 b4 = *reinterpret_cast<const float4*>(bias_lds + cq);
-      const float bcol[4] = {b4.x, b4.y, b4.z, b4.w};
       float o[4] = {v4.x, v4.y, v4.z, v4.w};
-      float zz[4];
+      float zz[4] = {0.f, 0.f, 0.f, 0.f};
       float in1[4] = {0.f, 0.f, 0.f, 0.f};
       if constexpr (kR1) {
         const float4 c4 = *reinterpret_cast<const float4*>(img1 + brow * N + cq);
         in1[0] = c4.x; in1[1] = c4.y; in1[2] = c4.z; in1[3] = c4.w;
       }
+      if constexpr (EPI == 1) {
+        const float4 b4 = *reinterpret_cast<const float4*>(bias_lds + cq);
+        const float bcol[4] = {b4.x, b4.y, b4.z, b4.w};
 #pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        zz[t] = __fadd_rn(o[t], bcol[t]);
-        const float y = zz[t] > 0.0f ? zz[t] : __fmul_rn(a_slope, zz[t]);
-        o[t] = kR1 ? __fadd_rn(in1[t], y) : y;
+        for (int t = 0; t < 4; ++t) {
+          zz[t] = __fadd_rn(o[t], bcol[t]);
+          const float y = zz[t] > 0.0f ? zz[t] : __fmul_rn(a_slope, zz[t]);
+          o[t] = kR1 ? __fadd_rn(in1[t], y) : y;
+        }
       }
       if (grow < M) {
-        const int oo = brow * N + cq;
+        if constexpr (EPI == 4) {   // epilogue<4>'s self-term backward on C (every column is a self column)
+          float in2[4] = {0.f, 0.f, 0.f, 0.f};
+          if constexpr (kR2) {
+            const float4 p4 = *reinterpret_cast<const float4*>(img2 + brow * N + cq);
+            in2[0] = p4.x; in2[1] = p4.y; in2[2] = p4.z; in2[3] = p4.w;
+          }
+#pragma unroll
+          for (int t = 0; t < 4; ++t) {
+            ep = __fadd_rn(ep, __fmul_rn(o[t], in1[t]));
+            zz[t] = __fmul_rn(sc_self, o[t]);
+            if (kR2) zz[t] = __fadd_rn(in2[t], zz[t]);
+          }
+        }
+        const int oy = brow * ldy + cq, oz = brow * ldz + cq;
         if (g.nt_io) {
-          Out4<float>::st_nt(yb + oo, o, true, 4);
-          if constexpr (kZ) Out4<float>::st_nt(zb + oo, zz, true, 4);
+          Out4<float>::st_nt(yb + oy, o, true, 4);
+          if constexpr (kZ) Out4<float>::st_nt(zb + oz, zz, true, 4);
         } else {
-          Out4<float>::st(yb + oo, o, true, 4);
-          if constexpr (kZ) Out4<float>::st(zb + oo, zz, true, 4);
+          Out4<float>::st(yb + oy, o, true, 4);
+          if constexpr (kZ) Out4<float>::st(zb + oz, zz, true, 4);
         }
       }
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   }
+  if constexpr (EPI == 4) tile_partial(reinterpret_cast<float*>(ws32_smem), ep, g.part, blockIdx.x);
 }
 
 // HGIN_NT_WS32 = 0 keeps the tiled kernel for the fp32 forward GEMM.
@@ -1507,11 +1546,11 @@ bool ws32_enabled() {
   return on;
 }
 
-template <int K, int N, bool kR1, bool kZ>
-int launch_ws32(const WsArgs32& a, hipStream_t s, const char* what) {
+template <int K, int N, int EPI, bool kR1, bool kZ, bool kR2>
+int launch_ws32(const WsArgs32& a, hipStream_t s, const char* what, int64_t* grid_out = nullptr) {
   constexpr int lds = Ws32Ring<K, N, kR1>::BYTES;
   static_assert(lds <= 160 * 1024, "LDS");
-  auto kern = k_ws_f32<K, N, kR1, kZ>;
+  auto kern = k_ws_f32<K, N, EPI, kR1, kZ, kR2>;
   static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
                                                      hipFuncAttributeMaxDynamicSharedMemorySize, lds);
   if (attr != hipSuccess) {
@@ -1521,6 +1560,7 @@ int launch_ws32(const WsArgs32& a, hipStream_t s, const char* what) {
   const int64_t nblk = ceil_div(a.M, (int64_t)Ws32Cfg<K, N>::BM);
   const int64_t grid = nblk < ws_grid() ? nblk : ws_grid();
   kern<<<(unsigned)grid, Ws32Cfg<K, N>::NT, lds, s>>>(a);
+  if (grid_out) *grid_out = grid;
   return check_launch(what);
 }
 
@@ -1529,17 +1569,40 @@ int launch_ws32(const WsArgs32& a, hipStream_t s, const char* what) {
 int try_ws_f32(const float* a1, int64_t lda1, int64_t k1, const float* a2_eps, const float* w, const float* bias,
                const float* prelu, const float* accum, float* z, float* y, int64_t M, int64_t N, int64_t K,
                hipStream_t s, const char* what) {
-  // (profiles/r02/gemm_ws_f32_fwd.txt)
+  // (profiles/r02/gemm_ws_f32.txt)
   if (!ws32_enabled() || !gemm_split_enabled() || M < 1 || K != N || K != 256 || k1 != K || a2_eps != nullptr)
     return -1;
   if (!aligned16(a1) || lda1 % 4 || lda1 >= (int64_t(1) << 24) || !aligned16(w) || !aligned16(y) ||
       (z && !aligned16(z)) || (accum && !aligned16(accum)))
     return -1;
-  WsArgs32 g{a1, lda1, w, bias, prelu, accum, z, y, M, gemm_nt_io(M, N, 4), ws_nt_in()};
-  if (accum && z) return launch_ws32<256, 256, true, true>(g, s, what);
-  if (accum) return launch_ws32<256, 256, true, false>(g, s, what);
-  if (z) return launch_ws32<256, 256, false, true>(g, s, what);
-  return launch_ws32<256, 256, false, false>(g, s, what);
+  WsArgs32 g{a1, lda1, w, bias, prelu, accum, N, nullptr, 0, z, N, y, N, nullptr, nullptr, M, gemm_nt_io(M, N, 4),
+             ws_nt_in()};
+  if (accum && z) return launch_ws32<256, 256, 1, true, true, false>(g, s, what);
+  if (accum) return launch_ws32<256, 256, 1, true, false, false>(g, s, what);
+  if (z) return launch_ws32<256, 256, 1, false, true, false>(g, s, what);
+  return launch_ws32<256, 256, 1, false, false, false>(g, s, what);
+}
+
+// The dX GEMM with the self-term backward (EPI 4, hgin_gemm_nt_combine_f32) in the same form: C = A B^T with
+// B packed [N, K], K = N = 256, the self term on every column (cs = 0); x_dst [, g_x_dst, g_prev] rows of any
+// 16-B aligned stride.  Returns -1 when it does not apply; *grid_out = the workgroups (= eps partials).
+int try_ws_f32_comb(const float* a, int64_t lda, const float* b, int64_t ldb, float* c, int64_t ldc, int64_t M,
+                    int64_t N, int64_t K, const CombEpi& ce, hipStream_t s, const char* what, int64_t* grid_out) {
+  if (!ws32_enabled() || !gemm_split_enabled() || M < 1 || K != N || K != 256 || ldb != K || ce.cs != 0) return -1;
+  auto ok = [](const void* p, int64_t ld) {
+    return p == nullptr || (aligned16(p) && ld % 4 == 0 && ld < (int64_t(1) << 24));
+  };
+  const float* xd = static_cast<const float*>(ce.xd);
+  float* gd = static_cast<float*>(ce.gd);
+  const float* gp = static_cast<const float*>(ce.gp);
+  if (!xd || !aligned16(b) || !ok(a, lda) || !ok(c, ldc) || !ok(xd, ce.ldxd) || !ok(gd, ce.ldgd) ||
+      !ok(gp, ce.ldgp) || (gp && !gd))
+    return -1;
+  WsArgs32 g{a, lda, b, nullptr, nullptr, xd, ce.ldxd, gp, ce.ldgp, gd, ce.ldgd, c, ldc, ce.eps, ce.part, M,
+             gemm_nt_io(M, N, 4), ws_nt_in()};
+  if (gd && gp) return launch_ws32<256, 256, 4, true, true, true>(g, s, what, grid_out);
+  if (gd) return launch_ws32<256, 256, 4, true, true, false>(g, s, what, grid_out);
+  return launch_ws32<256, 256, 4, true, false, false>(g, s, what, grid_out);
 }
 
 // K-tile depth of the bf16 NT kernel (HGIN_NT_BKH = 64 / 128).  128: twice the A bytes per prefetch (32 KB
@@ -1993,9 +2056,13 @@ int gemm_nt_combine(const char* what, const T* a, int64_t lda, const T* b, int64
   else if constexpr (sizeof(T) == 2)
     rc = launch_nt_bf16<4, uint16_t>(Src2h{a, lda, nullptr, 0, K}, Src2h{b, ldb, nullptr, 0, K}, M, N, K, nullptr,
                                      nullptr, nullptr, nullptr, c, ldc, s, what, ce, &tiles);
-  else
-    rc = launch_nt<4>(Src2{a, lda, nullptr, 0, K}, Src2{b, ldb, nullptr, 0, K}, M, N, K, nullptr, nullptr, nullptr,
-                      nullptr, c, ldc, s, what, ce, &tiles);
+  else if constexpr (sizeof(T) == 4) {
+    ce.nt_io = gemm_nt_io(M, N, 4);
+    rc = try_ws_f32_comb(a, lda, b, ldb, c, ldc, M, N, K, ce, s, what, &tiles);
+    if (rc < 0)
+      rc = launch_nt<4>(Src2{a, lda, nullptr, 0, K}, Src2{b, ldb, nullptr, 0, K}, M, N, K, nullptr, nullptr, nullptr,
+                        nullptr, c, ldc, s, what, ce, &tiles);
+  }
   if (rc) return rc;
   const int64_t nb = ceil_div(tiles, kPartChunk);
   if (nb == 1) {

@@ -118,6 +118,37 @@ def run_dx(M, K, N, comb, *, g):
     return out
 
 
+DX_F32_CASES = [  # (M, want_gx, with g_prev) — the fp32 dX GEMM with the self-term backward, K = N = 256
+    (150_001, True, True), (99_999, True, False), (40_000, False, False), (33, True, True),
+]
+
+
+def run_dx_f32(M, want_gx, with_prev, *, g):
+    """fp32 ops.gemm_nt_combine (k_ws_f32 EPI 4 by default): c within the fp32 bound of an fp64 evaluation,
+    g_x_dst exactly fp32((1 + eps) c) [+ g_prev] on the kernel's own c, the eps gradient within 1e-5."""
+    K = N = 256
+    a = torch.randn(M, K, device="cuda", generator=g)
+    b = torch.randn(N, K, device="cuda", generator=g) / K ** 0.5
+    xd = torch.randn(M, N, device="cuda", generator=g)
+    eps = torch.tensor([0.3], device="cuda")
+    prev = torch.randn(M, N, device="cuda", generator=g) if with_prev else None
+    prev0 = prev.clone() if with_prev else None
+    c, gx, ge = ops.gemm_nt_combine(a, b, xd, eps, 0, want_gx, g_prev=prev)
+    cr = a.double() @ b.double().t()
+    assert bool(((c.double() - cr).abs() <= 1e-6 * cr.abs() + 1e-5 * (a.double().abs() @ b.double().abs().t())
+                 ).all()), (M, "c")
+    ge_ref = float((c.double() * xd.double()).sum())
+    assert abs(float(ge) - ge_ref) <= 1e-5 * float((c.double() * xd.double()).abs().sum()), (M, float(ge), ge_ref)
+    out = {"c": c.cpu(), "tol_g_eps": ge.detach().reshape(1).cpu()}
+    if want_gx:
+        gr = (1.0 + eps) * c                      # fp32 (1 + eps), then the product, as the epilogue rounds them
+        if with_prev:
+            gr = prev0 + gr
+        assert torch.equal(gx, gr), (M, "g_x_dst")
+        out["gx"] = gx.cpu()
+    return out
+
+
 DW_CASES = [  # (M, N, K, k1 of a two-source B or 0) — the bf16 weight-gradient GEMM (ops.gemm_tn)
     (300_007, 256, 256, 0), (1, 256, 256, 0), (45, 256, 128, 0), (100_000, 128, 256, 128), (77_777, 128, 128, 0),
     (64_001, 256, 256, 256), (200_003, 256, 512, 256), (9_000, 128, 512, 200), (5, 256, 512, 0),
@@ -143,6 +174,7 @@ def main():
     res = {f"{c}": run(*c, g=g) for c in CASES}
     res.update({f"f32{c}": run_f32(*c, g=g) for c in F32_CASES})
     res.update({f"dx{c}": run_dx(*c, g=g) for c in DX_CASES})
+    res.update({f"dxf32{c}": run_dx_f32(*c, g=g) for c in DX_F32_CASES})
     res.update({f"dw{c}": run_dw(*c, g=g) for c in DW_CASES})
     torch.save(res, sys.argv[1])
     print("gemm child ok", {k: v for k, v in os.environ.items() if k.startswith("HGIN_")}, flush=True)

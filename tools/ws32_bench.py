@@ -43,6 +43,19 @@ def main():
         out.append({"M": M, "K": K, "N": N, "accum": with_acc, "ms": round(ms, 4), "GB_s": round(byt / ms / 1e6, 1),
                     "tflops_equiv": round(2.0 * M * N * K / ms / 1e9, 1)})
         del a, acc
+    # the dX GEMM with the self-term backward (EPI 4): read g_z, x_dst [, g_prev], write C [, g_x_dst]
+    for M, want_gx, with_prev in [(6_000_000, True, False), (3_000_000, True, True), (1_000_000, False, False)]:
+        K = N = 256
+        a = torch.randn(M, K, device="cuda")
+        b = torch.randn(N, K, device="cuda") / K ** 0.5
+        xd = torch.randn(M, N, device="cuda")
+        eps = torch.tensor([0.3], device="cuda")
+        prev = torch.randn(M, N, device="cuda") if with_prev else None
+        ms = timeit(lambda: ops.gemm_nt_combine(a, b, xd, eps, 0, want_gx, g_prev=prev))
+        byt = 4.0 * M * (K + N * (2 + (1 if want_gx else 0) + (1 if with_prev else 0)))
+        out.append({"combine": True, "M": M, "want_gx": want_gx, "g_prev": with_prev, "ms": round(ms, 4),
+                    "GB_s": round(byt / ms / 1e6, 1)})
+        del a, xd, prev
     print(json.dumps({"HGIN_NT_WS32": os.environ.get("HGIN_NT_WS32", "1"), "shapes": out}))
 
 
