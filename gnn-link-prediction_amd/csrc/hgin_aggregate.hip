@@ -197,6 +197,7 @@ int launch_aggregate(const int32_t* rowptr, const int32_t* col, int64_t n_rows, 
   const int64_t waves = ceil_div(n_rows, kRowsPerWave);
   const int64_t blocks = ceil_div(waves, 256 / kWave);
   const bool nt = agg_nt(combine, n_rows, (int64_t)(f_src + (combine == HGIN_COMBINE_CONCAT ? f_dst : 0)) * 4);
+  HGIN_TRACE("k_aggregate<f32,G%d,mode%d>", G, combine);
 #define HGIN_AGG_L(UV, NTV, TAIL)                                                                           \
   k_aggregate<VEC, G, UV, NTV, TAIL><<<dim3((unsigned)blocks), 256, 0, s>>>(rowptr, col, n_rows, x_src, ld_src, \
                                                                            f_src, x_dst, ld_dst, f_dst, eps,     \
@@ -358,6 +359,7 @@ int launch_aggregate_bf16(const int32_t* rowptr, const int32_t* col, int64_t n_r
                           int combine, uint16_t* out, int64_t ld_out, hipStream_t s) {
   constexpr int kRowsPerWave = kWave / G;
   const int64_t blocks = ceil_div(ceil_div(n_rows, kRowsPerWave), 256 / kWave);
+  HGIN_TRACE("k_aggregate<bf16,G%d,mode%d>", G, combine);
 #define HGIN_AGGB_L(UV, NTV, TAIL)                                    \
   k_aggregate_bf16<VEC, G, UV, NTV, TAIL><<<dim3((unsigned)blocks), 256, 0, s>>>( \
       rowptr, col, n_rows, x_src, ld_src, f_src, x_dst, ld_dst, f_dst, eps, combine, out, ld_out)
@@ -567,6 +569,7 @@ int launch_agg_q(int lanes_needed, const int32_t* rowptr, const int32_t* col, in
   constexpr int kU = NQ >= 4 ? 4 : 8;
   const bool nt = agg_nt(combine, n_rows, (int64_t)(f_src + (combine == HGIN_COMBINE_CONCAT ? f_dst : 0)) * (int64_t)sizeof(T));
   const bool tail = agg_tail_batched();
+  HGIN_TRACE("k_agg_q<%s,NQ%d,mode%d>", sizeof(T) == 4 ? "f32" : "bf16", NQ, combine);
 #define HGIN_AGGQ_L(GV, NTV, TAIL, BLOCKS)                                                                      \
   k_agg_q<T, NQ, GV, kU, NTV, TAIL><<<dim3((unsigned)(BLOCKS)), 256, 0, s>>>(rowptr, col, n_rows, x_src, ld_src, \
                                                                             f_src, x_dst, ld_dst, f_dst, eps,   \
@@ -731,6 +734,7 @@ int launch_agg_pipe_g(const int32_t* rowptr, const int32_t* col, int64_t n_rows,
   static const int64_t slots = agg_resident_blocks(k_agg_pipe<T, G, U, NT>);
   const int64_t need = ceil_div(n_rows, (int64_t)(256 / G));
   const int64_t blocks = need < slots ? need : slots;
+  HGIN_TRACE("k_agg_pipe<%s,G%d,mode%d>", sizeof(T) == 4 ? "f32" : "bf16", G, combine);
   k_agg_pipe<T, G, U, NT><<<dim3((unsigned)blocks), 256, 0, s>>>(rowptr, col, n_rows, x_src, ld_src, f_src, x_dst,
                                                                   ld_dst, f_dst, eps, combine, out, ld_out);
   return HGIN_OK;
@@ -908,6 +912,7 @@ int aggregate_long(const char* what, const int32_t* col, const int32_t* items, i
                  what);
   hipStream_t s = as_stream(stream);
   const unsigned pb = (unsigned)ceil_div(n_items, 4);
+  HGIN_TRACE("k_long_partial+k_long_combine<%s,mode%d>", sizeof(T) == 4 ? "f32" : "bf16", combine);
   k_long_partial<T, 8><<<pb, 256, 0, s>>>(col, items, n_items, x_src, ld_src, (int)f_src, partial);
   const unsigned cb = (unsigned)ceil_div(n_long, 4);
   k_long_combine<T><<<cb, 256, 0, s>>>(long_rows, item_ptr, n_long, partial, (int)f_src, x_dst, ld_dst, eps, combine,

@@ -15,6 +15,16 @@ constexpr int kWave = 64;  // CDNA wavefront
 
 void set_error(const char* fmt, ...);
 
+// Launch trace (hgin_trace_enable / hgin_trace_read): when on, every dispatch site records which kernel variant
+// it launched, so tests can prove which instantiations a call exercised.  Off by default; one relaxed atomic load
+// per launch when off.
+bool trace_on();
+void trace_launch(const char* fmt, ...);
+#define HGIN_TRACE(...)                                       \
+  do {                                                        \
+    if (::hgin::trace_on()) ::hgin::trace_launch(__VA_ARGS__); \
+  } while (0)
+
 inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 
 // Launch bookkeeping: returns 0 or the hipError_t of the launch (after recording a message).

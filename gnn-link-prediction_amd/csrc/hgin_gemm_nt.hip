@@ -509,6 +509,8 @@ int64_t launch_nt_tn(bool vec, const Src2& a, const Src2& b, int64_t M, int64_t 
   const int64_t tiles = ceil_div(N, BN) * ceil_div(M, BM);
   const bool xcd = xcd_remap_enabled();
   dim3 grid((unsigned)(xcd ? round_up8(tiles) : tiles));
+  HGIN_TRACE("k_gemm_nt<EPI%d,%dx%d,%s,N%lld,K%lld>", EPI, (NW / WN) * 64, WN * TN * 32,
+             gemm_split_enabled() ? "split" : "mfma32", (long long)N, (long long)K);
 #define HGIN_NT_F32(CLEAN, SPLIT)                                                                           \
   k_gemm_nt<EPI, CLEAN, TN, WN, SPLIT, NW><<<grid, NW * 64, 0, s>>>(a, b, M, N, K, bias, prelu, accum, z, y, ldc, \
                                                                     vec_out, tiles, xcd, ce)
@@ -1180,6 +1182,7 @@ int launch_ws_kn(const WsArgs& a, hipStream_t s, const char* what, int64_t* grid
     }
     const int64_t nblk = ceil_div(a.M, (int64_t)WsCfg<K, N>::BM);
     const int64_t grid = nblk < ws_grid() ? nblk : ws_grid();
+    HGIN_TRACE("k_ws_bf16<%d,%d,EPI%d>", K, N, EPI);
     kern<<<(unsigned)grid, WsCfg<K, N>::NT, lds, s>>>(a);
     if (grid_out) *grid_out = grid;
     return check_launch(what);
@@ -1559,6 +1562,7 @@ int launch_ws32(const WsArgs32& a, hipStream_t s, const char* what, int64_t* gri
   }
   const int64_t nblk = ceil_div(a.M, (int64_t)Ws32Cfg<K, N>::BM);
   const int64_t grid = nblk < ws_grid() ? nblk : ws_grid();
+  HGIN_TRACE("k_ws_f32<%d,%d,EPI%d>", K, N, EPI);
   kern<<<(unsigned)grid, Ws32Cfg<K, N>::NT, lds, s>>>(a);
   if (grid_out) *grid_out = grid;
   return check_launch(what);
@@ -1639,6 +1643,7 @@ int launch_nt_bf16(const Src2h& a, const Src2h& b, int64_t M, int64_t N, int64_t
     const int64_t tiles = ceil_div(N, BN) * ceil_div(M, BM);                                                 \
     const bool xcd = xcd_remap_enabled();                                                                    \
     dim3 grid((unsigned)(xcd ? round_up8(tiles) : tiles));                                                   \
+    HGIN_TRACE("k_gemm_nt_bf16<EPI%d,%dx%d,N%lld,K%lld>", EPI, BM, BN, (long long)N, (long long)K);       \
     if (deep)                                                                                                \
       k_gemm_nt_bf16<EPI, true, TNV, WNV, OutT, 128><<<grid, 256, 0, s>>>(a, b, M, N, K, bias, prelu, accum, \
                                                                           z, y, ldc, vec_out, tiles, xcd, ce); \
@@ -1963,6 +1968,7 @@ int launch_nt2(const T* a1, int64_t lda1, int64_t k1, const T* a2, int64_t lda2,
     }                                                                                                          \
     const int64_t tiles = ceil_div(M, 128) * (N / BNV);                                                        \
     dim3 grid((unsigned)(xcd ? round_up8(tiles) : tiles));                                                     \
+    HGIN_TRACE("k_nt2<EPI%d,BN%d>", EPI, BNV);                                                                 \
     kern<<<grid, 256, lds, s>>>(a1, lda1, a2, lda2, k1, eps2, bp, M, N, K, bias, prelu, accum, z, y, ldc,      \
                                 vec_out, tiles, xcd, ce);                                                      \
     if (tiles_out) *tiles_out = tiles;                                                                         \

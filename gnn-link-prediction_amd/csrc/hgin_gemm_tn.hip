@@ -1209,6 +1209,7 @@ int64_t launch_wsd(const uint16_t* a, int64_t lda, const uint16_t* b1, int64_t l
     const char* v = getenv("HGIN_WS_NT");
     return !(v && v[0] == '0');
   }();
+  HGIN_TRACE("k_wsd_bf16<%d,%d>", NV, KV);
   kern<<<(unsigned)grid, 512, lds, s>>>(a, lda, b1, ldb1, b2, ldb2, k1, M, slab, ld_slab, nt);
   return grid;
 }
@@ -1225,6 +1226,7 @@ int64_t launch_wsd(const float* a, int64_t lda, const float* b1, int64_t ldb1, c
     const char* v = getenv("HGIN_WS_NT");
     return !(v && v[0] == '0');
   }();
+  HGIN_TRACE("k_wsd_f32<%d,%d>", NV, KV);
   kern<<<(unsigned)grid, 512, lds, s>>>(a, lda, b1, ldb1, b2, ldb2, k1, M, slab, ld_slab, nt);
   return grid;
 }
@@ -1410,6 +1412,7 @@ int gemm_tn_impl(const char* what, const T* a, int64_t lda, const T* b1, int64_t
   int64_t tile_n = 128;
   if (small) {
     HGIN_ARG_CHECK(!pro_in, "%s: no fused prologue for N or K < 16", what);
+    HGIN_TRACE("k_tn_small<N%lld,K%lld>", (long long)N, (long long)K);
     k_tn_small<T><<<(unsigned)S_eff, 256, 0, s>>>(a, lda, b1, ldb1, b2, ldb2, k1, M, (int)N, (int)K, rows, slab);
   } else if (int64_t g = (!pro_in && vec) ? try_wsd<T>(a, lda, b1, ldb1, k1, b2, ldb2, M, N, K, slab,
                                                         tn_ws_slabs(M, N, K), s)
@@ -1420,6 +1423,7 @@ int gemm_tn_impl(const char* what, const T* a, int64_t lda, const T* b1, int64_t
     const TnGrid tg{128, tiles_n, tiles_n * ceil_div(K, 128), tiles_n * ceil_div(K, 128) * S_eff, xcd_remap_enabled()};
     dim3 grid((unsigned)(tg.xcd ? round_up8(tg.n_work) : tg.n_work));
     HGIN_ARG_CHECK(!pro_in, "%s: no fused prologue for bf16", what);
+    HGIN_TRACE("k_gemm_tn_bf16<%s,N%lld,K%lld>", tn_bf16_tr() ? "tr" : "regt", (long long)N, (long long)K);
     if (tn_bf16_tr()) {
       if (vec && N % 8 == 0 && K % 8 == 0)
         k_gemm_tn_bf16_tr<true><<<grid, 256, 0, s>>>(a, lda, b1, ldb1, b2, ldb2, k1, M, N, K, rows, slab, tg);
@@ -1440,6 +1444,8 @@ int gemm_tn_impl(const char* what, const T* a, int64_t lda, const T* b1, int64_t
     // loop, 3-5 % faster than prefetch at 2 waves)
     const bool clean = vec && N % tile_n == 0 && K % 128 == 0 && k1 % 128 == 0;
     const bool split = gemm_split_enabled();
+    HGIN_TRACE("k_gemm_tn_partial<%s,%s,N%lld,K%lld>", pro_in ? "prelu_bwd_fused" : "plain", split ? "split" : "mfma32",
+               (long long)N, (long long)K);
 #define HGIN_TN_LAUNCH(CLEAN, TNR, SPLIT, PRO, LATE)                                                          \
   k_gemm_tn_partial<CLEAN, TNR, SPLIT, PRO, LATE><<<grid, 256, 0, s>>>(a, lda, b1, ldb1, b2, ldb2, k1, M, N, K, \
                                                                         rows, vec, slab, tg, pro)

@@ -1,5 +1,8 @@
 // Error reporting for the C ABI (include/hgin.h).
+#include <atomic>
 #include <cstdarg>
+#include <cstring>
+#include <mutex>
 
 #include "hgin_common.h"
 
@@ -14,6 +17,23 @@ void set_error(const char* fmt, ...) {
   vsnprintf(buf, sizeof(buf), fmt, ap);
   va_end(ap);
   g_last_error = buf;
+}
+
+static std::atomic<bool> g_trace{false};
+static std::mutex g_trace_mu;
+static std::string g_trace_buf;
+
+bool trace_on() { return g_trace.load(std::memory_order_relaxed); }
+
+void trace_launch(const char* fmt, ...) {
+  char buf[256];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  std::lock_guard<std::mutex> lk(g_trace_mu);
+  g_trace_buf += buf;
+  g_trace_buf += '\n';
 }
 
 bool xcd_remap_enabled() {
@@ -37,3 +57,22 @@ bool gemm_split_enabled() {
 extern "C" int hgin_abi_version(void) { return HGIN_ABI_VERSION; }
 
 extern "C" const char* hgin_last_error(void) { return hgin::g_last_error.c_str(); }
+
+extern "C" int hgin_trace_enable(int on) {
+  std::lock_guard<std::mutex> lk(hgin::g_trace_mu);
+  hgin::g_trace_buf.clear();
+  hgin::g_trace.store(on != 0, std::memory_order_relaxed);
+  return HGIN_OK;
+}
+
+extern "C" size_t hgin_trace_read(char* buf, size_t cap) {
+  std::lock_guard<std::mutex> lk(hgin::g_trace_mu);
+  const size_t n = hgin::g_trace_buf.size();
+  if (buf && cap > 0) {
+    const size_t c = n < cap - 1 ? n : cap - 1;
+    std::memcpy(buf, hgin::g_trace_buf.data(), c);
+    buf[c] = '\0';
+    if (c == n) hgin::g_trace_buf.clear();
+  }
+  return n;
+}

@@ -174,8 +174,10 @@ _SIGS = {
     "hgin_nt_planes_size": ([_I64, _I64, _I32, ctypes.POINTER(_SZ)], _I32),
     "hgin_nt_planes_f32": ([_P, _I64, _I64, _I64, _P, _P], _I32),
     "hgin_nt_planes_bf16": ([_P, _I64, _I64, _I64, _P, _P], _I32),
+    "hgin_trace_enable": ([_I32], _I32),
+    "hgin_trace_read": ([ctypes.c_char_p, _SZ], _SZ),
 }
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 
 def lib() -> ctypes.CDLL:
@@ -209,6 +211,25 @@ def check(rc: int, what: str) -> None:
 
 def call(name: str, *args) -> None:
     check(getattr(lib(), name)(*args), name)
+
+
+class trace_launches:
+    """Context manager recording the kernel variant of every libhgin.so launch issued inside it
+    (hgin_trace_enable / hgin_trace_read); ``.kernels`` is the list of tags, in launch order."""
+
+    def __enter__(self):
+        self.kernels = []
+        lib().hgin_trace_enable(1)
+        return self
+
+    def __exit__(self, *exc):
+        h = lib()
+        n = h.hgin_trace_read(None, 0)
+        buf = ctypes.create_string_buffer(n + 1)
+        h.hgin_trace_read(buf, n + 1)
+        h.hgin_trace_enable(0)
+        self.kernels = [t for t in buf.value.decode().split("\n") if t]
+        return False
 
 
 def exported_symbols():

@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define HGIN_ABI_VERSION 2
+#define HGIN_ABI_VERSION 3
 
 #define HGIN_OK 0
 #define HGIN_E_ARG (-1)        /* bad size / null pointer / unsupported combination */
@@ -46,6 +46,14 @@ extern "C" {
 
 int hgin_abi_version(void);
 const char* hgin_last_error(void);
+
+/* Launch trace (test / diagnostics; no reference counterpart).  hgin_trace_enable(1) clears the record and
+ * starts recording, at every dispatch site, the kernel variant launched (one '\n'-terminated tag per launch,
+ * e.g. "k_ws_f32<256,256,EPI1>"); hgin_trace_enable(0) stops.  hgin_trace_read copies the record into buf
+ * (NUL-terminated, at most cap - 1 bytes; the record is drained when it fits) and returns its full length.
+ * Host-side only: nothing is synchronised. */
+int hgin_trace_enable(int on);
+size_t hgin_trace_read(char* buf, size_t cap);
 
 /* ---- A12: COO -> CSR / CSC (stable) ------------------------------------------------------------
  * Replaces nothing in the reference directly: PyG scatters unsorted COO with atomics

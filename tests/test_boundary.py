@@ -14,7 +14,7 @@ HEADER = os.path.join(ROOT, "include", "hgin.h")
 
 def declared_symbols():
     text = open(HEADER).read()
-    return sorted(set(re.findall(r"^\s*(?:int|const char\*)\s+(hgin_\w+)\s*\(", text, re.M)))
+    return sorted(set(re.findall(r"^\s*(?:int|size_t|const char\*)\s+(hgin_\w+)\s*\(", text, re.M)))
 
 
 def test_header_declares_the_bound_api():

@@ -195,11 +195,11 @@ def test_linear_prelu_bf16_autograd():
 
 # ------------------------------------------------------------------------- model: tolerance sweep
 def _fixture_bf16_vs_fp32(case):
-    from conftest import fixture_inputs, fixture_model_kwargs, load_fixture
+    from conftest import fixture_inputs, fixture_model_kwargs, fixture_state_dict, load_fixture
     from hgin.train import mape
     fx = load_fixture(case)
     model = HetroGIN(**fixture_model_kwargs(fx))
-    model.load_state_dict({k[3:]: v for k, v in fx.items() if k.startswith("sd.")})
+    model.load_state_dict(fixture_state_dict(fx))
     model = model.to(DEV).train()
     x, ei, batch, y = fixture_inputs(fx, DEV)
     out = model({t: v.to(BF) for t, v in x.items()}, ei, batch)
@@ -216,7 +216,7 @@ def _fixture_bf16_vs_fp32(case):
     return err_out, errs, float(loss), float(fx["loss_value"])
 
 
-@pytest.mark.parametrize("case", ["cfg1_L2", "wide_L3", "w128_L2"])
+@pytest.mark.parametrize("case", ["cfg1_L2", "wide_L3", "w128_L2", "w256_L3"])
 def test_model_bf16_tolerance_sweep(case):
     """bf16 features/activations vs the fp32 reference fixtures.  Bounds: output rel-L2 <= 3e-2, loss within
     2 %, median parameter-gradient rel-L2 <= 5e-2 (bf16 has an 8-bit mantissa: 2^-9 = 2e-3 per rounding,

@@ -353,6 +353,36 @@ def test_mlp_bwd_fused(M, N, K1, K2, want_gz, strided):
     assert all(torch.equal(p, q) for p, q in zip(again[:3], (g_w, g_a, g_b)))    # deterministic
 
 
+def test_mlp_bwd_fused_cfg3_layer0_shape():
+    """The largest GEMM of the cfg3 step at its own shape: the first layer's fused PReLU + bias backward + dW
+    (N = 256, K = 256 + 256 = [aggregate | x_dst], 1M rows; cfg3 runs it at 3-6M), against float64, with the
+    launch trace proving the fused kernel (not the two-pass fallback) ran."""
+    from hgin import _lib
+    M, N, K1, K2 = 1 << 20, 256, 256, 256
+    gen = torch.Generator(device=DEV).manual_seed(11)
+    gy = torch.randn(M, N, device=DEV, generator=gen)
+    z = torch.randn(M, N, device=DEV, generator=gen)
+    a = torch.tensor([0.25], device=DEV)
+    b1 = torch.randn(M, K1, device=DEV, generator=gen)
+    b2 = torch.randn(M, K2, device=DEV, generator=gen)
+    with _lib.trace_launches() as tr:
+        g_w, g_a, g_b, g_z = ops.mlp_bwd_w(gy, z, a, b1, b2)
+    torch.cuda.synchronize()
+    assert g_z is None
+    assert "k_gemm_tn_partial<prelu_bwd_fused,split,N256,K512>" in tr.kernels, tr.kernels
+    assert "k_rows_bwd<0,f32>" not in tr.kernels
+    zr, gyr = z.double(), gy.double()
+    ga_ref = float((torch.where(zr > 0, torch.zeros_like(zr), zr) * gyr).sum())
+    assert abs(float(g_a) - ga_ref) <= 1e-5 * (float((zr * gyr).abs().sum()) + 1)
+    gzd = torch.where(zr > 0, gyr, 0.25 * gyr)
+    del zr, gyr, z, gy
+    assert ((g_b.double() - gzd.sum(0)).abs() <= 1e-5 * gzd.abs().sum(0) + 1e-6).all()
+    b = torch.cat((b1, b2), 1).double()
+    ref_w = gzd.t() @ b
+    bound = 1e-5 * (gzd.abs().t() @ b.abs() + 1)
+    assert ((g_w.double() - ref_w).abs() <= bound).all()
+
+
 def test_combine_bwd():
     g = torch.randn(900, 130, device=DEV)
     x = torch.randn(900, 64, device=DEV)

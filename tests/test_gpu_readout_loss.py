@@ -5,7 +5,7 @@ import numpy as np
 import pytest
 import torch
 
-from conftest import fixture_inputs, fixture_model_kwargs, load_fixture
+from conftest import fixture_inputs, fixture_model_kwargs, fixture_state_dict, load_fixture
 from hgin import HetroGIN, ops
 from hgin.train import mape, train_step
 
@@ -59,11 +59,11 @@ def test_head_mape_deterministic_and_no_sync_needed():
         assert torch.equal(a, b)
 
 
-@pytest.mark.parametrize("case", ["cfg1_L2", "wide_L3", "w128_L2"])
+@pytest.mark.parametrize("case", ["cfg1_L2", "wide_L3", "w128_L2", "w256_L3"])
 def test_fused_loss_matches_reference_fixture(case):
     fx = load_fixture(case)
     model = HetroGIN(**fixture_model_kwargs(fx))
-    model.load_state_dict({k[3:]: v for k, v in fx.items() if k.startswith("sd.")})
+    model.load_state_dict(fixture_state_dict(fx))
     model = model.to(DEV).train()
     x, ei, batch, y = fixture_inputs(fx, DEV)
     out, lv = model.forward_loss(dict(x), ei, batch, y)

@@ -6,7 +6,8 @@ import pytest
 import torch
 
 import models as dropin_models
-from conftest import CASES, fixture_model_kwargs, load_fixture
+from conftest import (CASES, assert_state_dict_digests, fixture_model_kwargs, fixture_state_dict, is_compact,
+                      load_fixture)
 from hgin import GINConv, GINLayer, HetroGAT, HetroGIN, ops
 from hgin.data import CONFIGS, REL_LP, REL_PL, collate, scaled_config, synthetic_graph
 from hgin.models import make_activation
@@ -28,11 +29,14 @@ def test_init_and_state_dict_match_reference(case):
     model = HetroGIN(**kw)
     assert kw["input_channels"] == fx["meta"]["input_channels_after_ctor"]  # mutated like the reference
     sd = model.state_dict()
-    assert list(sd) == [k[3:] for k in fx if k.startswith("sd.")]
-    for k, v in sd.items():
-        assert torch.equal(v, fx["sd." + k]), k
+    if is_compact(fx):
+        assert_state_dict_digests(fx, sd)
+    else:
+        assert list(sd) == [k[3:] for k in fx if k.startswith("sd.")]
+        for k, v in sd.items():
+            assert torch.equal(v, fx["sd." + k]), k
     # a reference checkpoint loads strictly (train.py:327)
-    model.load_state_dict({k[3:]: v for k, v in fx.items() if k.startswith("sd.")}, strict=True)
+    model.load_state_dict(fixture_state_dict(fx), strict=True)
 
 
 def test_forward_refuses_cpu_tensors():

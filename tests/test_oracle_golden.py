@@ -3,7 +3,8 @@ models.py (tests/golden/make_golden.py).  Everything is compared bit-for-bit: sa
 import pytest
 import torch
 
-from conftest import CASES, fixture_inputs, fixture_model_kwargs, load_fixture
+from conftest import (CASES, assert_state_dict_digests, fixture_inputs, fixture_model_kwargs, is_compact,
+                      load_fixture)
 from oracle.pyg_cpu import OracleHetroGIN, mape, propagate_sum
 
 
@@ -23,9 +24,12 @@ def test_oracle_reproduces_reference(case):
     model = OracleHetroGIN(**kw)
     assert kw["input_channels"] == fx["meta"]["input_channels_after_ctor"]
     sd = model.state_dict()
-    assert list(sd) == [k[3:] for k in fx if k.startswith("sd.")]
-    for k, v in sd.items():
-        assert torch.equal(v, fx["sd." + k]), k
+    if is_compact(fx):
+        assert_state_dict_digests(fx, sd)
+    else:
+        assert list(sd) == [k[3:] for k in fx if k.startswith("sd.")]
+        for k, v in sd.items():
+            assert torch.equal(v, fx["sd." + k]), k
     x, ei, batch, y = fixture_inputs(fx)
     model.set_record(True)
     opt = torch.optim.Adam(lr=1e-3, params=model.parameters(), weight_decay=0)
@@ -35,16 +39,28 @@ def test_oracle_reproduces_reference(case):
     # per-relation aggregates (propagate results) in layer / relation order
     for li, conv in enumerate(model.convs):
         for key, layer in conv.convs.items():
-            assert torch.equal(layer.conv.trace[0], fx[f"agg.{li}.{key}"]), (li, key)
+            agg, k = layer.conv.trace[0], f"agg.{li}.{key}"
+            if is_compact(fx):   # sampled rows bit-exact, whole-tensor float64 sums to rounding
+                assert torch.equal(agg[fx["rows." + k]], fx[k]), (li, key)
+                assert torch.allclose(_sums(agg), fx["sums." + k], rtol=1e-12, atol=0), (li, key)
+            else:
+                assert torch.equal(agg, fx[k]), (li, key)
     lv = mape(out, y.reshape(-1, 1))
     assert torch.equal(lv, fx["loss_value"])
     torch.sqrt(lv).backward()
     for n, p in model.named_parameters():
         g = p.grad if p.grad is not None else torch.zeros(0)
         assert torch.equal(g, fx["grad." + n]), n
+    if is_compact(fx):
+        return                       # compact fixtures carry no Adam step (the full-size cases pin it)
     opt.step()
     for n, p in model.named_parameters():
         assert torch.equal(p, fx["step." + n]), n
+
+
+def _sums(t):
+    d = t.detach().double()
+    return torch.stack([d.sum(), d.abs().sum(), (d * d).sum()])
 
 
 def test_propagate_equals_sequential_edge_order():
