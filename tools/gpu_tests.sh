@@ -7,7 +7,7 @@ OUT=gpurun_out/${TAG:-tests}
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 timeout -k 10 ${LIMIT:-600} python -u -m pytest ${TESTS:-tests} -m gpu -x -v --timeout 240 --timeout-method thread \
-  ${K:+-k "$K"} > "$OUT/pytest.log" 2>&1
+  ${K:+-k "$K"} ${EXTRA:-} > "$OUT/pytest.log" 2>&1
 rc=$?
 echo "pytest rc $rc" | tee "$OUT/status.txt"
 tail -30 "$OUT/pytest.log"
