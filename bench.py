@@ -191,31 +191,84 @@ def csr_build_ms(graph, dev) -> dict:
     return out
 
 
-def one_gpu_reference(cfg, n_comp: int, dev, adam: str, warmup: int = 2, steps: int = 5) -> dict:
+def one_gpu_reference(cfg, n_comp: int, dev, adam: str, graph_mode: bool, warmup: int = 2, steps: int = 5) -> dict:
     """The 1-GPU point of the strong-scaling curve measured inside an N > 1 run: rank 0 alone trains ALL n_comp
-    components (the graph the N ranks split) on its GPU, a fresh model from the same seed, 2 warm-up steps +
-    the median of 5 HIP-event-timed steps; the other ranks wait at a barrier."""
+    components (the graph the N ranks split) on its GPU, a fresh model from the same seed, in the timed run's
+    execution mode (eager, or one hipGraph replay per step with ``--graph``), 2 warm-up steps + the median of 5
+    HIP-event-timed steps; the other ranks wait at a barrier."""
     from hgin import HetroGIN
     from hgin.data import rank_components
+    from hgin.graphs import CapturedStaticStep
     from hgin.train import train_step
     graph, _ = rank_components(cfg, 0, 1, device=dev, n_components=n_comp)
     torch.manual_seed(1997)
     model = HetroGIN(**cfg.model_kwargs({"link": cfg.f_link, "path": cfg.f_path, "node": cfg.f_node})).to(dev)
-    opt = torch.optim.Adam(lr=1e-3, params=model.parameters(), **({"fused": True} if adam == "fused" else {}))
-    for _ in range(warmup):
-        train_step(model, opt, graph)
+    opt = torch.optim.Adam(lr=1e-3, params=model.parameters(), capturable=graph_mode,
+                           **({"fused": True} if adam == "fused" else {}))
+    if graph_mode:
+        stepper = CapturedStaticStep(model, opt, graph, warmup=warmup)
+        step = stepper.step
+    else:
+        step = lambda: train_step(model, opt, graph)  # noqa: E731
+        for _ in range(warmup):
+            step()
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(steps + 1)]
     torch.cuda.synchronize()
     ev[0].record()
     for i in range(steps):
-        train_step(model, opt, graph)
+        step()
         ev[i + 1].record()
     torch.cuda.synchronize()
     ms = statistics.median(ev[i].elapsed_time(ev[i + 1]) for i in range(steps))
-    del graph, model, opt
+    del graph, model, opt, step
     torch.cuda.empty_cache()
     return {"ms_per_step_median": round(ms, 4), "components": n_comp, "warmup": warmup, "steps": steps,
+            "execution": "hipgraph (one replay per step)" if graph_mode else "eager",
             "what": "rank 0 alone, all components of the split graph, after the timed region"}
+
+
+def batches_extra(dev, n_graphs: int = 256, batch: int = 8, warmup: int = 5, steps: int = 200) -> dict:
+    """The reference's actual training loop (dataset.py:26, :239-244, train.py:25-44): shuffled
+    batches of 8 small graphs.  Here: a cfg1-schema GraphStore (n_graphs RouteNet-sized graphs, 0.5x-1.5x cfg1,
+    the reference's always-on normalisation applied once at build), each step = one device collation launch
+    (GraphStore.collate_into) + one hipGraph replay of the whole train step (hgin/graphs.py CapturedTrainStep).
+    HIP events around the timed batches; reported beside the headline, not in it."""
+    import numpy as np
+
+    from hgin import HetroGIN
+    from hgin.data import CONFIGS, CONV_RELATIONS, scaled_config, synthetic_graph
+    from hgin.graphs import CapturedTrainStep
+    from hgin.store import GraphStore
+    base = CONFIGS["cfg1"]
+    rng = np.random.default_rng(0)
+    graphs = [synthetic_graph(scaled_config(base, float(rng.uniform(0.5, 1.5)), name=f"g{i}"), seed=i)
+              for i in range(n_graphs)]
+    store = GraphStore.build(graphs, device=dev, normalize=True)
+    order = [rng.choice(n_graphs, batch, replace=False).tolist() for _ in range(warmup + steps)]
+    conv_edges = [sum(int(store.edge_off[r][g + 1] - store.edge_off[r][g]) for r in CONV_RELATIONS for g in ids)
+                  for ids in order[warmup:]]
+    torch.manual_seed(1997)
+    model = HetroGIN(**base.model_kwargs({"link": base.f_link, "path": base.f_path, "node": base.f_node})).to(dev)
+    opt = torch.optim.Adam(lr=1e-3, params=model.parameters(), capturable=True)
+    stepper = CapturedTrainStep(model, opt, store, batch, warmup_ids=order[:warmup], warmup=warmup)
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    s.record()
+    for ids in order[warmup:]:
+        loss = stepper.step(ids)
+    e.record()
+    torch.cuda.synchronize()
+    wall = (time.perf_counter() - t0) / steps
+    ms = s.elapsed_time(e) / steps
+    return {"workload": f"{n_graphs} cfg1-schema graphs (7/7/3 raw features, normalised; sizes 0.5x-1.5x of "
+                        f"{base.nodes} nodes / {base.graph_edges} edges) resident, shuffled batches of {batch}, "
+                        f"hidden {base.hidden}, {base.layers} layers, fp32",
+            "execution": "device collation (one batched-copy launch) + one hipGraph replay per batch",
+            "batches": steps, "ms_per_batch": round(ms, 4), "host_ms_per_batch": round(wall * 1e3, 4),
+            "graphs_per_s": round(batch / (ms / 1e3), 1),
+            "edges_per_s": round(float(np.mean(conv_edges)) / (ms / 1e3), 1),
+            "mean_conv_edges_per_batch": float(np.mean(conv_edges)), "final_loss": float(loss)}
 
 
 def extras(graph, dev) -> dict:
@@ -261,6 +314,36 @@ def extras(graph, dev) -> dict:
                                  "GB_s": round(b / (ms / 1e3) / 1e9, 1),
                                  "frac_hbm": round(b / (ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4)}
     return res
+
+
+def traffic_file(name: str):
+    """The newest committed PMC traffic record for this config (profiles/r*/traffic_<cfg>.json)."""
+    import glob
+    fs = sorted(glob.glob(os.path.join(ROOT, "profiles", "r[0-9][0-9]", f"traffic_{name}.json")))
+    return fs[-1] if fs else None
+
+
+def gemm_fields(m, bf16: bool, steps: int, t_step: float, what: str):
+    """One GEMM family's roofline fields from the probe's HIP events over whole calls: HBM (algorithmic bytes
+    / time) and the matrix cores (bf16-product FLOP/s / the 2.5 PFLOP/s dense bf16 peak; an fp32 multiply-add
+    costs six bf16 products in the 3-way split, so its fp32-equivalent rate is a sixth of that)."""
+    if not m:
+        return None
+    sec = m["avg_ms"] / 1e3
+    gbs = m["avg_bytes"] / sec / 1e9
+    tfs = m["avg_work"] / sec / 1e12
+    products = 1 if bf16 else 6
+    mfma = tfs * products
+    hf, mf = gbs / HBM_PEAK_GBS, mfma / BF16_MFMA_PEAK_TFS
+    return {"kernel": what, "bound": "hbm" if hf >= mf else "mfma",
+            "hbm": {"achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(hf, 4)},
+            "mfma": {"achieved": round(mfma, 1), "peak": BF16_MFMA_PEAK_TFS, "unit": "TFLOP/s (bf16 products)",
+                     "frac": round(mf, 4), "products_per_fma": products,
+                     "fp32_equivalent_tflops": None if bf16 else round(tfs, 2)},
+            "bytes_per_launch": m["avg_bytes"], "flops_per_launch": m["avg_work"],
+            "avg_launch_ms": round(m["avg_ms"], 5), "launches_per_step": m["launches"] / steps,
+            "ms_per_step": round(m["total_ms"] / steps, 3),
+            "share_of_step": round(m["total_ms"] / steps / (t_step * 1e3), 4)}
 
 
 def main():
@@ -316,9 +399,9 @@ def main():
         elem = 2 if cfg.feat_dtype == "bf16" else 4
         widths0 = {"path": cfg.f_path, "link": cfg.f_link, "node": cfg.f_node}
         widths = {t: cfg.hidden for t in widths0}
-        # forward: one all-gather per layer; backward: one reduce-scatter per layer above the first (the raw
-        # features need no gradient)
-        xchg = dst_part.exchange_bytes(widths0, elem) + (2 * cfg.layers - 1) * dst_part.exchange_bytes(widths, elem)
+        # forward: one all-gather per layer (the first of raw features, L - 1 of hidden embeddings); backward: one
+        # reduce-scatter per layer above the first (the raw features need no gradient): 2L - 2 hidden rounds
+        xchg = dst_part.exchange_bytes(widths0, elem) + (2 * cfg.layers - 2) * dst_part.exchange_bytes(widths, elem)
         part_desc = (f"one connected graph, destination rows of every node type split over {world} rank(s) "
                      f"(per-layer all-gather of source embeddings / reduce-scatter of their gradients, "
                      f"{xchg / 1e9:.2f} GB received per rank per step)")
@@ -397,17 +480,18 @@ def main():
     ref1 = None
     if world > 1 and partition == "components" and args.skew == "uniform" and not (args.no_ref1 or args.prune_dead):
         if rank == 0:
-            ref1 = one_gpu_reference(cfg, n_comp, dev, args.adam)
+            ref1 = one_gpu_reference(cfg, n_comp, dev, args.adam, args.graph)
         barrier()
 
     extra = None
     if rank == 0 and not no_extras:
         extra = extras(graph, dev)
+        extra["batches"] = batches_extra(dev)
 
     out = None
     if rank == 0:
         value = total_conv_edges / t_step
-        roofline = gemm = None
+        roofline = gemm = gemm_dw = gemm_dx = None
         if probe is not None:
             s = probe.summary()
             a = s.get("aggregate")
@@ -422,27 +506,24 @@ def main():
                             "launches_per_step": a["launches"] / steps_recorded,
                             "share_of_step": round(a["total_ms"] / steps_recorded / (t_step * 1e3), 4),
                             "timing": "HIP events on the launching stream, untimed probe pass after the timed steps"}
-                tf = os.path.join(ROOT, "profiles", "r02", f"traffic_{cfg.name}.json")
-                if os.path.exists(tf) and partition == "connected" and args.skew == "uniform" and world == 1:
+                tf = traffic_file(cfg.name)
+                if tf and partition == "connected" and args.skew == "uniform" and world == 1:
                     tr = json.load(open(tf))
                     roofline["traffic"] = tr.get("bytes_per_launch")
                     roofline["traffic_source"] = tr.get("source")
-            m = s.get("gin_mlp")
-            if m:
-                gbs = m["avg_bytes"] / (m["avg_ms"] / 1e3) / 1e9
-                tfs = m["avg_work"] / (m["avg_ms"] / 1e3) / 1e12
-                # the GIN / readout MLP GEMMs are HBM-bound at these shapes (K <= 512, N <= 256: far below the
-                # MFMA ridge), so they are reported against HBM; the FLOP rate is given beside it
-                gemm = {"bound": "hbm", "kernel": (f"hgin_gin_mlp_fwd_{'bf16' if bf16 else 'f32'} ("
-                                                   f"{'k_ws_bf16 / k_gemm_nt_bf16' if bf16 else 'k_ws_f32 / k_gemm_nt'}"
-                                                   f" + bias/PReLU/accum epilogue)"),
-                        "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                        "frac": round(gbs / HBM_PEAK_GBS, 4), "bytes_per_launch": m["avg_bytes"],
-                        "tflops": round(tfs, 2),
-                        "mfma_peak_tflops": mfma_peak, "arith": ("bf16 MFMA" if bf16 else
-                                                                 "fp32 as a 3-way bf16 split (6 bf16 MFMA products)"),
-                        "avg_launch_ms": round(m["avg_ms"], 5), "launches_per_step": m["launches"] / steps_recorded,
-                        "share_of_step": round(m["total_ms"] / steps_recorded / (t_step * 1e3), 4)}
+                    roofline["traffic_measured"] = (f"committed constant: PMC FETCH_SIZE / WRITE_SIZE passes of an "
+                                                    f"earlier rocprofv3 run of this command "
+                                                    f"({os.path.relpath(tf, ROOT)}), not counters of this run")
+            gemm = gemm_fields(s.get("gin_mlp"), bf16, steps_recorded, t_step, "forward MLP GEMM "
+                               f"(hgin_gin_mlp_fwd_{'bf16' if bf16 else 'f32'}: "
+                               f"{'k_ws_bf16 / k_gemm_nt_bf16' if bf16 else 'k_ws_f32 / k_gemm_nt'} + bias / PReLU / "
+                               f"accum epilogue)")
+            gemm_dw = gemm_fields(s.get("gemm_dw"), bf16, steps_recorded, t_step,
+                                  "weight-gradient GEMMs (hgin_gin_mlp_bwd_w_* / hgin_gemm_tn_*, incl. the fused or "
+                                  "separate PReLU backward and the slab sums)")
+            gemm_dx = gemm_fields(s.get("gemm_dx"), bf16, steps_recorded, t_step,
+                                  "input-gradient GEMMs (hgin_gemm_nt_combine_* / hgin_gemm_nt_*, incl. the "
+                                  "self-term backward epilogue and its eps sum)")
         wl = (f"{cfg.name}: {cfg.layers}-layer HeteroGIN, {cfg.nodes} nodes / {cfg.graph_edges} edges total, 3 node "
               f"types x {len(graph.edge_index)} edge types, hidden {cfg.hidden} {'bf16' if bf16 else 'fp32'}, "
               f"{part_desc}" + (", dst ~ Zipf(1.1)" if args.skew == "zipf" else ""))
@@ -468,7 +549,7 @@ def main():
                           "skew": args.skew, "prune_dead": bool(args.prune_dead),
                           "execution": "hipgraph (one replay per step)" if args.graph else "eager",
                           "optimizer": f"torch.optim.Adam(lr=1e-3), {args.adam}"},
-               "roofline": roofline, "gemm": gemm, "csr_build": csr_ms, "extras": extra, "final_loss": final_loss}
+               "roofline": roofline, "gemm": gemm, "gemm_dw": gemm_dw, "gemm_dx": gemm_dx, "csr_build": csr_ms, "extras": extra, "final_loss": final_loss}
         if ref1 is not None:
             # strong scaling against the same graph on one GPU: t_1gpu / t_step (ideal: N)
             out["one_gpu_reference"] = ref1

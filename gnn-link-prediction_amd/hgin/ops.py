@@ -327,9 +327,20 @@ def gemm_nt(a: Tensor, b: Tensor) -> Tensor:
     M, K = a.shape
     N = b.shape[0]
     c = torch.empty(M, N, dtype=a.dtype, device=a.device)
-    _lib.call(f"hgin_gemm_nt_{_sfx(a)}", _p(a), a.stride(0), _p(b), b.stride(0), _p(c), c.stride(0), M, N, K,
-              _p(nt_planes(b)), _stream(a))
+    _probed("gemm_dx", 2.0 * M * N * K, a.element_size() * (M * K + N * K + M * N),
+            lambda: _lib.call(f"hgin_gemm_nt_{_sfx(a)}", _p(a), a.stride(0), _p(b), b.stride(0), _p(c), c.stride(0),
+                              M, N, K, _p(nt_planes(b)), _stream(a)))
     return c
+
+
+def _probed(kind: str, flops: float, nbytes: float, launch) -> None:
+    """Run ``launch``; inside a profiling window, timed with HIP events as ``kind`` (work = FLOPs, plus its
+    algorithmic HBM bytes)."""
+    probe = profiling.active()
+    if probe is None:
+        launch()
+    else:
+        probe.around(kind, flops, launch, nbytes)
 
 
 def gemm_nt_combine(a: Tensor, b: Tensor, x_dst: Tensor, eps: Tensor, cs: int, want_gx: bool,
@@ -351,10 +362,14 @@ def gemm_nt_combine(a: Tensor, b: Tensor, x_dst: Tensor, eps: Tensor, cs: int, w
     nbytes = ctypes.c_size_t(0)
     _lib.check(_lib.lib().hgin_gemm_nt_combine_workspace_size(M, N, ctypes.byref(nbytes)), "nt_combine_workspace")
     ws = _workspace(nbytes.value, a.device)
-    _lib.call(f"hgin_gemm_nt_combine_{_sfx(a)}", _p(a), a.stride(0), _p(b), b.stride(0), _p(c), c.stride(0), M, N, K,
-              _p(x_dst), x_dst.stride(0), _p(gx), gx.stride(0) if gx is not None else 0, _p(g_prev),
-              g_prev.stride(0) if g_prev is not None else 0, cs, _p(eps), _p(g_eps),
-              _p(ws), nbytes.value, _p(nt_planes(b)), _stream(a))
+    s = a.element_size()
+    nb = s * (M * K + N * K + M * N + M * (N - cs) * (1 + int(gx is not None) + int(g_prev is not None)))
+    _probed("gemm_dx", 2.0 * M * N * K, nb,
+            lambda: _lib.call(f"hgin_gemm_nt_combine_{_sfx(a)}", _p(a), a.stride(0), _p(b), b.stride(0), _p(c),
+                              c.stride(0), M, N, K, _p(x_dst), x_dst.stride(0), _p(gx),
+                              gx.stride(0) if gx is not None else 0, _p(g_prev),
+                              g_prev.stride(0) if g_prev is not None else 0, cs, _p(eps), _p(g_eps),
+                              _p(ws), nbytes.value, _p(nt_planes(b)), _stream(a)))
     return c, gx, g_eps
 
 
@@ -371,9 +386,10 @@ def gemm_tn(a: Tensor, b1: Tensor, b2: Optional[Tensor] = None) -> Tensor:
     nbytes = ctypes.c_size_t(0)
     _lib.check(_lib.lib().hgin_gemm_tn_workspace_size(M, N, K, ctypes.byref(nbytes)), "gemm_tn_workspace_size")
     ws = _workspace(nbytes.value, a.device)
-    _lib.call(f"hgin_gemm_tn_{_sfx(a)}", _p(a), a.stride(0), _p(b1), b1.stride(0), k1, _p(b2),
-              b2.stride(0) if b2 is not None else 0, M, N, K, _p(out), out.stride(0), _p(ws), nbytes.value,
-              _stream(a))
+    _probed("gemm_dw", 2.0 * M * N * K, a.element_size() * M * (N + K) + 4 * N * K,
+            lambda: _lib.call(f"hgin_gemm_tn_{_sfx(a)}", _p(a), a.stride(0), _p(b1), b1.stride(0), k1, _p(b2),
+                              b2.stride(0) if b2 is not None else 0, M, N, K, _p(out), out.stride(0), _p(ws),
+                              nbytes.value, _stream(a)))
     return out
 
 
@@ -405,9 +421,13 @@ def mlp_bwd_w(g_y: Tensor, z: Tensor, prelu: Tensor, b1: Tensor, b2: Optional[Te
     _lib.check(_lib.lib().hgin_gin_mlp_bwd_w_workspace_size(M, N, K, z.element_size(), int(g_z is not None),
                                                             ctypes.byref(nbytes)), "gin_mlp_bwd_w_workspace_size")
     ws = _workspace(nbytes.value, dev)
-    _lib.call(f"hgin_gin_mlp_bwd_w_{_sfx(z)}", _p(g_y), g_y.stride(0), _p(z), z.stride(0), _p(prelu), _p(b1),
-              b1.stride(0), k1, _p(b2), b2.stride(0) if b2 is not None else 0, M, N, K, _p(g_w), g_w.stride(0),
-              _p(g_a), _p(g_b), _p(g_z), N, _p(ws), nbytes.value, _stream(z))
+    s = z.element_size()
+    # fused: g_y, z and B read once; otherwise the PReLU-backward pass (g_y, z read, g_z written) + the TN GEMM
+    nb = (s * M * (2 * N + K) if g_z is None else s * M * (3 * N) + s * M * (N + K)) + 4 * N * K
+    _probed("gemm_dw", 2.0 * M * N * K, nb,
+            lambda: _lib.call(f"hgin_gin_mlp_bwd_w_{_sfx(z)}", _p(g_y), g_y.stride(0), _p(z), z.stride(0), _p(prelu),
+                              _p(b1), b1.stride(0), k1, _p(b2), b2.stride(0) if b2 is not None else 0, M, N, K,
+                              _p(g_w), g_w.stride(0), _p(g_a), _p(g_b), _p(g_z), N, _p(ws), nbytes.value, _stream(z)))
     return g_w, g_a, g_b, g_z
 
 
@@ -476,10 +496,13 @@ def _zero(device) -> Tensor:
 
 def _backward_aggregate(graph: RelationGraph, g_agg: Tensor, prev: Optional[Tensor] = None) -> Tensor:
     """d x_src = index_add over the reversed relation = the A3 kernel on the CSC (edge order kept).  ``prev``:
-    a running gradient of the source type, accumulated onto in place (ADD self term with eps 0: prev + sum)."""
+    a running gradient of the source type, added in the same pass (ADD self term with eps 0: prev + sum) into a
+    fresh buffer — the same HBM bytes as accumulating in place (prev read once, the sum written once), without
+    aliasing the kernels' restrict-qualified x_dst / out (include/hgin.h: out must not overlap any input)."""
     csc = graph.csc
     if prev is not None:
-        return aggregate_into(csc, g_agg, prev, _zero(g_agg.device), COMBINE_ADD, prev)
+        out = torch.empty_like(prev)
+        return aggregate_into(csc, g_agg, prev, _zero(g_agg.device), COMBINE_ADD, out)
     g = torch.empty(graph.n_src, g_agg.size(1), dtype=g_agg.dtype, device=g_agg.device)
     return aggregate_into(csc, g_agg, None, None, COMBINE_NONE, g)
 

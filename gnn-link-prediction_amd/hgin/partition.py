@@ -21,6 +21,16 @@ in the same order); the backward's source-gradient sums and the weight-gradient 
 ranks, so gradients agree within fp32 summation-order tolerance (tests/test_partition_gloo.py,
 tests/test_gpu_dist.py).
 
+Overlap (device tensors): a layer's all-gathers are all issued at the layer's start on a communication stream
+(``DstRangePartition.prefetch``) and the compute stream waits for each table only just before its first
+relation, so the link / node gathers run under the first relations' kernels.  Because the gather's autograd
+node runs on that stream, PyTorch runs its backward — the reduce-scatter — there too and makes only the
+gradient's consumer wait (the autograd engine's cross-stream hand-off), so each table's reduce-scatter starts
+as soon as its gradient is complete and overlaps the remaining relations' backward.  (Bucketing the three
+reduce-scatters into one collective would need two strided repacks of GB-sized tables at cfg3 for a saving of
+two collective latencies; per-table collectives, overlapped, are the better trade at these sizes.)  The
+arithmetic is unchanged, so the results are bitwise those of the serial schedule (``overlap=False``).
+
 Not supported here (they pool or normalise across the whole graph): ``global_feats``, BatchNorm in the
 readout, dropout > 0.  ``HGIN_DIST_BACKEND=gloo`` rehearsals stage CUDA tensors through the host (gloo's
 collectives are CPU ones); RCCL runs them on the device.
@@ -97,12 +107,21 @@ class _AllGatherRows(torch.autograd.Function):
         return (out if n_local == chunk else out[:n_local]), None, None, None
 
 
+def _collectives() -> bool:
+    return dist.is_available() and dist.is_initialized()
+
+
 class DstRangePartition:
-    """1D destination-range partition of a hetero graph's node types over the ranks of ``group``."""
+    """1D destination-range partition of a hetero graph's node types over the ranks of ``group``.
+
+    ``overlap`` (default on): issue each layer's all-gathers together on a communication stream (device tensors
+    only; see the module docstring); off: one blocking gather per table at its first use."""
 
     def __init__(self, n_nodes: Dict[str, int], rank: Optional[int] = None, world: Optional[int] = None,
-                 group=None):
+                 group=None, overlap: bool = True):
         self.group = group
+        self.overlap = overlap
+        self._comm = {}
         self.world = int(world if world is not None else _world(group))
         self.rank = int(rank if rank is not None else _rank(group))
         if not 0 <= self.rank < self.world:
@@ -133,18 +152,59 @@ class DstRangePartition:
         return HeteroGraph(x, ei, graph.y[plo:phi], batch)
 
     def gather(self, x_local: torch.Tensor, t: str) -> torch.Tensor:
-        """The full [N_t, F] table of type t (differentiable: the backward reduce-scatters to the owners)."""
+        """The full [N_t, F] table of type t (differentiable: the backward reduce-scatters to the owners).  With
+        a process group the collective runs at every world size (at 1 it is the backend's copy)."""
         lo, hi = self.rows(t)
         if x_local.shape[0] != hi - lo:
             raise ValueError(f"{t!r}: rank {self.rank} owns {hi - lo} rows, got {x_local.shape[0]}")
-        if self.world == 1:
+        if self.world == 1 and not _collectives():
             return x_local
         return _AllGatherRows.apply(x_local, self.n_nodes[t], self.chunk[t], self.group)
+
+    def _comm_stream(self, device) -> torch.cuda.Stream:
+        s = self._comm.get(device)
+        if s is None:
+            s = self._comm[device] = torch.cuda.Stream(device=device)
+        return s
+
+    def prefetch(self, tables: Dict[str, torch.Tensor]) -> Dict[str, "_Pending"]:
+        """Issue the gathers of ``tables`` (type -> owned rows) now: on the communication stream when overlapping
+        device tensors, else lazily (each one blocking at its first use)."""
+        out = {}
+        for t, x in tables.items():
+            if self.overlap and x.is_cuda and (self.world > 1 or _collectives()):
+                cur = torch.cuda.current_stream(x.device)
+                comm = self._comm_stream(x.device)
+                comm.wait_stream(cur)                    # x_local is produced on the compute stream
+                x.record_stream(comm)
+                with torch.cuda.stream(comm):
+                    full = self.gather(x, t)
+                out[t] = _Pending(full, comm)
+            else:
+                out[t] = _Pending(None, None, lambda x=x, t=t: self.gather(x, t))
+        return out
 
     def exchange_bytes(self, widths: Dict[str, int], elem: int) -> int:
         """Bytes one rank receives per all-gather round of the given per-type widths (the backward's
         reduce-scatter moves the same amount)."""
         return sum((self.world - 1) * self.chunk[t] * w * elem for t, w in widths.items())
+
+
+class _Pending:
+    """A gathered table that may still be in flight on the communication stream."""
+
+    def __init__(self, full, stream, thunk=None):
+        self.full, self.stream, self.thunk = full, stream, thunk
+
+    def get(self) -> torch.Tensor:
+        if self.full is None:
+            self.full = self.thunk()
+        elif self.stream is not None:
+            cur = torch.cuda.current_stream(self.full.device)
+            cur.wait_stream(self.stream)                 # the table has landed
+            self.full.record_stream(cur)                 # allocated on the comm stream, read on this one
+            self.stream = None
+        return self.full
 
 
 def _check_supported(model) -> None:
@@ -168,18 +228,23 @@ def _select_features(model, x_dict) -> None:
 def _layer(part: DstRangePartition, hetero_conv, x_local: Dict[str, torch.Tensor], edge_index_dict):
     """One HeteroConv layer on (gathered sources, owned destinations); the per-destination relation sum as
     hgin.conv.HeteroConv's relation loop does it (running sum in the GEMM epilogue where the conv offers it)."""
-    full: Dict[str, torch.Tensor] = {}
     outs: Dict[str, list] = {}
     skip = getattr(hetero_conv, "skip", ())
-    for rel, ei in edge_index_dict.items():
+    live = [(rel, ei) for rel, ei in edge_index_dict.items()
+            if "__".join(rel) in hetero_conv.convs and "__".join(rel) not in skip]
+    srcs = []
+    for rel, _ in live:
+        if rel[0] == rel[2]:
+            raise NotImplementedError("dst-range partition: same-type relations")
+        if rel[0] not in srcs:
+            srcs.append(rel[0])
+    pending = part.prefetch({t: x_local[t] for t in srcs})     # every gather of the layer, in first-use order
+    full: Dict[str, torch.Tensor] = {}
+    for rel, ei in live:
         src, _, dst = rel
         key = "__".join(rel)
-        if key not in hetero_conv.convs or key in skip:
-            continue
-        if src == dst:
-            raise NotImplementedError("dst-range partition: same-type relations")
         if src not in full:
-            full[src] = part.gather(x_local[src], src)
+            full[src] = pending[src].get()
         conv = hetero_conv.convs[key]
         lst = outs.setdefault(dst, [])
         if getattr(conv, "supports_accum", False) and len(lst) == 1:
@@ -199,9 +264,18 @@ def forward_loss(model, part: DstRangePartition, local: HeteroGraph):
     for i in range(model.num_layers):   # models.py:355-359
         x = _layer(part, model.convs[i], x, local.edge_index_dict())
     m = int(local.y.numel())
-    if m == 0:   # no owned paths: a zero that still reaches every gathered table (the backward's collectives)
-        return x["path"][:0], x["path"].sum() * 0.0
     readout = getattr(model, "_readout", None)
+    if m == 0:
+        # No owned paths.  The readout still runs (on the empty row block) so every readout parameter gets a
+        # (zero) gradient as on the other ranks — GradAllReducer's layout and Adam's state stay rank-independent
+        # — and the zero loss sum still reaches every gathered table (the backward's collectives).
+        if readout is not None:
+            out = readout(x["path"], origin_path, None, None, None, None)
+        else:
+            out = torch.cat((x["path"], origin_path), 1) if model.concat_path else x["path"]
+            for seq in model.readout:
+                out = seq(out)
+        return out, out.sum() * 0.0 + x["path"].sum() * 0.0
     if readout is not None:
         out, lv = readout(x["path"], origin_path, None, None, local.y, None)
     else:   # a plain module stack (the CPU oracle in tests): cat + Sequential readout + train.py's mape

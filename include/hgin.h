@@ -82,6 +82,8 @@ int hgin_csr_build(const int64_t* edge_index, int64_t n_edges, int key_row, int6
  *   ADD:    out[r, f]                    = agg + ((1 + eps[0]) * x_dst[r, f])   (f_dst == f_src)
  *   CONCAT: out[r, 0:f_src] = agg;  out[r, f_src:f_src+f_dst] = (1 + eps[0]) * x_dst[r, :]
  * eps: device float[1] (the GINConv eps Parameter, models.py:191-194).  Rows with no edges get 0.
+ * out must not overlap x_src or x_dst (the kernels read them through restrict-qualified pointers); the
+ * backward's running-gradient accumulation (ADD, eps 0) writes a fresh buffer for that reason.
  * Bit-exact against CPU scatter_add_ + cat / add on the same inputs. */
 int hgin_aggregate_f32(const int32_t* rowptr, const int32_t* col, int64_t n_rows,
                        const float* x_src, int64_t ld_src, int64_t f_src,

@@ -108,15 +108,23 @@ def _part_worker(rank, world, port, outdir, feat):
     from hgin.partition import DstRangePartition, forward_loss, train_step
     cfg = _cfg(feat)
     g = synthetic_graph(cfg, seed=3, device="cuda")
-    part = DstRangePartition({t: g.num_nodes(t) for t in g.x})
-    local = part.local_graph(g)
-    model = _model(cfg)
-    with torch.no_grad():
-        out, _ = forward_loss(model, part, local)
-    lv = train_step(model, torch.optim.SGD(model.parameters(), lr=0.0), part, local)
-    torch.save({"loss": lv.cpu(), "out": out.float().cpu(), "rows": part.rows("path"),
-                "grads": {n: (p.grad.cpu() if p.grad is not None else None) for n, p in model.named_parameters()}},
-               os.path.join(outdir, f"rank{rank}.pt"))
+    res = {}
+    for overlap in (True, False):    # the overlapped schedule (default) and the serial one: bitwise equal
+        part = DstRangePartition({t: g.num_nodes(t) for t in g.x}, overlap=overlap)
+        local = part.local_graph(g)
+        model = _model(cfg)
+        with torch.no_grad():
+            out, _ = forward_loss(model, part, local)
+        lv = train_step(model, torch.optim.SGD(model.parameters(), lr=0.0), part, local)
+        res[overlap] = {"loss": lv.cpu(), "out": out.float().cpu(), "rows": part.rows("path"),
+                        "grads": {n: (p.grad.cpu() if p.grad is not None else None)
+                                  for n, p in model.named_parameters()}}
+    a, b = res[True], res[False]
+    assert torch.equal(a["out"], b["out"]) and torch.equal(a["loss"], b["loss"])
+    for n, ga in a["grads"].items():
+        gb = b["grads"][n]
+        assert (ga is None) == (gb is None) and (ga is None or torch.equal(ga, gb)), n
+    torch.save(a, os.path.join(outdir, f"rank{rank}.pt"))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -161,3 +169,64 @@ def test_dst_range_partition_equals_single_device(feat, world):
             assert torch.equal(g0, r["grads"][n]), n
         err = float((g0.double() - p.grad.double().cpu()).norm())
         assert err <= tol * float(p.grad.double().norm()) + 1e-6 * g_scale, (n, err)
+
+
+def _rccl_worker(outdir):
+    """World size 1 over RCCL: the process group comes up before any other GPU work of this child; then the
+    component-DP step (GradAllReducer's all-reduce) and the dst-range partition's all-gather / reduce-scatter
+    (overlapped on the communication stream) run their collectives on the "nccl" (= RCCL) backend."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=os.environ["HGIN_TEST_PORT"])
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", rank=0, world_size=1)
+    assert dist.get_backend() == "nccl"
+    from hgin.data import synthetic_graph
+    from hgin.dist import GradAllReducer
+    from hgin.partition import DstRangePartition
+    from hgin.partition import train_step as part_step
+    from hgin.train import train_step
+    cfg = _cfg("f32")
+    g = synthetic_graph(cfg, seed=3, device="cuda")
+    res = {}
+    for mode in ("plain", "reducer", "partition"):
+        model = _model(cfg)
+        opt = torch.optim.SGD(model.parameters(), lr=0.0)
+        if mode == "plain":
+            lv = train_step(model, opt, g)
+        elif mode == "reducer":
+            red = GradAllReducer(model.parameters())
+            lv = train_step(model, opt, g, reducer=red)
+            red.check()
+        else:
+            part = DstRangePartition({t: g.num_nodes(t) for t in g.x})
+            lv = part_step(model, opt, part, part.local_graph(g))
+        torch.cuda.synchronize()
+        res[mode] = {"loss": lv.cpu(), "grads": {n: (p.grad.cpu() if p.grad is not None else None)
+                                                 for n, p in model.named_parameters()}}
+    torch.save(res, os.path.join(outdir, "rccl.pt"))
+    dist.destroy_process_group()
+
+
+def test_rccl_world1_collectives_equal_plain_step():
+    """The "nccl" backend on the hardware: one train_step through GradAllReducer (one RCCL all-reduce of
+    [grads | presence | S | m]) and one through the dst-range partition (RCCL all-gathers / reduce-scatters)
+    equal the reducer-free step: loss within 1e-6, gradients within 1e-5 of their norm (the reducer
+    back-propagates S = m * mape and rescales, the plain step sqrt(mape): different roundings of the same
+    gradient)."""
+    with tempfile.TemporaryDirectory() as d:
+        ctx = mp.get_context("spawn")
+        os.environ["HGIN_TEST_PORT"] = str(_free_port())
+        p = ctx.Process(target=_rccl_worker, args=(d,))
+        p.start()
+        p.join(timeout=240)
+        assert p.exitcode == 0, p.exitcode
+        res = torch.load(os.path.join(d, "rccl.pt"), weights_only=True)
+    base = res["plain"]
+    for mode in ("reducer", "partition"):
+        r = res[mode]
+        assert abs(float(r["loss"]) - float(base["loss"])) <= 1e-6 * float(base["loss"]), mode
+        for n, g0 in base["grads"].items():
+            g1 = r["grads"][n]
+            assert (g0 is None) == (g1 is None), (mode, n)
+            if g0 is not None:
+                err = float((g1.double() - g0.double()).norm())
+                assert err <= 1e-5 * float(g0.double().norm()) + 1e-9, (mode, n, err)

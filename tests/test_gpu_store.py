@@ -217,3 +217,17 @@ def test_captured_train_step_matches_eager():
             err = float((p3.grad - p4.grad).double().norm())
             assert err <= 1e-5 * float(p4.grad.double().norm()) + 1e-9, (n, err)
     assert g_cap
+
+
+def test_store_build_normalize_equals_reference_fixture():
+    """GraphStore.build(normalize=True) holds exactly the features the reference's own normalize
+    (dataset.py:33-58, executed by tests/golden/make_golden_normalize.py) produces for the same collated graphs."""
+    from conftest import load_fixture
+    from hgin.data import CONFIGS, synthetic_graph
+    from hgin.store import GraphStore
+    fx = load_fixture("normalize_ref")
+    graphs = [synthetic_graph(CONFIGS["cfg1"], seed=s) for s in fx["meta"]["graph_seeds"]]
+    st = GraphStore.build(graphs, device="cuda", normalize=True)
+    for t in ("path", "link", "node"):
+        n = st.x[t].shape[0]
+        assert torch.equal(st.x[t].cpu(), fx[f"out.x.{t}"][:n]), t

@@ -26,19 +26,19 @@ def _free_port():
     return p
 
 
-def _cfg():
+def _cfg(n_path=301):
     import dataclasses
 
     from hgin.data import CONFIGS, scaled_config
     # cfg2 schema (divided / bl features: no column slicing), odd counts so world 3 pads its last blocks
     c = scaled_config(CONFIGS["cfg2"], 0.0005, name="cfg2-tiny")
-    return dataclasses.replace(c, n_path=301, n_link=151, n_node=52, f_path=16, f_link=12, f_node=8, hidden=16,
+    return dataclasses.replace(c, n_path=n_path, n_link=151, n_node=52, f_path=16, f_link=12, f_node=8, hidden=16,
                                layers=3)
 
 
-def _graph():
+def _graph(n_path=301):
     from hgin.data import synthetic_graph
-    return synthetic_graph(_cfg(), seed=5)
+    return synthetic_graph(_cfg(n_path), seed=5)
 
 
 def _model():
@@ -48,12 +48,12 @@ def _model():
     return OracleHetroGIN(**cfg.model_kwargs({"link": cfg.f_link, "path": cfg.f_path, "node": cfg.f_node}))
 
 
-def _worker(rank, world, port, outdir):
+def _worker(rank, world, port, outdir, n_path):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     torch.set_num_threads(1)
     from hgin.partition import DstRangePartition, train_step
-    g = _graph()
+    g = _graph(n_path)
     part = DstRangePartition({t: g.num_nodes(t) for t in g.x})
     local = part.local_graph(g)
     model = _model()
@@ -64,14 +64,16 @@ def _worker(rank, world, port, outdir):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_dst_range_partition_trains_as_one_graph(world):
+@pytest.mark.parametrize("world,n_path", [(2, 301), (3, 301), (3, 4)])
+def test_dst_range_partition_trains_as_one_graph(world, n_path):
+    """(3, 4): chunks of 2 paths, so rank 2 owns none — it still runs the (empty) readout, so every rank sends
+    the same gradient layout and holds every readout gradient (zero contribution from it)."""
     from oracle.pyg_cpu import mape
     torch.set_num_threads(1)
     with tempfile.TemporaryDirectory() as d:
-        mp.spawn(_worker, args=(world, _free_port(), d), nprocs=world, join=True)
+        mp.spawn(_worker, args=(world, _free_port(), d, n_path), nprocs=world, join=True)
         rs = [torch.load(os.path.join(d, f"rank{r}.pt"), weights_only=True) for r in range(world)]
-    g = _graph()
+    g = _graph(n_path)
     # the ranks' edge sets: every edge exactly once, at the rank owning its destination, in the original order
     for rel, e in g.edge_index.items():
         key = "__".join(rel)
@@ -102,7 +104,10 @@ def test_dst_range_partition_trains_as_one_graph(world):
         for r in rs[1:]:
             assert torch.equal(r["grads"][n], g0), n      # one all-reduce: every rank holds the same sum
         err = float((g0.double() - p.grad.double()).norm())
-        assert err <= 1e-5 * float(p.grad.double().norm()) + 1e-9, (n, err)
+        # 4 paths: the scalar slope / eps gradients are short sums of cancelling terms, split differently over
+        # the ranks than on one device (fp32 summation order): 1e-4 of the norm there, 1e-5 otherwise
+        tol = 1e-5 if n_path > 100 else 1e-4
+        assert err <= tol * float(p.grad.double().norm()) + 1e-9, (n, err)
 
 
 def test_partition_rows_and_exchange_bytes():

@@ -66,3 +66,16 @@ def test_normalize_reference_columns():
     c, mean, std = NORMALIZATION["link"][2]
     assert torch.equal(out["link"][:, c], (x["link"][:, c] - mean) / std)
     assert not torch.equal(out["link"], x["link"])      # input untouched, output normalised
+
+
+def test_normalize_reference_equals_reference_executed_fixture():
+    """F2 pinned to the reference itself: tests/golden/normalize_ref.pt was made by executing dataset.py:33-58
+    (GNN21Dataset.normalize) on collated cfg1 features plus extreme values; normalize_reference reproduces it
+    bit for bit, every node type and column."""
+    from conftest import load_fixture
+    fx = load_fixture("normalize_ref")
+    x = {t: fx[f"in.x.{t}"] for t in ("path", "link", "node")}
+    out = normalize_reference(x)
+    for t in x:
+        assert torch.equal(out[t], fx[f"out.x.{t}"]), t
+        assert torch.equal(x[t], fx[f"in.x.{t}"]), t           # the input dict is not modified
