@@ -35,13 +35,6 @@ def make_activation(spec):
         raise ValueError(f"unsupported activation {spec!r}; expected one of {sorted(_ACTS)}") from None
 
 
-def _global_pool(x: torch.Tensor, batch: torch.Tensor, reduce: str) -> torch.Tensor:
-    size = int(batch.max().item()) + 1 if batch.numel() else 0
-    idx = batch.view(-1, 1).expand_as(x)
-    return torch.zeros(size, x.size(1), dtype=x.dtype, device=x.device).scatter_reduce(
-        0, idx, x, reduce=reduce, include_self=False)
-
-
 def _host_call_device(model: torch.nn.Module, x_dict, edge_index_dict, path_batch):
     """The HIP device to run a host-resident call on, or None when inputs and parameters are already on it.
 
@@ -192,19 +185,16 @@ class HetroGIN(torch.nn.Module):
         self._select_features(x_dict)
         origin_input = x_dict.copy()
 
-        mean_f = max_f = None
-        if self.global_feats:   # models.py:347-352
-            mean_f = _global_pool(origin_input["path"], path_batch, "mean")
-            max_f = _global_pool(origin_input["path"], path_batch, "amax")
-            mean_f = torch.gather(mean_f, 0, path_batch.unsqueeze(1).repeat(1, mean_f.shape[1]))
-            max_f = torch.gather(max_f, 0, path_batch.unsqueeze(1).repeat(1, max_f.shape[1]))
+        pooled = None
+        if self.global_feats:   # models.py:347-352: [mean | max] per graph, gathered to the rows, in one launch
+            pooled = ops.global_pool(origin_input["path"], path_batch)
 
         for i in range(self.num_layers):   # models.py:355-359
             x_dict = self.convs[i](x_dict, edge_index_dict)
             if self.dropout > 0.0 and self.training:
                 for k in list(x_dict.keys()):
                     x_dict[k] = torch.nn.functional.dropout(x_dict[k], p=self.dropout, training=True)
-        return self._readout(x_dict["path"], origin_input["path"], mean_f, max_f, y, m_valid)
+        return self._readout(x_dict["path"], origin_input["path"], pooled, y, m_valid)
 
     def _select_features(self, x_dict):
         """models.py:333-342 feature slicing (assigns into the caller's dict, as the reference does)."""
@@ -219,17 +209,18 @@ class HetroGIN(torch.nn.Module):
                 x_dict["path"] = x_dict["path"][:, 0:6]
                 x_dict["link"] = x_dict["link"][:, 0:3]
 
-    def _readout(self, x_path, origin_path, mean_f, max_f, y, m_valid):
-        """models.py:362-376 on the final path embeddings (+ F3's fused head + loss when ``y`` is given)."""
+    def _readout(self, x_path, origin_path, pooled, y, m_valid):
+        """models.py:362-376 on the final path embeddings (+ F3's fused head + loss when ``y`` is given);
+        ``pooled`` = [mean | max] global features per row (GLOBAL_FEATS) or None."""
         x2 = None   # second column block of the readout input, read in place instead of torch.cat
         if self.concat_path:   # models.py:362-371
-            if self.global_feats:
-                x = torch.cat((x_path, origin_path, mean_f, max_f), 1)
+            if pooled is not None:
+                x = torch.cat((x_path, origin_path, pooled), 1)
             else:
                 x, x2 = x_path, origin_path
         else:
-            if self.global_feats:
-                x = torch.cat((x_path, mean_f, max_f), 1)
+            if pooled is not None:
+                x = torch.cat((x_path, pooled), 1)
             else:
                 x = x_path
 

@@ -808,6 +808,23 @@ def gin_conv(x_src: Tensor, x_dst: Tensor, eps: Tensor, weight: Tensor, bias: Te
     return _GINConvFn.apply(x_src, x_dst, eps, _rowmajor(weight), bias.contiguous(), prelu, accum, graph, mode)
 
 
+def global_pool(x: Tensor, batch: Tensor) -> Tensor:
+    """[N, 2F] = [global_mean_pool | global_max_pool](x, batch) gathered back to the rows (models.py:347-352), on
+    hgin_global_pool_*: one deterministic launch, no host sync.  ``batch`` must be non-decreasing (PyG
+    collation).  The pooled inputs are data (raw path features): no gradient flows through the pooling."""
+    require_device(x, batch, what="hgin.global_pool")
+    x = _rowmajor(_f32(x, "x"))
+    if torch.is_grad_enabled() and x.requires_grad:
+        raise NotImplementedError("hgin.global_pool: no backward (the reference pools the raw input features)")
+    if batch.dtype != torch.long or batch.dim() != 1 or batch.numel() != x.size(0):
+        raise ValueError("hgin.global_pool: batch must be int64 [N] with one entry per row")
+    n, f = x.shape
+    out = torch.empty(n, 2 * f, dtype=x.dtype, device=x.device)
+    _lib.call(f"hgin_global_pool_{_sfx(x)}", _p(batch.contiguous()), n, _p(x), x.stride(0), f, _p(out), out.stride(0),
+              _stream(x))
+    return out
+
+
 # ---------------------------------------------------------------------------------------------------
 # F3: fused readout head + MAPE loss
 # ---------------------------------------------------------------------------------------------------

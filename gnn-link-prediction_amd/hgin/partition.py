@@ -270,14 +270,14 @@ def forward_loss(model, part: DstRangePartition, local: HeteroGraph):
         # (zero) gradient as on the other ranks — GradAllReducer's layout and Adam's state stay rank-independent
         # — and the zero loss sum still reaches every gathered table (the backward's collectives).
         if readout is not None:
-            out = readout(x["path"], origin_path, None, None, None, None)
+            out = readout(x["path"], origin_path, None, None, None)
         else:
             out = torch.cat((x["path"], origin_path), 1) if model.concat_path else x["path"]
             for seq in model.readout:
                 out = seq(out)
         return out, out.sum() * 0.0 + x["path"].sum() * 0.0
     if readout is not None:
-        out, lv = readout(x["path"], origin_path, None, None, local.y, None)
+        out, lv = readout(x["path"], origin_path, None, local.y, None)
     else:   # a plain module stack (the CPU oracle in tests): cat + Sequential readout + train.py's mape
         from .train import mape
         h = torch.cat((x["path"], origin_path), 1) if model.concat_path else x["path"]

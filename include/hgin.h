@@ -90,6 +90,19 @@ int hgin_aggregate_f32(const int32_t* rowptr, const int32_t* col, int64_t n_rows
                        const float* x_dst, int64_t ld_dst, int64_t f_dst,
                        const float* eps, int combine, float* out, int64_t ld_out, void* stream);
 
+/* ---- A7 input: global mean / max pooling of the path features (GLOBAL_FEATS) --------------------------
+ * Replaces torch_geometric.nn.global_mean_pool / global_max_pool of origin_input["path"] by path_batch and the
+ * torch.gather that broadcasts them back to the rows (models.py:347-352; torch_scatter scatter mean / max):
+ *   out[r, 0:f]  = mean of x[q, :] over the rows q of r's graph   (sequential row-order fp32 sum, one division)
+ *   out[r, f:2f] = max  of x[q, :] over the same rows             (NaN propagates)
+ * batch: int64 [n_rows] graph ids, non-decreasing (PyG collation, dataset.py:239-244: each graph's rows are one
+ * contiguous run; ids may skip values).  Deterministic; the mean is bit-identical to CPU scatter mean.
+ * f <= 4096; out must not overlap x.  No workspace, no host synchronisation. */
+int hgin_global_pool_f32(const int64_t* batch, int64_t n_rows, const float* x, int64_t ldx, int64_t f,
+                         float* out, int64_t ld_out, void* stream);
+int hgin_global_pool_bf16(const int64_t* batch, int64_t n_rows, const uint16_t* x, int64_t ldx, int64_t f,
+                          uint16_t* out, int64_t ld_out, void* stream);
+
 /* ---- A9: backward of the combine -----------------------------------------------------------------
  * Replaces the autograd of `(1 + eps) * x_r` + cat/add (models.py:212-215):
  *   g_x_dst[r, f] = (1 + eps) * g[r, f]                 (written if g_x_dst != NULL)

@@ -4,7 +4,7 @@ import numpy as np
 import pytest
 import torch
 
-from hgin import ops
+from hgin import _lib, ops
 from oracle import c_oracle as co
 from oracle.pyg_cpu import propagate_sum
 
@@ -533,3 +533,29 @@ def test_gemm_nt_combine(dtype, M, K, F_src, F_dst, want_gx):
     ref = (c0[:, F_src:].double() * xd.double()).sum()
     bound = 1e-5 * float((c0[:, F_src:].double() * xd.double()).abs().sum()) + 1e-6
     assert abs(float(ge) - float(ref)) <= bound and abs(float(ge0) - float(ref)) <= bound
+
+
+@pytest.mark.parametrize("F", [1, 4, 7, 300])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_global_pool_vs_cpu_scatter(F, dtype):
+    """hgin_global_pool_*: [mean | max] of every graph's rows broadcast to its rows (models.py:347-352); the mean
+    bit-identical to CPU scatter_reduce "mean" (sequential sum, one division), the max exact; graph ids that skip
+    values, one-row graphs, a graph longer than a 256-row window, NaN propagation in the max."""
+    g = torch.Generator().manual_seed(F)
+    sizes = [1, 5, 700, 3, 1, 40, 257]
+    ids = [0, 1, 3, 4, 9, 10, 11]                       # 2, 5-8 have no rows
+    batch = torch.cat([torch.full((n,), i, dtype=torch.long) for n, i in zip(sizes, ids)])
+    x = torch.randn(batch.numel(), F + 3, generator=g)[:, 1:1 + F].to(dtype)    # strided rows
+    x[10, 0] = float("nan")                             # graph 3 (rows 6..705): its max / mean are NaN in column 0
+    xf = x.float()
+    size = int(batch.max()) + 1
+    idx = batch.view(-1, 1).expand(-1, F)
+    mean = torch.zeros(size, F).scatter_reduce(0, idx, xf, reduce="mean", include_self=False)
+    mx = torch.zeros(size, F).scatter_reduce(0, idx, xf, reduce="amax", include_self=False)
+    want = torch.cat([mean[batch], mx[batch]], 1).to(dtype)
+    with _lib.trace_launches() as tr:
+        got = ops.global_pool(x.to(DEV), batch.to(DEV)).cpu()
+    assert any(t.startswith("k_seg_pool") for t in tr.kernels)
+    assert torch.equal(got.isnan(), want.isnan())
+    ok = got.isnan() | (got == want)
+    assert bool(ok.all()), (~ok).nonzero()[:10]

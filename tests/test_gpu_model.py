@@ -295,8 +295,7 @@ def test_evaluate_host_resident_call(case):
     with torch.set_grad_enabled(False):
         out = model(dict(x), ei, batch)
         out2 = model(dict(x), ei, batch)
-    # (global_feats pools with torch's scatter_reduce, whose device atomics are not run-to-run bitwise)
-    assert out.device.type == "cpu" and _close(out, out2, 1e-6)
+    assert out.device.type == "cpu" and torch.equal(out, out2)    # bitwise run to run (global pooling included)
     assert all(p.device.type == "cpu" for p in model.parameters())
     assert all(b.device.type == "cpu" for b in model.buffers())
     if fx["meta"]["mlp_bn"]:
@@ -346,3 +345,21 @@ def test_layer_fn_equals_per_relation_autograd(feat):
             continue
         rel = float((a.double() - b.double()).norm() / (b.double().norm() + 1e-30))
         assert rel <= (1e-6 if feat == "f32" else 1e-2), rel
+
+
+def test_global_feats_bitwise_deterministic_and_no_aten_scatter():
+    """GLOBAL_FEATS (models.py:347-352) on the collated two-graph fixture: the pooling runs on hgin_global_pool_f32
+    (launch trace), the forward output and every gradient are bitwise identical run to run."""
+    fx = load_fixture("collate2_global_bn")
+    res = []
+    for _ in range(2):
+        model = _model_from_fixture(fx)
+        x, ei, batch, y = fixture_inputs(fx, DEV)
+        with _lib.trace_launches() as tr:
+            out = model(dict(x), ei, batch)
+            torch.sqrt(mape(out, y.reshape(-1, 1))).backward()
+        torch.cuda.synchronize()
+        assert any(t.startswith("k_seg_pool<f32") for t in tr.kernels), tr.kernels
+        res.append([out.detach().clone()] + [p.grad.clone() for p in model.parameters() if p.grad is not None])
+    for a, b in zip(*res):
+        assert torch.equal(a, b)
