@@ -771,6 +771,186 @@ int try_agg_pipe(const int32_t* rowptr, const int32_t* col, int64_t n_rows, cons
   return check_launch(what);
 }
 
+// ---------------------------------------------------------------------------------------------------
+// k_agg_lds — the fp32 F = 256 aggregate with its neighbour rows gathered into LDS by DMA
+// (MI355X_MICROARCH.md "Indexed rows: gather into LDS": global_load_lds_dwordx4 with a per-lane source address,
+// ~72 KiB+ in flight per CU).  Opt-in A/B against the register gather (HGIN_AGG_LDS = 1; ring depth
+// HGIN_AGG_LDS_D = 8 / 12 / 16 / 24 rows per wave).
+//   * Each wave owns a contiguous range of destination rows and a private ring of D 1-KiB LDS slots; no barriers.
+//   * Its item stream is, row by row, the row's neighbour rows in edge order, then (ADD) the row's x_dst row; one
+//     DMA instruction moves one 1-KiB row (64 lanes x 16 B).  The issue cursor runs D items ahead of the consumer.
+//   * Edge indices come in 64-entry chunks, one coalesced dword per lane by inline-asm load, double-buffered one
+//     chunk ahead and read with v_readlane — no compiler-visible vector load, so the compiler never inserts a
+//     vmcnt(0) that would drain the ring.  The consumer waits vmcnt(D - 1) (loads, LDS-DMA and stores retire in
+//     issue order for vmcnt: exactly D - 1 items were issued after the one it reads in steady state), vmcnt(0)
+//     while the stream drains.
+//   * The sum is taken from LDS in edge order with __fadd_rn, the self term as in k_aggregate: bit-identical.
+constexpr int kLdsRow = 1024;   // bytes of one F = 256 fp32 row = one DMA instruction
+
+template <int D, bool NT>
+__global__ __launch_bounds__(256) void k_agg_lds(const int32_t* __restrict__ rowptr, const int32_t* __restrict__ col,
+                                                 int64_t n_rows, const float* __restrict__ x_src, int64_t ld_src,
+                                                 const float* __restrict__ x_dst, int64_t ld_dst,
+                                                 const float* __restrict__ eps, int combine, float* __restrict__ out,
+                                                 int64_t ld_out, int64_t rows_per_wave) {
+  extern __shared__ __attribute__((aligned(16))) char agg_lds_ring[];
+  const int lane = threadIdx.x & (kWave - 1);
+  // wave-uniform (readfirstlane): every index / rowptr value below is then scalar — s_load, which waits on
+  // lgkmcnt, not vmcnt, so the compiler never drains the DMA ring for them
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+  char* ring = agg_lds_ring + wave * (D * kLdsRow);
+  const int64_t r0 = ((int64_t)blockIdx.x * 4 + wave) * rows_per_wave;
+  if (r0 >= n_rows) return;
+  const int64_t r1 = r0 + rows_per_wave < n_rows ? r0 + rows_per_wave : n_rows;
+  const bool add = combine == HGIN_COMBINE_ADD;
+  const float s = add ? __fadd_rn(1.0f, eps[0]) : 1.0f;
+  const int e0 = rowptr[r0];
+  const int e1 = rowptr[r1];
+
+  // edge-index chunks (64 per chunk, lane i holds col[base + i]); chunk c covers edges [e0 + 64 c, e0 + 64 c + 64)
+  auto load_chunk = [&](int c) -> int {
+    int v = 0;
+    const int e = e0 + c * 64 + lane;
+    const int ec = e < e1 ? e : (e1 > e0 ? e1 - 1 : e0);   // clamp inside the stream (a valid address)
+    const int32_t* p = col + ec;
+    if (e1 > e0) asm volatile("global_load_dword %0, %1, off" : "=v"(v) : "v"(p) : "memory");
+    return v;
+  };
+  int ck_cur = load_chunk(0);
+  int ck_nxt = load_chunk(1);
+  int ck_idx = 0;                       // chunk held in ck_cur
+  wait_vm<0>();
+
+  // issue cursor
+  int64_t ir = r0;
+  int ie = e0, iend = rowptr[r0 + 1];
+  bool iself = false;                   // the current issue row's self item was issued
+  int issued = 0, consumed = 0;
+  const uintptr_t xs = reinterpret_cast<uintptr_t>(x_src) + (uintptr_t)lane * 16;
+  const uintptr_t xd = reinterpret_cast<uintptr_t>(x_dst) + (uintptr_t)lane * 16;
+
+  auto issue_next = [&]() {
+    // next item of the stream: an edge of row ir, or (ADD) row ir's self row, else advance to the next row
+    while (ir < r1) {
+      if (ie < iend) {
+        const int c = (ie - e0) >> 6;
+        if (c != ck_idx) {              // crossed into the next chunk: it was loaded >= 64 items ago
+          ck_cur = ck_nxt;
+          ck_idx = c;
+          ck_nxt = load_chunk(c + 1);
+        }
+        const int src = __builtin_amdgcn_readlane(ck_cur, (ie - e0) & 63);
+        const void* g = reinterpret_cast<const void*>(xs + (uintptr_t)((int64_t)src * ld_src * 4));
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the slot's previous ds_read has returned
+        glds16_asm<false>(g, ring + (issued % D) * kLdsRow);
+        ++ie;
+        ++issued;
+        return;
+      }
+      if (add && !iself) {
+        const void* g = reinterpret_cast<const void*>(xd + (uintptr_t)(ir * ld_dst * 4));
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        glds16_asm<NT>(g, ring + (issued % D) * kLdsRow);
+        iself = true;
+        ++issued;
+        return;
+      }
+      ++ir;
+      iself = false;
+      if (ir < r1) iend = rowptr[__builtin_amdgcn_readfirstlane((int)(ir + 1))];
+    }
+  };
+  auto wait_item = [&]() {
+    if (issued - consumed == D) wait_vm<D - 1>(); else wait_vm<0>();
+  };
+
+  for (int j = 0; j < D; ++j) issue_next();
+  for (int64_t r = r0; r < r1; ++r) {
+    const int beg = rowptr[r], end = rowptr[r + 1];
+    float4 acc = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    for (int k = beg; k < end; ++k) {
+      wait_item();
+      const float4 v = *reinterpret_cast<const float4*>(ring + (consumed % D) * kLdsRow + lane * 16);
+      acc = make_float4(__fadd_rn(acc.x, v.x), __fadd_rn(acc.y, v.y), __fadd_rn(acc.z, v.z), __fadd_rn(acc.w, v.w));
+      ++consumed;
+      issue_next();
+    }
+    float4 o = acc;
+    if (add) {
+      wait_item();
+      const float4 v = *reinterpret_cast<const float4*>(ring + (consumed % D) * kLdsRow + lane * 16);
+      o = make_float4(__fadd_rn(acc.x, __fmul_rn(s, v.x)), __fadd_rn(acc.y, __fmul_rn(s, v.y)),
+                      __fadd_rn(acc.z, __fmul_rn(s, v.z)), __fadd_rn(acc.w, __fmul_rn(s, v.w)));
+      ++consumed;
+      issue_next();
+    }
+    Vec<4>::store_s<NT>(out + r * ld_out + lane * 4, o);
+  }
+  wait_vm<0>();
+}
+
+int agg_lds_depth() {   // 0: off (the register gather runs)
+  static const int d = [] {
+    const char* on = getenv("HGIN_AGG_LDS");
+    if (!(on && on[0] == '1')) return 0;
+    const char* v = getenv("HGIN_AGG_LDS_D");
+    const int x = v ? atoi(v) : 16;
+    return (x == 8 || x == 12 || x == 16 || x == 24) ? x : 16;
+  }();
+  return d;
+}
+
+template <int D, bool NT>
+int launch_agg_lds(const int32_t* rowptr, const int32_t* col, int64_t n_rows, const float* x_src, int64_t ld_src,
+                   const float* x_dst, int64_t ld_dst, const float* eps, int combine, float* out, int64_t ld_out,
+                   hipStream_t s) {
+  constexpr int lds = 4 * D * kLdsRow;
+  auto kern = k_agg_lds<D, NT>;
+  static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                                                     hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+  if (attr != hipSuccess) {
+    set_error("hgin_aggregate_f32: hipFuncSetAttribute failed: %s", hipGetErrorString(attr));
+    return (int)attr;
+  }
+  static const int64_t slots = [&] {
+    int per_cu = 0, dev = 0, cus = 256;
+    hipDeviceProp_t prop;
+    if (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&prop, dev) == hipSuccess)
+      cus = prop.multiProcessorCount;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 256, lds) != hipSuccess || per_cu <= 0)
+      per_cu = 1;
+    return (int64_t)per_cu * cus;
+  }();
+  // every resident wave one contiguous range of rows (uniform graphs: near-equal edge counts per range)
+  const int64_t waves = slots * 4;
+  const int64_t rpw = ceil_div(n_rows, waves);
+  const int64_t blocks = ceil_div(ceil_div(n_rows, rpw), 4);
+  HGIN_TRACE("k_agg_lds<D%d,mode%d>", D, combine);
+  kern<<<dim3((unsigned)blocks), 256, lds, s>>>(rowptr, col, n_rows, x_src, ld_src, x_dst, ld_dst, eps, combine, out,
+                                                ld_out, rpw);
+  return check_launch("hgin_aggregate_f32");
+}
+
+// Returns -1000 when the LDS gather is off or does not take these operands (fp32, F = 256, NONE / ADD,
+// 16-B aligned rows).
+int try_agg_lds(const int32_t* rowptr, const int32_t* col, int64_t n_rows, const float* x_src, int64_t ld_src,
+                int64_t f_src, const float* x_dst, int64_t ld_dst, int64_t f_dst, const float* eps, int combine,
+                float* out, int64_t ld_out, hipStream_t s) {
+  const int d = agg_lds_depth();
+  if (!d || f_src != 256 || combine == HGIN_COMBINE_CONCAT) return -1000;
+  if (!aligned16(x_src) || ld_src % 4 || !aligned16(out) || ld_out % 4) return -1000;
+  if (combine == HGIN_COMBINE_ADD && (f_dst != 256 || !aligned16(x_dst) || ld_dst % 4)) return -1000;
+  const bool nt = agg_nt(combine, n_rows, 1024);
+#define HGIN_LDS_D(DV)                                                                                          \
+  return nt ? launch_agg_lds<DV, true>(rowptr, col, n_rows, x_src, ld_src, x_dst, ld_dst, eps, combine, out, ld_out, s) \
+            : launch_agg_lds<DV, false>(rowptr, col, n_rows, x_src, ld_src, x_dst, ld_dst, eps, combine, out, ld_out, s);
+  if (d == 8) { HGIN_LDS_D(8) }
+  if (d == 12) { HGIN_LDS_D(12) }
+  if (d == 24) { HGIN_LDS_D(24) }
+  HGIN_LDS_D(16)
+#undef HGIN_LDS_D
+}
+
 int check_aggregate_args(const char* what, const int32_t* rowptr, int64_t n_rows, int64_t ld_src, int64_t f_src,
                          const void* x_dst, int64_t ld_dst, int64_t f_dst, const float* eps, int combine,
                          const void* out, int64_t ld_out) {
@@ -967,6 +1147,11 @@ extern "C" int hgin_aggregate_f32(const int32_t* rowptr, const int32_t* col, int
   const bool vec4 = f_src % 4 == 0 && aligned16(x_src) && ld_src % 4 == 0 && aligned16(out) && ld_out % 4 == 0 &&
                     dst_ok && (f_src > 0 || f_dst > 0);
   const int fd = combine == HGIN_COMBINE_CONCAT ? (int)f_dst : 0;
+  {
+    const int rc = try_agg_lds(rowptr, col, n_rows, x_src, ld_src, f_src, x_dst, ld_dst, f_dst, eps, combine, out,
+                               ld_out, s);
+    if (rc != -1000) return rc;
+  }
   {
     const int rc = try_agg_pipe<float>(rowptr, col, n_rows, x_src, ld_src, (int)f_src, x_dst, ld_dst, (int)f_dst, eps,
                                        combine, out, ld_out, s, "hgin_aggregate_f32");

@@ -9,7 +9,9 @@ fixtures (tests/variant_child.py), so the non-default paths pytest's own process
                               bit-identical to the default (every variant sums each row in edge order);
   * HGIN_XCD=0              — GEMM tiles in plain order instead of XCD-contiguous: bit-identical;
   * HGIN_NT2=1              — the LDS-DMA NT GEMM (k_nt2) instead of the register-staged one: bit-identical;
-  * HGIN_GEMM_NT_IO=1       — non-temporal GEMM epilogue streams at every size (default: > 512 MiB): bit-identical.
+  * HGIN_GEMM_NT_IO=1       — non-temporal GEMM epilogue streams at every size (default: > 512 MiB): bit-identical;
+  * HGIN_AGG_LDS=1 (+ _D)   — the fp32 F = 256 aggregate gathering neighbour rows into LDS by DMA (k_agg_lds, the
+                              w256_L3 fixture's forward ADD and backward NONE / ADD launches): bit-identical.
 
 Each child is a separate interpreter started with subprocess (never an exec of this process).
 """
@@ -35,8 +37,11 @@ VARIANTS = {
     "nt2_on": {"HGIN_NT2": "1"},
     "agg_nt_all": {"HGIN_AGG_NT": "1"},
     "gemm_nt_io": {"HGIN_GEMM_NT_IO": "1"},
+    "agg_lds8": {"HGIN_AGG_LDS": "1", "HGIN_AGG_LDS_D": "8"},
+    "agg_lds16": {"HGIN_AGG_LDS": "1", "HGIN_AGG_LDS_D": "16"},
 }
-BITWISE_EQUAL_TO_DEFAULT = ("slab2pass", "agg_nq2", "agg_pipe", "agg_notail", "xcd_off", "nt2_on", "agg_nt_all", "gemm_nt_io")
+BITWISE_EQUAL_TO_DEFAULT = ("slab2pass", "agg_nq2", "agg_pipe", "agg_notail", "xcd_off", "nt2_on", "agg_nt_all", "gemm_nt_io",
+                            "agg_lds8", "agg_lds16")
 
 _results = {}
 

@@ -17,7 +17,7 @@ for p in (HERE, ROOT, os.path.join(ROOT, "gnn-link-prediction_amd")):
 
 import torch  # noqa: E402
 
-from conftest import fixture_inputs, fixture_model_kwargs, load_fixture  # noqa: E402
+from conftest import fixture_inputs, fixture_model_kwargs, fixture_state_dict, load_fixture  # noqa: E402
 from hgin import HetroGIN  # noqa: E402
 from hgin.train import mape  # noqa: E402
 
@@ -25,7 +25,7 @@ from hgin.train import mape  # noqa: E402
 def run(case):
     fx = load_fixture(case)
     model = HetroGIN(**fixture_model_kwargs(fx))
-    model.load_state_dict({k[3:]: v for k, v in fx.items() if k.startswith("sd.")})
+    model.load_state_dict(fixture_state_dict(fx))
     model = model.to("cuda").train()
     x, ei, batch, y = fixture_inputs(fx, "cuda")
     out = model(dict(x), ei, batch)
@@ -49,7 +49,7 @@ def run(case):
 
 def main():
     torch.cuda.init()
-    res = {case: run(case) for case in ("cfg1_L2", "w128_L2", "wide_L3")}
+    res = {case: run(case) for case in ("cfg1_L2", "w128_L2", "wide_L3", "w256_L3")}
     torch.save(res, sys.argv[1])
     print("variant ok", {k: v for k, v in os.environ.items() if k.startswith("HGIN_")}, flush=True)
 
