@@ -779,11 +779,13 @@ int try_agg_pipe(const int32_t* rowptr, const int32_t* col, int64_t n_rows, cons
 //   * Each wave owns a contiguous range of destination rows and a private ring of D 1-KiB LDS slots; no barriers.
 //   * Its item stream is, row by row, the row's neighbour rows in edge order, then (ADD) the row's x_dst row; one
 //     DMA instruction moves one 1-KiB row (64 lanes x 16 B).  The issue cursor runs D items ahead of the consumer.
-//   * Edge indices come in 64-entry chunks, one coalesced dword per lane by inline-asm load, double-buffered one
-//     chunk ahead and read with v_readlane — no compiler-visible vector load, so the compiler never inserts a
-//     vmcnt(0) that would drain the ring.  The consumer waits vmcnt(D - 1) (loads, LDS-DMA and stores retire in
-//     issue order for vmcnt: exactly D - 1 items were issued after the one it reads in steady state), vmcnt(0)
-//     while the stream drains.
+//   * Edge indices come in 64-entry chunks, DMA'd into a per-wave double buffer in LDS (global_load_lds_dword, one
+//     index per lane) one chunk ahead, and read back with a broadcast ds_read: no compiler-visible vector load,
+//     so the compiler never inserts a vmcnt(0) that would drain the ring, and no VGPR is written asynchronously
+//     behind the compiler's back.  The consumer waits vmcnt(D - 1) (loads, LDS-DMA and stores retire in issue
+//     order for vmcnt: exactly D - 1 items were issued after the one it reads in steady state), vmcnt(0) while
+//     the stream drains.  A chunk's DMA is issued >= 64 items before its first index is read, so a later
+//     vmcnt(D - 1) wait (D <= 24) has always retired it.
 //   * The sum is taken from LDS in edge order with __fadd_rn, the self term as in k_aggregate: bit-identical.
 constexpr int kLdsRow = 1024;   // bytes of one F = 256 fp32 row = one DMA instruction
 
@@ -799,6 +801,7 @@ __global__ __launch_bounds__(256) void k_agg_lds(const int32_t* __restrict__ row
   // lgkmcnt, not vmcnt, so the compiler never drains the DMA ring for them
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
   char* ring = agg_lds_ring + wave * (D * kLdsRow);
+  int32_t* idx_buf = reinterpret_cast<int32_t*>(agg_lds_ring + 4 * D * kLdsRow) + wave * 128;   // 2 x 64 indices
   const int64_t r0 = ((int64_t)blockIdx.x * 4 + wave) * rows_per_wave;
   if (r0 >= n_rows) return;
   const int64_t r1 = r0 + rows_per_wave < n_rows ? r0 + rows_per_wave : n_rows;
@@ -807,18 +810,18 @@ __global__ __launch_bounds__(256) void k_agg_lds(const int32_t* __restrict__ row
   const int e0 = rowptr[r0];
   const int e1 = rowptr[r1];
 
-  // edge-index chunks (64 per chunk, lane i holds col[base + i]); chunk c covers edges [e0 + 64 c, e0 + 64 c + 64)
-  auto load_chunk = [&](int c) -> int {
-    int v = 0;
+  // edge-index chunk c (edges [e0 + 64 c, e0 + 64 c + 64), clamped inside the stream) -> idx_buf[(c & 1) * 64 + lane]
+  auto load_chunk = [&](int c) {
+    if (e1 <= e0) return;
     const int e = e0 + c * 64 + lane;
-    const int ec = e < e1 ? e : (e1 > e0 ? e1 - 1 : e0);   // clamp inside the stream (a valid address)
-    const int32_t* p = col + ec;
-    if (e1 > e0) asm volatile("global_load_dword %0, %1, off" : "=v"(v) : "v"(p) : "memory");
-    return v;
+    const int32_t* p = col + (e < e1 ? e : e1 - 1);
+    const uint32_t m0 = __builtin_amdgcn_readfirstlane(
+        (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)(reinterpret_cast<char*>(idx_buf + (c & 1) * 64)));
+    asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dword %0, off" ::"v"(p), "s"(m0) : "memory", "m0");
   };
-  int ck_cur = load_chunk(0);
-  int ck_nxt = load_chunk(1);
-  int ck_idx = 0;                       // chunk held in ck_cur
+  load_chunk(0);
+  load_chunk(1);
+  int ck_idx = 0;                       // highest chunk whose successor's DMA has been issued - 1
   wait_vm<0>();
 
   // issue cursor
@@ -834,12 +837,11 @@ __global__ __launch_bounds__(256) void k_agg_lds(const int32_t* __restrict__ row
     while (ir < r1) {
       if (ie < iend) {
         const int c = (ie - e0) >> 6;
-        if (c != ck_idx) {              // crossed into the next chunk: it was loaded >= 64 items ago
-          ck_cur = ck_nxt;
+        if (c != ck_idx) {              // entered chunk c (DMA'd >= 64 items ago): prefetch chunk c + 1
           ck_idx = c;
-          ck_nxt = load_chunk(c + 1);
+          load_chunk(c + 1);
         }
-        const int src = __builtin_amdgcn_readlane(ck_cur, (ie - e0) & 63);
+        const int src = __builtin_amdgcn_readfirstlane(idx_buf[(c & 1) * 64 + ((ie - e0) & 63)]);
         const void* g = reinterpret_cast<const void*>(xs + (uintptr_t)((int64_t)src * ld_src * 4));
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the slot's previous ds_read has returned
         glds16_asm<false>(g, ring + (issued % D) * kLdsRow);
@@ -904,7 +906,7 @@ template <int D, bool NT>
 int launch_agg_lds(const int32_t* rowptr, const int32_t* col, int64_t n_rows, const float* x_src, int64_t ld_src,
                    const float* x_dst, int64_t ld_dst, const float* eps, int combine, float* out, int64_t ld_out,
                    hipStream_t s) {
-  constexpr int lds = 4 * D * kLdsRow;
+  constexpr int lds = 4 * D * kLdsRow + 4 * 128 * 4;    // row rings + per-wave double-buffered index chunks
   auto kern = k_agg_lds<D, NT>;
   static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
                                                      hipFuncAttributeMaxDynamicSharedMemorySize, lds);
