@@ -835,7 +835,14 @@ __global__ __launch_bounds__(256, 2) void k_gemm_tn_bf16_tr(const uint16_t* __re
 // the last block are zeroed in LDS before use.  Each workgroup's N x K partial goes to its fp32 slab; the slabs
 // are added by k_slab_reduce in fixed order: deterministic (a different M partition from the tiled kernel,
 // so equal within fp32 reassociation, not bitwise).
-template <int N, int K>
+// PRO (the PReLU backward folded in, hgin_gin_mlp_bwd_w_bf16 when g_z is wanted): the A image is DMA'd as g_y
+// with a second image of z beside it (same rows, same swizzle, so a chunk of one lines up with the same elements of
+// the other); once a block has landed, every thread rewrites its fixed chunks of the A image in place as
+// g_z = z > 0 ? g_y : slope * g_y (fp32 arithmetic, one RNE rounding: k_rows_bwd<0>'s), stores them to the g_z
+// output (the dX GEMM's operand) and keeps per-thread column sums of the unrounded g_z and the slope sum
+// (z <= 0 ? z * g_y), reduced per workgroup in fixed order into the [N][slabs] / [slabs] partials k_slab_reduce
+// finishes.  g_w is bit-identical to k_rows_bwd<0> + the plain kernel (same g_z, same grid).
+template <int N, int K, bool PRO = false>
 struct WsdCfg {
   static constexpr int NT = 512;
   static constexpr int WM = N / 64;                  // waves along n (64 rows each)
@@ -844,22 +851,49 @@ struct WsdCfg {
   static constexpr int BM = 32;                      // m rows per block
   static constexpr int RA = N * 2, RB = K * 2;       // image row bytes
   static constexpr int A_BYTES = BM * RA, B_BYTES = BM * RB;
-  static constexpr int SLOT = A_BYTES + B_BYTES;
-  static constexpr int NST = 4;
+  static constexpr int Z_BYTES = PRO ? A_BYTES : 0;  // the z image (PRO)
+  static constexpr int SLOT = A_BYTES + Z_BYTES + B_BYTES;
+  static constexpr int NST = PRO ? 3 : 4;
   static constexpr int PA = A_BYTES / 1024 / 8, PB = B_BYTES / 1024 / 8;   // DMA pieces per wave per block
-  static constexpr int P = PA + PB;
+  static constexpr int P = PA + (PRO ? PA : 0) + PB;
+  static constexpr int CH = A_BYTES / 16 / NT;       // PRO: A chunks per thread per block = g_z stores per wave
   static_assert(TK >= 1 && A_BYTES % 8192 == 0 && B_BYTES % 8192 == 0 && SLOT * NST <= 147456, "shape");
 };
 
+// vmcnt bound before block i of a weight-stationary dW ring: the DMA pieces of the (NST - 2) later blocks plus the
+// PRO stores issued after block i's DMA (min(i, NST - 1) blocks' worth: fewer while the ring fills).
+template <int NST, int P, int S>
+__device__ __forceinline__ void wsd_wait(int64_t i) {
+  if constexpr (S == 0) {
+    wait_vm<(NST - 2) * P>();
+  } else {
+    static_assert(NST == 2 || NST == 3, "wsd_wait");
+    if (i == 0) wait_vm<(NST - 2) * P>();
+    else if (NST == 3 && i == 1) wait_vm<(NST - 2) * P + S>();
+    else wait_vm<(NST - 2) * P + (NST - 1) * S>();
+  }
+}
+
 __device__ __forceinline__ int wsd_swz(int row) { return ((row & 3) << 2) | ((row >> 2) & 3); }
 
-template <int N, int K>
+struct WsdPro {   // the PRO variant's extra operands (unused otherwise)
+  const void* z;
+  int64_t ldz;
+  const float* slope;
+  void* gz;          // g_z output [M, N] (ld ldgz)
+  int64_t ldgz;
+  float* pcol;       // [N][gridDim.x] column sums of g_z
+  float* ps;         // [gridDim.x] slope sums
+  char* dump;        // 16-B store target of the lanes whose rows are past M (every wave issues the same stores)
+};
+
+template <int N, int K, bool PRO>
 __global__ __launch_bounds__(512, 1) void k_wsd_bf16(const uint16_t* __restrict__ A, int64_t lda,
                                                      const uint16_t* __restrict__ B1, int64_t ldb1,
                                                      const uint16_t* __restrict__ B2, int64_t ldb2, int64_t K1,
                                                      int64_t M, float* __restrict__ slab, int64_t ld_slab,
-                                                     bool nt_in) {
-  using C = WsdCfg<N, K>;
+                                                     bool nt_in, WsdPro pro) {
+  using C = WsdCfg<N, K, PRO>;
   constexpr int NST = C::NST;
   extern __shared__ __attribute__((aligned(16))) char wsd_smem[];
   const int tid = threadIdx.x;
@@ -896,6 +930,8 @@ __global__ __launch_bounds__(512, 1) void k_wsd_bf16(const uint16_t* __restrict_
       const int c = ((off % C::RA) >> 4) ^ wsd_swz(r);
       r = r < rmax ? r : rmax;                       // (rows past M are zeroed in LDS before use)
       dma(ab + (r * (int)lda + c * 8), base + piece * 1024);
+      if constexpr (PRO)                             // z: the same rows and swizzle, the image beside A
+        dma(static_cast<const uint16_t*>(pro.z) + (r0 + r) * pro.ldz + c * 8, base + C::A_BYTES + piece * 1024);
     }
 #pragma unroll
     for (int q = 0; q < C::PB; ++q) {
@@ -905,9 +941,18 @@ __global__ __launch_bounds__(512, 1) void k_wsd_bf16(const uint16_t* __restrict_
       const int c = ((off % C::RB) >> 4) ^ wsd_swz(r);
       r = r < rmax ? r : rmax;
       const int k = c * 8;
-      dma(k < k1 ? b1 + (r * (int)ldb1 + k) : b2 + (r * (int)ldb2 + (k - k1)), base + C::A_BYTES + piece * 1024);
+      dma(k < k1 ? b1 + (r * (int)ldb1 + k) : b2 + (r * (int)ldb2 + (k - k1)),
+          base + C::A_BYTES + C::Z_BYTES + piece * 1024);
     }
   };
+  // PRO: per-thread partial sums over every block of this workgroup (fixed chunks -> fixed columns)
+  float csum[PRO ? C::CH : 1][8];
+  float ssum = 0.0f;
+  const float sl = PRO ? pro.slope[0] : 0.0f;
+#pragma unroll
+  for (int q = 0; q < (PRO ? C::CH : 1); ++q)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) csum[q][j] = 0.0f;
 
   f32x16 acc[2][C::TK];
 #pragma unroll
@@ -931,7 +976,7 @@ __global__ __launch_bounds__(512, 1) void k_wsd_bf16(const uint16_t* __restrict_
     if (i < my) issue(i);
 
   for (int64_t i = 0; i < my; ++i) {
-    if (i + NST - 2 < my) wait_vm<(NST - 2) * C::P>(); else wait_vm<0>();
+    if (i + NST - 2 < my) wsd_wait<NST, C::P, PRO ? C::CH : 0>(i); else wait_vm<0>();
     __builtin_amdgcn_s_barrier();                  // block i landed for every wave; slot of block i-1 is free
     asm volatile("" ::: "memory");
     if (i + NST - 1 < my) issue(i + NST - 1);
@@ -941,12 +986,48 @@ __global__ __launch_bounds__(512, 1) void k_wsd_bf16(const uint16_t* __restrict_
       const int valid = (int)(M - r0);
       uint4* p = reinterpret_cast<uint4*>(wsd_smem + sbase);
       for (int ch = tid; ch < C::SLOT / 16; ch += C::NT) {
-        const int inb = ch * 16 >= C::A_BYTES;
-        const int row = inb ? (ch * 16 - C::A_BYTES) / C::RB : (ch * 16) / C::RA;
+        const int ob = ch * 16;
+        const int inb = ob >= C::A_BYTES + C::Z_BYTES;
+        const int row = inb ? (ob - C::A_BYTES - C::Z_BYTES) / C::RB : (ob % C::A_BYTES) / C::RA;
         if (row >= valid) p[ch] = make_uint4(0u, 0u, 0u, 0u);
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+    }
+    if constexpr (PRO) {   // g_z in place of g_y, its store, the partial sums (zeroed rows contribute 0)
+#pragma unroll
+      for (int q = 0; q < C::CH; ++q) {
+        const int ch = q * C::NT + tid;
+        const int row = ch / (C::RA / 16);
+        const int c = (ch % (C::RA / 16)) ^ wsd_swz(row);   // logical 8-column chunk
+        uint4* pa = reinterpret_cast<uint4*>(wsd_smem + sbase + ch * 16);
+        const uint4 gy = *pa, zz = *reinterpret_cast<const uint4*>(wsd_smem + sbase + C::A_BYTES + ch * 16);
+        const uint32_t gw[4] = {gy.x, gy.y, gy.z, gy.w}, zw[4] = {zz.x, zz.y, zz.z, zz.w};
+        uint32_t ow[4];
+#pragma unroll
+        for (int w = 0; w < 4; ++w) {
+          float o2[2];
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            const float g = h ? bf_hi(gw[w]) : bf_lo(gw[w]);
+            const float zv = h ? bf_hi(zw[w]) : bf_lo(zw[w]);
+            const bool pos = zv > 0.0f;
+            o2[h] = pos ? g : __fmul_rn(sl, g);
+            csum[q][2 * w + h] = __fadd_rn(csum[q][2 * w + h], o2[h]);
+            if (!pos) ssum = __fadd_rn(ssum, __fmul_rn(zv, g));
+          }
+          ow[w] = pack_bf2(o2[0], o2[1]);
+        }
+        const uint4 o = make_uint4(ow[0], ow[1], ow[2], ow[3]);
+        *pa = o;
+        const int64_t gr = r0 + row;
+        uint16_t* gzp = static_cast<uint16_t*>(pro.gz) + gr * pro.ldgz + c * 8;
+        uint4* dst = gr < M ? reinterpret_cast<uint4*>(gzp) : reinterpret_cast<uint4*>(pro.dump + (int64_t)ch * 16);
+        *dst = o;
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();                // every thread's g_z chunks are in the image
       asm volatile("" ::: "memory");
     }
     __builtin_amdgcn_s_setprio(1);
@@ -964,7 +1045,7 @@ __global__ __launch_bounds__(512, 1) void k_wsd_bf16(const uint16_t* __restrict_
       for (int t = 0; t < C::TK; ++t) {
         const int col = wk * (C::TK * 32) + t * 32 + 16 * (g & 1) + 4 * pp;
         const int row = 16 * kb + 8 * (g >> 1) + q4;
-        const int bb = sbase + C::A_BYTES;
+        const int bb = sbase + C::A_BYTES + C::Z_BYTES;
         const bf16x4 b0 = tr(bb + tr_off(C::RB, row, col)), b1 = tr(bb + tr_off(C::RB, row + 4, col));
         fb[t] = __builtin_shufflevector(b0, b1, 0, 1, 2, 3, 4, 5, 6, 7);
       }
@@ -976,6 +1057,34 @@ __global__ __launch_bounds__(512, 1) void k_wsd_bf16(const uint16_t* __restrict_
     }
     __builtin_amdgcn_s_setprio(0);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // this wave's reads of the slot are done
+  }
+  if constexpr (PRO) {   // fixed-order workgroup sums: column n over the 32 image rows, the slope over the threads
+    wait_vm<0>();
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    float* red = reinterpret_cast<float*>(wsd_smem);   // [NT][CH * 8], then [NT] slope partials
+#pragma unroll
+    for (int q = 0; q < C::CH; ++q)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) red[tid * (C::CH * 8) + q * 8 + j] = csum[q][j];
+    red[C::NT * C::CH * 8 + tid] = ssum;
+    __syncthreads();
+    constexpr int CPR = C::RA / 16;   // chunks per image row
+    for (int n = tid; n < N; n += C::NT) {
+      const int c = n >> 3, j = n & 7;
+      float tot = 0.0f;
+      for (int row = 0; row < C::BM; ++row) {
+        const int ch = row * CPR + (c ^ wsd_swz(row));
+        tot = __fadd_rn(tot, red[(ch % C::NT) * (C::CH * 8) + (ch / C::NT) * 8 + j]);
+      }
+      pro.pcol[(int64_t)n * gridDim.x + blockIdx.x] = tot;
+    }
+    float* sr = red + C::NT * C::CH * 8;
+    for (int off = C::NT / 2; off > 0; off >>= 1) {
+      __syncthreads();
+      if (tid < off) sr[tid] = __fadd_rn(sr[tid], sr[tid + off]);
+    }
+    if (tid == 0) pro.ps[blockIdx.x] = sr[0];
   }
   // this workgroup's slab [N][ld_slab] (the caller offsets slab to its column block)
   float* out = slab + (int64_t)blockIdx.x * N * ld_slab;
@@ -997,29 +1106,37 @@ __global__ __launch_bounds__(512, 1) void k_wsd_bf16(const uint16_t* __restrict_
 // k_gemm_tn_partial arithmetic).  16-row m-blocks of A and B (fp32, linear images) stream HBM -> LDS by DMA into
 // a 3-deep ring; per block one pass splits both into three bf16 planes (each element once per CU, into
 // swizzled m-major plane images read by ds_read_b64_tr_b16), then each wave runs its 2 x TK tiles x 6 products.
-template <int N, int K>
+// PRO (N = 256: every thread splits exactly one 8-column group of A per block): A is DMA'd as g_y with z beside it;
+// the split pass forms g_z = z > 0 ? g_y : slope * g_y (k_rows_bwd<0>'s arithmetic), stores it (fp32, the dX GEMM's
+// operand), keeps the column / slope partial sums, then splits g_z — g_w bit-identical to the two-pass form.  The z
+// image costs the ring one slot (2 deep).
+template <int N, int K, bool PRO = false>
 struct WsdF32Cfg {
   static constexpr int NT = 512;
   static constexpr int WM = N / 64, WK = 8 / WM, TK = K / WK / 32;
   static constexpr int BM = 16;                              // one 16-deep MFMA k-step per block
   static constexpr int A_BYTES = BM * N * 4, B_BYTES = BM * K * 4;
-  static constexpr int SLOT = A_BYTES + B_BYTES;
-  static constexpr int NST = 3;
+  static constexpr int Z_BYTES = PRO ? A_BYTES : 0;
+  static constexpr int SLOT = A_BYTES + Z_BYTES + B_BYTES;
+  static constexpr int NST = PRO ? 2 : 3;
   static constexpr int PA_ROW = N * 2, PB_ROW = K * 2;       // plane image row bytes (bf16)
   static constexpr int PA_BYTES = BM * PA_ROW, PB_BYTES = BM * PB_ROW;   // one plane
   static constexpr int PLANES = 3 * (PA_BYTES + PB_BYTES);
   static constexpr int LDS = SLOT * NST + PLANES;
   static constexpr int PA = A_BYTES / 1024 / 8, PB = B_BYTES / 1024 / 8;
-  static constexpr int P = PA + PB;
+  static constexpr int P = PA + (PRO ? PA : 0) + PB;
+  static constexpr int S = PRO ? 2 : 0;                      // g_z stores per wave per block (2 x 16 B per thread)
   static_assert(TK >= 1 && A_BYTES % 8192 == 0 && B_BYTES % 8192 == 0 && LDS <= 147456, "shape");
+  static_assert(!PRO || BM * N / 8 == NT, "PRO: one A group per thread");
 };
 
-template <int N, int K>
+template <int N, int K, bool PRO>
 __global__ __launch_bounds__(512, 1) void k_wsd_f32(const float* __restrict__ A, int64_t lda,
                                                     const float* __restrict__ B1, int64_t ldb1,
                                                     const float* __restrict__ B2, int64_t ldb2, int64_t K1, int64_t M,
-                                                    float* __restrict__ slab, int64_t ld_slab, bool nt_in) {
-  using C = WsdF32Cfg<N, K>;
+                                                    float* __restrict__ slab, int64_t ld_slab, bool nt_in,
+                                                    WsdPro pro) {
+  using C = WsdF32Cfg<N, K, PRO>;
   constexpr int NST = C::NST;
   extern __shared__ __attribute__((aligned(16))) char wsdf_smem[];
   const int tid = threadIdx.x;
@@ -1056,6 +1173,9 @@ __global__ __launch_bounds__(512, 1) void k_wsd_f32(const float* __restrict__ A,
       int r = off / (N * 4);
       r = r < rmax ? r : rmax;                       // (rows past M are zeroed at the split)
       dma(ab + (r * (int)lda + (off % (N * 4)) / 4), base + piece * 1024);
+      if constexpr (PRO)
+        dma(static_cast<const float*>(pro.z) + (r0 + r) * pro.ldz + (off % (N * 4)) / 4,
+            base + C::A_BYTES + piece * 1024);
     }
 #pragma unroll
     for (int q = 0; q < C::PB; ++q) {
@@ -1064,9 +1184,15 @@ __global__ __launch_bounds__(512, 1) void k_wsd_f32(const float* __restrict__ A,
       int r = off / (K * 4);
       r = r < rmax ? r : rmax;
       const int k = (off % (K * 4)) / 4;
-      dma(k < k1 ? b1 + (r * (int)ldb1 + k) : b2 + (r * (int)ldb2 + (k - k1)), base + C::A_BYTES + piece * 1024);
+      dma(k < k1 ? b1 + (r * (int)ldb1 + k) : b2 + (r * (int)ldb2 + (k - k1)),
+          base + C::A_BYTES + C::Z_BYTES + piece * 1024);
     }
   };
+  float csum[8];
+  float ssum = 0.0f;
+  const float sl = PRO ? pro.slope[0] : 0.0f;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) csum[j] = 0.0f;
 
   f32x16 acc[2][C::TK];
 #pragma unroll
@@ -1087,7 +1213,7 @@ __global__ __launch_bounds__(512, 1) void k_wsd_f32(const float* __restrict__ A,
     if (i < my) issue(i);
 
   for (int64_t i = 0; i < my; ++i) {
-    if (i + NST - 2 < my) wait_vm<(NST - 2) * C::P>(); else wait_vm<0>();
+    if (i + NST - 2 < my) wsd_wait<NST, C::P, C::S>(i); else wait_vm<0>();
     __builtin_amdgcn_s_barrier();   // block i landed for every wave; slot i-1 and the plane images are free
     asm volatile("" ::: "memory");
     if (i + NST - 1 < my) issue(i + NST - 1);
@@ -1105,9 +1231,33 @@ __global__ __launch_bounds__(512, 1) void k_wsd_f32(const float* __restrict__ A,
         const int cols = isA ? N : K;
         const int e0 = (isA ? grp : grp - CA) * 8;
         const int row = e0 / cols, col = e0 % cols;
-        const float* src = reinterpret_cast<const float*>(fbase + (isA ? 0 : C::A_BYTES)) + e0;
+        const float* src = reinterpret_cast<const float*>(fbase + (isA ? 0 : C::A_BYTES + C::Z_BYTES)) + e0;
         float4 v0 = *reinterpret_cast<const float4*>(src), v1 = *reinterpret_cast<const float4*>(src + 4);
         if (row >= valid) v0 = v1 = make_float4(0.f, 0.f, 0.f, 0.f);
+        if constexpr (PRO) {
+          if (isA) {   // g_z from g_y (v0, v1) and z; its store; the partial sums
+            const float* zs = reinterpret_cast<const float*>(fbase + C::A_BYTES) + e0;
+            float4 z0 = *reinterpret_cast<const float4*>(zs), z1 = *reinterpret_cast<const float4*>(zs + 4);
+            if (row >= valid) z0 = z1 = make_float4(0.f, 0.f, 0.f, 0.f);
+            float g[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+            const float zz[8] = {z0.x, z0.y, z0.z, z0.w, z1.x, z1.y, z1.z, z1.w};
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+              const bool pos = zz[j] > 0.0f;
+              const float o = pos ? g[j] : __fmul_rn(sl, g[j]);
+              csum[j] = __fadd_rn(csum[j], o);
+              if (!pos) ssum = __fadd_rn(ssum, __fmul_rn(zz[j], g[j]));
+              g[j] = o;
+            }
+            v0 = make_float4(g[0], g[1], g[2], g[3]);
+            v1 = make_float4(g[4], g[5], g[6], g[7]);
+            const int64_t gr = r0 + row;
+            float* gzp = gr < M ? static_cast<float*>(pro.gz) + gr * pro.ldgz + col
+                                : reinterpret_cast<float*>(pro.dump + (int64_t)t * 32);
+            *reinterpret_cast<float4*>(gzp) = v0;
+            *reinterpret_cast<float4*>(gzp + 4) = v1;
+          }
+        }
         uint2 o0[3], o1[3];
         split4(v0, o0);
         split4(v1, o1);
@@ -1161,6 +1311,27 @@ __global__ __launch_bounds__(512, 1) void k_wsd_f32(const float* __restrict__ A,
     __builtin_amdgcn_s_setprio(0);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   }
+  if constexpr (PRO) {   // fixed-order workgroup sums: column n over the 16 block rows, the slope over the threads
+    wait_vm<0>();
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    float* red = reinterpret_cast<float*>(wsdf_smem);   // [NT][8], then [NT] slope partials
+#pragma unroll
+    for (int j = 0; j < 8; ++j) red[tid * 8 + j] = csum[j];
+    red[C::NT * 8 + tid] = ssum;
+    __syncthreads();
+    for (int n = tid; n < N; n += C::NT) {   // thread t split row t / (N / 8), columns (t % (N / 8)) * 8 .. + 7
+      float tot = 0.0f;
+      for (int row = 0; row < C::BM; ++row) tot = __fadd_rn(tot, red[(row * (N / 8) + (n >> 3)) * 8 + (n & 7)]);
+      pro.pcol[(int64_t)n * gridDim.x + blockIdx.x] = tot;
+    }
+    float* sr = red + C::NT * 8;
+    for (int off = C::NT / 2; off > 0; off >>= 1) {
+      __syncthreads();
+      if (tid < off) sr[tid] = __fadd_rn(sr[tid], sr[tid + off]);
+    }
+    if (tid == 0) pro.ps[blockIdx.x] = sr[0];
+  }
   float* out = slab + (int64_t)blockIdx.x * N * ld_slab;
   const int li = lane & 31, lh = lane >> 5;
 #pragma unroll
@@ -1187,6 +1358,15 @@ bool wsd_enabled() {
   return on;
 }
 
+// HGIN_WSD_PRO = 0 keeps the separate PReLU-backward pass (k_rows_bwd<0>) ahead of the weight-stationary dW.
+bool wsd_pro_enabled() {
+  static const bool on = [] {
+    const char* v = getenv("HGIN_WSD_PRO");
+    return !(v && v[0] == '0');
+  }();
+  return on;
+}
+
 int64_t wsd_cus() {
   static const int64_t g = [] {
     int dev = 0;
@@ -1197,11 +1377,12 @@ int64_t wsd_cus() {
   return g;
 }
 
-template <int NV, int KV>
+template <int NV, int KV, bool PRO = false>
 int64_t launch_wsd(const uint16_t* a, int64_t lda, const uint16_t* b1, int64_t ldb1, const uint16_t* b2,
-                   int64_t ldb2, int64_t k1, int64_t M, float* slab, int64_t ld_slab, int64_t grid, hipStream_t s) {
-  constexpr int lds = WsdCfg<NV, KV>::SLOT * WsdCfg<NV, KV>::NST;
-  auto kern = k_wsd_bf16<NV, KV>;
+                   int64_t ldb2, int64_t k1, int64_t M, float* slab, int64_t ld_slab, int64_t grid, hipStream_t s,
+                   const WsdPro& pro = WsdPro{}) {
+  constexpr int lds = WsdCfg<NV, KV, PRO>::SLOT * WsdCfg<NV, KV, PRO>::NST;
+  auto kern = k_wsd_bf16<NV, KV, PRO>;
   static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
                                                      hipFuncAttributeMaxDynamicSharedMemorySize, lds);
   if (attr != hipSuccess) return 0;
@@ -1209,16 +1390,17 @@ int64_t launch_wsd(const uint16_t* a, int64_t lda, const uint16_t* b1, int64_t l
     const char* v = getenv("HGIN_WS_NT");
     return !(v && v[0] == '0');
   }();
-  HGIN_TRACE("k_wsd_bf16<%d,%d>", NV, KV);
-  kern<<<(unsigned)grid, 512, lds, s>>>(a, lda, b1, ldb1, b2, ldb2, k1, M, slab, ld_slab, nt);
+  HGIN_TRACE("k_wsd_bf16<%d,%d%s>", NV, KV, PRO ? ",prelu_bwd_fused" : "");
+  kern<<<(unsigned)grid, 512, lds, s>>>(a, lda, b1, ldb1, b2, ldb2, k1, M, slab, ld_slab, nt, pro);
   return grid;
 }
 
-template <int NV, int KV>
+template <int NV, int KV, bool PRO = false>
 int64_t launch_wsd(const float* a, int64_t lda, const float* b1, int64_t ldb1, const float* b2, int64_t ldb2,
-                   int64_t k1, int64_t M, float* slab, int64_t ld_slab, int64_t grid, hipStream_t s) {
-  constexpr int lds = WsdF32Cfg<NV, KV>::LDS;
-  auto kern = k_wsd_f32<NV, KV>;
+                   int64_t k1, int64_t M, float* slab, int64_t ld_slab, int64_t grid, hipStream_t s,
+                   const WsdPro& pro = WsdPro{}) {
+  constexpr int lds = WsdF32Cfg<NV, KV, PRO>::LDS;
+  auto kern = k_wsd_f32<NV, KV, PRO>;
   static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
                                                      hipFuncAttributeMaxDynamicSharedMemorySize, lds);
   if (attr != hipSuccess) return 0;
@@ -1226,8 +1408,8 @@ int64_t launch_wsd(const float* a, int64_t lda, const float* b1, int64_t ldb1, c
     const char* v = getenv("HGIN_WS_NT");
     return !(v && v[0] == '0');
   }();
-  HGIN_TRACE("k_wsd_f32<%d,%d>", NV, KV);
-  kern<<<(unsigned)grid, 512, lds, s>>>(a, lda, b1, ldb1, b2, ldb2, k1, M, slab, ld_slab, nt);
+  HGIN_TRACE("k_wsd_f32<%d,%d%s>", NV, KV, PRO ? ",prelu_bwd_fused" : "");
+  kern<<<(unsigned)grid, 512, lds, s>>>(a, lda, b1, ldb1, b2, ldb2, k1, M, slab, ld_slab, nt, pro);
   return grid;
 }
 
@@ -1242,6 +1424,57 @@ int64_t wsd_cols(const T* a, int64_t lda, const T* b1, int64_t ldb1, int64_t k1,
   const T* p2 = kk1 < KV ? b2 + (c0 + kk1 - k1) : p1;
   const int64_t l2 = kk1 < KV ? ldb2 : l1;
   return launch_wsd<NV, KV>(a, lda, p1, l1, p2, l2, kk1, M, slab + c0, ld_slab, grid, s);
+}
+
+// The PReLU-backward-fused weight-stationary dW (bf16, single column pass: N in {128, 256}, K in {128, 256}):
+// g_w slabs + g_z + bias / slope partials in one launch.  Returns the slab count, or 0 when it does not apply.
+template <typename T>
+int64_t try_wsd_pro(const T* gy, int64_t ldgy, const T* b1, int64_t ldb1, int64_t k1, const T* b2, int64_t ldb2,
+                    int64_t M, int64_t N, int64_t K, float* slab, int64_t max_slabs, const WsdPro& pro,
+                    hipStream_t s) {
+  if constexpr (sizeof(T) == 4) {   // fp32 (split mode): N = 256, K in {128, 256}
+    constexpr int64_t vw = 4;
+    if (!wsd_enabled() || !wsd_pro_enabled() || !gemm_split_enabled() || M < 1 || N != 256 ||
+        (K != 128 && K != 256) || k1 % vw)
+      return 0;
+    auto ok = [](const void* p, int64_t ld) { return aligned16(p) && ld % vw == 0 && ld < (int64_t(1) << 24); };
+    if (!ok(gy, ldgy) || !ok(pro.z, pro.ldz) || !ok(pro.gz, pro.ldgz) || (k1 > 0 && !ok(b1, ldb1)) ||
+        (k1 < K && !ok(b2, ldb2)))
+      return 0;
+    int64_t grid = wsd_cus();
+    const int64_t nblk = ceil_div(M, (int64_t)16);
+    if (grid > nblk) grid = nblk;
+    if (grid > max_slabs) grid = max_slabs;
+    const float* p1 = k1 > 0 ? b1 : b2;
+    const int64_t l1 = k1 > 0 ? ldb1 : ldb2;
+    const float* p2 = k1 < K ? b2 : p1;
+    const int64_t l2 = k1 < K ? ldb2 : l1;
+    if (K == 256) return launch_wsd<256, 256, true>(gy, ldgy, p1, l1, p2, l2, k1, M, slab, K, grid, s, pro);
+    return launch_wsd<256, 128, true>(gy, ldgy, p1, l1, p2, l2, k1, M, slab, K, grid, s, pro);
+  } else {
+    constexpr int64_t vw = 8;
+    if (!wsd_enabled() || !wsd_pro_enabled() || M < 1 || (N != 128 && N != 256) || (K != 128 && K != 256) ||
+        k1 % vw)
+      return 0;
+    auto ok = [](const void* p, int64_t ld) { return aligned16(p) && ld % vw == 0 && ld < (int64_t(1) << 24); };
+    if (!ok(gy, ldgy) || !ok(pro.z, pro.ldz) || !ok(pro.gz, pro.ldgz) || (k1 > 0 && !ok(b1, ldb1)) ||
+        (k1 < K && !ok(b2, ldb2)))
+      return 0;
+    int64_t grid = wsd_cus();
+    const int64_t nblk = ceil_div(M, (int64_t)32);
+    if (grid > nblk) grid = nblk;
+    if (grid > max_slabs) grid = max_slabs;
+    const uint16_t* p1 = k1 > 0 ? b1 : b2;
+    const int64_t l1 = k1 > 0 ? ldb1 : ldb2;
+    const uint16_t* p2 = k1 < K ? b2 : p1;
+    const int64_t l2 = k1 < K ? ldb2 : l1;
+#define HGIN_WSD_PRO(NV, KV) return launch_wsd<NV, KV, true>(gy, ldgy, p1, l1, p2, l2, k1, M, slab, K, grid, s, pro);
+    if (N == 256 && K == 256) HGIN_WSD_PRO(256, 256)
+    if (N == 256 && K == 128) HGIN_WSD_PRO(256, 128)
+    if (N == 128 && K == 256) HGIN_WSD_PRO(128, 256)
+    HGIN_WSD_PRO(128, 128)
+#undef HGIN_WSD_PRO
+  }
 }
 
 template <typename T>
@@ -1496,11 +1729,21 @@ int gemm_tn_entry(const char* what, const T* a, int64_t lda, const T* b1, int64_
 // PReLU backward into g_z (the caller's buffer, or workspace scratch) followed by the plain TN GEMM.
 bool mlp_bwd_w_fused(int64_t N, int64_t K, size_t elem) { return elem == 4 && !tn_is_small(N, K); }
 
+// the weight-stationary PRO kernel's partials: [N][slabs] column sums, [slabs] slope sums, the 16-B dump of every
+// thread's out-of-range g_z stores (NT x CH chunks)
+size_t wsd_pro_ws_bytes(int64_t M, int64_t N, int64_t K) {
+  const int64_t S = tn_ws_slabs(M, N, K);
+  return align_up(sizeof(float) * (size_t)(N * S), 256) + align_up(sizeof(float) * (size_t)S, 256) +
+         align_up((size_t)16 * 512 * 2, 256);
+}
+
 size_t mlp_bwd_w_ws_bytes(int64_t M, int64_t N, int64_t K, size_t elem, bool have_gz) {
   if (mlp_bwd_w_fused(N, K, elem) && !have_gz) return tn_ws_bytes(M, N, K) + pro_ws_bytes(M, N, K);
   size_t pw = 0;
   hgin_prelu_bwd_workspace_size(M, N, &pw);
-  return align_up(pw, 256) + tn_ws_bytes(M, N, K) + (have_gz ? 0 : align_up(elem * (size_t)(M * N), 256));
+  const size_t two_pass = align_up(pw, 256) + tn_ws_bytes(M, N, K) + (have_gz ? 0 : align_up(elem * (size_t)(M * N), 256));
+  const size_t pro = tn_ws_bytes(M, N, K) + wsd_pro_ws_bytes(M, N, K);
+  return two_pass > pro ? two_pass : pro;
 }
 
 template <typename T>
@@ -1523,6 +1766,31 @@ int mlp_bwd_w_entry(const char* what, const T* g_y, int64_t ld_gy, const T* z, i
     TnPro pro{z, ldz, prelu, nullptr, nullptr, 0};
     return gemm_tn_impl<T>(what, g_y, ld_gy, b1, ldb1, k1, b2, ldb2, M, N, K, g_w, ldw, workspace, workspace_bytes,
                            s, &pro, g_bias, g_prelu);
+  }
+  if (g_z && M > 0 && prelu && g_y && z) {   // the weight-stationary dW with the PReLU backward folded in
+    char* ws = static_cast<char*>(workspace);
+    const size_t tw = tn_ws_bytes(M, N, K);
+    const int64_t S = tn_ws_slabs(M, N, K);
+    WsdPro pro{z, ldz, prelu, g_z, ld_gz, reinterpret_cast<float*>(ws + tw), nullptr, nullptr};
+    pro.ps = reinterpret_cast<float*>(ws + tw + align_up(sizeof(float) * (size_t)(N * S), 256));
+    pro.dump = ws + tw + align_up(sizeof(float) * (size_t)(N * S), 256) + align_up(sizeof(float) * (size_t)S, 256);
+    float* slab = reinterpret_cast<float*>(ws);
+    if (const int64_t g = try_wsd_pro<T>(g_y, ld_gy, b1, ldb1, k1, b2, ldb2, M, N, K, slab, S, pro, s)) {
+      const int64_t NK = N * K;
+      const int64_t G = ceil_div(g, kSlabGroup);
+      if (slab_fused_enabled() && G <= kSlabMaxG) {
+        const int64_t n_red = ceil_div(NK, kSlabCols);
+        k_slab_reduce<<<(unsigned)(n_red + N + 1), 256, 0, s>>>(slab, g, NK, g_w, K, ldw, n_red, pro.pcol, pro.ps, g,
+                                                                 g_bias, g_prelu);
+        return check_launch(what);
+      }
+      float* part = reinterpret_cast<float*>(ws + align_up(sizeof(float) * (size_t)(S * NK), 256));
+      dim3 g1((unsigned)ceil_div(ceil_div(NK, 4), 256), (unsigned)G);
+      k_slab_reduce1<<<g1, 256, 0, s>>>(slab, g, NK, part);
+      k_slab_reduce2<<<(unsigned)ceil_div(NK, 256), 256, 0, s>>>(part, G, NK, g_w, K, ldw);
+      k_pro_final<<<(unsigned)(N + 1), 256, 0, s>>>(pro.pcol, pro.ps, g, g, g_bias, g_prelu);
+      return check_launch(what);
+    }
   }
   size_t pw = 0;
   hgin_prelu_bwd_workspace_size(M, N, &pw);

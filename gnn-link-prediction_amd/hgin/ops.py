@@ -403,7 +403,9 @@ def mlp_bwd_w(g_y: Tensor, z: Tensor, prelu: Tensor, b1: Tensor, b2: Optional[Te
     """Backward of prelu([b1 | b2] @ W^T + b) up to the weights: (g_w [N, K] fp32, g_a [1], g_b [N], g_z).
 
     g_z = z > 0 ? g_y : a * g_y is formed inside the weight-gradient GEMM where fused (mlp_bwd_fused) and
-    then returned as None unless ``want_gz``; otherwise (bf16, narrow layers) it is materialised."""
+    then returned as None unless ``want_gz``; otherwise (bf16, narrow layers) it is materialised — by the
+    weight-stationary dW itself where it takes the shape (k_wsd_*<..., prelu_bwd_fused>: g_z formed in its LDS
+    staging and stored, no separate PReLU-backward pass), else by hgin_prelu_bwd_* ahead of the TN GEMM."""
     g_y, b1 = _rowmajor(g_y), _rowmajor(b1)
     if b2 is not None:
         b2 = _rowmajor(b2)
@@ -422,8 +424,9 @@ def mlp_bwd_w(g_y: Tensor, z: Tensor, prelu: Tensor, b1: Tensor, b2: Optional[Te
                                                             ctypes.byref(nbytes)), "gin_mlp_bwd_w_workspace_size")
     ws = _workspace(nbytes.value, dev)
     s = z.element_size()
-    # fused: g_y, z and B read once; otherwise the PReLU-backward pass (g_y, z read, g_z written) + the TN GEMM
-    nb = (s * M * (2 * N + K) if g_z is None else s * M * (3 * N) + s * M * (N + K)) + 4 * N * K
+    # algorithmic: g_y, z and B read once, g_z written when it is returned (the weight-stationary kernels form it in
+    # their staging and store it; elsewhere a separate PReLU-backward pass writes it and the TN GEMM reads it back)
+    nb = s * M * (2 * N + K + (N if g_z is not None else 0)) + 4 * N * K
     _probed("gemm_dw", 2.0 * M * N * K, nb,
             lambda: _lib.call(f"hgin_gin_mlp_bwd_w_{_sfx(z)}", _p(g_y), g_y.stride(0), _p(z), z.stride(0), _p(prelu),
                               _p(b1), b1.stride(0), k1, _p(b2), b2.stride(0) if b2 is not None else 0, M, N, K,

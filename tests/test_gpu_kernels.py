@@ -320,7 +320,8 @@ def test_prelu_bwd_strided_grad():
 @pytest.mark.parametrize("M,N,K1,K2", [(1000, 128, 256, 0), (600, 128, 128, 128), (50000, 128, 128, 128),
                                        (3000, 128, 128, 128),
                                        (20011, 32, 128, 0), (3001, 17, 64, 64), (777, 100, 6, 3), (5, 8, 4, 4),
-                                       (129, 256, 100, 28), (0, 64, 64, 0)])
+                                       (129, 256, 100, 28), (0, 64, 64, 0),
+                                       (20011, 256, 256, 0), (3001, 256, 64, 64), (7, 256, 128, 128)])
 @pytest.mark.parametrize("want_gz", [False, True])
 @pytest.mark.parametrize("strided", [False, True])
 def test_mlp_bwd_fused(M, N, K1, K2, want_gz, strided):
@@ -559,3 +560,36 @@ def test_global_pool_vs_cpu_scatter(F, dtype):
     assert torch.equal(got.isnan(), want.isnan())
     ok = got.isnan() | (got == want)
     assert bool(ok.all()), (~ok).nonzero()[:10]
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("M,N,K1,K2", [(100003, 256, 256, 0), (4099, 256, 128, 0), (33, 256, 256, 0),
+                                       (20000, 128, 128, 128), (1, 128, 256, 0)])
+def test_wsd_prelu_fused_equals_two_pass(dtype, M, N, K1, K2):
+    """The weight-stationary dW with the PReLU backward folded in (k_wsd_*<..., prelu_bwd_fused>, taken whenever g_z
+    is wanted at these shapes): g_z bit-identical to hgin_prelu_bwd_* (the same fp32 arithmetic and rounding), g_w
+    bit-identical to the plain weight-stationary dW on that g_z (same M partition and product order), bias / slope
+    gradients within 1e-5 of a float64 evaluation (fixed-order sums, another grouping)."""
+    from hgin import _lib
+    gen = torch.Generator(device=DEV).manual_seed(M + N + K1)
+    gy = torch.randn(M, N, device=DEV, generator=gen).to(dtype)
+    z = torch.randn(M, N, device=DEV, generator=gen).to(dtype)
+    a = torch.tensor([0.3], device=DEV)
+    b1 = torch.randn(M, K1, device=DEV, generator=gen).to(dtype)
+    b2 = torch.randn(M, K2, device=DEV, generator=gen).to(dtype) if K2 else None
+    with _lib.trace_launches() as tr:
+        g_w, g_a, g_b, g_z = ops.mlp_bwd_w(gy, z, a, b1, b2, want_gz=True)
+    torch.cuda.synchronize()
+    fused = [t for t in tr.kernels if "prelu_bwd_fused" in t and t.startswith("k_wsd")]
+    if dtype == torch.bfloat16 or N == 256:
+        assert fused and not any(t.startswith("k_rows_bwd") for t in tr.kernels), tr.kernels
+    gz2, _, _ = ops.prelu_bwd(gy, z, a)
+    assert torch.equal(g_z, gz2)
+    assert torch.equal(g_w, ops.gemm_tn(gz2, b1, b2))
+    gzd = torch.where(z.double() > 0, gy.double(), gy.double() * 0.3)
+    assert ((g_b.double() - gzd.sum(0)).abs() <= 1e-5 * gzd.abs().sum(0) + 1e-6).all()
+    zr = z.double()
+    ga_ref = (torch.where(zr > 0, torch.zeros_like(zr), zr) * gy.double()).sum()
+    assert abs(float(g_a) - float(ga_ref)) <= 1e-5 * (float((zr * gy.double()).abs().sum()) + 1)
+    again = ops.mlp_bwd_w(gy, z, a, b1, b2, want_gz=True)
+    assert all(torch.equal(p, q) for p, q in zip(again, (g_w, g_a, g_b, g_z)))
