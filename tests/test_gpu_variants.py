@@ -47,6 +47,11 @@ VARIANTS = {
 BITWISE_EQUAL_TO_DEFAULT = ("slab2pass", "agg_nq2", "agg_pipe", "agg_notail", "xcd_off", "nt2_on", "agg_nt_all", "gemm_nt_io",
                             "agg_lds8", "agg_lds16", "wsd_pro_off")
 
+# Scalar / column-sum gradients a variant regroups: the dX kernel's eps-gradient partials (one per tile in k_nt2, one
+# per workgroup in the weight-stationary k_ws_f32) and the bias / PReLU-slope sums (per workgroup in the fused
+# weight-stationary dW, per row block in k_rows_bwd<0>).  Everything else must stay bit-identical.
+REGROUPED = {"nt2_on": (".conv.eps",), "wsd_pro_off": (".mlp.0.bias", ".mlp.1.weight")}
+
 _results = {}
 
 
@@ -75,8 +80,8 @@ def test_variant_bitwise_equal_default(name):
     for case in ref:
         assert ref[case].keys() == got[case].keys()
         for k in ref[case]:
-            if name == "wsd_pro_off" and (k.endswith(".mlp.0.bias") or k.endswith(".mlp.1.weight")):
-                # bias / PReLU-slope gradients: the same fp32 g_z summed in another fixed grouping
+            if any(k.endswith(sfx) for sfx in REGROUPED.get(name, ())):
+                # a gradient that is a fixed-order sum whose grouping the variant changes (not its terms)
                 a, b = ref[case][k].double(), got[case][k].double()
                 assert float((a - b).norm()) <= 1e-6 * float(b.norm()) + 1e-12, (name, case, k)
                 continue
