@@ -212,7 +212,7 @@ void launch_rows_bwd(bool vec, unsigned nblk, int rpb, hipStream_t s, const T* i
   const bool nt = rows_cfg().nt < 0 ? sizeof(T) == 4 : rows_cfg().nt == 1;
   // non-temporal output stores once the output exceeds 512 MiB (HGIN_ROWS_NT_OUT = 0 / 1 forces)
   const bool nt_out = rows_cfg().nt_out < 0 ? M * N * (int64_t)sizeof(T) > (int64_t(512) << 20) : rows_cfg().nt_out == 1;
-  HGIN_TRACE("k_rows_bwd<%d,%s>", MODE, sizeof(T) == 4 ? "f32" : "bf16");
+  HGIN_TRACE("k_rows_bwd<%d,%s,N%d>", MODE, sizeof(T) == 4 ? "f32" : "bf16", N);
   if (vec && nt) {
     if (u4)
       k_rows_bwd<MODE, 4, T, 4, true><<<nblk, 256, 0, s>>>(in0, ld0, in1, ld1, M, N, scalar, out, ldo, part_col, part_s, rpb, nt_out);

@@ -371,7 +371,7 @@ def test_mlp_bwd_fused_cfg3_layer0_shape():
     torch.cuda.synchronize()
     assert g_z is None
     assert "k_gemm_tn_partial<prelu_bwd_fused,split,N256,K512>" in tr.kernels, tr.kernels
-    assert "k_rows_bwd<0,f32>" not in tr.kernels
+    assert not any(t.startswith("k_rows_bwd<0") for t in tr.kernels)
     zr, gyr = z.double(), gy.double()
     ga_ref = float((torch.where(zr > 0, torch.zeros_like(zr), zr) * gyr).sum())
     assert abs(float(g_a) - ga_ref) <= 1e-5 * (float((zr * gyr).abs().sum()) + 1)

@@ -144,7 +144,8 @@ def test_forward_backward_step_vs_reference(case):
     if case == "w256_L3":   # the headline's kernels ran inside this parity check
         missing = [k for k in W256_KERNELS if not any(re.fullmatch(k, t) for t in tr.kernels)]
         assert not missing, (missing, sorted(set(tr.kernels)))
-        assert not any(t.startswith("k_rows_bwd<0") for t in tr.kernels), sorted(set(tr.kernels))
+        # no separate PReLU-backward pass at the GIN width (the narrower readout layers still run one)
+        assert "k_rows_bwd<0,f32,N256>" not in tr.kernels, sorted(set(tr.kernels))
     no_grad = set(fx["meta"]["no_grad_params"])
     g_scale = max(float(fx["grad." + n].double().norm()) for n, _ in model.named_parameters() if n not in no_grad)
     grads = {}
