@@ -1125,9 +1125,10 @@ struct WsdF32Cfg {
   static constexpr int LDS = SLOT * NST + PLANES;
   static constexpr int PA = A_BYTES / 1024 / 8, PB = B_BYTES / 1024 / 8;
   static constexpr int P = PA + (PRO ? PA : 0) + PB;
-  static constexpr int S = PRO ? 2 : 0;                      // g_z stores per wave per block (2 x 16 B per thread)
+  static constexpr int S = PRO ? 2 : 0;                      // g_z stores per A-splitting wave per block (2 x 16 B)
   static_assert(TK >= 1 && A_BYTES % 8192 == 0 && B_BYTES % 8192 == 0 && LDS <= 147456, "shape");
-  static_assert(!PRO || BM * N / 8 == NT, "PRO: one A group per thread");
+  static_assert(!PRO || BM * N / 8 <= NT, "PRO: at most one A group per thread");
+  static constexpr int CA = BM * N / 8;                      // A groups (threads t < CA split one each)
 };
 
 template <int N, int K, bool PRO>
@@ -1212,8 +1213,14 @@ __global__ __launch_bounds__(512, 1) void k_wsd_f32(const float* __restrict__ A,
   for (int i = 0; i < NST - 1; ++i)
     if (i < my) issue(i);
 
+  // (N = 128: only waves 0-3 split A groups and store g_z; each wave waits on its own count)
+  const bool stores = PRO && wave * 64 < C::CA;
   for (int64_t i = 0; i < my; ++i) {
-    if (i + NST - 2 < my) wsd_wait<NST, C::P, C::S>(i); else wait_vm<0>();
+    if (i + NST - 2 < my) {
+      if (stores) wsd_wait<NST, C::P, C::S>(i); else wsd_wait<NST, C::P, 0>(i);
+    } else {
+      wait_vm<0>();
+    }
     __builtin_amdgcn_s_barrier();   // block i landed for every wave; slot i-1 and the plane images are free
     asm volatile("" ::: "memory");
     if (i + NST - 1 < my) issue(i + NST - 1);
@@ -1426,16 +1433,48 @@ int64_t wsd_cols(const T* a, int64_t lda, const T* b1, int64_t ldb1, int64_t k1,
   return launch_wsd<NV, KV>(a, lda, p1, l1, p2, l2, kk1, M, slab + c0, ld_slab, grid, s);
 }
 
+// Column passes of the PReLU-fused dW: [0, KV) with the fold (forms + stores g_z, the partial sums), then for K = 512
+// [256, 512) as the plain kernel on the stored g_z — the same two passes, slabs and product order as the unfused
+// K = 512 path, so g_w stays bit-identical to it.
+template <typename T>
+int64_t wsd_pro_passes(const T* gy, int64_t ldgy, const T* b1, int64_t ldb1, int64_t k1, const T* b2, int64_t ldb2,
+                       int64_t M, int64_t N, int64_t K, float* slab, int64_t grid, const WsdPro& pro, hipStream_t s) {
+  const int64_t KV = K == 512 ? 256 : K;
+  auto srcs = [&](int64_t c0, const T*& p1, int64_t& l1, const T*& p2, int64_t& l2, int64_t& kk1) {
+    kk1 = k1 > c0 ? (k1 - c0 < KV ? k1 - c0 : KV) : 0;
+    p1 = kk1 > 0 ? b1 + c0 : b2;
+    l1 = kk1 > 0 ? ldb1 : ldb2;
+    p2 = kk1 < KV ? b2 + (c0 + kk1 - k1) : p1;
+    l2 = kk1 < KV ? ldb2 : l1;
+  };
+  const T* p1;
+  const T* p2;
+  int64_t l1, l2, kk1;
+  srcs(0, p1, l1, p2, l2, kk1);
+  int64_t g;
+#define HGIN_PRO_PASS(NV, KVV) g = launch_wsd<NV, KVV, true>(gy, ldgy, p1, l1, p2, l2, kk1, M, slab, K, grid, s, pro);
+  if (N == 256 && KV == 256) { HGIN_PRO_PASS(256, 256) }
+  else if (N == 256) { HGIN_PRO_PASS(256, 128) }
+  else if (KV == 256) { HGIN_PRO_PASS(128, 256) }
+  else { HGIN_PRO_PASS(128, 128) }
+#undef HGIN_PRO_PASS
+  if (!g || K != 512) return g;
+  srcs(256, p1, l1, p2, l2, kk1);
+  const T* gz = static_cast<const T*>(pro.gz);
+  if (N == 256) return launch_wsd<256, 256>(gz, pro.ldgz, p1, l1, p2, l2, kk1, M, slab + 256, K, grid, s);
+  return launch_wsd<128, 256>(gz, pro.ldgz, p1, l1, p2, l2, kk1, M, slab + 256, K, grid, s);
+}
+
 // The PReLU-backward-fused weight-stationary dW (bf16, single column pass: N in {128, 256}, K in {128, 256}):
 // g_w slabs + g_z + bias / slope partials in one launch.  Returns the slab count, or 0 when it does not apply.
 template <typename T>
 int64_t try_wsd_pro(const T* gy, int64_t ldgy, const T* b1, int64_t ldb1, int64_t k1, const T* b2, int64_t ldb2,
                     int64_t M, int64_t N, int64_t K, float* slab, int64_t max_slabs, const WsdPro& pro,
                     hipStream_t s) {
-  if constexpr (sizeof(T) == 4) {   // fp32 (split mode): N = 256, K in {128, 256}
+  if constexpr (sizeof(T) == 4) {   // fp32 (split mode): N in {128, 256}, K in {128, 256, 512}
     constexpr int64_t vw = 4;
-    if (!wsd_enabled() || !wsd_pro_enabled() || !gemm_split_enabled() || M < 1 || N != 256 ||
-        (K != 128 && K != 256) || k1 % vw)
+    if (!wsd_enabled() || !wsd_pro_enabled() || !gemm_split_enabled() || M < 1 || (N != 128 && N != 256) ||
+        (K != 128 && K != 256 && K != 512) || k1 % vw)
       return 0;
     auto ok = [](const void* p, int64_t ld) { return aligned16(p) && ld % vw == 0 && ld < (int64_t(1) << 24); };
     if (!ok(gy, ldgy) || !ok(pro.z, pro.ldz) || !ok(pro.gz, pro.ldgz) || (k1 > 0 && !ok(b1, ldb1)) ||
@@ -1445,16 +1484,11 @@ int64_t try_wsd_pro(const T* gy, int64_t ldgy, const T* b1, int64_t ldb1, int64_
     const int64_t nblk = ceil_div(M, (int64_t)16);
     if (grid > nblk) grid = nblk;
     if (grid > max_slabs) grid = max_slabs;
-    const float* p1 = k1 > 0 ? b1 : b2;
-    const int64_t l1 = k1 > 0 ? ldb1 : ldb2;
-    const float* p2 = k1 < K ? b2 : p1;
-    const int64_t l2 = k1 < K ? ldb2 : l1;
-    if (K == 256) return launch_wsd<256, 256, true>(gy, ldgy, p1, l1, p2, l2, k1, M, slab, K, grid, s, pro);
-    return launch_wsd<256, 128, true>(gy, ldgy, p1, l1, p2, l2, k1, M, slab, K, grid, s, pro);
+    return wsd_pro_passes<T>(gy, ldgy, b1, ldb1, k1, b2, ldb2, M, N, K, slab, grid, pro, s);
   } else {
     constexpr int64_t vw = 8;
-    if (!wsd_enabled() || !wsd_pro_enabled() || M < 1 || (N != 128 && N != 256) || (K != 128 && K != 256) ||
-        k1 % vw)
+    if (!wsd_enabled() || !wsd_pro_enabled() || M < 1 || (N != 128 && N != 256) ||
+        (K != 128 && K != 256 && K != 512) || k1 % vw)
       return 0;
     auto ok = [](const void* p, int64_t ld) { return aligned16(p) && ld % vw == 0 && ld < (int64_t(1) << 24); };
     if (!ok(gy, ldgy) || !ok(pro.z, pro.ldz) || !ok(pro.gz, pro.ldgz) || (k1 > 0 && !ok(b1, ldb1)) ||
@@ -1464,16 +1498,7 @@ int64_t try_wsd_pro(const T* gy, int64_t ldgy, const T* b1, int64_t ldb1, int64_
     const int64_t nblk = ceil_div(M, (int64_t)32);
     if (grid > nblk) grid = nblk;
     if (grid > max_slabs) grid = max_slabs;
-    const uint16_t* p1 = k1 > 0 ? b1 : b2;
-    const int64_t l1 = k1 > 0 ? ldb1 : ldb2;
-    const uint16_t* p2 = k1 < K ? b2 : p1;
-    const int64_t l2 = k1 < K ? ldb2 : l1;
-#define HGIN_WSD_PRO(NV, KV) return launch_wsd<NV, KV, true>(gy, ldgy, p1, l1, p2, l2, k1, M, slab, K, grid, s, pro);
-    if (N == 256 && K == 256) HGIN_WSD_PRO(256, 256)
-    if (N == 256 && K == 128) HGIN_WSD_PRO(256, 128)
-    if (N == 128 && K == 256) HGIN_WSD_PRO(128, 256)
-    HGIN_WSD_PRO(128, 128)
-#undef HGIN_WSD_PRO
+    return wsd_pro_passes<T>(gy, ldgy, b1, ldb1, k1, b2, ldb2, M, N, K, slab, grid, pro, s);
   }
 }
 
