@@ -56,7 +56,8 @@ __device__ __forceinline__ TnWork tn_work(const TnGrid& g) {
 // g_z = z > 0 ? g_y : slope * g_y from the g_y / z streams (the g_z stream of a separate PReLU-backward pass
 // is never written and re-read), and the workgroups of the first K tile also produce the bias / slope
 // gradients as per-split partials (column sums of g_z; sum of z * g_y over z <= 0), summed afterwards in a
-// fixed order.  (g_z is never written: the dX GEMM applies the same prologue to its A operand.)  Reference: autograd of PReLU + Linear bias
+// fixed order.  gz != NULL: the workgroups of the first K tile also store the g_z they formed (the dX GEMM's
+// operand, when the layer needs an input gradient).  Reference: autograd of PReLU + Linear bias
 // (models.py:237-238) reached from train.py:43.
 struct TnPro {
   const void* z;        // [M, N] pre-activation, row stride ldz (A's element type)
@@ -65,6 +66,8 @@ struct TnPro {
   float* pcol;          // [N][S] column-sum partials
   float* ps;            // [N tiles][S] slope-sum partials
   int64_t S;
+  float* gz = nullptr;  // optional g_z output [M, N] (fp32), row stride ldgz
+  int64_t ldgz = 0;
 };
 
 // Fixed-order combine of the per-thread prologue partials of one workgroup: 8 row groups of csum per
@@ -275,9 +278,29 @@ __global__ __launch_bounds__(256, (kPro && !kLateZ) ? 2 : 3) void k_gemm_tn_part
     }
   };
   // the 4 x 4 block regrouped: column c4 + t gets (row r4 .. r4 + 3) as one float4
+  const bool store_gz = kPro && pro.gz != nullptr && work.k0 == 0 && stage_a;   // workgroup / wave-uniform
   auto store_stage = [&]() {
     if constexpr (kPro && kLateZ) load_z(m_ld);
     if constexpr (kPro) prologue();
+    if constexpr (kPro) {
+      if (store_gz) {   // rows m_ld + r4a + j, columns n0 + c4a .. + 3 (rows past me were zeroed: skipped)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int64_t gm = m_ld + r4a + j;
+          const int64_t gn = n0 + c4a;
+          if (gm >= me) continue;
+          float* dst = pro.gz + gm * pro.ldgz + gn;
+          if (kClean) {
+            *reinterpret_cast<float4*>(dst) = va[j];
+          } else {
+            const float g[4] = {va[j].x, va[j].y, va[j].z, va[j].w};
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+              if (gn + q < N) dst[q] = g[q];
+          }
+        }
+      }
+    }
     if constexpr (kSplit) {
       auto put = [&](uint32_t* img, int col, int r, const float4 v) {
         uint2 o[3];
@@ -1702,7 +1725,8 @@ int gemm_tn_impl(const char* what, const T* a, int64_t lda, const T* b1, int64_t
     // loop, 3-5 % faster than prefetch at 2 waves)
     const bool clean = vec && N % tile_n == 0 && K % 128 == 0 && k1 % 128 == 0;
     const bool split = gemm_split_enabled();
-    HGIN_TRACE("k_gemm_tn_partial<%s,%s,N%lld,K%lld>", pro_in ? "prelu_bwd_fused" : "plain", split ? "split" : "mfma32",
+    HGIN_TRACE("k_gemm_tn_partial<%s,%s,N%lld,K%lld>",
+               pro_in ? (pro_in->gz ? "prelu_bwd_fused+gz" : "prelu_bwd_fused") : "plain", split ? "split" : "mfma32",
                (long long)N, (long long)K);
 #define HGIN_TN_LAUNCH(CLEAN, TNR, SPLIT, PRO, LATE)                                                          \
   k_gemm_tn_partial<CLEAN, TNR, SPLIT, PRO, LATE><<<grid, 256, 0, s>>>(a, lda, b1, ldb1, b2, ldb2, k1, M, N, K, \
@@ -1768,7 +1792,9 @@ size_t mlp_bwd_w_ws_bytes(int64_t M, int64_t N, int64_t K, size_t elem, bool hav
   hgin_prelu_bwd_workspace_size(M, N, &pw);
   const size_t two_pass = align_up(pw, 256) + tn_ws_bytes(M, N, K) + (have_gz ? 0 : align_up(elem * (size_t)(M * N), 256));
   const size_t pro = tn_ws_bytes(M, N, K) + wsd_pro_ws_bytes(M, N, K);
-  return two_pass > pro ? two_pass : pro;
+  const size_t tiled = tn_ws_bytes(M, N, K) + pro_ws_bytes(M, N, K);   // the tiled prologue storing g_z
+  const size_t m = two_pass > pro ? two_pass : pro;
+  return m > tiled ? m : tiled;
 }
 
 template <typename T>
@@ -1815,6 +1841,16 @@ int mlp_bwd_w_entry(const char* what, const T* g_y, int64_t ld_gy, const T* z, i
       k_slab_reduce2<<<(unsigned)ceil_div(NK, 256), 256, 0, s>>>(part, G, NK, g_w, K, ldw);
       k_pro_final<<<(unsigned)(N + 1), 256, 0, s>>>(pro.pcol, pro.ps, g, g, g_bias, g_prelu);
       return check_launch(what);
+    }
+    // fp32 shapes the weight-stationary kernels do not take (e.g. the readout's Linear(128, 32)): the tiled dW with
+    // the prologue, its first-K-tile workgroups storing the g_z they form (no separate PReLU-backward pass)
+    if (mlp_bwd_w_fused(N, K, sizeof(T)) && ld_gz % 4 == 0) {
+      TnPro pro2{z, ldz, prelu, nullptr, nullptr, 0};
+      pro2.gz = reinterpret_cast<float*>(g_z);
+      pro2.ldgz = ld_gz;
+      if (tn_ws_bytes(M, N, K) + pro_ws_bytes(M, N, K) <= workspace_bytes)
+        return gemm_tn_impl<T>(what, g_y, ld_gy, b1, ldb1, k1, b2, ldb2, M, N, K, g_w, ldw, workspace,
+                               workspace_bytes, s, &pro2, g_bias, g_prelu);
     }
   }
   size_t pw = 0;

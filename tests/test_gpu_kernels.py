@@ -564,12 +564,15 @@ def test_global_pool_vs_cpu_scatter(F, dtype):
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("M,N,K1,K2", [(100003, 256, 256, 0), (4099, 256, 128, 0), (33, 256, 256, 0),
-                                       (20000, 128, 128, 128), (1, 128, 256, 0)])
+                                       (20000, 128, 128, 128), (1, 128, 256, 0),
+                                       (30011, 256, 256, 256), (50000, 128, 256, 256), (17, 128, 384, 128),
+                                       (60001, 32, 128, 0), (3001, 64, 64, 64)])
 def test_wsd_prelu_fused_equals_two_pass(dtype, M, N, K1, K2):
     """The weight-stationary dW with the PReLU backward folded in (k_wsd_*<..., prelu_bwd_fused>, taken whenever g_z
-    is wanted at these shapes): g_z bit-identical to hgin_prelu_bwd_* (the same fp32 arithmetic and rounding), g_w
-    bit-identical to the plain weight-stationary dW on that g_z (same M partition and product order), bias / slope
-    gradients within 1e-5 of a float64 evaluation (fixed-order sums, another grouping)."""
+    is wanted at these shapes; K = 512 = the fused pass over columns [0, 256) + a plain pass over [256, 512) on the
+    stored g_z): g_z bit-identical to hgin_prelu_bwd_* (the same fp32 arithmetic and rounding), g_w bit-identical to
+    the plain weight-stationary dW on that g_z (same M partition, passes and product order), bias / slope gradients
+    within 1e-5 of a float64 evaluation (fixed-order sums, another grouping)."""
     from hgin import _lib
     gen = torch.Generator(device=DEV).manual_seed(M + N + K1)
     gy = torch.randn(M, N, device=DEV, generator=gen).to(dtype)
@@ -580,12 +583,18 @@ def test_wsd_prelu_fused_equals_two_pass(dtype, M, N, K1, K2):
     with _lib.trace_launches() as tr:
         g_w, g_a, g_b, g_z = ops.mlp_bwd_w(gy, z, a, b1, b2, want_gz=True)
     torch.cuda.synchronize()
-    fused = [t for t in tr.kernels if "prelu_bwd_fused" in t and t.startswith("k_wsd")]
-    if dtype == torch.bfloat16 or N == 256:
+    fused = [t for t in tr.kernels if "prelu_bwd_fused" in t]
+    if N in (128, 256) or dtype == torch.float32:   # bf16 narrow layers keep the separate pass
         assert fused and not any(t.startswith("k_rows_bwd") for t in tr.kernels), tr.kernels
     gz2, _, _ = ops.prelu_bwd(gy, z, a)
     assert torch.equal(g_z, gz2)
-    assert torch.equal(g_w, ops.gemm_tn(gz2, b1, b2))
+    if N in (128, 256):   # the weight-stationary form: the same kernel / partition as the plain dW on g_z
+        assert torch.equal(g_w, ops.gemm_tn(gz2, b1, b2))
+    else:                 # the tiled fused kernel: its own split of M; against float64
+        b = b1 if b2 is None else torch.cat((b1, b2), 1)
+        gzd = gz2.double()
+        ref_w = gzd.t() @ b.double()
+        assert ((g_w.double() - ref_w).abs() <= 1e-5 * (gzd.abs().t() @ b.double().abs() + 1)).all()
     gzd = torch.where(z.double() > 0, gy.double(), gy.double() * 0.3)
     assert ((g_b.double() - gzd.sum(0)).abs() <= 1e-5 * gzd.abs().sum(0) + 1e-6).all()
     zr = z.double()
