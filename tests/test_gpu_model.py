@@ -59,7 +59,7 @@ W256_KERNELS = (r"k_gemm_nt<EPI1,\d+x\d+,split,N256,K512>",                # fir
                 r"k_ws_f32<256,256,EPI1>",                                  # layers 1-2 forward
                 r"k_gemm_tn_partial<prelu_bwd_fused,split,N256,K512>",      # first layer dW + PReLU / bias grads
                 r"k_wsd_f32<256,256,prelu_bwd_fused>",                      # layers 1-2 dW + PReLU bwd (g_z out)
-                r"k_ws_f32<256,256,EPI4>")                                  # layers 1-2 dX + self-term backward                              # PReLU backward where dX needs g_z
+                r"k_ws_f32<256,256,EPI4>")                                  # layers 1-2 dX + self-term backward
 
 
 @pytest.mark.parametrize("case", CASES)
@@ -144,7 +144,7 @@ def test_forward_backward_step_vs_reference(case):
     if case == "w256_L3":   # the headline's kernels ran inside this parity check
         missing = [k for k in W256_KERNELS if not any(re.fullmatch(k, t) for t in tr.kernels)]
         assert not missing, (missing, sorted(set(tr.kernels)))
-        # no separate PReLU-backward pass at the GIN width (the narrower readout layers still run one)
+        # no separate PReLU-backward pass at the GIN width (the fp32 step folds it into every dW GEMM)
         assert "k_rows_bwd<0,f32,N256>" not in tr.kernels, sorted(set(tr.kernels))
     no_grad = set(fx["meta"]["no_grad_params"])
     g_scale = max(float(fx["grad." + n].double().norm()) for n, _ in model.named_parameters() if n not in no_grad)
