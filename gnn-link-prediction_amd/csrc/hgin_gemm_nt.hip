@@ -595,6 +595,331 @@ int launch_nt(const Src2& a, const Src2& b, int64_t M, int64_t N, int64_t K, con
   return check_launch(what);
 }
 
+// ---- "h2" mode (HGIN_F32_GEMM=h2): fp32 operands as two scaled fp16 terms, three products ------------------
+// Each fp32 operand row is scaled by a power of two 2^e (exact) and written as h1 = fp16(a 2^e), h2 = fp16(a 2^e -
+// h1) (RNE; the residual is exact in fp32), so a 2^e = h1 + h2 to within 2^-22 |a 2^e|; a product is formed from
+// the three v_mfma_f32_32x32x16_f16 terms h2 g1, h1 g2, h1 g1 (the dropped h2 g2 is below 2^-22 |ab|) with fp32
+// accumulation, and the result is scaled back exactly in the epilogue — the two-term split of 3xTF32 (TF32 and fp16
+// carry the same 11-bit significand), half the matrix-core work and two thirds of the LDS image of the six-product
+// bf16 split.  fp16's narrow exponent range is what the scaling is for:
+//   * B (the weight [N, K]): one exponent per row n, from the row's max (k_h2_planes, once per call): the scaled
+//     row max lies in [2^13, 2^14).
+//   * A rows: the tile's K loop discovers them — a row's exponent is set at its first nonzero K-tile (scaled max
+//     in [2^7, 2^8)) and lowered only when a later K-tile's max could reach 2^15 (fp16 max 65504); the row's
+//     accumulators are then scaled by the same exact power of two before the next products land.  Elements far
+//     below their row's max lose low bits only below 2^-24 of the scaled unit (2^-32 of the row max).
+// Results differ from the six-product split by rounding only (both are within the fp32-evaluation bound of an
+// exact product; tests/test_gpu_kernels.py::test_h2_gemm_*).
+using f16x8 = __attribute__((ext_vector_type(8))) _Float16;
+using f16x2v = __attribute__((ext_vector_type(2))) _Float16;
+constexpr int kH2RowWords = 32;       // LDS row: 2 planes x 32 fp16 of one K-tile = 8 16-B chunks
+constexpr int kH2Unset = -100000;     // row exponent before the row's first nonzero K-tile
+
+// chunk c of plane p of row r at slot (4p + c) ^ swz(r): a ds_read_b128 lane group (16 rows, one (p, c)) covers
+// 2 row parities x 8 swizzles = 16 distinct slots; the staging stores (4 rows x 8 lanes x 8 B per 32 lanes)
+// cover 4 disjoint 16-bank blocks (swz bit 2 follows row bit 1)
+__device__ __forceinline__ int h2_swz(int r) { return (((r >> 1) & 1) << 2) | ((r >> 2) & 3); }
+__device__ __forceinline__ int h2_word(int r, int p, int c) { return ((p * 4 + c) ^ h2_swz(r)) << 2; }
+
+__device__ __forceinline__ uint32_t cvt_pk_f16(float lo, float hi) {
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2_t{lo, hi}, f16x2v));
+}
+__device__ __forceinline__ void h2_split2(float x0, float x1, uint32_t& hi, uint32_t& lo) {
+  hi = cvt_pk_f16(x0, x1);
+  const f16x2v h = __builtin_bit_cast(f16x2v, hi);
+  lo = cvt_pk_f16(x0 - (float)h.x, x1 - (float)h.y);
+}
+__device__ __forceinline__ uint32_t absbits(float x) { return __float_as_uint(x) & 0x7fffffffu; }
+// max over the 8 consecutive lanes of a staging row (quad swaps, then the mirrored half-row)
+__device__ __forceinline__ uint32_t umax8(uint32_t v) {
+  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false));
+  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, false));
+  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x141, 0xF, 0xF, false));
+  return v;
+}
+// A row exponent after a K-tile whose |max| has the bits mbits; d = the accumulator rescale (0 = none)
+__device__ __forceinline__ int h2_row_exp(uint32_t mbits, int cur, int& d) {
+  d = 0;
+  if (mbits == 0) return cur;
+  int be = (int)(mbits >> 23);
+  be = be < 1 ? 1 : (be > 254 ? 254 : be);
+  if (cur == kH2Unset) return 134 - be;                 // max 2^e in [2^7, 2^8)
+  if (be + cur > 141) {                                 // max 2^e could reach 2^15
+    d = 134 - be - cur;
+    return 134 - be;
+  }
+  return cur;
+}
+
+// B planes: [N][K / 32][2][32] fp16 (hi, lo of B[n, k] 2^f[n]), then int32 f[N] at byte N * K * 4.
+size_t h2_planes_bytes(int64_t N, int64_t K) { return (size_t)N * (size_t)K * 4 + align_up((size_t)N * 4, 256); }
+
+__global__ __launch_bounds__(64) void k_h2_planes(const float* __restrict__ b, int64_t ldb, int64_t K,
+                                                  uint16_t* __restrict__ out, int* __restrict__ fexp) {
+  const int64_t n = blockIdx.x;
+  const int lane = threadIdx.x;
+  const float* row = b + n * ldb;
+  uint32_t m = 0;
+  for (int64_t k = lane; k < K; k += 64) m = max(m, absbits(row[k]));
+  for (int off = 32; off > 0; off >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, off));
+  int f = 0;
+  if (m) {
+    int be = (int)(m >> 23);
+    be = be < 1 ? 1 : (be > 254 ? 254 : be);
+    f = 140 - be;                                       // row max 2^f in [2^13, 2^14)
+  }
+  if (lane == 0) fexp[n] = f;
+  uint16_t* o = out + n * K * 2;
+  for (int64_t k = 2 * lane; k < K; k += 128) {
+    uint32_t hi, lo;
+    h2_split2(__builtin_ldexpf(row[k], f), __builtin_ldexpf(row[k + 1], f), hi, lo);
+    const int64_t base = (k / 32) * 64 + (k % 32);
+    *reinterpret_cast<uint32_t*>(o + base) = hi;
+    *reinterpret_cast<uint32_t*>(o + base + 32) = lo;
+  }
+}
+
+// The clean-tile NT GEMM of k_gemm_nt in h2 mode (same tiling, epilogue and XCD order; A from Src2 with the eps2
+// self term; B from k_h2_planes).  Requirements (h2_eligible): K and k1 multiples of 32, 16-B aligned A rows.
+template <int EPI, int TN, int WNv, int OCC>
+__global__ __launch_bounds__(256, OCC) void k_gemm_nt_h2(Src2 A, const uint16_t* __restrict__ Bp,
+                                                      const int* __restrict__ bexp, int64_t M, int64_t N, int64_t K,
+                                                      const float* __restrict__ bias, const float* __restrict__ prelu,
+                                                      const float* __restrict__ accum, float* __restrict__ Z,
+                                                      float* __restrict__ Y, int64_t ldc, bool vec_out, int64_t n_tiles,
+                                                      bool xcd, CombEpi ce) {
+  constexpr int NT = 256;
+  constexpr int WN = WNv;
+  constexpr int WM = 4 / WN;
+  constexpr int BM = WM * 64;
+  constexpr int BN = WN * TN * 32;
+  constexpr int WCOLS = TN * 32;
+  constexpr int kStageW = (BM + BN) * kH2RowWords;
+  constexpr int kEpiW = 4 * 32 * (WCOLS + 4);
+  __shared__ __attribute__((aligned(16))) float smem[kStageW > kEpiW ? kStageW : kEpiW];
+  __shared__ __attribute__((aligned(16))) int row_e[BM];
+  __shared__ __attribute__((aligned(16))) int row_d[BM];
+  __shared__ int resc;
+  uint32_t* Ash = reinterpret_cast<uint32_t*>(smem);
+  uint32_t* Bsh = Ash + BM * kH2RowWords;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wm = wave / WN;
+  const int wn = wave % WN;
+  const int li = lane & 31;
+  const int lh = lane >> 5;
+  const int qd = tid & 7;
+  const int64_t n_tiles_n = (N + BN - 1) / BN;
+  const int64_t q = xcd ? xcd_logical(blockIdx.x, gridDim.x) : (int64_t)blockIdx.x;
+  if (q >= n_tiles) return;
+  const int64_t m0 = (q / n_tiles_n) * BM;
+  const int64_t n0 = (q % n_tiles_n) * BN;
+  if (tid < BM) row_e[tid] = kH2Unset;
+  if (tid == 0) resc = -1;
+
+  f32x16 acc[2][TN];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < TN; ++b)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[a][b][e] = 0.0f;
+
+  float4 ra[BM / 32];
+  uint4 rb[BN / 32];
+  const float sc2 = self_scale(A.eps2);
+  bool scale_a = false;
+  auto load_a = [&](int64_t k0) {
+    load_tile<true, BM, NT>(ra, A, m0, M, k0, K, tid, sc2);
+    scale_a = A.eps2 != nullptr && k0 >= A.k1;
+  };
+  auto load_b = [&](int64_t k0) {
+#pragma unroll
+    for (int i = 0; i < BN / 32; ++i) {
+      int64_t n = n0 + (tid >> 3) + 32 * i;
+      n = n < N ? n : N - 1;
+      rb[i] = *reinterpret_cast<const uint4*>(Bp + n * K * 2 + (k0 / 32) * 64 + qd * 8);
+    }
+  };
+  auto stage = [&](int tile) {
+    if (scale_a) scale_tile<BM, NT>(ra, sc2);
+#pragma unroll
+    for (int i = 0; i < BM / 32; ++i) {
+      const int rr = (tid >> 3) + 32 * i;
+      const float4 v = ra[i];
+      const uint32_t mb = umax8(max(max(absbits(v.x), absbits(v.y)), max(absbits(v.z), absbits(v.w))));
+      const int cur = row_e[rr];
+      int d;
+      const int e = h2_row_exp(mb, cur, d);
+      if (qd == 0) {
+        row_e[rr] = e;
+        row_d[rr] = d;
+      }
+      if (d != 0) resc = tile;
+      const int es = e == kH2Unset ? 0 : e;
+      uint2 hi, lo;
+      h2_split2(__builtin_ldexpf(v.x, es), __builtin_ldexpf(v.y, es), hi.x, lo.x);
+      h2_split2(__builtin_ldexpf(v.z, es), __builtin_ldexpf(v.w, es), hi.y, lo.y);
+      uint32_t* row = Ash + rr * kH2RowWords + (qd & 1) * 2;
+      *reinterpret_cast<uint2*>(row + h2_word(rr, 0, qd >> 1)) = hi;
+      *reinterpret_cast<uint2*>(row + h2_word(rr, 1, qd >> 1)) = lo;
+    }
+#pragma unroll
+    for (int i = 0; i < BN / 32; ++i) {
+      const int rr = (tid >> 3) + 32 * i;
+      *reinterpret_cast<uint4*>(Bsh + rr * kH2RowWords + h2_word(rr, qd >> 2, qd & 3)) = rb[i];
+    }
+  };
+  load_a(0);
+  load_b(0);
+  __syncthreads();   // row_e / resc initialised
+  stage(0);
+  __syncthreads();
+  for (int64_t k0 = 0; k0 < K; k0 += kBK) {
+    const int tile = (int)(k0 / kBK);
+    const bool more = k0 + kBK < K;
+    if (resc == tile) {   // some row's exponent was lowered for this K-tile: rescale its accumulators (rare)
+#pragma unroll
+      for (int tm = 0; tm < 2; ++tm)
+#pragma unroll
+        for (int e4 = 0; e4 < 4; ++e4) {
+          const int4 d4 = *reinterpret_cast<const int4*>(row_d + wm * 64 + tm * 32 + 8 * e4 + 4 * lh);
+          const int dd[4] = {d4.x, d4.y, d4.z, d4.w};
+#pragma unroll
+          for (int tn = 0; tn < TN; ++tn)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) acc[tm][tn][4 * e4 + j] = __builtin_ldexpf(acc[tm][tn][4 * e4 + j], dd[j]);
+        }
+    }
+    if (more) {
+      load_a(k0 + kBK);
+      load_b(k0 + kBK);
+    }
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb) {
+      f16x8 fa[2][2], fb[TN][2];
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        const int r = wm * 64 + t * 32 + li;
+#pragma unroll
+        for (int p = 0; p < 2; ++p)
+          fa[t][p] = *reinterpret_cast<const f16x8*>(Ash + r * kH2RowWords + h2_word(r, p, kb * 2 + lh));
+      }
+#pragma unroll
+      for (int t = 0; t < TN; ++t) {
+        const int r = wn * WCOLS + t * 32 + li;
+#pragma unroll
+        for (int p = 0; p < 2; ++p)
+          fb[t][p] = *reinterpret_cast<const f16x8*>(Bsh + r * kH2RowWords + h2_word(r, p, kb * 2 + lh));
+      }
+#pragma unroll
+      for (int tm = 0; tm < 2; ++tm)
+#pragma unroll
+        for (int tn = 0; tn < TN; ++tn) {   // smallest terms first
+          acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fa[tm][1], fb[tn][0], acc[tm][tn], 0, 0, 0);
+          acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fa[tm][0], fb[tn][1], acc[tm][tn], 0, 0, 0);
+          acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fa[tm][0], fb[tn][0], acc[tm][tn], 0, 0, 0);
+        }
+    }
+    __builtin_amdgcn_s_setprio(0);
+    if (more) {
+      __syncthreads();
+      stage(tile + 1);
+      __syncthreads();
+    }
+  }
+  // scale back: C = acc 2^-(e_row + f_col), exact
+  int fc[TN];
+#pragma unroll
+  for (int tn = 0; tn < TN; ++tn) {
+    const int64_t col = n0 + wn * WCOLS + tn * 32 + li;
+    fc[tn] = col < N ? bexp[col] : 0;
+  }
+#pragma unroll
+  for (int tm = 0; tm < 2; ++tm)
+#pragma unroll
+    for (int e4 = 0; e4 < 4; ++e4) {
+      const int4 r4 = *reinterpret_cast<const int4*>(row_e + wm * 64 + tm * 32 + 8 * e4 + 4 * lh);
+      const int er[4] = {r4.x == kH2Unset ? 0 : r4.x, r4.y == kH2Unset ? 0 : r4.y, r4.z == kH2Unset ? 0 : r4.z,
+                         r4.w == kH2Unset ? 0 : r4.w};
+#pragma unroll
+      for (int tn = 0; tn < TN; ++tn)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[tm][tn][4 * e4 + j] = __builtin_ldexpf(acc[tm][tn][4 * e4 + j], -(er[j] + fc[tn]));
+    }
+  float ep = 0.0f;
+  epilogue<EPI, TN, float>(acc, smem, wave, wm, wn, lane, li, lh, m0, n0, M, N, bias, prelu, accum, Z, Y, ldc,
+                           vec_out, ce, &ep);
+  if constexpr (EPI == 4) tile_partial(smem, ep, ce.part, q);
+}
+
+// occupancy bound of k_gemm_nt_h2 (HGIN_H2_OCC = 2 / 3 waves per SIMD; A/B)
+int h2_occ() {
+  static const int v = [] {
+    const char* e = getenv("HGIN_H2_OCC");
+    return e ? atoi(e) : 2;
+  }();
+  return v;
+}
+
+bool h2_eligible(const float* a1, int64_t lda1, int64_t k1, const float* a2, int64_t lda2, const void* planes,
+                 int64_t K) {
+  if (!planes || !gemm_h2_enabled()) return false;
+  if (K % kBK || k1 % kBK) return false;
+  if (k1 > 0 && (!aligned16(a1) || lda1 % 4)) return false;
+  if (k1 < K && (!aligned16(a2) || lda2 % 4)) return false;
+  return true;
+}
+
+template <int EPI>
+int launch_nt_h2(const Src2& a, const void* planes, int64_t M, int64_t N, int64_t K, const float* bias,
+                 const float* prelu, const float* accum, float* z, float* y, int64_t ldc, hipStream_t s,
+                 const char* what, const CombEpi& ce_in = CombEpi{}, int64_t* tiles_out = nullptr) {
+  CombEpi ce = ce_in;
+  ce.nt_io = gemm_nt_io(M, N, 4);
+  const bool vec_out = ldc % 4 == 0 && aligned16(y) && (z == nullptr || aligned16(z)) &&
+                       (accum == nullptr || aligned16(accum)) &&
+                       (EPI != 4 || (aligned16(ce.xd) && ce.ldxd % 4 == 0 &&
+                                     (ce.gd == nullptr || (aligned16(ce.gd) && ce.ldgd % 4 == 0))));
+  const uint16_t* bp = static_cast<const uint16_t*>(planes);
+  const int* fexp = reinterpret_cast<const int*>(static_cast<const char*>(planes) + (size_t)N * (size_t)K * 4);
+  const bool xcd = xcd_remap_enabled();
+  int64_t tiles;
+#define HGIN_NT_H2(TNV, WNV)                                                                                      \
+  {                                                                                                               \
+    constexpr int BM = (4 / WNV) * 64, BN = WNV * TNV * 32;                                                       \
+    tiles = ceil_div(N, BN) * ceil_div(M, BM);                                                                    \
+    dim3 grid((unsigned)(xcd ? round_up8(tiles) : tiles));                                                        \
+    HGIN_TRACE("k_gemm_nt_h2<EPI%d,%dx%d,N%lld,K%lld>", EPI, BM, BN, (long long)N, (long long)K);                  \
+    if (h2_occ() == 3)                                                                                            \
+      k_gemm_nt_h2<EPI, TNV, WNV, 3><<<grid, 256, 0, s>>>(a, bp, fexp, M, N, K, bias, prelu, accum, z, y, ldc,     \
+                                                          vec_out, tiles, xcd, ce);                               \
+    else                                                                                                          \
+      k_gemm_nt_h2<EPI, TNV, WNV, 2><<<grid, 256, 0, s>>>(a, bp, fexp, M, N, K, bias, prelu, accum, z, y, ldc,     \
+                                                          vec_out, tiles, xcd, ce);                               \
+  }
+  if (N <= 32)
+    HGIN_NT_H2(1, 1)
+  else if (use_bm64<EPI == 4 ? 0 : EPI>(M, N))
+    HGIN_NT_H2(1, 4)
+  else
+    HGIN_NT_H2(2, 2)
+#undef HGIN_NT_H2
+  if (tiles_out) *tiles_out = tiles;
+  return check_launch(what);
+}
+
+int h2_planes(const float* b, int64_t ldb, int64_t N, int64_t K, void* out, hipStream_t s, const char* what) {
+  HGIN_ARG_CHECK(N > 0 && K > 0 && K % kBK == 0, "%s: K must be a positive multiple of %d", what, kBK);
+  HGIN_ARG_CHECK(b && out && ldb >= K && aligned16(out), "%s: bad operand / alignment", what);
+  int* fexp = reinterpret_cast<int*>(static_cast<char*>(out) + (size_t)N * (size_t)K * 4);
+  k_h2_planes<<<(unsigned)N, 64, 0, s>>>(b, ldb, K, static_cast<uint16_t*>(out), fexp);
+  return check_launch(what);
+}
+
 int check_a(const char* what, const float* a1, int64_t lda1, int64_t k1, const float* a2, int64_t lda2, int64_t K) {
   HGIN_ARG_CHECK(k1 >= 0 && k1 <= K, "%s: k1 out of [0, K]", what);
   HGIN_ARG_CHECK(k1 == 0 || (a1 && lda1 >= k1), "%s: bad A1", what);
@@ -1938,7 +2263,7 @@ bool nt2_eligible(const T* a1, int64_t lda1, int64_t k1, const T* a2, int64_t ld
   using P = Nt2<T>;
   constexpr int EPR = 16 / (int)sizeof(T);   // elements per 16 B
   if (!planes || !nt2_enabled()) return false;
-  if (P::kF32 && !split_mode) return false;   // the exact-f32 MFMA mode keeps k_gemm_nt
+  if (P::kF32 && (!split_mode || gemm_h2_enabled())) return false;   // mfma32 / h2 modes keep their own kernels
   if (K % P::KS || k1 % P::KS || nt2_bn<T>(N) == 0) return false;
   if (k1 > 0 && (!aligned16(a1) || lda1 % EPR)) return false;
   if (k1 < K && (!aligned16(a2) || lda2 % EPR)) return false;
@@ -2064,7 +2389,11 @@ int gemm_nt_combine(const char* what, const T* a, int64_t lda, const T* b, int64
                                      nullptr, nullptr, nullptr, c, ldc, s, what, ce, &tiles);
   else if constexpr (sizeof(T) == 4) {
     ce.nt_io = gemm_nt_io(M, N, 4);
-    rc = try_ws_f32_comb(a, lda, b, ldb, c, ldc, M, N, K, ce, s, what, &tiles);
+    rc = h2_eligible(a, lda, K, nullptr, 0, b_planes, K)
+             ? launch_nt_h2<4>(Src2{a, lda, nullptr, 0, K}, b_planes, M, N, K, nullptr, nullptr, nullptr, nullptr, c,
+                               ldc, s, what, ce, &tiles)
+             : -1;
+    if (rc < 0) rc = try_ws_f32_comb(a, lda, b, ldb, c, ldc, M, N, K, ce, s, what, &tiles);
     if (rc < 0)
       rc = launch_nt<4>(Src2{a, lda, nullptr, 0, K}, Src2{b, ldb, nullptr, 0, K}, M, N, K, nullptr, nullptr, nullptr,
                         nullptr, c, ldc, s, what, ce, &tiles);
@@ -2168,6 +2497,9 @@ extern "C" int hgin_gin_mlp_fwd_f32(const float* a1, int64_t lda1, int64_t k1, c
   if (nt2_eligible<float>(a1, lda1, k1, a2, lda2, w_planes, N, K, gemm_split_enabled()))
     return launch_nt2<float, 1, float>(a1, lda1, k1, a2, lda2, a2_eps, w_planes, M, N, K, bias, prelu, accum, z, y, N,
                                        as_stream(stream), "hgin_gin_mlp_fwd_f32");
+  if (h2_eligible(a1, lda1, k1, a2, lda2, w_planes, K))
+    return launch_nt_h2<1>(Src2{a1, lda1, a2, lda2, k1, a2_eps}, w_planes, M, N, K, bias, prelu, accum, z, y, N,
+                           as_stream(stream), "hgin_gin_mlp_fwd_f32");
   {
     const int rc = try_ws_f32(a1, lda1, k1, a2_eps, w, bias, prelu, accum, z, y, M, N, K, as_stream(stream),
                               "hgin_gin_mlp_fwd_f32");
@@ -2188,6 +2520,9 @@ extern "C" int hgin_linear_fwd_f32(const float* a1, int64_t lda1, int64_t k1, co
   if (nt2_eligible<float>(a1, lda1, k1, a2, lda2, w_planes, N, K, gemm_split_enabled()))
     return launch_nt2<float, 2, float>(a1, lda1, k1, a2, lda2, nullptr, w_planes, M, N, K, bias, nullptr, nullptr,
                                        nullptr, y, N, as_stream(stream), "hgin_linear_fwd_f32");
+  if (h2_eligible(a1, lda1, k1, a2, lda2, w_planes, K))
+    return launch_nt_h2<2>(Src2{a1, lda1, a2, lda2, k1}, w_planes, M, N, K, bias, nullptr, nullptr, nullptr, y, N,
+                           as_stream(stream), "hgin_linear_fwd_f32");
   return launch_nt<2>(Src2{a1, lda1, a2, lda2, k1}, Src2{w, K, nullptr, 0, K}, M, N, K, bias, nullptr, nullptr,
                       nullptr, y, N, as_stream(stream), "hgin_linear_fwd_f32");
 }
@@ -2202,17 +2537,22 @@ extern "C" int hgin_gemm_nt_f32(const float* a, int64_t lda, const float* b, int
   if (nt2_eligible<float>(a, lda, K, nullptr, 0, b_planes, N, K, gemm_split_enabled()))
     return launch_nt2<float, 0, float>(a, lda, K, nullptr, 0, nullptr, b_planes, M, N, K, nullptr, nullptr, nullptr,
                                        nullptr, c, ldc, as_stream(stream), "hgin_gemm_nt_f32");
+  if (h2_eligible(a, lda, K, nullptr, 0, b_planes, K))
+    return launch_nt_h2<0>(Src2{a, lda, nullptr, 0, K}, b_planes, M, N, K, nullptr, nullptr, nullptr, nullptr, c, ldc,
+                           as_stream(stream), "hgin_gemm_nt_f32");
   return launch_nt<0>(Src2{a, lda, nullptr, 0, K}, Src2{b, ldb, nullptr, 0, K}, M, N, K, nullptr, nullptr, nullptr,
                       nullptr, c, ldc, as_stream(stream), "hgin_gemm_nt_f32");
 }
 
 extern "C" int hgin_nt_planes_size(int64_t N, int64_t K, int elem_bytes, size_t* bytes) {
   HGIN_ARG_CHECK(bytes && N >= 0 && K >= 0 && (elem_bytes == 4 || elem_bytes == 2), "hgin_nt_planes_size: bad args");
-  *bytes = elem_bytes == 4 ? nt_planes_bytes<float>(N, K) : nt_planes_bytes<uint16_t>(N, K);
+  *bytes = elem_bytes == 4 ? (gemm_h2_enabled() ? h2_planes_bytes(N, K) : nt_planes_bytes<float>(N, K))
+                           : nt_planes_bytes<uint16_t>(N, K);
   return HGIN_OK;
 }
 
 extern "C" int hgin_nt_planes_f32(const float* b, int64_t ldb, int64_t N, int64_t K, void* out, void* stream) {
+  if (gemm_h2_enabled()) return h2_planes(b, ldb, N, K, out, as_stream(stream), "hgin_nt_planes_f32");
   return nt_planes<float>(b, ldb, N, K, out, as_stream(stream), "hgin_nt_planes_f32");
 }
 

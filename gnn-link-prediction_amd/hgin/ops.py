@@ -83,6 +83,9 @@ LONG_ROW_MIN = int(os.environ.get("HGIN_LONG_ROW", "2048"))
 # The LDS-DMA NT GEMM (hgin_gemm_nt.hip k_nt2) is measured slower than the register-staged one and off by
 # default; HGIN_NT2=1 selects it (the C side reads the same switch).
 NT2 = os.environ.get("HGIN_NT2", "0") == "1"
+# HGIN_F32_GEMM=h2: fp32 NT GEMMs as two scaled fp16 terms (3 products; hgin_gemm_nt.hip k_gemm_nt_h2), whose
+# weight operand is pre-split once per call by hgin_nt_planes_f32
+H2 = os.environ.get("HGIN_F32_GEMM") == "h2"
 LONG_CHUNK = 1024
 
 
@@ -306,12 +309,16 @@ def combine_bwd(g: Tensor, x_dst: Tensor, eps: Tensor, want_gx: bool):
 def nt_planes(b: Tensor) -> Optional[Tensor]:
     """The B operand [N, K] of an NT GEMM pre-converted for the LDS-DMA kernel (hgin_nt_planes_*: fp32 -> its
     three bf16 split planes, bf16 -> a swizzled copy; N * K * 6 or N * K * 2 bytes), or None where that kernel
-    does not take the shape (the register-staged kernel runs; the result is bit-identical either way)."""
-    if not NT2:
+    does not take the shape (the register-staged kernel runs; the result is bit-identical either way).  In h2
+    mode (fp32): its scaled fp16 hi / lo planes and per-row exponents (N * K * 4 bytes + N int32)."""
+    h2 = H2 and b.dtype == torch.float32
+    if not (NT2 or h2):
         return None
     N, K = b.shape
     ks = 32 if b.dtype == torch.float32 else 64
-    if N == 0 or K == 0 or K % ks or N % 128 or b.stride(1) != 1 or b.data_ptr() % 16 or b.stride(0) % (16 // b.element_size()):
+    if N == 0 or K == 0 or K % ks or b.stride(1) != 1:
+        return None
+    if not h2 and (N % 128 or b.data_ptr() % 16 or b.stride(0) % (16 // b.element_size())):
         return None
     nbytes = ctypes.c_size_t(0)
     _lib.check(_lib.lib().hgin_nt_planes_size(N, K, b.element_size(), ctypes.byref(nbytes)), "hgin_nt_planes_size")
