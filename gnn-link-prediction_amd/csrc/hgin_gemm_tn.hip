@@ -109,9 +109,11 @@ using bf16x8 = __attribute__((ext_vector_type(8))) __bf16;
 // kSplit: fp32 operands on the bf16 matrix cores (hgin_common.h split4): the transposed column runs of 4 m
 // are written as three bf16 planes ([col][3 x 32 m + pad] rows of kSplitRowWords words) and a lane reads
 // 8 consecutive m of a plane (one 16-deep k-block) per ds_read_b128.
-// kPro: A = g_y and the PReLU-backward prologue above (TnPro).  kLateZ: z is loaded when the stage is
+// kPro: A = g_y and the PReLU-backward prologue above (TnPro).  kGz: the first K tile's workgroups also store the
+// g_z they form (TnPro::gz; its own instantiation: the store code in the others made the kLateZ kernel spill, 38
+// scratch ops, fused dW 6.6 -> 8.7 ms per cfg3 layer-0 launch).  kLateZ: z is loaded when the stage is
 // written to LDS instead of with the register prefetch (16 fewer VGPRs live across the MFMA cluster).
-template <bool kClean, int TNR, bool kSplit, bool kPro, bool kLateZ = false>
+template <bool kClean, int TNR, bool kSplit, bool kPro, bool kLateZ = false, bool kGz = false>
 __global__ __launch_bounds__(256, (kPro && !kLateZ) ? 2 : 3) void k_gemm_tn_partial(const float* __restrict__ A, int64_t lda,
                                                             const float* __restrict__ B1, int64_t ldb1,
                                                             const float* __restrict__ B2, int64_t ldb2, int64_t K1,
@@ -278,12 +280,12 @@ __global__ __launch_bounds__(256, (kPro && !kLateZ) ? 2 : 3) void k_gemm_tn_part
     }
   };
   // the 4 x 4 block regrouped: column c4 + t gets (row r4 .. r4 + 3) as one float4
-  const bool store_gz = kPro && pro.gz != nullptr && work.k0 == 0 && stage_a;   // workgroup / wave-uniform
+  const bool store_gz = kPro && kGz && work.k0 == 0 && stage_a;   // workgroup / wave-uniform
   auto store_stage = [&]() {
     if constexpr (kPro && kLateZ) load_z(m_ld);
     if constexpr (kPro) prologue();
     if constexpr (kPro) {
-      if (store_gz) {   // rows m_ld + r4a + j, columns n0 + c4a .. + 3 (rows past me were zeroed: skipped)
+      if (kGz && store_gz) {   // rows m_ld + r4a + j, columns n0 + c4a .. + 3 (rows past me were zeroed: skipped)
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           const int64_t gm = m_ld + r4a + j;
@@ -1728,13 +1730,14 @@ int gemm_tn_impl(const char* what, const T* a, int64_t lda, const T* b1, int64_t
     HGIN_TRACE("k_gemm_tn_partial<%s,%s,N%lld,K%lld>",
                pro_in ? (pro_in->gz ? "prelu_bwd_fused+gz" : "prelu_bwd_fused") : "plain", split ? "split" : "mfma32",
                (long long)N, (long long)K);
-#define HGIN_TN_LAUNCH(CLEAN, TNR, SPLIT, PRO, LATE)                                                          \
-  k_gemm_tn_partial<CLEAN, TNR, SPLIT, PRO, LATE><<<grid, 256, 0, s>>>(a, lda, b1, ldb1, b2, ldb2, k1, M, N, K, \
-                                                                        rows, vec, slab, tg, pro)
-#define HGIN_TN_PRO(CLEAN, TNR, SPLIT)                                          \
-  if (!pro_in) HGIN_TN_LAUNCH(CLEAN, TNR, SPLIT, false, false);                 \
-  else if (late) HGIN_TN_LAUNCH(CLEAN, TNR, SPLIT, true, true);                 \
-  else HGIN_TN_LAUNCH(CLEAN, TNR, SPLIT, true, false);
+#define HGIN_TN_LAUNCH(CLEAN, TNR, SPLIT, PRO, LATE, GZ)                                                           \
+  k_gemm_tn_partial<CLEAN, TNR, SPLIT, PRO, LATE, GZ><<<grid, 256, 0, s>>>(a, lda, b1, ldb1, b2, ldb2, k1, M, N, K, \
+                                                                            rows, vec, slab, tg, pro)
+#define HGIN_TN_PRO(CLEAN, TNR, SPLIT)                                                \
+  if (!pro_in) HGIN_TN_LAUNCH(CLEAN, TNR, SPLIT, false, false, false);                \
+  else if (pro_in->gz) HGIN_TN_LAUNCH(CLEAN, TNR, SPLIT, true, false, true); /* (late z + gz spills) */ \
+  else if (late) HGIN_TN_LAUNCH(CLEAN, TNR, SPLIT, true, true, false);              \
+  else HGIN_TN_LAUNCH(CLEAN, TNR, SPLIT, true, false, false);
 #define HGIN_TN_CLEAN(TNR, SPLIT) \
   if (clean) { HGIN_TN_PRO(true, TNR, SPLIT) } else { HGIN_TN_PRO(false, TNR, SPLIT) }
     if (tile_n == 32) {
