@@ -366,12 +366,18 @@ __device__ __forceinline__ void tile_partial(float* smem, float ep, float* part,
   if (t == 0) part[q] = smem[0];
 }
 
-template <int EPI, bool kClean, int TN, int WNv, bool kSplit, int NW = 4>
+// kBdma (split mode, clean tiles, N a multiple of BN): the B operand comes pre-split — hgin_nt_planes_f32's three
+// bf16 planes, whose per-stage rows are already the LDS image's rows (same chunk swizzle) — and each K-tile's B
+// image is copied HBM/L2 -> LDS by global_load_lds_dwordx4 (inline asm, per-lane source addresses), issued after
+// the first barrier of a K-tile step and awaited (vmcnt 0) before the second: the A split pass between them hides its
+// latency.  No B split VALU (a quarter of the loop's VALU at K = 512, N = 256), no B prefetch registers.
+template <int EPI, bool kClean, int TN, int WNv, bool kSplit, int NW = 4, bool kBdma = false>
 __global__ __launch_bounds__(NW * 64, NW == 8 ? 2 : 3) void k_gemm_nt(Src2 A, Src2 B, int64_t M, int64_t N, int64_t K,
                                                     const float* __restrict__ bias, const float* __restrict__ prelu,
                                                     const float* __restrict__ accum, float* __restrict__ Z,
                                                     float* __restrict__ Y, int64_t ldc, bool vec_out,
-                                                    int64_t n_tiles, bool xcd, CombEpi ce) {
+                                                    int64_t n_tiles, bool xcd, CombEpi ce,
+                                                    const uint16_t* __restrict__ Bp = nullptr) {
   constexpr int NT = NW * 64;             // threads
   constexpr int WN = WNv;                 // waves along N
   constexpr int WM = NW / WN;             // waves along M
@@ -408,32 +414,54 @@ __global__ __launch_bounds__(NW * 64, NW == 8 ? 2 : 3) void k_gemm_nt(Src2 A, Sr
 #pragma unroll
       for (int e = 0; e < 16; ++e) acc[a][b][e] = 0.0f;
 
-  float4 ra[BM / (NT / 8)], rb[BN >= NT / 8 ? BN / (NT / 8) : 1];
+  float4 ra[BM / (NT / 8)], rb[(BN >= NT / 8 && !kBdma) ? BN / (NT / 8) : 1];
   const float sc2 = self_scale(A.eps2);
   bool scale_a = false;   // ra holds a clean p2 tile still to be scaled by sc2
   auto load_a = [&](int64_t k0) {
     load_tile<kClean, BM, NT>(ra, A, m0, M, k0, K, tid, sc2);
     scale_a = kClean && A.eps2 != nullptr && k0 >= A.k1;
   };
+  constexpr int kBChunks = BN * kSplitRowWordsNT / 4;       // 16-B chunks of the B image
+  constexpr int kBInst = kBdma ? kBChunks / 64 / NW : 1;    // LDS-DMA instructions per wave per K-tile
+  static_assert(!kBdma || (kSplit && kClean && kBChunks % (64 * NW) == 0), "kBdma shape");
+  uint32_t boff[kBInst];   // byte offset of this lane's chunk inside one stage of the planes
+  if constexpr (kBdma) {
+#pragma unroll
+    for (int i = 0; i < kBInst; ++i) {
+      const int j = (wave * kBInst + i) * 64 + lane;        // image chunk: row j / 12, word group j % 12
+      const int rr = j / 12, w = j % 12;
+      boff[i] = (uint32_t)((((w >> 2) * N + n0 + rr) * 64) + (w & 3) * 16);
+    }
+  }
+  auto dma_b = [&](int64_t k0) {
+    if constexpr (kBdma) {
+      const char* base = reinterpret_cast<const char*>(Bp) + (k0 / kBK) * 3 * N * 64;
+#pragma unroll
+      for (int i = 0; i < kBInst; ++i)
+        glds16_asm(base + boff[i], reinterpret_cast<char*>(Bsh) + (wave * kBInst + i) * 1024);
+    }
+  };
   auto stage = [&]() {
     if (scale_a) scale_tile<BM, NT>(ra, sc2);
     if constexpr (kSplit) {
       store_tile_split<BM, NT>(Ash, ra, tid);
-      store_tile_split<BN, NT>(Bsh, rb, tid);
+      if constexpr (!kBdma) store_tile_split<BN, NT>(Bsh, rb, tid);
     } else {
       store_tile<BM, NT>(As, ra, tid);
       store_tile<BN, NT>(Bs, rb, tid);
     }
   };
   load_a(0);
-  load_tile<kClean, BN, NT>(rb, B, n0, N, 0, K, tid);
+  if constexpr (kBdma) dma_b(0);
+  else load_tile<kClean, BN, NT>(rb, B, n0, N, 0, K, tid);
   stage();
+  if constexpr (kBdma) wait_vm<0>();
   __syncthreads();
   for (int64_t k0 = 0; k0 < K; k0 += kBK) {
     const bool more = k0 + kBK < K;
     if (more) {   // next K-tile's global loads stay in flight under this K-tile's MFMAs
       load_a(k0 + kBK);
-      load_tile<kClean, BN, NT>(rb, B, n0, N, k0 + kBK, K, tid);
+      if constexpr (!kBdma) load_tile<kClean, BN, NT>(rb, B, n0, N, k0 + kBK, K, tid);
     }
     __builtin_amdgcn_s_setprio(1);   // keep the MFMA cluster together (T5)
     if constexpr (kSplit) {
@@ -489,7 +517,9 @@ __global__ __launch_bounds__(NW * 64, NW == 8 ? 2 : 3) void k_gemm_nt(Src2 A, Sr
     __builtin_amdgcn_s_setprio(0);
     if (more) {
       __syncthreads();
+      dma_b(k0 + kBK);
       stage();
+      if constexpr (kBdma) wait_vm<0>();
       __syncthreads();
     }
   }
@@ -500,20 +530,39 @@ __global__ __launch_bounds__(NW * 64, NW == 8 ? 2 : 3) void k_gemm_nt(Src2 A, Sr
   if constexpr (EPI == 4) tile_partial(smem, ep, ce.part, q);
 }
 
+// HGIN_NT_BDMA=0: the 128 x 128 split-mode tile splits B itself even where pre-split planes are passed
+bool nt_bdma_enabled() {
+  static const bool on = [] {
+    const char* v = getenv("HGIN_NT_BDMA");
+    return !(v && v[0] == '0');
+  }();
+  return on;
+}
+
 template <int EPI, int TN, int WN, int NW = 4>
 int64_t launch_nt_tn(bool vec, const Src2& a, const Src2& b, int64_t M, int64_t N, int64_t K, const float* bias,
                      const float* prelu, const float* accum, float* z, float* y, int64_t ldc, bool vec_out,
-                     hipStream_t s, const CombEpi& ce) {
+                     hipStream_t s, const CombEpi& ce, const void* planes = nullptr) {
   constexpr int BM = (NW / WN) * 64;
   constexpr int BN = WN * TN * 32;
   const int64_t tiles = ceil_div(N, BN) * ceil_div(M, BM);
   const bool xcd = xcd_remap_enabled();
   dim3 grid((unsigned)(xcd ? round_up8(tiles) : tiles));
+  if constexpr (TN == 2 && WN == 2 && NW == 4) {
+    if (planes && vec && gemm_split_enabled() && !gemm_h2_enabled() && N % BN == 0 && nt_bdma_enabled() &&
+        (int64_t)N * K * 6 < (int64_t(1) << 32)) {
+      HGIN_TRACE("k_gemm_nt<EPI%d,%dx%d,split_bdma,N%lld,K%lld>", EPI, BM, BN, (long long)N, (long long)K);
+      k_gemm_nt<EPI, true, 2, 2, true, 4, true><<<grid, 256, 0, s>>>(a, b, M, N, K, bias, prelu, accum, z, y, ldc,
+                                                                     vec_out, tiles, xcd, ce,
+                                                                     static_cast<const uint16_t*>(planes));
+      return tiles;
+    }
+  }
   HGIN_TRACE("k_gemm_nt<EPI%d,%dx%d,%s,N%lld,K%lld>", EPI, (NW / WN) * 64, WN * TN * 32,
              gemm_split_enabled() ? "split" : "mfma32", (long long)N, (long long)K);
 #define HGIN_NT_F32(CLEAN, SPLIT)                                                                           \
   k_gemm_nt<EPI, CLEAN, TN, WN, SPLIT, NW><<<grid, NW * 64, 0, s>>>(a, b, M, N, K, bias, prelu, accum, z, y, ldc, \
-                                                                    vec_out, tiles, xcd, ce)
+                                                                    vec_out, tiles, xcd, ce, nullptr)
   if (gemm_split_enabled()) {
     if (vec) HGIN_NT_F32(true, true); else HGIN_NT_F32(false, true);
   } else {
@@ -573,7 +622,7 @@ bool gemm_nt_io(int64_t M, int64_t N, int64_t elem) {
 template <int EPI>
 int launch_nt(const Src2& a, const Src2& b, int64_t M, int64_t N, int64_t K, const float* bias, const float* prelu,
               const float* accum, float* z, float* y, int64_t ldc, hipStream_t s, const char* what,
-              const CombEpi& ce_in = CombEpi{}, int64_t* tiles_out = nullptr) {
+              const CombEpi& ce_in = CombEpi{}, int64_t* tiles_out = nullptr, const void* planes = nullptr) {
   CombEpi ce = ce_in;
   ce.nt_io = gemm_nt_io(M, N, 4);
   const bool vec = K % kBK == 0 && a.k1 % kBK == 0 && aligned16(a.p1) && a.ld1 % 4 == 0 &&
@@ -590,7 +639,7 @@ int launch_nt(const Src2& a, const Src2& b, int64_t M, int64_t N, int64_t K, con
   else if (use_bm64<EPI == 4 ? 0 : EPI>(M, N))
     tiles = launch_nt_tn<EPI, 1, 4>(vec, a, b, M, N, K, bias, prelu, accum, z, y, ldc, vec_out, s, ce);
   else
-    tiles = launch_nt_tn<EPI, 2, 2>(vec, a, b, M, N, K, bias, prelu, accum, z, y, ldc, vec_out, s, ce);
+    tiles = launch_nt_tn<EPI, 2, 2>(vec, a, b, M, N, K, bias, prelu, accum, z, y, ldc, vec_out, s, ce, planes);
   if (tiles_out) *tiles_out = tiles;
   return check_launch(what);
 }
@@ -2396,7 +2445,7 @@ int gemm_nt_combine(const char* what, const T* a, int64_t lda, const T* b, int64
     if (rc < 0) rc = try_ws_f32_comb(a, lda, b, ldb, c, ldc, M, N, K, ce, s, what, &tiles);
     if (rc < 0)
       rc = launch_nt<4>(Src2{a, lda, nullptr, 0, K}, Src2{b, ldb, nullptr, 0, K}, M, N, K, nullptr, nullptr, nullptr,
-                        nullptr, c, ldc, s, what, ce, &tiles);
+                        nullptr, c, ldc, s, what, ce, &tiles, b_planes);
   }
   if (rc) return rc;
   const int64_t nb = ceil_div(tiles, kPartChunk);
@@ -2506,7 +2555,7 @@ extern "C" int hgin_gin_mlp_fwd_f32(const float* a1, int64_t lda1, int64_t k1, c
     if (rc >= 0) return rc;
   }
   return launch_nt<1>(Src2{a1, lda1, a2, lda2, k1, a2_eps}, Src2{w, K, nullptr, 0, K}, M, N, K, bias, prelu, accum, z, y,
-                      N, as_stream(stream), "hgin_gin_mlp_fwd_f32");
+                      N, as_stream(stream), "hgin_gin_mlp_fwd_f32", CombEpi{}, nullptr, w_planes);
 }
 
 extern "C" int hgin_linear_fwd_f32(const float* a1, int64_t lda1, int64_t k1, const float* a2, int64_t lda2,
@@ -2524,7 +2573,7 @@ extern "C" int hgin_linear_fwd_f32(const float* a1, int64_t lda1, int64_t k1, co
     return launch_nt_h2<2>(Src2{a1, lda1, a2, lda2, k1}, w_planes, M, N, K, bias, nullptr, nullptr, nullptr, y, N,
                            as_stream(stream), "hgin_linear_fwd_f32");
   return launch_nt<2>(Src2{a1, lda1, a2, lda2, k1}, Src2{w, K, nullptr, 0, K}, M, N, K, bias, nullptr, nullptr,
-                      nullptr, y, N, as_stream(stream), "hgin_linear_fwd_f32");
+                      nullptr, y, N, as_stream(stream), "hgin_linear_fwd_f32", CombEpi{}, nullptr, w_planes);
 }
 
 extern "C" int hgin_gemm_nt_f32(const float* a, int64_t lda, const float* b, int64_t ldb, float* c, int64_t ldc,
@@ -2541,7 +2590,7 @@ extern "C" int hgin_gemm_nt_f32(const float* a, int64_t lda, const float* b, int
     return launch_nt_h2<0>(Src2{a, lda, nullptr, 0, K}, b_planes, M, N, K, nullptr, nullptr, nullptr, nullptr, c, ldc,
                            as_stream(stream), "hgin_gemm_nt_f32");
   return launch_nt<0>(Src2{a, lda, nullptr, 0, K}, Src2{b, ldb, nullptr, 0, K}, M, N, K, nullptr, nullptr, nullptr,
-                      nullptr, c, ldc, as_stream(stream), "hgin_gemm_nt_f32");
+                      nullptr, c, ldc, as_stream(stream), "hgin_gemm_nt_f32", CombEpi{}, nullptr, b_planes);
 }
 
 extern "C" int hgin_nt_planes_size(int64_t N, int64_t K, int elem_bytes, size_t* bytes) {

@@ -33,9 +33,10 @@ constexpr int kTnLd = kTnBM + 4;   // [col][m] image row stride (floats)
 struct TnGrid {
   int64_t tile_n;    // output-tile rows along N (128, or 32 for N <= 32)
   int64_t tiles_n;   // tiles along N
-  int64_t tiles;     // tiles_n * tiles along K
+  int64_t tiles;     // tiles_n * tiles along K (of this launch)
   int64_t n_work;    // tiles * splits
   int xcd;
+  int64_t kt0 = 0;   // first K tile of this launch
 };
 struct TnWork {
   int64_t n0, k0, split;
@@ -48,7 +49,7 @@ __device__ __forceinline__ TnWork tn_work(const TnGrid& g) {
   const int64_t t = q % g.tiles;
   w.split = q / g.tiles;
   w.n0 = (t % g.tiles_n) * g.tile_n;
-  w.k0 = (t / g.tiles_n) * 128;
+  w.k0 = (g.kt0 + t / g.tiles_n) * 128;
   return w;
 }
 
@@ -109,11 +110,14 @@ using bf16x8 = __attribute__((ext_vector_type(8))) __bf16;
 // kSplit: fp32 operands on the bf16 matrix cores (hgin_common.h split4): the transposed column runs of 4 m
 // are written as three bf16 planes ([col][3 x 32 m + pad] rows of kSplitRowWords words) and a lane reads
 // 8 consecutive m of a plane (one 16-deep k-block) per ds_read_b128.
-// kPro: A = g_y and the PReLU-backward prologue above (TnPro).  kGz: the first K tile's workgroups also store the
+// kPro: A = g_y and the PReLU-backward prologue above (TnPro).  kNoSums (a launch over the K tiles after the
+// first): g_z is formed but the bias / slope sums, which only the first K tile's workgroups keep, are not — 3 of the
+// 6 VALU ops per A element, skipped by 3 of 4 workgroups at K = 512 (a runtime branch on the K tile instead made
+// the kernel spill).  kGz: the first K tile's workgroups also store the
 // g_z they form (TnPro::gz; its own instantiation: the store code in the others made the kLateZ kernel spill, 38
 // scratch ops, fused dW 6.6 -> 8.7 ms per cfg3 layer-0 launch).  kLateZ: z is loaded when the stage is
 // written to LDS instead of with the register prefetch (16 fewer VGPRs live across the MFMA cluster).
-template <bool kClean, int TNR, bool kSplit, bool kPro, bool kLateZ = false, bool kGz = false>
+template <bool kClean, int TNR, bool kSplit, bool kPro, bool kLateZ = false, bool kGz = false, bool kNoSums = false>
 __global__ __launch_bounds__(256, (kPro && !kLateZ) ? 2 : 3) void k_gemm_tn_partial(const float* __restrict__ A, int64_t lda,
                                                             const float* __restrict__ B1, int64_t ldb1,
                                                             const float* __restrict__ B2, int64_t ldb2, int64_t K1,
@@ -264,19 +268,30 @@ __global__ __launch_bounds__(256, (kPro && !kLateZ) ? 2 : 3) void k_gemm_tn_part
   const float slope = kPro ? pro.slope[0] : 0.0f;
   auto prologue = [&]() {
     if (!stage_a) return;
+    if constexpr (!kNoSums) {
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {   // branch-free (a data-dependent branch per element splits the block and
-                                    // the scheduler then keeps every loaded value alive: heavy spilling)
-      float g[4] = {va[j].x, va[j].y, va[j].z, va[j].w};
-      const float zz[4] = {vz[j].x, vz[j].y, vz[j].z, vz[j].w};
+      for (int j = 0; j < 4; ++j) {   // branch-free (a data-dependent branch per element splits the block and
+                                      // the scheduler then keeps every loaded value alive: heavy spilling)
+        float g[4] = {va[j].x, va[j].y, va[j].z, va[j].w};
+        const float zz[4] = {vz[j].x, vz[j].y, vz[j].z, vz[j].w};
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const bool pos = zz[q] > 0.0f;
-        ssc[q] = __fadd_rn(ssc[q], pos ? 0.0f : __fmul_rn(zz[q], g[q]));
-        g[q] = pos ? g[q] : __fmul_rn(slope, g[q]);
-        csum[q] = __fadd_rn(csum[q], g[q]);
+        for (int q = 0; q < 4; ++q) {
+          const bool pos = zz[q] > 0.0f;
+          ssc[q] = __fadd_rn(ssc[q], pos ? 0.0f : __fmul_rn(zz[q], g[q]));
+          g[q] = pos ? g[q] : __fmul_rn(slope, g[q]);
+          csum[q] = __fadd_rn(csum[q], g[q]);
+        }
+        va[j] = make_float4(g[0], g[1], g[2], g[3]);
       }
-      va[j] = make_float4(g[0], g[1], g[2], g[3]);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        float g[4] = {va[j].x, va[j].y, va[j].z, va[j].w};
+        const float zz[4] = {vz[j].x, vz[j].y, vz[j].z, vz[j].w};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) g[q] = zz[q] > 0.0f ? g[q] : __fmul_rn(slope, g[q]);
+        va[j] = make_float4(g[0], g[1], g[2], g[3]);
+      }
     }
   };
   // the 4 x 4 block regrouped: column c4 + t gets (row r4 .. r4 + 3) as one float4
@@ -398,7 +413,7 @@ __global__ __launch_bounds__(256, (kPro && !kLateZ) ? 2 : 3) void k_gemm_tn_part
       __syncthreads();
     }
   }
-  if constexpr (kPro) {
+  if constexpr (kPro && !kNoSums) {
     if (work.k0 == 0)   // workgroup-uniform
       pro_partials<4>(pro, smem, TNR, r4a >> 2, c4a, stage_a, csum, ssc, n0, N, work.split);
   }
@@ -1580,6 +1595,15 @@ int64_t tn_target_wgs() {
 
 // Fused PReLU-backward prologue: z loaded with the register prefetch (2 waves / SIMD, the extra 16-32 live
 // VGPRs) or at LDS-store time (3 waves / SIMD for fp32).  HGIN_TN_LATEZ=0/1.
+// HGIN_TN_NOSUMS=0: the fused dW in one launch, every workgroup keeping the (unused) bias / slope sums
+bool tn_nosums_enabled() {
+  static const bool on = [] {
+    const char* v = getenv("HGIN_TN_NOSUMS");
+    return !(v && v[0] == '0');
+  }();
+  return on;
+}
+
 bool tn_late_z() {
   static const bool v = [] {
     const char* e = getenv("HGIN_TN_LATEZ");
@@ -1740,7 +1764,22 @@ int gemm_tn_impl(const char* what, const T* a, int64_t lda, const T* b1, int64_t
   else HGIN_TN_LAUNCH(CLEAN, TNR, SPLIT, true, false, false);
 #define HGIN_TN_CLEAN(TNR, SPLIT) \
   if (clean) { HGIN_TN_PRO(true, TNR, SPLIT) } else { HGIN_TN_PRO(false, TNR, SPLIT) }
-    if (tile_n == 32) {
+    const int64_t kts = ceil_div(K, 128);
+    if (pro_in && !pro_in->gz && late && clean && split && tile_n == 128 && kts > 1 && tn_nosums_enabled()) {
+      // the first K tile (g_z + the bias / slope sums), then the others (g_z alone) as a second launch
+      TnGrid t1 = tg, t2 = tg;
+      t1.tiles = tiles_n;
+      t1.n_work = tiles_n * S_eff;
+      t2.tiles = tiles_n * (kts - 1);
+      t2.n_work = t2.tiles * S_eff;
+      t2.kt0 = 1;
+      k_gemm_tn_partial<true, 128, true, true, true, false, false>
+          <<<(unsigned)(t1.xcd ? round_up8(t1.n_work) : t1.n_work), 256, 0, s>>>(a, lda, b1, ldb1, b2, ldb2, k1, M, N,
+                                                                                K, rows, vec, slab, t1, pro);
+      k_gemm_tn_partial<true, 128, true, true, true, false, true>
+          <<<(unsigned)(t2.xcd ? round_up8(t2.n_work) : t2.n_work), 256, 0, s>>>(a, lda, b1, ldb1, b2, ldb2, k1, M, N,
+                                                                                K, rows, vec, slab, t2, pro);
+    } else if (tile_n == 32) {
       if (split) { HGIN_TN_CLEAN(32, true) } else { HGIN_TN_CLEAN(32, false) }
     } else {
       if (split) { HGIN_TN_CLEAN(128, true) } else { HGIN_TN_CLEAN(128, false) }

@@ -86,6 +86,9 @@ NT2 = os.environ.get("HGIN_NT2", "0") == "1"
 # HGIN_F32_GEMM=h2: fp32 NT GEMMs as two scaled fp16 terms (3 products; hgin_gemm_nt.hip k_gemm_nt_h2), whose
 # weight operand is pre-split once per call by hgin_nt_planes_f32
 H2 = os.environ.get("HGIN_F32_GEMM") == "h2"
+# fp32 split mode: the 128 x 128 NT tile copies its B stages from pre-split planes by LDS-DMA (k_gemm_nt kBdma);
+# HGIN_NT_BDMA=0 keeps the per-tile split
+BDMA = os.environ.get("HGIN_NT_BDMA", "1") != "0" and os.environ.get("HGIN_F32_GEMM", "split") not in ("mfma32", "h2")
 LONG_CHUNK = 1024
 
 
@@ -310,9 +313,11 @@ def nt_planes(b: Tensor) -> Optional[Tensor]:
     """The B operand [N, K] of an NT GEMM pre-converted for the LDS-DMA kernel (hgin_nt_planes_*: fp32 -> its
     three bf16 split planes, bf16 -> a swizzled copy; N * K * 6 or N * K * 2 bytes), or None where that kernel
     does not take the shape (the register-staged kernel runs; the result is bit-identical either way).  In h2
-    mode (fp32): its scaled fp16 hi / lo planes and per-row exponents (N * K * 4 bytes + N int32)."""
+    mode (fp32): its scaled fp16 hi / lo planes and per-row exponents (N * K * 4 bytes + N int32).  fp32 split mode
+    (default): the same three planes feed the register-staged 128 x 128 tile's B stages by LDS-DMA (bit-identical)."""
     h2 = H2 and b.dtype == torch.float32
-    if not (NT2 or h2):
+    bdma = BDMA and b.dtype == torch.float32
+    if not (NT2 or h2 or bdma):
         return None
     N, K = b.shape
     ks = 32 if b.dtype == torch.float32 else 64

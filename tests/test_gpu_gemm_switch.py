@@ -8,7 +8,9 @@
                               k_gemm_tn_bf16_tr, and k_gemm_nt for the fp32 forward GEMM, whose default at K = N = 256
                               is k_ws_f32) for every shape (the weight-stationary dW kernel k_wsd_bf16 is
                               the default at N, K in {128, 256});
-  * HGIN_NT_BKH=128         — the tiled kernel with 128-deep K-tiles (with the weight-stationary form off).
+  * HGIN_NT_BKH=128         — the tiled kernel with 128-deep K-tiles (with the weight-stationary form off);
+  * HGIN_NT_BDMA=0 (tiled)  — the fp32 128 x 128 tile splitting its B stages itself instead of copying them from
+                              pre-split planes by LDS-DMA.
 
 Every child checks its outputs against an fp32 evaluation of the same bf16 operands; the three settings must
 agree bit for bit (same products, same per-accumulator k order, same epilogue arithmetic), except the combine's
@@ -26,7 +28,8 @@ pytestmark = pytest.mark.gpu
 HERE = os.path.dirname(os.path.abspath(__file__))
 
 SWITCHES = {"default": {}, "tiled": {"HGIN_NT_WS": "0", "HGIN_TN_WS": "0", "HGIN_NT_WS32": "0"},
-            "tiled_bk128": {"HGIN_NT_WS": "0", "HGIN_NT_BKH": "128", "HGIN_TN_WS": "0", "HGIN_NT_WS32": "0"}}
+            "tiled_bk128": {"HGIN_NT_WS": "0", "HGIN_NT_BKH": "128", "HGIN_TN_WS": "0", "HGIN_NT_WS32": "0"},
+            "tiled_nobdma": {"HGIN_NT_WS": "0", "HGIN_TN_WS": "0", "HGIN_NT_WS32": "0", "HGIN_NT_BDMA": "0"}}
 _results = {}
 
 
@@ -49,7 +52,7 @@ def test_switch_within_tolerance(name):
     _run(name)        # the child checks against fp32 itself
 
 
-@pytest.mark.parametrize("name", ["tiled", "tiled_bk128"])
+@pytest.mark.parametrize("name", ["tiled", "tiled_bk128", "tiled_nobdma"])
 def test_switch_bitwise_equal_default(name):
     ref, got = _run("default"), _run(name)
     assert ref.keys() == got.keys()
