@@ -1885,8 +1885,9 @@ int mlp_bwd_w_entry(const char* what, const T* g_y, int64_t ld_gy, const T* z, i
       return check_launch(what);
     }
     // fp32 shapes the weight-stationary kernels do not take (e.g. the readout's Linear(128, 32)): the tiled dW with
-    // the prologue, its first-K-tile workgroups storing the g_z they form (no separate PReLU-backward pass)
-    if (mlp_bwd_w_fused(N, K, sizeof(T)) && ld_gz % 4 == 0) {
+    // the prologue, its first-K-tile workgroups storing the g_z they form (no separate PReLU-backward pass).
+    // HGIN_WSD_PRO=0 turns this fold off as well (the separate pass + plain dW below).
+    if (wsd_pro_enabled() && mlp_bwd_w_fused(N, K, sizeof(T)) && ld_gz % 4 == 0) {
       TnPro pro2{z, ldz, prelu, nullptr, nullptr, 0};
       pro2.gz = reinterpret_cast<float*>(g_z);
       pro2.ldgz = ld_gz;
