@@ -53,7 +53,9 @@ BITWISE_EQUAL_TO_DEFAULT = ("slab2pass", "agg_nq2", "agg_pipe", "agg_notail", "x
 # Scalar / column-sum gradients a variant regroups: the dX kernel's eps-gradient partials (one per tile in k_nt2, one
 # per workgroup in the weight-stationary k_ws_f32) and the bias / PReLU-slope sums (per workgroup in the fused
 # weight-stationary dW, per row block in k_rows_bwd<0>).  Everything else must stay bit-identical.
-REGROUPED = {"nt2_on": (".conv.eps",), "wsd_pro_off": (".mlp.0.bias", ".mlp.1.weight")}
+# (wsd_pro_off: every Linear bias / PReLU slope behind a fused PReLU backward — GIN MLPs and readout layers alike —
+# is summed per row block by the separate pass instead of per workgroup of the fused dW)
+REGROUPED = {"nt2_on": (".conv.eps",), "wsd_pro_off": (".0.bias", ".1.weight")}
 
 _results = {}
 
