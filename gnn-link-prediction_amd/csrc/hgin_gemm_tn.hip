@@ -110,25 +110,24 @@ using bf16x8 = __attribute__((ext_vector_type(8))) __bf16;
 // kSplit: fp32 operands on the bf16 matrix cores (hgin_common.h split4): the transposed column runs of 4 m
 // are written as three bf16 planes ([col][3 x 32 m + pad] rows of kSplitRowWords words) and a lane reads
 // 8 consecutive m of a plane (one 16-deep k-block) per ds_read_b128.
-// kPro: A = g_y and the PReLU-backward prologue above (TnPro).  kNoSums (a launch over the K tiles after the
+// kPro: A = g_y and the PReLU-backward prologue above (TnPro).  kNoSums (the workgroups of the K tiles after the
 // first): g_z is formed but the bias / slope sums, which only the first K tile's workgroups keep, are not — 3 of the
-// 6 VALU ops per A element, skipped by 3 of 4 workgroups at K = 512 (a runtime branch on the K tile instead made
-// the kernel spill).  kGz: the first K tile's workgroups also store the
+// 6 VALU ops per A element, skipped by 3 of 4 workgroups at K = 512.  The kernel (k_gemm_tn_partial, kDual) picks
+// one of two inlined bodies per workgroup; a branch on the K tile inside the prologue instead made it spill, and two
+// launches (first K tile, then the rest) left most CUs idle in each.  kGz: the first K tile's workgroups also store the
 // g_z they form (TnPro::gz; its own instantiation: the store code in the others made the kLateZ kernel spill, 38
 // scratch ops, fused dW 6.6 -> 8.7 ms per cfg3 layer-0 launch).  kLateZ: z is loaded when the stage is
 // written to LDS instead of with the register prefetch (16 fewer VGPRs live across the MFMA cluster).
-template <bool kClean, int TNR, bool kSplit, bool kPro, bool kLateZ = false, bool kGz = false, bool kNoSums = false>
-__global__ __launch_bounds__(256, (kPro && !kLateZ) ? 2 : 3) void k_gemm_tn_partial(const float* __restrict__ A, int64_t lda,
-                                                            const float* __restrict__ B1, int64_t ldb1,
-                                                            const float* __restrict__ B2, int64_t ldb2, int64_t K1,
-                                                            int64_t M, int64_t N, int64_t K, int64_t rows_per_split,
-                                                            bool vec, float* __restrict__ slab, TnGrid grid,
-                                                            TnPro pro) {
+template <bool kClean, int TNR, bool kSplit, bool kPro, bool kLateZ, bool kGz, bool kNoSums>
+__device__ __forceinline__ void tn_partial_body(const float* __restrict__ A, int64_t lda, const float* __restrict__ B1,
+                                                int64_t ldb1, const float* __restrict__ B2, int64_t ldb2, int64_t K1,
+                                                int64_t M, int64_t N, int64_t K, int64_t rows_per_split, bool vec,
+                                                float* __restrict__ slab, const TnPro& pro, float* smem,
+                                                const TnWork& work) {
   constexpr int WGN = TNR == 128 ? 2 : 4;        // waves along K
   constexpr int BMN = TNR == 128 ? 2 : 1;        // 32 x 32 MFMA blocks per wave along N
   constexpr int BMK = TNR == 128 ? 2 : 1;        // ... and along K
   constexpr int kRowW = kSplit ? kSplitRowWords : kTnLd;
-  __shared__ __attribute__((aligned(16))) float smem[(TNR + 128) * kRowW];
   float* At = smem;                  // [n][m]
   float* Bt = smem + TNR * kRowW;    // [k][m]
   uint32_t* Ath = reinterpret_cast<uint32_t*>(At);
@@ -138,8 +137,6 @@ __global__ __launch_bounds__(256, (kPro && !kLateZ) ? 2 : 3) void k_gemm_tn_part
   const int wave = tid >> 6;
   const int wm = wave / WGN, wn = wave % WGN;
   const int li = lane & 31, lh = lane >> 5;
-  const TnWork work = tn_work(grid);
-  if (!work.valid) return;
   const int64_t n0 = work.n0;
   const int64_t k0 = work.k0;
   const int64_t mb = work.split * rows_per_split;
@@ -430,6 +427,25 @@ __global__ __launch_bounds__(256, (kPro && !kLateZ) ? 2 : 3) void k_gemm_tn_part
         if (n < N) out[n * K + k] = acc[tm][tn][e];
       }
     }
+}
+
+template <bool kClean, int TNR, bool kSplit, bool kPro, bool kLateZ = false, bool kGz = false, bool kDual = false>
+__global__ __launch_bounds__(256, (kPro && !kLateZ) ? 2 : 3) void k_gemm_tn_partial(const float* __restrict__ A, int64_t lda,
+                                                            const float* __restrict__ B1, int64_t ldb1,
+                                                            const float* __restrict__ B2, int64_t ldb2, int64_t K1,
+                                                            int64_t M, int64_t N, int64_t K, int64_t rows_per_split,
+                                                            bool vec, float* __restrict__ slab, TnGrid grid,
+                                                            TnPro pro) {
+  constexpr int kRowW = kSplit ? kSplitRowWords : kTnLd;
+  __shared__ __attribute__((aligned(16))) float smem[(TNR + 128) * kRowW];
+  const TnWork work = tn_work(grid);
+  if (!work.valid) return;
+  if (kDual && work.k0 != 0)   // workgroup-uniform
+    tn_partial_body<kClean, TNR, kSplit, kPro, kLateZ, kGz, true>(A, lda, B1, ldb1, B2, ldb2, K1, M, N, K,
+                                                                   rows_per_split, vec, slab, pro, smem, work);
+  else
+    tn_partial_body<kClean, TNR, kSplit, kPro, kLateZ, kGz, false>(A, lda, B1, ldb1, B2, ldb2, K1, M, N, K,
+                                                                    rows_per_split, vec, slab, pro, smem, work);
 }
 
 // Small weight gradients (N or K < 16, e.g. the readout head Linear(32, 1)): no MFMA tile to fill, so a
@@ -1766,19 +1782,9 @@ int gemm_tn_impl(const char* what, const T* a, int64_t lda, const T* b1, int64_t
   if (clean) { HGIN_TN_PRO(true, TNR, SPLIT) } else { HGIN_TN_PRO(false, TNR, SPLIT) }
     const int64_t kts = ceil_div(K, 128);
     if (pro_in && !pro_in->gz && late && clean && split && tile_n == 128 && kts > 1 && tn_nosums_enabled()) {
-      // the first K tile (g_z + the bias / slope sums), then the others (g_z alone) as a second launch
-      TnGrid t1 = tg, t2 = tg;
-      t1.tiles = tiles_n;
-      t1.n_work = tiles_n * S_eff;
-      t2.tiles = tiles_n * (kts - 1);
-      t2.n_work = t2.tiles * S_eff;
-      t2.kt0 = 1;
-      k_gemm_tn_partial<true, 128, true, true, true, false, false>
-          <<<(unsigned)(t1.xcd ? round_up8(t1.n_work) : t1.n_work), 256, 0, s>>>(a, lda, b1, ldb1, b2, ldb2, k1, M, N,
-                                                                                K, rows, vec, slab, t1, pro);
-      k_gemm_tn_partial<true, 128, true, true, true, false, true>
-          <<<(unsigned)(t2.xcd ? round_up8(t2.n_work) : t2.n_work), 256, 0, s>>>(a, lda, b1, ldb1, b2, ldb2, k1, M, N,
-                                                                                K, rows, vec, slab, t2, pro);
+      // one launch; the workgroups past the first K tile run the body without the bias / slope sums
+      k_gemm_tn_partial<true, 128, true, true, true, false, true><<<grid, 256, 0, s>>>(
+          a, lda, b1, ldb1, b2, ldb2, k1, M, N, K, rows, vec, slab, tg, pro);
     } else if (tile_n == 32) {
       if (split) { HGIN_TN_CLEAN(32, true) } else { HGIN_TN_CLEAN(32, false) }
     } else {
