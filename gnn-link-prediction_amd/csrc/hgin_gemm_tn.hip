@@ -1611,11 +1611,13 @@ int64_t tn_target_wgs() {
 
 // Fused PReLU-backward prologue: z loaded with the register prefetch (2 waves / SIMD, the extra 16-32 live
 // VGPRs) or at LDS-store time (3 waves / SIMD for fp32).  HGIN_TN_LATEZ=0/1.
-// HGIN_TN_NOSUMS=0: the fused dW in one launch, every workgroup keeping the (unused) bias / slope sums
+// HGIN_TN_NOSUMS=1: the fused dW's workgroups past the first K tile skip the bias / slope sums (kDual).  Measured, not
+// adopted: bit-identical but 6.87 vs 6.71 ms per cfg3 layer-0 launch (the two inlined bodies cost the kernel its
+// register headroom: 168 VGPRs and a small spill), profiles/r03/rocprofv3_summary_cfg3_s9.txt.
 bool tn_nosums_enabled() {
   static const bool on = [] {
     const char* v = getenv("HGIN_TN_NOSUMS");
-    return !(v && v[0] == '0');
+    return v && v[0] == '1';
   }();
   return on;
 }

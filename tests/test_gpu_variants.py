@@ -44,11 +44,11 @@ VARIANTS = {
     "agg_lds16": {"HGIN_AGG_LDS": "1", "HGIN_AGG_LDS_D": "16"},
     "wsd_pro_off": {"HGIN_WSD_PRO": "0"},
     "nt_bdma_off": {"HGIN_NT_BDMA": "0"},
-    "tn_nosums_off": {"HGIN_TN_NOSUMS": "0"},
+    "tn_nosums_on": {"HGIN_TN_NOSUMS": "1"},
     "f32_h2": {"HGIN_F32_GEMM": "h2"},
 }
 BITWISE_EQUAL_TO_DEFAULT = ("slab2pass", "agg_nq2", "agg_pipe", "agg_notail", "xcd_off", "nt2_on", "agg_nt_all", "gemm_nt_io",
-                            "agg_lds8", "agg_lds16", "wsd_pro_off", "nt_bdma_off", "tn_nosums_off")
+                            "agg_lds8", "agg_lds16", "wsd_pro_off", "nt_bdma_off", "tn_nosums_on")
 
 # Scalar / column-sum gradients a variant regroups: the dX kernel's eps-gradient partials (one per tile in k_nt2, one
 # per workgroup in the weight-stationary k_ws_f32) and the bias / PReLU-slope sums (per workgroup in the fused
