@@ -372,7 +372,7 @@ __device__ __forceinline__ void tile_partial(float* smem, float ep, float* part,
 // the first barrier of a K-tile step and awaited (vmcnt 0) before the second: the A split pass between them hides its
 // latency.  No B split VALU (a quarter of the loop's VALU at K = 512, N = 256), no B prefetch registers.
 template <int EPI, bool kClean, int TN, int WNv, bool kSplit, int NW = 4, bool kBdma = false>
-__global__ __launch_bounds__(NW * 64, NW == 8 ? 2 : 3) void k_gemm_nt(Src2 A, Src2 B, int64_t M, int64_t N, int64_t K,
+__global__ __launch_bounds__(NW * 64, TN == 4 ? 1 : (NW == 8 ? 2 : 3)) void k_gemm_nt(Src2 A, Src2 B, int64_t M, int64_t N, int64_t K,
                                                     const float* __restrict__ bias, const float* __restrict__ prelu,
                                                     const float* __restrict__ accum, float* __restrict__ Z,
                                                     float* __restrict__ Y, int64_t ldc, bool vec_out,
@@ -539,6 +539,145 @@ bool nt_bdma_enabled() {
   return on;
 }
 
+// k_nt_pipe — the fp32 split-mode NT GEMM for N a multiple of 256 and K a multiple of 64 (the first layer's K = 512
+// forward of cfg3) as a software pipeline at one 4-wave workgroup per CU (one wave per SIMD, 512 registers: the
+// 64 x 128 accumulator tile of each wave lives in AGPRs):
+//   * 128 x 256 tiles — A (fp32, read once from HBM: the whole N = 256 in one tile) is split once per tile;
+//   * B arrives pre-split (hgin_nt_planes_f32: the per-stage rows are the LDS image's rows), so staging it is
+//     plain 16-B copies — no B split VALU;
+//   * two LDS stage buffers (2 x 72 KB, two distinct __shared__ arrays so the compiler knows that the staging
+//     stores of K-tile t + 1 and the fragment reads of K-tile t do not alias) and register prefetch one K-tile ahead:
+//     step t splits and stores tile t + 1 into one buffer while the MFMAs of tile t read the other, then ONE barrier.
+//     The split VALU of t + 1 and the MFMAs of t are in one basic block, free to interleave (the PMC of the 3-wave
+//     register-staged kernel, profiles/r03/gemm_pmc_k512.txt: its VALU and MFMA time add up to 95 % of the SIMD
+//     cycles, i.e. they hardly overlap).
+// Products, k order per accumulator and the epilogue are k_gemm_nt's: bit-identical to it.
+template <int EPI>
+__global__ __launch_bounds__(256, 1) void k_nt_pipe(Src2 A, int64_t M, int64_t N, int64_t K,
+                                                   const float* __restrict__ bias, const float* __restrict__ prelu,
+                                                   const float* __restrict__ accum, float* __restrict__ Z,
+                                                   float* __restrict__ Y, int64_t ldc, bool vec_out, int64_t n_tiles,
+                                                   bool xcd, CombEpi ce, const uint16_t* __restrict__ Bp) {
+  constexpr int NT = 256, TN = 4, WN = 2, BM = 128, BN = 256, WCOLS = 128;
+  constexpr int kRowW = kSplitRowWordsNT;
+  constexpr int kBufW = (BM + BN) * kRowW;          // 18432 words = 72 KB per stage buffer
+  constexpr int kBCh = BN * kRowW / 4 / NT;         // 16-B B chunks per thread per K-tile (12)
+  __shared__ __attribute__((aligned(16))) float smem0[kBufW];
+  __shared__ __attribute__((aligned(16))) float smem1[kBufW];
+  uint32_t* A0 = reinterpret_cast<uint32_t*>(smem0);
+  uint32_t* B0 = A0 + BM * kRowW;
+  uint32_t* A1 = reinterpret_cast<uint32_t*>(smem1);
+  uint32_t* B1 = A1 + BM * kRowW;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wm = wave / WN;
+  const int wn = wave % WN;
+  const int li = lane & 31;
+  const int lh = lane >> 5;
+  const int64_t n_tiles_n = N / BN;
+  const int64_t q = xcd ? xcd_logical(blockIdx.x, gridDim.x) : (int64_t)blockIdx.x;
+  if (q >= n_tiles) return;
+  const int64_t m0 = (q / n_tiles_n) * BM;
+  const int64_t n0 = (q % n_tiles_n) * BN;
+
+  f32x16 acc[2][TN];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < TN; ++b)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[a][b][e] = 0.0f;
+
+  // B: thread tid stages image row tid (12 chunks: plane w / 4, slot w % 4 = the planes' stage row (n0 + tid, plane),
+  // byte w % 4 * 16), so its sources are one base plus compile-time / uniform offsets (no per-chunk address
+  // registers); the row-per-lane LDS stores (192-B stride) are 4-way bank-conflicted, 12 per K-tile
+  static_assert(BN == NT, "one B row per thread");
+  const int64_t stage_bytes = 3 * N * 64;
+  const int64_t plane_bytes = N * 64;
+  const char* brow = reinterpret_cast<const char*>(Bp) + (n0 + tid) * 64;
+  float4 ra[BM / 32];
+  using u4x4 = __attribute__((ext_vector_type(16))) unsigned int;
+  u4x4 rb0, rb1, rb2;   // the row's three 64-B plane segments (as arrays of uint4 they were demoted to scratch)
+  static_assert(kBCh == 12, "three planes x four 16-B chunks");
+  const float sc2 = self_scale(A.eps2);
+  bool scale_a = false;
+  const int64_t T = K / kBK;
+  auto load = [&](int64_t t) {   // K-tile t (clamped: the pipeline's last prefetch re-reads the last tile)
+    t = t < T ? t : T - 1;
+    const int64_t k0 = t * kBK;
+    load_tile<true, BM, NT>(ra, A, m0, M, k0, K, tid, sc2);
+    scale_a = A.eps2 != nullptr && k0 >= A.k1;
+    const char* base = brow + t * stage_bytes;
+    rb0 = *reinterpret_cast<const u4x4*>(base);
+    rb1 = *reinterpret_cast<const u4x4*>(base + plane_bytes);
+    rb2 = *reinterpret_cast<const u4x4*>(base + 2 * plane_bytes);
+  };
+  auto stage = [&](uint32_t* As, uint32_t* Bs) {
+    if (scale_a) scale_tile<BM, NT>(ra, sc2);
+    store_tile_split<BM, NT>(As, ra, tid);
+    *reinterpret_cast<u4x4*>(Bs + tid * kRowW) = rb0;
+    *reinterpret_cast<u4x4*>(Bs + tid * kRowW + 16) = rb1;
+    *reinterpret_cast<u4x4*>(Bs + tid * kRowW + 32) = rb2;
+  };
+  auto mma = [&](const uint32_t* As, const uint32_t* Bs) {
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb) {
+      bf16x8 fa[2][3], fb[TN][3];
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int p = 0; p < 3; ++p)
+          fa[t][p] = *reinterpret_cast<const bf16x8*>(As + (wm * 64 + t * 32 + li) * kRowW + p * 16 +
+                                                      nt_chunk(li, kb * 2 + lh));
+#pragma unroll
+      for (int t = 0; t < TN; ++t)
+#pragma unroll
+        for (int p = 0; p < 3; ++p)
+          fb[t][p] = *reinterpret_cast<const bf16x8*>(Bs + (wn * WCOLS + t * 32 + li) * kRowW + p * 16 +
+                                                      nt_chunk(li, kb * 2 + lh));
+#pragma unroll
+      for (int tm = 0; tm < 2; ++tm)
+#pragma unroll
+        for (int tn = 0; tn < TN; ++tn) {   // k_gemm_nt's order: smallest terms first
+          acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[tm][2], fb[tn][0], acc[tm][tn], 0, 0, 0);
+          acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[tm][1], fb[tn][1], acc[tm][tn], 0, 0, 0);
+          acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[tm][0], fb[tn][2], acc[tm][tn], 0, 0, 0);
+          acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[tm][1], fb[tn][0], acc[tm][tn], 0, 0, 0);
+          acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[tm][0], fb[tn][1], acc[tm][tn], 0, 0, 0);
+          acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[tm][0], fb[tn][0], acc[tm][tn], 0, 0, 0);
+        }
+    }
+  };
+  load(0);
+  stage(A0, B0);
+  load(1);
+  __syncthreads();
+  for (int64_t t = 0; t < T; t += 2) {   // T even: tile t from buffer 0, tile t + 1 from buffer 1
+    stage(A1, B1);                        // tile t + 1
+    load(t + 2);
+    mma(A0, B0);                          // tile t
+    __syncthreads();
+    stage(A0, B0);                        // tile t + 2 (clamped at the end: unused)
+    load(t + 3);
+    mma(A1, B1);                          // tile t + 1
+    __syncthreads();
+  }
+  float ep = 0.0f;
+  epilogue<EPI, TN, float>(acc, smem0, wave, wm, wn, lane, li, lh, m0, n0, M, N, bias, prelu, accum, Z, Y, ldc,
+                           vec_out, ce, &ep);
+  if constexpr (EPI == 4) tile_partial(smem0, ep, ce.part, q);
+}
+
+// HGIN_NT_TN4: 1 = the register-staged kernel at 128 x 256 (one workgroup per CU); 2 = k_nt_pipe
+int nt_tn4_mode() {
+  static const int v = [] {
+    const char* e = getenv("HGIN_NT_TN4");
+    return e ? atoi(e) : 0;
+  }();
+  return v;
+}
+
 template <int EPI, int TN, int WN, int NW = 4>
 int64_t launch_nt_tn(bool vec, const Src2& a, const Src2& b, int64_t M, int64_t N, int64_t K, const float* bias,
                      const float* prelu, const float* accum, float* z, float* y, int64_t ldc, bool vec_out,
@@ -549,6 +688,25 @@ int64_t launch_nt_tn(bool vec, const Src2& a, const Src2& b, int64_t M, int64_t 
   const bool xcd = xcd_remap_enabled();
   dim3 grid((unsigned)(xcd ? round_up8(tiles) : tiles));
   if constexpr (TN == 2 && WN == 2 && NW == 4) {
+    // 128 x 256 tiles (A read once at N = 256; one workgroup per CU): HGIN_NT_TN4=1 the register-staged kernel,
+    // 2 the software pipeline k_nt_pipe (K a multiple of 64)
+    const int tn4 = nt_tn4_mode();
+    if (tn4 && planes && vec && gemm_split_enabled() && !gemm_h2_enabled() && N % 256 == 0 && nt_bdma_enabled() &&
+        (tn4 == 1 || K % 64 == 0) && (int64_t)N * K * 6 < (int64_t(1) << 32)) {
+      const int64_t t4 = ceil_div(N, 256) * ceil_div(M, 128);
+      dim3 g4((unsigned)(xcd ? round_up8(t4) : t4));
+      if (tn4 == 2) {
+        HGIN_TRACE("k_nt_pipe<EPI%d,128x256,N%lld,K%lld>", EPI, (long long)N, (long long)K);
+        k_nt_pipe<EPI><<<g4, 256, 0, s>>>(a, M, N, K, bias, prelu, accum, z, y, ldc, vec_out, t4, xcd, ce,
+                                          static_cast<const uint16_t*>(planes));
+      } else {
+        HGIN_TRACE("k_gemm_nt<EPI%d,128x256,split_bdma,N%lld,K%lld>", EPI, (long long)N, (long long)K);
+        k_gemm_nt<EPI, true, 4, 2, true, 4, true><<<g4, 256, 0, s>>>(a, b, M, N, K, bias, prelu, accum, z, y, ldc,
+                                                                     vec_out, t4, xcd, ce,
+                                                                     static_cast<const uint16_t*>(planes));
+      }
+      return t4;
+    }
     if (planes && vec && gemm_split_enabled() && !gemm_h2_enabled() && N % BN == 0 && nt_bdma_enabled() &&
         (int64_t)N * K * 6 < (int64_t(1) << 32)) {
       HGIN_TRACE("k_gemm_nt<EPI%d,%dx%d,split_bdma,N%lld,K%lld>", EPI, BM, BN, (long long)N, (long long)K);
