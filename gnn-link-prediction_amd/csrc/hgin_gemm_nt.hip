@@ -371,13 +371,18 @@ __device__ __forceinline__ void tile_partial(float* smem, float ep, float* part,
 // image is copied HBM/L2 -> LDS by global_load_lds_dwordx4 (inline asm, per-lane source addresses), issued after
 // the first barrier of a K-tile step and awaited (vmcnt 0) before the second: the A split pass between them hides its
 // latency.  No B split VALU (a quarter of the loop's VALU at K = 512, N = 256), no B prefetch registers.
-template <int EPI, bool kClean, int TN, int WNv, bool kSplit, int NW = 4, bool kBdma = false>
-__global__ __launch_bounds__(NW * 64, TN == 4 ? 1 : (NW == 8 ? 2 : 3)) void k_gemm_nt(Src2 A, Src2 B, int64_t M, int64_t N, int64_t K,
+//
+// kApl > 0 (with kBdma; its value = workgroups per CU): the A operand comes pre-split as well — row images (hgin_a_planes_f32: [M][K / 32][192 B], each
+// 192-B record exactly the LDS image row of that row's K-tile, chunk swizzle included), prefetched into registers as
+// six 16-B chunks per thread per K-tile and stored to LDS unchanged: no split VALU in the loop at all.
+template <int EPI, bool kClean, int TN, int WNv, bool kSplit, int NW = 4, bool kBdma = false, int kApl = 0>
+__global__ __launch_bounds__(NW * 64, TN == 4 ? 1 : (NW == 8 ? 2 : (kApl ? kApl : 3))) void k_gemm_nt(Src2 A, Src2 B, int64_t M, int64_t N, int64_t K,
                                                     const float* __restrict__ bias, const float* __restrict__ prelu,
                                                     const float* __restrict__ accum, float* __restrict__ Z,
                                                     float* __restrict__ Y, int64_t ldc, bool vec_out,
                                                     int64_t n_tiles, bool xcd, CombEpi ce,
-                                                    const uint16_t* __restrict__ Bp = nullptr) {
+                                                    const uint16_t* __restrict__ Bp = nullptr,
+                                                    const uint8_t* __restrict__ Ap = nullptr) {
   constexpr int NT = NW * 64;             // threads
   constexpr int WN = WNv;                 // waves along N
   constexpr int WM = NW / WN;             // waves along M
@@ -414,12 +419,27 @@ __global__ __launch_bounds__(NW * 64, TN == 4 ? 1 : (NW == 8 ? 2 : 3)) void k_ge
 #pragma unroll
       for (int e = 0; e < 16; ++e) acc[a][b][e] = 0.0f;
 
-  float4 ra[BM / (NT / 8)], rb[(BN >= NT / 8 && !kBdma) ? BN / (NT / 8) : 1];
+  float4 ra[kApl ? 1 : BM / (NT / 8)], rb[(BN >= NT / 8 && !kBdma) ? BN / (NT / 8) : 1];
+  constexpr int kAInst = kApl ? BM * 12 / NT : 1;             // 16-B A-image chunks per thread per K-tile
+  static_assert(!kApl || (kBdma && (BM * 12) % NT == 0), "kApl shape");
+  using u32x4 = __attribute__((ext_vector_type(4))) unsigned int;
+  u32x4 rap[kAInst];
   const float sc2 = self_scale(A.eps2);
   bool scale_a = false;   // ra holds a clean p2 tile still to be scaled by sc2
   auto load_a = [&](int64_t k0) {
-    load_tile<kClean, BM, NT>(ra, A, m0, M, k0, K, tid, sc2);
-    scale_a = kClean && A.eps2 != nullptr && k0 >= A.k1;
+    if constexpr (kApl) {
+      const int64_t kts = K / kBK;
+#pragma unroll
+      for (int i = 0; i < kAInst; ++i) {
+        const int j = tid + NT * i;
+        int64_t gr = m0 + j / 12;
+        gr = gr < M ? gr : M - 1;
+        rap[i] = *reinterpret_cast<const u32x4*>(Ap + (gr * kts + k0 / kBK) * 192 + (j % 12) * 16);
+      }
+    } else {
+      load_tile<kClean, BM, NT>(ra, A, m0, M, k0, K, tid, sc2);
+      scale_a = kClean && A.eps2 != nullptr && k0 >= A.k1;
+    }
   };
   constexpr int kBChunks = BN * kSplitRowWordsNT / 4;       // 16-B chunks of the B image
   constexpr int kBInst = kBdma ? kBChunks / 64 / NW : 1;    // LDS-DMA instructions per wave per K-tile
@@ -442,13 +462,21 @@ __global__ __launch_bounds__(NW * 64, TN == 4 ? 1 : (NW == 8 ? 2 : 3)) void k_ge
     }
   };
   auto stage = [&]() {
-    if (scale_a) scale_tile<BM, NT>(ra, sc2);
-    if constexpr (kSplit) {
-      store_tile_split<BM, NT>(Ash, ra, tid);
-      if constexpr (!kBdma) store_tile_split<BN, NT>(Bsh, rb, tid);
+    if constexpr (kApl) {
+#pragma unroll
+      for (int i = 0; i < kAInst; ++i) {
+        const int j = tid + NT * i;
+        *reinterpret_cast<u32x4*>(reinterpret_cast<char*>(Ash) + (j / 12) * 192 + (j % 12) * 16) = rap[i];
+      }
     } else {
-      store_tile<BM, NT>(As, ra, tid);
-      store_tile<BN, NT>(Bs, rb, tid);
+      if (scale_a) scale_tile<BM, NT>(ra, sc2);
+      if constexpr (kSplit) {
+        store_tile_split<BM, NT>(Ash, ra, tid);
+        if constexpr (!kBdma) store_tile_split<BN, NT>(Bsh, rb, tid);
+      } else {
+        store_tile<BM, NT>(As, ra, tid);
+        store_tile<BN, NT>(Bs, rb, tid);
+      }
     }
   };
   load_a(0);
@@ -2765,4 +2793,67 @@ extern "C" int hgin_nt_planes_f32(const float* b, int64_t ldb, int64_t N, int64_
 
 extern "C" int hgin_nt_planes_bf16(const uint16_t* b, int64_t ldb, int64_t N, int64_t K, void* out, void* stream) {
   return nt_planes<uint16_t>(b, ldb, N, K, out, as_stream(stream), "hgin_nt_planes_bf16");
+}
+
+// ---- pre-split A operand (k_gemm_nt<..., kApl>) --------------------------------------------------------------
+namespace hgin {
+namespace {
+// A row images: [M][K / 32][192 B]; record (r, kt) holds plane p's logical 16-B chunk c (k = 32 kt + 8 c .. + 7) at
+// slot 4 p + (c ^ ((r >> 2) & 3)) — exactly the LDS image row k_gemm_nt's split mode stages for that K-tile.
+__global__ __launch_bounds__(256) void k_a_planes(const float* __restrict__ a, int64_t lda, int64_t M, int64_t K,
+                                                  uint8_t* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;   // (row, K-tile, chunk)
+  const int64_t kts = K / kBK;
+  if (i >= M * kts * 4) return;
+  const int c = (int)(i & 3);
+  const int64_t kt = (i >> 2) % kts;
+  const int64_t r = (i >> 2) / kts;
+  const float* src = a + r * lda + kt * kBK + c * 8;
+  uint2 x[3], y[3];
+  split4(*reinterpret_cast<const float4*>(src), x);
+  split4(*reinterpret_cast<const float4*>(src + 4), y);
+  uint8_t* rec = out + (r * kts + kt) * 192;
+  const int slot = c ^ (int)((r >> 2) & 3);
+#pragma unroll
+  for (int p = 0; p < 3; ++p)
+    *reinterpret_cast<uint4*>(rec + (4 * p + slot) * 16) = make_uint4(x[p].x, x[p].y, y[p].x, y[p].y);
+}
+}  // namespace
+}  // namespace hgin
+
+using namespace hgin;
+
+extern "C" int hgin_a_planes_f32(const float* a, int64_t lda, int64_t M, int64_t K, void* out, void* stream) {
+  HGIN_ARG_CHECK(a && out && M >= 0 && K % kBK == 0 && lda % 4 == 0 && aligned16(a), "hgin_a_planes_f32: bad args");
+  const int64_t n = M * (K / kBK) * 4;
+  if (n == 0) return HGIN_OK;
+  k_a_planes<<<dim3((unsigned)ceil_div(n, 256)), 256, 0, as_stream(stream)>>>(a, lda, M, K,
+                                                                               static_cast<uint8_t*>(out));
+  return check_launch("hgin_a_planes_f32");
+}
+
+// y = prelu(A W^T + b) [+ accum] with A as hgin_a_planes_f32 row images and W as hgin_nt_planes_f32 planes
+extern "C" int hgin_gin_mlp_fwd_apl_f32(const void* a_planes, const void* w_planes, const float* bias,
+                                        const float* prelu, const float* accum, float* z, float* y, int64_t M,
+                                        int64_t N, int64_t K, void* stream) {
+  HGIN_ARG_CHECK(a_planes && w_planes && bias && prelu && y && N % 128 == 0 && K % kBK == 0 && M >= 0,
+                 "hgin_gin_mlp_fwd_apl_f32: bad args");
+  if (M == 0) return HGIN_OK;
+  CombEpi ce{};
+  ce.nt_io = gemm_nt_io(M, N, 4);
+  const int64_t tiles = ceil_div(N, 128) * ceil_div(M, 128);
+  const bool xcd = xcd_remap_enabled();
+  dim3 grid((unsigned)(xcd ? round_up8(tiles) : tiles));
+  static const int occ = [] {
+    const char* v = getenv("HGIN_APL_OCC");
+    return v && v[0] == '3' ? 3 : 2;
+  }();
+  HGIN_TRACE("k_gemm_nt<EPI1,128x128,split_bdma_apl%d,N%lld,K%lld>", occ, (long long)N, (long long)K);
+#define HGIN_APL(O)                                                                                                  \
+  k_gemm_nt<1, true, 2, 2, true, 4, true, O><<<grid, 256, 0, as_stream(stream)>>>(                                   \
+      Src2{nullptr, 0, nullptr, 0, K}, Src2{nullptr, 0, nullptr, 0, K}, M, N, K, bias, prelu, accum, z, y, N, true,  \
+      tiles, xcd, ce, static_cast<const uint16_t*>(w_planes), static_cast<const uint8_t*>(a_planes))
+  if (occ == 3) HGIN_APL(3); else HGIN_APL(2);
+#undef HGIN_APL
+  return check_launch("hgin_gin_mlp_fwd_apl_f32");
 }

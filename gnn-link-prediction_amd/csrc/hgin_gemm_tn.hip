@@ -904,16 +904,12 @@ struct WsdCfg {
   static constexpr int WM = N / 64;                  // waves along n (64 rows each)
   static constexpr int WK = 8 / WM;                  // waves along k
   static constexpr int TK = K / WK / 32;             // 32-col MFMA tiles per wave along k
-  // m rows per block: PRO at N = 256 streams three images per block (g_y, z, B), so it takes 16-row blocks in a
-  // 6-slot ring (5 blocks, 120 KB, in flight) instead of 32-row blocks in 3 slots (2 blocks, 96 KB): 1.40 ms per
-  // cfg5 launch at ≈ 4.6 TB/s with the 3-slot ring
-  static constexpr int BM = (PRO && N >= 256 && K >= 256) ? 16 : 32;
+  static constexpr int BM = 32;                      // m rows per block
   static constexpr int RA = N * 2, RB = K * 2;       // image row bytes
   static constexpr int A_BYTES = BM * RA, B_BYTES = BM * RB;
   static constexpr int Z_BYTES = PRO ? A_BYTES : 0;  // the z image (PRO)
   static constexpr int SLOT = A_BYTES + Z_BYTES + B_BYTES;
-  static constexpr int NST_FIT = 147456 / SLOT;
-  static constexpr int NST = PRO ? (NST_FIT < 6 ? NST_FIT : 6) : 4;
+  static constexpr int NST = PRO ? 3 : 4;
   static constexpr int PA = A_BYTES / 1024 / 8, PB = B_BYTES / 1024 / 8;   // DMA pieces per wave per block
   static constexpr int P = PA + (PRO ? PA : 0) + PB;
   static constexpr int CH = A_BYTES / 16 / NT;       // PRO: A chunks per thread per block = g_z stores per wave
@@ -922,20 +918,16 @@ struct WsdCfg {
 
 // vmcnt bound before block i of a weight-stationary dW ring: the DMA pieces of the (NST - 2) later blocks plus the
 // PRO stores issued after block i's DMA (min(i, NST - 1) blocks' worth: fewer while the ring fills).
-template <int NST, int P, int S, int J = 0>
-__device__ __forceinline__ void wsd_wait_from(int64_t i) {   // vmcnt((NST - 2) P + min(i, NST - 1) S), i >= J
-  if constexpr (J == NST - 1) {
-    wait_vm<(NST - 2) * P + (NST - 1) * S>();
-  } else {
-    if (i == J) wait_vm<(NST - 2) * P + J * S>();
-    else wsd_wait_from<NST, P, S, J + 1>(i);
-  }
-}
 template <int NST, int P, int S>
 __device__ __forceinline__ void wsd_wait(int64_t i) {
-  static_assert((NST - 2) * P + (NST - 1) * S <= 63, "vmcnt is 6 bits");
-  if constexpr (S == 0) wait_vm<(NST - 2) * P>();
-  else wsd_wait_from<NST, P, S>(i);
+  if constexpr (S == 0) {
+    wait_vm<(NST - 2) * P>();
+  } else {
+    static_assert(NST == 2 || NST == 3, "wsd_wait");
+    if (i == 0) wait_vm<(NST - 2) * P>();
+    else if (NST == 3 && i == 1) wait_vm<(NST - 2) * P + S>();
+    else wait_vm<(NST - 2) * P + (NST - 1) * S>();
+  }
 }
 
 __device__ __forceinline__ int wsd_swz(int row) { return ((row & 3) << 2) | ((row >> 2) & 3); }
