@@ -372,17 +372,16 @@ __device__ __forceinline__ void tile_partial(float* smem, float ep, float* part,
 // the first barrier of a K-tile step and awaited (vmcnt 0) before the second: the A split pass between them hides its
 // latency.  No B split VALU (a quarter of the loop's VALU at K = 512, N = 256), no B prefetch registers.
 //
-// kApl > 0 (with kBdma; its value = workgroups per CU): the A operand comes pre-split as well — row images (hgin_a_planes_f32: [M][K / 32][192 B], each
-// 192-B record exactly the LDS image row of that row's K-tile, chunk swizzle included), prefetched into registers as
-// six 16-B chunks per thread per K-tile and stored to LDS unchanged: no split VALU in the loop at all.
-template <int EPI, bool kClean, int TN, int WNv, bool kSplit, int NW = 4, bool kBdma = false, int kApl = 0>
-__global__ __launch_bounds__(NW * 64, TN == 4 ? 1 : (NW == 8 ? 2 : (kApl ? kApl : 3))) void k_gemm_nt(Src2 A, Src2 B, int64_t M, int64_t N, int64_t K,
+// kBdma == 2: the B image is double-buffered in LDS and tile t + 1's DMA is issued at the top of step t, beside the A
+// prefetch, so it lands under step t's MFMAs instead of between the step's two barriers (73.7 KB of LDS: 2 workgroups
+// per CU).
+template <int EPI, bool kClean, int TN, int WNv, bool kSplit, int NW = 4, int kBdma = 0>
+__global__ __launch_bounds__(NW * 64, TN == 4 ? 1 : (NW == 8 || kBdma == 2 ? 2 : 3)) void k_gemm_nt(Src2 A, Src2 B, int64_t M, int64_t N, int64_t K,
                                                     const float* __restrict__ bias, const float* __restrict__ prelu,
                                                     const float* __restrict__ accum, float* __restrict__ Z,
                                                     float* __restrict__ Y, int64_t ldc, bool vec_out,
                                                     int64_t n_tiles, bool xcd, CombEpi ce,
-                                                    const uint16_t* __restrict__ Bp = nullptr,
-                                                    const uint8_t* __restrict__ Ap = nullptr) {
+                                                    const uint16_t* __restrict__ Bp = nullptr) {
   constexpr int NT = NW * 64;             // threads
   constexpr int WN = WNv;                 // waves along N
   constexpr int WM = NW / WN;             // waves along M
@@ -390,7 +389,7 @@ __global__ __launch_bounds__(NW * 64, TN == 4 ? 1 : (NW == 8 ? 2 : (kApl ? kApl 
   constexpr int BN = WN * TN * 32;        // columns per workgroup tile
   constexpr int WCOLS = TN * 32;          // columns per wave
   constexpr int kRowW = kSplit ? kSplitRowWordsNT : kLds;   // 4-B words per LDS row
-  __shared__ __attribute__((aligned(16))) float smem[(BM + BN) * kRowW];
+  __shared__ __attribute__((aligned(16))) float smem[(BM + BN * (kBdma == 2 ? 2 : 1)) * kRowW];
   float* As = smem;
   float* Bs = smem + BM * kRowW;
   uint32_t* Ash = reinterpret_cast<uint32_t*>(As);
@@ -419,27 +418,12 @@ __global__ __launch_bounds__(NW * 64, TN == 4 ? 1 : (NW == 8 ? 2 : (kApl ? kApl 
 #pragma unroll
       for (int e = 0; e < 16; ++e) acc[a][b][e] = 0.0f;
 
-  float4 ra[kApl ? 1 : BM / (NT / 8)], rb[(BN >= NT / 8 && !kBdma) ? BN / (NT / 8) : 1];
-  constexpr int kAInst = kApl ? BM * 12 / NT : 1;             // 16-B A-image chunks per thread per K-tile
-  static_assert(!kApl || (kBdma && (BM * 12) % NT == 0), "kApl shape");
-  using u32x4 = __attribute__((ext_vector_type(4))) unsigned int;
-  u32x4 rap[kAInst];
+  float4 ra[BM / (NT / 8)], rb[(BN >= NT / 8 && !kBdma) ? BN / (NT / 8) : 1];
   const float sc2 = self_scale(A.eps2);
   bool scale_a = false;   // ra holds a clean p2 tile still to be scaled by sc2
   auto load_a = [&](int64_t k0) {
-    if constexpr (kApl) {
-      const int64_t kts = K / kBK;
-#pragma unroll
-      for (int i = 0; i < kAInst; ++i) {
-        const int j = tid + NT * i;
-        int64_t gr = m0 + j / 12;
-        gr = gr < M ? gr : M - 1;
-        rap[i] = *reinterpret_cast<const u32x4*>(Ap + (gr * kts + k0 / kBK) * 192 + (j % 12) * 16);
-      }
-    } else {
-      load_tile<kClean, BM, NT>(ra, A, m0, M, k0, K, tid, sc2);
-      scale_a = kClean && A.eps2 != nullptr && k0 >= A.k1;
-    }
+    load_tile<kClean, BM, NT>(ra, A, m0, M, k0, K, tid, sc2);
+    scale_a = kClean && A.eps2 != nullptr && k0 >= A.k1;
   };
   constexpr int kBChunks = BN * kSplitRowWordsNT / 4;       // 16-B chunks of the B image
   constexpr int kBInst = kBdma ? kBChunks / 64 / NW : 1;    // LDS-DMA instructions per wave per K-tile
@@ -456,27 +440,19 @@ __global__ __launch_bounds__(NW * 64, TN == 4 ? 1 : (NW == 8 ? 2 : (kApl ? kApl 
   auto dma_b = [&](int64_t k0) {
     if constexpr (kBdma) {
       const char* base = reinterpret_cast<const char*>(Bp) + (k0 / kBK) * 3 * N * 64;
+      char* dst = reinterpret_cast<char*>(Bsh) + (kBdma == 2 ? ((k0 / kBK) & 1) * BN * kSplitRowWordsNT * 4 : 0);
 #pragma unroll
-      for (int i = 0; i < kBInst; ++i)
-        glds16_asm(base + boff[i], reinterpret_cast<char*>(Bsh) + (wave * kBInst + i) * 1024);
+      for (int i = 0; i < kBInst; ++i) glds16_asm(base + boff[i], dst + (wave * kBInst + i) * 1024);
     }
   };
   auto stage = [&]() {
-    if constexpr (kApl) {
-#pragma unroll
-      for (int i = 0; i < kAInst; ++i) {
-        const int j = tid + NT * i;
-        *reinterpret_cast<u32x4*>(reinterpret_cast<char*>(Ash) + (j / 12) * 192 + (j % 12) * 16) = rap[i];
-      }
+    if (scale_a) scale_tile<BM, NT>(ra, sc2);
+    if constexpr (kSplit) {
+      store_tile_split<BM, NT>(Ash, ra, tid);
+      if constexpr (!kBdma) store_tile_split<BN, NT>(Bsh, rb, tid);
     } else {
-      if (scale_a) scale_tile<BM, NT>(ra, sc2);
-      if constexpr (kSplit) {
-        store_tile_split<BM, NT>(Ash, ra, tid);
-        if constexpr (!kBdma) store_tile_split<BN, NT>(Bsh, rb, tid);
-      } else {
-        store_tile<BM, NT>(As, ra, tid);
-        store_tile<BN, NT>(Bs, rb, tid);
-      }
+      store_tile<BM, NT>(As, ra, tid);
+      store_tile<BN, NT>(Bs, rb, tid);
     }
   };
   load_a(0);
@@ -490,7 +466,9 @@ __global__ __launch_bounds__(NW * 64, TN == 4 ? 1 : (NW == 8 ? 2 : (kApl ? kApl 
     if (more) {   // next K-tile's global loads stay in flight under this K-tile's MFMAs
       load_a(k0 + kBK);
       if constexpr (!kBdma) load_tile<kClean, BN, NT>(rb, B, n0, N, k0 + kBK, K, tid);
+      if constexpr (kBdma == 2) dma_b(k0 + kBK);   // into the other B buffer (last read in step t - 1)
     }
+    const uint32_t* Bcur = Bsh + (kBdma == 2 ? ((k0 / kBK) & 1) * BN * kSplitRowWordsNT : 0);
     __builtin_amdgcn_s_setprio(1);   // keep the MFMA cluster together (T5)
     if constexpr (kSplit) {
       // two 16-deep k-blocks; lane (i, h) reads k = 16 kb + 8 h .. +7 of each plane (one ds_read_b128)
@@ -507,7 +485,7 @@ __global__ __launch_bounds__(NW * 64, TN == 4 ? 1 : (NW == 8 ? 2 : (kApl ? kApl 
         for (int t = 0; t < TN; ++t)
 #pragma unroll
           for (int p = 0; p < 3; ++p)
-            fb[t][p] = *reinterpret_cast<const bf16x8*>(Bsh + (wn * WCOLS + t * 32 + li) * kSplitRowWordsNT + p * 16 +
+            fb[t][p] = *reinterpret_cast<const bf16x8*>(Bcur + (wn * WCOLS + t * 32 + li) * kSplitRowWordsNT + p * 16 +
                                                         nt_chunk(li, kb * 2 + lh));
 #pragma unroll
         for (int tm = 0; tm < 2; ++tm)
@@ -545,7 +523,7 @@ __global__ __launch_bounds__(NW * 64, TN == 4 ? 1 : (NW == 8 ? 2 : (kApl ? kApl 
     __builtin_amdgcn_s_setprio(0);
     if (more) {
       __syncthreads();
-      dma_b(k0 + kBK);
+      if constexpr (kBdma == 1) dma_b(k0 + kBK);
       stage();
       if constexpr (kBdma) wait_vm<0>();
       __syncthreads();
@@ -556,6 +534,15 @@ __global__ __launch_bounds__(NW * 64, TN == 4 ? 1 : (NW == 8 ? 2 : (kApl ? kApl 
   epilogue<EPI, TN, float>(acc, smem, wave, wm, wn, lane, li, lh, m0, n0, M, N, bias, prelu, accum, Z, Y, ldc,
                            vec_out, ce, &ep);
   if constexpr (EPI == 4) tile_partial(smem, ep, ce.part, q);
+}
+
+// HGIN_NT_BDB=1: the 128 x 128 split-mode tile with B double-buffered (k_gemm_nt<..., kBdma = 2>; A/B)
+bool nt_bdb_enabled() {
+  static const bool on = [] {
+    const char* v = getenv("HGIN_NT_BDB");
+    return v && v[0] == '1';
+  }();
+  return on;
 }
 
 // HGIN_NT_BDMA=0: the 128 x 128 split-mode tile splits B itself even where pre-split planes are passed
@@ -706,6 +693,157 @@ int nt_tn4_mode() {
   return v;
 }
 
+// k_nt_pp — the fp32 split-mode NT GEMM (N a multiple of 128, clean tiles, B pre-split by hgin_nt_planes_f32) as a
+// ping-pong of two 4-wave halves (cdna_hip_programming.md, MI355X_MICROARCH.md "Two waves per SIMD"): one 8-wave
+// workgroup per CU computes a 256 x 128 tile as two 128 x 128 halves that share the B image.  Each SIMD holds one wave
+// of each half, and the halves alternate roles every phase (one raw barrier per phase):
+//   phase a(t): half 0 runs its 48 MFMAs per wave on K-tile t   | half 1 splits + stores its A tile t, issues the
+//                                                                 B DMA of t + 1 and its A loads of t + 1
+//   phase b(t): half 1 runs its MFMAs on K-tile t               | half 0 splits + stores its A tile t + 1 and issues
+//                                                                 its A loads of t + 2
+// so the matrix pipe of every SIMD is fed by one wave while the split VALU, LDS stores and memory issue of the other
+// wave run beside it (the 3-workgroup register-staged tile serialises them: MFMA ~45 % busy, profiles/r03/).  B is
+// double-buffered (the DMA of t + 1 lands under the phases of t); A loads have two phases of cover.
+// Products, per-accumulator k order and the epilogue are k_gemm_nt's: bit-identical to it.
+template <int EPI>
+__global__ __launch_bounds__(512, 1) void k_nt_pp(Src2 A, int64_t M, int64_t N, int64_t K,
+                                                 const float* __restrict__ bias, const float* __restrict__ prelu,
+                                                 const float* __restrict__ accum, float* __restrict__ Z,
+                                                 float* __restrict__ Y, int64_t ldc, bool vec_out, int64_t n_tiles,
+                                                 bool xcd, CombEpi ce, const uint16_t* __restrict__ Bp) {
+  constexpr int RW = kSplitRowWordsNT;            // 48 words per image row
+  constexpr int IMG = 128 * RW;                   // words per 128-row image
+  __shared__ __attribute__((aligned(16))) uint32_t smem[4 * IMG];   // A half 0, A half 1, B buffer 0, B buffer 1
+  const int tid = threadIdx.x;
+  const int t4 = tid & 255;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int half = wave >> 2;
+  const int w4 = wave & 3;
+  const int wm = w4 >> 1, wn = w4 & 1;
+  const int li = lane & 31, lh = lane >> 5;
+  const int64_t n_tiles_n = N / 128;
+  const int64_t q = xcd ? xcd_logical(blockIdx.x, gridDim.x) : (int64_t)blockIdx.x;
+  if (q >= n_tiles) return;
+  const int64_t m0 = (q / n_tiles_n) * 256 + half * 128;   // this half's rows
+  const int64_t n0 = (q % n_tiles_n) * 128;
+  uint32_t* Aimg = smem + half * IMG;
+  uint32_t* Bimg = smem + 2 * IMG;
+  const int T = (int)(K / kBK);
+
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[a][b][e] = 0.0f;
+
+  float4 ra0[4], ra1[4];   // A prefetch two K-tiles deep (tile t in ra<t & 1>)
+  const float sc2 = self_scale(A.eps2);
+  auto load_a = [&](float4 (&r)[4], int t) {
+    load_tile<true, 128, 256>(r, A, m0, M, (int64_t)t * kBK, K, t4, sc2);
+  };
+  auto stage_a = [&](float4 (&r)[4], int t) {
+    if (A.eps2 != nullptr && (int64_t)t * kBK >= A.k1) scale_tile<128, 256>(r, sc2);
+    store_tile_split<128, 256>(Aimg, r, t4);
+  };
+  uint32_t boff[6];
+#pragma unroll
+  for (int i = 0; i < 6; ++i) {
+    const int j = (w4 * 6 + i) * 64 + lane;   // image chunk: row j / 12, word group j % 12
+    const int rr = j / 12, w = j % 12;
+    boff[i] = (uint32_t)((((w >> 2) * N + n0 + rr) * 64) + (w & 3) * 16);
+  }
+  auto dma_b = [&](int t) {   // half 1 only
+    const char* base = reinterpret_cast<const char*>(Bp) + (int64_t)t * 3 * N * 64;
+    char* dst = reinterpret_cast<char*>(Bimg + (t & 1) * IMG) + w4 * 6 * 1024;
+#pragma unroll
+    for (int i = 0; i < 6; ++i) glds16_asm(base + boff[i], dst + i * 1024);
+  };
+  auto mfma_tile = [&](int t) {
+    const uint32_t* Bs = Bimg + (t & 1) * IMG;
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb) {
+      bf16x8 fa[2][3], fb[2][3];
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int p = 0; p < 3; ++p) {
+          fa[u][p] = *reinterpret_cast<const bf16x8*>(Aimg + (wm * 64 + u * 32 + li) * RW + p * 16 +
+                                                      nt_chunk(li, kb * 2 + lh));
+          fb[u][p] = *reinterpret_cast<const bf16x8*>(Bs + (wn * 64 + u * 32 + li) * RW + p * 16 +
+                                                      nt_chunk(li, kb * 2 + lh));
+        }
+#pragma unroll
+      for (int tm = 0; tm < 2; ++tm)
+#pragma unroll
+        for (int tn = 0; tn < 2; ++tn) {   // k_gemm_nt's order: smallest terms first
+          acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[tm][2], fb[tn][0], acc[tm][tn], 0, 0, 0);
+          acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[tm][1], fb[tn][1], acc[tm][tn], 0, 0, 0);
+          acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[tm][0], fb[tn][2], acc[tm][tn], 0, 0, 0);
+          acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[tm][1], fb[tn][0], acc[tm][tn], 0, 0, 0);
+          acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[tm][0], fb[tn][1], acc[tm][tn], 0, 0, 0);
+          acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[tm][0], fb[tn][0], acc[tm][tn], 0, 0, 0);
+        }
+    }
+  };
+
+  // prologue: B(0) by half 1; half 0 stages A(0) and prefetches A(1), A(2); half 1 prefetches A(0), A(1)
+  if (half == 1) dma_b(0);
+  load_a(ra0, 0);
+  if (half == 0) stage_a(ra0, 0);
+  if (T > 1) load_a(ra1, 1);
+  if (half == 0 && T > 2) load_a(ra0, 2);
+  if (half == 1) {   // B(0) landed (the A loads issued after it may still be in flight)
+    if (T > 1) wait_vm<8>();
+    else wait_vm<4>();
+  }
+  __syncthreads();
+  // one K-tile: phase a — half 0 computes tile t, half 1 stages its tile t (from rc), issues B(t + 1) and A(t + 2)
+  // (into rc); phase b — half 1 computes tile t, half 0 stages its tile t + 1 (from rn) and issues A(t + 3) (into rn)
+  auto ktile = [&](int t, float4 (&rc)[4], float4 (&rn)[4]) {
+    if (half == 0) {
+      __builtin_amdgcn_s_setprio(1);
+      mfma_tile(t);
+      __builtin_amdgcn_s_setprio(0);
+    } else {
+      stage_a(rc, t);
+      if (t + 1 < T) dma_b(t + 1);
+      if (t + 2 < T) load_a(rc, t + 2);
+    }
+    __syncthreads();
+    if (half == 1) {
+      __builtin_amdgcn_s_setprio(1);
+      mfma_tile(t);
+      __builtin_amdgcn_s_setprio(0);
+      if (t + 2 < T) wait_vm<4>();        // B(t + 1) landed before half 0 reads it (A(t + 2) may be in flight)
+      else if (t + 1 < T) wait_vm<0>();
+    } else if (t + 1 < T) {
+      stage_a(rn, t + 1);
+      if (t + 3 < T) load_a(rn, t + 3);
+    }
+    __syncthreads();
+  };
+  for (int t = 0; t < T; t += 2) {
+    ktile(t, ra0, ra1);
+    if (t + 1 < T) ktile(t + 1, ra1, ra0);
+  }
+
+  float ep = 0.0f;
+  epilogue<EPI, 2, float>(acc, reinterpret_cast<float*>(smem), wave, wm, wn, lane, li, lh, m0, n0, M, N, bias, prelu,
+                          accum, Z, Y, ldc, vec_out, ce, &ep);
+}
+
+// HGIN_NT_PP=1: k_nt_pp for the fp32 split-mode 128-column tiles (A/B)
+bool nt_pp_enabled() {
+  static const bool on = [] {
+    const char* v = getenv("HGIN_NT_PP");
+    return v && v[0] == '1';
+  }();
+  return on;
+}
+
 template <int EPI, int TN, int WN, int NW = 4>
 int64_t launch_nt_tn(bool vec, const Src2& a, const Src2& b, int64_t M, int64_t N, int64_t K, const float* bias,
                      const float* prelu, const float* accum, float* z, float* y, int64_t ldc, bool vec_out,
@@ -729,7 +867,7 @@ int64_t launch_nt_tn(bool vec, const Src2& a, const Src2& b, int64_t M, int64_t 
                                           static_cast<const uint16_t*>(planes));
       } else {
         HGIN_TRACE("k_gemm_nt<EPI%d,128x256,split_bdma,N%lld,K%lld>", EPI, (long long)N, (long long)K);
-        k_gemm_nt<EPI, true, 4, 2, true, 4, true><<<g4, 256, 0, s>>>(a, b, M, N, K, bias, prelu, accum, z, y, ldc,
+        k_gemm_nt<EPI, true, 4, 2, true, 4, 1><<<g4, 256, 0, s>>>(a, b, M, N, K, bias, prelu, accum, z, y, ldc,
                                                                      vec_out, t4, xcd, ce,
                                                                      static_cast<const uint16_t*>(planes));
       }
@@ -737,10 +875,25 @@ int64_t launch_nt_tn(bool vec, const Src2& a, const Src2& b, int64_t M, int64_t 
     }
     if (planes && vec && gemm_split_enabled() && !gemm_h2_enabled() && N % BN == 0 && nt_bdma_enabled() &&
         (int64_t)N * K * 6 < (int64_t(1) << 32)) {
+      if (EPI != 4 && nt_pp_enabled()) {
+        const int64_t tp = ceil_div(N, 128) * ceil_div(M, 256);
+        dim3 gp((unsigned)(xcd ? round_up8(tp) : tp));
+        HGIN_TRACE("k_nt_pp<EPI%d,256x128,N%lld,K%lld>", EPI, (long long)N, (long long)K);
+        k_nt_pp<EPI><<<gp, 512, 0, s>>>(a, M, N, K, bias, prelu, accum, z, y, ldc, vec_out, tp, xcd, ce,
+                                        static_cast<const uint16_t*>(planes));
+        return tp;
+      }
+      if (nt_bdb_enabled()) {
+        HGIN_TRACE("k_gemm_nt<EPI%d,%dx%d,split_bdma2,N%lld,K%lld>", EPI, BM, BN, (long long)N, (long long)K);
+        k_gemm_nt<EPI, true, 2, 2, true, 4, 2><<<grid, 256, 0, s>>>(a, b, M, N, K, bias, prelu, accum, z, y, ldc,
+                                                                    vec_out, tiles, xcd, ce,
+                                                                    static_cast<const uint16_t*>(planes));
+        return tiles;
+      }
       HGIN_TRACE("k_gemm_nt<EPI%d,%dx%d,split_bdma,N%lld,K%lld>", EPI, BM, BN, (long long)N, (long long)K);
-      k_gemm_nt<EPI, true, 2, 2, true, 4, true><<<grid, 256, 0, s>>>(a, b, M, N, K, bias, prelu, accum, z, y, ldc,
-                                                                     vec_out, tiles, xcd, ce,
-                                                                     static_cast<const uint16_t*>(planes));
+      k_gemm_nt<EPI, true, 2, 2, true, 4, 1><<<grid, 256, 0, s>>>(a, b, M, N, K, bias, prelu, accum, z, y, ldc,
+                                                                  vec_out, tiles, xcd, ce,
+                                                                  static_cast<const uint16_t*>(planes));
       return tiles;
     }
   }
@@ -2795,65 +2948,3 @@ extern "C" int hgin_nt_planes_bf16(const uint16_t* b, int64_t ldb, int64_t N, in
   return nt_planes<uint16_t>(b, ldb, N, K, out, as_stream(stream), "hgin_nt_planes_bf16");
 }
 
-// ---- pre-split A operand (k_gemm_nt<..., kApl>) --------------------------------------------------------------
-namespace hgin {
-namespace {
-// A row images: [M][K / 32][192 B]; record (r, kt) holds plane p's logical 16-B chunk c (k = 32 kt + 8 c .. + 7) at
-// slot 4 p + (c ^ ((r >> 2) & 3)) — exactly the LDS image row k_gemm_nt's split mode stages for that K-tile.
-__global__ __launch_bounds__(256) void k_a_planes(const float* __restrict__ a, int64_t lda, int64_t M, int64_t K,
-                                                  uint8_t* __restrict__ out) {
-  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;   // (row, K-tile, chunk)
-  const int64_t kts = K / kBK;
-  if (i >= M * kts * 4) return;
-  const int c = (int)(i & 3);
-  const int64_t kt = (i >> 2) % kts;
-  const int64_t r = (i >> 2) / kts;
-  const float* src = a + r * lda + kt * kBK + c * 8;
-  uint2 x[3], y[3];
-  split4(*reinterpret_cast<const float4*>(src), x);
-  split4(*reinterpret_cast<const float4*>(src + 4), y);
-  uint8_t* rec = out + (r * kts + kt) * 192;
-  const int slot = c ^ (int)((r >> 2) & 3);
-#pragma unroll
-  for (int p = 0; p < 3; ++p)
-    *reinterpret_cast<uint4*>(rec + (4 * p + slot) * 16) = make_uint4(x[p].x, x[p].y, y[p].x, y[p].y);
-}
-}  // namespace
-}  // namespace hgin
-
-using namespace hgin;
-
-extern "C" int hgin_a_planes_f32(const float* a, int64_t lda, int64_t M, int64_t K, void* out, void* stream) {
-  HGIN_ARG_CHECK(a && out && M >= 0 && K % kBK == 0 && lda % 4 == 0 && aligned16(a), "hgin_a_planes_f32: bad args");
-  const int64_t n = M * (K / kBK) * 4;
-  if (n == 0) return HGIN_OK;
-  k_a_planes<<<dim3((unsigned)ceil_div(n, 256)), 256, 0, as_stream(stream)>>>(a, lda, M, K,
-                                                                               static_cast<uint8_t*>(out));
-  return check_launch("hgin_a_planes_f32");
-}
-
-// y = prelu(A W^T + b) [+ accum] with A as hgin_a_planes_f32 row images and W as hgin_nt_planes_f32 planes
-extern "C" int hgin_gin_mlp_fwd_apl_f32(const void* a_planes, const void* w_planes, const float* bias,
-                                        const float* prelu, const float* accum, float* z, float* y, int64_t M,
-                                        int64_t N, int64_t K, void* stream) {
-  HGIN_ARG_CHECK(a_planes && w_planes && bias && prelu && y && N % 128 == 0 && K % kBK == 0 && M >= 0,
-                 "hgin_gin_mlp_fwd_apl_f32: bad args");
-  if (M == 0) return HGIN_OK;
-  CombEpi ce{};
-  ce.nt_io = gemm_nt_io(M, N, 4);
-  const int64_t tiles = ceil_div(N, 128) * ceil_div(M, 128);
-  const bool xcd = xcd_remap_enabled();
-  dim3 grid((unsigned)(xcd ? round_up8(tiles) : tiles));
-  static const int occ = [] {
-    const char* v = getenv("HGIN_APL_OCC");
-    return v && v[0] == '3' ? 3 : 2;
-  }();
-  HGIN_TRACE("k_gemm_nt<EPI1,128x128,split_bdma_apl%d,N%lld,K%lld>", occ, (long long)N, (long long)K);
-#define HGIN_APL(O)                                                                                                  \
-  k_gemm_nt<1, true, 2, 2, true, 4, true, O><<<grid, 256, 0, as_stream(stream)>>>(                                   \
-      Src2{nullptr, 0, nullptr, 0, K}, Src2{nullptr, 0, nullptr, 0, K}, M, N, K, bias, prelu, accum, z, y, N, true,  \
-      tiles, xcd, ce, static_cast<const uint16_t*>(w_planes), static_cast<const uint8_t*>(a_planes))
-  if (occ == 3) HGIN_APL(3); else HGIN_APL(2);
-#undef HGIN_APL
-  return check_launch("hgin_gin_mlp_fwd_apl_f32");
-}
