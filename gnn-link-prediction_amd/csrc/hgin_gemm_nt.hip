@@ -240,8 +240,31 @@ struct CombEpi {
 // results in LDS, then writes row-contiguous 4-column groups (bias, PReLU, accum applied on the way out).
 // A lane always owns the same 4 columns, so its bias values are loaded once, and the accum rows it will
 // need are loaded before the LDS round trip: no dependent global load inside the store loop.
-template <int EPI, int TN, typename OutT>
-__device__ __forceinline__ void epilogue(const f32x16 (&acc)[2][TN], float* smem, int wave, int wm, int wn, int lane,
+using f32x4v = __attribute__((ext_vector_type(4))) float;
+
+// C/D layouts: f32x16 acc[2][TN] — 32 x 32 MFMA tiles (row = (reg & 3) + 8 (reg >> 2) + 4 (lane >> 5), col = lane & 31);
+// f32x4v acc[4][2 TN] — 16 x 16 tiles of v_mfma_f32_16x16x32_bf16 (row = 4 (lane >> 4) + reg, col = lane & 15).
+template <int TN>
+__device__ __forceinline__ void park_acc(const f32x16 (&acc)[2][TN], float* Cw, int kLc, int tm, int lane) {
+  const int li = lane & 31, lh = lane >> 5;
+#pragma unroll
+  for (int tn = 0; tn < TN; ++tn)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) Cw[((e & 3) + 8 * (e >> 2) + 4 * lh) * kLc + tn * 32 + li] = acc[tm][tn][e];
+}
+template <int TN2>
+__device__ __forceinline__ void park_acc(const f32x4v (&acc)[4][TN2], float* Cw, int kLc, int tm, int lane) {
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int bn = 0; bn < TN2; ++bn)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        Cw[(j * 16 + 4 * (lane >> 4) + i) * kLc + bn * 16 + (lane & 15)] = acc[2 * tm + j][bn][i];
+}
+
+template <int EPI, int TN, typename OutT, typename AccT = f32x16[2][TN]>
+__device__ __forceinline__ void epilogue(const AccT& acc, float* smem, int wave, int wm, int wn, int lane,
                                          int li, int lh, int64_t m0, int64_t n0, int64_t M, int64_t N,
                                          const float* __restrict__ bias, const float* __restrict__ prelu,
                                          const OutT* __restrict__ accum, OutT* __restrict__ Z, OutT* __restrict__ Y,
@@ -293,10 +316,7 @@ __device__ __forceinline__ void epilogue(const f32x16 (&acc)[2][TN], float* smem
                                  : Out4<OutT>::ld_raw(gp + row * ce.ldgp + (col - ce.cs), full, nv);
       }
     }
-#pragma unroll
-    for (int tn = 0; tn < TN; ++tn)
-#pragma unroll
-      for (int e = 0; e < 16; ++e) Cw[((e & 3) + 8 * (e >> 2) + 4 * lh) * kLc + tn * 32 + li] = acc[tm][tn][e];
+    park_acc(acc, Cw, kLc, tm, lane);
     __syncthreads();
 #pragma unroll
     for (int j = 0; j < kJ; ++j) {
@@ -375,7 +395,10 @@ __device__ __forceinline__ void tile_partial(float* smem, float ep, float* part,
 // kBdma == 2: the B image is double-buffered in LDS and tile t + 1's DMA is issued at the top of step t, beside the A
 // prefetch, so it lands under step t's MFMAs instead of between the step's two barriers (73.7 KB of LDS: 2 workgroups
 // per CU).
-template <int EPI, bool kClean, int TN, int WNv, bool kSplit, int NW = 4, int kBdma = 0>
+//
+// kM16 (split mode): the products as v_mfma_f32_16x16x32_bf16 (16 x 16 tiles, one 32-deep k-step per K-tile) instead of
+// 32 x 32 x 16 — MI355X_MICROARCH.md "DVFS give-back" (7): on random operands the 16 x 16 x 32 shape holds a higher clock.
+template <int EPI, bool kClean, int TN, int WNv, bool kSplit, int NW = 4, int kBdma = 0, bool kM16 = false>
 __global__ __launch_bounds__(NW * 64, TN == 4 ? 1 : (NW == 8 || kBdma == 2 ? 2 : 3)) void k_gemm_nt(Src2 A, Src2 B, int64_t M, int64_t N, int64_t K,
                                                     const float* __restrict__ bias, const float* __restrict__ prelu,
                                                     const float* __restrict__ accum, float* __restrict__ Z,
@@ -417,6 +440,12 @@ __global__ __launch_bounds__(NW * 64, TN == 4 ? 1 : (NW == 8 || kBdma == 2 ? 2 :
     for (int b = 0; b < TN; ++b)
 #pragma unroll
       for (int e = 0; e < 16; ++e) acc[a][b][e] = 0.0f;
+  f32x4v acc16[kM16 ? 4 : 1][kM16 ? 2 * TN : 1];
+#pragma unroll
+  for (int a = 0; a < (kM16 ? 4 : 1); ++a)
+#pragma unroll
+    for (int b = 0; b < (kM16 ? 2 * TN : 1); ++b) acc16[a][b] = f32x4v{0.f, 0.f, 0.f, 0.f};
+  static_assert(!kM16 || kSplit, "kM16 needs split mode");
 
   float4 ra[BM / (NT / 8)], rb[(BN >= NT / 8 && !kBdma) ? BN / (NT / 8) : 1];
   const float sc2 = self_scale(A.eps2);
@@ -470,7 +499,38 @@ __global__ __launch_bounds__(NW * 64, TN == 4 ? 1 : (NW == 8 || kBdma == 2 ? 2 :
     }
     const uint32_t* Bcur = Bsh + (kBdma == 2 ? ((k0 / kBK) & 1) * BN * kSplitRowWordsNT : 0);
     __builtin_amdgcn_s_setprio(1);   // keep the MFMA cluster together (T5)
-    if constexpr (kSplit) {
+    if constexpr (kM16) {
+      // one 32-deep k-step: lane l reads row l & 15 of a 16-row block, k = 8 (l >> 4) .. +7 of each plane
+      const int r16 = lane & 15, c16 = lane >> 4;
+#pragma unroll
+      for (int th = 0; th < 2; ++th) {   // two 32-row halves of the wave tile (bounds the fragment registers)
+        bf16x8 fa[2][3];
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+#pragma unroll
+          for (int p = 0; p < 3; ++p)
+            fa[u][p] = *reinterpret_cast<const bf16x8*>(Ash + (wm * 64 + (2 * th + u) * 16 + r16) * kSplitRowWordsNT +
+                                                        p * 16 + nt_chunk(r16, c16));
+#pragma unroll
+        for (int tn = 0; tn < 2 * TN; ++tn) {
+          bf16x8 fb[3];
+#pragma unroll
+          for (int p = 0; p < 3; ++p)
+            fb[p] = *reinterpret_cast<const bf16x8*>(Bcur + (wn * WCOLS + tn * 16 + r16) * kSplitRowWordsNT + p * 16 +
+                                                     nt_chunk(r16, c16));
+#pragma unroll
+          for (int u = 0; u < 2; ++u) {   // k_gemm_nt's product order: smallest terms first
+            f32x4v& c = acc16[2 * th + u][tn];
+            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[u][2], fb[0], c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[u][1], fb[1], c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[u][0], fb[2], c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[u][1], fb[0], c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[u][0], fb[1], c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[u][0], fb[0], c, 0, 0, 0);
+          }
+        }
+      }
+    } else if constexpr (kSplit) {
       // two 16-deep k-blocks; lane (i, h) reads k = 16 kb + 8 h .. +7 of each plane (one ds_read_b128)
 #pragma unroll
       for (int kb = 0; kb < 2; ++kb) {
@@ -531,9 +591,22 @@ __global__ __launch_bounds__(NW * 64, TN == 4 ? 1 : (NW == 8 || kBdma == 2 ? 2 :
   }
 
   float ep = 0.0f;
-  epilogue<EPI, TN, float>(acc, smem, wave, wm, wn, lane, li, lh, m0, n0, M, N, bias, prelu, accum, Z, Y, ldc,
-                           vec_out, ce, &ep);
+  if constexpr (kM16)
+    epilogue<EPI, TN, float, f32x4v[4][2 * TN]>(acc16, smem, wave, wm, wn, lane, li, lh, m0, n0, M, N, bias, prelu,
+                                                accum, Z, Y, ldc, vec_out, ce, &ep);
+  else
+    epilogue<EPI, TN, float>(acc, smem, wave, wm, wn, lane, li, lh, m0, n0, M, N, bias, prelu, accum, Z, Y, ldc,
+                             vec_out, ce, &ep);
   if constexpr (EPI == 4) tile_partial(smem, ep, ce.part, q);
+}
+
+// HGIN_NT_M16=1: the 128 x 128 split-mode tile (B by LDS-DMA) on v_mfma_f32_16x16x32_bf16 (k_gemm_nt<..., kM16>; A/B)
+bool nt_m16_enabled() {
+  static const bool on = [] {
+    const char* v = getenv("HGIN_NT_M16");
+    return v && v[0] == '1';
+  }();
+  return on;
 }
 
 // HGIN_NT_BDB=1: the 128 x 128 split-mode tile with B double-buffered (k_gemm_nt<..., kBdma = 2>; A/B)
@@ -888,6 +961,13 @@ int64_t launch_nt_tn(bool vec, const Src2& a, const Src2& b, int64_t M, int64_t 
         k_gemm_nt<EPI, true, 2, 2, true, 4, 2><<<grid, 256, 0, s>>>(a, b, M, N, K, bias, prelu, accum, z, y, ldc,
                                                                     vec_out, tiles, xcd, ce,
                                                                     static_cast<const uint16_t*>(planes));
+        return tiles;
+      }
+      if (nt_m16_enabled()) {
+        HGIN_TRACE("k_gemm_nt<EPI%d,%dx%d,split_bdma_m16,N%lld,K%lld>", EPI, BM, BN, (long long)N, (long long)K);
+        k_gemm_nt<EPI, true, 2, 2, true, 4, 1, true><<<grid, 256, 0, s>>>(a, b, M, N, K, bias, prelu, accum, z, y,
+                                                                          ldc, vec_out, tiles, xcd, ce,
+                                                                          static_cast<const uint16_t*>(planes));
         return tiles;
       }
       HGIN_TRACE("k_gemm_nt<EPI%d,%dx%d,split_bdma,N%lld,K%lld>", EPI, BM, BN, (long long)N, (long long)K);

@@ -38,7 +38,8 @@ SWITCHES = {"default": {}, "tiled": {"HGIN_NT_WS": "0", "HGIN_TN_WS": "0", "HGIN
             "tile_128x256": {"HGIN_NT_WS": "0", "HGIN_TN_WS": "0", "HGIN_NT_WS32": "0", "HGIN_NT_TN4": "1"},
             "nt_pipe": {"HGIN_NT_WS": "0", "HGIN_TN_WS": "0", "HGIN_NT_WS32": "0", "HGIN_NT_TN4": "2"},
             "nt_bdb": {"HGIN_NT_WS": "0", "HGIN_TN_WS": "0", "HGIN_NT_WS32": "0", "HGIN_NT_BDB": "1"},
-            "nt_pp": {"HGIN_NT_WS": "0", "HGIN_TN_WS": "0", "HGIN_NT_WS32": "0", "HGIN_NT_PP": "1"}}
+            "nt_pp": {"HGIN_NT_WS": "0", "HGIN_TN_WS": "0", "HGIN_NT_WS32": "0", "HGIN_NT_PP": "1"},
+            "nt_m16": {"HGIN_NT_WS": "0", "HGIN_TN_WS": "0", "HGIN_NT_WS32": "0", "HGIN_NT_M16": "1"}}
 _results = {}
 
 

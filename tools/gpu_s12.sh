@@ -11,7 +11,7 @@ step() {
   local rc=$?; echo "$name $rc" >> "$OUT/status.txt"; tail -6 "$OUT/$name.out"
   [ $rc -eq 0 ] || { echo "FATAL $name $rc"; tail -30 "$OUT/$name.out"; tail -20 "$OUT/$name.err"; exit $rc; }
 }
-step sw 600 python -u -m pytest tests/test_gpu_gemm_switch.py -x -q --timeout 400 --timeout-method thread -k "nt_pp or default"
+step sw 600 python -u -m pytest tests/test_gpu_gemm_switch.py -x -q --timeout 400 --timeout-method thread -k "nt_m16 or default"
 step ab_default 240 python tools/h2_bench.py
-step ab_pp 240 env HGIN_NT_PP=1 python tools/h2_bench.py
+step ab_m16 240 env HGIN_NT_M16=1 python tools/h2_bench.py
 echo done >> "$OUT/status.txt"
