@@ -6,6 +6,8 @@ At these sizes the CPU oracle cannot run the whole step, so the checks are size-
   * sampled destination rows of the real aggregate bit-exact against the C oracle over exactly those rows'
     neighbours (in edge order), with and without the concat / add self term;
   * train steps with a finite, changing loss and finite gradients;
+  * cfg5 (bf16) against cfg3 (fp32) on the same 100M-edge graph and parameters: the mixed-precision tolerance sweep of
+    BASELINE configs[4] at full size (the fixture-scale sweep is tests/test_gpu_bf16.py);
   * cfg4: the 8-component graph trained as 8 separate components (gradients accumulated, one
     ``sync_sqrt_mean``, exactly what 8 ranks do through the all-reduce) equals the single-batch step on the
     union (hgin/dist.py), within fp32 summation-order tolerance.
@@ -142,3 +144,33 @@ def test_cfg4_components_equal_union_step():
         assert err <= 1e-4 * float(ref_grads[n].double().norm()) + 1e-6 * g_scale, (n, err)
     del model
     torch.cuda.empty_cache()
+
+
+def test_cfg5_bf16_vs_cfg3_fp32_full_size():
+    """BASELINE configs[4]'s mixed-precision sweep at full size: one forward + backward of the 100M-edge graph with
+    bf16 storage (cfg5) against the same graph, features and parameters in fp32 (cfg3).  cfg5's features are cfg3's
+    rounded to bf16 (same generator stream), so the difference is the bf16 arithmetic path alone.  Bounds as the
+    fixture-scale sweep (tests/test_gpu_bf16.py): output rel-L2 <= 3e-2, loss within 2 %, median parameter-gradient
+    rel-L2 <= 5e-2."""
+    from hgin.train import mape
+    res = {}
+    for name in ("cfg3", "cfg5"):
+        cfg = CONFIGS[name]
+        g = synthetic_graph(cfg, seed=0, device=DEV)
+        model = _model(cfg)
+        out = model(g.x_dict(), g.edge_index_dict(), g.batch["path"])
+        lv = mape(out, g.y.reshape(-1, 1))
+        torch.sqrt(lv).backward()
+        res[name] = (out.detach().float().clone(), float(lv.detach()),
+                     {n: p.grad.detach().double().clone() for n, p in model.named_parameters() if p.grad is not None})
+        del g, model, out, lv
+        torch.cuda.empty_cache()
+    (o32, l32, g32), (o16, l16, g16) = res["cfg3"], res["cfg5"]
+    err_out = float((o16.double() - o32.double()).norm() / o32.double().norm())
+    assert set(g16) == set(g32)
+    errs = {n: float((g16[n] - g32[n]).norm() / g32[n].norm()) for n in g32 if float(g32[n].norm()) > 0}
+    print(f"\n[bf16 full size] out rel-L2 {err_out:.3e}, loss {l16:.6f} vs {l32:.6f}, grad rel-L2 median "
+          f"{np.median(list(errs.values())):.3e} max {max(errs.values()):.3e}")
+    assert np.isfinite(l16) and err_out <= 3e-2
+    assert abs(l16 - l32) <= 2e-2 * abs(l32)
+    assert np.median(list(errs.values())) <= 5e-2
