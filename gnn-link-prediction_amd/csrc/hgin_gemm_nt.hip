@@ -1822,16 +1822,30 @@ __global__ __launch_bounds__((WsCfg<K, N>::NT), 1) void k_ws_bf16(WsArgs g) {
     char* abase = ws_smem + (int)(i % NST) * R::SLOT;
     if (scale_any) {
       constexpr int CH = C::A_BYTES / 16;                        // 16-B chunks of the A image
+      constexpr int RC = C::ROWB / 16;                           // chunks per image row
       const int tq = tid_o();
+      constexpr bool kHalf = K >= 256 && (CH / 2) % C::NT == 0;
+      if (kHalf && k1 == K / 2) {
+        // equal halves (the concat of a 256-wide aggregate and a 256-wide x_dst): the row swizzle c ^ (r & 15) keeps
+        // bit log2(RC / 2) >= 4, so the self half is exactly slots [RC / 2, RC) of every row — visit only those
 #pragma unroll
-      for (int q = 0; q < CH / C::NT; ++q) {
-        const int ch = q * C::NT + tq;
-        const int r = ch / (C::ROWB / 16);
-        const int c = (ch % (C::ROWB / 16)) ^ (r & 15);          // logical chunk at this slot
-        if (c * 8 >= k1) {
-          uint4* pu = reinterpret_cast<uint4*>(abase + ch * 16);
+        for (int q = 0; q < CH / 2 / C::NT; ++q) {
+          const int j = q * C::NT + tq;
+          uint4* pu = reinterpret_cast<uint4*>(abase + ((j / (RC / 2)) * RC + RC / 2 + j % (RC / 2)) * 16);
           const uint4 u = *pu;
           *pu = make_uint4(scale_bf2(u.x, sc2), scale_bf2(u.y, sc2), scale_bf2(u.z, sc2), scale_bf2(u.w, sc2));
+        }
+      } else {
+#pragma unroll
+        for (int q = 0; q < CH / C::NT; ++q) {
+          const int ch = q * C::NT + tq;
+          const int r = ch / RC;
+          const int c = (ch % RC) ^ (r & 15);                    // logical chunk at this slot
+          if (c * 8 >= k1) {
+            uint4* pu = reinterpret_cast<uint4*>(abase + ch * 16);
+            const uint4 u = *pu;
+            *pu = make_uint4(scale_bf2(u.x, sc2), scale_bf2(u.y, sc2), scale_bf2(u.z, sc2), scale_bf2(u.w, sc2));
+          }
         }
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
