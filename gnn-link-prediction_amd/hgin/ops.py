@@ -560,7 +560,15 @@ def _gin_forward(x_src, x_dst, eps, weight, bias, prelu, accum, graph: RelationG
         # read back (2 * N_dst * F_dst * s bytes less per relation); comb holds the aggregate only
         comb = torch.empty(graph.n_dst, f_src, dtype=x_src.dtype, device=x_src.device)
         aggregate_into(graph.csr, x_src, None, None, COMBINE_NONE, comb)
-        z, y = gin_mlp_fwd(comb, w_op, bias, prelu, accum, comb2=x_dst, eps2=eps)
+        if x_src.dtype == torch.bfloat16 and eps is not None and weight.dtype == torch.float32:
+            # bf16 storage: (1 + eps) is folded into the self half of the weight operand, [W_agg | (1 + eps) W_self]
+            # rounded to bf16 once from the fp32 master, instead of bf16((1 + eps) x_dst) on every row — the same
+            # product with one bf16 rounding fewer and no eps-scaling pass in the GEMM (k_ws_bf16 K = 512: 3.31 ->
+            # 2.78 ms at M = 6M, profiles/r03/s17).  The backward keeps the unfolded operand (dW, eps gradient).
+            w_f = torch.cat((weight[:, :f_src], weight[:, f_src:] * (1.0 + eps)), 1).to(torch.bfloat16)
+            z, y = gin_mlp_fwd(comb, w_f, bias, prelu, accum, comb2=x_dst)
+        else:
+            z, y = gin_mlp_fwd(comb, w_op, bias, prelu, accum, comb2=x_dst, eps2=eps)
     else:
         width = f_src + (x_dst.size(1) if mode == COMBINE_CONCAT else 0)
         comb = torch.empty(graph.n_dst, width, dtype=x_src.dtype, device=x_src.device)
