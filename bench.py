@@ -52,6 +52,9 @@ METRIC = json.load(open(os.path.join(ROOT, "BASELINE.json")))["metric"]
 HBM_PEAK_GBS = 8000.0        # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
 F32_MFMA_PEAK_TFS = 157.3    # v_mfma_f32_32x32x2_f32 dense peak (= f32 vector peak)
 BF16_MFMA_PEAK_TFS = 2500.0  # v_mfma_f32_32x32x16_bf16 dense peak (no sparsity)
+# what a bare bf16 MFMA loop sustains on random operands once the chip lowers its clock under load (MI355X_MICROARCH.md
+# "DVFS give-back" (1): 1,247 TF/s at 1.90-1.95 GHz; the 2.5 PF peak assumes 2.4 GHz) — reported beside the peak
+BF16_MFMA_RANDOM_TFS = 1247.0
 CPU_SAMPLE_EDGES = 1_000_000  # convolved edges of the bounded CPU-baseline sample (~10-30 s of CPU work)
 
 
@@ -339,7 +342,10 @@ def gemm_fields(m, bf16: bool, steps: int, t_step: float, what: str):
             "hbm": {"achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(hf, 4)},
             "mfma": {"achieved": round(mfma, 1), "peak": BF16_MFMA_PEAK_TFS, "unit": "TFLOP/s (bf16 products)",
                      "frac": round(mf, 4), "products_per_fma": products,
-                     "fp32_equivalent_tflops": None if bf16 else round(tfs, 2)},
+                     "fp32_equivalent_tflops": None if bf16 else round(tfs, 2),
+                     "random_operand_loop": {"tflops": BF16_MFMA_RANDOM_TFS, "frac": round(mfma / BF16_MFMA_RANDOM_TFS, 4),
+                                             "source": "MI355X_MICROARCH.md DVFS give-back (1): bare bf16 MFMA loop, "
+                                                       "random operands, 1.90-1.95 GHz"}},
             "bytes_per_launch": m["avg_bytes"], "flops_per_launch": m["avg_work"],
             "avg_launch_ms": round(m["avg_ms"], 5), "launches_per_step": m["launches"] / steps,
             "ms_per_step": round(m["total_ms"] / steps, 3),
