@@ -70,12 +70,18 @@ bool xcd_remap_enabled();   // HGIN_XCD=0 disables (A/B measurements); default o
 __device__ __forceinline__ float bf2f(uint32_t h) { return __uint_as_float(h << 16); }
 __device__ __forceinline__ float bf_lo(uint32_t w) { return __uint_as_float(w << 16); }
 __device__ __forceinline__ float bf_hi(uint32_t w) { return __uint_as_float(w & 0xffff0000u); }
-__device__ __forceinline__ uint32_t f2bf(float f) {
-  const uint32_t u = __float_as_uint(f);
-  if ((u & 0x7fffffffu) > 0x7f800000u) return 0x7fc0u;
-  return (u + 0x7fffu + ((u >> 16) & 1u)) >> 16;
+// The rounding is gfx950's v_cvt_pk_bf16_f32 (RNE: equal to the integer form (u + 0x7fff + lsb) >> 16 on every
+// non-NaN input, tools/bf16_cvt_check.hip over 1M bit patterns incl. denormals, ties and overflow), with NaN lanes
+// replaced by 0x7FC0 (the instruction keeps the sign and payload; torch canonicalises).
+using f32x2_cvt_t = __attribute__((ext_vector_type(2))) float;
+using bf16x2_cvt_t = __attribute__((ext_vector_type(2))) __bf16;
+__device__ __forceinline__ uint32_t pack_bf2(float lo, float hi) {
+  uint32_t p = __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2_cvt_t{lo, hi}, bf16x2_cvt_t));
+  if (lo != lo) p = (p & 0xffff0000u) | 0x7fc0u;
+  if (hi != hi) p = (p & 0x0000ffffu) | 0x7fc00000u;
+  return p;
 }
-__device__ __forceinline__ uint32_t pack_bf2(float lo, float hi) { return f2bf(lo) | (f2bf(hi) << 16); }
+__device__ __forceinline__ uint32_t f2bf(float f) { return pack_bf2(f, 0.0f) & 0xffffu; }
 
 // fp32 GEMMs on the bf16 matrix cores ("split" mode of hgin_gemm_nt / hgin_gemm_tn): each fp32 operand
 // a = a1 + a2 + a3 with a1 = bf16(a), a2 = bf16(a - a1), a3 = bf16(a - a1 - a2) (RNE; every residual is
