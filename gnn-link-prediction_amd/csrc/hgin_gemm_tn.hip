@@ -1182,7 +1182,7 @@ struct WsdF32Cfg {
   static constexpr int PA = A_BYTES / 1024 / 8, PB = B_BYTES / 1024 / 8;
   static constexpr int P = PA + (PRO ? PA : 0) + PB;
   static constexpr int S = PRO ? 2 : 0;                      // g_z stores per A-splitting wave per block (2 x 16 B)
-  static_assert(TK >= 1 && A_BYTES % 8192 == 0 && B_BYTES % 8192 == 0 && LDS <= 147456, "shape");
+  static_assert(TK >= 1 && A_BYTES % 8192 == 0 && B_BYTES % 8192 == 0 && LDS <= 163840, "shape");
   static_assert(!PRO || BM * N / 8 <= NT, "PRO: at most one A group per thread");
   static constexpr int CA = BM * N / 8;                      // A groups (threads t < CA split one each)
 };
@@ -1490,12 +1490,15 @@ int64_t wsd_cols(const T* a, int64_t lda, const T* b1, int64_t ldb1, int64_t k1,
 }
 
 // Column passes of the PReLU-fused dW: [0, KV) with the fold (forms + stores g_z, the partial sums), then for K = 512
-// [256, 512) as the plain kernel on the stored g_z — the same two passes, slabs and product order as the unfused
-// K = 512 path, so g_w stays bit-identical to it.
+// at N = 256 [256, 512) as the plain kernel on the stored g_z — the same two passes, slabs and product order as the
+// unfused K = 512 path, so g_w stays bit-identical to it.  N = 128, K = 512 (the readout's first Linear on
+// [x_path | raw]) fits the whole 128 x 512 output in the registers of one pass (the 256 x 256 accumulator footprint):
+// g_y, z and B are streamed once and nothing re-reads g_z; per output element the products and their order are the
+// two-pass form's, so g_w is bit-identical to it as well.
 template <typename T>
 int64_t wsd_pro_passes(const T* gy, int64_t ldgy, const T* b1, int64_t ldb1, int64_t k1, const T* b2, int64_t ldb2,
                        int64_t M, int64_t N, int64_t K, float* slab, int64_t grid, const WsdPro& pro, hipStream_t s) {
-  const int64_t KV = K == 512 ? 256 : K;
+  const int64_t KV = (K == 512 && N == 256) ? 256 : K;
   auto srcs = [&](int64_t c0, const T*& p1, int64_t& l1, const T*& p2, int64_t& l2, int64_t& kk1) {
     kk1 = k1 > c0 ? (k1 - c0 < KV ? k1 - c0 : KV) : 0;
     p1 = kk1 > 0 ? b1 + c0 : b2;
@@ -1511,10 +1514,11 @@ int64_t wsd_pro_passes(const T* gy, int64_t ldgy, const T* b1, int64_t ldb1, int
 #define HGIN_PRO_PASS(NV, KVV) g = launch_wsd<NV, KVV, true>(gy, ldgy, p1, l1, p2, l2, kk1, M, slab, K, grid, s, pro);
   if (N == 256 && KV == 256) { HGIN_PRO_PASS(256, 256) }
   else if (N == 256) { HGIN_PRO_PASS(256, 128) }
+  else if (KV == 512) { HGIN_PRO_PASS(128, 512) }
   else if (KV == 256) { HGIN_PRO_PASS(128, 256) }
   else { HGIN_PRO_PASS(128, 128) }
 #undef HGIN_PRO_PASS
-  if (!g || K != 512) return g;
+  if (!g || K != 512 || KV == 512) return g;
   srcs(256, p1, l1, p2, l2, kk1);
   const T* gz = static_cast<const T*>(pro.gz);
   if (N == 256) return launch_wsd<256, 256>(gz, pro.ldgz, p1, l1, p2, l2, kk1, M, slab + 256, K, grid, s);
