@@ -390,10 +390,8 @@ int dispatch_g_bf16(int lanes_needed, const int32_t* rowptr, const int32_t* col,
 }
 
 // ---------------------------------------------------------------------------------------------------
-// Wide-lane variant (both element types): each lane owns NQ 16-B quads (NQ*16 B of a row), so a wave
-// covers kWave/G rows with G = F / (NQ * elems-per-quad) — more rows, hence more independent neighbour
-// rows in flight per wave, for the short (degree 5-10) rows of the GIN relations.  Same per-feature
-// sequential edge-order sums as the kernels above (bit-identical results).
+// 16-B quads of a feature row (fp32: 4, bf16: 8 elements) for the pipelined walk below.  (A wide-lane variant
+// with 2-4 quads per lane, k_agg_q, and an LDS-DMA gather, k_agg_lds, were measured and removed: DESIGN.md §3.)
 template <typename T>
 struct Quad;
 template <>
@@ -429,185 +427,6 @@ __device__ __forceinline__ void st_quad(void* p, const uint4& v) {
   const u4v t = {v.x, v.y, v.z, v.w};
   if (NT) __builtin_nontemporal_store(t, reinterpret_cast<u4v*>(p));
   else *reinterpret_cast<u4v*>(p) = t;
-}
-
-template <typename T, int NQ, int G, int U, bool NT, bool kTail>
-__global__ __launch_bounds__(256) void k_agg_q(const int32_t* __restrict__ rowptr, const int32_t* __restrict__ col,
-                                               int64_t n_rows, const T* __restrict__ x_src, int64_t ld_src, int f_src,
-                                               const T* __restrict__ x_dst, int64_t ld_dst, int f_dst,
-                                               const float* __restrict__ eps, int combine, T* __restrict__ out,
-                                               int64_t ld_out) {
-  constexpr int E = Quad<T>::E;
-  constexpr int VEC = E * NQ;
-  constexpr int kRowsPerWave = kWave / G;
-  const int lane = threadIdx.x & (kWave - 1);
-  const int grp = lane / G;
-  const int gl = lane % G;
-  const int64_t wave_id = (int64_t)blockIdx.x * (blockDim.x / kWave) + (threadIdx.x / kWave);
-  const int64_t r = wave_id * kRowsPerWave + grp;
-  if (r >= n_rows) return;
-  const int beg = rowptr[r];
-  const int end = rowptr[r + 1];
-  const float s = combine != HGIN_COMBINE_NONE ? __fadd_rn(1.0f, eps[0]) : 1.0f;
-  T* __restrict__ orow = out + r * ld_out;
-  for (int f0 = gl * VEC; f0 < f_src; f0 += G * VEC) {
-    float acc[VEC];
-#pragma unroll
-    for (int c = 0; c < VEC; ++c) acc[c] = 0.0f;
-    int k = beg;
-    if constexpr (kTail) {
-      for (; k < end; k += U) {   // batched tail, as k_aggregate
-        const int n = end - k;
-        uint4 v[U][NQ];
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-#pragma unroll
-          for (int q = 0; q < NQ; ++q) v[u][q] = make_uint4(0u, 0u, 0u, 0u);
-          if (u < n) {
-            const T* p = x_src + (int64_t)col[k + u] * ld_src + f0;
-#pragma unroll
-            for (int q = 0; q < NQ; ++q) v[u][q] = ld_quad<false>(p + q * E);
-          }
-        }
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-          if (u < n) {
-#pragma unroll
-            for (int q = 0; q < NQ; ++q) {
-              float f[E];
-              Quad<T>::unpack(v[u][q], f);
-#pragma unroll
-              for (int c = 0; c < E; ++c) acc[q * E + c] = __fadd_rn(acc[q * E + c], f[c]);
-            }
-          }
-        }
-      }
-    }
-    for (; !kTail && k + U <= end; k += U) {
-      int idx[U];
-#pragma unroll
-      for (int u = 0; u < U; ++u) idx[u] = col[k + u];
-      uint4 v[U][NQ];
-#pragma unroll
-      for (int u = 0; u < U; ++u)
-#pragma unroll
-        for (int q = 0; q < NQ; ++q) v[u][q] = ld_quad<false>(x_src + (int64_t)idx[u] * ld_src + f0 + q * E);
-#pragma unroll
-      for (int u = 0; u < U; ++u)
-#pragma unroll
-        for (int q = 0; q < NQ; ++q) {
-          float f[E];
-          Quad<T>::unpack(v[u][q], f);
-#pragma unroll
-          for (int c = 0; c < E; ++c) acc[q * E + c] = __fadd_rn(acc[q * E + c], f[c]);
-        }
-    }
-    for (; !kTail && k < end; ++k) {
-      const T* p = x_src + (int64_t)col[k] * ld_src + f0;
-      uint4 v[NQ];
-#pragma unroll
-      for (int q = 0; q < NQ; ++q) v[q] = ld_quad<false>(p + q * E);
-#pragma unroll
-      for (int q = 0; q < NQ; ++q) {
-        float f[E];
-        Quad<T>::unpack(v[q], f);
-#pragma unroll
-        for (int c = 0; c < E; ++c) acc[q * E + c] = __fadd_rn(acc[q * E + c], f[c]);
-      }
-    }
-    if (combine == HGIN_COMBINE_ADD) {
-#pragma unroll
-      for (int q = 0; q < NQ; ++q) {
-        float f[E];
-        Quad<T>::unpack(ld_quad<NT>(x_dst + r * ld_dst + f0 + q * E), f);
-#pragma unroll
-        for (int c = 0; c < E; ++c) acc[q * E + c] = __fadd_rn(acc[q * E + c], __fmul_rn(s, f[c]));
-      }
-    }
-#pragma unroll
-    for (int q = 0; q < NQ; ++q) st_quad<NT>(orow + f0 + q * E, Quad<T>::pack(acc + q * E));
-  }
-  if (combine == HGIN_COMBINE_CONCAT) {
-    for (int f0 = gl * VEC; f0 < f_dst; f0 += G * VEC) {
-#pragma unroll
-      for (int q = 0; q < NQ; ++q) {
-        float f[E];
-        Quad<T>::unpack(ld_quad<NT>(x_dst + r * ld_dst + f0 + q * E), f);
-#pragma unroll
-        for (int c = 0; c < E; ++c) f[c] = __fmul_rn(s, f[c]);
-        st_quad<NT>(orow + f_src + f0 + q * E, Quad<T>::pack(f));
-      }
-    }
-  }
-}
-
-// Quads per lane (HGIN_AGG_NQ = 1, 2 or 4 forces one; tools/agg_bench.py).  Default, measured
-// (profiles/r01_agg_nq_variants.txt): 4 quads for the ADD / NONE (backward) aggregates — +15-47 % for bf16,
-// 0-15 % for fp32 — and the 1-quad kernels for CONCAT, whose second output stream made wide lanes 10-60 %
-// slower.
-int agg_nq_env() {
-  static const int v = [] {
-    const char* e = getenv("HGIN_AGG_NQ");
-    const int x = e ? atoi(e) : 0;
-    return (x == 1 || x == 2 || x == 4) ? x : 0;
-  }();
-  return v;
-}
-int agg_nq(int combine) {
-  const int env = agg_nq_env();
-  if (env) return env;
-  // with the batched tail the 1-quad kernels are as fast or faster for every mode (profiles/r01_agg_tail.txt):
-  // the wide lanes only paid off while short rows were walked one neighbour at a time
-  if (agg_tail_batched()) return 1;
-  return combine == HGIN_COMBINE_CONCAT ? 1 : 4;
-}
-
-template <typename T, int NQ>
-int launch_agg_q(int lanes_needed, const int32_t* rowptr, const int32_t* col, int64_t n_rows, const T* x_src,
-                 int64_t ld_src, int f_src, const T* x_dst, int64_t ld_dst, int f_dst, const float* eps, int combine,
-                 T* out, int64_t ld_out, hipStream_t s, const char* what) {
-  constexpr int kU = NQ >= 4 ? 4 : 8;
-  const bool nt = agg_nt(combine, n_rows, (int64_t)(f_src + (combine == HGIN_COMBINE_CONCAT ? f_dst : 0)) * (int64_t)sizeof(T));
-  const bool tail = agg_tail_batched();
-  HGIN_TRACE("k_agg_q<%s,NQ%d,mode%d>", sizeof(T) == 4 ? "f32" : "bf16", NQ, combine);
-#define HGIN_AGGQ_L(GV, NTV, TAIL, BLOCKS)                                                                      \
-  k_agg_q<T, NQ, GV, kU, NTV, TAIL><<<dim3((unsigned)(BLOCKS)), 256, 0, s>>>(rowptr, col, n_rows, x_src, ld_src, \
-                                                                            f_src, x_dst, ld_dst, f_dst, eps,   \
-                                                                            combine, out, ld_out)
-#define HGIN_AGGQ_G(GV)                                                                 \
-  {                                                                                     \
-    const int64_t blocks = ceil_div(ceil_div(n_rows, kWave / GV), 256 / kWave);         \
-    if (nt) { if (tail) HGIN_AGGQ_L(GV, true, true, blocks); else HGIN_AGGQ_L(GV, true, false, blocks); } \
-    else { if (tail) HGIN_AGGQ_L(GV, false, true, blocks); else HGIN_AGGQ_L(GV, false, false, blocks); } \
-    return check_launch(what);                                                          \
-  }
-  if (lanes_needed <= 2) HGIN_AGGQ_G(2)
-  if (lanes_needed <= 4) HGIN_AGGQ_G(4)
-  if (lanes_needed <= 8) HGIN_AGGQ_G(8)
-  if (lanes_needed <= 16) HGIN_AGGQ_G(16)
-  if (lanes_needed <= 32) HGIN_AGGQ_G(32)
-  HGIN_AGGQ_G(64)
-#undef HGIN_AGGQ_G
-#undef HGIN_AGGQ_L
-}
-
-// Try the wide-lane kernel with nq quads per lane; returns -1000 when the shapes do not allow it.
-template <typename T>
-int try_agg_wide(int nq, const int32_t* rowptr, const int32_t* col, int64_t n_rows, const T* x_src, int64_t ld_src,
-                 int f_src, const T* x_dst, int64_t ld_dst, int f_dst, const float* eps, int combine, T* out,
-                 int64_t ld_out, hipStream_t s, const char* what) {
-  const int vec = Quad<T>::E * nq;
-  const int fd = combine == HGIN_COMBINE_CONCAT ? f_dst : 0;
-  if (f_src % vec || fd % vec || (combine == HGIN_COMBINE_ADD && f_dst % vec)) return -1000;
-  const int widest = f_src > fd ? f_src : fd;
-  const int lanes = (widest + vec - 1) / vec;
-  if (nq == 2)
-    return launch_agg_q<T, 2>(lanes, rowptr, col, n_rows, x_src, ld_src, f_src, x_dst, ld_dst, f_dst, eps, combine,
-                              out, ld_out, s, what);
-  if (nq == 4)
-    return launch_agg_q<T, 4>(lanes, rowptr, col, n_rows, x_src, ld_src, f_src, x_dst, ld_dst, f_dst, eps, combine,
-                              out, ld_out, s, what);
-  return -1000;
 }
 
 // ---------------------------------------------------------------------------------------------------
@@ -769,188 +588,6 @@ int try_agg_pipe(const int32_t* rowptr, const int32_t* col, int64_t n_rows, cons
 #undef HGIN_PIPE_G
   if (rc) return rc;
   return check_launch(what);
-}
-
-// ---------------------------------------------------------------------------------------------------
-// k_agg_lds — the fp32 F = 256 aggregate with its neighbour rows gathered into LDS by DMA
-// (MI355X_MICROARCH.md "Indexed rows: gather into LDS": global_load_lds_dwordx4 with a per-lane source address,
-// ~72 KiB+ in flight per CU).  Opt-in A/B against the register gather (HGIN_AGG_LDS = 1; ring depth
-// HGIN_AGG_LDS_D = 8 / 12 / 16 / 24 rows per wave).
-//   * Each wave owns a contiguous range of destination rows and a private ring of D 1-KiB LDS slots; no barriers.
-//   * Its item stream is, row by row, the row's neighbour rows in edge order, then (ADD) the row's x_dst row; one
-//     DMA instruction moves one 1-KiB row (64 lanes x 16 B).  The issue cursor runs D items ahead of the consumer.
-//   * Edge indices come in 64-entry chunks, DMA'd into a per-wave double buffer in LDS (global_load_lds_dword, one
-//     index per lane) one chunk ahead, and read back with a broadcast ds_read: no compiler-visible vector load,
-//     so the compiler never inserts a vmcnt(0) that would drain the ring, and no VGPR is written asynchronously
-//     behind the compiler's back.  The consumer waits vmcnt(D - 1) (loads, LDS-DMA and stores retire in issue
-//     order for vmcnt: exactly D - 1 items were issued after the one it reads in steady state), vmcnt(0) while
-//     the stream drains.  A chunk's DMA is issued >= 64 items before its first index is read, so a later
-//     vmcnt(D - 1) wait (D <= 24) has always retired it.
-//   * The sum is taken from LDS in edge order with __fadd_rn, the self term as in k_aggregate: bit-identical.
-constexpr int kLdsRow = 1024;   // bytes of one F = 256 fp32 row = one DMA instruction
-
-template <int D, bool NT>
-__global__ __launch_bounds__(256) void k_agg_lds(const int32_t* __restrict__ rowptr, const int32_t* __restrict__ col,
-                                                 int64_t n_rows, const float* __restrict__ x_src, int64_t ld_src,
-                                                 const float* __restrict__ x_dst, int64_t ld_dst,
-                                                 const float* __restrict__ eps, int combine, float* __restrict__ out,
-                                                 int64_t ld_out, int64_t rows_per_wave) {
-  extern __shared__ __attribute__((aligned(16))) char agg_lds_ring[];
-  const int lane = threadIdx.x & (kWave - 1);
-  // wave-uniform (readfirstlane): every index / rowptr value below is then scalar — s_load, which waits on
-  // lgkmcnt, not vmcnt, so the compiler never drains the DMA ring for them
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
-  char* ring = agg_lds_ring + wave * (D * kLdsRow);
-  int32_t* idx_buf = reinterpret_cast<int32_t*>(agg_lds_ring + 4 * D * kLdsRow) + wave * 128;   // 2 x 64 indices
-  const int64_t r0 = ((int64_t)blockIdx.x * 4 + wave) * rows_per_wave;
-  if (r0 >= n_rows) return;
-  const int64_t r1 = r0 + rows_per_wave < n_rows ? r0 + rows_per_wave : n_rows;
-  const bool add = combine == HGIN_COMBINE_ADD;
-  const float s = add ? __fadd_rn(1.0f, eps[0]) : 1.0f;
-  const int e0 = rowptr[r0];
-  const int e1 = rowptr[r1];
-
-  // edge-index chunk c (edges [e0 + 64 c, e0 + 64 c + 64), clamped inside the stream) -> idx_buf[(c & 1) * 64 + lane]
-  auto load_chunk = [&](int c) {
-    if (e1 <= e0) return;
-    const int e = e0 + c * 64 + lane;
-    const int32_t* p = col + (e < e1 ? e : e1 - 1);
-    const uint32_t m0 = __builtin_amdgcn_readfirstlane(
-        (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)(reinterpret_cast<char*>(idx_buf + (c & 1) * 64)));
-    asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dword %0, off" ::"v"(p), "s"(m0) : "memory", "m0");
-  };
-  load_chunk(0);
-  load_chunk(1);
-  int ck_idx = 0;                       // highest chunk whose successor's DMA has been issued - 1
-  wait_vm<0>();
-
-  // issue cursor
-  int64_t ir = r0;
-  int ie = e0, iend = rowptr[r0 + 1];
-  bool iself = false;                   // the current issue row's self item was issued
-  int issued = 0, consumed = 0;
-  const uintptr_t xs = reinterpret_cast<uintptr_t>(x_src) + (uintptr_t)lane * 16;
-  const uintptr_t xd = reinterpret_cast<uintptr_t>(x_dst) + (uintptr_t)lane * 16;
-
-  auto issue_next = [&]() {
-    // next item of the stream: an edge of row ir, or (ADD) row ir's self row, else advance to the next row
-    while (ir < r1) {
-      if (ie < iend) {
-        const int c = (ie - e0) >> 6;
-        if (c != ck_idx) {              // entered chunk c (DMA'd >= 64 items ago): prefetch chunk c + 1
-          ck_idx = c;
-          load_chunk(c + 1);
-        }
-        const int src = __builtin_amdgcn_readfirstlane(idx_buf[(c & 1) * 64 + ((ie - e0) & 63)]);
-        const void* g = reinterpret_cast<const void*>(xs + (uintptr_t)((int64_t)src * ld_src * 4));
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the slot's previous ds_read has returned
-        glds16_asm<false>(g, ring + (issued % D) * kLdsRow);
-        ++ie;
-        ++issued;
-        return;
-      }
-      if (add && !iself) {
-        const void* g = reinterpret_cast<const void*>(xd + (uintptr_t)(ir * ld_dst * 4));
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        glds16_asm<NT>(g, ring + (issued % D) * kLdsRow);
-        iself = true;
-        ++issued;
-        return;
-      }
-      ++ir;
-      iself = false;
-      if (ir < r1) iend = rowptr[__builtin_amdgcn_readfirstlane((int)(ir + 1))];
-    }
-  };
-  auto wait_item = [&]() {
-    if (issued - consumed == D) wait_vm<D - 1>(); else wait_vm<0>();
-  };
-
-  for (int j = 0; j < D; ++j) issue_next();
-  for (int64_t r = r0; r < r1; ++r) {
-    const int beg = rowptr[r], end = rowptr[r + 1];
-    float4 acc = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-    for (int k = beg; k < end; ++k) {
-      wait_item();
-      const float4 v = *reinterpret_cast<const float4*>(ring + (consumed % D) * kLdsRow + lane * 16);
-      acc = make_float4(__fadd_rn(acc.x, v.x), __fadd_rn(acc.y, v.y), __fadd_rn(acc.z, v.z), __fadd_rn(acc.w, v.w));
-      ++consumed;
-      issue_next();
-    }
-    float4 o = acc;
-    if (add) {
-      wait_item();
-      const float4 v = *reinterpret_cast<const float4*>(ring + (consumed % D) * kLdsRow + lane * 16);
-      o = make_float4(__fadd_rn(acc.x, __fmul_rn(s, v.x)), __fadd_rn(acc.y, __fmul_rn(s, v.y)),
-                      __fadd_rn(acc.z, __fmul_rn(s, v.z)), __fadd_rn(acc.w, __fmul_rn(s, v.w)));
-      ++consumed;
-      issue_next();
-    }
-    Vec<4>::store_s<NT>(out + r * ld_out + lane * 4, o);
-  }
-  wait_vm<0>();
-}
-
-int agg_lds_depth() {   // 0: off (the register gather runs)
-  static const int d = [] {
-    const char* on = getenv("HGIN_AGG_LDS");
-    if (!(on && on[0] == '1')) return 0;
-    const char* v = getenv("HGIN_AGG_LDS_D");
-    const int x = v ? atoi(v) : 16;
-    return (x == 8 || x == 12 || x == 16 || x == 24) ? x : 16;
-  }();
-  return d;
-}
-
-template <int D, bool NT>
-int launch_agg_lds(const int32_t* rowptr, const int32_t* col, int64_t n_rows, const float* x_src, int64_t ld_src,
-                   const float* x_dst, int64_t ld_dst, const float* eps, int combine, float* out, int64_t ld_out,
-                   hipStream_t s) {
-  constexpr int lds = 4 * D * kLdsRow + 4 * 128 * 4;    // row rings + per-wave double-buffered index chunks
-  auto kern = k_agg_lds<D, NT>;
-  static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
-                                                     hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-  if (attr != hipSuccess) {
-    set_error("hgin_aggregate_f32: hipFuncSetAttribute failed: %s", hipGetErrorString(attr));
-    return (int)attr;
-  }
-  static const int64_t slots = [&] {
-    int per_cu = 0, dev = 0, cus = 256;
-    hipDeviceProp_t prop;
-    if (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&prop, dev) == hipSuccess)
-      cus = prop.multiProcessorCount;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 256, lds) != hipSuccess || per_cu <= 0)
-      per_cu = 1;
-    return (int64_t)per_cu * cus;
-  }();
-  // every resident wave one contiguous range of rows (uniform graphs: near-equal edge counts per range)
-  const int64_t waves = slots * 4;
-  const int64_t rpw = ceil_div(n_rows, waves);
-  const int64_t blocks = ceil_div(ceil_div(n_rows, rpw), 4);
-  HGIN_TRACE("k_agg_lds<D%d,mode%d>", D, combine);
-  kern<<<dim3((unsigned)blocks), 256, lds, s>>>(rowptr, col, n_rows, x_src, ld_src, x_dst, ld_dst, eps, combine, out,
-                                                ld_out, rpw);
-  return check_launch("hgin_aggregate_f32");
-}
-
-// Returns -1000 when the LDS gather is off or does not take these operands (fp32, F = 256, NONE / ADD,
-// 16-B aligned rows).
-int try_agg_lds(const int32_t* rowptr, const int32_t* col, int64_t n_rows, const float* x_src, int64_t ld_src,
-                int64_t f_src, const float* x_dst, int64_t ld_dst, int64_t f_dst, const float* eps, int combine,
-                float* out, int64_t ld_out, hipStream_t s) {
-  const int d = agg_lds_depth();
-  if (!d || f_src != 256 || combine == HGIN_COMBINE_CONCAT) return -1000;
-  if (!aligned16(x_src) || ld_src % 4 || !aligned16(out) || ld_out % 4) return -1000;
-  if (combine == HGIN_COMBINE_ADD && (f_dst != 256 || !aligned16(x_dst) || ld_dst % 4)) return -1000;
-  const bool nt = agg_nt(combine, n_rows, 1024);
-#define HGIN_LDS_D(DV)                                                                                          \
-  return nt ? launch_agg_lds<DV, true>(rowptr, col, n_rows, x_src, ld_src, x_dst, ld_dst, eps, combine, out, ld_out, s) \
-            : launch_agg_lds<DV, false>(rowptr, col, n_rows, x_src, ld_src, x_dst, ld_dst, eps, combine, out, ld_out, s);
-  if (d == 8) { HGIN_LDS_D(8) }
-  if (d == 12) { HGIN_LDS_D(12) }
-  if (d == 24) { HGIN_LDS_D(24) }
-  HGIN_LDS_D(16)
-#undef HGIN_LDS_D
 }
 
 int check_aggregate_args(const char* what, const int32_t* rowptr, int64_t n_rows, int64_t ld_src, int64_t f_src,
@@ -1125,11 +762,6 @@ extern "C" int hgin_aggregate_bf16(const int32_t* rowptr, const int32_t* col, in
                                           eps, combine, out, ld_out, s, "hgin_aggregate_bf16");
     if (rc != -1000) return rc;
   }
-  if (vec8 && agg_nq(combine) > 1) {
-    const int rc = try_agg_wide<uint16_t>(agg_nq(combine), rowptr, col, n_rows, x_src, ld_src, (int)f_src, x_dst, ld_dst,
-                                          (int)f_dst, eps, combine, out, ld_out, s, "hgin_aggregate_bf16");
-    if (rc != -1000) return rc;
-  }
   if (vec8)
     return dispatch_g_bf16<8>((int)ceil_div(widest, 8), rowptr, col, n_rows, x_src, ld_src, (int)f_src, x_dst, ld_dst,
                               (int)f_dst, eps, combine, out, ld_out, s);
@@ -1150,18 +782,8 @@ extern "C" int hgin_aggregate_f32(const int32_t* rowptr, const int32_t* col, int
                     dst_ok && (f_src > 0 || f_dst > 0);
   const int fd = combine == HGIN_COMBINE_CONCAT ? (int)f_dst : 0;
   {
-    const int rc = try_agg_lds(rowptr, col, n_rows, x_src, ld_src, f_src, x_dst, ld_dst, f_dst, eps, combine, out,
-                               ld_out, s);
-    if (rc != -1000) return rc;
-  }
-  {
     const int rc = try_agg_pipe<float>(rowptr, col, n_rows, x_src, ld_src, (int)f_src, x_dst, ld_dst, (int)f_dst, eps,
                                        combine, out, ld_out, s, "hgin_aggregate_f32");
-    if (rc != -1000) return rc;
-  }
-  if (vec4 && agg_nq(combine) > 1) {
-    const int rc = try_agg_wide<float>(agg_nq(combine), rowptr, col, n_rows, x_src, ld_src, (int)f_src, x_dst, ld_dst,
-                                       (int)f_dst, eps, combine, out, ld_out, s, "hgin_aggregate_f32");
     if (rc != -1000) return rc;
   }
   if (vec4) {

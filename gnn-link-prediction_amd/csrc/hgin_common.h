@@ -113,7 +113,6 @@ __device__ __forceinline__ void split4(const float4 v, uint2 (&o)[3]) {
 // 16 rows of a ds_read_b128 lane group fall on 16 distinct 16-B bank slots (13 is odd).
 constexpr int kSplitRowWords = 52;
 bool gemm_split_enabled();   // HGIN_F32_GEMM=mfma32 selects the exact f32-MFMA kernels; default split
-bool gemm_h2_enabled();      // HGIN_F32_GEMM=h2: the scaled two-term fp16 split (hgin_gemm_nt.hip, k_gemm_nt_h2)
 
 // LDS-DMA (global_load_lds_dwordx4: 64 lanes x 16 B into 1 KiB at a wave-uniform LDS address) issued from
 // inline asm: the compiler does not see it, so it does not guard the kernel's later LDS reads with a vmcnt(0)

@@ -391,15 +391,8 @@ __device__ __forceinline__ void tile_partial(float* smem, float ep, float* part,
 // image is copied HBM/L2 -> LDS by global_load_lds_dwordx4 (inline asm, per-lane source addresses), issued after
 // the first barrier of a K-tile step and awaited (vmcnt 0) before the second: the A split pass between them hides its
 // latency.  No B split VALU (a quarter of the loop's VALU at K = 512, N = 256), no B prefetch registers.
-//
-// kBdma == 2: the B image is double-buffered in LDS and tile t + 1's DMA is issued at the top of step t, beside the A
-// prefetch, so it lands under step t's MFMAs instead of between the step's two barriers (73.7 KB of LDS: 2 workgroups
-// per CU).
-//
-// kM16 (split mode): the products as v_mfma_f32_16x16x32_bf16 (16 x 16 tiles, one 32-deep k-step per K-tile) instead of
-// 32 x 32 x 16 — MI355X_MICROARCH.md "DVFS give-back" (7): on random operands the 16 x 16 x 32 shape holds a higher clock.
-template <int EPI, bool kClean, int TN, int WNv, bool kSplit, int NW = 4, int kBdma = 0, bool kM16 = false>
-__global__ __launch_bounds__(NW * 64, TN == 4 ? 1 : (NW == 8 || kBdma == 2 ? 2 : 3)) void k_gemm_nt(Src2 A, Src2 B, int64_t M, int64_t N, int64_t K,
+template <int EPI, bool kClean, int TN, int WNv, bool kSplit, int NW = 4, int kBdma = 0>
+__global__ __launch_bounds__(NW * 64, NW == 8 ? 2 : 3) void k_gemm_nt(Src2 A, Src2 B, int64_t M, int64_t N, int64_t K,
                                                     const float* __restrict__ bias, const float* __restrict__ prelu,
                                                     const float* __restrict__ accum, float* __restrict__ Z,
                                                     float* __restrict__ Y, int64_t ldc, bool vec_out,
@@ -412,7 +405,7 @@ __global__ __launch_bounds__(NW * 64, TN == 4 ? 1 : (NW == 8 || kBdma == 2 ? 2 :
   constexpr int BN = WN * TN * 32;        // columns per workgroup tile
   constexpr int WCOLS = TN * 32;          // columns per wave
   constexpr int kRowW = kSplit ? kSplitRowWordsNT : kLds;   // 4-B words per LDS row
-  __shared__ __attribute__((aligned(16))) float smem[(BM + BN * (kBdma == 2 ? 2 : 1)) * kRowW];
+  __shared__ __attribute__((aligned(16))) float smem[(BM + BN) * kRowW];
   float* As = smem;
   float* Bs = smem + BM * kRowW;
   uint32_t* Ash = reinterpret_cast<uint32_t*>(As);
@@ -440,12 +433,6 @@ __global__ __launch_bounds__(NW * 64, TN == 4 ? 1 : (NW == 8 || kBdma == 2 ? 2 :
     for (int b = 0; b < TN; ++b)
 #pragma unroll
       for (int e = 0; e < 16; ++e) acc[a][b][e] = 0.0f;
-  f32x4v acc16[kM16 ? 4 : 1][kM16 ? 2 * TN : 1];
-#pragma unroll
-  for (int a = 0; a < (kM16 ? 4 : 1); ++a)
-#pragma unroll
-    for (int b = 0; b < (kM16 ? 2 * TN : 1); ++b) acc16[a][b] = f32x4v{0.f, 0.f, 0.f, 0.f};
-  static_assert(!kM16 || kSplit, "kM16 needs split mode");
 
   float4 ra[BM / (NT / 8)], rb[(BN >= NT / 8 && !kBdma) ? BN / (NT / 8) : 1];
   const float sc2 = self_scale(A.eps2);
@@ -469,7 +456,7 @@ __global__ __launch_bounds__(NW * 64, TN == 4 ? 1 : (NW == 8 || kBdma == 2 ? 2 :
   auto dma_b = [&](int64_t k0) {
     if constexpr (kBdma) {
       const char* base = reinterpret_cast<const char*>(Bp) + (k0 / kBK) * 3 * N * 64;
-      char* dst = reinterpret_cast<char*>(Bsh) + (kBdma == 2 ? ((k0 / kBK) & 1) * BN * kSplitRowWordsNT * 4 : 0);
+      char* dst = reinterpret_cast<char*>(Bsh);
 #pragma unroll
       for (int i = 0; i < kBInst; ++i) glds16_asm(base + boff[i], dst + (wave * kBInst + i) * 1024);
     }
@@ -495,42 +482,10 @@ __global__ __launch_bounds__(NW * 64, TN == 4 ? 1 : (NW == 8 || kBdma == 2 ? 2 :
     if (more) {   // next K-tile's global loads stay in flight under this K-tile's MFMAs
       load_a(k0 + kBK);
       if constexpr (!kBdma) load_tile<kClean, BN, NT>(rb, B, n0, N, k0 + kBK, K, tid);
-      if constexpr (kBdma == 2) dma_b(k0 + kBK);   // into the other B buffer (last read in step t - 1)
     }
-    const uint32_t* Bcur = Bsh + (kBdma == 2 ? ((k0 / kBK) & 1) * BN * kSplitRowWordsNT : 0);
+    const uint32_t* Bcur = Bsh;
     __builtin_amdgcn_s_setprio(1);   // keep the MFMA cluster together (T5)
-    if constexpr (kM16) {
-      // one 32-deep k-step: lane l reads row l & 15 of a 16-row block, k = 8 (l >> 4) .. +7 of each plane
-      const int r16 = lane & 15, c16 = lane >> 4;
-#pragma unroll
-      for (int th = 0; th < 2; ++th) {   // two 32-row halves of the wave tile (bounds the fragment registers)
-        bf16x8 fa[2][3];
-#pragma unroll
-        for (int u = 0; u < 2; ++u)
-#pragma unroll
-          for (int p = 0; p < 3; ++p)
-            fa[u][p] = *reinterpret_cast<const bf16x8*>(Ash + (wm * 64 + (2 * th + u) * 16 + r16) * kSplitRowWordsNT +
-                                                        p * 16 + nt_chunk(r16, c16));
-#pragma unroll
-        for (int tn = 0; tn < 2 * TN; ++tn) {
-          bf16x8 fb[3];
-#pragma unroll
-          for (int p = 0; p < 3; ++p)
-            fb[p] = *reinterpret_cast<const bf16x8*>(Bcur + (wn * WCOLS + tn * 16 + r16) * kSplitRowWordsNT + p * 16 +
-                                                     nt_chunk(r16, c16));
-#pragma unroll
-          for (int u = 0; u < 2; ++u) {   // k_gemm_nt's product order: smallest terms first
-            f32x4v& c = acc16[2 * th + u][tn];
-            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[u][2], fb[0], c, 0, 0, 0);
-            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[u][1], fb[1], c, 0, 0, 0);
-            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[u][0], fb[2], c, 0, 0, 0);
-            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[u][1], fb[0], c, 0, 0, 0);
-            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[u][0], fb[1], c, 0, 0, 0);
-            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[u][0], fb[0], c, 0, 0, 0);
-          }
-        }
-      }
-    } else if constexpr (kSplit) {
+    if constexpr (kSplit) {
       // two 16-deep k-blocks; lane (i, h) reads k = 16 kb + 8 h .. +7 of each plane (one ds_read_b128)
 #pragma unroll
       for (int kb = 0; kb < 2; ++kb) {
@@ -583,7 +538,7 @@ __global__ __launch_bounds__(NW * 64, TN == 4 ? 1 : (NW == 8 || kBdma == 2 ? 2 :
     __builtin_amdgcn_s_setprio(0);
     if (more) {
       __syncthreads();
-      if constexpr (kBdma == 1) dma_b(k0 + kBK);
+      if constexpr (kBdma) dma_b(k0 + kBK);
       stage();
       if constexpr (kBdma) wait_vm<0>();
       __syncthreads();
@@ -591,31 +546,9 @@ __global__ __launch_bounds__(NW * 64, TN == 4 ? 1 : (NW == 8 || kBdma == 2 ? 2 :
   }
 
   float ep = 0.0f;
-  if constexpr (kM16)
-    epilogue<EPI, TN, float, f32x4v[4][2 * TN]>(acc16, smem, wave, wm, wn, lane, li, lh, m0, n0, M, N, bias, prelu,
-                                                accum, Z, Y, ldc, vec_out, ce, &ep);
-  else
-    epilogue<EPI, TN, float>(acc, smem, wave, wm, wn, lane, li, lh, m0, n0, M, N, bias, prelu, accum, Z, Y, ldc,
-                             vec_out, ce, &ep);
+  epilogue<EPI, TN, float>(acc, smem, wave, wm, wn, lane, li, lh, m0, n0, M, N, bias, prelu, accum, Z, Y, ldc,
+                           vec_out, ce, &ep);
   if constexpr (EPI == 4) tile_partial(smem, ep, ce.part, q);
-}
-
-// HGIN_NT_M16=1: the 128 x 128 split-mode tile (B by LDS-DMA) on v_mfma_f32_16x16x32_bf16 (k_gemm_nt<..., kM16>; A/B)
-bool nt_m16_enabled() {
-  static const bool on = [] {
-    const char* v = getenv("HGIN_NT_M16");
-    return v && v[0] == '1';
-  }();
-  return on;
-}
-
-// HGIN_NT_BDB=1: the 128 x 128 split-mode tile with B double-buffered (k_gemm_nt<..., kBdma = 2>; A/B)
-bool nt_bdb_enabled() {
-  static const bool on = [] {
-    const char* v = getenv("HGIN_NT_BDB");
-    return v && v[0] == '1';
-  }();
-  return on;
 }
 
 // HGIN_NT_BDMA=0: the 128 x 128 split-mode tile splits B itself even where pre-split planes are passed
@@ -623,296 +556,6 @@ bool nt_bdma_enabled() {
   static const bool on = [] {
     const char* v = getenv("HGIN_NT_BDMA");
     return !(v && v[0] == '0');
-  }();
-  return on;
-}
-
-// k_nt_pipe — the fp32 split-mode NT GEMM for N a multiple of 256 and K a multiple of 64 (the first layer's K = 512
-// forward of cfg3) as a software pipeline at one 4-wave workgroup per CU (one wave per SIMD, 512 registers: the
-// 64 x 128 accumulator tile of each wave lives in AGPRs):
-//   * 128 x 256 tiles — A (fp32, read once from HBM: the whole N = 256 in one tile) is split once per tile;
-//   * B arrives pre-split (hgin_nt_planes_f32: the per-stage rows are the LDS image's rows), so staging it is
-//     plain 16-B copies — no B split VALU;
-//   * two LDS stage buffers (2 x 72 KB, two distinct __shared__ arrays so the compiler knows that the staging
-//     stores of K-tile t + 1 and the fragment reads of K-tile t do not alias) and register prefetch one K-tile ahead:
-//     step t splits and stores tile t + 1 into one buffer while the MFMAs of tile t read the other, then ONE barrier.
-//     The split VALU of t + 1 and the MFMAs of t are in one basic block, free to interleave (the PMC of the 3-wave
-//     register-staged kernel, profiles/r03/gemm_pmc_k512.txt: its VALU and MFMA time add up to 95 % of the SIMD
-//     cycles, i.e. they hardly overlap).
-// Products, k order per accumulator and the epilogue are k_gemm_nt's: bit-identical to it.
-template <int EPI>
-__global__ __launch_bounds__(256, 1) void k_nt_pipe(Src2 A, int64_t M, int64_t N, int64_t K,
-                                                   const float* __restrict__ bias, const float* __restrict__ prelu,
-                                                   const float* __restrict__ accum, float* __restrict__ Z,
-                                                   float* __restrict__ Y, int64_t ldc, bool vec_out, int64_t n_tiles,
-                                                   bool xcd, CombEpi ce, const uint16_t* __restrict__ Bp) {
-  constexpr int NT = 256, TN = 4, WN = 2, BM = 128, BN = 256, WCOLS = 128;
-  constexpr int kRowW = kSplitRowWordsNT;
-  constexpr int kBufW = (BM + BN) * kRowW;          // 18432 words = 72 KB per stage buffer
-  constexpr int kBCh = BN * kRowW / 4 / NT;         // 16-B B chunks per thread per K-tile (12)
-  __shared__ __attribute__((aligned(16))) float smem0[kBufW];
-  __shared__ __attribute__((aligned(16))) float smem1[kBufW];
-  uint32_t* A0 = reinterpret_cast<uint32_t*>(smem0);
-  uint32_t* B0 = A0 + BM * kRowW;
-  uint32_t* A1 = reinterpret_cast<uint32_t*>(smem1);
-  uint32_t* B1 = A1 + BM * kRowW;
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wave = tid >> 6;
-  const int wm = wave / WN;
-  const int wn = wave % WN;
-  const int li = lane & 31;
-  const int lh = lane >> 5;
-  const int64_t n_tiles_n = N / BN;
-  const int64_t q = xcd ? xcd_logical(blockIdx.x, gridDim.x) : (int64_t)blockIdx.x;
-  if (q >= n_tiles) return;
-  const int64_t m0 = (q / n_tiles_n) * BM;
-  const int64_t n0 = (q % n_tiles_n) * BN;
-
-  f32x16 acc[2][TN];
-#pragma unroll
-  for (int a = 0; a < 2; ++a)
-#pragma unroll
-    for (int b = 0; b < TN; ++b)
-#pragma unroll
-      for (int e = 0; e < 16; ++e) acc[a][b][e] = 0.0f;
-
-  // B: thread tid stages image row tid (12 chunks: plane w / 4, slot w % 4 = the planes' stage row (n0 + tid, plane),
-  // byte w % 4 * 16), so its sources are one base plus compile-time / uniform offsets (no per-chunk address
-  // registers); the row-per-lane LDS stores (192-B stride) are 4-way bank-conflicted, 12 per K-tile
-  static_assert(BN == NT, "one B row per thread");
-  const int64_t stage_bytes = 3 * N * 64;
-  const int64_t plane_bytes = N * 64;
-  const char* brow = reinterpret_cast<const char*>(Bp) + (n0 + tid) * 64;
-  float4 ra[BM / 32];
-  using u4x4 = __attribute__((ext_vector_type(16))) unsigned int;
-  u4x4 rb0, rb1, rb2;   // the row's three 64-B plane segments (as arrays of uint4 they were demoted to scratch)
-  static_assert(kBCh == 12, "three planes x four 16-B chunks");
-  const float sc2 = self_scale(A.eps2);
-  bool scale_a = false;
-  const int64_t T = K / kBK;
-  auto load = [&](int64_t t) {   // K-tile t (clamped: the pipeline's last prefetch re-reads the last tile)
-    t = t < T ? t : T - 1;
-    const int64_t k0 = t * kBK;
-    load_tile<true, BM, NT>(ra, A, m0, M, k0, K, tid, sc2);
-    scale_a = A.eps2 != nullptr && k0 >= A.k1;
-    const char* base = brow + t * stage_bytes;
-    rb0 = *reinterpret_cast<const u4x4*>(base);
-    rb1 = *reinterpret_cast<const u4x4*>(base + plane_bytes);
-    rb2 = *reinterpret_cast<const u4x4*>(base + 2 * plane_bytes);
-  };
-  auto stage = [&](uint32_t* As, uint32_t* Bs) {
-    if (scale_a) scale_tile<BM, NT>(ra, sc2);
-    store_tile_split<BM, NT>(As, ra, tid);
-    *reinterpret_cast<u4x4*>(Bs + tid * kRowW) = rb0;
-    *reinterpret_cast<u4x4*>(Bs + tid * kRowW + 16) = rb1;
-    *reinterpret_cast<u4x4*>(Bs + tid * kRowW + 32) = rb2;
-  };
-  auto mma = [&](const uint32_t* As, const uint32_t* Bs) {
-#pragma unroll
-    for (int kb = 0; kb < 2; ++kb) {
-      bf16x8 fa[2][3], fb[TN][3];
-#pragma unroll
-      for (int t = 0; t < 2; ++t)
-#pragma unroll
-        for (int p = 0; p < 3; ++p)
-          fa[t][p] = *reinterpret_cast<const bf16x8*>(As + (wm * 64 + t * 32 + li) * kRowW + p * 16 +
-                                                      nt_chunk(li, kb * 2 + lh));
-#pragma unroll
-      for (int t = 0; t < TN; ++t)
-#pragma unroll
-        for (int p = 0; p < 3; ++p)
-          fb[t][p] = *reinterpret_cast<const bf16x8*>(Bs + (wn * WCOLS + t * 32 + li) * kRowW + p * 16 +
-                                                      nt_chunk(li, kb * 2 + lh));
-#pragma unroll
-      for (int tm = 0; tm < 2; ++tm)
-#pragma unroll
-        for (int tn = 0; tn < TN; ++tn) {   // k_gemm_nt's order: smallest terms first
-          acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[tm][2], fb[tn][0], acc[tm][tn], 0, 0, 0);
-          acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[tm][1], fb[tn][1], acc[tm][tn], 0, 0, 0);
-          acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[tm][0], fb[tn][2], acc[tm][tn], 0, 0, 0);
-          acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[tm][1], fb[tn][0], acc[tm][tn], 0, 0, 0);
-          acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[tm][0], fb[tn][1], acc[tm][tn], 0, 0, 0);
-          acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[tm][0], fb[tn][0], acc[tm][tn], 0, 0, 0);
-        }
-    }
-  };
-  load(0);
-  stage(A0, B0);
-  load(1);
-  __syncthreads();
-  for (int64_t t = 0; t < T; t += 2) {   // T even: tile t from buffer 0, tile t + 1 from buffer 1
-    stage(A1, B1);                        // tile t + 1
-    load(t + 2);
-    mma(A0, B0);                          // tile t
-    __syncthreads();
-    stage(A0, B0);                        // tile t + 2 (clamped at the end: unused)
-    load(t + 3);
-    mma(A1, B1);                          // tile t + 1
-    __syncthreads();
-  }
-  float ep = 0.0f;
-  epilogue<EPI, TN, float>(acc, smem0, wave, wm, wn, lane, li, lh, m0, n0, M, N, bias, prelu, accum, Z, Y, ldc,
-                           vec_out, ce, &ep);
-  if constexpr (EPI == 4) tile_partial(smem0, ep, ce.part, q);
-}
-
-// HGIN_NT_TN4: 1 = the register-staged kernel at 128 x 256 (one workgroup per CU); 2 = k_nt_pipe
-int nt_tn4_mode() {
-  static const int v = [] {
-    const char* e = getenv("HGIN_NT_TN4");
-    return e ? atoi(e) : 0;
-  }();
-  return v;
-}
-
-// k_nt_pp — the fp32 split-mode NT GEMM (N a multiple of 128, clean tiles, B pre-split by hgin_nt_planes_f32) as a
-// ping-pong of two 4-wave halves (cdna_hip_programming.md, MI355X_MICROARCH.md "Two waves per SIMD"): one 8-wave
-// workgroup per CU computes a 256 x 128 tile as two 128 x 128 halves that share the B image.  Each SIMD holds one wave
-// of each half, and the halves alternate roles every phase (one raw barrier per phase):
-//   phase a(t): half 0 runs its 48 MFMAs per wave on K-tile t   | half 1 splits + stores its A tile t, issues the
-//                                                                 B DMA of t + 1 and its A loads of t + 1
-//   phase b(t): half 1 runs its MFMAs on K-tile t               | half 0 splits + stores its A tile t + 1 and issues
-//                                                                 its A loads of t + 2
-// so the matrix pipe of every SIMD is fed by one wave while the split VALU, LDS stores and memory issue of the other
-// wave run beside it (the 3-workgroup register-staged tile serialises them: MFMA ~45 % busy, profiles/r03/).  B is
-// double-buffered (the DMA of t + 1 lands under the phases of t); A loads have two phases of cover.
-// Products, per-accumulator k order and the epilogue are k_gemm_nt's: bit-identical to it.
-template <int EPI>
-__global__ __launch_bounds__(512, 1) void k_nt_pp(Src2 A, int64_t M, int64_t N, int64_t K,
-                                                 const float* __restrict__ bias, const float* __restrict__ prelu,
-                                                 const float* __restrict__ accum, float* __restrict__ Z,
-                                                 float* __restrict__ Y, int64_t ldc, bool vec_out, int64_t n_tiles,
-                                                 bool xcd, CombEpi ce, const uint16_t* __restrict__ Bp) {
-  constexpr int RW = kSplitRowWordsNT;            // 48 words per image row
-  constexpr int IMG = 128 * RW;                   // words per 128-row image
-  __shared__ __attribute__((aligned(16))) uint32_t smem[4 * IMG];   // A half 0, A half 1, B buffer 0, B buffer 1
-  const int tid = threadIdx.x;
-  const int t4 = tid & 255;
-  const int lane = tid & 63;
-  const int wave = tid >> 6;
-  const int half = wave >> 2;
-  const int w4 = wave & 3;
-  const int wm = w4 >> 1, wn = w4 & 1;
-  const int li = lane & 31, lh = lane >> 5;
-  const int64_t n_tiles_n = N / 128;
-  const int64_t q = xcd ? xcd_logical(blockIdx.x, gridDim.x) : (int64_t)blockIdx.x;
-  if (q >= n_tiles) return;
-  const int64_t m0 = (q / n_tiles_n) * 256 + half * 128;   // this half's rows
-  const int64_t n0 = (q % n_tiles_n) * 128;
-  uint32_t* Aimg = smem + half * IMG;
-  uint32_t* Bimg = smem + 2 * IMG;
-  const int T = (int)(K / kBK);
-
-  f32x16 acc[2][2];
-#pragma unroll
-  for (int a = 0; a < 2; ++a)
-#pragma unroll
-    for (int b = 0; b < 2; ++b)
-#pragma unroll
-      for (int e = 0; e < 16; ++e) acc[a][b][e] = 0.0f;
-
-  float4 ra0[4], ra1[4];   // A prefetch two K-tiles deep (tile t in ra<t & 1>)
-  const float sc2 = self_scale(A.eps2);
-  auto load_a = [&](float4 (&r)[4], int t) {
-    load_tile<true, 128, 256>(r, A, m0, M, (int64_t)t * kBK, K, t4, sc2);
-  };
-  auto stage_a = [&](float4 (&r)[4], int t) {
-    if (A.eps2 != nullptr && (int64_t)t * kBK >= A.k1) scale_tile<128, 256>(r, sc2);
-    store_tile_split<128, 256>(Aimg, r, t4);
-  };
-  uint32_t boff[6];
-#pragma unroll
-  for (int i = 0; i < 6; ++i) {
-    const int j = (w4 * 6 + i) * 64 + lane;   // image chunk: row j / 12, word group j % 12
-    const int rr = j / 12, w = j % 12;
-    boff[i] = (uint32_t)((((w >> 2) * N + n0 + rr) * 64) + (w & 3) * 16);
-  }
-  auto dma_b = [&](int t) {   // half 1 only
-    const char* base = reinterpret_cast<const char*>(Bp) + (int64_t)t * 3 * N * 64;
-    char* dst = reinterpret_cast<char*>(Bimg + (t & 1) * IMG) + w4 * 6 * 1024;
-#pragma unroll
-    for (int i = 0; i < 6; ++i) glds16_asm(base + boff[i], dst + i * 1024);
-  };
-  auto mfma_tile = [&](int t) {
-    const uint32_t* Bs = Bimg + (t & 1) * IMG;
-#pragma unroll
-    for (int kb = 0; kb < 2; ++kb) {
-      bf16x8 fa[2][3], fb[2][3];
-#pragma unroll
-      for (int u = 0; u < 2; ++u)
-#pragma unroll
-        for (int p = 0; p < 3; ++p) {
-          fa[u][p] = *reinterpret_cast<const bf16x8*>(Aimg + (wm * 64 + u * 32 + li) * RW + p * 16 +
-                                                      nt_chunk(li, kb * 2 + lh));
-          fb[u][p] = *reinterpret_cast<const bf16x8*>(Bs + (wn * 64 + u * 32 + li) * RW + p * 16 +
-                                                      nt_chunk(li, kb * 2 + lh));
-        }
-#pragma unroll
-      for (int tm = 0; tm < 2; ++tm)
-#pragma unroll
-        for (int tn = 0; tn < 2; ++tn) {   // k_gemm_nt's order: smallest terms first
-          acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[tm][2], fb[tn][0], acc[tm][tn], 0, 0, 0);
-          acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[tm][1], fb[tn][1], acc[tm][tn], 0, 0, 0);
-          acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[tm][0], fb[tn][2], acc[tm][tn], 0, 0, 0);
-          acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[tm][1], fb[tn][0], acc[tm][tn], 0, 0, 0);
-          acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[tm][0], fb[tn][1], acc[tm][tn], 0, 0, 0);
-          acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[tm][0], fb[tn][0], acc[tm][tn], 0, 0, 0);
-        }
-    }
-  };
-
-  // prologue: B(0) by half 1; half 0 stages A(0) and prefetches A(1), A(2); half 1 prefetches A(0), A(1)
-  if (half == 1) dma_b(0);
-  load_a(ra0, 0);
-  if (half == 0) stage_a(ra0, 0);
-  if (T > 1) load_a(ra1, 1);
-  if (half == 0 && T > 2) load_a(ra0, 2);
-  if (half == 1) {   // B(0) landed (the A loads issued after it may still be in flight)
-    if (T > 1) wait_vm<8>();
-    else wait_vm<4>();
-  }
-  __syncthreads();
-  // one K-tile: phase a — half 0 computes tile t, half 1 stages its tile t (from rc), issues B(t + 1) and A(t + 2)
-  // (into rc); phase b — half 1 computes tile t, half 0 stages its tile t + 1 (from rn) and issues A(t + 3) (into rn)
-  auto ktile = [&](int t, float4 (&rc)[4], float4 (&rn)[4]) {
-    if (half == 0) {
-      __builtin_amdgcn_s_setprio(1);
-      mfma_tile(t);
-      __builtin_amdgcn_s_setprio(0);
-    } else {
-      stage_a(rc, t);
-      if (t + 1 < T) dma_b(t + 1);
-      if (t + 2 < T) load_a(rc, t + 2);
-    }
-    __syncthreads();
-    if (half == 1) {
-      __builtin_amdgcn_s_setprio(1);
-      mfma_tile(t);
-      __builtin_amdgcn_s_setprio(0);
-      if (t + 2 < T) wait_vm<4>();        // B(t + 1) landed before half 0 reads it (A(t + 2) may be in flight)
-      else if (t + 1 < T) wait_vm<0>();
-    } else if (t + 1 < T) {
-      stage_a(rn, t + 1);
-      if (t + 3 < T) load_a(rn, t + 3);
-    }
-    __syncthreads();
-  };
-  for (int t = 0; t < T; t += 2) {
-    ktile(t, ra0, ra1);
-    if (t + 1 < T) ktile(t + 1, ra1, ra0);
-  }
-
-  float ep = 0.0f;
-  epilogue<EPI, 2, float>(acc, reinterpret_cast<float*>(smem), wave, wm, wn, lane, li, lh, m0, n0, M, N, bias, prelu,
-                          accum, Z, Y, ldc, vec_out, ce, &ep);
-}
-
-// HGIN_NT_PP=1: k_nt_pp for the fp32 split-mode 128-column tiles (A/B)
-bool nt_pp_enabled() {
-  static const bool on = [] {
-    const char* v = getenv("HGIN_NT_PP");
-    return v && v[0] == '1';
   }();
   return on;
 }
@@ -927,49 +570,8 @@ int64_t launch_nt_tn(bool vec, const Src2& a, const Src2& b, int64_t M, int64_t 
   const bool xcd = xcd_remap_enabled();
   dim3 grid((unsigned)(xcd ? round_up8(tiles) : tiles));
   if constexpr (TN == 2 && WN == 2 && NW == 4) {
-    // 128 x 256 tiles (A read once at N = 256; one workgroup per CU): HGIN_NT_TN4=1 the register-staged kernel,
-    // 2 the software pipeline k_nt_pipe (K a multiple of 64)
-    const int tn4 = nt_tn4_mode();
-    if (tn4 && planes && vec && gemm_split_enabled() && !gemm_h2_enabled() && N % 256 == 0 && nt_bdma_enabled() &&
-        (tn4 == 1 || K % 64 == 0) && (int64_t)N * K * 6 < (int64_t(1) << 32)) {
-      const int64_t t4 = ceil_div(N, 256) * ceil_div(M, 128);
-      dim3 g4((unsigned)(xcd ? round_up8(t4) : t4));
-      if (tn4 == 2) {
-        HGIN_TRACE("k_nt_pipe<EPI%d,128x256,N%lld,K%lld>", EPI, (long long)N, (long long)K);
-        k_nt_pipe<EPI><<<g4, 256, 0, s>>>(a, M, N, K, bias, prelu, accum, z, y, ldc, vec_out, t4, xcd, ce,
-                                          static_cast<const uint16_t*>(planes));
-      } else {
-        HGIN_TRACE("k_gemm_nt<EPI%d,128x256,split_bdma,N%lld,K%lld>", EPI, (long long)N, (long long)K);
-        k_gemm_nt<EPI, true, 4, 2, true, 4, 1><<<g4, 256, 0, s>>>(a, b, M, N, K, bias, prelu, accum, z, y, ldc,
-                                                                     vec_out, t4, xcd, ce,
-                                                                     static_cast<const uint16_t*>(planes));
-      }
-      return t4;
-    }
-    if (planes && vec && gemm_split_enabled() && !gemm_h2_enabled() && N % BN == 0 && nt_bdma_enabled() &&
+    if (planes && vec && gemm_split_enabled() && N % BN == 0 && nt_bdma_enabled() &&
         (int64_t)N * K * 6 < (int64_t(1) << 32)) {
-      if (EPI != 4 && nt_pp_enabled()) {
-        const int64_t tp = ceil_div(N, 128) * ceil_div(M, 256);
-        dim3 gp((unsigned)(xcd ? round_up8(tp) : tp));
-        HGIN_TRACE("k_nt_pp<EPI%d,256x128,N%lld,K%lld>", EPI, (long long)N, (long long)K);
-        k_nt_pp<EPI><<<gp, 512, 0, s>>>(a, M, N, K, bias, prelu, accum, z, y, ldc, vec_out, tp, xcd, ce,
-                                        static_cast<const uint16_t*>(planes));
-        return tp;
-      }
-      if (nt_bdb_enabled()) {
-        HGIN_TRACE("k_gemm_nt<EPI%d,%dx%d,split_bdma2,N%lld,K%lld>", EPI, BM, BN, (long long)N, (long long)K);
-        k_gemm_nt<EPI, true, 2, 2, true, 4, 2><<<grid, 256, 0, s>>>(a, b, M, N, K, bias, prelu, accum, z, y, ldc,
-                                                                    vec_out, tiles, xcd, ce,
-                                                                    static_cast<const uint16_t*>(planes));
-        return tiles;
-      }
-      if (nt_m16_enabled()) {
-        HGIN_TRACE("k_gemm_nt<EPI%d,%dx%d,split_bdma_m16,N%lld,K%lld>", EPI, BM, BN, (long long)N, (long long)K);
-        k_gemm_nt<EPI, true, 2, 2, true, 4, 1, true><<<grid, 256, 0, s>>>(a, b, M, N, K, bias, prelu, accum, z, y,
-                                                                          ldc, vec_out, tiles, xcd, ce,
-                                                                          static_cast<const uint16_t*>(planes));
-        return tiles;
-      }
       HGIN_TRACE("k_gemm_nt<EPI%d,%dx%d,split_bdma,N%lld,K%lld>", EPI, BM, BN, (long long)N, (long long)K);
       k_gemm_nt<EPI, true, 2, 2, true, 4, 1><<<grid, 256, 0, s>>>(a, b, M, N, K, bias, prelu, accum, z, y, ldc,
                                                                   vec_out, tiles, xcd, ce,
@@ -1063,331 +665,6 @@ int launch_nt(const Src2& a, const Src2& b, int64_t M, int64_t N, int64_t K, con
   return check_launch(what);
 }
 
-// ---- "h2" mode (HGIN_F32_GEMM=h2): fp32 operands as two scaled fp16 terms, three products ------------------
-// Each fp32 operand row is scaled by a power of two 2^e (exact) and written as h1 = fp16(a 2^e), h2 = fp16(a 2^e -
-// h1) (RNE; the residual is exact in fp32), so a 2^e = h1 + h2 to within 2^-22 |a 2^e|; a product is formed from
-// the three v_mfma_f32_32x32x16_f16 terms h2 g1, h1 g2, h1 g1 (the dropped h2 g2 is below 2^-22 |ab|) with fp32
-// accumulation, and the result is scaled back exactly in the epilogue — the two-term split of 3xTF32 (TF32 and fp16
-// carry the same 11-bit significand), half the matrix-core work and two thirds of the LDS image of the six-product
-// bf16 split.  fp16's narrow exponent range is what the scaling is for:
-//   * B (the weight [N, K]): one exponent per row n, from the row's max (k_h2_planes, once per call): the scaled
-//     row max lies in [2^13, 2^14).
-//   * A rows: the tile's K loop discovers them — a row's exponent is set at its first nonzero K-tile (scaled max
-//     in [2^7, 2^8)) and lowered only when a later K-tile's max could reach 2^15 (fp16 max 65504); the row's
-//     accumulators are then scaled by the same exact power of two before the next products land.  Elements far
-//     below their row's max lose low bits only below 2^-24 of the scaled unit (2^-32 of the row max).
-// Results differ from the six-product split by rounding only (both are within the fp32-evaluation bound of an
-// exact product; tests/test_gpu_kernels.py::test_h2_gemm_*).
-using f16x8 = __attribute__((ext_vector_type(8))) _Float16;
-using f16x2v = __attribute__((ext_vector_type(2))) _Float16;
-constexpr int kH2RowWords = 32;       // LDS row: 2 planes x 32 fp16 of one K-tile = 8 16-B chunks
-constexpr int kH2Unset = -100000;     // row exponent before the row's first nonzero K-tile
-
-// chunk c of plane p of row r at slot (4p + c) ^ swz(r): a ds_read_b128 lane group (16 rows, one (p, c)) covers
-// 2 row parities x 8 swizzles = 16 distinct slots; the staging stores (4 rows x 8 lanes x 8 B per 32 lanes)
-// cover 4 disjoint 16-bank blocks (swz bit 2 follows row bit 1)
-__device__ __forceinline__ int h2_swz(int r) { return (((r >> 1) & 1) << 2) | ((r >> 2) & 3); }
-__device__ __forceinline__ int h2_word(int r, int p, int c) { return ((p * 4 + c) ^ h2_swz(r)) << 2; }
-
-__device__ __forceinline__ uint32_t cvt_pk_f16(float lo, float hi) {
-  return __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2_t{lo, hi}, f16x2v));
-}
-__device__ __forceinline__ void h2_split2(float x0, float x1, uint32_t& hi, uint32_t& lo) {
-  hi = cvt_pk_f16(x0, x1);
-  const f16x2v h = __builtin_bit_cast(f16x2v, hi);
-  lo = cvt_pk_f16(x0 - (float)h.x, x1 - (float)h.y);
-}
-__device__ __forceinline__ uint32_t absbits(float x) { return __float_as_uint(x) & 0x7fffffffu; }
-// max over the 8 consecutive lanes of a staging row (quad swaps, then the mirrored half-row)
-__device__ __forceinline__ uint32_t umax8(uint32_t v) {
-  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false));
-  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, false));
-  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x141, 0xF, 0xF, false));
-  return v;
-}
-// A row exponent after a K-tile whose |max| has the bits mbits; d = the accumulator rescale (0 = none)
-__device__ __forceinline__ int h2_row_exp(uint32_t mbits, int cur, int& d) {
-  d = 0;
-  if (mbits == 0) return cur;
-  int be = (int)(mbits >> 23);
-  be = be < 1 ? 1 : (be > 254 ? 254 : be);
-  if (cur == kH2Unset) return 134 - be;                 // max 2^e in [2^7, 2^8)
-  if (be + cur > 141) {                                 // max 2^e could reach 2^15
-    d = 134 - be - cur;
-    return 134 - be;
-  }
-  return cur;
-}
-
-// B planes: [N][K / 32][2][32] fp16 (hi, lo of B[n, k] 2^f[n]), then int32 f[N] at byte N * K * 4.
-size_t h2_planes_bytes(int64_t N, int64_t K) { return (size_t)N * (size_t)K * 4 + align_up((size_t)N * 4, 256); }
-
-__global__ __launch_bounds__(64) void k_h2_planes(const float* __restrict__ b, int64_t ldb, int64_t K,
-                                                  uint16_t* __restrict__ out, int* __restrict__ fexp) {
-  const int64_t n = blockIdx.x;
-  const int lane = threadIdx.x;
-  const float* row = b + n * ldb;
-  uint32_t m = 0;
-  for (int64_t k = lane; k < K; k += 64) m = max(m, absbits(row[k]));
-  for (int off = 32; off > 0; off >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, off));
-  int f = 0;
-  if (m) {
-    int be = (int)(m >> 23);
-    be = be < 1 ? 1 : (be > 254 ? 254 : be);
-    f = 140 - be;                                       // row max 2^f in [2^13, 2^14)
-  }
-  if (lane == 0) fexp[n] = f;
-  uint16_t* o = out + n * K * 2;
-  for (int64_t k = 2 * lane; k < K; k += 128) {
-    uint32_t hi, lo;
-    h2_split2(__builtin_ldexpf(row[k], f), __builtin_ldexpf(row[k + 1], f), hi, lo);
-    const int64_t base = (k / 32) * 64 + (k % 32);
-    *reinterpret_cast<uint32_t*>(o + base) = hi;
-    *reinterpret_cast<uint32_t*>(o + base + 32) = lo;
-  }
-}
-
-// The clean-tile NT GEMM of k_gemm_nt in h2 mode (same tiling, epilogue and XCD order; A from Src2 with the eps2
-// self term; B from k_h2_planes).  Requirements (h2_eligible): K and k1 multiples of 32, 16-B aligned A rows.
-template <int EPI, int TN, int WNv, int OCC>
-__global__ __launch_bounds__(256, OCC) void k_gemm_nt_h2(Src2 A, const uint16_t* __restrict__ Bp,
-                                                      const int* __restrict__ bexp, int64_t M, int64_t N, int64_t K,
-                                                      const float* __restrict__ bias, const float* __restrict__ prelu,
-                                                      const float* __restrict__ accum, float* __restrict__ Z,
-                                                      float* __restrict__ Y, int64_t ldc, bool vec_out, int64_t n_tiles,
-                                                      bool xcd, CombEpi ce) {
-  constexpr int NT = 256;
-  constexpr int WN = WNv;
-  constexpr int WM = 4 / WN;
-  constexpr int BM = WM * 64;
-  constexpr int BN = WN * TN * 32;
-  constexpr int WCOLS = TN * 32;
-  constexpr int kStageW = (BM + BN) * kH2RowWords;
-  constexpr int kEpiW = 4 * 32 * (WCOLS + 4);
-  __shared__ __attribute__((aligned(16))) float smem[kStageW > kEpiW ? kStageW : kEpiW];
-  __shared__ __attribute__((aligned(16))) int row_e[BM];
-  __shared__ __attribute__((aligned(16))) int row_d[BM];
-  __shared__ int resc;
-  uint32_t* Ash = reinterpret_cast<uint32_t*>(smem);
-  uint32_t* Bsh = Ash + BM * kH2RowWords;
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wave = tid >> 6;
-  const int wm = wave / WN;
-  const int wn = wave % WN;
-  const int li = lane & 31;
-  const int lh = lane >> 5;
-  const int qd = tid & 7;
-  const int64_t n_tiles_n = (N + BN - 1) / BN;
-  const int64_t q = xcd ? xcd_logical(blockIdx.x, gridDim.x) : (int64_t)blockIdx.x;
-  if (q >= n_tiles) return;
-  const int64_t m0 = (q / n_tiles_n) * BM;
-  const int64_t n0 = (q % n_tiles_n) * BN;
-  if (tid < BM) row_e[tid] = kH2Unset;
-  if (tid == 0) resc = -1;
-
-  f32x16 acc[2][TN];
-#pragma unroll
-  for (int a = 0; a < 2; ++a)
-#pragma unroll
-    for (int b = 0; b < TN; ++b)
-#pragma unroll
-      for (int e = 0; e < 16; ++e) acc[a][b][e] = 0.0f;
-
-  float4 ra[BM / 32];
-  uint4 rb[BN / 32];
-  const float sc2 = self_scale(A.eps2);
-  bool scale_a = false;
-  auto load_a = [&](int64_t k0) {
-    load_tile<true, BM, NT>(ra, A, m0, M, k0, K, tid, sc2);
-    scale_a = A.eps2 != nullptr && k0 >= A.k1;
-  };
-  auto load_b = [&](int64_t k0) {
-#pragma unroll
-    for (int i = 0; i < BN / 32; ++i) {
-      int64_t n = n0 + (tid >> 3) + 32 * i;
-      n = n < N ? n : N - 1;
-      rb[i] = *reinterpret_cast<const uint4*>(Bp + n * K * 2 + (k0 / 32) * 64 + qd * 8);
-    }
-  };
-  auto stage = [&](int tile) {
-    if (scale_a) scale_tile<BM, NT>(ra, sc2);
-#pragma unroll
-    for (int i = 0; i < BM / 32; ++i) {
-      const int rr = (tid >> 3) + 32 * i;
-      const float4 v = ra[i];
-      const uint32_t mb = umax8(max(max(absbits(v.x), absbits(v.y)), max(absbits(v.z), absbits(v.w))));
-      const int cur = row_e[rr];
-      int d;
-      const int e = h2_row_exp(mb, cur, d);
-      if (qd == 0) {
-        row_e[rr] = e;
-        row_d[rr] = d;
-      }
-      if (d != 0) resc = tile;
-      const int es = e == kH2Unset ? 0 : e;
-      uint2 hi, lo;
-      h2_split2(__builtin_ldexpf(v.x, es), __builtin_ldexpf(v.y, es), hi.x, lo.x);
-      h2_split2(__builtin_ldexpf(v.z, es), __builtin_ldexpf(v.w, es), hi.y, lo.y);
-      uint32_t* row = Ash + rr * kH2RowWords + (qd & 1) * 2;
-      *reinterpret_cast<uint2*>(row + h2_word(rr, 0, qd >> 1)) = hi;
-      *reinterpret_cast<uint2*>(row + h2_word(rr, 1, qd >> 1)) = lo;
-    }
-#pragma unroll
-    for (int i = 0; i < BN / 32; ++i) {
-      const int rr = (tid >> 3) + 32 * i;
-      *reinterpret_cast<uint4*>(Bsh + rr * kH2RowWords + h2_word(rr, qd >> 2, qd & 3)) = rb[i];
-    }
-  };
-  load_a(0);
-  load_b(0);
-  __syncthreads();   // row_e / resc initialised
-  stage(0);
-  __syncthreads();
-  for (int64_t k0 = 0; k0 < K; k0 += kBK) {
-    const int tile = (int)(k0 / kBK);
-    const bool more = k0 + kBK < K;
-    if (resc == tile) {   // some row's exponent was lowered for this K-tile: rescale its accumulators (rare)
-#pragma unroll
-      for (int tm = 0; tm < 2; ++tm)
-#pragma unroll
-        for (int e4 = 0; e4 < 4; ++e4) {
-          const int4 d4 = *reinterpret_cast<const int4*>(row_d + wm * 64 + tm * 32 + 8 * e4 + 4 * lh);
-          const int dd[4] = {d4.x, d4.y, d4.z, d4.w};
-#pragma unroll
-          for (int tn = 0; tn < TN; ++tn)
-#pragma unroll
-            for (int j = 0; j < 4; ++j) acc[tm][tn][4 * e4 + j] = __builtin_ldexpf(acc[tm][tn][4 * e4 + j], dd[j]);
-        }
-    }
-    if (more) {
-      load_a(k0 + kBK);
-      load_b(k0 + kBK);
-    }
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int kb = 0; kb < 2; ++kb) {
-      f16x8 fa[2][2], fb[TN][2];
-#pragma unroll
-      for (int t = 0; t < 2; ++t) {
-        const int r = wm * 64 + t * 32 + li;
-#pragma unroll
-        for (int p = 0; p < 2; ++p)
-          fa[t][p] = *reinterpret_cast<const f16x8*>(Ash + r * kH2RowWords + h2_word(r, p, kb * 2 + lh));
-      }
-#pragma unroll
-      for (int t = 0; t < TN; ++t) {
-        const int r = wn * WCOLS + t * 32 + li;
-#pragma unroll
-        for (int p = 0; p < 2; ++p)
-          fb[t][p] = *reinterpret_cast<const f16x8*>(Bsh + r * kH2RowWords + h2_word(r, p, kb * 2 + lh));
-      }
-#pragma unroll
-      for (int tm = 0; tm < 2; ++tm)
-#pragma unroll
-        for (int tn = 0; tn < TN; ++tn) {   // smallest terms first
-          acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fa[tm][1], fb[tn][0], acc[tm][tn], 0, 0, 0);
-          acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fa[tm][0], fb[tn][1], acc[tm][tn], 0, 0, 0);
-          acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fa[tm][0], fb[tn][0], acc[tm][tn], 0, 0, 0);
-        }
-    }
-    __builtin_amdgcn_s_setprio(0);
-    if (more) {
-      __syncthreads();
-      stage(tile + 1);
-      __syncthreads();
-    }
-  }
-  // scale back: C = acc 2^-(e_row + f_col), exact
-  int fc[TN];
-#pragma unroll
-  for (int tn = 0; tn < TN; ++tn) {
-    const int64_t col = n0 + wn * WCOLS + tn * 32 + li;
-    fc[tn] = col < N ? bexp[col] : 0;
-  }
-#pragma unroll
-  for (int tm = 0; tm < 2; ++tm)
-#pragma unroll
-    for (int e4 = 0; e4 < 4; ++e4) {
-      const int4 r4 = *reinterpret_cast<const int4*>(row_e + wm * 64 + tm * 32 + 8 * e4 + 4 * lh);
-      const int er[4] = {r4.x == kH2Unset ? 0 : r4.x, r4.y == kH2Unset ? 0 : r4.y, r4.z == kH2Unset ? 0 : r4.z,
-                         r4.w == kH2Unset ? 0 : r4.w};
-#pragma unroll
-      for (int tn = 0; tn < TN; ++tn)
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-          acc[tm][tn][4 * e4 + j] = __builtin_ldexpf(acc[tm][tn][4 * e4 + j], -(er[j] + fc[tn]));
-    }
-  float ep = 0.0f;
-  epilogue<EPI, TN, float>(acc, smem, wave, wm, wn, lane, li, lh, m0, n0, M, N, bias, prelu, accum, Z, Y, ldc,
-                           vec_out, ce, &ep);
-  if constexpr (EPI == 4) tile_partial(smem, ep, ce.part, q);
-}
-
-// occupancy bound of k_gemm_nt_h2 (HGIN_H2_OCC = 2 / 3 waves per SIMD; A/B)
-int h2_occ() {
-  static const int v = [] {
-    const char* e = getenv("HGIN_H2_OCC");
-    return e ? atoi(e) : 2;
-  }();
-  return v;
-}
-
-bool h2_eligible(const float* a1, int64_t lda1, int64_t k1, const float* a2, int64_t lda2, const void* planes,
-                 int64_t K) {
-  if (!planes || !gemm_h2_enabled()) return false;
-  if (K % kBK || k1 % kBK) return false;
-  if (k1 > 0 && (!aligned16(a1) || lda1 % 4)) return false;
-  if (k1 < K && (!aligned16(a2) || lda2 % 4)) return false;
-  return true;
-}
-
-template <int EPI>
-int launch_nt_h2(const Src2& a, const void* planes, int64_t M, int64_t N, int64_t K, const float* bias,
-                 const float* prelu, const float* accum, float* z, float* y, int64_t ldc, hipStream_t s,
-                 const char* what, const CombEpi& ce_in = CombEpi{}, int64_t* tiles_out = nullptr) {
-  CombEpi ce = ce_in;
-  ce.nt_io = gemm_nt_io(M, N, 4);
-  const bool vec_out = ldc % 4 == 0 && aligned16(y) && (z == nullptr || aligned16(z)) &&
-                       (accum == nullptr || aligned16(accum)) &&
-                       (EPI != 4 || (aligned16(ce.xd) && ce.ldxd % 4 == 0 &&
-                                     (ce.gd == nullptr || (aligned16(ce.gd) && ce.ldgd % 4 == 0))));
-  const uint16_t* bp = static_cast<const uint16_t*>(planes);
-  const int* fexp = reinterpret_cast<const int*>(static_cast<const char*>(planes) + (size_t)N * (size_t)K * 4);
-  const bool xcd = xcd_remap_enabled();
-  int64_t tiles;
-#define HGIN_NT_H2(TNV, WNV)                                                                                      \
-  {                                                                                                               \
-    constexpr int BM = (4 / WNV) * 64, BN = WNV * TNV * 32;                                                       \
-    tiles = ceil_div(N, BN) * ceil_div(M, BM);                                                                    \
-    dim3 grid((unsigned)(xcd ? round_up8(tiles) : tiles));                                                        \
-    HGIN_TRACE("k_gemm_nt_h2<EPI%d,%dx%d,N%lld,K%lld>", EPI, BM, BN, (long long)N, (long long)K);                  \
-    if (h2_occ() == 3)                                                                                            \
-      k_gemm_nt_h2<EPI, TNV, WNV, 3><<<grid, 256, 0, s>>>(a, bp, fexp, M, N, K, bias, prelu, accum, z, y, ldc,     \
-                                                          vec_out, tiles, xcd, ce);                               \
-    else                                                                                                          \
-      k_gemm_nt_h2<EPI, TNV, WNV, 2><<<grid, 256, 0, s>>>(a, bp, fexp, M, N, K, bias, prelu, accum, z, y, ldc,     \
-                                                          vec_out, tiles, xcd, ce);                               \
-  }
-  if (N <= 32)
-    HGIN_NT_H2(1, 1)
-  else if (use_bm64<EPI == 4 ? 0 : EPI>(M, N))
-    HGIN_NT_H2(1, 4)
-  else
-    HGIN_NT_H2(2, 2)
-#undef HGIN_NT_H2
-  if (tiles_out) *tiles_out = tiles;
-  return check_launch(what);
-}
-
-int h2_planes(const float* b, int64_t ldb, int64_t N, int64_t K, void* out, hipStream_t s, const char* what) {
-  HGIN_ARG_CHECK(N > 0 && K > 0 && K % kBK == 0, "%s: K must be a positive multiple of %d", what, kBK);
-  HGIN_ARG_CHECK(b && out && ldb >= K && aligned16(out), "%s: bad operand / alignment", what);
-  int* fexp = reinterpret_cast<int*>(static_cast<char*>(out) + (size_t)N * (size_t)K * 4);
-  k_h2_planes<<<(unsigned)N, 64, 0, s>>>(b, ldb, K, static_cast<uint16_t*>(out), fexp);
-  return check_launch(what);
-}
-
 int check_a(const char* what, const float* a1, int64_t lda1, int64_t k1, const float* a2, int64_t lda2, int64_t K) {
   HGIN_ARG_CHECK(k1 >= 0 && k1 <= K, "%s: k1 out of [0, K]", what);
   HGIN_ARG_CHECK(k1 == 0 || (a1 && lda1 >= k1), "%s: bad A1", what);
@@ -1405,7 +682,7 @@ int check_a(const char* what, const float* a1, int64_t lda1, int64_t k1, const f
 // once: ~43 flop/B at K = 256, N = 128, far below the bf16 MFMA ridge), so the tile keeps the whole of N
 // per workgroup where it can and the epilogue writes 8-B bf16 quads.
 // LDS-DMA (global_load_lds_dwordx4: 64 lanes x 16 B into 1 KiB at a wave-uniform LDS address) and counted
-// vector-memory waits, shared by k_ws_bf16 and k_nt2.
+// vector-memory waits, used by k_ws_bf16.
 typedef __attribute__((address_space(3))) void lds_void_t;
 typedef __attribute__((address_space(1))) void glb_void_t;
 
@@ -2481,31 +1758,19 @@ int check_a_h(const char* what, const uint16_t* a1, int64_t lda1, int64_t k1, co
 }
 
 // ---------------------------------------------------------------------------------------------------
-// k_nt2 — the same NT GEMM (fp32 split / bf16) and the same epilogues, restructured around LDS-DMA staging
-// (cdna_hip_programming.md §5 "Async global->LDS copy", "Pipelining across barriers"): the 128-row A stage
-// and the B stage go global -> LDS with global_load_lds_dwordx4 into an NST-deep ring of LDS buffers, with a
-// counted vmcnt and ONE raw s_barrier per stage (the 2-barrier register-staged loop above sits at that
-// structure's ceiling, ~40 % of the matrix-core rate at the cfg3 shapes).
-//   * B is pre-converted once per call (k_nt_planes, hgin_nt_planes): fp32 -> the three bf16 split planes
-//     (bf16: one plane), laid out per K-stage exactly as the LDS image ([stage][plane][N][stage k], XOR-
-//     swizzled 16-B chunks), so a stage is a plain contiguous copy and no workgroup re-splits W.
-//   * A stays fp32 in LDS (128-B rows of 32 k; bf16: 64 k) and each wave splits its own fragments after the
-//     ds_read (the two N-waves of a row split it twice: 88 VALU per 48 MFMA, issued between MFMAs).
-//   * Workgroup tile 128 x BN (BN = 256 or 128, the whole of N for the GIN layers, so A streams from HBM
-//     once), 2 x 2 waves of 64 x BN/2; per k16 the MFMAs run in the order of k_gemm_nt, so the result is
-//     bit-identical to it (same products, same per-accumulator order).
-// LDS image swizzles (16-B chunks; a ds_read_b128 lane group of 16 rows / columns hits 16 distinct slots):
-//   A (128-B rows):     chunk c of row r at slot c ^ ((r >> 1) & 7)
+// Pre-split weight planes (hgin_nt_planes_*): the B operand of the split-mode NT GEMMs ([N, K], small) converted once
+// per call into the per-K-stage LDS image of the kBdma kernels — fp32: the three bf16 split planes, bf16: one plane —
+// laid out [stage][plane][N][stage k] with XOR-swizzled 16-B chunks, so a stage is a plain contiguous copy (LDS-DMA)
+// and no workgroup re-splits W.  (An LDS-DMA restructuring of the whole NT GEMM around these planes, k_nt2, was
+// measured slower and removed: DESIGN.md §3.)
 //   B fp32 planes (64-B rows of 32 k): chunk c of column n at c ^ ((n >> 2) & 3)
 //   B bf16 (128-B rows of 64 k):       chunk c of column n at c ^ ((n >> 1) & 7)
 template <typename T>
 struct Nt2 {
   static constexpr bool kF32 = sizeof(T) == 4;
   static constexpr int KS = kF32 ? 32 : 64;       // K elements per stage
-  static constexpr int KB = KS / 16;              // 16-deep MFMA k-blocks per stage
   static constexpr int NP = kF32 ? 3 : 1;         // B planes
   static constexpr int BROW = kF32 ? 64 : 128;    // bytes of one B plane row per stage
-  static constexpr int A_BYTES = 128 * 128;       // 128 rows x 128 B
 };
 
 // B planes, global layout [K / KS][NP][N][KS] (2-B elements), chunks swizzled as in the LDS image.
@@ -2538,255 +1803,6 @@ __global__ __launch_bounds__(256) void k_nt_planes(const T* __restrict__ b, int6
 #pragma unroll
   for (int p = 0; p < P::NP; ++p)
     *reinterpret_cast<uint4*>(out + (((s * P::NP + p) * N + n) * P::BROW + q * 16) / 2) = o[p];
-}
-
-// One NT GEMM on the LDS-DMA structure.  A: [M, K] as [p1 (columns < k1) | eps-scaled p2], element type T;
-// Bp: planes of B [N, K] (k_nt_planes).  Requirements (checked by nt2_eligible): K, k1 multiples of KS, A
-// rows 16-B aligned, N a multiple of BN.
-template <typename T, int EPI, int BN, int NST, typename OutT>
-__global__ __launch_bounds__(256, 1) void k_nt2(const T* __restrict__ a1, int64_t lda1, const T* __restrict__ a2,
-                                                int64_t lda2, int64_t k1, const float* __restrict__ eps2,
-                                                const uint16_t* __restrict__ Bp, int64_t M, int64_t N, int64_t K,
-                                                const float* __restrict__ bias, const float* __restrict__ prelu,
-                                                const OutT* __restrict__ accum, OutT* __restrict__ Z,
-                                                OutT* __restrict__ Y, int64_t ldc, bool vec_out, int64_t n_tiles,
-                                                bool xcd, CombEpi ce) {
-  using P = Nt2<T>;
-  constexpr int TN = BN / 64;                            // 32-col MFMA tiles per wave (wave tile 64 x BN/2)
-  constexpr int WC = BN / 2;
-  constexpr int B_BYTES = P::NP * BN * P::BROW;
-  constexpr int STAGE = P::A_BYTES + B_BYTES;
-  constexpr int A_INS = P::A_BYTES / 1024 / 4;           // glds per wave per stage
-  constexpr int BP_INS = BN * P::BROW / 1024 / 4;        // per plane
-  constexpr int G = A_INS + P::NP * BP_INS;
-  extern __shared__ __attribute__((aligned(16))) char nt2_smem[];
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wave = tid >> 6;
-  const int wm = wave >> 1;
-  const int wn = wave & 1;
-  const int li = lane & 31;
-  const int lh = lane >> 5;
-  const int64_t n_tiles_n = N / BN;
-  const int64_t q = xcd ? xcd_logical(blockIdx.x, gridDim.x) : (int64_t)blockIdx.x;
-  if (q >= n_tiles) return;
-  const int64_t m0 = (q / n_tiles_n) * 128;
-  const int64_t n0 = (q % n_tiles_n) * BN;
-  const int64_t S = K / P::KS;
-  const float sc2 = eps2 ? __fadd_rn(1.0f, eps2[0]) : 1.0f;
-
-  // per-lane A source rows of this wave's glds instructions (rows past M clamp to M - 1; their products
-  // land in rows that are never stored)
-  int64_t a_row_off1[A_INS], a_row_off2[A_INS];
-  int a_chunk[A_INS];
-#pragma unroll
-  for (int i = 0; i < A_INS; ++i) {
-    const int r = (wave * A_INS + i) * 8 + (lane >> 3);
-    int64_t gr = m0 + r;
-    gr = gr < M ? gr : M - 1;
-    a_row_off1[i] = gr * lda1;
-    a_row_off2[i] = gr * lda2;
-    a_chunk[i] = ((lane & 7) ^ ((r >> 1) & 7)) * (16 / (int)sizeof(T));
-  }
-  const uintptr_t u1 = reinterpret_cast<uintptr_t>(a1), u2 = reinterpret_cast<uintptr_t>(a2);
-  auto issue = [&](int64_t s, int buf) {
-    char* base = nt2_smem + buf * STAGE;
-    const int64_t k0 = s * P::KS;
-    const bool first = k0 < k1;
-    const T* src = reinterpret_cast<const T*>(first ? u1 : u2);
-    const int64_t kk = first ? k0 : k0 - k1;
-#pragma unroll
-    for (int i = 0; i < A_INS; ++i)
-      glds16(src + (first ? a_row_off1[i] : a_row_off2[i]) + kk + a_chunk[i], base + (wave * A_INS + i) * 1024);
-    const char* bsrc = reinterpret_cast<const char*>(Bp) + ((s * P::NP) * N + n0) * P::BROW;
-#pragma unroll
-    for (int p = 0; p < P::NP; ++p)
-#pragma unroll
-      for (int j = 0; j < BP_INS; ++j) {
-        const int off = (wave * BP_INS + j) * 1024;
-        glds16(bsrc + (int64_t)p * N * P::BROW + off + lane * 16, base + P::A_BYTES + p * BN * P::BROW + off);
-      }
-  };
-
-  f32x16 acc[2][TN];
-#pragma unroll
-  for (int x = 0; x < 2; ++x)
-#pragma unroll
-    for (int y = 0; y < TN; ++y)
-#pragma unroll
-      for (int e = 0; e < 16; ++e) acc[x][y][e] = 0.0f;
-
-#pragma unroll
-  for (int s = 0; s < NST - 1; ++s)
-    if (s < S) issue(s, s);
-
-  for (int64_t s = 0; s < S; ++s) {
-    // stage s landed for this wave's DMAs: everything issued after it may stay in flight
-    const int64_t ahead = (S - 1 < s + NST - 2 ? S - 1 : s + NST - 2) - s;
-    if constexpr (NST >= 4) {
-      if (ahead >= 2) wait_vm<2 * G>(); else if (ahead == 1) wait_vm<G>(); else wait_vm<0>();
-    } else if constexpr (NST == 3) {
-      if (ahead >= 1) wait_vm<G>(); else wait_vm<0>();
-    } else {
-      wait_vm<0>();
-    }
-    __builtin_amdgcn_s_barrier();      // every wave's stage-s DMAs landed; every wave is done with stage s-1
-    asm volatile("" ::: "memory");
-    if (s + NST - 1 < S) issue(s + NST - 1, (int)((s + NST - 1) % NST));
-    const char* base = nt2_smem + (s % NST) * STAGE;
-    const bool scale = eps2 != nullptr && s * P::KS >= k1;
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int kb = 0; kb < P::KB; ++kb) {
-      bf16x8 fa[2][P::NP], fb[TN][P::NP];
-#pragma unroll
-      for (int tm = 0; tm < 2; ++tm) {
-        const int r = wm * 64 + tm * 32 + li;
-        const char* row = base + r * 128;
-        const int sw = (r >> 1) & 7;
-        if constexpr (P::kF32) {
-          const int c0 = kb * 4 + lh * 2;
-          float4 v0 = *reinterpret_cast<const float4*>(row + ((c0 ^ sw) << 4));
-          float4 v1 = *reinterpret_cast<const float4*>(row + (((c0 + 1) ^ sw) << 4));
-          if (scale) {
-            v0 = make_float4(__fmul_rn(sc2, v0.x), __fmul_rn(sc2, v0.y), __fmul_rn(sc2, v0.z), __fmul_rn(sc2, v0.w));
-            v1 = make_float4(__fmul_rn(sc2, v1.x), __fmul_rn(sc2, v1.y), __fmul_rn(sc2, v1.z), __fmul_rn(sc2, v1.w));
-          }
-          uint2 o0[3], o1[3];
-          split4(v0, o0);
-          split4(v1, o1);
-#pragma unroll
-          for (int p = 0; p < 3; ++p) {
-            const uint4 u = make_uint4(o0[p].x, o0[p].y, o1[p].x, o1[p].y);
-            fa[tm][p] = __builtin_bit_cast(bf16x8, u);
-          }
-        } else {
-          const int c = kb * 2 + lh;
-          uint4 u = *reinterpret_cast<const uint4*>(row + ((c ^ sw) << 4));
-          if (scale) u = make_uint4(scale_bf2(u.x, sc2), scale_bf2(u.y, sc2), scale_bf2(u.z, sc2), scale_bf2(u.w, sc2));
-          fa[tm][0] = __builtin_bit_cast(bf16x8, u);
-        }
-      }
-#pragma unroll
-      for (int tn = 0; tn < TN; ++tn) {
-        const int n = wn * WC + tn * 32 + li;
-        const int c = kb * 2 + lh;
-        const int slot = P::kF32 ? (c ^ ((n >> 2) & 3)) : (c ^ ((n >> 1) & 7));
-#pragma unroll
-        for (int p = 0; p < P::NP; ++p)
-          fb[tn][p] = *reinterpret_cast<const bf16x8*>(base + P::A_BYTES + p * BN * P::BROW + n * P::BROW + (slot << 4));
-      }
-#pragma unroll
-      for (int tm = 0; tm < 2; ++tm)
-#pragma unroll
-        for (int tn = 0; tn < TN; ++tn) {
-          if constexpr (P::kF32) {   // k_gemm_nt's order: smallest terms first
-            acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[tm][2], fb[tn][0], acc[tm][tn], 0, 0, 0);
-            acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[tm][1], fb[tn][1], acc[tm][tn], 0, 0, 0);
-            acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[tm][0], fb[tn][2], acc[tm][tn], 0, 0, 0);
-            acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[tm][1], fb[tn][0], acc[tm][tn], 0, 0, 0);
-            acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[tm][0], fb[tn][1], acc[tm][tn], 0, 0, 0);
-            acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[tm][0], fb[tn][0], acc[tm][tn], 0, 0, 0);
-          } else {
-            acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[tm][0], fb[tn][0], acc[tm][tn], 0, 0, 0);
-          }
-        }
-    }
-    __builtin_amdgcn_s_setprio(0);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // this wave's reads of the buffer are done
-  }
-
-  float ep = 0.0f;
-  float* smem = reinterpret_cast<float*>(nt2_smem);
-  epilogue<EPI, TN, OutT>(acc, smem, wave, wm, wn, lane, li, lh, m0, n0, M, N, bias, prelu, accum, Z, Y, ldc,
-                          vec_out, ce, &ep);
-  if constexpr (EPI == 4) tile_partial(smem, ep, ce.part, q);
-}
-
-template <typename T, int BN, int NST>
-constexpr size_t nt2_lds_bytes() {
-  using P = Nt2<T>;
-  constexpr size_t stage = P::A_BYTES + (size_t)P::NP * BN * P::BROW;
-  constexpr size_t ring = stage * NST;
-  constexpr size_t epi = 4 * 32 * (BN / 2 + 4) * 4;
-  return ring > epi ? ring : epi;
-}
-
-// Tile / ring-depth variants of k_nt2 (HGIN_NT2_TILE: 0 = BN 256 with the default depth (fp32 2, bf16 3 stages);
-// 1 = BN 128, deeper ring (fp32 3, bf16 4 stages): more A bytes in flight per CU, A read by two tiles).
-int nt2_tile() {
-  static const int v = [] {
-    const char* e = getenv("HGIN_NT2_TILE");
-    return e ? atoi(e) : 0;
-  }();
-  return v;
-}
-
-// Measured (profiles/r02/nt2_not_adopted_*.txt, cfg3 / cfg5 shapes): bit-identical, but 5-16 % slower than
-// k_gemm_nt in fp32 and 1.5-1.7x slower in bf16 — at one 128 x 256 workgroup per CU the three B planes fill
-// the LDS ring and only one 16-KB A stage is in flight per CU, against three register-prefetched tiles in
-// k_gemm_nt.  So it is off by default; HGIN_NT2=1 selects it where planes are passed.
-bool nt2_enabled() {
-  static const bool on = [] {
-    const char* v = getenv("HGIN_NT2");
-    return v && v[0] == '1';
-  }();
-  return on;
-}
-
-template <typename T>
-int nt2_bn(int64_t N) {
-  return N % 256 == 0 ? 256 : (N % 128 == 0 ? 128 : 0);
-}
-
-template <typename T>
-bool nt2_eligible(const T* a1, int64_t lda1, int64_t k1, const T* a2, int64_t lda2, const void* planes, int64_t N,
-                  int64_t K, bool split_mode) {
-  using P = Nt2<T>;
-  constexpr int EPR = 16 / (int)sizeof(T);   // elements per 16 B
-  if (!planes || !nt2_enabled()) return false;
-  if (P::kF32 && (!split_mode || gemm_h2_enabled())) return false;   // mfma32 / h2 modes keep their own kernels
-  if (K % P::KS || k1 % P::KS || nt2_bn<T>(N) == 0) return false;
-  if (k1 > 0 && (!aligned16(a1) || lda1 % EPR)) return false;
-  if (k1 < K && (!aligned16(a2) || lda2 % EPR)) return false;
-  return true;
-}
-
-template <typename T, int EPI, typename OutT>
-int launch_nt2(const T* a1, int64_t lda1, int64_t k1, const T* a2, int64_t lda2, const float* eps2,
-               const void* planes, int64_t M, int64_t N, int64_t K, const float* bias, const float* prelu,
-               const OutT* accum, OutT* z, OutT* y, int64_t ldc, hipStream_t s, const char* what,
-               const CombEpi& ce = CombEpi{}, int64_t* tiles_out = nullptr) {
-  const bool vec_out = ldc % 4 == 0 && aligned16(y) && (z == nullptr || aligned16(z)) &&
-                       (accum == nullptr || aligned16(accum)) &&
-                       (EPI != 4 || (aligned16(ce.xd) && ce.ldxd % 4 == 0 &&
-                                     (ce.gd == nullptr || (aligned16(ce.gd) && ce.ldgd % 4 == 0))));
-  const bool xcd = xcd_remap_enabled();
-  const uint16_t* bp = static_cast<const uint16_t*>(planes);
-#define HGIN_NT2_LAUNCH(BNV, NSTV)                                                                             \
-  {                                                                                                            \
-    constexpr size_t lds = nt2_lds_bytes<T, BNV, NSTV>();                                                      \
-    auto kern = k_nt2<T, EPI, BNV, NSTV, OutT>;                                                                \
-    static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),                    \
-                                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds); \
-    if (attr != hipSuccess) {                                                                                  \
-      set_error("%s: hipFuncSetAttribute failed: %s", what, hipGetErrorString(attr));                         \
-      return (int)attr;                                                                                        \
-    }                                                                                                          \
-    const int64_t tiles = ceil_div(M, 128) * (N / BNV);                                                        \
-    dim3 grid((unsigned)(xcd ? round_up8(tiles) : tiles));                                                     \
-    HGIN_TRACE("k_nt2<EPI%d,BN%d>", EPI, BNV);                                                                 \
-    kern<<<grid, 256, lds, s>>>(a1, lda1, a2, lda2, k1, eps2, bp, M, N, K, bias, prelu, accum, z, y, ldc,      \
-                                vec_out, tiles, xcd, ce);                                                      \
-    if (tiles_out) *tiles_out = tiles;                                                                         \
-  }
-  constexpr bool F32 = Nt2<T>::kF32;
-  if (N % 256 == 0 && nt2_tile() == 0)
-    HGIN_NT2_LAUNCH(256, (F32 ? 2 : 3))
-  else
-    HGIN_NT2_LAUNCH(128, (F32 ? 3 : 4))
-#undef HGIN_NT2_LAUNCH
-  return check_launch(what);
 }
 
 template <typename T>
@@ -2863,19 +1879,12 @@ int gemm_nt_combine(const char* what, const T* a, int64_t lda, const T* b, int64
   ce.ldgp = ld_gp;
   int64_t tiles = 0;
   int rc;
-  if (nt2_eligible<T>(a, lda, K, nullptr, 0, b_planes, N, K, gemm_split_enabled()))
-    rc = launch_nt2<T, 4, T>(a, lda, K, nullptr, 0, nullptr, b_planes, M, N, K, nullptr, nullptr, nullptr, nullptr, c,
-                             ldc, s, what, ce, &tiles);
-  else if constexpr (sizeof(T) == 2)
+  if constexpr (sizeof(T) == 2)
     rc = launch_nt_bf16<4, uint16_t>(Src2h{a, lda, nullptr, 0, K}, Src2h{b, ldb, nullptr, 0, K}, M, N, K, nullptr,
                                      nullptr, nullptr, nullptr, c, ldc, s, what, ce, &tiles);
   else if constexpr (sizeof(T) == 4) {
     ce.nt_io = gemm_nt_io(M, N, 4);
-    rc = h2_eligible(a, lda, K, nullptr, 0, b_planes, K)
-             ? launch_nt_h2<4>(Src2{a, lda, nullptr, 0, K}, b_planes, M, N, K, nullptr, nullptr, nullptr, nullptr, c,
-                               ldc, s, what, ce, &tiles)
-             : -1;
-    if (rc < 0) rc = try_ws_f32_comb(a, lda, b, ldb, c, ldc, M, N, K, ce, s, what, &tiles);
+    rc = try_ws_f32_comb(a, lda, b, ldb, c, ldc, M, N, K, ce, s, what, &tiles);
     if (rc < 0)
       rc = launch_nt<4>(Src2{a, lda, nullptr, 0, K}, Src2{b, ldb, nullptr, 0, K}, M, N, K, nullptr, nullptr, nullptr,
                         nullptr, c, ldc, s, what, ce, &tiles, b_planes);
@@ -2931,9 +1940,6 @@ extern "C" int hgin_gin_mlp_fwd_bf16(const uint16_t* a1, int64_t lda1, int64_t k
   if (M == 0 || N == 0) return HGIN_OK;
   HGIN_ARG_CHECK(w && bias && prelu && y, "hgin_gin_mlp_fwd_bf16: NULL operand");
   if (int rc = check_a_h("hgin_gin_mlp_fwd_bf16", a1, lda1, k1, a2, lda2, K)) return rc;
-  if (nt2_eligible<uint16_t>(a1, lda1, k1, a2, lda2, w_planes, N, K, true))
-    return launch_nt2<uint16_t, 1, uint16_t>(a1, lda1, k1, a2, lda2, a2_eps, w_planes, M, N, K, bias, prelu, accum, z, y,
-                                             N, as_stream(stream), "hgin_gin_mlp_fwd_bf16");
   return launch_nt_bf16<1, uint16_t>(Src2h{a1, lda1, a2, lda2, k1, a2_eps}, Src2h{w, K, nullptr, 0, K}, M, N, K, bias, prelu,
                                      accum, z, y, N, as_stream(stream), "hgin_gin_mlp_fwd_bf16");
 }
@@ -2946,9 +1952,6 @@ extern "C" int hgin_linear_fwd_bf16(const uint16_t* a1, int64_t lda1, int64_t k1
   if (M == 0 || N == 0) return HGIN_OK;
   HGIN_ARG_CHECK(w && bias && y, "hgin_linear_fwd_bf16: NULL operand");
   if (int rc = check_a_h("hgin_linear_fwd_bf16", a1, lda1, k1, a2, lda2, K)) return rc;
-  if (nt2_eligible<uint16_t>(a1, lda1, k1, a2, lda2, w_planes, N, K, true))
-    return launch_nt2<uint16_t, 2, float>(a1, lda1, k1, a2, lda2, nullptr, w_planes, M, N, K, bias, nullptr, nullptr,
-                                          nullptr, y, N, as_stream(stream), "hgin_linear_fwd_bf16");
   return launch_nt_bf16<2, float>(Src2h{a1, lda1, a2, lda2, k1}, Src2h{w, K, nullptr, 0, K}, M, N, K, bias, nullptr,
                                   nullptr, nullptr, y, N, as_stream(stream), "hgin_linear_fwd_bf16");
 }
@@ -2960,9 +1963,6 @@ extern "C" int hgin_gemm_nt_bf16(const uint16_t* a, int64_t lda, const uint16_t*
   if (M == 0 || N == 0) return HGIN_OK;
   HGIN_ARG_CHECK(a && b && c, "hgin_gemm_nt_bf16: NULL operand");
   HGIN_ARG_CHECK(lda >= K && ldb >= K && ldc >= N, "hgin_gemm_nt_bf16: leading dimension too small");
-  if (nt2_eligible<uint16_t>(a, lda, K, nullptr, 0, b_planes, N, K, true))
-    return launch_nt2<uint16_t, 0, uint16_t>(a, lda, K, nullptr, 0, nullptr, b_planes, M, N, K, nullptr, nullptr,
-                                             nullptr, nullptr, c, ldc, as_stream(stream), "hgin_gemm_nt_bf16");
   return launch_nt_bf16<0, uint16_t>(Src2h{a, lda, nullptr, 0, K}, Src2h{b, ldb, nullptr, 0, K}, M, N, K, nullptr,
                                      nullptr, nullptr, nullptr, c, ldc, as_stream(stream), "hgin_gemm_nt_bf16");
 }
@@ -2976,12 +1976,6 @@ extern "C" int hgin_gin_mlp_fwd_f32(const float* a1, int64_t lda1, int64_t k1, c
   if (M == 0 || N == 0) return HGIN_OK;
   HGIN_ARG_CHECK(w && bias && prelu && y, "hgin_gin_mlp_fwd_f32: NULL operand");
   if (int rc = check_a("hgin_gin_mlp_fwd_f32", a1, lda1, k1, a2, lda2, K)) return rc;
-  if (nt2_eligible<float>(a1, lda1, k1, a2, lda2, w_planes, N, K, gemm_split_enabled()))
-    return launch_nt2<float, 1, float>(a1, lda1, k1, a2, lda2, a2_eps, w_planes, M, N, K, bias, prelu, accum, z, y, N,
-                                       as_stream(stream), "hgin_gin_mlp_fwd_f32");
-  if (h2_eligible(a1, lda1, k1, a2, lda2, w_planes, K))
-    return launch_nt_h2<1>(Src2{a1, lda1, a2, lda2, k1, a2_eps}, w_planes, M, N, K, bias, prelu, accum, z, y, N,
-                           as_stream(stream), "hgin_gin_mlp_fwd_f32");
   {
     const int rc = try_ws_f32(a1, lda1, k1, a2_eps, w, bias, prelu, accum, z, y, M, N, K, as_stream(stream),
                               "hgin_gin_mlp_fwd_f32");
@@ -2999,12 +1993,6 @@ extern "C" int hgin_linear_fwd_f32(const float* a1, int64_t lda1, int64_t k1, co
   if (M == 0 || N == 0) return HGIN_OK;
   HGIN_ARG_CHECK(w && bias && y, "hgin_linear_fwd_f32: NULL operand");
   if (int rc = check_a("hgin_linear_fwd_f32", a1, lda1, k1, a2, lda2, K)) return rc;
-  if (nt2_eligible<float>(a1, lda1, k1, a2, lda2, w_planes, N, K, gemm_split_enabled()))
-    return launch_nt2<float, 2, float>(a1, lda1, k1, a2, lda2, nullptr, w_planes, M, N, K, bias, nullptr, nullptr,
-                                       nullptr, y, N, as_stream(stream), "hgin_linear_fwd_f32");
-  if (h2_eligible(a1, lda1, k1, a2, lda2, w_planes, K))
-    return launch_nt_h2<2>(Src2{a1, lda1, a2, lda2, k1}, w_planes, M, N, K, bias, nullptr, nullptr, nullptr, y, N,
-                           as_stream(stream), "hgin_linear_fwd_f32");
   return launch_nt<2>(Src2{a1, lda1, a2, lda2, k1}, Src2{w, K, nullptr, 0, K}, M, N, K, bias, nullptr, nullptr,
                       nullptr, y, N, as_stream(stream), "hgin_linear_fwd_f32", CombEpi{}, nullptr, w_planes);
 }
@@ -3016,25 +2004,17 @@ extern "C" int hgin_gemm_nt_f32(const float* a, int64_t lda, const float* b, int
   if (M == 0 || N == 0) return HGIN_OK;
   HGIN_ARG_CHECK(a && b && c, "hgin_gemm_nt_f32: NULL operand");
   HGIN_ARG_CHECK(lda >= K && ldb >= K && ldc >= N, "hgin_gemm_nt_f32: leading dimension too small");
-  if (nt2_eligible<float>(a, lda, K, nullptr, 0, b_planes, N, K, gemm_split_enabled()))
-    return launch_nt2<float, 0, float>(a, lda, K, nullptr, 0, nullptr, b_planes, M, N, K, nullptr, nullptr, nullptr,
-                                       nullptr, c, ldc, as_stream(stream), "hgin_gemm_nt_f32");
-  if (h2_eligible(a, lda, K, nullptr, 0, b_planes, K))
-    return launch_nt_h2<0>(Src2{a, lda, nullptr, 0, K}, b_planes, M, N, K, nullptr, nullptr, nullptr, nullptr, c, ldc,
-                           as_stream(stream), "hgin_gemm_nt_f32");
   return launch_nt<0>(Src2{a, lda, nullptr, 0, K}, Src2{b, ldb, nullptr, 0, K}, M, N, K, nullptr, nullptr, nullptr,
                       nullptr, c, ldc, as_stream(stream), "hgin_gemm_nt_f32", CombEpi{}, nullptr, b_planes);
 }
 
 extern "C" int hgin_nt_planes_size(int64_t N, int64_t K, int elem_bytes, size_t* bytes) {
   HGIN_ARG_CHECK(bytes && N >= 0 && K >= 0 && (elem_bytes == 4 || elem_bytes == 2), "hgin_nt_planes_size: bad args");
-  *bytes = elem_bytes == 4 ? (gemm_h2_enabled() ? h2_planes_bytes(N, K) : nt_planes_bytes<float>(N, K))
-                           : nt_planes_bytes<uint16_t>(N, K);
+  *bytes = elem_bytes == 4 ? nt_planes_bytes<float>(N, K) : nt_planes_bytes<uint16_t>(N, K);
   return HGIN_OK;
 }
 
 extern "C" int hgin_nt_planes_f32(const float* b, int64_t ldb, int64_t N, int64_t K, void* out, void* stream) {
-  if (gemm_h2_enabled()) return h2_planes(b, ldb, N, K, out, as_stream(stream), "hgin_nt_planes_f32");
   return nt_planes<float>(b, ldb, N, K, out, as_stream(stream), "hgin_nt_planes_f32");
 }
 

@@ -110,15 +110,11 @@ using bf16x8 = __attribute__((ext_vector_type(8))) __bf16;
 // kSplit: fp32 operands on the bf16 matrix cores (hgin_common.h split4): the transposed column runs of 4 m
 // are written as three bf16 planes ([col][3 x 32 m + pad] rows of kSplitRowWords words) and a lane reads
 // 8 consecutive m of a plane (one 16-deep k-block) per ds_read_b128.
-// kPro: A = g_y and the PReLU-backward prologue above (TnPro).  kNoSums (the workgroups of the K tiles after the
-// first): g_z is formed but the bias / slope sums, which only the first K tile's workgroups keep, are not — 3 of the
-// 6 VALU ops per A element, skipped by 3 of 4 workgroups at K = 512.  The kernel (k_gemm_tn_partial, kDual) picks
-// one of two inlined bodies per workgroup; a branch on the K tile inside the prologue instead made it spill, and two
-// launches (first K tile, then the rest) left most CUs idle in each.  kGz: the first K tile's workgroups also store the
+// kPro: A = g_y and the PReLU-backward prologue above (TnPro).  kGz: the first K tile's workgroups also store the
 // g_z they form (TnPro::gz; its own instantiation: the store code in the others made the kLateZ kernel spill, 38
 // scratch ops, fused dW 6.6 -> 8.7 ms per cfg3 layer-0 launch).  kLateZ: z is loaded when the stage is
 // written to LDS instead of with the register prefetch (16 fewer VGPRs live across the MFMA cluster).
-template <bool kClean, int TNR, bool kSplit, bool kPro, bool kLateZ, bool kGz, bool kNoSums>
+template <bool kClean, int TNR, bool kSplit, bool kPro, bool kLateZ, bool kGz>
 __device__ __forceinline__ void tn_partial_body(const float* __restrict__ A, int64_t lda, const float* __restrict__ B1,
                                                 int64_t ldb1, const float* __restrict__ B2, int64_t ldb2, int64_t K1,
                                                 int64_t M, int64_t N, int64_t K, int64_t rows_per_split, bool vec,
@@ -265,30 +261,19 @@ __device__ __forceinline__ void tn_partial_body(const float* __restrict__ A, int
   const float slope = kPro ? pro.slope[0] : 0.0f;
   auto prologue = [&]() {
     if (!stage_a) return;
-    if constexpr (!kNoSums) {
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {   // branch-free (a data-dependent branch per element splits the block and
-                                      // the scheduler then keeps every loaded value alive: heavy spilling)
-        float g[4] = {va[j].x, va[j].y, va[j].z, va[j].w};
-        const float zz[4] = {vz[j].x, vz[j].y, vz[j].z, vz[j].w};
+    for (int j = 0; j < 4; ++j) {   // branch-free (a data-dependent branch per element splits the block and
+                                    // the scheduler then keeps every loaded value alive: heavy spilling)
+      float g[4] = {va[j].x, va[j].y, va[j].z, va[j].w};
+      const float zz[4] = {vz[j].x, vz[j].y, vz[j].z, vz[j].w};
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const bool pos = zz[q] > 0.0f;
-          ssc[q] = __fadd_rn(ssc[q], pos ? 0.0f : __fmul_rn(zz[q], g[q]));
-          g[q] = pos ? g[q] : __fmul_rn(slope, g[q]);
-          csum[q] = __fadd_rn(csum[q], g[q]);
-        }
-        va[j] = make_float4(g[0], g[1], g[2], g[3]);
+      for (int q = 0; q < 4; ++q) {
+        const bool pos = zz[q] > 0.0f;
+        ssc[q] = __fadd_rn(ssc[q], pos ? 0.0f : __fmul_rn(zz[q], g[q]));
+        g[q] = pos ? g[q] : __fmul_rn(slope, g[q]);
+        csum[q] = __fadd_rn(csum[q], g[q]);
       }
-    } else {
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        float g[4] = {va[j].x, va[j].y, va[j].z, va[j].w};
-        const float zz[4] = {vz[j].x, vz[j].y, vz[j].z, vz[j].w};
-#pragma unroll
-        for (int q = 0; q < 4; ++q) g[q] = zz[q] > 0.0f ? g[q] : __fmul_rn(slope, g[q]);
-        va[j] = make_float4(g[0], g[1], g[2], g[3]);
-      }
+      va[j] = make_float4(g[0], g[1], g[2], g[3]);
     }
   };
   // the 4 x 4 block regrouped: column c4 + t gets (row r4 .. r4 + 3) as one float4
@@ -410,7 +395,7 @@ __device__ __forceinline__ void tn_partial_body(const float* __restrict__ A, int
       __syncthreads();
     }
   }
-  if constexpr (kPro && !kNoSums) {
+  if constexpr (kPro) {
     if (work.k0 == 0)   // workgroup-uniform
       pro_partials<4>(pro, smem, TNR, r4a >> 2, c4a, stage_a, csum, ssc, n0, N, work.split);
   }
@@ -429,7 +414,7 @@ __device__ __forceinline__ void tn_partial_body(const float* __restrict__ A, int
     }
 }
 
-template <bool kClean, int TNR, bool kSplit, bool kPro, bool kLateZ = false, bool kGz = false, bool kDual = false>
+template <bool kClean, int TNR, bool kSplit, bool kPro, bool kLateZ = false, bool kGz = false>
 __global__ __launch_bounds__(256, (kPro && !kLateZ) ? 2 : 3) void k_gemm_tn_partial(const float* __restrict__ A, int64_t lda,
                                                             const float* __restrict__ B1, int64_t ldb1,
                                                             const float* __restrict__ B2, int64_t ldb2, int64_t K1,
@@ -440,12 +425,8 @@ __global__ __launch_bounds__(256, (kPro && !kLateZ) ? 2 : 3) void k_gemm_tn_part
   __shared__ __attribute__((aligned(16))) float smem[(TNR + 128) * kRowW];
   const TnWork work = tn_work(grid);
   if (!work.valid) return;
-  if (kDual && work.k0 != 0)   // workgroup-uniform
-    tn_partial_body<kClean, TNR, kSplit, kPro, kLateZ, kGz, true>(A, lda, B1, ldb1, B2, ldb2, K1, M, N, K,
-                                                                   rows_per_split, vec, slab, pro, smem, work);
-  else
-    tn_partial_body<kClean, TNR, kSplit, kPro, kLateZ, kGz, false>(A, lda, B1, ldb1, B2, ldb2, K1, M, N, K,
-                                                                    rows_per_split, vec, slab, pro, smem, work);
+  tn_partial_body<kClean, TNR, kSplit, kPro, kLateZ, kGz>(A, lda, B1, ldb1, B2, ldb2, K1, M, N, K, rows_per_split, vec,
+                                                          slab, pro, smem, work);
 }
 
 // Small weight gradients (N or K < 16, e.g. the readout head Linear(32, 1)): no MFMA tile to fill, so a
@@ -593,155 +574,10 @@ bool slab_fused_enabled() {
 }
 
 // ---------------------------------------------------------------------------------------------------
-// bf16 operands (cfg5): out[N, K] (fp32) = A^T [B1 | B2] on v_mfma_f32_32x32x16_bf16.  A bf16 fragment
-// holds 8 consecutive k (= 8 consecutive rows m here) of one column, but both operands are stored
-// m-major, so each stage is transposed on its way into LDS: a thread loads an 8 x 8 block (8 rows m x
-// 16 B of columns; a wave-load covers 8 rows x 128-B segments), transposes it in registers (16-bit
-// lane shuffles of 32 words) and writes 8 column-runs of 8 m as 16-B stores into [col][m] images with
-// 144-B rows, from which every fragment is one conflict-free ds_read_b128 as in the NT kernel.  Waves 0-1
-// stage A, waves 2-3 stage B.  64 rows of M per stage, register prefetch of the next stage.
+// bf16 operands (cfg5): 64 rows of M per stage.  (A register-transposing bf16 dW kernel, measured 1.9x slower than
+// the transposed-read kernel below, was removed: DESIGN.md §3.)
 constexpr int kTnBMh = 64;
-constexpr int kTnLdH = kTnBMh + 8;
 
-template <bool kVec>
-__global__ __launch_bounds__(256, 2) void k_gemm_tn_bf16_partial(const uint16_t* __restrict__ A, int64_t lda,
-                                                                 const uint16_t* __restrict__ B1, int64_t ldb1,
-                                                                 const uint16_t* __restrict__ B2, int64_t ldb2,
-                                                                 int64_t K1, int64_t M, int64_t N, int64_t K,
-                                                                 int64_t rows_per_split, float* __restrict__ slab,
-                                                                 TnGrid grid) {
-  __shared__ __attribute__((aligned(16))) uint16_t smem[2 * 128 * kTnLdH];
-  uint16_t* At = smem;
-  uint16_t* Bt = smem + 128 * kTnLdH;
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wave = tid >> 6;
-  const int wm = wave >> 1, wn = wave & 1;
-  const int li = lane & 31, lh = lane >> 5;
-  const TnWork work = tn_work(grid);
-  if (!work.valid) return;
-  const int64_t n0 = work.n0;
-  const int64_t k0 = work.k0;
-  const int64_t mb = work.split * rows_per_split;
-  const int64_t me = mb + rows_per_split < M ? mb + rows_per_split : M;
-  const bool isB = tid >= 128;
-  // row blocks vary fastest across lanes: a ds_write_b128 lane group (8 lanes) then writes one column run
-  // of 8 x 16 B (conflict-free); with the column chunks fastest its 8 lanes hit rows 8 apart = 288 words,
-  // one bank group: 8-way conflicts (SQ_LDS_BANK_CONFLICT 6.5x the LDS-active cycles)
-  const int rb = tid & 7;           // 8-row block of the 64-row stage
-  const int cq = (tid & 127) >> 3;  // 8-column chunk of the 128-wide tile
-  uint16_t* T = isB ? Bt : At;
-
-  f32x16 acc[2][2];
-#pragma unroll
-  for (int a = 0; a < 2; ++a)
-#pragma unroll
-    for (int b = 0; b < 2; ++b)
-#pragma unroll
-      for (int e = 0; e < 16; ++e) acc[a][b][e] = 0.0f;
-
-  uint32_t v[8][4];
-  // vector path: k1 % 8 == 0, so a thread's 8-column chunk lies wholly in A, B1 or B2 — one base pointer
-  // and row stride per thread for the whole kernel
-  const int64_t c0 = (isB ? k0 : n0) + 8 * cq;
-  const int64_t lim = isB ? K : N;
-  const uint16_t* vbase = !isB ? A + c0 : (c0 < K1 ? B1 + c0 : B2 + (c0 - K1));
-  const int64_t vld = !isB ? lda : (c0 < K1 ? ldb1 : ldb2);
-  const bool vok = c0 + 7 < lim;
-  auto load_stage = [&](int64_t m0) {
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int64_t gm = m0 + 8 * rb + i;
-      v[i][0] = v[i][1] = v[i][2] = v[i][3] = 0u;
-      if (gm >= me) continue;
-      if (kVec) {
-        if (vok) {
-          const uint4 x = *reinterpret_cast<const uint4*>(vbase + gm * vld);
-          v[i][0] = x.x; v[i][1] = x.y; v[i][2] = x.z; v[i][3] = x.w;
-        } else {
-#pragma unroll
-          for (int w = 0; w < 4; ++w) {
-            const uint32_t lo = c0 + 2 * w < lim ? vbase[gm * vld + 2 * w] : 0u;
-            const uint32_t hi = c0 + 2 * w + 1 < lim ? vbase[gm * vld + 2 * w + 1] : 0u;
-            v[i][w] = lo | (hi << 16);
-          }
-        }
-      } else {
-        uint32_t t[8];
-#pragma unroll
-        for (int c = 0; c < 8; ++c) {
-          const int64_t k = c0 + c;
-          t[c] = 0u;
-          if (k < lim) t[c] = !isB ? A[gm * lda + k] : (k < K1 ? B1[gm * ldb1 + k] : B2[gm * ldb2 + (k - K1)]);
-        }
-#pragma unroll
-        for (int w = 0; w < 4; ++w) v[i][w] = t[2 * w] | (t[2 * w + 1] << 16);
-      }
-    }
-  };
-  auto store_stage = [&]() {
-#pragma unroll
-    for (int c = 0; c < 8; ++c) {
-      uint32_t w[4];
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const uint32_t a = v[2 * e][c >> 1], b = v[2 * e + 1][c >> 1];
-        w[e] = (c & 1) ? ((a >> 16) | (b & 0xffff0000u)) : ((a & 0xffffu) | (b << 16));
-      }
-      *reinterpret_cast<uint4*>(T + (8 * cq + c) * kTnLdH + 8 * rb) = make_uint4(w[0], w[1], w[2], w[3]);
-    }
-  };
-  load_stage(mb);
-  store_stage();
-  __syncthreads();
-  for (int64_t m0 = mb; m0 < me; m0 += kTnBMh) {
-    const bool more = m0 + kTnBMh < me;
-    if (more) load_stage(m0 + kTnBMh);
-    __builtin_amdgcn_s_setprio(1);   // keep the MFMA cluster together (T5)
-#pragma unroll
-    for (int st = 0; st < kTnBMh / 16; ++st) {
-      bf16x8 fa[2], fb[2];
-#pragma unroll
-      for (int t = 0; t < 2; ++t) {
-        fa[t] = *reinterpret_cast<const bf16x8*>(At + (wm * 64 + t * 32 + li) * kTnLdH + st * 16 + lh * 8);
-        fb[t] = *reinterpret_cast<const bf16x8*>(Bt + (wn * 64 + t * 32 + li) * kTnLdH + st * 16 + lh * 8);
-      }
-#pragma unroll
-      for (int tm = 0; tm < 2; ++tm)
-#pragma unroll
-        for (int tn = 0; tn < 2; ++tn)
-          acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[tm], fb[tn], acc[tm][tn], 0, 0, 0);
-    }
-    __builtin_amdgcn_s_setprio(0);
-    if (more) {
-      __syncthreads();
-      store_stage();
-      __syncthreads();
-    }
-  }
-  float* out = slab + work.split * N * K;
-#pragma unroll
-  for (int tm = 0; tm < 2; ++tm)
-#pragma unroll
-    for (int tn = 0; tn < 2; ++tn) {
-      const int64_t k = k0 + wn * 64 + tn * 32 + li;
-      if (k >= K) continue;
-#pragma unroll
-      for (int e = 0; e < 16; ++e) {
-        const int64_t n = n0 + wm * 64 + tm * 32 + (e & 3) + 8 * (e >> 2) + 4 * lh;
-        if (n < N) out[n * K + k] = acc[tm][tn][e];
-      }
-    }
-}
-
-
-// bf16 TN with hardware-transposed fragment reads (gfx950 ds_read_b64_tr_b16): the 64-row stages of A [m][n]
-// and B [m][k] go to LDS exactly as loaded (16-B chunks, m-major rows of 128 bf16 = 256 B, no register
-// transpose), and each MFMA fragment — 8 consecutive m of one column — is gathered by two transposed reads
-// (4 rows x 16 columns per 16-lane group each).  Image layout (b) of cdna_hip_programming.md T10: chunk ch of
-// row r at 256 r + 16 (ch ^ (((r & 3) << 2) | ((r >> 2) & 3))): the 16-B stores and both transposed reads
-// are bank-conflict-free (checked by enumeration).  Waves 0-1 stage A, waves 2-3 B; register prefetch of the
-// next stage under the MFMAs; 2 x 2 waves of 64 x 64 outputs.
 using bf16x4 = __attribute__((ext_vector_type(4))) __bf16;
 typedef bf16x4 __attribute__((address_space(3))) lds_bf16x4;
 
@@ -1592,15 +1428,6 @@ int64_t try_wsd(const T* a, int64_t lda, const T* b1, int64_t ldb1, int64_t k1, 
 
 bool tn_is_small(int64_t N, int64_t K) { return N < 16 || K < 16; }
 
-// bf16 dW kernel: transposed LDS reads (default) or the register-transposing kernel (HGIN_TN_BF16=regt).
-bool tn_bf16_tr() {
-  static const bool v = [] {
-    const char* e = getenv("HGIN_TN_BF16");
-    return !(e && std::string(e) == "regt");
-  }();
-  return v;
-}
-
 // Workgroups a split-M launch aims for (HGIN_TN_WGS, <= 1024 = the workspace sizing target).  768 = one
 // resident round at 3 workgroups per CU: measured (profiles/r01_gemm_variants_*.txt) 1.35x faster than 1024
 // (1.33 rounds, the last one a third full) for the bf16 kernel, 4-6 % for fp32.
@@ -1611,27 +1438,6 @@ int64_t tn_target_wgs() {
     return x >= 64 && x <= 1024 ? x : (int64_t)1024;
   }();
   return t;
-}
-
-// Fused PReLU-backward prologue: z loaded with the register prefetch (2 waves / SIMD, the extra 16-32 live
-// VGPRs) or at LDS-store time (3 waves / SIMD for fp32).  HGIN_TN_LATEZ=0/1.
-// HGIN_TN_NOSUMS=1: the fused dW's workgroups past the first K tile skip the bias / slope sums (kDual).  Measured, not
-// adopted: bit-identical but 6.87 vs 6.71 ms per cfg3 layer-0 launch (the two inlined bodies cost the kernel its
-// register headroom: 168 VGPRs and a small spill), profiles/r03/rocprofv3_summary_cfg3_s9.txt.
-bool tn_nosums_enabled() {
-  static const bool on = [] {
-    const char* v = getenv("HGIN_TN_NOSUMS");
-    return v && v[0] == '1';
-  }();
-  return on;
-}
-
-bool tn_late_z() {
-  static const bool v = [] {
-    const char* e = getenv("HGIN_TN_LATEZ");
-    return e ? atoi(e) != 0 : true;
-  }();
-  return v;
 }
 
 int64_t tn_splits(int64_t M, int64_t N, int64_t K, int64_t stage_rows = kTnBM, int64_t target = 1024) {
@@ -1737,7 +1543,6 @@ int gemm_tn_impl(const char* what, const T* a, int64_t lda, const T* b1, int64_t
                                       align_up(sizeof(float) * (size_t)(N * tn_splits(M, N, K)), 256));
     pro.S = S_eff;
   }
-  const bool late = tn_late_z();
   int64_t tile_n = 128;
   if (small) {
     HGIN_ARG_CHECK(!pro_in, "%s: no fused prologue for N or K < 16", what);
@@ -1752,17 +1557,11 @@ int gemm_tn_impl(const char* what, const T* a, int64_t lda, const T* b1, int64_t
     const TnGrid tg{128, tiles_n, tiles_n * ceil_div(K, 128), tiles_n * ceil_div(K, 128) * S_eff, xcd_remap_enabled()};
     dim3 grid((unsigned)(tg.xcd ? round_up8(tg.n_work) : tg.n_work));
     HGIN_ARG_CHECK(!pro_in, "%s: no fused prologue for bf16", what);
-    HGIN_TRACE("k_gemm_tn_bf16<%s,N%lld,K%lld>", tn_bf16_tr() ? "tr" : "regt", (long long)N, (long long)K);
-    if (tn_bf16_tr()) {
-      if (vec && N % 8 == 0 && K % 8 == 0)
-        k_gemm_tn_bf16_tr<true><<<grid, 256, 0, s>>>(a, lda, b1, ldb1, b2, ldb2, k1, M, N, K, rows, slab, tg);
-      else
-        k_gemm_tn_bf16_tr<false><<<grid, 256, 0, s>>>(a, lda, b1, ldb1, b2, ldb2, k1, M, N, K, rows, slab, tg);
-    } else if (vec) {
-      k_gemm_tn_bf16_partial<true><<<grid, 256, 0, s>>>(a, lda, b1, ldb1, b2, ldb2, k1, M, N, K, rows, slab, tg);
-    } else {
-      k_gemm_tn_bf16_partial<false><<<grid, 256, 0, s>>>(a, lda, b1, ldb1, b2, ldb2, k1, M, N, K, rows, slab, tg);
-    }
+    HGIN_TRACE("k_gemm_tn_bf16<tr,N%lld,K%lld>", (long long)N, (long long)K);
+    if (vec && N % 8 == 0 && K % 8 == 0)
+      k_gemm_tn_bf16_tr<true><<<grid, 256, 0, s>>>(a, lda, b1, ldb1, b2, ldb2, k1, M, N, K, rows, slab, tg);
+    else
+      k_gemm_tn_bf16_tr<false><<<grid, 256, 0, s>>>(a, lda, b1, ldb1, b2, ldb2, k1, M, N, K, rows, slab, tg);
   } else {
     tile_n = N <= 32 ? 32 : 128;
     const int64_t tiles_n = ceil_div(N, tile_n);
@@ -1782,16 +1581,10 @@ int gemm_tn_impl(const char* what, const T* a, int64_t lda, const T* b1, int64_t
 #define HGIN_TN_PRO(CLEAN, TNR, SPLIT)                                                \
   if (!pro_in) HGIN_TN_LAUNCH(CLEAN, TNR, SPLIT, false, false, false);                \
   else if (pro_in->gz) HGIN_TN_LAUNCH(CLEAN, TNR, SPLIT, true, false, true); /* (late z + gz spills) */ \
-  else if (late) HGIN_TN_LAUNCH(CLEAN, TNR, SPLIT, true, true, false);              \
-  else HGIN_TN_LAUNCH(CLEAN, TNR, SPLIT, true, false, false);
+  else HGIN_TN_LAUNCH(CLEAN, TNR, SPLIT, true, true, false);
 #define HGIN_TN_CLEAN(TNR, SPLIT) \
   if (clean) { HGIN_TN_PRO(true, TNR, SPLIT) } else { HGIN_TN_PRO(false, TNR, SPLIT) }
-    const int64_t kts = ceil_div(K, 128);
-    if (pro_in && !pro_in->gz && late && clean && split && tile_n == 128 && kts > 1 && tn_nosums_enabled()) {
-      // one launch; the workgroups past the first K tile run the body without the bias / slope sums
-      k_gemm_tn_partial<true, 128, true, true, true, false, true><<<grid, 256, 0, s>>>(
-          a, lda, b1, ldb1, b2, ldb2, k1, M, N, K, rows, vec, slab, tg, pro);
-    } else if (tile_n == 32) {
+    if (tile_n == 32) {
       if (split) { HGIN_TN_CLEAN(32, true) } else { HGIN_TN_CLEAN(32, false) }
     } else {
       if (split) { HGIN_TN_CLEAN(128, true) } else { HGIN_TN_CLEAN(128, false) }

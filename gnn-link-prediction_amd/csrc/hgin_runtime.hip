@@ -52,14 +52,6 @@ bool gemm_split_enabled() {
   return on;
 }
 
-bool gemm_h2_enabled() {
-  static const bool on = [] {
-    const char* v = getenv("HGIN_F32_GEMM");
-    return v && std::string(v) == "h2";
-  }();
-  return on;
-}
-
 }  // namespace hgin
 
 extern "C" int hgin_abi_version(void) { return HGIN_ABI_VERSION; }

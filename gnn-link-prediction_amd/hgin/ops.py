@@ -80,15 +80,9 @@ def _workspace(nbytes: int, device) -> Tensor:
 # wave, chunk sums added in a fixed order: deterministic, re-associated).  Uniform GIN graphs (max in-degree
 # ~40 at cfg3) never reach it, so their aggregates stay bit-exact.  HGIN_LONG_ROW=0 keeps every row sequential.
 LONG_ROW_MIN = int(os.environ.get("HGIN_LONG_ROW", "2048"))
-# The LDS-DMA NT GEMM (hgin_gemm_nt.hip k_nt2) is measured slower than the register-staged one and off by
-# default; HGIN_NT2=1 selects it (the C side reads the same switch).
-NT2 = os.environ.get("HGIN_NT2", "0") == "1"
-# HGIN_F32_GEMM=h2: fp32 NT GEMMs as two scaled fp16 terms (3 products; hgin_gemm_nt.hip k_gemm_nt_h2), whose
-# weight operand is pre-split once per call by hgin_nt_planes_f32
-H2 = os.environ.get("HGIN_F32_GEMM") == "h2"
 # fp32 split mode: the 128 x 128 NT tile copies its B stages from pre-split planes by LDS-DMA (k_gemm_nt kBdma);
 # HGIN_NT_BDMA=0 keeps the per-tile split
-BDMA = os.environ.get("HGIN_NT_BDMA", "1") != "0" and os.environ.get("HGIN_F32_GEMM", "split") not in ("mfma32", "h2")
+BDMA = os.environ.get("HGIN_NT_BDMA", "1") != "0" and os.environ.get("HGIN_F32_GEMM", "split") != "mfma32"
 LONG_CHUNK = 1024
 
 
@@ -310,20 +304,15 @@ def combine_bwd(g: Tensor, x_dst: Tensor, eps: Tensor, want_gx: bool):
 
 
 def nt_planes(b: Tensor) -> Optional[Tensor]:
-    """The B operand [N, K] of an NT GEMM pre-converted for the LDS-DMA kernel (hgin_nt_planes_*: fp32 -> its
-    three bf16 split planes, bf16 -> a swizzled copy; N * K * 6 or N * K * 2 bytes), or None where that kernel
-    does not take the shape (the register-staged kernel runs; the result is bit-identical either way).  In h2
-    mode (fp32): its scaled fp16 hi / lo planes and per-row exponents (N * K * 4 bytes + N int32).  fp32 split mode
-    (default): the same three planes feed the register-staged 128 x 128 tile's B stages by LDS-DMA (bit-identical)."""
-    h2 = H2 and b.dtype == torch.float32
-    bdma = BDMA and b.dtype == torch.float32
-    if not (NT2 or h2 or bdma):
+    """The fp32 B operand [N, K] of an NT GEMM pre-converted into its three bf16 split planes (hgin_nt_planes_f32,
+    N * K * 6 bytes), which the split-mode 128 x 128 tile copies into LDS by DMA instead of splitting B per tile
+    (bit-identical), or None where that kernel does not take the shape."""
+    if not (BDMA and b.dtype == torch.float32):
         return None
     N, K = b.shape
-    ks = 32 if b.dtype == torch.float32 else 64
-    if N == 0 or K == 0 or K % ks or b.stride(1) != 1:
+    if N == 0 or K == 0 or K % 32 or b.stride(1) != 1:
         return None
-    if not h2 and (N % 128 or b.data_ptr() % 16 or b.stride(0) % (16 // b.element_size())):
+    if N % 128 or b.data_ptr() % 16 or b.stride(0) % 4:
         return None
     nbytes = ctypes.c_size_t(0)
     _lib.check(_lib.lib().hgin_nt_planes_size(N, K, b.element_size(), ctypes.byref(nbytes)), "hgin_nt_planes_size")

@@ -4,14 +4,10 @@ fixtures (tests/variant_child.py), so the non-default paths pytest's own process
   * HGIN_F32_GEMM=mfma32    — the exact-f32 MFMA GEMM (v_mfma_f32_32x32x2_f32) instead of the 3-way bf16 split:
                               fixture tolerances (1e-5 outputs, 1e-4 gradients);
   * HGIN_SLAB_REDUCE=2pass  — the two-launch weight-gradient slab sum: bit-identical to the one-launch default;
-  * HGIN_AGG_NQ=2 / HGIN_AGG_PIPE=1 / HGIN_AGG_TAIL=0 / HGIN_AGG_NT=1 — aggregate lane-width / pipelined / tail /
-                              non-temporal-stream variants:
+  * HGIN_AGG_PIPE=1 / HGIN_AGG_TAIL=0 / HGIN_AGG_NT=1 — aggregate pipelined / tail / non-temporal-stream variants:
                               bit-identical to the default (every variant sums each row in edge order);
   * HGIN_XCD=0              — GEMM tiles in plain order instead of XCD-contiguous: bit-identical;
-  * HGIN_NT2=1              — the LDS-DMA NT GEMM (k_nt2) instead of the register-staged one: bit-identical;
   * HGIN_GEMM_NT_IO=1       — non-temporal GEMM epilogue streams at every size (default: > 512 MiB): bit-identical;
-  * HGIN_AGG_LDS=1 (+ _D)   — the fp32 F = 256 aggregate gathering neighbour rows into LDS by DMA (k_agg_lds, the
-                              w256_L3 fixture's forward ADD and backward NONE / ADD launches): bit-identical;
   * HGIN_WSD_PRO=0          — the separate PReLU-backward pass ahead of the weight-stationary dW instead of the
                               fused one: bit-identical (same g_z, same dW partition; the bias / slope sums are
                               grouped differently, so those two gradients are compared within fixture tolerance).
@@ -33,29 +29,22 @@ VARIANTS = {
     "default": {},
     "mfma32": {"HGIN_F32_GEMM": "mfma32"},
     "slab2pass": {"HGIN_SLAB_REDUCE": "2pass"},
-    "agg_nq2": {"HGIN_AGG_NQ": "2"},
     "agg_pipe": {"HGIN_AGG_PIPE": "1"},
     "agg_notail": {"HGIN_AGG_TAIL": "0"},
     "xcd_off": {"HGIN_XCD": "0"},
-    "nt2_on": {"HGIN_NT2": "1"},
     "agg_nt_all": {"HGIN_AGG_NT": "1"},
     "gemm_nt_io": {"HGIN_GEMM_NT_IO": "1"},
-    "agg_lds8": {"HGIN_AGG_LDS": "1", "HGIN_AGG_LDS_D": "8"},
-    "agg_lds16": {"HGIN_AGG_LDS": "1", "HGIN_AGG_LDS_D": "16"},
     "wsd_pro_off": {"HGIN_WSD_PRO": "0"},
     "nt_bdma_off": {"HGIN_NT_BDMA": "0"},
-    "tn_nosums_on": {"HGIN_TN_NOSUMS": "1"},
-    "f32_h2": {"HGIN_F32_GEMM": "h2"},
 }
-BITWISE_EQUAL_TO_DEFAULT = ("slab2pass", "agg_nq2", "agg_pipe", "agg_notail", "xcd_off", "nt2_on", "agg_nt_all", "gemm_nt_io",
-                            "agg_lds8", "agg_lds16", "wsd_pro_off", "nt_bdma_off", "tn_nosums_on")
+BITWISE_EQUAL_TO_DEFAULT = ("slab2pass", "agg_pipe", "agg_notail", "xcd_off", "agg_nt_all", "gemm_nt_io", "wsd_pro_off",
+                            "nt_bdma_off")
 
-# Scalar / column-sum gradients a variant regroups: the dX kernel's eps-gradient partials (one per tile in k_nt2, one
-# per workgroup in the weight-stationary k_ws_f32) and the bias / PReLU-slope sums (per workgroup in the fused
+# Scalar / column-sum gradients a variant regroups: the bias / PReLU-slope sums (per workgroup in the fused
 # weight-stationary dW, per row block in k_rows_bwd<0>).  Everything else must stay bit-identical.
 # (wsd_pro_off: every Linear bias / PReLU slope behind a fused PReLU backward — GIN MLPs and readout layers alike —
 # is summed per row block by the separate pass instead of per workgroup of the fused dW)
-REGROUPED = {"nt2_on": (".conv.eps",), "wsd_pro_off": (".0.bias", ".1.weight")}
+REGROUPED = {"wsd_pro_off": (".0.bias", ".1.weight")}
 
 _results = {}
 
