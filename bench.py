@@ -80,6 +80,10 @@ def parse():
                     help="N > 1 components split: skip rank 0's single-GPU run of all the components (scaling_vs_1gpu)")
     ap.add_argument("--adam", choices=("foreach", "fused"), default="foreach",
                     help="torch.optim.Adam implementation (train.py's optimizer, same update rule)")
+    ap.add_argument("--no-cfg5", action="store_true",
+                    help="cfg3 at N = 1: skip the bf16 twin (BASELINE configs[4]) timed after the headline as extras.cfg5")
+    ap.add_argument("--cpu-full", default=None, metavar="CFG",
+                    help="only time the CPU baseline (oracle) on the FULL named config (e.g. cfg2) and print its record")
     ap.add_argument("--graph", action="store_true",
                     help="one hipGraph replay per step (default: the step issued from Python; measured equal on cfg2 "
                          "and cfg5 — the step is GPU-bound, the host runs ahead)")
@@ -94,9 +98,21 @@ def cpu_threads() -> int:
     return max(1, n)
 
 
-def cpu_baseline(cfg) -> dict:
+def host_ram_gb() -> float:
+    try:
+        for line in open("/proc/meminfo"):
+            if line.startswith("MemTotal:"):
+                return round(int(line.split()[1]) / 2 ** 20, 1)
+    except OSError:
+        pass
+    return 0.0
+
+
+def cpu_baseline(cfg, full_graph: bool = False) -> dict:
     """The oracle (torch CPU ops == the PyG CPU path) on a bounded sample of the same workload, on this box's
-    host cores: 2 warm-up steps, then the median of 5."""
+    host cores: 2 warm-up steps, then the median of 5.  full_graph: the whole config instead of
+    the ~1M-edge sample (cfg1 and cfg2 in full; a separate ``--cpu-full`` run, not the default
+    bench line)."""
     from hgin.data import scaled_config, synthetic_graph
     from oracle.pyg_cpu import OracleHetroGIN, train_step
     threads = cpu_threads()
@@ -104,7 +120,7 @@ def cpu_baseline(cfg) -> dict:
     torch.set_num_threads(threads)
     full = cfg
     # same schema and widths, every count scaled to ~1M convolved edges (the rate is per edge)
-    if cfg.conv_edges > CPU_SAMPLE_EDGES:
+    if cfg.conv_edges > CPU_SAMPLE_EDGES and not full_graph:
         cfg = scaled_config(cfg, CPU_SAMPLE_EDGES / cfg.conv_edges, name=f"{cfg.name}-cpu-sample")
     # the reference's CPU path is fp32 only: a bf16 config is timed on its fp32 counterpart
     cfg = dataclasses.replace(cfg, feat_dtype="f32", components=1)
@@ -136,7 +152,8 @@ def cpu_baseline(cfg) -> dict:
                       f"layers, fp32), 2 warm-up + median of 5 train steps (fwd + sqrt-MAPE + bwd + Adam) of "
                       f"oracle/pyg_cpu.py (torch CPU ops = the reference's PyG CPU path), {threads} threads, "
                       f"{cpu_model}",
-            "ms_per_step": round(dt * 1e3, 2)}
+            "ms_per_step": round(dt * 1e3, 2), "host_ram_gb": host_ram_gb(),
+            "step_times_s": [round(t, 3) for t in times]}
 
 
 def zipf_dst(cfg, graph, dev, s: float = 1.1, seed: int = 7):
@@ -319,6 +336,60 @@ def extras(graph, dev) -> dict:
     return res
 
 
+def cfg5_extra(dev, adam: str, warmup: int = 2, steps: int = 5) -> dict:
+    """BASELINE configs[4] (cfg5: cfg3's graph and model with bf16 features + bf16 MFMA, fp32 accumulate) timed in the
+    same run after the cfg3 headline has been freed: warm-up, then `steps` steps bracketed by hipDeviceSynchronize
+    (wall) with HIP events per step, then an untimed probe pass for its aggregate roofline and GEMM families."""
+    from hgin import HetroGIN, profiling
+    from hgin.data import CONFIGS, synthetic_graph
+    from hgin.train import train_step
+    cfg = CONFIGS["cfg5"]
+    graph = synthetic_graph(cfg, seed=0, device=dev)
+    torch.manual_seed(1997)
+    model = HetroGIN(**cfg.model_kwargs({"link": cfg.f_link, "path": cfg.f_path, "node": cfg.f_node})).to(dev)
+    opt = torch.optim.Adam(lr=1e-3, params=model.parameters(), weight_decay=0,
+                           **({"fused": True} if adam == "fused" else {}))
+    for _ in range(warmup):
+        train_step(model, opt, graph)
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(steps + 1)]
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    ev[0].record()
+    for i in range(steps):
+        loss = train_step(model, opt, graph)
+        ev[i + 1].record()
+    torch.cuda.synchronize()
+    t_step = (time.perf_counter() - t0) / steps
+    t_med = statistics.median(ev[i].elapsed_time(ev[i + 1]) for i in range(steps)) / 1e3
+    probe = profiling.start()
+    for _ in range(2):
+        train_step(model, opt, graph)
+    profiling.stop()
+    s = probe.summary()
+    a = s.get("aggregate")
+    roofline = None
+    if a:
+        achieved = a["avg_work"] / (a["avg_ms"] / 1e3) / 1e9
+        roofline = {"bound": "hbm", "kernel": "hgin_aggregate_bf16 (k_agg_pipe: CSR forward + CSC backward)",
+                    "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": round(achieved / HBM_PEAK_GBS, 4), "bytes_per_launch": a["avg_work"],
+                    "avg_launch_ms": round(a["avg_ms"], 5), "launches_per_step": a["launches"] / 2}
+    out = {"workload": f"cfg5 (BASELINE configs[4]): cfg3's {cfg.nodes} nodes / {cfg.graph_edges} edges, hidden "
+                       f"{cfg.hidden}, {cfg.layers} layers, bf16 features + bf16 MFMA, fp32 accumulate, one GPU",
+           "steps": steps, "warmup": warmup, "ms_per_step": round(t_step * 1e3, 4),
+           "ms_per_step_median": round(t_med * 1e3, 4), "value": round(cfg.conv_edges / t_step, 1),
+           "unit": "edges/s", "dtype": "bf16", "roofline": roofline,
+           "gemm": gemm_fields(s.get("gin_mlp"), True, 2, t_step, "forward MLP GEMM (hgin_gin_mlp_fwd_bf16)"),
+           "gemm_dw": gemm_fields(s.get("gemm_dw"), True, 2, t_step, "weight-gradient GEMMs (bf16)"),
+           "gemm_dx": gemm_fields(s.get("gemm_dx"), True, 2, t_step, "input-gradient GEMMs (bf16)"),
+           "final_loss": float(loss),
+           "timing": "after the cfg3 headline's graph and model were freed; wall clock over the steps bracketed by "
+                     "hipDeviceSynchronize, per-step HIP events for the median, separate probe pass"}
+    del graph, model, opt, probe
+    torch.cuda.empty_cache()
+    return out
+
+
 def traffic_file(name: str):
     """The newest committed PMC traffic record for this config (profiles/r*/traffic_<cfg>.json)."""
     import glob
@@ -335,17 +406,23 @@ def gemm_fields(m, bf16: bool, steps: int, t_step: float, what: str):
     sec = m["avg_ms"] / 1e3
     gbs = m["avg_bytes"] / sec / 1e9
     tfs = m["avg_work"] / sec / 1e12
-    products = 1 if bf16 else 6
+    # the fp32 GEMM mode libhgin.so runs (hgin_common.h gemm_split_enabled: the same process-static switch)
+    mfma32 = not bf16 and os.environ.get("HGIN_F32_GEMM") == "mfma32"
+    mode = "bf16" if bf16 else ("f32 MFMA (v_mfma_f32_32x32x2_f32)" if mfma32 else "fp32 as 3-way bf16 split, 6 products")
+    products = 1 if (bf16 or mfma32) else 6
+    peak = F32_MFMA_PEAK_TFS if mfma32 else BF16_MFMA_PEAK_TFS
     mfma = tfs * products
-    hf, mf = gbs / HBM_PEAK_GBS, mfma / BF16_MFMA_PEAK_TFS
-    return {"kernel": what, "bound": "hbm" if hf >= mf else "mfma",
+    hf, mf = gbs / HBM_PEAK_GBS, mfma / peak
+    return {"kernel": what, "mode": mode, "bound": "hbm" if hf >= mf else "mfma",
             "hbm": {"achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(hf, 4)},
-            "mfma": {"achieved": round(mfma, 1), "peak": BF16_MFMA_PEAK_TFS, "unit": "TFLOP/s (bf16 products)",
+            "mfma": {"achieved": round(mfma, 1), "peak": peak,
+                     "unit": "TFLOP/s (f32)" if mfma32 else "TFLOP/s (bf16 products)",
                      "frac": round(mf, 4), "products_per_fma": products,
                      "fp32_equivalent_tflops": None if bf16 else round(tfs, 2),
-                     "random_operand_loop": {"tflops": BF16_MFMA_RANDOM_TFS, "frac": round(mfma / BF16_MFMA_RANDOM_TFS, 4),
-                                             "source": "MI355X_MICROARCH.md DVFS give-back (1): bare bf16 MFMA loop, "
-                                                       "random operands, 1.90-1.95 GHz"}},
+                     "random_operand_loop": None if mfma32 else {
+                         "tflops": BF16_MFMA_RANDOM_TFS, "frac": round(mfma / BF16_MFMA_RANDOM_TFS, 4),
+                         "source": "MI355X_MICROARCH.md DVFS give-back (1): bf16 MFMA loop, random operands, "
+                                   "1.90-1.95 GHz"}},
             "bytes_per_launch": m["avg_bytes"], "flops_per_launch": m["avg_work"],
             "avg_launch_ms": round(m["avg_ms"], 5), "launches_per_step": m["launches"] / steps,
             "ms_per_step": round(m["total_ms"] / steps, 3),
@@ -354,6 +431,11 @@ def gemm_fields(m, bf16: bool, steps: int, t_step: float, what: str):
 
 def main():
     args = parse()
+    if args.cpu_full:
+        from hgin.data import CONFIGS
+        rec = cpu_baseline(CONFIGS[args.cpu_full], full_graph=True)
+        print(json.dumps({"cpu_baseline_full": args.cpu_full, **rec}), flush=True)
+        return rec
     from hgin import HetroGIN, _lib, profiling
     from hgin.data import CONFIGS, rank_components, synthetic_graph
     from hgin.dist import GradAllReducer
@@ -430,6 +512,7 @@ def main():
     opt = torch.optim.Adam(lr=1e-3, params=model.parameters(), weight_decay=0, capturable=args.graph,
                            **({"fused": True} if args.adam == "fused" else {}))
     reducer = GradAllReducer(model.parameters()) if (world > 1 or partition == "dst-range") else None
+    stepper = None
 
     def barrier():
         if world > 1:
@@ -473,6 +556,8 @@ def main():
         dist.all_reduce(dt, op=dist.ReduceOp.MAX)
     t_step, t_med = float(dt[0].item()), float(dt[1].item())
     final_loss = float(loss)
+    if reducer is not None:
+        reducer.check()   # one host sync after the timed region: every rank reduced the same parameter set
 
     # untimed per-kernel pass: the same eager step with HIP events around the aggregate and GEMM launches
     probe = None
@@ -556,10 +641,19 @@ def main():
                           "execution": "hipgraph (one replay per step)" if args.graph else "eager",
                           "optimizer": f"torch.optim.Adam(lr=1e-3), {args.adam}"},
                "roofline": roofline, "gemm": gemm, "gemm_dw": gemm_dw, "gemm_dx": gemm_dx, "csr_build": csr_ms, "extras": extra, "final_loss": final_loss}
+        if (world == 1 and cfg.name == "cfg3" and partition == "connected" and args.skew == "uniform" and
+                not (no_extras or args.no_cfg5 or args.prune_dead or args.graph)):
+            # BASELINE configs[4] in the same driver-run line: free the cfg3 graph / model first (60 + 35 GB)
+            del graph, model, opt, step, eager_step, stepper, probe, reducer
+            torch.cuda.synchronize()
+            torch.cuda.empty_cache()
+            out["extras"]["cfg5"] = cfg5_extra(dev, args.adam)
         if ref1 is not None:
             # strong scaling against the same graph on one GPU: t_1gpu / t_step (ideal: N)
             out["one_gpu_reference"] = ref1
             out["scaling_vs_1gpu"] = round(ref1["ms_per_step_median"] / (t_med * 1e3), 3)
+        # the worst-case device footprint of this rank: its share, rank 0's all-component reference and the extras
+        out["peak_device_mem_gb"] = round(torch.cuda.max_memory_allocated(dev) / 1e9, 2)
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(cfg)
         else:

@@ -174,12 +174,13 @@ _SIGS = {
     "hgin_nt_planes_size": ([_I64, _I64, _I32, ctypes.POINTER(_SZ)], _I32),
     "hgin_nt_planes_f32": ([_P, _I64, _I64, _I64, _P, _P], _I32),
     "hgin_nt_planes_bf16": ([_P, _I64, _I64, _I64, _P, _P], _I32),
-    "hgin_global_pool_f32": ([_P, _I64, _P, _I64, _I64, _P, _I64, _P], _I32),
-    "hgin_global_pool_bf16": ([_P, _I64, _P, _I64, _I64, _P, _I64, _P], _I32),
+    "hgin_global_pool_workspace_size": ([_I64, _I64, ctypes.POINTER(_SZ)], _I32),
+    "hgin_global_pool_f32": ([_P, _I64, _P, _I64, _I64, _P, _I64, _P, _P, _SZ, _P], _I32),
+    "hgin_global_pool_bf16": ([_P, _I64, _P, _I64, _I64, _P, _I64, _P, _P, _SZ, _P], _I32),
     "hgin_trace_enable": ([_I32], _I32),
     "hgin_trace_read": ([ctypes.c_char_p, _SZ], _SZ),
 }
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 
 def lib() -> ctypes.CDLL:

@@ -27,7 +27,7 @@ from torch import Tensor
 from . import _lib, profiling
 
 COMBINE_NONE, COMBINE_ADD, COMBINE_CONCAT = 0, 1, 2
-STATUS_ROW_OOR, STATUS_COL_OOR = 1, 2
+STATUS_ROW_OOR, STATUS_COL_OOR, STATUS_UNSORTED = 1, 2, 4
 
 
 def _p(t: Optional[Tensor]):
@@ -820,10 +820,16 @@ def gin_conv(x_src: Tensor, x_dst: Tensor, eps: Tensor, weight: Tensor, bias: Te
     return _GINConvFn.apply(x_src, x_dst, eps, _rowmajor(weight), bias.contiguous(), prelu, accum, graph, mode)
 
 
-def global_pool(x: Tensor, batch: Tensor) -> Tensor:
+_last_pool_status: Optional[Tensor] = None
+
+
+def global_pool(x: Tensor, batch: Tensor, check: bool = False) -> Tensor:
     """[N, 2F] = [global_mean_pool | global_max_pool](x, batch) gathered back to the rows (models.py:347-352), on
-    hgin_global_pool_*: one deterministic launch, no host sync.  ``batch`` must be non-decreasing (PyG
-    collation).  The pooled inputs are data (raw path features): no gradient flows through the pooling."""
+    hgin_global_pool_*: deterministic, no host sync.  ``batch`` must be non-decreasing (PyG collation); the kernel
+    flags a descending pair in a device status word (HGIN_STATUS_UNSORTED), read by ``check_pool_order()`` (one host
+    sync) or at once with ``check=True``.  The pooled inputs are data (raw path features): no gradient flows through
+    the pooling."""
+    global _last_pool_status
     require_device(x, batch, what="hgin.global_pool")
     x = _rowmajor(_f32(x, "x"))
     if torch.is_grad_enabled() and x.requires_grad:
@@ -832,9 +838,23 @@ def global_pool(x: Tensor, batch: Tensor) -> Tensor:
         raise ValueError("hgin.global_pool: batch must be int64 [N] with one entry per row")
     n, f = x.shape
     out = torch.empty(n, 2 * f, dtype=x.dtype, device=x.device)
+    status = torch.zeros(1, dtype=torch.int32, device=x.device)
+    nbytes = ctypes.c_size_t(0)
+    _lib.check(_lib.lib().hgin_global_pool_workspace_size(n, f, ctypes.byref(nbytes)), "global_pool_workspace_size")
+    ws = _workspace(nbytes.value, x.device)
     _lib.call(f"hgin_global_pool_{_sfx(x)}", _p(batch.contiguous()), n, _p(x), x.stride(0), f, _p(out), out.stride(0),
-              _stream(x))
+              _p(status), _p(ws), nbytes.value, _stream(x))
+    _last_pool_status = status
+    if check:
+        check_pool_order()
     return out
+
+
+def check_pool_order() -> None:
+    """Raise if the last global_pool call saw a batch vector that is not non-decreasing (one host sync)."""
+    st = _last_pool_status
+    if st is not None and int(st.item()) & STATUS_UNSORTED:
+        raise ValueError("hgin.global_pool: batch must be non-decreasing (PyG collation order)")
 
 
 # ---------------------------------------------------------------------------------------------------

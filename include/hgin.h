@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define HGIN_ABI_VERSION 3
+#define HGIN_ABI_VERSION 4
 
 #define HGIN_OK 0
 #define HGIN_E_ARG (-1)        /* bad size / null pointer / unsupported combination */
@@ -43,6 +43,7 @@ extern "C" {
 /* status word bits written by hgin_csr_build into *d_status (device int32) */
 #define HGIN_STATUS_ROW_OOR 1  /* a row index (the sorted key) was < 0 or >= n_rows */
 #define HGIN_STATUS_COL_OOR 2  /* a column index was < 0 or >= n_cols               */
+#define HGIN_STATUS_UNSORTED 4 /* a batch vector was not non-decreasing (global pooling) */
 
 int hgin_abi_version(void);
 const char* hgin_last_error(void);
@@ -96,12 +97,18 @@ int hgin_aggregate_f32(const int32_t* rowptr, const int32_t* col, int64_t n_rows
  *   out[r, 0:f]  = mean of x[q, :] over the rows q of r's graph   (sequential row-order fp32 sum, one division)
  *   out[r, f:2f] = max  of x[q, :] over the same rows             (NaN propagates)
  * batch: int64 [n_rows] graph ids, non-decreasing (PyG collation, dataset.py:239-244: each graph's rows are one
- * contiguous run; ids may skip values).  Deterministic; the mean is bit-identical to CPU scatter mean.
- * f <= 4096; out must not overlap x.  No workspace, no host synchronisation. */
+ * contiguous run; ids may skip values); a descending pair ORs HGIN_STATUS_UNSORTED into *d_status (device int32,
+ * caller zeroes it) and the outputs are then unspecified.  Deterministic; for graphs of at most 4096 rows the mean
+ * is bit-identical to CPU scatter mean; longer graphs are summed in 2048-row chunk partials added in chunk order
+ * (within fp32 rounding of the sequential sum).  f <= 4096; out must not overlap x.  No host synchronisation.
+ * workspace: hgin_global_pool_workspace_size(n_rows, f). */
+int hgin_global_pool_workspace_size(int64_t n_rows, int64_t f, size_t* bytes);
 int hgin_global_pool_f32(const int64_t* batch, int64_t n_rows, const float* x, int64_t ldx, int64_t f,
-                         float* out, int64_t ld_out, void* stream);
+                         float* out, int64_t ld_out, int* d_status, void* workspace, size_t workspace_bytes,
+                         void* stream);
 int hgin_global_pool_bf16(const int64_t* batch, int64_t n_rows, const uint16_t* x, int64_t ldx, int64_t f,
-                          uint16_t* out, int64_t ld_out, void* stream);
+                          uint16_t* out, int64_t ld_out, int* d_status, void* workspace, size_t workspace_bytes,
+                          void* stream);
 
 /* ---- A9: backward of the combine -----------------------------------------------------------------
  * Replaces the autograd of `(1 + eps) * x_r` + cat/add (models.py:212-215):

@@ -563,6 +563,53 @@ def test_global_pool_vs_cpu_scatter(F, dtype):
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_global_pool_long_segments(dtype):
+    """GLOBAL_FEATS on big graphs (one graph of millions of path rows must not be one workgroup's serial
+    walk): segments longer than 4096 rows go through 2048-row chunk partials added in chunk order — deterministic, the
+    mean within fp32 rounding of a float64 evaluation, the max exact; short segments beside them stay bit-identical
+    to CPU scatter mean; a single-graph batch of 1M rows; a NaN inside a long segment propagates."""
+    g = torch.Generator().manual_seed(3)
+    F = 5
+    for sizes in ([1_000_000], [3, 4096, 4097, 10, 9000, 2047, 2049, 1, 6000]):
+        batch = torch.cat([torch.full((n,), i, dtype=torch.long) for i, n in enumerate(sizes)])
+        x = torch.randn(batch.numel(), F, generator=g).to(dtype)
+        if len(sizes) > 1:
+            x[4200, 2] = float("nan")                     # inside the 4097-row graph
+        xf = x.double()
+        size = len(sizes)
+        idx = batch.view(-1, 1).expand(-1, F)
+        mean = torch.zeros(size, F, dtype=torch.float64).index_add_(0, batch, xf) / torch.tensor(sizes).view(-1, 1)
+        mx = torch.zeros(size, F, dtype=torch.float64).scatter_reduce(0, idx, xf, reduce="amax", include_self=False)
+        absm = torch.zeros(size, F, dtype=torch.float64).index_add_(0, batch, xf.abs()) / torch.tensor(sizes).view(-1, 1)
+        got = ops.global_pool(x.to(DEV), batch.to(DEV), check=True)
+        got2 = ops.global_pool(x.to(DEV), batch.to(DEV))
+        assert torch.equal(got.isnan(), got2.isnan()) and bool((got.isnan() | (got == got2)).all())   # deterministic
+        got = got.cpu().double()
+        gm, gx = got[:, :F], got[:, F:]
+        ulp = 2 ** -7 if dtype == torch.bfloat16 else 2 ** -20
+        wm = mean[batch]
+        assert torch.equal(gm.isnan(), wm.isnan())
+        fin = ~wm.isnan()
+        assert bool(((gm - wm).abs()[fin] <= ulp * absm[batch][fin] + 1e-30).all())
+        assert torch.equal(gx.isnan(), mx[batch].isnan())
+        assert bool((gx == mx[batch.view(-1)]).logical_or(gx.isnan()).all())
+        # short graphs (<= 4096 rows): bit-identical to the CPU scatter mean of the stored dtype
+        short = torch.tensor([n <= 4096 for n in sizes])[batch]
+        cpu = torch.zeros(size, F).scatter_reduce(0, idx, x.float(), reduce="mean", include_self=False)[batch].to(dtype)
+        gs = got[short][:, :F].to(torch.float32).to(dtype)
+        assert torch.equal(gs.isnan(), cpu[short].isnan()) and bool((gs.isnan() | (gs == cpu[short])).all())
+
+
+def test_global_pool_unsorted_batch_raises():
+    """A batch vector that is not non-decreasing is flagged on the device (HGIN_STATUS_UNSORTED) and raised."""
+    batch = torch.tensor([0, 0, 2, 1, 1, 3], dtype=torch.long, device=DEV)
+    x = torch.randn(6, 4, device=DEV)
+    with pytest.raises(ValueError, match="non-decreasing"):
+        ops.global_pool(x, batch, check=True)
+    ops.global_pool(x, batch.sort().values, check=True)   # sorted: no error
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("M,N,K1,K2", [(100003, 256, 256, 0), (4099, 256, 128, 0), (33, 256, 256, 0),
                                        (20000, 128, 128, 128), (1, 128, 256, 0),
                                        (30011, 256, 256, 256), (50000, 128, 256, 256), (17, 128, 384, 128),

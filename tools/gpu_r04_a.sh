@@ -1,0 +1,34 @@
+#!/bin/bash
+# Round 4, first tree on the GPU: full GPU suite, the driver's bench command (cfg3 headline + extras.cfg5), a kernel
+# profile of the reference's real loop (extras.batches workload, tools/batch_bench.py cfg1 schema), and the 2-rank
+# rehearsals of the N > 1 legs with the probe on (cfg3 -> cfg4 split, and cfg5).  Every GPU step time-limited; the
+# script stops at the first failure.
+set -u
+cd "$(dirname "$0")/.."
+OUT=gpurun_out/${TAG:-r04a}
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+run() {  # name, limit, command...
+  local name=$1 lim=$2; shift 2
+  timeout -k 10 "$lim" "$@" > "$OUT/$name.out" 2> "$OUT/$name.err"
+  local rc=$?; echo "$name $rc $(date +%T)" >> "$OUT/status.txt"
+  [ $rc -eq 0 ] || { echo "FATAL $name $rc"; tail -30 "$OUT/$name.out"; tail -30 "$OUT/$name.err"; exit $rc; }
+}
+echo "start $(date)" > "$OUT/status.txt"
+if [ "${SUITE:-1}" = "1" ]; then
+  run pytest_gpu 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread
+  tail -2 "$OUT/pytest_gpu.out"
+fi
+run smoke 200 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')"
+run bench 600 python bench.py --gpus 1 --steps 20 --warmup 5
+tail -c 600 "$OUT/bench.out"
+run prof_batches 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_batches" -o run -- \
+  python3 tools/batch_bench.py --schema cfg1 --steps 20 --warmup 3
+if [ "${REHEARSE:-1}" = "1" ]; then
+  export HGIN_DIST_BACKEND=gloo
+  run rehearse_cfg3 700 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
+    --master-port 29517 bench.py --gpus 2 --steps 5 --warmup 2
+  run rehearse_cfg5 700 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
+    --master-port 29518 bench.py --gpus 2 --steps 5 --warmup 2 --config cfg5
+fi
+echo "done $(date)" >> "$OUT/status.txt"
