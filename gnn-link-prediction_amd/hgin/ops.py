@@ -84,6 +84,7 @@ LONG_ROW_MIN = int(os.environ.get("HGIN_LONG_ROW", "2048"))
 # HGIN_NT_BDMA=0 keeps the per-tile split
 BDMA = os.environ.get("HGIN_NT_BDMA", "1") != "0" and os.environ.get("HGIN_F32_GEMM", "split") != "mfma32"
 LONG_CHUNK = 1024
+DW512_WSD = os.environ.get("HGIN_DW512", "wsd") == "wsd"
 
 
 @dataclass
@@ -416,7 +417,11 @@ def mlp_bwd_w(g_y: Tensor, z: Tensor, prelu: Tensor, b1: Tensor, b2: Optional[Te
     K = k1 + (b2.shape[1] if b2 is not None else 0)
     dev = z.device
     fused = mlp_bwd_fused(z, N, K)
-    g_z = torch.empty_like(z) if (want_gz or not fused) else None
+    # the first layer's fp32 K = 512 dW (no input gradient, so g_z is not wanted): through the weight-stationary
+    # two-pass form (PReLU-fused pass over columns [0, 256) storing g_z into a scratch, plain pass over [256, 512) on
+    # it) instead of the tiled fused kernel (HGIN_DW512 = wsd / tiled)
+    scratch_gz = fused and not want_gz and z.dtype == torch.float32 and N == 256 and K == 512 and DW512_WSD
+    g_z = torch.empty_like(z) if (want_gz or not fused or scratch_gz) else None
     g_w = torch.empty(N, K, dtype=torch.float32, device=dev)
     g_a = torch.empty(1, dtype=torch.float32, device=dev)
     g_b = torch.empty(N, dtype=torch.float32, device=dev)
@@ -432,7 +437,7 @@ def mlp_bwd_w(g_y: Tensor, z: Tensor, prelu: Tensor, b1: Tensor, b2: Optional[Te
             lambda: _lib.call(f"hgin_gin_mlp_bwd_w_{_sfx(z)}", _p(g_y), g_y.stride(0), _p(z), z.stride(0), _p(prelu),
                               _p(b1), b1.stride(0), k1, _p(b2), b2.stride(0) if b2 is not None else 0, M, N, K,
                               _p(g_w), g_w.stride(0), _p(g_a), _p(g_b), _p(g_z), N, _p(ws), nbytes.value, _stream(z)))
-    return g_w, g_a, g_b, g_z
+    return g_w, g_a, g_b, (None if scratch_gz else g_z)
 
 
 def self_wgrad(G: Tensor, weight: Tensor, f: int, concat: bool, eps: Tensor):

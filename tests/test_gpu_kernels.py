@@ -357,7 +357,9 @@ def test_mlp_bwd_fused(M, N, K1, K2, want_gz, strided):
 def test_mlp_bwd_fused_cfg3_layer0_shape():
     """The largest GEMM of the cfg3 step at its own shape: the first layer's fused PReLU + bias backward + dW
     (N = 256, K = 256 + 256 = [aggregate | x_dst], 1M rows; cfg3 runs it at 3-6M), against float64, with the
-    launch trace proving the fused kernel (not the two-pass fallback) ran."""
+    launch trace proving the PReLU backward was folded into the dW (no separate k_rows_bwd<0> pass): by default the
+    weight-stationary two-pass form (HGIN_DW512=wsd: the PReLU-fused pass over columns [0, 256) storing g_z into a
+    scratch, the plain pass over [256, 512)), with HGIN_DW512=tiled the tiled fused kernel."""
     from hgin import _lib
     M, N, K1, K2 = 1 << 20, 256, 256, 256
     gen = torch.Generator(device=DEV).manual_seed(11)
@@ -370,7 +372,9 @@ def test_mlp_bwd_fused_cfg3_layer0_shape():
         g_w, g_a, g_b, g_z = ops.mlp_bwd_w(gy, z, a, b1, b2)
     torch.cuda.synchronize()
     assert g_z is None
-    assert "k_gemm_tn_partial<prelu_bwd_fused,split,N256,K512>" in tr.kernels, tr.kernels
+    want = (("k_wsd_f32<256,256,prelu_bwd_fused>", "k_wsd_f32<256,256>") if ops.DW512_WSD else
+            ("k_gemm_tn_partial<prelu_bwd_fused,split,N256,K512>",))
+    assert all(k in tr.kernels for k in want), tr.kernels
     assert not any(t.startswith("k_rows_bwd<0") for t in tr.kernels)
     zr, gyr = z.double(), gy.double()
     ga_ref = float((torch.where(zr > 0, torch.zeros_like(zr), zr) * gyr).sum())
