@@ -22,6 +22,9 @@ fi
 run smoke 200 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')"
 run bench 600 python bench.py --gpus 1 --steps 20 --warmup 5
 tail -c 600 "$OUT/bench.out"
+HGIN_DW512=tiled run bench_dw512_tiled 300 python bench.py --no-cpu-baseline --no-extras --no-probe --steps 10 --warmup 3
+run bench_dw512_wsd 300 python bench.py --no-cpu-baseline --no-extras --no-probe --steps 10 --warmup 3
+grep -o '"ms_per_step": [0-9.]*' "$OUT/bench_dw512_tiled.out" "$OUT/bench_dw512_wsd.out"
 run prof_batches 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_batches" -o run -- \
   python3 tools/batch_bench.py --schema cfg1 --steps 20 --warmup 3
 if [ "${REHEARSE:-1}" = "1" ]; then
