@@ -392,7 +392,7 @@ __device__ __forceinline__ void tile_partial(float* smem, float ep, float* part,
 // the first barrier of a K-tile step and awaited (vmcnt 0) before the second: the A split pass between them hides its
 // latency.  No B split VALU (a quarter of the loop's VALU at K = 512, N = 256), no B prefetch registers.
 template <int EPI, bool kClean, int TN, int WNv, bool kSplit, int NW = 4, int kBdma = 0>
-__global__ __launch_bounds__(NW * 64, NW == 8 ? 2 : 3) void k_gemm_nt(Src2 A, Src2 B, int64_t M, int64_t N, int64_t K,
+__global__ __launch_bounds__(NW * 64, (NW == 8 || TN == 4) ? 2 : 3) void k_gemm_nt(Src2 A, Src2 B, int64_t M, int64_t N, int64_t K,
                                                     const float* __restrict__ bias, const float* __restrict__ prelu,
                                                     const float* __restrict__ accum, float* __restrict__ Z,
                                                     float* __restrict__ Y, int64_t ldc, bool vec_out,
@@ -489,30 +489,32 @@ __global__ __launch_bounds__(NW * 64, NW == 8 ? 2 : 3) void k_gemm_nt(Src2 A, Sr
       // two 16-deep k-blocks; lane (i, h) reads k = 16 kb + 8 h .. +7 of each plane (one ds_read_b128)
 #pragma unroll
       for (int kb = 0; kb < 2; ++kb) {
-        bf16x8 fa[2][3], fb[TN][3];
+        bf16x8 fa[2][3];
 #pragma unroll
         for (int t = 0; t < 2; ++t)
 #pragma unroll
           for (int p = 0; p < 3; ++p)
             fa[t][p] = *reinterpret_cast<const bf16x8*>(Ash + (wm * 64 + t * 32 + li) * kSplitRowWordsNT + p * 16 +
                                                         nt_chunk(li, kb * 2 + lh));
+        // B fragments one 32-column block at a time (TN = 4: 12 instead of 48 fragment VGPRs live); per accumulator
+        // the same six products in the same order
 #pragma unroll
-        for (int t = 0; t < TN; ++t)
+        for (int tn = 0; tn < TN; ++tn) {
+          bf16x8 fb[3];
 #pragma unroll
           for (int p = 0; p < 3; ++p)
-            fb[t][p] = *reinterpret_cast<const bf16x8*>(Bcur + (wn * WCOLS + t * 32 + li) * kSplitRowWordsNT + p * 16 +
-                                                        nt_chunk(li, kb * 2 + lh));
+            fb[p] = *reinterpret_cast<const bf16x8*>(Bcur + (wn * WCOLS + tn * 32 + li) * kSplitRowWordsNT + p * 16 +
+                                                     nt_chunk(li, kb * 2 + lh));
 #pragma unroll
-        for (int tm = 0; tm < 2; ++tm)
-#pragma unroll
-          for (int tn = 0; tn < TN; ++tn) {   // smallest terms first
-            acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[tm][2], fb[tn][0], acc[tm][tn], 0, 0, 0);
-            acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[tm][1], fb[tn][1], acc[tm][tn], 0, 0, 0);
-            acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[tm][0], fb[tn][2], acc[tm][tn], 0, 0, 0);
-            acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[tm][1], fb[tn][0], acc[tm][tn], 0, 0, 0);
-            acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[tm][0], fb[tn][1], acc[tm][tn], 0, 0, 0);
-            acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[tm][0], fb[tn][0], acc[tm][tn], 0, 0, 0);
+          for (int tm = 0; tm < 2; ++tm) {   // smallest terms first
+            acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[tm][2], fb[0], acc[tm][tn], 0, 0, 0);
+            acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[tm][1], fb[1], acc[tm][tn], 0, 0, 0);
+            acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[tm][0], fb[2], acc[tm][tn], 0, 0, 0);
+            acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[tm][1], fb[0], acc[tm][tn], 0, 0, 0);
+            acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[tm][0], fb[1], acc[tm][tn], 0, 0, 0);
+            acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[tm][0], fb[0], acc[tm][tn], 0, 0, 0);
           }
+        }
       }
     } else {
 #pragma unroll
@@ -560,6 +562,16 @@ bool nt_bdma_enabled() {
   return on;
 }
 
+// HGIN_NT_T256=1: the split-mode tile at N a multiple of 256 as 128 x 256 (4 waves of 64 x 128, 128 accumulator VGPRs
+// each) at two workgroups per CU (A split once per 256 columns: half the split VALU per MFMA of the 128 x 128 tile).
+bool nt_t256_enabled() {
+  static const bool on = [] {
+    const char* v = getenv("HGIN_NT_T256");
+    return v && v[0] == '1';
+  }();
+  return on;
+}
+
 template <int EPI, int TN, int WN, int NW = 4>
 int64_t launch_nt_tn(bool vec, const Src2& a, const Src2& b, int64_t M, int64_t N, int64_t K, const float* bias,
                      const float* prelu, const float* accum, float* z, float* y, int64_t ldc, bool vec_out,
@@ -570,6 +582,16 @@ int64_t launch_nt_tn(bool vec, const Src2& a, const Src2& b, int64_t M, int64_t 
   const bool xcd = xcd_remap_enabled();
   dim3 grid((unsigned)(xcd ? round_up8(tiles) : tiles));
   if constexpr (TN == 2 && WN == 2 && NW == 4) {
+    if (planes && vec && gemm_split_enabled() && N % 256 == 0 && nt_bdma_enabled() && nt_t256_enabled() &&
+        (int64_t)N * K * 6 < (int64_t(1) << 32)) {
+      const int64_t t2 = (N / 256) * ceil_div(M, 128);
+      dim3 g2((unsigned)(xcd ? round_up8(t2) : t2));
+      HGIN_TRACE("k_gemm_nt<EPI%d,128x256,split_bdma,N%lld,K%lld>", EPI, (long long)N, (long long)K);
+      k_gemm_nt<EPI, true, 4, 2, true, 4, 1><<<g2, 256, 0, s>>>(a, b, M, N, K, bias, prelu, accum, z, y, ldc,
+                                                                  vec_out, t2, xcd, ce,
+                                                                  static_cast<const uint16_t*>(planes));
+      return t2;
+    }
     if (planes && vec && gemm_split_enabled() && N % BN == 0 && nt_bdma_enabled() &&
         (int64_t)N * K * 6 < (int64_t(1) << 32)) {
       HGIN_TRACE("k_gemm_nt<EPI%d,%dx%d,split_bdma,N%lld,K%lld>", EPI, BM, BN, (long long)N, (long long)K);

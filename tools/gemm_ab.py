@@ -1,0 +1,89 @@
+"""Per-launch time of the fp32 GEMM shapes the cfg3 step runs, under the process-static HGIN_* switches of the
+calling environment (one process per variant; tools/gpu_gemm_ab.sh runs the variants back to back).
+
+    python tools/gemm_ab.py [--M 6000000] [--reps 10] [--only fwd512,fwd512acc,fwd256,dw512,dw256pro,dx256]
+
+Prints one JSON line: {"env": {...}, "<shape>": {"ms": median ms per launch, "tflops_bf16_products": ...}, ...}.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import statistics
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "gnn-link-prediction_amd")]
+
+import torch  # noqa: E402
+
+from hgin import ops  # noqa: E402
+
+
+def timed(fn, reps):
+    for _ in range(3):
+        fn()
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(reps + 1)]
+    torch.cuda.synchronize()
+    ev[0].record()
+    for i in range(reps):
+        fn()
+        ev[i + 1].record()
+    torch.cuda.synchronize()
+    return statistics.median(ev[i].elapsed_time(ev[i + 1]) for i in range(reps))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--M", type=int, default=6_000_000)
+    ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--only", default="fwd512,fwd512acc,fwd256,dw512,dw256pro,dx256")
+    args = ap.parse_args()
+    M = args.M
+    g = torch.Generator(device="cuda").manual_seed(1)
+    N = 256
+    res = {"env": {k: v for k, v in os.environ.items() if k.startswith("HGIN_")}, "M": M}
+    s = torch.tensor([0.25], device="cuda")
+    b = torch.randn(N, device="cuda", generator=g)
+    for name in args.only.split(","):
+        if name.startswith("fwd"):
+            K = 512 if "512" in name else 256
+            a = torch.randn(M, K, device="cuda", generator=g)
+            w = torch.randn(N, K, device="cuda", generator=g) / K ** 0.5
+            acc = torch.randn(M, N, device="cuda", generator=g) if name.endswith("acc") else None
+            if K == 512:
+                eps2 = torch.tensor([0.1], device="cuda")
+                fn = lambda: ops.gin_mlp_fwd(a[:, :256], w, b, s, acc, comb2=a[:, 256:], eps2=eps2)   # noqa: E731
+            else:
+                fn = lambda: ops.gin_mlp_fwd(a, w, b, s, acc)   # noqa: E731
+            flops = 2.0 * M * N * K
+        elif name.startswith("dw"):
+            K = 512 if "512" in name else 256
+            a = torch.randn(M, K, device="cuda", generator=g)
+            gy = torch.randn(M, N, device="cuda", generator=g)
+            z = torch.randn(M, N, device="cuda", generator=g)
+            want = name.endswith("pro")
+            if K == 512:
+                fn = lambda: ops.mlp_bwd_w(gy, z, s, a[:, :256], a[:, 256:], want_gz=want)   # noqa: E731
+            else:
+                fn = lambda: ops.mlp_bwd_w(gy, z, s, a, want_gz=want)   # noqa: E731
+            flops = 2.0 * M * N * K
+        elif name == "dx256":
+            gz = torch.randn(M, N, device="cuda", generator=g)
+            w = torch.randn(N, N, device="cuda", generator=g) / 16
+            xd = torch.randn(M, N, device="cuda", generator=g)
+            eps = torch.tensor([0.1], device="cuda")
+            fn = lambda: ops.gemm_nt_combine(gz, w.t().contiguous(), xd, eps, 0, want_gx=True)   # noqa: E731
+            flops = 2.0 * M * N * N
+        else:
+            raise SystemExit(f"unknown shape {name}")
+        ms = timed(fn, args.reps)
+        res[name] = {"ms": round(ms, 4), "tflops_bf16_products": round(6 * flops / (ms / 1e3) / 1e12, 1)}
+        del fn
+        torch.cuda.empty_cache()
+    print(json.dumps(res), flush=True)
+
+
+if __name__ == "__main__":
+    main()
