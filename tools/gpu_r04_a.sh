@@ -27,6 +27,12 @@ run bench_dw512_wsd 300 python bench.py --no-cpu-baseline --no-extras --no-probe
 grep -o '"ms_per_step": [0-9.]*' "$OUT/bench_dw512_tiled.out" "$OUT/bench_dw512_wsd.out"
 run prof_batches 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_batches" -o run -- \
   python3 tools/batch_bench.py --schema cfg1 --steps 20 --warmup 3
+if [ "${GEMMAB:-1}" = "1" ]; then
+  run gemm_ab_default 300 python tools/gemm_ab.py
+  run gemm_ab_t256 300 env HGIN_NT_T256=1 python tools/gemm_ab.py --only fwd512,fwd512acc
+  run gemm_ab_dwtiled 300 env HGIN_DW512=tiled python tools/gemm_ab.py --only dw512
+  cat "$OUT"/gemm_ab_*.out
+fi
 if [ "${REHEARSE:-1}" = "1" ]; then
   export HGIN_DIST_BACKEND=gloo
   run rehearse_cfg3 700 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
