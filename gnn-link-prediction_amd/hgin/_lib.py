@@ -177,6 +177,14 @@ _SIGS = {
     "hgin_global_pool_workspace_size": ([_I64, _I64, ctypes.POINTER(_SZ)], _I32),
     "hgin_global_pool_f32": ([_P, _I64, _P, _I64, _I64, _P, _I64, _P, _P, _SZ, _P], _I32),
     "hgin_global_pool_bf16": ([_P, _I64, _P, _I64, _I64, _P, _I64, _P, _P, _SZ, _P], _I32),
+    "hgin_gat_logits_f32": ([_P, _I64, _I64, _I64, _I64, _P, _P, _P], _I32),
+    "hgin_gat_fwd_f32": ([_P, _P, _I64, _I64, _I64, _P, _I64, _P, _P, ctypes.c_float, _P, _P, _I64, _P, _P, _I64, _P],
+                         _I32),
+    "hgin_gat_bwd_dst_f32": ([_P, _P, _I64, _I64, _I64, _P, _I64, _P, _I64, _P, _P, _P, ctypes.c_float, _P, _P, _P,
+                              _P, _I64, _P], _I32),
+    "hgin_gat_bwd_src_f32": ([_P, _P, _P, _I64, _I64, _I64, _P, _I64, _P, _P, _P, _P, _P, _I64, _P], _I32),
+    "hgin_gat_wsum_workspace_size": ([_I64, _I64, _I64, ctypes.POINTER(_SZ)], _I32),
+    "hgin_gat_wsum_f32": ([_P, _I64, _I64, _I64, _I64, _P, _P, _P, _SZ, _P], _I32),
     "hgin_trace_enable": ([_I32], _I32),
     "hgin_trace_read": ([ctypes.c_char_p, _SZ], _SZ),
 }

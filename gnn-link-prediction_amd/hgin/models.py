@@ -7,8 +7,8 @@ edge_index_dict, path_batch) -> Tensor[N_path, 1]`` are those of the reference, 
 reference checkpoint (``train.py:327``) work unchanged.  Message passing runs on libhgin.so; the readout
 MLP and the optional global pooling are small dense torch ops on the device.
 
-``HetroGAT`` (``models.py:380-506``) is out of scope (the north star names GIN only) and
-raises on construction.
+``HetroGAT`` (``models.py:380-506``, SURVEY.md §8 F4's second conv family) shares HetroGIN's feature slicing, relation
+loop and readout, with the GATConv layers of ``hgin/gat.py``.
 """
 from __future__ import annotations
 
@@ -248,9 +248,63 @@ class HetroGIN(torch.nn.Module):
         return x
 
 
-class HetroGAT(torch.nn.Module):
-    """models.py:380-506 — out of scope for the MI355X hot path."""
+class HetroGAT(HetroGIN):
+    """models.py:380-506 (built by train.py:120-125 when config["MODEL"] == "GAT"): the same feature slicing,
+    HeteroConv relation loop and readout as HetroGIN, with PyG 2.0.2 GATConv layers (hgin/gat.py: HIP edge
+    softmax + weighted aggregate on the relation's CSR / CSC, projections on the MFMA GEMMs).  As in the reference:
+    ``input_channels`` is read, not mutated; the first layer is ``GATConv((-1, -1), H, heads=heads, concat=True)``
+    (lazy input projections, materialised at the first forward), later layers ``GATConv(H, H)`` — which cannot
+    take the first layer's H * heads outputs, so the reference (and this drop-in) runs only with one layer when
+    heads > 1; the readout's first Linear takes H * heads + concat_size + global_feats_size columns."""
 
-    def __init__(self, *args, **kwargs):
-        super().__init__()
-        raise NotImplementedError("HetroGAT is not part of the MI355X hot path (SURVEY.md §2 / §8)")
+    def __init__(self, input_channels: dict, node_embedding_size: int, message_passing_layers: int, dropout: float,
+                 heads: int, concat_path: bool, bl_features: bool, divided_features: bool, global_feats: bool,
+                 mlp_layers: list, act, mlp_head_act, mlp_bn: bool):
+        torch.nn.Module.__init__(self)
+        from .gat import GATConv
+        self.num_layers = message_passing_layers
+        self.dropout = dropout
+        self.concat_path = concat_path
+        self.mlp_layers = mlp_layers
+        self.global_feats = global_feats
+        self.heads = heads
+        self.bl_features = bl_features
+        self.divided_features = divided_features
+        self.global_feats_size = 8 if global_feats else 0
+        if concat_path:   # models.py:396-405: the width of the sliced path features
+            if divided_features and bl_features:
+                self.concat_size = input_channels["path"]
+            elif divided_features:
+                self.concat_size = input_channels["path"] - 1
+            elif bl_features:
+                self.concat_size = input_channels["path"] - 3
+            else:
+                self.concat_size = input_channels["path"] - 4
+        else:
+            self.concat_size = 0
+        self.convs = torch.nn.ModuleList()
+        self.readout = torch.nn.ModuleList()
+        H = node_embedding_size
+        rels = (("path", "uses", "link"), ("link", "includes", "path"), ("link", "connects", "node"),
+                ("node", "has", "link"))
+        # models.py:413-418 first layer; :421-426 remaining layers
+        self.convs.append(HeteroConv({r: GATConv((-1, -1), H, heads=heads, concat=True) for r in rels}, aggr="sum"))
+        for _ in range(self.num_layers - 1):
+            self.convs.append(HeteroConv({r: GATConv(H, H) for r in rels}, aggr="sum"))
+        # models.py:429-459 readout
+        act = make_activation(act)
+        width0 = H * heads + self.concat_size + self.global_feats_size
+        for i in range(len(mlp_layers)):
+            lin = torch.nn.Linear(width0 if i == 0 else mlp_layers[i - 1], mlp_layers[i])
+            if mlp_bn:
+                self.readout.append(torch.nn.Sequential(lin, torch.nn.BatchNorm1d(num_features=mlp_layers[i]), act))
+            else:
+                self.readout.append(torch.nn.Sequential(lin, act))
+        if mlp_head_act is None:
+            self.readout.append(torch.nn.Sequential(torch.nn.Linear(mlp_layers[-1], 1)))
+        else:
+            self.readout.append(torch.nn.Sequential(torch.nn.Linear(mlp_layers[-1], 1),
+                                                    make_activation(mlp_head_act)))
+
+    def prune_dead(self, enable: bool = True):
+        raise NotImplementedError("HetroGAT: dead-relation pruning is a HetroGIN benchmark option")

@@ -384,6 +384,35 @@ int hgin_dot_decode_bwd_f32(const int32_t* rowptr, const int32_t* col, const int
                             int64_t n_rows, const float* g_score, const float* z_other,
                             int64_t ld_other, int64_t F, float* g_z, int64_t ld_g, void* stream);
 
+/* ---- F4 widening: HetroGAT's graph attention (models.py:380-506, PyG 2.0.2 GATConv) ---------------------------
+ * x_s / x_d: projected source / destination features [N, H * C] (row stride ld*), edges = the relation after
+ * GATConv's self-loop handling, as CSR by destination (rowptr, col) and CSC by source (cptr, cdst, cpos = the CSR
+ * position of each CSC entry).  fp32; one thread per (row, head); every sum in a fixed order (deterministic).
+ *   hgin_gat_logits_f32:  a[n, h] = sum_c x[n, h, c] att[h, c]
+ *   hgin_gat_fwd_f32:     alpha[k, h] (CSR order) = softmax over the row of leaky_relu(a_s[j_k, h] + a_d[i, h], slope)
+ *                         (exp(e - max) / (sum + 1e-16), PyG's softmax); out[i, h, :] = sum_k alpha x_s[j_k, h, :]
+ *                         + bias [+ accum].  a_d, bias, accum may be NULL.
+ *   hgin_gat_bwd_dst_f32: g_pre[k, h] = d loss / d (a_s[j_k, h] + a_d[i, h]) (softmax + leaky_relu backward),
+ *                         g_ad[i, h] = sum_k g_pre, g_xd[i, h, :] = g_ad[i, h] att_dst[h, :] (g_ad / g_xd may be NULL)
+ *   hgin_gat_bwd_src_f32: g_as[j, h] = sum_k g_pre, g_xs[j, h, :] = sum_k alpha g_out[i_k, h, :] + g_as att_src[h, :]
+ *   hgin_gat_wsum_f32:    out[h * C + c] = sum_n w[n, h] x[n, h * C + c] (w NULL: 1), fixed 256-row blocks in order;
+ *                         workspace: hgin_gat_wsum_workspace_size. */
+int hgin_gat_logits_f32(const float* x, int64_t ldx, int64_t n, int64_t H, int64_t C, const float* att, float* a,
+                        void* stream);
+int hgin_gat_fwd_f32(const int32_t* rowptr, const int32_t* col, int64_t n_dst, int64_t H, int64_t C, const float* xs,
+                     int64_t ldxs, const float* as, const float* ad, float slope, const float* bias, const float* accum,
+                     int64_t ld_acc, float* alpha, float* out, int64_t ldo, void* stream);
+int hgin_gat_bwd_dst_f32(const int32_t* rowptr, const int32_t* col, int64_t n_dst, int64_t H, int64_t C,
+                         const float* xs, int64_t ldxs, const float* g_out, int64_t ldg, const float* alpha,
+                         const float* as, const float* ad, float slope, const float* att_dst, float* g_pre, float* g_ad,
+                         float* g_xd, int64_t ldgxd, void* stream);
+int hgin_gat_bwd_src_f32(const int32_t* cptr, const int32_t* cdst, const int32_t* cpos, int64_t n_src, int64_t H,
+                         int64_t C, const float* g_out, int64_t ldg, const float* alpha, const float* g_pre,
+                         const float* att_src, float* g_as, float* g_xs, int64_t ldgxs, void* stream);
+int hgin_gat_wsum_workspace_size(int64_t n, int64_t H, int64_t C, size_t* bytes);
+int hgin_gat_wsum_f32(const float* x, int64_t ldx, int64_t n, int64_t H, int64_t C, const float* w, float* out,
+                      void* workspace, size_t workspace_bytes, void* stream);
+
 #ifdef __cplusplus
 }
 #endif
