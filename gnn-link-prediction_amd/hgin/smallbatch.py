@@ -1,0 +1,305 @@
+"""The reference's real training loop as four launches per batch (dataset.py:26, :239-244;
+train.py:25-44): ``SmallBatchStep`` runs a HetroGIN train step over a padded batch of small graphs with the fused
+kernels of ``csrc/hgin_smallbatch.hip`` (GIN forward and backward one workgroup per graph, readout + MAPE + readout
+backward in 16-row tiles, one fixed-order gradient reduction that applies the sqrt-MAPE scale), followed by torch's
+Adam, captured once into a hipGraph and replayed per batch after one device collation launch.
+
+It takes the model train.py builds from config.json (``HetroGIN`` with GINLayer convs, Linear + shared PReLU
+readout, Linear head, no BatchNorm / global features / dropout) at small widths: hidden <= 64, first-layer GEMM
+K <= 128, readout widths <= 256, <= 3 hidden readout layers, <= 4 layers, fp32.  ``SmallBatchStep.supports(model)``
+says whether it applies; ``hgin.graphs.CapturedTrainStep`` (one launch per op, any shape) is the general path.
+
+Parameters' ``.grad`` become views of one flat gradient buffer the reduction kernel writes (replays rewrite them in
+place); the step returns the batch's device ``loss_value`` (train.py:40), no host sync.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Sequence
+
+import torch
+
+from . import _lib, ops
+from .conv import GINConv, GINLayer
+from .models import HetroGIN
+from .store import GraphStore
+
+MAX_L, MAX_HID, REL = 4, 3, 4
+TYPES = ("path", "link", "node")
+RELS = (("path", "uses", "link"), ("link", "includes", "path"), ("link", "connects", "node"), ("node", "has", "link"))
+_P = ctypes.c_void_p
+_I64 = ctypes.c_int64
+_I32 = ctypes.c_int32
+
+
+class _SbConv(ctypes.Structure):
+    _fields_ = [("w", _P), ("b", _P), ("slope", _P), ("eps", _P), ("goff", _I64)]
+
+
+class _SbArgs(ctypes.Structure):   # field for field csrc/hgin_smallbatch.hip SbArgs
+    _fields_ = [("x", _P * 3), ("ldx", _I64 * 3), ("fdim", _I32 * 3), ("cols", (_I32 * 8) * 3),
+                ("rowptr", _P * REL), ("col", _P * REL), ("cptr", _P * REL), ("cdst", _P * REL),
+                ("goff", _P), ("G", _I32), ("y", _P), ("m_valid", _P),
+                ("L", _I32), ("H", _I32), ("conv", (_SbConv * REL) * MAX_L),
+                ("concat_path", _I32), ("nhid", _I32), ("rw", _I32 * MAX_HID),
+                ("row_w", _P * MAX_HID), ("row_b", _P * MAX_HID), ("ro_slope", _P), ("head_w", _P), ("head_b", _P),
+                ("ro_goff", _I64 * MAX_HID), ("ro_slope_goff", _I64), ("head_goff", _I64),
+                ("p_gin", _I64), ("p_ro", _I64),
+                ("act", _P), ("act_off", (_I64 * 3) * MAX_L),
+                ("comb", _P), ("comb_off", (_I64 * REL) * MAX_L),
+                ("zb", _P), ("zb_off", (_I64 * REL) * MAX_L),
+                ("gA", _P), ("gB", _P), ("g_off", _I64 * 3),
+                ("gz", _P), ("gc", _P), ("gz_off", _I64 * 3), ("gc_off", _I64 * 3),
+                ("part_gin", _P), ("part_ro", _P), ("loss_part", _P), ("n_tiles", _I32),
+                ("gflat", _P), ("loss_value", _P)]
+
+
+_OFFSET_FIELDS = ("goff", "m_valid", "conv", "rw", "ro_goff", "p_ro", "act_off", "zb_off", "gc_off", "n_tiles",
+                  "loss_value")
+
+
+def check_layout() -> None:
+    """The ctypes mirror of SbArgs against the library's own sizeof / offsetof (raises on an ABI mismatch)."""
+    lib = _lib.lib()
+    if ctypes.sizeof(_SbArgs) != int(lib.hgin_sb_args_size()):
+        raise RuntimeError(f"SbArgs: {ctypes.sizeof(_SbArgs)} != {lib.hgin_sb_args_size()} bytes")
+    offs = (ctypes.c_int64 * len(_OFFSET_FIELDS))()
+    _lib.check(lib.hgin_sb_args_offsets(offs, len(_OFFSET_FIELDS)), "hgin_sb_args_offsets")
+    for name, o in zip(_OFFSET_FIELDS, offs):
+        if getattr(_SbArgs, name).offset != o:
+            raise RuntimeError(f"SbArgs.{name}: offset {getattr(_SbArgs, name).offset} != {o}")
+
+
+def _column_map(model: HetroGIN, raw: dict) -> dict:
+    """The raw feature columns models.py:333-342 keeps per type, as index lists (the model's own slicing applied to
+    column-index rows)."""
+    probe = {t: torch.arange(raw[t], dtype=torch.float32).reshape(1, -1) for t in TYPES}
+    model._select_features(probe)
+    return {t: [int(v) for v in probe[t].reshape(-1).tolist()] for t in TYPES}
+
+
+def _structure(model: torch.nn.Module):
+    """(convs[l][r] -> (Linear, PReLU weight, eps), hidden readout Linears, the shared slope, head Linear) or a reason
+    string when the fused step does not take the model."""
+    if type(model) is not HetroGIN:
+        return "not a HetroGIN"
+    if model.global_feats or model.dropout > 0.0:
+        return "global features / dropout"
+    if not 1 <= model.num_layers <= MAX_L:
+        return "layers"
+    convs = []
+    for l, hc in enumerate(model.convs):
+        if hc.skip or hc.aggr != "sum":
+            return "pruned relations / aggr"
+        row = []
+        for r in RELS:
+            key = "__".join(r)
+            if key not in hc.convs or not isinstance(hc.convs[key], GINLayer):
+                return f"relation {key}"
+            conv: GINConv = hc.convs[key].conv
+            nn = conv.nn
+            if not (isinstance(nn, torch.nn.Sequential) and len(nn) == 2 and isinstance(nn[0], torch.nn.Linear)
+                    and nn[0].bias is not None and isinstance(nn[1], torch.nn.PReLU) and nn[1].weight.numel() == 1):
+                return "GIN MLP"
+            if conv.concat != (l == 0) or not isinstance(conv.eps, torch.nn.Parameter):
+                return "combine mode / eps"
+            row.append((nn[0], nn[1].weight, conv.eps))
+        if len(hc.convs) != REL:
+            return "relation set"
+        convs.append(row)
+    ro = list(model.readout)
+    hidden, slope = [], None
+    for seq in ro[:-1]:
+        if not (len(seq) == 2 and isinstance(seq[0], torch.nn.Linear) and isinstance(seq[1], torch.nn.PReLU)
+                and seq[1].weight.numel() == 1):
+            return "readout layer"
+        if slope is not None and seq[1].weight is not slope:
+            return "readout activation not shared"
+        slope = seq[1].weight
+        hidden.append(seq[0])
+    head = ro[-1]
+    if not (len(head) == 1 and isinstance(head[0], torch.nn.Linear) and head[0].out_features == 1
+            and head[0].bias is not None):
+        return "head"
+    if not 1 <= len(hidden) <= MAX_HID:
+        return "readout depth"
+    H = model.convs[0].convs["path__uses__link"].conv.nn[0].out_features
+    if H > 64 or any(l.out_features > 256 for l in hidden):
+        return "widths"
+    if any(p.dtype != torch.float32 for p in model.parameters()):
+        return "dtype"
+    return convs, hidden, slope, head[0], H
+
+
+class SmallBatchStep:
+    """Fused HetroGIN train step over padded small-graph batches (see the module docstring)."""
+
+    @staticmethod
+    def supports(model: torch.nn.Module) -> bool:
+        return not isinstance(_structure(model), str)
+
+    def __init__(self, model: HetroGIN, opt: torch.optim.Optimizer, store: GraphStore, batch_size: int,
+                 warmup_ids: Sequence[Sequence[int]], warmup: int = 2):
+        st = _structure(model)
+        if isinstance(st, str):
+            raise ValueError(f"SmallBatchStep: model not supported ({st}); use hgin.graphs.CapturedTrainStep")
+        if not all(g.get("capturable", False) for g in opt.param_groups):
+            raise ValueError("SmallBatchStep needs a capturable optimizer (e.g. Adam(..., capturable=True))")
+        if not warmup_ids:
+            raise ValueError("SmallBatchStep needs at least one warm-up batch")
+        convs, hidden, slope, head, H = st
+        self.model, self.opt, self.store = model, opt, store
+        dev = store.device
+        pb = store.padded_batch(batch_size)
+        self.batch = pb
+        if any(store.x[t].dtype != torch.float32 for t in TYPES):
+            raise ValueError("SmallBatchStep: fp32 features only")
+        raw = {t: int(store.x[t].shape[1]) for t in TYPES}
+        cols = _column_map(model, raw)
+        fdim = {t: len(cols[t]) for t in TYPES}
+        if any(f > 8 for f in fdim.values()):
+            raise ValueError("SmallBatchStep: at most 8 input feature columns per type")
+        L = model.num_layers
+        K0 = [fdim[s] + fdim[d] for (s, _, d) in RELS]
+        if max(K0) > 128:
+            raise ValueError("SmallBatchStep: first-layer K > 128")
+        cap = {t: int(pb.x[t].shape[0]) for t in TYPES}
+        a = _SbArgs()
+        keep = []   # tensors whose pointers the args hold
+
+        def P(t: torch.Tensor):
+            keep.append(t)
+            return t.data_ptr()
+
+        for ti, t in enumerate(TYPES):
+            a.x[ti] = P(pb.x[t])
+            a.ldx[ti] = pb.x[t].stride(0)
+            a.fdim[ti] = fdim[t]
+            for k, c in enumerate(cols[t]):
+                a.cols[ti][k] = c
+        for ri, r in enumerate(RELS):
+            a.rowptr[ri], a.col[ri] = P(pb.csr[r].rowptr), P(pb.csr[r].col)
+            a.cptr[ri], a.cdst[ri] = P(pb.csc[r].rowptr), P(pb.csc[r].col)
+        a.goff, a.G, a.y, a.m_valid = P(pb.goff), batch_size, P(pb.y), P(pb.m_valid)
+        a.L, a.H = L, H
+        # flat gradient layout: GIN convs (W, b, slope, eps per layer / relation), then the readout
+        off = 0
+        param_off = {}
+        for l in range(L):
+            for ri, r in enumerate(RELS):
+                lin, pw, eps = convs[l][ri]
+                K = K0[ri] if l == 0 else H
+                if tuple(lin.weight.shape) != (H, K):
+                    raise ValueError(f"SmallBatchStep: layer {l} {r} weight {tuple(lin.weight.shape)} != {(H, K)}")
+                c = a.conv[l][ri]
+                c.w, c.b, c.slope, c.eps, c.goff = P(lin.weight), P(lin.bias), P(pw), P(eps), off
+                param_off[lin.weight] = off
+                param_off[lin.bias] = off + H * K
+                param_off[pw] = off + H * K + H
+                param_off[eps] = off + H * K + H + 1
+                off += H * K + H + 2
+        p_gin = off
+        a.concat_path = int(bool(model.concat_path))
+        a.nhid = len(hidden)
+        w0 = H + (fdim["path"] if model.concat_path else 0)
+        win = w0
+        for i, lin in enumerate(hidden):
+            if tuple(lin.weight.shape) != (lin.out_features, win):
+                raise ValueError("SmallBatchStep: readout widths")
+            a.rw[i] = lin.out_features
+            a.row_w[i], a.row_b[i] = P(lin.weight), P(lin.bias)
+            a.ro_goff[i] = off
+            param_off[lin.weight] = off
+            param_off[lin.bias] = off + lin.weight.numel()
+            off += lin.weight.numel() + lin.out_features
+            win = lin.out_features
+        a.ro_slope, a.ro_slope_goff = P(slope), off
+        param_off[slope] = off
+        off += 1
+        a.head_w, a.head_b, a.head_goff = P(head.weight), P(head.bias), off
+        param_off[head.weight] = off
+        param_off[head.bias] = off + head.weight.numel()
+        off += head.weight.numel() + 1
+        a.p_gin, a.p_ro = p_gin, off - p_gin
+        params = list(model.parameters())
+        if {id(p) for p in params} != {id(p) for p in param_off}:
+            raise ValueError("SmallBatchStep: the model has parameters outside the fused step")
+        # scratch
+        f32 = dict(dtype=torch.float32, device=dev)
+
+        def blocks(sizes):
+            offs, tot = [], 0
+            for n in sizes:
+                offs.append(tot)
+                tot += n
+            return offs, torch.zeros(max(tot, 1), **f32)
+
+        act_sizes = [cap[t] * H for _ in range(L) for t in TYPES]
+        o, self.act = blocks(act_sizes)
+        a.act = P(self.act)
+        for l in range(L):
+            for ti in range(3):
+                a.act_off[l][ti] = o[l * 3 + ti]
+        kdim = lambda l, ri: K0[ri] if l == 0 else H   # noqa: E731
+        o, self.comb = blocks([cap[RELS[ri][2]] * kdim(l, ri) for l in range(L) for ri in range(REL)])
+        a.comb = P(self.comb)
+        o2, self.zb = blocks([cap[RELS[ri][2]] * H for l in range(L) for ri in range(REL)])
+        a.zb = P(self.zb)
+        for l in range(L):
+            for ri in range(REL):
+                a.comb_off[l][ri] = o[l * REL + ri]
+                a.zb_off[l][ri] = o2[l * REL + ri]
+        o, self.gA = blocks([cap[t] * H for t in TYPES])
+        _, self.gB = blocks([cap[t] * H for t in TYPES])
+        a.gA, a.gB = P(self.gA), P(self.gB)
+        for ti in range(3):
+            a.g_off[ti] = o[ti]
+        kmax = max(max(K0), H)
+        o, self.gz = blocks([cap[t] * H for t in TYPES])
+        o2, self.gc = blocks([cap[t] * kmax for t in TYPES])
+        a.gz, a.gc = P(self.gz), P(self.gc)
+        for ti in range(3):
+            a.gz_off[ti], a.gc_off[ti] = o[ti], o2[ti]
+        n_tiles = (cap["path"] + 15) // 16
+        self.part_gin = torch.zeros(batch_size * p_gin, **f32)
+        self.part_ro = torch.zeros(n_tiles * a.p_ro, **f32)
+        self.loss_part = torch.zeros(n_tiles, **f32)
+        a.part_gin, a.part_ro, a.loss_part, a.n_tiles = P(self.part_gin), P(self.part_ro), P(self.loss_part), n_tiles
+        self.gflat = torch.zeros(off, **f32)
+        self.loss_value = torch.zeros((), **f32)
+        a.gflat, a.loss_value = P(self.gflat), P(self.loss_value)
+        for p in params:
+            o = param_off[p]
+            p.grad = self.gflat[o:o + p.numel()].view_as(p)
+        widths = (ctypes.c_int32 * MAX_HID)(*[a.rw[i] for i in range(MAX_HID)])
+        lds = ctypes.c_size_t(0)
+        _lib.check(_lib.lib().hgin_sb_readout_lds_bytes(H, fdim["path"], a.concat_path, a.nhid, widths,
+                                                        ctypes.byref(lds)), "hgin_sb_readout_lds_bytes")
+        if lds.value > 160 * 1024:
+            raise ValueError("SmallBatchStep: readout tile exceeds LDS")
+        check_layout()
+        self.args, self._keep, self.lds = a, keep, lds.value
+        # warm-up on a side stream (optimizer state, allocator pools), then capture kernels + Adam once
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            for i in range(max(1, warmup)):
+                store.collate_into(warmup_ids[i % len(warmup_ids)], pb)
+                self._launch()
+                opt.step()
+        torch.cuda.current_stream().wait_stream(side)
+        torch.cuda.synchronize()
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph):
+            self._launch()
+            opt.step()
+
+    def _launch(self) -> None:
+        _lib.call("hgin_sb_step", ctypes.addressof(self.args), ctypes.sizeof(self.args), self.lds,
+                  ops._stream(self.gflat))
+
+    def step(self, ids: Sequence[int]) -> torch.Tensor:
+        """One training step on the graphs ``ids``; returns the device loss_value (no host sync)."""
+        self.store.collate_into(ids, self.batch)
+        self.graph.replay()
+        return self.loss_value

@@ -207,7 +207,9 @@ class GraphStore:
                              torch.zeros(E, dtype=torch.int32, device=dev), cap_n[s], cap_n[d])
             ops.attach_relation_graph(ei[r], cap_n[s], cap_n[d], csr[r], csc[r])
         m_valid = torch.zeros(1, dtype=torch.int32, device=dev)
-        return PaddedBatch(x, ei, y, batch, m_valid, csr, csc, batch_size)
+        # per-graph node offsets [path | link | node] x (batch_size + 1) (the fused small-batch step's graph ranges)
+        goff = torch.zeros(3 * (batch_size + 1), dtype=torch.int32, device=dev)
+        return PaddedBatch(x, ei, y, batch, m_valid, csr, csc, batch_size, goff)
 
     def collate_into(self, ids: Sequence[int], out: "PaddedBatch") -> "PaddedBatch":
         """Refill ``out`` with the graphs ``ids``: valid rows first; the CSR / CSC rows past the batch get
@@ -217,11 +219,11 @@ class GraphStore:
         if len(ids) > out.batch_size:
             raise ValueError(f"collate_into: {len(ids)} graphs > batch capacity {out.batch_size}")
         self._launch(ids, nodes, edges, b_node, b_edge, out.x, out.batch, out.y, out.edge_index, out.csr, out.csc,
-                     out.m_valid)
+                     out.m_valid, out.goff, out.batch_size)
         return out
 
     def _launch(self, ids, nodes, edges, b_node, b_edge, x_out, batch_out, y_out, ei_out, csr_out, csc_out,
-                m_valid) -> None:
+                m_valid, goff=None, cap_graphs: int = 0) -> None:
         descs: List[tuple] = []
 
         def ptr(t: Tensor, elem_off: int) -> int:
@@ -272,6 +274,13 @@ class GraphStore:
             descs.append((0, ptr(cc.rowptr, n_s), cc.rowptr.numel() - n_s, E, FILL_I32))
         if m_valid is not None:
             descs.append((0, ptr(m_valid, 0), 1, int(b_node["path"][-1]), FILL_I32))
+        if goff is not None:   # graph j's rows of type t: [goff[t][j], goff[t][j + 1]); graphs past the batch: empty
+            for ti, t in enumerate(("path", "link", "node")):
+                if t not in b_node:
+                    continue
+                for j in range(cap_graphs + 1):
+                    v = int(b_node[t][min(j, len(ids))])
+                    descs.append((0, ptr(goff, ti * (cap_graphs + 1) + j), 1, v, FILL_I32))
 
         arr = np.zeros(len(descs), dtype=DESC_DTYPE)
         if descs:
@@ -292,3 +301,4 @@ class PaddedBatch(HeteroGraph):
     csr: Dict[EdgeType, ops.Csr] = None
     csc: Dict[EdgeType, ops.Csr] = None
     batch_size: int = 0
+    goff: Tensor = None   # int32 [3 * (batch_size + 1)]: per-graph node offsets, path | link | node

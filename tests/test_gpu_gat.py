@@ -9,7 +9,9 @@ import ctypes
 import pytest
 import torch
 
-from conftest import DEV, fixture_inputs, load_fixture
+from conftest import fixture_inputs, load_fixture
+
+DEV = "cuda"
 
 pytestmark = pytest.mark.gpu
 
