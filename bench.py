@@ -250,14 +250,17 @@ def one_gpu_reference(cfg, n_comp: int, dev, adam: str, graph_mode: bool, warmup
 def batches_extra(dev, n_graphs: int = 256, batch: int = 8, warmup: int = 5, steps: int = 200) -> dict:
     """The reference's actual training loop (dataset.py:26, :239-244, train.py:25-44): shuffled
     batches of 8 small graphs.  Here: a cfg1-schema GraphStore (n_graphs RouteNet-sized graphs, 0.5x-1.5x cfg1,
-    the reference's always-on normalisation applied once at build), each step = one device collation launch
-    (GraphStore.collate_into) + one hipGraph replay of the whole train step (hgin/graphs.py CapturedTrainStep).
-    HIP events around the timed batches; reported beside the headline, not in it."""
+    the reference's always-on normalisation applied once at build); each step = one device collation launch
+    (GraphStore.collate_into) + one hipGraph replay of the whole train step: the fused small-batch step
+    (hgin/smallbatch.py: four kernels + Adam) where it takes the model, and the general per-op path
+    (hgin/graphs.py CapturedTrainStep) beside it.  HIP events around the timed batches; reported beside the
+    headline, not in it."""
     import numpy as np
 
     from hgin import HetroGIN
     from hgin.data import CONFIGS, CONV_RELATIONS, scaled_config, synthetic_graph
     from hgin.graphs import CapturedTrainStep
+    from hgin.smallbatch import SmallBatchStep
     from hgin.store import GraphStore
     base = CONFIGS["cfg1"]
     rng = np.random.default_rng(0)
@@ -267,28 +270,47 @@ def batches_extra(dev, n_graphs: int = 256, batch: int = 8, warmup: int = 5, ste
     order = [rng.choice(n_graphs, batch, replace=False).tolist() for _ in range(warmup + steps)]
     conv_edges = [sum(int(store.edge_off[r][g + 1] - store.edge_off[r][g]) for r in CONV_RELATIONS for g in ids)
                   for ids in order[warmup:]]
+
+    def run(kind):
+        torch.manual_seed(1997)
+        model = HetroGIN(**base.model_kwargs({"link": base.f_link, "path": base.f_path, "node": base.f_node})).to(dev)
+        opt = torch.optim.Adam(lr=1e-3, params=model.parameters(), capturable=True)
+        if kind == "fused":
+            stepper = SmallBatchStep(model, opt, store, batch, warmup_ids=order[:warmup], warmup=warmup)
+        else:
+            stepper = CapturedTrainStep(model, opt, store, batch, warmup_ids=order[:warmup], warmup=warmup)
+        torch.cuda.synchronize()
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        t0 = time.perf_counter()
+        s.record()
+        for ids in order[warmup:]:
+            loss = stepper.step(ids)
+        e.record()
+        torch.cuda.synchronize()
+        wall = (time.perf_counter() - t0) / steps
+        return s.elapsed_time(e) / steps, wall, float(loss)
+
     torch.manual_seed(1997)
-    model = HetroGIN(**base.model_kwargs({"link": base.f_link, "path": base.f_path, "node": base.f_node})).to(dev)
-    opt = torch.optim.Adam(lr=1e-3, params=model.parameters(), capturable=True)
-    stepper = CapturedTrainStep(model, opt, store, batch, warmup_ids=order[:warmup], warmup=warmup)
-    torch.cuda.synchronize()
-    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    t0 = time.perf_counter()
-    s.record()
-    for ids in order[warmup:]:
-        loss = stepper.step(ids)
-    e.record()
-    torch.cuda.synchronize()
-    wall = (time.perf_counter() - t0) / steps
-    ms = s.elapsed_time(e) / steps
-    return {"workload": f"{n_graphs} cfg1-schema graphs (7/7/3 raw features, normalised; sizes 0.5x-1.5x of "
-                        f"{base.nodes} nodes / {base.graph_edges} edges) resident, shuffled batches of {batch}, "
-                        f"hidden {base.hidden}, {base.layers} layers, fp32",
-            "execution": "device collation (one batched-copy launch) + one hipGraph replay per batch",
-            "batches": steps, "ms_per_batch": round(ms, 4), "host_ms_per_batch": round(wall * 1e3, 4),
-            "graphs_per_s": round(batch / (ms / 1e3), 1),
-            "edges_per_s": round(float(np.mean(conv_edges)) / (ms / 1e3), 1),
-            "mean_conv_edges_per_batch": float(np.mean(conv_edges)), "final_loss": float(loss)}
+    probe_model = HetroGIN(**base.model_kwargs({"link": base.f_link, "path": base.f_path, "node": base.f_node}))
+    kinds = (["fused"] if SmallBatchStep.supports(probe_model) else []) + ["general"]
+    res = {k: run(k) for k in kinds}
+    ms, wall, loss = res[kinds[0]]
+    out = {"workload": f"{n_graphs} cfg1-schema graphs (7/7/3 raw features, normalised; sizes 0.5x-1.5x of "
+                       f"{base.nodes} nodes / {base.graph_edges} edges) resident, shuffled batches of {batch}, "
+                       f"hidden {base.hidden}, {base.layers} layers, fp32",
+           "execution": ("device collation (one batched-copy launch) + one hipGraph replay per batch of the fused "
+                         "small-batch step (4 kernels + Adam)" if kinds[0] == "fused" else
+                         "device collation (one batched-copy launch) + one hipGraph replay per batch"),
+           "batches": steps, "ms_per_batch": round(ms, 4), "host_ms_per_batch": round(wall * 1e3, 4),
+           "graphs_per_s": round(batch / (ms / 1e3), 1),
+           "edges_per_s": round(float(np.mean(conv_edges)) / (ms / 1e3), 1),
+           "mean_conv_edges_per_batch": float(np.mean(conv_edges)), "final_loss": loss}
+    if "fused" in res:
+        g_ms, g_wall, g_loss = res["general"]
+        out["general_path"] = {"ms_per_batch": round(g_ms, 4), "host_ms_per_batch": round(g_wall * 1e3, 4),
+                               "final_loss": g_loss,
+                               "execution": "per-op HIP kernels as one hipGraph replay (hgin/graphs.py)"}
+    return out
 
 
 def extras(graph, dev) -> dict:
