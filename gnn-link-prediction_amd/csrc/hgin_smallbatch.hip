@@ -87,6 +87,7 @@ struct SbArgs {
   float* gz;                // [3] blocks of cap_t x H     (per destination type: graphs are row-disjoint)
   float* gc;                // [3] blocks of cap_t x Kmax
   int64_t gz_off[3], gc_off[3];
+  int kmax;                 // row stride of the gc blocks (relations into one type may differ in K)
   float* part_gin;          // [G][p_gin]
   float* part_ro;           // [n_tiles][p_ro]
   float* loss_part;         // [n_tiles]
@@ -358,7 +359,7 @@ __global__ __launch_bounds__(kSbThreads) void k_sb_gin_bwd(SbArgs a) {
       const float* comb = a.comb + a.comb_off[l][r];
       const float* gy = gcur + a.g_off[d];
       float* gz = a.gz + a.gz_off[d] + (int64_t)n0[d] * H;   // this graph's rows of d
-      float* gc = a.gc + a.gc_off[d] + (int64_t)n0[d] * K;
+      float* gc = a.gc + a.gc_off[d] + (int64_t)n0[d] * a.kmax;   // rows of stride kmax: graph-disjoint
       // g_z, the slope partial (sum over z <= 0 of g_y z)
       float spart = 0.0f;
       for (int idx = tid; idx < rows * H; idx += kSbThreads) {
@@ -413,7 +414,7 @@ __global__ __launch_bounds__(kSbThreads) void k_sb_gin_bwd(SbArgs a) {
           float* gx = gnxt + a.g_off[d] + row * H + k;
           *gx = __fadd_rn(*gx, __fmul_rn(sc, gcv));
         }
-        gc[i * K + k] = gcv;
+        gc[(int64_t)i * a.kmax + k] = gcv;
       }
       const float esum = block_sum(epart, red);   // (also the barrier before the CSC pass reads gc)
       if (tid == 0) part[cv.goff + (int64_t)H * K + H + 1] = esum;
@@ -424,7 +425,7 @@ __global__ __launch_bounds__(kSbThreads) void k_sb_gin_bwd(SbArgs a) {
         for (int idx = tid; idx < srows * H; idx += kSbThreads) {
           const int u = n0[s] + idx / H, k = idx % H;
           float v = 0.0f;
-          for (int e = cp[u]; e < cp[u + 1]; ++e) v = __fadd_rn(v, gc[(int64_t)(cd[e] - n0[d]) * K + k]);
+          for (int e = cp[u]; e < cp[u + 1]; ++e) v = __fadd_rn(v, gc[(int64_t)(cd[e] - n0[d]) * a.kmax + k]);
           float* gx = gnxt + a.g_off[s] + (int64_t)u * H + k;
           *gx = __fadd_rn(*gx, v);
         }

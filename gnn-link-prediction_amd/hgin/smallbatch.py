@@ -49,7 +49,7 @@ class _SbArgs(ctypes.Structure):   # field for field csrc/hgin_smallbatch.hip Sb
                 ("comb", _P), ("comb_off", (_I64 * REL) * MAX_L),
                 ("zb", _P), ("zb_off", (_I64 * REL) * MAX_L),
                 ("gA", _P), ("gB", _P), ("g_off", _I64 * 3),
-                ("gz", _P), ("gc", _P), ("gz_off", _I64 * 3), ("gc_off", _I64 * 3),
+                ("gz", _P), ("gc", _P), ("gz_off", _I64 * 3), ("gc_off", _I64 * 3), ("kmax", _I32),
                 ("part_gin", _P), ("part_ro", _P), ("loss_part", _P), ("n_tiles", _I32),
                 ("gflat", _P), ("loss_value", _P)]
 
@@ -257,7 +257,7 @@ class SmallBatchStep:
         kmax = max(max(K0), H)
         o, self.gz = blocks([cap[t] * H for t in TYPES])
         o2, self.gc = blocks([cap[t] * kmax for t in TYPES])
-        a.gz, a.gc = P(self.gz), P(self.gc)
+        a.gz, a.gc, a.kmax = P(self.gz), P(self.gc), kmax
         for ti in range(3):
             a.gz_off[ti], a.gc_off[ti] = o[ti], o2[ti]
         n_tiles = (cap["path"] + 15) // 16
