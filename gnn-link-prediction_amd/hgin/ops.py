@@ -83,6 +83,9 @@ LONG_ROW_MIN = int(os.environ.get("HGIN_LONG_ROW", "2048"))
 # fp32 split mode: the 128 x 128 NT tile copies its B stages from pre-split planes by LDS-DMA (k_gemm_nt kBdma);
 # HGIN_NT_BDMA=0 keeps the per-tile split
 BDMA = os.environ.get("HGIN_NT_BDMA", "1") != "0" and os.environ.get("HGIN_F32_GEMM", "split") != "mfma32"
+# libhgin's weight-stationary fp32 forms (try_ws_f32 / try_ws_f32_comb) take K = N = 256 with one A source before
+# the tiled kernel is considered; they read W directly, so no split planes are built for them
+WS32 = os.environ.get("HGIN_NT_WS32", "1")[:1] != "0" and os.environ.get("HGIN_F32_GEMM", "split") != "mfma32"
 LONG_CHUNK = 1024
 DW512_WSD = os.environ.get("HGIN_DW512", "wsd") == "wsd"
 
@@ -304,13 +307,16 @@ def combine_bwd(g: Tensor, x_dst: Tensor, eps: Tensor, want_gx: bool):
     return gx, g_eps
 
 
-def nt_planes(b: Tensor) -> Optional[Tensor]:
+def nt_planes(b: Tensor, M: int = 1 << 20, ws_form: bool = False) -> Optional[Tensor]:
     """The fp32 B operand [N, K] of an NT GEMM pre-converted into its three bf16 split planes (hgin_nt_planes_f32,
     N * K * 6 bytes), which the split-mode 128 x 128 tile copies into LDS by DMA instead of splitting B per tile
-    (bit-identical), or None where that kernel does not take the shape."""
-    if not (BDMA and b.dtype == torch.float32):
+    (bit-identical), or None where that kernel does not take the shape: ``ws_form`` = the call qualifies for
+    libhgin's weight-stationary form (which reads W itself), and M = 0 launches nothing."""
+    if not (BDMA and b.dtype == torch.float32) or M == 0:
         return None
     N, K = b.shape
+    if ws_form and WS32 and N == 256 and K == 256:
+        return None
     if N == 0 or K == 0 or K % 32 or b.stride(1) != 1:
         return None
     if N % 128 or b.data_ptr() % 16 or b.stride(0) % 4:
@@ -329,9 +335,10 @@ def gemm_nt(a: Tensor, b: Tensor) -> Tensor:
     M, K = a.shape
     N = b.shape[0]
     c = torch.empty(M, N, dtype=a.dtype, device=a.device)
+    planes = nt_planes(b, M)
     _probed("gemm_dx", 2.0 * M * N * K, a.element_size() * (M * K + N * K + M * N),
             lambda: _lib.call(f"hgin_gemm_nt_{_sfx(a)}", _p(a), a.stride(0), _p(b), b.stride(0), _p(c), c.stride(0),
-                              M, N, K, _p(nt_planes(b)), _stream(a)))
+                              M, N, K, _p(planes), _stream(a)))
     return c
 
 
@@ -366,12 +373,13 @@ def gemm_nt_combine(a: Tensor, b: Tensor, x_dst: Tensor, eps: Tensor, cs: int, w
     ws = _workspace(nbytes.value, a.device)
     s = a.element_size()
     nb = s * (M * K + N * K + M * N + M * (N - cs) * (1 + int(gx is not None) + int(g_prev is not None)))
+    planes = nt_planes(b, M, ws_form=cs == 0 and b.stride(0) == K)
     _probed("gemm_dx", 2.0 * M * N * K, nb,
             lambda: _lib.call(f"hgin_gemm_nt_combine_{_sfx(a)}", _p(a), a.stride(0), _p(b), b.stride(0), _p(c),
                               c.stride(0), M, N, K, _p(x_dst), x_dst.stride(0), _p(gx),
                               gx.stride(0) if gx is not None else 0, _p(g_prev),
                               g_prev.stride(0) if g_prev is not None else 0, cs, _p(eps), _p(g_eps),
-                              _p(ws), nbytes.value, _p(nt_planes(b)), _stream(a)))
+                              _p(ws), nbytes.value, _p(planes), _stream(a)))
     return c, gx, g_eps
 
 
@@ -471,7 +479,7 @@ def gin_mlp_fwd(comb: Tensor, weight: Tensor, bias: Tensor, prelu: Optional[Tens
     z = torch.empty(M, N, dtype=dt, device=comb.device) if (save_z and prelu is not None) else None
     y = torch.empty(M, N, dtype=dt if prelu is not None else torch.float32, device=comb.device)
     ld2 = comb2.stride(0) if comb2 is not None else 0
-    planes = nt_planes(weight) if weight.stride(1) == 1 else None
+    planes = nt_planes(weight, M, ws_form=comb2 is None and prelu is not None) if weight.stride(1) == 1 else None
 
     def launch():
         if prelu is None:
