@@ -1246,6 +1246,263 @@ __global__ __launch_bounds__(512, 1) void k_wsd_f32(const float* __restrict__ A,
     }
 }
 
+// k_wsp_f32 — k_wsd_f32 at N = K = 256 (the GIN width) as a two-stage software pipeline: iteration i runs the MFMAs
+// of block i on plane buffer i & 1 and the split (PRO: the g_z formation, its store, the partial sums) of block i + 1
+// into plane buffer (i + 1) & 1 — independent work, so one barrier per block.  Waves 0-3 split first and waves 4-7
+// multiply first: the two waves sharing a SIMD (w, w + 4) run the VALU split and the MFMAs side by side instead of
+// both splitting, then both multiplying (MI355X_MICROARCH.md, "try a stagger").
+// The fp32 staging is ONE slot (g_y | z | B, 48 KB): thread t splits exactly the 32 B at byte 32 t of each image,
+// which is what its own wave's DMA pieces wrote, so a wave waits only on its own vmcnt before splitting and refills
+// its slice with the next block as soon as its split has read it — no cross-wave hazard on the slot, and the fill
+// has a whole block of MFMAs to land.  LDS: 48 KB slot + two 48 KB plane buffers = 144 KB.
+// Same blocks per workgroup, same per-thread groups, same per-element products in the same order: g_w, g_z and the
+// partial sums are bit-identical to k_wsd_f32 (HGIN_WSD_PIPE = 0 keeps it).
+struct WspF32Cfg {
+  static constexpr int N = 256, K = 256, NT = 512, WM = 4, TK = 4, BM = 16;
+  static constexpr int A_BYTES = BM * N * 4, B_BYTES = BM * K * 4;
+  template <bool PRO>
+  static constexpr int slot() { return A_BYTES * (PRO ? 2 : 1) + B_BYTES; }
+  static constexpr int PA_ROW = N * 2, PB_ROW = K * 2, PA_BYTES = BM * PA_ROW, PB_BYTES = BM * PB_ROW;
+  static constexpr int PLANES = 3 * (PA_BYTES + PB_BYTES);
+  template <bool PRO>
+  static constexpr int lds() { return slot<PRO>() + 2 * PLANES; }
+  static constexpr int PA = A_BYTES / 1024 / 8, PB = B_BYTES / 1024 / 8;   // DMA pieces per wave per image
+  static_assert(2 * A_BYTES + B_BYTES + 2 * PLANES <= 163840 && BM * N / 8 == NT && BM * K / 8 == NT,
+                "one A and one B group per thread");
+  static_assert(PA * 1024 * 8 == A_BYTES && 32 * NT == A_BYTES, "thread t's 32 B lie in its own wave's pieces");
+};
+
+template <bool PRO>
+__global__ __launch_bounds__(512, 1) void k_wsp_f32(const float* __restrict__ A, int64_t lda,
+                                                    const float* __restrict__ B1, int64_t ldb1,
+                                                    const float* __restrict__ B2, int64_t ldb2, int64_t K1, int64_t M,
+                                                    float* __restrict__ slab, int64_t ld_slab, bool nt_in,
+                                                    WsdPro pro) {
+  using C = WspF32Cfg;
+  constexpr int N = C::N, K = C::K;
+  constexpr int Z_OFF = C::A_BYTES, B_OFF = C::A_BYTES * (PRO ? 2 : 1);
+  extern __shared__ __attribute__((aligned(16))) char wsp_smem[];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wm = wave % C::WM, wk = wave / C::WM;
+  const int64_t nblk = (M + C::BM - 1) / C::BM;
+  const int64_t G = gridDim.x;
+  if ((int64_t)blockIdx.x >= nblk) return;
+  const int64_t my = (nblk - 1 - blockIdx.x) / G + 1;
+  char* const planes0 = wsp_smem + C::slot<PRO>();
+
+  auto tid_o = [&]() {
+    int t;
+    asm volatile("v_mov_b32 %0, %1" : "=v"(t) : "v"(tid));
+    return t;
+  };
+  auto dma = [&](const void* src, void* dst) {
+    if (nt_in) glds16_asm<true>(src, dst); else glds16_asm(src, dst);
+  };
+  const int k1 = (int)K1;
+  auto issue = [&](int64_t i) {   // this wave's slice of block i: g_y [, z] and B pieces
+    const int64_t r0 = ((int64_t)blockIdx.x + i * G) * C::BM;
+    const int rmax = (int)(M - 1 - r0 < C::BM ? M - 1 - r0 : C::BM - 1);
+    const int ln = tid_o() & 63;
+    const float* ab = A + r0 * lda;
+    const float* b1 = B1 + r0 * ldb1;
+    const float* b2 = B2 + r0 * ldb2;
+#pragma unroll
+    for (int q = 0; q < C::PA; ++q) {
+      const int piece = wave * C::PA + q;
+      const int off = piece * 1024 + ln * 16;
+      int r = off / (N * 4);
+      r = r < rmax ? r : rmax;                       // (rows past M are zeroed at the split)
+      dma(ab + (r * (int)lda + (off % (N * 4)) / 4), wsp_smem + piece * 1024);
+      if constexpr (PRO)
+        dma(static_cast<const float*>(pro.z) + (r0 + r) * pro.ldz + (off % (N * 4)) / 4,
+            wsp_smem + Z_OFF + piece * 1024);
+    }
+#pragma unroll
+    for (int q = 0; q < C::PB; ++q) {
+      const int piece = wave * C::PB + q;
+      const int off = piece * 1024 + ln * 16;
+      int r = off / (K * 4);
+      r = r < rmax ? r : rmax;
+      const int k = (off % (K * 4)) / 4;
+      dma(k < k1 ? b1 + (r * (int)ldb1 + k) : b2 + (r * (int)ldb2 + (k - k1)), wsp_smem + B_OFF + piece * 1024);
+    }
+  };
+  float csum[8];
+  float ssum = 0.0f;
+  const float sl = PRO ? pro.slope[0] : 0.0f;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) csum[j] = 0.0f;
+
+  f32x16 acc[2][C::TK];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < C::TK; ++b)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[a][b][e] = 0.0f;
+
+  const int g = lane >> 4, q4 = (lane >> 2) & 3, pp = lane & 3;
+  auto tr_off = [&](int rowbytes, int row, int col) {
+    return rowbytes * row + 16 * ((col >> 3) ^ wsd_swz(row));
+  };
+  auto tr = [&](int off) { return __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(wsp_smem + off)); };
+
+  // block j (landed in this wave's slice) -> plane buffer j & 1, then the slice is refilled with block j + 1
+  auto split = [&](int64_t j) {
+    wait_vm<0>();                                    // this wave's pieces of block j (and its older stores)
+    char* pl = planes0 + (int)(j & 1) * C::PLANES;
+    const int64_t r0 = ((int64_t)blockIdx.x + j * G) * C::BM;
+    const int valid = M - r0 < C::BM ? (int)(M - r0) : C::BM;
+    const int t = tid_o();
+    const int row = t / (N / 8), col = (t % (N / 8)) * 8;
+    const int off = C::PA_ROW * row + 16 * ((col >> 3) ^ wsd_swz(row));   // PA_ROW == PB_ROW
+    float4 va0 = *reinterpret_cast<const float4*>(wsp_smem + 32 * t);
+    float4 va1 = *reinterpret_cast<const float4*>(wsp_smem + 32 * t + 16);
+    float4 vb0 = *reinterpret_cast<const float4*>(wsp_smem + B_OFF + 32 * t);
+    float4 vb1 = *reinterpret_cast<const float4*>(wsp_smem + B_OFF + 32 * t + 16);
+    float4 z0 = make_float4(0.f, 0.f, 0.f, 0.f), z1 = z0;
+    if constexpr (PRO) {
+      z0 = *reinterpret_cast<const float4*>(wsp_smem + Z_OFF + 32 * t);
+      z1 = *reinterpret_cast<const float4*>(wsp_smem + Z_OFF + 32 * t + 16);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the slice is read: refill it
+    if (j + 1 < my) issue(j + 1);
+    if (row >= valid) va0 = va1 = vb0 = vb1 = z0 = z1 = make_float4(0.f, 0.f, 0.f, 0.f);
+    if constexpr (PRO) {   // g_z from g_y and z; its store; the partial sums (k_wsd_f32's arithmetic)
+      float gg[8] = {va0.x, va0.y, va0.z, va0.w, va1.x, va1.y, va1.z, va1.w};
+      const float zz[8] = {z0.x, z0.y, z0.z, z0.w, z1.x, z1.y, z1.z, z1.w};
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const bool pos = zz[e] > 0.0f;
+        const float o = pos ? gg[e] : __fmul_rn(sl, gg[e]);
+        csum[e] = __fadd_rn(csum[e], o);
+        if (!pos) ssum = __fadd_rn(ssum, __fmul_rn(zz[e], gg[e]));
+        gg[e] = o;
+      }
+      va0 = make_float4(gg[0], gg[1], gg[2], gg[3]);
+      va1 = make_float4(gg[4], gg[5], gg[6], gg[7]);
+      const int64_t gr = r0 + row;
+      float* gzp = gr < M ? static_cast<float*>(pro.gz) + gr * pro.ldgz + col
+                          : reinterpret_cast<float*>(pro.dump + (int64_t)t * 32);
+      *reinterpret_cast<float4*>(gzp) = va0;
+      *reinterpret_cast<float4*>(gzp + 4) = va1;
+    }
+    uint2 o0[3], o1[3];
+    split4(va0, o0);
+    split4(va1, o1);
+#pragma unroll
+    for (int p = 0; p < 3; ++p)
+      *reinterpret_cast<uint4*>(pl + p * C::PA_BYTES + off) = make_uint4(o0[p].x, o0[p].y, o1[p].x, o1[p].y);
+    split4(vb0, o0);
+    split4(vb1, o1);
+#pragma unroll
+    for (int p = 0; p < 3; ++p)
+      *reinterpret_cast<uint4*>(pl + 3 * C::PA_BYTES + p * C::PB_BYTES + off) =
+          make_uint4(o0[p].x, o0[p].y, o1[p].x, o1[p].y);
+  };
+  // block i's products from plane buffer i & 1 (k_wsd_f32's fragments and order)
+  auto mfma = [&](int64_t i) {
+    const int pa0 = C::slot<PRO>() + (int)(i & 1) * C::PLANES, pb0 = pa0 + 3 * C::PA_BYTES;
+    bf16x8 fa[2][3];
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const int col = wm * 64 + t * 32 + 16 * (g & 1) + 4 * pp;
+      const int row = 8 * (g >> 1) + q4;
+#pragma unroll
+      for (int p = 0; p < 3; ++p) {
+        const int o = pa0 + p * C::PA_BYTES + 2 * (col & 7);
+        const bf16x4 a0 = tr(o + tr_off(C::PA_ROW, row, col)), a1 = tr(o + tr_off(C::PA_ROW, row + 4, col));
+        fa[t][p] = __builtin_shufflevector(a0, a1, 0, 1, 2, 3, 4, 5, 6, 7);
+      }
+    }
+#pragma unroll
+    for (int tn = 0; tn < C::TK; ++tn) {
+      bf16x8 fb[3];
+      const int col = wk * (C::TK * 32) + tn * 32 + 16 * (g & 1) + 4 * pp;
+      const int row = 8 * (g >> 1) + q4;
+#pragma unroll
+      for (int p = 0; p < 3; ++p) {
+        const int o = pb0 + p * C::PB_BYTES + 2 * (col & 7);
+        const bf16x4 b0 = tr(o + tr_off(C::PB_ROW, row, col)), b1 = tr(o + tr_off(C::PB_ROW, row + 4, col));
+        fb[p] = __builtin_shufflevector(b0, b1, 0, 1, 2, 3, 4, 5, 6, 7);
+      }
+#pragma unroll
+      for (int tm = 0; tm < 2; ++tm) {
+        acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[tm][2], fb[0], acc[tm][tn], 0, 0, 0);
+        acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[tm][1], fb[1], acc[tm][tn], 0, 0, 0);
+        acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[tm][0], fb[2], acc[tm][tn], 0, 0, 0);
+        acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[tm][1], fb[0], acc[tm][tn], 0, 0, 0);
+        acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[tm][0], fb[1], acc[tm][tn], 0, 0, 0);
+        acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[tm][0], fb[0], acc[tm][tn], 0, 0, 0);
+      }
+    }
+  };
+
+  issue(0);
+  split(0);
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  for (int64_t i = 0; i + 1 < my; ++i) {
+    __builtin_amdgcn_s_barrier();   // planes of block i written by every wave; those of block i - 1 read by every wave
+    asm volatile("" ::: "memory");
+    if (wave < 4) {
+      split(i + 1);
+      mfma(i);
+    } else {
+      mfma(i);
+      split(i + 1);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // this wave's plane writes and fragment reads are done
+  }
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+  mfma(my - 1);
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  if constexpr (PRO) {   // k_wsd_f32's fixed-order workgroup sums (same thread -> group map)
+    wait_vm<0>();
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    float* red = reinterpret_cast<float*>(wsp_smem);   // [NT][8], then [NT] slope partials
+#pragma unroll
+    for (int j = 0; j < 8; ++j) red[tid * 8 + j] = csum[j];
+    red[C::NT * 8 + tid] = ssum;
+    __syncthreads();
+    for (int n = tid; n < N; n += C::NT) {
+      float tot = 0.0f;
+      for (int row = 0; row < C::BM; ++row) tot = __fadd_rn(tot, red[(row * (N / 8) + (n >> 3)) * 8 + (n & 7)]);
+      pro.pcol[(int64_t)n * gridDim.x + blockIdx.x] = tot;
+    }
+    float* sr = red + C::NT * 8;
+    for (int off = C::NT / 2; off > 0; off >>= 1) {
+      __syncthreads();
+      if (tid < off) sr[tid] = __fadd_rn(sr[tid], sr[tid + off]);
+    }
+    if (tid == 0) pro.ps[blockIdx.x] = sr[0];
+  }
+  float* out = slab + (int64_t)blockIdx.x * N * ld_slab;
+  const int li = lane & 31, lh = lane >> 5;
+#pragma unroll
+  for (int tm = 0; tm < 2; ++tm)
+#pragma unroll
+    for (int tn = 0; tn < C::TK; ++tn) {
+      const int k = wk * (C::TK * 32) + tn * 32 + li;
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int n = wm * 64 + tm * 32 + (e & 3) + 8 * (e >> 2) + 4 * lh;
+        out[n * ld_slab + k] = acc[tm][tn][e];
+      }
+    }
+}
+
+bool wsp_enabled() {   // HGIN_WSD_PIPE = 1 / 0: the pipelined form at N = K = 256 (default off until measured)
+  static const bool on = [] {
+    const char* v = getenv("HGIN_WSD_PIPE");
+    return v && v[0] == '1';
+  }();
+  return on;
+}
+
 // Weight-stationary dW launch (HGIN_TN_WS = 0 / 1; default on): bf16, N in {128, 256}, K in {128, 256, 512},
 // k1 a multiple of 8, 16-B aligned rows (leading dimensions multiples of 8, below 2^24).  Returns the slab
 // count, or 0 when it does not apply.
@@ -1298,15 +1555,28 @@ template <int NV, int KV, bool PRO = false>
 int64_t launch_wsd(const float* a, int64_t lda, const float* b1, int64_t ldb1, const float* b2, int64_t ldb2,
                    int64_t k1, int64_t M, float* slab, int64_t ld_slab, int64_t grid, hipStream_t s,
                    const WsdPro& pro = WsdPro{}) {
+  static const bool nt = [] {
+    const char* v = getenv("HGIN_WS_NT");
+    return !(v && v[0] == '0');
+  }();
+  if constexpr (NV == 256 && KV == 256) {
+    if (wsp_enabled()) {
+      auto kp = k_wsp_f32<PRO>;
+      constexpr int plds = WspF32Cfg::lds<PRO>();
+      static const hipError_t pattr = hipFuncSetAttribute(reinterpret_cast<const void*>(kp),
+                                                          hipFuncAttributeMaxDynamicSharedMemorySize, plds);
+      if (pattr == hipSuccess) {
+        HGIN_TRACE("k_wsp_f32<%d,%d%s>", NV, KV, PRO ? ",prelu_bwd_fused" : "");
+        kp<<<(unsigned)grid, 512, plds, s>>>(a, lda, b1, ldb1, b2, ldb2, k1, M, slab, ld_slab, nt, pro);
+        return grid;
+      }
+    }
+  }
   constexpr int lds = WsdF32Cfg<NV, KV, PRO>::LDS;
   auto kern = k_wsd_f32<NV, KV, PRO>;
   static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
                                                      hipFuncAttributeMaxDynamicSharedMemorySize, lds);
   if (attr != hipSuccess) return 0;
-  static const bool nt = [] {
-    const char* v = getenv("HGIN_WS_NT");
-    return !(v && v[0] == '0');
-  }();
   HGIN_TRACE("k_wsd_f32<%d,%d%s>", NV, KV, PRO ? ",prelu_bwd_fused" : "");
   kern<<<(unsigned)grid, 512, lds, s>>>(a, lda, b1, ldb1, b2, ldb2, k1, M, slab, ld_slab, nt, pro);
   return grid;

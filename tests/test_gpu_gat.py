@@ -86,6 +86,9 @@ def test_forward_backward_step_vs_reference(case):
     torch.sqrt(lv).backward()
     for n, p in model.named_parameters():
         want = fx[f"grad.{n}"]
+        if want.numel() == 0:        # the reference left it None (its relation does not reach the readout)
+            assert p.grad is None, n
+            continue
         assert p.grad is not None, n
         d = (p.grad.detach().double().cpu() - want.double()).norm()
         assert float(d) <= 1e-4 * float(want.double().norm()) + 1e-7, (n, float(d), float(want.norm()))

@@ -10,7 +10,10 @@ fixtures (tests/variant_child.py), so the non-default paths pytest's own process
   * HGIN_GEMM_NT_IO=1       — non-temporal GEMM epilogue streams at every size (default: > 512 MiB): bit-identical;
   * HGIN_WSD_PRO=0          — the separate PReLU-backward pass ahead of the weight-stationary dW instead of the
                               fused one: bit-identical (same g_z, same dW partition; the bias / slope sums are
-                              grouped differently, so those two gradients are compared within fixture tolerance).
+                              grouped differently, so those two gradients are compared within fixture tolerance);
+  * HGIN_NT_BDMA=0          — the NT GEMM splitting B per tile instead of copying pre-split planes: bit-identical;
+  * HGIN_WSD_PIPE=1         — the software-pipelined weight-stationary fp32 dW at N = K = 256 (k_wsp_f32):
+                              bit-identical.
 
 Each child is a separate interpreter started with subprocess (never an exec of this process).
 """
@@ -36,9 +39,10 @@ VARIANTS = {
     "gemm_nt_io": {"HGIN_GEMM_NT_IO": "1"},
     "wsd_pro_off": {"HGIN_WSD_PRO": "0"},
     "nt_bdma_off": {"HGIN_NT_BDMA": "0"},
+    "wsd_pipe": {"HGIN_WSD_PIPE": "1"},
 }
 BITWISE_EQUAL_TO_DEFAULT = ("slab2pass", "agg_pipe", "agg_notail", "xcd_off", "agg_nt_all", "gemm_nt_io", "wsd_pro_off",
-                            "nt_bdma_off")
+                            "nt_bdma_off", "wsd_pipe")
 
 # Scalar / column-sum gradients a variant regroups: the bias / PReLU-slope sums (per workgroup in the fused
 # weight-stationary dW, per row block in k_rows_bwd<0>).  Everything else must stay bit-identical.
