@@ -577,6 +577,12 @@ def main():
     if world > 1:
         dist.all_reduce(dt, op=dist.ReduceOp.MAX)
     t_step, t_med = float(dt[0].item()), float(dt[1].item())
+    # every rank's peak device footprint over setup + warm-up + the timed steps (before the probe / reference passes)
+    peak = torch.zeros(world, dtype=torch.float64, device=dev)
+    peak[rank] = torch.cuda.max_memory_allocated(dev) / 1e9
+    if world > 1:
+        dist.all_reduce(peak)
+    peak_per_rank = [round(float(v), 2) for v in peak.tolist()]
     final_loss = float(loss)
     if reducer is not None:
         reducer.check()   # one host sync after the timed region: every rank reduced the same parameter set
@@ -676,6 +682,7 @@ def main():
             out["scaling_vs_1gpu"] = round(ref1["ms_per_step_median"] / (t_med * 1e3), 3)
         # the worst-case device footprint of this rank: its share, rank 0's all-component reference and the extras
         out["peak_device_mem_gb"] = round(torch.cuda.max_memory_allocated(dev) / 1e9, 2)
+        out["peak_device_mem_gb_timed_per_rank"] = peak_per_rank
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(cfg)
         else:

@@ -494,12 +494,19 @@ extern "C" int hgin_sb_step(const void* args, size_t args_bytes, size_t readout_
                  "hgin_sb_step: unsupported shape");
   hipStream_t s = as_stream(stream);
   HGIN_TRACE("k_sb_step");
-  static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(k_sb_readout),
-                                                     hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-  if (attr != hipSuccess) {
-    set_error("hgin_sb_step: hipFuncSetAttribute failed: %s", hipGetErrorString(attr));
-    return (int)attr;
+  // the readout kernel's dynamic LDS may use what its static reduction array leaves of the CU's 160 KiB
+  static const int dyn_max = [] {
+    hipFuncAttributes fa;
+    if (hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(k_sb_readout)) != hipSuccess) return -1;
+    const int m = 160 * 1024 - (int)fa.sharedSizeBytes;
+    return hipFuncSetAttribute(reinterpret_cast<const void*>(k_sb_readout),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, m) == hipSuccess ? m : -1;
+  }();
+  if (dyn_max < 0) {
+    set_error("hgin_sb_step: could not raise the readout kernel's dynamic LDS limit");
+    return (int)hipErrorInvalidValue;
   }
+  HGIN_ARG_CHECK((int64_t)readout_lds <= dyn_max, "hgin_sb_step: readout LDS %zu above %d", readout_lds, dyn_max);
   k_sb_gin_fwd<<<a.G, kSbThreads, 0, s>>>(a);
   k_sb_readout<<<a.n_tiles, kSbThreads, readout_lds, s>>>(a);
   k_sb_gin_bwd<<<a.G, kSbThreads, 0, s>>>(a);

@@ -16,8 +16,8 @@ run() {  # name, limit, command...
 }
 echo "start $(date)" > "$OUT/status.txt"
 if [ "${SUITE:-1}" = "1" ]; then
-  run pytest_gpu 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread
-  tail -2 "$OUT/pytest_gpu.out"
+  run pytest_gpu 900 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread
+  tail -2 "$OUT/pytest_gpu.out"; grep -q " failed" "$OUT/pytest_gpu.out" && { grep -E "^(FAILED|ERROR)" "$OUT/pytest_gpu.out"; exit 1; }
 fi
 run smoke 200 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')"
 run bench 600 python bench.py --gpus 1 --steps 20 --warmup 5
