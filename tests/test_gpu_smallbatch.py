@@ -86,8 +86,9 @@ def test_fused_steps_train_like_the_general_path():
 def test_supports_and_refusals():
     from hgin.smallbatch import SmallBatchStep
     cfg = CONFIGS["cfg1"]
-    kw = cfg.model_kwargs({"link": 7, "path": 7, "node": 3})
-    assert SmallBatchStep.supports(HetroGIN(**dict(kw)))
-    assert not SmallBatchStep.supports(HetroGIN(**dict(kw, global_feats=True, bl_features=True)))
-    assert not SmallBatchStep.supports(HetroGIN(**dict(kw, mlp_bn=True)))
-    assert not SmallBatchStep.supports(HetroGIN(**dict(kw, node_embedding_size=128)))
+    # (HetroGIN mutates its input_channels dict, as the reference does: a fresh one per model)
+    kw = lambda **o: dict(cfg.model_kwargs({"link": 7, "path": 7, "node": 3}), **o)   # noqa: E731
+    assert SmallBatchStep.supports(HetroGIN(**kw()))
+    assert not SmallBatchStep.supports(HetroGIN(**kw(global_feats=True, bl_features=True)))
+    assert not SmallBatchStep.supports(HetroGIN(**kw(mlp_bn=True)))
+    assert not SmallBatchStep.supports(HetroGIN(**kw(node_embedding_size=128)))
