@@ -25,6 +25,9 @@ if [ "${REHEARSE:-1}" = "1" ]; then
   tail -c 1500 "$OUT/rehearse_cfg5.out"
   unset HGIN_DIST_BACKEND
 fi
+if [ "${PMC:-1}" = "1" ]; then
+  run gemm_pmc2 900 env OUT="$OUT/gemm_pmc2" bash tools/gpu_gemm_pmc2.sh
+fi
 if [ "${CPUFULL:-1}" = "1" ]; then
   run cpu_full_cfg2 1000 python bench.py --cpu-full cfg2
   cat "$OUT/cpu_full_cfg2.out"
