@@ -1674,6 +1674,291 @@ int launch_ws32(const WsArgs32& a, hipStream_t s, const char* what, int64_t* gri
   return check_launch(what);
 }
 
+// k_wsf_f32 — k_ws_f32 (K = N = 256; EPI 1, and EPI 4 without g_prev) with one wave per SIMD and the split of the
+// next block placed between this block's MFMAs (HGIN_WS_PIPE = 1):
+//   * 4 waves, each holding W rows 64 w .. 64 w + 63 as split B fragments: 384 registers, which one wave per SIMD can
+//     hold (the SIMD's 512-entry file: planes 0 and 1 in the 256 AGPRs, plane 2 in VGPRs; gfx950 MFMAs take A / B
+//     operands from AGPRs).  hipcc does not place operands that way by itself, so the MFMAs are inline asm with "a"
+//     constraints on those planes; the accumulator chains need no wait states between MFMAs, and the VALU that reads
+//     an accumulator after a block's last MFMA is behind explicit s_nops;
+//   * per block of 32 rows and k-step: three A-plane fragments (shared by the wave's two 32-column tiles), twelve
+//     v_mfma_f32_32x32x16_bf16 in k_ws_f32's product order;
+//   * the fp32 A slot is one 32 KB image in per-wave slices (wave w DMAs and splits rows 8 w .. 8 w + 7: it waits on
+//     its own vmcnt only, and refills its slice once its split has read it); the split of block i + 1 runs one row
+//     per k-step in the second half of block i's k-loop, between its MFMAs (an MFMA holds vector issue for 8 of its 32
+//     cycles: MI355X_MICROARCH.md), into the other of two 48 KB plane buffers — one barrier per block;
+//   * the epilogue works from the accumulators: lane (li, lh) owns columns 64 w + 32 c + li, rows (e & 3) + 8 (e >> 2)
+//     + 4 lh; each dword store writes two full 128-B row segments.  Its row image (accum / x_dst) is DMA'd per wave as
+//     the wave's 64 columns (8 KB; the 32-column halves of rows with bit 2 set swapped, so the two half-waves' reads
+//     fall in different banks) and refilled once read;
+//   * per output the products, their order and the epilogue arithmetic are k_ws_f32's: y / z / C / g_x_dst are
+//     bit-identical to it; EPI 4's eps-gradient partial sums the same terms in another order (one partial per
+//     workgroup, as before).
+// LDS: 32 KB A slot + 2 x 48 KB plane buffers + 32 KB row image = 160 KB.  Input DMAs and output stores are always
+// non-temporal: the launcher takes this form only where k_ws_f32 would choose both.
+// (each MFMA statement opens with s_nop 1: hipcc pads nothing around inline asm, and an operand it has just moved
+// into place with a VALU / v_accvgpr write needs 2 wait states before an MFMA reads it; tools/check_ws_asm.py checks
+// that no other instruction touches an accumulator between the MFMAs of its chain)
+using u32x4v = __attribute__((ext_vector_type(4))) unsigned int;
+__device__ __forceinline__ void mfma_b_agpr(f32x16& acc, const bf16x8& a, const u32x4v& b) {
+  asm volatile("s_nop 1\n\tv_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+v"(acc) : "v"(a), "a"(b));
+}
+__device__ __forceinline__ void mfma_b_vgpr(f32x16& acc, const bf16x8& a, const u32x4v& b) {
+  asm volatile("s_nop 1\n\tv_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+v"(acc) : "v"(a), "v"(b));
+}
+__device__ __forceinline__ void mfma_b_agpr_first(f32x16& acc, const bf16x8& a, const u32x4v& b) {
+  asm volatile("s_nop 1\n\tv_mfma_f32_32x32x16_bf16 %0, %1, %2, 0" : "=&v"(acc) : "v"(a), "a"(b));
+}
+
+template <int EPI, bool kR1, bool kZ>
+__global__ __launch_bounds__(256, 1) void k_wsf_f32(WsArgs32 g) {
+  constexpr int K = 256, KS = K / 16, BM = 32;
+  constexpr int A_BYTES = BM * K * 4, PROW = K * 2, PL = BM * PROW, SW = 31;
+  constexpr int P_OFF = A_BYTES, PBUF = 3 * PL, R1_OFF = P_OFF + 2 * PBUF;
+  constexpr int RA = 8, RR = kR1 ? 8 : 0;                 // DMA pieces per wave per block
+  constexpr int S = 32 * (kZ ? 2 : 1);                     // dword stores per lane per block
+  constexpr int WAIT_A = 8 + S < 63 ? 8 + S : 63;          // split waits on A(i + 1): r1(i) and stores(i - 1) after it
+  constexpr int WAIT_R = S + RA < 63 ? S + RA : 63;        // epilogue waits on r1(i): stores(i - 1), A(i + 2) after it
+  constexpr int WAIT_S = S < 63 ? S : 63;
+  static_assert(EPI == 1 || kR1, "EPI 4 reads x_dst");
+  extern __shared__ __attribute__((aligned(16))) char wsf_smem[];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // uniform: LDS / DMA bases in SGPRs
+  const int li = lane & 31;
+  const int lh = lane >> 5;
+  const int64_t M = g.M;
+  const int64_t nblk = (M + BM - 1) / BM;
+  const int64_t G = gridDim.x;
+  if ((int64_t)blockIdx.x >= nblk) return;
+  const int64_t my = (nblk - 1 - blockIdx.x) / G + 1;
+
+  // W rows 64 w + 32 c + li, k = 16 t + 8 lh .. + 7, as three bf16 planes (k_ws_f32's fragment layout):
+  // planes 0 / 1 used only through "a" operands (AGPRs), plane 2 through "v" operands
+  u32x4v w01[2][KS][2], w2[2][KS];
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {
+    const float* wr = g.w + (int64_t)(wave * 64 + c * 32 + li) * K + lh * 8;
+#pragma unroll
+    for (int t = 0; t < KS; ++t) {
+      const float4 v0 = *reinterpret_cast<const float4*>(wr + t * 16);
+      const float4 v1 = *reinterpret_cast<const float4*>(wr + t * 16 + 4);
+      uint2 o0[3], o1[3];
+      split4(v0, o0);
+      split4(v1, o1);
+      w01[c][t][0] = u32x4v{o0[0].x, o0[0].y, o1[0].x, o1[0].y};
+      w01[c][t][1] = u32x4v{o0[1].x, o0[1].y, o1[1].x, o1[1].y};
+      w2[c][t] = u32x4v{o0[2].x, o0[2].y, o1[2].x, o1[2].y};
+    }
+  }
+  float bcol[2] = {0.0f, 0.0f};
+  if constexpr (EPI == 1) {
+    bcol[0] = g.bias[wave * 64 + li];
+    bcol[1] = g.bias[wave * 64 + 32 + li];
+  }
+  const float a_slope = EPI == 1 ? __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(g.prelu[0]))) : 0.0f;
+  const float sc_self = EPI == 4 ? __fadd_rn(1.0f, __int_as_float(__builtin_amdgcn_readfirstlane(
+                                                        __float_as_int(g.eps[0])))) : 0.0f;
+  float ep = 0.0f;
+  wait_vm<0>();                          // the prologue's loads (W, bias) are done before the counted DMA ring starts
+  asm volatile("s_nop 4" ::: "memory");  // (the AGPR writes of the W planes settle before the first MFMA reads them)
+
+  auto tid_o = [&]() {
+    int t;
+    asm volatile("v_mov_b32 %0, %1" : "=v"(t) : "v"(tid));
+    return t;
+  };
+  auto rows_of = [&](int64_t i, int64_t& r0, int& rmax) {
+    r0 = ((int64_t)blockIdx.x + i * G) * BM;
+    rmax = (int)(M - 1 - r0 < BM ? M - 1 - r0 : BM - 1);
+  };
+  auto issue_a = [&](int64_t i) {   // rows 8 w .. 8 w + 7 of block i into this wave's slice
+    int64_t r0;
+    int rmax;
+    rows_of(i, r0, rmax);
+    const int ln = tid_o() & 63;
+#pragma unroll
+    for (int j = 0; j < RA; ++j) {
+      const int row = 8 * wave + j;
+      const int r = row < rmax ? row : rmax;   // (rows past M are zeroed at the split)
+      glds16_asm<true>(g.a + (r0 + r) * g.lda + ln * 4, wsf_smem + row * 1024);
+    }
+  };
+  auto issue_r1 = [&](int64_t i) {  // this wave's 64 columns of block i's row image: piece j = rows 4j .. 4j + 3
+    int64_t r0;
+    int rmax;
+    rows_of(i, r0, rmax);
+    const int ln = tid_o() & 63;
+#pragma unroll
+    for (int j = 0; j < RR; ++j) {
+      const int row = 4 * j + (ln >> 4);
+      const int r = row < rmax ? row : rmax;
+      const int col = ((ln & 15) * 4) ^ (((row >> 2) & 1) << 5);
+      glds16_asm<true>(g.r1 + (r0 + r) * g.ldr1 + wave * 64 + col, wsf_smem + R1_OFF + wave * 8192 + j * 1024);
+    }
+  };
+  // one row of block j's slice (row 8 w + q) -> its three plane rows in plane buffer j & 1
+  auto split_row = [&](int64_t j, int q) {
+    char* pl = wsf_smem + P_OFF + (int)(j & 1) * PBUF;
+    const int64_t r0 = ((int64_t)blockIdx.x + j * G) * BM;
+    const int ln = tid_o() & 63;
+    const int r = 8 * wave + q, k = ln * 4;
+    const float4 v = *reinterpret_cast<const float4*>(wsf_smem + r * 1024 + ln * 16);
+    const float4 x = r0 + r < M ? v : make_float4(0.f, 0.f, 0.f, 0.f);
+    uint2 o[3];
+    split4(x, o);
+    const int off = r * PROW + 16 * ((k >> 3) ^ (r & SW)) + 8 * ((k >> 2) & 1);
+#pragma unroll
+    for (int p = 0; p < 3; ++p) *reinterpret_cast<uint2*>(pl + p * PL + off) = o[p];
+  };
+
+  // block i's products (k_ws_f32's fragments and product order), one row of block i + 1's split per k-step in the
+  // second half (its VALU issues in the MFMAs' shadow)
+  auto mfma = [&](int64_t i, f32x16 (&acc)[2]) {
+    const int fl = tid_o() & 63;
+    const int fsw16 = (((fl >> 5) ^ (fl & 31)) & SW) << 4;   // chunk 2t + lh of row li sits at (2t + lh) ^ (li & SW)
+    const char* planes = wsf_smem + P_OFF + (int)(i & 1) * PBUF + (fl & 31) * PROW;
+    auto ld = [&](int t, int p) {
+      return __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(planes + p * PL + ((32 * t) ^ fsw16)));
+    };
+    const bool nxt = i + 1 < my;
+    bf16x8 a0 = ld(0, 0), a1 = ld(0, 1), a2 = ld(0, 2);
+#pragma unroll
+    for (int t = 0; t < KS; ++t) {
+      if (t >= KS / 2 && nxt) {
+        if (t == KS / 2) {   // block i + 1 landed in this wave's slice (counted)
+          if (i == 0) wait_vm<RR>(); else wait_vm<WAIT_A>();
+        }
+        split_row(i + 1, t - KS / 2);
+      }
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        if (t == 0) mfma_b_agpr_first(acc[c], a2, w01[c][t][0]); else mfma_b_agpr(acc[c], a2, w01[c][t][0]);
+        mfma_b_agpr(acc[c], a1, w01[c][t][1]);
+        mfma_b_vgpr(acc[c], a0, w2[c][t]);
+        mfma_b_agpr(acc[c], a1, w01[c][t][0]);
+        mfma_b_agpr(acc[c], a0, w01[c][t][1]);
+        mfma_b_agpr(acc[c], a0, w01[c][t][0]);
+      }
+      if (t + 1 < KS) {
+        a0 = ld(t + 1, 0);
+        a1 = ld(t + 1, 1);
+        a2 = ld(t + 1, 2);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    // the last MFMAs' results reach the VALU that reads them after 18 wait states (32x32: 16 passes + 2)
+    asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 3" : "+v"(acc[0]), "+v"(acc[1]));
+    if (nxt) {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the slice is read: refill it with block i + 2
+      if (i + 2 < my) issue_a(i + 2);
+    }
+  };
+
+  // block i's outputs from the accumulators (epilogue<1> / epilogue<4>'s arithmetic per element)
+  auto epilogue = [&](int64_t i, const f32x16 (&acc)[2], auto checked) {
+    const int64_t r0 = ((int64_t)blockIdx.x + i * G) * BM;
+    const float* img = reinterpret_cast<const float*>(wsf_smem + R1_OFF + wave * 8192) + 4 * lh * 64 + li;
+    // the leading dimensions pass through an opaque move per block, so the compiler cannot hoist the 64 per-element
+    // addresses out of the block loop (they would not fit beside the W slice)
+    int64_t ldy = g.ldy, ldz = g.ldz;
+    asm volatile("" : "+s"(ldy), "+s"(ldz));
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      const int col = wave * 64 + 32 * c + li;
+      // scalar row bases + a 32-bit lane byte offset (global_store_dword's SGPR-base form: no per-element 64-bit
+      // address registers)
+      const uint32_t voy = (uint32_t)(4 * lh * (int)ldy + col) * 4u;
+      const uint32_t voz = kZ ? (uint32_t)(4 * lh * (int)ldz + col) * 4u : 0u;
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int rb = (e & 3) + 8 * (e >> 2);   // the row less 4 lh (uniform); its bit 2 is lh
+        const float in1 = kR1 ? img[rb * 64 + 32 * (c ^ lh)] : 0.0f;
+        float o = acc[c][e], zz;
+        if constexpr (EPI == 1) {
+          zz = __fadd_rn(o, bcol[c]);
+          const float y = zz > 0.0f ? zz : __fmul_rn(a_slope, zz);
+          o = kR1 ? __fadd_rn(in1, y) : y;
+        } else {
+          zz = __fmul_rn(sc_self, o);
+        }
+        if (!decltype(checked)::value || r0 + rb + 4 * lh < M) {   // (only a grid's last block is partial)
+          if constexpr (EPI == 4) ep = __fadd_rn(ep, __fmul_rn(o, in1));
+          char* yb = reinterpret_cast<char*>(g.y + (r0 + rb) * ldy);
+          __builtin_nontemporal_store(o, reinterpret_cast<float*>(yb + voy));
+          if constexpr (kZ) {
+            char* zb = reinterpret_cast<char*>(g.z + (r0 + rb) * ldz);
+            __builtin_nontemporal_store(zz, reinterpret_cast<float*>(zb + voz));
+          }
+        }
+        if ((e & 3) == 3) __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+  };
+
+  // prologue: block 0 split whole, block 1 and the row image of block 0 in flight
+  issue_a(0);
+  wait_vm<0>();
+#pragma unroll
+  for (int q = 0; q < 8; ++q) split_row(0, q);
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  if (my > 1) issue_a(1);
+  if constexpr (kR1) issue_r1(0);
+  // Vector-memory order per wave in iteration i: A(i + 2) after the split's reads (end of the k-loop), r1(i + 1) after
+  // the epilogue's image reads, then the epilogue's S stores.  The split of block i + 1 waits on A(i + 1) (issued
+  // at the end of iteration i - 1's k-loop: r1(i) and stores(i - 1) follow it); the epilogue waits on r1(i) (stores
+  // (i - 1) and A(i + 2) follow it).  Counts above 63 are capped (waiting slightly more).
+  for (int64_t i = 0; i < my; ++i) {
+    __builtin_amdgcn_s_barrier();   // planes of block i written by every wave; those of block i - 1 read by every wave
+    asm volatile("" ::: "memory");
+    f32x16 acc[2];
+    mfma(i, acc);
+    if constexpr (kR1) {
+      if (i >= 1 && i + 2 < my) wait_vm<WAIT_R>();
+      else if (i >= 1 && i + 1 < my) wait_vm<WAIT_S>();
+      else wait_vm<0>();
+    }
+    const int64_t r0 = ((int64_t)blockIdx.x + i * G) * BM;
+    if (r0 + BM <= M) epilogue(i, acc, std::false_type{}); else epilogue(i, acc, std::true_type{});
+    if constexpr (kR1) {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the image is read
+      if (i + 1 < my) issue_r1(i + 1);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // this wave's plane writes are done
+  }
+  if constexpr (EPI == 4) {
+    wait_vm<0>();
+    tile_partial(reinterpret_cast<float*>(wsf_smem), ep, g.part, blockIdx.x);
+  }
+}
+
+bool wsf_enabled() {   // HGIN_WS_PIPE = 1 / 0: the pipelined fp32 forward / dX form (default off until measured)
+  static const bool on = [] {
+    const char* v = getenv("HGIN_WS_PIPE");
+    return v && v[0] == '1';
+  }();
+  return on;
+}
+
+template <int EPI, bool kR1, bool kZ>
+int launch_wsf(const WsArgs32& a, hipStream_t s, const char* what, int64_t* grid_out = nullptr) {
+  constexpr int lds = 32768 + 6 * 16384 + (kR1 ? 32768 : 0);
+  static_assert(lds <= 160 * 1024, "LDS");
+  auto kern = k_wsf_f32<EPI, kR1, kZ>;
+  static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                                                     hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+  if (attr != hipSuccess) {
+    set_error("%s: hipFuncSetAttribute failed: %s", what, hipGetErrorString(attr));
+    return (int)attr;
+  }
+  const int64_t nblk = ceil_div(a.M, (int64_t)32);
+  const int64_t grid = nblk < ws_grid() ? nblk : ws_grid();
+  HGIN_TRACE("k_wsf_f32<256,256,EPI%d>", EPI);
+  kern<<<(unsigned)grid, 256, lds, s>>>(a);
+  if (grid_out) *grid_out = grid;
+  return check_launch(what);
+}
+
 // Returns -1 when the fp32 weight-stationary form does not apply (the caller launches the tiled kernel): split
 // mode, one A source (no eps-scaled second half), K = N = 256, 16-B aligned rows, packed W / z / y / accum.
 int try_ws_f32(const float* a1, int64_t lda1, int64_t k1, const float* a2_eps, const float* w, const float* bias,
@@ -1687,6 +1972,12 @@ int try_ws_f32(const float* a1, int64_t lda1, int64_t k1, const float* a2_eps, c
     return -1;
   WsArgs32 g{a1, lda1, w, bias, prelu, accum, N, nullptr, 0, z, N, y, N, nullptr, nullptr, M, gemm_nt_io(M, N, 4),
              ws_nt_in()};
+  if (wsf_enabled() && g.nt_io && g.nt_in) {
+    if (accum && z) return launch_wsf<1, true, true>(g, s, what);
+    if (accum) return launch_wsf<1, true, false>(g, s, what);
+    if (z) return launch_wsf<1, false, true>(g, s, what);
+    return launch_wsf<1, false, false>(g, s, what);
+  }
   if (accum && z) return launch_ws32<256, 256, 1, true, true, false>(g, s, what);
   if (accum) return launch_ws32<256, 256, 1, true, false, false>(g, s, what);
   if (z) return launch_ws32<256, 256, 1, false, true, false>(g, s, what);
@@ -1710,6 +2001,10 @@ int try_ws_f32_comb(const float* a, int64_t lda, const float* b, int64_t ldb, fl
     return -1;
   WsArgs32 g{a, lda, b, nullptr, nullptr, xd, ce.ldxd, gp, ce.ldgp, gd, ce.ldgd, c, ldc, ce.eps, ce.part, M,
              gemm_nt_io(M, N, 4), ws_nt_in()};
+  if (wsf_enabled() && !gp && g.nt_io && g.nt_in) {
+    if (gd) return launch_wsf<4, true, true>(g, s, what, grid_out);
+    return launch_wsf<4, true, false>(g, s, what, grid_out);
+  }
   if (gd && gp) return launch_ws32<256, 256, 4, true, true, true>(g, s, what, grid_out);
   if (gd) return launch_ws32<256, 256, 4, true, true, false>(g, s, what, grid_out);
   return launch_ws32<256, 256, 4, true, false, false>(g, s, what, grid_out);

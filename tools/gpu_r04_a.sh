@@ -25,7 +25,8 @@ tail -c 600 "$OUT/bench.out"
 HGIN_DW512=tiled run bench_dw512_tiled 300 python bench.py --no-cpu-baseline --no-extras --no-probe --steps 10 --warmup 3
 run bench_dw512_wsd 300 python bench.py --no-cpu-baseline --no-extras --no-probe --steps 10 --warmup 3
 HGIN_WSD_PIPE=1 run bench_wsd_pipe 300 python bench.py --no-cpu-baseline --no-extras --no-probe --steps 10 --warmup 3
-grep -o '"ms_per_step": [0-9.]*' "$OUT/bench_dw512_tiled.out" "$OUT/bench_dw512_wsd.out" "$OUT/bench_wsd_pipe.out"
+HGIN_WSD_PIPE=1 HGIN_WS_PIPE=1 run bench_both_pipe 300 python bench.py --no-cpu-baseline --no-extras --no-probe --steps 10 --warmup 3
+grep -o '"ms_per_step": [0-9.]*' "$OUT"/bench_dw512_*.out "$OUT"/bench_*pipe.out
 run prof_batches 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_batches" -o run -- \
   python3 tools/batches_prof.py --steps 100
 if [ "${GEMMAB:-1}" = "1" ]; then
@@ -33,6 +34,7 @@ if [ "${GEMMAB:-1}" = "1" ]; then
   run gemm_ab_t256 300 env HGIN_NT_T256=1 python tools/gemm_ab.py --only fwd512,fwd512acc
   run gemm_ab_dwtiled 300 env HGIN_DW512=tiled python tools/gemm_ab.py --only dw512
   run gemm_ab_wsdpipe 300 env HGIN_WSD_PIPE=1 python tools/gemm_ab.py --only dw512,dw256pro
+  run gemm_ab_wspipe 300 env HGIN_WS_PIPE=1 python tools/gemm_ab.py --only fwd256,dx256
   cat "$OUT"/gemm_ab_*.out
 fi
 if [ "${REHEARSE:-1}" = "1" ]; then
