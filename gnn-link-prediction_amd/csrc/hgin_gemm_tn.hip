@@ -1495,10 +1495,12 @@ __global__ __launch_bounds__(512, 1) void k_wsp_f32(const float* __restrict__ A,
     }
 }
 
-bool wsp_enabled() {   // HGIN_WSD_PIPE = 1 / 0: the pipelined form at N = K = 256 (default off until measured)
+// HGIN_WSD_PIPE = 0 keeps k_wsd_f32 at N = K = 256 (the pipelined form: cfg3 187.8 -> 185.9 ms, the K = 512 dW at
+// M = 6M 10.85 -> 10.05 ms, the PReLU-fused K = 256 dW 5.92 -> 5.65 ms: profiles/r04/gpu_a/)
+bool wsp_enabled() {
   static const bool on = [] {
     const char* v = getenv("HGIN_WSD_PIPE");
-    return v && v[0] == '1';
+    return !(v && v[0] == '0');
   }();
   return on;
 }

@@ -1,26 +1,34 @@
 // F1 — the reference's real training loop (dataset.py:26, :239-244; train.py:25-44): shuffled batches of a few small
 // network graphs.  A batch of 8 RouteNet-sized graphs is a few thousand vertices, so the general path (one launch per
 // relation, layer and GEMM family, ~100 per step even as one hipGraph replay) is bound by kernel boundaries, not work.
-// Here the whole train step of a HetroGIN over a padded batch (hgin/store.py PaddedBatch) is four launches:
+// Here the whole train step of a HetroGIN over a padded batch (hgin/store.py PaddedBatch) is 5 L + 1 launches (one
+// fewer: the first layer needs no input gradient), every one spread over all rows of the batch (the graphs are
+// disjoint, but a workgroup per graph leaves all but a handful of CUs idle and serialises each graph's dependent
+// gathers — measured 1.15 ms per batch against the general path's 0.71):
 //
-//   k_sb_gin_fwd   one workgroup per graph of the batch (graphs are disjoint: no cross-workgroup dependency): every
-//                  layer, every relation — the CSR aggregate in edge order, the (1 + eps) x_dst self term (concat in the
-//                  first layer, add above it: models.py:210-215), Linear + PReLU (models.py:236-239), the per-
-//                  destination relation sum (HeteroConv, models.py:286-298) — with workgroup barriers between phases;
-//   k_sb_readout   16-row tiles of path rows: the readout MLP (models.py:300-330, :362-376: hidden Linear + the ONE
-//                  shared PReLU, Linear head), the MAPE numerator sum_rows |(out - y) / y| (train.py:12-13) and the
-//                  readout backward seeded with d sum|u| / d out = sgn(u) / y, per-tile weight-gradient partials;
-//   k_sb_gin_bwd   one workgroup per graph: the GIN backward, layers in reverse (PReLU, bias, weight, eps gradients as
-//                  per-graph partials; the input gradients through the self term and the CSC aggregate);
-//   k_sb_final     every parameter gradient = its partials summed in a fixed order, times d sqrt(loss) / d sum|u| =
-//                  100 / (2 m sqrt(loss_value)) (train.py:40-43; the seed above is linear), written into one flat
-//                  gradient buffer whose views are the parameters' .grad; loss_value = 100 sum|u| / m.
+//   k_sb_agg    (per layer)   thread per (relation, destination row, column): the CSR aggregate in edge order and the
+//                             (1 + eps) x_dst self term (concat in the first layer, add above it: models.py:210-215);
+//   k_sb_mlp    (per layer)   thread per (node type, row, output column): Linear + PReLU of every relation into the
+//                             type (models.py:236-239) and their sum in relation order (HeteroConv, models.py:286-298);
+//   k_sb_readout              16-row tiles of path rows: the readout MLP (models.py:300-330, :362-376: hidden Linear
+//                             + the ONE shared PReLU, Linear head), the MAPE numerator sum_rows |(out - y) / y|
+//                             (train.py:12-13) and the readout backward seeded with d sum|u| / d out = sgn(u) / y,
+//                             per-tile weight-gradient partials;
+//   k_sb_bwd_z  (per layer)   thread per (relation, destination row): g_z = PReLU'(z) g_y and g_comb = g_z W;
+//   k_sb_bwd_w  (per layer)   workgroup per (row chunk, relation): the chunk's partial W / bias / slope / eps gradients;
+//   k_sb_bwd_in (layers > 0)  thread per (node type, row, column): the layer input's gradient — every relation's self
+//                             term and CSC aggregate of g_comb, in relation order;
+//   k_sb_final                every parameter gradient = its partials summed in a fixed order, times d sqrt(loss) /
+//                             d sum|u| = 100 / (2 m sqrt(loss_value)) (train.py:40-43; the seed above is linear),
+//                             written into one flat gradient buffer whose views are the parameters' .grad;
+//                             loss_value = 100 sum|u| / m.
 //
-// The optimizer (torch Adam, fused) follows in the same hipGraph.  Every sum runs in a fixed order (deterministic).
-// The aggregates are the GIN path's (sequential edge-order fp32 sums: bit-identical); the GEMM-shaped sums and the
-// deferred loss scaling re-associate, so the step agrees with the general path within fp32 tolerances
-// (tests/test_gpu_smallbatch.py).  Limits (checked by the host, hgin/smallbatch.py): H <= 64, every GEMM K <= 128,
-// readout widths <= 256, at most 3 hidden readout layers and 4 GIN layers, fp32.
+// The optimizer (torch Adam, fused) follows in the same hipGraph.  Every sum runs in a fixed order (deterministic;
+// the row chunks of the partials are fixed fractions of the batch's rows).  The aggregates are the GIN path's
+// (sequential edge-order fp32 sums: bit-identical); the GEMM-shaped sums and the deferred loss scaling re-associate,
+// so the step agrees with the general path within fp32 tolerances (tests/test_gpu_smallbatch.py).  Limits (checked
+// by the host, hgin/smallbatch.py): H <= 64, every GEMM K <= 128, readout widths <= 256, at most 3 hidden readout
+// layers and 4 GIN layers, fp32.
 #include "hgin_common.h"
 
 #include <cstddef>
@@ -84,11 +92,13 @@ struct SbArgs {
   float* gA;                // [3] blocks of cap_t x H  (gradient of the current layer's outputs)
   float* gB;                // same (gradient of its inputs)
   int64_t g_off[3];
-  float* gz;                // [3] blocks of cap_t x H     (per destination type: graphs are row-disjoint)
-  float* gc;                // [3] blocks of cap_t x Kmax
-  int64_t gz_off[3], gc_off[3];
-  int kmax;                 // row stride of the gc blocks (relations into one type may differ in K)
-  float* part_gin;          // [G][p_gin]
+  float* gz;                // [4] blocks of cap_dst x H     (per relation)
+  float* gc;                // [4] blocks of cap_dst x Kmax
+  int64_t gz_off[kRel], gc_off[kRel];
+  int kmax;                 // row stride of the gc blocks (relations differ in K)
+  int cap[3];               // row capacity per node type (grid sizes)
+  float* part_gin;          // [n_parts][p_gin]
+  int n_parts;              // row chunks of the weight-gradient partials
   float* part_ro;           // [n_tiles][p_ro]
   float* loss_part;         // [n_tiles]
   int n_tiles;
@@ -116,70 +126,65 @@ __device__ float block_sum(float v, float* red) {
   return s;
 }
 
-__global__ __launch_bounds__(kSbThreads) void k_sb_gin_fwd(SbArgs a) {
-  const int j = blockIdx.x;
-  const int tid = threadIdx.x;
-  const int H = a.H;
-  int n0[3], n1[3];
-#pragma unroll
-  for (int t = 0; t < 3; ++t) {
-    n0[t] = a.goff[t * (a.G + 1) + j];
-    n1[t] = a.goff[t * (a.G + 1) + j + 1];
-  }
-  for (int l = 0; l < a.L; ++l) {
-    for (int r = 0; r < kRel; ++r) {
-      const int s = kRelSrc[r], d = kRelDst[r];
-      const int K = kdim(a, l, r);
-      const SbConv& cv = a.conv[l][r];
-      const float sc = __fadd_rn(1.0f, cv.eps[0]);
-      const int rows = n1[d] - n0[d];
-      float* comb = a.comb + a.comb_off[l][r];
-      const int32_t* rp = a.rowptr[r];
-      const int32_t* cl = a.col[r];
-      // comb = [aggregate | (1 + eps) x_dst] (concat, first layer) or aggregate + (1 + eps) x_dst (add)
-      for (int idx = tid; idx < rows * K; idx += kSbThreads) {
-        const int i = n0[d] + idx / K;
-        const int k = idx % K;
-        float v = 0.0f;
-        if (l == 0) {
-          const int fs = a.fdim[s];
-          if (k < fs) {
-            const float* xs = a.x[s];
-            const int64_t ld = a.ldx[s];
-            const int c = a.cols[s][k];
-            for (int e = rp[i]; e < rp[i + 1]; ++e) v = __fadd_rn(v, xs[(int64_t)cl[e] * ld + c]);
-          } else {
-            v = __fmul_rn(sc, a.x[d][(int64_t)i * a.ldx[d] + a.cols[d][k - fs]]);
-          }
-        } else {
-          const float* xs = a.act + a.act_off[l - 1][s];
-          for (int e = rp[i]; e < rp[i + 1]; ++e) v = __fadd_rn(v, xs[(int64_t)cl[e] * H + k]);
-          v = __fadd_rn(v, __fmul_rn(sc, a.act[a.act_off[l - 1][d] + (int64_t)i * H + k]));
-        }
-        comb[(int64_t)i * K + k] = v;
-      }
-      __syncthreads();
-      // z = comb W^T + b; y = prelu(z); the layer output of d = the sum over its relations (first one stores)
-      const bool first = (r == 0 || r == 1 || r == 2);   // r = 3 (node -> link) adds onto path -> link's output
-      float* zb = a.zb + a.zb_off[l][r];
-      float* act = a.act + a.act_off[l][d];
-      const float slope = cv.slope[0];
-      for (int idx = tid; idx < rows * H; idx += kSbThreads) {
-        const int i = n0[d] + idx / H;
-        const int h = idx % H;
-        const float* cr = comb + (int64_t)i * K;
-        const float* wr = cv.w + (int64_t)h * K;
-        float z = 0.0f;
-        for (int k = 0; k < K; ++k) z = fmaf(cr[k], wr[k], z);
-        z = __fadd_rn(z, cv.b[h]);
-        zb[(int64_t)i * H + h] = z;
-        const float yv = z > 0.0f ? z : __fmul_rn(slope, z);
-        float* o = act + (int64_t)i * H + h;
-        *o = first ? yv : __fadd_rn(*o, yv);
-      }
-      __syncthreads();
+__device__ __forceinline__ int nrows(const SbArgs& a, int t) { return a.goff[t * (a.G + 1) + a.G]; }
+
+// comb_r = [aggregate | (1 + eps) x_dst] (concat, first layer) or aggregate + (1 + eps) x_dst (add); grid.y = relation
+__global__ __launch_bounds__(kSbThreads) void k_sb_agg(SbArgs a, int l) {
+  const int r = blockIdx.y;
+  const int s = kRelSrc[r], d = kRelDst[r];
+  const int K = kdim(a, l, r);
+  const int64_t idx = (int64_t)blockIdx.x * kSbThreads + threadIdx.x;
+  if (idx >= (int64_t)nrows(a, d) * K) return;
+  const int i = (int)(idx / K), k = (int)(idx % K);
+  const SbConv& cv = a.conv[l][r];
+  const float sc = __fadd_rn(1.0f, cv.eps[0]);
+  const int32_t* rp = a.rowptr[r];
+  const int32_t* cl = a.col[r];
+  float v = 0.0f;
+  if (l == 0) {
+    const int fs = a.fdim[s];
+    if (k < fs) {
+      const float* xs = a.x[s];
+      const int64_t ld = a.ldx[s];
+      const int c = a.cols[s][k];
+      for (int e = rp[i]; e < rp[i + 1]; ++e) v = __fadd_rn(v, xs[(int64_t)cl[e] * ld + c]);
+    } else {
+      v = __fmul_rn(sc, a.x[d][(int64_t)i * a.ldx[d] + a.cols[d][k - fs]]);
     }
+  } else {
+    const int H = a.H;
+    const float* xs = a.act + a.act_off[l - 1][s];
+    for (int e = rp[i]; e < rp[i + 1]; ++e) v = __fadd_rn(v, xs[(int64_t)cl[e] * H + k]);
+    v = __fadd_rn(v, __fmul_rn(sc, a.act[a.act_off[l - 1][d] + (int64_t)i * H + k]));
   }
+  a.comb[a.comb_off[l][r] + (int64_t)i * K + k] = v;
+}
+
+// the layer output of type t, column h: the sum over the relations into t (relation order) of prelu(comb W^T + b);
+// z kept per relation for the backward.  grid.y = node type
+__global__ __launch_bounds__(kSbThreads) void k_sb_mlp(SbArgs a, int l) {
+  const int t = blockIdx.y;
+  const int H = a.H;
+  const int64_t idx = (int64_t)blockIdx.x * kSbThreads + threadIdx.x;
+  if (idx >= (int64_t)nrows(a, t) * H) return;
+  const int i = (int)(idx / H), h = (int)(idx % H);
+  float y = 0.0f;
+  bool first = true;
+  for (int r = 0; r < kRel; ++r) {
+    if (kRelDst[r] != t) continue;
+    const int K = kdim(a, l, r);
+    const SbConv& cv = a.conv[l][r];
+    const float* cr = a.comb + a.comb_off[l][r] + (int64_t)i * K;
+    const float* wr = cv.w + (int64_t)h * K;
+    float z = 0.0f;
+    for (int k = 0; k < K; ++k) z = fmaf(cr[k], wr[k], z);
+    z = __fadd_rn(z, cv.b[h]);
+    a.zb[a.zb_off[l][r] + (int64_t)i * H + h] = z;
+    const float yv = z > 0.0f ? z : __fmul_rn(cv.slope[0], z);
+    y = first ? yv : __fadd_rn(y, yv);
+    first = false;
+  }
+  a.act[a.act_off[l][t] + (int64_t)i * H + h] = y;
 }
 
 // One 16-row tile of path rows: readout forward, loss partial, readout backward (unscaled), weight-gradient partials.
@@ -323,119 +328,106 @@ __global__ __launch_bounds__(kSbThreads) void k_sb_readout(SbArgs a) {
   }
 }
 
-__global__ __launch_bounds__(kSbThreads) void k_sb_gin_bwd(SbArgs a) {
+// layer l's output gradient of type d (gcur: written by the readout for path rows, by k_sb_bwd_in of layer l + 1
+// otherwise); the last layer's link / node outputs feed nothing (models.py:362-376 reads path only)
+__device__ __forceinline__ float gout(const SbArgs& a, const float* gcur, int l, int d, int64_t q) {
+  return (l == a.L - 1 && d != 0) ? 0.0f : gcur[a.g_off[d] + q];
+}
+
+// g_z = PReLU'(z) g_y and g_comb = g_z W for one destination row of one relation (grid.y = relation)
+__global__ __launch_bounds__(kSbThreads) void k_sb_bwd_z(SbArgs a, int l, const float* gcur) {
+  const int r = blockIdx.y;
+  const int d = kRelDst[r];
+  const int H = a.H, K = kdim(a, l, r);
+  const int i = blockIdx.x * kSbThreads + threadIdx.x;
+  if (i >= nrows(a, d)) return;
+  const SbConv& cv = a.conv[l][r];
+  const float slope = cv.slope[0];
+  const float* zb = a.zb + a.zb_off[l][r] + (int64_t)i * H;
+  float* gz = a.gz + a.gz_off[r] + (int64_t)i * H;
+  for (int h = 0; h < H; ++h) {
+    const float z = zb[h], g = gout(a, gcur, l, d, (int64_t)i * H + h);
+    gz[h] = z > 0.0f ? g : __fmul_rn(slope, g);
+  }
+  float* gc = a.gc + a.gc_off[r] + (int64_t)i * a.kmax;   // (this thread's own g_z row, read back)
+  for (int k = 0; k < K; ++k) {
+    float v = 0.0f;
+    for (int h = 0; h < H; ++h) v = fmaf(gz[h], cv.w[(int64_t)h * K + k], v);
+    gc[k] = v;
+  }
+}
+
+// one row chunk's partial W / bias / slope / eps gradients of one relation (grid = n_parts x relations); rows of
+// chunk p: [p c, (p + 1) c), c = ceil(rows / n_parts)
+__global__ __launch_bounds__(kSbThreads) void k_sb_bwd_w(SbArgs a, int l, const float* gcur) {
   __shared__ float red[kSbThreads];
-  const int j = blockIdx.x;
+  const int p = blockIdx.x, r = blockIdx.y;
+  const int s = kRelSrc[r], d = kRelDst[r];
+  const int H = a.H, K = kdim(a, l, r);
   const int tid = threadIdx.x;
+  const int rows = nrows(a, d);
+  const int ch = (rows + a.n_parts - 1) / a.n_parts;
+  const int i0 = p * ch < rows ? p * ch : rows, i1 = (p + 1) * ch < rows ? (p + 1) * ch : rows;
+  const SbConv& cv = a.conv[l][r];
+  float* part = a.part_gin + (int64_t)p * a.p_gin + cv.goff;
+  const float* gz = a.gz + a.gz_off[r];
+  const float* comb = a.comb + a.comb_off[l][r];
+  // g_W[h][k] = sum_i g_z[i][h] comb[i][k]; g_b[h] = sum_i g_z[i][h] (the chunk's rows in order)
+  for (int q = tid; q < H * (K + 1); q += kSbThreads) {
+    const int h = q / (K + 1), k = q % (K + 1);
+    float v = 0.0f;
+    for (int i = i0; i < i1; ++i) {
+      const float g = gz[(int64_t)i * H + h];
+      v = k < K ? fmaf(g, comb[(int64_t)i * K + k], v) : __fadd_rn(v, g);
+    }
+    part[k < K ? (int64_t)h * K + k : (int64_t)H * K + h] = v;
+  }
+  // the slope (sum over z <= 0 of g_y z) and eps (g_comb over the self columns times x_dst) partials
+  const float* zb = a.zb + a.zb_off[l][r];
+  const int fs = l == 0 ? a.fdim[s] : 0;
+  const float* gc = a.gc + a.gc_off[r];
+  float sp = 0.0f, epv = 0.0f;
+  for (int q = tid; q < (i1 - i0) * H; q += kSbThreads) {
+    const int64_t qq = (int64_t)i0 * H + q;
+    const float z = zb[qq];
+    if (z <= 0.0f) sp = fmaf(gout(a, gcur, l, d, qq), z, sp);
+  }
+  const int KS = K - fs;
+  for (int q = tid; q < (i1 - i0) * KS; q += kSbThreads) {
+    const int i = i0 + q / KS, k = fs + q % KS;
+    const float xv = l == 0 ? a.x[d][(int64_t)i * a.ldx[d] + a.cols[d][k - fs]]
+                            : a.act[a.act_off[l - 1][d] + (int64_t)i * H + k];
+    epv = fmaf(gc[(int64_t)i * a.kmax + k], xv, epv);
+  }
+  const float ssum = block_sum(sp, red);
+  const float esum = block_sum(epv, red);
+  if (tid == 0) {
+    part[(int64_t)H * K + H] = ssum;
+    part[(int64_t)H * K + H + 1] = esum;
+  }
+}
+
+// the gradient of layer l's input of type t (l > 0: layer l - 1's output): per relation in order, the self term
+// (1 + eps) g_comb where t is the destination (add mode: every column) and the CSC aggregate of g_comb where t is
+// the source (edge order).  grid.y = node type
+__global__ __launch_bounds__(kSbThreads) void k_sb_bwd_in(SbArgs a, int l, float* gnxt) {
+  const int t = blockIdx.y;
   const int H = a.H;
-  int n0[3], n1[3];
-#pragma unroll
-  for (int t = 0; t < 3; ++t) {
-    n0[t] = a.goff[t * (a.G + 1) + j];
-    n1[t] = a.goff[t * (a.G + 1) + j + 1];
-  }
-  float* part = a.part_gin + (int64_t)j * a.p_gin;
-  float* gcur = a.gA;
-  float* gnxt = a.gB;
-  // the last layer's link / node outputs feed nothing (models.py:362-376 reads path only): zero gradient
-  for (int t = 1; t < 3; ++t)
-    for (int idx = tid; idx < (n1[t] - n0[t]) * H; idx += kSbThreads) gcur[a.g_off[t] + (int64_t)n0[t] * H + idx] = 0.0f;
-  // padding-free: path rows of this graph were written by k_sb_readout (rows < m_valid)
-  __syncthreads();
-  for (int l = a.L - 1; l >= 0; --l) {
-    if (l > 0) {
-      for (int t = 0; t < 3; ++t)
-        for (int idx = tid; idx < (n1[t] - n0[t]) * H; idx += kSbThreads)
-          gnxt[a.g_off[t] + (int64_t)n0[t] * H + idx] = 0.0f;
+  const int64_t idx = (int64_t)blockIdx.x * kSbThreads + threadIdx.x;
+  if (idx >= (int64_t)nrows(a, t) * H) return;
+  const int u = (int)(idx / H), k = (int)(idx % H);
+  float v = 0.0f;
+  for (int r = 0; r < kRel; ++r) {
+    const float* gc = a.gc + a.gc_off[r];
+    if (kRelDst[r] == t)
+      v = __fadd_rn(v, __fmul_rn(__fadd_rn(1.0f, a.conv[l][r].eps[0]), gc[(int64_t)u * a.kmax + k]));
+    if (kRelSrc[r] == t) {
+      const int32_t* cp = a.cptr[r];
+      const int32_t* cd = a.cdst[r];
+      for (int e = cp[u]; e < cp[u + 1]; ++e) v = __fadd_rn(v, gc[(int64_t)cd[e] * a.kmax + k]);
     }
-    __syncthreads();
-    for (int r = 0; r < kRel; ++r) {
-      const int s = kRelSrc[r], d = kRelDst[r];
-      const int K = kdim(a, l, r);
-      const SbConv& cv = a.conv[l][r];
-      const int rows = n1[d] - n0[d];
-      const float slope = cv.slope[0];
-      const float* zb = a.zb + a.zb_off[l][r];
-      const float* comb = a.comb + a.comb_off[l][r];
-      const float* gy = gcur + a.g_off[d];
-      float* gz = a.gz + a.gz_off[d] + (int64_t)n0[d] * H;   // this graph's rows of d
-      float* gc = a.gc + a.gc_off[d] + (int64_t)n0[d] * a.kmax;   // rows of stride kmax: graph-disjoint
-      // g_z, the slope partial (sum over z <= 0 of g_y z)
-      float spart = 0.0f;
-      for (int idx = tid; idx < rows * H; idx += kSbThreads) {
-        const int64_t q = (int64_t)n0[d] * H + idx;
-        const float z = zb[q], g = gy[q];
-        if (z <= 0.0f) spart = fmaf(g, z, spart);
-        gz[idx] = z > 0.0f ? g : __fmul_rn(slope, g);
-      }
-      const float ssum = block_sum(spart, red);
-      if (tid == 0) part[cv.goff + (int64_t)H * K + H] = ssum;
-      // g_W[h][k] = sum_i g_z[i][h] comb[i][k] (row groups, then the groups in order); g_b[h] = sum_i g_z[i][h]
-      {
-        const int P = H * (K + 1);                 // K weight columns + the bias column
-        const int RG = P >= kSbThreads ? 1 : kSbThreads / P;
-        for (int base = 0; base < P; base += kSbThreads) {
-          const int pidx = base + (RG > 1 ? tid % P : tid);
-          const int rg = RG > 1 ? tid / P : 0;
-          float v = 0.0f;
-          const bool live = pidx < P && rg < RG;
-          if (live) {
-            const int h = pidx / (K + 1), k = pidx % (K + 1);
-            for (int i = rg; i < rows; i += RG) {
-              const float g = gz[i * H + h];
-              v = k < K ? fmaf(g, comb[((int64_t)n0[d] + i) * K + k], v) : __fadd_rn(v, g);
-            }
-          }
-          __syncthreads();
-          red[tid] = v;
-          __syncthreads();
-          if (rg == 0 && pidx < P) {
-            float t = red[tid];
-            for (int g2 = 1; g2 < RG; ++g2) t = __fadd_rn(t, red[g2 * P + tid]);
-            const int h = pidx / (K + 1), k = pidx % (K + 1);
-            part[cv.goff + (k < K ? (int64_t)h * K + k : (int64_t)H * K + h)] = t;
-          }
-          if (RG > 1) break;
-        }
-      }
-      // g_comb = g_z W: the self term's gradient (eps; x_dst above the first layer) and the aggregate's
-      const int fs = l == 0 ? a.fdim[s] : 0;   // first self column (concat) / 0 (add: every column)
-      const float sc = __fadd_rn(1.0f, cv.eps[0]);
-      float epart = 0.0f;
-      for (int idx = tid; idx < rows * K; idx += kSbThreads) {
-        const int i = idx / K, k = idx % K;
-        float gcv = 0.0f;
-        for (int h = 0; h < H; ++h) gcv = fmaf(gz[i * H + h], cv.w[(int64_t)h * K + k], gcv);
-        const int64_t row = (int64_t)n0[d] + i;
-        if (l == 0) {
-          if (k >= fs) epart = fmaf(gcv, a.x[d][row * a.ldx[d] + a.cols[d][k - fs]], epart);
-        } else {
-          epart = fmaf(gcv, a.act[a.act_off[l - 1][d] + row * H + k], epart);
-          float* gx = gnxt + a.g_off[d] + row * H + k;
-          *gx = __fadd_rn(*gx, __fmul_rn(sc, gcv));
-        }
-        gc[(int64_t)i * a.kmax + k] = gcv;
-      }
-      const float esum = block_sum(epart, red);   // (also the barrier before the CSC pass reads gc)
-      if (tid == 0) part[cv.goff + (int64_t)H * K + H + 1] = esum;
-      if (l > 0) {   // the aggregate's input gradient, by source rows (CSC of the relation), edge order
-        const int32_t* cp = a.cptr[r];
-        const int32_t* cd = a.cdst[r];
-        const int srows = n1[s] - n0[s];
-        for (int idx = tid; idx < srows * H; idx += kSbThreads) {
-          const int u = n0[s] + idx / H, k = idx % H;
-          float v = 0.0f;
-          for (int e = cp[u]; e < cp[u + 1]; ++e) v = __fadd_rn(v, gc[(int64_t)(cd[e] - n0[d]) * a.kmax + k]);
-          float* gx = gnxt + a.g_off[s] + (int64_t)u * H + k;
-          *gx = __fadd_rn(*gx, v);
-        }
-      }
-      __syncthreads();
-    }
-    float* t = gcur;
-    gcur = gnxt;
-    gnxt = t;
   }
+  gnxt[a.g_off[t] + (int64_t)u * H + k] = v;
 }
 
 __global__ __launch_bounds__(kSbThreads) void k_sb_final(SbArgs a) {
@@ -456,7 +448,7 @@ __global__ __launch_bounds__(kSbThreads) void k_sb_final(SbArgs a) {
   for (int64_t e = (int64_t)blockIdx.x * kSbThreads + threadIdx.x; e < P; e += (int64_t)gridDim.x * kSbThreads) {
     float s = 0.0f;
     if (e < a.p_gin) {
-      for (int g = 0; g < a.G; ++g) s = __fadd_rn(s, a.part_gin[(int64_t)g * a.p_gin + e]);
+      for (int g = 0; g < a.n_parts; ++g) s = __fadd_rn(s, a.part_gin[(int64_t)g * a.p_gin + e]);
     } else {
       for (int t = 0; t < ntile; ++t) s = __fadd_rn(s, a.part_ro[(int64_t)t * a.p_ro + (e - a.p_gin)]);
     }
@@ -489,7 +481,7 @@ extern "C" int hgin_sb_step(const void* args, size_t args_bytes, size_t readout_
                  sizeof(SbArgs));
   SbArgs a;
   std::memcpy(&a, args, sizeof(SbArgs));
-  HGIN_ARG_CHECK(a.G >= 1 && a.L >= 1 && a.L <= kSbMaxL && a.H >= 1 && a.H <= 64 && a.nhid >= 1 &&
+  HGIN_ARG_CHECK(a.G >= 1 && a.L >= 1 && a.L <= kSbMaxL && a.H >= 1 && a.H <= 64 && a.nhid >= 1 && a.kmax <= 128 &&
                      a.nhid <= kSbMaxHid && a.n_tiles >= 1 && readout_lds <= 160 * 1024,
                  "hgin_sb_step: unsupported shape");
   hipStream_t s = as_stream(stream);
@@ -507,9 +499,33 @@ extern "C" int hgin_sb_step(const void* args, size_t args_bytes, size_t readout_
     return (int)hipErrorInvalidValue;
   }
   HGIN_ARG_CHECK((int64_t)readout_lds <= dyn_max, "hgin_sb_step: readout LDS %zu above %d", readout_lds, dyn_max);
-  k_sb_gin_fwd<<<a.G, kSbThreads, 0, s>>>(a);
+  auto blocks = [](int64_t n) { return (unsigned)(n > 0 ? ceil_div(n, (int64_t)kSbThreads) : 1); };
+  int capd_max = 0, capt_max = 0, kmx = 0;
+  for (int t = 0; t < 3; ++t) capt_max = a.cap[t] > capt_max ? a.cap[t] : capt_max;
+  for (int r = 0; r < kRel; ++r) {
+    capd_max = a.cap[kRelDst[r]] > capd_max ? a.cap[kRelDst[r]] : capd_max;
+    const int K0 = a.fdim[kRelSrc[r]] + a.fdim[kRelDst[r]];
+    kmx = K0 > kmx ? K0 : kmx;
+  }
+  HGIN_ARG_CHECK(kmx <= a.kmax && a.H <= a.kmax && a.n_parts >= 1 && capt_max >= 1, "hgin_sb_step: kmax / n_parts");
+  for (int l = 0; l < a.L; ++l) {
+    const int K = l == 0 ? kmx : a.H;
+    k_sb_agg<<<dim3(blocks((int64_t)capd_max * K), kRel), kSbThreads, 0, s>>>(a, l);
+    k_sb_mlp<<<dim3(blocks((int64_t)capt_max * a.H), 3), kSbThreads, 0, s>>>(a, l);
+  }
   k_sb_readout<<<a.n_tiles, kSbThreads, readout_lds, s>>>(a);
-  k_sb_gin_bwd<<<a.G, kSbThreads, 0, s>>>(a);
+  float* gcur = a.gA;
+  float* gnxt = a.gB;
+  for (int l = a.L - 1; l >= 0; --l) {
+    k_sb_bwd_z<<<dim3(blocks(capd_max), kRel), kSbThreads, 0, s>>>(a, l, gcur);
+    k_sb_bwd_w<<<dim3(a.n_parts, kRel), kSbThreads, 0, s>>>(a, l, gcur);
+    if (l > 0) {
+      k_sb_bwd_in<<<dim3(blocks((int64_t)capt_max * a.H), 3), kSbThreads, 0, s>>>(a, l, gnxt);
+      float* tt = gcur;
+      gcur = gnxt;
+      gnxt = tt;
+    }
+  }
   const int64_t P = a.p_gin + a.p_ro;
   const int64_t fb = ceil_div(P, kSbThreads);
   k_sb_final<<<(unsigned)(fb < 256 ? fb : 256), kSbThreads, 0, s>>>(a);

@@ -1,8 +1,9 @@
-"""The reference's real training loop as four launches per batch (dataset.py:26, :239-244;
+"""The reference's real training loop in a handful of launches per batch (dataset.py:26, :239-244;
 train.py:25-44): ``SmallBatchStep`` runs a HetroGIN train step over a padded batch of small graphs with the fused
-kernels of ``csrc/hgin_smallbatch.hip`` (GIN forward and backward one workgroup per graph, readout + MAPE + readout
-backward in 16-row tiles, one fixed-order gradient reduction that applies the sqrt-MAPE scale), followed by torch's
-Adam, captured once into a hipGraph and replayed per batch after one device collation launch.
+kernels of ``csrc/hgin_smallbatch.hip`` (per layer one aggregate and one MLP launch over every relation and row of the
+batch, the readout + MAPE + readout backward in 16-row tiles, per layer two or three backward launches, one
+fixed-order gradient reduction that applies the sqrt-MAPE scale: 5 L + 1 launches), followed by torch's Adam,
+captured once into a hipGraph and replayed per batch after one device collation launch.
 
 It takes the model train.py builds from config.json (``HetroGIN`` with GINLayer convs, Linear + shared PReLU
 readout, Linear head, no BatchNorm / global features / dropout) at small widths: hidden <= 64, first-layer GEMM
@@ -25,6 +26,7 @@ from .models import HetroGIN
 from .store import GraphStore
 
 MAX_L, MAX_HID, REL = 4, 3, 4
+N_PARTS = 32   # row chunks of the weight-gradient partials (fixed: the reduction order does not depend on the batch)
 TYPES = ("path", "link", "node")
 RELS = (("path", "uses", "link"), ("link", "includes", "path"), ("link", "connects", "node"), ("node", "has", "link"))
 _P = ctypes.c_void_p
@@ -49,8 +51,9 @@ class _SbArgs(ctypes.Structure):   # field for field csrc/hgin_smallbatch.hip Sb
                 ("comb", _P), ("comb_off", (_I64 * REL) * MAX_L),
                 ("zb", _P), ("zb_off", (_I64 * REL) * MAX_L),
                 ("gA", _P), ("gB", _P), ("g_off", _I64 * 3),
-                ("gz", _P), ("gc", _P), ("gz_off", _I64 * 3), ("gc_off", _I64 * 3), ("kmax", _I32),
-                ("part_gin", _P), ("part_ro", _P), ("loss_part", _P), ("n_tiles", _I32),
+                ("gz", _P), ("gc", _P), ("gz_off", _I64 * REL), ("gc_off", _I64 * REL), ("kmax", _I32),
+                ("cap", _I32 * 3), ("part_gin", _P), ("n_parts", _I32), ("part_ro", _P), ("loss_part", _P),
+                ("n_tiles", _I32),
                 ("gflat", _P), ("loss_value", _P)]
 
 
@@ -255,13 +258,16 @@ class SmallBatchStep:
         for ti in range(3):
             a.g_off[ti] = o[ti]
         kmax = max(max(K0), H)
-        o, self.gz = blocks([cap[t] * H for t in TYPES])
-        o2, self.gc = blocks([cap[t] * kmax for t in TYPES])
+        o, self.gz = blocks([cap[r[2]] * H for r in RELS])
+        o2, self.gc = blocks([cap[r[2]] * kmax for r in RELS])
         a.gz, a.gc, a.kmax = P(self.gz), P(self.gc), kmax
-        for ti in range(3):
-            a.gz_off[ti], a.gc_off[ti] = o[ti], o2[ti]
+        for ri in range(REL):
+            a.gz_off[ri], a.gc_off[ri] = o[ri], o2[ri]
+        for ti, t in enumerate(TYPES):
+            a.cap[ti] = cap[t]
         n_tiles = (cap["path"] + 15) // 16
-        self.part_gin = torch.zeros(batch_size * p_gin, **f32)
+        a.n_parts = N_PARTS
+        self.part_gin = torch.zeros(N_PARTS * p_gin, **f32)
         self.part_ro = torch.zeros(n_tiles * a.p_ro, **f32)
         self.loss_part = torch.zeros(n_tiles, **f32)
         a.part_gin, a.part_ro, a.loss_part, a.n_tiles = P(self.part_gin), P(self.part_ro), P(self.loss_part), n_tiles

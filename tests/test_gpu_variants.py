@@ -12,7 +12,7 @@ fixtures (tests/variant_child.py), so the non-default paths pytest's own process
                               fused one: bit-identical (same g_z, same dW partition; the bias / slope sums are
                               grouped differently, so those two gradients are compared within fixture tolerance);
   * HGIN_NT_BDMA=0          — the NT GEMM splitting B per tile instead of copying pre-split planes: bit-identical;
-  * HGIN_WSD_PIPE=1         — the software-pipelined weight-stationary fp32 dW at N = K = 256 (k_wsp_f32):
+  * HGIN_WSD_PIPE=0         — k_wsd_f32 instead of the software-pipelined fp32 dW at N = K = 256 (k_wsp_f32):
                               bit-identical;
   * HGIN_WS_PIPE=1          — the one-wave-per-SIMD pipelined fp32 forward / dX GEMM (k_wsf_f32, with
                               HGIN_GEMM_NT_IO=1 so it runs at fixture sizes): bit-identical but for the regrouped GIN
@@ -42,12 +42,12 @@ VARIANTS = {
     "gemm_nt_io": {"HGIN_GEMM_NT_IO": "1"},
     "wsd_pro_off": {"HGIN_WSD_PRO": "0"},
     "nt_bdma_off": {"HGIN_NT_BDMA": "0"},
-    "wsd_pipe": {"HGIN_WSD_PIPE": "1"},
+    "wsd_pipe_off": {"HGIN_WSD_PIPE": "0"},
     # the pipelined forward / dX form runs only with non-temporal epilogue streams (forced here: the fixtures are small)
     "ws_pipe": {"HGIN_WS_PIPE": "1", "HGIN_GEMM_NT_IO": "1"},
 }
 BITWISE_EQUAL_TO_DEFAULT = ("slab2pass", "agg_pipe", "agg_notail", "xcd_off", "agg_nt_all", "gemm_nt_io", "wsd_pro_off",
-                            "nt_bdma_off", "wsd_pipe", "ws_pipe")
+                            "nt_bdma_off", "wsd_pipe_off", "ws_pipe")
 
 # Scalar / column-sum gradients a variant regroups: the bias / PReLU-slope sums (per workgroup in the fused
 # weight-stationary dW, per row block in k_rows_bwd<0>).  Everything else must stay bit-identical.
