@@ -153,7 +153,10 @@ def cpu_baseline(cfg, full_graph: bool = False) -> dict:
                       f"oracle/pyg_cpu.py (torch CPU ops = the reference's PyG CPU path), {threads} threads, "
                       f"{cpu_model}",
             "ms_per_step": round(dt * 1e3, 2), "host_ram_gb": host_ram_gb(),
-            "step_times_s": [round(t, 3) for t in times]}
+            "step_times_s": [round(t, 3) for t in times],
+            # the box's host is shared with other tenants' jobs: its load when the sample ran (1-minute average over
+            # all of the machine's CPUs) says how contended the 16 threads were (DESIGN.md §5 CPU baseline)
+            "host_loadavg_1m": round(os.getloadavg()[0], 1), "host_cpus": os.cpu_count()}
 
 
 def zipf_dst(cfg, graph, dev, s: float = 1.1, seed: int = 7):
