@@ -1717,9 +1717,7 @@ __global__ __launch_bounds__(256, 1) void k_wsf_f32(WsArgs32 g) {
   constexpr int P_OFF = A_BYTES, PBUF = 3 * PL, R1_OFF = P_OFF + 2 * PBUF;
   constexpr int RA = 8, RR = kR1 ? 8 : 0;                 // DMA pieces per wave per block
   constexpr int S = 32 * (kZ ? 2 : 1);                     // dword stores per lane per block
-  constexpr int WAIT_A = 8 + S < 63 ? 8 + S : 63;          // split waits on A(i + 1): r1(i) and stores(i - 1) after it
-  constexpr int WAIT_R = S + RA < 63 ? S + RA : 63;        // epilogue waits on r1(i): stores(i - 1), A(i + 2) after it
-  constexpr int WAIT_S = S < 63 ? S : 63;
+  constexpr int WAIT_A = RR + S < 63 ? RR + S : 63;        // split waits on A(i + 1): stores(i - 1), r1(i) after it
   static_assert(EPI == 1 || kR1, "EPI 4 reads x_dst");
   extern __shared__ __attribute__((aligned(16))) char wsf_smem[];
   const int tid = threadIdx.x;
@@ -1904,19 +1902,17 @@ __global__ __launch_bounds__(256, 1) void k_wsf_f32(WsArgs32 g) {
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   if (my > 1) issue_a(1);
   if constexpr (kR1) issue_r1(0);
-  // Vector-memory order per wave in iteration i: A(i + 2) after the split's reads (end of the k-loop), r1(i + 1) after
-  // the epilogue's image reads, then the epilogue's S stores.  The split of block i + 1 waits on A(i + 1) (issued
-  // at the end of iteration i - 1's k-loop: r1(i) and stores(i - 1) follow it); the epilogue waits on r1(i) (stores
-  // (i - 1) and A(i + 2) follow it).  Counts above 63 are capped (waiting slightly more).
+  // Vector-memory order per wave in iteration i: A(i + 2) at the end of the k-loop (after the split's reads), the
+  // epilogue's S stores, then r1(i + 1) (after the epilogue's image reads).  The split of block i + 1 waits on A(i + 1)
+  // (issued at the end of iteration i - 1's k-loop: stores(i - 1) and r1(i) follow it; at i = 0 only r1(0)); the
+  // epilogue waits on r1(i) (only A(i + 2) follows it).  Counts above 63 are capped (waiting slightly more).
   for (int64_t i = 0; i < my; ++i) {
     __builtin_amdgcn_s_barrier();   // planes of block i written by every wave; those of block i - 1 read by every wave
     asm volatile("" ::: "memory");
     f32x16 acc[2];
     mfma(i, acc);
-    if constexpr (kR1) {
-      if (i >= 1 && i + 2 < my) wait_vm<WAIT_R>();
-      else if (i >= 1 && i + 1 < my) wait_vm<WAIT_S>();
-      else wait_vm<0>();
+    if constexpr (kR1) {   // r1(i) landed: only A(i + 2) was issued after it
+      if (i + 2 < my) wait_vm<RA>(); else wait_vm<0>();
     }
     const int64_t r0 = ((int64_t)blockIdx.x + i * G) * BM;
     if (r0 + BM <= M) epilogue(i, acc, std::false_type{}); else epilogue(i, acc, std::true_type{});
