@@ -1,10 +1,11 @@
 #!/bin/bash
-# Round-3 final tree evidence: full GPU suite + smoke, then per config (cfg3 headline, cfg5 bf16): the bench line, the
-# rocprofv3 kernel-trace summary of the same bench command (no probe / extras / CPU baseline), and the aggregate
-# family's PMC FETCH_SIZE / WRITE_SIZE in separate passes.  Every step time-limited; stop at the first failure.
+# Final-tree evidence: full GPU suite + smoke, the driver's bench command (cfg3 headline with extras.cfg5 / batches and
+# the CPU baseline), then per config (cfg3, cfg5 bf16): the rocprofv3 kernel-trace summary of the bench command (no
+# probe / extras / CPU baseline) and the aggregate family's PMC FETCH_SIZE / WRITE_SIZE in separate passes.  Every step
+# time-limited; stop at the first failure.
 set -u
 cd "$(dirname "$0")/.."
-OUT=gpurun_out/${TAG:-final_r03}
+OUT=gpurun_out/${TAG:-final}
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 step() {
@@ -13,10 +14,10 @@ step() {
   local rc=$?; echo "$name $rc" >> "$OUT/status.txt"; tail -2 "$OUT/$name.out" | cut -c1-300
   [ $rc -eq 0 ] || { echo "FATAL $name $rc"; tail -30 "$OUT/$name.out"; tail -20 "$OUT/$name.err"; exit $rc; }
 }
-step suite 700 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread
+step suite 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread
 step smoke 200 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')"
+step bench 600 python bench.py --gpus 1 --steps 20 --warmup 5
 for C in cfg3 cfg5; do
-  step bench_$C 400 python bench.py --config $C
   step prof_$C 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_$C" -o run -- \
       python3 bench.py --config $C --no-cpu-baseline --no-probe --no-extras
   f=$(find "$OUT/prof_$C" -name '*kernel_stats.csv' | head -1)
