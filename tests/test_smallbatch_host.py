@@ -1,0 +1,42 @@
+"""Host side of the fused small-batch step (hgin/smallbatch.py) on the CPU: the ctypes mirror of the kernels' argument
+block against the library's own sizeof / offsetof (no device call), which models it takes, and that a model it does
+not take is refused with the reason.  The step itself is tests/test_gpu_smallbatch.py."""
+import pytest
+import torch
+
+from hgin import HetroGIN
+from hgin.data import CONFIGS
+from hgin.smallbatch import SmallBatchStep, _structure, check_layout
+
+
+def _kw(**o):
+    # (HetroGIN edits its input_channels dict in place, as the reference does: a fresh one per model)
+    return dict(CONFIGS["cfg1"].model_kwargs({"link": 7, "path": 7, "node": 3}), **o)
+
+
+def test_argument_block_layout_matches_the_library():
+    check_layout()
+
+
+def test_supported_models():
+    assert SmallBatchStep.supports(HetroGIN(**_kw()))
+    assert SmallBatchStep.supports(HetroGIN(**_kw(message_passing_layers=3)))
+    assert SmallBatchStep.supports(HetroGIN(**_kw(mlp_layers=[64, 32, 16])))
+
+
+@pytest.mark.parametrize("override,reason", [
+    ({"global_feats": True, "bl_features": True}, "global features"),
+    ({"mlp_bn": True}, "readout layer"),
+    ({"node_embedding_size": 128}, "widths"),
+    ({"message_passing_layers": 5}, "layers"),
+])
+def test_refused_models_say_why(override, reason):
+    st = _structure(HetroGIN(**_kw(**override)))
+    assert isinstance(st, str) and reason in st, st
+
+
+def test_refuses_a_non_capturable_optimizer_before_touching_the_device():
+    model = HetroGIN(**_kw())
+    opt = torch.optim.Adam(model.parameters(), lr=1e-3)   # capturable=False
+    with pytest.raises(ValueError, match="capturable"):
+        SmallBatchStep(model, opt, store=None, batch_size=8, warmup_ids=[[0]])
