@@ -295,8 +295,15 @@ def batches_extra(dev, n_graphs: int = 256, batch: int = 8, warmup: int = 5, ste
 
     torch.manual_seed(1997)
     probe_model = HetroGIN(**base.model_kwargs({"link": base.f_link, "path": base.f_path, "node": base.f_node}))
-    kinds = (["fused"] if SmallBatchStep.supports(probe_model) else []) + ["general"]
-    res = {k: run(k) for k in kinds}
+    res = {"general": run("general")}
+    fused_error = None
+    if SmallBatchStep.supports(probe_model):
+        try:
+            res["fused"] = run("fused")
+        except Exception as exc:   # reported in the line, not fatal to the headline
+            fused_error = f"{type(exc).__name__}: {exc}"[:300]
+    # the main figure is the faster of the two executions; the other is reported beside it
+    kinds = sorted(res, key=lambda k: res[k][0])
     ms, wall, loss = res[kinds[0]]
     out = {"workload": f"{n_graphs} cfg1-schema graphs (7/7/3 raw features, normalised; sizes 0.5x-1.5x of "
                        f"{base.nodes} nodes / {base.graph_edges} edges) resident, shuffled batches of {batch}, "
@@ -308,11 +315,14 @@ def batches_extra(dev, n_graphs: int = 256, batch: int = 8, warmup: int = 5, ste
            "graphs_per_s": round(batch / (ms / 1e3), 1),
            "edges_per_s": round(float(np.mean(conv_edges)) / (ms / 1e3), 1),
            "mean_conv_edges_per_batch": float(np.mean(conv_edges)), "final_loss": loss}
-    if "fused" in res:
-        g_ms, g_wall, g_loss = res["general"]
-        out["general_path"] = {"ms_per_batch": round(g_ms, 4), "host_ms_per_batch": round(g_wall * 1e3, 4),
-                               "final_loss": g_loss,
-                               "execution": "per-op HIP kernels as one hipGraph replay (hgin/graphs.py)"}
+    if len(kinds) > 1:
+        o_ms, o_wall, o_loss = res[kinds[1]]
+        out["general_path" if kinds[1] == "general" else "fused_path"] = {
+            "ms_per_batch": round(o_ms, 4), "host_ms_per_batch": round(o_wall * 1e3, 4), "final_loss": o_loss,
+            "execution": ("per-op HIP kernels as one hipGraph replay (hgin/graphs.py)" if kinds[1] == "general" else
+                          "the fused small-batch step (5 L + 1 kernels + Adam) as one hipGraph replay")}
+    if fused_error:
+        out["fused_path_error"] = fused_error
     return out
 
 
