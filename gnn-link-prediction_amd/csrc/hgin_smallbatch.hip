@@ -10,7 +10,7 @@
 //                             (1 + eps) x_dst self term (concat in the first layer, add above it: models.py:210-215);
 //   k_sb_mlp    (per layer)   thread per (node type, row, output column): Linear + PReLU of every relation into the
 //                             type (models.py:236-239) and their sum in relation order (HeteroConv, models.py:286-298);
-//   k_sb_readout              16-row tiles of path rows: the readout MLP (models.py:300-330, :362-376: hidden Linear
+//   k_sb_readout              tiles of 16-64 path rows: the readout MLP (models.py:300-330, :362-376: hidden Linear
 //                             + the ONE shared PReLU, Linear head), the MAPE numerator sum_rows |(out - y) / y|
 //                             (train.py:12-13) and the readout backward seeded with d sum|u| / d out = sgn(u) / y,
 //                             per-tile weight-gradient partials;
@@ -38,7 +38,8 @@ namespace hgin {
 namespace {
 
 constexpr int kSbThreads = 256;
-constexpr int kSbRows = 16;         // readout rows per workgroup
+constexpr int kSbRows = 16;         // readout rows per workgroup in hgin_sb_readout_lds_bytes (per 16 rows; the
+                                    // launch uses a.ro_rows = 16, 32 or 64, whichever LDS allows)
 constexpr int kSbMaxL = 4;
 constexpr int kSbMaxHid = 3;
 constexpr int kRel = 4;
@@ -102,6 +103,7 @@ struct SbArgs {
   float* part_ro;           // [n_tiles][p_ro]
   float* loss_part;         // [n_tiles]
   int n_tiles;
+  int ro_rows;              // path rows per readout tile (16, 32 or 64)
   // outputs
   float* gflat;             // [p_gin + p_ro]
   float* loss_value;        // [1]
@@ -187,16 +189,18 @@ __global__ __launch_bounds__(kSbThreads) void k_sb_mlp(SbArgs a, int l) {
   a.act[a.act_off[l][t] + (int64_t)i * H + h] = y;
 }
 
-// One 16-row tile of path rows: readout forward, loss partial, readout backward (unscaled), weight-gradient partials.
+// One tile of a.ro_rows path rows (the host picks 64, 32 or 16 by LDS: fewer tiles = fewer readout weight-gradient
+// partials to write and to sum): readout forward, loss partial, readout backward (unscaled), weight-gradient partials.
 __global__ __launch_bounds__(kSbThreads) void k_sb_readout(SbArgs a) {
   extern __shared__ float sm[];
   __shared__ float red[kSbThreads];
   const int tid = threadIdx.x;
   const int H = a.H;
   const int m = a.m_valid[0];
-  const int r0 = blockIdx.x * kSbRows;
+  const int R = a.ro_rows;
+  const int r0 = blockIdx.x * R;
   if (r0 >= m) return;
-  const int nr = m - r0 < kSbRows ? m - r0 : kSbRows;
+  const int nr = m - r0 < R ? m - r0 : R;
   const int fp = a.concat_path ? a.fdim[0] : 0;
   const int w0 = H + fp;
   int win[kSbMaxHid + 1];   // input width of layer i (i = nhid: the head)
@@ -208,15 +212,15 @@ __global__ __launch_bounds__(kSbThreads) void k_sb_readout(SbArgs a) {
   float* in0 = sm;
   float* zs[kSbMaxHid];
   float* ys[kSbMaxHid];
-  float* p = in0 + kSbRows * w0;
+  float* p = in0 + R * w0;
   for (int i = 0; i < a.nhid; ++i) {
     zs[i] = p;
-    ys[i] = p + kSbRows * a.rw[i];
-    p += 2 * kSbRows * a.rw[i];
+    ys[i] = p + R * a.rw[i];
+    p += 2 * R * a.rw[i];
   }
   float* gb0 = p;
-  float* gb1 = p + kSbRows * maxw;
-  float* outv = gb1 + kSbRows * maxw;   // [16]
+  float* gb1 = p + R * maxw;
+  float* outv = gb1 + R * maxw;   // [R]
   const float* xp = a.act + a.act_off[a.L - 1][0];
   for (int idx = tid; idx < nr * w0; idx += kSbThreads) {
     const int rr = idx / w0, k = idx % w0;
@@ -434,7 +438,7 @@ __global__ __launch_bounds__(kSbThreads) void k_sb_final(SbArgs a) {
   __shared__ float red[kSbThreads];
   __shared__ float scale_s;
   const int m = a.m_valid[0];
-  const int ntile = (m + kSbRows - 1) / kSbRows;
+  const int ntile = (m + a.ro_rows - 1) / a.ro_rows;
   if (threadIdx.x == 0) {
     float s = 0.0f;
     for (int t = 0; t < ntile; ++t) s = __fadd_rn(s, a.loss_part[t]);
@@ -482,7 +486,8 @@ extern "C" int hgin_sb_step(const void* args, size_t args_bytes, size_t readout_
   SbArgs a;
   std::memcpy(&a, args, sizeof(SbArgs));
   HGIN_ARG_CHECK(a.G >= 1 && a.L >= 1 && a.L <= kSbMaxL && a.H >= 1 && a.H <= 64 && a.nhid >= 1 && a.kmax <= 128 &&
-                     a.nhid <= kSbMaxHid && a.n_tiles >= 1 && readout_lds <= 160 * 1024,
+                     a.nhid <= kSbMaxHid && a.n_tiles >= 1 && readout_lds <= 160 * 1024 &&
+                     (a.ro_rows == 16 || a.ro_rows == 32 || a.ro_rows == 64),
                  "hgin_sb_step: unsupported shape");
   hipStream_t s = as_stream(stream);
   HGIN_TRACE("k_sb_step");

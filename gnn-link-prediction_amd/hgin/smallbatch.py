@@ -1,7 +1,7 @@
 """The reference's real training loop in a handful of launches per batch (dataset.py:26, :239-244;
 train.py:25-44): ``SmallBatchStep`` runs a HetroGIN train step over a padded batch of small graphs with the fused
 kernels of ``csrc/hgin_smallbatch.hip`` (per layer one aggregate and one MLP launch over every relation and row of the
-batch, the readout + MAPE + readout backward in 16-row tiles, per layer two or three backward launches, one
+batch, the readout + MAPE + readout backward in tiles of 16-64 rows, per layer two or three backward launches, one
 fixed-order gradient reduction that applies the sqrt-MAPE scale: 5 L + 1 launches), followed by torch's Adam,
 captured once into a hipGraph and replayed per batch after one device collation launch.
 
@@ -26,7 +26,7 @@ from .models import HetroGIN
 from .store import GraphStore
 
 MAX_L, MAX_HID, REL = 4, 3, 4
-N_PARTS = 32   # row chunks of the weight-gradient partials (fixed: the reduction order does not depend on the batch)
+N_PARTS = 128  # row chunks of the weight-gradient partials (fixed: the reduction order does not depend on the batch)
 TYPES = ("path", "link", "node")
 RELS = (("path", "uses", "link"), ("link", "includes", "path"), ("link", "connects", "node"), ("node", "has", "link"))
 _P = ctypes.c_void_p
@@ -53,7 +53,7 @@ class _SbArgs(ctypes.Structure):   # field for field csrc/hgin_smallbatch.hip Sb
                 ("gA", _P), ("gB", _P), ("g_off", _I64 * 3),
                 ("gz", _P), ("gc", _P), ("gz_off", _I64 * REL), ("gc_off", _I64 * REL), ("kmax", _I32),
                 ("cap", _I32 * 3), ("part_gin", _P), ("n_parts", _I32), ("part_ro", _P), ("loss_part", _P),
-                ("n_tiles", _I32),
+                ("n_tiles", _I32), ("ro_rows", _I32),
                 ("gflat", _P), ("loss_value", _P)]
 
 
@@ -265,12 +265,9 @@ class SmallBatchStep:
             a.gz_off[ri], a.gc_off[ri] = o[ri], o2[ri]
         for ti, t in enumerate(TYPES):
             a.cap[ti] = cap[t]
-        n_tiles = (cap["path"] + 15) // 16
         a.n_parts = N_PARTS
         self.part_gin = torch.zeros(N_PARTS * p_gin, **f32)
-        self.part_ro = torch.zeros(n_tiles * a.p_ro, **f32)
-        self.loss_part = torch.zeros(n_tiles, **f32)
-        a.part_gin, a.part_ro, a.loss_part, a.n_tiles = P(self.part_gin), P(self.part_ro), P(self.loss_part), n_tiles
+        a.part_gin = P(self.part_gin)
         self.gflat = torch.zeros(off, **f32)
         self.loss_value = torch.zeros((), **f32)
         a.gflat, a.loss_value = P(self.gflat), P(self.loss_value)
@@ -281,10 +278,19 @@ class SmallBatchStep:
         lds = ctypes.c_size_t(0)
         _lib.check(_lib.lib().hgin_sb_readout_lds_bytes(H, fdim["path"], a.concat_path, a.nhid, widths,
                                                         ctypes.byref(lds)), "hgin_sb_readout_lds_bytes")
-        if lds.value > 160 * 1024:
+        # the tile's LDS is linear in its rows (the call sizes 16); the tallest of 64 / 32 / 16 rows that fits beside
+        # the kernel's 1 KiB static array
+        rows = next((r for r in (64, 32, 16) if lds.value * r // 16 <= 159 * 1024), None)
+        if rows is None:
             raise ValueError("SmallBatchStep: readout tile exceeds LDS")
+        a.ro_rows = rows
+        n_tiles = (cap["path"] + rows - 1) // rows
+        a.n_tiles = n_tiles
+        self.part_ro = torch.zeros(n_tiles * a.p_ro, **f32)
+        self.loss_part = torch.zeros(n_tiles, **f32)
+        a.part_ro, a.loss_part = P(self.part_ro), P(self.loss_part)
         check_layout()
-        self.args, self._keep, self.lds = a, keep, lds.value
+        self.args, self._keep, self.lds = a, keep, lds.value * rows // 16
         # warm-up on a side stream (optimizer state, allocator pools), then capture kernels + Adam once
         side = torch.cuda.Stream()
         side.wait_stream(torch.cuda.current_stream())

@@ -1,7 +1,8 @@
 #!/bin/bash
-# Round 4, second GPU call: the 2-rank rehearsals of bench.py's N > 1 legs with the probe on (cfg3 -> the cfg4
-# component split, and cfg5), each rank logging its peak device memory; then the CPU baseline on the FULL cfg2 graph
-# (bench.py --cpu-full cfg2, the box's host cores).  Every GPU step time-limited; the script stops at the first
+# Round 4: the fused small-batch step's parity tests and profile; SQ counter passes of the weight-stationary fp32 GEMMs;
+# the 2-rank rehearsals of bench.py's N > 1 legs with the probe on (cfg3 -> the cfg4 component split, and cfg5), each
+# rank logging its peak device memory; then the CPU baseline on the FULL cfg2 graph (bench.py --cpu-full cfg2, the box's
+# host cores).  Every GPU step time-limited; the script stops at the first
 # failure.
 set -u
 cd "$(dirname "$0")/.."
@@ -15,6 +16,16 @@ run() {  # name, limit, command...
   [ $rc -eq 0 ] || { echo "FATAL $name $rc"; tail -30 "$OUT/$name.out"; tail -30 "$OUT/$name.err"; exit $rc; }
 }
 echo "start $(date)" > "$OUT/status.txt"
+if [ "${SB:-1}" = "1" ]; then   # the fused small-batch step: parity, then its profile
+  run pytest_sb 300 python -u -m pytest tests/test_gpu_smallbatch.py -q --timeout 120 --timeout-method thread
+  tail -2 "$OUT/pytest_sb.out"
+  run prof_batches 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_batches" -o run -- \
+    python3 tools/batches_prof.py --steps 100
+  tail -c 700 "$OUT/prof_batches.out"
+fi
+if [ "${PMC:-1}" = "1" ]; then
+  run gemm_pmc2 900 env OUT="$OUT/gemm_pmc2" bash tools/gpu_gemm_pmc2.sh
+fi
 if [ "${REHEARSE:-1}" = "1" ]; then
   export HGIN_DIST_BACKEND=gloo
   run rehearse_cfg3 700 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
@@ -24,9 +35,6 @@ if [ "${REHEARSE:-1}" = "1" ]; then
     --master-port 29518 bench.py --gpus 2 --steps 5 --warmup 2 --config cfg5
   tail -c 1500 "$OUT/rehearse_cfg5.out"
   unset HGIN_DIST_BACKEND
-fi
-if [ "${PMC:-1}" = "1" ]; then
-  run gemm_pmc2 900 env OUT="$OUT/gemm_pmc2" bash tools/gpu_gemm_pmc2.sh
 fi
 if [ "${CPUFULL:-1}" = "1" ]; then
   run cpu_full_cfg2 1000 python bench.py --cpu-full cfg2
