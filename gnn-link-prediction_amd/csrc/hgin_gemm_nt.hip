@@ -562,12 +562,14 @@ bool nt_bdma_enabled() {
   return on;
 }
 
-// HGIN_NT_T256=1: the split-mode tile at N a multiple of 256 as 128 x 256 (4 waves of 64 x 128, 128 accumulator VGPRs
-// each) at two workgroups per CU (A split once per 256 columns: half the split VALU per MFMA of the 128 x 128 tile).
+// The split-mode tile at N a multiple of 256 as 128 x 256 (4 waves of 64 x 128, 128 accumulator VGPRs each) at two
+// workgroups per CU (A split once per 256 columns: half the split VALU per MFMA of the 128 x 128 tile): the first
+// layer's K = 512 forward at M = 6M 9.61 -> 9.38 ms, with accum 10.18 -> 10.03 ms (profiles/r04/gpu_a/gemm_ab_*.json);
+// bit-identical (tests/test_gpu_gemm_switch.py).  HGIN_NT_T256=0 keeps the 128 x 128 tile.
 bool nt_t256_enabled() {
   static const bool on = [] {
     const char* v = getenv("HGIN_NT_T256");
-    return v && v[0] == '1';
+    return !(v && v[0] == '0');
   }();
   return on;
 }

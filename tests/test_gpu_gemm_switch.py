@@ -11,7 +11,8 @@
   * HGIN_NT_BKH=128         — the tiled kernel with 128-deep K-tiles (with the weight-stationary form off);
   * HGIN_NT_BDMA=0 (tiled)  — the fp32 128 x 128 tile splitting its B stages itself instead of copying them from
                               pre-split planes by LDS-DMA;
-  * HGIN_NT_T256=1          — the fp32 split tile at 128 x 256 (N a multiple of 256: the K = 512 forward);
+  * HGIN_NT_T256=0          — the fp32 split tile at 128 x 128 instead of 128 x 256 (N a multiple of 256: the
+                              K = 512 forward);
   * HGIN_WS_PIPE=1          — the one-wave-per-SIMD pipelined fp32 forward / dX form (k_wsf_f32; with
                               HGIN_GEMM_NT_IO=1, its precondition, so it runs at these sizes);
   * HGIN_WSD_PIPE=0         — k_wsd_f32 instead of the pipelined fp32 dW (k_wsp_f32);
@@ -36,7 +37,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 SWITCHES = {"default": {}, "tiled": {"HGIN_NT_WS": "0", "HGIN_TN_WS": "0", "HGIN_NT_WS32": "0"},
             "tiled_bk128": {"HGIN_NT_WS": "0", "HGIN_NT_BKH": "128", "HGIN_TN_WS": "0", "HGIN_NT_WS32": "0"},
             "tiled_nobdma": {"HGIN_NT_WS": "0", "HGIN_TN_WS": "0", "HGIN_NT_WS32": "0", "HGIN_NT_BDMA": "0"},
-            "t256": {"HGIN_NT_T256": "1"},
+            "t256_off": {"HGIN_NT_T256": "0"},
             "ws_pipe": {"HGIN_WS_PIPE": "1", "HGIN_GEMM_NT_IO": "1"},
             "wsd_pipe_off": {"HGIN_WSD_PIPE": "0"}}
 _results = {}
@@ -61,7 +62,7 @@ def test_switch_within_tolerance(name):
     _run(name)        # the child checks against fp32 itself
 
 
-@pytest.mark.parametrize("name", ["tiled", "tiled_bk128", "tiled_nobdma", "t256", "ws_pipe", "wsd_pipe_off"])
+@pytest.mark.parametrize("name", ["tiled", "tiled_bk128", "tiled_nobdma", "t256_off", "ws_pipe", "wsd_pipe_off"])
 def test_switch_bitwise_equal_default(name):
     ref, got = _run("default"), _run(name)
     assert ref.keys() == got.keys()
