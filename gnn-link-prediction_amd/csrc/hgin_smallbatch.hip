@@ -10,12 +10,13 @@
 //                             (1 + eps) x_dst self term (concat in the first layer, add above it: models.py:210-215);
 //   k_sb_mlp    (per layer)   thread per (node type, row, output column): Linear + PReLU of every relation into the
 //                             type (models.py:236-239) and their sum in relation order (HeteroConv, models.py:286-298);
-//   k_sb_readout              tiles of 16-64 path rows: the readout MLP (models.py:300-330, :362-376: hidden Linear
+//   k_sb_readout              tiles of 16 path rows: the readout MLP (models.py:300-330, :362-376: hidden Linear
 //                             + the ONE shared PReLU, Linear head), the MAPE numerator sum_rows |(out - y) / y|
 //                             (train.py:12-13) and the readout backward seeded with d sum|u| / d out = sgn(u) / y,
-//                             per-tile weight-gradient partials;
+//                             each layer's input and pre-activation gradient rows kept for the weight gradients;
 //   k_sb_bwd_z  (per layer)   thread per (relation, destination row): g_z = PReLU'(z) g_y and g_comb = g_z W;
-//   k_sb_bwd_w  (per layer)   workgroup per (row chunk, relation): the chunk's partial W / bias / slope / eps gradients;
+//   k_sb_bwd_w  (per layer)   workgroup per (row chunk, relation): the chunk's partial W / bias / slope / eps gradients
+//                             (the last layer's launch also the readout layers' partial W / bias gradients);
 //   k_sb_bwd_in (layers > 0)  thread per (node type, row, column): the layer input's gradient — every relation's self
 //                             term and CSC aggregate of g_comb, in relation order;
 //   k_sb_final                every parameter gradient = its partials summed in a fixed order, times d sqrt(loss) /
@@ -38,8 +39,8 @@ namespace hgin {
 namespace {
 
 constexpr int kSbThreads = 256;
-constexpr int kSbRows = 16;         // readout rows per workgroup in hgin_sb_readout_lds_bytes (per 16 rows; the
-                                    // launch uses a.ro_rows = 16, 32 or 64, whichever LDS allows)
+constexpr int kSbRows = 16;         // path rows per readout tile
+constexpr int kSbMaxW = 256;        // widest readout layer input / output
 constexpr int kSbMaxL = 4;
 constexpr int kSbMaxHid = 3;
 constexpr int kRel = 4;
@@ -100,10 +101,13 @@ struct SbArgs {
   int cap[3];               // row capacity per node type (grid sizes)
   float* part_gin;          // [n_parts][p_gin]
   int n_parts;              // row chunks of the weight-gradient partials
-  float* part_ro;           // [n_tiles][p_ro]
+  float* part_ro;           // [n_parts][p_ro] (row chunks of the path rows; the slope entry comes from slope_part)
   float* loss_part;         // [n_tiles]
-  int n_tiles;
-  int ro_rows;              // path rows per readout tile (16, 32 or 64)
+  float* slope_part;        // [n_tiles] the shared readout slope's gradient
+  int n_tiles;              // readout tiles of kSbRows path rows
+  int ro_wlds;              // 1: the readout tiles stage the hidden weights in LDS
+  float* ro_in[kSbMaxHid + 1];   // readout layer i's input rows [cap_path][win_i] (i = nhid: the head)
+  float* ro_gz[kSbMaxHid + 1];   // its pre-activation gradient rows [cap_path][rw_i] (the head: [cap_path])
   // outputs
   float* gflat;             // [p_gin + p_ro]
   float* loss_value;        // [1]
@@ -189,15 +193,19 @@ __global__ __launch_bounds__(kSbThreads) void k_sb_mlp(SbArgs a, int l) {
   a.act[a.act_off[l][t] + (int64_t)i * H + h] = y;
 }
 
-// One tile of a.ro_rows path rows (the host picks 64, 32 or 16 by LDS: fewer tiles = fewer readout weight-gradient
-// partials to write and to sum): readout forward, loss partial, readout backward (unscaled), weight-gradient partials.
+// One tile of kSbRows path rows: readout forward, loss partial, readout backward (unscaled) down to the path
+// embeddings' gradient.  Each layer's input rows and pre-activation gradient rows go to ro_in / ro_gz, from which
+// the readout blocks of k_sb_bwd_w form the weight-gradient partials over the same row chunks as the GIN's (a tile
+// that also reduced its own rows' weight gradients spent most of its time there and left n_tiles partials to sum).
+// The hidden weights are staged in LDS when they fit (row stride K | 1: odd, so the forward's column-per-thread reads
+// and the backward's row-per-thread reads are both free of bank conflicts).
 __global__ __launch_bounds__(kSbThreads) void k_sb_readout(SbArgs a) {
   extern __shared__ float sm[];
   __shared__ float red[kSbThreads];
   const int tid = threadIdx.x;
   const int H = a.H;
   const int m = a.m_valid[0];
-  const int R = a.ro_rows;
+  constexpr int R = kSbRows;
   const int r0 = blockIdx.x * R;
   if (r0 >= m) return;
   const int nr = m - r0 < R ? m - r0 : R;
@@ -206,13 +214,29 @@ __global__ __launch_bounds__(kSbThreads) void k_sb_readout(SbArgs a) {
   int win[kSbMaxHid + 1];   // input width of layer i (i = nhid: the head)
   win[0] = w0;
   for (int i = 0; i < a.nhid; ++i) win[i + 1] = a.rw[i];
-  // LDS: in0 [16][w0] | per hidden layer z_i, y_i [16][rw_i] | gbuf x2 [16][maxw]
   int maxw = w0;
   for (int i = 0; i < a.nhid; ++i) maxw = a.rw[i] > maxw ? a.rw[i] : maxw;
-  float* in0 = sm;
+  // LDS: [W_i [rw_i][win_i | 1] when ro_wlds] in0 [R][w0] | per hidden layer z_i, y_i [R][rw_i] | gbuf x2 [R][maxw]
+  float* p = sm;
+  const float* W[kSbMaxHid];
+  int ldw[kSbMaxHid];
+  for (int i = 0; i < a.nhid; ++i) {
+    const int K = win[i], N = a.rw[i];
+    if (a.ro_wlds) {
+      const int ks = K | 1;
+      for (int idx = tid; idx < N * K; idx += kSbThreads) p[(idx / K) * ks + idx % K] = a.row_w[i][idx];
+      W[i] = p;
+      ldw[i] = ks;
+      p += N * ks;
+    } else {
+      W[i] = a.row_w[i];
+      ldw[i] = K;
+    }
+  }
+  float* in0 = p;
   float* zs[kSbMaxHid];
   float* ys[kSbMaxHid];
-  float* p = in0 + R * w0;
+  p = in0 + R * w0;
   for (int i = 0; i < a.nhid; ++i) {
     zs[i] = p;
     ys[i] = p + R * a.rw[i];
@@ -225,21 +249,25 @@ __global__ __launch_bounds__(kSbThreads) void k_sb_readout(SbArgs a) {
   for (int idx = tid; idx < nr * w0; idx += kSbThreads) {
     const int rr = idx / w0, k = idx % w0;
     const int64_t row = r0 + rr;
-    in0[rr * w0 + k] = k < H ? xp[row * H + k] : a.x[0][row * a.ldx[0] + a.cols[0][k - H]];
+    const float v = k < H ? xp[row * H + k] : a.x[0][row * a.ldx[0] + a.cols[0][k - H]];
+    in0[rr * w0 + k] = v;
+    a.ro_in[0][(int64_t)r0 * w0 + idx] = v;
   }
   __syncthreads();
   const float slope = a.ro_slope[0];
   for (int i = 0; i < a.nhid; ++i) {
     const float* in = i == 0 ? in0 : ys[i - 1];
-    const int K = win[i], N = a.rw[i];
+    const int K = win[i], N = a.rw[i], lw = ldw[i];
     for (int idx = tid; idx < nr * N; idx += kSbThreads) {
       const int rr = idx / N, o = idx % N;
-      const float* wr = a.row_w[i] + (int64_t)o * K;
+      const float* wr = W[i] + (int64_t)o * lw;
       float z = 0.0f;
       for (int k = 0; k < K; ++k) z = fmaf(in[rr * K + k], wr[k], z);
       z = __fadd_rn(z, a.row_b[i][o]);
       zs[i][rr * N + o] = z;
-      ys[i][rr * N + o] = z > 0.0f ? z : __fmul_rn(slope, z);
+      const float yv = z > 0.0f ? z : __fmul_rn(slope, z);
+      ys[i][rr * N + o] = yv;
+      a.ro_in[i + 1][(int64_t)r0 * N + idx] = yv;
     }
     __syncthreads();
   }
@@ -255,7 +283,9 @@ __global__ __launch_bounds__(kSbThreads) void k_sb_readout(SbArgs a) {
     const float u = __fdiv_rn(__fsub_rn(o, yv), yv);
     lp = fabsf(u);
     const float sg = u > 0.0f ? 1.0f : (u < 0.0f ? -1.0f : 0.0f);
-    outv[tid] = __fdiv_rn(sg, yv);   // d |u| / d out
+    const float go = __fdiv_rn(sg, yv);   // d |u| / d out
+    outv[tid] = go;
+    a.ro_gz[a.nhid][r0 + tid] = go;
   }
   // fixed-order tile sum of |u| (rows in order)
   red[tid] = tid < nr ? lp : 0.0f;
@@ -264,19 +294,6 @@ __global__ __launch_bounds__(kSbThreads) void k_sb_readout(SbArgs a) {
     float s = 0.0f;
     for (int rr = 0; rr < nr; ++rr) s = __fadd_rn(s, red[rr]);
     a.loss_part[blockIdx.x] = s;
-  }
-  __syncthreads();
-  float* part = a.part_ro + (int64_t)blockIdx.x * a.p_ro - a.p_gin;   // indexed by the flat readout offsets
-  // head gradients: g_w[k] = sum_rows g_out y_last[k]; g_b = sum_rows g_out; g_y_last = g_out w
-  for (int k = tid; k < KL; k += kSbThreads) {
-    float s = 0.0f;
-    for (int rr = 0; rr < nr; ++rr) s = fmaf(outv[rr], yl[rr * KL + k], s);
-    part[a.head_goff + k] = s;
-  }
-  if (tid == 0) {
-    float s = 0.0f;
-    for (int rr = 0; rr < nr; ++rr) s = __fadd_rn(s, outv[rr]);
-    part[a.head_goff + KL] = s;
   }
   for (int idx = tid; idx < nr * KL; idx += kSbThreads) {
     const int rr = idx / KL, k = idx % KL;
@@ -287,35 +304,24 @@ __global__ __launch_bounds__(kSbThreads) void k_sb_readout(SbArgs a) {
   float* g_y = gb0;
   float* g_next = gb1;
   for (int i = a.nhid - 1; i >= 0; --i) {
-    const int K = win[i], N = a.rw[i];
-    const float* in = i == 0 ? in0 : ys[i - 1];
+    const int K = win[i], N = a.rw[i], lw = ldw[i];
     // g_z (in place over g_y) and the slope partial
     for (int idx = tid; idx < nr * N; idx += kSbThreads) {
       const float z = zs[i][idx];
       const float g = g_y[idx];
       if (z <= 0.0f) slope_part = fmaf(g, z, slope_part);
-      g_y[idx] = z > 0.0f ? g : __fmul_rn(slope, g);
+      const float gz = z > 0.0f ? g : __fmul_rn(slope, g);
+      g_y[idx] = gz;
+      a.ro_gz[i][(int64_t)r0 * N + idx] = gz;
     }
     __syncthreads();
-    // g_W[o][k] = sum_rows g_z[o] in[k]; g_b[o] = sum_rows g_z[o]
-    const int64_t wo = a.ro_goff[i];
-    for (int idx = tid; idx < N * K; idx += kSbThreads) {
-      const int o = idx / K, k = idx % K;
+    // g_in[k] = sum_o g_z[o] W[o][k] (the first layer: only the path embeddings' H columns have a gradient)
+    const int KG = i == 0 ? H : K;
+    for (int idx = tid; idx < nr * KG; idx += kSbThreads) {
+      const int rr = idx / KG, k = idx % KG;
       float s = 0.0f;
-      for (int rr = 0; rr < nr; ++rr) s = fmaf(g_y[rr * N + o], in[rr * K + k], s);
-      part[wo + idx] = s;
-    }
-    for (int o = tid; o < N; o += kSbThreads) {
-      float s = 0.0f;
-      for (int rr = 0; rr < nr; ++rr) s = __fadd_rn(s, g_y[rr * N + o]);
-      part[wo + (int64_t)N * K + o] = s;
-    }
-    // g_in[k] = sum_o g_z[o] W[o][k]
-    for (int idx = tid; idx < nr * K; idx += kSbThreads) {
-      const int rr = idx / K, k = idx % K;
-      float s = 0.0f;
-      for (int o = 0; o < N; ++o) s = fmaf(g_y[rr * N + o], a.row_w[i][(int64_t)o * K + k], s);
-      g_next[rr * K + k] = s;
+      for (int o = 0; o < N; ++o) s = fmaf(g_y[rr * N + o], W[i][(int64_t)o * lw + k], s);
+      g_next[rr * KG + k] = s;
     }
     __syncthreads();
     float* t = g_y;
@@ -323,12 +329,64 @@ __global__ __launch_bounds__(kSbThreads) void k_sb_readout(SbArgs a) {
     g_next = t;
   }
   const float sp = block_sum(slope_part, red);
-  if (tid == 0) part[a.ro_slope_goff] = sp;
-  // the path embeddings' gradient (first H columns of the readout input) for the GIN backward
+  if (tid == 0) a.slope_part[blockIdx.x] = sp;
+  // the path embeddings' gradient for the GIN backward
   float* gpath = a.gA + a.g_off[0];
-  for (int idx = tid; idx < nr * H; idx += kSbThreads) {
-    const int rr = idx / H, k = idx % H;
-    gpath[(int64_t)(r0 + rr) * H + k] = g_y[rr * w0 + k];
+  for (int idx = tid; idx < nr * H; idx += kSbThreads) gpath[(int64_t)r0 * H + idx] = g_y[idx];
+}
+
+// the readout blocks of k_sb_bwd_w: layer i's (i = nhid: the head's) partial weight / bias gradients over row chunk p
+// of the m valid path rows, g_W[o][k] = sum_rows g_z[o] in[k], g_b[o] = sum_rows g_z[o], the chunk's rows in order
+// (staged kRoSub rows at a time)
+constexpr int kRoSub = 16;
+
+__device__ void ro_weight_part(const SbArgs& a, int p, int i, float* s_in, float* s_g) {
+  const int tid = threadIdx.x;
+  const int m = a.m_valid[0];
+  const int ch = (m + a.n_parts - 1) / a.n_parts;
+  const int i0 = p * ch < m ? p * ch : m, i1 = (p + 1) * ch < m ? (p + 1) * ch : m;
+  const int w0 = a.H + (a.concat_path ? a.fdim[0] : 0);
+  const int K = i == 0 ? w0 : a.rw[i - 1];
+  const int N = i < a.nhid ? a.rw[i] : 1;
+  const int E = N * (K + 1);
+  const float* in = a.ro_in[i];
+  const float* gz = a.ro_gz[i];
+  float* part = a.part_ro + (int64_t)p * a.p_ro - a.p_gin;   // indexed by the flat readout offsets
+  const int64_t wo = i < a.nhid ? a.ro_goff[i] : a.head_goff;
+  constexpr int J = 8;
+  for (int q0 = 0; q0 < E; q0 += J * kSbThreads) {
+    float acc[J];
+#pragma unroll
+    for (int j = 0; j < J; ++j) acc[j] = 0.0f;
+    for (int rb = i0; rb < i1; rb += kRoSub) {
+      const int nr = i1 - rb < kRoSub ? i1 - rb : kRoSub;
+      __syncthreads();
+      for (int idx = tid; idx < nr * K; idx += kSbThreads) s_in[idx] = in[(int64_t)rb * K + idx];
+      for (int idx = tid; idx < nr * N; idx += kSbThreads) s_g[idx] = gz[(int64_t)rb * N + idx];
+      __syncthreads();
+#pragma unroll
+      for (int j = 0; j < J; ++j) {
+        const int q = q0 + j * kSbThreads + tid;
+        if (q < E) {
+          const int o = q / (K + 1), k = q % (K + 1);
+          float v = acc[j];
+          if (k < K) {
+            for (int rr = 0; rr < nr; ++rr) v = fmaf(s_g[rr * N + o], s_in[rr * K + k], v);
+          } else {
+            for (int rr = 0; rr < nr; ++rr) v = __fadd_rn(v, s_g[rr * N + o]);
+          }
+          acc[j] = v;
+        }
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < J; ++j) {
+      const int q = q0 + j * kSbThreads + tid;
+      if (q < E) {
+        const int o = q / (K + 1), k = q % (K + 1);
+        part[wo + (k < K ? (int64_t)o * K + k : (int64_t)N * K + o)] = acc[j];
+      }
+    }
   }
 }
 
@@ -361,11 +419,16 @@ __global__ __launch_bounds__(kSbThreads) void k_sb_bwd_z(SbArgs a, int l, const 
   }
 }
 
-// one row chunk's partial W / bias / slope / eps gradients of one relation (grid = n_parts x relations); rows of
-// chunk p: [p c, (p + 1) c), c = ceil(rows / n_parts)
+// one row chunk's partial W / bias / slope / eps gradients of one relation (grid = n_parts x relations, plus the
+// readout layers' blocks in the last layer's launch); rows of chunk p: [p c, (p + 1) c), c = ceil(rows / n_parts)
 __global__ __launch_bounds__(kSbThreads) void k_sb_bwd_w(SbArgs a, int l, const float* gcur) {
   __shared__ float red[kSbThreads];
+  __shared__ float stage[2 * kRoSub * kSbMaxW];
   const int p = blockIdx.x, r = blockIdx.y;
+  if (r >= kRel) {   // the last layer's launch carries the readout's blocks (grid.y = kRel + nhid + 1)
+    ro_weight_part(a, p, r - kRel, stage, stage + kRoSub * kSbMaxW);
+    return;
+  }
   const int s = kRelSrc[r], d = kRelDst[r];
   const int H = a.H, K = kdim(a, l, r);
   const int tid = threadIdx.x;
@@ -434,31 +497,43 @@ __global__ __launch_bounds__(kSbThreads) void k_sb_bwd_in(SbArgs a, int l, float
   gnxt[a.g_off[t] + (int64_t)u * H + k] = v;
 }
 
+// every gradient entry = its n_parts partials in a fixed order (thread (j, g) of a 32-entry group sums parts g, g + 8,
+// ...; then the 8 group sums in order), times the sqrt-MAPE scale; the loss and the shared readout slope from the
+// per-tile partials (thread t sums tiles t, t + 256, ..., then a tree); every block recomputes the scale
 __global__ __launch_bounds__(kSbThreads) void k_sb_final(SbArgs a) {
   __shared__ float red[kSbThreads];
-  __shared__ float scale_s;
+  const int tid = threadIdx.x;
   const int m = a.m_valid[0];
-  const int ntile = (m + a.ro_rows - 1) / a.ro_rows;
-  if (threadIdx.x == 0) {
-    float s = 0.0f;
-    for (int t = 0; t < ntile; ++t) s = __fadd_rn(s, a.loss_part[t]);
-    const float lv = __fdiv_rn(__fmul_rn(100.0f, s), (float)m);       // 100 * mean |u| (train.py:12-13)
-    scale_s = __fdiv_rn(__fdiv_rn(100.0f, (float)m), __fmul_rn(2.0f, sqrtf(lv)));
-    if (blockIdx.x == 0) a.loss_value[0] = lv;
+  const int ntile = (m + kSbRows - 1) / kSbRows;
+  float lp = 0.0f, sp = 0.0f;
+  for (int t = tid; t < ntile; t += kSbThreads) {
+    lp = __fadd_rn(lp, a.loss_part[t]);
+    sp = __fadd_rn(sp, a.slope_part[t]);
   }
-  __syncthreads();
-  const float scale = scale_s;
+  const float s = block_sum(lp, red);
+  const float slope_sum = block_sum(sp, red);
+  const float lv = __fdiv_rn(__fmul_rn(100.0f, s), (float)m);       // 100 * mean |u| (train.py:12-13)
+  const float scale = __fdiv_rn(__fdiv_rn(100.0f, (float)m), __fmul_rn(2.0f, sqrtf(lv)));
+  if (blockIdx.x == 0 && tid == 0) a.loss_value[0] = lv;
   const int64_t P = a.p_gin + a.p_ro;
-  for (int64_t e = (int64_t)blockIdx.x * kSbThreads + threadIdx.x; e < P; e += (int64_t)gridDim.x * kSbThreads) {
-    float s = 0.0f;
+  const int j = tid & 31, g = tid >> 5;
+  for (int64_t e0 = (int64_t)blockIdx.x * 32; e0 < P; e0 += (int64_t)gridDim.x * 32) {
+    const int64_t e = e0 + j;
+    float v = 0.0f;
     if (e < a.p_gin) {
-      for (int g = 0; g < a.n_parts; ++g) s = __fadd_rn(s, a.part_gin[(int64_t)g * a.p_gin + e]);
-    } else {
-      for (int t = 0; t < ntile; ++t) s = __fadd_rn(s, a.part_ro[(int64_t)t * a.p_ro + (e - a.p_gin)]);
+      for (int pp = g; pp < a.n_parts; pp += 8) v = __fadd_rn(v, a.part_gin[(int64_t)pp * a.p_gin + e]);
+    } else if (e < P && e != a.ro_slope_goff) {
+      for (int pp = g; pp < a.n_parts; pp += 8) v = __fadd_rn(v, a.part_ro[(int64_t)pp * a.p_ro + (e - a.p_gin)]);
     }
-    a.gflat[e] = __fmul_rn(s, scale);
+    red[tid] = v;
+    __syncthreads();
+    if (g == 0 && e < P) {
+      float t = 0.0f;
+      for (int q = 0; q < 8; ++q) t = __fadd_rn(t, red[q * 32 + j]);
+      a.gflat[e] = __fmul_rn(e == a.ro_slope_goff ? slope_sum : t, scale);
+    }
+    __syncthreads();
   }
-  (void)red;
 }
 
 }  // namespace
@@ -467,27 +542,32 @@ __global__ __launch_bounds__(kSbThreads) void k_sb_final(SbArgs a) {
 using namespace hgin;
 
 extern "C" int hgin_sb_readout_lds_bytes(int64_t H, int64_t f_path, int concat_path, int nhid, const int32_t* widths,
-                                         size_t* bytes) {
+                                         int with_weights, size_t* bytes) {
   HGIN_ARG_CHECK(bytes && widths && nhid >= 1 && nhid <= kSbMaxHid && H >= 1, "hgin_sb_readout_lds_bytes: bad args");
   const int64_t w0 = H + (concat_path ? f_path : 0);
   int64_t maxw = w0, tot = w0;
+  int64_t wts = 0, win = w0;
   for (int i = 0; i < nhid; ++i) {
+    HGIN_ARG_CHECK(widths[i] >= 1 && widths[i] <= kSbMaxW, "hgin_sb_readout_lds_bytes: width %d", (int)widths[i]);
     tot += 2 * widths[i];
     maxw = widths[i] > maxw ? widths[i] : maxw;
+    wts += widths[i] * (win | 1);
+    win = widths[i];
   }
-  *bytes = sizeof(float) * (size_t)(kSbRows * (tot + 2 * maxw) + kSbRows);
+  HGIN_ARG_CHECK(w0 <= kSbMaxW, "hgin_sb_readout_lds_bytes: input width %lld", (long long)w0);
+  *bytes = sizeof(float) * (size_t)(kSbRows * (tot + 2 * maxw) + kSbRows + (with_weights ? wts : 0));
   return HGIN_OK;
 }
 
-// args: a host pointer to the filled SbArgs struct (layout in hgin/smallbatch.py); n_tiles = ceil(cap_path / 16).
+// args: a host pointer to the filled SbArgs struct (layout in hgin/smallbatch.py); n_tiles = ceil(cap_path / 16);
+// readout_lds = hgin_sb_readout_lds_bytes(..., with_weights = ro_wlds, ...).
 extern "C" int hgin_sb_step(const void* args, size_t args_bytes, size_t readout_lds, void* stream) {
   HGIN_ARG_CHECK(args && args_bytes == sizeof(SbArgs), "hgin_sb_step: args %zu bytes, expected %zu", args_bytes,
                  sizeof(SbArgs));
   SbArgs a;
   std::memcpy(&a, args, sizeof(SbArgs));
   HGIN_ARG_CHECK(a.G >= 1 && a.L >= 1 && a.L <= kSbMaxL && a.H >= 1 && a.H <= 64 && a.nhid >= 1 && a.kmax <= 128 &&
-                     a.nhid <= kSbMaxHid && a.n_tiles >= 1 && readout_lds <= 160 * 1024 &&
-                     (a.ro_rows == 16 || a.ro_rows == 32 || a.ro_rows == 64),
+                     a.nhid <= kSbMaxHid && a.n_tiles >= 1 && readout_lds <= 160 * 1024,
                  "hgin_sb_step: unsupported shape");
   hipStream_t s = as_stream(stream);
   HGIN_TRACE("k_sb_step");
@@ -523,7 +603,7 @@ extern "C" int hgin_sb_step(const void* args, size_t args_bytes, size_t readout_
   float* gnxt = a.gB;
   for (int l = a.L - 1; l >= 0; --l) {
     k_sb_bwd_z<<<dim3(blocks(capd_max), kRel), kSbThreads, 0, s>>>(a, l, gcur);
-    k_sb_bwd_w<<<dim3(a.n_parts, kRel), kSbThreads, 0, s>>>(a, l, gcur);
+    k_sb_bwd_w<<<dim3(a.n_parts, l == a.L - 1 ? kRel + a.nhid + 1 : kRel), kSbThreads, 0, s>>>(a, l, gcur);
     if (l > 0) {
       k_sb_bwd_in<<<dim3(blocks((int64_t)capt_max * a.H), 3), kSbThreads, 0, s>>>(a, l, gnxt);
       float* tt = gcur;
@@ -532,8 +612,8 @@ extern "C" int hgin_sb_step(const void* args, size_t args_bytes, size_t readout_
     }
   }
   const int64_t P = a.p_gin + a.p_ro;
-  const int64_t fb = ceil_div(P, kSbThreads);
-  k_sb_final<<<(unsigned)(fb < 256 ? fb : 256), kSbThreads, 0, s>>>(a);
+  const int64_t fb = ceil_div(P, (int64_t)32);
+  k_sb_final<<<(unsigned)(fb < 1024 ? fb : 1024), kSbThreads, 0, s>>>(a);
   return check_launch("hgin_sb_step");
 }
 

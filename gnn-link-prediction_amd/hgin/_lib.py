@@ -187,7 +187,7 @@ _SIGS = {
     "hgin_gat_wsum_f32": ([_P, _I64, _I64, _I64, _I64, _P, _P, _P, _SZ, _P], _I32),
     "hgin_sb_args_size": ([], _SZ),
     "hgin_sb_args_offsets": ([_P, _I64], _I32),
-    "hgin_sb_readout_lds_bytes": ([_I64, _I64, _I32, _I32, _P, ctypes.POINTER(_SZ)], _I32),
+    "hgin_sb_readout_lds_bytes": ([_I64, _I64, _I32, _I32, _P, _I32, ctypes.POINTER(_SZ)], _I32),
     "hgin_sb_step": ([_P, _SZ, _SZ, _P], _I32),
     "hgin_trace_enable": ([_I32], _I32),
     "hgin_trace_read": ([ctypes.c_char_p, _SZ], _SZ),

@@ -1,7 +1,7 @@
 """The reference's real training loop in a handful of launches per batch (dataset.py:26, :239-244;
 train.py:25-44): ``SmallBatchStep`` runs a HetroGIN train step over a padded batch of small graphs with the fused
 kernels of ``csrc/hgin_smallbatch.hip`` (per layer one aggregate and one MLP launch over every relation and row of the
-batch, the readout + MAPE + readout backward in tiles of 16-64 rows, per layer two or three backward launches, one
+batch, the readout + MAPE + readout backward in tiles of 16 rows, per layer two or three backward launches, one
 fixed-order gradient reduction that applies the sqrt-MAPE scale: 5 L + 1 launches), followed by torch's Adam,
 captured once into a hipGraph and replayed per batch after one device collation launch.
 
@@ -53,7 +53,8 @@ class _SbArgs(ctypes.Structure):   # field for field csrc/hgin_smallbatch.hip Sb
                 ("gA", _P), ("gB", _P), ("g_off", _I64 * 3),
                 ("gz", _P), ("gc", _P), ("gz_off", _I64 * REL), ("gc_off", _I64 * REL), ("kmax", _I32),
                 ("cap", _I32 * 3), ("part_gin", _P), ("n_parts", _I32), ("part_ro", _P), ("loss_part", _P),
-                ("n_tiles", _I32), ("ro_rows", _I32),
+                ("slope_part", _P), ("n_tiles", _I32), ("ro_wlds", _I32),
+                ("ro_in", _P * (MAX_HID + 1)), ("ro_gz", _P * (MAX_HID + 1)),
                 ("gflat", _P), ("loss_value", _P)]
 
 
@@ -276,21 +277,30 @@ class SmallBatchStep:
             p.grad = self.gflat[o:o + p.numel()].view_as(p)
         widths = (ctypes.c_int32 * MAX_HID)(*[a.rw[i] for i in range(MAX_HID)])
         lds = ctypes.c_size_t(0)
-        _lib.check(_lib.lib().hgin_sb_readout_lds_bytes(H, fdim["path"], a.concat_path, a.nhid, widths,
-                                                        ctypes.byref(lds)), "hgin_sb_readout_lds_bytes")
-        # the tile's LDS is linear in its rows (the call sizes 16); the tallest of 64 / 32 / 16 rows that fits beside
-        # the kernel's 1 KiB static array
-        rows = next((r for r in (64, 32, 16) if lds.value * r // 16 <= 159 * 1024), None)
-        if rows is None:
+        # the readout tile stages its hidden weights in LDS when they fit beside its 1 KiB static array
+        for wl in (1, 0):
+            _lib.check(_lib.lib().hgin_sb_readout_lds_bytes(H, fdim["path"], a.concat_path, a.nhid, widths, wl,
+                                                            ctypes.byref(lds)), "hgin_sb_readout_lds_bytes")
+            if lds.value <= 159 * 1024:
+                break
+        else:
             raise ValueError("SmallBatchStep: readout tile exceeds LDS")
-        a.ro_rows = rows
-        n_tiles = (cap["path"] + rows - 1) // rows
+        a.ro_wlds = wl
+        n_tiles = (cap["path"] + 15) // 16
         a.n_tiles = n_tiles
-        self.part_ro = torch.zeros(n_tiles * a.p_ro, **f32)
+        self.part_ro = torch.zeros(N_PARTS * a.p_ro, **f32)
         self.loss_part = torch.zeros(n_tiles, **f32)
-        a.part_ro, a.loss_part = P(self.part_ro), P(self.loss_part)
+        self.slope_part = torch.zeros(n_tiles, **f32)
+        a.part_ro, a.loss_part, a.slope_part = P(self.part_ro), P(self.loss_part), P(self.slope_part)
+        # per readout layer (the head last): input rows and pre-activation gradient rows
+        ro_w = [w0] + [a.rw[i] for i in range(a.nhid)]
+        self.ro_in = [torch.zeros(cap["path"] * ro_w[i], **f32) for i in range(a.nhid + 1)]
+        self.ro_gz = [torch.zeros(cap["path"] * (ro_w[i + 1] if i < a.nhid else 1), **f32)
+                      for i in range(a.nhid + 1)]
+        for i in range(a.nhid + 1):
+            a.ro_in[i], a.ro_gz[i] = P(self.ro_in[i]), P(self.ro_gz[i])
         check_layout()
-        self.args, self._keep, self.lds = a, keep, lds.value * rows // 16
+        self.args, self._keep, self.lds = a, keep, lds.value
         # warm-up on a side stream (optimizer state, allocator pools), then capture kernels + Adam once
         side = torch.cuda.Stream()
         side.wait_stream(torch.cuda.current_stream())
