@@ -10,7 +10,7 @@
 //                             (1 + eps) x_dst self term (concat in the first layer, add above it: models.py:210-215);
 //   k_sb_mlp    (per layer)   thread per (node type, row, output column): Linear + PReLU of every relation into the
 //                             type (models.py:236-239) and their sum in relation order (HeteroConv, models.py:286-298);
-//   k_sb_readout              tiles of 16 path rows: the readout MLP (models.py:300-330, :362-376: hidden Linear
+//   k_sb_readout              tiles of 8 path rows:  the readout MLP (models.py:300-330, :362-376: hidden Linear
 //                             + the ONE shared PReLU, Linear head), the MAPE numerator sum_rows |(out - y) / y|
 //                             (train.py:12-13) and the readout backward seeded with d sum|u| / d out = sgn(u) / y,
 //                             each layer's input and pre-activation gradient rows kept for the weight gradients;
@@ -39,7 +39,7 @@ namespace hgin {
 namespace {
 
 constexpr int kSbThreads = 256;
-constexpr int kSbRows = 16;         // path rows per readout tile
+constexpr int kSbRows = 8;          // path rows per readout tile (hgin/smallbatch.py RO_ROWS)
 constexpr int kSbMaxW = 256;        // widest readout layer input / output
 constexpr int kSbMaxL = 4;
 constexpr int kSbMaxHid = 3;
@@ -335,26 +335,38 @@ __global__ __launch_bounds__(kSbThreads) void k_sb_readout(SbArgs a) {
   for (int idx = tid; idx < nr * H; idx += kSbThreads) gpath[(int64_t)r0 * H + idx] = g_y[idx];
 }
 
-// the readout blocks of k_sb_bwd_w: layer i's (i = nhid: the head's) partial weight / bias gradients over row chunk p
-// of the m valid path rows, g_W[o][k] = sum_rows g_z[o] in[k], g_b[o] = sum_rows g_z[o], the chunk's rows in order
-// (staged kRoSub rows at a time)
+// the readout blocks of k_sb_bwd_w: over row chunk p of the m valid path rows, one group of kRoJ x kSbThreads of
+// layer i's (i = nhid: the head's) partial weight / bias gradients, g_W[o][k] = sum_rows g_z[o] in[k],
+// g_b[o] = sum_rows g_z[o], the chunk's rows in order (staged kRoSub rows at a time).  Block y-index u (after the
+// relations' kRel) -> (layer, group): the layers' groups in order.
 constexpr int kRoSub = 16;
+constexpr int kRoJ = 8;
 
-__device__ void ro_weight_part(const SbArgs& a, int p, int i, float* s_in, float* s_g) {
+__device__ __forceinline__ int ro_in_width(const SbArgs& a, int i) {
+  return i == 0 ? a.H + (a.concat_path ? a.fdim[0] : 0) : a.rw[i - 1];
+}
+__device__ __forceinline__ int ro_groups(const SbArgs& a, int i) {
+  const int N = i < a.nhid ? a.rw[i] : 1;
+  return (N * (ro_in_width(a, i) + 1) + kRoJ * kSbThreads - 1) / (kRoJ * kSbThreads);
+}
+
+__device__ void ro_weight_part(const SbArgs& a, int p, int u, float* s_in, float* s_g) {
+  int i = 0;
+  while (i < a.nhid && u >= ro_groups(a, i)) u -= ro_groups(a, i++);
   const int tid = threadIdx.x;
   const int m = a.m_valid[0];
   const int ch = (m + a.n_parts - 1) / a.n_parts;
   const int i0 = p * ch < m ? p * ch : m, i1 = (p + 1) * ch < m ? (p + 1) * ch : m;
-  const int w0 = a.H + (a.concat_path ? a.fdim[0] : 0);
-  const int K = i == 0 ? w0 : a.rw[i - 1];
+  const int K = ro_in_width(a, i);
   const int N = i < a.nhid ? a.rw[i] : 1;
   const int E = N * (K + 1);
   const float* in = a.ro_in[i];
   const float* gz = a.ro_gz[i];
   float* part = a.part_ro + (int64_t)p * a.p_ro - a.p_gin;   // indexed by the flat readout offsets
   const int64_t wo = i < a.nhid ? a.ro_goff[i] : a.head_goff;
-  constexpr int J = 8;
-  for (int q0 = 0; q0 < E; q0 += J * kSbThreads) {
+  constexpr int J = kRoJ;
+  {
+    const int q0 = u * J * kSbThreads;
     float acc[J];
 #pragma unroll
     for (int j = 0; j < J; ++j) acc[j] = 0.0f;
@@ -425,7 +437,7 @@ __global__ __launch_bounds__(kSbThreads) void k_sb_bwd_w(SbArgs a, int l, const 
   __shared__ float red[kSbThreads];
   __shared__ float stage[2 * kRoSub * kSbMaxW];
   const int p = blockIdx.x, r = blockIdx.y;
-  if (r >= kRel) {   // the last layer's launch carries the readout's blocks (grid.y = kRel + nhid + 1)
+  if (r >= kRel) {   // the last layer's launch carries the readout's blocks (grid.y = kRel + their groups)
     ro_weight_part(a, p, r - kRel, stage, stage + kRoSub * kSbMaxW);
     return;
   }
@@ -593,6 +605,14 @@ extern "C" int hgin_sb_step(const void* args, size_t args_bytes, size_t readout_
     kmx = K0 > kmx ? K0 : kmx;
   }
   HGIN_ARG_CHECK(kmx <= a.kmax && a.H <= a.kmax && a.n_parts >= 1 && capt_max >= 1, "hgin_sb_step: kmax / n_parts");
+  HGIN_ARG_CHECK((int64_t)a.n_tiles * kSbRows >= a.cap[0], "hgin_sb_step: %d readout tiles of %d rows < %d path rows",
+                 a.n_tiles, kSbRows, a.cap[0]);
+  int ro_blocks = 0;   // the readout weight-gradient blocks' groups (ro_groups, on the host)
+  for (int i = 0, win = a.H + (a.concat_path ? a.fdim[0] : 0); i <= a.nhid; ++i) {
+    const int N = i < a.nhid ? a.rw[i] : 1;
+    ro_blocks += (N * (win + 1) + kRoJ * kSbThreads - 1) / (kRoJ * kSbThreads);
+    if (i < a.nhid) win = a.rw[i];
+  }
   for (int l = 0; l < a.L; ++l) {
     const int K = l == 0 ? kmx : a.H;
     k_sb_agg<<<dim3(blocks((int64_t)capd_max * K), kRel), kSbThreads, 0, s>>>(a, l);
@@ -603,7 +623,7 @@ extern "C" int hgin_sb_step(const void* args, size_t args_bytes, size_t readout_
   float* gnxt = a.gB;
   for (int l = a.L - 1; l >= 0; --l) {
     k_sb_bwd_z<<<dim3(blocks(capd_max), kRel), kSbThreads, 0, s>>>(a, l, gcur);
-    k_sb_bwd_w<<<dim3(a.n_parts, l == a.L - 1 ? kRel + a.nhid + 1 : kRel), kSbThreads, 0, s>>>(a, l, gcur);
+    k_sb_bwd_w<<<dim3(a.n_parts, l == a.L - 1 ? kRel + ro_blocks : kRel), kSbThreads, 0, s>>>(a, l, gcur);
     if (l > 0) {
       k_sb_bwd_in<<<dim3(blocks((int64_t)capt_max * a.H), 3), kSbThreads, 0, s>>>(a, l, gnxt);
       float* tt = gcur;

@@ -1,7 +1,7 @@
 """The reference's real training loop in a handful of launches per batch (dataset.py:26, :239-244;
 train.py:25-44): ``SmallBatchStep`` runs a HetroGIN train step over a padded batch of small graphs with the fused
 kernels of ``csrc/hgin_smallbatch.hip`` (per layer one aggregate and one MLP launch over every relation and row of the
-batch, the readout + MAPE + readout backward in tiles of 16 rows, per layer two or three backward launches, one
+batch, the readout + MAPE + readout backward in tiles of 8 rows, per layer two or three backward launches, one
 fixed-order gradient reduction that applies the sqrt-MAPE scale: 5 L + 1 launches), followed by torch's Adam,
 captured once into a hipGraph and replayed per batch after one device collation launch.
 
@@ -27,6 +27,7 @@ from .store import GraphStore
 
 MAX_L, MAX_HID, REL = 4, 3, 4
 N_PARTS = 128  # row chunks of the weight-gradient partials (fixed: the reduction order does not depend on the batch)
+RO_ROWS = 8    # path rows per readout tile (csrc/hgin_smallbatch.hip kSbRows; the launcher checks the tile count)
 TYPES = ("path", "link", "node")
 RELS = (("path", "uses", "link"), ("link", "includes", "path"), ("link", "connects", "node"), ("node", "has", "link"))
 _P = ctypes.c_void_p
@@ -286,7 +287,7 @@ class SmallBatchStep:
         else:
             raise ValueError("SmallBatchStep: readout tile exceeds LDS")
         a.ro_wlds = wl
-        n_tiles = (cap["path"] + 15) // 16
+        n_tiles = (cap["path"] + RO_ROWS - 1) // RO_ROWS
         a.n_tiles = n_tiles
         self.part_ro = torch.zeros(N_PARTS * a.p_ro, **f32)
         self.loss_part = torch.zeros(n_tiles, **f32)
