@@ -255,7 +255,7 @@ def batches_extra(dev, n_graphs: int = 256, batch: int = 8, warmup: int = 5, ste
     batches of 8 small graphs.  Here: a cfg1-schema GraphStore (n_graphs RouteNet-sized graphs, 0.5x-1.5x cfg1,
     the reference's always-on normalisation applied once at build); each step = one device collation launch
     (GraphStore.collate_into) + one hipGraph replay of the whole train step: the fused small-batch step
-    (hgin/smallbatch.py: 5 L + 1 kernels + Adam) where it takes the model, and the general per-op path
+    (hgin/smallbatch.py: 3 L + 1 kernels + fused Adam) where it takes the model, and the general per-op path
     (hgin/graphs.py CapturedTrainStep) beside it.  HIP events around the timed batches; reported beside the
     headline, not in it."""
     import numpy as np
@@ -313,7 +313,7 @@ def batches_extra(dev, n_graphs: int = 256, batch: int = 8, warmup: int = 5, ste
                        f"{base.nodes} nodes / {base.graph_edges} edges) resident, shuffled batches of {batch}, "
                        f"hidden {base.hidden}, {base.layers} layers, fp32",
            "execution": ("device collation (one batched-copy launch) + one hipGraph replay per batch of the fused "
-                         "small-batch step (5 L + 1 kernels + Adam)" if kinds[0] == "fused" else
+                         "small-batch step (3 L + 1 kernels + fused Adam)" if kinds[0] == "fused" else
                          "device collation (one batched-copy launch) + one hipGraph replay per batch"),
            "batches": steps, "ms_per_batch": round(ms, 4), "host_ms_per_batch": round(wall * 1e3, 4),
            "graphs_per_s": round(batch / (ms / 1e3), 1),
@@ -325,7 +325,7 @@ def batches_extra(dev, n_graphs: int = 256, batch: int = 8, warmup: int = 5, ste
         out["general_path" if kinds[1] == "general" else "fused_path"] = {
             "ms_per_batch": round(o_ms, 4), "host_ms_per_batch": round(o_wall * 1e3, 4), "final_loss": o_loss,
             "execution": ("per-op HIP kernels as one hipGraph replay (hgin/graphs.py)" if kinds[1] == "general" else
-                          "the fused small-batch step (5 L + 1 kernels + Adam) as one hipGraph replay")}
+                          "the fused small-batch step (3 L + 1 kernels + fused Adam) as one hipGraph replay")}
     if fused_error:
         out["fused_path_error"] = fused_error
     return out

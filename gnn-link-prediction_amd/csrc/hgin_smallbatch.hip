@@ -1,21 +1,22 @@
 // F1 — the reference's real training loop (dataset.py:26, :239-244; train.py:25-44): shuffled batches of a few small
 // network graphs.  A batch of 8 RouteNet-sized graphs is a few thousand vertices, so the general path (one launch per
 // relation, layer and GEMM family, ~100 per step even as one hipGraph replay) is bound by kernel boundaries, not work.
-// Here the whole train step of a HetroGIN over a padded batch (hgin/store.py PaddedBatch) is 5 L + 1 launches (one
+// Here the whole train step of a HetroGIN over a padded batch (hgin/store.py PaddedBatch) is 3 L + 1 launches (one
 // fewer: the first layer needs no input gradient), every one spread over all rows of the batch (the graphs are
 // disjoint, but a workgroup per graph leaves all but a handful of CUs idle and serialises each graph's dependent
-// gathers — measured 1.15 ms per batch against the general path's 0.71):
+// gathers — measured 1.15 ms per batch against the general path's 0.71).  Launch boundaries only where a phase reads
+// rows another workgroup wrote (the aggregates and the readout); row-local phases share a launch:
 //
-//   k_sb_agg    (per layer)   thread per (relation, destination row, column): the CSR aggregate in edge order and the
-//                             (1 + eps) x_dst self term (concat in the first layer, add above it: models.py:210-215);
-//   k_sb_mlp    (per layer)   thread per (node type, row, output column): Linear + PReLU of every relation into the
-//                             type (models.py:236-239) and their sum in relation order (HeteroConv, models.py:286-298);
+//   k_sb_fwd    (per layer)   32 rows of one node type per workgroup: the CSR aggregate in edge order and the
+//                             (1 + eps) x_dst self term of every relation into the type (concat in the first layer,
+//                             add above it: models.py:210-215), then Linear + PReLU per relation (models.py:236-239)
+//                             and their sum in relation order (HeteroConv, models.py:286-298);
 //   k_sb_readout              tiles of 8 path rows:  the readout MLP (models.py:300-330, :362-376: hidden Linear
 //                             + the ONE shared PReLU, Linear head), the MAPE numerator sum_rows |(out - y) / y|
 //                             (train.py:12-13) and the readout backward seeded with d sum|u| / d out = sgn(u) / y,
 //                             each layer's input and pre-activation gradient rows kept for the weight gradients;
-//   k_sb_bwd_z  (per layer)   thread per (relation, destination row): g_z = PReLU'(z) g_y and g_comb = g_z W;
-//   k_sb_bwd_w  (per layer)   workgroup per (row chunk, relation): the chunk's partial W / bias / slope / eps gradients
+//   k_sb_bwd_w  (per layer)   workgroup per (row chunk, relation): the chunk's g_z = PReLU'(z) g_y and g_comb = g_z W,
+//                             then its partial W / bias / slope / eps gradients
 //                             (the last layer's launch also the readout layers' partial W / bias gradients);
 //   k_sb_bwd_in (layers > 0)  thread per (node type, row, column): the layer input's gradient — every relation's self
 //                             term and CSC aggregate of g_comb, in relation order;
@@ -134,63 +135,77 @@ __device__ float block_sum(float v, float* red) {
 
 __device__ __forceinline__ int nrows(const SbArgs& a, int t) { return a.goff[t * (a.G + 1) + a.G]; }
 
-// comb_r = [aggregate | (1 + eps) x_dst] (concat, first layer) or aggregate + (1 + eps) x_dst (add); grid.y = relation
-__global__ __launch_bounds__(kSbThreads) void k_sb_agg(SbArgs a, int l) {
-  const int r = blockIdx.y;
-  const int s = kRelSrc[r], d = kRelDst[r];
-  const int K = kdim(a, l, r);
-  const int64_t idx = (int64_t)blockIdx.x * kSbThreads + threadIdx.x;
-  if (idx >= (int64_t)nrows(a, d) * K) return;
-  const int i = (int)(idx / K), k = (int)(idx % K);
-  const SbConv& cv = a.conv[l][r];
-  const float sc = __fadd_rn(1.0f, cv.eps[0]);
-  const int32_t* rp = a.rowptr[r];
-  const int32_t* cl = a.col[r];
-  float v = 0.0f;
-  if (l == 0) {
-    const int fs = a.fdim[s];
-    if (k < fs) {
-      const float* xs = a.x[s];
-      const int64_t ld = a.ldx[s];
-      const int c = a.cols[s][k];
-      for (int e = rp[i]; e < rp[i + 1]; ++e) v = __fadd_rn(v, xs[(int64_t)cl[e] * ld + c]);
-    } else {
-      v = __fmul_rn(sc, a.x[d][(int64_t)i * a.ldx[d] + a.cols[d][k - fs]]);
-    }
-  } else {
-    const int H = a.H;
-    const float* xs = a.act + a.act_off[l - 1][s];
-    for (int e = rp[i]; e < rp[i + 1]; ++e) v = __fadd_rn(v, xs[(int64_t)cl[e] * H + k]);
-    v = __fadd_rn(v, __fmul_rn(sc, a.act[a.act_off[l - 1][d] + (int64_t)i * H + k]));
-  }
-  a.comb[a.comb_off[l][r] + (int64_t)i * K + k] = v;
-}
+// One layer's forward for kSbFwdRows rows of node type t (grid = row blocks x types): per relation into t (relation
+// order) comb_r = [aggregate | (1 + eps) x_dst] (concat, first layer) or aggregate + (1 + eps) x_dst (add), the
+// aggregate a sequential edge-order sum (models.py:210-215); then per row and output column the sum over those
+// relations of prelu(comb_r W_r^T + b_r) (models.py:236-239; HeteroConv's sum, models.py:286-298), z kept per
+// relation for the backward.  comb_r also goes to HBM (the weight gradients read it).
+constexpr int kSbFwdRows = 32;
 
-// the layer output of type t, column h: the sum over the relations into t (relation order) of prelu(comb W^T + b);
-// z kept per relation for the backward.  grid.y = node type
-__global__ __launch_bounds__(kSbThreads) void k_sb_mlp(SbArgs a, int l) {
+__global__ __launch_bounds__(kSbThreads) void k_sb_fwd(SbArgs a, int l) {
+  __shared__ float s_comb[2][kSbFwdRows * 128];   // <= 2 relations into a type, K <= kmax <= 128
   const int t = blockIdx.y;
+  const int tid = threadIdx.x;
   const int H = a.H;
-  const int64_t idx = (int64_t)blockIdx.x * kSbThreads + threadIdx.x;
-  if (idx >= (int64_t)nrows(a, t) * H) return;
-  const int i = (int)(idx / H), h = (int)(idx % H);
-  float y = 0.0f;
-  bool first = true;
+  const int n = nrows(a, t);
+  const int r0 = blockIdx.x * kSbFwdRows;
+  if (r0 >= n) return;
+  const int nr = n - r0 < kSbFwdRows ? n - r0 : kSbFwdRows;
+  int slot = 0;
   for (int r = 0; r < kRel; ++r) {
     if (kRelDst[r] != t) continue;
+    const int s = kRelSrc[r];
     const int K = kdim(a, l, r);
     const SbConv& cv = a.conv[l][r];
-    const float* cr = a.comb + a.comb_off[l][r] + (int64_t)i * K;
-    const float* wr = cv.w + (int64_t)h * K;
-    float z = 0.0f;
-    for (int k = 0; k < K; ++k) z = fmaf(cr[k], wr[k], z);
-    z = __fadd_rn(z, cv.b[h]);
-    a.zb[a.zb_off[l][r] + (int64_t)i * H + h] = z;
-    const float yv = z > 0.0f ? z : __fmul_rn(cv.slope[0], z);
-    y = first ? yv : __fadd_rn(y, yv);
-    first = false;
+    const float sc = __fadd_rn(1.0f, cv.eps[0]);
+    const int32_t* rp = a.rowptr[r];
+    const int32_t* cl = a.col[r];
+    float* comb = a.comb + a.comb_off[l][r] + (int64_t)r0 * K;
+    for (int idx = tid; idx < nr * K; idx += kSbThreads) {
+      const int i = r0 + idx / K, k = idx % K;
+      float v = 0.0f;
+      if (l == 0) {
+        const int fs = a.fdim[s];
+        if (k < fs) {
+          const float* xs = a.x[s];
+          const int64_t ld = a.ldx[s];
+          const int c = a.cols[s][k];
+          for (int e = rp[i]; e < rp[i + 1]; ++e) v = __fadd_rn(v, xs[(int64_t)cl[e] * ld + c]);
+        } else {
+          v = __fmul_rn(sc, a.x[t][(int64_t)i * a.ldx[t] + a.cols[t][k - fs]]);
+        }
+      } else {
+        const float* xs = a.act + a.act_off[l - 1][s];
+        for (int e = rp[i]; e < rp[i + 1]; ++e) v = __fadd_rn(v, xs[(int64_t)cl[e] * H + k]);
+        v = __fadd_rn(v, __fmul_rn(sc, a.act[a.act_off[l - 1][t] + (int64_t)i * H + k]));
+      }
+      s_comb[slot][idx] = v;
+      comb[idx] = v;
+    }
+    ++slot;
   }
-  a.act[a.act_off[l][t] + (int64_t)i * H + h] = y;
+  __syncthreads();
+  for (int idx = tid; idx < nr * H; idx += kSbThreads) {
+    const int ii = idx / H, h = idx % H;
+    float y = 0.0f;
+    bool first = true;
+    int sl = 0;
+    for (int r = 0; r < kRel; ++r) {
+      if (kRelDst[r] != t) continue;
+      const int K = kdim(a, l, r);
+      const SbConv& cv = a.conv[l][r];
+      const float* cr = s_comb[sl++] + ii * K;
+      const float* wr = cv.w + (int64_t)h * K;
+      float z = 0.0f;
+      for (int k = 0; k < K; ++k) z = fmaf(cr[k], wr[k], z);
+      z = __fadd_rn(z, cv.b[h]);
+      a.zb[a.zb_off[l][r] + (int64_t)(r0 + ii) * H + h] = z;
+      const float yv = z > 0.0f ? z : __fmul_rn(cv.slope[0], z);
+      y = first ? yv : __fadd_rn(y, yv);
+      first = false;
+    }
+    a.act[a.act_off[l][t] + (int64_t)(r0 + ii) * H + h] = y;
+  }
 }
 
 // One tile of kSbRows path rows: readout forward, loss partial, readout backward (unscaled) down to the path
@@ -408,29 +423,6 @@ __device__ __forceinline__ float gout(const SbArgs& a, const float* gcur, int l,
   return (l == a.L - 1 && d != 0) ? 0.0f : gcur[a.g_off[d] + q];
 }
 
-// g_z = PReLU'(z) g_y and g_comb = g_z W for one destination row of one relation (grid.y = relation)
-__global__ __launch_bounds__(kSbThreads) void k_sb_bwd_z(SbArgs a, int l, const float* gcur) {
-  const int r = blockIdx.y;
-  const int d = kRelDst[r];
-  const int H = a.H, K = kdim(a, l, r);
-  const int i = blockIdx.x * kSbThreads + threadIdx.x;
-  if (i >= nrows(a, d)) return;
-  const SbConv& cv = a.conv[l][r];
-  const float slope = cv.slope[0];
-  const float* zb = a.zb + a.zb_off[l][r] + (int64_t)i * H;
-  float* gz = a.gz + a.gz_off[r] + (int64_t)i * H;
-  for (int h = 0; h < H; ++h) {
-    const float z = zb[h], g = gout(a, gcur, l, d, (int64_t)i * H + h);
-    gz[h] = z > 0.0f ? g : __fmul_rn(slope, g);
-  }
-  float* gc = a.gc + a.gc_off[r] + (int64_t)i * a.kmax;   // (this thread's own g_z row, read back)
-  for (int k = 0; k < K; ++k) {
-    float v = 0.0f;
-    for (int h = 0; h < H; ++h) v = fmaf(gz[h], cv.w[(int64_t)h * K + k], v);
-    gc[k] = v;
-  }
-}
-
 // one row chunk's partial W / bias / slope / eps gradients of one relation (grid = n_parts x relations, plus the
 // readout layers' blocks in the last layer's launch); rows of chunk p: [p c, (p + 1) c), c = ceil(rows / n_parts)
 __global__ __launch_bounds__(kSbThreads) void k_sb_bwd_w(SbArgs a, int l, const float* gcur) {
@@ -449,8 +441,29 @@ __global__ __launch_bounds__(kSbThreads) void k_sb_bwd_w(SbArgs a, int l, const 
   const int i0 = p * ch < rows ? p * ch : rows, i1 = (p + 1) * ch < rows ? (p + 1) * ch : rows;
   const SbConv& cv = a.conv[l][r];
   float* part = a.part_gin + (int64_t)p * a.p_gin + cv.goff;
-  const float* gz = a.gz + a.gz_off[r];
+  float* gz = a.gz + a.gz_off[r];
   const float* comb = a.comb + a.comb_off[l][r];
+  const float* zb = a.zb + a.zb_off[l][r];
+  float* gc = a.gc + a.gc_off[r];
+  // the chunk's rows first: g_z = PReLU'(z) g_y, then g_comb = g_z W (row-local; k_sb_bwd_in reads every row's
+  // g_comb after this launch)
+  {
+    const float slope = cv.slope[0];
+    for (int q = tid; q < (i1 - i0) * H; q += kSbThreads) {
+      const int64_t qq = (int64_t)i0 * H + q;
+      const float z = zb[qq], g = gout(a, gcur, l, d, qq);
+      gz[qq] = z > 0.0f ? g : __fmul_rn(slope, g);
+    }
+    __syncthreads();
+    for (int q = tid; q < (i1 - i0) * K; q += kSbThreads) {
+      const int i = i0 + q / K, k = q % K;
+      const float* gzr = gz + (int64_t)i * H;
+      float v = 0.0f;
+      for (int h = 0; h < H; ++h) v = fmaf(gzr[h], cv.w[(int64_t)h * K + k], v);
+      gc[(int64_t)i * a.kmax + k] = v;
+    }
+    __syncthreads();
+  }
   // g_W[h][k] = sum_i g_z[i][h] comb[i][k]; g_b[h] = sum_i g_z[i][h] (the chunk's rows in order)
   for (int q = tid; q < H * (K + 1); q += kSbThreads) {
     const int h = q / (K + 1), k = q % (K + 1);
@@ -462,9 +475,7 @@ __global__ __launch_bounds__(kSbThreads) void k_sb_bwd_w(SbArgs a, int l, const 
     part[k < K ? (int64_t)h * K + k : (int64_t)H * K + h] = v;
   }
   // the slope (sum over z <= 0 of g_y z) and eps (g_comb over the self columns times x_dst) partials
-  const float* zb = a.zb + a.zb_off[l][r];
   const int fs = l == 0 ? a.fdim[s] : 0;
-  const float* gc = a.gc + a.gc_off[r];
   float sp = 0.0f, epv = 0.0f;
   for (int q = tid; q < (i1 - i0) * H; q += kSbThreads) {
     const int64_t qq = (int64_t)i0 * H + q;
@@ -597,10 +608,9 @@ extern "C" int hgin_sb_step(const void* args, size_t args_bytes, size_t readout_
   }
   HGIN_ARG_CHECK((int64_t)readout_lds <= dyn_max, "hgin_sb_step: readout LDS %zu above %d", readout_lds, dyn_max);
   auto blocks = [](int64_t n) { return (unsigned)(n > 0 ? ceil_div(n, (int64_t)kSbThreads) : 1); };
-  int capd_max = 0, capt_max = 0, kmx = 0;
+  int capt_max = 0, kmx = 0;
   for (int t = 0; t < 3; ++t) capt_max = a.cap[t] > capt_max ? a.cap[t] : capt_max;
   for (int r = 0; r < kRel; ++r) {
-    capd_max = a.cap[kRelDst[r]] > capd_max ? a.cap[kRelDst[r]] : capd_max;
     const int K0 = a.fdim[kRelSrc[r]] + a.fdim[kRelDst[r]];
     kmx = K0 > kmx ? K0 : kmx;
   }
@@ -613,16 +623,12 @@ extern "C" int hgin_sb_step(const void* args, size_t args_bytes, size_t readout_
     ro_blocks += (N * (win + 1) + kRoJ * kSbThreads - 1) / (kRoJ * kSbThreads);
     if (i < a.nhid) win = a.rw[i];
   }
-  for (int l = 0; l < a.L; ++l) {
-    const int K = l == 0 ? kmx : a.H;
-    k_sb_agg<<<dim3(blocks((int64_t)capd_max * K), kRel), kSbThreads, 0, s>>>(a, l);
-    k_sb_mlp<<<dim3(blocks((int64_t)capt_max * a.H), 3), kSbThreads, 0, s>>>(a, l);
-  }
+  const unsigned fwd_blocks = (unsigned)ceil_div((int64_t)capt_max, (int64_t)kSbFwdRows);
+  for (int l = 0; l < a.L; ++l) k_sb_fwd<<<dim3(fwd_blocks, 3), kSbThreads, 0, s>>>(a, l);
   k_sb_readout<<<a.n_tiles, kSbThreads, readout_lds, s>>>(a);
   float* gcur = a.gA;
   float* gnxt = a.gB;
   for (int l = a.L - 1; l >= 0; --l) {
-    k_sb_bwd_z<<<dim3(blocks(capd_max), kRel), kSbThreads, 0, s>>>(a, l, gcur);
     k_sb_bwd_w<<<dim3(a.n_parts, l == a.L - 1 ? kRel + ro_blocks : kRel), kSbThreads, 0, s>>>(a, l, gcur);
     if (l > 0) {
       k_sb_bwd_in<<<dim3(blocks((int64_t)capt_max * a.H), 3), kSbThreads, 0, s>>>(a, l, gnxt);

@@ -1,8 +1,8 @@
 """The reference's real training loop in a handful of launches per batch (dataset.py:26, :239-244;
 train.py:25-44): ``SmallBatchStep`` runs a HetroGIN train step over a padded batch of small graphs with the fused
-kernels of ``csrc/hgin_smallbatch.hip`` (per layer one aggregate and one MLP launch over every relation and row of the
-batch, the readout + MAPE + readout backward in tiles of 8 rows, per layer two or three backward launches, one
-fixed-order gradient reduction that applies the sqrt-MAPE scale: 5 L + 1 launches), followed by torch's Adam,
+kernels of ``csrc/hgin_smallbatch.hip`` (per layer one aggregate + MLP launch over every relation and row of the
+batch, the readout + MAPE + readout backward in tiles of 8 rows, per layer one or two backward launches, one
+fixed-order gradient reduction that applies the sqrt-MAPE scale: 3 L + 1 launches), followed by torch's fused Adam,
 captured once into a hipGraph and replayed per batch after one device collation launch.
 
 It takes the model train.py builds from config.json (``HetroGIN`` with GINLayer convs, Linear + shared PReLU

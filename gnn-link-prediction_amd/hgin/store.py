@@ -222,75 +222,127 @@ class GraphStore:
                      out.m_valid, out.goff, out.batch_size)
         return out
 
-    def _launch(self, ids, nodes, edges, b_node, b_edge, x_out, batch_out, y_out, ei_out, csr_out, csc_out,
-                m_valid, goff=None, cap_graphs: int = 0) -> None:
-        descs: List[tuple] = []
+    def _template(self):
+        """Per-graph copy-descriptor tables (built once per store): for every graph and descriptor group (one group
+        per buffer and relation) the source pointer, the count and the store-side part of the index shift, plus per
+        group how its destination and shift follow the batch offsets.  A batch then costs a handful of numpy ops
+        on a (graphs x groups) table instead of a Python loop per graph and buffer.  The store's tensors are fixed
+        at construction, so the table is built on first use and kept."""
+        tpl = getattr(self, "_tpl", None)
+        if tpl is not None:
+            return tpl
+        col = {t: i for i, t in enumerate(self.types)}
+        col.update({r: len(self.types) + i for i, r in enumerate(self.relations)})
+        G = self.num_graphs
+        cnt_tab = np.zeros((G, len(col)), dtype=np.int64)
+        for t in self.types:
+            cnt_tab[:, col[t]] = np.diff(self.node_off[t])
+        for r in self.relations:
+            cnt_tab[:, col[r]] = np.diff(self.edge_off[r])
+        no = {t: self.node_off[t][:-1] for t in self.types}
+        eo = {r: self.edge_off[r][:-1] for r in self.relations}
+        zero = np.zeros(G, dtype=np.int64)
 
-        def ptr(t: Tensor, elem_off: int) -> int:
-            return t.data_ptr() + int(elem_off) * t.element_size()
+        def P(t: Tensor, off):
+            return np.int64(t.data_ptr()) + off * t.element_size()
 
+        # (src pointer [G], count [G], shift [G], dst selector, dst column, dst rows -> elements, dst constant
+        #  selector, shift column or -1, shift += j, kind)
+        spec = []
         for t in self.types:
             F = self.x[t].shape[1]
-            for j, g in enumerate(ids):
-                n = int(nodes[t][j])
-                if n == 0:
-                    continue
-                s_off, b_off = int(self.node_off[t][g]), int(b_node[t][j])
-                descs.append((ptr(self.x[t], s_off * F), ptr(x_out[t], b_off * F), n * F, 0,
-                              _COPY_KIND[self.x[t].element_size()]))
-                descs.append((0, ptr(batch_out[t], b_off), n, j, FILL_I64))
-        for j, g in enumerate(ids):
-            n = int(nodes["path"][j])
-            if n:
-                descs.append((ptr(self.y, self.node_off["path"][g]), ptr(y_out, b_node["path"][j]), n, 0, COPY_F32))
-
+            spec.append((P(self.x[t], no[t] * F), cnt_tab[:, col[t]] * F, zero, ("x", t), col[t], F, None, -1, 0,
+                         _COPY_KIND[self.x[t].element_size()]))
+            spec.append((zero, cnt_tab[:, col[t]], zero, ("batch", t), col[t], 1, None, -1, 1, FILL_I64))
+        spec.append((P(self.y, no["path"]), cnt_tab[:, col["path"]], zero, ("y", None), col["path"], 1, None, -1, 0,
+                     COPY_F32))
         for r in self.relations:
-            s, _, d = r
-            E = int(b_edge[r][-1])
-            n_s, n_d = int(b_node[s][-1]), int(b_node[d][-1])
-            e, cr, cc = ei_out[r], csr_out[r], csc_out[r]
-            e_cap = e.shape[1]                    # row stride of the [2, E] edge_index buffer
+            s_, _, d = r
             se, sc, ss = self.edge_index[r], self.csr[r], self.csc[r]
             E_store = se.shape[1]
-            for j, g in enumerate(ids):
-                m = int(edges[r][j])
-                es, eb = int(self.edge_off[r][g]), int(b_edge[r][j])
-                ds_s, db_s = int(self.node_off[s][g]), int(b_node[s][j])
-                ds_d, db_d = int(self.node_off[d][g]), int(b_node[d][j])
-                nd, ns = int(nodes[d][j]), int(nodes[s][j])
-                if m:
-                    descs.append((ptr(se, es), ptr(e, eb), m, db_s - ds_s, COPY_I64_ADD))              # src row
-                    descs.append((ptr(se, E_store + es), ptr(e, e_cap + eb), m, db_d - ds_d, COPY_I64_ADD))  # dst
-                    descs.append((ptr(sc.col, es), ptr(cr.col, eb), m, db_s - ds_s, COPY_I32_ADD))
-                    descs.append((ptr(sc.perm, es), ptr(cr.perm, eb), m, eb - es, COPY_I32_ADD))
-                    descs.append((ptr(ss.col, es), ptr(cc.col, eb), m, db_d - ds_d, COPY_I32_ADD))
-                    descs.append((ptr(ss.perm, es), ptr(cc.perm, eb), m, eb - es, COPY_I32_ADD))
-                if nd:
-                    descs.append((ptr(sc.rowptr, ds_d), ptr(cr.rowptr, db_d), nd, eb - es, COPY_I32_ADD))
-                if ns:
-                    descs.append((ptr(ss.rowptr, ds_s), ptr(cc.rowptr, db_s), ns, eb - es, COPY_I32_ADD))
-            # rowptr[n .. capacity] = E: the last row's end, and empty rows for padding vertices
-            descs.append((0, ptr(cr.rowptr, n_d), cr.rowptr.numel() - n_d, E, FILL_I32))
-            descs.append((0, ptr(cc.rowptr, n_s), cc.rowptr.numel() - n_s, E, FILL_I32))
-        if m_valid is not None:
-            descs.append((0, ptr(m_valid, 0), 1, int(b_node["path"][-1]), FILL_I32))
-        if goff is not None:   # graph j's rows of type t: [goff[t][j], goff[t][j + 1]); graphs past the batch: empty
-            for ti, t in enumerate(("path", "link", "node")):
-                if t not in b_node:
-                    continue
-                for j in range(cap_graphs + 1):
-                    v = int(b_node[t][min(j, len(ids))])
-                    descs.append((0, ptr(goff, ti * (cap_graphs + 1) + j), 1, v, FILL_I32))
+            m, cr_ = cnt_tab[:, col[r]], col[r]
+            spec += [
+                (P(se, eo[r]), m, -no[s_], ("ei", r), cr_, 1, None, col[s_], 0, COPY_I64_ADD),          # src row
+                (P(se, E_store + eo[r]), m, -no[d], ("ei", r), cr_, 1, "e_cap", col[d], 0, COPY_I64_ADD),  # dst
+                (P(sc.col, eo[r]), m, -no[s_], ("csr.col", r), cr_, 1, None, col[s_], 0, COPY_I32_ADD),
+                (P(sc.perm, eo[r]), m, -eo[r], ("csr.perm", r), cr_, 1, None, cr_, 0, COPY_I32_ADD),
+                (P(ss.col, eo[r]), m, -no[d], ("csc.col", r), cr_, 1, None, col[d], 0, COPY_I32_ADD),
+                (P(ss.perm, eo[r]), m, -eo[r], ("csc.perm", r), cr_, 1, None, cr_, 0, COPY_I32_ADD),
+                (P(sc.rowptr, no[d]), cnt_tab[:, col[d]], -eo[r], ("csr.rowptr", r), col[d], 1, None, cr_, 0,
+                 COPY_I32_ADD),
+                (P(ss.rowptr, no[s_]), cnt_tab[:, col[s_]], -eo[r], ("csc.rowptr", r), col[s_], 1, None, cr_, 0,
+                 COPY_I32_ADD),
+            ]
+        tab = {
+            "col": col, "cnt": cnt_tab,
+            "src": np.stack([q[0] for q in spec], 1), "count": np.stack([q[1] for q in spec], 1),
+            "shift": np.stack([q[2] for q in spec], 1),
+            "dsel": [q[3] for q in spec], "dcol": np.array([q[4] for q in spec]),
+            "dmul": np.array([q[5] for q in spec], dtype=np.int64), "csel": [q[6] for q in spec],
+            "acol": np.array([max(q[7], 0) for q in spec]), "amask": np.array([int(q[7] >= 0) for q in spec]),
+            "jadd": np.array([q[8] for q in spec], dtype=np.int64), "kind": np.array([q[9] for q in spec]),
+        }
+        self._tpl = tab
+        return tab
 
-        arr = np.zeros(len(descs), dtype=DESC_DTYPE)
-        if descs:
-            cols = list(zip(*descs))
-            for name, vals in zip(("src", "dst", "count", "add", "kind"), cols):
-                arr[name] = vals
+    def _launch(self, ids, nodes, edges, b_node, b_edge, x_out, batch_out, y_out, ei_out, csr_out, csc_out,
+                m_valid, goff=None, cap_graphs: int = 0) -> None:
+        """One batched-copy launch filling the output buffers with the graphs ``ids``."""
+        arr = self._descriptors(ids, x_out, batch_out, y_out, ei_out, csr_out, csc_out, m_valid, goff, cap_graphs)
         host = torch.from_numpy(arr.view(np.uint8)).pin_memory()
         dev_desc = host.to(self.device, non_blocking=True)
         max_count = int(arr["count"].max()) if len(arr) else 0
         _lib.call("hgin_batched_copy", ops._p(dev_desc), len(arr), max_count, ops._stream(dev_desc))
+
+    def _descriptors(self, ids, x_out, batch_out, y_out, ei_out, csr_out, csc_out, m_valid, goff=None,
+                     cap_graphs: int = 0) -> np.ndarray:
+        """The copy descriptors of a batch: the per-graph descriptor groups of ``_template`` shifted by the batch
+        offsets, then the tail fills (padding rows' rowptr, m_valid, the per-graph offsets)."""
+        tab = self._template()
+        ids = np.asarray(ids, dtype=np.int64)
+        J = len(ids)
+        C = tab["cnt"][ids]
+        B = np.cumsum(C, 0) - C                      # batch offset of graph j, per node type / relation
+        tot = C.sum(0)
+        col = tab["col"]
+        outs = {"x": x_out, "batch": batch_out, "y": {None: y_out}, "ei": ei_out,
+                "csr.col": {r: c.col for r, c in csr_out.items()}, "csr.perm": {r: c.perm for r, c in csr_out.items()},
+                "csr.rowptr": {r: c.rowptr for r, c in csr_out.items()},
+                "csc.col": {r: c.col for r, c in csc_out.items()}, "csc.perm": {r: c.perm for r, c in csc_out.items()},
+                "csc.rowptr": {r: c.rowptr for r, c in csc_out.items()}}
+        dts = [outs[a][b] for a, b in tab["dsel"]]
+        dbase = np.array([t.data_ptr() for t in dts], dtype=np.int64)
+        des = np.array([t.element_size() for t in dts], dtype=np.int64)
+        dconst = np.array([dts[k].shape[1] if c == "e_cap" else 0 for k, c in enumerate(tab["csel"])],
+                          dtype=np.int64)
+        main = np.zeros((J, len(dts)), dtype=DESC_DTYPE)
+        main["src"] = tab["src"][ids]
+        main["count"] = tab["count"][ids]
+        main["dst"] = dbase + (B[:, tab["dcol"]] * tab["dmul"] + dconst) * des
+        main["add"] = tab["shift"][ids] + B[:, tab["acol"]] * tab["amask"] + np.arange(J)[:, None] * tab["jadd"]
+        main["kind"] = tab["kind"]
+        tail = []
+        for r in self.relations:
+            s_, _, d = r
+            E, n_s, n_d = int(tot[col[r]]), int(tot[col[s_]]), int(tot[col[d]])
+            cr, cc = csr_out[r].rowptr, csc_out[r].rowptr
+            # rowptr[n .. capacity] = E: the last row's end, and empty rows for padding vertices
+            tail.append((0, cr.data_ptr() + 4 * n_d, cr.numel() - n_d, E, FILL_I32))
+            tail.append((0, cc.data_ptr() + 4 * n_s, cc.numel() - n_s, E, FILL_I32))
+        if m_valid is not None:
+            tail.append((0, m_valid.data_ptr(), 1, int(tot[col["path"]]), FILL_I32))
+        if goff is not None:   # graph j's rows of type t: [goff[t][j], goff[t][j + 1]); graphs past the batch: empty
+            for ti, t in enumerate(("path", "link", "node")):
+                if t in col:
+                    offs = np.concatenate([[0], np.cumsum(C[:, col[t]])])
+                    for j in range(cap_graphs + 1):
+                        tail.append((0, goff.data_ptr() + 4 * (ti * (cap_graphs + 1) + j), 1,
+                                     int(offs[min(j, J)]), FILL_I32))
+        ta = np.zeros(len(tail), dtype=DESC_DTYPE)
+        if tail:
+            for k, name in enumerate(("src", "dst", "count", "add", "kind")):
+                ta[name] = [q[k] for q in tail]
+        return np.concatenate([main.reshape(-1), ta])
 
 
 @dataclass

@@ -414,7 +414,7 @@ int hgin_gat_wsum_f32(const float* x, int64_t ldx, int64_t n, int64_t H, int64_t
                       void* workspace, size_t workspace_bytes, void* stream);
 
 /* ---- F1: the fused small-batch train step (the reference's real loop: batches of small graphs) -------------------
- * hgin_sb_step: a HetroGIN forward + sqrt-MAPE backward over a padded batch in 5 L + 1 launches
+ * hgin_sb_step: a HetroGIN forward + sqrt-MAPE backward over a padded batch in 3 L + 1 launches
  * (csrc/hgin_smallbatch.hip); args points to the host-filled SbArgs struct (hgin/smallbatch.py mirrors its layout;
  * hgin_sb_args_size() = its size), readout_lds = hgin_sb_readout_lds_bytes(..., with_weights = args' ro_wlds, ...):
  * the readout tile's dynamic LDS, with the hidden readout weights staged or not.  Writes every parameter gradient

@@ -1,5 +1,5 @@
 """The fused small-batch train step (hgin/smallbatch.py, csrc/hgin_smallbatch.hip): the reference's real loop
-(dataset.py:26, :239-244; train.py:25-44) in four launches + Adam per batch, against the general path — eager exact-
+(dataset.py:26, :239-244; train.py:25-44) in 3 L + 1 launches + Adam per batch, against the general path — eager exact-
 batch steps through the per-op HIP kernels (hgin.train.train_step), which are themselves pinned to the reference
 fixtures (tests/test_gpu_model.py).  Same batches, same initial parameters: loss values within 1e-5 relative, the
 gradients within 1e-5 of their norm (the fused kernels re-associate the GEMM-shaped sums and apply the sqrt-MAPE scale

@@ -79,3 +79,99 @@ def test_normalize_reference_equals_reference_executed_fixture():
     for t in x:
         assert torch.equal(out[t], fx[f"out.x.{t}"]), t
         assert torch.equal(x[t], fx[f"in.x.{t}"]), t           # the input dict is not modified
+
+
+def _emulate_batched_copy(arr):
+    """csrc/hgin_collate.hip's hgin_batched_copy restated on host memory (CPU tensors' addresses)."""
+    from hgin import store
+    size = {store.COPY_F32: 4, store.COPY_B16: 2, store.COPY_I32_ADD: 4, store.COPY_I64_ADD: 8,
+            store.FILL_I64: 8, store.FILL_I32: 4}
+    ctype = {4: ctypes.c_int32, 8: ctypes.c_int64, 2: ctypes.c_int16}
+    for d in arr:
+        n, k, add = int(d["count"]), int(d["kind"]), int(d["add"])
+        if n == 0:
+            continue
+        ct = ctype[size[k]]
+        dst = np.ctypeslib.as_array((ct * n).from_address(int(d["dst"])))
+        if k in (store.FILL_I64, store.FILL_I32):
+            dst[:] = add
+            continue
+        src = np.ctypeslib.as_array((ct * n).from_address(int(d["src"])))
+        dst[:] = src + add if k in (store.COPY_I32_ADD, store.COPY_I64_ADD) else src
+
+
+def test_batch_descriptors_fill_the_padded_batch():
+    """The per-graph descriptor tables (GraphStore._template / _descriptors) against the collation they stand for:
+    host tensors stand in for device buffers and the batched copy is emulated on them; every buffer of the padded
+    batch equals the graphs' rows concatenated with the batch's index shifts (PyG's collate, hgin.data.collate)."""
+    from hgin import ops
+    rng = np.random.default_rng(0)
+    types = ("path", "link", "node")
+    rels = (("path", "uses", "link"), ("link", "includes", "path"), ("node", "has", "link"))
+    G = 5
+    nc = {t: rng.integers(0, 6, G) for t in types}
+    nc["path"][0] = 3
+    ec = {r: rng.integers(0, 9, G) for r in rels}
+    node_off = {t: np.concatenate([[0], np.cumsum(c)]).astype(np.int64) for t, c in nc.items()}
+    edge_off = {r: np.concatenate([[0], np.cumsum(c)]).astype(np.int64) for r, c in ec.items()}
+    x = {t: torch.randn(int(node_off[t][-1]), 3) for t in types}
+    y = torch.rand(int(node_off["path"][-1]))
+    ei, csr, csc = {}, {}, {}
+    for r in rels:
+        s, _, d = r
+        E = int(edge_off[r][-1])
+        ei[r] = torch.randint(0, 50, (2, E))
+        csr[r] = ops.Csr(torch.randint(0, 50, (int(node_off[d][-1]) + 1,), dtype=torch.int32),
+                         torch.randint(0, 50, (E,), dtype=torch.int32), torch.randint(0, 50, (E,), dtype=torch.int32),
+                         int(node_off[d][-1]), int(node_off[s][-1]))
+        csc[r] = ops.Csr(torch.randint(0, 50, (int(node_off[s][-1]) + 1,), dtype=torch.int32),
+                         torch.randint(0, 50, (E,), dtype=torch.int32), torch.randint(0, 50, (E,), dtype=torch.int32),
+                         int(node_off[s][-1]), int(node_off[d][-1]))
+    st = GraphStore(x, y, ei, node_off, edge_off, csr, csc)
+    cap = 4
+    cap_n = {t: int(cap * nc[t].max()) for t in types}
+    cap_e = {r: int(cap * ec[r].max()) for r in rels}
+    for ids in ([2, 0, 2], [4], [1, 3, 0, 2]):
+        xo = {t: torch.full((cap_n[t], 3), -7.0) for t in types}
+        bo = {t: torch.full((cap_n[t],), -7, dtype=torch.long) for t in types}
+        yo = torch.full((cap_n["path"],), -7.0)
+        eo = {r: torch.full((2, cap_e[r]), -7, dtype=torch.long) for r in rels}
+        mk = lambda n, e: ops.Csr(torch.full((n + 1,), -7, dtype=torch.int32), torch.full((e,), -7, dtype=torch.int32),  # noqa: E731
+                                  torch.full((e,), -7, dtype=torch.int32), n, 0)
+        cro = {r: mk(cap_n[r[2]], cap_e[r]) for r in rels}
+        cco = {r: mk(cap_n[r[0]], cap_e[r]) for r in rels}
+        mv = torch.zeros(1, dtype=torch.int32)
+        goff = torch.full((3 * (cap + 1),), -7, dtype=torch.int32)
+        _emulate_batched_copy(st._descriptors(ids, xo, bo, yo, eo, cro, cco, mv, goff, cap))
+        b = {t: np.concatenate([[0], np.cumsum([nc[t][g] for g in ids])]) for t in types}
+        be = {r: np.concatenate([[0], np.cumsum([ec[r][g] for g in ids])]) for r in rels}
+        for t in types:
+            n = int(b[t][-1])
+            want = torch.cat([x[t][node_off[t][g]:node_off[t][g + 1]] for g in ids])
+            assert torch.equal(xo[t][:n], want), t
+            assert bo[t][:n].tolist() == [j for j, g in enumerate(ids) for _ in range(nc[t][g])]
+            assert (xo[t][n:] == -7).all()
+        assert torch.equal(yo[:int(b["path"][-1])], torch.cat([y[node_off["path"][g]:node_off["path"][g + 1]]
+                                                                for g in ids]))
+        assert mv.item() == b["path"][-1]
+        for ti, t in enumerate(types):
+            assert goff[ti * (cap + 1):(ti + 1) * (cap + 1)].tolist() == [int(b[t][min(j, len(ids))])
+                                                                          for j in range(cap + 1)]
+        for r in rels:
+            s, _, d = r
+            E = int(be[r][-1])
+            seg = lambda g: slice(int(edge_off[r][g]), int(edge_off[r][g + 1]))  # noqa: E731
+            sh = lambda t, j, g: int(b[t][j] - node_off[t][g])  # noqa: E731
+            want_ei = torch.cat([ei[r][:, seg(g)] + torch.tensor([[sh(s, j, g)], [sh(d, j, g)]])
+                                 for j, g in enumerate(ids)], 1)
+            assert torch.equal(eo[r][:, :E], want_ei), r
+            for out, src, shc, rt in ((cro[r], csr[r], s, d), (cco[r], csc[r], d, s)):
+                assert out.col[:E].tolist() == [int(v) + sh(shc, j, g) for j, g in enumerate(ids)
+                                                for v in src.col[seg(g)]]
+                assert out.perm[:E].tolist() == [int(v) + int(be[r][j] - edge_off[r][g]) for j, g in enumerate(ids)
+                                                 for v in src.perm[seg(g)]]
+                n = int(b[rt][-1])
+                assert out.rowptr[:n].tolist() == [int(v) + int(be[r][j] - edge_off[r][g])
+                                                   for j, g in enumerate(ids)
+                                                   for v in src.rowptr[node_off[rt][g]:node_off[rt][g + 1]]]
+                assert (out.rowptr[n:] == E).all()

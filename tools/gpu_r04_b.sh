@@ -17,7 +17,7 @@ run() {  # name, limit, command...
 }
 echo "start $(date)" > "$OUT/status.txt"
 if [ "${SB:-1}" = "1" ]; then   # the fused small-batch step: parity, then its profile
-  run pytest_sb 300 python -u -m pytest tests/test_gpu_smallbatch.py -q --timeout 120 --timeout-method thread
+  run pytest_sb 300 python -u -m pytest tests/test_gpu_smallbatch.py tests/test_gpu_store.py -q --timeout 120 --timeout-method thread
   tail -2 "$OUT/pytest_sb.out"
   run prof_batches 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_batches" -o run -- \
     python3 tools/batches_prof.py --steps 100
