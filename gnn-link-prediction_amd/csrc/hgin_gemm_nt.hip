@@ -1676,6 +1676,223 @@ int launch_ws32(const WsArgs32& a, hipStream_t s, const char* what, int64_t* gri
   return check_launch(what);
 }
 
+// k_wss_f32 — k_ws_f32's forward (EPI 1, K = N = 256) as a two-stage software pipeline with the two waves of a SIMD
+// staggered (default; HGIN_WS_STAGGER = 0 keeps k_ws_f32; k_wsp_f32's schedule applied to the forward): iteration i runs the MFMAs of block i
+// on plane buffer i & 1 and the split of block i + 1 into buffer (i + 1) & 1, one barrier per block.  Waves 0-3
+// (one per SIMD) run the epilogue of block i - 1 and the split of block i + 1, then their MFMAs; waves 4-7 run their
+// MFMAs first, then the epilogue of block i and the split — so each SIMD's VALU work sits beside the other wave's
+// MFMAs instead of every wave splitting, then multiplying, then storing in lockstep.
+//   * LDS: one 32 KB fp32 A slot in per-wave slices (a thread splits exactly the 64 B its own wave's DMA wrote, so a
+//     wave waits only on its own vmcnt and refills its slice right after reading it) + two 48 KB plane buffers;
+//   * the epilogue works from the accumulator registers: lane (li, lh) holds column 32 w + li of rows
+//     (e & 3) + 8 (e >> 2) + 4 lh — the bias is one register, the accum rows are read straight from HBM, and y / z
+//     go out as 32-lane 128-B row segments (no staging: the LDS holds the two plane buffers);
+//   * same W fragments, A fragments, product order and epilogue arithmetic as k_ws_f32: bit-identical results.
+template <bool kR1, bool kZ>
+__global__ __launch_bounds__(512, 1) void k_wss_f32(WsArgs32 g) {
+  using C = Ws32Cfg<256, 256>;
+  constexpr int K = 256, N = 256;
+  constexpr int PLANES = 3 * C::PL;                                // one plane buffer
+  constexpr int PL0 = C::A_BYTES;                                  // plane buffers follow the A slot
+  static_assert(C::BM == 32 && C::NW == 8 && C::G4 == 4 && C::PA == 4, "one 4 KB slice and 4 split groups per wave");
+  extern __shared__ __attribute__((aligned(16))) char wss_smem[];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int li = lane & 31;
+  const int lh = lane >> 5;
+  const int64_t M = g.M;
+  const int64_t nblk = (M + C::BM - 1) / C::BM;
+  const int64_t G = gridDim.x;
+  if ((int64_t)blockIdx.x >= nblk) return;
+  const int64_t my = (nblk - 1 - blockIdx.x) / G + 1;
+
+  uint4 wf[C::KS][3];   // W[32 wave + li][16 t + 8 lh .. + 7] as three bf16 planes (k_ws_f32's B fragments)
+  {
+    const float* wr = g.w + (int64_t)(wave * 32 + li) * K + lh * 8;
+#pragma unroll
+    for (int t = 0; t < C::KS; ++t) {
+      const float4 v0 = *reinterpret_cast<const float4*>(wr + t * 16);
+      const float4 v1 = *reinterpret_cast<const float4*>(wr + t * 16 + 4);
+      uint2 o0[3], o1[3];
+      split4(v0, o0);
+      split4(v1, o1);
+#pragma unroll
+      for (int p = 0; p < 3; ++p) wf[t][p] = make_uint4(o0[p].x, o0[p].y, o1[p].x, o1[p].y);
+    }
+  }
+  const float bcol = g.bias[wave * 32 + li];
+  const float a_slope = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(g.prelu[0])));
+#pragma unroll
+  for (int t = 0; t < C::KS; ++t)
+#pragma unroll
+    for (int p = 0; p < 3; ++p) asm volatile("" ::"v"(wf[t][p].x), "v"(wf[t][p].y), "v"(wf[t][p].z), "v"(wf[t][p].w));
+
+  auto tid_o = [&]() {
+    int t;
+    asm volatile("v_mov_b32 %0, %1" : "=v"(t) : "v"(tid));
+    return t;
+  };
+  auto issue = [&](int64_t i) {   // this wave's 4 KB slice of block i's A rows
+    const int64_t r0 = ((int64_t)blockIdx.x + i * G) * C::BM;
+    const int rmax = (int)(M - 1 - r0 < C::BM ? M - 1 - r0 : C::BM - 1);
+    const float* ab = g.a + r0 * g.lda;
+    const int ln = tid_o() & 63;
+#pragma unroll
+    for (int q = 0; q < C::PA; ++q) {
+      const int piece = wave * C::PA + q;
+      const int off = piece * 1024 + ln * 16;
+      int r = off / (K * 4);
+      r = r < rmax ? r : rmax;
+      const float* src = ab + (r * (int)g.lda + (off % (K * 4)) / 4);
+      if (g.nt_in) glds16_asm<true>(src, wss_smem + piece * 1024); else glds16_asm(src, wss_smem + piece * 1024);
+    }
+  };
+  // block j (in this wave's slice) -> plane buffer j & 1; the slice is then refilled with block j + 1
+  auto split = [&](int64_t j) {
+    wait_vm<0>();
+    char* pl = wss_smem + PL0 + (int)(j & 1) * PLANES;
+    const int ln = tid_o() & 63;
+    float4 v[C::G4];
+#pragma unroll
+    for (int q = 0; q < C::G4; ++q) v[q] = *reinterpret_cast<const float4*>(wss_smem + (wave * C::PA + q) * 1024 + ln * 16);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (j + 1 < my) issue(j + 1);
+#pragma unroll
+    for (int q = 0; q < C::G4; ++q) {
+      const int grp = ((wave * C::PA + q) * 1024 + ln * 16) / 16;
+      const int r = grp / (K / 4), k = (grp % (K / 4)) * 4;
+      uint2 o[3];
+      split4(v[q], o);
+      const int off = r * C::PROW + 16 * ((k >> 3) ^ (r & C::SW)) + 8 * ((k >> 2) & 1);
+#pragma unroll
+      for (int p = 0; p < 3; ++p) *reinterpret_cast<uint2*>(pl + p * C::PL + off) = o[p];
+    }
+  };
+  f32x16 acc;
+  auto mfma = [&](int64_t i) {   // k_ws_f32's fragments and product order
+    const char* planes = wss_smem + PL0 + (int)(i & 1) * PLANES;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) acc[e] = 0.0f;
+    const int fl = tid_o() & 63;
+    const int frow = (fl & 31) * C::PROW;
+    const int fsw = ((fl >> 5) ^ (fl & 31)) & C::SW;
+    auto frag = [&](int t, uint4 (&f)[3]) {
+      const int off = frow + ((2 * t ^ fsw) << 4);
+      f[0] = *reinterpret_cast<const uint4*>(planes + off);
+      f[1] = *reinterpret_cast<const uint4*>(planes + C::PL + off);
+      f[2] = *reinterpret_cast<const uint4*>(planes + 2 * C::PL + off);
+    };
+    uint4 fa[2][3];
+    frag(0, fa[0]);
+#pragma unroll
+    for (int t = 0; t < C::KS; ++t) {
+      if (t + 1 < C::KS) frag(t + 1, fa[(t + 1) & 1]);
+      const uint4(&f)[3] = fa[t & 1];
+      const bf16x8 a0 = __builtin_bit_cast(bf16x8, f[0]), a1 = __builtin_bit_cast(bf16x8, f[1]),
+                   a2 = __builtin_bit_cast(bf16x8, f[2]);
+      const bf16x8 b0 = __builtin_bit_cast(bf16x8, wf[t][0]), b1 = __builtin_bit_cast(bf16x8, wf[t][1]),
+                   b2 = __builtin_bit_cast(bf16x8, wf[t][2]);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a2, b0, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b1, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b2, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b0, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b1, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b0, acc, 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+  // epilogue<1> of block i from the accumulators: z = acc + b, y = prelu(z) [+ accum].  Buffer loads / stores from
+  // the block's row base (SGPR resources) with one lane offset: no per-row 64-bit addresses held in VGPRs.
+  auto epilogue = [&](int64_t i) {
+    const int64_t r0 = ((int64_t)blockIdx.x + i * G) * C::BM;
+    const int nr = M - r0 < C::BM ? (int)(M - r0) : C::BM;
+    constexpr int kRsrc = 0x00020000;
+    const auto ry = __builtin_amdgcn_make_buffer_rsrc(g.y + r0 * N, 0, C::BM * N * 4, kRsrc);
+    const auto rz = __builtin_amdgcn_make_buffer_rsrc(kZ ? g.z + r0 * N : g.y, 0, C::BM * N * 4, kRsrc);
+    const auto ra = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(kR1 ? g.r1 + r0 * N : g.y), 0,
+                                                      C::BM * N * 4, kRsrc);
+    const int vo = (4 * lh * N + wave * 32 + li) * 4;
+    float in1[16];
+    if constexpr (kR1) {
+#pragma unroll
+      for (int e = 0; e < 16; ++e)
+        in1[e] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(ra, vo, ((e & 3) + 8 * (e >> 2)) * N * 4, 0));
+    }
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      const int row = (e & 3) + 8 * (e >> 2) + 4 * lh;
+      const int so = ((e & 3) + 8 * (e >> 2)) * N * 4;
+      const float zz = __fadd_rn(acc[e], bcol);
+      const float y = zz > 0.0f ? zz : __fmul_rn(a_slope, zz);
+      const float o = kR1 ? __fadd_rn(in1[e], y) : y;
+      if (row < nr) {
+        if (g.nt_io) {
+          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(o), ry, vo, so, 2);
+          if constexpr (kZ) __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(zz), rz, vo, so, 2);
+        } else {
+          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(o), ry, vo, so, 0);
+          if constexpr (kZ) __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(zz), rz, vo, so, 0);
+        }
+      }
+    }
+  };
+
+  issue(0);
+  split(0);
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  // one loop per wave group (the same barrier count: s_barrier counts arrivals, not program points), so the
+  // accumulators are dead during each group's split
+  if (wave < 4) {
+    for (int64_t i = 0; i < my; ++i) {
+      __builtin_amdgcn_s_barrier();   // block i's planes written by every wave; block i - 1's read by every wave
+      asm volatile("" ::: "memory");
+      if (i > 0) epilogue(i - 1);
+      if (i + 1 < my) split(i + 1);
+      mfma(i);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // this wave's plane writes and fragment reads are done
+    }
+    epilogue(my - 1);
+  } else {
+    for (int64_t i = 0; i < my; ++i) {
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      mfma(i);
+      epilogue(i);
+      if (i + 1 < my) split(i + 1);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    }
+  }
+}
+
+// HGIN_WS_STAGGER = 0 keeps k_ws_f32.  Default on: fwd256 at M = 6M 4.95 -> 4.49 ms per launch, the cfg3 step
+// 183.3 -> 179.4 ms (profiles/r04/gpu_s).
+bool wss_enabled() {
+  static const bool on = [] {
+    const char* v = getenv("HGIN_WS_STAGGER");
+    return !(v && v[0] == '0');
+  }();
+  return on;
+}
+
+template <bool kR1, bool kZ>
+int launch_wss(const WsArgs32& a, hipStream_t s, const char* what) {
+  constexpr int lds = Ws32Cfg<256, 256>::A_BYTES + 2 * 3 * Ws32Cfg<256, 256>::PL;
+  static_assert(lds <= 160 * 1024, "LDS");
+  auto kern = k_wss_f32<kR1, kZ>;
+  static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                                                     hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+  if (attr != hipSuccess) {
+    set_error("%s: hipFuncSetAttribute failed: %s", what, hipGetErrorString(attr));
+    return (int)attr;
+  }
+  const int64_t nblk = ceil_div(a.M, (int64_t)Ws32Cfg<256, 256>::BM);
+  const int64_t grid = nblk < ws_grid() ? nblk : ws_grid();
+  HGIN_TRACE("k_wss_f32<%d,%d>", (int)kR1, (int)kZ);
+  kern<<<(unsigned)grid, 512, lds, s>>>(a);
+  return check_launch(what);
+}
+
 // k_wsf_f32 — k_ws_f32 (K = N = 256; EPI 1, and EPI 4 without g_prev) with one wave per SIMD and the split of the
 // next block placed between this block's MFMAs (HGIN_WS_PIPE = 1):
 //   * 4 waves, each holding W rows 64 w .. 64 w + 63 as split B fragments: 384 registers, which one wave per SIMD can
@@ -1975,6 +2192,12 @@ int try_ws_f32(const float* a1, int64_t lda1, int64_t k1, const float* a2_eps, c
     if (accum) return launch_wsf<1, true, false>(g, s, what);
     if (z) return launch_wsf<1, false, true>(g, s, what);
     return launch_wsf<1, false, false>(g, s, what);
+  }
+  if (wss_enabled()) {
+    if (accum && z) return launch_wss<true, true>(g, s, what);
+    if (accum) return launch_wss<true, false>(g, s, what);
+    if (z) return launch_wss<false, true>(g, s, what);
+    return launch_wss<false, false>(g, s, what);
   }
   if (accum && z) return launch_ws32<256, 256, 1, true, true, false>(g, s, what);
   if (accum) return launch_ws32<256, 256, 1, true, false, false>(g, s, what);

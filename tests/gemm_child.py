@@ -59,7 +59,7 @@ def run(M, K, N, with_acc, save_z, k1, eps=None, *, g):
 F32_CASES = [  # (M, K, N, accum, save_z) — fp32 forward (split mode: k_ws_f32 at K = N = 256 by default)
     (300_007, 256, 256, True, True), (1, 256, 256, True, True), (31, 256, 256, False, True),
     (70_001, 256, 256, True, False), (65, 128, 128, False, False), (20_000, 128, 128, True, True),
-    (40_000, 512, 256, True, True),
+    (40_000, 512, 256, True, True), (1_025, 256, 256, False, False),
     (200_003, 512, 256, True, True),   # enough row tiles for the 128-row tiles (+ B planes by LDS-DMA / the 128 x 256 tile)
 ]
 

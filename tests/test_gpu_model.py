@@ -56,7 +56,7 @@ def _layer_input(fx, li, key, n_src):
 
 # the kernels the headline width runs (K = 512 first layer, K = N = 256 above it), as trace tags
 W256_KERNELS = (r"k_gemm_nt<EPI1,\d+x\d+,split,N256,K512>",                # first layer forward (eps-scaled self half)
-                r"k_ws_f32<256,256,EPI1>",                                  # layers 1-2 forward
+                r"k_ws(s_f32<[01],[01]>|_f32<256,256,EPI1>)",              # layers 1-2 forward (staggered)
                 r"k_ws[dp]_f32<256,256,prelu_bwd_fused>",                   # dW + PReLU bwd (g_z out): every layer
                 r"k_ws[dp]_f32<256,256>",                                   # first layer dW, columns [256, 512)
                 r"k_ws_f32<256,256,EPI4>")                                  # layers 1-2 dX + self-term backward
