@@ -653,7 +653,7 @@ def main():
                                                     f"({os.path.relpath(tf, ROOT)}), not counters of this run")
             gemm = gemm_fields(s.get("gin_mlp"), bf16, steps_recorded, t_step, "forward MLP GEMM "
                                f"(hgin_gin_mlp_fwd_{'bf16' if bf16 else 'f32'}: "
-                               f"{'k_ws_bf16 / k_gemm_nt_bf16' if bf16 else 'k_ws_f32 / k_gemm_nt'} + bias / PReLU / "
+                               f"{'k_ws_bf16 / k_gemm_nt_bf16' if bf16 else 'k_wss_f32 / k_ws_f32 / k_gemm_nt'} + bias / PReLU / "
                                f"accum epilogue)")
             gemm_dw = gemm_fields(s.get("gemm_dw"), bf16, steps_recorded, t_step,
                                   "weight-gradient GEMMs (hgin_gin_mlp_bwd_w_* / hgin_gemm_tn_*, incl. the fused or "
