@@ -1804,21 +1804,20 @@ __global__ __launch_bounds__(512, 1) void k_wss_f32(WsArgs32 g) {
   };
   // epilogue<1> of block i from the accumulators: z = acc + b, y = prelu(z) [+ accum].  Buffer loads / stores from
   // the block's row base (SGPR resources) with one lane offset: no per-row 64-bit addresses held in VGPRs.
-  auto epilogue = [&](int64_t i) {
+  constexpr int kRsrc = 0x00020000;
+  const int vo = (4 * lh * N + wave * 32 + li) * 4;
+  auto load_r1 = [&](int64_t i, float (&in1)[16]) {   // block i's accum rows at this lane's 16 outputs
+    const int64_t r0 = ((int64_t)blockIdx.x + i * G) * C::BM;
+    const auto ra = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(g.r1 + r0 * N), 0, C::BM * N * 4, kRsrc);
+#pragma unroll
+    for (int e = 0; e < 16; ++e)
+      in1[e] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(ra, vo, ((e & 3) + 8 * (e >> 2)) * N * 4, 0));
+  };
+  auto epilogue = [&](int64_t i, const float (&in1)[16]) {
     const int64_t r0 = ((int64_t)blockIdx.x + i * G) * C::BM;
     const int nr = M - r0 < C::BM ? (int)(M - r0) : C::BM;
-    constexpr int kRsrc = 0x00020000;
     const auto ry = __builtin_amdgcn_make_buffer_rsrc(g.y + r0 * N, 0, C::BM * N * 4, kRsrc);
     const auto rz = __builtin_amdgcn_make_buffer_rsrc(kZ ? g.z + r0 * N : g.y, 0, C::BM * N * 4, kRsrc);
-    const auto ra = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(kR1 ? g.r1 + r0 * N : g.y), 0,
-                                                      C::BM * N * 4, kRsrc);
-    const int vo = (4 * lh * N + wave * 32 + li) * 4;
-    float in1[16];
-    if constexpr (kR1) {
-#pragma unroll
-      for (int e = 0; e < 16; ++e)
-        in1[e] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(ra, vo, ((e & 3) + 8 * (e >> 2)) * N * 4, 0));
-    }
 #pragma unroll
     for (int e = 0; e < 16; ++e) {
       const int row = (e & 3) + 8 * (e >> 2) + 4 * lh;
@@ -1843,22 +1842,31 @@ __global__ __launch_bounds__(512, 1) void k_wss_f32(WsArgs32 g) {
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   // one loop per wave group (the same barrier count: s_barrier counts arrivals, not program points), so the
   // accumulators are dead during each group's split
+  // (with an accum stream, waves 0-3 read block i's accum rows right after its MFMAs — in flight across the barrier,
+  // consumed by the epilogue at the top of the next iteration — and waves 4-7 between their MFMAs and epilogue)
+  float in1[16];
+#pragma unroll
+  for (int e = 0; e < 16; ++e) in1[e] = 0.0f;
   if (wave < 4) {
     for (int64_t i = 0; i < my; ++i) {
       __builtin_amdgcn_s_barrier();   // block i's planes written by every wave; block i - 1's read by every wave
       asm volatile("" ::: "memory");
-      if (i > 0) epilogue(i - 1);
+      if (i > 0) epilogue(i - 1, in1);
       if (i + 1 < my) split(i + 1);
       mfma(i);
+      __builtin_amdgcn_sched_barrier(0);
+      if constexpr (kR1) load_r1(i, in1);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // this wave's plane writes and fragment reads are done
     }
-    epilogue(my - 1);
+    epilogue(my - 1, in1);
   } else {
     for (int64_t i = 0; i < my; ++i) {
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
       mfma(i);
-      epilogue(i);
+      __builtin_amdgcn_sched_barrier(0);
+      if constexpr (kR1) load_r1(i, in1);
+      epilogue(i, in1);
       if (i + 1 < my) split(i + 1);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     }
@@ -1871,6 +1879,14 @@ bool wss_enabled() {
   static const bool on = [] {
     const char* v = getenv("HGIN_WS_STAGGER");
     return !(v && v[0] == '0');
+  }();
+  return on;
+}
+
+bool wss_acc_enabled() {   // HGIN_WS_STAGGER_ACC = 1: the staggered form also for the accumulating forward
+  static const bool on = [] {
+    const char* v = getenv("HGIN_WS_STAGGER_ACC");
+    return v && v[0] == '1';
   }();
   return on;
 }
@@ -2193,9 +2209,13 @@ int try_ws_f32(const float* a1, int64_t lda1, int64_t k1, const float* a2_eps, c
     if (z) return launch_wsf<1, false, true>(g, s, what);
     return launch_wsf<1, false, false>(g, s, what);
   }
-  // the staggered form where it measured faster: without an accum stream (with one, its accum rows are read in the
-  // epilogue at HBM latency: 2.81 vs 2.67 ms per launch at M = 3M, profiles/r04/final)
-  if (wss_enabled() && !accum) {
+  // the staggered form where it measured faster: without an accum stream.  With one (HGIN_WS_STAGGER_ACC = 1) its
+  // accum rows come in as 4-byte lane loads in the accumulator layout: 6.94 vs k_ws_f32's 5.73 ms per launch at
+  // M = 6M even with waves 0-3 loading them across the barrier (profiles/r04/gpu_q; 2.81 vs 2.67 ms at M = 3M when
+  // read in the epilogue, profiles/r04/final)
+  if (wss_enabled() && (!accum || wss_acc_enabled())) {
+    if (accum && z) return launch_wss<true, true>(g, s, what);
+    if (accum) return launch_wss<true, false>(g, s, what);
     if (z) return launch_wss<false, true>(g, s, what);
     return launch_wss<false, false>(g, s, what);
   }

@@ -17,6 +17,7 @@
                               HGIN_GEMM_NT_IO=1, its precondition, so it runs at these sizes);
   * HGIN_WSD_PIPE=0         — k_wsd_f32 instead of the pipelined fp32 dW (k_wsp_f32);
   * HGIN_WS_STAGGER=0       — k_ws_f32 instead of the staggered two-stage fp32 forward (k_wss_f32);
+  * HGIN_WS_STAGGER_ACC=1   — the staggered forward also for the accumulating calls;
   (The measured-and-removed fp32 tile variants — 128 x 256 / k_nt_pipe, double-buffered B, the ping-pong k_nt_pp and
   the 16 x 16 x 32 MFMA tile — are listed in DESIGN.md §3 with their commits.)
 
@@ -41,7 +42,8 @@ SWITCHES = {"default": {}, "tiled": {"HGIN_NT_WS": "0", "HGIN_TN_WS": "0", "HGIN
             "t256_off": {"HGIN_NT_T256": "0"},
             "ws_pipe": {"HGIN_WS_PIPE": "1", "HGIN_GEMM_NT_IO": "1"},
             "wsd_pipe_off": {"HGIN_WSD_PIPE": "0"},
-            "ws_stagger_off": {"HGIN_WS_STAGGER": "0"}}
+            "ws_stagger_off": {"HGIN_WS_STAGGER": "0"},
+            "ws_stagger_acc": {"HGIN_WS_STAGGER_ACC": "1"}}
 _results = {}
 
 
@@ -65,7 +67,7 @@ def test_switch_within_tolerance(name):
 
 
 @pytest.mark.parametrize("name", ["tiled", "tiled_bk128", "tiled_nobdma", "t256_off", "ws_pipe", "wsd_pipe_off",
-                                  "ws_stagger_off"])
+                                  "ws_stagger_off", "ws_stagger_acc"])
 def test_switch_bitwise_equal_default(name):
     ref, got = _run("default"), _run(name)
     assert ref.keys() == got.keys()
