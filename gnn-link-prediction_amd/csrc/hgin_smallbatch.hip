@@ -208,8 +208,8 @@ __global__ __launch_bounds__(kSbThreads) void k_sb_fwd(SbArgs a, int l) {
   }
 }
 
-// One tile of kSbRows path rows: readout forward, loss partial, readout backward (unscaled) down to the path
-// embeddings' gradient.  Each layer's input rows and pre-activation gradient rows go to ro_in / ro_gz, from which
+// Tiles of kSbRows path rows (a grid-stride loop over the batch's tiles): readout forward, loss partial, readout
+// backward (unscaled) down to the path embeddings' gradient.  Each layer's input rows and pre-activation gradient rows go to ro_in / ro_gz, from which
 // the readout blocks of k_sb_bwd_w form the weight-gradient partials over the same row chunks as the GIN's (a tile
 // that also reduced its own rows' weight gradients spent most of its time there and left n_tiles partials to sum).
 // The hidden weights are staged in LDS when they fit (row stride K | 1: odd, so the forward's column-per-thread reads
@@ -221,9 +221,6 @@ __global__ __launch_bounds__(kSbThreads) void k_sb_readout(SbArgs a) {
   const int H = a.H;
   const int m = a.m_valid[0];
   constexpr int R = kSbRows;
-  const int r0 = blockIdx.x * R;
-  if (r0 >= m) return;
-  const int nr = m - r0 < R ? m - r0 : R;
   const int fp = a.concat_path ? a.fdim[0] : 0;
   const int w0 = H + fp;
   int win[kSbMaxHid + 1];   // input width of layer i (i = nhid: the head)
@@ -261,93 +258,100 @@ __global__ __launch_bounds__(kSbThreads) void k_sb_readout(SbArgs a) {
   float* gb1 = p + R * maxw;
   float* outv = gb1 + R * maxw;   // [R]
   const float* xp = a.act + a.act_off[a.L - 1][0];
-  for (int idx = tid; idx < nr * w0; idx += kSbThreads) {
-    const int rr = idx / w0, k = idx % w0;
-    const int64_t row = r0 + rr;
-    const float v = k < H ? xp[row * H + k] : a.x[0][row * a.ldx[0] + a.cols[0][k - H]];
-    in0[rr * w0 + k] = v;
-    a.ro_in[0][(int64_t)r0 * w0 + idx] = v;
-  }
-  __syncthreads();
-  const float slope = a.ro_slope[0];
-  for (int i = 0; i < a.nhid; ++i) {
-    const float* in = i == 0 ? in0 : ys[i - 1];
-    const int K = win[i], N = a.rw[i], lw = ldw[i];
-    for (int idx = tid; idx < nr * N; idx += kSbThreads) {
-      const int rr = idx / N, o = idx % N;
-      const float* wr = W[i] + (int64_t)o * lw;
-      float z = 0.0f;
-      for (int k = 0; k < K; ++k) z = fmaf(in[rr * K + k], wr[k], z);
-      z = __fadd_rn(z, a.row_b[i][o]);
-      zs[i][rr * N + o] = z;
-      const float yv = z > 0.0f ? z : __fmul_rn(slope, z);
-      ys[i][rr * N + o] = yv;
-      a.ro_in[i + 1][(int64_t)r0 * N + idx] = yv;
+  // tiles in a grid-stride loop: the weights are staged once per workgroup
+  const int ntile = (m + R - 1) / R;
+  for (int tile = blockIdx.x; tile < ntile; tile += gridDim.x) {
+    const int r0 = tile * R;
+    const int nr = m - r0 < R ? m - r0 : R;
+    __syncthreads();   // the staged weights / the previous tile's LDS reads
+    for (int idx = tid; idx < nr * w0; idx += kSbThreads) {
+      const int rr = idx / w0, k = idx % w0;
+      const int64_t row = r0 + rr;
+      const float v = k < H ? xp[row * H + k] : a.x[0][row * a.ldx[0] + a.cols[0][k - H]];
+      in0[rr * w0 + k] = v;
+      a.ro_in[0][(int64_t)r0 * w0 + idx] = v;
     }
     __syncthreads();
-  }
-  const int KL = win[a.nhid];
-  const float* yl = ys[a.nhid - 1];
-  // head + loss numerator + seed, one thread per row
-  float lp = 0.0f;
-  if (tid < nr) {
-    float o = 0.0f;
-    for (int k = 0; k < KL; ++k) o = fmaf(yl[tid * KL + k], a.head_w[k], o);
-    o = __fadd_rn(o, a.head_b[0]);
-    const float yv = a.y[r0 + tid];
-    const float u = __fdiv_rn(__fsub_rn(o, yv), yv);
-    lp = fabsf(u);
-    const float sg = u > 0.0f ? 1.0f : (u < 0.0f ? -1.0f : 0.0f);
-    const float go = __fdiv_rn(sg, yv);   // d |u| / d out
-    outv[tid] = go;
-    a.ro_gz[a.nhid][r0 + tid] = go;
-  }
-  // fixed-order tile sum of |u| (rows in order)
-  red[tid] = tid < nr ? lp : 0.0f;
-  __syncthreads();
-  if (tid == 0) {
-    float s = 0.0f;
-    for (int rr = 0; rr < nr; ++rr) s = __fadd_rn(s, red[rr]);
-    a.loss_part[blockIdx.x] = s;
-  }
-  for (int idx = tid; idx < nr * KL; idx += kSbThreads) {
-    const int rr = idx / KL, k = idx % KL;
-    gb0[rr * KL + k] = __fmul_rn(outv[rr], a.head_w[k]);
-  }
-  __syncthreads();
-  float slope_part = 0.0f;   // this thread's share of the shared slope's gradient (fixed assignment)
-  float* g_y = gb0;
-  float* g_next = gb1;
-  for (int i = a.nhid - 1; i >= 0; --i) {
-    const int K = win[i], N = a.rw[i], lw = ldw[i];
-    // g_z (in place over g_y) and the slope partial
-    for (int idx = tid; idx < nr * N; idx += kSbThreads) {
-      const float z = zs[i][idx];
-      const float g = g_y[idx];
-      if (z <= 0.0f) slope_part = fmaf(g, z, slope_part);
-      const float gz = z > 0.0f ? g : __fmul_rn(slope, g);
-      g_y[idx] = gz;
-      a.ro_gz[i][(int64_t)r0 * N + idx] = gz;
+    const float slope = a.ro_slope[0];
+    for (int i = 0; i < a.nhid; ++i) {
+      const float* in = i == 0 ? in0 : ys[i - 1];
+      const int K = win[i], N = a.rw[i], lw = ldw[i];
+      for (int idx = tid; idx < nr * N; idx += kSbThreads) {
+        const int rr = idx / N, o = idx % N;
+        const float* wr = W[i] + (int64_t)o * lw;
+        float z = 0.0f;
+        for (int k = 0; k < K; ++k) z = fmaf(in[rr * K + k], wr[k], z);
+        z = __fadd_rn(z, a.row_b[i][o]);
+        zs[i][rr * N + o] = z;
+        const float yv = z > 0.0f ? z : __fmul_rn(slope, z);
+        ys[i][rr * N + o] = yv;
+        a.ro_in[i + 1][(int64_t)r0 * N + idx] = yv;
+      }
+      __syncthreads();
     }
+    const int KL = win[a.nhid];
+    const float* yl = ys[a.nhid - 1];
+    // head + loss numerator + seed, one thread per row
+    float lp = 0.0f;
+    if (tid < nr) {
+      float o = 0.0f;
+      for (int k = 0; k < KL; ++k) o = fmaf(yl[tid * KL + k], a.head_w[k], o);
+      o = __fadd_rn(o, a.head_b[0]);
+      const float yv = a.y[r0 + tid];
+      const float u = __fdiv_rn(__fsub_rn(o, yv), yv);
+      lp = fabsf(u);
+      const float sg = u > 0.0f ? 1.0f : (u < 0.0f ? -1.0f : 0.0f);
+      const float go = __fdiv_rn(sg, yv);   // d |u| / d out
+      outv[tid] = go;
+      a.ro_gz[a.nhid][r0 + tid] = go;
+    }
+    // fixed-order tile sum of |u| (rows in order)
+    red[tid] = tid < nr ? lp : 0.0f;
     __syncthreads();
-    // g_in[k] = sum_o g_z[o] W[o][k] (the first layer: only the path embeddings' H columns have a gradient)
-    const int KG = i == 0 ? H : K;
-    for (int idx = tid; idx < nr * KG; idx += kSbThreads) {
-      const int rr = idx / KG, k = idx % KG;
+    if (tid == 0) {
       float s = 0.0f;
-      for (int o = 0; o < N; ++o) s = fmaf(g_y[rr * N + o], W[i][(int64_t)o * lw + k], s);
-      g_next[rr * KG + k] = s;
+      for (int rr = 0; rr < nr; ++rr) s = __fadd_rn(s, red[rr]);
+      a.loss_part[tile] = s;
+    }
+    for (int idx = tid; idx < nr * KL; idx += kSbThreads) {
+      const int rr = idx / KL, k = idx % KL;
+      gb0[rr * KL + k] = __fmul_rn(outv[rr], a.head_w[k]);
     }
     __syncthreads();
-    float* t = g_y;
-    g_y = g_next;
-    g_next = t;
+    float slope_part = 0.0f;   // this thread's share of the shared slope's gradient (fixed assignment)
+    float* g_y = gb0;
+    float* g_next = gb1;
+    for (int i = a.nhid - 1; i >= 0; --i) {
+      const int K = win[i], N = a.rw[i], lw = ldw[i];
+      // g_z (in place over g_y) and the slope partial
+      for (int idx = tid; idx < nr * N; idx += kSbThreads) {
+        const float z = zs[i][idx];
+        const float g = g_y[idx];
+        if (z <= 0.0f) slope_part = fmaf(g, z, slope_part);
+        const float gz = z > 0.0f ? g : __fmul_rn(slope, g);
+        g_y[idx] = gz;
+        a.ro_gz[i][(int64_t)r0 * N + idx] = gz;
+      }
+      __syncthreads();
+      // g_in[k] = sum_o g_z[o] W[o][k] (the first layer: only the path embeddings' H columns have a gradient)
+      const int KG = i == 0 ? H : K;
+      for (int idx = tid; idx < nr * KG; idx += kSbThreads) {
+        const int rr = idx / KG, k = idx % KG;
+        float s = 0.0f;
+        for (int o = 0; o < N; ++o) s = fmaf(g_y[rr * N + o], W[i][(int64_t)o * lw + k], s);
+        g_next[rr * KG + k] = s;
+      }
+      __syncthreads();
+      float* t = g_y;
+      g_y = g_next;
+      g_next = t;
+    }
+    const float sp = block_sum(slope_part, red);
+    if (tid == 0) a.slope_part[tile] = sp;
+    // the path embeddings' gradient for the GIN backward
+    float* gpath = a.gA + a.g_off[0];
+    for (int idx = tid; idx < nr * H; idx += kSbThreads) gpath[(int64_t)r0 * H + idx] = g_y[idx];
   }
-  const float sp = block_sum(slope_part, red);
-  if (tid == 0) a.slope_part[blockIdx.x] = sp;
-  // the path embeddings' gradient for the GIN backward
-  float* gpath = a.gA + a.g_off[0];
-  for (int idx = tid; idx < nr * H; idx += kSbThreads) gpath[(int64_t)r0 * H + idx] = g_y[idx];
 }
 
 // the readout blocks of k_sb_bwd_w: over row chunk p of the m valid path rows, one group of kRoJ x kSbThreads of
@@ -625,6 +629,8 @@ extern "C" int hgin_sb_step(const void* args, size_t args_bytes, size_t readout_
   }
   const unsigned fwd_blocks = (unsigned)ceil_div((int64_t)capt_max, (int64_t)kSbFwdRows);
   for (int l = 0; l < a.L; ++l) k_sb_fwd<<<dim3(fwd_blocks, 3), kSbThreads, 0, s>>>(a, l);
+  // one tile per workgroup (a grid of 512 looping over the tiles, staging the weights once each: 52.9 vs 35 us per
+  // batch, profiles/r04/gpu_r — the tiles' serial layer chains want the parallelism, not fewer weight stagings)
   k_sb_readout<<<a.n_tiles, kSbThreads, readout_lds, s>>>(a);
   float* gcur = a.gA;
   float* gnxt = a.gB;
