@@ -14,8 +14,10 @@
 //                                                                                  (k_gat_bwd_src, CSC)
 //   g_att_src[h, c] = sum_j g_a_s[j, h] x_s[j, h, c], g_att_dst likewise, g_bias = sum_i g_out[i, :]  (k_gat_wsum)
 // Deterministic: every sum runs in a fixed order (edges in CSR / CSC order = the edge list's order within a row, as
-// the reference's scatter_add; column sums by fixed row blocks, then blocks in order); no atomics.  One thread per
-// (row, head): the GAT widths are small (H * C = 64 .. 128 here), and the walk over a row's edges is short.
+// the reference's scatter_add; column sums by fixed row blocks, then blocks in order); no atomics.  Two forms: a
+// G-lane group per row with lanes across the H * C columns (the default, below: coalesced 16-B row reads, several
+// rows in flight, online softmax statistics), and one thread per (row, head) for the shapes it does not take
+// (C not a multiple of 4 with C / 4 a power of two, H * C > 256, unaligned rows; HGIN_GAT_WAVE = 0 forces it).
 #include "hgin_common.h"
 
 namespace hgin {
@@ -162,6 +164,287 @@ __global__ __launch_bounds__(256) void k_gat_wsum_final(const float* __restrict_
   out[f] = s;
 }
 
+// ---------------------------------------------------------------------------------------------------------------
+// Wave-group forms (round 5; the default wherever C % 4 == 0, C / 4 a power of two, H * C <= 256, 16-B aligned rows):
+// a G-lane group per row, G = the next power of two >= H * C / 4 (G = 32 for the reference's HEADS 16 x C 8: two rows
+// per wave), lane gl owning the float4 of columns 4 gl .. 4 gl + 3 (head hq = 4 gl / C), so every gathered x_s / g_out
+// row is one contiguous G x 16-B read and up to kGatU rows are in flight per group; the per-head work runs on the
+// group's lanes as (edge slot, head) pairs or on each head's first column lane.  No LDS, no atomics; every sum in a
+// fixed order (per-column sums over a row's edges in CSR / CSC order, as the thread-per-(row, head) kernels).
+constexpr int kGatU = 8;
+
+template <int G>
+__device__ __forceinline__ float group_sum_pow2(float v, int width) {   // xor butterfly over `width` aligned lanes
+  for (int off = 1; off < width; off <<= 1) v = __fadd_rn(v, __shfl_xor(v, off, G));
+  return v;
+}
+
+// a[n, h] = sum_c x[n, h C + c] att[h C + c]: each lane its 4 columns in order, then the head's C / 4 lanes.
+template <int G>
+__global__ __launch_bounds__(256) void k_gat_logits_w(const float* __restrict__ x, int64_t ldx, int64_t n, int H,
+                                                      int C, const float* __restrict__ att, float* __restrict__ a) {
+  const int gl = threadIdx.x % G;
+  const int64_t r = ((int64_t)blockIdx.x * 256 + threadIdx.x) / G;
+  if (r >= n) return;
+  const int HC4 = H * C / 4;
+  float s = 0.0f;
+  if (gl < HC4) {
+    const float4 v = *reinterpret_cast<const float4*>(x + r * ldx + 4 * gl);
+    const float4 w = *reinterpret_cast<const float4*>(att + 4 * gl);
+    s = __fadd_rn(__fadd_rn(__fadd_rn(__fmul_rn(v.x, w.x), __fmul_rn(v.y, w.y)), __fmul_rn(v.z, w.z)),
+                  __fmul_rn(v.w, w.w));
+  }
+  s = group_sum_pow2<G>(s, C / 4);
+  if (gl < HC4 && (4 * gl) % C == 0) a[r * H + (4 * gl) / C] = s;
+}
+
+// Forward.  Phase 1 on (slot, head) lanes (ES = G / H slots): the online max / exp-sum of the head's logits over the
+// slot's edges (rb + slot, + ES, ...), merged over the slots in slot order -> m_h, den_h = sum + 1e-16.  Phase 2 on
+// column lanes: per edge in CSR order alpha = exp(e - m_h) / den_h (stored by the head's first lane: the backward's
+// alpha) and out += x_s[j] * alpha, U rows in flight; then + bias, accum + (the thread-per-(row, head) kernel's order).
+template <int G>
+__global__ __launch_bounds__(256) void k_gat_fwd_w(const int32_t* __restrict__ rowptr, const int32_t* __restrict__ col,
+                                                   int64_t n_dst, int H, int C, const float* __restrict__ xs,
+                                                   int64_t ldxs, const float* __restrict__ as,
+                                                   const float* __restrict__ ad, float slope,
+                                                   const float* __restrict__ bias, const float* __restrict__ accum,
+                                                   int64_t ld_acc, float* __restrict__ alpha, float* __restrict__ out,
+                                                   int64_t ldo) {
+  const int gl = threadIdx.x % G;
+  const int64_t i = ((int64_t)blockIdx.x * 256 + threadIdx.x) / G;
+  if (i >= n_dst) return;
+  const int rb = rowptr[i], re = rowptr[i + 1];
+  const int ES = G / H;
+  const int slot = gl / H, h1 = gl % H;
+  float m = -INFINITY, s = 0.0f;
+  if (slot < ES) {
+    const float adv = ad ? ad[i * H + h1] : 0.0f;
+    for (int k = rb + slot; k < re; k += ES) {
+      const float e = lrelu(__fadd_rn(as[(int64_t)col[k] * H + h1], adv), slope);
+      if (e > m) {
+        s = __fadd_rn(__fmul_rn(s, expf(__fsub_rn(m, e))), 1.0f);
+        m = e;
+      } else {
+        s = __fadd_rn(s, expf(__fsub_rn(e, m)));
+      }
+    }
+  }
+  for (int q = 1; q < ES; ++q) {   // slot 0 merges slots 1 .. ES - 1 in order (every lane runs the shuffles)
+    const float m2 = __shfl(m, gl + q * H < G ? gl + q * H : gl, G);
+    const float s2 = __shfl(s, gl + q * H < G ? gl + q * H : gl, G);
+    if (slot == 0 && m2 != -INFINITY) {
+      if (m == -INFINITY) {
+        m = m2;
+        s = s2;
+      } else {
+        const float M = fmaxf(m, m2);
+        s = __fadd_rn(__fmul_rn(s, expf(__fsub_rn(m, M))), __fmul_rn(s2, expf(__fsub_rn(m2, M))));
+        m = M;
+      }
+    }
+  }
+  const float den = __fadd_rn(s, 1e-16f);
+  const int HC4 = H * C / 4;
+  const int hq = gl < HC4 ? (4 * gl) / C : 0;
+  const float mh = __shfl(m, hq, G), dh = __shfl(den, hq, G);
+  if (gl >= HC4) return;
+  const bool first = (4 * gl) % C == 0;
+  const float adq = ad ? ad[i * H + hq] : 0.0f;
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int k0 = rb; k0 < re; k0 += kGatU) {
+    const int nk = re - k0;
+    float av[kGatU];
+    float4 xv[kGatU];
+#pragma unroll
+    for (int u = 0; u < kGatU; ++u) {
+      av[u] = 0.0f;
+      xv[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (u < nk) {
+        const int64_t j = col[k0 + u];
+        av[u] = as[j * H + hq];
+        xv[u] = *reinterpret_cast<const float4*>(xs + j * ldxs + 4 * gl);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < kGatU; ++u) {
+      if (u < nk) {
+        const float e = expf(__fsub_rn(lrelu(__fadd_rn(av[u], adq), slope), mh));
+        const float al = __fdiv_rn(e, dh);
+        if (first) alpha[(int64_t)(k0 + u) * H + hq] = al;
+        acc.x = __fadd_rn(acc.x, __fmul_rn(xv[u].x, al));
+        acc.y = __fadd_rn(acc.y, __fmul_rn(xv[u].y, al));
+        acc.z = __fadd_rn(acc.z, __fmul_rn(xv[u].z, al));
+        acc.w = __fadd_rn(acc.w, __fmul_rn(xv[u].w, al));
+      }
+    }
+  }
+  if (bias) {
+    const float4 b = *reinterpret_cast<const float4*>(bias + 4 * gl);
+    acc = make_float4(__fadd_rn(acc.x, b.x), __fadd_rn(acc.y, b.y), __fadd_rn(acc.z, b.z), __fadd_rn(acc.w, b.w));
+  }
+  if (accum) {
+    const float4 c = *reinterpret_cast<const float4*>(accum + i * ld_acc + 4 * gl);
+    acc = make_float4(__fadd_rn(c.x, acc.x), __fadd_rn(c.y, acc.y), __fadd_rn(c.z, acc.z), __fadd_rn(c.w, acc.w));
+  }
+  *reinterpret_cast<float4*>(out + i * ldo + 4 * gl) = acc;
+}
+
+// Backward, destination side.  Phase A (column lanes, CSR order, U rows in flight): g_alpha_k = <g_out[i, h, :],
+// x_s[j_k, h, :]> (each lane its 4 products, then the head's C / 4 lanes), S_h = sum_k alpha_k g_alpha_k; the head's
+// first lane stores g_alpha_k.  Phase B (the head's first lane, CSR order): g_pre_k = leaky'(pre_k) alpha_k
+// (g_alpha_k - S_h) over its own stores, g_a_d = sum_k g_pre_k; g_x_d = g_a_d att_dst on the column lanes.
+template <int G>
+__global__ __launch_bounds__(256) void k_gat_bwd_dst_w(const int32_t* __restrict__ rowptr,
+                                                       const int32_t* __restrict__ col, int64_t n_dst, int H, int C,
+                                                       const float* __restrict__ xs, int64_t ldxs,
+                                                       const float* __restrict__ g_out, int64_t ldg,
+                                                       const float* __restrict__ alpha, const float* __restrict__ as,
+                                                       const float* __restrict__ ad, float slope,
+                                                       const float* __restrict__ att_dst, float* __restrict__ g_pre,
+                                                       float* __restrict__ g_ad, float* __restrict__ g_xd,
+                                                       int64_t ldgxd) {
+  const int gl = threadIdx.x % G;
+  const int64_t i = ((int64_t)blockIdx.x * 256 + threadIdx.x) / G;
+  if (i >= n_dst) return;
+  const int rb = rowptr[i], re = rowptr[i + 1];
+  const int HC4 = H * C / 4;
+  const bool lane_on = gl < HC4;
+  const int hq = lane_on ? (4 * gl) / C : 0;
+  const bool first = lane_on && (4 * gl) % C == 0;
+  const float4 go = lane_on ? *reinterpret_cast<const float4*>(g_out + i * ldg + 4 * gl) : make_float4(0.f, 0.f, 0.f, 0.f);
+  float S = 0.0f;
+  for (int k0 = rb; k0 < re; k0 += kGatU) {
+    const int nk = re - k0;
+    float av[kGatU];
+    float4 xv[kGatU];
+#pragma unroll
+    for (int u = 0; u < kGatU; ++u) {
+      av[u] = 0.0f;
+      xv[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (lane_on && u < nk) {
+        const int64_t j = col[k0 + u];
+        av[u] = alpha[(int64_t)(k0 + u) * H + hq];
+        xv[u] = *reinterpret_cast<const float4*>(xs + j * ldxs + 4 * gl);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < kGatU; ++u) {
+      if (u < nk) {   // (uniform over the group: the shuffles below run on every lane)
+        float p = __fadd_rn(__fadd_rn(__fadd_rn(__fmul_rn(go.x, xv[u].x), __fmul_rn(go.y, xv[u].y)),
+                                      __fmul_rn(go.z, xv[u].z)), __fmul_rn(go.w, xv[u].w));
+        p = group_sum_pow2<G>(p, C / 4);
+        S = __fadd_rn(S, __fmul_rn(av[u], p));
+        if (first) g_pre[(int64_t)(k0 + u) * H + hq] = p;   // g_alpha for now
+      }
+    }
+  }
+  float gsum = 0.0f;
+  if (first) {
+    const float adv = ad ? ad[i * H + hq] : 0.0f;
+    for (int k = rb; k < re; ++k) {
+      const int64_t q = (int64_t)k * H + hq;
+      const float ge = __fmul_rn(alpha[q], __fsub_rn(g_pre[q], S));
+      const float pre = __fadd_rn(as[(int64_t)col[k] * H + hq], adv);
+      const float gp = pre > 0.0f ? ge : __fmul_rn(ge, slope);
+      g_pre[q] = gp;
+      gsum = __fadd_rn(gsum, gp);
+    }
+    if (g_ad) g_ad[i * H + hq] = gsum;
+  }
+  if (g_xd) {
+    const int src = lane_on ? hq * (C / 4) : gl;
+    gsum = __shfl(gsum, src, G);
+    if (lane_on) {
+      const float4 at = *reinterpret_cast<const float4*>(att_dst + 4 * gl);
+      *reinterpret_cast<float4*>(g_xd + i * ldgxd + 4 * gl) =
+          make_float4(__fmul_rn(gsum, at.x), __fmul_rn(gsum, at.y), __fmul_rn(gsum, at.z), __fmul_rn(gsum, at.w));
+    }
+  }
+}
+
+// Backward, source side, on the CSC (entries k: destination cdst[k], CSR position cpos[k]), in CSC order:
+// g_a_s[j, h] = sum_k g_pre (the head's first lane), g_x_s[j, cols] = sum_k alpha g_out[i_k, cols] + g_a_s att_src.
+template <int G>
+__global__ __launch_bounds__(256) void k_gat_bwd_src_w(const int32_t* __restrict__ cptr, const int32_t* __restrict__ cdst,
+                                                       const int32_t* __restrict__ cpos, int64_t n_src, int H, int C,
+                                                       const float* __restrict__ g_out, int64_t ldg,
+                                                       const float* __restrict__ alpha,
+                                                       const float* __restrict__ g_pre,
+                                                       const float* __restrict__ att_src, float* __restrict__ g_as,
+                                                       float* __restrict__ g_xs, int64_t ldgxs) {
+  const int gl = threadIdx.x % G;
+  const int64_t j = ((int64_t)blockIdx.x * 256 + threadIdx.x) / G;
+  if (j >= n_src) return;
+  const int HC4 = H * C / 4;
+  const bool lane_on = gl < HC4;
+  const int hq = lane_on ? (4 * gl) / C : 0;
+  const bool first = lane_on && (4 * gl) % C == 0;
+  const int rb = cptr[j], re = cptr[j + 1];
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  float gas = 0.0f;
+  if (lane_on) {
+    for (int k0 = rb; k0 < re; k0 += kGatU) {
+      const int nk = re - k0;
+      float av[kGatU], pv[kGatU];
+      float4 gv[kGatU];
+#pragma unroll
+      for (int u = 0; u < kGatU; ++u) {
+        av[u] = pv[u] = 0.0f;
+        gv[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (u < nk) {
+          const int64_t p = (int64_t)cpos[k0 + u] * H + hq;
+          av[u] = alpha[p];
+          if (first) pv[u] = g_pre[p];
+          gv[u] = *reinterpret_cast<const float4*>(g_out + (int64_t)cdst[k0 + u] * ldg + 4 * gl);
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < kGatU; ++u) {
+        if (u < nk) {
+          gas = __fadd_rn(gas, pv[u]);
+          acc.x = __fadd_rn(acc.x, __fmul_rn(gv[u].x, av[u]));
+          acc.y = __fadd_rn(acc.y, __fmul_rn(gv[u].y, av[u]));
+          acc.z = __fadd_rn(acc.z, __fmul_rn(gv[u].z, av[u]));
+          acc.w = __fadd_rn(acc.w, __fmul_rn(gv[u].w, av[u]));
+        }
+      }
+    }
+  }
+  if (first) g_as[j * H + hq] = gas;
+  gas = __shfl(gas, lane_on ? hq * (C / 4) : gl, G);
+  if (lane_on) {
+    const float4 at = *reinterpret_cast<const float4*>(att_src + 4 * gl);
+    *reinterpret_cast<float4*>(g_xs + j * ldgxs + 4 * gl) =
+        make_float4(__fadd_rn(acc.x, __fmul_rn(gas, at.x)), __fadd_rn(acc.y, __fmul_rn(gas, at.y)),
+                    __fadd_rn(acc.z, __fmul_rn(gas, at.z)), __fadd_rn(acc.w, __fmul_rn(gas, at.w)));
+  }
+}
+
+// The wave-group form applies: C a multiple of 4 with C / 4 a power of two, H * C <= 256, 16-B aligned rows.
+int gat_group(int64_t H, int64_t C) {
+  static const bool off = [] {
+    const char* v = getenv("HGIN_GAT_WAVE");
+    return v && v[0] == '0';
+  }();
+  if (off || C % 4 || ((C / 4) & (C / 4 - 1)) || H * C > 256) return 0;
+  int g = 1;
+  while (g < H * C / 4) g <<= 1;
+  return g < (int)H ? 0 : g;
+}
+
+inline bool al16(const void* p, int64_t ld) { return p == nullptr || (aligned16(p) && ld % 4 == 0); }
+
+#define HGIN_GAT_G(G, KERN, ...)                                                                                \
+  switch (G) {                                                                                                \
+    case 1: KERN<1><<<(unsigned)ceil_div(rows, 256 / 1), 256, 0, s>>>(__VA_ARGS__); break;                     \
+    case 2: KERN<2><<<(unsigned)ceil_div(rows, 256 / 2), 256, 0, s>>>(__VA_ARGS__); break;                     \
+    case 4: KERN<4><<<(unsigned)ceil_div(rows, 256 / 4), 256, 0, s>>>(__VA_ARGS__); break;                     \
+    case 8: KERN<8><<<(unsigned)ceil_div(rows, 256 / 8), 256, 0, s>>>(__VA_ARGS__); break;                     \
+    case 16: KERN<16><<<(unsigned)ceil_div(rows, 256 / 16), 256, 0, s>>>(__VA_ARGS__); break;                  \
+    case 32: KERN<32><<<(unsigned)ceil_div(rows, 256 / 32), 256, 0, s>>>(__VA_ARGS__); break;                  \
+    default: KERN<64><<<(unsigned)ceil_div(rows, 256 / 64), 256, 0, s>>>(__VA_ARGS__); break;                  \
+  }
+
 inline unsigned blocks_for(int64_t n) { return (unsigned)ceil_div(n > 0 ? n : 1, 256); }
 
 }  // namespace
@@ -174,6 +457,13 @@ extern "C" int hgin_gat_logits_f32(const float* x, int64_t ldx, int64_t n, int64
   HGIN_ARG_CHECK(n >= 0 && H >= 1 && C >= 1 && ldx >= H * C, "hgin_gat_logits_f32: bad sizes");
   if (n == 0) return HGIN_OK;
   HGIN_ARG_CHECK(x && att && a, "hgin_gat_logits_f32: NULL operand");
+  if (const int G = gat_group(H, C); G && al16(x, ldx) && aligned16(att)) {
+    HGIN_TRACE("k_gat_logits_w<%d>", G);
+    const int64_t rows = n;
+    hipStream_t s = as_stream(stream);
+    HGIN_GAT_G(G, k_gat_logits_w, x, ldx, n, (int)H, (int)C, att, a)
+    return check_launch("hgin_gat_logits_f32");
+  }
   HGIN_TRACE("k_gat_logits");
   k_gat_logits<<<blocks_for(n * H), 256, 0, as_stream(stream)>>>(x, ldx, n, (int)H, (int)C, att, a);
   return check_launch("hgin_gat_logits_f32");
@@ -187,6 +477,15 @@ extern "C" int hgin_gat_fwd_f32(const int32_t* rowptr, const int32_t* col, int64
                  "hgin_gat_fwd_f32: bad sizes");
   if (n_dst == 0) return HGIN_OK;
   HGIN_ARG_CHECK(rowptr && col && xs && as && alpha && out, "hgin_gat_fwd_f32: NULL operand");
+  if (const int G = gat_group(H, C);
+      G && al16(xs, ldxs) && al16(out, ldo) && al16(accum, ld_acc) && (!bias || aligned16(bias))) {
+    HGIN_TRACE("k_gat_fwd_w<%d>", G);
+    const int64_t rows = n_dst;
+    hipStream_t s = as_stream(stream);
+    HGIN_GAT_G(G, k_gat_fwd_w, rowptr, col, n_dst, (int)H, (int)C, xs, ldxs, as, ad, slope, bias, accum, ld_acc, alpha,
+               out, ldo)
+    return check_launch("hgin_gat_fwd_f32");
+  }
   HGIN_TRACE("k_gat_fwd");
   k_gat_fwd<<<blocks_for(n_dst * H), 256, 0, as_stream(stream)>>>(rowptr, col, n_dst, (int)H, (int)C, xs, ldxs, as, ad,
                                                                   slope, bias, accum, ld_acc, alpha, out, ldo);
@@ -202,6 +501,15 @@ extern "C" int hgin_gat_bwd_dst_f32(const int32_t* rowptr, const int32_t* col, i
   if (n_dst == 0) return HGIN_OK;
   HGIN_ARG_CHECK(rowptr && col && xs && g_out && alpha && as && g_pre && (!g_xd || (att_dst && ad)),
                  "hgin_gat_bwd_dst_f32: NULL operand");
+  if (const int G = gat_group(H, C);
+      G && al16(xs, ldxs) && al16(g_out, ldg) && al16(g_xd, ldgxd) && (!g_xd || aligned16(att_dst))) {
+    HGIN_TRACE("k_gat_bwd_dst_w<%d>", G);
+    const int64_t rows = n_dst;
+    hipStream_t s = as_stream(stream);
+    HGIN_GAT_G(G, k_gat_bwd_dst_w, rowptr, col, n_dst, (int)H, (int)C, xs, ldxs, g_out, ldg, alpha, as, ad, slope,
+               att_dst, g_pre, g_ad, g_xd, ldgxd)
+    return check_launch("hgin_gat_bwd_dst_f32");
+  }
   HGIN_TRACE("k_gat_bwd_dst");
   k_gat_bwd_dst<<<blocks_for(n_dst * H), 256, 0, as_stream(stream)>>>(rowptr, col, n_dst, (int)H, (int)C, xs, ldxs,
                                                                       g_out, ldg, alpha, as, ad, slope, att_dst, g_pre,
@@ -217,6 +525,14 @@ extern "C" int hgin_gat_bwd_src_f32(const int32_t* cptr, const int32_t* cdst, co
   if (n_src == 0) return HGIN_OK;
   HGIN_ARG_CHECK(cptr && cdst && cpos && g_out && alpha && g_pre && att_src && g_as && g_xs,
                  "hgin_gat_bwd_src_f32: NULL operand");
+  if (const int G = gat_group(H, C); G && al16(g_out, ldg) && al16(g_xs, ldgxs) && aligned16(att_src)) {
+    HGIN_TRACE("k_gat_bwd_src_w<%d>", G);
+    const int64_t rows = n_src;
+    hipStream_t s = as_stream(stream);
+    HGIN_GAT_G(G, k_gat_bwd_src_w, cptr, cdst, cpos, n_src, (int)H, (int)C, g_out, ldg, alpha, g_pre, att_src, g_as,
+               g_xs, ldgxs)
+    return check_launch("hgin_gat_bwd_src_f32");
+  }
   HGIN_TRACE("k_gat_bwd_src");
   k_gat_bwd_src<<<blocks_for(n_src * H), 256, 0, as_stream(stream)>>>(cptr, cdst, cpos, n_src, (int)H, (int)C, g_out,
                                                                       ldg, alpha, g_pre, att_src, g_as, g_xs, ldgxs);

@@ -1676,29 +1676,44 @@ int launch_ws32(const WsArgs32& a, hipStream_t s, const char* what, int64_t* gri
   return check_launch(what);
 }
 
-// k_wss_f32 — k_ws_f32's forward (EPI 1, K = N = 256) as a two-stage software pipeline with the two waves of a SIMD
-// staggered (default; HGIN_WS_STAGGER = 0 keeps k_ws_f32; k_wsp_f32's schedule applied to the forward): iteration i runs the MFMAs of block i
-// on plane buffer i & 1 and the split of block i + 1 into buffer (i + 1) & 1, one barrier per block.  Waves 0-3
-// (one per SIMD) run the epilogue of block i - 1 and the split of block i + 1, then their MFMAs; waves 4-7 run their
-// MFMAs first, then the epilogue of block i and the split — so each SIMD's VALU work sits beside the other wave's
-// MFMAs instead of every wave splitting, then multiplying, then storing in lockstep.
-//   * LDS: one 32 KB fp32 A slot in per-wave slices (a thread splits exactly the 64 B its own wave's DMA wrote, so a
-//     wave waits only on its own vmcnt and refills its slice right after reading it) + two 48 KB plane buffers;
-//   * the epilogue works from the accumulator registers: lane (li, lh) holds column 32 w + li of rows
-//     (e & 3) + 8 (e >> 2) + 4 lh — the bias is one register, the accum rows are read straight from HBM, and y / z
-//     go out as 32-lane 128-B row segments (no staging: the LDS holds the two plane buffers);
-//   * same W fragments, A fragments, product order and epilogue arithmetic as k_ws_f32: bit-identical results.
-template <bool kR1, bool kZ>
+// k_wss_f32 — k_ws_f32 (K = N = 256) as a two-stage software pipeline with the two waves of a SIMD staggered
+// (default; HGIN_WS_STAGGER = 0 keeps k_ws_f32): iteration i runs the MFMAs of block i on plane buffer i & 1 and
+// the split of block i + 1 into buffer (i + 1) & 1, one barrier per block.  Waves 0-3 (one per SIMD) run the
+// epilogue of block i - 1 and the split of block i + 1, then their MFMAs; waves 4-7 run their MFMAs first, then the
+// epilogue of block i and the split — so each SIMD's VALU work sits beside the other wave's MFMAs instead of every
+// wave splitting, then multiplying, then storing in lockstep.
+//   * EPI 1: the forward MLP GEMM (z = acc + b, y = prelu(z) [+ accum]); EPI 4 (round 5): the dX GEMM with the
+//     self-term backward (C = g_comb, g_x_dst = (1 + eps) C, the eps-gradient partial sum of C x_dst), every column a
+//     self column, no g_prev (that call keeps k_ws_f32, whose g_prev rows arrive in the block's dead A slot);
+//   * LDS: one 32 KB fp32 A slot in per-wave slices (a wave splits exactly the 4 KB its own DMA wrote, so it waits
+//     only on its own vmcnt and refills its slice right after reading it) + two 48 KB plane buffers [+ with a row
+//     operand (accum / x_dst) a 32 KB row image: wave w's 32 x 32 column slice, DMA'd by the wave itself right
+//     after its epilogue has read the previous block's, read back in the accumulator layout — 160 KB in all];
+//   * every wait on the DMA / store stream is counted (a wave's vector-memory ops retire in issue order), so the
+//     split waits only for its A slice and the epilogue only for its row slice;
+//   * the epilogue works from the accumulators: lane (li, lh) holds column 32 w + li of rows (e & 3) + 8 (e >> 2)
+//     + 4 lh — the bias is one register, and y / z go out as 32-lane 128-B row segments by buffer stores from the
+//     block's row base (SGPR resources, one lane offset);
+//   * same W fragments, A fragments, product order and epilogue arithmetic as k_ws_f32: y / z / C / g_x_dst are
+//     bit-identical to it (EPI 4's eps partial sums the same terms in another order, one partial per workgroup).
+// Round 4 read the accum rows as 4-byte lane loads in the accumulator layout instead (2.81 vs k_ws_f32's 2.67 ms per
+// launch at M = 3M: HBM latency in the epilogue, profiles/r04/gpu_q); the row image replaces that.
+template <int EPI, bool kR1, bool kZ>
 __global__ __launch_bounds__(512, 1) void k_wss_f32(WsArgs32 g) {
   using C = Ws32Cfg<256, 256>;
   constexpr int K = 256, N = 256;
   constexpr int PLANES = 3 * C::PL;                                // one plane buffer
   constexpr int PL0 = C::A_BYTES;                                  // plane buffers follow the A slot
+  constexpr int R1_OFF = PL0 + 2 * PLANES;                         // row image: 8 per-wave 4 KB slices
+  constexpr int PR = kR1 ? 4 : 0;                                  // row-image DMA pieces per wave per block
+  constexpr int S = 16 * (kZ ? 2 : 1);                             // dword stores per lane per block
   static_assert(C::BM == 32 && C::NW == 8 && C::G4 == 4 && C::PA == 4, "one 4 KB slice and 4 split groups per wave");
+  static_assert(EPI == 1 || (EPI == 4 && kR1), "EPI 4 reads x_dst");
+  static_assert(R1_OFF + (kR1 ? 8 * 4096 : 0) <= 163840 && S + PR <= 63, "LDS / vmcnt");
   extern __shared__ __attribute__((aligned(16))) char wss_smem[];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
-  const int wave = tid >> 6;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform: SGPR arithmetic below
   const int li = lane & 31;
   const int lh = lane >> 5;
   const int64_t M = g.M;
@@ -1721,8 +1736,11 @@ __global__ __launch_bounds__(512, 1) void k_wss_f32(WsArgs32 g) {
       for (int p = 0; p < 3; ++p) wf[t][p] = make_uint4(o0[p].x, o0[p].y, o1[p].x, o1[p].y);
     }
   }
-  const float bcol = g.bias[wave * 32 + li];
-  const float a_slope = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(g.prelu[0])));
+  const float bcol = EPI == 1 ? g.bias[wave * 32 + li] : 0.0f;
+  const float a_slope = EPI == 1 ? __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(g.prelu[0]))) : 0.0f;
+  const float sc_self = EPI == 4 ? __fadd_rn(1.0f, __int_as_float(__builtin_amdgcn_readfirstlane(
+                                                        __float_as_int(g.eps[0])))) : 0.0f;
+  float ep = 0.0f;                                               // EPI 4: this thread's eps-gradient partial
 #pragma unroll
   for (int t = 0; t < C::KS; ++t)
 #pragma unroll
@@ -1732,6 +1750,9 @@ __global__ __launch_bounds__(512, 1) void k_wss_f32(WsArgs32 g) {
     int t;
     asm volatile("v_mov_b32 %0, %1" : "=v"(t) : "v"(tid));
     return t;
+  };
+  auto dma = [&](const void* src, void* dst) {
+    if (g.nt_in) glds16_asm<true>(src, dst); else glds16_asm(src, dst);
   };
   auto issue = [&](int64_t i) {   // this wave's 4 KB slice of block i's A rows
     const int64_t r0 = ((int64_t)blockIdx.x + i * G) * C::BM;
@@ -1744,13 +1765,24 @@ __global__ __launch_bounds__(512, 1) void k_wss_f32(WsArgs32 g) {
       const int off = piece * 1024 + ln * 16;
       int r = off / (K * 4);
       r = r < rmax ? r : rmax;
-      const float* src = ab + (r * (int)g.lda + (off % (K * 4)) / 4);
-      if (g.nt_in) glds16_asm<true>(src, wss_smem + piece * 1024); else glds16_asm(src, wss_smem + piece * 1024);
+      dma(ab + (r * (int)g.lda + (off % (K * 4)) / 4), wss_smem + piece * 1024);
     }
   };
-  // block j (in this wave's slice) -> plane buffer j & 1; the slice is then refilled with block j + 1
+  char* const rimg = wss_smem + R1_OFF + wave * 4096;             // this wave's row slice: [32 rows][32 columns]
+  auto issue_rows = [&](int64_t i) {   // block i's rows, columns 32 w .. 32 w + 31 (rows past M clamped to the last)
+    const int64_t r0 = ((int64_t)blockIdx.x + i * G) * C::BM;
+    const int rmax = (int)(M - 1 - r0 < C::BM ? M - 1 - r0 : C::BM - 1);
+    const float* src = g.r1 + r0 * g.ldr1 + wave * 32;
+    const int ln = tid_o() & 63;
+#pragma unroll
+    for (int q = 0; q < PR; ++q) {
+      int r = q * 8 + (ln >> 3);
+      r = r < rmax ? r : rmax;
+      dma(src + (r * (int)g.ldr1 + (ln & 7) * 4), rimg + q * 1024);
+    }
+  };
+  // block j (in this wave's slice, landed) -> plane buffer j & 1; the slice is then refilled with block j + 1
   auto split = [&](int64_t j) {
-    wait_vm<0>();
     char* pl = wss_smem + PL0 + (int)(j & 1) * PLANES;
     const int ln = tid_o() & 63;
     float4 v[C::G4];
@@ -1802,74 +1834,103 @@ __global__ __launch_bounds__(512, 1) void k_wss_f32(WsArgs32 g) {
       __builtin_amdgcn_sched_barrier(0);
     }
   };
-  // epilogue<1> of block i from the accumulators: z = acc + b, y = prelu(z) [+ accum].  Buffer loads / stores from
-  // the block's row base (SGPR resources) with one lane offset: no per-row 64-bit addresses held in VGPRs.
+  // the epilogue of block i from the accumulators (k_ws_f32's epilogue<1> / <4> arithmetic).  Buffer stores from the
+  // block's row base (SGPR resources, one lane offset per output): no per-row 64-bit addresses held in VGPRs.
   constexpr int kRsrc = 0x00020000;
-  const int vo = (4 * lh * N + wave * 32 + li) * 4;
-  auto load_r1 = [&](int64_t i, float (&in1)[16]) {   // block i's accum rows at this lane's 16 outputs
-    const int64_t r0 = ((int64_t)blockIdx.x + i * G) * C::BM;
-    const auto ra = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(g.r1 + r0 * N), 0, C::BM * N * 4, kRsrc);
-#pragma unroll
-    for (int e = 0; e < 16; ++e)
-      in1[e] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(ra, vo, ((e & 3) + 8 * (e >> 2)) * N * 4, 0));
-  };
-  auto epilogue = [&](int64_t i, const float (&in1)[16]) {
+  const int ldy = EPI == 1 ? N : (int)g.ldy, ldz = EPI == 1 ? N : (int)g.ldz;
+  auto epilogue = [&](int64_t i) {
     const int64_t r0 = ((int64_t)blockIdx.x + i * G) * C::BM;
     const int nr = M - r0 < C::BM ? (int)(M - r0) : C::BM;
-    const auto ry = __builtin_amdgcn_make_buffer_rsrc(g.y + r0 * N, 0, C::BM * N * 4, kRsrc);
-    const auto rz = __builtin_amdgcn_make_buffer_rsrc(kZ ? g.z + r0 * N : g.y, 0, C::BM * N * 4, kRsrc);
+    const auto ry = __builtin_amdgcn_make_buffer_rsrc(g.y + r0 * ldy, 0, C::BM * ldy * 4, kRsrc);
+    const auto rz = __builtin_amdgcn_make_buffer_rsrc(kZ ? g.z + r0 * ldz : g.y, 0, C::BM * ldz * 4, kRsrc);
+    // lane offsets recomputed per block (tid_o hides tid's value): nothing of the epilogue stays live in VGPRs
+    const int el = tid_o() & 63, eli = el & 31, elh = el >> 5;
+    const int voy = (4 * elh * ldy + wave * 32 + eli) * 4, voz = (4 * elh * ldz + wave * 32 + eli) * 4;
+    const float* img = reinterpret_cast<const float*>(rimg) + 4 * elh * 32 + eli;
 #pragma unroll
     for (int e = 0; e < 16; ++e) {
-      const int row = (e & 3) + 8 * (e >> 2) + 4 * lh;
-      const int so = ((e & 3) + 8 * (e >> 2)) * N * 4;
-      const float zz = __fadd_rn(acc[e], bcol);
-      const float y = zz > 0.0f ? zz : __fmul_rn(a_slope, zz);
-      const float o = kR1 ? __fadd_rn(in1[e], y) : y;
-      if (row < nr) {
-        if (g.nt_io) {
-          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(o), ry, vo, so, 2);
-          if constexpr (kZ) __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(zz), rz, vo, so, 2);
+      const int rb = (e & 3) + 8 * (e >> 2);                     // this lane's row: rb + 4 lh
+      const float in1 = kR1 ? img[rb * 32] : 0.0f;
+      if ((e & 3) == 3) __builtin_amdgcn_sched_barrier(0);       // at most 4 row values in flight
+      float o, zz;
+      if constexpr (EPI == 1) {
+        zz = __fadd_rn(acc[e], bcol);
+        const float y = zz > 0.0f ? zz : __fmul_rn(a_slope, zz);
+        o = kR1 ? __fadd_rn(in1, y) : y;
+      } else {
+        o = acc[e];
+        zz = __fmul_rn(sc_self, o);
+      }
+      if (rb + 4 * elh < nr) {
+        if constexpr (EPI == 4) ep = __fadd_rn(ep, __fmul_rn(o, in1));
+        const int aux = g.nt_io ? 2 : 0;
+        if (aux) {
+          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(o), ry, voy, rb * ldy * 4, 2);
+          if constexpr (kZ) __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(zz), rz, voz, rb * ldz * 4, 2);
         } else {
-          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(o), ry, vo, so, 0);
-          if constexpr (kZ) __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(zz), rz, vo, so, 0);
+          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(o), ry, voy, rb * ldy * 4, 0);
+          if constexpr (kZ) __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(zz), rz, voz, rb * ldz * 4, 0);
         }
       }
     }
+    if constexpr (kR1) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the row slice is read: refill it
   };
 
+  // Per wave the vector-memory stream is: A(0), A(1) [split(0)], R(0), then per block j the epilogue's stores E(j),
+  // R(j + 1), A(j + 2) [split(j + 1)] (waves 4-7 run E(j) after block j's MFMAs, waves 0-3 before block j + 1's).
+  // Hence the split of block j + 1 waits until at most S + PR ops issued after A(j + 1) are pending (PR at waves
+  // 0-3's first split, which no epilogue precedes), and the epilogue of block j until at most PA are pending after
+  // R(j): the A pieces that follow it — of block j + 2 at waves 0-3, of block j + 1 at waves 4-7 (R(0): none yet) —
+  // when that block exists.
   issue(0);
+  wait_vm<0>();
   split(0);
+  if constexpr (kR1) issue_rows(0);
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  auto wait_rows = [&](int64_t j, bool first) {   // before the epilogue of block j (first: waves 0-3)
+    if constexpr (kR1) {
+      if (first ? j + 2 < my : (j >= 1 && j + 1 < my)) wait_vm<C::PA>(); else wait_vm<0>();
+    }
+  };
   // one loop per wave group (the same barrier count: s_barrier counts arrivals, not program points), so the
   // accumulators are dead during each group's split
-  // (with an accum stream, waves 0-3 read block i's accum rows right after its MFMAs — in flight across the barrier,
-  // consumed by the epilogue at the top of the next iteration — and waves 4-7 between their MFMAs and epilogue)
-  float in1[16];
-#pragma unroll
-  for (int e = 0; e < 16; ++e) in1[e] = 0.0f;
   if (wave < 4) {
     for (int64_t i = 0; i < my; ++i) {
       __builtin_amdgcn_s_barrier();   // block i's planes written by every wave; block i - 1's read by every wave
       asm volatile("" ::: "memory");
-      if (i > 0) epilogue(i - 1, in1);
-      if (i + 1 < my) split(i + 1);
+      if (i > 0) {
+        wait_rows(i - 1, true);
+        epilogue(i - 1);
+        if (kR1) issue_rows(i);
+      }
+      if (i + 1 < my) {
+        if (i == 0) wait_vm<PR>(); else wait_vm<S + PR>();
+        split(i + 1);
+      }
       mfma(i);
-      __builtin_amdgcn_sched_barrier(0);
-      if constexpr (kR1) load_r1(i, in1);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // this wave's plane writes and fragment reads are done
     }
-    epilogue(my - 1, in1);
+    wait_rows(my - 1, true);
+    epilogue(my - 1);
   } else {
     for (int64_t i = 0; i < my; ++i) {
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
       mfma(i);
       __builtin_amdgcn_sched_barrier(0);
-      if constexpr (kR1) load_r1(i, in1);
-      epilogue(i, in1);
-      if (i + 1 < my) split(i + 1);
+      wait_rows(i, false);
+      epilogue(i);
+      if (i + 1 < my) {
+        if (kR1) issue_rows(i + 1);
+        wait_vm<S + PR>();
+        split(i + 1);
+      }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     }
+  }
+  if constexpr (EPI == 4) {
+    wait_vm<0>();
+    tile_partial(reinterpret_cast<float*>(wss_smem), ep, g.part, blockIdx.x);
   }
 }
 
@@ -1883,19 +1944,11 @@ bool wss_enabled() {
   return on;
 }
 
-bool wss_acc_enabled() {   // HGIN_WS_STAGGER_ACC = 1: the staggered form also for the accumulating forward
-  static const bool on = [] {
-    const char* v = getenv("HGIN_WS_STAGGER_ACC");
-    return v && v[0] == '1';
-  }();
-  return on;
-}
-
-template <bool kR1, bool kZ>
-int launch_wss(const WsArgs32& a, hipStream_t s, const char* what) {
-  constexpr int lds = Ws32Cfg<256, 256>::A_BYTES + 2 * 3 * Ws32Cfg<256, 256>::PL;
+template <int EPI, bool kR1, bool kZ>
+int launch_wss(const WsArgs32& a, hipStream_t s, const char* what, int64_t* grid_out = nullptr) {
+  constexpr int lds = Ws32Cfg<256, 256>::A_BYTES + 2 * 3 * Ws32Cfg<256, 256>::PL + (kR1 ? 8 * 4096 : 0);
   static_assert(lds <= 160 * 1024, "LDS");
-  auto kern = k_wss_f32<kR1, kZ>;
+  auto kern = k_wss_f32<EPI, kR1, kZ>;
   static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
                                                      hipFuncAttributeMaxDynamicSharedMemorySize, lds);
   if (attr != hipSuccess) {
@@ -1904,288 +1957,8 @@ int launch_wss(const WsArgs32& a, hipStream_t s, const char* what) {
   }
   const int64_t nblk = ceil_div(a.M, (int64_t)Ws32Cfg<256, 256>::BM);
   const int64_t grid = nblk < ws_grid() ? nblk : ws_grid();
-  HGIN_TRACE("k_wss_f32<%d,%d>", (int)kR1, (int)kZ);
+  HGIN_TRACE("k_wss_f32<EPI%d,%d,%d>", EPI, (int)kR1, (int)kZ);
   kern<<<(unsigned)grid, 512, lds, s>>>(a);
-  return check_launch(what);
-}
-
-// k_wsf_f32 — k_ws_f32 (K = N = 256; EPI 1, and EPI 4 without g_prev) with one wave per SIMD and the split of the
-// next block placed between this block's MFMAs (HGIN_WS_PIPE = 1):
-//   * 4 waves, each holding W rows 64 w .. 64 w + 63 as split B fragments: 384 registers, which one wave per SIMD can
-//     hold (the SIMD's 512-entry file: planes 0 and 1 in the 256 AGPRs, plane 2 in VGPRs; gfx950 MFMAs take A / B
-//     operands from AGPRs).  hipcc does not place operands that way by itself, so the MFMAs are inline asm with "a"
-//     constraints on those planes; the accumulator chains need no wait states between MFMAs, and the VALU that reads
-//     an accumulator after a block's last MFMA is behind explicit s_nops;
-//   * per block of 32 rows and k-step: three A-plane fragments (shared by the wave's two 32-column tiles), twelve
-//     v_mfma_f32_32x32x16_bf16 in k_ws_f32's product order;
-//   * the fp32 A slot is one 32 KB image in per-wave slices (wave w DMAs and splits rows 8 w .. 8 w + 7: it waits on
-//     its own vmcnt only, and refills its slice once its split has read it); the split of block i + 1 runs one row
-//     per k-step in the second half of block i's k-loop, between its MFMAs (an MFMA holds vector issue for 8 of its 32
-//     cycles: MI355X_MICROARCH.md), into the other of two 48 KB plane buffers — one barrier per block;
-//   * the epilogue works from the accumulators: lane (li, lh) owns columns 64 w + 32 c + li, rows (e & 3) + 8 (e >> 2)
-//     + 4 lh; each dword store writes two full 128-B row segments.  Its row image (accum / x_dst) is DMA'd per wave as
-//     the wave's 64 columns (8 KB; the 32-column halves of rows with bit 2 set swapped, so the two half-waves' reads
-//     fall in different banks) and refilled once read;
-//   * per output the products, their order and the epilogue arithmetic are k_ws_f32's: y / z / C / g_x_dst are
-//     bit-identical to it; EPI 4's eps-gradient partial sums the same terms in another order (one partial per
-//     workgroup, as before).
-// LDS: 32 KB A slot + 2 x 48 KB plane buffers + 32 KB row image = 160 KB.  Input DMAs and output stores are always
-// non-temporal: the launcher takes this form only where k_ws_f32 would choose both.
-// (each MFMA statement opens with s_nop 1: hipcc pads nothing around inline asm, and an operand it has just moved
-// into place with a VALU / v_accvgpr write needs 2 wait states before an MFMA reads it; tools/check_ws_asm.py checks
-// that no other instruction touches an accumulator between the MFMAs of its chain)
-using u32x4v = __attribute__((ext_vector_type(4))) unsigned int;
-__device__ __forceinline__ void mfma_b_agpr(f32x16& acc, const bf16x8& a, const u32x4v& b) {
-  asm volatile("s_nop 1\n\tv_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+v"(acc) : "v"(a), "a"(b));
-}
-__device__ __forceinline__ void mfma_b_vgpr(f32x16& acc, const bf16x8& a, const u32x4v& b) {
-  asm volatile("s_nop 1\n\tv_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+v"(acc) : "v"(a), "v"(b));
-}
-__device__ __forceinline__ void mfma_b_agpr_first(f32x16& acc, const bf16x8& a, const u32x4v& b) {
-  asm volatile("s_nop 1\n\tv_mfma_f32_32x32x16_bf16 %0, %1, %2, 0" : "=&v"(acc) : "v"(a), "a"(b));
-}
-
-template <int EPI, bool kR1, bool kZ>
-__global__ __launch_bounds__(256, 1) void k_wsf_f32(WsArgs32 g) {
-  constexpr int K = 256, KS = K / 16, BM = 32;
-  constexpr int A_BYTES = BM * K * 4, PROW = K * 2, PL = BM * PROW, SW = 31;
-  constexpr int P_OFF = A_BYTES, PBUF = 3 * PL, R1_OFF = P_OFF + 2 * PBUF;
-  constexpr int RA = 8, RR = kR1 ? 8 : 0;                 // DMA pieces per wave per block
-  constexpr int S = 32 * (kZ ? 2 : 1);                     // dword stores per lane per block
-  constexpr int WAIT_A = RR + S < 63 ? RR + S : 63;        // split waits on A(i + 1): stores(i - 1), r1(i) after it
-  static_assert(EPI == 1 || kR1, "EPI 4 reads x_dst");
-  extern __shared__ __attribute__((aligned(16))) char wsf_smem[];
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // uniform: LDS / DMA bases in SGPRs
-  const int li = lane & 31;
-  const int lh = lane >> 5;
-  const int64_t M = g.M;
-  const int64_t nblk = (M + BM - 1) / BM;
-  const int64_t G = gridDim.x;
-  if ((int64_t)blockIdx.x >= nblk) return;
-  const int64_t my = (nblk - 1 - blockIdx.x) / G + 1;
-
-  // W rows 64 w + 32 c + li, k = 16 t + 8 lh .. + 7, as three bf16 planes (k_ws_f32's fragment layout):
-  // planes 0 / 1 used only through "a" operands (AGPRs), plane 2 through "v" operands
-  u32x4v w01[2][KS][2], w2[2][KS];
-#pragma unroll
-  for (int c = 0; c < 2; ++c) {
-    const float* wr = g.w + (int64_t)(wave * 64 + c * 32 + li) * K + lh * 8;
-#pragma unroll
-    for (int t = 0; t < KS; ++t) {
-      const float4 v0 = *reinterpret_cast<const float4*>(wr + t * 16);
-      const float4 v1 = *reinterpret_cast<const float4*>(wr + t * 16 + 4);
-      uint2 o0[3], o1[3];
-      split4(v0, o0);
-      split4(v1, o1);
-      w01[c][t][0] = u32x4v{o0[0].x, o0[0].y, o1[0].x, o1[0].y};
-      w01[c][t][1] = u32x4v{o0[1].x, o0[1].y, o1[1].x, o1[1].y};
-      w2[c][t] = u32x4v{o0[2].x, o0[2].y, o1[2].x, o1[2].y};
-    }
-  }
-  float bcol[2] = {0.0f, 0.0f};
-  if constexpr (EPI == 1) {
-    bcol[0] = g.bias[wave * 64 + li];
-    bcol[1] = g.bias[wave * 64 + 32 + li];
-  }
-  const float a_slope = EPI == 1 ? __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(g.prelu[0]))) : 0.0f;
-  const float sc_self = EPI == 4 ? __fadd_rn(1.0f, __int_as_float(__builtin_amdgcn_readfirstlane(
-                                                        __float_as_int(g.eps[0])))) : 0.0f;
-  float ep = 0.0f;
-  wait_vm<0>();                          // the prologue's loads (W, bias) are done before the counted DMA ring starts
-  asm volatile("s_nop 4" ::: "memory");  // (the AGPR writes of the W planes settle before the first MFMA reads them)
-
-  auto tid_o = [&]() {
-    int t;
-    asm volatile("v_mov_b32 %0, %1" : "=v"(t) : "v"(tid));
-    return t;
-  };
-  auto rows_of = [&](int64_t i, int64_t& r0, int& rmax) {
-    r0 = ((int64_t)blockIdx.x + i * G) * BM;
-    rmax = (int)(M - 1 - r0 < BM ? M - 1 - r0 : BM - 1);
-  };
-  auto issue_a = [&](int64_t i) {   // rows 8 w .. 8 w + 7 of block i into this wave's slice
-    int64_t r0;
-    int rmax;
-    rows_of(i, r0, rmax);
-    const int ln = tid_o() & 63;
-#pragma unroll
-    for (int j = 0; j < RA; ++j) {
-      const int row = 8 * wave + j;
-      const int r = row < rmax ? row : rmax;   // (rows past M are zeroed at the split)
-      glds16_asm<true>(g.a + (r0 + r) * g.lda + ln * 4, wsf_smem + row * 1024);
-    }
-  };
-  auto issue_r1 = [&](int64_t i) {  // this wave's 64 columns of block i's row image: piece j = rows 4j .. 4j + 3
-    int64_t r0;
-    int rmax;
-    rows_of(i, r0, rmax);
-    const int ln = tid_o() & 63;
-#pragma unroll
-    for (int j = 0; j < RR; ++j) {
-      const int row = 4 * j + (ln >> 4);
-      const int r = row < rmax ? row : rmax;
-      const int col = ((ln & 15) * 4) ^ (((row >> 2) & 1) << 5);
-      glds16_asm<true>(g.r1 + (r0 + r) * g.ldr1 + wave * 64 + col, wsf_smem + R1_OFF + wave * 8192 + j * 1024);
-    }
-  };
-  // one row of block j's slice (row 8 w + q) -> its three plane rows in plane buffer j & 1
-  auto split_row = [&](int64_t j, int q) {
-    char* pl = wsf_smem + P_OFF + (int)(j & 1) * PBUF;
-    const int64_t r0 = ((int64_t)blockIdx.x + j * G) * BM;
-    const int ln = tid_o() & 63;
-    const int r = 8 * wave + q, k = ln * 4;
-    const float4 v = *reinterpret_cast<const float4*>(wsf_smem + r * 1024 + ln * 16);
-    const float4 x = r0 + r < M ? v : make_float4(0.f, 0.f, 0.f, 0.f);
-    uint2 o[3];
-    split4(x, o);
-    const int off = r * PROW + 16 * ((k >> 3) ^ (r & SW)) + 8 * ((k >> 2) & 1);
-#pragma unroll
-    for (int p = 0; p < 3; ++p) *reinterpret_cast<uint2*>(pl + p * PL + off) = o[p];
-  };
-
-  // block i's products (k_ws_f32's fragments and product order), one row of block i + 1's split per k-step in the
-  // second half (its VALU issues in the MFMAs' shadow)
-  auto mfma = [&](int64_t i, f32x16 (&acc)[2]) {
-    const int fl = tid_o() & 63;
-    const int fsw16 = (((fl >> 5) ^ (fl & 31)) & SW) << 4;   // chunk 2t + lh of row li sits at (2t + lh) ^ (li & SW)
-    const char* planes = wsf_smem + P_OFF + (int)(i & 1) * PBUF + (fl & 31) * PROW;
-    auto ld = [&](int t, int p) {
-      return __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(planes + p * PL + ((32 * t) ^ fsw16)));
-    };
-    const bool nxt = i + 1 < my;
-    bf16x8 a0 = ld(0, 0), a1 = ld(0, 1), a2 = ld(0, 2);
-#pragma unroll
-    for (int t = 0; t < KS; ++t) {
-      if (t >= KS / 2 && nxt) {
-        if (t == KS / 2) {   // block i + 1 landed in this wave's slice (counted)
-          if (i == 0) wait_vm<RR>(); else wait_vm<WAIT_A>();
-        }
-        split_row(i + 1, t - KS / 2);
-      }
-#pragma unroll
-      for (int c = 0; c < 2; ++c) {
-        if (t == 0) mfma_b_agpr_first(acc[c], a2, w01[c][t][0]); else mfma_b_agpr(acc[c], a2, w01[c][t][0]);
-        mfma_b_agpr(acc[c], a1, w01[c][t][1]);
-        mfma_b_vgpr(acc[c], a0, w2[c][t]);
-        mfma_b_agpr(acc[c], a1, w01[c][t][0]);
-        mfma_b_agpr(acc[c], a0, w01[c][t][1]);
-        mfma_b_agpr(acc[c], a0, w01[c][t][0]);
-      }
-      if (t + 1 < KS) {
-        a0 = ld(t + 1, 0);
-        a1 = ld(t + 1, 1);
-        a2 = ld(t + 1, 2);
-      }
-      __builtin_amdgcn_sched_barrier(0);
-    }
-    // the last MFMAs' results reach the VALU that reads them after 18 wait states (32x32: 16 passes + 2)
-    asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 3" : "+v"(acc[0]), "+v"(acc[1]));
-    if (nxt) {
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the slice is read: refill it with block i + 2
-      if (i + 2 < my) issue_a(i + 2);
-    }
-  };
-
-  // block i's outputs from the accumulators (epilogue<1> / epilogue<4>'s arithmetic per element)
-  auto epilogue = [&](int64_t i, const f32x16 (&acc)[2], auto checked) {
-    const int64_t r0 = ((int64_t)blockIdx.x + i * G) * BM;
-    const float* img = reinterpret_cast<const float*>(wsf_smem + R1_OFF + wave * 8192) + 4 * lh * 64 + li;
-    // the leading dimensions pass through an opaque move per block, so the compiler cannot hoist the 64 per-element
-    // addresses out of the block loop (they would not fit beside the W slice)
-    int64_t ldy = g.ldy, ldz = g.ldz;
-    asm volatile("" : "+s"(ldy), "+s"(ldz));
-#pragma unroll
-    for (int c = 0; c < 2; ++c) {
-      const int col = wave * 64 + 32 * c + li;
-      // scalar row bases + a 32-bit lane byte offset (global_store_dword's SGPR-base form: no per-element 64-bit
-      // address registers)
-      const uint32_t voy = (uint32_t)(4 * lh * (int)ldy + col) * 4u;
-      const uint32_t voz = kZ ? (uint32_t)(4 * lh * (int)ldz + col) * 4u : 0u;
-#pragma unroll
-      for (int e = 0; e < 16; ++e) {
-        const int rb = (e & 3) + 8 * (e >> 2);   // the row less 4 lh (uniform); its bit 2 is lh
-        const float in1 = kR1 ? img[rb * 64 + 32 * (c ^ lh)] : 0.0f;
-        float o = acc[c][e], zz;
-        if constexpr (EPI == 1) {
-          zz = __fadd_rn(o, bcol[c]);
-          const float y = zz > 0.0f ? zz : __fmul_rn(a_slope, zz);
-          o = kR1 ? __fadd_rn(in1, y) : y;
-        } else {
-          zz = __fmul_rn(sc_self, o);
-        }
-        if (!decltype(checked)::value || r0 + rb + 4 * lh < M) {   // (only a grid's last block is partial)
-          if constexpr (EPI == 4) ep = __fadd_rn(ep, __fmul_rn(o, in1));
-          char* yb = reinterpret_cast<char*>(g.y + (r0 + rb) * ldy);
-          __builtin_nontemporal_store(o, reinterpret_cast<float*>(yb + voy));
-          if constexpr (kZ) {
-            char* zb = reinterpret_cast<char*>(g.z + (r0 + rb) * ldz);
-            __builtin_nontemporal_store(zz, reinterpret_cast<float*>(zb + voz));
-          }
-        }
-        if ((e & 3) == 3) __builtin_amdgcn_sched_barrier(0);
-      }
-    }
-  };
-
-  // prologue: block 0 split whole, block 1 and the row image of block 0 in flight
-  issue_a(0);
-  wait_vm<0>();
-#pragma unroll
-  for (int q = 0; q < 8; ++q) split_row(0, q);
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  if (my > 1) issue_a(1);
-  if constexpr (kR1) issue_r1(0);
-  // Vector-memory order per wave in iteration i: A(i + 2) at the end of the k-loop (after the split's reads), the
-  // epilogue's S stores, then r1(i + 1) (after the epilogue's image reads).  The split of block i + 1 waits on A(i + 1)
-  // (issued at the end of iteration i - 1's k-loop: stores(i - 1) and r1(i) follow it; at i = 0 only r1(0)); the
-  // epilogue waits on r1(i) (only A(i + 2) follows it).  Counts above 63 are capped (waiting slightly more).
-  for (int64_t i = 0; i < my; ++i) {
-    __builtin_amdgcn_s_barrier();   // planes of block i written by every wave; those of block i - 1 read by every wave
-    asm volatile("" ::: "memory");
-    f32x16 acc[2];
-    mfma(i, acc);
-    if constexpr (kR1) {   // r1(i) landed: only A(i + 2) was issued after it
-      if (i + 2 < my) wait_vm<RA>(); else wait_vm<0>();
-    }
-    const int64_t r0 = ((int64_t)blockIdx.x + i * G) * BM;
-    if (r0 + BM <= M) epilogue(i, acc, std::false_type{}); else epilogue(i, acc, std::true_type{});
-    if constexpr (kR1) {
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the image is read
-      if (i + 1 < my) issue_r1(i + 1);
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // this wave's plane writes are done
-  }
-  if constexpr (EPI == 4) {
-    wait_vm<0>();
-    tile_partial(reinterpret_cast<float*>(wsf_smem), ep, g.part, blockIdx.x);
-  }
-}
-
-bool wsf_enabled() {   // HGIN_WS_PIPE = 1 / 0: the pipelined fp32 forward / dX form (default off until measured)
-  static const bool on = [] {
-    const char* v = getenv("HGIN_WS_PIPE");
-    return v && v[0] == '1';
-  }();
-  return on;
-}
-
-template <int EPI, bool kR1, bool kZ>
-int launch_wsf(const WsArgs32& a, hipStream_t s, const char* what, int64_t* grid_out = nullptr) {
-  constexpr int lds = 32768 + 6 * 16384 + (kR1 ? 32768 : 0);
-  static_assert(lds <= 160 * 1024, "LDS");
-  auto kern = k_wsf_f32<EPI, kR1, kZ>;
-  static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
-                                                     hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-  if (attr != hipSuccess) {
-    set_error("%s: hipFuncSetAttribute failed: %s", what, hipGetErrorString(attr));
-    return (int)attr;
-  }
-  const int64_t nblk = ceil_div(a.M, (int64_t)32);
-  const int64_t grid = nblk < ws_grid() ? nblk : ws_grid();
-  HGIN_TRACE("k_wsf_f32<256,256,EPI%d>", EPI);
-  kern<<<(unsigned)grid, 256, lds, s>>>(a);
   if (grid_out) *grid_out = grid;
   return check_launch(what);
 }
@@ -2203,21 +1976,11 @@ int try_ws_f32(const float* a1, int64_t lda1, int64_t k1, const float* a2_eps, c
     return -1;
   WsArgs32 g{a1, lda1, w, bias, prelu, accum, N, nullptr, 0, z, N, y, N, nullptr, nullptr, M, gemm_nt_io(M, N, 4),
              ws_nt_in()};
-  if (wsf_enabled() && g.nt_io && g.nt_in) {
-    if (accum && z) return launch_wsf<1, true, true>(g, s, what);
-    if (accum) return launch_wsf<1, true, false>(g, s, what);
-    if (z) return launch_wsf<1, false, true>(g, s, what);
-    return launch_wsf<1, false, false>(g, s, what);
-  }
-  // the staggered form where it measured faster: without an accum stream.  With one (HGIN_WS_STAGGER_ACC = 1) its
-  // accum rows come in as 4-byte lane loads in the accumulator layout: 6.94 vs k_ws_f32's 5.73 ms per launch at
-  // M = 6M even with waves 0-3 loading them across the barrier (profiles/r04/gpu_q; 2.81 vs 2.67 ms at M = 3M when
-  // read in the epilogue, profiles/r04/final)
-  if (wss_enabled() && (!accum || wss_acc_enabled())) {
-    if (accum && z) return launch_wss<true, true>(g, s, what);
-    if (accum) return launch_wss<true, false>(g, s, what);
-    if (z) return launch_wss<false, true>(g, s, what);
-    return launch_wss<false, false>(g, s, what);
+  if (wss_enabled()) {
+    if (accum && z) return launch_wss<1, true, true>(g, s, what);
+    if (accum) return launch_wss<1, true, false>(g, s, what);
+    if (z) return launch_wss<1, false, true>(g, s, what);
+    return launch_wss<1, false, false>(g, s, what);
   }
   if (accum && z) return launch_ws32<256, 256, 1, true, true, false>(g, s, what);
   if (accum) return launch_ws32<256, 256, 1, true, false, false>(g, s, what);
@@ -2242,9 +2005,9 @@ int try_ws_f32_comb(const float* a, int64_t lda, const float* b, int64_t ldb, fl
     return -1;
   WsArgs32 g{a, lda, b, nullptr, nullptr, xd, ce.ldxd, gp, ce.ldgp, gd, ce.ldgd, c, ldc, ce.eps, ce.part, M,
              gemm_nt_io(M, N, 4), ws_nt_in()};
-  if (wsf_enabled() && !gp && g.nt_io && g.nt_in) {
-    if (gd) return launch_wsf<4, true, true>(g, s, what, grid_out);
-    return launch_wsf<4, true, false>(g, s, what, grid_out);
+  if (wss_enabled() && !gp) {   // (with g_prev: k_ws_f32, whose g_prev rows arrive in the block's dead A slot)
+    if (gd) return launch_wss<4, true, true>(g, s, what, grid_out);
+    return launch_wss<4, true, false>(g, s, what, grid_out);
   }
   if (gd && gp) return launch_ws32<256, 256, 4, true, true, true>(g, s, what, grid_out);
   if (gd) return launch_ws32<256, 256, 4, true, true, false>(g, s, what, grid_out);

@@ -1017,10 +1017,10 @@ struct WsdF32Cfg {
   static constexpr int LDS = SLOT * NST + PLANES;
   static constexpr int PA = A_BYTES / 1024 / 8, PB = B_BYTES / 1024 / 8;
   static constexpr int P = PA + (PRO ? PA : 0) + PB;
-  static constexpr int S = PRO ? 2 : 0;                      // g_z stores per A-splitting wave per block (2 x 16 B)
+  static constexpr int CA = BM * N / 4;                      // A float4 groups (thread t: t, t + NT, ...)
+  static constexpr int S = PRO ? CA / NT : 0;                // g_z stores (16 B) per thread per block
   static_assert(TK >= 1 && A_BYTES % 8192 == 0 && B_BYTES % 8192 == 0 && LDS <= 163840, "shape");
-  static_assert(!PRO || BM * N / 8 <= NT, "PRO: at most one A group per thread");
-  static constexpr int CA = BM * N / 8;                      // A groups (threads t < CA split one each)
+  static_assert(!PRO || (CA % NT == 0 && CA / NT <= 2 && NT % (N / 4) == 0), "PRO: fixed columns per thread");
 };
 
 template <int N, int K, bool PRO>
@@ -1081,11 +1081,11 @@ __global__ __launch_bounds__(512, 1) void k_wsd_f32(const float* __restrict__ A,
           base + C::A_BYTES + C::Z_BYTES + piece * 1024);
     }
   };
-  float csum[8];
+  float csum[4];
   float ssum = 0.0f;
   const float sl = PRO ? pro.slope[0] : 0.0f;
 #pragma unroll
-  for (int j = 0; j < 8; ++j) csum[j] = 0.0f;
+  for (int j = 0; j < 4; ++j) csum[j] = 0.0f;
 
   f32x16 acc[2][C::TK];
 #pragma unroll
@@ -1105,11 +1105,9 @@ __global__ __launch_bounds__(512, 1) void k_wsd_f32(const float* __restrict__ A,
   for (int i = 0; i < NST - 1; ++i)
     if (i < my) issue(i);
 
-  // (N = 128: only waves 0-3 split A groups and store g_z; each wave waits on its own count)
-  const bool stores = PRO && wave * 64 < C::CA;
   for (int64_t i = 0; i < my; ++i) {
     if (i + NST - 2 < my) {
-      if (stores) wsd_wait<NST, C::P, C::S>(i); else wsd_wait<NST, C::P, 0>(i);
+      wsd_wait<NST, C::P, C::S>(i);
     } else {
       wait_vm<0>();
     }
@@ -1119,54 +1117,51 @@ __global__ __launch_bounds__(512, 1) void k_wsd_f32(const float* __restrict__ A,
     const char* fbase = wsdf_smem + (int)(i % NST) * C::SLOT;
     const int64_t r0 = ((int64_t)blockIdx.x + i * G) * C::BM;
     const int valid = M - r0 < C::BM ? (int)(M - r0) : C::BM;
-    {   // split both fp32 images into three bf16 planes (8 consecutive columns = one 16-B chunk per plane)
+    {   // split both fp32 images into three bf16 planes, one float4 (half a 16-B plane chunk) per lane and step:
+        // consecutive lanes read consecutive 16-B pieces (conflict-free; 32 B per lane was 2-way conflicted)
       const int t = tid_o();
-      constexpr int CA = C::BM * N / 8, CT = C::BM * (N + K) / 8;   // 8-element groups
+      constexpr int CA = C::CA, CT = C::BM * (N + K) / 4;   // float4 groups
 #pragma unroll
       for (int q = 0; q < (CT + C::NT - 1) / C::NT; ++q) {
         const int grp = q * C::NT + t;
         if (CT % C::NT != 0 && grp >= CT) break;
         const bool isA = grp < CA;
         const int cols = isA ? N : K;
-        const int e0 = (isA ? grp : grp - CA) * 8;
+        const int e0 = (isA ? grp : grp - CA) * 4;
         const int row = e0 / cols, col = e0 % cols;
         const float* src = reinterpret_cast<const float*>(fbase + (isA ? 0 : C::A_BYTES + C::Z_BYTES)) + e0;
-        float4 v0 = *reinterpret_cast<const float4*>(src), v1 = *reinterpret_cast<const float4*>(src + 4);
-        if (row >= valid) v0 = v1 = make_float4(0.f, 0.f, 0.f, 0.f);
+        float4 v = *reinterpret_cast<const float4*>(src);
+        if (row >= valid) v = make_float4(0.f, 0.f, 0.f, 0.f);
         if constexpr (PRO) {
-          if (isA) {   // g_z from g_y (v0, v1) and z; its store; the partial sums
+          if (isA) {   // g_z from g_y and z; its store; the partial sums (columns fixed per thread)
             const float* zs = reinterpret_cast<const float*>(fbase + C::A_BYTES) + e0;
-            float4 z0 = *reinterpret_cast<const float4*>(zs), z1 = *reinterpret_cast<const float4*>(zs + 4);
-            if (row >= valid) z0 = z1 = make_float4(0.f, 0.f, 0.f, 0.f);
-            float g[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
-            const float zz[8] = {z0.x, z0.y, z0.z, z0.w, z1.x, z1.y, z1.z, z1.w};
+            float4 z4 = *reinterpret_cast<const float4*>(zs);
+            if (row >= valid) z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+            float gg[4] = {v.x, v.y, v.z, v.w};
+            const float zz[4] = {z4.x, z4.y, z4.z, z4.w};
 #pragma unroll
-            for (int j = 0; j < 8; ++j) {
+            for (int j = 0; j < 4; ++j) {
               const bool pos = zz[j] > 0.0f;
-              const float o = pos ? g[j] : __fmul_rn(sl, g[j]);
+              const float o = pos ? gg[j] : __fmul_rn(sl, gg[j]);
               csum[j] = __fadd_rn(csum[j], o);
-              if (!pos) ssum = __fadd_rn(ssum, __fmul_rn(zz[j], g[j]));
-              g[j] = o;
+              if (!pos) ssum = __fadd_rn(ssum, __fmul_rn(zz[j], gg[j]));
+              gg[j] = o;
             }
-            v0 = make_float4(g[0], g[1], g[2], g[3]);
-            v1 = make_float4(g[4], g[5], g[6], g[7]);
+            v = make_float4(gg[0], gg[1], gg[2], gg[3]);
             const int64_t gr = r0 + row;
             float* gzp = gr < M ? static_cast<float*>(pro.gz) + gr * pro.ldgz + col
-                                : reinterpret_cast<float*>(pro.dump + (int64_t)t * 32);
-            *reinterpret_cast<float4*>(gzp) = v0;
-            *reinterpret_cast<float4*>(gzp + 4) = v1;
+                                : reinterpret_cast<float*>(pro.dump + (int64_t)t * 32 + 16 * q);
+            *reinterpret_cast<float4*>(gzp) = v;
           }
         }
-        uint2 o0[3], o1[3];
-        split4(v0, o0);
-        split4(v1, o1);
+        uint2 o[3];
+        split4(v, o);
         const int prow = isA ? C::PA_ROW : C::PB_ROW;
         char* pl = planes + (isA ? 0 : 3 * C::PA_BYTES);
         const int pbytes = isA ? C::PA_BYTES : C::PB_BYTES;
-        const int off = prow * row + 16 * ((col >> 3) ^ wsd_swz(row));
+        const int off = prow * row + 16 * ((col >> 3) ^ wsd_swz(row)) + 8 * ((col >> 2) & 1);
 #pragma unroll
-        for (int p = 0; p < 3; ++p)
-          *reinterpret_cast<uint4*>(pl + p * pbytes + off) = make_uint4(o0[p].x, o0[p].y, o1[p].x, o1[p].y);
+        for (int p = 0; p < 3; ++p) *reinterpret_cast<uint2*>(pl + p * pbytes + off) = o[p];
       }
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -1210,21 +1205,20 @@ __global__ __launch_bounds__(512, 1) void k_wsd_f32(const float* __restrict__ A,
     __builtin_amdgcn_s_setprio(0);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   }
-  if constexpr (PRO) {   // fixed-order workgroup sums: column n over the 16 block rows, the slope over the threads
+  if constexpr (PRO) {   // fixed-order workgroup sums: column n over the threads that own it, the slope over all
     wait_vm<0>();
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
-    float* red = reinterpret_cast<float*>(wsdf_smem);   // [NT][8], then [NT] slope partials
-#pragma unroll
-    for (int j = 0; j < 8; ++j) red[tid * 8 + j] = csum[j];
-    red[C::NT * 8 + tid] = ssum;
+    float* red = reinterpret_cast<float*>(wsdf_smem);   // [NT][4], then [NT] slope partials
+    *reinterpret_cast<float4*>(red + tid * 4) = make_float4(csum[0], csum[1], csum[2], csum[3]);
+    red[C::NT * 4 + tid] = ssum;
     __syncthreads();
-    for (int n = tid; n < N; n += C::NT) {   // thread t split row t / (N / 8), columns (t % (N / 8)) * 8 .. + 7
+    for (int n = tid; n < N; n += C::NT) {   // thread t owns columns (t % (N / 4)) * 4 .. + 3
       float tot = 0.0f;
-      for (int row = 0; row < C::BM; ++row) tot = __fadd_rn(tot, red[(row * (N / 8) + (n >> 3)) * 8 + (n & 7)]);
+      for (int m = 0; m < C::NT / (N / 4); ++m) tot = __fadd_rn(tot, red[(m * (N / 4) + (n >> 2)) * 4 + (n & 3)]);
       pro.pcol[(int64_t)n * gridDim.x + blockIdx.x] = tot;
     }
-    float* sr = red + C::NT * 8;
+    float* sr = red + C::NT * 4;
     for (int off = C::NT / 2; off > 0; off >>= 1) {
       __syncthreads();
       if (tid < off) sr[tid] = __fadd_rn(sr[tid], sr[tid + off]);
@@ -1251,12 +1245,13 @@ __global__ __launch_bounds__(512, 1) void k_wsd_f32(const float* __restrict__ A,
 // into plane buffer (i + 1) & 1 — independent work, so one barrier per block.  Waves 0-3 split first and waves 4-7
 // multiply first: the two waves sharing a SIMD (w, w + 4) run the VALU split and the MFMAs side by side instead of
 // both splitting, then both multiplying (MI355X_MICROARCH.md, "try a stagger").
-// The fp32 staging is ONE slot (g_y | z | B, 48 KB): thread t splits exactly the 32 B at byte 32 t of each image,
-// which is what its own wave's DMA pieces wrote, so a wave waits only on its own vmcnt before splitting and refills
-// its slice with the next block as soon as its split has read it — no cross-wave hazard on the slot, and the fill
-// has a whole block of MFMAs to land.  LDS: 48 KB slot + two 48 KB plane buffers = 144 KB.
-// Same blocks per workgroup, same per-thread groups, same per-element products in the same order: g_w, g_z and the
-// partial sums are bit-identical to k_wsd_f32 (HGIN_WSD_PIPE = 0 keeps it).
+// The fp32 staging is ONE slot (g_y | z | B, 48 KB): wave w splits exactly rows 2 w, 2 w + 1 of each image, which
+// is what its own DMA pieces wrote, so a wave waits only on its own vmcnt before splitting and refills its slice
+// with the next block as soon as its split has read it — no cross-wave hazard on the slot, and the fill has a whole
+// block of MFMAs to land.  LDS: 48 KB slot + two 48 KB plane buffers = 144 KB.
+// Same blocks per workgroup, planes and per-element products in the same order as k_wsd_f32: g_w and g_z are
+// bit-identical to it; the bias / slope partials are summed in another fixed order (round 5: the lane -> column map
+// that makes the slice reads conflict-free).  k_wsd_f32 no longer serves N = K = 256.
 struct WspF32Cfg {
   static constexpr int N = 256, K = 256, NT = 512, WM = 4, TK = 4, BM = 16;
   static constexpr int A_BYTES = BM * N * 4, B_BYTES = BM * K * 4;
@@ -1329,11 +1324,11 @@ __global__ __launch_bounds__(512, 1) void k_wsp_f32(const float* __restrict__ A,
       dma(k < k1 ? b1 + (r * (int)ldb1 + k) : b2 + (r * (int)ldb2 + (k - k1)), wsp_smem + B_OFF + piece * 1024);
     }
   };
-  float csum[8];
+  float csum[4];
   float ssum = 0.0f;
   const float sl = PRO ? pro.slope[0] : 0.0f;
 #pragma unroll
-  for (int j = 0; j < 8; ++j) csum[j] = 0.0f;
+  for (int j = 0; j < 4; ++j) csum[j] = 0.0f;
 
   f32x16 acc[2][C::TK];
 #pragma unroll
@@ -1349,58 +1344,58 @@ __global__ __launch_bounds__(512, 1) void k_wsp_f32(const float* __restrict__ A,
   };
   auto tr = [&](int off) { return __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(wsp_smem + off)); };
 
-  // block j (landed in this wave's slice) -> plane buffer j & 1, then the slice is refilled with block j + 1
+  // block j (landed in this wave's slice) -> plane buffer j & 1, then the slice is refilled with block j + 1.
+  // Wave w's slice is rows 2 w, 2 w + 1 of each image; lane l splits columns 4 l .. 4 l + 3 of both rows, so every
+  // ds_read_b128 of the slice is 64 consecutive 16-B pieces (conflict-free; the earlier 32-B-per-lane reads were 2-way
+  // conflicted: SQ_LDS_BANK_CONFLICT 32 % of the LDS-active cycles, profiles/r04/gpu_b/gemm_pmc2_sq.txt), and each
+  // plane row half-chunk goes out as one ds_write_b64 (16 contiguous lanes = 128 contiguous bytes).
   auto split = [&](int64_t j) {
     wait_vm<0>();                                    // this wave's pieces of block j (and its older stores)
     char* pl = planes0 + (int)(j & 1) * C::PLANES;
     const int64_t r0 = ((int64_t)blockIdx.x + j * G) * C::BM;
     const int valid = M - r0 < C::BM ? (int)(M - r0) : C::BM;
-    const int t = tid_o();
-    const int row = t / (N / 8), col = (t % (N / 8)) * 8;
-    const int off = C::PA_ROW * row + 16 * ((col >> 3) ^ wsd_swz(row));   // PA_ROW == PB_ROW
-    float4 va0 = *reinterpret_cast<const float4*>(wsp_smem + 32 * t);
-    float4 va1 = *reinterpret_cast<const float4*>(wsp_smem + 32 * t + 16);
-    float4 vb0 = *reinterpret_cast<const float4*>(wsp_smem + B_OFF + 32 * t);
-    float4 vb1 = *reinterpret_cast<const float4*>(wsp_smem + B_OFF + 32 * t + 16);
-    float4 z0 = make_float4(0.f, 0.f, 0.f, 0.f), z1 = z0;
-    if constexpr (PRO) {
-      z0 = *reinterpret_cast<const float4*>(wsp_smem + Z_OFF + 32 * t);
-      z1 = *reinterpret_cast<const float4*>(wsp_smem + Z_OFF + 32 * t + 16);
+    const int ln = tid_o() & 63;
+    const int rw = 2 * wave;
+    float4 va[2], vb[2], zv[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int o = (rw + h) * (N * 4) + 16 * ln;   // N == K: the images share the row pitch
+      va[h] = *reinterpret_cast<const float4*>(wsp_smem + o);
+      vb[h] = *reinterpret_cast<const float4*>(wsp_smem + B_OFF + o);
+      zv[h] = PRO ? *reinterpret_cast<const float4*>(wsp_smem + Z_OFF + o) : make_float4(0.f, 0.f, 0.f, 0.f);
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the slice is read: refill it
     if (j + 1 < my) issue(j + 1);
-    if (row >= valid) va0 = va1 = vb0 = vb1 = z0 = z1 = make_float4(0.f, 0.f, 0.f, 0.f);
-    if constexpr (PRO) {   // g_z from g_y and z; its store; the partial sums (k_wsd_f32's arithmetic)
-      float gg[8] = {va0.x, va0.y, va0.z, va0.w, va1.x, va1.y, va1.z, va1.w};
-      const float zz[8] = {z0.x, z0.y, z0.z, z0.w, z1.x, z1.y, z1.z, z1.w};
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const bool pos = zz[e] > 0.0f;
-        const float o = pos ? gg[e] : __fmul_rn(sl, gg[e]);
-        csum[e] = __fadd_rn(csum[e], o);
-        if (!pos) ssum = __fadd_rn(ssum, __fmul_rn(zz[e], gg[e]));
-        gg[e] = o;
+    for (int h = 0; h < 2; ++h) {
+      const int row = rw + h;
+      if (row >= valid) va[h] = vb[h] = zv[h] = make_float4(0.f, 0.f, 0.f, 0.f);
+      if constexpr (PRO) {   // g_z from g_y and z; its store; the partial sums (k_rows_bwd<0>'s arithmetic)
+        float gg[4] = {va[h].x, va[h].y, va[h].z, va[h].w};
+        const float zz[4] = {zv[h].x, zv[h].y, zv[h].z, zv[h].w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const bool pos = zz[e] > 0.0f;
+          const float o = pos ? gg[e] : __fmul_rn(sl, gg[e]);
+          csum[e] = __fadd_rn(csum[e], o);
+          if (!pos) ssum = __fadd_rn(ssum, __fmul_rn(zz[e], gg[e]));
+          gg[e] = o;
+        }
+        va[h] = make_float4(gg[0], gg[1], gg[2], gg[3]);
+        const int64_t gr = r0 + row;
+        float* gzp = gr < M ? static_cast<float*>(pro.gz) + gr * pro.ldgz + 4 * ln
+                            : reinterpret_cast<float*>(pro.dump + (int64_t)(wave * 64 + ln) * 32 + 16 * h);
+        *reinterpret_cast<float4*>(gzp) = va[h];
       }
-      va0 = make_float4(gg[0], gg[1], gg[2], gg[3]);
-      va1 = make_float4(gg[4], gg[5], gg[6], gg[7]);
-      const int64_t gr = r0 + row;
-      float* gzp = gr < M ? static_cast<float*>(pro.gz) + gr * pro.ldgz + col
-                          : reinterpret_cast<float*>(pro.dump + (int64_t)t * 32);
-      *reinterpret_cast<float4*>(gzp) = va0;
-      *reinterpret_cast<float4*>(gzp + 4) = va1;
+      const int off = C::PA_ROW * row + 16 * ((ln >> 1) ^ wsd_swz(row)) + 8 * (ln & 1);   // PA_ROW == PB_ROW
+      uint2 o[3];
+      split4(va[h], o);
+#pragma unroll
+      for (int p = 0; p < 3; ++p) *reinterpret_cast<uint2*>(pl + p * C::PA_BYTES + off) = o[p];
+      split4(vb[h], o);
+#pragma unroll
+      for (int p = 0; p < 3; ++p) *reinterpret_cast<uint2*>(pl + 3 * C::PA_BYTES + p * C::PB_BYTES + off) = o[p];
     }
-    uint2 o0[3], o1[3];
-    split4(va0, o0);
-    split4(va1, o1);
-#pragma unroll
-    for (int p = 0; p < 3; ++p)
-      *reinterpret_cast<uint4*>(pl + p * C::PA_BYTES + off) = make_uint4(o0[p].x, o0[p].y, o1[p].x, o1[p].y);
-    split4(vb0, o0);
-    split4(vb1, o1);
-#pragma unroll
-    for (int p = 0; p < 3; ++p)
-      *reinterpret_cast<uint4*>(pl + 3 * C::PA_BYTES + p * C::PB_BYTES + off) =
-          make_uint4(o0[p].x, o0[p].y, o1[p].x, o1[p].y);
   };
   // block i's products from plane buffer i & 1 (k_wsd_f32's fragments and order)
   auto mfma = [&](int64_t i) {
@@ -1459,21 +1454,20 @@ __global__ __launch_bounds__(512, 1) void k_wsp_f32(const float* __restrict__ A,
   asm volatile("" ::: "memory");
   mfma(my - 1);
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  if constexpr (PRO) {   // k_wsd_f32's fixed-order workgroup sums (same thread -> group map)
+  if constexpr (PRO) {   // fixed-order workgroup sums: column n = 4 l + e over the 8 waves' row pairs
     wait_vm<0>();
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
-    float* red = reinterpret_cast<float*>(wsp_smem);   // [NT][8], then [NT] slope partials
-#pragma unroll
-    for (int j = 0; j < 8; ++j) red[tid * 8 + j] = csum[j];
-    red[C::NT * 8 + tid] = ssum;
+    float* red = reinterpret_cast<float*>(wsp_smem);   // [NT][4], then [NT] slope partials
+    *reinterpret_cast<float4*>(red + tid * 4) = make_float4(csum[0], csum[1], csum[2], csum[3]);
+    red[C::NT * 4 + tid] = ssum;
     __syncthreads();
     for (int n = tid; n < N; n += C::NT) {
       float tot = 0.0f;
-      for (int row = 0; row < C::BM; ++row) tot = __fadd_rn(tot, red[(row * (N / 8) + (n >> 3)) * 8 + (n & 7)]);
+      for (int w = 0; w < C::NT / 64; ++w) tot = __fadd_rn(tot, red[(w * 64 + (n >> 2)) * 4 + (n & 3)]);
       pro.pcol[(int64_t)n * gridDim.x + blockIdx.x] = tot;
     }
-    float* sr = red + C::NT * 8;
+    float* sr = red + C::NT * 4;
     for (int off = C::NT / 2; off > 0; off >>= 1) {
       __syncthreads();
       if (tid < off) sr[tid] = __fadd_rn(sr[tid], sr[tid + off]);
@@ -1493,16 +1487,6 @@ __global__ __launch_bounds__(512, 1) void k_wsp_f32(const float* __restrict__ A,
         out[n * ld_slab + k] = acc[tm][tn][e];
       }
     }
-}
-
-// HGIN_WSD_PIPE = 0 keeps k_wsd_f32 at N = K = 256 (the pipelined form: cfg3 187.8 -> 185.9 ms, the K = 512 dW at
-// M = 6M 10.85 -> 10.05 ms, the PReLU-fused K = 256 dW 5.92 -> 5.65 ms: profiles/r04/gpu_a/)
-bool wsp_enabled() {
-  static const bool on = [] {
-    const char* v = getenv("HGIN_WSD_PIPE");
-    return !(v && v[0] == '0');
-  }();
-  return on;
 }
 
 // Weight-stationary dW launch (HGIN_TN_WS = 0 / 1; default on): bf16, N in {128, 256}, K in {128, 256, 512},
@@ -1561,27 +1545,25 @@ int64_t launch_wsd(const float* a, int64_t lda, const float* b1, int64_t ldb1, c
     const char* v = getenv("HGIN_WS_NT");
     return !(v && v[0] == '0');
   }();
-  if constexpr (NV == 256 && KV == 256) {
-    if (wsp_enabled()) {
-      auto kp = k_wsp_f32<PRO>;
-      constexpr int plds = WspF32Cfg::lds<PRO>();
-      static const hipError_t pattr = hipFuncSetAttribute(reinterpret_cast<const void*>(kp),
-                                                          hipFuncAttributeMaxDynamicSharedMemorySize, plds);
-      if (pattr == hipSuccess) {
-        HGIN_TRACE("k_wsp_f32<%d,%d%s>", NV, KV, PRO ? ",prelu_bwd_fused" : "");
-        kp<<<(unsigned)grid, 512, plds, s>>>(a, lda, b1, ldb1, b2, ldb2, k1, M, slab, ld_slab, nt, pro);
-        return grid;
-      }
-    }
+  if constexpr (NV == 256 && KV == 256) {   // the GIN width: the pipelined form (k_wsd_f32 measured 3-8 % slower
+    auto kp = k_wsp_f32<PRO>;                 // here, profiles/r04/gpu_a/; removed from this shape in round 5)
+    constexpr int plds = WspF32Cfg::lds<PRO>();
+    static const hipError_t pattr = hipFuncSetAttribute(reinterpret_cast<const void*>(kp),
+                                                        hipFuncAttributeMaxDynamicSharedMemorySize, plds);
+    if (pattr != hipSuccess) return 0;
+    HGIN_TRACE("k_wsp_f32<%d,%d%s>", NV, KV, PRO ? ",prelu_bwd_fused" : "");
+    kp<<<(unsigned)grid, 512, plds, s>>>(a, lda, b1, ldb1, b2, ldb2, k1, M, slab, ld_slab, nt, pro);
+    return grid;
+  } else {
+    constexpr int lds = WsdF32Cfg<NV, KV, PRO>::LDS;
+    auto kern = k_wsd_f32<NV, KV, PRO>;
+    static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                                                       hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    if (attr != hipSuccess) return 0;
+    HGIN_TRACE("k_wsd_f32<%d,%d%s>", NV, KV, PRO ? ",prelu_bwd_fused" : "");
+    kern<<<(unsigned)grid, 512, lds, s>>>(a, lda, b1, ldb1, b2, ldb2, k1, M, slab, ld_slab, nt, pro);
+    return grid;
   }
-  constexpr int lds = WsdF32Cfg<NV, KV, PRO>::LDS;
-  auto kern = k_wsd_f32<NV, KV, PRO>;
-  static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
-                                                     hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-  if (attr != hipSuccess) return 0;
-  HGIN_TRACE("k_wsd_f32<%d,%d%s>", NV, KV, PRO ? ",prelu_bwd_fused" : "");
-  kern<<<(unsigned)grid, 512, lds, s>>>(a, lda, b1, ldb1, b2, ldb2, k1, M, slab, ld_slab, nt, pro);
-  return grid;
 }
 
 // One weight-stationary pass over output columns [c0, c0 + KV) of B = [b1 (k1 columns) | b2].

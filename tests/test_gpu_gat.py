@@ -57,7 +57,7 @@ def test_attention_and_aggregate_vs_reference(case):
             g = gat_graph(ei[(src, key.split("__")[1], dst)], xs.size(0), xd.size(0), True)
             with _lib.trace_launches() as tr:
                 agg = _GatAttentionFn.apply(xs, xd, conv.att_src, conv.att_dst, None, None, g, H, C, 0.2)
-            assert "k_gat_fwd" in tr.kernels
+            assert any(t.startswith("k_gat_fwd_w<") for t in tr.kernels), tr.kernels   # the wave-group form
             want = fx[f"agg.0.{key}"]
             assert _close(agg.view(-1, H, C), want), (key, float((agg.cpu().view(-1, H, C) - want).abs().max()))
             # alpha of CSR position p belongs to edge perm[p] of the adjusted list
@@ -136,3 +136,37 @@ def test_later_layers_reject_multi_head_inputs_like_the_reference():
     model = HetroGAT(**kw).to(DEV)
     out = model(dict(x), ei, batch)
     assert out.shape == (x["path"].size(0), 1) and torch.isfinite(out).all()
+
+
+@pytest.mark.parametrize("H,C", [(16, 8), (4, 16), (1, 8), (3, 6), (2, 2)])
+def test_relation_forward_backward_vs_oracle(H, C):
+    """One relation's attention forward + backward, both kernel forms (the wave-group form for C in {8, 16}; the
+    thread-per-(row, head) form for C = 6, 2), against the oracle's GATConv restatement (oracle.pyg_cpu.gat_relation)
+    evaluated in float64 with autograd: output within 1e-5 (abs + rel), every gradient within 1e-5 of its norm."""
+    from hgin import _lib
+    from hgin.gat import _GatAttentionFn, gat_graph
+    from oracle.pyg_cpu import gat_relation
+    gen = torch.Generator().manual_seed(100 * H + C)
+    ns, nd, E = 700, 500, 6000
+    ei = torch.stack([torch.randint(0, ns, (E,), generator=gen), torch.randint(0, nd, (E,), generator=gen)])
+    ei[:, :40] = torch.arange(40).repeat(2, 1)                       # coincident indices: removed, then re-added
+    xs, xd = torch.randn(ns, H * C, generator=gen), torch.randn(nd, H * C, generator=gen)
+    att_s, att_d = 0.3 * torch.randn(1, H, C, generator=gen), 0.3 * torch.randn(1, H, C, generator=gen)
+    bias, g_out = torch.randn(H * C, generator=gen), torch.randn(nd, H * C, generator=gen)
+    ref = [t.double().requires_grad_() for t in (xs, xd, att_s, att_d, bias)]
+    _, agg = gat_relation(ref[0].view(ns, H, C), ref[1].view(nd, H, C), ei, ref[2], ref[3])
+    out_ref = agg.reshape(nd, H * C) + ref[4]
+    out_ref.backward(g_out.double())
+    dev = [t.to(DEV).requires_grad_() for t in (xs, xd, att_s, att_d, bias)]
+    graph = gat_graph(ei.to(DEV), ns, nd, True)
+    with _lib.trace_launches() as tr:
+        out = _GatAttentionFn.apply(dev[0], dev[1], dev[2], dev[3], dev[4], None, graph, H, C, 0.2)
+        out.backward(g_out.to(DEV))
+        torch.cuda.synchronize()
+    wave = C % 4 == 0
+    for k in ("k_gat_logits", "k_gat_fwd", "k_gat_bwd_dst", "k_gat_bwd_src"):
+        assert any(t.startswith(k + "_w<") for t in tr.kernels) == wave, (k, tr.kernels)
+    assert _close(out, out_ref), float((out.detach().cpu().double() - out_ref.detach()).abs().max())
+    for name, a, b in zip(("x_s", "x_d", "att_src", "att_dst", "bias"), dev, ref):
+        d = float((a.grad.double().cpu() - b.grad).norm())
+        assert d <= 1e-5 * float(b.grad.norm()) + 1e-9, (name, d, float(b.grad.norm()))

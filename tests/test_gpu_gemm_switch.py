@@ -13,13 +13,10 @@
                               pre-split planes by LDS-DMA;
   * HGIN_NT_T256=0          — the fp32 split tile at 128 x 128 instead of 128 x 256 (N a multiple of 256: the
                               K = 512 forward);
-  * HGIN_WS_PIPE=1          — the one-wave-per-SIMD pipelined fp32 forward / dX form (k_wsf_f32; with
-                              HGIN_GEMM_NT_IO=1, its precondition, so it runs at these sizes);
-  * HGIN_WSD_PIPE=0         — k_wsd_f32 instead of the pipelined fp32 dW (k_wsp_f32);
-  * HGIN_WS_STAGGER=0       — k_ws_f32 instead of the staggered two-stage fp32 forward (k_wss_f32);
-  * HGIN_WS_STAGGER_ACC=1   — the staggered forward also for the accumulating calls;
-  (The measured-and-removed fp32 tile variants — 128 x 256 / k_nt_pipe, double-buffered B, the ping-pong k_nt_pp and
-  the 16 x 16 x 32 MFMA tile — are listed in DESIGN.md §3 with their commits.)
+  * HGIN_WS_STAGGER=0       — k_ws_f32 instead of the staggered two-stage fp32 forward / dX-combine GEMM (k_wss_f32);
+  (The measured-and-removed variants — the fp32 128 x 256 / k_nt_pipe tiles, double-buffered B, the ping-pong k_nt_pp,
+  the 16 x 16 x 32 MFMA tile, and in round 5 the one-wave-per-SIMD k_wsf_f32 and k_wsd_f32 at N = K = 256 — are
+  listed in DESIGN.md §3 with their commits.)
 
 Every child checks its outputs against an fp32 evaluation of the same bf16 operands; the three settings must
 agree bit for bit (same products, same per-accumulator k order, same epilogue arithmetic), except the combine's
@@ -40,10 +37,7 @@ SWITCHES = {"default": {}, "tiled": {"HGIN_NT_WS": "0", "HGIN_TN_WS": "0", "HGIN
             "tiled_bk128": {"HGIN_NT_WS": "0", "HGIN_NT_BKH": "128", "HGIN_TN_WS": "0", "HGIN_NT_WS32": "0"},
             "tiled_nobdma": {"HGIN_NT_WS": "0", "HGIN_TN_WS": "0", "HGIN_NT_WS32": "0", "HGIN_NT_BDMA": "0"},
             "t256_off": {"HGIN_NT_T256": "0"},
-            "ws_pipe": {"HGIN_WS_PIPE": "1", "HGIN_GEMM_NT_IO": "1"},
-            "wsd_pipe_off": {"HGIN_WSD_PIPE": "0"},
-            "ws_stagger_off": {"HGIN_WS_STAGGER": "0"},
-            "ws_stagger_acc": {"HGIN_WS_STAGGER_ACC": "1"}}
+            "ws_stagger_off": {"HGIN_WS_STAGGER": "0"}}
 _results = {}
 
 
@@ -66,8 +60,7 @@ def test_switch_within_tolerance(name):
     _run(name)        # the child checks against fp32 itself
 
 
-@pytest.mark.parametrize("name", ["tiled", "tiled_bk128", "tiled_nobdma", "t256_off", "ws_pipe", "wsd_pipe_off",
-                                  "ws_stagger_off", "ws_stagger_acc"])
+@pytest.mark.parametrize("name", ["tiled", "tiled_bk128", "tiled_nobdma", "t256_off", "ws_stagger_off"])
 def test_switch_bitwise_equal_default(name):
     ref, got = _run("default"), _run(name)
     assert ref.keys() == got.keys()

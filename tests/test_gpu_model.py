@@ -56,10 +56,10 @@ def _layer_input(fx, li, key, n_src):
 
 # the kernels the headline width runs (K = 512 first layer, K = N = 256 above it), as trace tags
 W256_KERNELS = (r"k_gemm_nt<EPI1,\d+x\d+,split,N256,K512>",                # first layer forward (eps-scaled self half)
-                r"k_ws(s_f32<[01],[01]>|_f32<256,256,EPI1>)",              # layers 1-2 forward (staggered)
-                r"k_ws[dp]_f32<256,256,prelu_bwd_fused>",                   # dW + PReLU bwd (g_z out): every layer
-                r"k_ws[dp]_f32<256,256>",                                   # first layer dW, columns [256, 512)
-                r"k_ws_f32<256,256,EPI4>")                                  # layers 1-2 dX + self-term backward
+                r"k_wss_f32<EPI1,[01],[01]>",                               # layers 1-2 forward (staggered)
+                r"k_wsp_f32<256,256,prelu_bwd_fused>",                      # dW + PReLU bwd (g_z out): every layer
+                r"k_wsp_f32<256,256>",                                      # first layer dW, columns [256, 512)
+                r"k_wss_f32<EPI4,1,[01]>")                                  # layers 1-2 dX + self-term backward
 
 
 @pytest.mark.parametrize("case", CASES)

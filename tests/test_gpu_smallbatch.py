@@ -1,9 +1,14 @@
 """The fused small-batch train step (hgin/smallbatch.py, csrc/hgin_smallbatch.hip): the reference's real loop
-(dataset.py:26, :239-244; train.py:25-44) in 3 L + 1 launches + Adam per batch, against the general path — eager exact-
-batch steps through the per-op HIP kernels (hgin.train.train_step), which are themselves pinned to the reference
-fixtures (tests/test_gpu_model.py).  Same batches, same initial parameters: loss values within 1e-5 relative, the
-gradients within 1e-5 of their norm (the fused kernels re-associate the GEMM-shaped sums and apply the sqrt-MAPE scale
-after the reduction), parameters after several Adam steps within 1e-3 of their total change; bitwise run-to-run."""
+(dataset.py:26, :239-244; train.py:25-44) in 3 L + 1 launches + Adam per batch.
+
+* Against the CPU oracle (oracle/pyg_cpu.py, itself pinned bit-for-bit to the reference-executed fixtures), on the
+  batch collated on the host and checked against oracle/collate_np.py (the numpy restatement of PyG's
+  ``Batch.from_data_list``): loss within 1e-5 relative and every gradient within 1e-4 of its norm at L = 1, 2, 3; a
+  five-step Adam trajectory within 1e-4 relative per loss (train.py:31-44 = oracle.pyg_cpu.train_step).
+* Against the general path — eager exact-batch steps through the per-op HIP kernels (hgin.train.train_step): loss
+  values within 1e-5 relative, the gradients within 1e-5 of their norm (the fused kernels re-associate the GEMM-shaped
+  sums and apply the sqrt-MAPE scale after the reduction), parameters after several Adam steps within 1e-3 of their
+  total change; bitwise run-to-run."""
 import numpy as np
 import pytest
 import torch
@@ -30,6 +35,79 @@ def _model(cfg, layers=None):
     if layers:
         kw["message_passing_layers"] = layers
     return HetroGIN(**kw).to(DEV)
+
+
+def _oracle_twin(model, cfg, layers=None):
+    """OracleHetroGIN with the same constructor arguments and the HIP model's parameters (on the host)."""
+    from oracle.pyg_cpu import OracleHetroGIN
+    kw = cfg.model_kwargs({"link": cfg.f_link, "path": cfg.f_path, "node": cfg.f_node})
+    if layers:
+        kw["message_passing_layers"] = layers
+    ref = OracleHetroGIN(**kw)
+    ref.load_state_dict({k: v.detach().cpu() for k, v in model.state_dict().items()})
+    return ref
+
+
+def _host_batch(store, ids):
+    """The batch on the host, pinned to the numpy restatement of PyG's collation of the same graphs."""
+    from oracle import collate_np
+    b = store.collate(ids).to("cpu")
+    want = collate_np.collate([collate_np.from_graph(store.collate([i]).to("cpu")) for i in ids])
+    for t in b.x:
+        assert torch.equal(b.x[t], torch.from_numpy(want["x"][t])), t
+        assert torch.equal(b.batch[t], torch.from_numpy(want["batch"][t])), t
+    for r in b.edge_index:
+        assert torch.equal(b.edge_index[r], torch.from_numpy(want["edge_index"][r])), r
+    assert torch.equal(b.y, torch.from_numpy(want["y"]))
+    return b
+
+
+@pytest.mark.parametrize("layers", [1, 2, 3])
+def test_fused_step_vs_oracle(layers):
+    """One fused step (Adam at lr 0) against the CPU oracle's forward / sqrt-MAPE backward on the host-collated batch."""
+    from hgin.smallbatch import SmallBatchStep
+    from oracle.pyg_cpu import mape
+    store, cfg = _store(10, seed=11)
+    ids = [2, 8, 5, 0]
+    m1 = _model(cfg, layers)
+    ref = _oracle_twin(m1, cfg, layers)
+    o1 = torch.optim.Adam(m1.parameters(), lr=0.0, capturable=True)
+    step = SmallBatchStep(m1, o1, store, batch_size=5, warmup_ids=[ids], warmup=1)
+    lv = float(step.step(ids))
+    torch.cuda.synchronize()
+    b = _host_batch(store, ids)
+    out = ref(b.x_dict(), b.edge_index_dict(), b.batch["path"])
+    lv_ref = mape(out, b.y.reshape(-1, 1))
+    torch.sqrt(lv_ref).backward()
+    assert abs(lv - float(lv_ref)) <= 1e-5 * abs(float(lv_ref)), (lv, float(lv_ref))
+    for (n, p), (n2, q) in zip(m1.named_parameters(), ref.named_parameters()):
+        assert n == n2
+        want = q.grad if q.grad is not None else torch.zeros_like(q)
+        d = float((p.grad.detach().cpu() - want).double().norm())
+        assert d <= 1e-4 * float(want.double().norm()) + 1e-9, (n, d, float(want.norm()))
+
+
+def test_fused_trajectory_vs_oracle():
+    """Five shuffled batches with Adam(lr=1e-3) (train.py:31-44): the fused step's loss trajectory against
+    oracle.pyg_cpu.train_step on the host-collated batches, within 1e-4 relative per step."""
+    from hgin.smallbatch import SmallBatchStep
+    from oracle.pyg_cpu import train_step as oracle_step
+    store, cfg = _store(12, seed=13)
+    seq = [[1, 6, 10], [4, 0, 11], [8, 3, 5], [9, 7, 2], [3, 10, 1]]
+    m1 = _model(cfg)
+    ref = _oracle_twin(m1, cfg)
+    o1 = torch.optim.Adam(m1.parameters(), lr=1e-3, capturable=True)
+    step = SmallBatchStep(m1, o1, store, batch_size=3, warmup_ids=[seq[0]], warmup=1)
+    o2 = torch.optim.Adam(ref.parameters(), lr=1e-3)
+    hb = {tuple(ids): _host_batch(store, ids) for ids in seq}
+
+    def oracle(ids):
+        b = hb[tuple(ids)]
+        return float(oracle_step(ref, o2, b.x_dict(), b.edge_index_dict(), b.batch["path"], b.y))
+    oracle(seq[0])   # the warm-up's Adam step
+    for k, ids in enumerate(seq):
+        got, want = float(step.step(ids)), oracle(ids)
+        assert abs(got - want) <= 1e-4 * abs(want), (k, got, want)
 
 
 @pytest.mark.parametrize("layers", [2, 1, 3])

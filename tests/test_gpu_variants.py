@@ -12,12 +12,9 @@ fixtures (tests/variant_child.py), so the non-default paths pytest's own process
                               fused one: bit-identical (same g_z, same dW partition; the bias / slope sums are
                               grouped differently, so those two gradients are compared within fixture tolerance);
   * HGIN_NT_BDMA=0          — the NT GEMM splitting B per tile instead of copying pre-split planes: bit-identical;
-  * HGIN_WSD_PIPE=0         — k_wsd_f32 instead of the software-pipelined fp32 dW at N = K = 256 (k_wsp_f32):
-                              bit-identical;
-  * HGIN_WS_STAGGER=0       — k_ws_f32 instead of the staggered two-stage fp32 forward GEMM (k_wss_f32);
-  * HGIN_WS_PIPE=1          — the one-wave-per-SIMD pipelined fp32 forward / dX GEMM (k_wsf_f32, with
-                              HGIN_GEMM_NT_IO=1 so it runs at fixture sizes): bit-identical but for the regrouped GIN
-                              eps gradients.
+  * HGIN_WS_STAGGER=0       — k_ws_f32 instead of the staggered two-stage fp32 forward / dX-combine GEMM (k_wss_f32):
+                              bit-identical but for the regrouped GIN eps gradients (the dX GEMM's per-workgroup
+                              partials).
 
 Each child is a separate interpreter started with subprocess (never an exec of this process).
 """
@@ -43,21 +40,18 @@ VARIANTS = {
     "gemm_nt_io": {"HGIN_GEMM_NT_IO": "1"},
     "wsd_pro_off": {"HGIN_WSD_PRO": "0"},
     "nt_bdma_off": {"HGIN_NT_BDMA": "0"},
-    "wsd_pipe_off": {"HGIN_WSD_PIPE": "0"},
-    # the pipelined forward / dX form runs only with non-temporal epilogue streams (forced here: the fixtures are small)
-    "ws_pipe": {"HGIN_WS_PIPE": "1", "HGIN_GEMM_NT_IO": "1"},
     "ws_stagger_off": {"HGIN_WS_STAGGER": "0"},
 }
 BITWISE_EQUAL_TO_DEFAULT = ("slab2pass", "agg_pipe", "agg_notail", "xcd_off", "agg_nt_all", "gemm_nt_io", "wsd_pro_off",
-                            "nt_bdma_off", "wsd_pipe_off", "ws_pipe", "ws_stagger_off")
+                            "nt_bdma_off", "ws_stagger_off")
 
 # Scalar / column-sum gradients a variant regroups: the bias / PReLU-slope sums (per workgroup in the fused
 # weight-stationary dW, per row block in k_rows_bwd<0>).  Everything else must stay bit-identical.
 # (wsd_pro_off: every Linear bias / PReLU slope behind a fused PReLU backward — GIN MLPs and readout layers alike —
 # is summed per row block by the separate pass instead of per workgroup of the fused dW)
 REGROUPED = {"wsd_pro_off": (".0.bias", ".1.weight"),
-             # the dX GEMM's eps-gradient partials are per workgroup, and the pipelined form's workgroups differ
-             "ws_pipe": (".conv.eps",)}
+             # the dX GEMM's eps-gradient partials are per workgroup, summed per thread in another order by k_ws_f32
+             "ws_stagger_off": (".conv.eps",)}
 
 _results = {}
 

@@ -1,4 +1,4 @@
-"""Static check of the weight-stationary kernels (k_ws_bf16 / k_ws_f32 in hgin_gemm_nt.hip, k_wsd_* / k_wsp_f32 in
+"""Static check of the weight-stationary kernels (k_ws_bf16 / k_ws_f32 / k_wss_f32 in hgin_gemm_nt.hip, k_wsd_* / k_wsp_f32 in
 hgin_gemm_tn.hip)
 in their gfx950 assembly: the
 counted-vmcnt ring is only correct when the loop holds no compiler-visible vector-memory load (the compiler's
@@ -17,46 +17,6 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SRCS = [os.path.join(ROOT, "gnn-link-prediction_amd", "csrc", f) for f in ("hgin_gemm_nt.hip", "hgin_gemm_tn.hip")]
 
 
-def _regs(tok):
-    m = re.fullmatch(r"v\[(\d+):(\d+)\]", tok)
-    if m:
-        return set(range(int(m.group(1)), int(m.group(2)) + 1))
-    m = re.fullmatch(r"v(\d+)", tok)
-    return {int(m.group(1))} if m else set()
-
-
-def mfma_chain_hazards(body):
-    """k_wsf_f32's MFMAs are inline asm, so hipcc neither pads around them nor knows their results arrive late: check
-    that between an MFMA and the next MFMA continuing its accumulator chain no other instruction touches the
-    accumulator, and that a chain's result is read only after the s_nop padding (two s_nop 7)."""
-    lines = [ln.split(";")[0].strip() for ln in body.split("\n")]
-    for n, ln in enumerate(lines):
-        if not ln.startswith("v_mfma_f32_32x32x16_bf16"):
-            continue
-        dst = _regs(ln.split(None, 1)[1].split(",")[0].strip())
-        nops = 0
-        for k in range(n + 1, len(lines)):
-            x = lines[k]
-            if not x or x.startswith(".") or x.endswith(":"):
-                continue
-            if x.startswith("s_nop 7"):
-                nops += 1
-                continue
-            if x.startswith("v_mfma"):
-                ops = [o.strip() for o in x.split(None, 1)[1].split(",")]
-                if _regs(ops[0]) == dst and _regs(ops[3]) == dst:
-                    break                                   # the chain continues
-                if any(_regs(o) & dst for o in ops):
-                    return f"MFMA at line {n} feeds another MFMA's operand (line {k})"
-                continue
-            toks = re.findall(r"v\[\d+:\d+\]|v\d+", x)
-            if any(_regs(t) & dst for t in toks):
-                if nops >= 2:
-                    break                                   # read after the padding: the chain's end
-                return f"accumulator of the MFMA at line {n} touched at line {k} ({x[:40]})"
-    return ""
-
-
 def main():
     s = ""
     with tempfile.TemporaryDirectory() as d:
@@ -67,20 +27,13 @@ def main():
             subprocess.run(cmd, check=True, capture_output=True)
             s += open(out).read()
     bad = 0
-    for m in re.finditer(r"^(_ZN4hgin12_GLOBAL__N_1\d+k_wsf_f32\S*):", s, re.M):
-        body = s[m.end():s.index(".Lfunc_end", m.end())]
-        err = mfma_chain_hazards(body)
-        bad += bool(err)
-        name = re.search(r"(k_wsf_f32I.*?)EEEv", m.group(1)).group(1)
-        print(f"{'BAD' if err else 'ok '} {name}: inline-asm MFMA chains " + (err or "untouched between their MFMAs, "
-              "read only after the s_nop padding"))
-    for m in re.finditer(r"^(_ZN4hgin12_GLOBAL__N_1\d+k_ws(?:d?_bf16|[dpf]?_f32)\S*):", s, re.M):
+    for m in re.finditer(r"^(_ZN4hgin12_GLOBAL__N_1\d+k_ws(?:d?_bf16|[dps]?_f32)\S*):", s, re.M):
         body = s[m.end():s.index(".Lfunc_end", m.end())]
         loop = body[body.find("Loop Header"):] if "Loop Header" in body else body
         scratch = len(re.findall(r"\bscratch_(load|store)|buffer_(load|store)_dword\S* \S+, off, s\[0:3\]", body))
         loads_in_loop = len(re.findall(r"\bglobal_load_(?!lds)\w+", loop))
         waits = sorted(set(int(x) for x in re.findall(r"s_waitcnt vmcnt\((\d+)\)", loop)))
-        name = re.search(r"(k_ws(?:d?_bf16|[dpf]?_f32)I.*?)EEEv", m.group(1)).group(1)
+        name = re.search(r"(k_ws(?:d?_bf16|[dps]?_f32)I.*?)EEEv", m.group(1)).group(1)
         ok = scratch == 0 and loads_in_loop == 0
         bad += not ok
         print(f"{'ok ' if ok else 'BAD'} {name}: scratch ops {scratch}, VGPR-destination global loads in the loop "
