@@ -33,6 +33,7 @@ Rank 0 prints one JSON line.
 from __future__ import annotations
 
 import argparse
+import ctypes
 import dataclasses
 import json
 import os
@@ -250,21 +251,26 @@ def one_gpu_reference(cfg, n_comp: int, dev, adam: str, graph_mode: bool, warmup
             "what": "rank 0 alone, all components of the split graph, after the timed region"}
 
 
-def batches_extra(dev, n_graphs: int = 256, batch: int = 8, warmup: int = 5, steps: int = 200) -> dict:
+def batches_extra(dev, n_graphs: int = 256, batch: int = 8, warmup: int = 5, steps: int = 200,
+                  cfg_steps: int = 40) -> dict:
     """The reference's actual training loop (dataset.py:26, :239-244, train.py:25-44): shuffled
     batches of 8 small graphs.  Here: a cfg1-schema GraphStore (n_graphs RouteNet-sized graphs, 0.5x-1.5x cfg1,
     the reference's always-on normalisation applied once at build); each step = one device collation launch
     (GraphStore.collate_into) + one hipGraph replay of the whole train step: the fused small-batch step
-    (hgin/smallbatch.py: 3 L + 1 kernels + fused Adam) where it takes the model, and the general per-op path
-    (hgin/graphs.py CapturedTrainStep) beside it.  HIP events around the timed batches; reported beside the
-    headline, not in it."""
+    (hgin/smallbatch.py: 3 L + 1 kernels, Adam folded in) — the main figure whenever it takes config.json's model — and
+    the general per-op path (hgin/graphs.py CapturedTrainStep) beside it.  ``configs``: the reference's other model
+    switches (models.py / config.json) that the fused step refuses, each timed on the same batches through the path
+    that takes it — MLP_BN, GLOBAL_FEATS and DROPOUT > 0 (eager exact batches: BatchNorm statistics, pooling and
+    dropout must not see padding rows), NODE_EMBEDDING_SIZE 128 and MODEL = "GAT" (HEADS 16, config.json's hidden 8
+    and 1 layer) as hipGraph replays.  HIP events around the timed batches; reported beside the headline."""
     import numpy as np
 
-    from hgin import HetroGIN
+    from hgin import HetroGAT, HetroGIN
     from hgin.data import CONFIGS, CONV_RELATIONS, scaled_config, synthetic_graph
     from hgin.graphs import CapturedTrainStep
     from hgin.smallbatch import SmallBatchStep
     from hgin.store import GraphStore
+    from hgin.train import train_step
     base = CONFIGS["cfg1"]
     rng = np.random.default_rng(0)
     graphs = [synthetic_graph(scaled_config(base, float(rng.uniform(0.5, 1.5)), name=f"g{i}"), seed=i)
@@ -273,62 +279,202 @@ def batches_extra(dev, n_graphs: int = 256, batch: int = 8, warmup: int = 5, ste
     order = [rng.choice(n_graphs, batch, replace=False).tolist() for _ in range(warmup + steps)]
     conv_edges = [sum(int(store.edge_off[r][g + 1] - store.edge_off[r][g]) for r in CONV_RELATIONS for g in ids)
                   for ids in order[warmup:]]
+    ic = lambda: {"link": base.f_link, "path": base.f_path, "node": base.f_node}   # noqa: E731
 
-    def run(kind):
+    def build(overrides=None, gat=False):
         torch.manual_seed(1997)
-        model = HetroGIN(**base.model_kwargs({"link": base.f_link, "path": base.f_path, "node": base.f_node})).to(dev)
-        # the fused step's parameters share one flat gradient buffer: fused Adam (three multi-tensor launches
-        # instead of the foreach chain's ~26; same update rule).  The general path keeps the foreach form (measured
-        # faster there: 0.70 vs 0.90 ms per batch, profiles/r04/gpu_e)
-        opt = torch.optim.Adam(lr=1e-3, params=model.parameters(), capturable=True,
-                               **({"fused": True} if kind == "fused" else {}))
+        kw = base.model_kwargs(ic())
+        kw.update(overrides or {})
+        if gat:
+            kw = dict(kw, heads=16, node_embedding_size=8, message_passing_layers=1)
+            return HetroGAT(**kw).to(dev)
+        return HetroGIN(**kw).to(dev)
+
+    def run(kind, model, n_steps):
+        # the fused step folds Adam into its final kernel (SmallBatchStep(fold_optimizer=True)); the other paths run
+        # torch's foreach Adam (measured faster there than fused Adam: 0.70 vs 0.90 ms per batch, profiles/r04/gpu_e)
+        opt = torch.optim.Adam(lr=1e-3, params=model.parameters(), capturable=kind != "eager")
+        seq = order[warmup:warmup + n_steps]
         if kind == "fused":
             stepper = SmallBatchStep(model, opt, store, batch, warmup_ids=order[:warmup], warmup=warmup)
-        else:
+            step = stepper.step
+        elif kind == "captured":
             stepper = CapturedTrainStep(model, opt, store, batch, warmup_ids=order[:warmup], warmup=warmup)
+            step = stepper.step
+        else:   # eager exact batches: collation + every launch from the host per batch
+            step = lambda ids: train_step(model, opt, store.collate(ids))   # noqa: E731
+            for ids in order[:warmup]:
+                step(ids)
         torch.cuda.synchronize()
         s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         t0 = time.perf_counter()
         s.record()
-        for ids in order[warmup:]:
-            loss = stepper.step(ids)
+        for ids in seq:
+            loss = step(ids)
         e.record()
         torch.cuda.synchronize()
-        wall = (time.perf_counter() - t0) / steps
-        return s.elapsed_time(e) / steps, wall, float(loss)
+        wall = (time.perf_counter() - t0) / n_steps
+        return {"ms_per_batch": round(s.elapsed_time(e) / n_steps, 4), "host_ms_per_batch": round(wall * 1e3, 4),
+                "final_loss": float(loss), "batches": n_steps}
 
-    torch.manual_seed(1997)
-    probe_model = HetroGIN(**base.model_kwargs({"link": base.f_link, "path": base.f_path, "node": base.f_node}))
-    res = {"general": run("general")}
-    fused_error = None
-    if SmallBatchStep.supports(probe_model):
+    exec_desc = {"fused": "the fused small-batch step (3 L + 1 kernels, Adam folded into the last) as one hipGraph "
+                          "replay",
+                 "captured": "per-op HIP kernels as one hipGraph replay (hgin/graphs.py CapturedTrainStep)",
+                 "eager": "eager per-op HIP kernels on exact batches (store.collate + train_step)"}
+    fused_ok = SmallBatchStep.supports(build())
+    res, fused_error = {"general": run("captured", build(), steps)}, None
+    if fused_ok:
         try:
-            res["fused"] = run("fused")
+            res["fused"] = run("fused", build(), steps)
         except Exception as exc:   # reported in the line, not fatal to the headline
             fused_error = f"{type(exc).__name__}: {exc}"[:300]
-    # the main figure is the faster of the two executions; the other is reported beside it
-    kinds = sorted(res, key=lambda k: res[k][0])
-    ms, wall, loss = res[kinds[0]]
+    main_kind = "fused" if "fused" in res else "general"
+    m = res[main_kind]
     out = {"workload": f"{n_graphs} cfg1-schema graphs (7/7/3 raw features, normalised; sizes 0.5x-1.5x of "
                        f"{base.nodes} nodes / {base.graph_edges} edges) resident, shuffled batches of {batch}, "
-                       f"hidden {base.hidden}, {base.layers} layers, fp32",
-           "execution": ("device collation (one batched-copy launch) + one hipGraph replay per batch of the fused "
-                         "small-batch step (3 L + 1 kernels + fused Adam)" if kinds[0] == "fused" else
-                         "device collation (one batched-copy launch) + one hipGraph replay per batch"),
-           "batches": steps, "ms_per_batch": round(ms, 4), "host_ms_per_batch": round(wall * 1e3, 4),
-           "graphs_per_s": round(batch / (ms / 1e3), 1),
-           "edges_per_s": round(float(np.mean(conv_edges)) / (ms / 1e3), 1),
-           "mean_conv_edges_per_batch": float(np.mean(conv_edges)), "final_loss": loss,
-           "optimizer": "torch.optim.Adam(lr=1e-3, capturable=True" + (", fused=True)" if kinds[0] == "fused" else ")")}
-    if len(kinds) > 1:
-        o_ms, o_wall, o_loss = res[kinds[1]]
-        out["general_path" if kinds[1] == "general" else "fused_path"] = {
-            "ms_per_batch": round(o_ms, 4), "host_ms_per_batch": round(o_wall * 1e3, 4), "final_loss": o_loss,
-            "execution": ("per-op HIP kernels as one hipGraph replay (hgin/graphs.py)" if kinds[1] == "general" else
-                          "the fused small-batch step (3 L + 1 kernels + fused Adam) as one hipGraph replay")}
+                       f"hidden {base.hidden}, {base.layers} layers, fp32 (config.json's model)",
+           "execution": "device collation (one batched-copy launch) + " + exec_desc[
+               "fused" if main_kind == "fused" else "captured"],
+           "batches": steps, "ms_per_batch": m["ms_per_batch"], "host_ms_per_batch": m["host_ms_per_batch"],
+           "graphs_per_s": round(batch / (m["ms_per_batch"] / 1e3), 1),
+           "edges_per_s": round(float(np.mean(conv_edges)) / (m["ms_per_batch"] / 1e3), 1),
+           "mean_conv_edges_per_batch": float(np.mean(conv_edges)), "final_loss": m["final_loss"],
+           "optimizer": ("torch.optim.Adam(lr=1e-3) folded into the fused step's final kernel" if main_kind == "fused"
+                         else "torch.optim.Adam(lr=1e-3, capturable=True) (foreach)")}
+    if main_kind == "fused":
+        g = res["general"]
+        out["general_path"] = dict(g, execution=exec_desc["captured"],
+                                   optimizer="torch.optim.Adam(lr=1e-3, capturable=True) (foreach)")
+    # the reference's other switches, each through the path that takes it (SmallBatchStep.supports says which)
+    switches = {"mlp_bn": ({"mlp_bn": True}, False, "eager"), "global_feats": ({"global_feats": True}, False, "eager"),
+                "dropout_0.1": ({"dropout": 0.1}, False, "eager"),
+                "hidden_128": ({"node_embedding_size": 128}, False, "captured"),
+                "gat_heads16_h8_L1": ({}, True, "captured")}
+    cfgs = {}
+    for name, (ov, gat, kind) in switches.items():
+        try:
+            model = build(ov, gat)
+            if not gat and SmallBatchStep.supports(model):
+                kind = "fused"
+            r = run(kind, model, cfg_steps)
+            r["execution"] = exec_desc[kind]
+            r["fused_step"] = "takes it" if kind == "fused" else "refuses it (SmallBatchStep.supports)"
+            cfgs[name] = r
+        except Exception as exc:   # reported, not fatal
+            cfgs[name] = {"error": f"{type(exc).__name__}: {exc}"[:300]}
+        torch.cuda.empty_cache()
+    out["configs"] = cfgs
+    # the evaluation loops (train.py:70-113 test() after model.eval(), :322-348 evaluate()): config.json's
+    # VAL_BATCH_SIZE 1, and the training batch size, as captured replays (hgin/graphs.py CapturedEvalStep: device
+    # accumulators, one host sync per pass) beside the reference's eager form (forward + loss.item() per batch)
+    from hgin.graphs import CapturedEvalStep
+    from hgin.train import mape as mape_fn
+    ev = {}
+    model = build()
+    model.eval()
+    for bs in (1, batch):
+        seq = [order[warmup + i][:bs] for i in range(cfg_steps)]
+        try:
+            st = CapturedEvalStep(model, store, bs, warmup_ids=order[:warmup], warmup=2)
+            torch.cuda.synchronize()
+            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            t0 = time.perf_counter()
+            s.record()
+            for ids in seq:
+                st.step(ids)
+            e.record()
+            avg, _ = st.result(1)
+            wall_c = (time.perf_counter() - t0) / cfg_steps
+            t0 = time.perf_counter()
+            with torch.no_grad():
+                for ids in seq:
+                    b = store.collate(ids)
+                    float(mape_fn(model(b.x_dict(), b.edge_index_dict(), b.batch["path"]), b.y.reshape(-1, 1)))
+            wall_e = (time.perf_counter() - t0) / cfg_steps
+            ev[f"batch_{bs}"] = {"captured_ms_per_batch": round(s.elapsed_time(e) / cfg_steps, 4),
+                                 "captured_host_ms_per_batch": round(wall_c * 1e3, 4),
+                                 "eager_host_ms_per_batch": round(wall_e * 1e3, 4), "avg_loss": avg,
+                                 "batches": cfg_steps}
+            del st
+        except Exception as exc:   # reported, not fatal
+            ev[f"batch_{bs}"] = {"error": f"{type(exc).__name__}: {exc}"[:300]}
+    out["eval"] = dict(ev, execution="captured: one batched-copy launch + one hipGraph replay (forward + fused head / "
+                                     "MAPE + device accumulation) per batch; eager: collation + forward + "
+                                     "loss.item() per batch, as train.py's test() / evaluate()")
     if fused_error:
         out["fused_path_error"] = fused_error
     return out
+
+
+def gat_extra(dev, n_src: int = 6_000_000, n_dst: int = 3_000_000, E: int = 30_000_000, heads: int = 16, C: int = 8,
+              reps: int = 5) -> dict:
+    """HetroGAT's attention (models.py:413-418, PyG 2.0.2 GATConv; config.json HEADS 16 x hidden 8 = 128 columns) on
+    one cfg3-sized relation (cfg3's p -> l shape: 6M sources, 3M destinations, 30M uniform edges + GATConv's self
+    loops), after the headline: the forward attention kernel (hgin_gat_fwd_f32, k_gat_fwd_w) against HBM with its
+    algorithmic bytes E'(4 + 4 H C + 8 H) + N_dst (8 + 4 H + 4 H C) (col, the gathered x_s row, a_s, the alpha store;
+    rowptr, a_d, the output row), and the whole relation's attention forward + backward (logits, softmax-aggregate,
+    destination- and source-side backward, att / bias column sums).  HIP events, median of `reps`."""
+    from hgin import _lib
+    from hgin.gat import _GatAttentionFn, _logits, gat_graph
+    from hgin.ops import _p, _stream
+    g = torch.Generator(device=dev).manual_seed(7)
+    HC = heads * C
+    ei = torch.stack([torch.randint(0, n_src, (E,), device=dev, generator=g),
+                      torch.randint(0, n_dst, (E,), device=dev, generator=g)])
+    xs = torch.randn(n_src, HC, device=dev, generator=g)
+    xd = torch.randn(n_dst, HC, device=dev, generator=g)
+    att_s = (0.3 * torch.randn(1, heads, C, device=dev, generator=g)).requires_grad_()
+    att_d = (0.3 * torch.randn(1, heads, C, device=dev, generator=g)).requires_grad_()
+    bias = torch.zeros(HC, device=dev, requires_grad=True)
+    graph = gat_graph(ei, n_src, n_dst, True)
+    Ep = graph.n_edges
+    a_s = _logits(xs, att_s.detach().reshape(-1).contiguous(), heads, C)
+    a_d = _logits(xd, att_d.detach().reshape(-1).contiguous(), heads, C)
+    alpha = torch.empty(Ep, heads, device=dev)
+    out = torch.empty(n_dst, HC, device=dev)
+    kern = []
+
+    def fwd():
+        _lib.call("hgin_gat_fwd_f32", _p(graph.csr.rowptr), _p(graph.csr.col), n_dst, heads, C, _p(xs), xs.stride(0),
+                  _p(a_s), _p(a_d), ctypes.c_float(0.2), None, None, 0, _p(alpha), _p(out), out.stride(0),
+                  _stream(xs))
+
+    def timed(fn):
+        fn()
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(reps + 1)]
+        torch.cuda.synchronize()
+        ev[0].record()
+        for i in range(reps):
+            fn()
+            ev[i + 1].record()
+        torch.cuda.synchronize()
+        return statistics.median(ev[i].elapsed_time(ev[i + 1]) for i in range(reps))
+
+    with _lib.trace_launches() as tr:
+        fwd()
+        torch.cuda.synchronize()
+    kern = sorted(set(tr.kernels))
+    f_ms = timed(fwd)
+    algo = Ep * (4 + 4 * HC + 8 * heads) + n_dst * (8 + 4 * heads + 4 * HC)
+    xs_g, xd_g = xs.requires_grad_(), xd.requires_grad_()
+    g_out = torch.randn(n_dst, HC, device=dev, generator=g)
+
+    def fwd_bwd():
+        o = _GatAttentionFn.apply(xs_g, xd_g, att_s, att_d, bias, None, graph, heads, C, 0.2)
+        o.backward(g_out)
+    fb_ms = timed(fwd_bwd)
+    achieved = algo / (f_ms / 1e3) / 1e9
+    res = {"workload": f"one relation: {n_src} sources -> {n_dst} destinations, {E} uniform edges + self loops = {Ep} "
+                       f"(GATConv's bipartite self-loop handling), heads {heads} x {C} = {HC} fp32 columns",
+           "kernel": ",".join(kern), "fwd_attention_ms": round(f_ms, 4),
+           "fwd_roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                            "frac": round(achieved / HBM_PEAK_GBS, 4), "bytes_per_launch": algo},
+           "fwd_bwd_attention_ms": round(fb_ms, 4),
+           "edges_per_s_fwd_bwd": round(Ep / (fb_ms / 1e3), 1),
+           "timing": "HIP events, median of %d launches after one untimed" % reps}
+    del ei, xs, xd, graph, alpha, out, g_out, xs_g, xd_g
+    torch.cuda.empty_cache()
+    return res
 
 
 def extras(graph, dev) -> dict:
@@ -694,6 +840,7 @@ def main():
             torch.cuda.synchronize()
             torch.cuda.empty_cache()
             out["extras"]["cfg5"] = cfg5_extra(dev, args.adam)
+            out["extras"]["gat"] = gat_extra(dev)
         if ref1 is not None:
             # strong scaling against the same graph on one GPU: t_1gpu / t_step (ideal: N)
             out["one_gpu_reference"] = ref1

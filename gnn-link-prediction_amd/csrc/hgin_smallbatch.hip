@@ -25,7 +25,8 @@
 //                             written into one flat gradient buffer whose views are the parameters' .grad;
 //                             loss_value = 100 sum|u| / m.
 //
-// The optimizer (torch Adam, fused) follows in the same hipGraph.  Every sum runs in a fixed order (deterministic;
+// The optimizer: Adam folded into k_sb_final (each gradient entry updates its parameter and moments where it is
+// formed: no gradient round trip, no optimizer launches), or torch's optimizer after the step in the same hipGraph.  Every sum runs in a fixed order (deterministic;
 // the row chunks of the partials are fixed fractions of the batch's rows).  The aggregates are the GIN path's
 // (sequential edge-order fp32 sums: bit-identical); the GEMM-shaped sums and the deferred loss scaling re-associate,
 // so the step agrees with the general path within fp32 tolerances (tests/test_gpu_smallbatch.py).  Limits (checked
@@ -112,6 +113,12 @@ struct SbArgs {
   // outputs
   float* gflat;             // [p_gin + p_ro]
   float* loss_value;        // [1]
+  // the optimizer, folded into k_sb_final (adam_step NULL: the host runs torch's optimizer after the step)
+  float* pflat;             // [p_gin + p_ro] the parameters (their tensors are views of it), gflat's layout
+  float* mflat;             // Adam first moments, same layout
+  float* vflat;             // Adam second moments
+  float* adam_step;         // [1] Adam's step count (advanced by the step's first launch)
+  float lr, beta1, beta2, adam_eps, weight_decay;
 };
 
 __device__ __forceinline__ int kdim(const SbArgs& a, int l, int r) {
@@ -149,6 +156,7 @@ __global__ __launch_bounds__(kSbThreads) void k_sb_fwd(SbArgs a, int l) {
   const int H = a.H;
   const int n = nrows(a, t);
   const int r0 = blockIdx.x * kSbFwdRows;
+  if (a.adam_step && l == 0 && blockIdx.x == 0 && t == 0 && tid == 0) a.adam_step[0] += 1.0f;   // read by k_sb_final
   if (r0 >= n) return;
   const int nr = n - r0 < kSbFwdRows ? n - r0 : kSbFwdRows;
   int slot = 0;
@@ -527,9 +535,32 @@ __global__ __launch_bounds__(kSbThreads) void k_sb_bwd_in(SbArgs a, int l, float
 // every gradient entry = its n_parts partials in a fixed order (thread (j, g) of a 32-entry group sums parts g, g + 8,
 // ...; then the 8 group sums in order), times the sqrt-MAPE scale; the loss and the shared readout slope from the
 // per-tile partials (thread t sums tiles t, t + 256, ..., then a tree); every block recomputes the scale
+// Adam (torch.optim.Adam's rule, amsgrad / maximize off; L2 weight decay folded into the gradient) on entry e, in
+// fp32: m = b1 m + (1 - b1) g, v = b2 v + (1 - b2) g^2, p -= (lr / (1 - b1^t)) m / (sqrt(v) / sqrt(1 - b2^t) + eps)
+struct AdamCoef {
+  float step_size, bc2_sqrt;
+};
+__device__ __forceinline__ void adam_update(const SbArgs& a, int64_t e, float gv, const AdamCoef& c) {
+  float p = a.pflat[e];
+  const float gd = a.weight_decay != 0.0f ? __fadd_rn(gv, __fmul_rn(a.weight_decay, p)) : gv;
+  const float m = __fadd_rn(__fmul_rn(a.beta1, a.mflat[e]), __fmul_rn(__fsub_rn(1.0f, a.beta1), gd));
+  const float v = __fadd_rn(__fmul_rn(a.beta2, a.vflat[e]), __fmul_rn(__fmul_rn(__fsub_rn(1.0f, a.beta2), gd), gd));
+  const float den = __fadd_rn(__fdiv_rn(sqrtf(v), c.bc2_sqrt), a.adam_eps);
+  p = __fsub_rn(p, __fmul_rn(c.step_size, __fdiv_rn(m, den)));
+  a.mflat[e] = m;
+  a.vflat[e] = v;
+  a.pflat[e] = p;
+}
+
 __global__ __launch_bounds__(kSbThreads) void k_sb_final(SbArgs a) {
   __shared__ float red[kSbThreads];
   const int tid = threadIdx.x;
+  AdamCoef ad{0.0f, 1.0f};
+  if (a.adam_step) {
+    const float st = a.adam_step[0];
+    ad.step_size = __fdiv_rn(a.lr, __fsub_rn(1.0f, powf(a.beta1, st)));
+    ad.bc2_sqrt = sqrtf(__fsub_rn(1.0f, powf(a.beta2, st)));
+  }
   const int m = a.m_valid[0];
   const int ntile = (m + kSbRows - 1) / kSbRows;
   float lp = 0.0f, sp = 0.0f;
@@ -557,7 +588,9 @@ __global__ __launch_bounds__(kSbThreads) void k_sb_final(SbArgs a) {
     if (g == 0 && e < P) {
       float t = 0.0f;
       for (int q = 0; q < 8; ++q) t = __fadd_rn(t, red[q * 32 + j]);
-      a.gflat[e] = __fmul_rn(e == a.ro_slope_goff ? slope_sum : t, scale);
+      const float gv = __fmul_rn(e == a.ro_slope_goff ? slope_sum : t, scale);
+      a.gflat[e] = gv;
+      if (a.adam_step) adam_update(a, e, gv, ad);
     }
     __syncthreads();
   }
@@ -598,14 +631,24 @@ extern "C" int hgin_sb_step(const void* args, size_t args_bytes, size_t readout_
                  "hgin_sb_step: unsupported shape");
   hipStream_t s = as_stream(stream);
   HGIN_TRACE("k_sb_step");
-  // the readout kernel's dynamic LDS may use what its static reduction array leaves of the CU's 160 KiB
-  static const int dyn_max = [] {
+  // the readout kernel's dynamic LDS may use what its static reduction array leaves of the CU's 160 KiB; the limit
+  // is a per-device attribute, so it is raised once per device this process launches on (idempotent if two threads
+  // race on it)
+  int dev = 0;
+  HGIN_ARG_CHECK(hipGetDevice(&dev) == hipSuccess && dev >= 0 && dev < 64, "hgin_sb_step: device id");
+  static int dyn_max_dev[64];   // 0: not raised yet on that device; -1: failed
+  if (dyn_max_dev[dev] == 0) {
     hipFuncAttributes fa;
-    if (hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(k_sb_readout)) != hipSuccess) return -1;
-    const int m = 160 * 1024 - (int)fa.sharedSizeBytes;
-    return hipFuncSetAttribute(reinterpret_cast<const void*>(k_sb_readout),
-                               hipFuncAttributeMaxDynamicSharedMemorySize, m) == hipSuccess ? m : -1;
-  }();
+    int m = -1;
+    if (hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(k_sb_readout)) == hipSuccess) {
+      m = 160 * 1024 - (int)fa.sharedSizeBytes;
+      if (hipFuncSetAttribute(reinterpret_cast<const void*>(k_sb_readout), hipFuncAttributeMaxDynamicSharedMemorySize,
+                              m) != hipSuccess)
+        m = -1;
+    }
+    dyn_max_dev[dev] = m;
+  }
+  const int dyn_max = dyn_max_dev[dev];
   if (dyn_max < 0) {
     set_error("hgin_sb_step: could not raise the readout kernel's dynamic LDS limit");
     return (int)hipErrorInvalidValue;
@@ -658,7 +701,8 @@ extern "C" int hgin_sb_args_offsets(int64_t* out, int64_t n) {
                           (int64_t)offsetof(SbArgs, ro_goff),  (int64_t)offsetof(SbArgs, p_ro),
                           (int64_t)offsetof(SbArgs, act_off),  (int64_t)offsetof(SbArgs, zb_off),
                           (int64_t)offsetof(SbArgs, gc_off),   (int64_t)offsetof(SbArgs, n_tiles),
-                          (int64_t)offsetof(SbArgs, loss_value)};
+                          (int64_t)offsetof(SbArgs, loss_value), (int64_t)offsetof(SbArgs, adam_step),
+                          (int64_t)offsetof(SbArgs, weight_decay)};
   const int64_t k = (int64_t)(sizeof(offs) / sizeof(offs[0]));
   HGIN_ARG_CHECK(out && n >= k, "hgin_sb_args_offsets: need %lld slots", (long long)k);
   for (int64_t i = 0; i < k; ++i) out[i] = offs[i];

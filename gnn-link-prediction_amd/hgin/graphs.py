@@ -1,4 +1,4 @@
-"""hipGraph-captured training step for shuffled mini-batches of small graphs.
+"""hipGraph-captured training and evaluation steps for shuffled mini-batches of small graphs.
 
 The reference's real workload is batches of 8 small network graphs (dataset.py:239-244, train.py:25-44):
 a few thousand vertices per step, so every kernel is tiny and the step is bound by the host issuing ~300
@@ -135,3 +135,67 @@ class CapturedStaticStep:
         loss_value = self.reducer.sync_sqrt_mean(*self.loss)
         self.opt_graph.replay()
         return loss_value
+
+
+class CapturedEvalStep:
+    """train.py's evaluation loops — ``test()`` (train.py:70-113, after ``model.eval()``, :192) and ``evaluate()``
+    (:322-348) — as one batched-copy launch + one hipGraph replay per batch: the forward and the fused head + MAPE
+    (F3, limited to the batch's paths by the padded batch's device count) under ``torch.no_grad()``, on the same
+    static-capacity buffers as ``CapturedTrainStep``.  The replay also adds the batch's loss_value and its path-
+    weighted form into device accumulators (the reference's ``running_loss += loss_value.item()`` and
+    ``running_loss_mape += mape * n_paths``), so a whole evaluation pass syncs the host once, in ``result()``.
+
+    The model must be in eval mode (BatchNorm then reads its running statistics and dropout is off: both
+    row-independent, so the padded batch equals the exact one); GLOBAL_FEATS pools over padding rows and is refused
+    (the eager forward takes it)."""
+
+    def __init__(self, model: torch.nn.Module, store: GraphStore, batch_size: int,
+                 warmup_ids: Sequence[Sequence[int]], warmup: int = 2):
+        if model.training:
+            raise ValueError("CapturedEvalStep: call model.eval() first (train.py:192, :329)")
+        if getattr(model, "global_feats", False):
+            raise ValueError("CapturedEvalStep: global_feats pools over padding rows; use the eager forward")
+        if not warmup_ids:
+            raise ValueError("CapturedEvalStep needs at least one warm-up batch")
+        self.model, self.store = model, store
+        self.batch: PaddedBatch = store.padded_batch(batch_size)
+        dev = self.batch.y.device
+        self.loss_sum = torch.zeros((), dtype=torch.float32, device=dev)
+        self.loss_paths = torch.zeros((), dtype=torch.float32, device=dev)
+        self.batches = 0
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side), torch.no_grad():
+            for i in range(max(1, warmup)):
+                store.collate_into(warmup_ids[i % len(warmup_ids)], self.batch)
+                self._forward()
+        torch.cuda.current_stream().wait_stream(side)
+        torch.cuda.synchronize()
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph), torch.no_grad():
+            self.out, self.loss = self._forward()
+            self.loss_sum.add_(self.loss)
+            self.loss_paths.add_(self.loss * self.batch.m_valid[0].to(torch.float32))
+
+    def _forward(self):
+        b = self.batch
+        return self.model.forward_loss(b.x_dict(), b.edge_index_dict(), b.batch["path"], b.y, b.m_valid)
+
+    def step(self, ids: Sequence[int]) -> torch.Tensor:
+        """Evaluate the graphs ``ids``; returns the batch's device loss_value (overwritten by the next step).  The
+        predictions are ``self.out[:n_paths]`` until then."""
+        self.store.collate_into(ids, self.batch)
+        self.graph.replay()
+        self.batches += 1
+        return self.loss
+
+    def reset(self) -> None:
+        self.loss_sum.zero_()
+        self.loss_paths.zero_()
+        self.batches = 0
+
+    def result(self, n_paths: int) -> tuple:
+        """(average loss over the batches, path-weighted MAPE) = test()'s (average_loss, mape_loss) for a loss_func
+        of MAPE; ``n_paths`` = the paths evaluated (the host knows the graphs).  One host sync."""
+        s, w = float(self.loss_sum), float(self.loss_paths)
+        return s / max(self.batches, 1), w / max(n_paths, 1)

@@ -12,6 +12,7 @@ loop and readout, with the GATConv layers of ``hgin/gat.py``.
 """
 from __future__ import annotations
 
+import weakref
 from typing import List
 
 import torch
@@ -54,6 +55,9 @@ def _host_call_device(model: torch.nn.Module, x_dict, edge_index_dict, path_batc
     return torch.device("cuda", torch.cuda.current_device())
 
 
+_LENT: "weakref.WeakKeyDictionary" = weakref.WeakKeyDictionary()   # model -> {id(t): (key, device copy, ref(t))}
+
+
 def _host_call(model: torch.nn.Module, dev, x_dict, edge_index_dict, path_batch):
     """Run ``model`` on ``dev`` for a host-resident inference call (``evaluate``, train.py:331-335 runs it under
     ``torch.set_grad_enabled(False)``): parameters and buffers are lent to the device for the call and restored
@@ -71,14 +75,24 @@ def _host_call(model: torch.nn.Module, dev, x_dict, edge_index_dict, path_batch)
         if id(t) not in seen:
             seen.add(id(t))
             lent.append((t, t.data))
+    # device copies are kept per model between calls (evaluate() runs one call per batch with unchanged weights) and
+    # re-copied when a tensor's version, storage or shape changed (load_state_dict, in-place edits)
+    cache = _LENT.setdefault(model, {})
     try:
         for t, d in lent:
-            t.data = d.to(dev)
+            key = (t._version, d.data_ptr(), tuple(d.shape), d.dtype, str(dev))
+            hit = cache.get(id(t))
+            if hit is None or hit[0] != key or hit[2]() is not t:
+                hit = (key, d.to(dev), weakref.ref(t))
+                cache[id(t)] = hit
+            t.data = hit[1]
         xd = {k: v.to(dev) for k, v in x_dict.items()}
         ed = {k: v.to(dev) for k, v in edge_index_dict.items()}
         pb = path_batch.to(dev) if path_batch is not None else None
         out = model._run(xd, ed, pb, None, None)
-        res = out.to(host)
+        res = out.to(host)   # (this call syncs the host anyway: an unsorted GLOBAL_FEATS batch vector raises here)
+        if getattr(model, "global_feats", False):
+            ops.check_pool_order()
     finally:
         for t, d in lent:
             t.data = d
@@ -86,6 +100,12 @@ def _host_call(model: torch.nn.Module, dev, x_dict, edge_index_dict, path_batch)
 
 
 class HetroGIN(torch.nn.Module):
+    """models.py:248-376 on the MI355X path (module docstring).  With ``global_feats`` the path batch vector must be
+    non-decreasing, as PyG's collation makes it (and GraphStore's batches are by construction): the pooling kernel
+    flags a descending pair in a device status word instead of syncing the host every step — the host-resident
+    ``evaluate()`` call checks it (and raises), a training step leaves it to ``ops.check_pool_order()``; an unsorted
+    vector otherwise yields unspecified pooled features."""
+
     def __init__(self, input_channels: dict, node_embedding_size: int, message_passing_layers: int, dropout: float,
                  concat_path: bool, bl_features: bool, divided_features: bool, global_feats: bool,
                  mlp_layers: list, act, mlp_head_act, mlp_bn: bool):

@@ -2,8 +2,8 @@
 train.py:25-44): ``SmallBatchStep`` runs a HetroGIN train step over a padded batch of small graphs with the fused
 kernels of ``csrc/hgin_smallbatch.hip`` (per layer one aggregate + MLP launch over every relation and row of the
 batch, the readout + MAPE + readout backward in tiles of 8 rows, per layer one or two backward launches, one
-fixed-order gradient reduction that applies the sqrt-MAPE scale: 3 L + 1 launches), followed by torch's fused Adam,
-captured once into a hipGraph and replayed per batch after one device collation launch.
+fixed-order gradient reduction that applies the sqrt-MAPE scale and, for Adam, the parameter update: 3 L + 1
+launches), captured once into a hipGraph and replayed per batch after one device collation launch.
 
 It takes the model train.py builds from config.json (``HetroGIN`` with GINLayer convs, Linear + shared PReLU
 readout, Linear head, no BatchNorm / global features / dropout) at small widths: hidden <= 64, first-layer GEMM
@@ -56,11 +56,24 @@ class _SbArgs(ctypes.Structure):   # field for field csrc/hgin_smallbatch.hip Sb
                 ("cap", _I32 * 3), ("part_gin", _P), ("n_parts", _I32), ("part_ro", _P), ("loss_part", _P),
                 ("slope_part", _P), ("n_tiles", _I32), ("ro_wlds", _I32),
                 ("ro_in", _P * (MAX_HID + 1)), ("ro_gz", _P * (MAX_HID + 1)),
-                ("gflat", _P), ("loss_value", _P)]
+                ("gflat", _P), ("loss_value", _P),
+                ("pflat", _P), ("mflat", _P), ("vflat", _P), ("adam_step", _P),
+                ("lr", ctypes.c_float), ("beta1", ctypes.c_float), ("beta2", ctypes.c_float),
+                ("adam_eps", ctypes.c_float), ("weight_decay", ctypes.c_float)]
 
 
 _OFFSET_FIELDS = ("goff", "m_valid", "conv", "rw", "ro_goff", "p_ro", "act_off", "zb_off", "gc_off", "n_tiles",
-                  "loss_value")
+                  "loss_value", "adam_step", "weight_decay")
+
+
+def foldable(opt: torch.optim.Optimizer) -> bool:
+    """Adam with one parameter group, float hyperparameters, amsgrad / maximize off: its update can run inside the
+    fused step's final kernel (csrc/hgin_smallbatch.hip adam_update)."""
+    if type(opt) is not torch.optim.Adam or len(opt.param_groups) != 1:
+        return False
+    g = opt.param_groups[0]
+    return (not g.get("amsgrad", False) and not g.get("maximize", False) and not g.get("differentiable", False)
+            and not isinstance(g["lr"], torch.Tensor) and all(not isinstance(b, torch.Tensor) for b in g["betas"]))
 
 
 def check_layout() -> None:
@@ -144,12 +157,13 @@ class SmallBatchStep:
         return not isinstance(_structure(model), str)
 
     def __init__(self, model: HetroGIN, opt: torch.optim.Optimizer, store: GraphStore, batch_size: int,
-                 warmup_ids: Sequence[Sequence[int]], warmup: int = 2):
+                 warmup_ids: Sequence[Sequence[int]], warmup: int = 2, fold_optimizer: bool = True):
         st = _structure(model)
         if isinstance(st, str):
             raise ValueError(f"SmallBatchStep: model not supported ({st}); use hgin.graphs.CapturedTrainStep")
-        if not all(g.get("capturable", False) for g in opt.param_groups):
-            raise ValueError("SmallBatchStep needs a capturable optimizer (e.g. Adam(..., capturable=True))")
+        self.folded = bool(fold_optimizer) and foldable(opt)
+        if not self.folded and not all(g.get("capturable", False) for g in opt.param_groups):
+            raise ValueError("SmallBatchStep needs Adam (folded into the step) or a capturable optimizer")
         if not warmup_ids:
             raise ValueError("SmallBatchStep needs at least one warm-up batch")
         convs, hidden, slope, head, H = st
@@ -276,6 +290,8 @@ class SmallBatchStep:
         for p in params:
             o = param_off[p]
             p.grad = self.gflat[o:o + p.numel()].view_as(p)
+        if self.folded:
+            self._fold_adam(a, params, param_off, off, convs, hidden, slope, head, L, keep)
         widths = (ctypes.c_int32 * MAX_HID)(*[a.rw[i] for i in range(MAX_HID)])
         lds = ctypes.c_size_t(0)
         # the readout tile stages its hidden weights in LDS when they fit beside its 1 KiB static array
@@ -302,20 +318,67 @@ class SmallBatchStep:
             a.ro_in[i], a.ro_gz[i] = P(self.ro_in[i]), P(self.ro_gz[i])
         check_layout()
         self.args, self._keep, self.lds = a, keep, lds.value
-        # warm-up on a side stream (optimizer state, allocator pools), then capture kernels + Adam once
+        # warm-up on a side stream (optimizer state, allocator pools), then capture the step (+ torch's optimizer
+        # when it is not folded) once
         side = torch.cuda.Stream()
         side.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(side):
             for i in range(max(1, warmup)):
                 store.collate_into(warmup_ids[i % len(warmup_ids)], pb)
                 self._launch()
-                opt.step()
+                if not self.folded:
+                    opt.step()
         torch.cuda.current_stream().wait_stream(side)
         torch.cuda.synchronize()
         self.graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self.graph):
             self._launch()
-            opt.step()
+            if not self.folded:
+                opt.step()
+
+    def _fold_adam(self, a, params, param_off, total, convs, hidden, slope, head, L, keep) -> None:
+        """The parameters become views of one flat buffer in the gradient layout, Adam's moments two more and its
+        step count one device scalar; the optimizer's state entries are re-pointed at them (its existing state, if
+        any, copied in), so opt.state_dict() stays meaningful.  The step then owns the optimizer: calling
+        opt.step() as well would update twice."""
+        g = self.opt.param_groups[0]
+        f32 = dict(dtype=torch.float32, device=self.gflat.device)
+        self.pflat = torch.empty(total, **f32)
+        self.mflat = torch.zeros(total, **f32)
+        self.vflat = torch.zeros(total, **f32)
+        self.adam_step = torch.zeros((), **f32)
+        steps = set()
+        with torch.no_grad():
+            for p in params:
+                o, n = param_off[p], p.numel()
+                self.pflat[o:o + n].copy_(p.detach().reshape(-1))
+                state = self.opt.state.get(p)
+                if state:
+                    self.mflat[o:o + n].copy_(state["exp_avg"].reshape(-1))
+                    self.vflat[o:o + n].copy_(state["exp_avg_sq"].reshape(-1))
+                    steps.add(float(state["step"]))
+        if len(steps) > 1:
+            raise ValueError("SmallBatchStep: the optimizer's parameters are at different step counts")
+        self.adam_step.fill_(steps.pop() if steps else 0.0)
+        for p in params:
+            o, n = param_off[p], p.numel()
+            p.data = self.pflat[o:o + n].view_as(p)
+            self.opt.state[p] = {"step": self.adam_step, "exp_avg": self.mflat[o:o + n].view_as(p),
+                                 "exp_avg_sq": self.vflat[o:o + n].view_as(p)}
+        # the kernels' parameter pointers: the views' (the struct was filled from the old storage)
+        for l in range(L):
+            for ri in range(REL):
+                lin, pw, eps = convs[l][ri]
+                c = a.conv[l][ri]
+                c.w, c.b, c.slope, c.eps = lin.weight.data_ptr(), lin.bias.data_ptr(), pw.data_ptr(), eps.data_ptr()
+        for i, lin in enumerate(hidden):
+            a.row_w[i], a.row_b[i] = lin.weight.data_ptr(), lin.bias.data_ptr()
+        a.ro_slope, a.head_w, a.head_b = slope.data_ptr(), head.weight.data_ptr(), head.bias.data_ptr()
+        keep += [self.pflat, self.mflat, self.vflat, self.adam_step]
+        a.pflat, a.mflat, a.vflat = self.pflat.data_ptr(), self.mflat.data_ptr(), self.vflat.data_ptr()
+        a.adam_step = self.adam_step.data_ptr()
+        a.lr, a.beta1, a.beta2 = float(g["lr"]), float(g["betas"][0]), float(g["betas"][1])
+        a.adam_eps, a.weight_decay = float(g["eps"]), float(g["weight_decay"])
 
     def _launch(self) -> None:
         _lib.call("hgin_sb_step", ctypes.addressof(self.args), ctypes.sizeof(self.args), self.lds,

@@ -308,6 +308,23 @@ def test_evaluate_host_resident_call(case):
     else:
         want = fx["out"]
     assert _close(out, want)
+    # the device copies of the weights persist between calls and follow every change of the host weights:
+    # load_state_dict (in place) and an in-place edit of one parameter
+    from hgin.models import _LENT
+    dev_copies = {k: v[1].data_ptr() for k, v in _LENT[model].items()}
+    with torch.set_grad_enabled(False):
+        model(dict(x), ei, batch)
+    assert {k: v[1].data_ptr() for k, v in _LENT[model].items()} == dev_copies   # no re-copy
+    sd2 = {k: (v * 1.01 if v.is_floating_point() else v) for k, v in sd.items()}
+    model.load_state_dict(sd2)
+    with torch.no_grad():
+        next(model.parameters()).mul_(0.5)
+        out3 = model(dict(x), ei, batch)
+        fresh = HetroGIN(**fixture_model_kwargs(fx))
+        fresh.load_state_dict(model.state_dict())
+        fresh.eval()
+        out4 = fresh(dict(x), ei, batch)
+    assert torch.equal(out3, out4) and not torch.equal(out3, out)
     model.train()
     with pytest.raises(RuntimeError, match="gradients enabled"):
         model(dict(x), ei, batch)

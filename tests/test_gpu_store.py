@@ -231,3 +231,45 @@ def test_store_build_normalize_equals_reference_fixture():
     for t in ("path", "link", "node"):
         n = st.x[t].shape[0]
         assert torch.equal(st.x[t].cpu(), fx[f"out.x.{t}"][:n]), t
+
+
+@pytest.mark.parametrize("mlp_bn", [False, True])
+def test_captured_eval_step_matches_eager(mlp_bn):
+    """train.py's test() loop (model.eval(), forward + MAPE per batch) as captured replays: every batch's loss and the
+    predictions of its paths equal an eager no-grad forward on the exact batch (BatchNorm in eval mode reads its
+    running statistics: row-independent), and the device accumulators give test()'s two averages."""
+    from hgin.graphs import CapturedEvalStep
+    from hgin.train import mape
+    graphs = _graphs(12, seed=9)
+    store = GraphStore.build(graphs, device=DEV)
+    cfg = CONFIGS["cfg1"]
+    torch.manual_seed(1997)
+    model = HetroGIN(**dict(cfg.model_kwargs({"link": 7, "path": 7, "node": 3}), mlp_bn=mlp_bn)).to(DEV)
+    if mlp_bn:   # non-trivial running statistics
+        for m in model.modules():
+            if isinstance(m, torch.nn.BatchNorm1d):
+                m.running_mean.uniform_(-0.5, 0.5)
+                m.running_var.uniform_(0.5, 2.0)
+    model.eval()
+    seq = [[4], [0, 7, 2], [11, 3, 9], [6, 1, 10], [8]]
+    ev = CapturedEvalStep(model, store, batch_size=3, warmup_ids=seq[:2], warmup=2)
+    losses, n_paths = [], 0
+    for ids in seq:
+        lv = float(ev.step(ids))
+        b = store.collate(ids)
+        n = int(b.y.numel())
+        got = ev.out[:n].detach().clone()
+        with torch.no_grad():
+            out = model(b.x_dict(), b.edge_index_dict(), b.batch["path"])
+            want = float(mape(out, b.y.reshape(-1, 1)))
+        assert abs(lv - want) <= 1e-6 * abs(want), (ids, lv, want)
+        assert torch.allclose(got.reshape(-1), out.reshape(-1), rtol=1e-6, atol=1e-6), ids
+        losses.append(want)
+        n_paths += n
+    avg, mape_w = ev.result(n_paths)
+    assert abs(avg - np.mean(losses)) <= 1e-5 * abs(np.mean(losses))
+    w = sum(l * int(store.collate(ids).y.numel()) for l, ids in zip(losses, seq)) / n_paths
+    assert abs(mape_w - w) <= 1e-5 * abs(w)
+    model.train()
+    with pytest.raises(ValueError, match="eval"):
+        CapturedEvalStep(model, store, batch_size=3, warmup_ids=seq[:1])

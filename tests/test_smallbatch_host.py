@@ -36,7 +36,16 @@ def test_refused_models_say_why(override, reason):
 
 
 def test_refuses_a_non_capturable_optimizer_before_touching_the_device():
+    """Adam is folded into the step (any capturable setting); another optimizer must be capturable, as must Adam
+    when folding is switched off."""
+    from hgin.smallbatch import foldable
     model = HetroGIN(**_kw())
-    opt = torch.optim.Adam(model.parameters(), lr=1e-3)   # capturable=False
+    assert foldable(torch.optim.Adam(model.parameters(), lr=1e-3))
+    assert not foldable(torch.optim.Adam(model.parameters(), lr=1e-3, amsgrad=True))
+    assert not foldable(torch.optim.AdamW(model.parameters(), lr=1e-3))
+    opt = torch.optim.SGD(model.parameters(), lr=1e-3)   # not capturable
     with pytest.raises(ValueError, match="capturable"):
         SmallBatchStep(model, opt, store=None, batch_size=8, warmup_ids=[[0]])
+    opt = torch.optim.Adam(model.parameters(), lr=1e-3)   # capturable=False, folding off
+    with pytest.raises(ValueError, match="capturable"):
+        SmallBatchStep(model, opt, store=None, batch_size=8, warmup_ids=[[0]], fold_optimizer=False)
