@@ -219,13 +219,24 @@ __global__ __launch_bounds__(256) void k_gat_fwd_w(const int32_t* __restrict__ r
   float m = -INFINITY, s = 0.0f;
   if (slot < ES) {
     const float adv = ad ? ad[i * H + h1] : 0.0f;
-    for (int k = rb + slot; k < re; k += ES) {
-      const float e = lrelu(__fadd_rn(as[(int64_t)col[k] * H + h1], adv), slope);
-      if (e > m) {
-        s = __fadd_rn(__fmul_rn(s, expf(__fsub_rn(m, e))), 1.0f);
-        m = e;
-      } else {
-        s = __fadd_rn(s, expf(__fsub_rn(e, m)));
+    for (int k0 = rb + slot; k0 < re; k0 += ES * kGatU) {   // kGatU of the slot's edges' logits loaded together
+      float av[kGatU];
+#pragma unroll
+      for (int u = 0; u < kGatU; ++u) {
+        const int k = k0 + u * ES;
+        av[u] = k < re ? as[(int64_t)col[k] * H + h1] : 0.0f;
+      }
+#pragma unroll
+      for (int u = 0; u < kGatU; ++u) {
+        if (k0 + u * ES < re) {
+          const float e = lrelu(__fadd_rn(av[u], adv), slope);
+          if (e > m) {
+            s = __fadd_rn(__fmul_rn(s, expf(__fsub_rn(m, e))), 1.0f);
+            m = e;
+          } else {
+            s = __fadd_rn(s, expf(__fsub_rn(e, m)));
+          }
+        }
       }
     }
   }
@@ -341,13 +352,29 @@ __global__ __launch_bounds__(256) void k_gat_bwd_dst_w(const int32_t* __restrict
   float gsum = 0.0f;
   if (first) {
     const float adv = ad ? ad[i * H + hq] : 0.0f;
-    for (int k = rb; k < re; ++k) {
-      const int64_t q = (int64_t)k * H + hq;
-      const float ge = __fmul_rn(alpha[q], __fsub_rn(g_pre[q], S));
-      const float pre = __fadd_rn(as[(int64_t)col[k] * H + hq], adv);
-      const float gp = pre > 0.0f ? ge : __fmul_rn(ge, slope);
-      g_pre[q] = gp;
-      gsum = __fadd_rn(gsum, gp);
+    for (int k0 = rb; k0 < re; k0 += kGatU) {   // kGatU edges' operands loaded together
+      float al[kGatU], ga[kGatU], av[kGatU];
+#pragma unroll
+      for (int u = 0; u < kGatU; ++u) {
+        const int k = k0 + u;
+        al[u] = ga[u] = av[u] = 0.0f;
+        if (k < re) {
+          const int64_t q = (int64_t)k * H + hq;
+          al[u] = alpha[q];
+          ga[u] = g_pre[q];
+          av[u] = as[(int64_t)col[k] * H + hq];
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < kGatU; ++u) {
+        if (k0 + u < re) {
+          const float ge = __fmul_rn(al[u], __fsub_rn(ga[u], S));
+          const float pre = __fadd_rn(av[u], adv);
+          const float gp = pre > 0.0f ? ge : __fmul_rn(ge, slope);
+          g_pre[(int64_t)(k0 + u) * H + hq] = gp;
+          gsum = __fadd_rn(gsum, gp);
+        }
+      }
     }
     if (g_ad) g_ad[i * H + hq] = gsum;
   }
