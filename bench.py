@@ -769,7 +769,11 @@ def main():
     extra = None
     if rank == 0 and not no_extras:
         extra = extras(graph, dev)
-        extra["batches"] = batches_extra(dev)
+        try:
+            extra["batches"] = batches_extra(dev)
+        except Exception as exc:   # reported in the line, not fatal to the headline
+            extra["batches"] = {"error": f"{type(exc).__name__}: {exc}"[:300]}
+            torch.cuda.empty_cache()
 
     out = None
     if rank == 0:
@@ -840,7 +844,11 @@ def main():
             torch.cuda.synchronize()
             torch.cuda.empty_cache()
             out["extras"]["cfg5"] = cfg5_extra(dev, args.adam)
-            out["extras"]["gat"] = gat_extra(dev)
+            try:   # a failing extra is reported in the line, never fatal to the headline
+                out["extras"]["gat"] = gat_extra(dev)
+            except Exception as exc:
+                out["extras"]["gat"] = {"error": f"{type(exc).__name__}: {exc}"[:300]}
+                torch.cuda.empty_cache()
         if ref1 is not None:
             # strong scaling against the same graph on one GPU: t_1gpu / t_step (ideal: N)
             out["one_gpu_reference"] = ref1
