@@ -346,7 +346,10 @@ def batches_extra(dev, n_graphs: int = 256, batch: int = 8, warmup: int = 5, ste
         out["general_path"] = dict(g, execution=exec_desc["captured"],
                                    optimizer="torch.optim.Adam(lr=1e-3, capturable=True) (foreach)")
     # the reference's other switches, each through the path that takes it (SmallBatchStep.supports says which)
-    switches = {"mlp_bn": ({"mlp_bn": True}, False, "eager"), "global_feats": ({"global_feats": True}, False, "eager"),
+    # (GLOBAL_FEATS needs BL_FEATURES: models.py:293 sizes the readout for [mean | max] of 4 path columns, which only
+    # the bl_features slicing keeps, models.py:333-342 — with 3 columns the reference's own Linear raises)
+    switches = {"mlp_bn": ({"mlp_bn": True}, False, "eager"),
+                "global_feats": ({"global_feats": True, "bl_features": True}, False, "eager"),
                 "dropout_0.1": ({"dropout": 0.1}, False, "eager"),
                 "hidden_128": ({"node_embedding_size": 128}, False, "captured"),
                 "gat_heads16_h8_L1": ({}, True, "captured")}
@@ -375,7 +378,7 @@ def batches_extra(dev, n_graphs: int = 256, batch: int = 8, warmup: int = 5, ste
     for bs in (1, batch):
         seq = [order[warmup + i][:bs] for i in range(cfg_steps)]
         try:
-            st = CapturedEvalStep(model, store, bs, warmup_ids=order[:warmup], warmup=2)
+            st = CapturedEvalStep(model, store, bs, warmup_ids=[ids[:bs] for ids in order[:warmup]], warmup=2)
             torch.cuda.synchronize()
             s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             t0 = time.perf_counter()
@@ -410,10 +413,11 @@ def gat_extra(dev, n_src: int = 6_000_000, n_dst: int = 3_000_000, E: int = 30_0
               reps: int = 5) -> dict:
     """HetroGAT's attention (models.py:413-418, PyG 2.0.2 GATConv; config.json HEADS 16 x hidden 8 = 128 columns) on
     one cfg3-sized relation (cfg3's p -> l shape: 6M sources, 3M destinations, 30M uniform edges + GATConv's self
-    loops), after the headline: the forward attention kernel (hgin_gat_fwd_f32, k_gat_fwd_w) against HBM with its
-    algorithmic bytes E'(4 + 4 H C + 8 H) + N_dst (8 + 4 H + 4 H C) (col, the gathered x_s row, a_s, the alpha store;
-    rowptr, a_d, the output row), and the whole relation's attention forward + backward (logits, softmax-aggregate,
-    destination- and source-side backward, att / bias column sums).  HIP events, median of `reps`."""
+    loops), after the headline: the forward attention kernel (hgin_gat_attn_fwd_f32, k_gat_attn_w: one pass, a_s formed
+    from the gathered x_s rows) against HBM with its algorithmic bytes E'(4 + 4 H C + 4 H) + N_dst (8 + 4 H + 4 H C)
+    (col, the gathered x_s row, the alpha store; rowptr, a_d, the output row), and the whole relation's attention
+    forward + backward (logits, softmax-aggregate, destination- and source-side backward, att / bias column sums).
+    HIP events, median of `reps`."""
     from hgin import _lib
     from hgin.gat import _GatAttentionFn, _logits, gat_graph
     from hgin.ops import _p, _stream
@@ -428,16 +432,17 @@ def gat_extra(dev, n_src: int = 6_000_000, n_dst: int = 3_000_000, E: int = 30_0
     bias = torch.zeros(HC, device=dev, requires_grad=True)
     graph = gat_graph(ei, n_src, n_dst, True)
     Ep = graph.n_edges
-    a_s = _logits(xs, att_s.detach().reshape(-1).contiguous(), heads, C)
     a_d = _logits(xd, att_d.detach().reshape(-1).contiguous(), heads, C)
     alpha = torch.empty(Ep, heads, device=dev)
     out = torch.empty(n_dst, HC, device=dev)
     kern = []
 
-    def fwd():
-        _lib.call("hgin_gat_fwd_f32", _p(graph.csr.rowptr), _p(graph.csr.col), n_dst, heads, C, _p(xs), xs.stride(0),
-                  _p(a_s), _p(a_d), ctypes.c_float(0.2), None, None, 0, _p(alpha), _p(out), out.stride(0),
-                  _stream(xs))
+    att_flat = att_s.detach().reshape(-1).contiguous()
+
+    def fwd():   # the forward attention as GATConv runs it (hgin/gat.py: the one-pass kernel, a_s from the x_s rows)
+        _lib.call("hgin_gat_attn_fwd_f32", _p(graph.csr.rowptr), _p(graph.csr.col), n_dst, heads, C, _p(xs),
+                  xs.stride(0), _p(att_flat), _p(a_d), ctypes.c_float(0.2), None, None, 0, _p(alpha), _p(out),
+                  out.stride(0), _stream(xs))
 
     def timed(fn):
         fn()
@@ -455,7 +460,7 @@ def gat_extra(dev, n_src: int = 6_000_000, n_dst: int = 3_000_000, E: int = 30_0
         torch.cuda.synchronize()
     kern = sorted(set(tr.kernels))
     f_ms = timed(fwd)
-    algo = Ep * (4 + 4 * HC + 8 * heads) + n_dst * (8 + 4 * heads + 4 * HC)
+    algo = Ep * (4 + 4 * HC + 4 * heads) + n_dst * (8 + 4 * heads + 4 * HC)
     xs_g, xd_g = xs.requires_grad_(), xd.requires_grad_()
     g_out = torch.randn(n_dst, HC, device=dev, generator=g)
 

@@ -138,8 +138,13 @@ __global__ __launch_bounds__(256) void k_gat_bwd_src(const int32_t* __restrict__
   }
 }
 
-// out[h * C + c] = sum_n w[n, h] x[n, h * C + c] (w NULL: weight 1), n in fixed 256-row blocks, then blocks in order.
+// out[h * C + c] = sum_n w[n, h] x[n, h * C + c] (w NULL: weight 1): per 256-row block a partial per column
+// (k_gat_wsum_part, a thread per column walking the block's rows in order), stored column-major [HC][nb]; then one
+// workgroup per column adds its nb partials — thread t the blocks t, t + 256, ... in order (coalesced), then a fixed
+// tree (k_gat_wsum_final).  Round 4's final pass had one thread per column walk all nb partials (5.4 ms per call at
+// 6M rows).
 constexpr int kWsumRows = 256;
+inline int64_t wsum_blocks(int64_t n) { return ceil_div(n > 0 ? n : 1, (int64_t)kWsumRows); }
 __global__ __launch_bounds__(256) void k_gat_wsum_part(const float* __restrict__ x, int64_t ldx, int64_t n, int H,
                                                        int C, const float* __restrict__ w, float* __restrict__ part) {
   const int64_t r0 = (int64_t)blockIdx.x * kWsumRows;
@@ -152,16 +157,23 @@ __global__ __launch_bounds__(256) void k_gat_wsum_part(const float* __restrict__
       const float v = x[r * ldx + f];
       s = __fadd_rn(s, w ? __fmul_rn(w[r * H + h], v) : v);
     }
-    part[(int64_t)blockIdx.x * HC + f] = s;
+    part[(int64_t)f * gridDim.x + blockIdx.x] = s;
   }
 }
-__global__ __launch_bounds__(256) void k_gat_wsum_final(const float* __restrict__ part, int64_t nb, int HC,
+__global__ __launch_bounds__(256) void k_gat_wsum_final(const float* __restrict__ part, int64_t nb,
                                                         float* __restrict__ out) {
-  const int f = blockIdx.x * 256 + threadIdx.x;
-  if (f >= HC) return;
+  __shared__ float red[256];
+  const int t = threadIdx.x;
+  const float* p = part + (int64_t)blockIdx.x * nb;
   float s = 0.0f;
-  for (int64_t b = 0; b < nb; ++b) s = __fadd_rn(s, part[b * HC + f]);
-  out[f] = s;
+  for (int64_t b = t; b < nb; b += 256) s = __fadd_rn(s, p[b]);
+  red[t] = s;
+  __syncthreads();
+  for (int off = 128; off > 0; off >>= 1) {
+    if (t < off) red[t] = __fadd_rn(red[t], red[t + off]);
+    __syncthreads();
+  }
+  if (t == 0) out[blockIdx.x] = red[0];
 }
 
 // ---------------------------------------------------------------------------------------------------------------
@@ -172,6 +184,7 @@ __global__ __launch_bounds__(256) void k_gat_wsum_final(const float* __restrict_
 // group's lanes as (edge slot, head) pairs or on each head's first column lane.  No LDS, no atomics; every sum in a
 // fixed order (per-column sums over a row's edges in CSR / CSC order, as the thread-per-(row, head) kernels).
 constexpr int kGatU = 8;
+constexpr int kGatElds = 32;   // k_gat_attn_w: edges per row whose logits wait in LDS for the alpha pass
 
 template <int G>
 __device__ __forceinline__ float group_sum_pow2(float v, int width) {   // xor butterfly over `width` aligned lanes
@@ -198,10 +211,14 @@ __global__ __launch_bounds__(256) void k_gat_logits_w(const float* __restrict__ 
   if (gl < HC4 && (4 * gl) % C == 0) a[r * H + (4 * gl) / C] = s;
 }
 
-// Forward.  Phase 1 on (slot, head) lanes (ES = G / H slots): the online max / exp-sum of the head's logits over the
-// slot's edges (rb + slot, + ES, ...), merged over the slots in slot order -> m_h, den_h = sum + 1e-16.  Phase 2 on
-// column lanes: per edge in CSR order alpha = exp(e - m_h) / den_h (stored by the head's first lane: the backward's
-// alpha) and out += x_s[j] * alpha, U rows in flight; then + bias, accum + (the thread-per-(row, head) kernel's order).
+// Forward.  The row's first G edge sources come in one coalesced load (lane gl: col[rb + gl]) and reach the other
+// lanes by ds_bpermute, and the x_s rows of its first kGatU edges are requested before any softmax arithmetic, so a
+// row of up to G edges costs two dependent memory round trips instead of one per phase and batch.  Phase 1 on
+// (slot, head) lanes (ES = G / H slots): the online max / exp-sum of the head's logits over the slot's edges (rb + slot,
+// + ES, ...), merged over the slots in slot order -> m_h, den_h = sum + 1e-16; the logits of the first ES * kGatU
+// edges stay in registers.  Phase 2 on column lanes, in CSR order: alpha = exp(e - m_h) / den_h with e taken from the
+// phase-1 lane that holds it (stored by the head's first lane: the backward's alpha) and out += x_s[j] * alpha; then
+// + bias, accum + (the thread-per-(row, head) kernel's order).
 template <int G>
 __global__ __launch_bounds__(256) void k_gat_fwd_w(const int32_t* __restrict__ rowptr, const int32_t* __restrict__ col,
                                                    int64_t n_dst, int H, int C, const float* __restrict__ xs,
@@ -210,34 +227,67 @@ __global__ __launch_bounds__(256) void k_gat_fwd_w(const int32_t* __restrict__ r
                                                    const float* __restrict__ bias, const float* __restrict__ accum,
                                                    int64_t ld_acc, float* __restrict__ alpha, float* __restrict__ out,
                                                    int64_t ldo) {
+  constexpr int U = kGatU;
   const int gl = threadIdx.x % G;
   const int64_t i = ((int64_t)blockIdx.x * 256 + threadIdx.x) / G;
   if (i >= n_dst) return;
   const int rb = rowptr[i], re = rowptr[i + 1];
+  const int deg = re - rb;
+  const int cj = gl < deg ? col[rb + gl] : 0;                    // the sources of edges 0 .. G - 1
+  // source of edge k (< deg) of the row; every lane of the group runs the shuffle (k may differ per lane)
+  auto src = [&](int k) -> int64_t {
+    const int sh = __shfl(cj, k & (G - 1), G);
+    return k < G ? (int64_t)sh : (int64_t)col[rb + k];
+  };
+  const int HC4 = H * C / 4;
+  const bool col_lane = gl < HC4;
+  // the first U edges' x_s rows, in flight during phase 1
+  float4 xv0[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int64_t j = src(u < deg ? u : 0);
+    xv0[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (col_lane && u < deg) xv0[u] = *reinterpret_cast<const float4*>(xs + j * ldxs + 4 * gl);
+  }
   const int ES = G / H;
   const int slot = gl / H, h1 = gl % H;
+  const bool ph1 = slot < ES;
+  const float adv = ph1 && ad ? ad[i * H + h1] : 0.0f;
   float m = -INFINITY, s = 0.0f;
-  if (slot < ES) {
-    const float adv = ad ? ad[i * H + h1] : 0.0f;
-    for (int k0 = rb + slot; k0 < re; k0 += ES * kGatU) {   // kGatU of the slot's edges' logits loaded together
-      float av[kGatU];
+  auto online = [&](float e) {
+    if (e > m) {
+      s = __fadd_rn(__fmul_rn(s, expf(__fsub_rn(m, e))), 1.0f);
+      m = e;
+    } else {
+      s = __fadd_rn(s, expf(__fsub_rn(e, m)));
+    }
+  };
+  float e0[U];   // logits of this lane's edges slot + ES t, t < U (phase-1 lanes)
+  {
+    float av[U];
 #pragma unroll
-      for (int u = 0; u < kGatU; ++u) {
+    for (int t = 0; t < U; ++t) {
+      const int k = slot + ES * t;
+      const int64_t j = src(k < deg ? k : 0);
+      av[t] = ph1 && k < deg ? as[j * H + h1] : 0.0f;
+    }
+#pragma unroll
+    for (int t = 0; t < U; ++t) {
+      e0[t] = lrelu(__fadd_rn(av[t], adv), slope);
+      if (ph1 && slot + ES * t < deg) online(e0[t]);
+    }
+  }
+  if (ph1) {   // rows longer than ES * U: the rest of the slot's edges
+    for (int k0 = rb + slot + ES * U; k0 < re; k0 += ES * U) {
+      float av[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
         const int k = k0 + u * ES;
         av[u] = k < re ? as[(int64_t)col[k] * H + h1] : 0.0f;
       }
 #pragma unroll
-      for (int u = 0; u < kGatU; ++u) {
-        if (k0 + u * ES < re) {
-          const float e = lrelu(__fadd_rn(av[u], adv), slope);
-          if (e > m) {
-            s = __fadd_rn(__fmul_rn(s, expf(__fsub_rn(m, e))), 1.0f);
-            m = e;
-          } else {
-            s = __fadd_rn(s, expf(__fsub_rn(e, m)));
-          }
-        }
-      }
+      for (int u = 0; u < U; ++u)
+        if (k0 + u * ES < re) online(lrelu(__fadd_rn(av[u], adv), slope));
     }
   }
   for (int q = 1; q < ES; ++q) {   // slot 0 merges slots 1 .. ES - 1 in order (every lane runs the shuffles)
@@ -255,40 +305,149 @@ __global__ __launch_bounds__(256) void k_gat_fwd_w(const int32_t* __restrict__ r
     }
   }
   const float den = __fadd_rn(s, 1e-16f);
-  const int HC4 = H * C / 4;
-  const int hq = gl < HC4 ? (4 * gl) / C : 0;
+  const int hq = col_lane ? (4 * gl) / C : 0;
   const float mh = __shfl(m, hq, G), dh = __shfl(den, hq, G);
-  if (gl >= HC4) return;
-  const bool first = (4 * gl) % C == 0;
+  const bool first = col_lane && (4 * gl) % C == 0;
   const float adq = ad ? ad[i * H + hq] : 0.0f;
   float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-  for (int k0 = rb; k0 < re; k0 += kGatU) {
-    const int nk = re - k0;
-    float av[kGatU];
-    float4 xv[kGatU];
+  auto add = [&](int k, float e, const float4& x) {   // edge k of the row, its logit, its x_s quad
+    const float al = __fdiv_rn(expf(__fsub_rn(e, mh)), dh);
+    if (first) __builtin_nontemporal_store(al, alpha + (int64_t)(rb + k) * H + hq);   // streamed once
+    acc.x = __fadd_rn(acc.x, __fmul_rn(x.x, al));
+    acc.y = __fadd_rn(acc.y, __fmul_rn(x.y, al));
+    acc.z = __fadd_rn(acc.z, __fmul_rn(x.z, al));
+    acc.w = __fadd_rn(acc.w, __fmul_rn(x.w, al));
+  };
+  // the logit of edge k < ES U: e0[k / ES] of lane (k % ES) H + hq (ES is a runtime value: the register is picked by
+  // selects, not by a dynamic index); every lane runs the shuffle
+  auto logit = [&](int k) {
+    const int t = k / ES;
+    float r = 0.0f;
 #pragma unroll
-    for (int u = 0; u < kGatU; ++u) {
-      av[u] = 0.0f;
+    for (int tt = 0; tt < U; ++tt) r = tt == t ? e0[tt] : r;
+    return __shfl(r, (k % ES) * H + hq, G);
+  };
+  // edges 0 .. U - 1: rows and logits already here
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const float e = logit(u);
+    if (col_lane && u < deg) add(u, e, xv0[u]);
+  }
+  for (int k0 = U; k0 < deg; k0 += U) {   // the rest, U rows in flight
+    float4 xv[U];
+    float ev[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int k = k0 + u;
+      // logits of edges below ES U come from phase 1's registers; beyond, reloaded
+      ev[u] = logit(k < ES * U ? k : 0);
+      const int64_t j = src(k < deg ? k : 0);
       xv[u] = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (u < nk) {
-        const int64_t j = col[k0 + u];
-        av[u] = as[j * H + hq];
+      if (col_lane && k < deg) {
         xv[u] = *reinterpret_cast<const float4*>(xs + j * ldxs + 4 * gl);
+        if (k >= ES * U) ev[u] = lrelu(__fadd_rn(as[j * H + hq], adq), slope);
       }
     }
 #pragma unroll
-    for (int u = 0; u < kGatU; ++u) {
-      if (u < nk) {
-        const float e = expf(__fsub_rn(lrelu(__fadd_rn(av[u], adq), slope), mh));
-        const float al = __fdiv_rn(e, dh);
-        if (first) alpha[(int64_t)(k0 + u) * H + hq] = al;
-        acc.x = __fadd_rn(acc.x, __fmul_rn(xv[u].x, al));
-        acc.y = __fadd_rn(acc.y, __fmul_rn(xv[u].y, al));
-        acc.z = __fadd_rn(acc.z, __fmul_rn(xv[u].z, al));
-        acc.w = __fadd_rn(acc.w, __fmul_rn(xv[u].w, al));
+    for (int u = 0; u < U; ++u)
+      if (col_lane && k0 + u < deg) add(k0 + u, ev[u], xv[u]);
+  }
+  if (!col_lane) return;
+  if (bias) {
+    const float4 b = *reinterpret_cast<const float4*>(bias + 4 * gl);
+    acc = make_float4(__fadd_rn(acc.x, b.x), __fadd_rn(acc.y, b.y), __fadd_rn(acc.z, b.z), __fadd_rn(acc.w, b.w));
+  }
+  if (accum) {
+    const float4 c = *reinterpret_cast<const float4*>(accum + i * ld_acc + 4 * gl);
+    acc = make_float4(__fadd_rn(c.x, acc.x), __fadd_rn(c.y, acc.y), __fadd_rn(c.z, acc.z), __fadd_rn(c.w, acc.w));
+  }
+  *reinterpret_cast<float4*>(out + i * ldo + 4 * gl) = acc;
+}
+
+// Forward in one pass over the row's edges (hgin_gat_attn_fwd_f32, the default of hgin/gat.py; round 5): the source
+// logit a_s[j, h] = x_s[j, h, :] . att_src[h, :] is formed from the x_s row the aggregate gathers anyway (each lane its
+// 4 products in order, then the head's C / 4 lanes: k_gat_logits_w's arithmetic, bit for bit), so no a_s table is
+// gathered; per edge in CSR order the online softmax keeps (m, s) and the exp-weighted row sum with the rescale
+// exp(m_old - m_new) when the maximum moves, out = acc / (s + 1e-16) (+ bias, accum +); the edge logits go into the
+// alpha slots on the way and become alpha = exp(e - m) / den in a second, L2-resident pass of the head's first lane over
+// its own stores.  Differs from the two-pass form only in rounding (the weighted sum is divided once at the end).
+template <int G, int U = kGatU>
+__global__ __launch_bounds__(256) void k_gat_attn_w(const int32_t* __restrict__ rowptr, const int32_t* __restrict__ col,
+                                                    int64_t n_dst, int H, int C, const float* __restrict__ xs,
+                                                    int64_t ldxs, const float* __restrict__ att_src,
+                                                    const float* __restrict__ ad, float slope,
+                                                    const float* __restrict__ bias, const float* __restrict__ accum,
+                                                    int64_t ld_acc, float* __restrict__ alpha, float* __restrict__ out,
+                                                    int64_t ldo) {
+  extern __shared__ float gat_elds[];   // per row of the block: the logits of its first kGatElds edges, [edge][head]
+  const int gl = threadIdx.x % G;
+  const int64_t i = ((int64_t)blockIdx.x * 256 + threadIdx.x) / G;
+  if (i >= n_dst) return;
+  float* const el = gat_elds + (threadIdx.x / G) * kGatElds * H;
+  const int rb = rowptr[i], re = rowptr[i + 1];
+  const int deg = re - rb;
+  const int cj = gl < deg ? col[rb + gl] : 0;                    // the sources of edges 0 .. G - 1
+  const int HC4 = H * C / 4;
+  const bool col_lane = gl < HC4;
+  const int hq = col_lane ? (4 * gl) / C : 0;
+  const bool first = col_lane && (4 * gl) % C == 0;
+  const float4 at = col_lane ? *reinterpret_cast<const float4*>(att_src + 4 * gl) : make_float4(0.f, 0.f, 0.f, 0.f);
+  const float adq = col_lane && ad ? ad[i * H + hq] : 0.0f;
+  float m = -INFINITY, s = 0.0f;
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int k0 = 0; k0 < deg; k0 += U) {
+    float4 xv[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int k = k0 + u < deg ? k0 + u : 0;
+      const int sh = __shfl(cj, k & (G - 1), G);                 // every lane runs the shuffle
+      const int64_t j = k < G ? (int64_t)sh : (int64_t)col[rb + k];
+      xv[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (col_lane && k0 + u < deg) xv[u] = *reinterpret_cast<const float4*>(xs + j * ldxs + 4 * gl);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (k0 + u < deg) {   // uniform over the group
+        float p = __fadd_rn(__fadd_rn(__fadd_rn(__fmul_rn(xv[u].x, at.x), __fmul_rn(xv[u].y, at.y)),
+                                      __fmul_rn(xv[u].z, at.z)), __fmul_rn(xv[u].w, at.w));
+        p = group_sum_pow2<G>(p, C / 4);                         // a_s[j, hq]
+        const float e = lrelu(__fadd_rn(p, adq), slope);
+        if (first) {   // the logit, until the alpha pass: in LDS for the first kGatElds edges, else in alpha
+          if (k0 + u < kGatElds) el[(k0 + u) * H + hq] = e;
+          else alpha[(int64_t)(rb + k0 + u) * H + hq] = e;
+        }
+        if (e > m) {
+          const float sc = expf(__fsub_rn(m, e));
+          s = __fadd_rn(__fmul_rn(s, sc), 1.0f);
+          acc = make_float4(__fadd_rn(__fmul_rn(acc.x, sc), xv[u].x), __fadd_rn(__fmul_rn(acc.y, sc), xv[u].y),
+                            __fadd_rn(__fmul_rn(acc.z, sc), xv[u].z), __fadd_rn(__fmul_rn(acc.w, sc), xv[u].w));
+          m = e;
+        } else {
+          const float w = expf(__fsub_rn(e, m));
+          s = __fadd_rn(s, w);
+          acc = make_float4(__fadd_rn(acc.x, __fmul_rn(w, xv[u].x)), __fadd_rn(acc.y, __fmul_rn(w, xv[u].y)),
+                            __fadd_rn(acc.z, __fmul_rn(w, xv[u].z)), __fadd_rn(acc.w, __fmul_rn(w, xv[u].w)));
+        }
       }
     }
   }
+  if (!col_lane) return;
+  const float den = __fadd_rn(s, 1e-16f);
+  if (first) {   // the logits stored above -> alpha (this lane's own stores, read back in order)
+    const int kl = deg < kGatElds ? deg : kGatElds;
+    for (int k = 0; k < kl; ++k)
+      __builtin_nontemporal_store(__fdiv_rn(expf(__fsub_rn(el[k * H + hq], m)), den), alpha + (int64_t)(rb + k) * H + hq);
+    for (int k0 = rb + kGatElds; k0 < re; k0 += U) {
+      float ev[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) ev[u] = k0 + u < re ? alpha[(int64_t)(k0 + u) * H + hq] : 0.0f;
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        if (k0 + u < re)
+          __builtin_nontemporal_store(__fdiv_rn(expf(__fsub_rn(ev[u], m)), den), alpha + (int64_t)(k0 + u) * H + hq);
+    }
+  }
+  acc = make_float4(__fdiv_rn(acc.x, den), __fdiv_rn(acc.y, den), __fdiv_rn(acc.z, den), __fdiv_rn(acc.w, den));
   if (bias) {
     const float4 b = *reinterpret_cast<const float4*>(bias + 4 * gl);
     acc = make_float4(__fadd_rn(acc.x, b.x), __fadd_rn(acc.y, b.y), __fadd_rn(acc.z, b.z), __fadd_rn(acc.w, b.w));
@@ -519,6 +678,42 @@ extern "C" int hgin_gat_fwd_f32(const int32_t* rowptr, const int32_t* col, int64
   return check_launch("hgin_gat_fwd_f32");
 }
 
+extern "C" int hgin_gat_attn_fwd_f32(const int32_t* rowptr, const int32_t* col, int64_t n_dst, int64_t H, int64_t C,
+                                     const float* xs, int64_t ldxs, const float* att_src, const float* ad, float slope,
+                                     const float* bias, const float* accum, int64_t ld_acc, float* alpha, float* out,
+                                     int64_t ldo, void* stream) {
+  HGIN_ARG_CHECK(n_dst >= 0 && H >= 1 && C >= 1 && ldxs >= H * C && ldo >= H * C && (!accum || ld_acc >= H * C),
+                 "hgin_gat_attn_fwd_f32: bad sizes");
+  if (n_dst == 0) return HGIN_OK;
+  HGIN_ARG_CHECK(rowptr && col && xs && att_src && alpha && out, "hgin_gat_attn_fwd_f32: NULL operand");
+  const int G = gat_group(H, C);
+  if (!(G && al16(xs, ldxs) && al16(out, ldo) && al16(accum, ld_acc) && (!bias || aligned16(bias)) &&
+        aligned16(att_src))) {
+    set_error("hgin_gat_attn_fwd_f32: needs the wave-group shape (C a multiple of 4 with C / 4 a power of two, "
+              "H * C <= 256, 16-B aligned rows); use hgin_gat_logits_f32 + hgin_gat_fwd_f32");
+    return HGIN_E_ARG;
+  }
+  HGIN_TRACE("k_gat_attn_w<%d>", G);
+  const int64_t rows = n_dst;
+  hipStream_t s = as_stream(stream);
+  // 4 rows of x_s in flight per group: 52 VGPRs, 8 waves per SIMD (8 rows: 68 VGPRs, 7 waves, 2.3 % slower; 16 rows:
+  // 4 waves, 42 % slower — profiles/r05/gat_u_ab.txt)
+  const size_t lds = sizeof(float) * (size_t)(256 / G) * kGatElds * (size_t)H;
+#define HGIN_GAT_ATTN(GV)                                                                                          \
+  case GV:                                                                                                        \
+    k_gat_attn_w<GV, 4><<<(unsigned)ceil_div(rows, (int64_t)(256 / GV)), 256, lds, s>>>(                          \
+        rowptr, col, n_dst, (int)H, (int)C, xs, ldxs, att_src, ad, slope, bias, accum, ld_acc, alpha, out, ldo);   \
+    break;
+  switch (G) {
+    HGIN_GAT_ATTN(1) HGIN_GAT_ATTN(2) HGIN_GAT_ATTN(4) HGIN_GAT_ATTN(8) HGIN_GAT_ATTN(16) HGIN_GAT_ATTN(32)
+    default: HGIN_GAT_ATTN(64)
+  }
+#undef HGIN_GAT_ATTN
+  return check_launch("hgin_gat_attn_fwd_f32");
+}
+
+extern "C" int hgin_gat_attn_supported(int64_t H, int64_t C) { return gat_group(H, C) != 0; }
+
 extern "C" int hgin_gat_bwd_dst_f32(const int32_t* rowptr, const int32_t* col, int64_t n_dst, int64_t H, int64_t C,
                                     const float* xs, int64_t ldxs, const float* g_out, int64_t ldg, const float* alpha,
                                     const float* as, const float* ad, float slope, const float* att_dst, float* g_pre,
@@ -568,7 +763,7 @@ extern "C" int hgin_gat_bwd_src_f32(const int32_t* cptr, const int32_t* cdst, co
 
 extern "C" int hgin_gat_wsum_workspace_size(int64_t n, int64_t H, int64_t C, size_t* bytes) {
   HGIN_ARG_CHECK(bytes && n >= 0 && H >= 1 && C >= 1, "hgin_gat_wsum_workspace_size: bad args");
-  *bytes = sizeof(float) * (size_t)ceil_div(n > 0 ? n : 1, kWsumRows) * (size_t)(H * C);
+  *bytes = sizeof(float) * (size_t)wsum_blocks(n) * (size_t)(H * C);
   return HGIN_OK;
 }
 
@@ -577,7 +772,7 @@ extern "C" int hgin_gat_wsum_f32(const float* x, int64_t ldx, int64_t n, int64_t
   HGIN_ARG_CHECK(n >= 0 && H >= 1 && C >= 1 && ldx >= H * C && out, "hgin_gat_wsum_f32: bad args");
   hipStream_t s = as_stream(stream);
   if (n == 0) return memset_async(out, 0, sizeof(float) * (size_t)(H * C), s, "hgin_gat_wsum_f32");
-  const int64_t nb = ceil_div(n, kWsumRows);
+  const int64_t nb = wsum_blocks(n);
   const size_t need = sizeof(float) * (size_t)nb * (size_t)(H * C);
   if (!workspace || workspace_bytes < need) {
     set_error("hgin_gat_wsum_f32: workspace %zu < %zu", workspace_bytes, need);
@@ -587,6 +782,6 @@ extern "C" int hgin_gat_wsum_f32(const float* x, int64_t ldx, int64_t n, int64_t
   float* part = static_cast<float*>(workspace);
   HGIN_TRACE("k_gat_wsum");
   k_gat_wsum_part<<<(unsigned)nb, 256, 0, s>>>(x, ldx, n, (int)H, (int)C, w, part);
-  k_gat_wsum_final<<<blocks_for(H * C), 256, 0, s>>>(part, nb, (int)(H * C), out);
+  k_gat_wsum_final<<<(unsigned)(H * C), 256, 0, s>>>(part, nb, out);
   return check_launch("hgin_gat_wsum_f32");
 }

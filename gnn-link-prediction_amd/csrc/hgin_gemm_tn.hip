@@ -1126,9 +1126,8 @@ __global__ __launch_bounds__(512, 1) void k_wsd_f32(const float* __restrict__ A,
         const int grp = q * C::NT + t;
         if (CT % C::NT != 0 && grp >= CT) break;
         const bool isA = grp < CA;
-        const int cols = isA ? N : K;
         const int e0 = (isA ? grp : grp - CA) * 4;
-        const int row = e0 / cols, col = e0 % cols;
+        const int row = isA ? e0 / N : e0 / K, col = isA ? e0 % N : e0 % K;   // constant divisors: shifts
         const float* src = reinterpret_cast<const float*>(fbase + (isA ? 0 : C::A_BYTES + C::Z_BYTES)) + e0;
         float4 v = *reinterpret_cast<const float4*>(src);
         if (row >= valid) v = make_float4(0.f, 0.f, 0.f, 0.f);

@@ -178,6 +178,9 @@ _SIGS = {
     "hgin_global_pool_f32": ([_P, _I64, _P, _I64, _I64, _P, _I64, _P, _P, _SZ, _P], _I32),
     "hgin_global_pool_bf16": ([_P, _I64, _P, _I64, _I64, _P, _I64, _P, _P, _SZ, _P], _I32),
     "hgin_gat_logits_f32": ([_P, _I64, _I64, _I64, _I64, _P, _P, _P], _I32),
+    "hgin_gat_attn_fwd_f32": ([_P, _P, _I64, _I64, _I64, _P, _I64, _P, _P, ctypes.c_float, _P, _P, _I64, _P, _P, _I64,
+                               _P], _I32),
+    "hgin_gat_attn_supported": ([_I64, _I64], _I32),
     "hgin_gat_fwd_f32": ([_P, _P, _I64, _I64, _I64, _P, _I64, _P, _P, ctypes.c_float, _P, _P, _I64, _P, _P, _I64, _P],
                          _I32),
     "hgin_gat_bwd_dst_f32": ([_P, _P, _I64, _I64, _I64, _P, _I64, _P, _I64, _P, _P, _P, ctypes.c_float, _P, _P, _P,
@@ -192,7 +195,7 @@ _SIGS = {
     "hgin_trace_enable": ([_I32], _I32),
     "hgin_trace_read": ([ctypes.c_char_p, _SZ], _SZ),
 }
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 
 def lib() -> ctypes.CDLL:

@@ -159,6 +159,12 @@ def _wsum(x: Tensor, w: Optional[Tensor], H: int, C: int) -> Tensor:
     return out
 
 
+def _attn_one_pass(H: int, C: int) -> bool:
+    """hgin_gat_attn_fwd_f32 takes the shape (the wave-group form: C a multiple of 4 with C / 4 a power of two,
+    H * C <= 256; HGIN_GAT_WAVE=0 turns it off); the tensors are contiguous and 16-B aligned by construction."""
+    return bool(_lib.lib().hgin_gat_attn_supported(int(H), int(C)))
+
+
 def _logits(x: Tensor, att: Tensor, H: int, C: int) -> Tensor:
     a = torch.empty(x.size(0), H, dtype=torch.float32, device=x.device)
     _lib.call("hgin_gat_logits_f32", _p(x), x.stride(0), x.size(0), H, C, _p(att), _p(a), _stream(x))
@@ -173,14 +179,23 @@ class _GatAttentionFn(torch.autograd.Function):
     def forward(ctx, xs, xd, att_src, att_dst, bias, accum, graph: GatGraph, H: int, C: int, slope: float):
         att_s = att_src.reshape(-1).contiguous()
         att_d = att_dst.reshape(-1).contiguous()
-        a_s = _logits(xs, att_s, H, C)
         a_d = _logits(xd, att_d, H, C) if xd is not None else None
         n_dst = graph.csr.n_rows
         alpha = torch.empty(graph.n_edges, H, dtype=torch.float32, device=xs.device)
         out = torch.empty(n_dst, H * C, dtype=torch.float32, device=xs.device)
-        _lib.call("hgin_gat_fwd_f32", _p(graph.csr.rowptr), _p(graph.csr.col), n_dst, H, C, _p(xs), xs.stride(0),
-                  _p(a_s), _p(a_d), ctypes.c_float(slope), _p(bias), _p(accum),
-                  accum.stride(0) if accum is not None else 0, _p(alpha), _p(out), out.stride(0), _stream(xs))
+        acc_ld = accum.stride(0) if accum is not None else 0
+        al16 = lambda t: t is None or (t.data_ptr() % 16 == 0 and (t.dim() < 2 or t.stride(0) % 4 == 0))  # noqa: E731
+        if _attn_one_pass(H, C) and al16(xs) and al16(accum) and al16(bias) and al16(att_s):
+            # one pass: a_s from the gathered x_s rows (hgin_gat_attn_fwd_f32); the backward forms a_s itself
+            a_s = None
+            _lib.call("hgin_gat_attn_fwd_f32", _p(graph.csr.rowptr), _p(graph.csr.col), n_dst, H, C, _p(xs),
+                      xs.stride(0), _p(att_s), _p(a_d), ctypes.c_float(slope), _p(bias), _p(accum), acc_ld, _p(alpha),
+                      _p(out), out.stride(0), _stream(xs))
+        else:
+            a_s = _logits(xs, att_s, H, C)
+            _lib.call("hgin_gat_fwd_f32", _p(graph.csr.rowptr), _p(graph.csr.col), n_dst, H, C, _p(xs), xs.stride(0),
+                      _p(a_s), _p(a_d), ctypes.c_float(slope), _p(bias), _p(accum), acc_ld, _p(alpha), _p(out),
+                      out.stride(0), _stream(xs))
         ctx.save_for_backward(xs, xd, att_s, att_d, a_s, a_d, alpha)
         ctx.graph, ctx.H, ctx.C, ctx.slope = graph, H, C, slope
         ctx.has_bias, ctx.has_accum = bias is not None, accum is not None
@@ -191,6 +206,8 @@ class _GatAttentionFn(torch.autograd.Function):
     def backward(ctx, g_out):
         xs, xd, att_s, att_d, a_s, a_d, alpha = ctx.saved_tensors
         graph, H, C, slope = ctx.graph, ctx.H, ctx.C, ctx.slope
+        if a_s is None:   # the one-pass forward formed a_s on the fly (same arithmetic as hgin_gat_logits_f32)
+            a_s = _logits(xs, att_s, H, C)
         g_out = g_out.contiguous()
         dev = g_out.device
         n_dst, n_src = graph.csr.n_rows, graph.csc.n_rows

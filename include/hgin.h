@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define HGIN_ABI_VERSION 4
+#define HGIN_ABI_VERSION 5
 
 #define HGIN_OK 0
 #define HGIN_E_ARG (-1)        /* bad size / null pointer / unsupported combination */
@@ -402,6 +402,18 @@ int hgin_gat_logits_f32(const float* x, int64_t ldx, int64_t n, int64_t H, int64
 int hgin_gat_fwd_f32(const int32_t* rowptr, const int32_t* col, int64_t n_dst, int64_t H, int64_t C, const float* xs,
                      int64_t ldxs, const float* as, const float* ad, float slope, const float* bias, const float* accum,
                      int64_t ld_acc, float* alpha, float* out, int64_t ldo, void* stream);
+/* Round 5 (ABI 5): the forward attention in one pass, a_s formed from the gathered x_s rows (no a_s table):
+ *   hgin_gat_attn_fwd_f32:  alpha / out as hgin_gat_fwd_f32 with a_s[j, h] = x_s[j, h, :] . att_src[h, :] (the same
+ *                           per-lane arithmetic as hgin_gat_logits_f32's group form), the weighted sum divided once by
+ *                           the softmax denominator at the end (online max / sum); needs the wave-group shape —
+ *   hgin_gat_attn_supported: 1 when (H, C) and HGIN_GAT_WAVE allow it (C a multiple of 4 with C / 4 a power of two,
+ *                           H * C <= 256; rows must also be 16-B aligned: HGIN_E_ARG otherwise).
+ *   Replaces hgin_gat_logits_f32 (for a_s) + hgin_gat_fwd_f32 at models.py:413-418's GATConv.forward. */
+int hgin_gat_attn_fwd_f32(const int32_t* rowptr, const int32_t* col, int64_t n_dst, int64_t H, int64_t C,
+                          const float* xs, int64_t ldxs, const float* att_src, const float* ad, float slope,
+                          const float* bias, const float* accum, int64_t ld_acc, float* alpha, float* out, int64_t ldo,
+                          void* stream);
+int hgin_gat_attn_supported(int64_t H, int64_t C);
 int hgin_gat_bwd_dst_f32(const int32_t* rowptr, const int32_t* col, int64_t n_dst, int64_t H, int64_t C,
                          const float* xs, int64_t ldxs, const float* g_out, int64_t ldg, const float* alpha,
                          const float* as, const float* ad, float slope, const float* att_dst, float* g_pre, float* g_ad,

@@ -57,7 +57,7 @@ def test_attention_and_aggregate_vs_reference(case):
             g = gat_graph(ei[(src, key.split("__")[1], dst)], xs.size(0), xd.size(0), True)
             with _lib.trace_launches() as tr:
                 agg = _GatAttentionFn.apply(xs, xd, conv.att_src, conv.att_dst, None, None, g, H, C, 0.2)
-            assert any(t.startswith("k_gat_fwd_w<") for t in tr.kernels), tr.kernels   # the wave-group form
+            assert any(t.startswith("k_gat_attn_w<") for t in tr.kernels), tr.kernels  # the one-pass form
             want = fx[f"agg.0.{key}"]
             assert _close(agg.view(-1, H, C), want), (key, float((agg.cpu().view(-1, H, C) - want).abs().max()))
             # alpha of CSR position p belongs to edge perm[p] of the adjusted list
@@ -70,6 +70,13 @@ def test_attention_and_aggregate_vs_reference(case):
                       _stream(xs))
             ref_alpha = fx[f"alpha.0.{key}"][g.csr.perm.long().cpu()]
             assert _close(alpha, ref_alpha), (key, float((alpha.cpu() - ref_alpha).abs().max()))
+            # the one-pass kernel's alpha and output against the same fixture (a_s formed from the x_s rows)
+            alpha1, out1 = torch.empty_like(alpha), torch.empty_like(out)
+            _lib.call("hgin_gat_attn_fwd_f32", _p(g.csr.rowptr), _p(g.csr.col), xd.size(0), H, C, _p(xs),
+                      xs.stride(0), _p(conv.att_src.reshape(-1).contiguous()), _p(a_d), ctypes.c_float(0.2), None,
+                      None, 0, _p(alpha1), _p(out1), out1.stride(0), _stream(xs))
+            assert _close(alpha1, ref_alpha), (key, float((alpha1.cpu() - ref_alpha).abs().max()))
+            assert _close(out1.view(-1, H, C), want), key
 
 
 @pytest.mark.parametrize("case", CASES)
@@ -163,9 +170,10 @@ def test_relation_forward_backward_vs_oracle(H, C):
         out = _GatAttentionFn.apply(dev[0], dev[1], dev[2], dev[3], dev[4], None, graph, H, C, 0.2)
         out.backward(g_out.to(DEV))
         torch.cuda.synchronize()
-    wave = C % 4 == 0
-    for k in ("k_gat_logits", "k_gat_fwd", "k_gat_bwd_dst", "k_gat_bwd_src"):
+    wave = C % 4 == 0   # the one-pass forward (k_gat_attn_w) + wave-group backward, else the thread forms
+    for k in ("k_gat_logits", "k_gat_attn", "k_gat_bwd_dst", "k_gat_bwd_src"):
         assert any(t.startswith(k + "_w<") for t in tr.kernels) == wave, (k, tr.kernels)
+    assert any(t == "k_gat_fwd" for t in tr.kernels) == (not wave), tr.kernels
     assert _close(out, out_ref), float((out.detach().cpu().double() - out_ref.detach()).abs().max())
     for name, a, b in zip(("x_s", "x_d", "att_src", "att_dst", "bias"), dev, ref):
         d = float((a.grad.double().cpu() - b.grad).norm())

@@ -69,6 +69,14 @@ def main():
             else:
                 fn = lambda: ops.mlp_bwd_w(gy, z, s, a, want_gz=want)   # noqa: E731
             flops = 2.0 * M * N * K
+        elif name == "dwro":   # the readout's first Linear(512, 128) dW with the PReLU backward (k_wsd_f32<128,512,PRO>)
+            N = 128
+            a = torch.randn(M, 512, device="cuda", generator=g)
+            gy = torch.randn(M, N, device="cuda", generator=g)
+            z = torch.randn(M, N, device="cuda", generator=g)
+            fn = lambda: ops.mlp_bwd_w(gy, z, s, a[:, :256], a[:, 256:], want_gz=True)   # noqa: E731
+            flops = 2.0 * M * N * 512
+            N = 256
         elif name == "dx256":
             gz = torch.randn(M, N, device="cuda", generator=g)
             w = torch.randn(N, N, device="cuda", generator=g) / 16
