@@ -17,7 +17,8 @@
 //                             each layer's input and pre-activation gradient rows kept for the weight gradients;
 //   k_sb_bwd_w  (per layer)   workgroup per (row chunk, relation): the chunk's g_z = PReLU'(z) g_y and g_comb = g_z W,
 //                             then its partial W / bias / slope / eps gradients
-//                             (the last layer's launch also the readout layers' partial W / bias gradients);
+//                             (the last and first layers' launches also the readout layers' partial W / bias
+//                             gradients, half each);
 //   k_sb_bwd_in (layers > 0)  thread per (node type, row, column): the layer input's gradient — every relation's self
 //                             term and CSC aggregate of g_comb, in relation order;
 //   k_sb_final                every parameter gradient = its partials summed in a fixed order, times d sqrt(loss) /
@@ -96,9 +97,8 @@ struct SbArgs {
   float* gA;                // [3] blocks of cap_t x H  (gradient of the current layer's outputs)
   float* gB;                // same (gradient of its inputs)
   int64_t g_off[3];
-  float* gz;                // [4] blocks of cap_dst x H     (per relation)
-  float* gc;                // [4] blocks of cap_dst x Kmax
-  int64_t gz_off[kRel], gc_off[kRel];
+  float* gc;                // [4] blocks of cap_dst x Kmax (g_comb per relation)
+  int64_t gc_off[kRel];
   int kmax;                 // row stride of the gc blocks (relations differ in K)
   int cap[3];               // row capacity per node type (grid sizes)
   float* part_gin;          // [n_parts][p_gin]
@@ -142,6 +142,110 @@ __device__ float block_sum(float v, float* red) {
 
 __device__ __forceinline__ int nrows(const SbArgs& a, int t) { return a.goff[t * (a.G + 1) + a.G]; }
 
+// sum over t < n of x[t sx] y[t sy], in t order (one fma chain onto acc); the operands are loaded 8 pairs at a time so
+// that a chain costs a memory round trip per 8 terms, not per term (the small-batch kernels are latency-bound chains)
+__device__ __forceinline__ float dot_chain(const float* x, int sx, const float* y, int sy, int n, float acc) {
+  int t = 0;
+  for (; t + 8 <= n; t += 8) {
+    float xv[8], yv[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      xv[j] = x[(t + j) * sx];
+      yv[j] = y[(t + j) * sy];
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc = fmaf(xv[j], yv[j], acc);
+  }
+  if (t < n) {   // the tail: clamped loads, the terms past n skipped
+    float xv[8], yv[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int u = t + j < n ? t + j : n - 1;
+      xv[j] = x[u * sx];
+      yv[j] = y[u * sy];
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      if (t + j < n) acc = fmaf(xv[j], yv[j], acc);
+  }
+  return acc;
+}
+
+// acc[j] += sum over t < n of x[j xr + t] y[t sy] for the rows j < nrow (<= 4; the rows past nrow reread row 0),
+// in t order: y loaded once per term for all the rows (a readout phase with >= 2 rows per thread: lanes along the
+// outputs read y, the rows' x are broadcasts)
+__device__ __forceinline__ void dot_rows4(const float* x, int xr, const float* y, int sy, int n, int nrow, float* acc) {
+  const int xo[4] = {0, nrow > 1 ? xr : 0, nrow > 2 ? 2 * xr : 0, nrow > 3 ? 3 * xr : 0};
+  for (int t = 0; t < n; t += 8) {
+    float yv[8], xv[4][8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int u = t + j < n ? t + j : n - 1;
+      yv[j] = y[u * sy];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) xv[r][j] = x[xo[r] + u];
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      if (t + j < n) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc[r] = fmaf(xv[r][j], yv[j], acc[r]);
+      }
+  }
+}
+
+// threads per output of a readout phase with nout outputs of len-term sums: a power of two <= 16 that keeps the
+// phase within one pass of the workgroup and >= 4 terms per thread (thread s of an output sums terms s, s + S, ...;
+// the S adjacent lanes then combine in a fixed xor tree, identical on every lane)
+__device__ __forceinline__ int split_of(int nout, int len) {
+  int S = 1;
+  while (S < 16 && nout * S * 2 <= kSbThreads && len >= 8 * S) S *= 2;
+  return S;
+}
+__device__ __forceinline__ float group_sum(float v, int S) {
+  for (int off = 1; off < S; off <<= 1) v = __fadd_rn(v, __shfl_xor(v, off));
+  return v;
+}
+
+// sum over t < n of x[t sx] onto acc, in t order (one add chain; 8 loads in flight)
+__device__ __forceinline__ float sum_chain(const float* x, int64_t sx, int n, float acc) {
+  int t = 0;
+  for (; t + 8 <= n; t += 8) {
+    float xv[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) xv[j] = x[(t + j) * sx];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc = __fadd_rn(acc, xv[j]);
+  }
+  if (t < n) {
+    float xv[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) xv[j] = x[(t + j < n ? t + j : n - 1) * sx];
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      if (t + j < n) acc = __fadd_rn(acc, xv[j]);
+  }
+  return acc;
+}
+
+// sum over edges e in [e0, e1) of xs[col[e] ld + c] onto acc, in edge order: 8 column indices, then their 8 values,
+// in flight at a time (two dependent round trips per 8 edges instead of per edge)
+__device__ __forceinline__ float gather_chain(const int32_t* col, int e0, int e1, const float* xs, int64_t ld, int c,
+                                              float acc) {
+  for (int e = e0; e < e1; e += 8) {
+    int ci[8];
+    float xv[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) ci[j] = col[e + j < e1 ? e + j : e1 - 1];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) xv[j] = xs[(int64_t)ci[j] * ld + c];
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      if (e + j < e1) acc = __fadd_rn(acc, xv[j]);
+  }
+  return acc;
+}
+
 // One layer's forward for kSbFwdRows rows of node type t (grid = row blocks x types): per relation into t (relation
 // order) comb_r = [aggregate | (1 + eps) x_dst] (concat, first layer) or aggregate + (1 + eps) x_dst (add), the
 // aggregate a sequential edge-order sum (models.py:210-215); then per row and output column the sum over those
@@ -178,13 +282,13 @@ __global__ __launch_bounds__(kSbThreads) void k_sb_fwd(SbArgs a, int l) {
           const float* xs = a.x[s];
           const int64_t ld = a.ldx[s];
           const int c = a.cols[s][k];
-          for (int e = rp[i]; e < rp[i + 1]; ++e) v = __fadd_rn(v, xs[(int64_t)cl[e] * ld + c]);
+          v = gather_chain(cl, rp[i], rp[i + 1], xs, ld, c, v);
         } else {
           v = __fmul_rn(sc, a.x[t][(int64_t)i * a.ldx[t] + a.cols[t][k - fs]]);
         }
       } else {
         const float* xs = a.act + a.act_off[l - 1][s];
-        for (int e = rp[i]; e < rp[i + 1]; ++e) v = __fadd_rn(v, xs[(int64_t)cl[e] * H + k]);
+        v = gather_chain(cl, rp[i], rp[i + 1], xs, H, k, v);
         v = __fadd_rn(v, __fmul_rn(sc, a.act[a.act_off[l - 1][t] + (int64_t)i * H + k]));
       }
       s_comb[slot][idx] = v;
@@ -204,8 +308,7 @@ __global__ __launch_bounds__(kSbThreads) void k_sb_fwd(SbArgs a, int l) {
       const SbConv& cv = a.conv[l][r];
       const float* cr = s_comb[sl++] + ii * K;
       const float* wr = cv.w + (int64_t)h * K;
-      float z = 0.0f;
-      for (int k = 0; k < K; ++k) z = fmaf(cr[k], wr[k], z);
+      float z = dot_chain(cr, 1, wr, 1, K, 0.0f);
       z = __fadd_rn(z, cv.b[h]);
       a.zb[a.zb_off[l][r] + (int64_t)(r0 + ii) * H + h] = z;
       const float yv = z > 0.0f ? z : __fmul_rn(cv.slope[0], z);
@@ -216,12 +319,75 @@ __global__ __launch_bounds__(kSbThreads) void k_sb_fwd(SbArgs a, int l) {
   }
 }
 
+// n contiguous floats from global memory into LDS, every load of a thread issued before its first store (one
+// memory round trip for up to J x kSbThreads floats)
+template <int J = 32>
+__device__ __forceinline__ void copy_flat(float* dst, const float* src, int n) {
+  for (int b = threadIdx.x; b < n; b += J * kSbThreads) {
+    float v[J];
+#pragma unroll
+    for (int j = 0; j < J; ++j) v[j] = src[b + j * kSbThreads < n ? b + j * kSbThreads : n - 1];
+#pragma unroll
+    for (int j = 0; j < J; ++j)
+      if (b + j * kSbThreads < n) dst[b + j * kSbThreads] = v[j];
+  }
+}
+
+// n / d for 0 <= n < 2^16, 1 <= d < 2^16 by one multiply-high: m = floor(2^32 / d) + 1 over-estimates 1 / d by less
+// than 2^-32, which moves n / d by less than 2^-16 < 1 / d, so the floor is exact
+struct FastDiv {
+  unsigned m;
+  int d;
+};
+__device__ __forceinline__ FastDiv fast_div(int d) { return {d > 1 ? 0xFFFFFFFFu / (unsigned)d + 1u : 0u, d}; }
+__device__ __forceinline__ int fdq(const FastDiv& f, int n) { return f.d > 1 ? (int)__umulhi((unsigned)n, f.m) : n; }
+
+// rows [nr][K] of src (row stride K) into dst [nr][K + 1] with a last column of ones (8 loads in flight per thread;
+// nr (K + 1) < 2^16)
+__device__ __forceinline__ void stage_ones(float* dst, const float* src, int nr, int K) {
+  const int K1 = K + 1, tot = nr * K1;
+  const FastDiv f = fast_div(K1);
+  for (int b = threadIdx.x; b < tot; b += 8 * kSbThreads) {
+    float v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int idx = b + j * kSbThreads;
+      const int rr = fdq(f, idx), k = idx - rr * K1;
+      const bool ld = idx < tot && k < K;
+      const float x = src[ld ? rr * K + k : 0];
+      v[j] = ld ? x : 1.0f;
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      if (b + j * kSbThreads < tot) dst[b + j * kSbThreads] = v[j];
+  }
+}
+
 // Tiles of kSbRows path rows (a grid-stride loop over the batch's tiles): readout forward, loss partial, readout
-// backward (unscaled) down to the path embeddings' gradient.  Each layer's input rows and pre-activation gradient rows go to ro_in / ro_gz, from which
-// the readout blocks of k_sb_bwd_w form the weight-gradient partials over the same row chunks as the GIN's (a tile
-// that also reduced its own rows' weight gradients spent most of its time there and left n_tiles partials to sum).
-// The hidden weights are staged in LDS when they fit (row stride K | 1: odd, so the forward's column-per-thread reads
-// and the backward's row-per-thread reads are both free of bank conflicts).
+// backward (unscaled) down to the path embeddings' gradient.  Each layer's input rows and pre-activation gradient rows
+// go to ro_in / ro_gz, from which the readout blocks of k_sb_bwd_w form the weight-gradient partials over the same
+// row chunks as the GIN's (a tile that also reduced its own rows' weight gradients spent most of its time there and
+// left n_tiles partials to sum).  kWL: the readout's parameters are staged in LDS in the flat gradient layout (rows
+// unpadded: the backward's lanes read along a W row, and the forward's, which read different W rows, start at rotated
+// columns when the row stride is even, so both are free of bank conflicts).  The layer loops are unrolled over kSbMaxHid so that every buffer pointer is a
+// known LDS (or global) address, and each phase splits its sums over split_of() lanes: a tile is a chain of short
+// dependent phases, and its time is their LDS round trips (profiles/r05: 34 us per batch when every term was one).
+// HGIN_SB_STAMPS (a diagnostic build only, tools/sb_stamps.py): thread 0 of each readout workgroup writes the
+// wall clock at its phase boundaries, each bwd_w block at its start and end (read back by hgin_sb_stamps_read)
+#ifdef HGIN_SB_STAMPS
+constexpr int kStampRo = 1024 * 16, kStampW = 2 * 2048 * 2;
+__device__ unsigned long long g_sb_stamps[kStampRo + kStampW];
+#define SB_STAMP(k) \
+  if (threadIdx.x == 0 && blockIdx.x < 1024) g_sb_stamps[blockIdx.x * 16 + (k)] = wall_clock64()
+#define SB_STAMP_W(l, k)                                                                      \
+  if (threadIdx.x == 0 && blockIdx.y * gridDim.x + blockIdx.x < 2048)                         \
+  g_sb_stamps[kStampRo + ((l) * 2048 + blockIdx.y * gridDim.x + blockIdx.x) * 2 + (k)] = wall_clock64()
+#else
+#define SB_STAMP(k)
+#define SB_STAMP_W(l, k)
+#endif
+
+template <bool kWL>
 __global__ __launch_bounds__(kSbThreads) void k_sb_readout(SbArgs a) {
   extern __shared__ float sm[];
   __shared__ float red[kSbThreads];
@@ -229,49 +395,94 @@ __global__ __launch_bounds__(kSbThreads) void k_sb_readout(SbArgs a) {
   const int H = a.H;
   const int m = a.m_valid[0];
   constexpr int R = kSbRows;
+  const int ntile = (m + R - 1) / R;
+  if ((int)blockIdx.x >= ntile) return;   // (the grid is sized for the capacity; uniform per workgroup)
+  SB_STAMP(0);
+  const int nh = a.nhid;
   const int fp = a.concat_path ? a.fdim[0] : 0;
   const int w0 = H + fp;
   int win[kSbMaxHid + 1];   // input width of layer i (i = nhid: the head)
   win[0] = w0;
-  for (int i = 0; i < a.nhid; ++i) win[i + 1] = a.rw[i];
   int maxw = w0;
-  for (int i = 0; i < a.nhid; ++i) maxw = a.rw[i] > maxw ? a.rw[i] : maxw;
-  // LDS: [W_i [rw_i][win_i | 1] when ro_wlds] in0 [R][w0] | per hidden layer z_i, y_i [R][rw_i] | gbuf x2 [R][maxw]
-  float* p = sm;
-  const float* W[kSbMaxHid];
-  int ldw[kSbMaxHid];
-  for (int i = 0; i < a.nhid; ++i) {
-    const int K = win[i], N = a.rw[i];
-    if (a.ro_wlds) {
-      const int ks = K | 1;
-      for (int idx = tid; idx < N * K; idx += kSbThreads) p[(idx / K) * ks + idx % K] = a.row_w[i][idx];
-      W[i] = p;
-      ldw[i] = ks;
-      p += N * ks;
-    } else {
-      W[i] = a.row_w[i];
-      ldw[i] = K;
+#pragma unroll
+  for (int i = 0; i < kSbMaxHid; ++i) {
+    win[i + 1] = i < nh ? a.rw[i] : 0;
+    maxw = i < nh && a.rw[i] > maxw ? a.rw[i] : maxw;
+  }
+  const int KL = a.rw[nh - 1];
+  // LDS: [kWL: per hidden layer W_i [rw_i][win_i | 1] (rows padded to an odd stride: the forward's lanes read
+  // different W rows, the backward's read along one; both conflict-free) and b_i [rw_i], then the head's W [KL]] in0
+  // [R][w0] | z_i, y_i [R][rw_i] per hidden layer | gbuf x2 [R][maxw] | outv [R].  (Float offsets, not pointer arrays:
+  // the pointers formed from them at each use are plain LDS addresses, where arrays of pointers became generic ones.)
+  int oW[kSbMaxHid], ldw[kSbMaxHid];
+  int off = 0;
+#pragma unroll
+  for (int i = 0; i < kSbMaxHid; ++i) {
+    oW[i] = off;
+    ldw[i] = kWL ? (win[i] | 1) : win[i];
+    if (kWL && i < nh) off += a.rw[i] * (ldw[i] + 1);
+  }
+  const int oH = off;
+  if (kWL) {
+    off += KL;
+    // every parameter load of a thread in flight at once (up to kStageW slots of each W), then the padded stores
+    constexpr int kStageW = 16;
+    float vw[kSbMaxHid][kStageW], vb[kSbMaxHid];
+#pragma unroll
+    for (int i = 0; i < kSbMaxHid; ++i) {
+      if (i < nh) {
+        const int n = win[i] * a.rw[i], N = a.rw[i];
+#pragma unroll
+        for (int j = 0; j < kStageW; ++j) vw[i][j] = a.row_w[i][tid + j * kSbThreads < n ? tid + j * kSbThreads : n - 1];
+        vb[i] = a.row_b[i][tid < N ? tid : N - 1];
+      }
+    }
+    const float vh = a.head_w[tid < KL ? tid : KL - 1];
+#pragma unroll
+    for (int i = 0; i < kSbMaxHid; ++i) {
+      if (i < nh) {
+        const int K = win[i], N = a.rw[i], n = K * N;
+        const FastDiv fk = fast_div(K);
+#pragma unroll
+        for (int j = 0; j < kStageW; ++j) {
+          const int idx = tid + j * kSbThreads;
+          const int q = fdq(fk, idx);
+          if (idx < n) sm[oW[i] + q * ldw[i] + idx - q * K] = vw[i][j];
+        }
+        for (int idx = tid + kStageW * kSbThreads; idx < n; idx += kSbThreads) {   // (wider layers than cfg1's)
+          const int q = idx / K;
+          sm[oW[i] + q * ldw[i] + idx - q * K] = a.row_w[i][idx];
+        }
+        for (int o = tid; o < N; o += kSbThreads) sm[oW[i] + N * ldw[i] + o] = o == tid ? vb[i] : a.row_b[i][o];
+      }
+    }
+    for (int k = tid; k < KL; k += kSbThreads) sm[oH + k] = k == tid ? vh : a.head_w[k];
+  }
+  const float* hw = kWL ? (const float*)(sm + oH) : a.head_w;
+  int oZ[kSbMaxHid], oY[kSbMaxHid];
+  float* in0 = sm + off;
+  off += R * w0;
+#pragma unroll
+  for (int i = 0; i < kSbMaxHid; ++i) {
+    oZ[i] = oY[i] = off;
+    if (i < nh) {
+      oY[i] = off + R * a.rw[i];
+      off += 2 * R * a.rw[i];
     }
   }
-  float* in0 = p;
-  float* zs[kSbMaxHid];
-  float* ys[kSbMaxHid];
-  p = in0 + R * w0;
-  for (int i = 0; i < a.nhid; ++i) {
-    zs[i] = p;
-    ys[i] = p + R * a.rw[i];
-    p += 2 * R * a.rw[i];
-  }
-  float* gb0 = p;
-  float* gb1 = p + R * maxw;
+  float* gb0 = sm + off;
+  float* gb1 = gb0 + R * maxw;
   float* outv = gb1 + R * maxw;   // [R]
+#define RO_W(i) (kWL ? (const float*)(sm + oW[i]) : a.row_w[i])
+#define RO_B(i) (kWL ? (const float*)(sm + oW[i] + a.rw[i] * ldw[i]) : a.row_b[i])
   const float* xp = a.act + a.act_off[a.L - 1][0];
-  // tiles in a grid-stride loop: the weights are staged once per workgroup
-  const int ntile = (m + R - 1) / R;
+  const float slope = a.ro_slope[0];
+  const float head_b = a.head_b[0];
   for (int tile = blockIdx.x; tile < ntile; tile += gridDim.x) {
     const int r0 = tile * R;
     const int nr = m - r0 < R ? m - r0 : R;
     __syncthreads();   // the staged weights / the previous tile's LDS reads
+    SB_STAMP(1);
     for (int idx = tid; idx < nr * w0; idx += kSbThreads) {
       const int rr = idx / w0, k = idx % w0;
       const int64_t row = r0 + rr;
@@ -280,42 +491,71 @@ __global__ __launch_bounds__(kSbThreads) void k_sb_readout(SbArgs a) {
       a.ro_in[0][(int64_t)r0 * w0 + idx] = v;
     }
     __syncthreads();
-    const float slope = a.ro_slope[0];
-    for (int i = 0; i < a.nhid; ++i) {
-      const float* in = i == 0 ? in0 : ys[i - 1];
-      const int K = win[i], N = a.rw[i], lw = ldw[i];
-      for (int idx = tid; idx < nr * N; idx += kSbThreads) {
-        const int rr = idx / N, o = idx % N;
-        const float* wr = W[i] + (int64_t)o * lw;
-        float z = 0.0f;
-        for (int k = 0; k < K; ++k) z = fmaf(in[rr * K + k], wr[k], z);
-        z = __fadd_rn(z, a.row_b[i][o]);
-        zs[i][rr * N + o] = z;
-        const float yv = z > 0.0f ? z : __fmul_rn(slope, z);
-        ys[i][rr * N + o] = yv;
-        a.ro_in[i + 1][(int64_t)r0 * N + idx] = yv;
+    SB_STAMP(2);
+#pragma unroll
+    for (int i = 0; i < kSbMaxHid; ++i) {
+      if (i < nh) {
+        const float* in = i == 0 ? in0 : sm + oY[i > 0 ? i - 1 : 0];
+        const int K = win[i], N = a.rw[i];
+        auto epi = [&](int q, int o, float z) {
+          z = __fadd_rn(z, RO_B(i)[o]);
+          sm[oZ[i] + q] = z;
+          const float yv = z > 0.0f ? z : __fmul_rn(slope, z);
+          sm[oY[i] + q] = yv;
+          a.ro_in[i + 1][(int64_t)r0 * N + q] = yv;
+        };
+        if (nr * N >= 2 * kSbThreads) {   // >= 2 rows per thread: up to 4 rows share each W load
+          const int CT = N < kSbThreads ? N : kSbThreads, RG = kSbThreads / CT;
+          for (int c0 = 0; c0 < N; c0 += CT) {
+            const int o = c0 + tid % CT;
+            if (tid < RG * CT && o < N) {
+              for (int rb = tid / CT; rb < nr; rb += 4 * RG) {
+                const int nrow = (nr - rb + RG - 1) / RG < 4 ? (nr - rb + RG - 1) / RG : 4;
+                float acc[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+                dot_rows4(in + rb * K, RG * K, RO_W(i) + o * ldw[i], 1, K, nrow, acc);
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                  if (j < nrow) epi((rb + j * RG) * N + o, o, acc[j]);
+              }
+            }
+          }
+        } else {
+          const int S = split_of(nr * N, K);
+          for (int idx = tid; idx < nr * N * S; idx += kSbThreads) {
+            const int q = idx / S, s = idx % S;
+            const int rr = q / N, o = q % N;
+            float z = dot_chain(in + rr * K + s, S, RO_W(i) + o * ldw[i] + s, S, (K - s + S - 1) / S, 0.0f);
+            z = group_sum(z, S);
+            if (s == 0) epi(q, o, z);
+          }
+        }
+        __syncthreads();
+        SB_STAMP(3 + i);
       }
-      __syncthreads();
     }
-    const int KL = win[a.nhid];
-    const float* yl = ys[a.nhid - 1];
-    // head + loss numerator + seed, one thread per row
-    float lp = 0.0f;
-    if (tid < nr) {
-      float o = 0.0f;
-      for (int k = 0; k < KL; ++k) o = fmaf(yl[tid * KL + k], a.head_w[k], o);
-      o = __fadd_rn(o, a.head_b[0]);
-      const float yv = a.y[r0 + tid];
-      const float u = __fdiv_rn(__fsub_rn(o, yv), yv);
-      lp = fabsf(u);
-      const float sg = u > 0.0f ? 1.0f : (u < 0.0f ? -1.0f : 0.0f);
-      const float go = __fdiv_rn(sg, yv);   // d |u| / d out
-      outv[tid] = go;
-      a.ro_gz[a.nhid][r0 + tid] = go;
+    const float* yl = sm + (nh == 1 ? oY[0] : (nh == 2 ? oY[1] : oY[2]));
+    // head + loss numerator + seed, split_of() lanes per row
+    {
+      const int S = split_of(nr, KL);
+      for (int idx = tid; idx < nr * S; idx += kSbThreads) {
+        const int rr = idx / S, s = idx % S;
+        float o = dot_chain(yl + rr * KL + s, S, hw + s, S, (KL - s + S - 1) / S, 0.0f);
+        o = group_sum(o, S);
+        if (s == 0) {
+          o = __fadd_rn(o, head_b);
+          const float yv = a.y[r0 + rr];
+          const float u = __fdiv_rn(__fsub_rn(o, yv), yv);
+          red[rr] = fabsf(u);
+          const float sg = u > 0.0f ? 1.0f : (u < 0.0f ? -1.0f : 0.0f);
+          const float go = __fdiv_rn(sg, yv);   // d |u| / d out
+          outv[rr] = go;
+          a.ro_gz[nh][r0 + rr] = go;
+        }
+      }
     }
-    // fixed-order tile sum of |u| (rows in order)
-    red[tid] = tid < nr ? lp : 0.0f;
     __syncthreads();
+    SB_STAMP(6);
+    // fixed-order tile sum of |u| (rows in order)
     if (tid == 0) {
       float s = 0.0f;
       for (int rr = 0; rr < nr; ++rr) s = __fadd_rn(s, red[rr]);
@@ -323,58 +563,147 @@ __global__ __launch_bounds__(kSbThreads) void k_sb_readout(SbArgs a) {
     }
     for (int idx = tid; idx < nr * KL; idx += kSbThreads) {
       const int rr = idx / KL, k = idx % KL;
-      gb0[rr * KL + k] = __fmul_rn(outv[rr], a.head_w[k]);
+      gb0[rr * KL + k] = __fmul_rn(outv[rr], hw[k]);
     }
     __syncthreads();
+    SB_STAMP(7);
     float slope_part = 0.0f;   // this thread's share of the shared slope's gradient (fixed assignment)
     float* g_y = gb0;
     float* g_next = gb1;
-    for (int i = a.nhid - 1; i >= 0; --i) {
-      const int K = win[i], N = a.rw[i], lw = ldw[i];
-      // g_z (in place over g_y) and the slope partial
-      for (int idx = tid; idx < nr * N; idx += kSbThreads) {
-        const float z = zs[i][idx];
-        const float g = g_y[idx];
-        if (z <= 0.0f) slope_part = fmaf(g, z, slope_part);
-        const float gz = z > 0.0f ? g : __fmul_rn(slope, g);
-        g_y[idx] = gz;
-        a.ro_gz[i][(int64_t)r0 * N + idx] = gz;
+#pragma unroll
+    for (int i = kSbMaxHid - 1; i >= 0; --i) {
+      if (i < nh) {
+        const int K = win[i], N = a.rw[i];
+        // g_z (in place over g_y) and the slope partial
+        for (int idx = tid; idx < nr * N; idx += kSbThreads) {
+          const float z = sm[oZ[i] + idx];
+          const float g = g_y[idx];
+          if (z <= 0.0f) slope_part = fmaf(g, z, slope_part);
+          const float gz = z > 0.0f ? g : __fmul_rn(slope, g);
+          g_y[idx] = gz;
+          a.ro_gz[i][(int64_t)r0 * N + idx] = gz;
+        }
+        __syncthreads();
+        SB_STAMP(8 + 2 * i);
+        // g_in[k] = sum_o g_z[o] W[o][k] (the first layer: only the path embeddings' H columns have a gradient)
+        const int KG = i == 0 ? H : K;
+        if (nr * KG >= 2 * kSbThreads) {   // >= 2 rows per thread: up to 4 rows share each W load
+          const int CT = KG < kSbThreads ? KG : kSbThreads, RG = kSbThreads / CT;
+          for (int c0 = 0; c0 < KG; c0 += CT) {
+            const int k = c0 + tid % CT;
+            if (tid < RG * CT && k < KG) {
+              for (int rb = tid / CT; rb < nr; rb += 4 * RG) {
+                const int nrow = (nr - rb + RG - 1) / RG < 4 ? (nr - rb + RG - 1) / RG : 4;
+                float acc[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+                dot_rows4(g_y + rb * N, RG * N, RO_W(i) + k, ldw[i], N, nrow, acc);
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                  if (j < nrow) g_next[(rb + j * RG) * KG + k] = acc[j];
+              }
+            }
+          }
+        } else {
+          const int S = split_of(nr * KG, N);
+          for (int idx = tid; idx < nr * KG * S; idx += kSbThreads) {
+            const int q = idx / S, s = idx % S;
+            const int rr = q / KG, k = q % KG;
+            float v = dot_chain(g_y + rr * N + s, S, RO_W(i) + s * ldw[i] + k, S * ldw[i], (N - s + S - 1) / S, 0.0f);
+            v = group_sum(v, S);
+            if (s == 0) g_next[q] = v;
+          }
+        }
+        __syncthreads();
+        SB_STAMP(9 + 2 * i);
+        float* t = g_y;
+        g_y = g_next;
+        g_next = t;
       }
-      __syncthreads();
-      // g_in[k] = sum_o g_z[o] W[o][k] (the first layer: only the path embeddings' H columns have a gradient)
-      const int KG = i == 0 ? H : K;
-      for (int idx = tid; idx < nr * KG; idx += kSbThreads) {
-        const int rr = idx / KG, k = idx % KG;
-        float s = 0.0f;
-        for (int o = 0; o < N; ++o) s = fmaf(g_y[rr * N + o], W[i][(int64_t)o * lw + k], s);
-        g_next[rr * KG + k] = s;
-      }
-      __syncthreads();
-      float* t = g_y;
-      g_y = g_next;
-      g_next = t;
     }
     const float sp = block_sum(slope_part, red);
+    SB_STAMP(12);
     if (tid == 0) a.slope_part[tile] = sp;
     // the path embeddings' gradient for the GIN backward
     float* gpath = a.gA + a.g_off[0];
     for (int idx = tid; idx < nr * H; idx += kSbThreads) gpath[(int64_t)r0 * H + idx] = g_y[idx];
+    SB_STAMP(13);
   }
 }
+#undef RO_W
+#undef RO_B
 
-// the readout blocks of k_sb_bwd_w: over row chunk p of the m valid path rows, one group of kRoJ x kSbThreads of
-// layer i's (i = nhid: the head's) partial weight / bias gradients, g_W[o][k] = sum_rows g_z[o] in[k],
-// g_b[o] = sum_rows g_z[o], the chunk's rows in order (staged kRoSub rows at a time).  Block y-index u (after the
-// relations' kRel) -> (layer, group): the layers' groups in order.
+// the readout blocks of k_sb_bwd_w: over row chunk p of the m valid path rows, one group of layer i's (i = nhid: the
+// head's) partial weight / bias gradients, g_W[o][k] = sum_rows g_z[o] in[k], g_b[o] = sum_rows g_z[o] (the bias as
+// an input column of ones: fmaf(g, 1, v) is the add), the chunk's rows in order (staged kRoSub rows at a time).
+// A group is ro_to(N) x (kSbThreads / ro_to(N)) threads, each an MO x MK register tile of (o, k) entries strided
+// by the thread grid (lanes read consecutive o: conflict-free; 6 LDS reads per 8 products, not 16).  Block y-index
+// u (after the relations' kRel) -> (layer, group): the layers' groups in order.
 constexpr int kRoSub = 16;
-constexpr int kRoJ = 8;
+constexpr int kRoMO = 4, kRoMK = 2;
+constexpr int kSbStage = kRoSub * (2 * kSbMaxW + 1);   // k_sb_bwd_w's staging floats
 
+__host__ __device__ __forceinline__ int ro_to(int N) {
+  int t = 1;
+  while (t < kSbThreads && kRoMO * t < N) t *= 2;
+  return t;
+}
+__host__ __device__ __forceinline__ int ro_groups_nk(int N, int K) {
+  const int tk = kSbThreads / ro_to(N);
+  return (K + 1 + kRoMK * tk - 1) / (kRoMK * tk);
+}
 __device__ __forceinline__ int ro_in_width(const SbArgs& a, int i) {
   return i == 0 ? a.H + (a.concat_path ? a.fdim[0] : 0) : a.rw[i - 1];
 }
 __device__ __forceinline__ int ro_groups(const SbArgs& a, int i) {
-  const int N = i < a.nhid ? a.rw[i] : 1;
-  return (N * (ro_in_width(a, i) + 1) + kRoJ * kSbThreads - 1) / (kRoJ * kSbThreads);
+  return ro_groups_nk(i < a.nhid ? a.rw[i] : 1, ro_in_width(a, i));
+}
+
+// one thread's register tile of a weight-gradient group: entries (oj[j], kj[jk]) of g_W's [N][K + 1] (column K: the
+// bias), strided by the group's TO x TK thread grid; the indices are clamped (read, never stored) past N / K + 1
+struct WgTile {
+  int to, tk, TO, TK, kc0;
+  int oj[kRoMO], kj[kRoMK];
+  float acc[kRoMO][kRoMK];
+};
+__device__ __forceinline__ void wg_setup(WgTile& t, int N, int K1, int u) {
+  t.TO = ro_to(N);
+  t.TK = kSbThreads / t.TO;
+  t.to = threadIdx.x % t.TO;
+  t.tk = threadIdx.x / t.TO;
+  t.kc0 = u * kRoMK * t.TK;
+#pragma unroll
+  for (int j = 0; j < kRoMO; ++j) t.oj[j] = t.to + t.TO * j < N ? t.to + t.TO * j : N - 1;
+#pragma unroll
+  for (int j = 0; j < kRoMK; ++j) t.kj[j] = t.kc0 + t.tk + t.TK * j < K1 ? t.kc0 + t.tk + t.TK * j : K1 - 1;
+#pragma unroll
+  for (int j = 0; j < kRoMO; ++j)
+#pragma unroll
+    for (int jk = 0; jk < kRoMK; ++jk) t.acc[j][jk] = 0.0f;
+}
+// acc += sum over the nr staged rows (in order) of s_g[rr][o] s_in[rr][k] (s_g [nr][N], s_in [nr][K1], LDS)
+__device__ __forceinline__ void wg_accum(WgTile& t, const float* s_g, const float* s_in, int nr, int N, int K1) {
+#pragma unroll 4
+  for (int rr = 0; rr < nr; ++rr) {
+    float g[kRoMO], x[kRoMK];
+#pragma unroll
+    for (int j = 0; j < kRoMO; ++j) g[j] = s_g[rr * N + t.oj[j]];
+#pragma unroll
+    for (int j = 0; j < kRoMK; ++j) x[j] = s_in[rr * K1 + t.kj[j]];
+#pragma unroll
+    for (int j = 0; j < kRoMO; ++j)
+#pragma unroll
+      for (int jk = 0; jk < kRoMK; ++jk) t.acc[j][jk] = fmaf(g[j], x[jk], t.acc[j][jk]);
+  }
+}
+// the tile's entries into part (W [N][K] row-major, then b [N])
+__device__ __forceinline__ void wg_store(const WgTile& t, float* part, int N, int K) {
+#pragma unroll
+  for (int j = 0; j < kRoMO; ++j) {
+#pragma unroll
+    for (int jk = 0; jk < kRoMK; ++jk) {
+      const int o = t.to + t.TO * j, k = t.kc0 + t.tk + t.TK * jk;
+      if (o < N && k <= K) part[k < K ? (int64_t)o * K + k : (int64_t)N * K + o] = t.acc[j][jk];
+    }
+  }
 }
 
 __device__ void ro_weight_part(const SbArgs& a, int p, int u, float* s_in, float* s_g) {
@@ -384,49 +713,23 @@ __device__ void ro_weight_part(const SbArgs& a, int p, int u, float* s_in, float
   const int m = a.m_valid[0];
   const int ch = (m + a.n_parts - 1) / a.n_parts;
   const int i0 = p * ch < m ? p * ch : m, i1 = (p + 1) * ch < m ? (p + 1) * ch : m;
-  const int K = ro_in_width(a, i);
+  const int K = ro_in_width(a, i), K1 = K + 1;
   const int N = i < a.nhid ? a.rw[i] : 1;
-  const int E = N * (K + 1);
   const float* in = a.ro_in[i];
   const float* gz = a.ro_gz[i];
-  float* part = a.part_ro + (int64_t)p * a.p_ro - a.p_gin;   // indexed by the flat readout offsets
-  const int64_t wo = i < a.nhid ? a.ro_goff[i] : a.head_goff;
-  constexpr int J = kRoJ;
-  {
-    const int q0 = u * J * kSbThreads;
-    float acc[J];
-#pragma unroll
-    for (int j = 0; j < J; ++j) acc[j] = 0.0f;
-    for (int rb = i0; rb < i1; rb += kRoSub) {
-      const int nr = i1 - rb < kRoSub ? i1 - rb : kRoSub;
-      __syncthreads();
-      for (int idx = tid; idx < nr * K; idx += kSbThreads) s_in[idx] = in[(int64_t)rb * K + idx];
-      for (int idx = tid; idx < nr * N; idx += kSbThreads) s_g[idx] = gz[(int64_t)rb * N + idx];
-      __syncthreads();
-#pragma unroll
-      for (int j = 0; j < J; ++j) {
-        const int q = q0 + j * kSbThreads + tid;
-        if (q < E) {
-          const int o = q / (K + 1), k = q % (K + 1);
-          float v = acc[j];
-          if (k < K) {
-            for (int rr = 0; rr < nr; ++rr) v = fmaf(s_g[rr * N + o], s_in[rr * K + k], v);
-          } else {
-            for (int rr = 0; rr < nr; ++rr) v = __fadd_rn(v, s_g[rr * N + o]);
-          }
-          acc[j] = v;
-        }
-      }
-    }
-#pragma unroll
-    for (int j = 0; j < J; ++j) {
-      const int q = q0 + j * kSbThreads + tid;
-      if (q < E) {
-        const int o = q / (K + 1), k = q % (K + 1);
-        part[wo + (k < K ? (int64_t)o * K + k : (int64_t)N * K + o)] = acc[j];
-      }
-    }
+  // indexed by the flat readout offsets
+  float* part = a.part_ro + (int64_t)p * a.p_ro - a.p_gin + (i < a.nhid ? a.ro_goff[i] : a.head_goff);
+  WgTile t;
+  wg_setup(t, N, K1, u);
+  for (int rb = i0; rb < i1; rb += kRoSub) {
+    const int nr = i1 - rb < kRoSub ? i1 - rb : kRoSub;
+    __syncthreads();
+    stage_ones(s_in, in + (int64_t)rb * K, nr, K);
+    copy_flat<8>(s_g, gz + (int64_t)rb * N, nr * N);
+    __syncthreads();
+    wg_accum(t, s_g, s_in, nr, N, K1);
   }
+  wg_store(t, part, N, K);
 }
 
 // layer l's output gradient of type d (gcur: written by the readout for path rows, by k_sb_bwd_in of layer l + 1
@@ -435,14 +738,17 @@ __device__ __forceinline__ float gout(const SbArgs& a, const float* gcur, int l,
   return (l == a.L - 1 && d != 0) ? 0.0f : gcur[a.g_off[d] + q];
 }
 
-// one row chunk's partial W / bias / slope / eps gradients of one relation (grid = n_parts x relations, plus the
-// readout layers' blocks in the last layer's launch); rows of chunk p: [p c, (p + 1) c), c = ceil(rows / n_parts)
-__global__ __launch_bounds__(kSbThreads) void k_sb_bwd_w(SbArgs a, int l, const float* gcur) {
+// one row chunk's partial W / bias / slope / eps gradients of one relation (grid = n_parts x relations, plus half
+// the readout layers' blocks in the last layer's launch and half in the first's); rows of chunk p: [p c, (p + 1) c),
+// c = ceil(rows / n_parts)
+__global__ __launch_bounds__(kSbThreads, 4) void k_sb_bwd_w(SbArgs a, int l, const float* gcur, int ro_first) {
   __shared__ float red[kSbThreads];
-  __shared__ float stage[2 * kRoSub * kSbMaxW];
+  __shared__ float stage[kSbStage];
   const int p = blockIdx.x, r = blockIdx.y;
-  if (r >= kRel) {   // the last layer's launch carries the readout's blocks (grid.y = kRel + their groups)
-    ro_weight_part(a, p, r - kRel, stage, stage + kRoSub * kSbMaxW);
+  SB_STAMP_W(l & 1, 0);
+  if (r >= kRel) {   // the readout's blocks: groups ro_first, ... (grid.y = kRel + their count)
+    ro_weight_part(a, p, r - kRel + ro_first, stage, stage + kRoSub * (kSbMaxW + 1));
+    SB_STAMP_W(l & 1, 1);
     return;
   }
   const int s = kRelSrc[r], d = kRelDst[r];
@@ -453,53 +759,59 @@ __global__ __launch_bounds__(kSbThreads) void k_sb_bwd_w(SbArgs a, int l, const 
   const int i0 = p * ch < rows ? p * ch : rows, i1 = (p + 1) * ch < rows ? (p + 1) * ch : rows;
   const SbConv& cv = a.conv[l][r];
   float* part = a.part_gin + (int64_t)p * a.p_gin + cv.goff;
-  float* gz = a.gz + a.gz_off[r];
   const float* comb = a.comb + a.comb_off[l][r];
   const float* zb = a.zb + a.zb_off[l][r];
   float* gc = a.gc + a.gc_off[r];
-  // the chunk's rows first: g_z = PReLU'(z) g_y, then g_comb = g_z W (row-local; k_sb_bwd_in reads every row's
-  // g_comb after this launch)
-  {
-    const float slope = cv.slope[0];
-    for (int q = tid; q < (i1 - i0) * H; q += kSbThreads) {
-      const int64_t qq = (int64_t)i0 * H + q;
-      const float z = zb[qq], g = gout(a, gcur, l, d, qq);
-      gz[qq] = z > 0.0f ? g : __fmul_rn(slope, g);
-    }
-    __syncthreads();
-    for (int q = tid; q < (i1 - i0) * K; q += kSbThreads) {
-      const int i = i0 + q / K, k = q % K;
-      const float* gzr = gz + (int64_t)i * H;
-      float v = 0.0f;
-      for (int h = 0; h < H; ++h) v = fmaf(gzr[h], cv.w[(int64_t)h * K + k], v);
-      gc[(int64_t)i * a.kmax + k] = v;
-    }
-    __syncthreads();
-  }
-  // g_W[h][k] = sum_i g_z[i][h] comb[i][k]; g_b[h] = sum_i g_z[i][h] (the chunk's rows in order)
-  for (int q = tid; q < H * (K + 1); q += kSbThreads) {
-    const int h = q / (K + 1), k = q % (K + 1);
-    float v = 0.0f;
-    for (int i = i0; i < i1; ++i) {
-      const float g = gz[(int64_t)i * H + h];
-      v = k < K ? fmaf(g, comb[(int64_t)i * K + k], v) : __fadd_rn(v, g);
-    }
-    part[k < K ? (int64_t)h * K + k : (int64_t)H * K + h] = v;
-  }
-  // the slope (sum over z <= 0 of g_y z) and eps (g_comb over the self columns times x_dst) partials
+  const float slope = cv.slope[0];
   const int fs = l == 0 ? a.fdim[s] : 0;
+  const int K1 = K + 1;
+  // the chunk's rows RS at a time in LDS (all of them at cfg1 sizes): g_z = PReLU'(z) g_y into s_g, comb with a
+  // column of ones into s_in; then g_comb = g_z W (row-local; k_sb_bwd_in reads every row's g_comb after this launch)
+  // with the eps partial (g_comb over the self columns times x_dst), and the register-tiled W / bias partials
+  // (wg_accum, the rows in order).  The slope partial: sum over z <= 0 of g_y z.  A group beyond the first (H (K + 1)
+  // above kRoMO x kRoMK x kSbThreads entries) stages the rows again.
+  // W [H][K] in LDS too when small (the g_comb dots read a column of it per output)
+  const int wsz = H * K <= 2048 ? H * K : 0;
+  const int rcap = (kSbStage - wsz) / (H + K1);
+  const int RS = (i1 - i0) < rcap ? (i1 - i0 > 0 ? i1 - i0 : 1) : rcap;
+  float* s_w = stage;
+  float* s_g = stage + wsz;
+  float* s_in = s_g + RS * H;
+  if (wsz) copy_flat<8>(s_w, cv.w, wsz);   // (visible after the first row block's barrier)
   float sp = 0.0f, epv = 0.0f;
-  for (int q = tid; q < (i1 - i0) * H; q += kSbThreads) {
-    const int64_t qq = (int64_t)i0 * H + q;
-    const float z = zb[qq];
-    if (z <= 0.0f) sp = fmaf(gout(a, gcur, l, d, qq), z, sp);
-  }
-  const int KS = K - fs;
-  for (int q = tid; q < (i1 - i0) * KS; q += kSbThreads) {
-    const int i = i0 + q / KS, k = fs + q % KS;
-    const float xv = l == 0 ? a.x[d][(int64_t)i * a.ldx[d] + a.cols[d][k - fs]]
-                            : a.act[a.act_off[l - 1][d] + (int64_t)i * H + k];
-    epv = fmaf(gc[(int64_t)i * a.kmax + k], xv, epv);
+  const int ng = ro_groups_nk(H, K);
+  for (int u = 0; u < ng; ++u) {
+    WgTile t;
+    wg_setup(t, H, K1, u);
+    for (int rb = i0; rb < i1; rb += RS) {
+      const int nr = i1 - rb < RS ? i1 - rb : RS;
+      __syncthreads();
+      stage_ones(s_in, comb + (int64_t)rb * K, nr, K);
+#pragma unroll 4
+      for (int idx = tid; idx < nr * H; idx += kSbThreads) {
+        const int64_t qq = (int64_t)rb * H + idx;
+        const float z = zb[qq], g = gout(a, gcur, l, d, qq);
+        s_g[idx] = z > 0.0f ? g : __fmul_rn(slope, g);
+        if (u == 0 && z <= 0.0f) sp = fmaf(g, z, sp);
+      }
+      __syncthreads();
+      if (u == 0) {
+        for (int idx = tid; idx < nr * K; idx += kSbThreads) {
+          const int rr = idx / K, k = idx % K;
+          const int i = rb + rr;
+          const float v = wsz ? dot_chain(s_g + rr * H, 1, s_w + k, K, H, 0.0f)
+                              : dot_chain(s_g + rr * H, 1, cv.w + k, K, H, 0.0f);
+          gc[(int64_t)i * a.kmax + k] = v;
+          if (k >= fs) {
+            const float xv = l == 0 ? a.x[d][(int64_t)i * a.ldx[d] + a.cols[d][k - fs]]
+                                    : a.act[a.act_off[l - 1][d] + (int64_t)i * H + k];
+            epv = fmaf(v, xv, epv);
+          }
+        }
+      }
+      wg_accum(t, s_g, s_in, nr, H, K1);
+    }
+    wg_store(t, part, H, K);
   }
   const float ssum = block_sum(sp, red);
   const float esum = block_sum(epv, red);
@@ -507,6 +819,7 @@ __global__ __launch_bounds__(kSbThreads) void k_sb_bwd_w(SbArgs a, int l, const 
     part[(int64_t)H * K + H] = ssum;
     part[(int64_t)H * K + H + 1] = esum;
   }
+  SB_STAMP_W(l & 1, 1);
 }
 
 // the gradient of layer l's input of type t (l > 0: layer l - 1's output): per relation in order, the self term
@@ -526,7 +839,7 @@ __global__ __launch_bounds__(kSbThreads) void k_sb_bwd_in(SbArgs a, int l, float
     if (kRelSrc[r] == t) {
       const int32_t* cp = a.cptr[r];
       const int32_t* cd = a.cdst[r];
-      for (int e = cp[u]; e < cp[u + 1]; ++e) v = __fadd_rn(v, gc[(int64_t)cd[e] * a.kmax + k]);
+      v = gather_chain(cd, cp[u], cp[u + 1], gc, a.kmax, k, v);
     }
   }
   gnxt[a.g_off[t] + (int64_t)u * H + k] = v;
@@ -578,10 +891,11 @@ __global__ __launch_bounds__(kSbThreads) void k_sb_final(SbArgs a) {
   for (int64_t e0 = (int64_t)blockIdx.x * 32; e0 < P; e0 += (int64_t)gridDim.x * 32) {
     const int64_t e = e0 + j;
     float v = 0.0f;
+    const int np = (a.n_parts - g + 7) / 8;   // parts g, g + 8, ...
     if (e < a.p_gin) {
-      for (int pp = g; pp < a.n_parts; pp += 8) v = __fadd_rn(v, a.part_gin[(int64_t)pp * a.p_gin + e]);
+      v = sum_chain(a.part_gin + (int64_t)g * a.p_gin + e, 8 * a.p_gin, np, v);
     } else if (e < P && e != a.ro_slope_goff) {
-      for (int pp = g; pp < a.n_parts; pp += 8) v = __fadd_rn(v, a.part_ro[(int64_t)pp * a.p_ro + (e - a.p_gin)]);
+      v = sum_chain(a.part_ro + (int64_t)g * a.p_ro + (e - a.p_gin), 8 * a.p_ro, np, v);
     }
     red[tid] = v;
     __syncthreads();
@@ -606,12 +920,12 @@ extern "C" int hgin_sb_readout_lds_bytes(int64_t H, int64_t f_path, int concat_p
   HGIN_ARG_CHECK(bytes && widths && nhid >= 1 && nhid <= kSbMaxHid && H >= 1, "hgin_sb_readout_lds_bytes: bad args");
   const int64_t w0 = H + (concat_path ? f_path : 0);
   int64_t maxw = w0, tot = w0;
-  int64_t wts = 0, win = w0;
+  int64_t wts = widths[nhid - 1], win = w0;   // the head's weights, then per layer W (odd row stride) and b
   for (int i = 0; i < nhid; ++i) {
     HGIN_ARG_CHECK(widths[i] >= 1 && widths[i] <= kSbMaxW, "hgin_sb_readout_lds_bytes: width %d", (int)widths[i]);
     tot += 2 * widths[i];
     maxw = widths[i] > maxw ? widths[i] : maxw;
-    wts += widths[i] * (win | 1);
+    wts += widths[i] * ((win | 1) + 1);
     win = widths[i];
   }
   HGIN_ARG_CHECK(w0 <= kSbMaxW, "hgin_sb_readout_lds_bytes: input width %lld", (long long)w0);
@@ -638,13 +952,16 @@ extern "C" int hgin_sb_step(const void* args, size_t args_bytes, size_t readout_
   HGIN_ARG_CHECK(hipGetDevice(&dev) == hipSuccess && dev >= 0 && dev < 64, "hgin_sb_step: device id");
   static int dyn_max_dev[64];   // 0: not raised yet on that device; -1: failed
   if (dyn_max_dev[dev] == 0) {
-    hipFuncAttributes fa;
-    int m = -1;
-    if (hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(k_sb_readout)) == hipSuccess) {
-      m = 160 * 1024 - (int)fa.sharedSizeBytes;
-      if (hipFuncSetAttribute(reinterpret_cast<const void*>(k_sb_readout), hipFuncAttributeMaxDynamicSharedMemorySize,
-                              m) != hipSuccess)
-        m = -1;
+    int m = 160 * 1024;   // the smaller of the two variants' limits (-1 if either failed)
+    for (const void* fn : {reinterpret_cast<const void*>(k_sb_readout<true>),
+                           reinterpret_cast<const void*>(k_sb_readout<false>)}) {
+      hipFuncAttributes fa;
+      int mf = -1;
+      if (hipFuncGetAttributes(&fa, fn) == hipSuccess) {
+        mf = 160 * 1024 - (int)fa.sharedSizeBytes;
+        if (hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, mf) != hipSuccess) mf = -1;
+      }
+      m = mf < m ? mf : m;
     }
     dyn_max_dev[dev] = m;
   }
@@ -667,18 +984,25 @@ extern "C" int hgin_sb_step(const void* args, size_t args_bytes, size_t readout_
   int ro_blocks = 0;   // the readout weight-gradient blocks' groups (ro_groups, on the host)
   for (int i = 0, win = a.H + (a.concat_path ? a.fdim[0] : 0); i <= a.nhid; ++i) {
     const int N = i < a.nhid ? a.rw[i] : 1;
-    ro_blocks += (N * (win + 1) + kRoJ * kSbThreads - 1) / (kRoJ * kSbThreads);
+    ro_blocks += ro_groups_nk(N, win);
     if (i < a.nhid) win = a.rw[i];
   }
   const unsigned fwd_blocks = (unsigned)ceil_div((int64_t)capt_max, (int64_t)kSbFwdRows);
   for (int l = 0; l < a.L; ++l) k_sb_fwd<<<dim3(fwd_blocks, 3), kSbThreads, 0, s>>>(a, l);
   // one tile per workgroup (a grid of 512 looping over the tiles, staging the weights once each: 52.9 vs 35 us per
   // batch, profiles/r04/gpu_r — the tiles' serial layer chains want the parallelism, not fewer weight stagings)
-  k_sb_readout<<<a.n_tiles, kSbThreads, readout_lds, s>>>(a);
+  if (a.ro_wlds)
+    k_sb_readout<true><<<a.n_tiles, kSbThreads, readout_lds, s>>>(a);
+  else
+    k_sb_readout<false><<<a.n_tiles, kSbThreads, readout_lds, s>>>(a);
   float* gcur = a.gA;
   float* gnxt = a.gB;
+  // the readout's weight-gradient groups ride in the last layer's launch and (L > 1) the first layer's, half each,
+  // so that each launch's blocks are resident at once (4 per CU)
+  const int ro_hi = a.L > 1 ? (ro_blocks + 1) / 2 : ro_blocks;
   for (int l = a.L - 1; l >= 0; --l) {
-    k_sb_bwd_w<<<dim3(a.n_parts, l == a.L - 1 ? kRel + ro_blocks : kRel), kSbThreads, 0, s>>>(a, l, gcur);
+    const int ro_n = l == a.L - 1 ? ro_hi : (l == 0 ? ro_blocks - ro_hi : 0);
+    k_sb_bwd_w<<<dim3(a.n_parts, kRel + ro_n), kSbThreads, 0, s>>>(a, l, gcur, l == a.L - 1 ? 0 : ro_hi);
     if (l > 0) {
       k_sb_bwd_in<<<dim3(blocks((int64_t)capt_max * a.H), 3), kSbThreads, 0, s>>>(a, l, gnxt);
       float* tt = gcur;
@@ -693,6 +1017,17 @@ extern "C" int hgin_sb_step(const void* args, size_t args_bytes, size_t readout_
 }
 
 extern "C" size_t hgin_sb_args_size(void) { return sizeof(SbArgs); }
+
+#ifdef HGIN_SB_STAMPS
+extern "C" int hgin_sb_stamps_read(unsigned long long* out, int64_t n) {
+  HGIN_ARG_CHECK(out && n >= kStampRo + kStampW, "hgin_sb_stamps_read: need %d slots", kStampRo + kStampW);
+  void* dev = nullptr;   // read, then cleared for the next step
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_sb_stamps), sizeof(g_sb_stamps)) != hipSuccess ||
+      hipGetSymbolAddress(&dev, HIP_SYMBOL(g_sb_stamps)) != hipSuccess || hipMemset(dev, 0, sizeof(g_sb_stamps)) != hipSuccess)
+    return -1;
+  return HGIN_OK;
+}
+#endif
 
 // offsets of the SbArgs fields the host mirror is checked against (hgin/smallbatch.py): one per field group
 extern "C" int hgin_sb_args_offsets(int64_t* out, int64_t n) {

@@ -52,7 +52,7 @@ class _SbArgs(ctypes.Structure):   # field for field csrc/hgin_smallbatch.hip Sb
                 ("comb", _P), ("comb_off", (_I64 * REL) * MAX_L),
                 ("zb", _P), ("zb_off", (_I64 * REL) * MAX_L),
                 ("gA", _P), ("gB", _P), ("g_off", _I64 * 3),
-                ("gz", _P), ("gc", _P), ("gz_off", _I64 * REL), ("gc_off", _I64 * REL), ("kmax", _I32),
+                ("gc", _P), ("gc_off", _I64 * REL), ("kmax", _I32),
                 ("cap", _I32 * 3), ("part_gin", _P), ("n_parts", _I32), ("part_ro", _P), ("loss_part", _P),
                 ("slope_part", _P), ("n_tiles", _I32), ("ro_wlds", _I32),
                 ("ro_in", _P * (MAX_HID + 1)), ("ro_gz", _P * (MAX_HID + 1)),
@@ -274,11 +274,10 @@ class SmallBatchStep:
         for ti in range(3):
             a.g_off[ti] = o[ti]
         kmax = max(max(K0), H)
-        o, self.gz = blocks([cap[r[2]] * H for r in RELS])
         o2, self.gc = blocks([cap[r[2]] * kmax for r in RELS])
-        a.gz, a.gc, a.kmax = P(self.gz), P(self.gc), kmax
+        a.gc, a.kmax = P(self.gc), kmax
         for ri in range(REL):
-            a.gz_off[ri], a.gc_off[ri] = o[ri], o2[ri]
+            a.gc_off[ri] = o2[ri]
         for ti, t in enumerate(TYPES):
             a.cap[ti] = cap[t]
         a.n_parts = N_PARTS
