@@ -462,8 +462,11 @@ __global__ __launch_bounds__(256) void k_gat_attn_w(const int32_t* __restrict__ 
 // Backward, destination side.  Phase A (column lanes, CSR order, U rows in flight): g_alpha_k = <g_out[i, h, :],
 // x_s[j_k, h, :]> (each lane its 4 products, then the head's C / 4 lanes), S_h = sum_k alpha_k g_alpha_k; the head's
 // first lane stores g_alpha_k.  Phase B (the head's first lane, CSR order): g_pre_k = leaky'(pre_k) alpha_k
-// (g_alpha_k - S_h) over its own stores, g_a_d = sum_k g_pre_k; g_x_d = g_a_d att_dst on the column lanes.
-template <int G>
+// (g_alpha_k - S_h) over its own stores, g_a_d = sum_k g_pre_k; g_x_d = g_a_d att_dst on the column lanes.  The row's
+// first G edge sources come in one coalesced load and reach the lanes by ds_bpermute (k_gat_attn_w's scheme), so a
+// batch of U edges costs one dependent round trip (both phases run their loops on every lane of the group: the
+// shuffles need them).
+template <int G, int U>
 __global__ __launch_bounds__(256) void k_gat_bwd_dst_w(const int32_t* __restrict__ rowptr,
                                                        const int32_t* __restrict__ col, int64_t n_dst, int H, int C,
                                                        const float* __restrict__ xs, int64_t ldxs,
@@ -477,69 +480,72 @@ __global__ __launch_bounds__(256) void k_gat_bwd_dst_w(const int32_t* __restrict
   const int64_t i = ((int64_t)blockIdx.x * 256 + threadIdx.x) / G;
   if (i >= n_dst) return;
   const int rb = rowptr[i], re = rowptr[i + 1];
+  const int deg = re - rb;
+  const int cj = gl < deg ? col[rb + gl] : 0;   // the sources of edges 0 .. G - 1
+  auto src = [&](int k) -> int64_t {           // (every lane of the group runs the shuffle)
+    const int sh = __shfl(cj, k & (G - 1), G);
+    return k < G ? (int64_t)sh : (int64_t)col[rb + k];
+  };
   const int HC4 = H * C / 4;
   const bool lane_on = gl < HC4;
   const int hq = lane_on ? (4 * gl) / C : 0;
   const bool first = lane_on && (4 * gl) % C == 0;
   const float4 go = lane_on ? *reinterpret_cast<const float4*>(g_out + i * ldg + 4 * gl) : make_float4(0.f, 0.f, 0.f, 0.f);
   float S = 0.0f;
-  for (int k0 = rb; k0 < re; k0 += kGatU) {
-    const int nk = re - k0;
-    float av[kGatU];
-    float4 xv[kGatU];
+  for (int k0 = 0; k0 < deg; k0 += U) {
+    float av[U];
+    float4 xv[U];
 #pragma unroll
-    for (int u = 0; u < kGatU; ++u) {
+    for (int u = 0; u < U; ++u) {
+      const int64_t j = src(k0 + u < deg ? k0 + u : 0);
       av[u] = 0.0f;
       xv[u] = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (lane_on && u < nk) {
-        const int64_t j = col[k0 + u];
-        av[u] = alpha[(int64_t)(k0 + u) * H + hq];
+      if (lane_on && k0 + u < deg) {
+        av[u] = alpha[(int64_t)(rb + k0 + u) * H + hq];
         xv[u] = *reinterpret_cast<const float4*>(xs + j * ldxs + 4 * gl);
       }
     }
 #pragma unroll
-    for (int u = 0; u < kGatU; ++u) {
-      if (u < nk) {   // (uniform over the group: the shuffles below run on every lane)
+    for (int u = 0; u < U; ++u) {
+      if (k0 + u < deg) {   // (uniform over the group: the shuffles below run on every lane)
         float p = __fadd_rn(__fadd_rn(__fadd_rn(__fmul_rn(go.x, xv[u].x), __fmul_rn(go.y, xv[u].y)),
                                       __fmul_rn(go.z, xv[u].z)), __fmul_rn(go.w, xv[u].w));
         p = group_sum_pow2<G>(p, C / 4);
         S = __fadd_rn(S, __fmul_rn(av[u], p));
-        if (first) g_pre[(int64_t)(k0 + u) * H + hq] = p;   // g_alpha for now
+        if (first) g_pre[(int64_t)(rb + k0 + u) * H + hq] = p;   // g_alpha for now
       }
     }
   }
   float gsum = 0.0f;
-  if (first) {
-    const float adv = ad ? ad[i * H + hq] : 0.0f;
-    for (int k0 = rb; k0 < re; k0 += kGatU) {   // kGatU edges' operands loaded together
-      float al[kGatU], ga[kGatU], av[kGatU];
+  const float adv = first && ad ? ad[i * H + hq] : 0.0f;
+  for (int k0 = 0; k0 < deg; k0 += U) {   // U edges' operands loaded together
+    float al[U], ga[U], av[U];
 #pragma unroll
-      for (int u = 0; u < kGatU; ++u) {
-        const int k = k0 + u;
-        al[u] = ga[u] = av[u] = 0.0f;
-        if (k < re) {
-          const int64_t q = (int64_t)k * H + hq;
-          al[u] = alpha[q];
-          ga[u] = g_pre[q];
-          av[u] = as[(int64_t)col[k] * H + hq];
-        }
-      }
-#pragma unroll
-      for (int u = 0; u < kGatU; ++u) {
-        if (k0 + u < re) {
-          const float ge = __fmul_rn(al[u], __fsub_rn(ga[u], S));
-          const float pre = __fadd_rn(av[u], adv);
-          const float gp = pre > 0.0f ? ge : __fmul_rn(ge, slope);
-          g_pre[(int64_t)(k0 + u) * H + hq] = gp;
-          gsum = __fadd_rn(gsum, gp);
-        }
+    for (int u = 0; u < U; ++u) {
+      const int64_t j = src(k0 + u < deg ? k0 + u : 0);
+      al[u] = ga[u] = av[u] = 0.0f;
+      if (first && k0 + u < deg) {
+        const int64_t q = (int64_t)(rb + k0 + u) * H + hq;
+        al[u] = alpha[q];
+        ga[u] = g_pre[q];
+        av[u] = as[j * H + hq];
       }
     }
-    if (g_ad) g_ad[i * H + hq] = gsum;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (first && k0 + u < deg) {
+        const float ge = __fmul_rn(al[u], __fsub_rn(ga[u], S));
+        const float pre = __fadd_rn(av[u], adv);
+        const float gp = pre > 0.0f ? ge : __fmul_rn(ge, slope);
+        g_pre[(int64_t)(rb + k0 + u) * H + hq] = gp;
+        gsum = __fadd_rn(gsum, gp);
+      }
+    }
   }
+  if (first && g_ad) g_ad[i * H + hq] = gsum;
   if (g_xd) {
-    const int src = lane_on ? hq * (C / 4) : gl;
-    gsum = __shfl(gsum, src, G);
+    const int srcl = lane_on ? hq * (C / 4) : gl;
+    gsum = __shfl(gsum, srcl, G);
     if (lane_on) {
       const float4 at = *reinterpret_cast<const float4*>(att_dst + 4 * gl);
       *reinterpret_cast<float4*>(g_xd + i * ldgxd + 4 * gl) =
@@ -550,7 +556,8 @@ __global__ __launch_bounds__(256) void k_gat_bwd_dst_w(const int32_t* __restrict
 
 // Backward, source side, on the CSC (entries k: destination cdst[k], CSR position cpos[k]), in CSC order:
 // g_a_s[j, h] = sum_k g_pre (the head's first lane), g_x_s[j, cols] = sum_k alpha g_out[i_k, cols] + g_a_s att_src.
-template <int G>
+// The row's first G CSC entries (destination, position) come in one coalesced load each, as in k_gat_bwd_dst_w.
+template <int G, int U>
 __global__ __launch_bounds__(256) void k_gat_bwd_src_w(const int32_t* __restrict__ cptr, const int32_t* __restrict__ cdst,
                                                        const int32_t* __restrict__ cpos, int64_t n_src, int H, int C,
                                                        const float* __restrict__ g_out, int64_t ldg,
@@ -566,33 +573,35 @@ __global__ __launch_bounds__(256) void k_gat_bwd_src_w(const int32_t* __restrict
   const int hq = lane_on ? (4 * gl) / C : 0;
   const bool first = lane_on && (4 * gl) % C == 0;
   const int rb = cptr[j], re = cptr[j + 1];
+  const int deg = re - rb;
+  const int cd = gl < deg ? cdst[rb + gl] : 0, cp = gl < deg ? cpos[rb + gl] : 0;
   float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
   float gas = 0.0f;
-  if (lane_on) {
-    for (int k0 = rb; k0 < re; k0 += kGatU) {
-      const int nk = re - k0;
-      float av[kGatU], pv[kGatU];
-      float4 gv[kGatU];
+  for (int k0 = 0; k0 < deg; k0 += U) {
+    float av[U], pv[U];
+    float4 gv[U];
 #pragma unroll
-      for (int u = 0; u < kGatU; ++u) {
-        av[u] = pv[u] = 0.0f;
-        gv[u] = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (u < nk) {
-          const int64_t p = (int64_t)cpos[k0 + u] * H + hq;
-          av[u] = alpha[p];
-          if (first) pv[u] = g_pre[p];
-          gv[u] = *reinterpret_cast<const float4*>(g_out + (int64_t)cdst[k0 + u] * ldg + 4 * gl);
-        }
+    for (int u = 0; u < U; ++u) {
+      const int k = k0 + u < deg ? k0 + u : 0;
+      const int sd = __shfl(cd, k & (G - 1), G), sp = __shfl(cp, k & (G - 1), G);   // (every lane)
+      const int64_t d = k < G ? sd : cdst[rb + k];
+      const int64_t p = (int64_t)(k < G ? sp : cpos[rb + k]) * H + hq;
+      av[u] = pv[u] = 0.0f;
+      gv[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (lane_on && k0 + u < deg) {
+        av[u] = alpha[p];
+        if (first) pv[u] = g_pre[p];
+        gv[u] = *reinterpret_cast<const float4*>(g_out + d * ldg + 4 * gl);
       }
+    }
 #pragma unroll
-      for (int u = 0; u < kGatU; ++u) {
-        if (u < nk) {
-          gas = __fadd_rn(gas, pv[u]);
-          acc.x = __fadd_rn(acc.x, __fmul_rn(gv[u].x, av[u]));
-          acc.y = __fadd_rn(acc.y, __fmul_rn(gv[u].y, av[u]));
-          acc.z = __fadd_rn(acc.z, __fmul_rn(gv[u].z, av[u]));
-          acc.w = __fadd_rn(acc.w, __fmul_rn(gv[u].w, av[u]));
-        }
+    for (int u = 0; u < U; ++u) {
+      if (lane_on && k0 + u < deg) {
+        gas = __fadd_rn(gas, pv[u]);
+        acc.x = __fadd_rn(acc.x, __fmul_rn(gv[u].x, av[u]));
+        acc.y = __fadd_rn(acc.y, __fmul_rn(gv[u].y, av[u]));
+        acc.z = __fadd_rn(acc.z, __fmul_rn(gv[u].z, av[u]));
+        acc.w = __fadd_rn(acc.w, __fmul_rn(gv[u].w, av[u]));
       }
     }
   }
@@ -620,6 +629,18 @@ int gat_group(int64_t H, int64_t C) {
 
 inline bool al16(const void* p, int64_t ld) { return p == nullptr || (aligned16(p) && ld % 4 == 0); }
 
+// the backward kernels take U edges in flight per group: 4 (8 measured 2 % slower over fwd + bwd at a 30M-edge
+// relation, profiles/r05/gat_bwd/)
+#define HGIN_GAT_GU(G, U, KERN, ...)                                                                            \
+  switch (G) {                                                                                                \
+    case 1: KERN<1, U><<<(unsigned)ceil_div(rows, 256 / 1), 256, 0, s>>>(__VA_ARGS__); break;                  \
+    case 2: KERN<2, U><<<(unsigned)ceil_div(rows, 256 / 2), 256, 0, s>>>(__VA_ARGS__); break;                  \
+    case 4: KERN<4, U><<<(unsigned)ceil_div(rows, 256 / 4), 256, 0, s>>>(__VA_ARGS__); break;                  \
+    case 8: KERN<8, U><<<(unsigned)ceil_div(rows, 256 / 8), 256, 0, s>>>(__VA_ARGS__); break;                  \
+    case 16: KERN<16, U><<<(unsigned)ceil_div(rows, 256 / 16), 256, 0, s>>>(__VA_ARGS__); break;               \
+    case 32: KERN<32, U><<<(unsigned)ceil_div(rows, 256 / 32), 256, 0, s>>>(__VA_ARGS__); break;               \
+    default: KERN<64, U><<<(unsigned)ceil_div(rows, 256 / 64), 256, 0, s>>>(__VA_ARGS__); break;               \
+  }
 #define HGIN_GAT_G(G, KERN, ...)                                                                                \
   switch (G) {                                                                                                \
     case 1: KERN<1><<<(unsigned)ceil_div(rows, 256 / 1), 256, 0, s>>>(__VA_ARGS__); break;                     \
@@ -728,8 +749,8 @@ extern "C" int hgin_gat_bwd_dst_f32(const int32_t* rowptr, const int32_t* col, i
     HGIN_TRACE("k_gat_bwd_dst_w<%d>", G);
     const int64_t rows = n_dst;
     hipStream_t s = as_stream(stream);
-    HGIN_GAT_G(G, k_gat_bwd_dst_w, rowptr, col, n_dst, (int)H, (int)C, xs, ldxs, g_out, ldg, alpha, as, ad, slope,
-               att_dst, g_pre, g_ad, g_xd, ldgxd)
+    HGIN_GAT_GU(G, 4, k_gat_bwd_dst_w, rowptr, col, n_dst, (int)H, (int)C, xs, ldxs, g_out, ldg, alpha, as, ad,
+                  slope, att_dst, g_pre, g_ad, g_xd, ldgxd)
     return check_launch("hgin_gat_bwd_dst_f32");
   }
   HGIN_TRACE("k_gat_bwd_dst");
@@ -751,8 +772,8 @@ extern "C" int hgin_gat_bwd_src_f32(const int32_t* cptr, const int32_t* cdst, co
     HGIN_TRACE("k_gat_bwd_src_w<%d>", G);
     const int64_t rows = n_src;
     hipStream_t s = as_stream(stream);
-    HGIN_GAT_G(G, k_gat_bwd_src_w, cptr, cdst, cpos, n_src, (int)H, (int)C, g_out, ldg, alpha, g_pre, att_src, g_as,
-               g_xs, ldgxs)
+    HGIN_GAT_GU(G, 4, k_gat_bwd_src_w, cptr, cdst, cpos, n_src, (int)H, (int)C, g_out, ldg, alpha, g_pre, att_src,
+                  g_as, g_xs, ldgxs)
     return check_launch("hgin_gat_bwd_src_f32");
   }
   HGIN_TRACE("k_gat_bwd_src");

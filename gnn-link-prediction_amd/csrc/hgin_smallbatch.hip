@@ -246,6 +246,20 @@ __device__ __forceinline__ float gather_chain(const int32_t* col, int e0, int e1
   return acc;
 }
 
+// n contiguous floats from global memory into LDS, every load of a thread issued before its first store (one
+// memory round trip for up to J x kSbThreads floats)
+template <int J = 32>
+__device__ __forceinline__ void copy_flat(float* dst, const float* src, int n) {
+  for (int b = threadIdx.x; b < n; b += J * kSbThreads) {
+    float v[J];
+#pragma unroll
+    for (int j = 0; j < J; ++j) v[j] = src[b + j * kSbThreads < n ? b + j * kSbThreads : n - 1];
+#pragma unroll
+    for (int j = 0; j < J; ++j)
+      if (b + j * kSbThreads < n) dst[b + j * kSbThreads] = v[j];
+  }
+}
+
 // One layer's forward for kSbFwdRows rows of node type t (grid = row blocks x types): per relation into t (relation
 // order) comb_r = [aggregate | (1 + eps) x_dst] (concat, first layer) or aggregate + (1 + eps) x_dst (add), the
 // aggregate a sequential edge-order sum (models.py:210-215); then per row and output column the sum over those
@@ -253,8 +267,11 @@ __device__ __forceinline__ float gather_chain(const int32_t* col, int e0, int e1
 // relation for the backward.  comb_r also goes to HBM (the weight gradients read it).
 constexpr int kSbFwdRows = 32;
 
+constexpr int kSbFwdW = 1024;   // k_sb_fwd stages a relation's W [H][K] in LDS when it has at most this many entries
+
 __global__ __launch_bounds__(kSbThreads) void k_sb_fwd(SbArgs a, int l) {
   __shared__ float s_comb[2][kSbFwdRows * 128];   // <= 2 relations into a type, K <= kmax <= 128
+  __shared__ float s_w[2][kSbFwdW];
   const int t = blockIdx.y;
   const int tid = threadIdx.x;
   const int H = a.H;
@@ -263,6 +280,20 @@ __global__ __launch_bounds__(kSbThreads) void k_sb_fwd(SbArgs a, int l) {
   if (a.adam_step && l == 0 && blockIdx.x == 0 && t == 0 && tid == 0) a.adam_step[0] += 1.0f;   // read by k_sb_final
   if (r0 >= n) return;
   const int nr = n - r0 < kSbFwdRows ? n - r0 : kSbFwdRows;
+  // the relations' small weights into LDS first: their loads fly with the aggregate's gathers
+  int wl = 0;   // bit sl: relation slot sl's W is in s_w[sl]
+  {
+    int sl = 0;
+    for (int r = 0; r < kRel; ++r) {
+      if (kRelDst[r] != t) continue;
+      const int HK = H * kdim(a, l, r);
+      if (HK <= kSbFwdW) {
+        wl |= 1 << sl;
+        copy_flat<4>(s_w[sl], a.conv[l][r].w, HK);
+      }
+      ++sl;
+    }
+  }
   int slot = 0;
   for (int r = 0; r < kRel; ++r) {
     if (kRelDst[r] != t) continue;
@@ -306,9 +337,9 @@ __global__ __launch_bounds__(kSbThreads) void k_sb_fwd(SbArgs a, int l) {
       if (kRelDst[r] != t) continue;
       const int K = kdim(a, l, r);
       const SbConv& cv = a.conv[l][r];
-      const float* cr = s_comb[sl++] + ii * K;
-      const float* wr = cv.w + (int64_t)h * K;
-      float z = dot_chain(cr, 1, wr, 1, K, 0.0f);
+      const float* cr = s_comb[sl] + ii * K;
+      float z = (wl >> sl) & 1 ? dot_chain(cr, 1, s_w[sl] + h * K, 1, K, 0.0f) : dot_chain(cr, 1, cv.w + (int64_t)h * K, 1, K, 0.0f);
+      ++sl;
       z = __fadd_rn(z, cv.b[h]);
       a.zb[a.zb_off[l][r] + (int64_t)(r0 + ii) * H + h] = z;
       const float yv = z > 0.0f ? z : __fmul_rn(cv.slope[0], z);
@@ -316,20 +347,6 @@ __global__ __launch_bounds__(kSbThreads) void k_sb_fwd(SbArgs a, int l) {
       first = false;
     }
     a.act[a.act_off[l][t] + (int64_t)(r0 + ii) * H + h] = y;
-  }
-}
-
-// n contiguous floats from global memory into LDS, every load of a thread issued before its first store (one
-// memory round trip for up to J x kSbThreads floats)
-template <int J = 32>
-__device__ __forceinline__ void copy_flat(float* dst, const float* src, int n) {
-  for (int b = threadIdx.x; b < n; b += J * kSbThreads) {
-    float v[J];
-#pragma unroll
-    for (int j = 0; j < J; ++j) v[j] = src[b + j * kSbThreads < n ? b + j * kSbThreads : n - 1];
-#pragma unroll
-    for (int j = 0; j < J; ++j)
-      if (b + j * kSbThreads < n) dst[b + j * kSbThreads] = v[j];
   }
 }
 
