@@ -2014,16 +2014,6 @@ int try_ws_f32_comb(const float* a, int64_t lda, const float* b, int64_t ldb, fl
   return launch_ws32<256, 256, 4, true, false, false>(g, s, what, grid_out);
 }
 
-// K-tile depth of the bf16 NT kernel (HGIN_NT_BKH = 64 / 128).  128: twice the A bytes per prefetch (32 KB
-// per workgroup) at 2 workgroups / CU instead of 3 — more of the A stream in flight per CU, half the barriers.
-bool bf16_bk128(int64_t K, int64_t k1) {
-  static const int env = [] {
-    const char* v = getenv("HGIN_NT_BKH");
-    return v ? atoi(v) : 64;
-  }();
-  return env == 128 && K % 128 == 0 && k1 % 128 == 0;
-}
-
 template <int EPI, typename OutT>
 int launch_nt_bf16(const Src2h& a, const Src2h& b, int64_t M, int64_t N, int64_t K, const float* bias,
                    const float* prelu, const OutT* accum, OutT* z, OutT* y, int64_t ldc, hipStream_t s,
@@ -2040,7 +2030,6 @@ int launch_nt_bf16(const Src2h& a, const Src2h& b, int64_t M, int64_t N, int64_t
                        (accum == nullptr || aligned16(accum)) &&
                        (EPI != 4 || (aligned16(ce.xd) && ce.ldxd % 4 == 0 &&
                                      (ce.gd == nullptr || (aligned16(ce.gd) && ce.ldgd % 4 == 0))));
-  const bool deep = vec && bf16_bk128(K, a.k1);
 #define HGIN_NT_BF16(TNV, WNV)                                                                                \
   {                                                                                                          \
     constexpr int BM = (4 / WNV) * 64;                                                                       \
@@ -2049,10 +2038,7 @@ int launch_nt_bf16(const Src2h& a, const Src2h& b, int64_t M, int64_t N, int64_t
     const bool xcd = xcd_remap_enabled();                                                                    \
     dim3 grid((unsigned)(xcd ? round_up8(tiles) : tiles));                                                   \
     HGIN_TRACE("k_gemm_nt_bf16<EPI%d,%dx%d,N%lld,K%lld>", EPI, BM, BN, (long long)N, (long long)K);       \
-    if (deep)                                                                                                \
-      k_gemm_nt_bf16<EPI, true, TNV, WNV, OutT, 128><<<grid, 256, 0, s>>>(a, b, M, N, K, bias, prelu, accum, \
-                                                                          z, y, ldc, vec_out, tiles, xcd, ce); \
-    else if (vec)                                                                                            \
+    if (vec)                                                                                                 \
       k_gemm_nt_bf16<EPI, true, TNV, WNV, OutT><<<grid, 256, 0, s>>>(a, b, M, N, K, bias, prelu, accum, z, y, \
                                                                      ldc, vec_out, tiles, xcd, ce);          \
     else                                                                                                     \

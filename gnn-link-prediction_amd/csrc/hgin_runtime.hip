@@ -58,6 +58,27 @@ extern "C" int hgin_abi_version(void) { return HGIN_ABI_VERSION; }
 
 extern "C" const char* hgin_last_error(void) { return hgin::g_last_error.c_str(); }
 
+extern "C" int hgin_host_alloc(size_t bytes, void** ptr) {
+  HGIN_ARG_CHECK(ptr && bytes > 0, "hgin_host_alloc: bad args");
+  *ptr = nullptr;
+  const hipError_t e = hipHostMalloc(ptr, bytes, hipHostMallocMapped | hipHostMallocCoherent);
+  if (e != hipSuccess) {
+    hgin::set_error("hgin_host_alloc: hipHostMalloc(%zu) failed: %s", bytes, hipGetErrorString(e));
+    return (int)e;
+  }
+  return HGIN_OK;
+}
+
+extern "C" int hgin_host_free(void* ptr) {
+  if (!ptr) return HGIN_OK;
+  const hipError_t e = hipHostFree(ptr);
+  if (e != hipSuccess) {
+    hgin::set_error("hgin_host_free: %s", hipGetErrorString(e));
+    return (int)e;
+  }
+  return HGIN_OK;
+}
+
 extern "C" int hgin_trace_enable(int on) {
   std::lock_guard<std::mutex> lk(hgin::g_trace_mu);
   hgin::g_trace_buf.clear();

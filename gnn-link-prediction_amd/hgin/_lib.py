@@ -192,10 +192,12 @@ _SIGS = {
     "hgin_sb_args_offsets": ([_P, _I64], _I32),
     "hgin_sb_readout_lds_bytes": ([_I64, _I64, _I32, _I32, _P, _I32, ctypes.POINTER(_SZ)], _I32),
     "hgin_sb_step": ([_P, _SZ, _SZ, _P], _I32),
+    "hgin_host_alloc": ([_SZ, ctypes.POINTER(ctypes.c_void_p)], _I32),
+    "hgin_host_free": ([_P], _I32),
     "hgin_trace_enable": ([_I32], _I32),
     "hgin_trace_read": ([ctypes.c_char_p, _SZ], _SZ),
 }
-ABI_VERSION = 5
+ABI_VERSION = 6
 
 
 def lib() -> ctypes.CDLL:

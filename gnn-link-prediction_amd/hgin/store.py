@@ -23,6 +23,9 @@ rebuild.  ``normalize=True`` applies the reference's always-on feature normalisa
 """
 from __future__ import annotations
 
+import ctypes
+import weakref
+
 from dataclasses import dataclass
 from typing import Dict, List, Optional, Sequence
 
@@ -215,11 +218,24 @@ class GraphStore:
         """Refill ``out`` with the graphs ``ids``: valid rows first; the CSR / CSC rows past the batch get
         empty ranges (padding vertices are isolated) and ``out.m_valid`` = the batch's path count, so the
         fused loss covers exactly the batch.  One batched-copy launch, no allocation, no host sync."""
-        ids, nodes, edges, b_node, b_edge = self.plan(ids)
+        ids = np.asarray(ids, dtype=np.int64)
+        if ids.size == 0:
+            raise ValueError("collate: empty batch")
+        if ids.min() < 0 or ids.max() >= self.num_graphs:
+            raise IndexError("collate: graph id out of range")
         if len(ids) > out.batch_size:
             raise ValueError(f"collate_into: {len(ids)} graphs > batch capacity {out.batch_size}")
-        self._launch(ids, nodes, edges, b_node, b_edge, out.x, out.batch, out.y, out.edge_index, out.csr, out.csc,
-                     out.m_valid, out.goff, out.batch_size)
+        # the table's output-side constants are computed once per padded batch (_DescPlan) and the table is written
+        # straight into the device-readable ring slot: the per-batch host work is what bounds this step at cfg1
+        # sizes (tools/sb_host.py)
+        plan = out.__dict__.get("_hgin_desc_plan")
+        if plan is None or plan.store is not self:
+            plan = out._hgin_desc_plan = _DescPlan(self, out)
+        slot = self._desc_slot(plan.max_bytes)
+        n, max_count = plan.fill(ids, slot[3])
+        stream = torch.cuda.current_stream(self.device)
+        _lib.call("hgin_batched_copy", ctypes.c_void_p(slot[0]), n, max_count, ctypes.c_void_p(stream.cuda_stream))
+        slot[2].record(stream)
         return out
 
     def _template(self):
@@ -289,10 +305,38 @@ class GraphStore:
                 m_valid, goff=None, cap_graphs: int = 0) -> None:
         """One batched-copy launch filling the output buffers with the graphs ``ids``."""
         arr = self._descriptors(ids, x_out, batch_out, y_out, ei_out, csr_out, csc_out, m_valid, goff, cap_graphs)
-        host = torch.from_numpy(arr.view(np.uint8)).pin_memory()
-        dev_desc = host.to(self.device, non_blocking=True)
         max_count = int(arr["count"].max()) if len(arr) else 0
-        _lib.call("hgin_batched_copy", ops._p(dev_desc), len(arr), max_count, ops._stream(dev_desc))
+        stream = torch.cuda.current_stream(self.device)
+        slot = self._desc_slot(arr.nbytes)
+        ctypes.memmove(slot[0], arr.ctypes.data, arr.nbytes)
+        # the copy kernel reads the table in place from device-visible host memory: no host -> device copy (a blit
+        # kernel and a launch boundary per batch, ~5 us of the small-batch step) ahead of it
+        _lib.call("hgin_batched_copy", ctypes.c_void_p(slot[0]), len(arr), max_count,
+                  ctypes.c_void_p(stream.cuda_stream))
+        slot[2].record(stream)
+
+    _DESC_SLOTS = 4
+
+    def _desc_slot(self, nbytes: int) -> list:
+        """A slot [pointer, capacity, event, structured view] of the ring of descriptor tables in coherent host
+        memory (hgin_host_alloc): refilled only once the copy launch that last read it has finished (its event;
+        an event that was never recorded counts as finished)."""
+        ring = self.__dict__.get("_desc_ring")
+        if ring is None:
+            ring = self._desc_ring = [[None, 0, torch.cuda.Event(), None] for _ in range(self._DESC_SLOTS)]
+            self._desc_next = 0
+            weakref.finalize(self, _free_desc_ring, ring)
+        slot = ring[self._desc_next]
+        self._desc_next = (self._desc_next + 1) % self._DESC_SLOTS
+        slot[2].synchronize()
+        if slot[1] < nbytes:
+            _free_desc_ring([slot])
+            cap = max(int(nbytes), 64 << 10) // DESC_DTYPE.itemsize * DESC_DTYPE.itemsize
+            p = ctypes.c_void_p()
+            _lib.call("hgin_host_alloc", cap, ctypes.byref(p))
+            slot[0], slot[1] = p.value, cap
+            slot[3] = np.frombuffer((ctypes.c_char * cap).from_address(p.value), dtype=DESC_DTYPE)
+        return slot
 
     def _descriptors(self, ids, x_out, batch_out, y_out, ei_out, csr_out, csc_out, m_valid, goff=None,
                      cap_graphs: int = 0) -> np.ndarray:
@@ -344,6 +388,91 @@ class GraphStore:
                 ta[name] = [q[k] for q in tail]
         return np.concatenate([main.reshape(-1), ta])
 
+
+
+def _free_desc_ring(ring) -> None:
+    for slot in ring:
+        if slot[0]:
+            slot[2].synchronize()
+            slot[3] = None
+            _lib.lib().hgin_host_free(ctypes.c_void_p(slot[0]))
+            slot[0], slot[1] = None, 0
+
+
+class _DescPlan:
+    """collate_into's descriptor table for one padded batch, with what depends only on its buffers precomputed: the
+    per-group destination pointers, the tails' destinations (the CSR / CSC rowptr past the batch, m_valid, the
+    per-graph offsets).  ``fill`` then writes a batch's table into a structured view in a few numpy operations —
+    the same table, entry for entry, as GraphStore._descriptors (tests/test_store_host.py)."""
+
+    def __init__(self, store: "GraphStore", out: "PaddedBatch"):
+        self.store = store
+        tab = self.tab = store._template()
+        col = tab["col"]
+        outs = {"x": out.x, "batch": out.batch, "y": {None: out.y}, "ei": out.edge_index,
+                "csr.col": {r: c.col for r, c in out.csr.items()}, "csr.perm": {r: c.perm for r, c in out.csr.items()},
+                "csr.rowptr": {r: c.rowptr for r, c in out.csr.items()},
+                "csc.col": {r: c.col for r, c in out.csc.items()}, "csc.perm": {r: c.perm for r, c in out.csc.items()},
+                "csc.rowptr": {r: c.rowptr for r, c in out.csc.items()}}
+        dts = [outs[a][b] for a, b in tab["dsel"]]
+        des = np.array([t.element_size() for t in dts], dtype=np.int64)
+        dconst = np.array([dts[k].shape[1] if c == "e_cap" else 0 for k, c in enumerate(tab["csel"])], dtype=np.int64)
+        self.dbase = np.array([t.data_ptr() for t in dts], dtype=np.int64) + dconst * des
+        self.dscale = tab["dmul"] * des
+        self.gd = len(dts)
+        rp_ptr, rp_numel, rp_ncol, rp_ecol = [], [], [], []
+        for r in store.relations:
+            s_, _, d = r
+            cr, cc = out.csr[r].rowptr, out.csc[r].rowptr
+            rp_ptr += [cr.data_ptr(), cc.data_ptr()]
+            rp_numel += [cr.numel(), cc.numel()]
+            rp_ncol += [col[d], col[s_]]
+            rp_ecol += [col[r], col[r]]
+        self.rp_ptr, self.rp_numel = np.array(rp_ptr, dtype=np.int64), np.array(rp_numel, dtype=np.int64)
+        self.rp_ncol, self.rp_ecol = np.array(rp_ncol), np.array(rp_ecol)
+        self.mv_ptr, self.mv_col = out.m_valid.data_ptr(), col["path"]
+        cap = self.cap = out.batch_size
+        gt = [(ti, col[t]) for ti, t in enumerate(("path", "link", "node")) if t in col]
+        self.g_cols = np.array([c for _, c in gt], dtype=np.int64)
+        self.g_ptr = np.array([[out.goff.data_ptr() + 4 * (ti * (cap + 1) + j) for j in range(cap + 1)]
+                               for ti, _ in gt], dtype=np.int64).reshape(-1)
+        self.n_tail = len(rp_ptr) + 1 + len(gt) * (cap + 1)
+        self.max_bytes = (cap * self.gd + self.n_tail) * DESC_DTYPE.itemsize
+
+    def fill(self, ids: np.ndarray, view: np.ndarray):
+        """Write the table of the graphs ``ids`` into ``view``; returns (entries, largest count)."""
+        tab = self.tab
+        J = len(ids)
+        C = tab["cnt"][ids]
+        B = np.cumsum(C, 0) - C
+        tot = C.sum(0)
+        nm = J * self.gd
+        main = view[:nm].reshape(J, self.gd)
+        main["src"] = tab["src"][ids]
+        cnt = tab["count"][ids]
+        main["count"] = cnt
+        main["dst"] = self.dbase + B[:, tab["dcol"]] * self.dscale
+        main["add"] = tab["shift"][ids] + B[:, tab["acol"]] * tab["amask"] + np.arange(J)[:, None] * tab["jadd"]
+        main["kind"] = tab["kind"]
+        main["reserved"] = 0
+        t = view[nm:nm + self.n_tail]
+        k = len(self.rp_ptr)
+        n = tot[self.rp_ncol]
+        t["src"] = 0
+        t["kind"] = FILL_I32
+        t["reserved"] = 0
+        t["dst"][:k] = self.rp_ptr + 4 * n
+        t["count"][:k] = self.rp_numel - n
+        t["add"][:k] = tot[self.rp_ecol]
+        t["dst"][k] = self.mv_ptr
+        t["count"][k:] = 1
+        t["add"][k] = tot[self.mv_col]
+        offs = np.zeros((J + 1, len(self.g_cols)), dtype=np.int64)
+        np.cumsum(C[:, self.g_cols], 0, out=offs[1:])
+        t["dst"][k + 1:] = self.g_ptr
+        t["add"][k + 1:] = offs[np.minimum(np.arange(self.cap + 1), J)].T.reshape(-1)
+        max_count = max(int(cnt.max()) if cnt.size else 0, int(t["count"].max()))
+        return nm + self.n_tail, max_count
 
 @dataclass
 class PaddedBatch(HeteroGraph):

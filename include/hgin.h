@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define HGIN_ABI_VERSION 5
+#define HGIN_ABI_VERSION 6
 
 #define HGIN_OK 0
 #define HGIN_E_ARG (-1)        /* bad size / null pointer / unsupported combination */
@@ -365,6 +365,12 @@ typedef struct hgin_copy_desc {
   int32_t reserved;
 } hgin_copy_desc;
 int hgin_batched_copy(const hgin_copy_desc* descs, int64_t n_desc, int64_t max_count, void* stream);
+/* Host memory the device reads in place (F1 collation, no reference counterpart): page-locked, mapped and coherent
+ * (hipHostMallocCoherent: not cached on the device, so a buffer refilled by the host between launches is never read
+ * stale).  hgin_batched_copy takes its descriptor table from such a buffer directly, without a host -> device copy
+ * ahead of it.  The caller owns the buffer and must not refill it before the launch reading it has finished. */
+int hgin_host_alloc(size_t bytes, void** ptr);
+int hgin_host_free(void* ptr);
 
 /* ---- A10: negative-edge sampler (NOT IN REFERENCE; build-defined) --------------
  * out[i] = hi32( philox4x32_10(counter = {lo32(offset+i), hi32(offset+i), 0, 0},

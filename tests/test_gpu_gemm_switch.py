@@ -8,14 +8,14 @@
                               k_gemm_tn_bf16_tr, and k_gemm_nt for the fp32 forward GEMM, whose default at K = N = 256
                               is k_ws_f32) for every shape (the weight-stationary dW kernel k_wsd_bf16 is
                               the default at N, K in {128, 256});
-  * HGIN_NT_BKH=128         — the tiled kernel with 128-deep K-tiles (with the weight-stationary form off);
   * HGIN_NT_BDMA=0 (tiled)  — the fp32 128 x 128 tile splitting its B stages itself instead of copying them from
                               pre-split planes by LDS-DMA;
   * HGIN_NT_T256=0          — the fp32 split tile at 128 x 128 instead of 128 x 256 (N a multiple of 256: the
                               K = 512 forward);
   * HGIN_WS_STAGGER=0       — k_ws_f32 instead of the staggered two-stage fp32 forward / dX-combine GEMM (k_wss_f32);
   (The measured-and-removed variants — the fp32 128 x 256 / k_nt_pipe tiles, double-buffered B, the ping-pong k_nt_pp,
-  the 16 x 16 x 32 MFMA tile, and in round 5 the one-wave-per-SIMD k_wsf_f32 and k_wsd_f32 at N = K = 256 — are
+  the 16 x 16 x 32 MFMA tile, and in round 5 the one-wave-per-SIMD k_wsf_f32, k_wsd_f32 at N = K = 256 and the
+  128-deep bf16 K-tiles — are
   listed in DESIGN.md §3 with their commits.)
 
 Every child checks its outputs against an fp32 evaluation of the same bf16 operands; the three settings must
@@ -34,7 +34,6 @@ pytestmark = pytest.mark.gpu
 HERE = os.path.dirname(os.path.abspath(__file__))
 
 SWITCHES = {"default": {}, "tiled": {"HGIN_NT_WS": "0", "HGIN_TN_WS": "0", "HGIN_NT_WS32": "0"},
-            "tiled_bk128": {"HGIN_NT_WS": "0", "HGIN_NT_BKH": "128", "HGIN_TN_WS": "0", "HGIN_NT_WS32": "0"},
             "tiled_nobdma": {"HGIN_NT_WS": "0", "HGIN_TN_WS": "0", "HGIN_NT_WS32": "0", "HGIN_NT_BDMA": "0"},
             "t256_off": {"HGIN_NT_T256": "0"},
             "ws_stagger_off": {"HGIN_WS_STAGGER": "0"}}

@@ -6,7 +6,7 @@ import numpy as np
 import pytest
 import torch
 
-from hgin.store import DESC_DTYPE, NORMALIZATION, GraphStore, normalize_reference
+from hgin.store import DESC_DTYPE, NORMALIZATION, GraphStore, PaddedBatch, _DescPlan, normalize_reference
 
 
 class _CopyDesc(ctypes.Structure):      # include/hgin.h: hgin_copy_desc
@@ -142,7 +142,16 @@ def test_batch_descriptors_fill_the_padded_batch():
         cco = {r: mk(cap_n[r[0]], cap_e[r]) for r in rels}
         mv = torch.zeros(1, dtype=torch.int32)
         goff = torch.full((3 * (cap + 1),), -7, dtype=torch.int32)
-        _emulate_batched_copy(st._descriptors(ids, xo, bo, yo, eo, cro, cco, mv, goff, cap))
+        arr = st._descriptors(ids, xo, bo, yo, eo, cro, cco, mv, goff, cap)
+        # collate_into's fast table (_DescPlan: output-side constants precomputed, written into a ring slot's
+        # view): entry for entry the same table
+        plan = _DescPlan(st, PaddedBatch(xo, eo, yo, bo, mv, cro, cco, cap, goff))
+        view = np.zeros(plan.max_bytes // DESC_DTYPE.itemsize + 3, dtype=DESC_DTYPE)
+        view["reserved"] = -1
+        n, max_count = plan.fill(np.asarray(ids, dtype=np.int64), view)
+        assert n == len(arr) and max_count == int(arr["count"].max())
+        assert view[:n].tobytes() == arr.tobytes()
+        _emulate_batched_copy(arr)
         b = {t: np.concatenate([[0], np.cumsum([nc[t][g] for g in ids])]) for t in types}
         be = {r: np.concatenate([[0], np.cumsum([ec[r][g] for g in ids])]) for r in rels}
         for t in types:
