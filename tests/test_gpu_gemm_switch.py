@@ -59,7 +59,7 @@ def test_switch_within_tolerance(name):
     _run(name)        # the child checks against fp32 itself
 
 
-@pytest.mark.parametrize("name", ["tiled", "tiled_bk128", "tiled_nobdma", "t256_off", "ws_stagger_off"])
+@pytest.mark.parametrize("name", ["tiled", "tiled_nobdma", "t256_off", "ws_stagger_off"])
 def test_switch_bitwise_equal_default(name):
     ref, got = _run("default"), _run(name)
     assert ref.keys() == got.keys()
