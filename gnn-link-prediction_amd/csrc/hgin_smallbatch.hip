@@ -107,7 +107,7 @@ struct SbArgs {
   float* loss_part;         // [n_tiles]
   float* slope_part;        // [n_tiles] the shared readout slope's gradient
   int n_tiles;              // readout tiles of kSbRows path rows
-  int ro_wlds;              // 1: the readout tiles stage the hidden weights in LDS
+  int ro_wlds;              // readout: 2 the 32-row MFMA tiles, 1 8-row tiles with the weights in LDS, 0 without
   float* ro_in[kSbMaxHid + 1];   // readout layer i's input rows [cap_path][win_i] (i = nhid: the head)
   float* ro_gz[kSbMaxHid + 1];   // its pre-activation gradient rows [cap_path][rw_i] (the head: [cap_path])
   // outputs
@@ -359,25 +359,58 @@ struct FastDiv {
 __device__ __forceinline__ FastDiv fast_div(int d) { return {d > 1 ? 0xFFFFFFFFu / (unsigned)d + 1u : 0u, d}; }
 __device__ __forceinline__ int fdq(const FastDiv& f, int n) { return f.d > 1 ? (int)__umulhi((unsigned)n, f.m) : n; }
 
-// rows [nr][K] of src (row stride K) into dst [nr][K + 1] with a last column of ones (8 loads in flight per thread;
-// nr (K + 1) < 2^16)
-__device__ __forceinline__ void stage_ones(float* dst, const float* src, int nr, int K) {
-  const int K1 = K + 1, tot = nr * K1;
-  const FastDiv f = fast_div(K1);
-  for (int b = threadIdx.x; b < tot; b += 8 * kSbThreads) {
-    float v[8];
+// The readout's parameters into LDS (kWL; otherwise only the offsets / strides of the global rows): per hidden layer
+// W_i [rw_i][win_i | 1] (rows padded to an odd stride: lanes reading different W rows and lanes reading along one
+// are both conflict-free) and b_i [rw_i], then the head's W [KL]; every load of a thread in flight at once (up to
+// kStageW slots of each W), then the padded stores.  Returns the first float past them.
+template <bool kWL>
+__device__ __forceinline__ int stage_ro_params(const SbArgs& a, float* sm, int nh, const int (&win)[kSbMaxHid + 1],
+                                               int KL, int (&oW)[kSbMaxHid], int (&ldw)[kSbMaxHid]) {
+  const int tid = threadIdx.x;
+  int off = 0;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int idx = b + j * kSbThreads;
-      const int rr = fdq(f, idx), k = idx - rr * K1;
-      const bool ld = idx < tot && k < K;
-      const float x = src[ld ? rr * K + k : 0];
-      v[j] = ld ? x : 1.0f;
-    }
-#pragma unroll
-    for (int j = 0; j < 8; ++j)
-      if (b + j * kSbThreads < tot) dst[b + j * kSbThreads] = v[j];
+  for (int i = 0; i < kSbMaxHid; ++i) {
+    oW[i] = off;
+    ldw[i] = kWL ? (win[i] | 1) : win[i];
+    if (kWL && i < nh) off += a.rw[i] * (ldw[i] + 1);
   }
+  if (kWL) {
+    const int oH = off;
+    off += KL;
+    // every parameter load of a thread in flight at once (up to kStageW slots of each W), then the padded stores
+    constexpr int kStageW = 16;
+    float vw[kSbMaxHid][kStageW], vb[kSbMaxHid];
+#pragma unroll
+    for (int i = 0; i < kSbMaxHid; ++i) {
+      if (i < nh) {
+        const int n = win[i] * a.rw[i], N = a.rw[i];
+#pragma unroll
+        for (int j = 0; j < kStageW; ++j) vw[i][j] = a.row_w[i][tid + j * kSbThreads < n ? tid + j * kSbThreads : n - 1];
+        vb[i] = a.row_b[i][tid < N ? tid : N - 1];
+      }
+    }
+    const float vh = a.head_w[tid < KL ? tid : KL - 1];
+#pragma unroll
+    for (int i = 0; i < kSbMaxHid; ++i) {
+      if (i < nh) {
+        const int K = win[i], N = a.rw[i], n = K * N;
+        const FastDiv fk = fast_div(K);
+#pragma unroll
+        for (int j = 0; j < kStageW; ++j) {
+          const int idx = tid + j * kSbThreads;
+          const int q = fdq(fk, idx);
+          if (idx < n) sm[oW[i] + q * ldw[i] + idx - q * K] = vw[i][j];
+        }
+        for (int idx = tid + kStageW * kSbThreads; idx < n; idx += kSbThreads) {   // (wider layers than cfg1's)
+          const int q = idx / K;
+          sm[oW[i] + q * ldw[i] + idx - q * K] = a.row_w[i][idx];
+        }
+        for (int o = tid; o < N; o += kSbThreads) sm[oW[i] + N * ldw[i] + o] = o == tid ? vb[i] : a.row_b[i][o];
+      }
+    }
+    for (int k = tid; k < KL; k += kSbThreads) sm[oH + k] = k == tid ? vh : a.head_w[k];
+  }
+  return off;
 }
 
 // Tiles of kSbRows path rows (a grid-stride loop over the batch's tiles): readout forward, loss partial, readout
@@ -432,49 +465,8 @@ __global__ __launch_bounds__(kSbThreads) void k_sb_readout(SbArgs a) {
   // [R][w0] | z_i, y_i [R][rw_i] per hidden layer | gbuf x2 [R][maxw] | outv [R].  (Float offsets, not pointer arrays:
   // the pointers formed from them at each use are plain LDS addresses, where arrays of pointers became generic ones.)
   int oW[kSbMaxHid], ldw[kSbMaxHid];
-  int off = 0;
-#pragma unroll
-  for (int i = 0; i < kSbMaxHid; ++i) {
-    oW[i] = off;
-    ldw[i] = kWL ? (win[i] | 1) : win[i];
-    if (kWL && i < nh) off += a.rw[i] * (ldw[i] + 1);
-  }
-  const int oH = off;
-  if (kWL) {
-    off += KL;
-    // every parameter load of a thread in flight at once (up to kStageW slots of each W), then the padded stores
-    constexpr int kStageW = 16;
-    float vw[kSbMaxHid][kStageW], vb[kSbMaxHid];
-#pragma unroll
-    for (int i = 0; i < kSbMaxHid; ++i) {
-      if (i < nh) {
-        const int n = win[i] * a.rw[i], N = a.rw[i];
-#pragma unroll
-        for (int j = 0; j < kStageW; ++j) vw[i][j] = a.row_w[i][tid + j * kSbThreads < n ? tid + j * kSbThreads : n - 1];
-        vb[i] = a.row_b[i][tid < N ? tid : N - 1];
-      }
-    }
-    const float vh = a.head_w[tid < KL ? tid : KL - 1];
-#pragma unroll
-    for (int i = 0; i < kSbMaxHid; ++i) {
-      if (i < nh) {
-        const int K = win[i], N = a.rw[i], n = K * N;
-        const FastDiv fk = fast_div(K);
-#pragma unroll
-        for (int j = 0; j < kStageW; ++j) {
-          const int idx = tid + j * kSbThreads;
-          const int q = fdq(fk, idx);
-          if (idx < n) sm[oW[i] + q * ldw[i] + idx - q * K] = vw[i][j];
-        }
-        for (int idx = tid + kStageW * kSbThreads; idx < n; idx += kSbThreads) {   // (wider layers than cfg1's)
-          const int q = idx / K;
-          sm[oW[i] + q * ldw[i] + idx - q * K] = a.row_w[i][idx];
-        }
-        for (int o = tid; o < N; o += kSbThreads) sm[oW[i] + N * ldw[i] + o] = o == tid ? vb[i] : a.row_b[i][o];
-      }
-    }
-    for (int k = tid; k < KL; k += kSbThreads) sm[oH + k] = k == tid ? vh : a.head_w[k];
-  }
+  int off = stage_ro_params<kWL>(a, sm, nh, win, KL, oW, ldw);
+  const int oH = off - (kWL ? KL : 0);
   const float* hw = kWL ? (const float*)(sm + oH) : a.head_w;
   int oZ[kSbMaxHid], oY[kSbMaxHid];
   float* in0 = sm + off;
@@ -648,15 +640,252 @@ __global__ __launch_bounds__(kSbThreads) void k_sb_readout(SbArgs a) {
 #undef RO_W
 #undef RO_B
 
+// ---------------------------------------------------------------------------------------------------------------
+// The readout on the matrix cores (hgin_sb_readout_lds_bytes mode 2, the default where it fits): tiles of 32 path
+// rows, each readout GEMM of the tile — the hidden layers' forward, their input gradients — as 32 x 32 blocks of
+// v_mfma_f32_32x32x2_f32 (fp32 products, fp32 accumulation) over LDS operands.  A quarter as many workgroups stage the
+// parameters, and a phase is a few dozen MFMAs per wave instead of a chain of dependent LDS round trips per output
+// (profiles/r05/sb/stamps_after.txt: 12 such phases made the 8-row scalar tile's ~20 us).
+constexpr int kSbRowsM = 32;
+typedef float sb_f32x16 __attribute__((ext_vector_type(16)));
+
+// C[32 x N] = A[32 x K] B[K x N] for one tile: A(r, k) = A[r lda + k] (rows >= nr read as zero), B(k, n) =
+// Bm[k bsk + n bsn].  The ceil(N / 32) column blocks go to the 4 waves; with fewer than 4 blocks a block's k-steps
+// are split over 2 or 4 waves (fixed split) and the partials, parked in red [4][32][33], are added in split order.
+// epi(r, n, v) receives every output of rows < nr and columns < N (v = 0 + the products in k order within a split).
+template <class Epi>
+__device__ __forceinline__ void tile_mfma(const float* A, int lda, int nr, const float* Bm, int bsk, int bsn, int N,
+                                          int K, float* red, Epi epi) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int li = lane & 31, lh = lane >> 5;
+  const int nb = (N + 31) >> 5;
+  const int ks = nb >= 3 ? 1 : (nb == 2 ? 2 : 4);
+  const int steps = (K + 1) >> 1;
+  const int sc = (steps + ks - 1) / ks;
+  const bool rok = li < nr;
+  const int rc = rok ? li : 0;
+  for (int task = w; task < nb * ks; task += 4) {
+    const int cb = task % nb, sp = task / nb;
+    const int n = cb * 32 + li;
+    const bool nok = n < N;
+    const int nc = nok ? n : N - 1;
+    const int s0 = sp * sc, s1 = s0 + sc < steps ? s0 + sc : steps;
+    sb_f32x16 acc;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) acc[j] = 0.0f;
+    for (int st = s0; st < s1; st += 4) {   // 4 k-steps' operands loaded together, then their MFMAs
+      float av[4], bv[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int k = 2 * (st + q) + lh;
+        const bool kok = st + q < s1 && k < K;
+        const int kc = k < K ? k : K - 1;
+        const float x = A[rc * lda + kc], y = Bm[kc * bsk + nc * bsn];
+        av[q] = rok && kok ? x : 0.0f;
+        bv[q] = nok && kok ? y : 0.0f;
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        if (st + q < s1) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[q], bv[q], acc, 0, 0, 0);
+    }
+    if (ks == 1) {
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        const int r = (j & 3) + 8 * (j >> 2) + 4 * lh;   // the 32 x 32 accumulator layout: column li, row r
+        if (r < nr && nok) epi(r, n, acc[j]);
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 16; ++j) red[(task * 32 + (j & 3) + 8 * (j >> 2) + 4 * lh) * 33 + li] = acc[j];
+    }
+  }
+  if (ks > 1) {
+    __syncthreads();
+    for (int idx = threadIdx.x; idx < nr * N; idx += kSbThreads) {
+      const int r = idx / N, n = idx % N, cb = n >> 5;
+      float v = 0.0f;
+      for (int sp = 0; sp < ks; ++sp) v = __fadd_rn(v, red[((sp * nb + cb) * 32 + r) * 33 + (n & 31)]);
+      epi(r, n, v);
+    }
+  }
+}
+
+__global__ __launch_bounds__(kSbThreads) void k_sb_readout_mfma(SbArgs a) {
+  extern __shared__ float sm[];
+  __shared__ float red1[kSbThreads];
+  const int tid = threadIdx.x;
+  const int H = a.H;
+  const int m = a.m_valid[0];
+  constexpr int R = kSbRowsM;
+  const int ntile = (m + R - 1) / R;
+  const int tile = blockIdx.x;
+  if (tile >= ntile) return;   // (the grid is sized for the capacity; uniform per workgroup)
+  SB_STAMP(0);
+  const int nh = a.nhid;
+  const int w0 = H + (a.concat_path ? a.fdim[0] : 0);
+  int win[kSbMaxHid + 1];
+  win[0] = w0;
+  int maxw = w0;
+#pragma unroll
+  for (int i = 0; i < kSbMaxHid; ++i) {
+    win[i + 1] = i < nh ? a.rw[i] : 0;
+    maxw = i < nh && a.rw[i] > maxw ? a.rw[i] : maxw;
+  }
+  const int KL = a.rw[nh - 1];
+  // LDS: the parameters (stage_ro_params) | in0 [R][w0 | 1] | z_i, y_i [R][rw_i | 1] per hidden layer | gbuf x2
+  // [R][maxw | 1] | outv [R] | red [4][32][33] (odd row strides everywhere: an MFMA operand read is 32 rows of one
+  // column)
+  int oW[kSbMaxHid], ldw[kSbMaxHid];
+  int off = stage_ro_params<true>(a, sm, nh, win, KL, oW, ldw);
+  const float* hw = sm + off - KL;
+  const int l0 = w0 | 1;
+  float* in0 = sm + off;
+  off += R * l0;
+  int oZ[kSbMaxHid], oY[kSbMaxHid], lz[kSbMaxHid];
+#pragma unroll
+  for (int i = 0; i < kSbMaxHid; ++i) {
+    oZ[i] = oY[i] = off;
+    lz[i] = 1;
+    if (i < nh) {
+      lz[i] = a.rw[i] | 1;
+      oY[i] = off + R * lz[i];
+      off += 2 * R * lz[i];
+    }
+  }
+  const int lg = maxw | 1;
+  float* gb0 = sm + off;
+  float* gb1 = gb0 + R * lg;
+  float* outv = gb1 + R * lg;
+  float* red = outv + R;
+  const float* xp = a.act + a.act_off[a.L - 1][0];
+  const float slope = a.ro_slope[0];
+  const float head_b = a.head_b[0];
+  const int r0 = tile * R;
+  const int nr = m - r0 < R ? m - r0 : R;
+  for (int idx = tid; idx < nr * w0; idx += kSbThreads) {
+    const int rr = idx / w0, k = idx % w0;
+    const int64_t row = r0 + rr;
+    const float v = k < H ? xp[row * H + k] : a.x[0][row * a.ldx[0] + a.cols[0][k - H]];
+    in0[rr * l0 + k] = v;
+    a.ro_in[0][(int64_t)r0 * w0 + idx] = v;
+  }
+  __syncthreads();   // the parameters and in0
+  SB_STAMP(2);
+#pragma unroll
+  for (int i = 0; i < kSbMaxHid; ++i) {
+    if (i < nh) {
+      const float* in = i == 0 ? in0 : sm + oY[i > 0 ? i - 1 : 0];
+      const int lin = i == 0 ? l0 : lz[i > 0 ? i - 1 : 0];
+      const int N = a.rw[i];
+      const float* b = sm + oW[i] + N * ldw[i];
+      tile_mfma(in, lin, nr, sm + oW[i], 1, ldw[i], N, win[i], red, [&](int r, int n, float v) {
+        const float z = __fadd_rn(v, b[n]);
+        sm[oZ[i] + r * lz[i] + n] = z;
+        const float yv = z > 0.0f ? z : __fmul_rn(slope, z);
+        sm[oY[i] + r * lz[i] + n] = yv;
+        a.ro_in[i + 1][(int64_t)(r0 + r) * N + n] = yv;
+      });
+      __syncthreads();
+      SB_STAMP(3 + i);
+    }
+  }
+  const int lyl = nh == 1 ? lz[0] : (nh == 2 ? lz[1] : lz[2]);
+  const float* yl = sm + (nh == 1 ? oY[0] : (nh == 2 ? oY[1] : oY[2]));
+  {   // head + loss numerator + seed, split_of() lanes per row
+    const int S = split_of(nr, KL);
+    for (int idx = tid; idx < nr * S; idx += kSbThreads) {
+      const int rr = idx / S, s = idx % S;
+      float o = dot_chain(yl + rr * lyl + s, S, hw + s, S, (KL - s + S - 1) / S, 0.0f);
+      o = group_sum(o, S);
+      if (s == 0) {
+        o = __fadd_rn(o, head_b);
+        const float yv = a.y[r0 + rr];
+        const float u = __fdiv_rn(__fsub_rn(o, yv), yv);
+        red1[rr] = fabsf(u);
+        const float sg = u > 0.0f ? 1.0f : (u < 0.0f ? -1.0f : 0.0f);
+        const float go = __fdiv_rn(sg, yv);   // d |u| / d out
+        outv[rr] = go;
+        a.ro_gz[nh][r0 + rr] = go;
+      }
+    }
+  }
+  __syncthreads();
+  SB_STAMP(6);
+  if (tid == 0) {   // fixed-order tile sum of |u| (rows in order)
+    float s = 0.0f;
+    for (int rr = 0; rr < nr; ++rr) s = __fadd_rn(s, red1[rr]);
+    a.loss_part[tile] = s;
+  }
+  for (int idx = tid; idx < nr * KL; idx += kSbThreads) {
+    const int rr = idx / KL, k = idx % KL;
+    gb0[rr * (KL | 1) + k] = __fmul_rn(outv[rr], hw[k]);
+  }
+  __syncthreads();
+  SB_STAMP(7);
+  float slope_part = 0.0f;   // this thread's share of the shared slope's gradient (fixed assignment)
+  float* g_y = gb0;
+  float* g_next = gb1;
+#pragma unroll
+  for (int i = kSbMaxHid - 1; i >= 0; --i) {
+    if (i < nh) {
+      const int K = win[i], N = a.rw[i], ly = N | 1;
+      // g_z (in place over g_y) and the slope partial, 4 elements' loads in flight per thread
+      for (int i0 = tid; i0 < nr * N; i0 += 4 * kSbThreads) {
+        float zv[4], gv[4];
+        int q[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int idx = i0 + u * kSbThreads < nr * N ? i0 + u * kSbThreads : i0;
+          const int rr = idx / N, o = idx - rr * N;
+          q[u] = rr * ly + o;
+          zv[u] = sm[oZ[i] + rr * lz[i] + o];
+          gv[u] = g_y[q[u]];
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int idx = i0 + u * kSbThreads;
+          if (idx < nr * N) {
+            if (zv[u] <= 0.0f) slope_part = fmaf(gv[u], zv[u], slope_part);
+            const float gz = zv[u] > 0.0f ? gv[u] : __fmul_rn(slope, gv[u]);
+            g_y[q[u]] = gz;
+            a.ro_gz[i][(int64_t)r0 * N + idx] = gz;
+          }
+        }
+      }
+      __syncthreads();
+      SB_STAMP(8 + 2 * i);
+      // g_in = g_z W (the first layer: only the path embeddings' H columns have a gradient)
+      const int KG = i == 0 ? H : K, lgn = KG | 1;
+      float* gn = g_next;
+      tile_mfma(g_y, ly, nr, sm + oW[i], ldw[i], 1, KG, N, red,
+                [&](int r, int n, float v) { gn[r * lgn + n] = v; });
+      __syncthreads();
+      SB_STAMP(9 + 2 * i);
+      float* t = g_y;
+      g_y = g_next;
+      g_next = t;
+    }
+  }
+  const float sp = block_sum(slope_part, red1);
+  SB_STAMP(12);
+  if (tid == 0) a.slope_part[tile] = sp;
+  float* gpath = a.gA + a.g_off[0];
+  for (int idx = tid; idx < nr * H; idx += kSbThreads) {
+    const int rr = idx / H, k = idx % H;
+    gpath[(int64_t)r0 * H + idx] = g_y[rr * (H | 1) + k];
+  }
+  SB_STAMP(13);
+}
+
 // the readout blocks of k_sb_bwd_w: over row chunk p of the m valid path rows, one group of layer i's (i = nhid: the
 // head's) partial weight / bias gradients, g_W[o][k] = sum_rows g_z[o] in[k], g_b[o] = sum_rows g_z[o] (the bias as
-// an input column of ones: fmaf(g, 1, v) is the add), the chunk's rows in order (staged kRoSub rows at a time).
-// A group is ro_to(N) x (kSbThreads / ro_to(N)) threads, each an MO x MK register tile of (o, k) entries strided
-// by the thread grid (lanes read consecutive o: conflict-free; 6 LDS reads per 8 products, not 16).  Block y-index
-// u (after the relations' kRel) -> (layer, group): the layers' groups in order.
-constexpr int kRoSub = 16;
+// an input column of ones: fmaf(g, 1, v) is the add), the chunk's rows in order (staged as many rows at a time as
+// the staging array holds: the whole chunk at cfg1 sizes).  A group is ro_to(N) x (kSbThreads / ro_to(N)) threads,
+// each an MO x MK register tile of (o, k) entries strided by the thread grid (lanes read consecutive o: conflict-free;
+// 6 LDS reads per 8 products, not 16).  Block y-index u (after the relations' kRel) -> (layer, group): the layers'
+// groups in order.
 constexpr int kRoMO = 4, kRoMK = 2;
-constexpr int kSbStage = kRoSub * (2 * kSbMaxW + 1);   // k_sb_bwd_w's staging floats
+constexpr int kSbStage = 8192;   // k_sb_bwd_w's staging floats (32 KiB: 16 rows of the widest readout layer)
 
 __host__ __device__ __forceinline__ int ro_to(int N) {
   int t = 1;
@@ -696,15 +925,19 @@ __device__ __forceinline__ void wg_setup(WgTile& t, int N, int K1, int u) {
 #pragma unroll
     for (int jk = 0; jk < kRoMK; ++jk) t.acc[j][jk] = 0.0f;
 }
-// acc += sum over the nr staged rows (in order) of s_g[rr][o] s_in[rr][k] (s_g [nr][N], s_in [nr][K1], LDS)
-__device__ __forceinline__ void wg_accum(WgTile& t, const float* s_g, const float* s_in, int nr, int N, int K1) {
+// acc += sum over the nr staged rows (in order) of s_g[rr][o] s_in[rr][k] (s_g [nr][N], s_in [nr][K] as copied from
+// HBM; column K, the bias's, reads as ones: fmaf(g, 1, v) is the add)
+__device__ __forceinline__ void wg_accum(WgTile& t, const float* s_g, const float* s_in, int nr, int N, int K) {
 #pragma unroll 4
   for (int rr = 0; rr < nr; ++rr) {
     float g[kRoMO], x[kRoMK];
 #pragma unroll
     for (int j = 0; j < kRoMO; ++j) g[j] = s_g[rr * N + t.oj[j]];
 #pragma unroll
-    for (int j = 0; j < kRoMK; ++j) x[j] = s_in[rr * K1 + t.kj[j]];
+    for (int j = 0; j < kRoMK; ++j) {
+      const float v = s_in[rr * K + (t.kj[j] < K ? t.kj[j] : 0)];
+      x[j] = t.kj[j] < K ? v : 1.0f;
+    }
 #pragma unroll
     for (int j = 0; j < kRoMO; ++j)
 #pragma unroll
@@ -723,7 +956,7 @@ __device__ __forceinline__ void wg_store(const WgTile& t, float* part, int N, in
   }
 }
 
-__device__ void ro_weight_part(const SbArgs& a, int p, int u, float* s_in, float* s_g) {
+__device__ void ro_weight_part(const SbArgs& a, int p, int u, float* stage) {
   int i = 0;
   while (i < a.nhid && u >= ro_groups(a, i)) u -= ro_groups(a, i++);
   const int tid = threadIdx.x;
@@ -738,13 +971,18 @@ __device__ void ro_weight_part(const SbArgs& a, int p, int u, float* s_in, float
   float* part = a.part_ro + (int64_t)p * a.p_ro - a.p_gin + (i < a.nhid ? a.ro_goff[i] : a.head_goff);
   WgTile t;
   wg_setup(t, N, K1, u);
-  for (int rb = i0; rb < i1; rb += kRoSub) {
-    const int nr = i1 - rb < kRoSub ? i1 - rb : kRoSub;
+  // the chunk's rows RS at a time (all of them at cfg1 sizes: one memory round trip), both images contiguous copies
+  const int rcap = kSbStage / (N + K);
+  const int RS = (i1 - i0) < rcap ? (i1 - i0 > 0 ? i1 - i0 : 1) : rcap;
+  float* s_g = stage;
+  float* s_in = stage + RS * N;
+  for (int rb = i0; rb < i1; rb += RS) {
+    const int nr = i1 - rb < RS ? i1 - rb : RS;
     __syncthreads();
-    stage_ones(s_in, in + (int64_t)rb * K, nr, K);
+    copy_flat<16>(s_in, in + (int64_t)rb * K, nr * K);
     copy_flat<8>(s_g, gz + (int64_t)rb * N, nr * N);
     __syncthreads();
-    wg_accum(t, s_g, s_in, nr, N, K1);
+    wg_accum(t, s_g, s_in, nr, N, K);
   }
   wg_store(t, part, N, K);
 }
@@ -764,7 +1002,7 @@ __global__ __launch_bounds__(kSbThreads, 4) void k_sb_bwd_w(SbArgs a, int l, con
   const int p = blockIdx.x, r = blockIdx.y;
   SB_STAMP_W(l & 1, 0);
   if (r >= kRel) {   // the readout's blocks: groups ro_first, ... (grid.y = kRel + their count)
-    ro_weight_part(a, p, r - kRel + ro_first, stage, stage + kRoSub * (kSbMaxW + 1));
+    ro_weight_part(a, p, r - kRel + ro_first, stage);
     SB_STAMP_W(l & 1, 1);
     return;
   }
@@ -789,7 +1027,7 @@ __global__ __launch_bounds__(kSbThreads, 4) void k_sb_bwd_w(SbArgs a, int l, con
   // above kRoMO x kRoMK x kSbThreads entries) stages the rows again.
   // W [H][K] in LDS too when small (the g_comb dots read a column of it per output)
   const int wsz = H * K <= 2048 ? H * K : 0;
-  const int rcap = (kSbStage - wsz) / (H + K1);
+  const int rcap = (kSbStage - wsz) / (H + K);
   const int RS = (i1 - i0) < rcap ? (i1 - i0 > 0 ? i1 - i0 : 1) : rcap;
   float* s_w = stage;
   float* s_g = stage + wsz;
@@ -803,7 +1041,7 @@ __global__ __launch_bounds__(kSbThreads, 4) void k_sb_bwd_w(SbArgs a, int l, con
     for (int rb = i0; rb < i1; rb += RS) {
       const int nr = i1 - rb < RS ? i1 - rb : RS;
       __syncthreads();
-      stage_ones(s_in, comb + (int64_t)rb * K, nr, K);
+      copy_flat<16>(s_in, comb + (int64_t)rb * K, nr * K);
 #pragma unroll 4
       for (int idx = tid; idx < nr * H; idx += kSbThreads) {
         const int64_t qq = (int64_t)rb * H + idx;
@@ -826,7 +1064,7 @@ __global__ __launch_bounds__(kSbThreads, 4) void k_sb_bwd_w(SbArgs a, int l, con
           }
         }
       }
-      wg_accum(t, s_g, s_in, nr, H, K1);
+      wg_accum(t, s_g, s_in, nr, H, K);
     }
     wg_store(t, part, H, K);
   }
@@ -892,7 +1130,8 @@ __global__ __launch_bounds__(kSbThreads) void k_sb_final(SbArgs a) {
     ad.bc2_sqrt = sqrtf(__fsub_rn(1.0f, powf(a.beta2, st)));
   }
   const int m = a.m_valid[0];
-  const int ntile = (m + kSbRows - 1) / kSbRows;
+  const int rows = a.ro_wlds == 2 ? kSbRowsM : kSbRows;   // the readout tiles' rows (one loss / slope partial each)
+  const int ntile = (m + rows - 1) / rows;
   float lp = 0.0f, sp = 0.0f;
   for (int t = tid; t < ntile; t += kSbThreads) {
     lp = __fadd_rn(lp, a.loss_part[t]);
@@ -946,6 +1185,12 @@ extern "C" int hgin_sb_readout_lds_bytes(int64_t H, int64_t f_path, int concat_p
     win = widths[i];
   }
   HGIN_ARG_CHECK(w0 <= kSbMaxW, "hgin_sb_readout_lds_bytes: input width %lld", (long long)w0);
+  if (with_weights == 2) {   // k_sb_readout_mfma: 32-row tiles, odd row strides, the split partials
+    int64_t act = w0 | 1;
+    for (int i = 0; i < nhid; ++i) act += 2 * (widths[i] | 1);
+    *bytes = sizeof(float) * (size_t)(wts + kSbRowsM * (act + 2 * (maxw | 1)) + kSbRowsM + 4 * 32 * 33);
+    return HGIN_OK;
+  }
   *bytes = sizeof(float) * (size_t)(kSbRows * (tot + 2 * maxw) + kSbRows + (with_weights ? wts : 0));
   return HGIN_OK;
 }
@@ -971,7 +1216,8 @@ extern "C" int hgin_sb_step(const void* args, size_t args_bytes, size_t readout_
   if (dyn_max_dev[dev] == 0) {
     int m = 160 * 1024;   // the smaller of the two variants' limits (-1 if either failed)
     for (const void* fn : {reinterpret_cast<const void*>(k_sb_readout<true>),
-                           reinterpret_cast<const void*>(k_sb_readout<false>)}) {
+                           reinterpret_cast<const void*>(k_sb_readout<false>),
+                           reinterpret_cast<const void*>(k_sb_readout_mfma)}) {
       hipFuncAttributes fa;
       int mf = -1;
       if (hipFuncGetAttributes(&fa, fn) == hipSuccess) {
@@ -1008,7 +1254,10 @@ extern "C" int hgin_sb_step(const void* args, size_t args_bytes, size_t readout_
   for (int l = 0; l < a.L; ++l) k_sb_fwd<<<dim3(fwd_blocks, 3), kSbThreads, 0, s>>>(a, l);
   // one tile per workgroup (a grid of 512 looping over the tiles, staging the weights once each: 52.9 vs 35 us per
   // batch, profiles/r04/gpu_r — the tiles' serial layer chains want the parallelism, not fewer weight stagings)
-  if (a.ro_wlds)
+  if (a.ro_wlds == 2)
+    k_sb_readout_mfma<<<(unsigned)ceil_div((int64_t)a.n_tiles * kSbRows, (int64_t)kSbRowsM), kSbThreads, readout_lds,
+                        s>>>(a);
+  else if (a.ro_wlds)
     k_sb_readout<true><<<a.n_tiles, kSbThreads, readout_lds, s>>>(a);
   else
     k_sb_readout<false><<<a.n_tiles, kSbThreads, readout_lds, s>>>(a);

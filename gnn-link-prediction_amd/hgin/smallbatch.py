@@ -16,6 +16,7 @@ place); the step returns the batch's device ``loss_value`` (train.py:40), no hos
 from __future__ import annotations
 
 import ctypes
+import os
 from typing import Sequence
 
 import torch
@@ -293,8 +294,9 @@ class SmallBatchStep:
             self._fold_adam(a, params, param_off, off, convs, hidden, slope, head, L, keep)
         widths = (ctypes.c_int32 * MAX_HID)(*[a.rw[i] for i in range(MAX_HID)])
         lds = ctypes.c_size_t(0)
-        # the readout tile stages its hidden weights in LDS when they fit beside its 1 KiB static array
-        for wl in (1, 0):
+        # the readout: 32-row tiles on the matrix cores where they fit (HGIN_SB_MFMA=0: the 8-row scalar tiles), else
+        # 8-row tiles with the hidden weights in LDS, else without (beside the tile's 1 KiB static array)
+        for wl in ((2, 1, 0) if os.environ.get("HGIN_SB_MFMA", "1") != "0" else (1, 0)):
             _lib.check(_lib.lib().hgin_sb_readout_lds_bytes(H, fdim["path"], a.concat_path, a.nhid, widths, wl,
                                                             ctypes.byref(lds)), "hgin_sb_readout_lds_bytes")
             if lds.value <= 159 * 1024:

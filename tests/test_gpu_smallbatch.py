@@ -62,10 +62,14 @@ def _host_batch(store, ids):
     return b
 
 
+@pytest.mark.parametrize("readout", ["mfma", "scalar"])
 @pytest.mark.parametrize("layers", [1, 2, 3])
-def test_fused_step_vs_oracle(layers):
-    """One fused step (Adam at lr 0) against the CPU oracle's forward / sqrt-MAPE backward on the host-collated batch."""
+def test_fused_step_vs_oracle(layers, readout, monkeypatch):
+    """One fused step (Adam at lr 0) against the CPU oracle's forward / sqrt-MAPE backward on the host-collated batch;
+    the readout on the 32-row MFMA tiles (default) and on the 8-row scalar tiles (HGIN_SB_MFMA=0)."""
     from hgin.smallbatch import SmallBatchStep
+    if readout == "scalar":
+        monkeypatch.setenv("HGIN_SB_MFMA", "0")
     from oracle.pyg_cpu import mape
     store, cfg = _store(10, seed=11)
     ids = [2, 8, 5, 0]
@@ -73,6 +77,7 @@ def test_fused_step_vs_oracle(layers):
     ref = _oracle_twin(m1, cfg, layers)
     o1 = torch.optim.Adam(m1.parameters(), lr=0.0, capturable=True)
     step = SmallBatchStep(m1, o1, store, batch_size=5, warmup_ids=[ids], warmup=1)
+    assert step.args.ro_wlds == (2 if readout == "mfma" else 1)
     lv = float(step.step(ids))
     torch.cuda.synchronize()
     b = _host_batch(store, ids)
