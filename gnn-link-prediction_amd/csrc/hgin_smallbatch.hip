@@ -125,13 +125,14 @@ __device__ __forceinline__ int kdim(const SbArgs& a, int l, int r) {
   return l == 0 ? a.fdim[kRelSrc[r]] + a.fdim[kRelDst[r]] : a.H;
 }
 
-// fixed-order block reduction (all threads call it; returns the sum to every thread)
+// fixed-order block reduction over NT threads (all threads call it; returns the sum to every thread)
+template <int NT = kSbThreads>
 __device__ float block_sum(float v, float* red) {
   const int t = threadIdx.x;
   __syncthreads();
   red[t] = v;
   __syncthreads();
-  for (int off = kSbThreads / 2; off > 0; off >>= 1) {
+  for (int off = NT / 2; off > 0; off >>= 1) {
     if (t < off) red[t] = __fadd_rn(red[t], red[t + off]);
     __syncthreads();
   }
@@ -197,9 +198,10 @@ __device__ __forceinline__ void dot_rows4(const float* x, int xr, const float* y
 // threads per output of a readout phase with nout outputs of len-term sums: a power of two <= 16 that keeps the
 // phase within one pass of the workgroup and >= 4 terms per thread (thread s of an output sums terms s, s + S, ...;
 // the S adjacent lanes then combine in a fixed xor tree, identical on every lane)
+template <int NT = kSbThreads>
 __device__ __forceinline__ int split_of(int nout, int len) {
   int S = 1;
-  while (S < 16 && nout * S * 2 <= kSbThreads && len >= 8 * S) S *= 2;
+  while (S < 16 && nout * S * 2 <= NT && len >= 8 * S) S *= 2;
   return S;
 }
 __device__ __forceinline__ float group_sum(float v, int S) {
@@ -363,7 +365,7 @@ __device__ __forceinline__ int fdq(const FastDiv& f, int n) { return f.d > 1 ? (
 // W_i [rw_i][win_i | 1] (rows padded to an odd stride: lanes reading different W rows and lanes reading along one
 // are both conflict-free) and b_i [rw_i], then the head's W [KL]; every load of a thread in flight at once (up to
 // kStageW slots of each W), then the padded stores.  Returns the first float past them.
-template <bool kWL>
+template <bool kWL, int NT = kSbThreads>
 __device__ __forceinline__ int stage_ro_params(const SbArgs& a, float* sm, int nh, const int (&win)[kSbMaxHid + 1],
                                                int KL, int (&oW)[kSbMaxHid], int (&ldw)[kSbMaxHid]) {
   const int tid = threadIdx.x;
@@ -385,7 +387,7 @@ __device__ __forceinline__ int stage_ro_params(const SbArgs& a, float* sm, int n
       if (i < nh) {
         const int n = win[i] * a.rw[i], N = a.rw[i];
 #pragma unroll
-        for (int j = 0; j < kStageW; ++j) vw[i][j] = a.row_w[i][tid + j * kSbThreads < n ? tid + j * kSbThreads : n - 1];
+        for (int j = 0; j < kStageW; ++j) vw[i][j] = a.row_w[i][tid + j * NT < n ? tid + j * NT : n - 1];
         vb[i] = a.row_b[i][tid < N ? tid : N - 1];
       }
     }
@@ -397,18 +399,18 @@ __device__ __forceinline__ int stage_ro_params(const SbArgs& a, float* sm, int n
         const FastDiv fk = fast_div(K);
 #pragma unroll
         for (int j = 0; j < kStageW; ++j) {
-          const int idx = tid + j * kSbThreads;
+          const int idx = tid + j * NT;
           const int q = fdq(fk, idx);
           if (idx < n) sm[oW[i] + q * ldw[i] + idx - q * K] = vw[i][j];
         }
-        for (int idx = tid + kStageW * kSbThreads; idx < n; idx += kSbThreads) {   // (wider layers than cfg1's)
+        for (int idx = tid + kStageW * NT; idx < n; idx += NT) {   // (wider layers than cfg1's)
           const int q = idx / K;
           sm[oW[i] + q * ldw[i] + idx - q * K] = a.row_w[i][idx];
         }
-        for (int o = tid; o < N; o += kSbThreads) sm[oW[i] + N * ldw[i] + o] = o == tid ? vb[i] : a.row_b[i][o];
+        for (int o = tid; o < N; o += NT) sm[oW[i] + N * ldw[i] + o] = o == tid ? vb[i] : a.row_b[i][o];
       }
     }
-    for (int k = tid; k < KL; k += kSbThreads) sm[oH + k] = k == tid ? vh : a.head_w[k];
+    for (int k = tid; k < KL; k += NT) sm[oH + k] = k == tid ? vh : a.head_w[k];
   }
   return off;
 }
@@ -647,24 +649,30 @@ __global__ __launch_bounds__(kSbThreads) void k_sb_readout(SbArgs a) {
 // parameters, and a phase is a few dozen MFMAs per wave instead of a chain of dependent LDS round trips per output
 // (profiles/r05/sb/stamps_after.txt: 12 such phases made the 8-row scalar tile's ~20 us).
 constexpr int kSbRowsM = 32;
+constexpr int kRoThreadsM = 512;   // 8 waves: 2 per SIMD, so one wave's LDS / MFMA latency overlaps the other's
 typedef float sb_f32x16 __attribute__((ext_vector_type(16)));
 
 // C[32 x N] = A[32 x K] B[K x N] for one tile: A(r, k) = A[r lda + k] (rows >= nr read as zero), B(k, n) =
-// Bm[k bsk + n bsn].  The ceil(N / 32) column blocks go to the 4 waves; with fewer than 4 blocks a block's k-steps
-// are split over 2 or 4 waves (fixed split) and the partials, parked in red [4][32][33], are added in split order.
+// Bm[k bsk + n bsn].  The ceil(N / 32) column blocks go to the NT / 64 waves; with fewer blocks than waves a block's
+// k-steps are split over the idle ones (a fixed power-of-two split) and the partials, parked in red [NT / 64][32][33],
+// are added in split order.
 // epi(r, n, v) receives every output of rows < nr and columns < N (v = 0 + the products in k order within a split).
-template <class Epi>
+template <int NT, class Epi>
 __device__ __forceinline__ void tile_mfma(const float* A, int lda, int nr, const float* Bm, int bsk, int bsn, int N,
                                           int K, float* red, Epi epi) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int li = lane & 31, lh = lane >> 5;
   const int nb = (N + 31) >> 5;
-  const int ks = nb >= 3 ? 1 : (nb == 2 ? 2 : 4);
+  constexpr int W = NT / 64;
+  // k-splits per block (a power of two) only for one or two column blocks: from three up, the partials' extra
+  // barrier and pass cost more than the idle waves would save (profiles/r05/sb/stamps_mfma512.txt)
+  int ks = 1;
+  while (nb <= 2 && nb * ks * 2 <= W) ks *= 2;
   const int steps = (K + 1) >> 1;
   const int sc = (steps + ks - 1) / ks;
   const bool rok = li < nr;
   const int rc = rok ? li : 0;
-  for (int task = w; task < nb * ks; task += 4) {
+  for (int task = w; task < nb * ks; task += W) {
     const int cb = task % nb, sp = task / nb;
     const int n = cb * 32 + li;
     const bool nok = n < N;
@@ -701,7 +709,7 @@ __device__ __forceinline__ void tile_mfma(const float* A, int lda, int nr, const
   }
   if (ks > 1) {
     __syncthreads();
-    for (int idx = threadIdx.x; idx < nr * N; idx += kSbThreads) {
+    for (int idx = threadIdx.x; idx < nr * N; idx += NT) {
       const int r = idx / N, n = idx % N, cb = n >> 5;
       float v = 0.0f;
       for (int sp = 0; sp < ks; ++sp) v = __fadd_rn(v, red[((sp * nb + cb) * 32 + r) * 33 + (n & 31)]);
@@ -710,9 +718,10 @@ __device__ __forceinline__ void tile_mfma(const float* A, int lda, int nr, const
   }
 }
 
-__global__ __launch_bounds__(kSbThreads) void k_sb_readout_mfma(SbArgs a) {
+__global__ __launch_bounds__(kRoThreadsM) void k_sb_readout_mfma(SbArgs a) {
   extern __shared__ float sm[];
-  __shared__ float red1[kSbThreads];
+  constexpr int NT = kRoThreadsM;
+  __shared__ float red1[NT];
   const int tid = threadIdx.x;
   const int H = a.H;
   const int m = a.m_valid[0];
@@ -736,7 +745,7 @@ __global__ __launch_bounds__(kSbThreads) void k_sb_readout_mfma(SbArgs a) {
   // [R][maxw | 1] | outv [R] | red [4][32][33] (odd row strides everywhere: an MFMA operand read is 32 rows of one
   // column)
   int oW[kSbMaxHid], ldw[kSbMaxHid];
-  int off = stage_ro_params<true>(a, sm, nh, win, KL, oW, ldw);
+  int off = stage_ro_params<true, NT>(a, sm, nh, win, KL, oW, ldw);
   const float* hw = sm + off - KL;
   const int l0 = w0 | 1;
   float* in0 = sm + off;
@@ -762,7 +771,7 @@ __global__ __launch_bounds__(kSbThreads) void k_sb_readout_mfma(SbArgs a) {
   const float head_b = a.head_b[0];
   const int r0 = tile * R;
   const int nr = m - r0 < R ? m - r0 : R;
-  for (int idx = tid; idx < nr * w0; idx += kSbThreads) {
+  for (int idx = tid; idx < nr * w0; idx += NT) {
     const int rr = idx / w0, k = idx % w0;
     const int64_t row = r0 + rr;
     const float v = k < H ? xp[row * H + k] : a.x[0][row * a.ldx[0] + a.cols[0][k - H]];
@@ -778,7 +787,7 @@ __global__ __launch_bounds__(kSbThreads) void k_sb_readout_mfma(SbArgs a) {
       const int lin = i == 0 ? l0 : lz[i > 0 ? i - 1 : 0];
       const int N = a.rw[i];
       const float* b = sm + oW[i] + N * ldw[i];
-      tile_mfma(in, lin, nr, sm + oW[i], 1, ldw[i], N, win[i], red, [&](int r, int n, float v) {
+      tile_mfma<NT>(in, lin, nr, sm + oW[i], 1, ldw[i], N, win[i], red, [&](int r, int n, float v) {
         const float z = __fadd_rn(v, b[n]);
         sm[oZ[i] + r * lz[i] + n] = z;
         const float yv = z > 0.0f ? z : __fmul_rn(slope, z);
@@ -792,8 +801,8 @@ __global__ __launch_bounds__(kSbThreads) void k_sb_readout_mfma(SbArgs a) {
   const int lyl = nh == 1 ? lz[0] : (nh == 2 ? lz[1] : lz[2]);
   const float* yl = sm + (nh == 1 ? oY[0] : (nh == 2 ? oY[1] : oY[2]));
   {   // head + loss numerator + seed, split_of() lanes per row
-    const int S = split_of(nr, KL);
-    for (int idx = tid; idx < nr * S; idx += kSbThreads) {
+    const int S = split_of<NT>(nr, KL);
+    for (int idx = tid; idx < nr * S; idx += NT) {
       const int rr = idx / S, s = idx % S;
       float o = dot_chain(yl + rr * lyl + s, S, hw + s, S, (KL - s + S - 1) / S, 0.0f);
       o = group_sum(o, S);
@@ -816,7 +825,7 @@ __global__ __launch_bounds__(kSbThreads) void k_sb_readout_mfma(SbArgs a) {
     for (int rr = 0; rr < nr; ++rr) s = __fadd_rn(s, red1[rr]);
     a.loss_part[tile] = s;
   }
-  for (int idx = tid; idx < nr * KL; idx += kSbThreads) {
+  for (int idx = tid; idx < nr * KL; idx += NT) {
     const int rr = idx / KL, k = idx % KL;
     gb0[rr * (KL | 1) + k] = __fmul_rn(outv[rr], hw[k]);
   }
@@ -830,12 +839,12 @@ __global__ __launch_bounds__(kSbThreads) void k_sb_readout_mfma(SbArgs a) {
     if (i < nh) {
       const int K = win[i], N = a.rw[i], ly = N | 1;
       // g_z (in place over g_y) and the slope partial, 4 elements' loads in flight per thread
-      for (int i0 = tid; i0 < nr * N; i0 += 4 * kSbThreads) {
+      for (int i0 = tid; i0 < nr * N; i0 += 4 * NT) {
         float zv[4], gv[4];
         int q[4];
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
-          const int idx = i0 + u * kSbThreads < nr * N ? i0 + u * kSbThreads : i0;
+          const int idx = i0 + u * NT < nr * N ? i0 + u * NT : i0;
           const int rr = idx / N, o = idx - rr * N;
           q[u] = rr * ly + o;
           zv[u] = sm[oZ[i] + rr * lz[i] + o];
@@ -843,7 +852,7 @@ __global__ __launch_bounds__(kSbThreads) void k_sb_readout_mfma(SbArgs a) {
         }
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
-          const int idx = i0 + u * kSbThreads;
+          const int idx = i0 + u * NT;
           if (idx < nr * N) {
             if (zv[u] <= 0.0f) slope_part = fmaf(gv[u], zv[u], slope_part);
             const float gz = zv[u] > 0.0f ? gv[u] : __fmul_rn(slope, gv[u]);
@@ -857,7 +866,7 @@ __global__ __launch_bounds__(kSbThreads) void k_sb_readout_mfma(SbArgs a) {
       // g_in = g_z W (the first layer: only the path embeddings' H columns have a gradient)
       const int KG = i == 0 ? H : K, lgn = KG | 1;
       float* gn = g_next;
-      tile_mfma(g_y, ly, nr, sm + oW[i], ldw[i], 1, KG, N, red,
+      tile_mfma<NT>(g_y, ly, nr, sm + oW[i], ldw[i], 1, KG, N, red,
                 [&](int r, int n, float v) { gn[r * lgn + n] = v; });
       __syncthreads();
       SB_STAMP(9 + 2 * i);
@@ -866,11 +875,11 @@ __global__ __launch_bounds__(kSbThreads) void k_sb_readout_mfma(SbArgs a) {
       g_next = t;
     }
   }
-  const float sp = block_sum(slope_part, red1);
+  const float sp = block_sum<NT>(slope_part, red1);
   SB_STAMP(12);
   if (tid == 0) a.slope_part[tile] = sp;
   float* gpath = a.gA + a.g_off[0];
-  for (int idx = tid; idx < nr * H; idx += kSbThreads) {
+  for (int idx = tid; idx < nr * H; idx += NT) {
     const int rr = idx / H, k = idx % H;
     gpath[(int64_t)r0 * H + idx] = g_y[rr * (H | 1) + k];
   }
@@ -1188,7 +1197,7 @@ extern "C" int hgin_sb_readout_lds_bytes(int64_t H, int64_t f_path, int concat_p
   if (with_weights == 2) {   // k_sb_readout_mfma: 32-row tiles, odd row strides, the split partials
     int64_t act = w0 | 1;
     for (int i = 0; i < nhid; ++i) act += 2 * (widths[i] | 1);
-    *bytes = sizeof(float) * (size_t)(wts + kSbRowsM * (act + 2 * (maxw | 1)) + kSbRowsM + 4 * 32 * 33);
+    *bytes = sizeof(float) * (size_t)(wts + kSbRowsM * (act + 2 * (maxw | 1)) + kSbRowsM + (kRoThreadsM / 64) * 32 * 33);
     return HGIN_OK;
   }
   *bytes = sizeof(float) * (size_t)(kSbRows * (tot + 2 * maxw) + kSbRows + (with_weights ? wts : 0));
@@ -1255,7 +1264,7 @@ extern "C" int hgin_sb_step(const void* args, size_t args_bytes, size_t readout_
   // one tile per workgroup (a grid of 512 looping over the tiles, staging the weights once each: 52.9 vs 35 us per
   // batch, profiles/r04/gpu_r — the tiles' serial layer chains want the parallelism, not fewer weight stagings)
   if (a.ro_wlds == 2)
-    k_sb_readout_mfma<<<(unsigned)ceil_div((int64_t)a.n_tiles * kSbRows, (int64_t)kSbRowsM), kSbThreads, readout_lds,
+    k_sb_readout_mfma<<<(unsigned)ceil_div((int64_t)a.n_tiles * kSbRows, (int64_t)kSbRowsM), kRoThreadsM, readout_lds,
                         s>>>(a);
   else if (a.ro_wlds)
     k_sb_readout<true><<<a.n_tiles, kSbThreads, readout_lds, s>>>(a);
