@@ -141,6 +141,27 @@ __device__ float block_sum(float v, float* red) {
   return s;
 }
 
+// two fixed-order block reductions at once (red: 2 NT floats): half the barriers of two block_sum calls, the same
+// tree and order for each value
+__device__ float2 block_sum2(float v, float w, float* red) {
+  constexpr int NT = kSbThreads;
+  const int t = threadIdx.x;
+  __syncthreads();
+  red[t] = v;
+  red[NT + t] = w;
+  __syncthreads();
+  for (int off = NT / 2; off > 0; off >>= 1) {
+    if (t < off) {
+      red[t] = __fadd_rn(red[t], red[t + off]);
+      red[NT + t] = __fadd_rn(red[NT + t], red[NT + t + off]);
+    }
+    __syncthreads();
+  }
+  const float2 r = make_float2(red[0], red[NT]);
+  __syncthreads();
+  return r;
+}
+
 __device__ __forceinline__ int nrows(const SbArgs& a, int t) { return a.goff[t * (a.G + 1) + a.G]; }
 
 // sum over t < n of x[t sx] y[t sy], in t order (one fma chain onto acc); the operands are loaded 8 pairs at a time so
@@ -1006,7 +1027,7 @@ __device__ __forceinline__ float gout(const SbArgs& a, const float* gcur, int l,
 // the readout layers' blocks in the last layer's launch and half in the first's); rows of chunk p: [p c, (p + 1) c),
 // c = ceil(rows / n_parts)
 __global__ __launch_bounds__(kSbThreads, 4) void k_sb_bwd_w(SbArgs a, int l, const float* gcur, int ro_first) {
-  __shared__ float red[kSbThreads];
+  __shared__ float red[2 * kSbThreads];   // (block_sum2)
   __shared__ float stage[kSbStage];
   const int p = blockIdx.x, r = blockIdx.y;
   SB_STAMP_W(l & 1, 0);
@@ -1077,8 +1098,8 @@ __global__ __launch_bounds__(kSbThreads, 4) void k_sb_bwd_w(SbArgs a, int l, con
     }
     wg_store(t, part, H, K);
   }
-  const float ssum = block_sum(sp, red);
-  const float esum = block_sum(epv, red);
+  const float2 se = block_sum2(sp, epv, red);
+  const float ssum = se.x, esum = se.y;
   if (tid == 0) {
     part[(int64_t)H * K + H] = ssum;
     part[(int64_t)H * K + H + 1] = esum;
@@ -1130,7 +1151,7 @@ __device__ __forceinline__ void adam_update(const SbArgs& a, int64_t e, float gv
 }
 
 __global__ __launch_bounds__(kSbThreads) void k_sb_final(SbArgs a) {
-  __shared__ float red[kSbThreads];
+  __shared__ float red[2 * kSbThreads];   // (block_sum2)
   const int tid = threadIdx.x;
   AdamCoef ad{0.0f, 1.0f};
   if (a.adam_step) {
@@ -1146,8 +1167,8 @@ __global__ __launch_bounds__(kSbThreads) void k_sb_final(SbArgs a) {
     lp = __fadd_rn(lp, a.loss_part[t]);
     sp = __fadd_rn(sp, a.slope_part[t]);
   }
-  const float s = block_sum(lp, red);
-  const float slope_sum = block_sum(sp, red);
+  const float2 ls = block_sum2(lp, sp, red);
+  const float s = ls.x, slope_sum = ls.y;
   const float lv = __fdiv_rn(__fmul_rn(100.0f, s), (float)m);       // 100 * mean |u| (train.py:12-13)
   const float scale = __fdiv_rn(__fdiv_rn(100.0f, (float)m), __fmul_rn(2.0f, sqrtf(lv)));
   if (blockIdx.x == 0 && tid == 0) a.loss_value[0] = lv;
