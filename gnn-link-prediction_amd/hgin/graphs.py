@@ -7,10 +7,12 @@ launches (Python, autograd, ctypes).  HIP graphs remove that: the step runs on s
 fused loss limited to the batch's paths through a device-side count), is captured once after a short
 warm-up, and each iteration is one batched-copy launch (``GraphStore.collate_into``) + one graph replay.
 
-Numerically the padded step is the unpadded step for row-independent readouts (no BatchNorm, no global
-pooling, no dropout — refused by ``_check_row_independent``): padding rows have no edges, so they never feed a real
-row; their loss rows are masked, so their gradients are exactly zero and add nothing to any parameter
-gradient.  The optimizer must be capturable (``torch.optim.Adam(..., capturable=True)``).
+Numerically the padded step is the unpadded step for row-independent readouts (no BatchNorm — refused by
+``_check_row_independent``; dropout draws its masks per replay, so a step with dropout equals an eager step in
+distribution, not bitwise): padding rows have no edges, so they never feed a real row; their loss rows
+are masked, so their gradients are exactly zero and add nothing to any parameter gradient.  GLOBAL_FEATS' pooling
+(models.py:347-352) sees the padding path rows as one more graph (collate_into gives them the id batch_size, past
+every real graph), so the real graphs' pooled features are the exact batch's.  The optimizer must be capturable (``torch.optim.Adam(..., capturable=True)``).
 """
 from __future__ import annotations
 
@@ -25,16 +27,12 @@ from .train import mape, train_step
 def _check_row_independent(model: torch.nn.Module) -> None:
     """A padded batch equals the exact batch only when nothing mixes rows across the batch outside the
     graph's edges: padding path rows carry stale data and still pass through the readout.  BatchNorm
-    (MLP_BN) takes batch statistics over them, global pooling (GLOBAL_FEATS) pools them (and syncs the host
-    during capture), dropout > 0 draws fresh randomness per replay — all three are refused."""
+    (MLP_BN) takes batch statistics over them: refused.  (Global pooling pools the padding rows as a graph of
+    their own; dropout is row-wise and draws fresh masks on every replay — the captured RNG offset advances —
+    as an eager step would: both allowed.)"""
     if any(isinstance(m, torch.nn.modules.batchnorm._BatchNorm) for m in model.modules()):
         raise ValueError("CapturedTrainStep: BatchNorm in the model (mlp_bn=True) would take batch statistics over "
                          "padding rows; use the eager train_step")
-    if getattr(model, "global_feats", False):
-        raise ValueError("CapturedTrainStep: global_feats pools over padding rows (and syncs the host during "
-                         "capture); use the eager train_step")
-    if getattr(model, "dropout", 0.0) > 0.0:
-        raise ValueError("CapturedTrainStep: dropout > 0 is not replayable; use the eager train_step")
 
 
 class CapturedTrainStep:
@@ -146,15 +144,13 @@ class CapturedEvalStep:
     ``running_loss_mape += mape * n_paths``), so a whole evaluation pass syncs the host once, in ``result()``.
 
     The model must be in eval mode (BatchNorm then reads its running statistics and dropout is off: both
-    row-independent, so the padded batch equals the exact one); GLOBAL_FEATS pools over padding rows and is refused
-    (the eager forward takes it)."""
+    row-independent, so the padded batch equals the exact one); GLOBAL_FEATS pools the padding path rows as a graph of
+    their own (collate_into's padding id), so the real graphs' pooled features are the exact batch's."""
 
     def __init__(self, model: torch.nn.Module, store: GraphStore, batch_size: int,
                  warmup_ids: Sequence[Sequence[int]], warmup: int = 2):
         if model.training:
             raise ValueError("CapturedEvalStep: call model.eval() first (train.py:192, :329)")
-        if getattr(model, "global_feats", False):
-            raise ValueError("CapturedEvalStep: global_feats pools over padding rows; use the eager forward")
         if not warmup_ids:
             raise ValueError("CapturedEvalStep needs at least one warm-up batch")
         self.model, self.store = model, store

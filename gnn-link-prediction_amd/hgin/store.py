@@ -382,6 +382,11 @@ class GraphStore:
                     for j in range(cap_graphs + 1):
                         tail.append((0, goff.data_ptr() + 4 * (ti * (cap_graphs + 1) + j), 1,
                                      int(offs[min(j, J)]), FILL_I32))
+            # the padding path rows' graph id: cap_graphs, past every real graph, so a pooled segment (GLOBAL_FEATS,
+            # models.py:347-352) never mixes them into a real graph and the batch vector stays sorted
+            bp = batch_out["path"]
+            n_p = int(tot[col["path"]])
+            tail.append((0, bp.data_ptr() + 8 * n_p, bp.numel() - n_p, cap_graphs, FILL_I64))
         ta = np.zeros(len(tail), dtype=DESC_DTYPE)
         if tail:
             for k, name in enumerate(("src", "dst", "count", "add", "kind")):
@@ -436,7 +441,8 @@ class _DescPlan:
         self.g_cols = np.array([c for _, c in gt], dtype=np.int64)
         self.g_ptr = np.array([[out.goff.data_ptr() + 4 * (ti * (cap + 1) + j) for j in range(cap + 1)]
                                for ti, _ in gt], dtype=np.int64).reshape(-1)
-        self.n_tail = len(rp_ptr) + 1 + len(gt) * (cap + 1)
+        self.bp_ptr, self.bp_numel = out.batch["path"].data_ptr(), out.batch["path"].numel()
+        self.n_tail = len(rp_ptr) + 1 + len(gt) * (cap + 1) + 1
         self.max_bytes = (cap * self.gd + self.n_tail) * DESC_DTYPE.itemsize
 
     def fill(self, ids: np.ndarray, view: np.ndarray):
@@ -469,8 +475,14 @@ class _DescPlan:
         t["add"][k] = tot[self.mv_col]
         offs = np.zeros((J + 1, len(self.g_cols)), dtype=np.int64)
         np.cumsum(C[:, self.g_cols], 0, out=offs[1:])
-        t["dst"][k + 1:] = self.g_ptr
-        t["add"][k + 1:] = offs[np.minimum(np.arange(self.cap + 1), J)].T.reshape(-1)
+        ng = len(self.g_ptr)
+        t["dst"][k + 1:k + 1 + ng] = self.g_ptr
+        t["add"][k + 1:k + 1 + ng] = offs[np.minimum(np.arange(self.cap + 1), J)].T.reshape(-1)
+        n_p = int(tot[self.mv_col])   # the padding path rows' graph id (GraphStore._descriptors)
+        t["dst"][-1] = self.bp_ptr + 8 * n_p
+        t["count"][-1] = self.bp_numel - n_p
+        t["add"][-1] = self.cap
+        t["kind"][-1] = FILL_I64
         max_count = max(int(cnt.max()) if cnt.size else 0, int(t["count"].max()))
         return nm + self.n_tail, max_count
 

@@ -219,6 +219,61 @@ def test_captured_train_step_matches_eager():
     assert g_cap
 
 
+def test_captured_train_step_global_feats_matches_eager():
+    """GLOBAL_FEATS (models.py:347-352) in the captured padded step: the padding path rows carry the graph id
+    batch_size (collate_into), so the per-graph [mean | max] pooling of the real graphs is the exact batch's; one
+    replay's loss and gradients equal an eager exact-batch backward on the same parameters."""
+    from hgin.graphs import CapturedTrainStep
+    graphs = _graphs(10, seed=17)
+    store = GraphStore.build(graphs, device=DEV)
+    cfg = CONFIGS["cfg1"]
+    kw = lambda: dict(cfg.model_kwargs({"link": 7, "path": 7, "node": 3}), global_feats=True, bl_features=True)  # noqa: E731
+    ids = [6, 2, 9]
+    torch.manual_seed(1997)
+    m1 = HetroGIN(**kw()).to(DEV)
+    step = CapturedTrainStep(m1, torch.optim.Adam(m1.parameters(), lr=0.0, capturable=True), store, batch_size=4,
+                             warmup_ids=[[1, 4, 7, 3], ids], warmup=2)
+    lv = float(step.step(ids))
+    torch.manual_seed(1997)
+    m2 = HetroGIN(**kw()).to(DEV)
+    b = store.collate(ids)
+    _, lv2 = m2.forward_loss(b.x_dict(), b.edge_index_dict(), b.batch["path"], b.y)
+    torch.sqrt(lv2).backward()
+    assert abs(lv - float(lv2)) <= 1e-5 * abs(float(lv2)), (lv, float(lv2))
+    for (n, p1), (_, p2) in zip(m1.named_parameters(), m2.named_parameters()):
+        assert (p1.grad is None) == (p2.grad is None), n
+        if p2.grad is not None:
+            err = float((p1.grad - p2.grad).double().norm())
+            assert err <= 1e-5 * float(p2.grad.double().norm()) + 1e-9, (n, err)
+
+
+def test_captured_train_step_with_dropout_draws_fresh_masks():
+    """dropout > 0 (models.py:358-359) in the captured step: replays of the same batch at lr 0 give different losses
+    (a fresh mask per replay, as eager steps draw), their mean within the spread of eager dropout steps on the exact
+    batch, and finite gradients."""
+    from hgin.graphs import CapturedTrainStep
+    from hgin.train import train_step
+    graphs = _graphs(8, seed=23)
+    store = GraphStore.build(graphs, device=DEV)
+    cfg = CONFIGS["cfg1"]
+    kw = lambda: dict(cfg.model_kwargs({"link": 7, "path": 7, "node": 3}), dropout=0.2)  # noqa: E731  (a fresh dict:
+    ids = [3, 5, 0]                                                                      # HetroGIN mutates it)
+    torch.manual_seed(1997)
+    m1 = HetroGIN(**kw()).to(DEV)
+    step = CapturedTrainStep(m1, torch.optim.Adam(m1.parameters(), lr=0.0, capturable=True), store, batch_size=3,
+                             warmup_ids=[ids], warmup=2)
+    cap = [float(step.step(ids)) for _ in range(8)]
+    assert len(set(cap)) > 1, cap
+    assert all(p.grad is None or bool(torch.isfinite(p.grad).all()) for p in m1.parameters())
+    torch.manual_seed(1997)
+    m2 = HetroGIN(**kw()).to(DEV)
+    o2 = torch.optim.Adam(m2.parameters(), lr=0.0)
+    eager = [float(train_step(m2, o2, store.collate(ids))) for _ in range(8)]
+    lo, hi = min(eager), max(eager)
+    span = hi - lo
+    assert lo - 2 * span <= float(np.mean(cap)) <= hi + 2 * span, (cap, eager)
+
+
 def test_store_build_normalize_equals_reference_fixture():
     """GraphStore.build(normalize=True) holds exactly the features the reference's own normalize
     (dataset.py:33-58, executed by tests/golden/make_golden_normalize.py) produces for the same collated graphs."""
@@ -233,8 +288,8 @@ def test_store_build_normalize_equals_reference_fixture():
         assert torch.equal(st.x[t].cpu(), fx[f"out.x.{t}"][:n]), t
 
 
-@pytest.mark.parametrize("mlp_bn", [False, True])
-def test_captured_eval_step_matches_eager(mlp_bn):
+@pytest.mark.parametrize("mlp_bn,global_feats", [(False, False), (True, False), (False, True)])
+def test_captured_eval_step_matches_eager(mlp_bn, global_feats):
     """train.py's test() loop (model.eval(), forward + MAPE per batch) as captured replays: every batch's loss and the
     predictions of its paths equal an eager no-grad forward on the exact batch (BatchNorm in eval mode reads its
     running statistics: row-independent), and the device accumulators give test()'s two averages."""
@@ -244,7 +299,10 @@ def test_captured_eval_step_matches_eager(mlp_bn):
     store = GraphStore.build(graphs, device=DEV)
     cfg = CONFIGS["cfg1"]
     torch.manual_seed(1997)
-    model = HetroGIN(**dict(cfg.model_kwargs({"link": 7, "path": 7, "node": 3}), mlp_bn=mlp_bn)).to(DEV)
+    kw = dict(cfg.model_kwargs({"link": 7, "path": 7, "node": 3}), mlp_bn=mlp_bn)
+    if global_feats:   # (the pooled GLOBAL_FEATS columns come with the raw-feature layout, models.py:347-352)
+        kw.update(global_feats=True, bl_features=True)
+    model = HetroGIN(**kw).to(DEV)
     if mlp_bn:   # non-trivial running statistics
         for m in model.modules():
             if isinstance(m, torch.nn.BatchNorm1d):
