@@ -348,7 +348,7 @@ def batches_extra(dev, n_graphs: int = 256, batch: int = 8, warmup: int = 5, ste
     # the reference's other switches, each through the path that takes it (SmallBatchStep.supports says which)
     # (GLOBAL_FEATS needs BL_FEATURES: models.py:293 sizes the readout for [mean | max] of 4 path columns, which only
     # the bl_features slicing keeps, models.py:333-342 — with 3 columns the reference's own Linear raises)
-    switches = {"mlp_bn": ({"mlp_bn": True}, False, "eager"),
+    switches = {"mlp_bn": ({"mlp_bn": True}, False, "captured"),
                 "global_feats": ({"global_feats": True, "bl_features": True}, False, "captured"),
                 "dropout_0.1": ({"dropout": 0.1}, False, "captured"),
                 "hidden_128": ({"node_embedding_size": 128}, False, "captured"),

@@ -7,9 +7,9 @@ launches (Python, autograd, ctypes).  HIP graphs remove that: the step runs on s
 fused loss limited to the batch's paths through a device-side count), is captured once after a short
 warm-up, and each iteration is one batched-copy launch (``GraphStore.collate_into``) + one graph replay.
 
-Numerically the padded step is the unpadded step for row-independent readouts (no BatchNorm — refused by
-``_check_row_independent``; dropout draws its masks per replay, so a step with dropout equals an eager step in
-distribution, not bitwise): padding rows have no edges, so they never feed a real row; their loss rows
+Numerically the padded step is the unpadded step (MLP_BN's batch statistics taken over the batch's rows only;
+dropout draws its masks per replay, so a step with dropout equals an eager step in distribution, not bitwise):
+padding rows have no edges, so they never feed a real row; their loss rows
 are masked, so their gradients are exactly zero and add nothing to any parameter gradient.  GLOBAL_FEATS' pooling
 (models.py:347-352) sees the padding path rows as one more graph (collate_into gives them the id batch_size, past
 every real graph), so the real graphs' pooled features are the exact batch's.  The optimizer must be capturable (``torch.optim.Adam(..., capturable=True)``).
@@ -26,13 +26,13 @@ from .train import mape, train_step
 
 def _check_row_independent(model: torch.nn.Module) -> None:
     """A padded batch equals the exact batch only when nothing mixes rows across the batch outside the
-    graph's edges: padding path rows carry stale data and still pass through the readout.  BatchNorm
-    (MLP_BN) takes batch statistics over them: refused.  (Global pooling pools the padding rows as a graph of
-    their own; dropout is row-wise and draws fresh masks on every replay — the captured RNG offset advances —
-    as an eager step would: both allowed.)"""
-    if any(isinstance(m, torch.nn.modules.batchnorm._BatchNorm) for m in model.modules()):
-        raise ValueError("CapturedTrainStep: BatchNorm in the model (mlp_bn=True) would take batch statistics over "
-                         "padding rows; use the eager train_step")
+    graph's edges: padding path rows carry stale data and still pass through the readout.  MLP_BN's BatchNorm1d
+    takes its statistics over the first m_valid rows only (models._masked_batch_norm); global pooling pools the
+    padding rows as a graph of their own; dropout is row-wise and draws fresh masks on every replay — the captured
+    RNG offset advances — as an eager step would.  Other BatchNorm kinds are refused."""
+    if any(isinstance(m, torch.nn.modules.batchnorm._BatchNorm) and not isinstance(m, torch.nn.BatchNorm1d)
+           for m in model.modules()):
+        raise ValueError("CapturedTrainStep: only BatchNorm1d (MLP_BN) takes the padded batch's masked statistics")
 
 
 class CapturedTrainStep:

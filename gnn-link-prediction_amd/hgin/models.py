@@ -258,7 +258,11 @@ class HetroGIN(torch.nn.Module):
             else:
                 if x2 is not None:
                     x = torch.cat((x, x2), 1)
-                x = seq(x)
+                if m_valid is not None and self.training and any(isinstance(m, torch.nn.BatchNorm1d) for m in seq):
+                    for mod in seq:   # a padded batch: MLP_BN's statistics over its first m_valid rows only
+                        x = _masked_batch_norm(x, mod, m_valid) if isinstance(mod, torch.nn.BatchNorm1d) else mod(x)
+                else:
+                    x = seq(x)
             x2 = None
         if y is not None:   # head with an activation / mlp_layers == []: unfused loss (train.py:12-13)
             if m_valid is not None:
@@ -266,6 +270,31 @@ class HetroGIN(torch.nn.Module):
             from .train import mape
             return x, mape(x, y.reshape(-1, 1))
         return x
+
+
+def _masked_batch_norm(x: torch.Tensor, bn: torch.nn.BatchNorm1d, m_valid: torch.Tensor) -> torch.Tensor:
+    """BatchNorm1d in training mode (models.py:303-313, MLP_BN) over the first m_valid rows of a padded batch
+    (hgin/graphs.py): those rows' mean and biased variance normalise every row (the padding rows' outputs feed only
+    masked loss rows), and the running statistics take the unbiased variance with the layer's momentum — torch's
+    BatchNorm on the exact batch, up to the order of the fp32 sums.  m_valid is a device count: no host sync, so
+    the step stays capturable."""
+    if bn.momentum is None:
+        raise NotImplementedError("masked BatchNorm: momentum=None (cumulative average) is not supported")
+    n = x.shape[0]
+    mask = (torch.arange(n, device=x.device) < m_valid.to(torch.int64)).to(x.dtype).unsqueeze(1)
+    m = m_valid.to(x.dtype)
+    mean = (x * mask).sum(0) / m
+    d = (x - mean) * mask
+    var = (d * d).sum(0) / m
+    if bn.track_running_stats:
+        with torch.no_grad():
+            bn.running_mean.mul_(1.0 - bn.momentum).add_(mean.detach() * bn.momentum)
+            bn.running_var.mul_(1.0 - bn.momentum).add_(var.detach() * (m / (m - 1.0)) * bn.momentum)
+            bn.num_batches_tracked.add_(1)
+    y = (x - mean) / torch.sqrt(var + bn.eps)
+    if bn.affine:
+        y = y * bn.weight + bn.bias
+    return y
 
 
 class HetroGAT(HetroGIN):

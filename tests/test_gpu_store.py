@@ -247,6 +247,42 @@ def test_captured_train_step_global_feats_matches_eager():
             assert err <= 1e-5 * float(p2.grad.double().norm()) + 1e-9, (n, err)
 
 
+def test_captured_train_step_mlp_bn_matches_eager():
+    """MLP_BN (models.py:303-313, training-mode BatchNorm1d in the readout) in the captured padded step: the batch
+    statistics over the first m_valid rows only (models._masked_batch_norm), so one replay's loss, gradients and
+    running statistics equal an eager exact-batch step's (torch's BatchNorm) on the same parameters."""
+    from hgin.graphs import CapturedTrainStep
+    graphs = _graphs(10, seed=29)
+    store = GraphStore.build(graphs, device=DEV)
+    cfg = CONFIGS["cfg1"]
+    kw = lambda: dict(cfg.model_kwargs({"link": 7, "path": 7, "node": 3}), mlp_bn=True)  # noqa: E731
+    ids = [8, 1, 4]
+    torch.manual_seed(1997)
+    m1 = HetroGIN(**kw()).to(DEV)
+    step = CapturedTrainStep(m1, torch.optim.Adam(m1.parameters(), lr=0.0, capturable=True), store, batch_size=4,
+                             warmup_ids=[[2, 5, 7, 0]], warmup=1)
+    torch.manual_seed(1997)
+    m2 = HetroGIN(**kw()).to(DEV)
+    with torch.no_grad():   # the warm-up and the capture moved m1's running statistics: start m2 from them
+        for b1, b2 in zip(m1.buffers(), m2.buffers()):
+            b2.copy_(b1)
+    lv = float(step.step(ids))
+    b = store.collate(ids)
+    _, lv2 = m2.forward_loss(b.x_dict(), b.edge_index_dict(), b.batch["path"], b.y)
+    torch.sqrt(lv2).backward()
+    assert abs(lv - float(lv2)) <= 1e-5 * abs(float(lv2)), (lv, float(lv2))
+    # (the bias of the Linear ahead of a BatchNorm has an exactly-zero gradient in exact arithmetic: both sides hold
+    # rounding noise there, so the bound has an absolute part scaled by the largest gradient)
+    scale = max(float(p.grad.double().norm()) for p in m2.parameters() if p.grad is not None)
+    for (n, p1), (_, p2) in zip(m1.named_parameters(), m2.named_parameters()):
+        assert (p1.grad is None) == (p2.grad is None), n
+        if p2.grad is not None:
+            err = float((p1.grad - p2.grad).double().norm())
+            assert err <= 1e-5 * float(p2.grad.double().norm()) + 1e-7 * scale, (n, err)
+    for (n, b1), (_, b2) in zip(m1.named_buffers(), m2.named_buffers()):
+        assert torch.allclose(b1.double(), b2.double(), rtol=1e-5, atol=1e-7), n
+
+
 def test_captured_train_step_with_dropout_draws_fresh_masks():
     """dropout > 0 (models.py:358-359) in the captured step: replays of the same batch at lr 0 give different losses
     (a fresh mask per replay, as eager steps draw), their mean within the spread of eager dropout steps on the exact
