@@ -31,7 +31,7 @@
 // the row chunks of the partials are fixed fractions of the batch's rows).  The aggregates are the GIN path's
 // (sequential edge-order fp32 sums: bit-identical); the GEMM-shaped sums and the deferred loss scaling re-associate,
 // so the step agrees with the general path within fp32 tolerances (tests/test_gpu_smallbatch.py).  Limits (checked
-// by the host, hgin/smallbatch.py): H <= 64, every GEMM K <= 128, readout widths <= 256, at most 3 hidden readout
+// by the host, hgin/smallbatch.py): H <= 128, every GEMM K <= 128, readout widths <= 256, at most 3 hidden readout
 // layers and 4 GIN layers, fp32.
 #include "hgin_common.h"
 
@@ -1232,7 +1232,7 @@ extern "C" int hgin_sb_step(const void* args, size_t args_bytes, size_t readout_
                  sizeof(SbArgs));
   SbArgs a;
   std::memcpy(&a, args, sizeof(SbArgs));
-  HGIN_ARG_CHECK(a.G >= 1 && a.L >= 1 && a.L <= kSbMaxL && a.H >= 1 && a.H <= 64 && a.nhid >= 1 && a.kmax <= 128 &&
+  HGIN_ARG_CHECK(a.G >= 1 && a.L >= 1 && a.L <= kSbMaxL && a.H >= 1 && a.H <= 128 && a.nhid >= 1 && a.kmax <= 128 &&
                      a.nhid <= kSbMaxHid && a.n_tiles >= 1 && readout_lds <= 160 * 1024,
                  "hgin_sb_step: unsupported shape");
   hipStream_t s = as_stream(stream);

@@ -6,7 +6,7 @@ fixed-order gradient reduction that applies the sqrt-MAPE scale and, for Adam, t
 launches), captured once into a hipGraph and replayed per batch after one device collation launch.
 
 It takes the model train.py builds from config.json (``HetroGIN`` with GINLayer convs, Linear + shared PReLU
-readout, Linear head, no BatchNorm / global features / dropout) at small widths: hidden <= 64, first-layer GEMM
+readout, Linear head, no BatchNorm / global features / dropout) at small widths: hidden <= 128, first-layer GEMM
 K <= 128, readout widths <= 256, <= 3 hidden readout layers, <= 4 layers, fp32.  ``SmallBatchStep.supports(model)``
 says whether it applies; ``hgin.graphs.CapturedTrainStep`` (one launch per op, any shape) is the general path.
 
@@ -143,7 +143,7 @@ def _structure(model: torch.nn.Module):
     if not 1 <= len(hidden) <= MAX_HID:
         return "readout depth"
     H = model.convs[0].convs["path__uses__link"].conv.nn[0].out_features
-    if H > 64 or any(l.out_features > 256 for l in hidden):
+    if H > 128 or any(l.out_features > 256 for l in hidden):
         return "widths"
     if any(p.dtype != torch.float32 for p in model.parameters()):
         return "dtype"

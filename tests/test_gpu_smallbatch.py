@@ -92,6 +92,35 @@ def test_fused_step_vs_oracle(layers, readout, monkeypatch):
         assert d <= 1e-4 * float(want.double().norm()) + 1e-9, (n, d, float(want.norm()))
 
 
+def test_fused_step_vs_oracle_hidden128():
+    """hidden 128 (config.json's EMBEDDING_SIZE widened: the k <= 128 GEMMs at their widest) through the fused step,
+    against the CPU oracle as above."""
+    from hgin.smallbatch import SmallBatchStep
+    from oracle.pyg_cpu import OracleHetroGIN, mape
+    store, cfg = _store(8, seed=19)
+    ids = [1, 6, 3]
+    kw = lambda: dict(cfg.model_kwargs({"link": cfg.f_link, "path": cfg.f_path, "node": cfg.f_node}),  # noqa: E731
+                      node_embedding_size=128)
+    torch.manual_seed(1997)
+    m1 = HetroGIN(**kw()).to(DEV)
+    ref = OracleHetroGIN(**kw())
+    ref.load_state_dict({k: v.detach().cpu() for k, v in m1.state_dict().items()})
+    step = SmallBatchStep(m1, torch.optim.Adam(m1.parameters(), lr=0.0, capturable=True), store, batch_size=4,
+                          warmup_ids=[ids], warmup=1)
+    lv = float(step.step(ids))
+    torch.cuda.synchronize()
+    b = _host_batch(store, ids)
+    out = ref(b.x_dict(), b.edge_index_dict(), b.batch["path"])
+    lv_ref = mape(out, b.y.reshape(-1, 1))
+    torch.sqrt(lv_ref).backward()
+    assert abs(lv - float(lv_ref)) <= 1e-5 * abs(float(lv_ref)), (lv, float(lv_ref))
+    for (n, p), (n2, q) in zip(m1.named_parameters(), ref.named_parameters()):
+        assert n == n2
+        want = q.grad if q.grad is not None else torch.zeros_like(q)
+        d = float((p.grad.detach().cpu() - want).double().norm())
+        assert d <= 1e-4 * float(want.double().norm()) + 1e-9, (n, d, float(want.norm()))
+
+
 def test_fused_trajectory_vs_oracle():
     """Five shuffled batches with Adam(lr=1e-3) (train.py:31-44): the fused step's loss trajectory against
     oracle.pyg_cpu.train_step on the host-collated batches, within 1e-4 relative per step."""
@@ -174,4 +203,5 @@ def test_supports_and_refusals():
     assert SmallBatchStep.supports(HetroGIN(**kw()))
     assert not SmallBatchStep.supports(HetroGIN(**kw(global_feats=True, bl_features=True)))
     assert not SmallBatchStep.supports(HetroGIN(**kw(mlp_bn=True)))
-    assert not SmallBatchStep.supports(HetroGIN(**kw(node_embedding_size=128)))
+    assert SmallBatchStep.supports(HetroGIN(**kw(node_embedding_size=128)))
+    assert not SmallBatchStep.supports(HetroGIN(**kw(node_embedding_size=256)))
