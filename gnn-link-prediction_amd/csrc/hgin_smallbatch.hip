@@ -77,6 +77,9 @@ struct SbArgs {
   int L, H;
   SbConv conv[kSbMaxL][kRel];
   int concat_path;
+  int pool_w;               // GLOBAL_FEATS (models.py:347-352): 2 x the sliced path columns ([mean | max]), else 0
+  int pool_ld;              // row stride of `pooled`: 2 x the raw path columns
+  const float* pooled;      // [cap_path][pool_ld]: per row its graph's [mean | max] of every raw path column
   int nhid;
   int rw[kSbMaxHid];        // hidden widths
   const float* row_w[kSbMaxHid];   // [rw[i], in_i]
@@ -382,6 +385,17 @@ struct FastDiv {
 __device__ __forceinline__ FastDiv fast_div(int d) { return {d > 1 ? 0xFFFFFFFFu / (unsigned)d + 1u : 0u, d}; }
 __device__ __forceinline__ int fdq(const FastDiv& f, int n) { return f.d > 1 ? (int)__umulhi((unsigned)n, f.m) : n; }
 
+// column k of path row `row`'s readout input (models.py:362-371): the final path embedding (H columns), then the
+// sliced raw path features when concat_path (fp columns), then GLOBAL_FEATS' [mean | max] of the sliced columns
+// over the row's graph (pool_w = 2 fp columns, read from the pooled rows of every raw column)
+__device__ __forceinline__ float readout_input(const SbArgs& a, const float* xp, int64_t row, int k, int H, int fp) {
+  if (k < H) return xp[row * H + k];
+  if (k < H + fp) return a.x[0][row * a.ldx[0] + a.cols[0][k - H]];
+  const int j = k - H - fp, f = a.pool_w >> 1;
+  const int c = j < f ? a.cols[0][j] : (a.pool_ld >> 1) + a.cols[0][j - f];
+  return a.pooled[row * a.pool_ld + c];
+}
+
 // The readout's parameters into LDS (kWL; otherwise only the offsets / strides of the global rows): per hidden layer
 // W_i [rw_i][win_i | 1] (rows padded to an odd stride: lanes reading different W rows and lanes reading along one
 // are both conflict-free) and b_i [rw_i], then the head's W [KL]; every load of a thread in flight at once (up to
@@ -473,7 +487,7 @@ __global__ __launch_bounds__(kSbThreads) void k_sb_readout(SbArgs a) {
   SB_STAMP(0);
   const int nh = a.nhid;
   const int fp = a.concat_path ? a.fdim[0] : 0;
-  const int w0 = H + fp;
+  const int w0 = H + fp + a.pool_w;
   int win[kSbMaxHid + 1];   // input width of layer i (i = nhid: the head)
   win[0] = w0;
   int maxw = w0;
@@ -518,7 +532,7 @@ __global__ __launch_bounds__(kSbThreads) void k_sb_readout(SbArgs a) {
     for (int idx = tid; idx < nr * w0; idx += kSbThreads) {
       const int rr = idx / w0, k = idx % w0;
       const int64_t row = r0 + rr;
-      const float v = k < H ? xp[row * H + k] : a.x[0][row * a.ldx[0] + a.cols[0][k - H]];
+      const float v = readout_input(a, xp, row, k, H, fp);
       in0[rr * w0 + k] = v;
       a.ro_in[0][(int64_t)r0 * w0 + idx] = v;
     }
@@ -752,7 +766,8 @@ __global__ __launch_bounds__(kRoThreadsM) void k_sb_readout_mfma(SbArgs a) {
   if (tile >= ntile) return;   // (the grid is sized for the capacity; uniform per workgroup)
   SB_STAMP(0);
   const int nh = a.nhid;
-  const int w0 = H + (a.concat_path ? a.fdim[0] : 0);
+  const int fp = a.concat_path ? a.fdim[0] : 0;
+  const int w0 = H + fp + a.pool_w;
   int win[kSbMaxHid + 1];
   win[0] = w0;
   int maxw = w0;
@@ -795,7 +810,7 @@ __global__ __launch_bounds__(kRoThreadsM) void k_sb_readout_mfma(SbArgs a) {
   for (int idx = tid; idx < nr * w0; idx += NT) {
     const int rr = idx / w0, k = idx % w0;
     const int64_t row = r0 + rr;
-    const float v = k < H ? xp[row * H + k] : a.x[0][row * a.ldx[0] + a.cols[0][k - H]];
+    const float v = readout_input(a, xp, row, k, H, fp);
     in0[rr * l0 + k] = v;
     a.ro_in[0][(int64_t)r0 * w0 + idx] = v;
   }
@@ -927,7 +942,7 @@ __host__ __device__ __forceinline__ int ro_groups_nk(int N, int K) {
   return (K + 1 + kRoMK * tk - 1) / (kRoMK * tk);
 }
 __device__ __forceinline__ int ro_in_width(const SbArgs& a, int i) {
-  return i == 0 ? a.H + (a.concat_path ? a.fdim[0] : 0) : a.rw[i - 1];
+  return i == 0 ? a.H + (a.concat_path ? a.fdim[0] : 0) + a.pool_w : a.rw[i - 1];
 }
 __device__ __forceinline__ int ro_groups(const SbArgs& a, int i) {
   return ro_groups_nk(i < a.nhid ? a.rw[i] : 1, ro_in_width(a, i));
@@ -1235,6 +1250,8 @@ extern "C" int hgin_sb_step(const void* args, size_t args_bytes, size_t readout_
   HGIN_ARG_CHECK(a.G >= 1 && a.L >= 1 && a.L <= kSbMaxL && a.H >= 1 && a.H <= 128 && a.nhid >= 1 && a.kmax <= 128 &&
                      a.nhid <= kSbMaxHid && a.n_tiles >= 1 && readout_lds <= 160 * 1024,
                  "hgin_sb_step: unsupported shape");
+  HGIN_ARG_CHECK(a.pool_w == 0 || (a.pooled && a.pool_w == 2 * a.fdim[0] && a.pool_ld >= a.pool_w),
+                 "hgin_sb_step: pooled features (pool_w %d, pool_ld %d)", a.pool_w, a.pool_ld);
   hipStream_t s = as_stream(stream);
   HGIN_TRACE("k_sb_step");
   // the readout kernel's dynamic LDS may use what its static reduction array leaves of the CU's 160 KiB; the limit
@@ -1275,7 +1292,7 @@ extern "C" int hgin_sb_step(const void* args, size_t args_bytes, size_t readout_
   HGIN_ARG_CHECK((int64_t)a.n_tiles * kSbRows >= a.cap[0], "hgin_sb_step: %d readout tiles of %d rows < %d path rows",
                  a.n_tiles, kSbRows, a.cap[0]);
   int ro_blocks = 0;   // the readout weight-gradient blocks' groups (ro_groups, on the host)
-  for (int i = 0, win = a.H + (a.concat_path ? a.fdim[0] : 0); i <= a.nhid; ++i) {
+  for (int i = 0, win = a.H + (a.concat_path ? a.fdim[0] : 0) + a.pool_w; i <= a.nhid; ++i) {
     const int N = i < a.nhid ? a.rw[i] : 1;
     ro_blocks += ro_groups_nk(N, win);
     if (i < a.nhid) win = a.rw[i];

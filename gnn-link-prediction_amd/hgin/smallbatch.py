@@ -45,7 +45,8 @@ class _SbArgs(ctypes.Structure):   # field for field csrc/hgin_smallbatch.hip Sb
                 ("rowptr", _P * REL), ("col", _P * REL), ("cptr", _P * REL), ("cdst", _P * REL),
                 ("goff", _P), ("G", _I32), ("y", _P), ("m_valid", _P),
                 ("L", _I32), ("H", _I32), ("conv", (_SbConv * REL) * MAX_L),
-                ("concat_path", _I32), ("nhid", _I32), ("rw", _I32 * MAX_HID),
+                ("concat_path", _I32), ("pool_w", _I32), ("pool_ld", _I32), ("pooled", _P),
+                ("nhid", _I32), ("rw", _I32 * MAX_HID),
                 ("row_w", _P * MAX_HID), ("row_b", _P * MAX_HID), ("ro_slope", _P), ("head_w", _P), ("head_b", _P),
                 ("ro_goff", _I64 * MAX_HID), ("ro_slope_goff", _I64), ("head_goff", _I64),
                 ("p_gin", _I64), ("p_ro", _I64),
@@ -102,8 +103,8 @@ def _structure(model: torch.nn.Module):
     string when the fused step does not take the model."""
     if type(model) is not HetroGIN:
         return "not a HetroGIN"
-    if model.global_feats or model.dropout > 0.0:
-        return "global features / dropout"
+    if model.dropout > 0.0:
+        return "dropout"
     if not 1 <= model.num_layers <= MAX_L:
         return "layers"
     convs = []
@@ -221,7 +222,11 @@ class SmallBatchStep:
         p_gin = off
         a.concat_path = int(bool(model.concat_path))
         a.nhid = len(hidden)
-        w0 = H + (fdim["path"] if model.concat_path else 0)
+        if model.global_feats:   # models.py:347-352: [mean | max] of the raw path rows per graph, pooled per step
+            if 2 * fdim["path"] != model.global_feats_size:
+                raise ValueError("SmallBatchStep: GLOBAL_FEATS needs 4 path feature columns")
+            a.pool_w, a.pool_ld = 2 * fdim["path"], 2 * raw["path"]
+        w0 = H + (fdim["path"] if model.concat_path else 0) + a.pool_w
         win = w0
         for i, lin in enumerate(hidden):
             if tuple(lin.weight.shape) != (lin.out_features, win):
@@ -297,7 +302,7 @@ class SmallBatchStep:
         # the readout: 32-row tiles on the matrix cores where they fit (HGIN_SB_MFMA=0: the 8-row scalar tiles), else
         # 8-row tiles with the hidden weights in LDS, else without (beside the tile's 1 KiB static array)
         for wl in ((2, 1, 0) if os.environ.get("HGIN_SB_MFMA", "1") != "0" else (1, 0)):
-            _lib.check(_lib.lib().hgin_sb_readout_lds_bytes(H, fdim["path"], a.concat_path, a.nhid, widths, wl,
+            _lib.check(_lib.lib().hgin_sb_readout_lds_bytes(H, w0 - H, int(w0 > H), a.nhid, widths, wl,
                                                             ctypes.byref(lds)), "hgin_sb_readout_lds_bytes")
             if lds.value <= 159 * 1024:
                 break
@@ -317,6 +322,17 @@ class SmallBatchStep:
                       for i in range(a.nhid + 1)]
         for i in range(a.nhid + 1):
             a.ro_in[i], a.ro_gz[i] = P(self.ro_in[i]), P(self.ro_gz[i])
+        self.pool = None
+        if a.pool_w:
+            self.pooled = torch.zeros(cap["path"], a.pool_ld, **f32)
+            a.pooled = P(self.pooled)
+            nb = ctypes.c_size_t(0)
+            _lib.check(_lib.lib().hgin_global_pool_workspace_size(cap["path"], raw["path"], ctypes.byref(nb)),
+                       "hgin_global_pool_workspace_size")
+            ws = torch.empty(max(nb.value, 1), dtype=torch.uint8, device=dev)
+            status = torch.zeros(1, dtype=torch.int32, device=dev)
+            self.pool = (P(pb.batch["path"]), cap["path"], P(pb.x["path"]), pb.x["path"].stride(0), raw["path"],
+                         a.pooled, a.pool_ld, P(status), P(ws), nb.value)
         check_layout()
         self.args, self._keep, self.lds = a, keep, lds.value
         # warm-up on a side stream (optimizer state, allocator pools), then capture the step (+ torch's optimizer
@@ -382,6 +398,8 @@ class SmallBatchStep:
         a.adam_eps, a.weight_decay = float(g["eps"]), float(g["weight_decay"])
 
     def _launch(self) -> None:
+        if self.pool is not None:   # the batch's raw path rows are all that is pooled: one launch ahead of the step
+            _lib.call("hgin_global_pool_f32", *self.pool, ops._stream(self.gflat))
         _lib.call("hgin_sb_step", ctypes.addressof(self.args), ctypes.sizeof(self.args), self.lds,
                   ops._stream(self.gflat))
 

@@ -92,21 +92,27 @@ def test_fused_step_vs_oracle(layers, readout, monkeypatch):
         assert d <= 1e-4 * float(want.double().norm()) + 1e-9, (n, d, float(want.norm()))
 
 
-def test_fused_step_vs_oracle_hidden128():
-    """hidden 128 (config.json's EMBEDDING_SIZE widened: the k <= 128 GEMMs at their widest) through the fused step,
-    against the CPU oracle as above."""
+@pytest.mark.parametrize("variant", ["hidden128", "global_feats", "global_feats_no_concat"])
+def test_fused_step_vs_oracle_variants(variant):
+    """Model variants through the fused step, against the CPU oracle as above: hidden 128 (config.json's
+    EMBEDDING_SIZE widened: the k <= 128 GEMMs at their widest) and GLOBAL_FEATS (models.py:347-352: each path row
+    also reads its graph's [mean | max] of the sliced path features, pooled per step from the batch's raw rows; the
+    padding rows pool as a graph of their own), with and without CONCAT_PATH."""
     from hgin.smallbatch import SmallBatchStep
     from oracle.pyg_cpu import OracleHetroGIN, mape
+    over = {"hidden128": dict(node_embedding_size=128),
+            "global_feats": dict(global_feats=True, bl_features=True),
+            "global_feats_no_concat": dict(global_feats=True, bl_features=True, concat_path=False)}[variant]
     store, cfg = _store(8, seed=19)
     ids = [1, 6, 3]
     kw = lambda: dict(cfg.model_kwargs({"link": cfg.f_link, "path": cfg.f_path, "node": cfg.f_node}),  # noqa: E731
-                      node_embedding_size=128)
+                      **over)
     torch.manual_seed(1997)
     m1 = HetroGIN(**kw()).to(DEV)
     ref = OracleHetroGIN(**kw())
     ref.load_state_dict({k: v.detach().cpu() for k, v in m1.state_dict().items()})
     step = SmallBatchStep(m1, torch.optim.Adam(m1.parameters(), lr=0.0, capturable=True), store, batch_size=4,
-                          warmup_ids=[ids], warmup=1)
+                          warmup_ids=[[0, 2]], warmup=1)
     lv = float(step.step(ids))
     torch.cuda.synchronize()
     b = _host_batch(store, ids)
@@ -201,7 +207,8 @@ def test_supports_and_refusals():
     # (HetroGIN mutates its input_channels dict, as the reference does: a fresh one per model)
     kw = lambda **o: dict(cfg.model_kwargs({"link": 7, "path": 7, "node": 3}), **o)   # noqa: E731
     assert SmallBatchStep.supports(HetroGIN(**kw()))
-    assert not SmallBatchStep.supports(HetroGIN(**kw(global_feats=True, bl_features=True)))
+    assert SmallBatchStep.supports(HetroGIN(**kw(global_feats=True, bl_features=True)))
+    assert not SmallBatchStep.supports(HetroGIN(**kw(dropout=0.1)))
     assert not SmallBatchStep.supports(HetroGIN(**kw(mlp_bn=True)))
     assert SmallBatchStep.supports(HetroGIN(**kw(node_embedding_size=128)))
     assert not SmallBatchStep.supports(HetroGIN(**kw(node_embedding_size=256)))

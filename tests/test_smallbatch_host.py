@@ -22,12 +22,14 @@ def test_supported_models():
     assert SmallBatchStep.supports(HetroGIN(**_kw()))
     assert SmallBatchStep.supports(HetroGIN(**_kw(message_passing_layers=3)))
     assert SmallBatchStep.supports(HetroGIN(**_kw(mlp_layers=[64, 32, 16])))
+    assert SmallBatchStep.supports(HetroGIN(**_kw(global_feats=True, bl_features=True)))
+    assert SmallBatchStep.supports(HetroGIN(**_kw(node_embedding_size=128)))
 
 
 @pytest.mark.parametrize("override,reason", [
-    ({"global_feats": True, "bl_features": True}, "global features"),
+    ({"dropout": 0.1}, "dropout"),
     ({"mlp_bn": True}, "readout layer"),
-    ({"node_embedding_size": 128}, "widths"),
+    ({"node_embedding_size": 256}, "widths"),
     ({"message_passing_layers": 5}, "layers"),
 ])
 def test_refused_models_say_why(override, reason):
