@@ -32,7 +32,8 @@
 // (sequential edge-order fp32 sums: bit-identical); the GEMM-shaped sums and the deferred loss scaling re-associate,
 // so the step agrees with the general path within fp32 tolerances (tests/test_gpu_smallbatch.py).  Limits (checked
 // by the host, hgin/smallbatch.py): H <= 128, every GEMM K <= 128, readout widths <= 256, at most 3 hidden readout
-// layers and 4 GIN layers, fp32.
+// layers and 4 GIN layers, fp32.  GLOBAL_FEATS: the first layer's launch also pools each graph's [mean | max]
+// (sb_pool), which the readout gathers by row; MLP_BN: the readout runs as the k_sb_bn_* launches (below).
 #include "hgin_common.h"
 
 #include <cstddef>
@@ -78,8 +79,9 @@ struct SbArgs {
   SbConv conv[kSbMaxL][kRel];
   int concat_path;
   int pool_w;               // GLOBAL_FEATS (models.py:347-352): 2 x the sliced path columns ([mean | max]), else 0
-  int pool_ld;              // row stride of `pooled`: 2 x the raw path columns
-  const float* pooled;      // [cap_path][pool_ld]: per row its graph's [mean | max] of every raw path column
+  int pool_ld;              // row stride of `pooled`
+  float* pooled;            // [G][pool_ld]: graph g's [mean | max] of the sliced path columns (k_sb_fwd, layer 0)
+  const int64_t* pbatch;    // [cap_path] the path rows' graph ids (PyG's batch vector)
   int nhid;
   int rw[kSbMaxHid];        // hidden widths
   const float* row_w[kSbMaxHid];   // [rw[i], in_i]
@@ -122,6 +124,17 @@ struct SbArgs {
   float* vflat;             // Adam second moments
   float* adam_step;         // [1] Adam's step count (advanced by the step's first launch)
   float lr, beta1, beta2, adam_eps, weight_decay;
+  // MLP_BN (models.py:303-313; ro_wlds 3, the k_sb_bn_* launches): hidden readout layer i = Linear -> BatchNorm1d
+  // (training mode: statistics over the batch's m valid path rows) -> the shared PReLU
+  const float* bn_w[kSbMaxHid];    // gamma [rw_i]
+  const float* bn_b[kSbMaxHid];    // beta [rw_i]
+  float* bn_rm[kSbMaxHid];         // running_mean / running_var, advanced in place once per step
+  float* bn_rv[kSbMaxHid];
+  int64_t* bn_nbt[kSbMaxHid];      // num_batches_tracked
+  int64_t bn_goff[kSbMaxHid];      // flat offsets of gamma's gradients, then beta's
+  float bn_eps, bn_mom;
+  float* bn_buf;                   // scratch, per hidden layer the bn_ptr blocks at bn_off[i][0..4]
+  int64_t bn_off[kSbMaxHid][5];
 };
 
 __device__ __forceinline__ int kdim(const SbArgs& a, int l, int r) {
@@ -295,10 +308,50 @@ constexpr int kSbFwdRows = 32;
 
 constexpr int kSbFwdW = 1024;   // k_sb_fwd stages a relation's W [H][K] in LDS when it has at most this many entries
 
+// GLOBAL_FEATS (models.py:347-352, global_mean_pool / global_max_pool of the sliced path features by the batch
+// vector): the first layer's fourth grid row, a workgroup per graph; the f sliced columns x 256 / f row lanes (rows
+// strided by the lane count), then per column the lanes' (sum, max) in lane order: sum / rows and the max (the first
+// maximum; a NaN propagates, as torch's max).  pooled[g] = [mean | max]; the readout gathers it by row (torch.gather,
+// models.py:350-351).
+__device__ void sb_pool(const SbArgs& a, float* red) {
+  const int f = a.pool_w >> 1, tid = threadIdx.x;
+  const int lanes = kSbThreads / f, c = tid % f, lane = tid / f;
+  for (int g = blockIdx.x; g < a.G; g += gridDim.x) {
+    const int lo = a.goff[g], hi = a.goff[g + 1];
+    float s = 0.0f, m = -INFINITY;
+    if (lane < lanes) {
+      const float* xc = a.x[0] + a.cols[0][c];
+      for (int r = lo + lane; r < hi; r += lanes) {
+        const float v = xc[(int64_t)r * a.ldx[0]];
+        s = __fadd_rn(s, v);
+        if (v > m || v != v) m = v;
+      }
+    }
+    __syncthreads();
+    red[tid] = s;
+    red[kSbThreads + tid] = m;
+    __syncthreads();
+    if (tid < f) {
+      float S = 0.0f, M = -INFINITY;
+      for (int q = 0; q < lanes; ++q) {
+        S = __fadd_rn(S, red[q * f + tid]);
+        const float v = red[kSbThreads + q * f + tid];
+        if (v > M || v != v) M = v;
+      }
+      a.pooled[(int64_t)g * a.pool_ld + tid] = __fdiv_rn(S, (float)(hi - lo));
+      a.pooled[(int64_t)g * a.pool_ld + f + tid] = M;
+    }
+  }
+}
+
 __global__ __launch_bounds__(kSbThreads) void k_sb_fwd(SbArgs a, int l) {
   __shared__ float s_comb[2][kSbFwdRows * 128];   // <= 2 relations into a type, K <= kmax <= 128
   __shared__ float s_w[2][kSbFwdW];
   const int t = blockIdx.y;
+  if (t == 3) {   // (the first layer with GLOBAL_FEATS)
+    sb_pool(a, &s_comb[0][0]);
+    return;
+  }
   const int tid = threadIdx.x;
   const int H = a.H;
   const int n = nrows(a, t);
@@ -391,9 +444,7 @@ __device__ __forceinline__ int fdq(const FastDiv& f, int n) { return f.d > 1 ? (
 __device__ __forceinline__ float readout_input(const SbArgs& a, const float* xp, int64_t row, int k, int H, int fp) {
   if (k < H) return xp[row * H + k];
   if (k < H + fp) return a.x[0][row * a.ldx[0] + a.cols[0][k - H]];
-  const int j = k - H - fp, f = a.pool_w >> 1;
-  const int c = j < f ? a.cols[0][j] : (a.pool_ld >> 1) + a.cols[0][j - f];
-  return a.pooled[row * a.pool_ld + c];
+  return a.pooled[a.pbatch[row] * a.pool_ld + (k - H - fp)];
 }
 
 // The readout's parameters into LDS (kWL; otherwise only the offsets / strides of the global rows): per hidden layer
@@ -922,6 +973,326 @@ __global__ __launch_bounds__(kRoThreadsM) void k_sb_readout_mfma(SbArgs a) {
   SB_STAMP(13);
 }
 
+// ---------------------------------------------------------------------------------------------------------------
+// MLP_BN (models.py:303-313, ro_wlds 3): each hidden readout layer is Linear -> BatchNorm1d -> the shared PReLU, and
+// the BatchNorm's training-mode statistics span the batch's m valid path rows — a reduction over every tile between
+// each layer's GEMM and its activation, forward and backward.  So the readout becomes 2 nhid + 1 launches over the
+// same 32-row tiles (tile_mfma for the GEMMs), each closing a layer at the reduction its successor needs:
+//   k_sb_bn_fwd(i)  layer i's input (i = 0: the readout input; else PReLU(BN(z_{i-1})) with the statistics merged
+//                   from the tiles' partials) -> z_i = W_i in + b_i, and the tile's (sum, M2) partials of z_i;
+//   k_sb_bn_head    the last hidden layer's BN + PReLU, the head, the MAPE numerator and seed (as the unfused
+//                   readout), g_y = PReLU'(y) (go w_head) and the tile's (sum g_y, sum g_y xhat) partials;
+//   k_sb_bn_bwd(i)  g_z = gamma invstd / m (m g_y - sum g_y - xhat sum g_y xhat) (the BatchNorm backward over the
+//                   batch), g_in = g_z W_i, then (i > 0) layer i - 1's g_y and partials, or (i = 0) the path
+//                   embeddings' gradient.
+// Statistics merge in tile order (sum of the tiles' sums; M2 = sum_t M2_t + n_t (mean_t - mean)^2, exact), every block
+// redoing the merge it needs (a few hundred partials: cheaper than a launch); the first block of each records them and
+// advances running_mean / running_var (unbiased, the layer's momentum) and num_batches_tracked once per step.  gamma's
+// and beta's gradients (sum g_y xhat, sum g_y) go to part_ro's first row chunk (the other chunks stay zero), so
+// k_sb_final scales them and folds Adam like every other entry.  Rows past m are never touched.
+constexpr int kBnWMax = 20480;   // a layer's W [N][K | 1] (+ b) is staged in LDS up to this many floats, else read via L2
+constexpr int kBnRed = (kRoThreadsM / 64) * 32 * 33;   // tile_mfma's k-split partials
+
+// bn_buf blocks of hidden layer i: 0 z [cap_path][N], 1 g_y [cap_path][N], 2 forward partials [tiles][2][N] (sum,
+// M2), 3 backward partials [tiles][2][N] (sum g_y, sum g_y xhat), 4 merged statistics [2][N] (mean, invstd)
+__device__ __forceinline__ float* bn_ptr(const SbArgs& a, int i, int k) { return a.bn_buf + a.bn_off[i][k]; }
+
+__host__ __device__ __forceinline__ bool bn_wl(int N, int K) { return N * ((K | 1) + 1) <= kBnWMax; }
+
+// layer i's batch mean / invstd into s_mean / s_inv (N floats each); the first block records them and advances the
+// running statistics
+__device__ void bn_merge_fwd(const SbArgs& a, int i, int m, int ntile, float* s_mean, float* s_inv, bool first) {
+  const int N = a.rw[i];
+  const float* pf = bn_ptr(a, i, 2);
+  float* st = bn_ptr(a, i, 4);
+  for (int c = threadIdx.x; c < N; c += blockDim.x) {
+    float S = 0.0f;
+#pragma unroll 8
+    for (int t = 0; t < ntile; ++t) S = __fadd_rn(S, pf[(int64_t)t * 2 * N + c]);
+    const float mean = __fdiv_rn(S, (float)m);
+    float M2 = 0.0f;
+#pragma unroll 8
+    for (int t = 0; t < ntile; ++t) {
+      const int nt = m - t * kSbRowsM < kSbRowsM ? m - t * kSbRowsM : kSbRowsM;
+      const float d = __fsub_rn(__fdiv_rn(pf[(int64_t)t * 2 * N + c], (float)nt), mean);
+      M2 = __fadd_rn(M2, __fadd_rn(pf[(int64_t)t * 2 * N + N + c], __fmul_rn((float)nt, __fmul_rn(d, d))));
+    }
+    const float var = __fdiv_rn(M2, (float)m);
+    const float inv = __fdiv_rn(1.0f, sqrtf(__fadd_rn(var, a.bn_eps)));
+    s_mean[c] = mean;
+    s_inv[c] = inv;
+    if (first) {
+      st[c] = mean;
+      st[N + c] = inv;
+      const float mo = a.bn_mom, keep = __fsub_rn(1.0f, mo);
+      const float unb = __fdiv_rn(M2, (float)(m - 1));
+      a.bn_rm[i][c] = __fadd_rn(__fmul_rn(keep, a.bn_rm[i][c]), __fmul_rn(mo, mean));
+      a.bn_rv[i][c] = __fadd_rn(__fmul_rn(keep, a.bn_rv[i][c]), __fmul_rn(mo, unb));
+    }
+  }
+  if (first && threadIdx.x == 0) a.bn_nbt[i][0] += 1;
+}
+
+// W_i [N][K] (+ b_i [N] after the rows) into LDS rows of stride K | 1
+__device__ void bn_stage_w(const SbArgs& a, int i, int N, int K, float* s_w, bool with_b) {
+  const int ld = K | 1;
+  for (int idx = threadIdx.x; idx < N * K; idx += blockDim.x) {
+    const int o = idx / K;
+    s_w[o * ld + idx - o * K] = a.row_w[i][idx];
+  }
+  if (with_b)
+    for (int o = threadIdx.x; o < N; o += blockDim.x) s_w[N * ld + o] = a.row_b[i][o];
+}
+
+// LDS floats of each launch (the kernels lay their arrays out in the same order)
+__host__ __device__ __forceinline__ int bn_fwd_floats(int N, int K, int Kp) {
+  return kSbRowsM * (K | 1) + (bn_wl(N, K) ? N * ((K | 1) + 1) : 0) + kSbRowsM * (N | 1) + kBnRed + 2 * Kp;
+}
+__host__ __device__ __forceinline__ int bn_head_floats(int N) { return 2 * N + 2 * kSbRowsM * (N | 1) + kSbRowsM + kRoThreadsM; }
+__host__ __device__ __forceinline__ int bn_bwd_floats(int N, int K, int KG) {
+  return 4 * N + kSbRowsM * (N | 1) + (bn_wl(N, K) ? N * (K | 1) : 0) + kSbRowsM * (KG | 1) + kBnRed + kRoThreadsM;
+}
+
+__global__ __launch_bounds__(kRoThreadsM) void k_sb_bn_fwd(SbArgs a, int i) {
+  extern __shared__ float sm[];
+  constexpr int NT = kRoThreadsM, R = kSbRowsM;
+  const int tid = threadIdx.x;
+  const int m = a.m_valid[0];
+  const int ntile = (m + R - 1) / R;
+  const int tile = blockIdx.x;
+  if (tile >= ntile) return;
+  const int r0 = tile * R, nr = m - r0 < R ? m - r0 : R;
+  const int H = a.H, fp = a.concat_path ? a.fdim[0] : 0;
+  const int K = i == 0 ? H + fp + a.pool_w : a.rw[i - 1];
+  const int N = a.rw[i], lk = K | 1, ln = N | 1;
+  const bool wl = bn_wl(N, K);
+  float* s_in = sm;                                    // [R][lk]
+  float* s_w = s_in + R * lk;                          // [N][lk] + b [N] (wl)
+  float* s_z = s_w + (wl ? N * (lk + 1) : 0);          // [R][ln]
+  float* red = s_z + R * ln;                           // kBnRed
+  float* s_mean = red + kBnRed;                        // [K] (i > 0: layer i - 1's statistics)
+  float* s_inv = s_mean + K;
+  if (i > 0) bn_merge_fwd(a, i - 1, m, ntile, s_mean, s_inv, tile == 0);
+  if (wl) bn_stage_w(a, i, N, K, s_w, true);
+  __syncthreads();
+  float* gin = a.ro_in[i];
+  if (i == 0) {
+    const float* xp = a.act + a.act_off[a.L - 1][0];
+    for (int idx = tid; idx < nr * K; idx += NT) {
+      const int rr = idx / K, k = idx - rr * K;
+      const float v = readout_input(a, xp, r0 + rr, k, H, fp);
+      s_in[rr * lk + k] = v;
+      gin[(int64_t)r0 * K + idx] = v;
+    }
+  } else {
+    const float* zp = bn_ptr(a, i - 1, 0);
+    const float* ga = a.bn_w[i - 1];
+    const float* be = a.bn_b[i - 1];
+    const float slope = a.ro_slope[0];
+    for (int idx = tid; idx < nr * K; idx += NT) {
+      const int rr = idx / K, k = idx - rr * K;
+      const float xh = __fmul_rn(__fsub_rn(zp[(int64_t)r0 * K + idx], s_mean[k]), s_inv[k]);
+      const float y = __fadd_rn(__fmul_rn(xh, ga[k]), be[k]);
+      const float v = y > 0.0f ? y : __fmul_rn(slope, y);
+      s_in[rr * lk + k] = v;
+      gin[(int64_t)r0 * K + idx] = v;
+    }
+  }
+  __syncthreads();
+  const float* Wp = wl ? s_w : a.row_w[i];
+  const float* bp = wl ? s_w + N * lk : a.row_b[i];
+  float* zg = bn_ptr(a, i, 0);
+  tile_mfma<NT>(s_in, lk, nr, Wp, 1, wl ? lk : K, N, K, red, [&](int r, int n, float v) {
+    const float z = __fadd_rn(v, bp[n]);
+    s_z[r * ln + n] = z;
+    zg[(int64_t)(r0 + r) * N + n] = z;
+  });
+  __syncthreads();
+  float* pf = bn_ptr(a, i, 2) + (int64_t)tile * 2 * N;
+  for (int c = tid; c < N; c += NT) {   // the tile's (sum, M2) per column, rows in order
+    float S = 0.0f;
+    for (int r = 0; r < nr; ++r) S = __fadd_rn(S, s_z[r * ln + c]);
+    const float mu = __fdiv_rn(S, (float)nr);
+    float M2 = 0.0f;
+    for (int r = 0; r < nr; ++r) {
+      const float d = __fsub_rn(s_z[r * ln + c], mu);
+      M2 = fmaf(d, d, M2);
+    }
+    pf[c] = S;
+    pf[N + c] = M2;
+  }
+}
+
+// layer i's backward seed from g_a (the gradient of its PReLU output, LDS [nr][lga]): g_y = PReLU'(y) g_a with
+// y = gamma xhat + beta recomputed from z_i and the layer's statistics (st: mean [N], invstd [N]), written to bn_g;
+// the tile's (sum g_y, sum g_y xhat) partials; returns this thread's share of the shared slope's gradient (sum over
+// y <= 0 of g_a y)
+__device__ float bn_seed_bwd(const SbArgs& a, int i, int tile, int r0, int nr, const float* g_a, int lga,
+                             const float* st) {
+  const int N = a.rw[i];
+  const float* zp = bn_ptr(a, i, 0);
+  float* gy = bn_ptr(a, i, 1);
+  float* pb = bn_ptr(a, i, 3) + (int64_t)tile * 2 * N;
+  const float slope = a.ro_slope[0];
+  float sp = 0.0f;
+  for (int c = threadIdx.x; c < N; c += blockDim.x) {
+    const float mean = st[c], inv = st[N + c], ga = a.bn_w[i][c], be = a.bn_b[i][c];
+    float Sg = 0.0f, Sgx = 0.0f;
+    for (int r = 0; r < nr; ++r) {
+      const int64_t q = (int64_t)(r0 + r) * N + c;
+      const float xh = __fmul_rn(__fsub_rn(zp[q], mean), inv);
+      const float y = __fadd_rn(__fmul_rn(xh, ga), be);
+      const float g = g_a[r * lga + c];
+      if (y <= 0.0f) sp = fmaf(g, y, sp);
+      const float gyv = y > 0.0f ? g : __fmul_rn(slope, g);
+      gy[q] = gyv;
+      Sg = __fadd_rn(Sg, gyv);
+      Sgx = fmaf(gyv, xh, Sgx);
+    }
+    pb[c] = Sg;
+    pb[N + c] = Sgx;
+  }
+  return sp;
+}
+
+__global__ __launch_bounds__(kRoThreadsM) void k_sb_bn_head(SbArgs a) {
+  extern __shared__ float sm[];
+  constexpr int NT = kRoThreadsM, R = kSbRowsM;
+  const int tid = threadIdx.x;
+  const int m = a.m_valid[0];
+  const int ntile = (m + R - 1) / R;
+  const int tile = blockIdx.x;
+  if (tile >= ntile) return;
+  const int r0 = tile * R, nr = m - r0 < R ? m - r0 : R;
+  const int nh = a.nhid, N = a.rw[nh - 1], ln = N | 1;
+  float* s_mean = sm;                 // [N]
+  float* s_inv = s_mean + N;          // [N]
+  float* s_a = s_inv + N;             // [R][ln] the activations, then g_a
+  float* s_go = s_a + R * ln;         // [R]
+  float* red1 = s_go + R;             // [NT]
+  bn_merge_fwd(a, nh - 1, m, ntile, s_mean, s_inv, tile == 0);
+  __syncthreads();
+  const float* zp = bn_ptr(a, nh - 1, 0);
+  const float* ga = a.bn_w[nh - 1];
+  const float* be = a.bn_b[nh - 1];
+  const float slope = a.ro_slope[0];
+  float* gin = a.ro_in[nh];
+  for (int idx = tid; idx < nr * N; idx += NT) {
+    const int rr = idx / N, k = idx - rr * N;
+    const float xh = __fmul_rn(__fsub_rn(zp[(int64_t)r0 * N + idx], s_mean[k]), s_inv[k]);
+    const float y = __fadd_rn(__fmul_rn(xh, ga[k]), be[k]);
+    const float v = y > 0.0f ? y : __fmul_rn(slope, y);
+    s_a[rr * ln + k] = v;
+    gin[(int64_t)r0 * N + idx] = v;
+  }
+  __syncthreads();
+  const float* hw = a.head_w;
+  const float head_b = a.head_b[0];
+  {   // head + loss numerator + seed (as k_sb_readout_mfma)
+    const int S = split_of<NT>(nr, N);
+    for (int idx = tid; idx < nr * S; idx += NT) {
+      const int rr = idx / S, s = idx % S;
+      float o = dot_chain(s_a + rr * ln + s, S, hw + s, S, (N - s + S - 1) / S, 0.0f);
+      o = group_sum(o, S);
+      if (s == 0) {
+        o = __fadd_rn(o, head_b);
+        const float yv = a.y[r0 + rr];
+        const float u = __fdiv_rn(__fsub_rn(o, yv), yv);
+        red1[rr] = fabsf(u);
+        const float sg = u > 0.0f ? 1.0f : (u < 0.0f ? -1.0f : 0.0f);
+        const float go = __fdiv_rn(sg, yv);   // d |u| / d out
+        s_go[rr] = go;
+        a.ro_gz[nh][r0 + rr] = go;
+      }
+    }
+  }
+  __syncthreads();
+  if (tid == 0) {
+    float s = 0.0f;
+    for (int rr = 0; rr < nr; ++rr) s = __fadd_rn(s, red1[rr]);
+    a.loss_part[tile] = s;
+  }
+  for (int idx = tid; idx < nr * N; idx += NT) {
+    const int rr = idx / N, k = idx - rr * N;
+    s_a[rr * ln + k] = __fmul_rn(s_go[rr], hw[k]);
+  }
+  __syncthreads();
+  // (the statistics from LDS: the global record is this launch's first block's)
+  const float sp = block_sum<NT>(bn_seed_bwd(a, nh - 1, tile, r0, nr, s_a, ln, s_mean), red1);
+  if (tid == 0) a.slope_part[tile] = sp;
+}
+
+__global__ __launch_bounds__(kRoThreadsM) void k_sb_bn_bwd(SbArgs a, int i) {
+  extern __shared__ float sm[];
+  constexpr int NT = kRoThreadsM, R = kSbRowsM;
+  const int tid = threadIdx.x;
+  const int m = a.m_valid[0];
+  const int ntile = (m + R - 1) / R;
+  const int tile = blockIdx.x;
+  if (tile >= ntile) return;
+  const int r0 = tile * R, nr = m - r0 < R ? m - r0 : R;
+  const int H = a.H, fp = a.concat_path ? a.fdim[0] : 0;
+  const int K = i == 0 ? H + fp + a.pool_w : a.rw[i - 1];
+  const int KG = i == 0 ? H : K;   // (the first layer: only the path embeddings' columns have a gradient)
+  const int N = a.rw[i], ln = N | 1, lk = K | 1, lg = KG | 1;
+  const bool wl = bn_wl(N, K);
+  float* s_c = sm;                    // [4][N]: mean, invstd, sum g_y, sum g_y xhat
+  float* s_gz = s_c + 4 * N;          // [R][ln]
+  float* s_w = s_gz + R * ln;         // [N][lk] (wl)
+  float* s_gi = s_w + (wl ? N * lk : 0);   // [R][lg]
+  float* red = s_gi + R * lg;         // kBnRed
+  float* red1 = red + kBnRed;         // [NT]
+  const float* pb = bn_ptr(a, i, 3);
+  const float* st = bn_ptr(a, i, 4);
+  float* part = a.part_ro - a.p_gin + a.bn_goff[i];   // the first row chunk's gamma, beta entries
+  for (int c = tid; c < N; c += NT) {
+    float Sg = 0.0f, Sgx = 0.0f;
+#pragma unroll 8
+    for (int t = 0; t < ntile; ++t) {
+      Sg = __fadd_rn(Sg, pb[(int64_t)t * 2 * N + c]);
+      Sgx = __fadd_rn(Sgx, pb[(int64_t)t * 2 * N + N + c]);
+    }
+    s_c[c] = st[c];
+    s_c[N + c] = st[N + c];
+    s_c[2 * N + c] = Sg;
+    s_c[3 * N + c] = Sgx;
+    if (tile == 0) {
+      part[c] = Sgx;       // d gamma
+      part[N + c] = Sg;    // d beta
+    }
+  }
+  if (wl) bn_stage_w(a, i, N, K, s_w, false);
+  __syncthreads();
+  const float* zp = bn_ptr(a, i, 0);
+  const float* gy = bn_ptr(a, i, 1);
+  const float fm = (float)m;
+  for (int idx = tid; idx < nr * N; idx += NT) {
+    const int rr = idx / N, c = idx - rr * N;
+    const int64_t q = (int64_t)r0 * N + idx;
+    const float xh = __fmul_rn(__fsub_rn(zp[q], s_c[c]), s_c[N + c]);
+    const float coef = __fdiv_rn(__fmul_rn(a.bn_w[i][c], s_c[N + c]), fm);
+    const float t = __fsub_rn(__fsub_rn(__fmul_rn(fm, gy[q]), s_c[2 * N + c]), __fmul_rn(xh, s_c[3 * N + c]));
+    const float gz = __fmul_rn(coef, t);
+    s_gz[rr * ln + c] = gz;
+    a.ro_gz[i][q] = gz;
+  }
+  __syncthreads();
+  const float* Wp = wl ? s_w : a.row_w[i];
+  tile_mfma<NT>(s_gz, ln, nr, Wp, wl ? lk : K, 1, KG, N, red,
+                [&](int r, int n, float v) { s_gi[r * lg + n] = v; });
+  __syncthreads();
+  if (i == 0) {
+    float* gpath = a.gA + a.g_off[0];
+    for (int idx = tid; idx < nr * H; idx += NT) {
+      const int rr = idx / H, k = idx - rr * H;
+      gpath[(int64_t)r0 * H + idx] = s_gi[rr * lg + k];
+    }
+    return;
+  }
+  const float sp = block_sum<NT>(bn_seed_bwd(a, i - 1, tile, r0, nr, s_gi, lg, bn_ptr(a, i - 1, 4)), red1);
+  if (tid == 0) a.slope_part[tile] = __fadd_rn(a.slope_part[tile], sp);
+}
+
 // the readout blocks of k_sb_bwd_w: over row chunk p of the m valid path rows, one group of layer i's (i = nhid: the
 // head's) partial weight / bias gradients, g_W[o][k] = sum_rows g_z[o] in[k], g_b[o] = sum_rows g_z[o] (the bias as
 // an input column of ones: fmaf(g, 1, v) is the add), the chunk's rows in order (staged as many rows at a time as
@@ -1175,7 +1546,7 @@ __global__ __launch_bounds__(kSbThreads) void k_sb_final(SbArgs a) {
     ad.bc2_sqrt = sqrtf(__fsub_rn(1.0f, powf(a.beta2, st)));
   }
   const int m = a.m_valid[0];
-  const int rows = a.ro_wlds == 2 ? kSbRowsM : kSbRows;   // the readout tiles' rows (one loss / slope partial each)
+  const int rows = a.ro_wlds >= 2 ? kSbRowsM : kSbRows;   // the readout tiles' rows (one loss / slope partial each)
   const int ntile = (m + rows - 1) / rows;
   float lp = 0.0f, sp = 0.0f;
   for (int t = tid; t < ntile; t += kSbThreads) {
@@ -1230,6 +1601,18 @@ extern "C" int hgin_sb_readout_lds_bytes(int64_t H, int64_t f_path, int concat_p
     win = widths[i];
   }
   HGIN_ARG_CHECK(w0 <= kSbMaxW, "hgin_sb_readout_lds_bytes: input width %lld", (long long)w0);
+  if (with_weights == 3) {   // MLP_BN: the largest of the k_sb_bn_* launches
+    int f = 0;
+    for (int i = 0; i < nhid; ++i) {
+      const int K = i == 0 ? (int)w0 : widths[i - 1], N = widths[i];
+      const int fw = bn_fwd_floats(N, K, i > 0 ? K : 0), fb = bn_bwd_floats(N, K, i == 0 ? (int)H : K);
+      f = fw > f ? fw : f;
+      f = fb > f ? fb : f;
+    }
+    const int fh = bn_head_floats(widths[nhid - 1]);
+    *bytes = sizeof(float) * (size_t)(fh > f ? fh : f);
+    return HGIN_OK;
+  }
   if (with_weights == 2) {   // k_sb_readout_mfma: 32-row tiles, odd row strides, the split partials
     int64_t act = w0 | 1;
     for (int i = 0; i < nhid; ++i) act += 2 * (widths[i] | 1);
@@ -1250,7 +1633,7 @@ extern "C" int hgin_sb_step(const void* args, size_t args_bytes, size_t readout_
   HGIN_ARG_CHECK(a.G >= 1 && a.L >= 1 && a.L <= kSbMaxL && a.H >= 1 && a.H <= 128 && a.nhid >= 1 && a.kmax <= 128 &&
                      a.nhid <= kSbMaxHid && a.n_tiles >= 1 && readout_lds <= 160 * 1024,
                  "hgin_sb_step: unsupported shape");
-  HGIN_ARG_CHECK(a.pool_w == 0 || (a.pooled && a.pool_w == 2 * a.fdim[0] && a.pool_ld >= a.pool_w),
+  HGIN_ARG_CHECK(a.pool_w == 0 || (a.pooled && a.pbatch && a.pool_w == 2 * a.fdim[0] && a.pool_ld >= a.pool_w),
                  "hgin_sb_step: pooled features (pool_w %d, pool_ld %d)", a.pool_w, a.pool_ld);
   hipStream_t s = as_stream(stream);
   HGIN_TRACE("k_sb_step");
@@ -1264,7 +1647,9 @@ extern "C" int hgin_sb_step(const void* args, size_t args_bytes, size_t readout_
     int m = 160 * 1024;   // the smaller of the two variants' limits (-1 if either failed)
     for (const void* fn : {reinterpret_cast<const void*>(k_sb_readout<true>),
                            reinterpret_cast<const void*>(k_sb_readout<false>),
-                           reinterpret_cast<const void*>(k_sb_readout_mfma)}) {
+                           reinterpret_cast<const void*>(k_sb_readout_mfma),
+                           reinterpret_cast<const void*>(k_sb_bn_fwd), reinterpret_cast<const void*>(k_sb_bn_head),
+                           reinterpret_cast<const void*>(k_sb_bn_bwd)}) {
       hipFuncAttributes fa;
       int mf = -1;
       if (hipFuncGetAttributes(&fa, fn) == hipSuccess) {
@@ -1298,10 +1683,29 @@ extern "C" int hgin_sb_step(const void* args, size_t args_bytes, size_t readout_
     if (i < a.nhid) win = a.rw[i];
   }
   const unsigned fwd_blocks = (unsigned)ceil_div((int64_t)capt_max, (int64_t)kSbFwdRows);
-  for (int l = 0; l < a.L; ++l) k_sb_fwd<<<dim3(fwd_blocks, 3), kSbThreads, 0, s>>>(a, l);
+  for (int l = 0; l < a.L; ++l) k_sb_fwd<<<dim3(fwd_blocks, l == 0 && a.pool_w ? 4 : 3), kSbThreads, 0, s>>>(a, l);
   // one tile per workgroup (a grid of 512 looping over the tiles, staging the weights once each: 52.9 vs 35 us per
   // batch, profiles/r04/gpu_r — the tiles' serial layer chains want the parallelism, not fewer weight stagings)
-  if (a.ro_wlds == 2)
+  if (a.ro_wlds == 3) {   // MLP_BN: 2 nhid + 1 launches over 32-row tiles (k_sb_bn_*)
+    HGIN_ARG_CHECK(a.bn_buf && a.m_valid, "hgin_sb_step: MLP_BN scratch");
+    const unsigned nt = (unsigned)ceil_div((int64_t)a.cap[0], (int64_t)kSbRowsM);
+    const int w0 = a.H + (a.concat_path ? a.fdim[0] : 0) + a.pool_w;
+    for (int i = 0; i < a.nhid; ++i) {
+      const int K = i == 0 ? w0 : a.rw[i - 1];
+      const size_t lb = sizeof(float) * (size_t)bn_fwd_floats(a.rw[i], K, i > 0 ? K : 0);
+      HGIN_ARG_CHECK((int64_t)lb <= dyn_max, "hgin_sb_step: MLP_BN LDS %zu above %d", lb, dyn_max);
+      k_sb_bn_fwd<<<nt, kRoThreadsM, lb, s>>>(a, i);
+    }
+    const size_t lh = sizeof(float) * (size_t)bn_head_floats(a.rw[a.nhid - 1]);
+    HGIN_ARG_CHECK((int64_t)lh <= dyn_max, "hgin_sb_step: MLP_BN LDS %zu above %d", lh, dyn_max);
+    k_sb_bn_head<<<nt, kRoThreadsM, lh, s>>>(a);
+    for (int i = a.nhid - 1; i >= 0; --i) {
+      const int K = i == 0 ? w0 : a.rw[i - 1];
+      const size_t lb = sizeof(float) * (size_t)bn_bwd_floats(a.rw[i], K, i == 0 ? a.H : K);
+      HGIN_ARG_CHECK((int64_t)lb <= dyn_max, "hgin_sb_step: MLP_BN LDS %zu above %d", lb, dyn_max);
+      k_sb_bn_bwd<<<nt, kRoThreadsM, lb, s>>>(a, i);
+    }
+  } else if (a.ro_wlds == 2)
     k_sb_readout_mfma<<<(unsigned)ceil_div((int64_t)a.n_tiles * kSbRows, (int64_t)kSbRowsM), kRoThreadsM, readout_lds,
                         s>>>(a);
   else if (a.ro_wlds)
@@ -1350,7 +1754,7 @@ extern "C" int hgin_sb_args_offsets(int64_t* out, int64_t n) {
                           (int64_t)offsetof(SbArgs, act_off),  (int64_t)offsetof(SbArgs, zb_off),
                           (int64_t)offsetof(SbArgs, gc_off),   (int64_t)offsetof(SbArgs, n_tiles),
                           (int64_t)offsetof(SbArgs, loss_value), (int64_t)offsetof(SbArgs, adam_step),
-                          (int64_t)offsetof(SbArgs, weight_decay)};
+                          (int64_t)offsetof(SbArgs, weight_decay), (int64_t)offsetof(SbArgs, bn_off)};
   const int64_t k = (int64_t)(sizeof(offs) / sizeof(offs[0]));
   HGIN_ARG_CHECK(out && n >= k, "hgin_sb_args_offsets: need %lld slots", (long long)k);
   for (int64_t i = 0; i < k; ++i) out[i] = offs[i];

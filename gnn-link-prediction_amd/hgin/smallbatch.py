@@ -6,8 +6,10 @@ fixed-order gradient reduction that applies the sqrt-MAPE scale and, for Adam, t
 launches), captured once into a hipGraph and replayed per batch after one device collation launch.
 
 It takes the model train.py builds from config.json (``HetroGIN`` with GINLayer convs, Linear + shared PReLU
-readout, Linear head, no BatchNorm / global features / dropout) at small widths: hidden <= 128, first-layer GEMM
-K <= 128, readout widths <= 256, <= 3 hidden readout layers, <= 4 layers, fp32.  ``SmallBatchStep.supports(model)``
+readout, Linear head) and its GLOBAL_FEATS (one pooling launch ahead of the step, models.py:347-352) and MLP_BN
+(the readout as 2 nhid + 1 launches around the BatchNorm's batch statistics, models.py:303-313) switches, not
+dropout, at small widths: hidden <= 128, first-layer GEMM K <= 128, readout widths <= 256, <= 3 hidden readout
+layers, <= 4 layers, fp32.  ``SmallBatchStep.supports(model)``
 says whether it applies; ``hgin.graphs.CapturedTrainStep`` (one launch per op, any shape) is the general path.
 
 Parameters' ``.grad`` become views of one flat gradient buffer the reduction kernel writes (replays rewrite them in
@@ -45,7 +47,7 @@ class _SbArgs(ctypes.Structure):   # field for field csrc/hgin_smallbatch.hip Sb
                 ("rowptr", _P * REL), ("col", _P * REL), ("cptr", _P * REL), ("cdst", _P * REL),
                 ("goff", _P), ("G", _I32), ("y", _P), ("m_valid", _P),
                 ("L", _I32), ("H", _I32), ("conv", (_SbConv * REL) * MAX_L),
-                ("concat_path", _I32), ("pool_w", _I32), ("pool_ld", _I32), ("pooled", _P),
+                ("concat_path", _I32), ("pool_w", _I32), ("pool_ld", _I32), ("pooled", _P), ("pbatch", _P),
                 ("nhid", _I32), ("rw", _I32 * MAX_HID),
                 ("row_w", _P * MAX_HID), ("row_b", _P * MAX_HID), ("ro_slope", _P), ("head_w", _P), ("head_b", _P),
                 ("ro_goff", _I64 * MAX_HID), ("ro_slope_goff", _I64), ("head_goff", _I64),
@@ -61,11 +63,14 @@ class _SbArgs(ctypes.Structure):   # field for field csrc/hgin_smallbatch.hip Sb
                 ("gflat", _P), ("loss_value", _P),
                 ("pflat", _P), ("mflat", _P), ("vflat", _P), ("adam_step", _P),
                 ("lr", ctypes.c_float), ("beta1", ctypes.c_float), ("beta2", ctypes.c_float),
-                ("adam_eps", ctypes.c_float), ("weight_decay", ctypes.c_float)]
+                ("adam_eps", ctypes.c_float), ("weight_decay", ctypes.c_float),
+                ("bn_w", _P * MAX_HID), ("bn_b", _P * MAX_HID), ("bn_rm", _P * MAX_HID), ("bn_rv", _P * MAX_HID),
+                ("bn_nbt", _P * MAX_HID), ("bn_goff", _I64 * MAX_HID), ("bn_eps", ctypes.c_float),
+                ("bn_mom", ctypes.c_float), ("bn_buf", _P), ("bn_off", (_I64 * 5) * MAX_HID)]
 
 
 _OFFSET_FIELDS = ("goff", "m_valid", "conv", "rw", "ro_goff", "p_ro", "act_off", "zb_off", "gc_off", "n_tiles",
-                  "loss_value", "adam_step", "weight_decay")
+                  "loss_value", "adam_step", "weight_decay", "bn_off")
 
 
 def foldable(opt: torch.optim.Optimizer) -> bool:
@@ -128,8 +133,14 @@ def _structure(model: torch.nn.Module):
             return "relation set"
         convs.append(row)
     ro = list(model.readout)
-    hidden, slope = [], None
+    hidden, slope, bns = [], None, []
     for seq in ro[:-1]:
+        seq = list(seq)
+        bn = None
+        if len(seq) == 3 and type(seq[1]) is torch.nn.BatchNorm1d:   # MLP_BN (models.py:303-313)
+            bn = seq.pop(1)
+            if not (bn.affine and bn.track_running_stats and bn.momentum is not None):
+                return "readout BatchNorm (needs affine, running statistics, a momentum)"
         if not (len(seq) == 2 and isinstance(seq[0], torch.nn.Linear) and isinstance(seq[1], torch.nn.PReLU)
                 and seq[1].weight.numel() == 1):
             return "readout layer"
@@ -137,6 +148,13 @@ def _structure(model: torch.nn.Module):
             return "readout activation not shared"
         slope = seq[1].weight
         hidden.append(seq[0])
+        bns.append(bn)
+    if any(b is None for b in bns):
+        if any(b is not None for b in bns):
+            return "readout BatchNorm on some layers only"
+        bns = None
+    elif len({(b.eps, b.momentum) for b in bns}) != 1:
+        return "readout BatchNorm eps / momentum differ between layers"
     head = ro[-1]
     if not (len(head) == 1 and isinstance(head[0], torch.nn.Linear) and head[0].out_features == 1
             and head[0].bias is not None):
@@ -148,7 +166,7 @@ def _structure(model: torch.nn.Module):
         return "widths"
     if any(p.dtype != torch.float32 for p in model.parameters()):
         return "dtype"
-    return convs, hidden, slope, head[0], H
+    return convs, hidden, slope, head[0], H, bns
 
 
 class SmallBatchStep:
@@ -168,7 +186,7 @@ class SmallBatchStep:
             raise ValueError("SmallBatchStep needs Adam (folded into the step) or a capturable optimizer")
         if not warmup_ids:
             raise ValueError("SmallBatchStep needs at least one warm-up batch")
-        convs, hidden, slope, head, H = st
+        convs, hidden, slope, head, H, bns = st
         self.model, self.opt, self.store = model, opt, store
         dev = store.device
         pb = store.padded_batch(batch_size)
@@ -225,7 +243,7 @@ class SmallBatchStep:
         if model.global_feats:   # models.py:347-352: [mean | max] of the raw path rows per graph, pooled per step
             if 2 * fdim["path"] != model.global_feats_size:
                 raise ValueError("SmallBatchStep: GLOBAL_FEATS needs 4 path feature columns")
-            a.pool_w, a.pool_ld = 2 * fdim["path"], 2 * raw["path"]
+            a.pool_w = a.pool_ld = 2 * fdim["path"]
         w0 = H + (fdim["path"] if model.concat_path else 0) + a.pool_w
         win = w0
         for i, lin in enumerate(hidden):
@@ -237,6 +255,14 @@ class SmallBatchStep:
             param_off[lin.weight] = off
             param_off[lin.bias] = off + lin.weight.numel()
             off += lin.weight.numel() + lin.out_features
+            if bns:   # its BatchNorm's gamma, then beta
+                bn = bns[i]
+                a.bn_w[i], a.bn_b[i] = P(bn.weight), P(bn.bias)
+                a.bn_rm[i], a.bn_rv[i] = P(bn.running_mean), P(bn.running_var)
+                a.bn_nbt[i] = P(bn.num_batches_tracked)
+                a.bn_goff[i] = off
+                param_off[bn.weight], param_off[bn.bias] = off, off + lin.out_features
+                off += 2 * lin.out_features
             win = lin.out_features
         a.ro_slope, a.ro_slope_goff = P(slope), off
         param_off[slope] = off
@@ -296,12 +322,14 @@ class SmallBatchStep:
             o = param_off[p]
             p.grad = self.gflat[o:o + p.numel()].view_as(p)
         if self.folded:
-            self._fold_adam(a, params, param_off, off, convs, hidden, slope, head, L, keep)
+            self._fold_adam(a, params, param_off, off, convs, hidden, slope, head, L, keep, bns)
         widths = (ctypes.c_int32 * MAX_HID)(*[a.rw[i] for i in range(MAX_HID)])
         lds = ctypes.c_size_t(0)
         # the readout: 32-row tiles on the matrix cores where they fit (HGIN_SB_MFMA=0: the 8-row scalar tiles), else
         # 8-row tiles with the hidden weights in LDS, else without (beside the tile's 1 KiB static array)
-        for wl in ((2, 1, 0) if os.environ.get("HGIN_SB_MFMA", "1") != "0" else (1, 0)):
+        # (MLP_BN: the k_sb_bn_* launches, mode 3)
+        modes = (3,) if bns else ((2, 1, 0) if os.environ.get("HGIN_SB_MFMA", "1") != "0" else (1, 0))
+        for wl in modes:
             _lib.check(_lib.lib().hgin_sb_readout_lds_bytes(H, w0 - H, int(w0 > H), a.nhid, widths, wl,
                                                             ctypes.byref(lds)), "hgin_sb_readout_lds_bytes")
             if lds.value <= 159 * 1024:
@@ -322,17 +350,21 @@ class SmallBatchStep:
                       for i in range(a.nhid + 1)]
         for i in range(a.nhid + 1):
             a.ro_in[i], a.ro_gz[i] = P(self.ro_in[i]), P(self.ro_gz[i])
-        self.pool = None
-        if a.pool_w:
-            self.pooled = torch.zeros(cap["path"], a.pool_ld, **f32)
-            a.pooled = P(self.pooled)
-            nb = ctypes.c_size_t(0)
-            _lib.check(_lib.lib().hgin_global_pool_workspace_size(cap["path"], raw["path"], ctypes.byref(nb)),
-                       "hgin_global_pool_workspace_size")
-            ws = torch.empty(max(nb.value, 1), dtype=torch.uint8, device=dev)
-            status = torch.zeros(1, dtype=torch.int32, device=dev)
-            self.pool = (P(pb.batch["path"]), cap["path"], P(pb.x["path"]), pb.x["path"].stride(0), raw["path"],
-                         a.pooled, a.pool_ld, P(status), P(ws), nb.value)
+        if bns:   # per hidden layer: z, g_y [cap_path][N], forward / backward tile partials [tiles][2][N], statistics
+            nt32 = (cap["path"] + 31) // 32
+            sizes = []
+            for i in range(a.nhid):
+                N = a.rw[i]
+                sizes += [cap["path"] * N, cap["path"] * N, nt32 * 2 * N, nt32 * 2 * N, 2 * N]
+            o, self.bn_buf = blocks(sizes)
+            a.bn_buf = P(self.bn_buf)
+            for i in range(a.nhid):
+                for k in range(5):
+                    a.bn_off[i][k] = o[5 * i + k]
+            a.bn_eps, a.bn_mom = float(bns[0].eps), float(bns[0].momentum)
+        if a.pool_w:   # per graph [mean | max], formed by the first layer's launch
+            self.pooled = torch.zeros(batch_size, a.pool_ld, **f32)
+            a.pooled, a.pbatch = P(self.pooled), P(pb.batch["path"])
         check_layout()
         self.args, self._keep, self.lds = a, keep, lds.value
         # warm-up on a side stream (optimizer state, allocator pools), then capture the step (+ torch's optimizer
@@ -353,7 +385,7 @@ class SmallBatchStep:
             if not self.folded:
                 opt.step()
 
-    def _fold_adam(self, a, params, param_off, total, convs, hidden, slope, head, L, keep) -> None:
+    def _fold_adam(self, a, params, param_off, total, convs, hidden, slope, head, L, keep, bns) -> None:
         """The parameters become views of one flat buffer in the gradient layout, Adam's moments two more and its
         step count one device scalar; the optimizer's state entries are re-pointed at them (its existing state, if
         any, copied in), so opt.state_dict() stays meaningful.  The step then owns the optimizer: calling
@@ -390,6 +422,8 @@ class SmallBatchStep:
                 c.w, c.b, c.slope, c.eps = lin.weight.data_ptr(), lin.bias.data_ptr(), pw.data_ptr(), eps.data_ptr()
         for i, lin in enumerate(hidden):
             a.row_w[i], a.row_b[i] = lin.weight.data_ptr(), lin.bias.data_ptr()
+            if bns:
+                a.bn_w[i], a.bn_b[i] = bns[i].weight.data_ptr(), bns[i].bias.data_ptr()
         a.ro_slope, a.head_w, a.head_b = slope.data_ptr(), head.weight.data_ptr(), head.bias.data_ptr()
         keep += [self.pflat, self.mflat, self.vflat, self.adam_step]
         a.pflat, a.mflat, a.vflat = self.pflat.data_ptr(), self.mflat.data_ptr(), self.vflat.data_ptr()
@@ -398,8 +432,6 @@ class SmallBatchStep:
         a.adam_eps, a.weight_decay = float(g["eps"]), float(g["weight_decay"])
 
     def _launch(self) -> None:
-        if self.pool is not None:   # the batch's raw path rows are all that is pooled: one launch ahead of the step
-            _lib.call("hgin_global_pool_f32", *self.pool, ops._stream(self.gflat))
         _lib.call("hgin_sb_step", ctypes.addressof(self.args), ctypes.sizeof(self.args), self.lds,
                   ops._stream(self.gflat))
 

@@ -92,27 +92,36 @@ def test_fused_step_vs_oracle(layers, readout, monkeypatch):
         assert d <= 1e-4 * float(want.double().norm()) + 1e-9, (n, d, float(want.norm()))
 
 
-@pytest.mark.parametrize("variant", ["hidden128", "global_feats", "global_feats_no_concat"])
+@pytest.mark.parametrize("variant", ["hidden128", "global_feats", "global_feats_no_concat", "mlp_bn",
+                                     "mlp_bn_global_feats", "mlp_bn_3hid"])
 def test_fused_step_vs_oracle_variants(variant):
     """Model variants through the fused step, against the CPU oracle as above: hidden 128 (config.json's
-    EMBEDDING_SIZE widened: the k <= 128 GEMMs at their widest) and GLOBAL_FEATS (models.py:347-352: each path row
+    EMBEDDING_SIZE widened: the k <= 128 GEMMs at their widest), GLOBAL_FEATS (models.py:347-352: each path row
     also reads its graph's [mean | max] of the sliced path features, pooled per step from the batch's raw rows; the
-    padding rows pool as a graph of their own), with and without CONCAT_PATH."""
+    padding rows pool as a graph of their own) with and without CONCAT_PATH, and MLP_BN (models.py:303-313:
+    training-mode BatchNorm1d over the batch's rows between each hidden Linear and the PReLU; the k_sb_bn_* launches)
+    — its running statistics and num_batches_tracked against the oracle's BatchNorm after the same step too.  With
+    BatchNorm the hidden Linears' biases have a zero gradient in exact arithmetic (the normalisation removes them), so
+    the gradient bound adds 1e-6 of the largest gradient norm."""
     from hgin.smallbatch import SmallBatchStep
     from oracle.pyg_cpu import OracleHetroGIN, mape
     over = {"hidden128": dict(node_embedding_size=128),
             "global_feats": dict(global_feats=True, bl_features=True),
-            "global_feats_no_concat": dict(global_feats=True, bl_features=True, concat_path=False)}[variant]
+            "global_feats_no_concat": dict(global_feats=True, bl_features=True, concat_path=False),
+            "mlp_bn": dict(mlp_bn=True),
+            "mlp_bn_global_feats": dict(mlp_bn=True, global_feats=True, bl_features=True),
+            "mlp_bn_3hid": dict(mlp_bn=True, mlp_layers=[64, 48, 16])}[variant]
     store, cfg = _store(8, seed=19)
     ids = [1, 6, 3]
     kw = lambda: dict(cfg.model_kwargs({"link": cfg.f_link, "path": cfg.f_path, "node": cfg.f_node}),  # noqa: E731
                       **over)
     torch.manual_seed(1997)
     m1 = HetroGIN(**kw()).to(DEV)
-    ref = OracleHetroGIN(**kw())
-    ref.load_state_dict({k: v.detach().cpu() for k, v in m1.state_dict().items()})
     step = SmallBatchStep(m1, torch.optim.Adam(m1.parameters(), lr=0.0, capturable=True), store, batch_size=4,
                           warmup_ids=[[0, 2]], warmup=1)
+    torch.cuda.synchronize()
+    ref = OracleHetroGIN(**kw())   # (after the warm-up step, which advanced MLP_BN's running statistics)
+    ref.load_state_dict({k: v.detach().cpu() for k, v in m1.state_dict().items()})
     lv = float(step.step(ids))
     torch.cuda.synchronize()
     b = _host_batch(store, ids)
@@ -120,22 +129,83 @@ def test_fused_step_vs_oracle_variants(variant):
     lv_ref = mape(out, b.y.reshape(-1, 1))
     torch.sqrt(lv_ref).backward()
     assert abs(lv - float(lv_ref)) <= 1e-5 * abs(float(lv_ref)), (lv, float(lv_ref))
+    gmax = max(float(q.grad.double().norm()) for q in ref.parameters() if q.grad is not None)
+    slack = 1e-6 * gmax if "mlp_bn" in variant else 1e-9
     for (n, p), (n2, q) in zip(m1.named_parameters(), ref.named_parameters()):
         assert n == n2
         want = q.grad if q.grad is not None else torch.zeros_like(q)
         d = float((p.grad.detach().cpu() - want).double().norm())
-        assert d <= 1e-4 * float(want.double().norm()) + 1e-9, (n, d, float(want.norm()))
+        assert d <= 1e-4 * float(want.double().norm()) + slack, (n, d, float(want.norm()))
+    for (n, u), (n2, v) in zip(m1.named_buffers(), ref.named_buffers()):
+        assert n == n2
+        if v.dtype == torch.int64:
+            assert torch.equal(u.cpu(), v), n
+        else:
+            assert torch.allclose(u.cpu(), v, rtol=1e-5, atol=1e-6), (n, float((u.cpu() - v).abs().max()))
 
 
-def test_fused_trajectory_vs_oracle():
-    """Five shuffled batches with Adam(lr=1e-3) (train.py:31-44): the fused step's loss trajectory against
-    oracle.pyg_cpu.train_step on the host-collated batches, within 1e-4 relative per step."""
+def test_fused_step_vs_reference_fixture_global_bn():
+    """The reference-executed fixture tests/golden/collate2_global_bn.pt (models.py run on two graphs collated
+    PyG-style, GLOBAL_FEATS + MLP_BN: tests/golden/make_golden.py) through the fused step.  The two graphs are
+    regenerated by the committed generator (seeds 4 and 5) and their device collation is bit-identical to the
+    fixture's inputs; then one step (Adam at lr 0): the loss within 1e-5 relative, every gradient within 1e-4 of its
+    norm plus 1e-6 of the largest (the BatchNorm-fed Linear biases are zero in exact arithmetic: rounding noise on
+    both sides), the reference's gradient-free (dead) relations exactly zero."""
+    import dataclasses
+
+    from conftest import fixture_model_kwargs, fixture_state_dict, load_fixture
     from hgin.smallbatch import SmallBatchStep
+    fx = load_fixture("collate2_global_bn")
+    cfg = dataclasses.replace(CONFIGS["cfg1"], bl_features=True)
+    store = GraphStore.build([synthetic_graph(cfg, seed=4), synthetic_graph(cfg, seed=5)], device=DEV,
+                             normalize=False)
+    b = store.collate([0, 1]).to("cpu")
+    for t in ("path", "link", "node"):
+        assert torch.equal(b.x[t], fx[f"in.x.{t}"]), t
+    for r in fx["meta"]["relations"]:
+        assert torch.equal(b.edge_index[tuple(r.split("__"))], fx[f"in.ei.{r}"]), r
+    assert torch.equal(b.y, fx["in.y"]) and torch.equal(b.batch["path"], fx["in.batch"])
+    model = HetroGIN(**fixture_model_kwargs(fx))
+    model.load_state_dict(fixture_state_dict(fx))
+    model = model.to(DEV)
+    step = SmallBatchStep(model, torch.optim.Adam(model.parameters(), lr=0.0, capturable=True), store, batch_size=2,
+                          warmup_ids=[[1, 0]], warmup=1)
+    assert step.args.ro_wlds == 3 and step.args.pool_w == 8
+    lv = float(step.step([0, 1]))
+    torch.cuda.synchronize()
+    want = float(fx["loss_value"])
+    assert abs(lv - want) <= 1e-5 * abs(want), (lv, want)
+    no_grad = set(fx["meta"]["no_grad_params"])
+    g_scale = max(float(fx["grad." + n].double().norm()) for n, _ in model.named_parameters() if n not in no_grad)
+    for n, p in model.named_parameters():
+        g = p.grad.detach().cpu()
+        if n in no_grad:
+            assert not g.any(), n
+            continue
+        ref = fx["grad." + n]
+        err = float((g.double() - ref.double()).norm())
+        assert err <= 1e-4 * float(ref.double().norm()) + 1e-6 * g_scale, (n, err, float(ref.norm()))
+
+
+@pytest.mark.parametrize("variant", ["default", "mlp_bn_global_feats"])
+def test_fused_trajectory_vs_oracle(variant):
+    """Five shuffled batches with Adam(lr=1e-3) (train.py:31-44): the fused step's loss trajectory against
+    oracle.pyg_cpu.train_step on the host-collated batches, within 1e-4 relative per step; with GLOBAL_FEATS + MLP_BN
+    the BatchNorm running statistics after the last step too (variances within 1e-3 of their norm: by then they
+    summarise parameters that fp32 re-association has moved apart; means within Adam's sign-noise bound on the
+    pre-BatchNorm biases; the one-step test holds both to 1e-5)."""
+    from hgin.smallbatch import SmallBatchStep
+    from oracle.pyg_cpu import OracleHetroGIN
     from oracle.pyg_cpu import train_step as oracle_step
     store, cfg = _store(12, seed=13)
     seq = [[1, 6, 10], [4, 0, 11], [8, 3, 5], [9, 7, 2], [3, 10, 1]]
-    m1 = _model(cfg)
-    ref = _oracle_twin(m1, cfg)
+    over = {} if variant == "default" else dict(mlp_bn=True, global_feats=True, bl_features=True)
+    kw = lambda: dict(cfg.model_kwargs({"link": cfg.f_link, "path": cfg.f_path, "node": cfg.f_node}),  # noqa: E731
+                      **over)
+    torch.manual_seed(1997)
+    m1 = HetroGIN(**kw()).to(DEV)
+    ref = OracleHetroGIN(**kw())
+    ref.load_state_dict({k: v.detach().cpu() for k, v in m1.state_dict().items()})
     o1 = torch.optim.Adam(m1.parameters(), lr=1e-3, capturable=True)
     step = SmallBatchStep(m1, o1, store, batch_size=3, warmup_ids=[seq[0]], warmup=1)
     o2 = torch.optim.Adam(ref.parameters(), lr=1e-3)
@@ -148,6 +218,18 @@ def test_fused_trajectory_vs_oracle():
     for k, ids in enumerate(seq):
         got, want = float(step.step(ids)), oracle(ids)
         assert abs(got - want) <= 1e-4 * abs(want), (k, got, want)
+    for (n, u), (n2, v) in zip(m1.named_buffers(), ref.named_buffers()):
+        assert n == n2
+        if v.dtype == torch.int64:
+            assert torch.equal(u.cpu(), v), n
+        elif n.endswith("running_mean"):
+            # the Linear biases ahead of a BatchNorm have rounding-noise gradients, which Adam turns into +-lr steps
+            # of either sign: over the six steps each bias (and so each batch mean of z) may differ by 2 lr per step
+            d = float((u.cpu() - v).abs().max())
+            assert d <= 2 * 1e-3 * 6 + 1e-3 * float(v.abs().max()), (n, d)
+        else:   # (the variances see no bias shift: the parameters' fp32 drift only)
+            d = float((u.cpu() - v).double().norm())
+            assert d <= 1e-3 * float(v.double().norm()) + 1e-6, (n, d, float(v.norm()))
 
 
 @pytest.mark.parametrize("layers", [2, 1, 3])
@@ -209,6 +291,6 @@ def test_supports_and_refusals():
     assert SmallBatchStep.supports(HetroGIN(**kw()))
     assert SmallBatchStep.supports(HetroGIN(**kw(global_feats=True, bl_features=True)))
     assert not SmallBatchStep.supports(HetroGIN(**kw(dropout=0.1)))
-    assert not SmallBatchStep.supports(HetroGIN(**kw(mlp_bn=True)))
+    assert SmallBatchStep.supports(HetroGIN(**kw(mlp_bn=True)))
     assert SmallBatchStep.supports(HetroGIN(**kw(node_embedding_size=128)))
     assert not SmallBatchStep.supports(HetroGIN(**kw(node_embedding_size=256)))

@@ -24,11 +24,12 @@ def test_supported_models():
     assert SmallBatchStep.supports(HetroGIN(**_kw(mlp_layers=[64, 32, 16])))
     assert SmallBatchStep.supports(HetroGIN(**_kw(global_feats=True, bl_features=True)))
     assert SmallBatchStep.supports(HetroGIN(**_kw(node_embedding_size=128)))
+    assert SmallBatchStep.supports(HetroGIN(**_kw(mlp_bn=True, global_feats=True, bl_features=True)))
 
 
 @pytest.mark.parametrize("override,reason", [
     ({"dropout": 0.1}, "dropout"),
-    ({"mlp_bn": True}, "readout layer"),
+    ({"mlp_head_act": "torch.nn.PReLU()"}, "head"),
     ({"node_embedding_size": 256}, "widths"),
     ({"message_passing_layers": 5}, "layers"),
 ])

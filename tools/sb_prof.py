@@ -20,6 +20,7 @@ def main():
     from hgin.store import GraphStore
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--model", default="{}", help='HetroGIN keyword overrides as JSON, e.g. {"mlp_bn": true}')
     args = ap.parse_args()
     dev = torch.device("cuda")
     base = CONFIGS["cfg1"]
@@ -29,7 +30,9 @@ def main():
     store = GraphStore.build(graphs, device=dev, normalize=True)
     order = [rng.choice(256, 8, replace=False).tolist() for _ in range(5 + args.steps)]
     torch.manual_seed(1997)
-    model = HetroGIN(**base.model_kwargs({"link": base.f_link, "path": base.f_path, "node": base.f_node})).to(dev)
+    kw = dict(base.model_kwargs({"link": base.f_link, "path": base.f_path, "node": base.f_node}),
+              **json.loads(args.model))
+    model = HetroGIN(**kw).to(dev)
     opt = torch.optim.Adam(lr=1e-3, params=model.parameters())
     st = SmallBatchStep(model, opt, store, 8, warmup_ids=order[:5], warmup=5)
     torch.cuda.synchronize()
@@ -39,7 +42,7 @@ def main():
         st.step(ids)
     e.record()
     torch.cuda.synchronize()
-    print(json.dumps({"ms_per_batch": s.elapsed_time(e) / args.steps}), flush=True)
+    print(json.dumps({"model": json.loads(args.model), "ms_per_batch": s.elapsed_time(e) / args.steps}), flush=True)
 
 
 if __name__ == "__main__":
