@@ -979,58 +979,77 @@ __global__ __launch_bounds__(kRoThreadsM) void k_sb_readout_mfma(SbArgs a) {
 // each layer's GEMM and its activation, forward and backward.  So the readout becomes 2 nhid + 1 launches over the
 // same 32-row tiles (tile_mfma for the GEMMs), each closing a layer at the reduction its successor needs:
 //   k_sb_bn_fwd(i)  layer i's input (i = 0: the readout input; else PReLU(BN(z_{i-1})) with the statistics merged
-//                   from the tiles' partials) -> z_i = W_i in + b_i, and the tile's (sum, M2) partials of z_i;
+//                   from the tiles' partials) -> z_i = W_i in + b_i, and the tile's (mean, M2) partials of z_i;
 //   k_sb_bn_head    the last hidden layer's BN + PReLU, the head, the MAPE numerator and seed (as the unfused
 //                   readout), g_y = PReLU'(y) (go w_head) and the tile's (sum g_y, sum g_y xhat) partials;
 //   k_sb_bn_bwd(i)  g_z = gamma invstd / m (m g_y - sum g_y - xhat sum g_y xhat) (the BatchNorm backward over the
 //                   batch), g_in = g_z W_i, then (i > 0) layer i - 1's g_y and partials, or (i = 0) the path
 //                   embeddings' gradient.
-// Statistics merge in tile order (sum of the tiles' sums; M2 = sum_t M2_t + n_t (mean_t - mean)^2, exact), every block
-// redoing the merge it needs (a few hundred partials: cheaper than a launch); the first block of each records them and
+// Statistics merge in a fixed order (Chan's pairwise (n, mean, M2) update, bn_merge_fwd), every block redoing the
+// merge it needs (a few hundred partials: cheaper than a launch); the first block of each records them and
 // advances running_mean / running_var (unbiased, the layer's momentum) and num_batches_tracked once per step.  gamma's
 // and beta's gradients (sum g_y xhat, sum g_y) go to part_ro's first row chunk (the other chunks stay zero), so
 // k_sb_final scales them and folds Adam like every other entry.  Rows past m are never touched.
 constexpr int kBnWMax = 20480;   // a layer's W [N][K | 1] (+ b) is staged in LDS up to this many floats, else read via L2
 constexpr int kBnRed = (kRoThreadsM / 64) * 32 * 33;   // tile_mfma's k-split partials
 
-// bn_buf blocks of hidden layer i: 0 z [cap_path][N], 1 g_y [cap_path][N], 2 forward partials [tiles][2][N] (sum,
+// bn_buf blocks of hidden layer i: 0 z [cap_path][N], 1 g_y [cap_path][N], 2 forward partials [tiles][2][N] (mean,
 // M2), 3 backward partials [tiles][2][N] (sum g_y, sum g_y xhat), 4 merged statistics [2][N] (mean, invstd)
 __device__ __forceinline__ float* bn_ptr(const SbArgs& a, int i, int k) { return a.bn_buf + a.bn_off[i][k]; }
 
 __host__ __device__ __forceinline__ bool bn_wl(int N, int K) { return N * ((K | 1) + 1) <= kBnWMax; }
 
-// layer i's batch mean / invstd into s_mean / s_inv (N floats each); the first block records them and advances the
-// running statistics
-__device__ void bn_merge_fwd(const SbArgs& a, int i, int m, int ntile, float* s_mean, float* s_inv, bool first) {
-  const int N = a.rw[i];
+// layer i's batch mean / invstd into s_mean / s_inv (N floats each) from the tiles' (mean, M2) partials: the
+// NT / N thread groups each merge every (NT / N)-th tile in order, then the groups' results merge in group order
+// (Chan et al.'s pairwise update: n = na + nb, d = mb - ma, mean = ma + d nb / n, M2 = M2a + M2b + d^2 na nb / n) —
+// a handful of loads in flight per thread instead of a few hundred dependent ones per column.  The first block
+// records the statistics and advances the running statistics.  red: 3 NT floats.
+__device__ __forceinline__ void chan_merge(float& n, float& mu, float& M2, float nb, float mb, float M2b) {
+  const float nn = __fadd_rn(n, nb);
+  const float d = __fsub_rn(mb, mu);
+  const float r = __fdiv_rn(nb, nn);
+  mu = __fadd_rn(mu, __fmul_rn(d, r));
+  M2 = __fadd_rn(__fadd_rn(M2, M2b), __fmul_rn(__fmul_rn(__fmul_rn(d, d), n), r));
+  n = nn;
+}
+__device__ void bn_merge_fwd(const SbArgs& a, int i, int m, int ntile, float* s_mean, float* s_inv, bool first,
+                             float* red) {
+  const int N = a.rw[i], NT = blockDim.x, tid = threadIdx.x;
+  const int P = NT / N, c = tid % N, p = tid / N;
   const float* pf = bn_ptr(a, i, 2);
-  float* st = bn_ptr(a, i, 4);
-  for (int c = threadIdx.x; c < N; c += blockDim.x) {
-    float S = 0.0f;
-#pragma unroll 8
-    for (int t = 0; t < ntile; ++t) S = __fadd_rn(S, pf[(int64_t)t * 2 * N + c]);
-    const float mean = __fdiv_rn(S, (float)m);
-    float M2 = 0.0f;
-#pragma unroll 8
-    for (int t = 0; t < ntile; ++t) {
-      const int nt = m - t * kSbRowsM < kSbRowsM ? m - t * kSbRowsM : kSbRowsM;
-      const float d = __fsub_rn(__fdiv_rn(pf[(int64_t)t * 2 * N + c], (float)nt), mean);
-      M2 = __fadd_rn(M2, __fadd_rn(pf[(int64_t)t * 2 * N + N + c], __fmul_rn((float)nt, __fmul_rn(d, d))));
-    }
-    const float var = __fdiv_rn(M2, (float)m);
-    const float inv = __fdiv_rn(1.0f, sqrtf(__fadd_rn(var, a.bn_eps)));
-    s_mean[c] = mean;
-    s_inv[c] = inv;
-    if (first) {
-      st[c] = mean;
-      st[N + c] = inv;
-      const float mo = a.bn_mom, keep = __fsub_rn(1.0f, mo);
-      const float unb = __fdiv_rn(M2, (float)(m - 1));
-      a.bn_rm[i][c] = __fadd_rn(__fmul_rn(keep, a.bn_rm[i][c]), __fmul_rn(mo, mean));
-      a.bn_rv[i][c] = __fadd_rn(__fmul_rn(keep, a.bn_rv[i][c]), __fmul_rn(mo, unb));
+  float n = 0.0f, mu = 0.0f, M2 = 0.0f;
+  if (p < P) {
+#pragma unroll 4
+    for (int t = p; t < ntile; t += P) {
+      const float nt = (float)(m - t * kSbRowsM < kSbRowsM ? m - t * kSbRowsM : kSbRowsM);
+      chan_merge(n, mu, M2, nt, pf[(int64_t)t * 2 * N + c], pf[(int64_t)t * 2 * N + N + c]);
     }
   }
-  if (first && threadIdx.x == 0) a.bn_nbt[i][0] += 1;
+  __syncthreads();
+  red[tid] = n;
+  red[NT + tid] = mu;
+  red[2 * NT + tid] = M2;
+  __syncthreads();
+  if (tid < N) {
+    float gn = 0.0f, gm = 0.0f, g2 = 0.0f;
+    for (int q = 0; q < P; ++q)
+      if (red[q * N + tid] > 0.0f) chan_merge(gn, gm, g2, red[q * N + tid], red[NT + q * N + tid], red[2 * NT + q * N + tid]);
+    const float var = __fdiv_rn(g2, (float)m);
+    const float inv = __fdiv_rn(1.0f, sqrtf(__fadd_rn(var, a.bn_eps)));
+    s_mean[tid] = gm;
+    s_inv[tid] = inv;
+    if (first) {
+      float* st = bn_ptr(a, i, 4);
+      st[tid] = gm;
+      st[N + tid] = inv;
+      const float mo = a.bn_mom, keep = __fsub_rn(1.0f, mo);
+      const float unb = __fdiv_rn(g2, (float)(m - 1));
+      a.bn_rm[i][tid] = __fadd_rn(__fmul_rn(keep, a.bn_rm[i][tid]), __fmul_rn(mo, gm));
+      a.bn_rv[i][tid] = __fadd_rn(__fmul_rn(keep, a.bn_rv[i][tid]), __fmul_rn(mo, unb));
+    }
+  }
+  if (first && tid == 0) a.bn_nbt[i][0] += 1;
+  __syncthreads();
 }
 
 // W_i [N][K] (+ b_i [N] after the rows) into LDS rows of stride K | 1
@@ -1048,7 +1067,7 @@ __device__ void bn_stage_w(const SbArgs& a, int i, int N, int K, float* s_w, boo
 __host__ __device__ __forceinline__ int bn_fwd_floats(int N, int K, int Kp) {
   return kSbRowsM * (K | 1) + (bn_wl(N, K) ? N * ((K | 1) + 1) : 0) + kSbRowsM * (N | 1) + kBnRed + 2 * Kp;
 }
-__host__ __device__ __forceinline__ int bn_head_floats(int N) { return 2 * N + 2 * kSbRowsM * (N | 1) + kSbRowsM + kRoThreadsM; }
+__host__ __device__ __forceinline__ int bn_head_floats(int N) { return 2 * N + kSbRowsM * (N | 1) + kSbRowsM + 3 * kRoThreadsM; }
 __host__ __device__ __forceinline__ int bn_bwd_floats(int N, int K, int KG) {
   return 4 * N + kSbRowsM * (N | 1) + (bn_wl(N, K) ? N * (K | 1) : 0) + kSbRowsM * (KG | 1) + kBnRed + kRoThreadsM;
 }
@@ -1072,7 +1091,7 @@ __global__ __launch_bounds__(kRoThreadsM) void k_sb_bn_fwd(SbArgs a, int i) {
   float* red = s_z + R * ln;                           // kBnRed
   float* s_mean = red + kBnRed;                        // [K] (i > 0: layer i - 1's statistics)
   float* s_inv = s_mean + K;
-  if (i > 0) bn_merge_fwd(a, i - 1, m, ntile, s_mean, s_inv, tile == 0);
+  if (i > 0) bn_merge_fwd(a, i - 1, m, ntile, s_mean, s_inv, tile == 0, red);
   if (wl) bn_stage_w(a, i, N, K, s_w, true);
   __syncthreads();
   float* gin = a.ro_in[i];
@@ -1118,27 +1137,29 @@ __global__ __launch_bounds__(kRoThreadsM) void k_sb_bn_fwd(SbArgs a, int i) {
       const float d = __fsub_rn(s_z[r * ln + c], mu);
       M2 = fmaf(d, d, M2);
     }
-    pf[c] = S;
+    pf[c] = mu;
     pf[N + c] = M2;
   }
 }
 
 // layer i's backward seed from g_a (the gradient of its PReLU output, LDS [nr][lga]): g_y = PReLU'(y) g_a with
 // y = gamma xhat + beta recomputed from z_i and the layer's statistics (st: mean [N], invstd [N]), written to bn_g;
-// the tile's (sum g_y, sum g_y xhat) partials; returns this thread's share of the shared slope's gradient (sum over
-// y <= 0 of g_a y)
+// the tile's (sum g_y, sum g_y xhat) partials (the NT / N thread groups take every (NT / N)-th row, then the groups
+// add in order; red: 2 NT floats); returns this thread's share of the shared slope's gradient (sum over y <= 0 of
+// g_a y)
 __device__ float bn_seed_bwd(const SbArgs& a, int i, int tile, int r0, int nr, const float* g_a, int lga,
-                             const float* st) {
-  const int N = a.rw[i];
+                             const float* st, float* red) {
+  const int N = a.rw[i], NT = blockDim.x, tid = threadIdx.x;
+  const int P = NT / N, c = tid % N, p = tid / N;
   const float* zp = bn_ptr(a, i, 0);
   float* gy = bn_ptr(a, i, 1);
   float* pb = bn_ptr(a, i, 3) + (int64_t)tile * 2 * N;
   const float slope = a.ro_slope[0];
-  float sp = 0.0f;
-  for (int c = threadIdx.x; c < N; c += blockDim.x) {
+  float sp = 0.0f, Sg = 0.0f, Sgx = 0.0f;
+  if (p < P) {
     const float mean = st[c], inv = st[N + c], ga = a.bn_w[i][c], be = a.bn_b[i][c];
-    float Sg = 0.0f, Sgx = 0.0f;
-    for (int r = 0; r < nr; ++r) {
+#pragma unroll 4
+    for (int r = p; r < nr; r += P) {
       const int64_t q = (int64_t)(r0 + r) * N + c;
       const float xh = __fmul_rn(__fsub_rn(zp[q], mean), inv);
       const float y = __fadd_rn(__fmul_rn(xh, ga), be);
@@ -1149,8 +1170,19 @@ __device__ float bn_seed_bwd(const SbArgs& a, int i, int tile, int r0, int nr, c
       Sg = __fadd_rn(Sg, gyv);
       Sgx = fmaf(gyv, xh, Sgx);
     }
-    pb[c] = Sg;
-    pb[N + c] = Sgx;
+  }
+  __syncthreads();
+  red[tid] = Sg;
+  red[NT + tid] = Sgx;
+  __syncthreads();
+  if (tid < N) {
+    float g = 0.0f, gx = 0.0f;
+    for (int q = 0; q < P; ++q) {
+      g = __fadd_rn(g, red[q * N + tid]);
+      gx = __fadd_rn(gx, red[NT + q * N + tid]);
+    }
+    pb[tid] = g;
+    pb[N + tid] = gx;
   }
   return sp;
 }
@@ -1169,8 +1201,8 @@ __global__ __launch_bounds__(kRoThreadsM) void k_sb_bn_head(SbArgs a) {
   float* s_inv = s_mean + N;          // [N]
   float* s_a = s_inv + N;             // [R][ln] the activations, then g_a
   float* s_go = s_a + R * ln;         // [R]
-  float* red1 = s_go + R;             // [NT]
-  bn_merge_fwd(a, nh - 1, m, ntile, s_mean, s_inv, tile == 0);
+  float* red1 = s_go + R;             // [3 NT] (the merge's, then block_sum's)
+  bn_merge_fwd(a, nh - 1, m, ntile, s_mean, s_inv, tile == 0, red1);
   __syncthreads();
   const float* zp = bn_ptr(a, nh - 1, 0);
   const float* ga = a.bn_w[nh - 1];
@@ -1218,7 +1250,7 @@ __global__ __launch_bounds__(kRoThreadsM) void k_sb_bn_head(SbArgs a) {
   }
   __syncthreads();
   // (the statistics from LDS: the global record is this launch's first block's)
-  const float sp = block_sum<NT>(bn_seed_bwd(a, nh - 1, tile, r0, nr, s_a, ln, s_mean), red1);
+  const float sp = block_sum<NT>(bn_seed_bwd(a, nh - 1, tile, r0, nr, s_a, ln, s_mean, red1), red1);
   if (tid == 0) a.slope_part[tile] = sp;
 }
 
@@ -1245,20 +1277,33 @@ __global__ __launch_bounds__(kRoThreadsM) void k_sb_bn_bwd(SbArgs a, int i) {
   const float* pb = bn_ptr(a, i, 3);
   const float* st = bn_ptr(a, i, 4);
   float* part = a.part_ro - a.p_gin + a.bn_goff[i];   // the first row chunk's gamma, beta entries
-  for (int c = tid; c < N; c += NT) {
+  {   // the tiles' (sum g_y, sum g_y xhat): NT / N thread groups over every (NT / N)-th tile, then the groups in order
+    const int P = NT / N, c = tid % N, p = tid / N;
     float Sg = 0.0f, Sgx = 0.0f;
-#pragma unroll 8
-    for (int t = 0; t < ntile; ++t) {
-      Sg = __fadd_rn(Sg, pb[(int64_t)t * 2 * N + c]);
-      Sgx = __fadd_rn(Sgx, pb[(int64_t)t * 2 * N + N + c]);
+    if (p < P) {
+#pragma unroll 4
+      for (int t = p; t < ntile; t += P) {
+        Sg = __fadd_rn(Sg, pb[(int64_t)t * 2 * N + c]);
+        Sgx = __fadd_rn(Sgx, pb[(int64_t)t * 2 * N + N + c]);
+      }
     }
-    s_c[c] = st[c];
-    s_c[N + c] = st[N + c];
-    s_c[2 * N + c] = Sg;
-    s_c[3 * N + c] = Sgx;
-    if (tile == 0) {
-      part[c] = Sgx;       // d gamma
-      part[N + c] = Sg;    // d beta
+    red[tid] = Sg;
+    red[NT + tid] = Sgx;
+    __syncthreads();
+    if (tid < N) {
+      float g = 0.0f, gx = 0.0f;
+      for (int q = 0; q < P; ++q) {
+        g = __fadd_rn(g, red[q * N + tid]);
+        gx = __fadd_rn(gx, red[NT + q * N + tid]);
+      }
+      s_c[tid] = st[tid];
+      s_c[N + tid] = st[N + tid];
+      s_c[2 * N + tid] = g;
+      s_c[3 * N + tid] = gx;
+      if (tile == 0) {
+        part[tid] = gx;      // d gamma
+        part[N + tid] = g;   // d beta
+      }
     }
   }
   if (wl) bn_stage_w(a, i, N, K, s_w, false);
@@ -1289,7 +1334,7 @@ __global__ __launch_bounds__(kRoThreadsM) void k_sb_bn_bwd(SbArgs a, int i) {
     }
     return;
   }
-  const float sp = block_sum<NT>(bn_seed_bwd(a, i - 1, tile, r0, nr, s_gi, lg, bn_ptr(a, i - 1, 4)), red1);
+  const float sp = block_sum<NT>(bn_seed_bwd(a, i - 1, tile, r0, nr, s_gi, lg, bn_ptr(a, i - 1, 4), red), red1);
   if (tid == 0) a.slope_part[tile] = __fadd_rn(a.slope_part[tile], sp);
 }
 
