@@ -135,7 +135,27 @@ struct SbArgs {
   float bn_eps, bn_mom;
   float* bn_buf;                   // scratch, per hidden layer the bn_ptr blocks at bn_off[i][0..4]
   int64_t bn_off[kSbMaxHid][5];
+  // DROPOUT (models.py:358-359: F.dropout of every node type's output after each layer, training mode)
+  int64_t* drop_ctr;               // [1] the step counter: fresh masks per step (advanced by k_sb_final)
+  uint64_t drop_seed;
+  uint32_t drop_thr;               // an element is dropped when its 32-bit hash is below round(p 2^32); 0: off
+  float drop_inv;                  // 1 / (1 - p)
 };
+
+// The dropout factor of element q (= row H + column) of layer l's type-t output: 0 (dropped, probability p) or
+// 1 / (1 - p), from a splitmix64 hash of (seed, step counter, l, t, q) — the same in the step's forward and backward,
+// fresh each step (torch's F.dropout draws from its generator instead: the same distribution, not the same masks)
+__device__ __forceinline__ float drop_factor(const SbArgs& a, int l, int t, int64_t q) {
+  if (a.drop_thr == 0u) return 1.0f;
+  uint64_t x = a.drop_seed + (uint64_t)a.drop_ctr[0] * 0x9E3779B97F4A7C15ull;
+  x ^= ((uint64_t)(l * 3 + t) << 56) ^ (uint64_t)q;
+  x ^= x >> 30;
+  x *= 0xBF58476D1CE4E5B9ull;
+  x ^= x >> 27;
+  x *= 0x94D049BB133111EBull;
+  x ^= x >> 31;
+  return (uint32_t)(x >> 32) < a.drop_thr ? 0.0f : a.drop_inv;
+}
 
 __device__ __forceinline__ int kdim(const SbArgs& a, int l, int r) {
   return l == 0 ? a.fdim[kRelSrc[r]] + a.fdim[kRelDst[r]] : a.H;
@@ -425,7 +445,8 @@ __global__ __launch_bounds__(kSbThreads) void k_sb_fwd(SbArgs a, int l) {
       y = first ? yv : __fadd_rn(y, yv);
       first = false;
     }
-    a.act[a.act_off[l][t] + (int64_t)(r0 + ii) * H + h] = y;
+    const int64_t q = (int64_t)(r0 + ii) * H + h;
+    a.act[a.act_off[l][t] + q] = a.drop_thr ? __fmul_rn(y, drop_factor(a, l, t, q)) : y;
   }
 }
 
@@ -1451,7 +1472,9 @@ __device__ void ro_weight_part(const SbArgs& a, int p, int u, float* stage) {
 // layer l's output gradient of type d (gcur: written by the readout for path rows, by k_sb_bwd_in of layer l + 1
 // otherwise); the last layer's link / node outputs feed nothing (models.py:362-376 reads path only)
 __device__ __forceinline__ float gout(const SbArgs& a, const float* gcur, int l, int d, int64_t q) {
-  return (l == a.L - 1 && d != 0) ? 0.0f : gcur[a.g_off[d] + q];
+  if (l == a.L - 1 && d != 0) return 0.0f;
+  const float g = gcur[a.g_off[d] + q];
+  return a.drop_thr ? __fmul_rn(g, drop_factor(a, l, d, q)) : g;   // (through the dropout of the layer's output)
 }
 
 // one row chunk's partial W / bias / slope / eps gradients of one relation (grid = n_parts x relations, plus half
@@ -1602,7 +1625,10 @@ __global__ __launch_bounds__(kSbThreads) void k_sb_final(SbArgs a) {
   const float s = ls.x, slope_sum = ls.y;
   const float lv = __fdiv_rn(__fmul_rn(100.0f, s), (float)m);       // 100 * mean |u| (train.py:12-13)
   const float scale = __fdiv_rn(__fdiv_rn(100.0f, (float)m), __fmul_rn(2.0f, sqrtf(lv)));
-  if (blockIdx.x == 0 && tid == 0) a.loss_value[0] = lv;
+  if (blockIdx.x == 0 && tid == 0) {
+    a.loss_value[0] = lv;
+    if (a.drop_thr) a.drop_ctr[0] += 1;   // (no kernel of this step reads it after this one starts)
+  }
   const int64_t P = a.p_gin + a.p_ro;
   const int j = tid & 31, g = tid >> 5;
   for (int64_t e0 = (int64_t)blockIdx.x * 32; e0 < P; e0 += (int64_t)gridDim.x * 32) {
@@ -1678,6 +1704,7 @@ extern "C" int hgin_sb_step(const void* args, size_t args_bytes, size_t readout_
   HGIN_ARG_CHECK(a.G >= 1 && a.L >= 1 && a.L <= kSbMaxL && a.H >= 1 && a.H <= 128 && a.nhid >= 1 && a.kmax <= 128 &&
                      a.nhid <= kSbMaxHid && a.n_tiles >= 1 && readout_lds <= 160 * 1024,
                  "hgin_sb_step: unsupported shape");
+  HGIN_ARG_CHECK(a.drop_thr == 0u || a.drop_ctr, "hgin_sb_step: dropout step counter");
   HGIN_ARG_CHECK(a.pool_w == 0 || (a.pooled && a.pbatch && a.pool_w == 2 * a.fdim[0] && a.pool_ld >= a.pool_w),
                  "hgin_sb_step: pooled features (pool_w %d, pool_ld %d)", a.pool_w, a.pool_ld);
   hipStream_t s = as_stream(stream);
@@ -1799,7 +1826,8 @@ extern "C" int hgin_sb_args_offsets(int64_t* out, int64_t n) {
                           (int64_t)offsetof(SbArgs, act_off),  (int64_t)offsetof(SbArgs, zb_off),
                           (int64_t)offsetof(SbArgs, gc_off),   (int64_t)offsetof(SbArgs, n_tiles),
                           (int64_t)offsetof(SbArgs, loss_value), (int64_t)offsetof(SbArgs, adam_step),
-                          (int64_t)offsetof(SbArgs, weight_decay), (int64_t)offsetof(SbArgs, bn_off)};
+                          (int64_t)offsetof(SbArgs, weight_decay), (int64_t)offsetof(SbArgs, bn_off),
+                          (int64_t)offsetof(SbArgs, drop_inv)};
   const int64_t k = (int64_t)(sizeof(offs) / sizeof(offs[0]));
   HGIN_ARG_CHECK(out && n >= k, "hgin_sb_args_offsets: need %lld slots", (long long)k);
   for (int64_t i = 0; i < k; ++i) out[i] = offs[i];

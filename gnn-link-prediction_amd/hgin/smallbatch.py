@@ -7,8 +7,8 @@ launches), captured once into a hipGraph and replayed per batch after one device
 
 It takes the model train.py builds from config.json (``HetroGIN`` with GINLayer convs, Linear + shared PReLU
 readout, Linear head) and its GLOBAL_FEATS (one pooling launch ahead of the step, models.py:347-352) and MLP_BN
-(the readout as 2 nhid + 1 launches around the BatchNorm's batch statistics, models.py:303-313) switches, not
-dropout, at small widths: hidden <= 128, first-layer GEMM K <= 128, readout widths <= 256, <= 3 hidden readout
+(the readout as 2 nhid + 1 launches around the BatchNorm's batch statistics, models.py:303-313) and DROPOUT
+(masks hashed per step, models.py:358-359) switches, at small widths: hidden <= 128, first-layer GEMM K <= 128, readout widths <= 256, <= 3 hidden readout
 layers, <= 4 layers, fp32.  ``SmallBatchStep.supports(model)``
 says whether it applies; ``hgin.graphs.CapturedTrainStep`` (one launch per op, any shape) is the general path.
 
@@ -66,11 +66,13 @@ class _SbArgs(ctypes.Structure):   # field for field csrc/hgin_smallbatch.hip Sb
                 ("adam_eps", ctypes.c_float), ("weight_decay", ctypes.c_float),
                 ("bn_w", _P * MAX_HID), ("bn_b", _P * MAX_HID), ("bn_rm", _P * MAX_HID), ("bn_rv", _P * MAX_HID),
                 ("bn_nbt", _P * MAX_HID), ("bn_goff", _I64 * MAX_HID), ("bn_eps", ctypes.c_float),
-                ("bn_mom", ctypes.c_float), ("bn_buf", _P), ("bn_off", (_I64 * 5) * MAX_HID)]
+                ("bn_mom", ctypes.c_float), ("bn_buf", _P), ("bn_off", (_I64 * 5) * MAX_HID),
+                ("drop_ctr", _P), ("drop_seed", ctypes.c_uint64), ("drop_thr", ctypes.c_uint32),
+                ("drop_inv", ctypes.c_float)]
 
 
 _OFFSET_FIELDS = ("goff", "m_valid", "conv", "rw", "ro_goff", "p_ro", "act_off", "zb_off", "gc_off", "n_tiles",
-                  "loss_value", "adam_step", "weight_decay", "bn_off")
+                  "loss_value", "adam_step", "weight_decay", "bn_off", "drop_inv")
 
 
 def foldable(opt: torch.optim.Optimizer) -> bool:
@@ -108,8 +110,8 @@ def _structure(model: torch.nn.Module):
     string when the fused step does not take the model."""
     if type(model) is not HetroGIN:
         return "not a HetroGIN"
-    if model.dropout > 0.0:
-        return "dropout"
+    if not 0.0 <= model.dropout < 1.0:
+        return "dropout probability"
     if not 1 <= model.num_layers <= MAX_L:
         return "layers"
     convs = []
@@ -362,6 +364,12 @@ class SmallBatchStep:
                 for k in range(5):
                     a.bn_off[i][k] = o[5 * i + k]
             a.bn_eps, a.bn_mom = float(bns[0].eps), float(bns[0].momentum)
+        if model.dropout > 0.0:   # models.py:358-359: masks hashed from a seed drawn here and a device step counter
+            self.drop_ctr = torch.zeros(1, dtype=torch.int64, device=dev)
+            a.drop_ctr = P(self.drop_ctr)
+            a.drop_seed = int(torch.randint(0, 2 ** 62, (1,)).item())
+            a.drop_thr = min(int(round(float(model.dropout) * 2 ** 32)), 2 ** 32 - 1)
+            a.drop_inv = 1.0 / (1.0 - float(model.dropout))
         if a.pool_w:   # per graph [mean | max], formed by the first layer's launch
             self.pooled = torch.zeros(batch_size, a.pool_ld, **f32)
             a.pooled, a.pbatch = P(self.pooled), P(pb.batch["path"])

@@ -187,6 +187,63 @@ def test_fused_step_vs_reference_fixture_global_bn():
         assert err <= 1e-4 * float(ref.double().norm()) + 1e-6 * g_scale, (n, err, float(ref.norm()))
 
 
+def test_fused_step_dropout_masks_and_gradients(monkeypatch):
+    """DROPOUT (models.py:358-359, here p = 0.3): the fused step hashes its masks per step — each layer's dropped
+    fraction within 0.05 of p over the batch's rows, and a second replay of the same batch draws new masks (another
+    loss at lr 0).  Given one step's masks — read back from its layer outputs, where a dropped element is an exact
+    zero — the CPU oracle with F.dropout applying those masks gives the same loss (1e-5 relative) and gradients (1e-4
+    of their norm) on the host-collated batch."""
+    from hgin.smallbatch import SmallBatchStep
+    from oracle.pyg_cpu import OracleHetroGIN, mape
+    p = 0.3
+    store, cfg = _store(8, seed=23)
+    ids = [2, 5, 7]
+    kw = lambda: dict(cfg.model_kwargs({"link": cfg.f_link, "path": cfg.f_path, "node": cfg.f_node}),  # noqa: E731
+                      dropout=p)
+    torch.manual_seed(1997)
+    m1 = HetroGIN(**kw()).to(DEV)
+    step = SmallBatchStep(m1, torch.optim.Adam(m1.parameters(), lr=0.0, capturable=True), store, batch_size=3,
+                          warmup_ids=[[0, 1]], warmup=1)
+    ref = OracleHetroGIN(**kw())
+    ref.load_state_dict({k: v.detach().cpu() for k, v in m1.state_dict().items()})
+    lv = float(step.step(ids))
+    torch.cuda.synchronize()
+    grads = [q.grad.detach().cpu().clone() for q in m1.parameters()]
+    act = step.act.detach().cpu().clone()
+    a = step.args
+    b = _host_batch(store, ids)
+    types = ("path", "link", "node")
+    n = {t: b.x[t].shape[0] for t in types}
+    assert len(set(n.values())) == 3
+    masks = {}
+    for l in range(a.L):
+        for ti, t in enumerate(types):
+            o = a.act_off[l][ti]
+            masks[(l, t)] = act[o:o + n[t] * a.H].view(n[t], a.H) != 0
+            frac = 1.0 - float(masks[(l, t)].float().mean())
+            assert abs(frac - p) < 0.05, (l, t, frac)
+    calls = {}
+
+    def replay_masks(x, p=0.5, training=True, inplace=False):
+        t = next(t for t in types if n[t] == x.shape[0])
+        l = calls.get(t, 0)
+        calls[t] = l + 1
+        return x * (masks[(l, t)].to(x.dtype) * (1.0 / (1.0 - p)))
+    monkeypatch.setattr(torch.nn.functional, "dropout", replay_masks)
+    out = ref(b.x_dict(), b.edge_index_dict(), b.batch["path"])
+    lv_ref = mape(out, b.y.reshape(-1, 1))
+    torch.sqrt(lv_ref).backward()
+    assert calls == {t: a.L for t in types}
+    assert abs(lv - float(lv_ref)) <= 1e-5 * abs(float(lv_ref)), (lv, float(lv_ref))
+    for g, (nm, q) in zip(grads, ref.named_parameters()):
+        want = q.grad if q.grad is not None else torch.zeros_like(q)
+        d = float((g - want).double().norm())
+        assert d <= 1e-4 * float(want.double().norm()) + 1e-9, (nm, d, float(want.norm()))
+    lv2 = float(step.step(ids))
+    torch.cuda.synchronize()
+    assert lv2 != lv and not torch.equal(step.act.detach().cpu(), act)
+
+
 @pytest.mark.parametrize("variant", ["default", "mlp_bn_global_feats"])
 def test_fused_trajectory_vs_oracle(variant):
     """Five shuffled batches with Adam(lr=1e-3) (train.py:31-44): the fused step's loss trajectory against
@@ -290,7 +347,7 @@ def test_supports_and_refusals():
     kw = lambda **o: dict(cfg.model_kwargs({"link": 7, "path": 7, "node": 3}), **o)   # noqa: E731
     assert SmallBatchStep.supports(HetroGIN(**kw()))
     assert SmallBatchStep.supports(HetroGIN(**kw(global_feats=True, bl_features=True)))
-    assert not SmallBatchStep.supports(HetroGIN(**kw(dropout=0.1)))
     assert SmallBatchStep.supports(HetroGIN(**kw(mlp_bn=True)))
+    assert SmallBatchStep.supports(HetroGIN(**kw(dropout=0.1)))
     assert SmallBatchStep.supports(HetroGIN(**kw(node_embedding_size=128)))
     assert not SmallBatchStep.supports(HetroGIN(**kw(node_embedding_size=256)))

@@ -28,7 +28,7 @@ def test_supported_models():
 
 
 @pytest.mark.parametrize("override,reason", [
-    ({"dropout": 0.1}, "dropout"),
+    ({"dropout": 1.0}, "dropout probability"),
     ({"mlp_head_act": "torch.nn.PReLU()"}, "head"),
     ({"node_embedding_size": 256}, "widths"),
     ({"message_passing_layers": 5}, "layers"),
