@@ -112,7 +112,8 @@ struct SbArgs {
   float* loss_part;         // [n_tiles]
   float* slope_part;        // [n_tiles] the shared readout slope's gradient
   int n_tiles;              // readout tiles of kSbRows path rows
-  int ro_wlds;              // readout: 2 the 32-row MFMA tiles, 1 8-row tiles with the weights in LDS, 0 without
+  int ro_wlds;              // readout: 2 the 32-row MFMA tiles (4: their weights read through the caches), 1 8-row
+                            // tiles with the weights in LDS, 0 without, 3 MLP_BN (k_sb_bn_*)
   float* ro_in[kSbMaxHid + 1];   // readout layer i's input rows [cap_path][win_i] (i = nhid: the head)
   float* ro_gz[kSbMaxHid + 1];   // its pre-activation gradient rows [cap_path][rw_i] (the head: [cap_path])
   // outputs
@@ -326,6 +327,11 @@ __device__ __forceinline__ void copy_flat(float* dst, const float* src, int n) {
 // relation for the backward.  comb_r also goes to HBM (the weight gradients read it).
 constexpr int kSbFwdRows = 32;
 
+typedef float sb_f32x16 __attribute__((ext_vector_type(16)));
+template <int NT, class Epi>
+__device__ __forceinline__ void tile_mfma(const float* A, int lda, int nr, const float* Bm, int bsk, int bsn, int N,
+                                          int K, float* red, Epi epi);
+
 constexpr int kSbFwdW = 1024;   // k_sb_fwd stages a relation's W [H][K] in LDS when it has at most this many entries
 
 // GLOBAL_FEATS (models.py:347-352, global_mean_pool / global_max_pool of the sliced path features by the batch
@@ -364,9 +370,15 @@ __device__ void sb_pool(const SbArgs& a, float* red) {
   }
 }
 
+// kM (hidden >= 64): the Linear of each relation on the matrix cores — tile_mfma over 32-column chunks of W staged in
+// LDS, the chunks' partial sums added in chunk order — instead of one dot chain per output (at H = 128 a 128-term
+// chain per output made the launch ~120 us); comb rows at an odd stride (the MFMA operand reads a column of rows)
+constexpr int kFwdMW = 128 * 33, kFwdMT = kSbFwdRows * 129;
+template <bool kM>
 __global__ __launch_bounds__(kSbThreads) void k_sb_fwd(SbArgs a, int l) {
-  __shared__ float s_comb[2][kSbFwdRows * 128];   // <= 2 relations into a type, K <= kmax <= 128
+  __shared__ float s_comb[2][kM ? kSbFwdRows * 129 : kSbFwdRows * 128];   // <= 2 relations into a type, K <= 128
   __shared__ float s_w[2][kSbFwdW];
+  __shared__ float s_m[kM ? kFwdMW + 2 * kFwdMT + (kSbThreads / 64) * 32 * 33 : 1];   // W chunk | z | y | partials
   const int t = blockIdx.y;
   if (t == 3) {   // (the first layer with GLOBAL_FEATS)
     sb_pool(a, &s_comb[0][0]);
@@ -421,12 +433,56 @@ __global__ __launch_bounds__(kSbThreads) void k_sb_fwd(SbArgs a, int l) {
         v = gather_chain(cl, rp[i], rp[i + 1], xs, H, k, v);
         v = __fadd_rn(v, __fmul_rn(sc, a.act[a.act_off[l - 1][t] + (int64_t)i * H + k]));
       }
-      s_comb[slot][idx] = v;
+      s_comb[slot][kM ? (idx / K) * (K | 1) + idx % K : idx] = v;
       comb[idx] = v;
     }
     ++slot;
   }
   __syncthreads();
+  if constexpr (kM) {
+    float* s_wc = s_m;               // [H][33]: W[:, kc : kc + 32]
+    float* s_z = s_m + kFwdMW;       // [32][H | 1]
+    float* s_y = s_z + kFwdMT;       // [32][H | 1]
+    float* red = s_y + kFwdMT;
+    const int ly = H | 1;
+    int sl = 0;
+    for (int r = 0; r < kRel; ++r) {
+      if (kRelDst[r] != t) continue;
+      const int K = kdim(a, l, r), lc = K | 1;
+      const SbConv& cv = a.conv[l][r];
+      for (int kc = 0; kc < K; kc += 32) {
+        const int kn = K - kc < 32 ? K - kc : 32;
+        __syncthreads();   // the previous chunk's / relation's readers of s_wc, s_z
+        for (int idx = tid; idx < H * 32; idx += kSbThreads) {
+          const int n = idx >> 5, kk = idx & 31;
+          if (kk < kn) s_wc[n * 33 + kk] = cv.w[(int64_t)n * K + kc + kk];
+        }
+        __syncthreads();
+        tile_mfma<kSbThreads>(s_comb[sl] + kc, lc, nr, s_wc, 1, 33, H, kn, red, [&](int rr, int n, float v) {
+          s_z[rr * ly + n] = kc == 0 ? v : __fadd_rn(s_z[rr * ly + n], v);
+        });
+      }
+      __syncthreads();
+      float* zb = a.zb + a.zb_off[l][r] + (int64_t)r0 * H;
+      const float slope = cv.slope[0];
+      for (int idx = tid; idx < nr * H; idx += kSbThreads) {
+        const int ii = idx / H, h = idx - ii * H;
+        const float z = __fadd_rn(s_z[ii * ly + h], cv.b[h]);
+        zb[idx] = z;
+        const float yv = z > 0.0f ? z : __fmul_rn(slope, z);
+        s_y[ii * ly + h] = sl == 0 ? yv : __fadd_rn(s_y[ii * ly + h], yv);
+      }
+      ++sl;
+    }
+    __syncthreads();
+    for (int idx = tid; idx < nr * H; idx += kSbThreads) {
+      const int ii = idx / H, h = idx - ii * H;
+      const float y = s_y[ii * ly + h];
+      const int64_t q = (int64_t)r0 * H + idx;
+      a.act[a.act_off[l][t] + q] = a.drop_thr ? __fmul_rn(y, drop_factor(a, l, t, q)) : y;
+    }
+    return;
+  }
   for (int idx = tid; idx < nr * H; idx += kSbThreads) {
     const int ii = idx / H, h = idx % H;
     float y = 0.0f;
@@ -757,7 +813,6 @@ __global__ __launch_bounds__(kSbThreads) void k_sb_readout(SbArgs a) {
 // (profiles/r05/sb/stamps_after.txt: 12 such phases made the 8-row scalar tile's ~20 us).
 constexpr int kSbRowsM = 32;
 constexpr int kRoThreadsM = 512;   // 8 waves: 2 per SIMD, so one wave's LDS / MFMA latency overlaps the other's
-typedef float sb_f32x16 __attribute__((ext_vector_type(16)));
 
 // C[32 x N] = A[32 x K] B[K x N] for one tile: A(r, k) = A[r lda + k] (rows >= nr read as zero), B(k, n) =
 // Bm[k bsk + n bsn].  The ceil(N / 32) column blocks go to the NT / 64 waves; with fewer blocks than waves a block's
@@ -825,6 +880,9 @@ __device__ __forceinline__ void tile_mfma(const float* A, int lda, int nr, const
   }
 }
 
+// kWL false (hgin_sb_readout_lds_bytes mode 4: the staged weights would not fit, e.g. hidden 128): the MFMA operands'
+// W rows and the head's W are read through the caches instead
+template <bool kWL>
 __global__ __launch_bounds__(kRoThreadsM) void k_sb_readout_mfma(SbArgs a) {
   extern __shared__ float sm[];
   constexpr int NT = kRoThreadsM;
@@ -853,8 +911,9 @@ __global__ __launch_bounds__(kRoThreadsM) void k_sb_readout_mfma(SbArgs a) {
   // [R][maxw | 1] | outv [R] | red [4][32][33] (odd row strides everywhere: an MFMA operand read is 32 rows of one
   // column)
   int oW[kSbMaxHid], ldw[kSbMaxHid];
-  int off = stage_ro_params<true, NT>(a, sm, nh, win, KL, oW, ldw);
-  const float* hw = sm + off - KL;
+  int off = stage_ro_params<kWL, NT>(a, sm, nh, win, KL, oW, ldw);
+  const float* hw = kWL ? (const float*)(sm + off - KL) : a.head_w;
+#define RO_WM(i) (kWL ? (const float*)(sm + oW[i]) : a.row_w[i])
   const int l0 = w0 | 1;
   float* in0 = sm + off;
   off += R * l0;
@@ -894,8 +953,8 @@ __global__ __launch_bounds__(kRoThreadsM) void k_sb_readout_mfma(SbArgs a) {
       const float* in = i == 0 ? in0 : sm + oY[i > 0 ? i - 1 : 0];
       const int lin = i == 0 ? l0 : lz[i > 0 ? i - 1 : 0];
       const int N = a.rw[i];
-      const float* b = sm + oW[i] + N * ldw[i];
-      tile_mfma<NT>(in, lin, nr, sm + oW[i], 1, ldw[i], N, win[i], red, [&](int r, int n, float v) {
+      const float* b = kWL ? (const float*)(sm + oW[i] + N * ldw[i]) : a.row_b[i];
+      tile_mfma<NT>(in, lin, nr, RO_WM(i), 1, ldw[i], N, win[i], red, [&](int r, int n, float v) {
         const float z = __fadd_rn(v, b[n]);
         sm[oZ[i] + r * lz[i] + n] = z;
         const float yv = z > 0.0f ? z : __fmul_rn(slope, z);
@@ -974,7 +1033,7 @@ __global__ __launch_bounds__(kRoThreadsM) void k_sb_readout_mfma(SbArgs a) {
       // g_in = g_z W (the first layer: only the path embeddings' H columns have a gradient)
       const int KG = i == 0 ? H : K, lgn = KG | 1;
       float* gn = g_next;
-      tile_mfma<NT>(g_y, ly, nr, sm + oW[i], ldw[i], 1, KG, N, red,
+      tile_mfma<NT>(g_y, ly, nr, RO_WM(i), ldw[i], 1, KG, N, red,
                 [&](int r, int n, float v) { gn[r * lgn + n] = v; });
       __syncthreads();
       SB_STAMP(9 + 2 * i);
@@ -993,6 +1052,7 @@ __global__ __launch_bounds__(kRoThreadsM) void k_sb_readout_mfma(SbArgs a) {
   }
   SB_STAMP(13);
 }
+#undef RO_WM
 
 // ---------------------------------------------------------------------------------------------------------------
 // MLP_BN (models.py:303-313, ro_wlds 3): each hidden readout layer is Linear -> BatchNorm1d -> the shared PReLU, and
@@ -1684,10 +1744,11 @@ extern "C" int hgin_sb_readout_lds_bytes(int64_t H, int64_t f_path, int concat_p
     *bytes = sizeof(float) * (size_t)(fh > f ? fh : f);
     return HGIN_OK;
   }
-  if (with_weights == 2) {   // k_sb_readout_mfma: 32-row tiles, odd row strides, the split partials
-    int64_t act = w0 | 1;
+  if (with_weights == 2 || with_weights == 4) {   // k_sb_readout_mfma: 32-row tiles, odd row strides, the split
+    int64_t act = w0 | 1;                            // partials (4: the weights through the caches)
     for (int i = 0; i < nhid; ++i) act += 2 * (widths[i] | 1);
-    *bytes = sizeof(float) * (size_t)(wts + kSbRowsM * (act + 2 * (maxw | 1)) + kSbRowsM + (kRoThreadsM / 64) * 32 * 33);
+    *bytes = sizeof(float) * (size_t)((with_weights == 2 ? wts : 0) + kSbRowsM * (act + 2 * (maxw | 1)) + kSbRowsM +
+                                      (kRoThreadsM / 64) * 32 * 33);
     return HGIN_OK;
   }
   *bytes = sizeof(float) * (size_t)(kSbRows * (tot + 2 * maxw) + kSbRows + (with_weights ? wts : 0));
@@ -1719,7 +1780,8 @@ extern "C" int hgin_sb_step(const void* args, size_t args_bytes, size_t readout_
     int m = 160 * 1024;   // the smaller of the two variants' limits (-1 if either failed)
     for (const void* fn : {reinterpret_cast<const void*>(k_sb_readout<true>),
                            reinterpret_cast<const void*>(k_sb_readout<false>),
-                           reinterpret_cast<const void*>(k_sb_readout_mfma),
+                           reinterpret_cast<const void*>(k_sb_readout_mfma<true>),
+                           reinterpret_cast<const void*>(k_sb_readout_mfma<false>),
                            reinterpret_cast<const void*>(k_sb_bn_fwd), reinterpret_cast<const void*>(k_sb_bn_head),
                            reinterpret_cast<const void*>(k_sb_bn_bwd)}) {
       hipFuncAttributes fa;
@@ -1755,7 +1817,13 @@ extern "C" int hgin_sb_step(const void* args, size_t args_bytes, size_t readout_
     if (i < a.nhid) win = a.rw[i];
   }
   const unsigned fwd_blocks = (unsigned)ceil_div((int64_t)capt_max, (int64_t)kSbFwdRows);
-  for (int l = 0; l < a.L; ++l) k_sb_fwd<<<dim3(fwd_blocks, l == 0 && a.pool_w ? 4 : 3), kSbThreads, 0, s>>>(a, l);
+  for (int l = 0; l < a.L; ++l) {
+    const dim3 g(fwd_blocks, l == 0 && a.pool_w ? 4 : 3);
+    if (a.H >= 64)
+      k_sb_fwd<true><<<g, kSbThreads, 0, s>>>(a, l);
+    else
+      k_sb_fwd<false><<<g, kSbThreads, 0, s>>>(a, l);
+  }
   // one tile per workgroup (a grid of 512 looping over the tiles, staging the weights once each: 52.9 vs 35 us per
   // batch, profiles/r04/gpu_r — the tiles' serial layer chains want the parallelism, not fewer weight stagings)
   if (a.ro_wlds == 3) {   // MLP_BN: 2 nhid + 1 launches over 32-row tiles (k_sb_bn_*)
@@ -1777,9 +1845,13 @@ extern "C" int hgin_sb_step(const void* args, size_t args_bytes, size_t readout_
       HGIN_ARG_CHECK((int64_t)lb <= dyn_max, "hgin_sb_step: MLP_BN LDS %zu above %d", lb, dyn_max);
       k_sb_bn_bwd<<<nt, kRoThreadsM, lb, s>>>(a, i);
     }
-  } else if (a.ro_wlds == 2)
-    k_sb_readout_mfma<<<(unsigned)ceil_div((int64_t)a.n_tiles * kSbRows, (int64_t)kSbRowsM), kRoThreadsM, readout_lds,
-                        s>>>(a);
+  } else if (a.ro_wlds == 2 || a.ro_wlds == 4) {
+    const unsigned g = (unsigned)ceil_div((int64_t)a.n_tiles * kSbRows, (int64_t)kSbRowsM);
+    if (a.ro_wlds == 2)
+      k_sb_readout_mfma<true><<<g, kRoThreadsM, readout_lds, s>>>(a);
+    else
+      k_sb_readout_mfma<false><<<g, kRoThreadsM, readout_lds, s>>>(a);
+  }
   else if (a.ro_wlds)
     k_sb_readout<true><<<a.n_tiles, kSbThreads, readout_lds, s>>>(a);
   else

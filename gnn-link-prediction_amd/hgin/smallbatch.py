@@ -327,10 +327,10 @@ class SmallBatchStep:
             self._fold_adam(a, params, param_off, off, convs, hidden, slope, head, L, keep, bns)
         widths = (ctypes.c_int32 * MAX_HID)(*[a.rw[i] for i in range(MAX_HID)])
         lds = ctypes.c_size_t(0)
-        # the readout: 32-row tiles on the matrix cores where they fit (HGIN_SB_MFMA=0: the 8-row scalar tiles), else
-        # 8-row tiles with the hidden weights in LDS, else without (beside the tile's 1 KiB static array)
+        # the readout: 32-row tiles on the matrix cores, their weights in LDS where they fit, else read through the
+        # caches (mode 4; HGIN_SB_MFMA=0: the 8-row scalar tiles, with the hidden weights in LDS, else without)
         # (MLP_BN: the k_sb_bn_* launches, mode 3)
-        modes = (3,) if bns else ((2, 1, 0) if os.environ.get("HGIN_SB_MFMA", "1") != "0" else (1, 0))
+        modes = (3,) if bns else ((2, 4, 1, 0) if os.environ.get("HGIN_SB_MFMA", "1") != "0" else (1, 0))
         for wl in modes:
             _lib.check(_lib.lib().hgin_sb_readout_lds_bytes(H, w0 - H, int(w0 > H), a.nhid, widths, wl,
                                                             ctypes.byref(lds)), "hgin_sb_readout_lds_bytes")

@@ -120,6 +120,7 @@ def test_fused_step_vs_oracle_variants(variant):
     step = SmallBatchStep(m1, torch.optim.Adam(m1.parameters(), lr=0.0, capturable=True), store, batch_size=4,
                           warmup_ids=[[0, 2]], warmup=1)
     torch.cuda.synchronize()
+    assert step.args.ro_wlds == {"hidden128": 4}.get(variant, 3 if "mlp_bn" in variant else 2)
     ref = OracleHetroGIN(**kw())   # (after the warm-up step, which advanced MLP_BN's running statistics)
     ref.load_state_dict({k: v.detach().cpu() for k, v in m1.state_dict().items()})
     lv = float(step.step(ids))
