@@ -373,12 +373,12 @@ __device__ void sb_pool(const SbArgs& a, float* red) {
 // kM (hidden >= 64): the Linear of each relation on the matrix cores — tile_mfma over 32-column chunks of W staged in
 // LDS, the chunks' partial sums added in chunk order — instead of one dot chain per output (at H = 128 a 128-term
 // chain per output made the launch ~120 us); comb rows at an odd stride (the MFMA operand reads a column of rows)
-constexpr int kFwdMW = 128 * 33, kFwdMT = kSbFwdRows * 129;
+constexpr int kFwdMW = 128 * 17, kFwdMT = kSbFwdRows * 129;   // W chunks of 16 columns; the z tile
 template <bool kM>
 __global__ __launch_bounds__(kSbThreads) void k_sb_fwd(SbArgs a, int l) {
   __shared__ float s_comb[2][kM ? kSbFwdRows * 129 : kSbFwdRows * 128];   // <= 2 relations into a type, K <= 128
   __shared__ float s_w[2][kSbFwdW];
-  __shared__ float s_m[kM ? kFwdMW + 2 * kFwdMT + (kSbThreads / 64) * 32 * 33 : 1];   // W chunk | z | y | partials
+  __shared__ float s_m[kM ? kFwdMW + kFwdMT + (kSbThreads / 64) * 32 * 33 : 1];   // W chunk | z | split partials
   const int t = blockIdx.y;
   if (t == 3) {   // (the first layer with GLOBAL_FEATS)
     sb_pool(a, &s_comb[0][0]);
@@ -440,46 +440,45 @@ __global__ __launch_bounds__(kSbThreads) void k_sb_fwd(SbArgs a, int l) {
   }
   __syncthreads();
   if constexpr (kM) {
-    float* s_wc = s_m;               // [H][33]: W[:, kc : kc + 32]
+    float* s_wc = s_m;               // [H][17]: W[:, kc : kc + 16]
     float* s_z = s_m + kFwdMW;       // [32][H | 1]
-    float* s_y = s_z + kFwdMT;       // [32][H | 1]
-    float* red = s_y + kFwdMT;
+    float* red = s_z + kFwdMT;
     const int ly = H | 1;
+    int nrel = 0;
+    for (int r = 0; r < kRel; ++r) nrel += kRelDst[r] == t;
+    float* act = a.act + a.act_off[l][t] + (int64_t)r0 * H;
     int sl = 0;
     for (int r = 0; r < kRel; ++r) {
       if (kRelDst[r] != t) continue;
       const int K = kdim(a, l, r), lc = K | 1;
       const SbConv& cv = a.conv[l][r];
-      for (int kc = 0; kc < K; kc += 32) {
-        const int kn = K - kc < 32 ? K - kc : 32;
+      for (int kc = 0; kc < K; kc += 16) {
+        const int kn = K - kc < 16 ? K - kc : 16;
         __syncthreads();   // the previous chunk's / relation's readers of s_wc, s_z
-        for (int idx = tid; idx < H * 32; idx += kSbThreads) {
-          const int n = idx >> 5, kk = idx & 31;
-          if (kk < kn) s_wc[n * 33 + kk] = cv.w[(int64_t)n * K + kc + kk];
+        for (int idx = tid; idx < H * 16; idx += kSbThreads) {
+          const int n = idx >> 4, kk = idx & 15;
+          if (kk < kn) s_wc[n * 17 + kk] = cv.w[(int64_t)n * K + kc + kk];
         }
         __syncthreads();
-        tile_mfma<kSbThreads>(s_comb[sl] + kc, lc, nr, s_wc, 1, 33, H, kn, red, [&](int rr, int n, float v) {
+        tile_mfma<kSbThreads>(s_comb[sl] + kc, lc, nr, s_wc, 1, 17, H, kn, red, [&](int rr, int n, float v) {
           s_z[rr * ly + n] = kc == 0 ? v : __fadd_rn(s_z[rr * ly + n], v);
         });
       }
       __syncthreads();
       float* zb = a.zb + a.zb_off[l][r] + (int64_t)r0 * H;
       const float slope = cv.slope[0];
+      // the relations' PReLU outputs summed in relation order in the output rows themselves (each element by the
+      // same thread), the dropout with the last
       for (int idx = tid; idx < nr * H; idx += kSbThreads) {
         const int ii = idx / H, h = idx - ii * H;
         const float z = __fadd_rn(s_z[ii * ly + h], cv.b[h]);
         zb[idx] = z;
         const float yv = z > 0.0f ? z : __fmul_rn(slope, z);
-        s_y[ii * ly + h] = sl == 0 ? yv : __fadd_rn(s_y[ii * ly + h], yv);
+        float y = sl == 0 ? yv : __fadd_rn(act[idx], yv);
+        if (sl == nrel - 1 && a.drop_thr) y = __fmul_rn(y, drop_factor(a, l, t, (int64_t)r0 * H + idx));
+        act[idx] = y;
       }
       ++sl;
-    }
-    __syncthreads();
-    for (int idx = tid; idx < nr * H; idx += kSbThreads) {
-      const int ii = idx / H, h = idx - ii * H;
-      const float y = s_y[ii * ly + h];
-      const int64_t q = (int64_t)r0 * H + idx;
-      a.act[a.act_off[l][t] + q] = a.drop_thr ? __fmul_rn(y, drop_factor(a, l, t, q)) : y;
     }
     return;
   }
@@ -814,14 +813,14 @@ __global__ __launch_bounds__(kSbThreads) void k_sb_readout(SbArgs a) {
 constexpr int kSbRowsM = 32;
 constexpr int kRoThreadsM = 512;   // 8 waves: 2 per SIMD, so one wave's LDS / MFMA latency overlaps the other's
 
-// C[32 x N] = A[32 x K] B[K x N] for one tile: A(r, k) = A[r lda + k] (rows >= nr read as zero), B(k, n) =
+// C[32 x N] = A[32 x K] B[K x N] for one tile: A(r, k) = A[r asr + k ask] (rows >= nr read as zero), B(k, n) =
 // Bm[k bsk + n bsn].  The ceil(N / 32) column blocks go to the NT / 64 waves; with fewer blocks than waves a block's
 // k-steps are split over the idle ones (a fixed power-of-two split) and the partials, parked in red [NT / 64][32][33],
 // are added in split order.
 // epi(r, n, v) receives every output of rows < nr and columns < N (v = 0 + the products in k order within a split).
 template <int NT, class Epi>
-__device__ __forceinline__ void tile_mfma(const float* A, int lda, int nr, const float* Bm, int bsk, int bsn, int N,
-                                          int K, float* red, Epi epi) {
+__device__ __forceinline__ void tile_mfma_s(const float* A, int asr, int ask, int nr, const float* Bm, int bsk, int bsn,
+                                            int N, int K, float* red, Epi epi) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int li = lane & 31, lh = lane >> 5;
   const int nb = (N + 31) >> 5;
@@ -850,7 +849,7 @@ __device__ __forceinline__ void tile_mfma(const float* A, int lda, int nr, const
         const int k = 2 * (st + q) + lh;
         const bool kok = st + q < s1 && k < K;
         const int kc = k < K ? k : K - 1;
-        const float x = A[rc * lda + kc], y = Bm[kc * bsk + nc * bsn];
+        const float x = A[rc * asr + kc * ask], y = Bm[kc * bsk + nc * bsn];
         av[q] = rok && kok ? x : 0.0f;
         bv[q] = nok && kok ? y : 0.0f;
       }
@@ -878,6 +877,13 @@ __device__ __forceinline__ void tile_mfma(const float* A, int lda, int nr, const
       epi(r, n, v);
     }
   }
+}
+
+// A(r, k) = A[r lda + k] (row-major A)
+template <int NT, class Epi>
+__device__ __forceinline__ void tile_mfma(const float* A, int lda, int nr, const float* Bm, int bsk, int bsn, int N,
+                                          int K, float* red, Epi epi) {
+  tile_mfma_s<NT>(A, lda, 1, nr, Bm, bsk, bsn, N, K, red, epi);
 }
 
 // kWL false (hgin_sb_readout_lds_bytes mode 4: the staged weights would not fit, e.g. hidden 128): the MFMA operands'
@@ -1540,9 +1546,14 @@ __device__ __forceinline__ float gout(const SbArgs& a, const float* gcur, int l,
 // one row chunk's partial W / bias / slope / eps gradients of one relation (grid = n_parts x relations, plus half
 // the readout layers' blocks in the last layer's launch and half in the first's); rows of chunk p: [p c, (p + 1) c),
 // c = ceil(rows / n_parts)
-__global__ __launch_bounds__(kSbThreads, 4) void k_sb_bwd_w(SbArgs a, int l, const float* gcur, int ro_first) {
+// kM (hidden >= 64): g_comb = g_z W and the W partial g_z^T comb on the matrix cores (tile_mfma over the staged rows;
+// the scalar register tiles at H = 128 re-staged the rows for 8 groups), the chunk's rows staged at once
+constexpr int kSbStageM = 16384, kSbRedM = (kSbThreads / 64) * 32 * 33;
+template <bool kM>
+__global__ __launch_bounds__(kSbThreads, kM ? 1 : 4) void k_sb_bwd_w(SbArgs a, int l, const float* gcur,
+                                                                     int ro_first) {
   __shared__ float red[2 * kSbThreads];   // (block_sum2)
-  __shared__ float stage[kSbStage];
+  __shared__ float stage[kM ? kSbStageM : kSbStage];
   const int p = blockIdx.x, r = blockIdx.y;
   SB_STAMP_W(l & 1, 0);
   if (r >= kRel) {   // the readout's blocks: groups ro_first, ... (grid.y = kRel + their count)
@@ -1564,6 +1575,63 @@ __global__ __launch_bounds__(kSbThreads, 4) void k_sb_bwd_w(SbArgs a, int l, con
   const float slope = cv.slope[0];
   const int fs = l == 0 ? a.fdim[s] : 0;
   const int K1 = K + 1;
+  if constexpr (kM) {
+    const int lg = H | 1, lk = K | 1;
+    const int rcap = (kSbStageM - kSbRedM) / (lg + lk);
+    const int RS = (i1 - i0) < rcap ? (i1 - i0 > 0 ? i1 - i0 : 1) : rcap;
+    float* s_g = stage;               // [RS][lg] g_z
+    float* s_in = s_g + RS * lg;      // [RS][lk] comb
+    float* redm = s_in + RS * lk;     // tile_mfma's split partials
+    float sp = 0.0f, epv = 0.0f, bsum = 0.0f;
+    for (int rb = i0; rb < i1; rb += RS) {
+      const int nr = i1 - rb < RS ? i1 - rb : RS;
+      __syncthreads();
+      for (int idx = tid; idx < nr * K; idx += kSbThreads) {
+        const int rr = idx / K;
+        s_in[rr * lk + idx - rr * K] = comb[(int64_t)rb * K + idx];
+      }
+#pragma unroll 4
+      for (int idx = tid; idx < nr * H; idx += kSbThreads) {
+        const int64_t qq = (int64_t)rb * H + idx;
+        const float z = zb[qq], g = gout(a, gcur, l, d, qq);
+        const int rr = idx / H;
+        s_g[rr * lg + idx - rr * H] = z > 0.0f ? g : __fmul_rn(slope, g);
+        if (z <= 0.0f) sp = fmaf(g, z, sp);
+      }
+      __syncthreads();
+      if (tid < H)   // the bias partial: the rows in order
+        for (int rr = 0; rr < nr; ++rr) bsum = __fadd_rn(bsum, s_g[rr * lg + tid]);
+      for (int sb = 0; sb < nr; sb += 32) {   // g_comb rows (row-local: k_sb_bwd_in reads them after this launch)
+        const int ns = nr - sb < 32 ? nr - sb : 32;
+        tile_mfma<kSbThreads>(s_g + sb * lg, lg, ns, cv.w, K, 1, K, H, redm, [&](int r, int k, float v) {
+          const int i = rb + sb + r;
+          gc[(int64_t)i * a.kmax + k] = v;
+          if (k >= fs) {
+            const float xv = l == 0 ? a.x[d][(int64_t)i * a.ldx[d] + a.cols[d][k - fs]]
+                                    : a.act[a.act_off[l - 1][d] + (int64_t)i * H + k];
+            epv = fmaf(v, xv, epv);
+          }
+        });
+      }
+      for (int h0 = 0; h0 < H; h0 += 32) {   // W partial [h][k] += sum over the staged rows of g_z[h] comb[k]
+        const int nh = H - h0 < 32 ? H - h0 : 32;
+        tile_mfma_s<kSbThreads>(s_g + h0, 1, lg, nh, s_in, lk, 1, K, nr, redm, [&](int r, int k, float v) {
+          float* e = part + (int64_t)(h0 + r) * K + k;
+          *e = rb == i0 ? v : __fadd_rn(*e, v);
+        });
+      }
+    }
+    if (i1 <= i0) {   // an empty chunk: zero partials
+      for (int e = tid; e < H * K; e += kSbThreads) part[e] = 0.0f;
+    }
+    if (tid < H) part[(int64_t)H * K + tid] = bsum;
+    const float2 se = block_sum2(sp, epv, red);
+    if (tid == 0) {
+      part[(int64_t)H * K + H] = se.x;
+      part[(int64_t)H * K + H + 1] = se.y;
+    }
+    return;
+  }
   // the chunk's rows RS at a time in LDS (all of them at cfg1 sizes): g_z = PReLU'(z) g_y into s_g, comb with a
   // column of ones into s_in; then g_comb = g_z W (row-local; k_sb_bwd_in reads every row's g_comb after this launch)
   // with the eps partial (g_comb over the self columns times x_dst), and the register-tiled W / bias partials
@@ -1863,7 +1931,11 @@ extern "C" int hgin_sb_step(const void* args, size_t args_bytes, size_t readout_
   const int ro_hi = a.L > 1 ? (ro_blocks + 1) / 2 : ro_blocks;
   for (int l = a.L - 1; l >= 0; --l) {
     const int ro_n = l == a.L - 1 ? ro_hi : (l == 0 ? ro_blocks - ro_hi : 0);
-    k_sb_bwd_w<<<dim3(a.n_parts, kRel + ro_n), kSbThreads, 0, s>>>(a, l, gcur, l == a.L - 1 ? 0 : ro_hi);
+    const dim3 gw(a.n_parts, kRel + ro_n);
+    if (a.H >= 64)
+      k_sb_bwd_w<true><<<gw, kSbThreads, 0, s>>>(a, l, gcur, l == a.L - 1 ? 0 : ro_hi);
+    else
+      k_sb_bwd_w<false><<<gw, kSbThreads, 0, s>>>(a, l, gcur, l == a.L - 1 ? 0 : ro_hi);
     if (l > 0) {
       k_sb_bwd_in<<<dim3(blocks((int64_t)capt_max * a.H), 3), kSbThreads, 0, s>>>(a, l, gnxt);
       float* tt = gcur;
