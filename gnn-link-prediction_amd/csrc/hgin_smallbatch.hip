@@ -306,6 +306,32 @@ __device__ __forceinline__ float gather_chain(const int32_t* col, int e0, int e1
   return acc;
 }
 
+// gather_chain for 4 (row range, column) pairs at once: 8 edges of each in flight per round trip (32 loads), each
+// pair's sum in its own edge order (bit-identical to gather_chain per pair); a pair with e0 >= e1 adds nothing
+__device__ __forceinline__ void gather_chain4(const int32_t* col, const int (&e0)[4], const int (&e1)[4],
+                                              const float* xs, int64_t ld, const int (&c)[4], float (&acc)[4]) {
+  int emax = 0;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) emax = e1[j] - e0[j] > emax ? e1[j] - e0[j] : emax;
+  for (int o = 0; o < emax; o += 8) {
+    int ci[4][8];
+    float xv[4][8];
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int u = 0; u < 8; ++u) ci[j][u] = e0[j] + o + u < e1[j] ? col[e0[j] + o + u] : 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int u = 0; u < 8; ++u) xv[j][u] = xs[(int64_t)ci[j][u] * ld + c[j]];
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        if (e0[j] + o + u < e1[j]) acc[j] = __fadd_rn(acc[j], xv[j][u]);
+  }
+}
+
 // n contiguous floats from global memory into LDS, every load of a thread issued before its first store (one
 // memory round trip for up to J x kSbThreads floats)
 template <int J = 32>
@@ -415,6 +441,37 @@ __global__ __launch_bounds__(kSbThreads) void k_sb_fwd(SbArgs a, int l) {
     const int32_t* rp = a.rowptr[r];
     const int32_t* cl = a.col[r];
     float* comb = a.comb + a.comb_off[l][r] + (int64_t)r0 * K;
+    if (kM && l > 0) {   // (wide rows: 4 elements' gather chains per thread in flight together)
+      const float* xs = a.act + a.act_off[l - 1][s];
+      const float* xd = a.act + a.act_off[l - 1][t];
+      for (int b0 = tid; b0 < nr * K; b0 += 4 * kSbThreads) {
+        int e0[4], e1[4], cc[4];
+        float v[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int idx = b0 + j * kSbThreads;
+          const bool ok = idx < nr * K;
+          const int i = r0 + (ok ? idx / K : 0);
+          cc[j] = ok ? idx % K : 0;
+          e0[j] = rp[i];
+          e1[j] = ok ? rp[i + 1] : e0[j];
+          v[j] = 0.0f;
+        }
+        gather_chain4(cl, e0, e1, xs, H, cc, v);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int idx = b0 + j * kSbThreads;
+          if (idx < nr * K) {
+            const int rr = idx / K;
+            const float w = __fadd_rn(v[j], __fmul_rn(sc, xd[(int64_t)(r0 + rr) * H + cc[j]]));
+            s_comb[slot][rr * (K | 1) + cc[j]] = w;
+            comb[idx] = w;
+          }
+        }
+      }
+      ++slot;
+      continue;
+    }
     for (int idx = tid; idx < nr * K; idx += kSbThreads) {
       const int i = r0 + idx / K, k = idx % K;
       float v = 0.0f;

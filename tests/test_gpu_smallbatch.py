@@ -93,7 +93,7 @@ def test_fused_step_vs_oracle(layers, readout, monkeypatch):
 
 
 @pytest.mark.parametrize("variant", ["hidden128", "global_feats", "global_feats_no_concat", "mlp_bn",
-                                     "mlp_bn_global_feats", "mlp_bn_3hid"])
+                                     "mlp_bn_global_feats", "mlp_bn_3hid", "mlp_bn_global_feats_h128_L3"])
 def test_fused_step_vs_oracle_variants(variant):
     """Model variants through the fused step, against the CPU oracle as above: hidden 128 (config.json's
     EMBEDDING_SIZE widened: the k <= 128 GEMMs at their widest), GLOBAL_FEATS (models.py:347-352: each path row
@@ -110,7 +110,9 @@ def test_fused_step_vs_oracle_variants(variant):
             "global_feats_no_concat": dict(global_feats=True, bl_features=True, concat_path=False),
             "mlp_bn": dict(mlp_bn=True),
             "mlp_bn_global_feats": dict(mlp_bn=True, global_feats=True, bl_features=True),
-            "mlp_bn_3hid": dict(mlp_bn=True, mlp_layers=[64, 48, 16])}[variant]
+            "mlp_bn_3hid": dict(mlp_bn=True, mlp_layers=[64, 48, 16]),
+            "mlp_bn_global_feats_h128_L3": dict(mlp_bn=True, global_feats=True, bl_features=True,
+                                                node_embedding_size=128, message_passing_layers=3)}[variant]
     store, cfg = _store(8, seed=19)
     ids = [1, 6, 3]
     kw = lambda: dict(cfg.model_kwargs({"link": cfg.f_link, "path": cfg.f_path, "node": cfg.f_node}),  # noqa: E731
