@@ -371,6 +371,7 @@ def batches_extra(dev, n_graphs: int = 256, batch: int = 8, warmup: int = 5, ste
     # VAL_BATCH_SIZE 1, and the training batch size, as captured replays (hgin/graphs.py CapturedEvalStep: device
     # accumulators, one host sync per pass) beside the reference's eager form (forward + loss.item() per batch)
     from hgin.graphs import CapturedEvalStep
+    from hgin.smallbatch import SmallBatchEval
     from hgin.train import mape as mape_fn
     ev = {}
     model = build()
@@ -399,11 +400,25 @@ def batches_extra(dev, n_graphs: int = 256, batch: int = 8, warmup: int = 5, ste
                                  "eager_host_ms_per_batch": round(wall_e * 1e3, 4), "avg_loss": avg,
                                  "batches": cfg_steps}
             del st
+            if SmallBatchEval.supports(model):   # the fused kernels' forward (hgin/smallbatch.py SmallBatchEval)
+                fe = SmallBatchEval(model, store, bs, warmup_ids=[ids[:bs] for ids in order[:warmup]], warmup=2)
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+                s.record()
+                for ids in seq:
+                    fe.step(ids)
+                e.record()
+                favg, _ = fe.result(1)
+                wall_f = (time.perf_counter() - t0) / cfg_steps
+                ev[f"batch_{bs}"].update(fused_ms_per_batch=round(s.elapsed_time(e) / cfg_steps, 4),
+                                         fused_host_ms_per_batch=round(wall_f * 1e3, 4), fused_avg_loss=favg)
+                del fe
         except Exception as exc:   # reported, not fatal
             ev[f"batch_{bs}"] = {"error": f"{type(exc).__name__}: {exc}"[:300]}
     out["eval"] = dict(ev, execution="captured: one batched-copy launch + one hipGraph replay (forward + fused head / "
-                                     "MAPE + device accumulation) per batch; eager: collation + forward + "
-                                     "loss.item() per batch, as train.py's test() / evaluate()")
+                                     "MAPE + device accumulation) per batch; fused: the same around the small-batch "
+                                     "kernels' forward (L + 2 launches); eager: collation + forward + loss.item() per "
+                                     "batch, as train.py's test() / evaluate()")
     if fused_error:
         out["fused_path_error"] = fused_error
     return out

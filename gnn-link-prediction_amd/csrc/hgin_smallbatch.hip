@@ -141,6 +141,11 @@ struct SbArgs {
   uint64_t drop_seed;
   uint32_t drop_thr;               // an element is dropped when its 32-bit hash is below round(p 2^32); 0: off
   float drop_inv;                  // 1 / (1 - p)
+  // evaluation (train.py:70-113 test(), :322-348 evaluate(); hgin/smallbatch.py SmallBatchEval): the forward
+  // launches, the readout up to its loss partial, and k_sb_final's loss only
+  int eval_only;
+  float* out_pred;                 // [cap_path] the head's outputs (eval; may be null)
+  float* loss_acc;                 // [2] += loss_value, += loss_value * m (eval: test()'s running sums)
 };
 
 // The dropout factor of element q (= row H + column) of layer l's type-t output: 0 (dropped, probability p) or
@@ -773,6 +778,7 @@ __global__ __launch_bounds__(kSbThreads) void k_sb_readout(SbArgs a) {
         o = group_sum(o, S);
         if (s == 0) {
           o = __fadd_rn(o, head_b);
+          if (a.out_pred) a.out_pred[r0 + rr] = o;
           const float yv = a.y[r0 + rr];
           const float u = __fdiv_rn(__fsub_rn(o, yv), yv);
           red[rr] = fabsf(u);
@@ -791,6 +797,7 @@ __global__ __launch_bounds__(kSbThreads) void k_sb_readout(SbArgs a) {
       for (int rr = 0; rr < nr; ++rr) s = __fadd_rn(s, red[rr]);
       a.loss_part[tile] = s;
     }
+    if (a.eval_only) continue;   // (uniform; the next tile's loop head syncs)
     for (int idx = tid; idx < nr * KL; idx += kSbThreads) {
       const int rr = idx / KL, k = idx % KL;
       gb0[rr * KL + k] = __fmul_rn(outv[rr], hw[k]);
@@ -1038,6 +1045,7 @@ __global__ __launch_bounds__(kRoThreadsM) void k_sb_readout_mfma(SbArgs a) {
       o = group_sum(o, S);
       if (s == 0) {
         o = __fadd_rn(o, head_b);
+        if (a.out_pred) a.out_pred[r0 + rr] = o;
         const float yv = a.y[r0 + rr];
         const float u = __fdiv_rn(__fsub_rn(o, yv), yv);
         red1[rr] = fabsf(u);
@@ -1055,6 +1063,7 @@ __global__ __launch_bounds__(kRoThreadsM) void k_sb_readout_mfma(SbArgs a) {
     for (int rr = 0; rr < nr; ++rr) s = __fadd_rn(s, red1[rr]);
     a.loss_part[tile] = s;
   }
+  if (a.eval_only) return;   // (uniform)
   for (int idx = tid; idx < nr * KL; idx += NT) {
     const int rr = idx / KL, k = idx % KL;
     gb0[rr * (KL | 1) + k] = __fmul_rn(outv[rr], hw[k]);
@@ -1813,7 +1822,12 @@ __global__ __launch_bounds__(kSbThreads) void k_sb_final(SbArgs a) {
   if (blockIdx.x == 0 && tid == 0) {
     a.loss_value[0] = lv;
     if (a.drop_thr) a.drop_ctr[0] += 1;   // (no kernel of this step reads it after this one starts)
+    if (a.eval_only) {
+      a.loss_acc[0] = __fadd_rn(a.loss_acc[0], lv);
+      a.loss_acc[1] = __fadd_rn(a.loss_acc[1], __fmul_rn(lv, (float)m));
+    }
   }
+  if (a.eval_only) return;
   const int64_t P = a.p_gin + a.p_ro;
   const int j = tid & 31, g = tid >> 5;
   for (int64_t e0 = (int64_t)blockIdx.x * 32; e0 < P; e0 += (int64_t)gridDim.x * 32) {
@@ -1981,6 +1995,11 @@ extern "C" int hgin_sb_step(const void* args, size_t args_bytes, size_t readout_
     k_sb_readout<true><<<a.n_tiles, kSbThreads, readout_lds, s>>>(a);
   else
     k_sb_readout<false><<<a.n_tiles, kSbThreads, readout_lds, s>>>(a);
+  if (a.eval_only) {   // the loss only (and the running sums)
+    HGIN_ARG_CHECK(a.loss_acc && a.ro_wlds != 3 && !a.drop_thr, "hgin_sb_step: eval (needs loss_acc; no MLP_BN, no dropout)");
+    k_sb_final<<<1, kSbThreads, 0, s>>>(a);
+    return check_launch("hgin_sb_step");
+  }
   float* gcur = a.gA;
   float* gnxt = a.gB;
   // the readout's weight-gradient groups ride in the last layer's launch and (L > 1) the first layer's, half each,
@@ -2028,7 +2047,7 @@ extern "C" int hgin_sb_args_offsets(int64_t* out, int64_t n) {
                           (int64_t)offsetof(SbArgs, gc_off),   (int64_t)offsetof(SbArgs, n_tiles),
                           (int64_t)offsetof(SbArgs, loss_value), (int64_t)offsetof(SbArgs, adam_step),
                           (int64_t)offsetof(SbArgs, weight_decay), (int64_t)offsetof(SbArgs, bn_off),
-                          (int64_t)offsetof(SbArgs, drop_inv)};
+                          (int64_t)offsetof(SbArgs, drop_inv), (int64_t)offsetof(SbArgs, loss_acc)};
   const int64_t k = (int64_t)(sizeof(offs) / sizeof(offs[0]));
   HGIN_ARG_CHECK(out && n >= k, "hgin_sb_args_offsets: need %lld slots", (long long)k);
   for (int64_t i = 0; i < k; ++i) out[i] = offs[i];

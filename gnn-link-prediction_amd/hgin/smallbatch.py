@@ -68,11 +68,11 @@ class _SbArgs(ctypes.Structure):   # field for field csrc/hgin_smallbatch.hip Sb
                 ("bn_nbt", _P * MAX_HID), ("bn_goff", _I64 * MAX_HID), ("bn_eps", ctypes.c_float),
                 ("bn_mom", ctypes.c_float), ("bn_buf", _P), ("bn_off", (_I64 * 5) * MAX_HID),
                 ("drop_ctr", _P), ("drop_seed", ctypes.c_uint64), ("drop_thr", ctypes.c_uint32),
-                ("drop_inv", ctypes.c_float)]
+                ("drop_inv", ctypes.c_float), ("eval_only", _I32), ("out_pred", _P), ("loss_acc", _P)]
 
 
 _OFFSET_FIELDS = ("goff", "m_valid", "conv", "rw", "ro_goff", "p_ro", "act_off", "zb_off", "gc_off", "n_tiles",
-                  "loss_value", "adam_step", "weight_decay", "bn_off", "drop_inv")
+                  "loss_value", "adam_step", "weight_decay", "bn_off", "drop_inv", "loss_acc")
 
 
 def foldable(opt: torch.optim.Optimizer) -> bool:
@@ -179,13 +179,17 @@ class SmallBatchStep:
         return not isinstance(_structure(model), str)
 
     def __init__(self, model: HetroGIN, opt: torch.optim.Optimizer, store: GraphStore, batch_size: int,
-                 warmup_ids: Sequence[Sequence[int]], warmup: int = 2, fold_optimizer: bool = True):
+                 warmup_ids: Sequence[Sequence[int]], warmup: int = 2, fold_optimizer: bool = True,
+                 _eval: bool = False):
         st = _structure(model)
         if isinstance(st, str):
             raise ValueError(f"SmallBatchStep: model not supported ({st}); use hgin.graphs.CapturedTrainStep")
-        self.folded = bool(fold_optimizer) and foldable(opt)
-        if not self.folded and not all(g.get("capturable", False) for g in opt.param_groups):
+        self._eval = bool(_eval)
+        self.folded = not self._eval and bool(fold_optimizer) and foldable(opt)
+        if not self._eval and not self.folded and not all(g.get("capturable", False) for g in opt.param_groups):
             raise ValueError("SmallBatchStep needs Adam (folded into the step) or a capturable optimizer")
+        if self._eval and st[-1]:
+            raise ValueError("SmallBatchEval: MLP_BN (eval-mode BatchNorm) is not fused; use hgin.graphs.CapturedEvalStep")
         if not warmup_ids:
             raise ValueError("SmallBatchStep needs at least one warm-up batch")
         convs, hidden, slope, head, H, bns = st
@@ -320,9 +324,10 @@ class SmallBatchStep:
         self.gflat = torch.zeros(off, **f32)
         self.loss_value = torch.zeros((), **f32)
         a.gflat, a.loss_value = P(self.gflat), P(self.loss_value)
-        for p in params:
-            o = param_off[p]
-            p.grad = self.gflat[o:o + p.numel()].view_as(p)
+        if not self._eval:
+            for p in params:
+                o = param_off[p]
+                p.grad = self.gflat[o:o + p.numel()].view_as(p)
         if self.folded:
             self._fold_adam(a, params, param_off, off, convs, hidden, slope, head, L, keep, bns)
         widths = (ctypes.c_int32 * MAX_HID)(*[a.rw[i] for i in range(MAX_HID)])
@@ -364,7 +369,12 @@ class SmallBatchStep:
                 for k in range(5):
                     a.bn_off[i][k] = o[5 * i + k]
             a.bn_eps, a.bn_mom = float(bns[0].eps), float(bns[0].momentum)
-        if model.dropout > 0.0:   # models.py:358-359: masks hashed from a seed drawn here and a device step counter
+        if self._eval:   # forward + loss only, the running sums on the device
+            a.eval_only = 1
+            self.out_pred = torch.zeros(cap["path"], **f32)
+            self.loss_acc = torch.zeros(2, **f32)
+            a.out_pred, a.loss_acc = P(self.out_pred), P(self.loss_acc)
+        elif model.dropout > 0.0:   # models.py:358-359: masks hashed from a seed drawn here and a device step counter
             self.drop_ctr = torch.zeros(1, dtype=torch.int64, device=dev)
             a.drop_ctr = P(self.drop_ctr)
             a.drop_seed = int(torch.randint(0, 2 ** 62, (1,)).item())
@@ -383,15 +393,18 @@ class SmallBatchStep:
             for i in range(max(1, warmup)):
                 store.collate_into(warmup_ids[i % len(warmup_ids)], pb)
                 self._launch()
-                if not self.folded:
+                if not self.folded and not self._eval:
                     opt.step()
         torch.cuda.current_stream().wait_stream(side)
         torch.cuda.synchronize()
         self.graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self.graph):
             self._launch()
-            if not self.folded:
+            if not self.folded and not self._eval:
                 opt.step()
+        self._ptrs = [p.data_ptr() for p in params]
+        if self._eval:
+            self.loss_acc.zero_()
 
     def _fold_adam(self, a, params, param_off, total, convs, hidden, slope, head, L, keep, bns) -> None:
         """The parameters become views of one flat buffer in the gradient layout, Adam's moments two more and its
@@ -448,3 +461,53 @@ class SmallBatchStep:
         self.store.collate_into(ids, self.batch)
         self.graph.replay()
         return self.loss_value
+
+
+class SmallBatchEval(SmallBatchStep):
+    """train.py's evaluation loops — ``test()`` (train.py:70-113, after ``model.eval()``) and ``evaluate()``
+    (:322-348) — on the fused small-batch kernels: per batch one device collation + one hipGraph replay of the L
+    forward launches, the readout up to its MAPE numerator (the head's outputs kept in ``out_pred``) and a one-block
+    loss launch that also adds the batch's loss_value and its path-weighted form into device accumulators (the
+    reference's ``running_loss += loss_value.item()`` and ``running_loss_mape += mape * n_paths``): a whole pass syncs
+    the host once, in ``result()``.  Same interface as ``hgin.graphs.CapturedEvalStep``; the model must be in eval
+    mode (dropout off), and MLP_BN models (eval-mode BatchNorm) go to CapturedEvalStep.
+
+    The replay reads the parameters in place: if they have been re-allocated since (a SmallBatchStep constructed
+    afterwards folds them into its flat buffer), ``step`` re-captures first."""
+
+    def __init__(self, model: HetroGIN, store: GraphStore, batch_size: int, warmup_ids: Sequence[Sequence[int]],
+                 warmup: int = 2):
+        if model.training:
+            raise ValueError("SmallBatchEval: call model.eval() first (train.py:192, :329)")
+        self._ctor = (store, batch_size, list(warmup_ids), warmup)
+        super().__init__(model, None, store, batch_size, warmup_ids, warmup, _eval=True)
+        self.batches = 0
+
+    @staticmethod
+    def supports(model: torch.nn.Module) -> bool:
+        st = _structure(model)
+        return not isinstance(st, str) and not st[-1]
+
+    def step(self, ids: Sequence[int]) -> torch.Tensor:
+        """Evaluate the graphs ``ids``; returns the batch's device loss_value (overwritten by the next step).  The
+        predictions are ``self.out_pred[:n_paths]`` until then."""
+        if [p.data_ptr() for p in self.model.parameters()] != self._ptrs:
+            acc, n = self.loss_acc.clone(), self.batches
+            store, bs, wids, w = self._ctor
+            SmallBatchStep.__init__(self, self.model, None, store, bs, wids, w, _eval=True)
+            self.loss_acc.copy_(acc)
+            self.batches = n
+        self.store.collate_into(ids, self.batch)
+        self.graph.replay()
+        self.batches += 1
+        return self.loss_value
+
+    def reset(self) -> None:
+        self.loss_acc.zero_()
+        self.batches = 0
+
+    def result(self, n_paths: int) -> tuple:
+        """(average loss over the batches, path-weighted MAPE) = test()'s (average_loss, mape_loss) for a loss_func
+        of MAPE; ``n_paths`` = the paths evaluated.  One host sync."""
+        s, w = (float(v) for v in self.loss_acc.cpu())
+        return s / max(self.batches, 1), w / max(n_paths, 1)

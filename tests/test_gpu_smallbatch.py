@@ -247,6 +247,62 @@ def test_fused_step_dropout_masks_and_gradients(monkeypatch):
     assert lv2 != lv and not torch.equal(step.act.detach().cpu(), act)
 
 
+@pytest.mark.parametrize("variant", ["default", "global_feats_dropout"])
+def test_fused_eval_vs_oracle_and_captured(variant):
+    """SmallBatchEval (train.py:70-113 test() / :322-348 evaluate() on the fused kernels) in eval mode: per batch the
+    loss within 1e-5 relative and the predictions within 1e-5 of the CPU oracle's eval-mode forward on the host-collated
+    batch (dropout off); result()'s running sums equal CapturedEvalStep's within 1e-5; after a SmallBatchStep on the
+    same model has folded its parameters into a flat buffer (and taken an Adam step), the evaluation re-captures and
+    follows the new parameters."""
+    from hgin.graphs import CapturedEvalStep
+    from hgin.smallbatch import SmallBatchEval, SmallBatchStep
+    from oracle.pyg_cpu import OracleHetroGIN, mape
+    store, cfg = _store(10, seed=29)
+    over = {} if variant == "default" else dict(global_feats=True, bl_features=True, dropout=0.2)
+    kw = lambda: dict(cfg.model_kwargs({"link": cfg.f_link, "path": cfg.f_path, "node": cfg.f_node}),  # noqa: E731
+                      **over)
+    torch.manual_seed(1997)
+    m = HetroGIN(**kw()).to(DEV).eval()
+    ev = SmallBatchEval(m, store, batch_size=4, warmup_ids=[[0, 1]], warmup=1)
+    seq = [[2, 5, 7], [1, 9], [3, 4, 6, 8]]
+
+    def check(ref):
+        n_paths = 0
+        for ids in seq:
+            lv = float(ev.step(ids))
+            torch.cuda.synchronize()
+            b = _host_batch(store, ids)
+            with torch.no_grad():
+                out = ref(b.x_dict(), b.edge_index_dict(), b.batch["path"])
+            lv_ref = float(mape(out, b.y.reshape(-1, 1)))
+            assert abs(lv - lv_ref) <= 1e-5 * abs(lv_ref), (ids, lv, lv_ref)
+            n = out.shape[0]
+            n_paths += n
+            assert torch.allclose(ev.out_pred[:n].cpu(), out.reshape(-1), rtol=1e-5, atol=1e-5), ids
+        return n_paths
+
+    ref = OracleHetroGIN(**kw())
+    ref.load_state_dict({k: v.detach().cpu() for k, v in m.state_dict().items()})
+    ref.eval()
+    n_paths = check(ref)
+    avg, mp = ev.result(n_paths)
+    ce = CapturedEvalStep(m, store, 4, warmup_ids=[[0, 1]], warmup=1)
+    for ids in seq:
+        ce.step(ids)
+    avg2, mp2 = ce.result(n_paths)
+    assert abs(avg - avg2) <= 1e-5 * abs(avg2) and abs(mp - mp2) <= 1e-5 * abs(mp2), (avg, avg2, mp, mp2)
+    # a training step folds the parameters elsewhere and moves them: the evaluation follows
+    m.train()
+    st = SmallBatchStep(m, torch.optim.Adam(m.parameters(), lr=1e-2), store, batch_size=4, warmup_ids=[[0, 1]],
+                        warmup=1)
+    st.step([3, 8])
+    m.eval()
+    torch.cuda.synchronize()
+    ref.load_state_dict({k: v.detach().cpu() for k, v in m.state_dict().items()})
+    ev.reset()
+    check(ref)
+
+
 @pytest.mark.parametrize("variant", ["default", "mlp_bn_global_feats"])
 def test_fused_trajectory_vs_oracle(variant):
     """Five shuffled batches with Adam(lr=1e-3) (train.py:31-44): the fused step's loss trajectory against
