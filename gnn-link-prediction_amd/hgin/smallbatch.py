@@ -403,6 +403,7 @@ class SmallBatchStep:
             if not self.folded and not self._eval:
                 opt.step()
         self._ptrs = [p.data_ptr() for p in params]
+        self._first, self._last = params[0], params[-1]
         if self._eval:
             self.loss_acc.zero_()
 
@@ -491,7 +492,9 @@ class SmallBatchEval(SmallBatchStep):
     def step(self, ids: Sequence[int]) -> torch.Tensor:
         """Evaluate the graphs ``ids``; returns the batch's device loss_value (overwritten by the next step).  The
         predictions are ``self.out_pred[:n_paths]`` until then."""
-        if [p.data_ptr() for p in self.model.parameters()] != self._ptrs:
+        # (a re-allocation — a folding SmallBatchStep, model.to() — moves every parameter: the first and the last
+        # are checked, cheaply, per batch)
+        if self._first.data_ptr() != self._ptrs[0] or self._last.data_ptr() != self._ptrs[-1]:
             acc, n = self.loss_acc.clone(), self.batches
             store, bs, wids, w = self._ctor
             SmallBatchStep.__init__(self, self.model, None, store, bs, wids, w, _eval=True)

@@ -21,6 +21,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--model", default="{}", help='HetroGIN keyword overrides as JSON, e.g. {"mlp_bn": true}')
+    ap.add_argument("--eval", type=int, default=0, help="> 0: SmallBatchEval at this batch size instead")
     args = ap.parse_args()
     dev = torch.device("cuda")
     base = CONFIGS["cfg1"]
@@ -33,8 +34,14 @@ def main():
     kw = dict(base.model_kwargs({"link": base.f_link, "path": base.f_path, "node": base.f_node}),
               **json.loads(args.model))
     model = HetroGIN(**kw).to(dev)
-    opt = torch.optim.Adam(lr=1e-3, params=model.parameters())
-    st = SmallBatchStep(model, opt, store, 8, warmup_ids=order[:5], warmup=5)
+    if args.eval:
+        from hgin.smallbatch import SmallBatchEval
+        model.eval()
+        order = [ids[:args.eval] for ids in order]
+        st = SmallBatchEval(model, store, args.eval, warmup_ids=order[:5], warmup=5)
+    else:
+        opt = torch.optim.Adam(lr=1e-3, params=model.parameters())
+        st = SmallBatchStep(model, opt, store, 8, warmup_ids=order[:5], warmup=5)
     torch.cuda.synchronize()
     s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     s.record()
