@@ -663,6 +663,14 @@ __device__ unsigned long long g_sb_stamps[kStampRo + kStampW];
 #define SB_STAMP_W(l, k)
 #endif
 
+// MLP_BN in evaluation (SmallBatchEval): hidden layer i's BatchNorm1d with its running statistics, an affine map per
+// column — (z - running_mean) / sqrt(running_var + eps) gamma + beta, torch's eval-mode order of operations
+__device__ __forceinline__ float bn_eval(const SbArgs& a, int i, int n, float z) {
+  if (!a.eval_only || !a.bn_w[i]) return z;
+  const float xh = __fdiv_rn(__fsub_rn(z, a.bn_rm[i][n]), sqrtf(__fadd_rn(a.bn_rv[i][n], a.bn_eps)));
+  return __fadd_rn(__fmul_rn(xh, a.bn_w[i][n]), a.bn_b[i][n]);
+}
+
 template <bool kWL>
 __global__ __launch_bounds__(kSbThreads) void k_sb_readout(SbArgs a) {
   extern __shared__ float sm[];
@@ -733,7 +741,7 @@ __global__ __launch_bounds__(kSbThreads) void k_sb_readout(SbArgs a) {
         const float* in = i == 0 ? in0 : sm + oY[i > 0 ? i - 1 : 0];
         const int K = win[i], N = a.rw[i];
         auto epi = [&](int q, int o, float z) {
-          z = __fadd_rn(z, RO_B(i)[o]);
+          z = bn_eval(a, i, o, __fadd_rn(z, RO_B(i)[o]));
           sm[oZ[i] + q] = z;
           const float yv = z > 0.0f ? z : __fmul_rn(slope, z);
           sm[oY[i] + q] = yv;
@@ -1025,7 +1033,7 @@ __global__ __launch_bounds__(kRoThreadsM) void k_sb_readout_mfma(SbArgs a) {
       const int N = a.rw[i];
       const float* b = kWL ? (const float*)(sm + oW[i] + N * ldw[i]) : a.row_b[i];
       tile_mfma<NT>(in, lin, nr, RO_WM(i), 1, ldw[i], N, win[i], red, [&](int r, int n, float v) {
-        const float z = __fadd_rn(v, b[n]);
+        const float z = bn_eval(a, i, n, __fadd_rn(v, b[n]));
         sm[oZ[i] + r * lz[i] + n] = z;
         const float yv = z > 0.0f ? z : __fmul_rn(slope, z);
         sm[oY[i] + r * lz[i] + n] = yv;
@@ -1996,7 +2004,7 @@ extern "C" int hgin_sb_step(const void* args, size_t args_bytes, size_t readout_
   else
     k_sb_readout<false><<<a.n_tiles, kSbThreads, readout_lds, s>>>(a);
   if (a.eval_only) {   // the loss only (and the running sums)
-    HGIN_ARG_CHECK(a.loss_acc && a.ro_wlds != 3 && !a.drop_thr, "hgin_sb_step: eval (needs loss_acc; no MLP_BN, no dropout)");
+    HGIN_ARG_CHECK(a.loss_acc && a.ro_wlds != 3 && !a.drop_thr, "hgin_sb_step: eval (needs loss_acc, no dropout)");
     k_sb_final<<<1, kSbThreads, 0, s>>>(a);
     return check_launch("hgin_sb_step");
   }

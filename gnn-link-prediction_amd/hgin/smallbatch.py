@@ -188,8 +188,6 @@ class SmallBatchStep:
         self.folded = not self._eval and bool(fold_optimizer) and foldable(opt)
         if not self._eval and not self.folded and not all(g.get("capturable", False) for g in opt.param_groups):
             raise ValueError("SmallBatchStep needs Adam (folded into the step) or a capturable optimizer")
-        if self._eval and st[-1]:
-            raise ValueError("SmallBatchEval: MLP_BN (eval-mode BatchNorm) is not fused; use hgin.graphs.CapturedEvalStep")
         if not warmup_ids:
             raise ValueError("SmallBatchStep needs at least one warm-up batch")
         convs, hidden, slope, head, H, bns = st
@@ -335,7 +333,9 @@ class SmallBatchStep:
         # the readout: 32-row tiles on the matrix cores, their weights in LDS where they fit, else read through the
         # caches (mode 4; HGIN_SB_MFMA=0: the 8-row scalar tiles, with the hidden weights in LDS, else without)
         # (MLP_BN: the k_sb_bn_* launches, mode 3)
-        modes = (3,) if bns else ((2, 4, 1, 0) if os.environ.get("HGIN_SB_MFMA", "1") != "0" else (1, 0))
+        # (MLP_BN in evaluation: the plain readout with BatchNorm's running-statistics affine map, bn_eval)
+        modes = (3,) if bns and not self._eval else ((2, 4, 1, 0) if os.environ.get("HGIN_SB_MFMA", "1") != "0"
+                                                     else (1, 0))
         for wl in modes:
             _lib.check(_lib.lib().hgin_sb_readout_lds_bytes(H, w0 - H, int(w0 > H), a.nhid, widths, wl,
                                                             ctypes.byref(lds)), "hgin_sb_readout_lds_bytes")
@@ -357,7 +357,9 @@ class SmallBatchStep:
                       for i in range(a.nhid + 1)]
         for i in range(a.nhid + 1):
             a.ro_in[i], a.ro_gz[i] = P(self.ro_in[i]), P(self.ro_gz[i])
-        if bns:   # per hidden layer: z, g_y [cap_path][N], forward / backward tile partials [tiles][2][N], statistics
+        if bns and self._eval:
+            a.bn_eps = float(bns[0].eps)
+        elif bns:   # per hidden layer: z, g_y [cap_path][N], forward / backward tile partials [tiles][2][N], statistics
             nt32 = (cap["path"] + 31) // 32
             sizes = []
             for i in range(a.nhid):
@@ -471,7 +473,7 @@ class SmallBatchEval(SmallBatchStep):
     loss launch that also adds the batch's loss_value and its path-weighted form into device accumulators (the
     reference's ``running_loss += loss_value.item()`` and ``running_loss_mape += mape * n_paths``): a whole pass syncs
     the host once, in ``result()``.  Same interface as ``hgin.graphs.CapturedEvalStep``; the model must be in eval
-    mode (dropout off), and MLP_BN models (eval-mode BatchNorm) go to CapturedEvalStep.
+    mode (dropout off; MLP_BN's BatchNorm reads its running statistics: an affine map in the readout's epilogue).
 
     The replay reads the parameters in place: if they have been re-allocated since (a SmallBatchStep constructed
     afterwards folds them into its flat buffer), ``step`` re-captures first."""
@@ -486,8 +488,7 @@ class SmallBatchEval(SmallBatchStep):
 
     @staticmethod
     def supports(model: torch.nn.Module) -> bool:
-        st = _structure(model)
-        return not isinstance(st, str) and not st[-1]
+        return not isinstance(_structure(model), str)
 
     def step(self, ids: Sequence[int]) -> torch.Tensor:
         """Evaluate the graphs ``ids``; returns the batch's device loss_value (overwritten by the next step).  The

@@ -247,18 +247,20 @@ def test_fused_step_dropout_masks_and_gradients(monkeypatch):
     assert lv2 != lv and not torch.equal(step.act.detach().cpu(), act)
 
 
-@pytest.mark.parametrize("variant", ["default", "global_feats_dropout"])
+@pytest.mark.parametrize("variant", ["default", "global_feats_dropout", "mlp_bn"])
 def test_fused_eval_vs_oracle_and_captured(variant):
     """SmallBatchEval (train.py:70-113 test() / :322-348 evaluate() on the fused kernels) in eval mode: per batch the
     loss within 1e-5 relative and the predictions within 1e-5 of the CPU oracle's eval-mode forward on the host-collated
-    batch (dropout off); result()'s running sums equal CapturedEvalStep's within 1e-5; after a SmallBatchStep on the
-    same model has folded its parameters into a flat buffer (and taken an Adam step), the evaluation re-captures and
+    batch (dropout off; MLP_BN's BatchNorm on its running statistics); result()'s running sums equal
+    CapturedEvalStep's within 1e-5; after a SmallBatchStep on the same model has folded its parameters into a flat
+    buffer (and taken an Adam step, which also moves MLP_BN's running statistics), the evaluation re-captures and
     follows the new parameters."""
     from hgin.graphs import CapturedEvalStep
     from hgin.smallbatch import SmallBatchEval, SmallBatchStep
     from oracle.pyg_cpu import OracleHetroGIN, mape
     store, cfg = _store(10, seed=29)
-    over = {} if variant == "default" else dict(global_feats=True, bl_features=True, dropout=0.2)
+    over = {"default": {}, "global_feats_dropout": dict(global_feats=True, bl_features=True, dropout=0.2),
+            "mlp_bn": dict(mlp_bn=True)}[variant]
     kw = lambda: dict(cfg.model_kwargs({"link": cfg.f_link, "path": cfg.f_path, "node": cfg.f_node}),  # noqa: E731
                       **over)
     torch.manual_seed(1997)

@@ -54,11 +54,11 @@ def test_refuses_a_non_capturable_optimizer_before_touching_the_device():
         SmallBatchStep(model, opt, store=None, batch_size=8, warmup_ids=[[0]], fold_optimizer=False)
 
 
-def test_fused_eval_takes_the_fused_models_without_batchnorm():
+def test_fused_eval_takes_the_fused_models():
     from hgin.smallbatch import SmallBatchEval
     assert SmallBatchEval.supports(HetroGIN(**_kw()))
     assert SmallBatchEval.supports(HetroGIN(**_kw(global_feats=True, bl_features=True, dropout=0.2)))
-    assert not SmallBatchEval.supports(HetroGIN(**_kw(mlp_bn=True)))   # eval-mode BatchNorm: CapturedEvalStep
+    assert SmallBatchEval.supports(HetroGIN(**_kw(mlp_bn=True)))   # eval-mode BatchNorm: an affine map
     m = HetroGIN(**_kw())
     with pytest.raises(ValueError, match="model.eval"):   # (before any device work)
         SmallBatchEval(m, None, 4, warmup_ids=[[0]])
