@@ -145,6 +145,12 @@ def test_fused_step_vs_oracle_variants(variant):
             assert torch.equal(u.cpu(), v), n
         else:
             assert torch.allclose(u.cpu(), v, rtol=1e-5, atol=1e-6), (n, float((u.cpu() - v).abs().max()))
+    # bitwise run to run (fixed-order sums everywhere, BatchNorm's merges included): the same batch again
+    g1 = [p.grad.detach().clone() for p in m1.parameters()]
+    assert float(step.step(ids)) == lv
+    torch.cuda.synchronize()
+    for g, p in zip(g1, m1.parameters()):
+        assert torch.equal(g, p.grad)
 
 
 def test_fused_step_vs_reference_fixture_global_bn():
