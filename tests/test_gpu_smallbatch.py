@@ -258,6 +258,40 @@ def test_fused_step_dropout_masks_and_gradients(monkeypatch):
     assert lv2 != lv and not torch.equal(step.act.detach().cpu(), act)
 
 
+@pytest.mark.parametrize("variant", ["default", "mlp_bn_global_feats"])
+def test_fused_step_ragged_batches_vs_oracle(variant):
+    """The epoch's ragged batches (the last DataLoader batch is short: dataset.py:239-244): one captured step of
+    capacity 4 replayed on 1, 4, 2 and 3 graphs, each step (Adam at lr 0) against the CPU oracle on its host-collated
+    batch — loss 1e-5, gradients 1e-4 of their norm (+1e-6 of the largest with MLP_BN)."""
+    from hgin.smallbatch import SmallBatchStep
+    from oracle.pyg_cpu import OracleHetroGIN, mape
+    store, cfg = _store(10, seed=31)
+    over = {} if variant == "default" else dict(mlp_bn=True, global_feats=True, bl_features=True)
+    kw = lambda: dict(cfg.model_kwargs({"link": cfg.f_link, "path": cfg.f_path, "node": cfg.f_node}),  # noqa: E731
+                      **over)
+    torch.manual_seed(1997)
+    m1 = HetroGIN(**kw()).to(DEV)
+    step = SmallBatchStep(m1, torch.optim.Adam(m1.parameters(), lr=0.0, capturable=True), store, batch_size=4,
+                          warmup_ids=[[0, 1, 2, 3]], warmup=1)
+    for ids in ([5], [1, 2, 3, 4], [7, 0], [9, 6, 8]):
+        torch.cuda.synchronize()
+        ref = OracleHetroGIN(**kw())
+        ref.load_state_dict({k: v.detach().cpu() for k, v in m1.state_dict().items()})
+        lv = float(step.step(ids))
+        torch.cuda.synchronize()
+        b = _host_batch(store, ids)
+        out = ref(b.x_dict(), b.edge_index_dict(), b.batch["path"])
+        lv_ref = mape(out, b.y.reshape(-1, 1))
+        torch.sqrt(lv_ref).backward()
+        assert abs(lv - float(lv_ref)) <= 1e-5 * abs(float(lv_ref)), (ids, lv, float(lv_ref))
+        gmax = max(float(q.grad.double().norm()) for q in ref.parameters() if q.grad is not None)
+        slack = 1e-6 * gmax if over else 1e-9
+        for (n, p), q in zip(m1.named_parameters(), ref.parameters()):
+            want = q.grad if q.grad is not None else torch.zeros_like(q)
+            d = float((p.grad.detach().cpu() - want).double().norm())
+            assert d <= 1e-4 * float(want.double().norm()) + slack, (ids, n, d, float(want.norm()))
+
+
 @pytest.mark.parametrize("variant", ["default", "global_feats_dropout", "mlp_bn"])
 def test_fused_eval_vs_oracle_and_captured(variant):
     """SmallBatchEval (train.py:70-113 test() / :322-348 evaluate() on the fused kernels) in eval mode: per batch the
