@@ -88,7 +88,63 @@ def parse():
     ap.add_argument("--graph", action="store_true",
                     help="one hipGraph replay per step (default: the step issued from Python; measured equal on cfg2 "
                          "and cfg5 — the step is GPU-bound, the host runs ahead)")
+    ap.add_argument("--launch-dry-run", action="store_true",
+                    help="print the rank-launch decision for --gpus as JSON and exit (touches no GPU)")
     return ap.parse_args()
+
+
+def launch_plan(gpus: int, env, n_devices: int) -> dict:
+    """How this invocation becomes `gpus` ranks (one process per GPU), decided before any HIP call.
+
+    * WORLD_SIZE set (torch.distributed.run started us): it must equal --gpus, otherwise the line would report a
+      different GPU count than asked for -> error.
+    * --gpus N > 1 without WORLD_SIZE: re-launch through torch.distributed.run as N fresh child ranks (a child
+      process, never an exec of this one), provided the node has N devices -> "spawn"; else error.
+    * --gpus 1 without WORLD_SIZE: run here.
+    HGIN_DIST_BACKEND=gloo is the 1-GPU rehearsal of the multi-rank path (ranks share the device), so the device
+    count is not checked for it.  ``n_devices`` is torch.cuda.device_count(), which does not initialise HIP."""
+    gloo = env.get("HGIN_DIST_BACKEND", "nccl") == "gloo"
+    if gpus < 1:
+        return {"action": "error", "reason": f"--gpus {gpus}: need at least one GPU"}
+    ws = env.get("WORLD_SIZE")
+    if ws is not None:
+        if not ws.isdigit() or int(ws) != gpus:
+            return {"action": "error",
+                    "reason": f"--gpus {gpus} but the launcher set WORLD_SIZE={ws}: refusing to report a run of "
+                              f"{ws} rank(s) as {gpus} GPU(s)"}
+        return {"action": "run", "world": gpus}
+    if gpus == 1:
+        return {"action": "run", "world": 1}
+    if n_devices < gpus and not gloo:
+        return {"action": "error", "reason": f"--gpus {gpus} but this node shows {n_devices} GPU(s)"}
+    return {"action": "spawn", "world": gpus,
+            "argv": [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
+                     "--master-addr", "127.0.0.1", "--master-port", "{port}", os.path.abspath(__file__)]}
+
+
+def _free_port() -> int:
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def apply_launch_plan(args) -> None:
+    """Carry out launch_plan before anything touches the GPU: exit non-zero on an error, or run the ranks as a child
+    torch.distributed.run and exit with its status."""
+    plan = launch_plan(args.gpus, os.environ, torch.cuda.device_count())
+    if args.launch_dry_run:
+        print(json.dumps(plan), flush=True)
+        raise SystemExit(0)
+    if plan["action"] == "error":
+        print(f"bench.py: {plan['reason']}", file=sys.stderr, flush=True)
+        raise SystemExit(2)
+    if plan["action"] == "spawn":
+        import subprocess
+        argv = [a.replace("{port}", str(_free_port())) for a in plan["argv"]] + sys.argv[1:]
+        print(f"bench.py: --gpus {args.gpus} without a launcher: starting {args.gpus} ranks via torch.distributed.run",
+              file=sys.stderr, flush=True)
+        raise SystemExit(subprocess.run(argv, env=dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")).returncode)
 
 
 def cpu_threads() -> int:
@@ -637,6 +693,8 @@ def gemm_fields(m, bf16: bool, steps: int, t_step: float, what: str):
 
 def main():
     args = parse()
+    if not args.cpu_full:
+        apply_launch_plan(args)
     if args.cpu_full:
         from hgin.data import CONFIGS
         rec = cpu_baseline(CONFIGS[args.cpu_full], full_graph=True)
@@ -653,8 +711,7 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus and rank == 0:
-        print(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
+    assert world == args.gpus, (world, args.gpus)   # apply_launch_plan guarantees it
     # One rank per GPU.  HGIN_DIST_BACKEND=gloo (+ more ranks than GPUs) is only for rehearsing the
     # multi-rank path on a 1-GPU box; the measured runs use RCCL ("nccl" on ROCm) over xGMI.
     backend = os.environ.get("HGIN_DIST_BACKEND", "nccl")

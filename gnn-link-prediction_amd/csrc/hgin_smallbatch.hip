@@ -1203,13 +1203,15 @@ __device__ void bn_merge_fwd(const SbArgs& a, int i, int m, int ntile, float* s_
       float* st = bn_ptr(a, i, 4);
       st[tid] = gm;
       st[N + tid] = inv;
+    }
+    if (first && m > 1) {   // (torch raises on a one-row training batch; here the running statistics stay as they are)
       const float mo = a.bn_mom, keep = __fsub_rn(1.0f, mo);
       const float unb = __fdiv_rn(g2, (float)(m - 1));
       a.bn_rm[i][tid] = __fadd_rn(__fmul_rn(keep, a.bn_rm[i][tid]), __fmul_rn(mo, gm));
       a.bn_rv[i][tid] = __fadd_rn(__fmul_rn(keep, a.bn_rv[i][tid]), __fmul_rn(mo, unb));
     }
   }
-  if (first && tid == 0) a.bn_nbt[i][0] += 1;
+  if (first && m > 1 && tid == 0) a.bn_nbt[i][0] += 1;
   __syncthreads();
 }
 

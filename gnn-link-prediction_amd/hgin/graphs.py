@@ -159,11 +159,18 @@ class CapturedEvalStep:
         self.loss_sum = torch.zeros((), dtype=torch.float32, device=dev)
         self.loss_paths = torch.zeros((), dtype=torch.float32, device=dev)
         self.batches = 0
+        self._warm = (list(warmup_ids), warmup)
+        self._capture()
+
+    def _capture(self) -> None:
+        """Warm up on a side stream, then capture forward + fused head / MAPE + the accumulation once.  The graph holds
+        the parameters' device pointers: they are recorded, and ``step`` re-captures if they move."""
+        warmup_ids, warmup = self._warm
         side = torch.cuda.Stream()
         side.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(side), torch.no_grad():
             for i in range(max(1, warmup)):
-                store.collate_into(warmup_ids[i % len(warmup_ids)], self.batch)
+                self.store.collate_into(warmup_ids[i % len(warmup_ids)], self.batch)
                 self._forward()
         torch.cuda.current_stream().wait_stream(side)
         torch.cuda.synchronize()
@@ -172,6 +179,11 @@ class CapturedEvalStep:
             self.out, self.loss = self._forward()
             self.loss_sum.add_(self.loss)
             self.loss_paths.add_(self.loss * self.batch.m_valid[0].to(torch.float32))
+        self._ptrs = self._param_ptrs()
+
+    def _param_ptrs(self):
+        ps = list(self.model.parameters())
+        return (ps[0].data_ptr(), ps[-1].data_ptr()) if ps else ()
 
     def _forward(self):
         b = self.batch
@@ -179,7 +191,13 @@ class CapturedEvalStep:
 
     def step(self, ids: Sequence[int]) -> torch.Tensor:
         """Evaluate the graphs ``ids``; returns the batch's device loss_value (overwritten by the next step).  The
-        predictions are ``self.out[:n_paths]`` until then."""
+        predictions are ``self.out[:n_paths]`` until then.  If the parameters were re-allocated since the capture (a
+        folding SmallBatchStep, model.to()), the step is re-captured first (the running sums are kept)."""
+        if self._param_ptrs() != self._ptrs:
+            acc = (self.loss_sum.clone(), self.loss_paths.clone())
+            self._capture()
+            self.loss_sum.copy_(acc[0])
+            self.loss_paths.copy_(acc[1])
         self.store.collate_into(ids, self.batch)
         self.graph.replay()
         self.batches += 1

@@ -55,7 +55,12 @@ def _host_call_device(model: torch.nn.Module, x_dict, edge_index_dict, path_batc
     return torch.device("cuda", torch.cuda.current_device())
 
 
-_LENT: "weakref.WeakKeyDictionary" = weakref.WeakKeyDictionary()   # model -> {id(t): (key, device copy, ref(t))}
+_LENT: "weakref.WeakKeyDictionary" = weakref.WeakKeyDictionary()   # model -> {id(t): (key, dev copy, ref(t), snapshot)}
+
+
+def release_device_cache(model: torch.nn.Module) -> None:
+    """Drop the device copies (and host snapshots) a host-resident model keeps between ``evaluate()`` calls."""
+    _LENT.pop(model, None)
 
 
 def _host_call(model: torch.nn.Module, dev, x_dict, edge_index_dict, path_batch):
@@ -76,14 +81,17 @@ def _host_call(model: torch.nn.Module, dev, x_dict, edge_index_dict, path_batch)
             seen.add(id(t))
             lent.append((t, t.data))
     # device copies are kept per model between calls (evaluate() runs one call per batch with unchanged weights) and
-    # re-copied when a tensor's version, storage or shape changed (load_state_dict, in-place edits)
+    # re-copied when a tensor's version, storage, shape or VALUES changed: load_state_dict, in-place edits, and edits
+    # through ``p.data`` (which do not bump ``p._version``) — each call compares the host tensor with a host snapshot
+    # taken when its copy was made (O(parameters) on the host; no device traffic).  The cache holds a device copy and a
+    # host snapshot of every parameter and buffer while the model lives: release_device_cache(model) drops them.
     cache = _LENT.setdefault(model, {})
     try:
         for t, d in lent:
             key = (t._version, d.data_ptr(), tuple(d.shape), d.dtype, str(dev))
             hit = cache.get(id(t))
-            if hit is None or hit[0] != key or hit[2]() is not t:
-                hit = (key, d.to(dev), weakref.ref(t))
+            if hit is None or hit[0] != key or hit[2]() is not t or not torch.equal(d, hit[3]):
+                hit = (key, d.to(dev), weakref.ref(t), d.clone())
                 cache[id(t)] = hit
             t.data = hit[1]
         xd = {k: v.to(dev) for k, v in x_dict.items()}
@@ -277,20 +285,26 @@ def _masked_batch_norm(x: torch.Tensor, bn: torch.nn.BatchNorm1d, m_valid: torch
     (hgin/graphs.py): those rows' mean and biased variance normalise every row (the padding rows' outputs feed only
     masked loss rows), and the running statistics take the unbiased variance with the layer's momentum — torch's
     BatchNorm on the exact batch, up to the order of the fp32 sums.  m_valid is a device count: no host sync, so
-    the step stays capturable."""
+    the step stays capturable.  Padding rows are selected out (not multiplied by 0), so an inf / NaN there cannot
+    reach the statistics.  A batch of one valid row (torch raises: "Expected more than 1 value per channel") leaves
+    the running statistics and num_batches_tracked unchanged, as the fused step's k_sb_bn does."""
     if bn.momentum is None:
         raise NotImplementedError("masked BatchNorm: momentum=None (cumulative average) is not supported")
     n = x.shape[0]
-    mask = (torch.arange(n, device=x.device) < m_valid.to(torch.int64)).to(x.dtype).unsqueeze(1)
+    mask = (torch.arange(n, device=x.device) < m_valid.to(torch.int64)).unsqueeze(1)
     m = m_valid.to(x.dtype)
-    mean = (x * mask).sum(0) / m
-    d = (x - mean) * mask
+    zero = x.new_zeros(())
+    mean = torch.where(mask, x, zero).sum(0) / m
+    d = torch.where(mask, x - mean, zero)
     var = (d * d).sum(0) / m
     if bn.track_running_stats:
         with torch.no_grad():
-            bn.running_mean.mul_(1.0 - bn.momentum).add_(mean.detach() * bn.momentum)
-            bn.running_var.mul_(1.0 - bn.momentum).add_(var.detach() * (m / (m - 1.0)) * bn.momentum)
-            bn.num_batches_tracked.add_(1)
+            upd = m > 1.0
+            rm = bn.running_mean * (1.0 - bn.momentum) + mean.detach() * bn.momentum
+            rv = bn.running_var * (1.0 - bn.momentum) + var.detach() * (m / torch.clamp(m - 1.0, min=1.0)) * bn.momentum
+            bn.running_mean.copy_(torch.where(upd, rm, bn.running_mean))
+            bn.running_var.copy_(torch.where(upd, rv, bn.running_var))
+            bn.num_batches_tracked.add_(upd.to(bn.num_batches_tracked.dtype).reshape(bn.num_batches_tracked.shape))
     y = (x - mean) / torch.sqrt(var + bn.eps)
     if bn.affine:
         y = y * bn.weight + bn.bias

@@ -75,14 +75,30 @@ _OFFSET_FIELDS = ("goff", "m_valid", "conv", "rw", "ro_goff", "p_ro", "act_off",
                   "loss_value", "adam_step", "weight_decay", "bn_off", "drop_inv", "loss_acc")
 
 
-def foldable(opt: torch.optim.Optimizer) -> bool:
-    """Adam with one parameter group, float hyperparameters, amsgrad / maximize off: its update can run inside the
-    fused step's final kernel (csrc/hgin_smallbatch.hip adam_update)."""
+def foldable(opt: torch.optim.Optimizer, params=None) -> bool:
+    """Adam with one parameter group, float hyperparameters, amsgrad / maximize / decoupled weight decay off: its update
+    can run inside the fused step's final kernel (csrc/hgin_smallbatch.hip adam_update, L2 weight decay through the
+    gradient).  With ``params`` (the model's parameters): the group must hold exactly those, all requiring gradients —
+    the folded update writes every parameter of the model."""
     if type(opt) is not torch.optim.Adam or len(opt.param_groups) != 1:
         return False
     g = opt.param_groups[0]
-    return (not g.get("amsgrad", False) and not g.get("maximize", False) and not g.get("differentiable", False)
-            and not isinstance(g["lr"], torch.Tensor) and all(not isinstance(b, torch.Tensor) for b in g["betas"]))
+    if (g.get("amsgrad", False) or g.get("maximize", False) or g.get("differentiable", False)
+            or g.get("decoupled_weight_decay", False) or isinstance(g["lr"], torch.Tensor)
+            or any(isinstance(b, torch.Tensor) for b in g["betas"])):
+        return False
+    if params is not None:
+        params = list(params)
+        if {id(p) for p in g["params"]} != {id(p) for p in params} or len(g["params"]) != len(params):
+            return False
+        if not all(p.requires_grad for p in params):
+            return False
+    return True
+
+
+def _hyper(opt: torch.optim.Optimizer) -> tuple:
+    g = opt.param_groups[0]
+    return (float(g["lr"]), float(g["betas"][0]), float(g["betas"][1]), float(g["eps"]), float(g["weight_decay"]))
 
 
 def check_layout() -> None:
@@ -185,7 +201,7 @@ class SmallBatchStep:
         if isinstance(st, str):
             raise ValueError(f"SmallBatchStep: model not supported ({st}); use hgin.graphs.CapturedTrainStep")
         self._eval = bool(_eval)
-        self.folded = not self._eval and bool(fold_optimizer) and foldable(opt)
+        self.folded = not self._eval and bool(fold_optimizer) and foldable(opt, model.parameters())
         if not self._eval and not self.folded and not all(g.get("capturable", False) for g in opt.param_groups):
             raise ValueError("SmallBatchStep needs Adam (folded into the step) or a capturable optimizer")
         if not warmup_ids:
@@ -414,7 +430,6 @@ class SmallBatchStep:
         step count one device scalar; the optimizer's state entries are re-pointed at them (its existing state, if
         any, copied in), so opt.state_dict() stays meaningful.  The step then owns the optimizer: calling
         opt.step() as well would update twice."""
-        g = self.opt.param_groups[0]
         f32 = dict(dtype=torch.float32, device=self.gflat.device)
         self.pflat = torch.empty(total, **f32)
         self.mflat = torch.zeros(total, **f32)
@@ -452,8 +467,49 @@ class SmallBatchStep:
         keep += [self.pflat, self.mflat, self.vflat, self.adam_step]
         a.pflat, a.mflat, a.vflat = self.pflat.data_ptr(), self.mflat.data_ptr(), self.vflat.data_ptr()
         a.adam_step = self.adam_step.data_ptr()
-        a.lr, a.beta1, a.beta2 = float(g["lr"]), float(g["betas"][0]), float(g["betas"][1])
-        a.adam_eps, a.weight_decay = float(g["eps"]), float(g["weight_decay"])
+        self._set_hyper(a)
+        self._params, self._param_off = params, param_off
+        self._state_first = self.opt.state[params[0]]["exp_avg"]
+
+    def _set_hyper(self, a) -> None:
+        self._hyp = _hyper(self.opt)
+        a.lr, a.beta1, a.beta2, a.adam_eps, a.weight_decay = self._hyp
+
+    def _sync_optimizer(self) -> None:
+        """The folded Adam's hyperparameters and state live in the captured launch and the flat buffers: follow the
+        optimizer when it has changed since — a new lr / betas / eps / weight_decay in its param group (an LR scheduler,
+        a manual edit) re-captures the step with them; a replaced state (opt.load_state_dict) is copied into the flat
+        moments and step count and re-pointed at them.  A changed parameter set raises."""
+        g = self.opt.param_groups
+        if len(g) != 1 or len(g[0]["params"]) != len(self._params) or any(
+                p is not q for p, q in zip(g[0]["params"], self._params)):
+            raise RuntimeError("SmallBatchStep: the folded optimizer's parameter groups changed; build a new step")
+        st = self.opt.state.get(self._params[0])
+        if st is None or st.get("exp_avg") is not self._state_first:
+            steps = set()
+            with torch.no_grad():
+                for p in self._params:
+                    o, n = self._param_off[p], p.numel()
+                    s = self.opt.state.get(p)
+                    if not s:
+                        raise RuntimeError("SmallBatchStep: the optimizer's new state misses a parameter")
+                    self.mflat[o:o + n].copy_(s["exp_avg"].reshape(-1))
+                    self.vflat[o:o + n].copy_(s["exp_avg_sq"].reshape(-1))
+                    steps.add(float(s["step"]))
+            if len(steps) != 1:
+                raise RuntimeError("SmallBatchStep: the optimizer's new state has parameters at different steps")
+            self.adam_step.fill_(steps.pop())
+            for p in self._params:
+                o, n = self._param_off[p], p.numel()
+                self.opt.state[p] = {"step": self.adam_step, "exp_avg": self.mflat[o:o + n].view_as(p),
+                                     "exp_avg_sq": self.vflat[o:o + n].view_as(p)}
+            self._state_first = self.opt.state[self._params[0]]["exp_avg"]
+        if _hyper(self.opt) != self._hyp:
+            self._set_hyper(self.args)
+            torch.cuda.synchronize()
+            self.graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(self.graph):
+                self._launch()
 
     def _launch(self) -> None:
         _lib.call("hgin_sb_step", ctypes.addressof(self.args), ctypes.sizeof(self.args), self.lds,
@@ -461,6 +517,8 @@ class SmallBatchStep:
 
     def step(self, ids: Sequence[int]) -> torch.Tensor:
         """One training step on the graphs ``ids``; returns the device loss_value (no host sync)."""
+        if self.folded:
+            self._sync_optimizer()
         self.store.collate_into(ids, self.batch)
         self.graph.replay()
         return self.loss_value

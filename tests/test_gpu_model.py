@@ -325,6 +325,16 @@ def test_evaluate_host_resident_call(case):
         fresh.eval()
         out4 = fresh(dict(x), ei, batch)
     assert torch.equal(out3, out4) and not torch.equal(out3, out)
+    # an edit through .data does not bump the parameter's version counter: still followed
+    next(model.parameters()).data.mul_(2.0)
+    with torch.no_grad():
+        out5 = model(dict(x), ei, batch)
+        fresh.load_state_dict(model.state_dict())
+        out6 = fresh(dict(x), ei, batch)
+    assert torch.equal(out5, out6) and not torch.equal(out5, out3)
+    from hgin.models import release_device_cache
+    release_device_cache(model)
+    assert model not in _LENT
     model.train()
     with pytest.raises(RuntimeError, match="gradients enabled"):
         model(dict(x), ei, batch)

@@ -46,6 +46,16 @@ def test_refuses_a_non_capturable_optimizer_before_touching_the_device():
     assert foldable(torch.optim.Adam(model.parameters(), lr=1e-3))
     assert not foldable(torch.optim.Adam(model.parameters(), lr=1e-3, amsgrad=True))
     assert not foldable(torch.optim.AdamW(model.parameters(), lr=1e-3))
+    #  updates the folded kernel would not reproduce, or parameters it would train against the caller's wish
+    if "decoupled_weight_decay" in torch.optim.Adam([torch.zeros(1, requires_grad=True)]).defaults:
+        assert not foldable(torch.optim.Adam(model.parameters(), lr=1e-3, weight_decay=1e-2,
+                                             decoupled_weight_decay=True))
+    params = list(model.parameters())
+    assert foldable(torch.optim.Adam(params, lr=1e-3, weight_decay=1e-2), params)
+    assert not foldable(torch.optim.Adam(params[1:], lr=1e-3), params)          # a parameter left out
+    params[0].requires_grad_(False)
+    assert not foldable(torch.optim.Adam(params, lr=1e-3), params)              # a frozen parameter
+    params[0].requires_grad_(True)
     opt = torch.optim.SGD(model.parameters(), lr=1e-3)   # not capturable
     with pytest.raises(ValueError, match="capturable"):
         SmallBatchStep(model, opt, store=None, batch_size=8, warmup_ids=[[0]])
