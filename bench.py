@@ -316,9 +316,9 @@ def batches_extra(dev, n_graphs: int = 256, batch: int = 8, warmup: int = 5, ste
     (hgin/smallbatch.py: 3 L + 1 kernels, Adam folded in) — the main figure whenever it takes config.json's model — and
     the general per-op path (hgin/graphs.py CapturedTrainStep) beside it.  ``configs``: the reference's other model
     switches (models.py / config.json) that the fused step refuses, each timed on the same batches through the path
-    that takes it — MLP_BN, GLOBAL_FEATS and DROPOUT > 0 (eager exact batches: BatchNorm statistics, pooling and
-    dropout must not see padding rows), NODE_EMBEDDING_SIZE 128 and MODEL = "GAT" (HEADS 16, config.json's hidden 8
-    and 1 layer) as hipGraph replays.  HIP events around the timed batches; reported beside the headline."""
+    that takes it — MLP_BN, GLOBAL_FEATS, DROPOUT > 0, NODE_EMBEDDING_SIZE 128 and MODEL = "GAT" (HEADS 16,
+    config.json's hidden 8 and 1 layer): all through the fused step now (HetroGAT included), the captured general path
+    for what it refuses.  HIP events around the timed batches; reported beside the headline."""
     import numpy as np
 
     from hgin import HetroGAT, HetroGIN
@@ -413,7 +413,7 @@ def batches_extra(dev, n_graphs: int = 256, batch: int = 8, warmup: int = 5, ste
     for name, (ov, gat, kind) in switches.items():
         try:
             model = build(ov, gat)
-            if not gat and SmallBatchStep.supports(model):
+            if SmallBatchStep.supports(model):   # (HetroGAT too: k_sb_gat_fwd / k_sb_gat_bwd)
                 kind = "fused"
             r = run(kind, model, cfg_steps)
             r["execution"] = exec_desc[kind]

@@ -20,39 +20,20 @@
 namespace hgin {
 namespace {
 
-// Batched tail (HGIN_AGG_TAIL = 0 / 1): GIN rows are short (uniform random graphs: mean degree 5-10), so
-// with full-batch-then-one-at-a-time walking most neighbours of most rows were fetched one dependent round
-// trip at a time.  Batched: every batch of up to U neighbour rows is in flight together (lanes past the
-// row's end issue nothing); the adds stay sequential in edge order (bit-identical).
-bool agg_tail_batched() {
-  static const bool v = [] {
-    const char* e = getenv("HGIN_AGG_TAIL");
-    return e ? atoi(e) != 0 : true;
-  }();
-  return v;
-}
-
-// Neighbour rows in flight per lane group (HGIN_AGG_U = 8 / 16; 16 only with the batched tail).
-int agg_u() {
-  static const int v = [] {
-    const char* e = getenv("HGIN_AGG_U");
-    return e && atoi(e) == 16 ? 16 : 8;
-  }();
-  return v;
-}
+// Batched tail: GIN rows are short (uniform random graphs: mean degree 5-10), so with full-batch-then-one-at-a-time
+// walking most neighbours of most rows were fetched one dependent round trip at a time.  Batched: every batch of up to
+// U = 8 neighbour rows is in flight together (lanes past the row's end issue nothing); the adds stay sequential in edge
+// order (bit-identical).  (Round 6: the one-at-a-time tail and U = 16 variants and their switches are gone: measured
+// slower or equal, profiles/r01_agg_tail.txt.)
+constexpr int kAggU = 8;
 
 // Non-temporal self-term loads / output stores (the streamed-once data) so they do not evict the gathered source
 // table from L2 / the Infinity Cache.  Measured: 3-9 % faster for the concat layer at every size
 // (profiles/r01_agg_nt.txt); for the other modes 1-2 % slower at cfg2, whose tables fit in the 256 MiB Infinity
 // Cache, and 4-5 % faster at cfg3, whose tables do not (aggregate 5.48-5.57 -> 5.77 TB/s, step 212-214 -> 209.6
 // ms: profiles/r02/agg_variants_cfg3.txt).  So: concat always, the other modes once the output stream alone
-// exceeds 512 MiB (cfg2's largest is 307 MB).  HGIN_AGG_NT = 0 / 1 forces one choice.
+// exceeds 512 MiB (cfg2's largest is 307 MB).
 bool agg_nt(int combine, int64_t n_rows, int64_t out_row_bytes) {
-  static const int env = [] {
-    const char* v = getenv("HGIN_AGG_NT");
-    return v ? atoi(v) : -1;
-  }();
-  if (env >= 0) return env != 0;
   return combine == HGIN_COMBINE_CONCAT || n_rows * out_row_bytes > (int64_t(512) << 20);
 }
 
@@ -101,9 +82,8 @@ struct Vec<4> {
   }
 };
 
-// kTail: the neighbour walk issues every batch's loads together, the last partial batch included (see
-// agg_tail_batched); otherwise full batches of U, then the remainder one neighbour at a time.
-template <int VEC, int G, int U, bool NT, bool kTail>
+// The neighbour walk issues every batch's loads together, the last partial batch included (kAggU above).
+template <int VEC, int G, int U, bool NT>
 __global__ __launch_bounds__(256) void k_aggregate(const int32_t* __restrict__ rowptr, const int32_t* __restrict__ col,
                                                    int64_t n_rows, const float* __restrict__ x_src, int64_t ld_src,
                                                    int f_src, const float* __restrict__ x_dst, int64_t ld_dst,
@@ -127,44 +107,22 @@ __global__ __launch_bounds__(256) void k_aggregate(const int32_t* __restrict__ r
     float acc[VEC];
 #pragma unroll
     for (int c = 0; c < VEC; ++c) acc[c] = 0.0f;
-    int k = beg;
-    if constexpr (kTail) {
-      // every batch, including a row's last partial one, issues its (up to U) neighbour loads together;
-      // lanes past the row's end load nothing and add nothing (rows are mostly shorter than U)
-      for (; k < end; k += U) {
-        const int n = end - k;
-        T v[U];
+    // every batch, including a row's last partial one, issues its (up to U) neighbour loads together;
+    // lanes past the row's end load nothing and add nothing (rows are mostly shorter than U)
+    for (int k = beg; k < end; k += U) {
+      const int n = end - k;
+      T v[U];
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
-          v[u] = T{};
-          if (u < n) v[u] = V::load(x_src + (int64_t)col[k + u] * ld_src + f0);
-        }
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-          if (u < n) {
-#pragma unroll
-            for (int c = 0; c < VEC; ++c) acc[c] = __fadd_rn(acc[c], V::get(v[u], c));
-          }
-        }
+      for (int u = 0; u < U; ++u) {
+        v[u] = T{};
+        if (u < n) v[u] = V::load(x_src + (int64_t)col[k + u] * ld_src + f0);
       }
-    } else {
-      for (; k + U <= end; k += U) {
-        int idx[U];
 #pragma unroll
-        for (int u = 0; u < U; ++u) idx[u] = col[k + u];
-        T v[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) v[u] = V::load(x_src + (int64_t)idx[u] * ld_src + f0);
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
+      for (int u = 0; u < U; ++u) {
+        if (u < n) {
 #pragma unroll
           for (int c = 0; c < VEC; ++c) acc[c] = __fadd_rn(acc[c], V::get(v[u], c));
         }
-      }
-      for (; k < end; ++k) {
-        const T v = V::load(x_src + (int64_t)col[k] * ld_src + f0);
-#pragma unroll
-        for (int c = 0; c < VEC; ++c) acc[c] = __fadd_rn(acc[c], V::get(v, c));
       }
     }
     T o;
@@ -198,14 +156,11 @@ int launch_aggregate(const int32_t* rowptr, const int32_t* col, int64_t n_rows, 
   const int64_t blocks = ceil_div(waves, 256 / kWave);
   const bool nt = agg_nt(combine, n_rows, (int64_t)(f_src + (combine == HGIN_COMBINE_CONCAT ? f_dst : 0)) * 4);
   HGIN_TRACE("k_aggregate<f32,G%d,mode%d>", G, combine);
-#define HGIN_AGG_L(UV, NTV, TAIL)                                                                           \
-  k_aggregate<VEC, G, UV, NTV, TAIL><<<dim3((unsigned)blocks), 256, 0, s>>>(rowptr, col, n_rows, x_src, ld_src, \
-                                                                           f_src, x_dst, ld_dst, f_dst, eps,     \
-                                                                           combine, out, ld_out)
-  const bool tail = agg_tail_batched();
-  if (agg_u() == 16 && tail) { if (nt) HGIN_AGG_L(16, true, true); else HGIN_AGG_L(16, false, true); }
-  else if (nt) { if (tail) HGIN_AGG_L(8, true, true); else HGIN_AGG_L(8, true, false); }
-  else { if (tail) HGIN_AGG_L(8, false, true); else HGIN_AGG_L(8, false, false); }
+#define HGIN_AGG_L(NTV)                                                                                    \
+  k_aggregate<VEC, G, kAggU, NTV><<<dim3((unsigned)blocks), 256, 0, s>>>(rowptr, col, n_rows, x_src, ld_src, \
+                                                                        f_src, x_dst, ld_dst, f_dst, eps,     \
+                                                                        combine, out, ld_out)
+  if (nt) HGIN_AGG_L(true); else HGIN_AGG_L(false);
 #undef HGIN_AGG_L
   return check_launch("hgin_aggregate_f32");
 }
@@ -266,7 +221,7 @@ struct BVec<8> {
   }
 };
 
-template <int VEC, int G, int U, bool NT, bool kTail>
+template <int VEC, int G, int U, bool NT>
 __global__ __launch_bounds__(256) void k_aggregate_bf16(const int32_t* __restrict__ rowptr,
                                                         const int32_t* __restrict__ col, int64_t n_rows,
                                                         const uint16_t* __restrict__ x_src, int64_t ld_src, int f_src,
@@ -291,47 +246,22 @@ __global__ __launch_bounds__(256) void k_aggregate_bf16(const int32_t* __restric
     float acc[VEC];
 #pragma unroll
     for (int c = 0; c < VEC; ++c) acc[c] = 0.0f;
-    int k = beg;
-    if constexpr (kTail) {
-      for (; k < end; k += U) {   // batched tail, as k_aggregate
-        const int n = end - k;
-        T v[U];
+    for (int k = beg; k < end; k += U) {   // batched tail, as k_aggregate
+      const int n = end - k;
+      T v[U];
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
-          v[u] = T{};
-          if (u < n) v[u] = V::load(x_src + (int64_t)col[k + u] * ld_src + f0);
-        }
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-          if (u < n) {
-            float f[VEC];
-            V::unpack(v[u], f);
-#pragma unroll
-            for (int c = 0; c < VEC; ++c) acc[c] = __fadd_rn(acc[c], f[c]);
-          }
-        }
+      for (int u = 0; u < U; ++u) {
+        v[u] = T{};
+        if (u < n) v[u] = V::load(x_src + (int64_t)col[k + u] * ld_src + f0);
       }
-    } else {
-      for (; k + U <= end; k += U) {
-        int idx[U];
 #pragma unroll
-        for (int u = 0; u < U; ++u) idx[u] = col[k + u];
-        T v[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) v[u] = V::load(x_src + (int64_t)idx[u] * ld_src + f0);
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
+      for (int u = 0; u < U; ++u) {
+        if (u < n) {
           float f[VEC];
           V::unpack(v[u], f);
 #pragma unroll
           for (int c = 0; c < VEC; ++c) acc[c] = __fadd_rn(acc[c], f[c]);
         }
-      }
-      for (; k < end; ++k) {
-        float f[VEC];
-        V::unpack(V::load(x_src + (int64_t)col[k] * ld_src + f0), f);
-#pragma unroll
-        for (int c = 0; c < VEC; ++c) acc[c] = __fadd_rn(acc[c], f[c]);
       }
     }
     if (combine == HGIN_COMBINE_ADD) {
@@ -360,14 +290,11 @@ int launch_aggregate_bf16(const int32_t* rowptr, const int32_t* col, int64_t n_r
   constexpr int kRowsPerWave = kWave / G;
   const int64_t blocks = ceil_div(ceil_div(n_rows, kRowsPerWave), 256 / kWave);
   HGIN_TRACE("k_aggregate<bf16,G%d,mode%d>", G, combine);
-#define HGIN_AGGB_L(UV, NTV, TAIL)                                    \
-  k_aggregate_bf16<VEC, G, UV, NTV, TAIL><<<dim3((unsigned)blocks), 256, 0, s>>>( \
+#define HGIN_AGGB_L(NTV)                                                                       \
+  k_aggregate_bf16<VEC, G, kAggU, NTV><<<dim3((unsigned)blocks), 256, 0, s>>>(                            \
       rowptr, col, n_rows, x_src, ld_src, f_src, x_dst, ld_dst, f_dst, eps, combine, out, ld_out)
-  const bool tail = agg_tail_batched();
   const bool nt = agg_nt(combine, n_rows, (int64_t)(f_src + (combine == HGIN_COMBINE_CONCAT ? f_dst : 0)) * 2);
-  if (agg_u() == 16 && tail) { if (nt) HGIN_AGGB_L(16, true, true); else HGIN_AGGB_L(16, false, true); }
-  else if (nt) { if (tail) HGIN_AGGB_L(8, true, true); else HGIN_AGGB_L(8, true, false); }
-  else { if (tail) HGIN_AGGB_L(8, false, true); else HGIN_AGGB_L(8, false, false); }
+  if (nt) HGIN_AGGB_L(true); else HGIN_AGGB_L(false);
 #undef HGIN_AGGB_L
   return check_launch("hgin_aggregate_bf16");
 }
@@ -444,13 +371,11 @@ __device__ __forceinline__ void st_quad(void* p, const uint4& v) {
 // shapes (cfg3 backward +7.8 %), fp32 6-9 % slower (fewer resident waves: 5-6 per SIMD against the one-row
 // kernels' short-lived 8), so the default is the pipelined walk for bf16 and the batched-tail kernel for fp32.
 // HGIN_AGG_PIPE = 0 / 1 forces one choice for both element types.
+// the pipelined walk for bf16 (1.7-1.9 % faster); fp32 keeps the batched-tail kernel (6-9 % faster there:
+// profiles/r01_agg_pipe.txt)
 template <typename T>
-bool agg_pipe_enabled() {
-  static const int v = [] {
-    const char* e = getenv("HGIN_AGG_PIPE");
-    return e ? atoi(e) : -1;
-  }();
-  return v >= 0 ? v != 0 : sizeof(T) == 2;
+constexpr bool agg_pipe_enabled() {
+  return sizeof(T) == 2;
 }
 
 template <int G>

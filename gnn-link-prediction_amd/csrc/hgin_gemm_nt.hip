@@ -566,13 +566,7 @@ bool nt_bdma_enabled() {
 // workgroups per CU (A split once per 256 columns: half the split VALU per MFMA of the 128 x 128 tile): the first
 // layer's K = 512 forward at M = 6M 9.61 -> 9.38 ms, with accum 10.18 -> 10.03 ms (profiles/r04/gpu_a/gemm_ab_*.json);
 // bit-identical (tests/test_gpu_gemm_switch.py).  HGIN_NT_T256=0 keeps the 128 x 128 tile.
-bool nt_t256_enabled() {
-  static const bool on = [] {
-    const char* v = getenv("HGIN_NT_T256");
-    return !(v && v[0] == '0');
-  }();
-  return on;
-}
+constexpr bool nt_t256_enabled() { return true; }
 
 template <int EPI, int TN, int WN, int NW = 4>
 int64_t launch_nt_tn(bool vec, const Src2& a, const Src2& b, int64_t M, int64_t N, int64_t K, const float* bias,
@@ -636,12 +630,6 @@ int64_t resident_slots(F kernel) {
 // MFMA); kRel64 = 0.8 keeps 128 unless the round count drops clearly (M = 100k: 100.6 -> 90.3 us, -10 %).
 template <int EPI>
 bool use_bm64(int64_t M, int64_t N) {
-  static const int env = [] {
-    const char* v = getenv("HGIN_NT_BM");
-    return v ? atoi(v) : 0;
-  }();
-  if (env == 64) return true;
-  if (env == 128) return false;
   static const int64_t slots128 = gemm_split_enabled() ? resident_slots(k_gemm_nt<EPI, true, 2, 2, true>)
                                                        : resident_slots(k_gemm_nt<EPI, true, 2, 2, false>);
   static const int64_t slots64 = gemm_split_enabled() ? resident_slots(k_gemm_nt<EPI, true, 1, 4, true>)
@@ -656,11 +644,6 @@ bool use_bm64(int64_t M, int64_t N) {
 // Non-temporal epilogue streams (HGIN_GEMM_NT_IO = 0 / 1 forces; default: once the output stream exceeds
 // 512 MiB, as the aggregate's streams — outputs read back only by later kernels, far beyond the caches).
 bool gemm_nt_io(int64_t M, int64_t N, int64_t elem) {
-  static const int env = [] {
-    const char* v = getenv("HGIN_GEMM_NT_IO");
-    return v ? atoi(v) : -1;
-  }();
-  if (env >= 0) return env != 0;
   return M * N * elem > (int64_t(512) << 20);
 }
 
@@ -891,12 +874,6 @@ __global__ __launch_bounds__(256, BKH == 64 ? 3 : 2) void k_gemm_nt_bf16(Src2h A
 
 template <int EPI, typename OutT>
 bool use_bm64_bf16(int64_t M, int64_t N) {
-  static const int env = [] {
-    const char* v = getenv("HGIN_NT_BM");
-    return v ? atoi(v) : 0;
-  }();
-  if (env == 64) return true;
-  if (env == 128) return false;
   static const int64_t slots128 = resident_slots(k_gemm_nt_bf16<EPI, true, 2, 2, OutT>);
   static const int64_t slots64 = resident_slots(k_gemm_nt_bf16<EPI, true, 1, 4, OutT>);
   constexpr double kRel64 = 0.8;
@@ -928,10 +905,12 @@ bool use_bm64_bf16(int64_t M, int64_t N) {
 // (the DMA lanes fetch pre-swizzled sources; a ds_read_b128 group of 16 rows hits 16 distinct bank slots);
 // accum rows linear; fp32 staging [16][N] with column bit 5 flipped on rows with bit 2 set (the two lane halves
 // of an accumulator store hit opposite bank halves).
-template <int K, int N>
+template <int K, int N, int CPW = 32>
 struct WsCfg {
-  static constexpr int NW = N / 32;                     // waves (one 32-column W slice each)
+  static constexpr int NW = N / CPW;                    // waves (one CPW-column W slice each)
   static constexpr int NT = NW * 64;
+  static constexpr int TN = CPW / 32;                   // 32-column MFMA tiles per wave
+  static constexpr int RPP = NT / (N / 4);              // epilogue rows per pass (a thread per 4-column group)
   static constexpr int KS = K / 16;                     // MFMA k-steps
   static constexpr int BM = K >= 256 ? 32 : 64;         // rows per block (A image >= 16 KB: the staging area)
   static constexpr int TM = BM / 32;
@@ -946,11 +925,13 @@ struct WsCfg {
   static_assert((A_BYTES / 16) % NT == 0, "eps-scaling pass");
 };
 
-template <int K, int N, int NIMG>
+template <int K, int N, int NIMG, int CPW = 32>
 struct WsRing {
-  static constexpr int SLOT = WsCfg<K, N>::A_BYTES + NIMG * WsCfg<K, N>::C_BYTES;
-  // ring depth: as deep as 144 KB of LDS allows, up to 4 (0: does not fit, the tiled kernel is used)
-  static constexpr int NST = SLOT * 4 <= 147456 ? 4 : SLOT * 3 <= 147456 ? 3 : SLOT * 2 <= 147456 ? 2 : 0;
+  static constexpr int SLOT = WsCfg<K, N, CPW>::A_BYTES + NIMG * WsCfg<K, N, CPW>::C_BYTES;
+  // ring depth: as deep as 144 KB of LDS allows (80 KB at CPW 64: two workgroups per CU), up to 4 (0: does not fit,
+  // the tiled kernel is used)
+  static constexpr int CAP = CPW == 64 ? 81920 : 147456;
+  static constexpr int NST = SLOT * 4 <= CAP ? 4 : SLOT * 3 <= CAP ? 3 : SLOT * 2 <= CAP ? 2 : 0;
   static constexpr int BYTES = SLOT * (NST > 0 ? NST : 1);
 };
 
@@ -1004,14 +985,15 @@ struct WsArgs32 {
   bool nt_in;
 };
 
-template <int K, int N, int EPI, bool kR1, bool kZ, bool kR2>
-__global__ __launch_bounds__((WsCfg<K, N>::NT), 1) void k_ws_bf16(WsArgs g) {
-  using C = WsCfg<K, N>;
+template <int K, int N, int EPI, bool kR1, bool kZ, bool kR2, int CPW = 32>
+__global__ __launch_bounds__((WsCfg<K, N, CPW>::NT), (CPW == 64 ? 2 : 1)) void k_ws_bf16(WsArgs g) {
+  using C = WsCfg<K, N, CPW>;
   constexpr int NIMG = (kR1 ? 1 : 0) + (kR2 ? 1 : 0);
-  using R = WsRing<K, N, NIMG>;
+  using R = WsRing<K, N, NIMG, CPW>;
   constexpr int NST = R::NST;
   constexpr int P = C::PA + NIMG * C::PC;                        // DMA instructions per wave per block
-  constexpr int S = C::TM * 4 * (kZ ? 2 : 1);                    // stores per lane per block
+  constexpr int NPASS = 16 / C::RPP;                             // epilogue passes per 16-row half
+  constexpr int S = C::TM * 2 * NPASS * (kZ ? 2 : 1);            // stores per lane per block
   constexpr int QPR = N / 4;                                     // 4-column groups per row
   constexpr int kWaitSteady = (NST - 2) * P + (NST - 1) * S < 63 ? (NST - 2) * P + (NST - 1) * S : 63;
   constexpr int kWaitEarly = (NST - 2) * P < 63 ? (NST - 2) * P : 63;
@@ -1027,12 +1009,13 @@ __global__ __launch_bounds__((WsCfg<K, N>::NT), 1) void k_ws_bf16(WsArgs g) {
   if ((int64_t)blockIdx.x >= nblk) return;
   const int64_t my = (nblk - 1 - blockIdx.x) / G + 1;             // blocks blockIdx.x + i G, i < my
 
-  // this wave's W slice as B fragments: lane (li, lh) holds W[32 wave + li][16 t + 8 lh .. + 7]
-  uint4 wf[C::KS];
-  {
-    const uint16_t* wr = g.w + (int64_t)(wave * 32 + li) * K + lh * 8;
+  // this wave's W slice as B fragments: lane (li, lh) holds W[CPW wave + 32 tn + li][16 t + 8 lh .. + 7]
+  uint4 wf[C::TN][C::KS];
 #pragma unroll
-    for (int t = 0; t < C::KS; ++t) wf[t] = *reinterpret_cast<const uint4*>(wr + t * 16);
+  for (int tn = 0; tn < C::TN; ++tn) {
+    const uint16_t* wr = g.w + (int64_t)(wave * CPW + tn * 32 + li) * K + lh * 8;
+#pragma unroll
+    for (int t = 0; t < C::KS; ++t) wf[tn][t] = *reinterpret_cast<const uint4*>(wr + t * 16);
   }
   // row-pass columns of this thread (fixed), bias, PReLU slope, eps scales
   const int cq = (tid % QPR) * 4;
@@ -1052,7 +1035,10 @@ __global__ __launch_bounds__((WsCfg<K, N>::NT), 1) void k_ws_bf16(WsArgs g) {
   // consume the prologue loads here, so that the compiler's own wait for them sits before the ring starts and
   // not inside the loop (where it would count the ring's DMAs)
 #pragma unroll
-  for (int t = 0; t < C::KS; ++t) asm volatile("" ::"v"(wf[t].x), "v"(wf[t].y), "v"(wf[t].z), "v"(wf[t].w));
+  for (int tn = 0; tn < C::TN; ++tn)
+#pragma unroll
+    for (int t = 0; t < C::KS; ++t)
+      asm volatile("" ::"v"(wf[tn][t].x), "v"(wf[tn][t].y), "v"(wf[tn][t].z), "v"(wf[tn][t].w));
 #pragma unroll
   for (int t = 0; t < 4; ++t) asm volatile("" ::"v"(bcol[t]));
 
@@ -1158,11 +1144,13 @@ __global__ __launch_bounds__((WsCfg<K, N>::NT), 1) void k_ws_bf16(WsArgs g) {
     uint16_t* yb = g.y + r0 * ldy;                                // block-uniform output bases
     uint16_t* zb = kZ ? g.z + r0 * ldz : nullptr;
 
-    f32x16 acc[C::TM];
+    f32x16 acc[C::TM][C::TN];
 #pragma unroll
     for (int tm = 0; tm < C::TM; ++tm)
 #pragma unroll
-      for (int e = 0; e < 16; ++e) acc[tm][e] = 0.0f;
+      for (int tn = 0; tn < C::TN; ++tn)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) acc[tm][tn][e] = 0.0f;
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int t = 0; t < C::KS; ++t) {
@@ -1170,8 +1158,11 @@ __global__ __launch_bounds__((WsCfg<K, N>::NT), 1) void k_ws_bf16(WsArgs g) {
       for (int tm = 0; tm < C::TM; ++tm) {
         const int r = tm * 32 + li;
         const uint4 u = *reinterpret_cast<const uint4*>(abase + r * C::ROWB + (((2 * t + lh) ^ (r & 15)) << 4));
-        acc[tm] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, u),
-                                                          __builtin_bit_cast(bf16x8, wf[t]), acc[tm], 0, 0, 0);
+#pragma unroll
+        for (int tn = 0; tn < C::TN; ++tn)
+          acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, u),
+                                                                __builtin_bit_cast(bf16x8, wf[tn][t]), acc[tm][tn], 0,
+                                                                0, 0);
       }
     }
     __builtin_amdgcn_s_setprio(0);
@@ -1187,17 +1178,19 @@ __global__ __launch_bounds__((WsCfg<K, N>::NT), 1) void k_ws_bf16(WsArgs g) {
         __builtin_amdgcn_s_barrier();             // A image reads / the previous half's staging reads are done
         asm volatile("" ::: "memory");
 #pragma unroll
-        for (int e8 = 0; e8 < 8; ++e8) {
-          const int e = 8 * h + e8;
-          const int row = (e & 3) + 8 * ((e >> 2) & 1) + 4 * lh;          // row within the 16-row half
-          stg[row * N + ((wave * 32 + li) ^ (((row >> 2) & 1) << 5))] = acc[tm][e];
-        }
+        for (int tn = 0; tn < C::TN; ++tn)
+#pragma unroll
+          for (int e8 = 0; e8 < 8; ++e8) {
+            const int e = 8 * h + e8;
+            const int row = (e & 3) + 8 * ((e >> 2) & 1) + 4 * lh;        // row within the 16-row half
+            stg[row * N + ((wave * CPW + tn * 32 + li) ^ (((row >> 2) & 1) << 5))] = acc[tm][tn][e];
+          }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
 #pragma unroll
-        for (int pass = 0; pass < 2; ++pass) {
-          const int row = pass * 8 + rq;
+        for (int pass = 0; pass < NPASS; ++pass) {
+          const int row = pass * C::RPP + rq;
           const int brow = tm * 32 + h * 16 + row;                        // row within the block
           const int64_t grow = r0 + brow;
           const float4 v4 = *reinterpret_cast<const float4*>(stg + row * N + (cq ^ (((row >> 2) & 1) << 5)));
@@ -1254,15 +1247,8 @@ bool ws_enabled() {
   return on;
 }
 
-// Non-temporal DMA of the streamed A / row-image rows (HGIN_WS_NT = 0 / 1; default on: 1-3 % faster at the
-// cfg5 shapes, profiles/r02/gemm_ws_bf16.txt).
-bool ws_nt_in() {
-  static const bool on = [] {
-    const char* v = getenv("HGIN_WS_NT");
-    return !(v && v[0] == '0');
-  }();
-  return on;
-}
+// Non-temporal DMA of the streamed A / row-image rows (1-3 % faster at the cfg5 shapes, profiles/r02/gemm_ws_bf16.txt).
+constexpr bool ws_nt_in() { return true; }
 
 int ws_grid() {
   static const int g = [] {
@@ -1274,24 +1260,30 @@ int ws_grid() {
   return g;
 }
 
-template <int K, int N, int EPI, bool kR1, bool kZ, bool kR2>
+// N = 256, K <= 256 without row images (the forward without accum, the plain dX): two 4-wave workgroups per CU, each
+// wave holding 64 W columns (128 VGPRs at K = 256) — while one workgroup runs its epilogue's barriers the other's
+// MFMAs run.  M = 3M, K = N = 256, bf16: 1.13 -> 1.04-1.07 ms (profiles/r06/gemm_ab_bf16.txt).  With a row image
+// (accum, x_dst) the 80 KB per workgroup leave a 2-deep ring and it measured slower (1.17 -> 1.19-1.23 ms), so those
+// keep 32 columns per wave and one workgroup per CU.
+template <int K, int N, int EPI, bool kR1, bool kZ, bool kR2, int CPW = (N == 256 && K <= 256 && !kR1 && !kR2) ? 64 : 32>
 int launch_ws_kn(const WsArgs& a, hipStream_t s, const char* what, int64_t* grid_out) {
-  using Ring = WsRing<K, N, (kR1 ? 1 : 0) + (kR2 ? 1 : 0)>;
+  using Ring = WsRing<K, N, (kR1 ? 1 : 0) + (kR2 ? 1 : 0), CPW>;
   if constexpr (Ring::NST < 2) {
     return -1;
   } else {
     constexpr int lds = Ring::BYTES;
-    auto kern = k_ws_bf16<K, N, EPI, kR1, kZ, kR2>;
+    auto kern = k_ws_bf16<K, N, EPI, kR1, kZ, kR2, CPW>;
     static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
                                                        hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     if (attr != hipSuccess) {
       set_error("%s: hipFuncSetAttribute failed: %s", what, hipGetErrorString(attr));
       return (int)attr;
     }
-    const int64_t nblk = ceil_div(a.M, (int64_t)WsCfg<K, N>::BM);
-    const int64_t grid = nblk < ws_grid() ? nblk : ws_grid();
-    HGIN_TRACE("k_ws_bf16<%d,%d,EPI%d>", K, N, EPI);
-    kern<<<(unsigned)grid, WsCfg<K, N>::NT, lds, s>>>(a);
+    const int64_t nblk = ceil_div(a.M, (int64_t)WsCfg<K, N, CPW>::BM);
+    const int64_t g_max = (int64_t)ws_grid() * (CPW == 64 ? 2 : 1);
+    const int64_t grid = nblk < g_max ? nblk : g_max;
+    HGIN_TRACE("k_ws_bf16<%d,%d,EPI%d%s>", K, N, EPI, CPW == 64 ? ",cpw64" : "");
+    kern<<<(unsigned)grid, WsCfg<K, N, CPW>::NT, lds, s>>>(a);
     if (grid_out) *grid_out = grid;
     return check_launch(what);
   }
@@ -1936,13 +1928,7 @@ __global__ __launch_bounds__(512, 1) void k_wss_f32(WsArgs32 g) {
 
 // HGIN_WS_STAGGER = 0 keeps k_ws_f32.  Default on: fwd256 at M = 6M 4.95 -> 4.49 ms per launch, the cfg3 step
 // 183.3 -> 179.4 ms (profiles/r04/gpu_s).
-bool wss_enabled() {
-  static const bool on = [] {
-    const char* v = getenv("HGIN_WS_STAGGER");
-    return !(v && v[0] == '0');
-  }();
-  return on;
-}
+constexpr bool wss_enabled() { return true; }
 
 template <int EPI, bool kR1, bool kZ>
 int launch_wss(const WsArgs32& a, hipStream_t s, const char* what, int64_t* grid_out = nullptr) {

@@ -565,13 +565,7 @@ __global__ __launch_bounds__(256) void k_slab_reduce(const float* __restrict__ s
   }
 }
 
-bool slab_fused_enabled() {
-  static const bool on = [] {
-    const char* e = getenv("HGIN_SLAB_REDUCE");
-    return !(e && std::string(e) == "2pass");
-  }();
-  return on;
-}
+constexpr bool slab_fused_enabled() { return true; }
 
 // ---------------------------------------------------------------------------------------------------
 // bf16 operands (cfg5): 64 rows of M per stage.  (A register-transposing bf16 dW kernel, measured 1.9x slower than
@@ -1522,15 +1516,12 @@ template <int NV, int KV, bool PRO = false>
 int64_t launch_wsd(const uint16_t* a, int64_t lda, const uint16_t* b1, int64_t ldb1, const uint16_t* b2,
                    int64_t ldb2, int64_t k1, int64_t M, float* slab, int64_t ld_slab, int64_t grid, hipStream_t s,
                    const WsdPro& pro = WsdPro{}) {
+  constexpr bool nt = true;   // non-temporal DMA of the streamed rows (1-3 % faster, profiles/r02/gemm_ws_bf16.txt)
   constexpr int lds = WsdCfg<NV, KV, PRO>::SLOT * WsdCfg<NV, KV, PRO>::NST;
   auto kern = k_wsd_bf16<NV, KV, PRO>;
   static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
                                                      hipFuncAttributeMaxDynamicSharedMemorySize, lds);
   if (attr != hipSuccess) return 0;
-  static const bool nt = [] {
-    const char* v = getenv("HGIN_WS_NT");
-    return !(v && v[0] == '0');
-  }();
   HGIN_TRACE("k_wsd_bf16<%d,%d%s>", NV, KV, PRO ? ",prelu_bwd_fused" : "");
   kern<<<(unsigned)grid, 512, lds, s>>>(a, lda, b1, ldb1, b2, ldb2, k1, M, slab, ld_slab, nt, pro);
   return grid;
@@ -1540,10 +1531,7 @@ template <int NV, int KV, bool PRO = false>
 int64_t launch_wsd(const float* a, int64_t lda, const float* b1, int64_t ldb1, const float* b2, int64_t ldb2,
                    int64_t k1, int64_t M, float* slab, int64_t ld_slab, int64_t grid, hipStream_t s,
                    const WsdPro& pro = WsdPro{}) {
-  static const bool nt = [] {
-    const char* v = getenv("HGIN_WS_NT");
-    return !(v && v[0] == '0');
-  }();
+  constexpr bool nt = true;   // non-temporal DMA of the streamed rows (1-3 % faster, profiles/r02/gemm_ws_bf16.txt)
   if constexpr (NV == 256 && KV == 256) {   // the GIN width: the pipelined form (k_wsd_f32 measured 3-8 % slower
     auto kp = k_wsp_f32<PRO>;                 // here, profiles/r04/gpu_a/; removed from this shape in round 5)
     constexpr int plds = WspF32Cfg::lds<PRO>();
@@ -1681,17 +1669,10 @@ int64_t try_wsd(const T* a, int64_t lda, const T* b1, int64_t ldb1, int64_t k1, 
 
 bool tn_is_small(int64_t N, int64_t K) { return N < 16 || K < 16; }
 
-// Workgroups a split-M launch aims for (HGIN_TN_WGS, <= 1024 = the workspace sizing target).  768 = one
-// resident round at 3 workgroups per CU: measured (profiles/r01_gemm_variants_*.txt) 1.35x faster than 1024
-// (1.33 rounds, the last one a third full) for the bf16 kernel, 4-6 % for fp32.
-int64_t tn_target_wgs() {
-  static const int64_t t = [] {
-    const char* v = getenv("HGIN_TN_WGS");
-    const int64_t x = v ? atoll(v) : 768;
-    return x >= 64 && x <= 1024 ? x : (int64_t)1024;
-  }();
-  return t;
-}
+// Workgroups a split-M launch aims for (<= 1024 = the workspace sizing target).  768 = one resident round at 3
+// workgroups per CU: measured (profiles/r01_gemm_variants_*.txt) 1.35x faster than 1024 (1.33 rounds, the last one a
+// third full) for the bf16 kernel, 4-6 % for fp32.
+constexpr int64_t tn_target_wgs() { return 768; }
 
 int64_t tn_splits(int64_t M, int64_t N, int64_t K, int64_t stage_rows = kTnBM, int64_t target = 1024) {
   int64_t S;

@@ -14,26 +14,18 @@ namespace {
 
 constexpr int kMinRowsPerBlock = 64;   // workspace sizing: the most blocks any variant launches
 
-// Rows per block / rows in flight per thread (HGIN_ROWS_RPB, HGIN_ROWS_U; tools/rows_bench.py,
-// profiles/r01_rows_variants.txt): 256-row blocks; 4 rows in flight for fp32 rows (2-4 % faster), 1 for bf16
-// (4 in flight was 20-40 % slower there).  u = 0: choose by element type.
+// Rows per block / rows in flight per thread (tools/rows_bench.py, profiles/r01_rows_variants.txt): 256-row blocks;
+// 4 rows in flight for fp32 rows (2-4 % faster), 1 for bf16 (4 in flight was 20-40 % slower there): u = 0 chooses by
+// element type; non-temporal inputs for fp32 (nt -1), outputs by size (nt_out -1).  (The round-1 switches that set
+// these are gone: the defaults are the measured choices.)
 struct RowsCfg {
   int rpb = 256;
   int u = 0;
-  int nt = -1;   // -1: fp32 on, bf16 off (measured); 0 / 1 forced
-  int nt_out = -1;   // -1: by output size; 0 / 1 forced
+  int nt = -1;       // -1: fp32 on, bf16 off (measured)
+  int nt_out = -1;   // -1: by output size
 };
 const RowsCfg& rows_cfg() {
-  static const RowsCfg c = [] {
-    RowsCfg r;
-    if (const char* v = getenv("HGIN_ROWS_RPB")) r.rpb = atoi(v);
-    if (const char* v = getenv("HGIN_ROWS_U")) r.u = atoi(v);
-    if (const char* v = getenv("HGIN_ROWS_NT")) r.nt = atoi(v) != 0;
-    if (const char* v = getenv("HGIN_ROWS_NT_OUT")) r.nt_out = atoi(v) != 0;
-    if (r.rpb != 64 && r.rpb != 128 && r.rpb != 256) r.rpb = 256;
-    if (r.u != 0 && r.u != 1 && r.u != 4) r.u = 0;
-    return r;
-  }();
+  static const RowsCfg c{};
   return c;
 }
 

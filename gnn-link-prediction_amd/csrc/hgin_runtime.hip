@@ -36,13 +36,7 @@ void trace_launch(const char* fmt, ...) {
   g_trace_buf += '\n';
 }
 
-bool xcd_remap_enabled() {
-  static const bool on = [] {
-    const char* v = getenv("HGIN_XCD");
-    return !(v && v[0] == '0');
-  }();
-  return on;
-}
+bool xcd_remap_enabled() { return true; }
 
 bool gemm_split_enabled() {
   static const bool on = [] {

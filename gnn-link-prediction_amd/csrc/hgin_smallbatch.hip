@@ -60,6 +60,18 @@ struct SbConv {
   int64_t goff;        // offset of this conv's gradients in the flat buffer: W, b, slope, eps
 };
 
+// HetroGAT's GATConv of relation r (models.py:413-418, PyG 2.0.2 GATConv(( -1, -1), C, heads, concat=True)): its
+// parameters and the offset of their gradients in the flat buffer: att_src [HC], att_dst [HC], bias [HC],
+// lin_src.weight [HC][K_src], lin_dst.weight [HC][K_dst] (GATConv's named_parameters order)
+struct SbGat {
+  const float* ws;     // lin_src.weight [HC][K_src]
+  const float* wd;     // lin_dst.weight [HC][K_dst]
+  const float* att_s;  // att_src [heads][C]
+  const float* att_d;  // att_dst [heads][C]
+  const float* b;      // bias [HC]
+  int64_t goff;
+};
+
 struct SbArgs {
   // batch
   const float* x[3];        // raw features per type (row stride ldx)
@@ -146,6 +158,17 @@ struct SbArgs {
   int eval_only;
   float* out_pred;                 // [cap_path] the head's outputs (eval; may be null)
   float* loss_acc;                 // [2] += loss_value, += loss_value * m (eval: test()'s running sums)
+  // bit 4 l + r: conv (l, r) cannot reach the readout, so its parameters get no gradient in the
+  // reference (.grad None) and torch's Adam skips them: the folded Adam leaves them (and their moments) untouched
+  uint32_t dead_conv;
+  // HetroGAT (models.py:380-506, train.py:120-125 MODEL == "GAT"): gat != 0 — the one layer is GATConvs (k_sb_gat_*),
+  // H = gat_heads x gat_c; conv[0][r].goff = gatc[r].goff
+  int gat;
+  int gat_heads, gat_c;
+  float gat_slope;                 // the attention logits' leaky ReLU slope (GATConv negative_slope, 0.2)
+  SbGat gatc[kRel];
+  float* gat_st;                   // per relation [cap_dst][heads][2 + K_src]: max logit, softmax denominator, the
+  int64_t gat_st_off[kRel];        // softmax-weighted sum of the raw source rows (the forward's per-head aggregate)
 };
 
 // The dropout factor of element q (= row H + column) of layer l's type-t output: 0 (dropped, probability p) or
@@ -1808,6 +1831,16 @@ __device__ __forceinline__ void adam_update(const SbArgs& a, int64_t e, float gv
   a.pflat[e] = p;
 }
 
+// entry e (< p_gin) belongs to a conv that cannot reach the readout (its parameter block [goff, goff + size))
+// (the convs' gradient blocks are contiguous in (layer, relation) order: the owner is the last conv starting at or
+// before e)
+__device__ __forceinline__ bool entry_dead(const SbArgs& a, int64_t e) {
+  for (int l = a.L - 1; l >= 0; --l)
+    for (int r = kRel - 1; r >= 0; --r)
+      if (e >= a.conv[l][r].goff) return (a.dead_conv >> (4 * l + r)) & 1u;
+  return false;
+}
+
 __global__ __launch_bounds__(kSbThreads) void k_sb_final(SbArgs a) {
   __shared__ float red[2 * kSbThreads];   // (block_sum2)
   const int tid = threadIdx.x;
@@ -1856,9 +1889,288 @@ __global__ __launch_bounds__(kSbThreads) void k_sb_final(SbArgs a) {
       for (int q = 0; q < 8; ++q) t = __fadd_rn(t, red[q * 32 + j]);
       const float gv = __fmul_rn(e == a.ro_slope_goff ? slope_sum : t, scale);
       a.gflat[e] = gv;
-      if (a.adam_step) adam_update(a, e, gv, ad);
+      if (a.adam_step && !(a.dead_conv && e < a.p_gin && entry_dead(a, e))) adam_update(a, e, gv, ad);
     }
     __syncthreads();
+  }
+}
+
+// ---------------------------------------------------------------------------------------------------
+// HetroGAT in the fused step (models.py:380-506; config.json MODEL "GAT": HEADS 16, NODE_EMBEDDING_SIZE 8, MP_LAYERS 1
+// — the reference's HetroGAT runs one layer when heads > 1).  A GATConv (PyG 2.0.2) of relation (s -> d) on the raw
+// (sliced) features x: x_s' = x_s W_s^T, x_d' = x_d W_d^T [HC = heads x C]; per head h the logits
+// e_ji = leaky_relu(a_s[j] + a_d[i]) with a_s[j] = x_s'[j, h, :] . att_s[h], a_d[i] = x_d'[i, h, :] . att_d[h], over the
+// edges into i after GATConv's self-loop handling (edges with src id == dst id removed, (i, i) appended for
+// i < min(N_s, N_d), bipartite relations included), softmax over them, out_i = sum_j alpha_ji x_s'[j] + bias; the
+// relations into a type summed in relation order (HeteroConv aggr 'sum').
+// The projections are linear, so they are folded: a_s[j] = x_s[j] . v_s[h] with v_s[h] = W_s[h]^T att_s[h] (K_src
+// values), and out_i[h] = W_s[h] u_i[h] + bias[h] with u_i[h] = sum_j alpha_ji x_s[j] (the softmax-weighted sum of the
+// K_src-wide raw rows): per edge and head K_src multiply-adds instead of C, no x_s' table.  The same sums in another
+// association than the reference's (fp32 tolerance, tests/test_gpu_smallbatch.py).
+// Backward (a linear chain in the seed g = d sum|u| / d out_i, which the readout leaves in gA):
+//   q_i[h] = W_s[h]^T g_i[h];  per edge g_alpha = x_s[j] . q_i[h];  S_i = sum_j alpha g_alpha;
+//   g_pre = alpha (g_alpha - S_i) leaky'(pre);  r[h] += g_pre x_s[j];  t[h] += (sum_j g_pre) x_d[i];
+//   g_W_s[h] = sum_i g_i[h] u_i[h]^T + att_s[h] r[h]^T,  g_att_s[h] = W_s[h] r[h],  g_bias = sum_i g_i,
+//   g_W_d[h] = att_d[h] t[h]^T,  g_att_d[h] = W_d[h] t[h]
+// — row-local sums, so no source-side (CSC) pass: the sources are the raw features, which need no gradient.
+constexpr int kGatK = 8;   // raw (sliced) feature columns per type (the host checks)
+
+// thread (row slot, head): rows of type t handled per workgroup pass
+__device__ __forceinline__ int gat_rows_per_pass(const SbArgs& a) { return kSbThreads / a.gat_heads; }
+
+template <int C>
+__device__ __forceinline__ void gat_fold(const float* w, const float* att, int h, int K, float (&v)[kGatK]) {
+#pragma unroll
+  for (int k = 0; k < kGatK; ++k) v[k] = 0.0f;
+#pragma unroll
+  for (int c = 0; c < C; ++c) {
+    const float at = att[h * C + c];
+#pragma unroll
+    for (int k = 0; k < kGatK; ++k)
+      if (k < K) v[k] = fmaf(at, w[(int64_t)(h * C + c) * K + k], v[k]);
+  }
+}
+
+__device__ __forceinline__ void gat_row(const SbArgs& a, int t, int64_t i, float (&x)[kGatK]) {
+  const int K = a.fdim[t];
+#pragma unroll
+  for (int k = 0; k < kGatK; ++k) x[k] = k < K ? a.x[t][i * a.ldx[t] + a.cols[t][k]] : 0.0f;
+}
+
+// the edges into row i of relation r after GATConv's self-loop handling, in the adjusted list's order (CSR edge order
+// without the j == i edges, then the appended loop)
+template <class F>
+__device__ __forceinline__ void gat_edges(const SbArgs& a, int r, int i, int n_src, int n_dst, F f) {
+  const int32_t* cl = a.col[r];
+  const int e1 = a.rowptr[r][i + 1];
+  for (int e = a.rowptr[r][i]; e < e1; ++e) {
+    const int j = cl[e];
+    if (j != i) f(j);
+  }
+  if (i < (n_src < n_dst ? n_src : n_dst)) f(i);
+}
+
+template <int C>
+__global__ __launch_bounds__(kSbThreads) void k_sb_gat_fwd(SbArgs a) {
+  __shared__ float red[2 * kSbThreads];
+  const int t = blockIdx.y;
+  if (t == 3) {   // GLOBAL_FEATS
+    sb_pool(a, red);
+    return;
+  }
+  const int tid = threadIdx.x;
+  if (a.adam_step && blockIdx.x == 0 && t == 0 && tid == 0) a.adam_step[0] += 1.0f;   // read by k_sb_final
+  const int NH = a.gat_heads, HC = NH * C, RS = gat_rows_per_pass(a);
+  const int slot = tid / NH, h = tid - slot * NH;
+  const int n = nrows(a, t);
+  const int i = blockIdx.x * RS + slot;
+  if (slot >= RS || i >= n) return;
+  const int fd = a.fdim[t];
+  float xi[kGatK];
+  gat_row(a, t, i, xi);
+  float y[C];
+  bool first = true;
+  for (int r = 0; r < kRel; ++r) {
+    if (kRelDst[r] != t) continue;
+    const int s = kRelSrc[r], fs = a.fdim[s];
+    const SbGat& g = a.gatc[r];
+    float vs[kGatK], vd[kGatK];
+    gat_fold<C>(g.ws, g.att_s, h, fs, vs);
+    gat_fold<C>(g.wd, g.att_d, h, fd, vd);
+    float ad = 0.0f;
+#pragma unroll
+    for (int k = 0; k < kGatK; ++k) ad = fmaf(vd[k], xi[k], ad);
+    float m = -INFINITY, ssum = 0.0f, u[kGatK];
+#pragma unroll
+    for (int k = 0; k < kGatK; ++k) u[k] = 0.0f;
+    gat_edges(a, r, i, nrows(a, s), n, [&](int j) {
+      float xj[kGatK];
+      gat_row(a, s, j, xj);
+      float as = 0.0f;
+#pragma unroll
+      for (int k = 0; k < kGatK; ++k) as = fmaf(vs[k], xj[k], as);
+      float ev = __fadd_rn(as, ad);
+      ev = ev > 0.0f ? ev : __fmul_rn(a.gat_slope, ev);
+      if (ev > m) {   // online softmax: rescale the running sums to the new maximum
+        const float sc = expf(m - ev);
+        ssum = fmaf(ssum, sc, 1.0f);
+#pragma unroll
+        for (int k = 0; k < kGatK; ++k) u[k] = fmaf(u[k], sc, xj[k]);
+        m = ev;
+      } else {
+        const float w = expf(ev - m);
+        ssum = __fadd_rn(ssum, w);
+#pragma unroll
+        for (int k = 0; k < kGatK; ++k) u[k] = fmaf(w, xj[k], u[k]);
+      }
+    });
+    const float den = __fadd_rn(ssum, 1e-16f);   // PyG softmax: / (sum + 1e-16)
+    float* st = a.gat_st + a.gat_st_off[r] + ((int64_t)i * NH + h) * (2 + fs);
+    st[0] = m;
+    st[1] = den;
+#pragma unroll
+    for (int k = 0; k < kGatK; ++k) {
+      u[k] = ssum > 0.0f ? __fdiv_rn(u[k], den) : 0.0f;
+      if (k < fs) st[2 + k] = u[k];
+    }
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+      const float* wr = g.ws + (int64_t)(h * C + c) * fs;
+      float o = 0.0f;
+#pragma unroll
+      for (int k = 0; k < kGatK; ++k)
+        if (k < fs) o = fmaf(wr[k], u[k], o);
+      o = __fadd_rn(o, g.b[h * C + c]);
+      y[c] = first ? o : __fadd_rn(y[c], o);
+    }
+    first = false;
+  }
+  float* out = a.act + a.act_off[0][t] + (int64_t)i * HC + h * C;
+#pragma unroll
+  for (int c = 0; c < C; ++c) {
+    const int64_t q = (int64_t)i * HC + h * C + c;
+    out[c] = a.drop_thr ? __fmul_rn(first ? 0.0f : y[c], drop_factor(a, 0, t, q)) : (first ? 0.0f : y[c]);
+  }
+}
+
+// one row chunk's partial gradients of one live relation's GATConv (grid = n_parts x (relations + the readout's weight
+// groups)); per thread (row slot, head) sums over its rows, then over the slots in a fixed order (xor tree within the
+// wave, then the waves in order)
+template <int C>
+__global__ __launch_bounds__(kSbThreads) void k_sb_gat_bwd(SbArgs a, const float* gcur) {
+  __shared__ float stage[kSbStage];
+  const int p = blockIdx.x, r = blockIdx.y;
+  if (r >= kRel) {
+    ro_weight_part(a, p, r - kRel, stage);
+    return;
+  }
+  if ((a.dead_conv >> r) & 1u) return;   // (its partials stay zero; its parameters are not stepped)
+  const int s = kRelSrc[r], d = kRelDst[r];
+  const int fs = a.fdim[s], fd = a.fdim[d];
+  const int NH = a.gat_heads, HC = NH * C, RS = gat_rows_per_pass(a);
+  const int tid = threadIdx.x, slot = tid / NH, h = tid - slot * NH;
+  const int rows = nrows(a, d), n_src = nrows(a, s);
+  const int ch = (rows + a.n_parts - 1) / a.n_parts;
+  const int i0 = p * ch < rows ? p * ch : rows, i1 = (p + 1) * ch < rows ? (p + 1) * ch : rows;
+  const SbGat& g = a.gatc[r];
+  float vs[kGatK], vd[kGatK];
+  gat_fold<C>(g.ws, g.att_s, h, fs, vs);
+  gat_fold<C>(g.wd, g.att_d, h, fd, vd);
+  float G[C][kGatK], bsum[C], rsum[kGatK], tsum[kGatK];
+#pragma unroll
+  for (int c = 0; c < C; ++c) {
+    bsum[c] = 0.0f;
+#pragma unroll
+    for (int k = 0; k < kGatK; ++k) G[c][k] = 0.0f;
+  }
+#pragma unroll
+  for (int k = 0; k < kGatK; ++k) rsum[k] = tsum[k] = 0.0f;
+  const float sl = a.gat_slope;
+  for (int rb = i0; rb < i1; rb += RS) {
+    const int i = rb + slot;
+    if (slot >= RS || i >= i1) continue;
+    float gy[C];
+#pragma unroll
+    for (int c = 0; c < C; ++c) gy[c] = gout(a, gcur, 0, d, (int64_t)i * HC + h * C + c);
+    float q[kGatK];
+#pragma unroll
+    for (int k = 0; k < kGatK; ++k) q[k] = 0.0f;
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+      bsum[c] = __fadd_rn(bsum[c], gy[c]);
+#pragma unroll
+      for (int k = 0; k < kGatK; ++k)
+        if (k < fs) q[k] = fmaf(g.ws[(int64_t)(h * C + c) * fs + k], gy[c], q[k]);
+    }
+    const float* st = a.gat_st + a.gat_st_off[r] + ((int64_t)i * NH + h) * (2 + fs);
+    const float m = st[0], den = st[1];
+#pragma unroll
+    for (int k = 0; k < kGatK; ++k) {
+      const float uk = k < fs ? st[2 + k] : 0.0f;
+#pragma unroll
+      for (int c = 0; c < C; ++c) G[c][k] = fmaf(gy[c], uk, G[c][k]);
+    }
+    float xi[kGatK];
+    gat_row(a, d, i, xi);
+    float ad = 0.0f;
+#pragma unroll
+    for (int k = 0; k < kGatK; ++k) ad = fmaf(vd[k], xi[k], ad);
+    // alpha and g_alpha of edge j (the forward's logit arithmetic)
+    auto edge = [&](int j, float (&xj)[kGatK], float& pre, float& al, float& ga) {
+      gat_row(a, s, j, xj);
+      float as = 0.0f;
+      ga = 0.0f;
+#pragma unroll
+      for (int k = 0; k < kGatK; ++k) {
+        as = fmaf(vs[k], xj[k], as);
+        ga = fmaf(xj[k], q[k], ga);
+      }
+      pre = __fadd_rn(as, ad);
+      const float ev = pre > 0.0f ? pre : __fmul_rn(sl, pre);
+      al = __fdiv_rn(expf(ev - m), den);
+    };
+    float S = 0.0f;
+    gat_edges(a, r, i, n_src, rows, [&](int j) {
+      float xj[kGatK], pre, al, ga;
+      edge(j, xj, pre, al, ga);
+      S = fmaf(al, ga, S);
+    });
+    float gad = 0.0f;
+    gat_edges(a, r, i, n_src, rows, [&](int j) {
+      float xj[kGatK], pre, al, ga;
+      edge(j, xj, pre, al, ga);
+      const float ge = __fmul_rn(al, __fsub_rn(ga, S));
+      const float gp = pre > 0.0f ? ge : __fmul_rn(sl, ge);
+      gad = __fadd_rn(gad, gp);
+#pragma unroll
+      for (int k = 0; k < kGatK; ++k) rsum[k] = fmaf(gp, xj[k], rsum[k]);
+    });
+#pragma unroll
+    for (int k = 0; k < kGatK; ++k) tsum[k] = fmaf(gad, xi[k], tsum[k]);
+  }
+  // the slots' sums per head: xor tree over the wave's slots (lanes h, h + NH, ...), then the waves in order
+  constexpr int V = C * kGatK + C + 2 * kGatK;
+  float* wred = stage;   // [waves][NH][V]
+  const int lane = tid & 63, w = tid >> 6;
+  auto put = [&](int v, float x) {
+    for (int off = NH; off < 64; off <<= 1) x = __fadd_rn(x, __shfl_xor(x, off));
+    if (lane < NH) wred[(w * NH + lane) * V + v] = x;
+  };
+#pragma unroll
+  for (int c = 0; c < C; ++c) {
+#pragma unroll
+    for (int k = 0; k < kGatK; ++k) put(c * kGatK + k, G[c][k]);
+    put(C * kGatK + c, bsum[c]);
+  }
+#pragma unroll
+  for (int k = 0; k < kGatK; ++k) {
+    put(C * kGatK + C + k, rsum[k]);
+    put(C * kGatK + C + kGatK + k, tsum[k]);
+  }
+  __syncthreads();
+  const int nw = kSbThreads / 64;
+  auto tot = [&](int hh, int v) {
+    float x = 0.0f;
+    for (int q = 0; q < nw; ++q) x = __fadd_rn(x, wred[(q * NH + hh) * V + v]);
+    return x;
+  };
+  float* part = a.part_gin + (int64_t)p * a.p_gin + g.goff;
+  for (int idx = tid; idx < HC; idx += kSbThreads) {   // att_src, att_dst, bias
+    const int hh = idx / C, c = idx - hh * C;
+    float as = 0.0f, adv = 0.0f;
+    for (int k = 0; k < fs; ++k) as = fmaf(g.ws[(int64_t)idx * fs + k], tot(hh, C * kGatK + C + k), as);
+    for (int k = 0; k < fd; ++k) adv = fmaf(g.wd[(int64_t)idx * fd + k], tot(hh, C * kGatK + C + kGatK + k), adv);
+    part[idx] = as;
+    part[HC + idx] = adv;
+    part[2 * HC + idx] = tot(hh, C * kGatK + c);
+  }
+  for (int idx = tid; idx < HC * fs; idx += kSbThreads) {   // lin_src.weight
+    const int o = idx / fs, k = idx - o * fs, hh = o / C, c = o - hh * C;
+    part[3 * HC + idx] = fmaf(g.att_s[o], tot(hh, C * kGatK + C + k), tot(hh, c * kGatK + k));
+  }
+  for (int idx = tid; idx < HC * fd; idx += kSbThreads) {   // lin_dst.weight
+    const int o = idx / fd, k = idx - o * fd, hh = o / C;
+    part[3 * HC + HC * fs + idx] = __fmul_rn(g.att_d[o], tot(hh, C * kGatK + C + kGatK + k));
   }
 }
 
@@ -1965,13 +2277,24 @@ extern "C" int hgin_sb_step(const void* args, size_t args_bytes, size_t readout_
     ro_blocks += ro_groups_nk(N, win);
     if (i < a.nhid) win = a.rw[i];
   }
-  const unsigned fwd_blocks = (unsigned)ceil_div((int64_t)capt_max, (int64_t)kSbFwdRows);
-  for (int l = 0; l < a.L; ++l) {
-    const dim3 g(fwd_blocks, l == 0 && a.pool_w ? 4 : 3);
-    if (a.H >= 64)
-      k_sb_fwd<true><<<g, kSbThreads, 0, s>>>(a, l);
-    else
-      k_sb_fwd<false><<<g, kSbThreads, 0, s>>>(a, l);
+  if (a.gat) {   // HetroGAT: one GATConv layer (k_sb_gat_fwd / k_sb_gat_bwd)
+    const int nh = a.gat_heads, c = a.gat_c;
+    HGIN_ARG_CHECK(a.L == 1 && nh >= 1 && nh <= 32 && (nh & (nh - 1)) == 0 && (c == 4 || c == 8 || c == 16) &&
+                       a.H == nh * c && a.gat_st && a.fdim[0] <= kGatK && a.fdim[1] <= kGatK && a.fdim[2] <= kGatK,
+                   "hgin_sb_step: GAT shape (heads %d, C %d, H %d)", nh, c, a.H);
+    const dim3 g((unsigned)ceil_div((int64_t)capt_max, (int64_t)(kSbThreads / nh)), a.pool_w ? 4 : 3);
+    if (c == 4) k_sb_gat_fwd<4><<<g, kSbThreads, 0, s>>>(a);
+    else if (c == 8) k_sb_gat_fwd<8><<<g, kSbThreads, 0, s>>>(a);
+    else k_sb_gat_fwd<16><<<g, kSbThreads, 0, s>>>(a);
+  } else {
+    const unsigned fwd_blocks = (unsigned)ceil_div((int64_t)capt_max, (int64_t)kSbFwdRows);
+    for (int l = 0; l < a.L; ++l) {
+      const dim3 g(fwd_blocks, l == 0 && a.pool_w ? 4 : 3);
+      if (a.H >= 64)
+        k_sb_fwd<true><<<g, kSbThreads, 0, s>>>(a, l);
+      else
+        k_sb_fwd<false><<<g, kSbThreads, 0, s>>>(a, l);
+    }
   }
   // one tile per workgroup (a grid of 512 looping over the tiles, staging the weights once each: 52.9 vs 35 us per
   // batch, profiles/r04/gpu_r — the tiles' serial layer chains want the parallelism, not fewer weight stagings)
@@ -2012,6 +2335,16 @@ extern "C" int hgin_sb_step(const void* args, size_t args_bytes, size_t readout_
   }
   float* gcur = a.gA;
   float* gnxt = a.gB;
+  if (a.gat) {   // the GATConv partials and every readout weight group in one launch
+    const dim3 gw(a.n_parts, kRel + ro_blocks);
+    if (a.gat_c == 4) k_sb_gat_bwd<4><<<gw, kSbThreads, 0, s>>>(a, gcur);
+    else if (a.gat_c == 8) k_sb_gat_bwd<8><<<gw, kSbThreads, 0, s>>>(a, gcur);
+    else k_sb_gat_bwd<16><<<gw, kSbThreads, 0, s>>>(a, gcur);
+    const int64_t P = a.p_gin + a.p_ro;
+    const int64_t fb = ceil_div(P, (int64_t)32);
+    k_sb_final<<<(unsigned)(fb < 1024 ? fb : 1024), kSbThreads, 0, s>>>(a);
+    return check_launch("hgin_sb_step");
+  }
   // the readout's weight-gradient groups ride in the last layer's launch and (L > 1) the first layer's, half each,
   // so that each launch's blocks are resident at once (4 per CU)
   const int ro_hi = a.L > 1 ? (ro_blocks + 1) / 2 : ro_blocks;
@@ -2057,7 +2390,9 @@ extern "C" int hgin_sb_args_offsets(int64_t* out, int64_t n) {
                           (int64_t)offsetof(SbArgs, gc_off),   (int64_t)offsetof(SbArgs, n_tiles),
                           (int64_t)offsetof(SbArgs, loss_value), (int64_t)offsetof(SbArgs, adam_step),
                           (int64_t)offsetof(SbArgs, weight_decay), (int64_t)offsetof(SbArgs, bn_off),
-                          (int64_t)offsetof(SbArgs, drop_inv), (int64_t)offsetof(SbArgs, loss_acc)};
+                          (int64_t)offsetof(SbArgs, drop_inv), (int64_t)offsetof(SbArgs, loss_acc),
+                          (int64_t)offsetof(SbArgs, dead_conv), (int64_t)offsetof(SbArgs, gatc),
+                          (int64_t)offsetof(SbArgs, gat_st_off)};
   const int64_t k = (int64_t)(sizeof(offs) / sizeof(offs[0]));
   HGIN_ARG_CHECK(out && n >= k, "hgin_sb_args_offsets: need %lld slots", (long long)k);
   for (int64_t i = 0; i < k; ++i) out[i] = offs[i];

@@ -197,7 +197,7 @@ _SIGS = {
     "hgin_trace_enable": ([_I32], _I32),
     "hgin_trace_read": ([ctypes.c_char_p, _SZ], _SZ),
 }
-ABI_VERSION = 6
+ABI_VERSION = 7
 
 
 def lib() -> ctypes.CDLL:

@@ -20,7 +20,6 @@ relations ``a + b``, bit-identical).  Everything runs on the device; CPU tensors
 """
 from __future__ import annotations
 
-import os
 from typing import Any, Callable, Dict, Optional, Tuple, Union
 
 import torch
@@ -30,9 +29,9 @@ from . import ops
 
 EdgeType = Tuple[str, str, str]
 
-# HeteroConv layers of GINLayers run as one autograd node (ops.hetero_gin_layer); HGIN_LAYER_FN=0 (or setting
-# this to False) keeps one autograd node per relation, whose shared-node-type gradients autograd adds itself.
-LAYER_FN = os.environ.get("HGIN_LAYER_FN", "1") != "0"
+# HeteroConv layers of GINLayers run as one autograd node (ops.hetero_gin_layer); setting this to False keeps one
+# autograd node per relation, whose shared-node-type gradients autograd adds itself (the equivalence test's reference).
+LAYER_FN = True
 
 
 def reset(value: Any) -> None:

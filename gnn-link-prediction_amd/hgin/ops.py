@@ -87,7 +87,10 @@ BDMA = os.environ.get("HGIN_NT_BDMA", "1") != "0" and os.environ.get("HGIN_F32_G
 # the tiled kernel is considered; they read W directly, so no split planes are built for them
 WS32 = os.environ.get("HGIN_NT_WS32", "1")[:1] != "0" and os.environ.get("HGIN_F32_GEMM", "split") != "mfma32"
 LONG_CHUNK = 1024
-DW512_WSD = os.environ.get("HGIN_DW512", "wsd") == "wsd"
+# the first layer's fp32 K = 512 dW without an input gradient: the weight-stationary PReLU-fused pass over columns
+# [0, 256) (storing g_z into a scratch) + a plain pass over [256, 512) (10.85 vs 12.33 ms at M = 6M on the tiled fused
+# kernel, profiles/r04/gpu_a/gemm_ab_*.json; the round-4 switch to the tiled form is gone)
+DW512_WSD = True
 
 
 @dataclass
@@ -427,7 +430,7 @@ def mlp_bwd_w(g_y: Tensor, z: Tensor, prelu: Tensor, b1: Tensor, b2: Optional[Te
     fused = mlp_bwd_fused(z, N, K)
     # the first layer's fp32 K = 512 dW (no input gradient, so g_z is not wanted): through the weight-stationary
     # two-pass form (PReLU-fused pass over columns [0, 256) storing g_z into a scratch, plain pass over [256, 512) on
-    # it) instead of the tiled fused kernel (HGIN_DW512 = wsd / tiled)
+    # it) instead of the tiled fused kernel
     scratch_gz = fused and not want_gz and z.dtype == torch.float32 and N == 256 and K == 512 and DW512_WSD
     g_z = torch.empty_like(z) if (want_gz or not fused or scratch_gz) else None
     g_w = torch.empty(N, K, dtype=torch.float32, device=dev)

@@ -6,7 +6,9 @@ fixed-order gradient reduction that applies the sqrt-MAPE scale and, for Adam, t
 launches), captured once into a hipGraph and replayed per batch after one device collation launch.
 
 It takes the model train.py builds from config.json (``HetroGIN`` with GINLayer convs, Linear + shared PReLU
-readout, Linear head) and its GLOBAL_FEATS (one pooling launch ahead of the step, models.py:347-352) and MLP_BN
+readout, Linear head; and for MODEL == "GAT" ``HetroGAT``'s one GATConv layer — heads a power of two <= 32,
+out_channels 4 / 8 / 16, heads x out_channels <= 128 — as k_sb_gat_fwd / k_sb_gat_bwd: 1 + readout + 2 launches) and its
+GLOBAL_FEATS (one pooling launch ahead of the step, models.py:347-352) and MLP_BN
 (the readout as 2 nhid + 1 launches around the BatchNorm's batch statistics, models.py:303-313) and DROPOUT
 (masks hashed per step, models.py:358-359) switches, at small widths: hidden <= 128, first-layer GEMM K <= 128, readout widths <= 256, <= 3 hidden readout
 layers, <= 4 layers, fp32.  ``SmallBatchStep.supports(model)``
@@ -18,7 +20,6 @@ place); the step returns the batch's device ``loss_value`` (train.py:40), no hos
 from __future__ import annotations
 
 import ctypes
-import os
 from typing import Sequence
 
 import torch
@@ -40,6 +41,10 @@ _I32 = ctypes.c_int32
 
 class _SbConv(ctypes.Structure):
     _fields_ = [("w", _P), ("b", _P), ("slope", _P), ("eps", _P), ("goff", _I64)]
+
+
+class _SbGat(ctypes.Structure):   # csrc/hgin_smallbatch.hip SbGat
+    _fields_ = [("ws", _P), ("wd", _P), ("att_s", _P), ("att_d", _P), ("b", _P), ("goff", _I64)]
 
 
 class _SbArgs(ctypes.Structure):   # field for field csrc/hgin_smallbatch.hip SbArgs
@@ -68,11 +73,15 @@ class _SbArgs(ctypes.Structure):   # field for field csrc/hgin_smallbatch.hip Sb
                 ("bn_nbt", _P * MAX_HID), ("bn_goff", _I64 * MAX_HID), ("bn_eps", ctypes.c_float),
                 ("bn_mom", ctypes.c_float), ("bn_buf", _P), ("bn_off", (_I64 * 5) * MAX_HID),
                 ("drop_ctr", _P), ("drop_seed", ctypes.c_uint64), ("drop_thr", ctypes.c_uint32),
-                ("drop_inv", ctypes.c_float), ("eval_only", _I32), ("out_pred", _P), ("loss_acc", _P)]
+                ("drop_inv", ctypes.c_float), ("eval_only", _I32), ("out_pred", _P), ("loss_acc", _P),
+                ("dead_conv", ctypes.c_uint32),
+                ("gat", _I32), ("gat_heads", _I32), ("gat_c", _I32), ("gat_slope", ctypes.c_float),
+                ("gatc", _SbGat * REL), ("gat_st", _P), ("gat_st_off", _I64 * REL)]
 
 
 _OFFSET_FIELDS = ("goff", "m_valid", "conv", "rw", "ro_goff", "p_ro", "act_off", "zb_off", "gc_off", "n_tiles",
-                  "loss_value", "adam_step", "weight_decay", "bn_off", "drop_inv", "loss_acc")
+                  "loss_value", "adam_step", "weight_decay", "bn_off", "drop_inv", "loss_acc",
+                  "dead_conv", "gatc", "gat_st_off")
 
 
 def foldable(opt: torch.optim.Optimizer, params=None) -> bool:
@@ -101,6 +110,21 @@ def _hyper(opt: torch.optim.Optimizer) -> tuple:
     return (float(g["lr"]), float(g["betas"][0]), float(g["betas"][1]), float(g["eps"]), float(g["weight_decay"]))
 
 
+def dead_convs(L: int) -> set:
+    """(layer, relation index) of the convs whose outputs cannot reach the readout: the reference's
+    autograd leaves their parameters' .grad None, so torch's Adam skips them (no step, no weight decay)."""
+    dead, live_types = set(), {"path"}
+    for l in range(L - 1, -1, -1):
+        needed = set()
+        for ri, (src, _, dst) in enumerate(RELS):
+            if dst in live_types:
+                needed.update((src, dst))
+            else:
+                dead.add((l, ri))
+        live_types = needed
+    return dead
+
+
 def check_layout() -> None:
     """The ctypes mirror of SbArgs against the library's own sizeof / offsetof (raises on an ABI mismatch)."""
     lib = _lib.lib()
@@ -121,15 +145,51 @@ def _column_map(model: HetroGIN, raw: dict) -> dict:
     return {t: [int(v) for v in probe[t].reshape(-1).tolist()] for t in TYPES}
 
 
+GAT_C = (4, 8, 16)   # GATConv out_channels the fused kernels are instantiated for (csrc/hgin_smallbatch.hip)
+
+
+def _gat_convs(model):
+    """HetroGAT (models.py:380-506): the one layer's GATConv per relation, or a reason string."""
+    from .gat import GATConv
+    if model.num_layers != 1:
+        return "HetroGAT layers (the fused step runs the reference's one-layer HetroGAT)"
+    hc = model.convs[0]
+    if hc.skip or hc.aggr != "sum" or len(hc.convs) != REL:
+        return "pruned relations / aggr / relation set"
+    row = []
+    for r in RELS:
+        key = "__".join(r)
+        conv = hc.convs[key] if key in hc.convs else None
+        if not isinstance(conv, GATConv):
+            return f"relation {key}"
+        nh, c = conv.heads, conv.out_channels
+        if (not conv.concat or not conv.add_self_loops or conv.dropout != 0.0 or conv.bias is None
+                or conv.lin_src is conv.lin_dst or nh & (nh - 1) or nh > 32 or c not in GAT_C or nh * c > 128):
+            return f"GATConv {key} (concat, self loops, no attention dropout, bias, heads a power of two <= 32, " \
+                   f"out_channels in {GAT_C}, heads x out_channels <= 128)"
+        row.append(conv)
+    if len({(c.heads, c.out_channels, c.negative_slope) for c in row}) != 1:
+        return "GATConv heads / widths / slopes differ between relations"
+    return [row]
+
+
 def _structure(model: torch.nn.Module):
-    """(convs[l][r] -> (Linear, PReLU weight, eps), hidden readout Linears, the shared slope, head Linear) or a reason
-    string when the fused step does not take the model."""
-    if type(model) is not HetroGIN:
-        return "not a HetroGIN"
+    """(convs, hidden readout Linears, the shared slope, head Linear, H, BatchNorms) or a reason string when the fused
+    step does not take the model.  HetroGIN: convs[l][r] = (Linear, PReLU weight, eps); HetroGAT: convs[0][r] = the
+    GATConv, H = heads x out_channels."""
+    from .models import HetroGAT
+    gat = type(model) is HetroGAT
+    if type(model) is not HetroGIN and not gat:
+        return "not a HetroGIN / HetroGAT"
     if not 0.0 <= model.dropout < 1.0:
         return "dropout probability"
     if not 1 <= model.num_layers <= MAX_L:
         return "layers"
+    if gat:
+        convs = _gat_convs(model)
+        if isinstance(convs, str):
+            return convs
+        return _readout_structure(model, convs, convs[0][0].heads * convs[0][0].out_channels)
     convs = []
     for l, hc in enumerate(model.convs):
         if hc.skip or hc.aggr != "sum":
@@ -150,6 +210,10 @@ def _structure(model: torch.nn.Module):
         if len(hc.convs) != REL:
             return "relation set"
         convs.append(row)
+    return _readout_structure(model, convs, model.convs[0].convs["path__uses__link"].conv.nn[0].out_features)
+
+
+def _readout_structure(model, convs, H):
     ro = list(model.readout)
     hidden, slope, bns = [], None, []
     for seq in ro[:-1]:
@@ -179,16 +243,30 @@ def _structure(model: torch.nn.Module):
         return "head"
     if not 1 <= len(hidden) <= MAX_HID:
         return "readout depth"
-    H = model.convs[0].convs["path__uses__link"].conv.nn[0].out_features
     if H > 128 or any(l.out_features > 256 for l in hidden):
         return "widths"
-    if any(p.dtype != torch.float32 for p in model.parameters()):
+    if any(p.dtype != torch.float32 for p in model.parameters()
+           if not isinstance(p, torch.nn.parameter.UninitializedParameter)):
         return "dtype"
     return convs, hidden, slope, head[0], H, bns
 
 
+def _materialize(model: torch.nn.Module, store: GraphStore, ids: Sequence[int]) -> None:
+    """HetroGAT's lazy (-1, -1) projections (PyG 2.0.2 Linear, models.py:413-418) take their shapes and glorot values
+    at the first forward, in forward order (the reference's RNG order): one general-path forward on a warm-up batch, in
+    eval mode (no dropout draw, no BatchNorm update), materialises them before the fused step lays out its buffers."""
+    b = store.collate(list(ids))
+    was = model.training
+    model.eval()
+    try:
+        with torch.no_grad():
+            model(b.x_dict(), b.edge_index_dict(), b.batch["path"])
+    finally:
+        model.train(was)
+
+
 class SmallBatchStep:
-    """Fused HetroGIN train step over padded small-graph batches (see the module docstring)."""
+    """Fused HetroGIN / HetroGAT train step over padded small-graph batches (see the module docstring)."""
 
     @staticmethod
     def supports(model: torch.nn.Module) -> bool:
@@ -196,7 +274,11 @@ class SmallBatchStep:
 
     def __init__(self, model: HetroGIN, opt: torch.optim.Optimizer, store: GraphStore, batch_size: int,
                  warmup_ids: Sequence[Sequence[int]], warmup: int = 2, fold_optimizer: bool = True,
-                 _eval: bool = False):
+                 readout: str = "auto", _eval: bool = False):
+        if readout not in ("auto", "scalar"):
+            raise ValueError("SmallBatchStep: readout is 'auto' (32-row MFMA tiles where they fit) or 'scalar'")
+        if warmup_ids and any(isinstance(p, torch.nn.parameter.UninitializedParameter) for p in model.parameters()):
+            _materialize(model, store, warmup_ids[0])
         st = _structure(model)
         if isinstance(st, str):
             raise ValueError(f"SmallBatchStep: model not supported ({st}); use hgin.graphs.CapturedTrainStep")
@@ -241,22 +323,60 @@ class SmallBatchStep:
             a.cptr[ri], a.cdst[ri] = P(pb.csc[r].rowptr), P(pb.csc[r].col)
         a.goff, a.G, a.y, a.m_valid = P(pb.goff), batch_size, P(pb.y), P(pb.m_valid)
         a.L, a.H = L, H
-        # flat gradient layout: GIN convs (W, b, slope, eps per layer / relation), then the readout
+        self.gat = not isinstance(convs[0][0], tuple)
+        self._ptr_refs = []   # (setter, tensor): the argument block's parameter pointers (re-pointed after folding)
+
+        def PP(setter, t: torch.Tensor):
+            self._ptr_refs.append((setter, t))
+            setter(P(t))
+
+        def field(obj, name):
+            return lambda v: setattr(obj, name, v)
+
+        def elem(arr, i):
+            def put(v):
+                arr[i] = v
+            return put
+        # flat gradient layout: the convs (GIN: W, b, slope, eps per layer / relation; GAT: att_src, att_dst, bias,
+        # lin_src.weight, lin_dst.weight per relation), then the readout
         off = 0
         param_off = {}
-        for l in range(L):
+        conv_params = {}   # (layer, relation) -> its parameters
+        if self.gat:
+            g0 = convs[0][0]
+            a.gat, a.gat_heads, a.gat_c, a.gat_slope = 1, g0.heads, g0.out_channels, float(g0.negative_slope)
             for ri, r in enumerate(RELS):
-                lin, pw, eps = convs[l][ri]
-                K = K0[ri] if l == 0 else H
-                if tuple(lin.weight.shape) != (H, K):
-                    raise ValueError(f"SmallBatchStep: layer {l} {r} weight {tuple(lin.weight.shape)} != {(H, K)}")
-                c = a.conv[l][ri]
-                c.w, c.b, c.slope, c.eps, c.goff = P(lin.weight), P(lin.bias), P(pw), P(eps), off
-                param_off[lin.weight] = off
-                param_off[lin.bias] = off + H * K
-                param_off[pw] = off + H * K + H
-                param_off[eps] = off + H * K + H + 1
-                off += H * K + H + 2
+                conv = convs[0][ri]
+                ks, kd = fdim[r[0]], fdim[r[2]]
+                if tuple(conv.lin_src.weight.shape) != (H, ks) or tuple(conv.lin_dst.weight.shape) != (H, kd):
+                    raise ValueError(f"SmallBatchStep: {r} projections {tuple(conv.lin_src.weight.shape)}, "
+                                     f"{tuple(conv.lin_dst.weight.shape)} != {(H, ks)}, {(H, kd)}")
+                gc = a.gatc[ri]
+                gc.goff = a.conv[0][ri].goff = off
+                prm = (conv.att_src, conv.att_dst, conv.bias, conv.lin_src.weight, conv.lin_dst.weight)
+                for name, t in zip(("att_s", "att_d", "b", "ws", "wd"), prm):
+                    PP(field(gc, name), t)
+                for t in prm:
+                    param_off[t] = off
+                    off += t.numel()
+                conv_params[(0, ri)] = prm
+        else:
+            for l in range(L):
+                for ri, r in enumerate(RELS):
+                    lin, pw, eps = convs[l][ri]
+                    K = K0[ri] if l == 0 else H
+                    if tuple(lin.weight.shape) != (H, K):
+                        raise ValueError(f"SmallBatchStep: layer {l} {r} weight {tuple(lin.weight.shape)} != {(H, K)}")
+                    c = a.conv[l][ri]
+                    c.goff = off
+                    for name, t in zip(("w", "b", "slope", "eps"), (lin.weight, lin.bias, pw, eps)):
+                        PP(field(c, name), t)
+                    param_off[lin.weight] = off
+                    param_off[lin.bias] = off + H * K
+                    param_off[pw] = off + H * K + H
+                    param_off[eps] = off + H * K + H + 1
+                    off += H * K + H + 2
+                    conv_params[(l, ri)] = (lin.weight, lin.bias, pw, eps)
         p_gin = off
         a.concat_path = int(bool(model.concat_path))
         a.nhid = len(hidden)
@@ -270,24 +390,29 @@ class SmallBatchStep:
             if tuple(lin.weight.shape) != (lin.out_features, win):
                 raise ValueError("SmallBatchStep: readout widths")
             a.rw[i] = lin.out_features
-            a.row_w[i], a.row_b[i] = P(lin.weight), P(lin.bias)
+            PP(elem(a.row_w, i), lin.weight)
+            PP(elem(a.row_b, i), lin.bias)
             a.ro_goff[i] = off
             param_off[lin.weight] = off
             param_off[lin.bias] = off + lin.weight.numel()
             off += lin.weight.numel() + lin.out_features
             if bns:   # its BatchNorm's gamma, then beta
                 bn = bns[i]
-                a.bn_w[i], a.bn_b[i] = P(bn.weight), P(bn.bias)
+                PP(elem(a.bn_w, i), bn.weight)
+                PP(elem(a.bn_b, i), bn.bias)
                 a.bn_rm[i], a.bn_rv[i] = P(bn.running_mean), P(bn.running_var)
                 a.bn_nbt[i] = P(bn.num_batches_tracked)
                 a.bn_goff[i] = off
                 param_off[bn.weight], param_off[bn.bias] = off, off + lin.out_features
                 off += 2 * lin.out_features
             win = lin.out_features
-        a.ro_slope, a.ro_slope_goff = P(slope), off
+        PP(field(a, "ro_slope"), slope)
+        a.ro_slope_goff = off
         param_off[slope] = off
         off += 1
-        a.head_w, a.head_b, a.head_goff = P(head.weight), P(head.bias), off
+        PP(field(a, "head_w"), head.weight)
+        PP(field(a, "head_b"), head.bias)
+        a.head_goff = off
         param_off[head.weight] = off
         param_off[head.bias] = off + head.weight.numel()
         off += head.weight.numel() + 1
@@ -295,6 +420,11 @@ class SmallBatchStep:
         params = list(model.parameters())
         if {id(p) for p in params} != {id(p) for p in param_off}:
             raise ValueError("SmallBatchStep: the model has parameters outside the fused step")
+        dead = dead_convs(L)
+        self.dead_params = set()   # ids of the parameters that get no gradient (.grad stays None, as in the reference)
+        for (l, ri) in dead:
+            a.dead_conv |= 1 << (4 * l + ri)
+            self.dead_params.update(id(t) for t in conv_params[(l, ri)])
         # scratch
         f32 = dict(dtype=torch.float32, device=dev)
 
@@ -330,6 +460,11 @@ class SmallBatchStep:
         a.gc, a.kmax = P(self.gc), kmax
         for ri in range(REL):
             a.gc_off[ri] = o2[ri]
+        if self.gat:   # per relation [cap_dst][heads][2 + K_src]: the forward's softmax state for the backward
+            o2, self.gat_st = blocks([cap[r[2]] * a.gat_heads * (2 + fdim[r[0]]) for r in RELS])
+            a.gat_st = P(self.gat_st)
+            for ri in range(REL):
+                a.gat_st_off[ri] = o2[ri]
         for ti, t in enumerate(TYPES):
             a.cap[ti] = cap[t]
         a.n_parts = N_PARTS
@@ -341,17 +476,17 @@ class SmallBatchStep:
         if not self._eval:
             for p in params:
                 o = param_off[p]
-                p.grad = self.gflat[o:o + p.numel()].view_as(p)
+                p.grad = None if id(p) in self.dead_params else self.gflat[o:o + p.numel()].view_as(p)
         if self.folded:
             self._fold_adam(a, params, param_off, off, convs, hidden, slope, head, L, keep, bns)
         widths = (ctypes.c_int32 * MAX_HID)(*[a.rw[i] for i in range(MAX_HID)])
         lds = ctypes.c_size_t(0)
         # the readout: 32-row tiles on the matrix cores, their weights in LDS where they fit, else read through the
-        # caches (mode 4; HGIN_SB_MFMA=0: the 8-row scalar tiles, with the hidden weights in LDS, else without)
+        # caches (mode 4); the 8-row scalar tiles (with the hidden weights in LDS, 1, else without, 0) where neither fits
+        # the LDS, or asked for (readout="scalar")
         # (MLP_BN: the k_sb_bn_* launches, mode 3)
         # (MLP_BN in evaluation: the plain readout with BatchNorm's running-statistics affine map, bn_eval)
-        modes = (3,) if bns and not self._eval else ((2, 4, 1, 0) if os.environ.get("HGIN_SB_MFMA", "1") != "0"
-                                                     else (1, 0))
+        modes = (3,) if bns and not self._eval else ((2, 4, 1, 0) if readout == "auto" else (1, 0))
         for wl in modes:
             _lib.check(_lib.lib().hgin_sb_readout_lds_bytes(H, w0 - H, int(w0 > H), a.nhid, widths, wl,
                                                             ctypes.byref(lds)), "hgin_sb_readout_lds_bytes")
@@ -429,7 +564,8 @@ class SmallBatchStep:
         """The parameters become views of one flat buffer in the gradient layout, Adam's moments two more and its
         step count one device scalar; the optimizer's state entries are re-pointed at them (its existing state, if
         any, copied in), so opt.state_dict() stays meaningful.  The step then owns the optimizer: calling
-        opt.step() as well would update twice."""
+        opt.step() as well would update twice.  The parameters of dead convs (no gradient in the reference) keep no
+        state, as in torch's Adam, which never steps them."""
         f32 = dict(dtype=torch.float32, device=self.gflat.device)
         self.pflat = torch.empty(total, **f32)
         self.mflat = torch.zeros(total, **f32)
@@ -441,7 +577,7 @@ class SmallBatchStep:
                 o, n = param_off[p], p.numel()
                 self.pflat[o:o + n].copy_(p.detach().reshape(-1))
                 state = self.opt.state.get(p)
-                if state:
+                if state and id(p) not in self.dead_params:
                     self.mflat[o:o + n].copy_(state["exp_avg"].reshape(-1))
                     self.vflat[o:o + n].copy_(state["exp_avg_sq"].reshape(-1))
                     steps.add(float(state["step"]))
@@ -451,25 +587,21 @@ class SmallBatchStep:
         for p in params:
             o, n = param_off[p], p.numel()
             p.data = self.pflat[o:o + n].view_as(p)
+            if id(p) in self.dead_params:
+                self.opt.state.pop(p, None)
+                continue
             self.opt.state[p] = {"step": self.adam_step, "exp_avg": self.mflat[o:o + n].view_as(p),
                                  "exp_avg_sq": self.vflat[o:o + n].view_as(p)}
         # the kernels' parameter pointers: the views' (the struct was filled from the old storage)
-        for l in range(L):
-            for ri in range(REL):
-                lin, pw, eps = convs[l][ri]
-                c = a.conv[l][ri]
-                c.w, c.b, c.slope, c.eps = lin.weight.data_ptr(), lin.bias.data_ptr(), pw.data_ptr(), eps.data_ptr()
-        for i, lin in enumerate(hidden):
-            a.row_w[i], a.row_b[i] = lin.weight.data_ptr(), lin.bias.data_ptr()
-            if bns:
-                a.bn_w[i], a.bn_b[i] = bns[i].weight.data_ptr(), bns[i].bias.data_ptr()
-        a.ro_slope, a.head_w, a.head_b = slope.data_ptr(), head.weight.data_ptr(), head.bias.data_ptr()
+        for setter, t in self._ptr_refs:
+            setter(t.data_ptr())
         keep += [self.pflat, self.mflat, self.vflat, self.adam_step]
         a.pflat, a.mflat, a.vflat = self.pflat.data_ptr(), self.mflat.data_ptr(), self.vflat.data_ptr()
         a.adam_step = self.adam_step.data_ptr()
         self._set_hyper(a)
         self._params, self._param_off = params, param_off
-        self._state_first = self.opt.state[params[0]]["exp_avg"]
+        self._live = [p for p in params if id(p) not in self.dead_params]
+        self._state_first = self.opt.state[self._live[0]]["exp_avg"]
 
     def _set_hyper(self, a) -> None:
         self._hyp = _hyper(self.opt)
@@ -484,11 +616,11 @@ class SmallBatchStep:
         if len(g) != 1 or len(g[0]["params"]) != len(self._params) or any(
                 p is not q for p, q in zip(g[0]["params"], self._params)):
             raise RuntimeError("SmallBatchStep: the folded optimizer's parameter groups changed; build a new step")
-        st = self.opt.state.get(self._params[0])
+        st = self.opt.state.get(self._live[0])
         if st is None or st.get("exp_avg") is not self._state_first:
             steps = set()
             with torch.no_grad():
-                for p in self._params:
+                for p in self._live:
                     o, n = self._param_off[p], p.numel()
                     s = self.opt.state.get(p)
                     if not s:
@@ -500,10 +632,13 @@ class SmallBatchStep:
                 raise RuntimeError("SmallBatchStep: the optimizer's new state has parameters at different steps")
             self.adam_step.fill_(steps.pop())
             for p in self._params:
+                if id(p) in self.dead_params:
+                    self.opt.state.pop(p, None)
+                    continue
                 o, n = self._param_off[p], p.numel()
                 self.opt.state[p] = {"step": self.adam_step, "exp_avg": self.mflat[o:o + n].view_as(p),
                                      "exp_avg_sq": self.vflat[o:o + n].view_as(p)}
-            self._state_first = self.opt.state[self._params[0]]["exp_avg"]
+            self._state_first = self.opt.state[self._live[0]]["exp_avg"]
         if _hyper(self.opt) != self._hyp:
             self._set_hyper(self.args)
             torch.cuda.synchronize()

@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define HGIN_ABI_VERSION 6
+#define HGIN_ABI_VERSION 7
 
 #define HGIN_OK 0
 #define HGIN_E_ARG (-1)        /* bad size / null pointer / unsupported combination */
@@ -432,13 +432,15 @@ int hgin_gat_wsum_f32(const float* x, int64_t ldx, int64_t n, int64_t H, int64_t
                       void* workspace, size_t workspace_bytes, void* stream);
 
 /* ---- F1: the fused small-batch train step (the reference's real loop: batches of small graphs) -------------------
- * hgin_sb_step: a HetroGIN forward + sqrt-MAPE backward over a padded batch in 3 L + 1 launches
+ * hgin_sb_step: a HetroGIN forward + sqrt-MAPE backward over a padded batch in 3 L + 1 launches, or (SbArgs.gat,
+ * ABI 7) a one-layer HetroGAT's (models.py:380-506: k_sb_gat_fwd, the readout, k_sb_gat_bwd, the final sum) — replaces
+ * the reference's train_one_epoch body (train.py:31-44) over DataLoader batches (dataset.py:239-244)
  * (csrc/hgin_smallbatch.hip); args points to the host-filled SbArgs struct (hgin/smallbatch.py mirrors its layout;
  * hgin_sb_args_size() = its size), readout_lds = hgin_sb_readout_lds_bytes(..., with_weights = args' ro_wlds, ...):
  * the readout tile's dynamic LDS, with the hidden readout weights staged or not.  Writes every parameter gradient
  * into the flat gradient buffer and loss_value.  Deterministic. */
 size_t hgin_sb_args_size(void);
-int hgin_sb_args_offsets(int64_t* out, int64_t n);   /* offsetof of 11 field groups, for the host mirror's check */
+int hgin_sb_args_offsets(int64_t* out, int64_t n);   /* offsetof of 19 field groups, for the host mirror's check */
 int hgin_sb_readout_lds_bytes(int64_t H, int64_t f_path, int concat_path, int nhid, const int32_t* widths,
                               int with_weights, size_t* bytes);
 int hgin_sb_step(const void* args, size_t args_bytes, size_t readout_lds, void* stream);

@@ -10,9 +10,7 @@
                               the default at N, K in {128, 256});
   * HGIN_NT_BDMA=0 (tiled)  — the fp32 128 x 128 tile splitting its B stages itself instead of copying them from
                               pre-split planes by LDS-DMA;
-  * HGIN_NT_T256=0          — the fp32 split tile at 128 x 128 instead of 128 x 256 (N a multiple of 256: the
-                              K = 512 forward);
-  * HGIN_WS_STAGGER=0       — k_ws_f32 instead of the staggered two-stage fp32 forward / dX-combine GEMM (k_wss_f32);
+  (round 6: the HGIN_NT_T256 / HGIN_WS_STAGGER switches are gone — their defaults are the measured choices)
   (The measured-and-removed variants — the fp32 128 x 256 / k_nt_pipe tiles, double-buffered B, the ping-pong k_nt_pp,
   the 16 x 16 x 32 MFMA tile, and in round 5 the one-wave-per-SIMD k_wsf_f32, k_wsd_f32 at N = K = 256 and the
   128-deep bf16 K-tiles — are
@@ -34,9 +32,7 @@ pytestmark = pytest.mark.gpu
 HERE = os.path.dirname(os.path.abspath(__file__))
 
 SWITCHES = {"default": {}, "tiled": {"HGIN_NT_WS": "0", "HGIN_TN_WS": "0", "HGIN_NT_WS32": "0"},
-            "tiled_nobdma": {"HGIN_NT_WS": "0", "HGIN_TN_WS": "0", "HGIN_NT_WS32": "0", "HGIN_NT_BDMA": "0"},
-            "t256_off": {"HGIN_NT_T256": "0"},
-            "ws_stagger_off": {"HGIN_WS_STAGGER": "0"}}
+            "tiled_nobdma": {"HGIN_NT_WS": "0", "HGIN_TN_WS": "0", "HGIN_NT_WS32": "0", "HGIN_NT_BDMA": "0"}}
 _results = {}
 
 
@@ -59,7 +55,7 @@ def test_switch_within_tolerance(name):
     _run(name)        # the child checks against fp32 itself
 
 
-@pytest.mark.parametrize("name", ["tiled", "tiled_nobdma", "t256_off", "ws_stagger_off"])
+@pytest.mark.parametrize("name", ["tiled", "tiled_nobdma"])
 def test_switch_bitwise_equal_default(name):
     ref, got = _run("default"), _run(name)
     assert ref.keys() == got.keys()

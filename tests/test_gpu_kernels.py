@@ -360,8 +360,8 @@ def test_mlp_bwd_fused_cfg3_layer0_shape():
     """The largest GEMM of the cfg3 step at its own shape: the first layer's fused PReLU + bias backward + dW
     (N = 256, K = 256 + 256 = [aggregate | x_dst], 1M rows; cfg3 runs it at 3-6M), against float64, with the
     launch trace proving the PReLU backward was folded into the dW (no separate k_rows_bwd<0> pass): by default the
-    weight-stationary two-pass form (HGIN_DW512=wsd: the PReLU-fused pass over columns [0, 256) storing g_z into a
-    scratch, the plain pass over [256, 512)), with HGIN_DW512=tiled the tiled fused kernel."""
+    weight-stationary two-pass form (the PReLU-fused pass over columns [0, 256) storing g_z into a scratch, the plain
+    pass over [256, 512))."""
     from hgin import _lib
     M, N, K1, K2 = 1 << 20, 256, 256, 256
     gen = torch.Generator(device=DEV).manual_seed(11)

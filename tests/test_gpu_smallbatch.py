@@ -48,6 +48,11 @@ def _oracle_twin(model, cfg, layers=None):
     return ref
 
 
+def _g(p):
+    """A fused-step parameter's gradient; the dead convs' parameters keep .grad None, as in the reference."""
+    return p.grad.detach() if p.grad is not None else torch.zeros_like(p.detach())
+
+
 def _host_batch(store, ids):
     """The batch on the host, pinned to the numpy restatement of PyG's collation of the same graphs."""
     from oracle import collate_np
@@ -66,17 +71,16 @@ def _host_batch(store, ids):
 @pytest.mark.parametrize("layers", [1, 2, 3])
 def test_fused_step_vs_oracle(layers, readout, monkeypatch):
     """One fused step (Adam at lr 0) against the CPU oracle's forward / sqrt-MAPE backward on the host-collated batch;
-    the readout on the 32-row MFMA tiles (default) and on the 8-row scalar tiles (HGIN_SB_MFMA=0)."""
+    the readout on the 32-row MFMA tiles (default) and on the 8-row scalar tiles (readout="scalar")."""
     from hgin.smallbatch import SmallBatchStep
-    if readout == "scalar":
-        monkeypatch.setenv("HGIN_SB_MFMA", "0")
     from oracle.pyg_cpu import mape
     store, cfg = _store(10, seed=11)
     ids = [2, 8, 5, 0]
     m1 = _model(cfg, layers)
     ref = _oracle_twin(m1, cfg, layers)
     o1 = torch.optim.Adam(m1.parameters(), lr=0.0, capturable=True)
-    step = SmallBatchStep(m1, o1, store, batch_size=5, warmup_ids=[ids], warmup=1)
+    step = SmallBatchStep(m1, o1, store, batch_size=5, warmup_ids=[ids], warmup=1,
+                          readout="auto" if readout == "mfma" else "scalar")
     assert step.args.ro_wlds == (2 if readout == "mfma" else 1)
     lv = float(step.step(ids))
     torch.cuda.synchronize()
@@ -87,8 +91,9 @@ def test_fused_step_vs_oracle(layers, readout, monkeypatch):
     assert abs(lv - float(lv_ref)) <= 1e-5 * abs(float(lv_ref)), (lv, float(lv_ref))
     for (n, p), (n2, q) in zip(m1.named_parameters(), ref.named_parameters()):
         assert n == n2
+        assert (p.grad is None) == (q.grad is None), n   # the dead convs' parameters: no gradient on either side
         want = q.grad if q.grad is not None else torch.zeros_like(q)
-        d = float((p.grad.detach().cpu() - want).double().norm())
+        d = float((_g(p).cpu() - want).double().norm())
         assert d <= 1e-4 * float(want.double().norm()) + 1e-9, (n, d, float(want.norm()))
 
 
@@ -142,7 +147,7 @@ def test_fused_step_vs_oracle_variants(variant):
     for (n, p), (n2, q) in zip(m1.named_parameters(), ref.named_parameters()):
         assert n == n2
         want = q.grad if q.grad is not None else torch.zeros_like(q)
-        d = float((p.grad.detach().cpu() - want).double().norm())
+        d = float((_g(p).cpu() - want).double().norm())
         assert d <= 1e-4 * float(want.double().norm()) + slack, (n, d, float(want.norm()))
     for (n, u), (n2, v) in zip(m1.named_buffers(), ref.named_buffers()):
         assert n == n2
@@ -151,11 +156,11 @@ def test_fused_step_vs_oracle_variants(variant):
         else:
             assert torch.allclose(u.cpu(), v, rtol=1e-5, atol=1e-6), (n, float((u.cpu() - v).abs().max()))
     # bitwise run to run (fixed-order sums everywhere, BatchNorm's merges included): the same batch again
-    g1 = [p.grad.detach().clone() for p in m1.parameters()]
+    g1 = [_g(p).clone() for p in m1.parameters()]
     assert float(step.step(ids)) == lv
     torch.cuda.synchronize()
     for g, p in zip(g1, m1.parameters()):
-        assert torch.equal(g, p.grad)
+        assert torch.equal(g, _g(p))
 
 
 def test_fused_step_vs_reference_fixture_global_bn():
@@ -192,7 +197,7 @@ def test_fused_step_vs_reference_fixture_global_bn():
     no_grad = set(fx["meta"]["no_grad_params"])
     g_scale = max(float(fx["grad." + n].double().norm()) for n, _ in model.named_parameters() if n not in no_grad)
     for n, p in model.named_parameters():
-        g = p.grad.detach().cpu()
+        g = _g(p).cpu()
         if n in no_grad:
             assert not g.any(), n
             continue
@@ -222,7 +227,7 @@ def test_fused_step_dropout_masks_and_gradients(monkeypatch):
     ref.load_state_dict({k: v.detach().cpu() for k, v in m1.state_dict().items()})
     lv = float(step.step(ids))
     torch.cuda.synchronize()
-    grads = [q.grad.detach().cpu().clone() for q in m1.parameters()]
+    grads = [_g(q).cpu().clone() for q in m1.parameters()]
     act = step.act.detach().cpu().clone()
     a = step.args
     b = _host_batch(store, ids)
@@ -288,7 +293,7 @@ def test_fused_step_ragged_batches_vs_oracle(variant):
         slack = 1e-6 * gmax if over else 1e-9
         for (n, p), q in zip(m1.named_parameters(), ref.parameters()):
             want = q.grad if q.grad is not None else torch.zeros_like(q)
-            d = float((p.grad.detach().cpu() - want).double().norm())
+            d = float((_g(p).cpu() - want).double().norm())
             assert d <= 1e-4 * float(want.double().norm()) + slack, (ids, n, d, float(want.norm()))
 
 
@@ -483,7 +488,7 @@ def test_fused_step_gradients_and_loss_equal_general_path(layers):
     with _lib.trace_launches() as tr:
         lv = float(step.step(ids))
         torch.cuda.synchronize()
-    g1 = {n: p.grad.detach().clone() for n, p in m1.named_parameters()}
+    g1 = {n: _g(p).clone() for n, p in m1.named_parameters()}
     m2 = _model(cfg, layers)
     b = store.collate(ids)
     _, lv2 = m2.forward_loss(b.x_dict(), b.edge_index_dict(), b.batch["path"], b.y)
@@ -497,7 +502,7 @@ def test_fused_step_gradients_and_loss_equal_general_path(layers):
     step.step(ids)
     torch.cuda.synchronize()
     for n, p in m1.named_parameters():
-        assert torch.equal(p.grad, g1[n]), n
+        assert torch.equal(_g(p), g1[n]), n
 
 
 def test_fused_steps_train_like_the_general_path():

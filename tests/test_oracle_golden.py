@@ -75,3 +75,41 @@ def test_propagate_equals_sequential_edge_order():
     for e in order.tolist():
         out[ei[1, e]] += x[ei[0, e]]
     assert torch.equal(ref, out)
+
+
+@pytest.mark.parametrize("case", ["gat_cfg1_h16", "gat_w16_h4"])
+def test_oracle_gat_reproduces_reference(case):
+    """OracleHetroGAT (the fused GAT step's checker) against the reference's HetroGAT executed over the shim's GATConv
+    (tests/golden/make_golden.py ``gat``): output, loss, every gradient (None for the dead relations) and the Adam step,
+    bit for bit."""
+    from oracle.pyg_cpu import OracleHetroGAT
+    fx = load_fixture(case)
+    m = fx["meta"]
+    sd = {k[3:]: v for k, v in fx.items() if k.startswith("sd.")}
+    dims = {}
+    for key in m["relations"]:
+        s, _, d = key.split("__")
+        if f"convs.0.convs.{key}.lin_src.weight" not in sd:   # (carried in the data, no conv: models.py:413-418)
+            continue
+        dims[s] = sd[f"convs.0.convs.{key}.lin_src.weight"].shape[1]
+        dims[d] = sd[f"convs.0.convs.{key}.lin_dst.weight"].shape[1]
+    model = OracleHetroGAT(dims, node_embedding_size=m["hidden"], heads=m["heads"], dropout=0.0,
+                           concat_path=m["concat_path"], bl_features=m["bl_features"],
+                           divided_features=m["divided_features"], global_feats=False, mlp_layers=list(m["mlp_layers"]),
+                           act="torch.nn.PReLU()", mlp_head_act=None, mlp_bn=False)
+    assert list(model.state_dict()) == list(sd)
+    model.load_state_dict(sd)
+    x = {t: fx[f"in.x.{t}"].clone() for t in ("path", "link", "node")}
+    ei = {tuple(r.split("__")): fx[f"in.ei.{r}"] for r in m["relations"]}
+    opt = torch.optim.Adam(lr=1e-3, params=model.parameters(), weight_decay=0)
+    out = model(x, ei, fx["in.batch"])
+    assert torch.equal(out, fx["out"]), float((out - fx["out"]).abs().max())
+    lv = mape(out, fx["in.y"].reshape(-1, 1))
+    assert torch.equal(lv, fx["loss_value"])
+    torch.sqrt(lv).backward()
+    for n, p in model.named_parameters():
+        g = p.grad if p.grad is not None else torch.zeros(0)
+        assert torch.equal(g, fx["grad." + n]), n
+    opt.step()
+    for n, p in model.named_parameters():
+        assert torch.equal(p.detach(), fx["step." + n]), n

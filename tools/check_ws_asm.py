@@ -1,5 +1,5 @@
-"""Static check of the weight-stationary kernels (k_ws_bf16 / k_ws_f32 / k_wss_f32 in hgin_gemm_nt.hip, k_wsd_* / k_wsp_f32 in
-hgin_gemm_tn.hip)
+"""Static check of the weight-stationary kernels (k_ws_bf16 / k_ws_f32 / k_wss_f32 in hgin_gemm_nt.hip, k_wsd_* / k_wsp_f32 / k_wsp_bf16
+in hgin_gemm_tn.hip)
 in their gfx950 assembly: the
 counted-vmcnt ring is only correct when the loop holds no compiler-visible vector-memory load (the compiler's
 own waits would not count the inline-asm DMAs), so every instantiation must have no scratch (spill) traffic,
@@ -27,13 +27,14 @@ def main():
             subprocess.run(cmd, check=True, capture_output=True)
             s += open(out).read()
     bad = 0
-    for m in re.finditer(r"^(_ZN4hgin12_GLOBAL__N_1\d+k_ws(?:d?_bf16|[dps]?_f32)\S*):", s, re.M):
+    for m in re.finditer(r"^(_ZN4hgin12_GLOBAL__N_1\d+k_ws(?:[dp]?_bf16|[dps]?_f32)\S*):", s, re.M):
         body = s[m.end():s.index(".Lfunc_end", m.end())]
         loop = body[body.find("Loop Header"):] if "Loop Header" in body else body
         scratch = len(re.findall(r"\bscratch_(load|store)|buffer_(load|store)_dword\S* \S+, off, s\[0:3\]", body))
         loads_in_loop = len(re.findall(r"\bglobal_load_(?!lds)\w+", loop))
         waits = sorted(set(int(x) for x in re.findall(r"s_waitcnt vmcnt\((\d+)\)", loop)))
-        name = re.search(r"(k_ws(?:d?_bf16|[dps]?_f32)I.*?)EEEv", m.group(1)).group(1)
+        nm = re.search(r"(k_ws(?:[dp]?_bf16|[dps]?_f32)(?:I.*?EEEv|(?=P)))", m.group(1))
+        name = nm.group(1) if nm else m.group(1)
         ok = scratch == 0 and loads_in_loop == 0
         bad += not ok
         print(f"{'ok ' if ok else 'BAD'} {name}: scratch ops {scratch}, VGPR-destination global loads in the loop "

@@ -1,5 +1,6 @@
 """The fused small-batch step alone (bench.py extras.batches' main figure), a rocprofv3 target:
-    rocprofv3 --kernel-trace --stats -- python3 tools/sb_prof.py [--steps 200]
+    rocprofv3 --kernel-trace --stats -- python3 tools/sb_prof.py [--steps 200] [--gat]
+(tools/sb_busy.py turns the kernel trace into kernel-busy vs wall time per batch)
 Prints the ms per batch (HIP events)."""
 import argparse
 import json
@@ -22,6 +23,7 @@ def main():
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--model", default="{}", help='HetroGIN keyword overrides as JSON, e.g. {"mlp_bn": true}')
     ap.add_argument("--eval", type=int, default=0, help="> 0: SmallBatchEval at this batch size instead")
+    ap.add_argument("--gat", action="store_true", help="HetroGAT (config.json MODEL GAT: HEADS 16, hidden 8, 1 layer)")
     args = ap.parse_args()
     dev = torch.device("cuda")
     base = CONFIGS["cfg1"]
@@ -33,7 +35,12 @@ def main():
     torch.manual_seed(1997)
     kw = dict(base.model_kwargs({"link": base.f_link, "path": base.f_path, "node": base.f_node}),
               **json.loads(args.model))
-    model = HetroGIN(**kw).to(dev)
+    if args.gat:
+        from hgin import HetroGAT
+        kw.update(heads=16, node_embedding_size=8, message_passing_layers=1)
+        model = HetroGAT(**kw).to(dev)
+    else:
+        model = HetroGIN(**kw).to(dev)
     if args.eval:
         from hgin.smallbatch import SmallBatchEval
         model.eval()
@@ -49,7 +56,8 @@ def main():
         st.step(ids)
     e.record()
     torch.cuda.synchronize()
-    print(json.dumps({"model": json.loads(args.model), "ms_per_batch": s.elapsed_time(e) / args.steps}), flush=True)
+    print(json.dumps({"model": json.loads(args.model), "gat": args.gat,
+                      "ms_per_batch": s.elapsed_time(e) / args.steps}), flush=True)
 
 
 if __name__ == "__main__":
