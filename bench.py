@@ -85,6 +85,8 @@ def parse():
                     help="cfg3 at N = 1: skip the bf16 twin (BASELINE configs[4]) timed after the headline as extras.cfg5")
     ap.add_argument("--cpu-full", default=None, metavar="CFG",
                     help="only time the CPU baseline (oracle) on the FULL named config (e.g. cfg2) and print its record")
+    ap.add_argument("--cpu-warmup", type=int, default=2, help="--cpu-full: warm-up steps (default 2)")
+    ap.add_argument("--cpu-steps", type=int, default=5, help="--cpu-full: timed steps, median reported (default 5)")
     ap.add_argument("--graph", action="store_true",
                     help="one hipGraph replay per step (default: the step issued from Python; measured equal on cfg2 "
                          "and cfg5 — the step is GPU-bound, the host runs ahead)")
@@ -165,7 +167,7 @@ def host_ram_gb() -> float:
     return 0.0
 
 
-def cpu_baseline(cfg, full_graph: bool = False) -> dict:
+def cpu_baseline(cfg, full_graph: bool = False, warmup: int = 2, steps: int = 5, progress: bool = False) -> dict:
     """The oracle (torch CPU ops == the PyG CPU path) on a bounded sample of the same workload, on this box's
     host cores: 2 warm-up steps, then the median of 5.  full_graph: the whole config instead of
     the ~1M-edge sample (cfg1 and cfg2 in full; a separate ``--cpu-full`` run, not the default
@@ -182,18 +184,35 @@ def cpu_baseline(cfg, full_graph: bool = False) -> dict:
     # the reference's CPU path is fp32 only: a bf16 config is timed on its fp32 counterpart
     cfg = dataclasses.replace(cfg, feat_dtype="f32", components=1)
     times = []
+    beat = None
+    if progress:   # a full cfg3 step takes minutes: a heartbeat line every 30 s keeps the run visibly alive
+        import threading
+        stop = threading.Event()
+        t_start = time.perf_counter()
+
+        def _beat():
+            while not stop.wait(30.0):
+                print(f"cpu_baseline: {time.perf_counter() - t_start:.0f} s", file=sys.stderr, flush=True)
+        beat = threading.Thread(target=_beat, daemon=True)
+        beat.start()
     try:
         g = synthetic_graph(cfg, seed=0, device="cpu")
         torch.manual_seed(1997)
         model = OracleHetroGIN(**cfg.model_kwargs({"link": cfg.f_link, "path": cfg.f_path, "node": cfg.f_node}))
         opt = torch.optim.Adam(lr=1e-3, params=model.parameters())
-        for i in range(7):
+        for i in range(warmup + steps):
             t0 = time.perf_counter()
             train_step(model, opt, g.x_dict(), g.edge_index_dict(), g.batch["path"], g.y)
-            if i >= 2:
-                times.append(time.perf_counter() - t0)
+            dt_i = time.perf_counter() - t0
+            if i >= warmup:
+                times.append(dt_i)
+            if progress:
+                print(json.dumps({"cpu_step": i, "warmup": i < warmup, "s": round(dt_i, 3),
+                                  "loadavg_1m": round(os.getloadavg()[0], 1)}), file=sys.stderr, flush=True)
     finally:
         torch.set_num_threads(prev)
+        if beat is not None:
+            stop.set()
     dt = statistics.median(times)
     cpu_model = ""
     try:
@@ -206,7 +225,7 @@ def cpu_baseline(cfg, full_graph: bool = False) -> dict:
     return {"value": round(cfg.conv_edges / dt, 1), "unit": "edges/s", "cores": threads, "kind": "port",
             "sample": f"{cfg.name}{' full graph' if cfg.nodes == full.nodes else ''} ({cfg.nodes} nodes / "
                       f"{cfg.graph_edges} edges, {cfg.conv_edges} convolved, hidden {cfg.hidden}, {cfg.layers} "
-                      f"layers, fp32), 2 warm-up + median of 5 train steps (fwd + sqrt-MAPE + bwd + Adam) of "
+                      f"layers, fp32), {warmup} warm-up + median of {steps} train steps (fwd + sqrt-MAPE + bwd + Adam) of "
                       f"oracle/pyg_cpu.py (torch CPU ops = the reference's PyG CPU path), {threads} threads, "
                       f"{cpu_model}",
             "ms_per_step": round(dt * 1e3, 2), "host_ram_gb": host_ram_gb(),
@@ -423,6 +442,18 @@ def batches_extra(dev, n_graphs: int = 256, batch: int = 8, warmup: int = 5, ste
             cfgs[name] = {"error": f"{type(exc).__name__}: {exc}"[:300]}
         torch.cuda.empty_cache()
     out["configs"] = cfgs
+    # kernel-busy time per batch beside the event-timed figure: the step is a few short kernels, so the gap between
+    # them (graph launch, dispatch) is a visible share of ms_per_batch.  Taken from the committed rocprofv3 kernel trace
+    # of the same workload (tools/sb_prof.py -> tools/sb_busy.py), not measured in this run.
+    for label, tgt in (("gin", out if main_kind == "fused" else None), ("gat", cfgs.get("gat_heads16_h8_L1"))):
+        path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r06", f"sb_busy_{label}.json")
+        if tgt is not None and tgt.get("execution") != exec_desc["captured"] and os.path.exists(path):
+            with open(path) as f:
+                busy = json.load(f)
+            tgt["kernel_ms_per_batch"] = busy["kernel_ms_per_batch"]
+            tgt["kernel_trace"] = {"file": os.path.relpath(path, os.path.dirname(os.path.abspath(__file__))),
+                                   "wall_ms_per_batch": busy["wall_ms_per_batch"],
+                                   "launches_per_batch": busy["launches_per_batch"]}
     # the evaluation loops (train.py:70-113 test() after model.eval(), :322-348 evaluate()): config.json's
     # VAL_BATCH_SIZE 1, and the training batch size, as captured replays (hgin/graphs.py CapturedEvalStep: device
     # accumulators, one host sync per pass) beside the reference's eager form (forward + loss.item() per batch)
@@ -697,7 +728,8 @@ def main():
         apply_launch_plan(args)
     if args.cpu_full:
         from hgin.data import CONFIGS
-        rec = cpu_baseline(CONFIGS[args.cpu_full], full_graph=True)
+        rec = cpu_baseline(CONFIGS[args.cpu_full], full_graph=True, warmup=args.cpu_warmup, steps=args.cpu_steps,
+                           progress=True)
         print(json.dumps({"cpu_baseline_full": args.cpu_full, **rec}), flush=True)
         return rec
     from hgin import HetroGIN, _lib, profiling

@@ -75,10 +75,16 @@ __device__ __forceinline__ float bf_hi(uint32_t w) { return __uint_as_float(w & 
 // replaced by 0x7FC0 (the instruction keeps the sign and payload; torch canonicalises).
 using f32x2_cvt_t = __attribute__((ext_vector_type(2))) float;
 using bf16x2_cvt_t = __attribute__((ext_vector_type(2))) __bf16;
+// The NaN fix-up is a real branch taken only by lanes holding a NaN: one v_cmp_u_f32 per pair on the common path
+// instead of two compares, two selects and the bit merges (the volatile asm keeps the compiler from flattening it
+// into selects) — the bf16 GEMM epilogues and the PReLU-fused dW pack every output element.
 __device__ __forceinline__ uint32_t pack_bf2(float lo, float hi) {
   uint32_t p = __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2_cvt_t{lo, hi}, bf16x2_cvt_t));
-  if (lo != lo) p = (p & 0xffff0000u) | 0x7fc0u;
-  if (hi != hi) p = (p & 0x0000ffffu) | 0x7fc00000u;
+  if (__builtin_expect(__builtin_isunordered(lo, hi), 0)) {
+    asm volatile("");
+    if (lo != lo) p = (p & 0xffff0000u) | 0x7fc0u;
+    if (hi != hi) p = (p & 0x0000ffffu) | 0x7fc00000u;
+  }
   return p;
 }
 __device__ __forceinline__ uint32_t f2bf(float f) { return pack_bf2(f, 0.0f) & 0xffffu; }

@@ -72,17 +72,19 @@ def _oracle(model, kw):
 
 def _check_grads(model, ref, slack_rel=0.0):
     gmax = max(float(q.grad.double().norm()) for q in ref.parameters() if q.grad is not None)
+    bad = []
     for (n, p), (n2, q) in zip(model.named_parameters(), ref.named_parameters()):
         assert n == n2
         assert (p.grad is None) == (q.grad is None), n
         want = q.grad if q.grad is not None else torch.zeros_like(q)
         d = float((_g(p).cpu() - want).double().norm())
-        assert d <= 1e-4 * float(want.double().norm()) + slack_rel * gmax + 1e-9, (n, d, float(want.norm()))
+        if not d <= 1e-4 * float(want.double().norm()) + slack_rel * gmax + 1e-9:
+            bad.append((n, d, float(want.norm())))
+    assert not bad, bad
 
 
 def test_fused_gat_step_vs_reference_fixture():
     from conftest import load_fixture
-    from hgin import _lib
     from hgin.smallbatch import SmallBatchStep
     fx = load_fixture("gat_cfg1_h16")
     m = fx["meta"]
@@ -103,10 +105,8 @@ def test_fused_gat_step_vs_reference_fixture():
     opt = torch.optim.Adam(model.parameters(), lr=0.0)
     step = SmallBatchStep(model, opt, store, batch_size=1, warmup_ids=[[0]], warmup=1)
     assert step.folded and step.gat and step.args.gat_heads == 16 and step.args.gat_c == 8
-    with _lib.trace_launches() as tr:
-        lv = float(step.step([0]))
-        torch.cuda.synchronize()
-    assert "k_sb_step" in tr.kernels
+    lv = float(step.step([0]))   # (a hipGraph replay: the launch trace records the capture, not the replays)
+    torch.cuda.synchronize()
     want = float(fx["loss_value"])
     assert abs(lv - want) <= 1e-5 * abs(want), (lv, want)
     for n, p in model.named_parameters():
@@ -153,6 +153,12 @@ def test_fused_gat_step_vs_oracle(variant, monkeypatch):
     step = SmallBatchStep(m1, torch.optim.Adam(m1.parameters(), lr=0.0), store, batch_size=4, warmup_ids=[[0, 2]],
                           warmup=1)
     torch.cuda.synchronize()
+    # GATConv's bias starts at 0 (reset_parameters): a destination row without edges (path rows past the link count get
+    # no self loop) then outputs exactly 0, which the dropout replay below would read as dropped — nonzero biases keep
+    # every kept element nonzero (written through the parameters, which are views of the step's flat buffer)
+    with torch.no_grad():
+        for conv in m1.convs[0].convs.values():
+            conv.bias.uniform_(-0.1, 0.1)
     ref = _oracle(m1, kw)   # (after the warm-up step, which advanced MLP_BN's running statistics)
     lv = float(step.step(ids))
     torch.cuda.synchronize()

@@ -39,9 +39,12 @@ def main():
     ap.add_argument("--M", type=int, default=6_000_000)
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--only", default="fwd512,fwd512acc,fwd256,dw512,dw256pro,dx256")
+    ap.add_argument("--lib", default=None, help="A/B: load this libhgin.so instead of the in-tree build (same ABI)")
     ap.add_argument("--dtype", choices=("f32", "bf16"), default="f32",
                     help="bf16: the cfg5 kernels (operands and outputs bf16); GB_s = algorithmic bytes / time")
     args = ap.parse_args()
+    if args.lib:
+        _lib.build = lambda *a, **k: os.path.abspath(args.lib)   # (tools only: the product always builds its own)
     M = args.M
     bf = args.dtype == "bf16"
     sz = 2 if bf else 4
@@ -52,7 +55,7 @@ def main():
         t = _randn(*shape, **kw)
         return t.to(torch.bfloat16) if bf and len(shape) == 2 and shape[0] == M else t
     N = 256
-    res = {"env": {k: v for k, v in os.environ.items() if k.startswith("HGIN_")}, "M": M}
+    res = {"env": {k: v for k, v in os.environ.items() if k.startswith("HGIN_")}, "M": M, "lib": args.lib}
     s = torch.tensor([0.25], device="cuda")
     b = torch.randn(N, device="cuda", generator=g)
     for name in args.only.split(","):
