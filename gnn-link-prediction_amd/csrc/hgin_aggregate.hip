@@ -357,7 +357,7 @@ __device__ __forceinline__ void st_quad(void* p, const uint4& v) {
 }
 
 // ---------------------------------------------------------------------------------------------------
-// Software-pipelined persistent walk (HGIN_AGG_PIPE = 1, the default; 0 selects the kernels above).
+// Software-pipelined persistent walk (the bf16 kernel; fp32 keeps the kernels above).
 // The kernels above pay up to four dependent memory round trips per destination row — rowptr, then the
 // row's col entries, then the neighbour rows, then the self-term row — and a wave exits after one row per
 // lane group.  Here every wave loops over rows r, r + S, r + 2S, ... (S = resident lane groups of the
@@ -370,9 +370,6 @@ __device__ __forceinline__ void st_quad(void* p, const uint4& v) {
 // Measured (tools/agg_bench.py, profiles/r01_agg_pipe.txt): bf16 1.7-1.9 % faster over the cfg2 / cfg3 relation
 // shapes (cfg3 backward +7.8 %), fp32 6-9 % slower (fewer resident waves: 5-6 per SIMD against the one-row
 // kernels' short-lived 8), so the default is the pipelined walk for bf16 and the batched-tail kernel for fp32.
-// HGIN_AGG_PIPE = 0 / 1 forces one choice for both element types.
-// the pipelined walk for bf16 (1.7-1.9 % faster); fp32 keeps the batched-tail kernel (6-9 % faster there:
-// profiles/r01_agg_pipe.txt)
 template <typename T>
 constexpr bool agg_pipe_enabled() {
   return sizeof(T) == 2;

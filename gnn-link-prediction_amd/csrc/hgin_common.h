@@ -62,7 +62,7 @@ inline int64_t round_up8(int64_t n) { return (n + kXcds - 1) / kXcds * kXcds; }
 __device__ __forceinline__ int64_t xcd_logical(int64_t L, int64_t padded_total) {
   return (L % kXcds) * (padded_total / kXcds) + L / kXcds;
 }
-bool xcd_remap_enabled();   // HGIN_XCD=0 disables (A/B measurements); default on
+bool xcd_remap_enabled();   // always on (the round-5 A/B switch is gone)
 
 // bf16 storage (cfg5): raw uint16_t bit patterns; arithmetic is always fp32.
 // Widening is exact; narrowing is round-to-nearest-even with NaN -> 0x7FC0, bit-identical to

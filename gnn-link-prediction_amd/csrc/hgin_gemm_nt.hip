@@ -622,7 +622,7 @@ int64_t resident_slots(F kernel) {
   return (int64_t)per_cu * prop.multiProcessorCount;
 }
 
-// Row-tile height for N > 32 (HGIN_NT_BM = 64 / 128 forces one).  A launch runs in "rounds" of resident
+// Row-tile height for N > 32.  A launch runs in "rounds" of resident
 // workgroups and its last round is usually partly empty (cfg2: 782 tiles of 128 rows on 768 slots = two
 // rounds for 1.02 rounds of work); 64-row tiles halve the granularity.  Pick the height with the smaller
 // estimated time = rounds x relative tile time.  Measured (profiles/r01_gemm_bm64.txt): a 64-row tile costs
@@ -1669,7 +1669,7 @@ int launch_ws32(const WsArgs32& a, hipStream_t s, const char* what, int64_t* gri
 }
 
 // k_wss_f32 — k_ws_f32 (K = N = 256) as a two-stage software pipeline with the two waves of a SIMD staggered
-// (default; HGIN_WS_STAGGER = 0 keeps k_ws_f32): iteration i runs the MFMAs of block i on plane buffer i & 1 and
+// (every K = N = 256 call k_ws_f32 does not need for g_prev): iteration i runs the MFMAs of block i on plane buffer i & 1 and
 // the split of block i + 1 into buffer (i + 1) & 1, one barrier per block.  Waves 0-3 (one per SIMD) run the
 // epilogue of block i - 1 and the split of block i + 1, then their MFMAs; waves 4-7 run their MFMAs first, then the
 // epilogue of block i and the split — so each SIMD's VALU work sits beside the other wave's MFMAs instead of every
@@ -1926,7 +1926,7 @@ __global__ __launch_bounds__(512, 1) void k_wss_f32(WsArgs32 g) {
   }
 }
 
-// HGIN_WS_STAGGER = 0 keeps k_ws_f32.  Default on: fwd256 at M = 6M 4.95 -> 4.49 ms per launch, the cfg3 step
+// Always on (round 6: the A/B switch is gone): fwd256 at M = 6M 4.95 -> 4.49 ms per launch, the cfg3 step
 // 183.3 -> 179.4 ms (profiles/r04/gpu_s).
 constexpr bool wss_enabled() { return true; }
 

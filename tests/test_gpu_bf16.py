@@ -99,6 +99,36 @@ def test_gin_mlp_fwd_bf16(M, N, K):
     assert ((y.double() - yr).abs() <= abs_b + 2.0 ** -7 * yr.abs() + 2.0 ** -7 * acc.double().abs()).all()
 
 
+@pytest.mark.parametrize("M,N,K,with_acc", [(3000, 256, 256, False), (3000, 256, 256, True), (2000, 256, 512, True),
+                                            (700, 128, 128, False)])
+def test_bf16_epilogue_nan_is_canonical(M, N, K, with_acc):
+    """A NaN reaching a bf16 epilogue is stored as torch's canonical 0x7FC0 (c10::BFloat16 rounding), whatever sign
+    and payload the fp32 value had: v_cvt_pk_bf16_f32 keeps them, pack_bf2 (hgin_common.h) fixes them up on a branch
+    only NaN lanes take.  A row holding +inf and -inf gives inf - inf NaNs (either sign) on the columns whose two
+    weights share a sign; every element of the other rows is bit-identical to the same call without the poisoned
+    rows."""
+    g = torch.Generator(device=DEV).manual_seed(M + K)
+    a = _bf(torch.randn(M, K, device=DEV, generator=g))
+    w = _bf(torch.randn(N, K, device=DEV, generator=g) / K ** 0.5)
+    b = torch.randn(N, device=DEV, generator=g)
+    s = torch.tensor([0.25], device=DEV)
+    acc = _bf(torch.randn(M, N, device=DEV, generator=g)) if with_acc else None
+    z0, y0 = ops.gin_mlp_fwd(a, w, b, s, acc)
+    bad = [5, 64, M - 1]
+    a[5, 3] = float("nan")
+    a[64, 0], a[64, 1] = float("inf"), float("-inf")     # inf - inf where the two weights share a sign
+    a[M - 1, K - 1] = -float("nan")
+    z, y = ops.gin_mlp_fwd(a, w, b, s, acc)
+    for out, ref in ((z, z0), (y, y0)):
+        bits = out.view(torch.int16)
+        assert bool(out[[5, M - 1]].isnan().all())
+        assert bool((out[64].isnan() | out[64].isinf()).all()) and bool(out[64].isnan().any())
+        assert bool((bits[out.isnan()] == 0x7FC0).all())
+        keep = torch.ones(M, dtype=torch.bool, device=DEV)
+        keep[bad] = False
+        assert torch.equal(bits[keep], ref.view(torch.int16)[keep])
+
+
 def test_gemm_bf16_identity_asymmetric():
     K = 64
     a = _bf(torch.eye(K, device=DEV))

@@ -59,7 +59,19 @@ def main():
     s = torch.tensor([0.25], device="cuda")
     b = torch.randn(N, device="cuda", generator=g)
     for name in args.only.split(","):
-        if name.startswith("fwd"):
+        if name.startswith("fwd512two"):
+            # the first layer's K = 512 forward as two K = 256 weight-stationary passes (a probe of its cost, not
+            # the same arithmetic: pass 1 stores the fp32 product of the aggregate half, pass 2 takes it as its
+            # accum row image — a real two-pass form would add it before the bias / PReLU, and carry the relation
+            # sum's accum as a second row image)
+            a = randn(M, 512, device="cuda", generator=g)
+            w = (torch.randn(N, 512, device="cuda", generator=g) / 512 ** 0.5).to(a.dtype)
+            w1, w2 = w[:, :256].contiguous(), w[:, 256:].contiguous()
+            a1, a2 = a[:, :256].contiguous(), a[:, 256:].contiguous()
+            byts = sz * (M * 512 + M * N * 2) + sz * 2 * M * N
+            fn = lambda: ops.gin_mlp_fwd(a2, w2, b, s, ops.gemm_nt(a1, w1))   # noqa: E731
+            flops = 2.0 * M * N * 512
+        elif name.startswith("fwd"):
             K = 512 if "512" in name else 256
             a = randn(M, K, device="cuda", generator=g)
             w = (torch.randn(N, K, device="cuda", generator=g) / K ** 0.5).to(a.dtype)
