@@ -983,6 +983,8 @@ struct WsArgs32 {
   int64_t M;
   bool nt_io;
   bool nt_in;
+  int64_t ldw = 0;             // W row stride (0: K) — k_wss_f32's K = 512 halves read W[:, 0:256] / W[:, 256:512]
+  const float* eps2 = nullptr; // k_wss_f32 kScale: A is scaled by 1 + eps2[0] before the split (the concat self term)
 };
 
 template <int K, int N, int EPI, bool kR1, bool kZ, bool kR2, int CPW = 32>
@@ -1690,7 +1692,13 @@ int launch_ws32(const WsArgs32& a, hipStream_t s, const char* what, int64_t* gri
 //     bit-identical to it (EPI 4's eps partial sums the same terms in another order, one partial per workgroup).
 // Round 4 read the accum rows as 4-byte lane loads in the accumulator layout instead (2.81 vs k_ws_f32's 2.67 ms per
 // launch at M = 3M: HBM latency in the epilogue, profiles/r04/gpu_q); the row image replaces that.
-template <int EPI, bool kR1, bool kZ>
+// Round 6, the first layer's K = 512 forward ([aggregate | (1 + eps) x_dst] W^T) as two launches
+// of this kernel: EPI 5 stores the raw fp32 accumulators of the aggregate half (W[:, 0:256], ldw = 512) into z; then
+// kInit starts every accumulator from that partial (the row image, read in the accumulator layout before the MFMAs)
+// and continues the same chain over the x_dst half (W[:, 256:512], kScale: A scaled by fl(1 + eps) before the split,
+// the tiled kernel's staging arithmetic) with EPI 1's epilogue.  An MFMA chain stored and reloaded in fp32 is the
+// same chain: z / y are bit-identical to the tiled K = 512 kernel (tests/test_gpu_gemm_switch.py).
+template <int EPI, bool kR1, bool kZ, bool kInit = false, bool kScale = false>
 __global__ __launch_bounds__(512, 1) void k_wss_f32(WsArgs32 g) {
   using C = Ws32Cfg<256, 256>;
   constexpr int K = 256, N = 256;
@@ -1700,7 +1708,9 @@ __global__ __launch_bounds__(512, 1) void k_wss_f32(WsArgs32 g) {
   constexpr int PR = kR1 ? 4 : 0;                                  // row-image DMA pieces per wave per block
   constexpr int S = 16 * (kZ ? 2 : 1);                             // dword stores per lane per block
   static_assert(C::BM == 32 && C::NW == 8 && C::G4 == 4 && C::PA == 4, "one 4 KB slice and 4 split groups per wave");
-  static_assert(EPI == 1 || (EPI == 4 && kR1), "EPI 4 reads x_dst");
+  static_assert(EPI == 1 || EPI == 5 || (EPI == 4 && kR1), "EPI 4 reads x_dst");
+  static_assert(!kInit || (EPI == 1 && kR1), "kInit: the partial arrives as the row image of an EPI 1 launch");
+  static_assert(EPI != 5 || (!kR1 && !kZ), "EPI 5 stores the raw accumulators only");
   static_assert(R1_OFF + (kR1 ? 8 * 4096 : 0) <= 163840 && S + PR <= 63, "LDS / vmcnt");
   extern __shared__ __attribute__((aligned(16))) char wss_smem[];
   const int tid = threadIdx.x;
@@ -1716,7 +1726,7 @@ __global__ __launch_bounds__(512, 1) void k_wss_f32(WsArgs32 g) {
 
   uint4 wf[C::KS][3];   // W[32 wave + li][16 t + 8 lh .. + 7] as three bf16 planes (k_ws_f32's B fragments)
   {
-    const float* wr = g.w + (int64_t)(wave * 32 + li) * K + lh * 8;
+    const float* wr = g.w + (int64_t)(wave * 32 + li) * (g.ldw ? g.ldw : K) + lh * 8;
 #pragma unroll
     for (int t = 0; t < C::KS; ++t) {
       const float4 v0 = *reinterpret_cast<const float4*>(wr + t * 16);
@@ -1732,6 +1742,8 @@ __global__ __launch_bounds__(512, 1) void k_wss_f32(WsArgs32 g) {
   const float a_slope = EPI == 1 ? __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(g.prelu[0]))) : 0.0f;
   const float sc_self = EPI == 4 ? __fadd_rn(1.0f, __int_as_float(__builtin_amdgcn_readfirstlane(
                                                         __float_as_int(g.eps[0])))) : 0.0f;
+  const float sc_a = kScale ? __fadd_rn(1.0f, __int_as_float(__builtin_amdgcn_readfirstlane(
+                                                  __float_as_int(g.eps2[0])))) : 1.0f;
   float ep = 0.0f;                                               // EPI 4: this thread's eps-gradient partial
 #pragma unroll
   for (int t = 0; t < C::KS; ++t)
@@ -1782,6 +1794,12 @@ __global__ __launch_bounds__(512, 1) void k_wss_f32(WsArgs32 g) {
     for (int q = 0; q < C::G4; ++q) v[q] = *reinterpret_cast<const float4*>(wss_smem + (wave * C::PA + q) * 1024 + ln * 16);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     if (j + 1 < my) issue(j + 1);
+    if constexpr (kScale) {
+#pragma unroll
+      for (int q = 0; q < C::G4; ++q)
+        v[q] = make_float4(__fmul_rn(sc_a, v[q].x), __fmul_rn(sc_a, v[q].y), __fmul_rn(sc_a, v[q].z),
+                           __fmul_rn(sc_a, v[q].w));
+    }
 #pragma unroll
     for (int q = 0; q < C::G4; ++q) {
       const int grp = ((wave * C::PA + q) * 1024 + ln * 16) / 16;
@@ -1796,8 +1814,15 @@ __global__ __launch_bounds__(512, 1) void k_wss_f32(WsArgs32 g) {
   f32x16 acc;
   auto mfma = [&](int64_t i) {   // k_ws_f32's fragments and product order
     const char* planes = wss_smem + PL0 + (int)(i & 1) * PLANES;
+    if constexpr (kInit) {   // the partial of the first K half, this wave's 32 columns in the accumulator layout
+      const int il = tid_o() & 63;
+      const float* img = reinterpret_cast<const float*>(rimg) + 4 * (il >> 5) * 32 + (il & 31);
 #pragma unroll
-    for (int e = 0; e < 16; ++e) acc[e] = 0.0f;
+      for (int e = 0; e < 16; ++e) acc[e] = img[((e & 3) + 8 * (e >> 2)) * 32];
+    } else {
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[e] = 0.0f;
+    }
     const int fl = tid_o() & 63;
     const int frow = (fl & 31) * C::PROW;
     const int fsw = ((fl >> 5) ^ (fl & 31)) & C::SW;
@@ -1842,13 +1867,17 @@ __global__ __launch_bounds__(512, 1) void k_wss_f32(WsArgs32 g) {
 #pragma unroll
     for (int e = 0; e < 16; ++e) {
       const int rb = (e & 3) + 8 * (e >> 2);                     // this lane's row: rb + 4 lh
-      const float in1 = kR1 ? img[rb * 32] : 0.0f;
+      constexpr bool kAcc = kR1 && !kInit;                        // the row image is the accum (EPI 1) / x_dst
+      const float in1 = kAcc ? img[rb * 32] : 0.0f;
       if ((e & 3) == 3) __builtin_amdgcn_sched_barrier(0);       // at most 4 row values in flight
       float o, zz;
-      if constexpr (EPI == 1) {
+      if constexpr (EPI == 5) {
+        o = acc[e];
+        zz = 0.0f;
+      } else if constexpr (EPI == 1) {
         zz = __fadd_rn(acc[e], bcol);
         const float y = zz > 0.0f ? zz : __fmul_rn(a_slope, zz);
-        o = kR1 ? __fadd_rn(in1, y) : y;
+        o = kAcc ? __fadd_rn(in1, y) : y;
       } else {
         o = acc[e];
         zz = __fmul_rn(sc_self, o);
@@ -1865,7 +1894,7 @@ __global__ __launch_bounds__(512, 1) void k_wss_f32(WsArgs32 g) {
         }
       }
     }
-    if constexpr (kR1) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the row slice is read: refill it
+    if constexpr (kR1 && !kInit) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the row slice is read: refill it
   };
 
   // Per wave the vector-memory stream is: A(0), A(1) [split(0)], R(0), then per block j the epilogue's stores E(j),
@@ -1880,8 +1909,31 @@ __global__ __launch_bounds__(512, 1) void k_wss_f32(WsArgs32 g) {
   if constexpr (kR1) issue_rows(0);
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   auto wait_rows = [&](int64_t j, bool first) {   // before the epilogue of block j (first: waves 0-3)
-    if constexpr (kR1) {
+    if constexpr (kR1 && !kInit) {
       if (first ? j + 2 < my : (j >= 1 && j + 1 < my)) wait_vm<C::PA>(); else wait_vm<0>();
+    }
+  };
+  // kInit: block i's rows must have landed before its MFMAs, and its slice is free once they have read it, so R(i + 1)
+  // is issued right after block i's MFMAs (a whole epilogue + split earlier than R(j + 1) above).  Younger than R(i)
+  // at block i's MFMAs: waves 0-3 — E(i - 1) and A(i + 2) [split(i + 1)] (R(0), issued after A(1) in the prologue: only
+  // A(2)); waves 4-7 — E(i - 1) and A(i + 1) [split(i)] (R(0): nothing).  The splits' waits count the same ops as above
+  // (R and E swap places).
+  auto wait_init = [&](int64_t i, bool first) {
+    if constexpr (kInit) {
+      const bool a_next = first ? i + 2 < my : i + 1 < my;
+      if (i == 0) {
+        if (first && a_next) wait_vm<C::PA>(); else wait_vm<0>();
+      } else {
+        if (a_next) wait_vm<S + C::PA>(); else wait_vm<S>();
+      }
+    }
+  };
+  auto issue_rows_next = [&](int64_t i) {   // kInit: block i + 1's rows, once block i's MFMAs have read the slice
+    if constexpr (kInit) {
+      if (i + 1 < my) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        issue_rows(i + 1);
+      }
     }
   };
   // one loop per wave group (the same barrier count: s_barrier counts arrivals, not program points), so the
@@ -1893,14 +1945,16 @@ __global__ __launch_bounds__(512, 1) void k_wss_f32(WsArgs32 g) {
       if (i > 0) {
         wait_rows(i - 1, true);
         epilogue(i - 1);
-        if (kR1) issue_rows(i);
+        if (kR1 && !kInit) issue_rows(i);
       }
       if (i + 1 < my) {
         if (i == 0) wait_vm<PR>(); else wait_vm<S + PR>();
         split(i + 1);
       }
+      wait_init(i, true);
       mfma(i);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // this wave's plane writes and fragment reads are done
+      issue_rows_next(i);
     }
     wait_rows(my - 1, true);
     epilogue(my - 1);
@@ -1908,12 +1962,14 @@ __global__ __launch_bounds__(512, 1) void k_wss_f32(WsArgs32 g) {
     for (int64_t i = 0; i < my; ++i) {
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
+      wait_init(i, false);
       mfma(i);
       __builtin_amdgcn_sched_barrier(0);
+      issue_rows_next(i);
       wait_rows(i, false);
       epilogue(i);
       if (i + 1 < my) {
-        if (kR1) issue_rows(i + 1);
+        if (kR1 && !kInit) issue_rows(i + 1);
         wait_vm<S + PR>();
         split(i + 1);
       }
@@ -1930,11 +1986,11 @@ __global__ __launch_bounds__(512, 1) void k_wss_f32(WsArgs32 g) {
 // 183.3 -> 179.4 ms (profiles/r04/gpu_s).
 constexpr bool wss_enabled() { return true; }
 
-template <int EPI, bool kR1, bool kZ>
+template <int EPI, bool kR1, bool kZ, bool kInit = false, bool kScale = false>
 int launch_wss(const WsArgs32& a, hipStream_t s, const char* what, int64_t* grid_out = nullptr) {
   constexpr int lds = Ws32Cfg<256, 256>::A_BYTES + 2 * 3 * Ws32Cfg<256, 256>::PL + (kR1 ? 8 * 4096 : 0);
   static_assert(lds <= 160 * 1024, "LDS");
-  auto kern = k_wss_f32<EPI, kR1, kZ>;
+  auto kern = k_wss_f32<EPI, kR1, kZ, kInit, kScale>;
   static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
                                                      hipFuncAttributeMaxDynamicSharedMemorySize, lds);
   if (attr != hipSuccess) {
@@ -1943,20 +1999,37 @@ int launch_wss(const WsArgs32& a, hipStream_t s, const char* what, int64_t* grid
   }
   const int64_t nblk = ceil_div(a.M, (int64_t)Ws32Cfg<256, 256>::BM);
   const int64_t grid = nblk < ws_grid() ? nblk : ws_grid();
-  HGIN_TRACE("k_wss_f32<EPI%d,%d,%d>", EPI, (int)kR1, (int)kZ);
+  HGIN_TRACE("k_wss_f32<EPI%d,%d,%d%s>", EPI, (int)kR1, (int)kZ, kInit ? ",init" : "");
   kern<<<(unsigned)grid, 512, lds, s>>>(a);
   if (grid_out) *grid_out = grid;
   return check_launch(what);
 }
 
 // Returns -1 when the fp32 weight-stationary form does not apply (the caller launches the tiled kernel): split
-// mode, one A source (no eps-scaled second half), K = N = 256, 16-B aligned rows, packed W / z / y / accum.
-int try_ws_f32(const float* a1, int64_t lda1, int64_t k1, const float* a2_eps, const float* w, const float* bias,
-               const float* prelu, const float* accum, float* z, float* y, int64_t M, int64_t N, int64_t K,
-               hipStream_t s, const char* what) {
+// mode, K = N = 256 with one A source, or (round 6) the first layer's K = 512 = [a1 | (1 + eps) a2] with 256 + 256
+// columns and no accum as two k_wss_f32 launches through z (or y when z is not kept); 16-B aligned rows, packed W /
+// z / y / accum.
+int try_ws_f32(const float* a1, int64_t lda1, int64_t k1, const float* a2, int64_t lda2, const float* a2_eps,
+               const float* w, const float* bias, const float* prelu, const float* accum, float* z, float* y,
+               int64_t M, int64_t N, int64_t K, hipStream_t s, const char* what) {
+  if (!ws32_enabled() || !gemm_split_enabled() || M < 1) return -1;
+  if (K == 512 && N == 256 && k1 == 256 && a2 && a2_eps && !accum && wss_enabled()) {
+    // (the relation that adds another's output keeps the tiled kernel: the partial and accum row images do not
+    // both fit beside the plane buffers)
+    auto ok = [](const void* p, int64_t ld) { return aligned16(p) && ld % 4 == 0 && ld < (int64_t(1) << 24); };
+    if (!ok(a1, lda1) || !ok(a2, lda2) || !aligned16(w) || !aligned16(y) || (z && !aligned16(z))) return -1;
+    float* part = z ? z : y;
+    const bool nt_io = gemm_nt_io(M, N, 4);
+    WsArgs32 g1{a1, lda1, w, nullptr, nullptr, nullptr, 0, nullptr, 0, nullptr, 0, part, N, nullptr, nullptr, M,
+                nt_io, ws_nt_in(), 512, nullptr};
+    if (int rc = launch_wss<5, false, false>(g1, s, what)) return rc;
+    WsArgs32 g2{a2, lda2, w + 256, bias, prelu, part, N, nullptr, 0, z, N, y, N, nullptr, nullptr, M, nt_io,
+                ws_nt_in(), 512, a2_eps};
+    if (z) return launch_wss<1, true, true, true, true>(g2, s, what);
+    return launch_wss<1, true, false, true, true>(g2, s, what);
+  }
   // (profiles/r02/gemm_ws_f32.txt)
-  if (!ws32_enabled() || !gemm_split_enabled() || M < 1 || K != N || K != 256 || k1 != K || a2_eps != nullptr)
-    return -1;
+  if (K != N || K != 256 || k1 != K || a2_eps != nullptr) return -1;
   if (!aligned16(a1) || lda1 % 4 || lda1 >= (int64_t(1) << 24) || !aligned16(w) || !aligned16(y) ||
       (z && !aligned16(z)) || (accum && !aligned16(accum)))
     return -1;
@@ -2270,8 +2343,8 @@ extern "C" int hgin_gin_mlp_fwd_f32(const float* a1, int64_t lda1, int64_t k1, c
   HGIN_ARG_CHECK(w && bias && prelu && y, "hgin_gin_mlp_fwd_f32: NULL operand");
   if (int rc = check_a("hgin_gin_mlp_fwd_f32", a1, lda1, k1, a2, lda2, K)) return rc;
   {
-    const int rc = try_ws_f32(a1, lda1, k1, a2_eps, w, bias, prelu, accum, z, y, M, N, K, as_stream(stream),
-                              "hgin_gin_mlp_fwd_f32");
+    const int rc = try_ws_f32(a1, lda1, k1, a2, lda2, a2_eps, w, bias, prelu, accum, z, y, M, N, K,
+                              as_stream(stream), "hgin_gin_mlp_fwd_f32");
     if (rc >= 0) return rc;
   }
   return launch_nt<1>(Src2{a1, lda1, a2, lda2, k1, a2_eps}, Src2{w, K, nullptr, 0, K}, M, N, K, bias, prelu, accum, z, y,

@@ -318,7 +318,7 @@ def nt_planes(b: Tensor, M: int = 1 << 20, ws_form: bool = False) -> Optional[Te
     if not (BDMA and b.dtype == torch.float32) or M == 0:
         return None
     N, K = b.shape
-    if ws_form and WS32 and N == 256 and K == 256:
+    if ws_form and WS32 and N == 256 and K in (256, 512):
         return None
     if N == 0 or K == 0 or K % 32 or b.stride(1) != 1:
         return None
@@ -482,7 +482,11 @@ def gin_mlp_fwd(comb: Tensor, weight: Tensor, bias: Tensor, prelu: Optional[Tens
     z = torch.empty(M, N, dtype=dt, device=comb.device) if (save_z and prelu is not None) else None
     y = torch.empty(M, N, dtype=dt if prelu is not None else torch.float32, device=comb.device)
     ld2 = comb2.stride(0) if comb2 is not None else 0
-    planes = nt_planes(weight, M, ws_form=comb2 is None and prelu is not None) if weight.stride(1) == 1 else None
+    # ws_form: libhgin's weight-stationary kernels take the call and read W themselves — K = N = 256 with one source,
+    # or the first layer's [aggregate | (1 + eps) x_dst] at 256 + 256 without accum (two k_wss_f32 passes)
+    ws_form = prelu is not None and ((comb2 is None and K == 256) or
+                                     (eps2 is not None and accum is None and k1 == 256 and K == 512))
+    planes = nt_planes(weight, M, ws_form=ws_form) if weight.stride(1) == 1 else None
 
     def launch():
         if prelu is None:

@@ -82,6 +82,40 @@ def run_f32(M, K, N, with_acc, save_z, *, g):
     return out
 
 
+F32_CONCAT_CASES = [  # (M, accum, save_z, eps, strided x_dst) — the first layer's fp32 forward [agg | (1 + eps) x_dst] W^T,
+    # K = 256 + 256, N = 256: two k_wss_f32 passes by default without accum (round 6), the tiled K = 512 kernel otherwise
+    (300_007, False, True, 0.37, False), (1, False, True, 0.37, False), (31, False, False, -0.2, False),
+    (70_001, False, True, 0.37, True), (100_003, True, True, 0.37, False), (5_000, False, False, 0.0, True),
+]
+
+
+def run_f32_concat(M, with_acc, save_z, eps, strided, *, g):
+    a1 = torch.randn(M, 256, device="cuda", generator=g)
+    xd = torch.randn(M, 384 if strided else 256, device="cuda", generator=g)[:, :256]
+    w = torch.randn(256, 512, device="cuda", generator=g) / 512 ** 0.5
+    b = torch.randn(256, device="cuda", generator=g)
+    s = torch.tensor([0.25], device="cuda")
+    e2 = torch.tensor([eps], device="cuda")
+    acc = torch.randn(M, 256, device="cuda", generator=g) if with_acc else None
+    from hgin import _lib
+    with _lib.trace_launches() as tr:
+        z, y = ops.gin_mlp_fwd(a1, w, b, s, acc, save_z=save_z, comb2=xd, eps2=e2)
+    if os.environ.get("HGIN_NT_WS32", "1") != "0" and not with_acc:   # the default takes the two-pass form
+        assert any(k.startswith("k_wss_f32<EPI5") for k in tr.kernels) and \
+            any(k.startswith("k_wss_f32<EPI1") and k.endswith(",init>") for k in tr.kernels), tr.kernels
+    sc = float(torch.tensor(1.0) + torch.tensor(eps))          # fl(1 + eps), as the kernels form it
+    a = torch.cat((a1.double(), (torch.tensor(sc) * xd.cpu()).to(xd.device).double()), 1)
+    zr = a @ w.double().t() + b.double()
+    yr = torch.where(zr > 0, zr, 0.25 * zr) + (acc.double() if with_acc else 0.0)
+    tol = lambda r: 1e-6 * r.abs() + 1e-5 * (a.abs() @ w.double().abs().t() + 1)   # noqa: E731
+    assert bool(((y.double() - yr).abs() <= tol(yr)).all()), (M, "concat y")
+    out = {"y": y.cpu()}
+    if save_z:
+        assert bool(((z.double() - zr).abs() <= tol(zr)).all()), (M, "concat z")
+        out["z"] = z.cpu()
+    return out
+
+
 DX_CASES = [  # (M, K, N, combine: None | (want_gx, with g_prev))  — the backward dX GEMMs (EPI 0 / 4)
     (200_003, 256, 256, None), (31, 512, 256, None), (70_000, 256, 128, None),
     (150_001, 256, 256, (True, True)), (99_999, 256, 256, (True, False)), (40_000, 256, 256, (False, False)),
@@ -174,6 +208,7 @@ def main():
     g = torch.Generator(device="cuda").manual_seed(7)
     res = {f"{c}": run(*c, g=g) for c in CASES}
     res.update({f"f32{c}": run_f32(*c, g=g) for c in F32_CASES})
+    res.update({f"f32cat{c}": run_f32_concat(*c, g=g) for c in F32_CONCAT_CASES})
     res.update({f"dx{c}": run_dx(*c, g=g) for c in DX_CASES})
     res.update({f"dxf32{c}": run_dx_f32(*c, g=g) for c in DX_F32_CASES})
     res.update({f"dw{c}": run_dw(*c, g=g) for c in DW_CASES})
