@@ -234,6 +234,7 @@ struct CombEpi {
   const void* gp = nullptr;   // optional: a gradient g_x_dst accumulates onto (may alias gd), row stride ldgp
   int64_t ldgp = 0;
   bool nt_io = false;         // non-temporal epilogue streams (outputs, accum / x_dst / g_prev rows)
+  bool zy = false;            // bf16 EPI 1 without accum: z may be left unwritten when the slope is > 0 (k_ws_bf16)
 };
 
 // Epilogue shared by the fp32 and bf16 kernels.  Per 32-row half (tm) each wave parks its 32 x WCOLS
@@ -961,6 +962,7 @@ struct WsArgs {
   int64_t M;
   bool nt_io;
   bool nt_in;
+  bool zy = false;    // EPI 1, z kept, no accum: skip the z stores when prelu[0] > 0 (z is then recoverable from y)
 };
 
 // Operands of one fp32 weight-stationary forward launch (k_ws_f32, below).
@@ -996,8 +998,10 @@ __global__ __launch_bounds__((WsCfg<K, N, CPW>::NT), (CPW == 64 ? 2 : 1)) void k
   constexpr int P = C::PA + NIMG * C::PC;                        // DMA instructions per wave per block
   constexpr int NPASS = 16 / C::RPP;                             // epilogue passes per 16-row half
   constexpr int S = C::TM * 2 * NPASS * (kZ ? 2 : 1);            // stores per lane per block
+  constexpr int S0 = C::TM * 2 * NPASS;                          // ... when the z stores are skipped (zy)
   constexpr int QPR = N / 4;                                     // 4-column groups per row
   constexpr int kWaitSteady = (NST - 2) * P + (NST - 1) * S < 63 ? (NST - 2) * P + (NST - 1) * S : 63;
+  constexpr int kWaitSteady0 = (NST - 2) * P + (NST - 1) * S0 < 63 ? (NST - 2) * P + (NST - 1) * S0 : 63;
   constexpr int kWaitEarly = (NST - 2) * P < 63 ? (NST - 2) * P : 63;
   extern __shared__ __attribute__((aligned(16))) char ws_smem[];
   const int tid = threadIdx.x;
@@ -1029,6 +1033,10 @@ __global__ __launch_bounds__((WsCfg<K, N, CPW>::NT), (CPW == 64 ? 2 : 1)) void k
   }
   const float a_slope = EPI == 1 ? g.prelu[0] : 0.0f;
   const float sc_self = EPI == 4 ? __fadd_rn(1.0f, g.eps[0]) : 0.0f;
+  // zy (bf16 forward without accum, y = prelu(z) exactly): with a positive slope, z > 0 <=> y > 0 and z = y / a, so
+  // the backward reads y instead (k_wsd_bf16 PRO's yalt) and the z stores — a third of this launch's HBM bytes — are
+  // skipped; a wave-uniform branch, and the vmcnt bound of the ring counts the stores actually issued
+  const bool skip_z = (EPI == 1 && kZ && !kR1) ? (g.zy && a_slope > 0.0f) : false;
   // eps-scaled second source (the first layer's concat self term): the A image's chunks with k >= k1 are
   // scaled in LDS once per block (bf16(s * v), the tiled kernel's staging arithmetic)
   const int64_t k1 = g.k1;
@@ -1101,7 +1109,11 @@ __global__ __launch_bounds__((WsCfg<K, N, CPW>::NT), (CPW == 64 ? 2 : 1)) void k
     // iterations of DMA + stores.  The counts are exact for full blocks; early iterations and a workgroup's
     // last blocks (the only partial block is the last) wait for more, never less.
     if (i + NST - 2 < my) {
-      if (i >= NST - 1) wait_vm<kWaitSteady>(); else wait_vm<kWaitEarly>();
+      if (i >= NST - 1) {
+        if (skip_z) wait_vm<kWaitSteady0>(); else wait_vm<kWaitSteady>();
+      } else {
+        wait_vm<kWaitEarly>();
+      }
     } else {
       wait_vm<0>();
     }
@@ -1224,10 +1236,12 @@ __global__ __launch_bounds__((WsCfg<K, N, CPW>::NT), (CPW == 64 ? 2 : 1)) void k
             const int oy = brow * (int)ldy + cq, oz = brow * (int)ldz + cq;
             if (g.nt_io) {
               Out4<uint16_t>::st_nt(yb + oy, o, true, 4);
-              if constexpr (kZ) Out4<uint16_t>::st_nt(zb + oz, zz, true, 4);
+              if constexpr (kZ)
+                if (!skip_z) Out4<uint16_t>::st_nt(zb + oz, zz, true, 4);
             } else {
               Out4<uint16_t>::st(yb + oy, o, true, 4);
-              if constexpr (kZ) Out4<uint16_t>::st(zb + oz, zz, true, 4);
+              if constexpr (kZ)
+                if (!skip_z) Out4<uint16_t>::st(zb + oz, zz, true, 4);
             }
           }
         }
@@ -1332,6 +1346,7 @@ int try_ws_bf16(const Src2h& a, const Src2h& b, int64_t M, int64_t N, int64_t K,
       w.ldr1 = N;
       w.z = z;
       w.ldz = N;
+      w.zy = ce.zy && z && !accum;
     } else if constexpr (EPI == 4) {
       const uint16_t* xd = static_cast<const uint16_t*>(ce.xd);
       uint16_t* gd = static_cast<uint16_t*>(ce.gd);
@@ -2308,6 +2323,20 @@ extern "C" int hgin_gin_mlp_fwd_bf16(const uint16_t* a1, int64_t lda1, int64_t k
   if (int rc = check_a_h("hgin_gin_mlp_fwd_bf16", a1, lda1, k1, a2, lda2, K)) return rc;
   return launch_nt_bf16<1, uint16_t>(Src2h{a1, lda1, a2, lda2, k1, a2_eps}, Src2h{w, K, nullptr, 0, K}, M, N, K, bias, prelu,
                                      accum, z, y, N, as_stream(stream), "hgin_gin_mlp_fwd_bf16");
+}
+
+extern "C" int hgin_gin_mlp_fwd_zy_bf16(const uint16_t* a1, int64_t lda1, int64_t k1, const uint16_t* a2, int64_t lda2,
+                                        const float* a2_eps, const uint16_t* w, const float* bias, const float* prelu,
+                                        uint16_t* z, uint16_t* y, int64_t M, int64_t N, int64_t K, void* stream) {
+  HGIN_ARG_CHECK(M >= 0 && N >= 0 && K >= 0, "hgin_gin_mlp_fwd_zy_bf16: negative size");
+  HGIN_ARG_CHECK(M < (int64_t(1) << 31) && N <= 65535 * 128, "hgin_gin_mlp_fwd_zy_bf16: size too large");
+  if (M == 0 || N == 0) return HGIN_OK;
+  HGIN_ARG_CHECK(w && bias && prelu && z && y, "hgin_gin_mlp_fwd_zy_bf16: NULL operand");
+  if (int rc = check_a_h("hgin_gin_mlp_fwd_zy_bf16", a1, lda1, k1, a2, lda2, K)) return rc;
+  CombEpi ce{};
+  ce.zy = true;
+  return launch_nt_bf16<1, uint16_t>(Src2h{a1, lda1, a2, lda2, k1, a2_eps}, Src2h{w, K, nullptr, 0, K}, M, N, K, bias,
+                                     prelu, nullptr, z, y, N, as_stream(stream), "hgin_gin_mlp_fwd_zy_bf16", ce);
 }
 
 extern "C" int hgin_linear_fwd_bf16(const uint16_t* a1, int64_t lda1, int64_t k1, const uint16_t* a2, int64_t lda2,

@@ -728,6 +728,9 @@ __global__ __launch_bounds__(256, 2) void k_gemm_tn_bf16_tr(const uint16_t* __re
 // output (the dX GEMM's operand) and keeps per-thread column sums of the unrounded g_z and the slope sum
 // (z <= 0 ? z * g_y), reduced per workgroup in fixed order into the [N][slabs] / [slabs] partials k_slab_reduce
 // finishes.  g_w is bit-identical to k_rows_bwd<0> + the plain kernel (same g_z, same grid).
+// zy (pro.yalt, round 6): the forward left z unwritten (hgin_gin_mlp_fwd_zy_bf16, slope > 0), so the z image is
+// DMA'd from y = prelu(z): y > 0 exactly where z > 0, so g_z (and g_w, the column sums) are the same bits; the slope
+// sum is sum(y g) / slope over y <= 0 (y = bf16(slope z) there: the same sum up to bf16 rounding of z).
 template <int N, int K, bool PRO = false>
 struct WsdCfg {
   static constexpr int NT = 512;
@@ -771,6 +774,7 @@ struct WsdPro {   // the PRO variant's extra operands (unused otherwise)
   float* pcol;       // [N][gridDim.x] column sums of g_z
   float* ps;         // [gridDim.x] slope sums
   char* dump;        // 16-B store target of the lanes whose rows are past M (every wave issues the same stores)
+  const void* yalt = nullptr;   // bf16 zy: y = prelu(z) of a forward without accum; read in place of z when slope > 0
 };
 
 template <int N, int K, bool PRO>
@@ -800,6 +804,9 @@ __global__ __launch_bounds__(512, 1) void k_wsd_bf16(const uint16_t* __restrict_
     if (nt_in) glds16_asm<true>(src, dst); else glds16_asm(src, dst);
   };
   const int k1 = (int)K1;
+  const float sl = PRO ? pro.slope[0] : 0.0f;
+  const bool zy = PRO && pro.yalt != nullptr && sl > 0.0f;   // (wave-uniform)
+  const uint16_t* zsrc = static_cast<const uint16_t*>(zy ? pro.yalt : pro.z);
   auto issue = [&](int64_t i) {
     char* base = wsd_smem + (int)(i % NST) * C::SLOT;
     const int64_t r0 = ((int64_t)blockIdx.x + i * G) * C::BM;
@@ -817,7 +824,7 @@ __global__ __launch_bounds__(512, 1) void k_wsd_bf16(const uint16_t* __restrict_
       r = r < rmax ? r : rmax;                       // (rows past M are zeroed in LDS before use)
       dma(ab + (r * (int)lda + c * 8), base + piece * 1024);
       if constexpr (PRO)                             // z: the same rows and swizzle, the image beside A
-        dma(static_cast<const uint16_t*>(pro.z) + (r0 + r) * pro.ldz + c * 8, base + C::A_BYTES + piece * 1024);
+        dma(zsrc + (r0 + r) * pro.ldz + c * 8, base + C::A_BYTES + piece * 1024);
     }
 #pragma unroll
     for (int q = 0; q < C::PB; ++q) {
@@ -834,7 +841,6 @@ __global__ __launch_bounds__(512, 1) void k_wsd_bf16(const uint16_t* __restrict_
   // PRO: per-thread partial sums over every block of this workgroup (fixed chunks -> fixed columns)
   float csum[PRO ? C::CH : 1][8];
   float ssum = 0.0f;
-  const float sl = PRO ? pro.slope[0] : 0.0f;
 #pragma unroll
   for (int q = 0; q < (PRO ? C::CH : 1); ++q)
 #pragma unroll
@@ -970,7 +976,7 @@ __global__ __launch_bounds__(512, 1) void k_wsd_bf16(const uint16_t* __restrict_
       __syncthreads();
       if (tid < off) sr[tid] = __fadd_rn(sr[tid], sr[tid + off]);
     }
-    if (tid == 0) pro.ps[blockIdx.x] = sr[0];
+    if (tid == 0) pro.ps[blockIdx.x] = zy ? __fdiv_rn(sr[0], sl) : sr[0];
   }
   // this workgroup's slab [N][ld_slab] (the caller offsets slab to its column block)
   float* out = slab + (int64_t)blockIdx.x * N * ld_slab;
@@ -986,6 +992,19 @@ __global__ __launch_bounds__(512, 1) void k_wsd_bf16(const uint16_t* __restrict_
         out[n * ld_slab + k] = acc[tm][tn][e];
       }
     }
+}
+
+// zy fallback (shapes the PRO kernel does not take): z restored in place from y where the forward skipped it —
+// z = y > 0 ? y : bf16(y / slope) when slope > 0 (otherwise the forward wrote z and nothing changes)
+__global__ __launch_bounds__(256) void k_zy_restore(const uint16_t* __restrict__ y, int64_t ldy, uint16_t* z, int64_t ldz,
+                                                    int64_t M, int64_t N, const float* __restrict__ slope) {
+  const float sl = slope[0];
+  if (!(sl > 0.0f)) return;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < M * N; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = i / N, c = i - r * N;
+    const float v = bf2f(y[r * ldy + c]);
+    z[r * ldz + c] = v > 0.0f ? y[r * ldy + c] : (uint16_t)f2bf(__fdiv_rn(v, sl));
+  }
 }
 
 // k_wsd_f32 — the fp32 weight gradient in the same streaming form (split mode: six bf16 products per pair, the
@@ -1882,7 +1901,7 @@ template <typename T>
 int mlp_bwd_w_entry(const char* what, const T* g_y, int64_t ld_gy, const T* z, int64_t ldz, const float* prelu,
                     const T* b1, int64_t ldb1, int64_t k1, const T* b2, int64_t ldb2, int64_t M, int64_t N, int64_t K,
                     float* g_w, int64_t ldw, float* g_prelu, float* g_bias, T* g_z, int64_t ld_gz, void* workspace,
-                    size_t workspace_bytes, void* stream) {
+                    size_t workspace_bytes, void* stream, const T* yalt = nullptr) {
   HGIN_ARG_CHECK(M >= 0 && N >= 0 && K >= 0 && k1 >= 0 && k1 <= K, "%s: bad sizes", what);
   HGIN_ARG_CHECK(N >= 1 && N <= 65535 * 128 && K >= 1 && K <= 65535 * 128, "%s: N/K out of range", what);
   HGIN_ARG_CHECK(prelu && g_prelu && g_bias && g_w && ldw >= K, "%s: NULL output / bad ldw", what);
@@ -1903,7 +1922,7 @@ int mlp_bwd_w_entry(const char* what, const T* g_y, int64_t ld_gy, const T* z, i
     char* ws = static_cast<char*>(workspace);
     const size_t tw = tn_ws_bytes(M, N, K);
     const int64_t S = tn_ws_slabs(M, N, K);
-    WsdPro pro{z, ldz, prelu, g_z, ld_gz, reinterpret_cast<float*>(ws + tw), nullptr, nullptr};
+    WsdPro pro{z, ldz, prelu, g_z, ld_gz, reinterpret_cast<float*>(ws + tw), nullptr, nullptr, yalt};
     pro.ps = reinterpret_cast<float*>(ws + tw + align_up(sizeof(float) * (size_t)(N * S), 256));
     pro.dump = ws + tw + align_up(sizeof(float) * (size_t)(N * S), 256) + align_up(sizeof(float) * (size_t)S, 256);
     float* slab = reinterpret_cast<float*>(ws);
@@ -1933,6 +1952,14 @@ int mlp_bwd_w_entry(const char* what, const T* g_y, int64_t ld_gy, const T* z, i
       if (tn_ws_bytes(M, N, K) + pro_ws_bytes(M, N, K) <= workspace_bytes)
         return gemm_tn_impl<T>(what, g_y, ld_gy, b1, ldb1, k1, b2, ldb2, M, N, K, g_w, ldw, workspace,
                                workspace_bytes, s, &pro2, g_bias, g_prelu);
+    }
+  }
+  if (yalt && M > 0) {   // zy, a shape the PRO kernel did not take: restore z from y first (no-op when slope <= 0)
+    if constexpr (sizeof(T) == 2) {
+      const int64_t n = M * N;
+      const unsigned nb = (unsigned)(ceil_div(n, 256) < 4096 ? ceil_div(n, 256) : 4096);
+      k_zy_restore<<<nb, 256, 0, s>>>(yalt, N, const_cast<T*>(z), ldz, M, N, prelu);
+      if (int rc = check_launch(what)) return rc;
     }
   }
   size_t pw = 0;
@@ -2007,4 +2034,14 @@ extern "C" int hgin_gin_mlp_bwd_w_bf16(const uint16_t* g_y, int64_t ld_gy, const
                                        void* workspace, size_t workspace_bytes, void* stream) {
   return mlp_bwd_w_entry<uint16_t>("hgin_gin_mlp_bwd_w_bf16", g_y, ld_gy, z, ldz, prelu, b1, ldb1, k1, b2, ldb2, M, N,
                                    K, g_w, ldw, g_prelu, g_bias, g_z, ld_gz, workspace, workspace_bytes, stream);
+}
+
+extern "C" int hgin_gin_mlp_bwd_w_zy_bf16(const uint16_t* g_y, int64_t ld_gy, uint16_t* z, const uint16_t* y,
+                                          const float* prelu, const uint16_t* b1, int64_t ldb1, int64_t k1,
+                                          const uint16_t* b2, int64_t ldb2, int64_t M, int64_t N, int64_t K,
+                                          float* g_w, int64_t ldw, float* g_prelu, float* g_bias, uint16_t* g_z,
+                                          int64_t ld_gz, void* workspace, size_t workspace_bytes, void* stream) {
+  HGIN_ARG_CHECK(M == 0 || (z && y && g_z), "hgin_gin_mlp_bwd_w_zy_bf16: z, y and g_z are required");
+  return mlp_bwd_w_entry<uint16_t>("hgin_gin_mlp_bwd_w_zy_bf16", g_y, ld_gy, z, N, prelu, b1, ldb1, k1, b2, ldb2, M, N,
+                                   K, g_w, ldw, g_prelu, g_bias, g_z, ld_gz, workspace, workspace_bytes, stream, y);
 }

@@ -1918,23 +1918,37 @@ constexpr int kGatK = 8;   // raw (sliced) feature columns per type (the host ch
 // thread (row slot, head): rows of type t handled per workgroup pass
 __device__ __forceinline__ int gat_rows_per_pass(const SbArgs& a) { return kSbThreads / a.gat_heads; }
 
-template <int C>
-__device__ __forceinline__ void gat_fold(const float* w, const float* att, int h, int K, float (&v)[kGatK]) {
-#pragma unroll
-  for (int k = 0; k < kGatK; ++k) v[k] = 0.0f;
-#pragma unroll
-  for (int c = 0; c < C; ++c) {
-    const float at = att[h * C + c];
-#pragma unroll
-    for (int k = 0; k < kGatK; ++k)
-      if (k < K) v[k] = fmaf(at, w[(int64_t)(h * C + c) * K + k], v[k]);
-  }
-}
-
 __device__ __forceinline__ void gat_row(const SbArgs& a, int t, int64_t i, float (&x)[kGatK]) {
   const int K = a.fdim[t];
 #pragma unroll
   for (int k = 0; k < kGatK; ++k) x[k] = k < K ? a.x[t][i * a.ldx[t] + a.cols[t][k]] : 0.0f;
+}
+
+// One relation's folded attention vectors and source projection staged in LDS by the whole block (round 6: every
+// thread used to form its head's v_s / v_d from C x K global loads of W and att, and read W_s again for its output —
+// ~300 dependent-latency loads per thread; now each thread makes at most a few of the NH x K folds, in the
+// per-thread fold's c order, so the values are the same bits).  sws [HC][fs] (W_s rows), svs [NH][kGatK], svd [NH][kGatK], sb [HC] (or
+// NULL: the bias is not needed).
+template <int C>
+__device__ __forceinline__ void gat_stage(const SbArgs& a, const SbGat& g, int fs, int fd, float* sws, float* svs,
+                                          float* svd, float* sb) {
+  const int NH = a.gat_heads, HC = NH * C;
+  for (int idx = threadIdx.x; idx < HC * fs; idx += kSbThreads) sws[idx] = g.ws[idx];
+  if (sb)
+    for (int idx = threadIdx.x; idx < HC; idx += kSbThreads) sb[idx] = g.b[idx];
+  for (int idx = threadIdx.x; idx < 2 * NH * kGatK; idx += kSbThreads) {
+    const bool dst = idx >= NH * kGatK;
+    const int j = dst ? idx - NH * kGatK : idx, h = j / kGatK, k = j - h * kGatK;
+    const int K = dst ? fd : fs;
+    const float* w = dst ? g.wd : g.ws;
+    const float* att = dst ? g.att_d : g.att_s;
+    float v = 0.0f;
+    if (k < K) {
+#pragma unroll
+      for (int c = 0; c < C; ++c) v = fmaf(att[h * C + c], w[(int64_t)(h * C + c) * K + k], v);
+    }
+    (dst ? svd : svs)[j] = v;
+  }
 }
 
 // the edges into row i of relation r after GATConv's self-loop handling, in the adjusted list's order (CSR edge order
@@ -1953,6 +1967,7 @@ __device__ __forceinline__ void gat_edges(const SbArgs& a, int r, int i, int n_s
 template <int C>
 __global__ __launch_bounds__(kSbThreads) void k_sb_gat_fwd(SbArgs a) {
   __shared__ float red[2 * kSbThreads];
+  __shared__ float sws[128 * kGatK], svs[32 * kGatK], svd[32 * kGatK], sb[128];
   const int t = blockIdx.y;
   if (t == 3) {   // GLOBAL_FEATS
     sb_pool(a, red);
@@ -1964,19 +1979,27 @@ __global__ __launch_bounds__(kSbThreads) void k_sb_gat_fwd(SbArgs a) {
   const int slot = tid / NH, h = tid - slot * NH;
   const int n = nrows(a, t);
   const int i = blockIdx.x * RS + slot;
-  if (slot >= RS || i >= n) return;
+  if (blockIdx.x * RS >= n) return;                 // (block-uniform: the staging below needs every thread)
+  const bool act = slot < RS && i < n;
   const int fd = a.fdim[t];
   float xi[kGatK];
-  gat_row(a, t, i, xi);
+  if (act) gat_row(a, t, i, xi);
   float y[C];
   bool first = true;
   for (int r = 0; r < kRel; ++r) {
     if (kRelDst[r] != t) continue;
     const int s = kRelSrc[r], fs = a.fdim[s];
     const SbGat& g = a.gatc[r];
+    __syncthreads();                                // (the previous relation's reads of the staged values)
+    gat_stage<C>(a, g, fs, fd, sws, svs, svd, sb);
+    __syncthreads();
+    if (!act) continue;
     float vs[kGatK], vd[kGatK];
-    gat_fold<C>(g.ws, g.att_s, h, fs, vs);
-    gat_fold<C>(g.wd, g.att_d, h, fd, vd);
+#pragma unroll
+    for (int k = 0; k < kGatK; ++k) {
+      vs[k] = svs[h * kGatK + k];
+      vd[k] = svd[h * kGatK + k];
+    }
     float ad = 0.0f;
 #pragma unroll
     for (int k = 0; k < kGatK; ++k) ad = fmaf(vd[k], xi[k], ad);
@@ -2015,16 +2038,17 @@ __global__ __launch_bounds__(kSbThreads) void k_sb_gat_fwd(SbArgs a) {
     }
 #pragma unroll
     for (int c = 0; c < C; ++c) {
-      const float* wr = g.ws + (int64_t)(h * C + c) * fs;
+      const float* wr = sws + (h * C + c) * fs;
       float o = 0.0f;
 #pragma unroll
       for (int k = 0; k < kGatK; ++k)
         if (k < fs) o = fmaf(wr[k], u[k], o);
-      o = __fadd_rn(o, g.b[h * C + c]);
+      o = __fadd_rn(o, sb[h * C + c]);
       y[c] = first ? o : __fadd_rn(y[c], o);
     }
     first = false;
   }
+  if (!act) return;
   float* out = a.act + a.act_off[0][t] + (int64_t)i * HC + h * C;
 #pragma unroll
   for (int c = 0; c < C; ++c) {
@@ -2053,9 +2077,19 @@ __global__ __launch_bounds__(kSbThreads) void k_sb_gat_bwd(SbArgs a, const float
   const int ch = (rows + a.n_parts - 1) / a.n_parts;
   const int i0 = p * ch < rows ? p * ch : rows, i1 = (p + 1) * ch < rows ? (p + 1) * ch : rows;
   const SbGat& g = a.gatc[r];
+  // staged W_s / folds after the wave-reduction area (at most 4 waves x 32 heads x 52 values, C = 4: 6656 floats)
+  constexpr int kGatStg = kSbStage - (128 * kGatK + 2 * 32 * kGatK);
+  float* sws = stage + kGatStg;
+  float* svs = sws + 128 * kGatK;
+  float* svd = svs + 32 * kGatK;
+  gat_stage<C>(a, g, fs, fd, sws, svs, svd, nullptr);
+  __syncthreads();
   float vs[kGatK], vd[kGatK];
-  gat_fold<C>(g.ws, g.att_s, h, fs, vs);
-  gat_fold<C>(g.wd, g.att_d, h, fd, vd);
+#pragma unroll
+  for (int k = 0; k < kGatK; ++k) {
+    vs[k] = svs[h * kGatK + k];
+    vd[k] = svd[h * kGatK + k];
+  }
   float G[C][kGatK], bsum[C], rsum[kGatK], tsum[kGatK];
 #pragma unroll
   for (int c = 0; c < C; ++c) {
@@ -2080,7 +2114,7 @@ __global__ __launch_bounds__(kSbThreads) void k_sb_gat_bwd(SbArgs a, const float
       bsum[c] = __fadd_rn(bsum[c], gy[c]);
 #pragma unroll
       for (int k = 0; k < kGatK; ++k)
-        if (k < fs) q[k] = fmaf(g.ws[(int64_t)(h * C + c) * fs + k], gy[c], q[k]);
+        if (k < fs) q[k] = fmaf(sws[(h * C + c) * fs + k], gy[c], q[k]);
     }
     const float* st = a.gat_st + a.gat_st_off[r] + ((int64_t)i * NH + h) * (2 + fs);
     const float m = st[0], den = st[1];

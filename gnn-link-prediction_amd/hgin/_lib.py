@@ -151,6 +151,9 @@ _SIGS = {
                                 _P, _I64, _P, _SZ, _P], _I32),
     "hgin_gin_mlp_bwd_w_bf16": ([_P, _I64, _P, _I64, _P, _P, _I64, _I64, _P, _I64, _I64, _I64, _I64, _P, _I64, _P, _P,
                                  _P, _I64, _P, _SZ, _P], _I32),
+    "hgin_gin_mlp_fwd_zy_bf16": ([_P, _I64, _I64, _P, _I64, _P, _P, _P, _P, _P, _P, _I64, _I64, _I64, _P], _I32),
+    "hgin_gin_mlp_bwd_w_zy_bf16": ([_P, _I64, _P, _P, _P, _P, _I64, _I64, _P, _I64, _I64, _I64, _I64, _P, _I64, _P,
+                                    _P, _P, _I64, _P, _SZ, _P], _I32),
     "hgin_self_wgrad_workspace_size": ([_I64, _I64, ctypes.POINTER(_SZ)], _I32),
     "hgin_self_wgrad_f32": ([_P, _I64, _P, _I64, _I64, _I64, _I64, _I32, _P, _P, _I64, _P, _P, _SZ, _P], _I32),
     "hgin_combine_bwd_bf16": ([_P, _I64, _P, _I64, _I64, _I64, _P, _P, _I64, _P, _P, _SZ, _P], _I32),
@@ -197,7 +200,7 @@ _SIGS = {
     "hgin_trace_enable": ([_I32], _I32),
     "hgin_trace_read": ([ctypes.c_char_p, _SZ], _SZ),
 }
-ABI_VERSION = 7
+ABI_VERSION = 8
 
 
 def lib() -> ctypes.CDLL:

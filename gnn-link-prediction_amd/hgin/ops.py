@@ -412,13 +412,15 @@ def mlp_bwd_fused(z: Tensor, n: int, k: int) -> bool:
 
 
 def mlp_bwd_w(g_y: Tensor, z: Tensor, prelu: Tensor, b1: Tensor, b2: Optional[Tensor] = None,
-              want_gz: bool = False):
+              want_gz: bool = False, y_alt: Optional[Tensor] = None):
     """Backward of prelu([b1 | b2] @ W^T + b) up to the weights: (g_w [N, K] fp32, g_a [1], g_b [N], g_z).
 
     g_z = z > 0 ? g_y : a * g_y is formed inside the weight-gradient GEMM where fused (mlp_bwd_fused) and
     then returned as None unless ``want_gz``; otherwise (bf16, narrow layers) it is materialised — by the
     weight-stationary dW itself where it takes the shape (k_wsd_*<..., prelu_bwd_fused>: g_z formed in its LDS
-    staging and stored, no separate PReLU-backward pass), else by hgin_prelu_bwd_* ahead of the TN GEMM."""
+    staging and stored, no separate PReLU-backward pass), else by hgin_prelu_bwd_* ahead of the TN GEMM.
+    ``y_alt``: the forward's y when it ran with zy (gin_mlp_fwd): read in place of z when the slope is > 0
+    (hgin_gin_mlp_bwd_w_zy_bf16)."""
     g_y, b1 = _rowmajor(g_y), _rowmajor(b1)
     if b2 is not None:
         b2 = _rowmajor(b2)
@@ -444,6 +446,15 @@ def mlp_bwd_w(g_y: Tensor, z: Tensor, prelu: Tensor, b1: Tensor, b2: Optional[Te
     # algorithmic: g_y, z and B read once, g_z written when it is returned (the weight-stationary kernels form it in
     # their staging and store it; elsewhere a separate PReLU-backward pass writes it and the TN GEMM reads it back)
     nb = s * M * (2 * N + K + (N if g_z is not None else 0)) + 4 * N * K
+    if y_alt is not None:
+        assert z.dtype == torch.bfloat16 and g_z is not None and z.is_contiguous() and y_alt.shape == z.shape \
+            and y_alt.is_contiguous(), "mlp_bwd_w: y_alt needs the bf16 zy layout"
+        _probed("gemm_dw", 2.0 * M * N * K, nb,
+                lambda: _lib.call("hgin_gin_mlp_bwd_w_zy_bf16", _p(g_y), g_y.stride(0), _p(z), _p(y_alt), _p(prelu),
+                                  _p(b1), b1.stride(0), k1, _p(b2), b2.stride(0) if b2 is not None else 0, M, N, K,
+                                  _p(g_w), g_w.stride(0), _p(g_a), _p(g_b), _p(g_z), N, _p(ws), nbytes.value,
+                                  _stream(z)))
+        return g_w, g_a, g_b, g_z
     _probed("gemm_dw", 2.0 * M * N * K, nb,
             lambda: _lib.call(f"hgin_gin_mlp_bwd_w_{_sfx(z)}", _p(g_y), g_y.stride(0), _p(z), z.stride(0), _p(prelu),
                               _p(b1), b1.stride(0), k1, _p(b2), b2.stride(0) if b2 is not None else 0, M, N, K,
@@ -467,12 +478,16 @@ def self_wgrad(G: Tensor, weight: Tensor, f: int, concat: bool, eps: Tensor):
 
 
 def gin_mlp_fwd(comb: Tensor, weight: Tensor, bias: Tensor, prelu: Optional[Tensor], accum: Optional[Tensor],
-                save_z: bool = True, comb2: Optional[Tensor] = None, eps2: Optional[Tensor] = None):
+                save_z: bool = True, comb2: Optional[Tensor] = None, eps2: Optional[Tensor] = None,
+                zy: bool = False):
     """y = prelu([comb | s * comb2] @ W^T + b) [+ accum]  (prelu None: plain Linear, y = z, nothing saved);
     s = 1 + eps2[0] when ``eps2`` is given (the concat GINConv's self term formed in the GEMM's loads), else 1.
 
     fp32 storage: everything fp32.  bf16 storage (cfg5): comb / comb2 / weight / accum / z / y bf16, bias and
-    prelu fp32; the plain Linear (the readout head) returns fp32."""
+    prelu fp32; the plain Linear (the readout head) returns fp32.
+
+    ``zy`` (bf16, no accum, z kept): hgin_gin_mlp_fwd_zy_bf16 — with a positive slope the kernel may leave z unwritten
+    (y = prelu(z) determines it); its backward must then be mlp_bwd_w(..., y_alt=y)."""
     M, k1 = comb.shape
     K = k1 + (comb2.shape[1] if comb2 is not None else 0)
     N = weight.shape[0]
@@ -487,11 +502,15 @@ def gin_mlp_fwd(comb: Tensor, weight: Tensor, bias: Tensor, prelu: Optional[Tens
     ws_form = prelu is not None and ((comb2 is None and K == 256) or
                                      (eps2 is not None and accum is None and k1 == 256 and K == 512))
     planes = nt_planes(weight, M, ws_form=ws_form) if weight.stride(1) == 1 else None
+    zy = zy and dt == torch.bfloat16 and prelu is not None and accum is None and z is not None
 
     def launch():
         if prelu is None:
             _lib.call(f"hgin_linear_fwd_{sfx}", _p(comb), comb.stride(0), k1, _p(comb2), ld2, _p(weight), _p(bias),
                       _p(y), M, N, K, _p(planes), _stream(comb))
+        elif zy:
+            _lib.call("hgin_gin_mlp_fwd_zy_bf16", _p(comb), comb.stride(0), k1, _p(comb2), ld2, _p(eps2), _p(weight),
+                      _p(bias), _p(prelu), _p(z), _p(y), M, N, K, _stream(comb))
         else:
             _lib.call(f"hgin_gin_mlp_fwd_{sfx}", _p(comb), comb.stride(0), k1, _p(comb2), ld2, _p(eps2), _p(weight),
                       _p(bias), _p(prelu), _p(accum), _p(z), _p(y), M, N, K, _p(planes), _stream(comb))
@@ -500,8 +519,10 @@ def gin_mlp_fwd(comb: Tensor, weight: Tensor, bias: Tensor, prelu: Optional[Tens
     if probe is None:
         launch()
     else:
+        # (the untimed probe pass may sync: with zy the weight-stationary kernel writes no z when the slope is > 0)
+        z_written = z is not None and not (zy and N in (128, 256) and K in (128, 256, 512) and float(prelu) > 0)
         probe.around("gin_mlp" if prelu is not None else "linear", 2.0 * M * N * K, launch,
-                     profiling.gemm_bytes(M, N, K, comb.element_size(), z is not None, accum is not None))
+                     profiling.gemm_bytes(M, N, K, comb.element_size(), z_written, accum is not None))
     return z, y
 
 
@@ -558,9 +579,11 @@ class _AggregateFn(torch.autograd.Function):
         return g_src, g_dst, (g_eps.view_as(eps) if need_eps and g_eps is not None else None), None, None
 
 
-def _gin_forward(x_src, x_dst, eps, weight, bias, prelu, accum, graph: RelationGraph, mode: int, data_inputs: bool):
+def _gin_forward(x_src, x_dst, eps, weight, bias, prelu, accum, graph: RelationGraph, mode: int, data_inputs: bool,
+                 zy: bool = False):
     """One GINConv + GINLayer MLP forward: y = prelu(comb @ W^T + b) [+ accum], comb = aggregate + self term.
-    Returns (y, w_op, comb, z) — what the backward needs besides x_dst / eps / prelu."""
+    Returns (y, w_op, comb, z) — what the backward needs besides x_dst / eps / prelu.  ``zy``: gin_mlp_fwd's z-from-y
+    mode (bf16 without accum); the backward then takes y_alt = y."""
     f_src = x_src.size(1)
     w_op = _as(weight, x_src.dtype)          # bf16 path: the GEMM reads a bf16 copy of the fp32 master
     if mode == COMBINE_CONCAT and data_inputs:
@@ -575,20 +598,21 @@ def _gin_forward(x_src, x_dst, eps, weight, bias, prelu, accum, graph: RelationG
             # product with one bf16 rounding fewer and no eps-scaling pass in the GEMM (k_ws_bf16 K = 512: 3.31 ->
             # 2.78 ms at M = 6M, profiles/r03/s17).  The backward keeps the unfolded operand (dW, eps gradient).
             w_f = torch.cat((weight[:, :f_src], weight[:, f_src:] * (1.0 + eps)), 1).to(torch.bfloat16)
-            z, y = gin_mlp_fwd(comb, w_f, bias, prelu, accum, comb2=x_dst)
+            z, y = gin_mlp_fwd(comb, w_f, bias, prelu, accum, comb2=x_dst, zy=zy)
         else:
-            z, y = gin_mlp_fwd(comb, w_op, bias, prelu, accum, comb2=x_dst, eps2=eps)
+            z, y = gin_mlp_fwd(comb, w_op, bias, prelu, accum, comb2=x_dst, eps2=eps, zy=zy)
     else:
         width = f_src + (x_dst.size(1) if mode == COMBINE_CONCAT else 0)
         comb = torch.empty(graph.n_dst, width, dtype=x_src.dtype, device=x_src.device)
         aggregate_into(graph.csr, x_src, x_dst, eps, mode, comb)
-        z, y = gin_mlp_fwd(comb, w_op, bias, prelu, accum)
+        z, y = gin_mlp_fwd(comb, w_op, bias, prelu, accum, zy=zy)
     return y, w_op, comb, z
 
 
 def _gin_backward(g_y, x_dst, eps, weight, prelu, comb, z, graph: RelationGraph, mode: int, f_src: int,
                   need_src: bool, need_dst: bool, need_eps: bool, need_w: bool,
-                  g_src_prev: Optional[Tensor] = None, g_dst_prev: Optional[Tensor] = None):
+                  g_src_prev: Optional[Tensor] = None, g_dst_prev: Optional[Tensor] = None,
+                  y_alt: Optional[Tensor] = None):
     """Backward of _gin_forward: (g_src, g_dst, g_eps, g_w, g_b, g_a).  ``g_src_prev`` / ``g_dst_prev``: running
     gradients of the source / destination node type from other relations, which g_src / g_dst accumulate onto
     in place inside the CSC aggregate (ADD mode, eps 0) and the dX GEMM's epilogue — autograd's sum over the
@@ -598,7 +622,7 @@ def _gin_backward(g_y, x_dst, eps, weight, prelu, comb, z, graph: RelationGraph,
     if need_src or need_dst:
         # (a side stream overlapping dW with the dX GEMM + CSC aggregate measured 1 % slower on cfg2 / cfg2bf:
         # each of these kernels already fills the 256 CUs)
-        g_w, g_a, g_b, g_z = mlp_bwd_w(g_y, z, prelu, comb, want_gz=True)
+        g_w, g_a, g_b, g_z = mlp_bwd_w(g_y, z, prelu, comb, want_gz=True, y_alt=y_alt)
         cs = f_src if mode == COMBINE_CONCAT else 0
         if mode != COMBINE_NONE and cs % 4 == 0 and x_dst.stride(1) == 1:
             # dX = g_z W [N_dst, K] with the self term's backward in the GEMM epilogue
@@ -617,17 +641,17 @@ def _gin_backward(g_y, x_dst, eps, weight, prelu, comb, z, graph: RelationGraph,
         # sum(g_comb[:, self] * x_dst) = sum(W_self * (g_z^T x_dst)), so one TN pass over
         # [aggregate | x_dst] yields dW and the eps gradient and the [N_dst, K] dX GEMM is skipped.
         if mode == COMBINE_CONCAT:
-            G, g_a, g_b, _ = mlp_bwd_w(g_y, z, prelu, comb[:, :f_src], x_dst)
+            G, g_a, g_b, _ = mlp_bwd_w(g_y, z, prelu, comb[:, :f_src], x_dst, y_alt=y_alt)
         else:
-            G, g_a, g_b, _ = mlp_bwd_w(g_y, z, prelu, comb, x_dst)
+            G, g_a, g_b, _ = mlp_bwd_w(g_y, z, prelu, comb, x_dst, y_alt=y_alt)
         g_w, g_eps = self_wgrad(G, weight, f_src, mode == COMBINE_CONCAT, eps)
         g_w = g_w if need_w else None
     elif mode == COMBINE_CONCAT and comb.size(1) == f_src:
         # the forward kept only the aggregate (inputs are data): dW of the self block = (1 + eps) g_z^T x_dst
-        G, g_a, g_b, _ = mlp_bwd_w(g_y, z, prelu, comb, x_dst)
+        G, g_a, g_b, _ = mlp_bwd_w(g_y, z, prelu, comb, x_dst, y_alt=y_alt)
         g_w = self_wgrad(G, weight, f_src, True, eps)[0] if need_w else None
     else:
-        g_w, g_a, g_b, _ = mlp_bwd_w(g_y, z, prelu, comb)
+        g_w, g_a, g_b, _ = mlp_bwd_w(g_y, z, prelu, comb, y_alt=y_alt)
     return g_src, g_dst, g_eps, g_w, g_b, g_a
 
 
@@ -684,10 +708,12 @@ class _HeteroGINLayerFn(torch.autograd.Function):
         for i, sp in enumerate(specs):
             eps, w, b, a = tensors[n_types + 4 * i: n_types + 4 * i + 4]
             data_inputs = not (need[sp.src] or need[sp.dst])
+            # bf16: the first relation into a type has no accum, so its y determines z (gin_mlp_fwd zy)
+            zy = xs[sp.src].dtype == torch.bfloat16 and sp.dst not in outs
             y, w_op, comb, z = _gin_forward(xs[sp.src], xs[sp.dst], eps, w, b, a, outs.get(sp.dst), sp.graph,
-                                            sp.mode, data_inputs)
+                                            sp.mode, data_inputs, zy=zy)
             outs[sp.dst] = y
-            saved += [w_op, comb, z]
+            saved += [w_op, comb, z, y if zy else None]
         ctx.specs, ctx.n_types = specs, n_types
         ctx.out_types = list(outs)
         ctx.f_src = [xs[sp.src].size(1) for sp in specs]
@@ -713,11 +739,11 @@ class _HeteroGINLayerFn(torch.autograd.Function):
             if g_y is None:
                 continue
             eps, _, _, prelu = params[4 * i: 4 * i + 4]
-            w_op, comb, z = saved[3 * i: 3 * i + 3]
+            w_op, comb, z, y_alt = saved[4 * i: 4 * i + 4]
             pn = need[nt + 4 * i: nt + 4 * i + 4]
             g_src, g_dst, g_eps, g_w, g_b, g_a = _gin_backward(
                 g_y, xs[sp.dst], eps, w_op, prelu, comb, z, sp.graph, sp.mode, ctx.f_src[i], need[sp.src],
-                need[sp.dst], pn[0], pn[1], g_src_prev=gx[sp.src], g_dst_prev=gx[sp.dst])
+                need[sp.dst], pn[0], pn[1], g_src_prev=gx[sp.src], g_dst_prev=gx[sp.dst], y_alt=y_alt)
             if need[sp.src]:
                 gx[sp.src] = g_src
             if need[sp.dst]:
@@ -767,13 +793,14 @@ class _LinearPReLUFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x1, x2, weight, bias, prelu):
         w_op = _as(weight, x1.dtype)
-        z, y = gin_mlp_fwd(x1, w_op, bias, prelu, None, comb2=x2)
-        ctx.save_for_backward(x1, x2, w_op, prelu, z)
+        zy = x1.dtype == torch.bfloat16 and prelu is not None   # (no accum: y determines z, gin_mlp_fwd zy)
+        z, y = gin_mlp_fwd(x1, w_op, bias, prelu, None, comb2=x2, zy=zy)
+        ctx.save_for_backward(x1, x2, w_op, prelu, z, y if zy else None)
         return y
 
     @staticmethod
     def backward(ctx, g_y):
-        x1, x2, weight, prelu, z = ctx.saved_tensors
+        x1, x2, weight, prelu, z, y_alt = ctx.saved_tensors
         need_x1, need_x2, need_w, need_b, need_a = ctx.needs_input_grad
         g_y = _rowmajor(g_y)
         k1 = x1.size(1)
@@ -785,7 +812,8 @@ class _LinearPReLUFn(torch.autograd.Function):
             g_x1 = gemm_nt(g_z, weight[:, :k1].t().contiguous()) if need_x1 else None
             g_x2 = gemm_nt(g_z, weight[:, k1:].t().contiguous()) if (need_x2 and x2 is not None) else None
         else:
-            g_w, g_a, g_b, g_z = mlp_bwd_w(g_y, z, prelu, x1, x2, want_gz=need_x1 or (need_x2 and x2 is not None))
+            g_w, g_a, g_b, g_z = mlp_bwd_w(g_y, z, prelu, x1, x2, want_gz=need_x1 or (need_x2 and x2 is not None),
+                                           y_alt=y_alt)
             g_x1 = gemm_nt(g_z, weight[:, :k1].t().contiguous()) if need_x1 else None
             g_x2 = gemm_nt(g_z, weight[:, k1:].t().contiguous()) if (need_x2 and x2 is not None) else None
         return (g_x1, g_x2, g_w if need_w else None, (g_b if need_b else None),

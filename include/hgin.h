@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define HGIN_ABI_VERSION 7
+#define HGIN_ABI_VERSION 8
 
 #define HGIN_OK 0
 #define HGIN_E_ARG (-1)        /* bad size / null pointer / unsupported combination */
@@ -294,6 +294,24 @@ int hgin_gin_mlp_bwd_w_bf16(const uint16_t* g_y, int64_t ld_gy, const uint16_t* 
 int hgin_combine_bwd_bf16(const uint16_t* g, int64_t ld_g, const uint16_t* x_dst, int64_t ld_dst,
                           int64_t n_rows, int64_t f_dst, const float* eps, uint16_t* g_x_dst, int64_t ld_gx,
                           float* g_eps, void* workspace, size_t workspace_bytes, void* stream);
+
+/* z from y (ABI 8, round 6): a GINLayer MLP forward with no accum has y = prelu(z) exactly, so with a positive slope
+ * z > 0 <=> y > 0 and z = y / slope.  hgin_gin_mlp_fwd_zy_bf16 = hgin_gin_mlp_fwd_bf16 (accum NULL) that may leave z
+ * unwritten — it skips the z stores on the device when prelu[0] > 0 (the weight-stationary kernel; elsewhere it writes
+ * z); hgin_gin_mlp_bwd_w_zy_bf16 = hgin_gin_mlp_bwd_w_bf16 for that layer (z / y / g_z dense [M, N], g_z required):
+ * when prelu[0] > 0 it reads y in place of z (the PReLU-fused weight-stationary dW; other shapes restore z from y
+ * in place first).  g_z, g_w and g_bias equal the plain pair's bit for bit; g_prelu = sum(y g_y | y <= 0) / slope,
+ * the same sum up to the bf16 rounding of z.  Replaces, for the relations whose output starts a type's sum
+ * (models.py:286-298 HeteroConv, the first relation into each type) and the readout's PReLU Linears, one of the
+ * layer's three row streams (the z write: a third of the forward GEMM's HBM bytes). */
+int hgin_gin_mlp_fwd_zy_bf16(const uint16_t* a1, int64_t lda1, int64_t k1, const uint16_t* a2, int64_t lda2,
+                             const float* a2_eps, const uint16_t* w, const float* bias, const float* prelu,
+                             uint16_t* z, uint16_t* y, int64_t M, int64_t N, int64_t K, void* stream);
+int hgin_gin_mlp_bwd_w_zy_bf16(const uint16_t* g_y, int64_t ld_gy, uint16_t* z, const uint16_t* y,
+                               const float* prelu, const uint16_t* b1, int64_t ldb1, int64_t k1,
+                               const uint16_t* b2, int64_t ldb2, int64_t M, int64_t N, int64_t K, float* g_w,
+                               int64_t ldw, float* g_prelu, float* g_bias, uint16_t* g_z, int64_t ld_gz,
+                               void* workspace, size_t workspace_bytes, void* stream);
 
 /* ---- F3: fused readout head + MAPE loss ------------------------------------------------------------
  * Replaces the head Linear(K, 1) (models.py:326-330, :373-374) and train.py:38-42:

@@ -338,3 +338,36 @@ def test_model_bf16_nonzero_eps_vs_fp32(case):
     assert err_out <= 3e-2 and abs(l16 - l32) <= 2e-2 * abs(l32)
     assert np.median(list(errs.values())) <= 5e-2
     assert eps_errs and max(eps_errs) <= 1e-1
+
+
+@pytest.mark.parametrize("M,N,K1,K2,slope", [(20000, 256, 256, 0, 0.25), (3000, 128, 128, 0, 0.25),
+                                              (5000, 256, 256, 256, 0.25), (4001, 128, 256, 256, 0.3),
+                                              (777, 64, 64, 0, 0.25), (9000, 256, 256, 0, -0.1),
+                                              (9000, 256, 256, 0, 0.0), (31, 256, 256, 0, 0.25)])
+def test_mlp_zy_bf16_matches_plain(M, N, K1, K2, slope):
+    """The z-from-y pair (hgin_gin_mlp_fwd_zy_bf16 / hgin_gin_mlp_bwd_w_zy_bf16, ABI 8): y bit-identical to the plain
+    forward; g_z, g_w and g_bias bit-identical to the plain backward on the written z (the sign of y is the sign of z
+    when the slope is > 0); g_prelu = sum(y g | y <= 0) / slope within the bf16 rounding of z.  With a slope <= 0 the
+    forward writes z and everything is bit-identical; N = 64 (no weight-stationary kernel) restores z from y in place
+    before the separate PReLU-backward pass."""
+    g = torch.Generator(device=DEV).manual_seed(M + N + K1)
+    a1 = _bf(torch.randn(M, K1, device=DEV, generator=g))
+    a2 = _bf(torch.randn(M, K2, device=DEV, generator=g)) if K2 else None
+    w = _bf(torch.randn(N, K1 + K2, device=DEV, generator=g) / (K1 + K2) ** 0.5)
+    b = torch.randn(N, device=DEV, generator=g)
+    s = torch.tensor([slope], device=DEV)
+    z0, y0 = ops.gin_mlp_fwd(a1, w, b, s, None, comb2=a2)
+    z1, y1 = ops.gin_mlp_fwd(a1, w, b, s, None, comb2=a2, zy=True)
+    assert torch.equal(y1.view(torch.int16), y0.view(torch.int16))
+    if slope <= 0:
+        assert torch.equal(z1.view(torch.int16), z0.view(torch.int16))
+    gy = _bf(torch.randn(M, N, device=DEV, generator=g))
+    r0 = ops.mlp_bwd_w(gy, z0, s, a1, a2, want_gz=True)
+    r1 = ops.mlp_bwd_w(gy, z1, s, a1, a2, want_gz=True, y_alt=y1)
+    assert torch.equal(r1[3].view(torch.int16), r0[3].view(torch.int16))      # g_z
+    assert torch.equal(r1[0], r0[0]) and torch.equal(r1[2], r0[2])            # g_w, g_bias
+    zd = z0.double()
+    bound = 2.0 ** -8 * float((torch.where(zd > 0, 0.0, zd) * gy.double()).abs().sum()) + 1e-6
+    assert abs(float(r1[1]) - float(r0[1])) <= bound, (float(r1[1]), float(r0[1]))
+    if slope <= 0:
+        assert torch.equal(r1[1], r0[1])
