@@ -447,8 +447,9 @@ def mlp_bwd_w(g_y: Tensor, z: Tensor, prelu: Tensor, b1: Tensor, b2: Optional[Te
     # their staging and store it; elsewhere a separate PReLU-backward pass writes it and the TN GEMM reads it back)
     nb = s * M * (2 * N + K + (N if g_z is not None else 0)) + 4 * N * K
     if y_alt is not None:
-        assert z.dtype == torch.bfloat16 and g_z is not None and z.is_contiguous() and y_alt.shape == z.shape \
-            and y_alt.is_contiguous(), "mlp_bwd_w: y_alt needs the bf16 zy layout"
+        if not (z.dtype == torch.bfloat16 and g_z is not None and z.is_contiguous() and y_alt.shape == z.shape
+                and y_alt.dtype == z.dtype and y_alt.is_contiguous()):
+            raise RuntimeError("mlp_bwd_w: y_alt needs the bf16 z-from-y layout (dense [M, N] z and y)")
         _probed("gemm_dw", 2.0 * M * N * K, nb,
                 lambda: _lib.call("hgin_gin_mlp_bwd_w_zy_bf16", _p(g_y), g_y.stride(0), _p(z), _p(y_alt), _p(prelu),
                                   _p(b1), b1.stride(0), k1, _p(b2), b2.stride(0) if b2 is not None else 0, M, N, K,

@@ -5,6 +5,9 @@ set -u
 OUT=gpurun_out/${TAG:-r06h}
 mkdir -p "$OUT"
 export PYTHONUNBUFFERED=1 TMPDIR=/tmp
+timeout -k 10 300 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_gpu_bf16.py -k "nan or gin_mlp_fwd" \
+  > "$OUT/pytest_nan.log" 2>&1 || { grep -E "^E |FAILED" "$OUT/pytest_nan.log" | head -20; tail -3 "$OUT/pytest_nan.log"; exit 1; }
+tail -1 "$OUT/pytest_nan.log"
 for rep in 1 2; do
   timeout -k 10 180 python -u tools/gemm_ab.py --M 3000000 --reps 10 --only fwd512acc,fwd512,fwd512two >> "$OUT/ab_k512.txt" 2>&1 \
     || { tail -20 "$OUT/ab_k512.txt"; exit 1; }
