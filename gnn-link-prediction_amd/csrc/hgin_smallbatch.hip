@@ -382,7 +382,7 @@ __device__ __forceinline__ void copy_flat(float* dst, const float* src, int n) {
 constexpr int kSbFwdRows = 32;
 
 typedef float sb_f32x16 __attribute__((ext_vector_type(16)));
-template <int NT, class Epi>
+template <int NT, int KB = 4, class Epi>
 __device__ __forceinline__ void tile_mfma(const float* A, int lda, int nr, const float* Bm, int bsk, int bsn, int N,
                                           int K, float* red, Epi epi);
 
@@ -427,11 +427,16 @@ __device__ void sb_pool(const SbArgs& a, float* red) {
 // kM (hidden >= 64): the Linear of each relation on the matrix cores — tile_mfma over 32-column chunks of W staged in
 // LDS, the chunks' partial sums added in chunk order — instead of one dot chain per output (at H = 128 a 128-term
 // chain per output made the launch ~120 us); comb rows at an odd stride (the MFMA operand reads a column of rows)
-constexpr int kFwdMW = 128 * 17, kFwdMT = kSbFwdRows * 129;   // W chunks of 16 columns; the z tile
+// kM blocks hold 8 rows (round 6): a thread's 4 gather chains of a 128-wide layer are then one gather_chain4 batch
+// instead of four after each other, the blocks are 4x as many and 3 fit a CU (hidden 128: 64.8 -> see DESIGN.md §3);
+// the MFMA tile's rows past 8 are zeros (tile_mfma's nr), and every output is the same sum in the same order
+constexpr int kSbFwdRowsM = 8;
+constexpr int kFwdMW = 128 * 17, kFwdMT = kSbFwdRowsM * 129;   // W chunks of 16 columns; the z tile
 template <bool kM>
 __global__ __launch_bounds__(kSbThreads) void k_sb_fwd(SbArgs a, int l) {
-  __shared__ float s_comb[2][kM ? kSbFwdRows * 129 : kSbFwdRows * 128];   // <= 2 relations into a type, K <= 128
-  __shared__ float s_w[2][kSbFwdW];
+  constexpr int R = kM ? kSbFwdRowsM : kSbFwdRows;   // rows per workgroup
+  __shared__ float s_comb[2][kM ? R * 129 : R * 128];   // <= 2 relations into a type, K <= 128
+  __shared__ float s_w[2][kM ? 1 : kSbFwdW];           // (kM: H * K > kSbFwdW, W goes through s_m in chunks)
   __shared__ float s_m[kM ? kFwdMW + kFwdMT + (kSbThreads / 64) * 32 * 33 : 1];   // W chunk | z | split partials
   const int t = blockIdx.y;
   if (t == 3) {   // (the first layer with GLOBAL_FEATS)
@@ -441,13 +446,13 @@ __global__ __launch_bounds__(kSbThreads) void k_sb_fwd(SbArgs a, int l) {
   const int tid = threadIdx.x;
   const int H = a.H;
   const int n = nrows(a, t);
-  const int r0 = blockIdx.x * kSbFwdRows;
+  const int r0 = blockIdx.x * R;
   if (a.adam_step && l == 0 && blockIdx.x == 0 && t == 0 && tid == 0) a.adam_step[0] += 1.0f;   // read by k_sb_final
   if (r0 >= n) return;
-  const int nr = n - r0 < kSbFwdRows ? n - r0 : kSbFwdRows;
+  const int nr = n - r0 < R ? n - r0 : R;
   // the relations' small weights into LDS first: their loads fly with the aggregate's gathers
-  int wl = 0;   // bit sl: relation slot sl's W is in s_w[sl]
-  {
+  int wl = 0;   // bit sl: relation slot sl's W is in s_w[sl] (the scalar Linear only: kM stages W in chunks)
+  if constexpr (!kM) {
     int sl = 0;
     for (int r = 0; r < kRel; ++r) {
       if (kRelDst[r] != t) continue;
@@ -526,7 +531,7 @@ __global__ __launch_bounds__(kSbThreads) void k_sb_fwd(SbArgs a, int l) {
   __syncthreads();
   if constexpr (kM) {
     float* s_wc = s_m;               // [H][17]: W[:, kc : kc + 16]
-    float* s_z = s_m + kFwdMW;       // [32][H | 1]
+    float* s_z = s_m + kFwdMW;       // [R][H | 1]
     float* red = s_z + kFwdMT;
     const int ly = H | 1;
     int nrel = 0;
@@ -913,7 +918,10 @@ constexpr int kRoThreadsM = 512;   // 8 waves: 2 per SIMD, so one wave's LDS / M
 // k-steps are split over the idle ones (a fixed power-of-two split) and the partials, parked in red [NT / 64][32][33],
 // are added in split order.
 // epi(r, n, v) receives every output of rows < nr and columns < N (v = 0 + the products in k order within a split).
-template <int NT, class Epi>
+// KB k-steps' operands are loaded together before their MFMAs: 4 for LDS operands; 16 where an operand comes through
+// the caches (a weight matrix too large to stage), so a 128-deep product is 4 dependent L2 round trips instead of 16
+// (round 6: hidden 128 / the GAT readout — the same products in the same order)
+template <int NT, int KB = 4, class Epi>
 __device__ __forceinline__ void tile_mfma_s(const float* A, int asr, int ask, int nr, const float* Bm, int bsk, int bsn,
                                             int N, int K, float* red, Epi epi) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -937,10 +945,10 @@ __device__ __forceinline__ void tile_mfma_s(const float* A, int asr, int ask, in
     sb_f32x16 acc;
 #pragma unroll
     for (int j = 0; j < 16; ++j) acc[j] = 0.0f;
-    for (int st = s0; st < s1; st += 4) {   // 4 k-steps' operands loaded together, then their MFMAs
-      float av[4], bv[4];
+    for (int st = s0; st < s1; st += KB) {   // KB k-steps' operands loaded together, then their MFMAs
+      float av[KB], bv[KB];
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
+      for (int q = 0; q < KB; ++q) {
         const int k = 2 * (st + q) + lh;
         const bool kok = st + q < s1 && k < K;
         const int kc = k < K ? k : K - 1;
@@ -949,7 +957,7 @@ __device__ __forceinline__ void tile_mfma_s(const float* A, int asr, int ask, in
         bv[q] = nok && kok ? y : 0.0f;
       }
 #pragma unroll
-      for (int q = 0; q < 4; ++q)
+      for (int q = 0; q < KB; ++q)
         if (st + q < s1) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[q], bv[q], acc, 0, 0, 0);
     }
     if (ks == 1) {
@@ -975,10 +983,10 @@ __device__ __forceinline__ void tile_mfma_s(const float* A, int asr, int ask, in
 }
 
 // A(r, k) = A[r lda + k] (row-major A)
-template <int NT, class Epi>
+template <int NT, int KB, class Epi>
 __device__ __forceinline__ void tile_mfma(const float* A, int lda, int nr, const float* Bm, int bsk, int bsn, int N,
                                           int K, float* red, Epi epi) {
-  tile_mfma_s<NT>(A, lda, 1, nr, Bm, bsk, bsn, N, K, red, epi);
+  tile_mfma_s<NT, KB>(A, lda, 1, nr, Bm, bsk, bsn, N, K, red, epi);
 }
 
 // kWL false (hgin_sb_readout_lds_bytes mode 4: the staged weights would not fit, e.g. hidden 128): the MFMA operands'
@@ -1055,7 +1063,7 @@ __global__ __launch_bounds__(kRoThreadsM) void k_sb_readout_mfma(SbArgs a) {
       const int lin = i == 0 ? l0 : lz[i > 0 ? i - 1 : 0];
       const int N = a.rw[i];
       const float* b = kWL ? (const float*)(sm + oW[i] + N * ldw[i]) : a.row_b[i];
-      tile_mfma<NT>(in, lin, nr, RO_WM(i), 1, ldw[i], N, win[i], red, [&](int r, int n, float v) {
+      tile_mfma<NT, kWL ? 4 : 16>(in, lin, nr, RO_WM(i), 1, ldw[i], N, win[i], red, [&](int r, int n, float v) {
         const float z = bn_eval(a, i, n, __fadd_rn(v, b[n]));
         sm[oZ[i] + r * lz[i] + n] = z;
         const float yv = z > 0.0f ? z : __fmul_rn(slope, z);
@@ -1136,7 +1144,7 @@ __global__ __launch_bounds__(kRoThreadsM) void k_sb_readout_mfma(SbArgs a) {
       // g_in = g_z W (the first layer: only the path embeddings' H columns have a gradient)
       const int KG = i == 0 ? H : K, lgn = KG | 1;
       float* gn = g_next;
-      tile_mfma<NT>(g_y, ly, nr, RO_WM(i), ldw[i], 1, KG, N, red,
+      tile_mfma<NT, kWL ? 4 : 16>(g_y, ly, nr, RO_WM(i), ldw[i], 1, KG, N, red,
                 [&](int r, int n, float v) { gn[r * lgn + n] = v; });
       __syncthreads();
       SB_STAMP(9 + 2 * i);
@@ -1702,7 +1710,7 @@ __global__ __launch_bounds__(kSbThreads, kM ? 1 : 4) void k_sb_bwd_w(SbArgs a, i
         for (int rr = 0; rr < nr; ++rr) bsum = __fadd_rn(bsum, s_g[rr * lg + tid]);
       for (int sb = 0; sb < nr; sb += 32) {   // g_comb rows (row-local: k_sb_bwd_in reads them after this launch)
         const int ns = nr - sb < 32 ? nr - sb : 32;
-        tile_mfma<kSbThreads>(s_g + sb * lg, lg, ns, cv.w, K, 1, K, H, redm, [&](int r, int k, float v) {
+        tile_mfma<kSbThreads, 16>(s_g + sb * lg, lg, ns, cv.w, K, 1, K, H, redm, [&](int r, int k, float v) {
           const int i = rb + sb + r;
           gc[(int64_t)i * a.kmax + k] = v;
           if (k >= fs) {
@@ -2321,7 +2329,7 @@ extern "C" int hgin_sb_step(const void* args, size_t args_bytes, size_t readout_
     else if (c == 8) k_sb_gat_fwd<8><<<g, kSbThreads, 0, s>>>(a);
     else k_sb_gat_fwd<16><<<g, kSbThreads, 0, s>>>(a);
   } else {
-    const unsigned fwd_blocks = (unsigned)ceil_div((int64_t)capt_max, (int64_t)kSbFwdRows);
+    const unsigned fwd_blocks = (unsigned)ceil_div((int64_t)capt_max, (int64_t)(a.H >= 64 ? kSbFwdRowsM : kSbFwdRows));
     for (int l = 0; l < a.L; ++l) {
       const dim3 g(fwd_blocks, l == 0 && a.pool_w ? 4 : 3);
       if (a.H >= 64)
