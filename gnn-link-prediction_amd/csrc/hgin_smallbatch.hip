@@ -2151,22 +2151,48 @@ __global__ __launch_bounds__(kSbThreads) void k_sb_gat_bwd(SbArgs a, const float
       const float ev = pre > 0.0f ? pre : __fmul_rn(sl, pre);
       al = __fdiv_rn(expf(ev - m), den);
     };
-    float S = 0.0f;
-    gat_edges(a, r, i, n_src, rows, [&](int j) {
-      float xj[kGatK], pre, al, ga;
-      edge(j, xj, pre, al, ga);
-      S = fmaf(al, ga, S);
-    });
     float gad = 0.0f;
-    gat_edges(a, r, i, n_src, rows, [&](int j) {
-      float xj[kGatK], pre, al, ga;
-      edge(j, xj, pre, al, ga);
-      const float ge = __fmul_rn(al, __fsub_rn(ga, S));
-      const float gp = pre > 0.0f ? ge : __fmul_rn(sl, ge);
-      gad = __fadd_rn(gad, gp);
+    if constexpr (C <= 8) {
+      // one walk (round 6): g_pre = lr' alpha (g_alpha - S) is linear in S = sum alpha g_alpha, so its sums split into
+      // sum lr' alpha g_alpha [x_s] - S sum lr' alpha [x_s], all four gathered in the walk that forms S — half the
+      // dependent memory round trips of the two-walk form below (the same sums in another association: fp32 tolerance)
+      float S = 0.0f, D = 0.0f, E = 0.0f, A[kGatK], B[kGatK];
 #pragma unroll
-      for (int k = 0; k < kGatK; ++k) rsum[k] = fmaf(gp, xj[k], rsum[k]);
-    });
+      for (int k = 0; k < kGatK; ++k) A[k] = B[k] = 0.0f;
+      gat_edges(a, r, i, n_src, rows, [&](int j) {
+        float xj[kGatK], pre, al, ga;
+        edge(j, xj, pre, al, ga);
+        S = fmaf(al, ga, S);
+        const float w1 = pre > 0.0f ? al : __fmul_rn(sl, al);
+        const float w2 = __fmul_rn(w1, ga);
+        D = __fadd_rn(D, w1);
+        E = __fadd_rn(E, w2);
+#pragma unroll
+        for (int k = 0; k < kGatK; ++k) {
+          A[k] = fmaf(w2, xj[k], A[k]);
+          B[k] = fmaf(w1, xj[k], B[k]);
+        }
+      });
+      gad = fmaf(-S, D, E);
+#pragma unroll
+      for (int k = 0; k < kGatK; ++k) rsum[k] = __fadd_rn(rsum[k], fmaf(-S, B[k], A[k]));
+    } else {   // (C = 16: G alone holds 128 registers, the one-walk sums would spill)
+      float S = 0.0f;
+      gat_edges(a, r, i, n_src, rows, [&](int j) {
+        float xj[kGatK], pre, al, ga;
+        edge(j, xj, pre, al, ga);
+        S = fmaf(al, ga, S);
+      });
+      gat_edges(a, r, i, n_src, rows, [&](int j) {
+        float xj[kGatK], pre, al, ga;
+        edge(j, xj, pre, al, ga);
+        const float ge = __fmul_rn(al, __fsub_rn(ga, S));
+        const float gp = pre > 0.0f ? ge : __fmul_rn(sl, ge);
+        gad = __fadd_rn(gad, gp);
+#pragma unroll
+        for (int k = 0; k < kGatK; ++k) rsum[k] = fmaf(gp, xj[k], rsum[k]);
+      });
+    }
 #pragma unroll
     for (int k = 0; k < kGatK; ++k) tsum[k] = fmaf(gad, xi[k], tsum[k]);
   }

@@ -20,7 +20,7 @@ place); the step returns the batch's device ``loss_value`` (train.py:40), no hos
 from __future__ import annotations
 
 import ctypes
-from typing import Sequence
+from typing import Optional, Sequence
 
 import torch
 
@@ -274,7 +274,7 @@ class SmallBatchStep:
 
     def __init__(self, model: HetroGIN, opt: torch.optim.Optimizer, store: GraphStore, batch_size: int,
                  warmup_ids: Sequence[Sequence[int]], warmup: int = 2, fold_optimizer: bool = True,
-                 readout: str = "auto", _eval: bool = False):
+                 readout: str = "auto", _eval: bool = False, n_parts: Optional[int] = None):
         if readout not in ("auto", "scalar"):
             raise ValueError("SmallBatchStep: readout is 'auto' (32-row MFMA tiles where they fit) or 'scalar'")
         if warmup_ids and any(isinstance(p, torch.nn.parameter.UninitializedParameter) for p in model.parameters()):
@@ -467,8 +467,13 @@ class SmallBatchStep:
                 a.gat_st_off[ri] = o2[ri]
         for ti, t in enumerate(TYPES):
             a.cap[ti] = cap[t]
-        a.n_parts = N_PARTS
-        self.part_gin = torch.zeros(N_PARTS * p_gin, **f32)
+        # row chunks of the weight-gradient partials: fixed per model, so the reduction order does not depend on the
+        # batch (n_parts: an override for A/B measurements)
+        self.n_parts = n_parts if n_parts is not None else N_PARTS
+        if not 1 <= self.n_parts <= 1024:
+            raise ValueError("SmallBatchStep: n_parts in [1, 1024]")
+        a.n_parts = self.n_parts
+        self.part_gin = torch.zeros(self.n_parts * p_gin, **f32)
         a.part_gin = P(self.part_gin)
         self.gflat = torch.zeros(off, **f32)
         self.loss_value = torch.zeros((), **f32)
@@ -497,7 +502,7 @@ class SmallBatchStep:
         a.ro_wlds = wl
         n_tiles = (cap["path"] + RO_ROWS - 1) // RO_ROWS
         a.n_tiles = n_tiles
-        self.part_ro = torch.zeros(N_PARTS * a.p_ro, **f32)
+        self.part_ro = torch.zeros(self.n_parts * a.p_ro, **f32)
         self.loss_part = torch.zeros(n_tiles, **f32)
         self.slope_part = torch.zeros(n_tiles, **f32)
         a.part_ro, a.loss_part, a.slope_part = P(self.part_ro), P(self.loss_part), P(self.slope_part)

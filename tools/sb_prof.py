@@ -24,6 +24,7 @@ def main():
     ap.add_argument("--model", default="{}", help='HetroGIN keyword overrides as JSON, e.g. {"mlp_bn": true}')
     ap.add_argument("--eval", type=int, default=0, help="> 0: SmallBatchEval at this batch size instead")
     ap.add_argument("--gat", action="store_true", help="HetroGAT (config.json MODEL GAT: HEADS 16, hidden 8, 1 layer)")
+    ap.add_argument("--n-parts", type=int, default=None, help="SmallBatchStep n_parts override (A/B)")
     args = ap.parse_args()
     dev = torch.device("cuda")
     base = CONFIGS["cfg1"]
@@ -48,7 +49,7 @@ def main():
         st = SmallBatchEval(model, store, args.eval, warmup_ids=order[:5], warmup=5)
     else:
         opt = torch.optim.Adam(lr=1e-3, params=model.parameters())
-        st = SmallBatchStep(model, opt, store, 8, warmup_ids=order[:5], warmup=5)
+        st = SmallBatchStep(model, opt, store, 8, warmup_ids=order[:5], warmup=5, n_parts=args.n_parts)
     torch.cuda.synchronize()
     s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     s.record()
@@ -56,7 +57,7 @@ def main():
         st.step(ids)
     e.record()
     torch.cuda.synchronize()
-    print(json.dumps({"model": json.loads(args.model), "gat": args.gat,
+    print(json.dumps({"model": json.loads(args.model), "gat": args.gat, "n_parts": st.n_parts,
                       "ms_per_batch": s.elapsed_time(e) / args.steps}), flush=True)
 
 
