@@ -461,32 +461,33 @@ def batches_extra(dev, n_graphs: int = 256, batch: int = 8, warmup: int = 5, ste
     from hgin.smallbatch import SmallBatchEval
     from hgin.train import mape as mape_fn
     ev = {}
-    model = build()
-    model.eval()
-    for bs in (1, batch):
+
+    def eval_loop(model, bs, key, captured=True):
         seq = [order[warmup + i][:bs] for i in range(cfg_steps)]
         try:
-            st = CapturedEvalStep(model, store, bs, warmup_ids=[ids[:bs] for ids in order[:warmup]], warmup=2)
-            torch.cuda.synchronize()
+            ev[key] = {"batches": cfg_steps}
             s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            if captured:
+                st = CapturedEvalStep(model, store, bs, warmup_ids=[ids[:bs] for ids in order[:warmup]], warmup=2)
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+                s.record()
+                for ids in seq:
+                    st.step(ids)
+                e.record()
+                avg, _ = st.result(1)
+                wall_c = (time.perf_counter() - t0) / cfg_steps
+                ev[key].update(captured_ms_per_batch=round(s.elapsed_time(e) / cfg_steps, 4),
+                               captured_host_ms_per_batch=round(wall_c * 1e3, 4), avg_loss=avg)
+                del st
             t0 = time.perf_counter()
-            s.record()
-            for ids in seq:
-                st.step(ids)
-            e.record()
-            avg, _ = st.result(1)
-            wall_c = (time.perf_counter() - t0) / cfg_steps
-            t0 = time.perf_counter()
+            tot = 0.0
             with torch.no_grad():
                 for ids in seq:
                     b = store.collate(ids)
-                    float(mape_fn(model(b.x_dict(), b.edge_index_dict(), b.batch["path"]), b.y.reshape(-1, 1)))
-            wall_e = (time.perf_counter() - t0) / cfg_steps
-            ev[f"batch_{bs}"] = {"captured_ms_per_batch": round(s.elapsed_time(e) / cfg_steps, 4),
-                                 "captured_host_ms_per_batch": round(wall_c * 1e3, 4),
-                                 "eager_host_ms_per_batch": round(wall_e * 1e3, 4), "avg_loss": avg,
-                                 "batches": cfg_steps}
-            del st
+                    tot += float(mape_fn(model(b.x_dict(), b.edge_index_dict(), b.batch["path"]), b.y.reshape(-1, 1)))
+            ev[key]["eager_host_ms_per_batch"] = round((time.perf_counter() - t0) / cfg_steps * 1e3, 4)
+            ev[key]["eager_avg_loss"] = tot / cfg_steps
             if SmallBatchEval.supports(model):   # the fused kernels' forward (hgin/smallbatch.py SmallBatchEval)
                 fe = SmallBatchEval(model, store, bs, warmup_ids=[ids[:bs] for ids in order[:warmup]], warmup=2)
                 torch.cuda.synchronize()
@@ -497,15 +498,27 @@ def batches_extra(dev, n_graphs: int = 256, batch: int = 8, warmup: int = 5, ste
                 e.record()
                 favg, _ = fe.result(1)
                 wall_f = (time.perf_counter() - t0) / cfg_steps
-                ev[f"batch_{bs}"].update(fused_ms_per_batch=round(s.elapsed_time(e) / cfg_steps, 4),
-                                         fused_host_ms_per_batch=round(wall_f * 1e3, 4), fused_avg_loss=favg)
+                ev[key].update(fused_ms_per_batch=round(s.elapsed_time(e) / cfg_steps, 4),
+                               fused_host_ms_per_batch=round(wall_f * 1e3, 4), fused_avg_loss=favg)
                 del fe
         except Exception as exc:   # reported, not fatal
-            ev[f"batch_{bs}"] = {"error": f"{type(exc).__name__}: {exc}"[:300]}
+            ev[key] = {"error": f"{type(exc).__name__}: {exc}"[:300]}
+
+    model = build()
+    model.eval()
+    for bs in (1, batch):
+        eval_loop(model, bs, f"batch_{bs}")
+    # HetroGAT's evaluation (train.py:120-125 MODEL == "GAT", config.json HEADS 16 x 8, 1 layer): fused and eager (the
+    # captured padded path refuses GATConv's bipartite self loops, hgin/graphs.py _check_no_bipartite_loops)
+    model = build(gat=True)
+    model.eval()
+    for bs in (1, batch):
+        eval_loop(model, bs, f"gat_batch_{bs}", captured=False)
+    del model
     out["eval"] = dict(ev, execution="captured: one batched-copy launch + one hipGraph replay (forward + fused head / "
                                      "MAPE + device accumulation) per batch; fused: the same around the small-batch "
-                                     "kernels' forward (L + 2 launches); eager: collation + forward + loss.item() per "
-                                     "batch, as train.py's test() / evaluate()")
+                                     "kernels' forward (L + 2 launches; HetroGAT: 1 + 2); eager: collation + forward + "
+                                     "loss.item() per batch, as train.py's test() / evaluate()")
     if fused_error:
         out["fused_path_error"] = fused_error
     return out

@@ -33,6 +33,19 @@ def _check_row_independent(model: torch.nn.Module) -> None:
     if any(isinstance(m, torch.nn.modules.batchnorm._BatchNorm) and not isinstance(m, torch.nn.BatchNorm1d)
            for m in model.modules()):
         raise ValueError("CapturedTrainStep: only BatchNorm1d (MLP_BN) takes the padded batch's masked statistics")
+    _check_no_bipartite_loops(model)
+
+
+def _check_no_bipartite_loops(model: torch.nn.Module) -> None:
+    """HetroGAT's GATConvs add the self loops (i, i) for i < min(N_src, N_dst) on bipartite relations (PyG 2.0.2,
+    models.py:413-418): on a padded batch N_src / N_dst are the capacities, so real destination rows between the two
+    real counts would gain a loop from a padding source row and their softmax would change.  The fused step
+    (hgin/smallbatch.py SmallBatchStep / SmallBatchEval) counts the real rows on the device and takes HetroGAT; the
+    captured padded path refuses it."""
+    from .gat import GATConv
+    if any(isinstance(m, GATConv) and m.add_self_loops for m in model.modules()):
+        raise ValueError("captured padded steps: GATConv's bipartite self loops depend on the batch's real row counts, "
+                         "which a padded batch hides — use SmallBatchStep / SmallBatchEval or eager steps")
 
 
 class CapturedTrainStep:
@@ -153,6 +166,7 @@ class CapturedEvalStep:
             raise ValueError("CapturedEvalStep: call model.eval() first (train.py:192, :329)")
         if not warmup_ids:
             raise ValueError("CapturedEvalStep needs at least one warm-up batch")
+        _check_no_bipartite_loops(model)
         self.model, self.store = model, store
         self.batch: PaddedBatch = store.padded_batch(batch_size)
         dev = self.batch.y.device

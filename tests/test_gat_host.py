@@ -64,3 +64,17 @@ def test_constructor_matches_reference_initialisation():
             assert isinstance(v, torch.nn.parameter.UninitializedParameter), k   # lazy until the first forward
             continue
         assert torch.equal(v, fx["sd." + k]), k   # constructor-time RNG draws in the reference's order
+
+
+def test_captured_padded_steps_refuse_gat_self_loops():
+    """The captured padded steps (hgin/graphs.py) refuse HetroGAT: GATConv's bipartite self loops (i, i) for
+    i < min(N_src, N_dst) would be counted on the padded capacities, giving real rows a loop from a padding source row;
+    HetroGIN passes the same check (the fused step takes HetroGAT on real row counts)."""
+    from hgin import HetroGAT, HetroGIN
+    from hgin.graphs import _check_no_bipartite_loops
+    fx = load_fixture("gat_cfg1_h16")
+    kw = _kwargs(fx)
+    with pytest.raises(ValueError, match="self loops"):
+        _check_no_bipartite_loops(HetroGAT(**kw))
+    gin_kw = {k: v for k, v in kw.items() if k != "heads"}
+    _check_no_bipartite_loops(HetroGIN(**gin_kw))
