@@ -540,12 +540,26 @@ def _zero(device) -> Tensor:
     return t
 
 
-def _backward_aggregate(graph: RelationGraph, g_agg: Tensor, prev: Optional[Tensor] = None) -> Tensor:
+class _LazySelf:
+    """A node type's running gradient that is still only (1 + eps) C: the first self-term contribution of an ADD-mode
+    GINConv (C = its g_comb), kept unmaterialised when the next use is a CSC aggregate's running gradient, which then
+    applies it as its own self term — the dX GEMM skips its g_x_dst stream (N_dst x F stores) and the aggregate reads C
+    instead of g_x_dst: the same sum, fl(fl(1 + eps) C) added after the edge sum in both."""
+    __slots__ = ("c", "eps")
+
+    def __init__(self, c: Tensor, eps: Tensor):
+        self.c, self.eps = c, eps
+
+
+def _backward_aggregate(graph: RelationGraph, g_agg: Tensor, prev=None) -> Tensor:
     """d x_src = index_add over the reversed relation = the A3 kernel on the CSC (edge order kept).  ``prev``:
     a running gradient of the source type, added in the same pass (ADD self term with eps 0: prev + sum) into a
     fresh buffer — the same HBM bytes as accumulating in place (prev read once, the sum written once), without
     aliasing the kernels' restrict-qualified x_dst / out (include/hgin.h: out must not overlap any input)."""
     csc = graph.csc
+    if isinstance(prev, _LazySelf):
+        out = torch.empty_like(prev.c)
+        return aggregate_into(csc, g_agg, prev.c, prev.eps, COMBINE_ADD, out)
     if prev is not None:
         out = torch.empty_like(prev)
         return aggregate_into(csc, g_agg, prev, _zero(g_agg.device), COMBINE_ADD, out)
@@ -612,12 +626,14 @@ def _gin_forward(x_src, x_dst, eps, weight, bias, prelu, accum, graph: RelationG
 
 def _gin_backward(g_y, x_dst, eps, weight, prelu, comb, z, graph: RelationGraph, mode: int, f_src: int,
                   need_src: bool, need_dst: bool, need_eps: bool, need_w: bool,
-                  g_src_prev: Optional[Tensor] = None, g_dst_prev: Optional[Tensor] = None,
-                  y_alt: Optional[Tensor] = None):
+                  g_src_prev=None, g_dst_prev: Optional[Tensor] = None,
+                  y_alt: Optional[Tensor] = None, lazy_dst: bool = False):
     """Backward of _gin_forward: (g_src, g_dst, g_eps, g_w, g_b, g_a).  ``g_src_prev`` / ``g_dst_prev``: running
     gradients of the source / destination node type from other relations, which g_src / g_dst accumulate onto
     in place inside the CSC aggregate (ADD mode, eps 0) and the dX GEMM's epilogue — autograd's sum over the
-    relations sharing a node type without separate add kernels (the returned tensors are then those buffers)."""
+    relations sharing a node type without separate add kernels (the returned tensors are then those buffers).
+    ``lazy_dst`` (ADD mode, no g_dst_prev): g_dst is returned as a _LazySelf for the caller's next CSC aggregate of the
+    same node type, and the dX GEMM writes no g_x_dst; ``g_src_prev`` may be such a _LazySelf."""
     g_y = _rowmajor(g_y)
     g_w = g_src = g_dst = g_eps = None
     if need_src or need_dst:
@@ -627,8 +643,11 @@ def _gin_backward(g_y, x_dst, eps, weight, prelu, comb, z, graph: RelationGraph,
         cs = f_src if mode == COMBINE_CONCAT else 0
         if mode != COMBINE_NONE and cs % 4 == 0 and x_dst.stride(1) == 1:
             # dX = g_z W [N_dst, K] with the self term's backward in the GEMM epilogue
-            g_comb, g_dst, g_eps = gemm_nt_combine(g_z, weight.t().contiguous(), x_dst, eps, cs, need_dst,
+            lazy = lazy_dst and need_dst and mode == COMBINE_ADD and g_dst_prev is None
+            g_comb, g_dst, g_eps = gemm_nt_combine(g_z, weight.t().contiguous(), x_dst, eps, cs, need_dst and not lazy,
                                                    g_prev=g_dst_prev if need_dst else None)
+            if lazy:
+                g_dst = _LazySelf(g_comb, eps)
         else:
             g_comb = gemm_nt(g_z, weight.t().contiguous())      # dX = g_z W   [N_dst, K]
             if mode != COMBINE_NONE:
@@ -734,6 +753,20 @@ class _HeteroGINLayerFn(torch.autograd.Function):
         g_of = dict(zip(ctx.out_types, g_outs))
         gx = [None] * nt
         gp = [None] * npar
+
+        def next_use_is_aggregate(i, t):
+            # the first relation after i in backward order that touches type t's running gradient reads it as a CSC
+            # aggregate's running gradient (t its source, ADD mode) — not as a dX epilogue's g_prev, not returned
+            for j in reversed(range(i)):
+                sj = specs[j]
+                if g_of.get(sj.dst) is None:
+                    continue
+                if sj.dst == t and need[t]:
+                    return False
+                if sj.src == t and need[t]:
+                    return sj.mode == COMBINE_ADD
+            return False
+
         for i in reversed(range(len(specs))):
             sp = specs[i]
             g_y = g_of.get(sp.dst)
@@ -744,7 +777,9 @@ class _HeteroGINLayerFn(torch.autograd.Function):
             pn = need[nt + 4 * i: nt + 4 * i + 4]
             g_src, g_dst, g_eps, g_w, g_b, g_a = _gin_backward(
                 g_y, xs[sp.dst], eps, w_op, prelu, comb, z, sp.graph, sp.mode, ctx.f_src[i], need[sp.src],
-                need[sp.dst], pn[0], pn[1], g_src_prev=gx[sp.src], g_dst_prev=gx[sp.dst], y_alt=y_alt)
+                need[sp.dst], pn[0], pn[1], g_src_prev=gx[sp.src], g_dst_prev=gx[sp.dst], y_alt=y_alt,
+                lazy_dst=sp.mode == COMBINE_ADD and gx[sp.dst] is None and sp.src != sp.dst
+                and next_use_is_aggregate(i, sp.dst))
             if need[sp.src]:
                 gx[sp.src] = g_src
             if need[sp.dst]:
