@@ -540,6 +540,9 @@ def _zero(device) -> Tensor:
     return t
 
 
+LAZY_SELF = True     # tests compare the lazy self-term gradient with the materialised one (bit-identical)
+
+
 class _LazySelf:
     """A node type's running gradient that is still only (1 + eps) C: the first self-term contribution of an ADD-mode
     GINConv (C = its g_comb), kept unmaterialised when the next use is a CSC aggregate's running gradient, which then
@@ -778,7 +781,7 @@ class _HeteroGINLayerFn(torch.autograd.Function):
             g_src, g_dst, g_eps, g_w, g_b, g_a = _gin_backward(
                 g_y, xs[sp.dst], eps, w_op, prelu, comb, z, sp.graph, sp.mode, ctx.f_src[i], need[sp.src],
                 need[sp.dst], pn[0], pn[1], g_src_prev=gx[sp.src], g_dst_prev=gx[sp.dst], y_alt=y_alt,
-                lazy_dst=sp.mode == COMBINE_ADD and gx[sp.dst] is None and sp.src != sp.dst
+                lazy_dst=LAZY_SELF and sp.mode == COMBINE_ADD and gx[sp.dst] is None and sp.src != sp.dst
                 and next_use_is_aggregate(i, sp.dst))
             if need[sp.src]:
                 gx[sp.src] = g_src

@@ -375,6 +375,40 @@ def test_layer_fn_equals_per_relation_autograd(feat):
         assert rel <= (1e-6 if feat == "f32" else 1e-2), rel
 
 
+def test_lazy_self_term_gradient_is_bitwise_the_materialised_one():
+    """ops._LazySelf (the first ADD-mode dX of a node type writes no g_x_dst; the next CSC aggregate of that type
+    applies fl(1 + eps) C as its own self term) against the materialised g_x_dst: every input and parameter
+    gradient bitwise equal at the headline width (fp32, K = N = 256 above the first layer), and the lazy run's
+    dX GEMMs without the g_x_dst stream (k_wss_f32<EPI4,1,0>) outnumber the materialised run's."""
+    import dataclasses
+    import re
+
+    from hgin.data import CONFIGS, scaled_config, synthetic_graph
+    cfg = dataclasses.replace(scaled_config(CONFIGS["cfg3"], 0.003, name="cfg3-small"), feat_dtype="f32")
+    g = synthetic_graph(cfg, seed=0, device=DEV)
+    res, n_nogd = [], []
+    for on in (True, False):
+        ops.LAZY_SELF = on
+        try:
+            torch.manual_seed(1997)
+            model = HetroGIN(**cfg.model_kwargs({"link": cfg.f_link, "path": cfg.f_path, "node": cfg.f_node})).to(DEV)
+            x = {t: v.clone().requires_grad_(True) for t, v in g.x.items()}
+            with _lib.trace_launches() as tr:
+                _, lv = model.forward_loss(dict(x), g.edge_index_dict(), g.batch["path"], g.y)
+                torch.sqrt(lv).backward()
+            torch.cuda.synchronize()
+            n_nogd.append(sum(1 for t in tr.kernels if re.match(r"k_wss_f32<EPI4,1,0>", t)))
+            res.append([lv.detach()] + [x[t].grad for t in ("path", "link", "node")] +
+                       [p.grad for p in model.parameters()])
+        finally:
+            ops.LAZY_SELF = True
+    assert n_nogd[0] > n_nogd[1], n_nogd
+    for a, b in zip(*res):
+        assert (a is None) == (b is None)
+        if a is not None:
+            assert torch.equal(a, b)
+
+
 def test_global_feats_bitwise_deterministic_and_no_aten_scatter():
     """GLOBAL_FEATS (models.py:347-352) on the collated two-graph fixture: the pooling runs on hgin_global_pool_f32
     (launch trace), the forward output and every gradient are bitwise identical run to run."""
