@@ -478,6 +478,13 @@ def self_wgrad(G: Tensor, weight: Tensor, f: int, concat: bool, eps: Tensor):
     return g_w, g_eps
 
 
+def zy_form(N: int, K: int) -> bool:
+    """Shapes whose bf16 forward is the weight-stationary k_ws_bf16 (N in {128, 256}, K in {128, 256, 512}), the
+    only kernel that skips z under zy.  Elsewhere the forward writes z anyway, and a y_alt backward would only add a
+    restore pass (k_zy_restore) over it — the readout's Linear(128, 32): 0.34 ms per cfg5 step."""
+    return N in (128, 256) and K in (128, 256, 512)
+
+
 def gin_mlp_fwd(comb: Tensor, weight: Tensor, bias: Tensor, prelu: Optional[Tensor], accum: Optional[Tensor],
                 save_z: bool = True, comb2: Optional[Tensor] = None, eps2: Optional[Tensor] = None,
                 zy: bool = False):
@@ -521,7 +528,7 @@ def gin_mlp_fwd(comb: Tensor, weight: Tensor, bias: Tensor, prelu: Optional[Tens
         launch()
     else:
         # (the untimed probe pass may sync: with zy the weight-stationary kernel writes no z when the slope is > 0)
-        z_written = z is not None and not (zy and N in (128, 256) and K in (128, 256, 512) and float(prelu) > 0)
+        z_written = z is not None and not (zy and zy_form(N, K) and float(prelu) > 0)
         probe.around("gin_mlp" if prelu is not None else "linear", 2.0 * M * N * K, launch,
                      profiling.gemm_bytes(M, N, K, comb.element_size(), z_written, accum is not None))
     return z, y
@@ -732,7 +739,7 @@ class _HeteroGINLayerFn(torch.autograd.Function):
             eps, w, b, a = tensors[n_types + 4 * i: n_types + 4 * i + 4]
             data_inputs = not (need[sp.src] or need[sp.dst])
             # bf16: the first relation into a type has no accum, so its y determines z (gin_mlp_fwd zy)
-            zy = xs[sp.src].dtype == torch.bfloat16 and sp.dst not in outs
+            zy = xs[sp.src].dtype == torch.bfloat16 and sp.dst not in outs and zy_form(w.size(0), w.size(1))
             y, w_op, comb, z = _gin_forward(xs[sp.src], xs[sp.dst], eps, w, b, a, outs.get(sp.dst), sp.graph,
                                             sp.mode, data_inputs, zy=zy)
             outs[sp.dst] = y
@@ -832,7 +839,8 @@ class _LinearPReLUFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x1, x2, weight, bias, prelu):
         w_op = _as(weight, x1.dtype)
-        zy = x1.dtype == torch.bfloat16 and prelu is not None   # (no accum: y determines z, gin_mlp_fwd zy)
+        # (no accum: y determines z, gin_mlp_fwd zy)
+        zy = x1.dtype == torch.bfloat16 and prelu is not None and zy_form(weight.size(0), weight.size(1))
         z, y = gin_mlp_fwd(x1, w_op, bias, prelu, None, comb2=x2, zy=zy)
         ctx.save_for_backward(x1, x2, w_op, prelu, z, y if zy else None)
         return y

@@ -9,7 +9,7 @@ import numpy as np
 import pytest
 import torch
 
-from hgin import HetroGIN, ops
+from hgin import HetroGIN, _lib, ops
 from oracle import c_oracle as co
 
 pytestmark = pytest.mark.gpu
@@ -137,11 +137,15 @@ def test_gemm_bf16_identity_asymmetric():
     assert torch.equal(c, b.t())
 
 
-@pytest.mark.parametrize("M,N,K", [(200, 64, 128), (1, 256, 3), (1031, 100, 77), (5000, 256, 128)])
+@pytest.mark.parametrize("M,N,K", [(200, 64, 128), (1, 256, 3), (1031, 100, 77), (5000, 256, 128),
+                                   # 32-wide K tiles (K % 64 != 0, K % 32 == 0): the readout's dX through Linear(128, 32)
+                                   (60001, 128, 32), (1031, 100, 96), (300, 32, 32)])
 def test_gemm_nt_bf16(M, N, K):
     a = _bf(torch.randn(M, K, device=DEV))
     b = _bf(torch.randn(N, K, device=DEV))
-    c = ops.gemm_nt(a, b)
+    with _lib.trace_launches() as tr:
+        c = ops.gemm_nt(a, b)
+    assert any(t.endswith(",k32>") for t in tr.kernels) == (K % 64 != 0 and K % 32 == 0 and N > 32), tr.kernels
     assert c.dtype == BF
     ref = a.double() @ b.double().t()
     abs_b, rel = _gemm_bound(a, b.t(), True)
