@@ -720,7 +720,7 @@ template <int BKH>
 struct TileH {
   static constexpr int kTpr = BKH / 8;        // threads per row
   static constexpr int kRp = 256 / kTpr;      // rows per pass
-  static constexpr int kLd = BKH + 8;         // LDS row stride (bf16): 144 B / 272 B, both conflict-free
+  static constexpr int kLd = BKH + 8;         // LDS row stride (bf16): 80 B / 144 B / 272 B, all conflict-free
 };
 
 template <bool kClean, int ROWS, int BKH = kBKh>
@@ -775,7 +775,7 @@ __device__ __forceinline__ void store_tile_h(uint16_t* __restrict__ dst, const u
 }
 
 template <int EPI, bool kClean, int TN, int WNv, typename OutT, int BKH = kBKh>
-__global__ __launch_bounds__(256, BKH == 64 ? 3 : 2) void k_gemm_nt_bf16(Src2h A, Src2h B, int64_t M, int64_t N, int64_t K,
+__global__ __launch_bounds__(256, BKH <= 64 ? 3 : 2) void k_gemm_nt_bf16(Src2h A, Src2h B, int64_t M, int64_t N, int64_t K,
                                                          const float* __restrict__ bias,
                                                          const float* __restrict__ prelu,
                                                          const OutT* __restrict__ accum, OutT* __restrict__ Z,
@@ -2098,8 +2098,12 @@ int launch_nt_bf16(const Src2h& a, const Src2h& b, int64_t M, int64_t N, int64_t
     const int rc = try_ws_bf16<EPI, OutT>(a, b, M, N, K, bias, prelu, accum, z, y, ldc, ce, s, what, tiles_out);
     if (rc >= 0) return rc;   // (EPI 4: *tiles_out = the grid, one eps-gradient partial per workgroup)
   }
-  const bool vec = K % kBKh == 0 && a.k1 % kBKh == 0 && aligned16(a.p1) && a.ld1 % 8 == 0 &&
-                   (a.k1 == K || (aligned16(a.p2) && a.ld2 % 8 == 0)) && aligned16(b.p1) && b.ld1 % 8 == 0;
+  const bool al = aligned16(a.p1) && a.ld1 % 8 == 0 && (a.k1 == K || (aligned16(a.p2) && a.ld2 % 8 == 0)) &&
+                  aligned16(b.p1) && b.ld1 % 8 == 0;
+  const bool vec = al && K % kBKh == 0 && a.k1 % kBKh == 0;
+  // K a multiple of 32 only (the readout's dX through Linear(128, 32): K = 32), N > 32: 32-wide K tiles with 16-B
+  // loads instead of the element-wise kClean = false loads over a half-empty 64-wide tile (1.10 ms per cfg5 step)
+  const bool vec32 = al && !vec && K % 32 == 0 && a.k1 % 32 == 0;
   const bool vec_out = ldc % 4 == 0 && aligned16(y) && (z == nullptr || aligned16(z)) &&
                        (accum == nullptr || aligned16(accum)) &&
                        (EPI != 4 || (aligned16(ce.xd) && ce.ldxd % 4 == 0 &&
@@ -2111,8 +2115,18 @@ int launch_nt_bf16(const Src2h& a, const Src2h& b, int64_t M, int64_t N, int64_t
     const int64_t tiles = ceil_div(N, BN) * ceil_div(M, BM);                                                 \
     const bool xcd = xcd_remap_enabled();                                                                    \
     dim3 grid((unsigned)(xcd ? round_up8(tiles) : tiles));                                                   \
-    HGIN_TRACE("k_gemm_nt_bf16<EPI%d,%dx%d,N%lld,K%lld>", EPI, BM, BN, (long long)N, (long long)K);       \
-    if (vec)                                                                                                 \
+    HGIN_TRACE("k_gemm_nt_bf16<EPI%d,%dx%d,N%lld,K%lld%s>", EPI, BM, BN, (long long)N, (long long)K,        \
+               (vec32 && EPI == 0 && BN >= TileH<32>::kRp) ? ",k32" : "");                                   \
+    bool k32 = false;                                                                                        \
+    if constexpr (BN >= TileH<32>::kRp) { /* (a 32-wide K tile loads 64 rows per pass) */                    \
+      if (vec32 && EPI == 0) {                                                                               \
+        k_gemm_nt_bf16<0, true, TNV, WNV, OutT, 32><<<grid, 256, 0, s>>>(a, b, M, N, K, bias, prelu, accum,   \
+                                                                         z, y, ldc, vec_out, tiles, xcd, ce); \
+        k32 = true;                                                                                          \
+      }                                                                                                      \
+    }                                                                                                        \
+    if (k32) {                                                                                               \
+    } else if (vec)                                                                                          \
       k_gemm_nt_bf16<EPI, true, TNV, WNV, OutT><<<grid, 256, 0, s>>>(a, b, M, N, K, bias, prelu, accum, z, y, \
                                                                      ldc, vec_out, tiles, xcd, ce);          \
     else                                                                                                     \
