@@ -926,12 +926,19 @@ struct WsCfg {
   static_assert((A_BYTES / 16) % NT == 0, "eps-scaling pass");
 };
 
+// Workgroups per CU: two at 64 columns per wave (below) and for the readout's K = 512, N = 128 forward (4-wave
+// workgroups: one per CU left each SIMD a single wave)
+template <int K, int N, int CPW>
+constexpr int ws_wpc() {
+  return (CPW == 64 || (K == 512 && N == 128)) ? 2 : 1;
+}
+
 template <int K, int N, int NIMG, int CPW = 32>
 struct WsRing {
   static constexpr int SLOT = WsCfg<K, N, CPW>::A_BYTES + NIMG * WsCfg<K, N, CPW>::C_BYTES;
-  // ring depth: as deep as 144 KB of LDS allows (80 KB at CPW 64: two workgroups per CU), up to 4 (0: does not fit,
+  // ring depth: as deep as 144 KB of LDS allows (80 KB with two workgroups per CU), up to 4 (0: does not fit,
   // the tiled kernel is used)
-  static constexpr int CAP = CPW == 64 ? 81920 : 147456;
+  static constexpr int CAP = ws_wpc<K, N, CPW>() == 2 ? 81920 : 147456;
   static constexpr int NST = SLOT * 4 <= CAP ? 4 : SLOT * 3 <= CAP ? 3 : SLOT * 2 <= CAP ? 2 : 0;
   static constexpr int BYTES = SLOT * (NST > 0 ? NST : 1);
 };
@@ -990,7 +997,7 @@ struct WsArgs32 {
 };
 
 template <int K, int N, int EPI, bool kR1, bool kZ, bool kR2, int CPW = 32>
-__global__ __launch_bounds__((WsCfg<K, N, CPW>::NT), (CPW == 64 ? 2 : 1)) void k_ws_bf16(WsArgs g) {
+__global__ __launch_bounds__((WsCfg<K, N, CPW>::NT), (ws_wpc<K, N, CPW>())) void k_ws_bf16(WsArgs g) {
   using C = WsCfg<K, N, CPW>;
   constexpr int NIMG = (kR1 ? 1 : 0) + (kR2 ? 1 : 0);
   using R = WsRing<K, N, NIMG, CPW>;
@@ -1296,9 +1303,10 @@ int launch_ws_kn(const WsArgs& a, hipStream_t s, const char* what, int64_t* grid
       return (int)attr;
     }
     const int64_t nblk = ceil_div(a.M, (int64_t)WsCfg<K, N, CPW>::BM);
-    const int64_t g_max = (int64_t)ws_grid() * (CPW == 64 ? 2 : 1);
+    const int64_t g_max = (int64_t)ws_grid() * ws_wpc<K, N, CPW>();
     const int64_t grid = nblk < g_max ? nblk : g_max;
-    HGIN_TRACE("k_ws_bf16<%d,%d,EPI%d%s>", K, N, EPI, CPW == 64 ? ",cpw64" : "");
+    HGIN_TRACE("k_ws_bf16<%d,%d,EPI%d%s>", K, N, EPI,
+               CPW == 64 ? ",cpw64" : ws_wpc<K, N, CPW>() == 2 ? ",wpc2" : "");
     kern<<<(unsigned)grid, WsCfg<K, N, CPW>::NT, lds, s>>>(a);
     if (grid_out) *grid_out = grid;
     return check_launch(what);

@@ -71,6 +71,13 @@ def main():
             byts = sz * (M * 512 + M * N * 2) + sz * 2 * M * N
             fn = lambda: ops.gin_mlp_fwd(a2, w2, b, s, ops.gemm_nt(a1, w1))   # noqa: E731
             flops = 2.0 * M * N * 512
+        elif name == "fwdro":   # the readout's first Linear(512, 128) + PReLU forward ([x_path | raw] read in place; zy)
+            a = randn(M, 512, device="cuda", generator=g)
+            w = (torch.randn(128, 512, device="cuda", generator=g) / 512 ** 0.5).to(a.dtype)
+            b128 = b[:128].contiguous()
+            fn = lambda: ops.gin_mlp_fwd(a[:, :256], w, b128, s, None, comb2=a[:, 256:], zy=bf)   # noqa: E731
+            byts = sz * M * (512 + 128 * (1 if bf else 2))    # (zy with a positive slope: y only)
+            flops = 2.0 * M * 128 * 512
         elif name.startswith("fwd"):
             K = 512 if "512" in name else 256
             a = randn(M, K, device="cuda", generator=g)
