@@ -1410,7 +1410,7 @@ struct Ws32Cfg {
   static constexpr int SW = (PROW / 16 < 32 ? PROW / 16 : 32) - 1;
   static constexpr int PA = A_BYTES / 1024 / NW, PC = C_BYTES / 1024 / NW;
   static constexpr int G4 = BM * K / 4 / NT;          // float4 groups per thread in the split pass
-  static_assert(K == N && A_BYTES % (1024 * NW) == 0 && C_BYTES % (1024 * NW) == 0, "shape");
+  static_assert(A_BYTES % (1024 * NW) == 0 && C_BYTES % (1024 * NW) == 0, "shape");
   static_assert(16 * N * 4 <= A_BYTES && G4 * NT * 4 == BM * K, "staging / split pass");
 };
 
@@ -1426,6 +1426,7 @@ struct Ws32Ring {
 
 template <int K, int N, int EPI, bool kR1, bool kZ, bool kR2>
 __global__ __launch_bounds__((Ws32Cfg<K, N>::NT), 1) void k_ws_f32(WsArgs32 g) {
+  static_assert(K == N, "square layers");
   using C = Ws32Cfg<K, N>;
   using R = Ws32Ring<K, N, kR1>;
   static_assert((EPI == 1 && !kR2) || (EPI == 4 && kR1 && (kZ || !kR2)), "epilogue operands");
@@ -1721,16 +1722,17 @@ int launch_ws32(const WsArgs32& a, hipStream_t s, const char* what, int64_t* gri
 // and continues the same chain over the x_dst half (W[:, 256:512], kScale: A scaled by fl(1 + eps) before the split,
 // the tiled kernel's staging arithmetic) with EPI 1's epilogue.  An MFMA chain stored and reloaded in fp32 is the
 // same chain: z / y are bit-identical to the tiled K = 512 kernel (tests/test_gpu_gemm_switch.py).
-template <int EPI, bool kR1, bool kZ, bool kInit = false, bool kScale = false>
+template <int EPI, bool kR1, bool kZ, bool kInit = false, bool kScale = false, int KV = 256>
 __global__ __launch_bounds__(512, 1) void k_wss_f32(WsArgs32 g) {
-  using C = Ws32Cfg<256, 256>;
-  constexpr int K = 256, N = 256;
+  using C = Ws32Cfg<KV, 256>;
+  constexpr int K = KV, N = 256;
   constexpr int PLANES = 3 * C::PL;                                // one plane buffer
   constexpr int PL0 = C::A_BYTES;                                  // plane buffers follow the A slot
   constexpr int R1_OFF = PL0 + 2 * PLANES;                         // row image: 8 per-wave 4 KB slices
   constexpr int PR = kR1 ? 4 : 0;                                  // row-image DMA pieces per wave per block
   constexpr int S = 16 * (kZ ? 2 : 1);                             // dword stores per lane per block
-  static_assert(C::BM == 32 && C::NW == 8 && C::G4 == 4 && C::PA == 4, "one 4 KB slice and 4 split groups per wave");
+  static_assert(C::BM == 32 && C::NW == 8 && C::G4 == C::PA && (K == 256 || (K == 128 && EPI == 5)),
+                "one PA KB slice and PA split groups per wave; K = 128: the plain product only");
   static_assert(EPI == 1 || EPI == 5 || (EPI == 4 && kR1), "EPI 4 reads x_dst");
   static_assert(!kInit || (EPI == 1 && kR1), "kInit: the partial arrives as the row image of an EPI 1 launch");
   static_assert(EPI != 5 || (!kR1 && !kZ), "EPI 5 stores the raw accumulators only");
@@ -2009,20 +2011,20 @@ __global__ __launch_bounds__(512, 1) void k_wss_f32(WsArgs32 g) {
 // 183.3 -> 179.4 ms (profiles/r04/gpu_s).
 constexpr bool wss_enabled() { return true; }
 
-template <int EPI, bool kR1, bool kZ, bool kInit = false, bool kScale = false>
+template <int EPI, bool kR1, bool kZ, bool kInit = false, bool kScale = false, int KV = 256>
 int launch_wss(const WsArgs32& a, hipStream_t s, const char* what, int64_t* grid_out = nullptr) {
-  constexpr int lds = Ws32Cfg<256, 256>::A_BYTES + 2 * 3 * Ws32Cfg<256, 256>::PL + (kR1 ? 8 * 4096 : 0);
+  constexpr int lds = Ws32Cfg<KV, 256>::A_BYTES + 2 * 3 * Ws32Cfg<KV, 256>::PL + (kR1 ? 8 * 4096 : 0);
   static_assert(lds <= 160 * 1024, "LDS");
-  auto kern = k_wss_f32<EPI, kR1, kZ, kInit, kScale>;
+  auto kern = k_wss_f32<EPI, kR1, kZ, kInit, kScale, KV>;
   static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
                                                      hipFuncAttributeMaxDynamicSharedMemorySize, lds);
   if (attr != hipSuccess) {
     set_error("%s: hipFuncSetAttribute failed: %s", what, hipGetErrorString(attr));
     return (int)attr;
   }
-  const int64_t nblk = ceil_div(a.M, (int64_t)Ws32Cfg<256, 256>::BM);
+  const int64_t nblk = ceil_div(a.M, (int64_t)Ws32Cfg<KV, 256>::BM);
   const int64_t grid = nblk < ws_grid() ? nblk : ws_grid();
-  HGIN_TRACE("k_wss_f32<EPI%d,%d,%d%s>", EPI, (int)kR1, (int)kZ, kInit ? ",init" : "");
+  HGIN_TRACE("k_wss_f32<EPI%d,%d,%d%s%s>", EPI, (int)kR1, (int)kZ, kInit ? ",init" : "", KV == 128 ? ",K128" : "");
   kern<<<(unsigned)grid, 512, lds, s>>>(a);
   if (grid_out) *grid_out = grid;
   return check_launch(what);
@@ -2068,6 +2070,20 @@ int try_ws_f32(const float* a1, int64_t lda1, int64_t k1, const float* a2, int64
   if (accum) return launch_ws32<256, 256, 1, true, false, false>(g, s, what);
   if (z) return launch_ws32<256, 256, 1, false, true, false>(g, s, what);
   return launch_ws32<256, 256, 1, false, false, false>(g, s, what);
+}
+
+// The plain fp32 NT GEMM (hgin_gemm_nt_f32: C = A B^T, B packed [N, K]) at N = 256, K = 128 / 256 as k_wss_f32's
+// raw-accumulator epilogue (EPI 5) — the readout's dX through its first Linear(512, 128) has K = 128.  Same W / A
+// fragments and product order as the tiled kernel, so C is bit-identical to it.  Returns -1 when it does not apply.
+int try_wss_plain(const float* a, int64_t lda, const float* b, int64_t ldb, float* c, int64_t ldc, int64_t M, int64_t N,
+                  int64_t K, hipStream_t s, const char* what) {
+  if (!ws32_enabled() || !gemm_split_enabled() || M < 1 || N != 256 || (K != 128 && K != 256) || ldb != K) return -1;
+  auto ok = [](const void* p, int64_t ld) { return aligned16(p) && ld % 4 == 0 && ld < (int64_t(1) << 20); };
+  if (!ok(a, lda) || !ok(c, ldc) || !aligned16(b)) return -1;
+  WsArgs32 g{a, lda, b, nullptr, nullptr, nullptr, 0, nullptr, 0, nullptr, 0, c, ldc, nullptr, nullptr, M,
+             gemm_nt_io(M, N, 4), ws_nt_in()};
+  if (K == 128) return launch_wss<5, false, false, false, false, 128>(g, s, what);
+  return launch_wss<5, false, false>(g, s, what);
 }
 
 // The dX GEMM with the self-term backward (EPI 4, hgin_gemm_nt_combine_f32) in the same form: C = A B^T with
@@ -2421,6 +2437,10 @@ extern "C" int hgin_gemm_nt_f32(const float* a, int64_t lda, const float* b, int
   if (M == 0 || N == 0) return HGIN_OK;
   HGIN_ARG_CHECK(a && b && c, "hgin_gemm_nt_f32: NULL operand");
   HGIN_ARG_CHECK(lda >= K && ldb >= K && ldc >= N, "hgin_gemm_nt_f32: leading dimension too small");
+  {
+    const int rc = try_wss_plain(a, lda, b, ldb, c, ldc, M, N, K, as_stream(stream), "hgin_gemm_nt_f32");
+    if (rc >= 0) return rc;
+  }
   return launch_nt<0>(Src2{a, lda, nullptr, 0, K}, Src2{b, ldb, nullptr, 0, K}, M, N, K, nullptr, nullptr, nullptr,
                       nullptr, c, ldc, as_stream(stream), "hgin_gemm_nt_f32", CombEpi{}, nullptr, b_planes);
 }

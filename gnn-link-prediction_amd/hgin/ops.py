@@ -318,7 +318,7 @@ def nt_planes(b: Tensor, M: int = 1 << 20, ws_form: bool = False) -> Optional[Te
     if not (BDMA and b.dtype == torch.float32) or M == 0:
         return None
     N, K = b.shape
-    if ws_form and WS32 and N == 256 and K in (256, 512):
+    if ws_form and WS32 and N == 256 and K in (128, 256, 512):
         return None
     if N == 0 or K == 0 or K % 32 or b.stride(1) != 1:
         return None
@@ -338,7 +338,7 @@ def gemm_nt(a: Tensor, b: Tensor) -> Tensor:
     M, K = a.shape
     N = b.shape[0]
     c = torch.empty(M, N, dtype=a.dtype, device=a.device)
-    planes = nt_planes(b, M)
+    planes = nt_planes(b, M, ws_form=N == 256 and K in (128, 256))   # (k_wss_f32 EPI 5 reads W itself)
     _probed("gemm_dx", 2.0 * M * N * K, a.element_size() * (M * K + N * K + M * N),
             lambda: _lib.call(f"hgin_gemm_nt_{_sfx(a)}", _p(a), a.stride(0), _p(b), b.stride(0), _p(c), c.stride(0),
                               M, N, K, _p(planes), _stream(a)))

@@ -184,6 +184,28 @@ def run_dx_f32(M, want_gx, with_prev, *, g):
     return out
 
 
+DX_F32_PLAIN_CASES = [  # (M, K, strided a) — the plain fp32 dX GEMM at N = 256 (k_wss_f32 EPI 5 by default, round 6)
+    (200_003, 128, False), (31, 128, False), (1, 128, True), (70_001, 256, False), (33_333, 128, True),
+]
+
+
+def run_dx_f32_plain(M, K, strided, *, g):
+    """fp32 ops.gemm_nt, N = 256: c within the fp32 bound of an fp64 evaluation (the readout's dX through its
+    Linear(512, 128) is K = 128)."""
+    N = 256
+    a = torch.randn(M, K + (64 if strided else 0), device="cuda", generator=g)[:, :K]
+    b = torch.randn(N, K, device="cuda", generator=g) / K ** 0.5
+    from hgin import _lib
+    with _lib.trace_launches() as tr:
+        c = ops.gemm_nt(a, b)
+    if os.environ.get("HGIN_NT_WS32", "1") != "0":
+        assert any(k.startswith("k_wss_f32<EPI5") for k in tr.kernels), tr.kernels
+    cr = a.double() @ b.double().t()
+    assert bool(((c.double() - cr).abs() <= 1e-6 * cr.abs() + 1e-5 * (a.double().abs() @ b.double().abs().t())
+                 ).all()), (M, K, "c")
+    return {"c": c.cpu()}
+
+
 DW_CASES = [  # (M, N, K, k1 of a two-source B or 0) — the bf16 weight-gradient GEMM (ops.gemm_tn)
     (300_007, 256, 256, 0), (1, 256, 256, 0), (45, 256, 128, 0), (100_000, 128, 256, 128), (77_777, 128, 128, 0),
     (64_001, 256, 256, 256), (200_003, 256, 512, 256), (9_000, 128, 512, 200), (5, 256, 512, 0),
@@ -211,6 +233,7 @@ def main():
     res.update({f"f32cat{c}": run_f32_concat(*c, g=g) for c in F32_CONCAT_CASES})
     res.update({f"dx{c}": run_dx(*c, g=g) for c in DX_CASES})
     res.update({f"dxf32{c}": run_dx_f32(*c, g=g) for c in DX_F32_CASES})
+    res.update({f"dxf32p{c}": run_dx_f32_plain(*c, g=g) for c in DX_F32_PLAIN_CASES})
     res.update({f"dw{c}": run_dw(*c, g=g) for c in DW_CASES})
     torch.save(res, sys.argv[1])
     print("gemm child ok", {k: v for k, v in os.environ.items() if k.startswith("HGIN_")}, flush=True)

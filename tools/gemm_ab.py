@@ -111,6 +111,13 @@ def main():
             byts = sz * M * (3 * N + 512)
             flops = 2.0 * M * N * 512
             N = 256
+        elif name in ("dxro", "dx256p"):   # the plain dX GEMM at N = 256: the readout's (K = 128), the GIN width's
+            K = 128 if name == "dxro" else 256
+            gz = randn(M, K, device="cuda", generator=g)
+            w = (torch.randn(N, K, device="cuda", generator=g) / K ** 0.5).to(gz.dtype)
+            byts = sz * M * (K + N)
+            fn = lambda: ops.gemm_nt(gz, w)   # noqa: E731
+            flops = 2.0 * M * N * K
         elif name == "dx256":
             gz = randn(M, N, device="cuda", generator=g)
             w = (torch.randn(N, N, device="cuda", generator=g) / 16).to(gz.dtype)
