@@ -889,9 +889,9 @@ bool use_bm64_bf16(int64_t M, int64_t N) {
 // 512, N = 128 / 256: the layer GEMMs of cfg5).  These GEMMs are HBM-bound (A read once, z / y written,
 // accum read: ~200 flop/B at K = 512), and the tiled kernel above streams A twice per row block (two 128-col
 // tiles, the second from L2) with one register-staged K-tile in flight per workgroup: ~4 TB/s.  Here:
-//   * one persistent workgroup per CU, N / 32 waves; wave w keeps W[32 w .. 32 w + 31][0 .. K) in registers
-//     as its MFMA B fragments for the whole launch (K / 16 x 16 B per lane: 128 VGPRs at K = 512), so W is
-//     read once per CU and A exactly once from HBM;
+//   * one persistent workgroup per CU (two where ws_wpc says so), N / 32 waves; wave w keeps
+//     W[32 w .. 32 w + 31][0 .. K) in registers as its MFMA B fragments for the whole launch (K / 16 x 16 B
+//     per lane: 128 VGPRs at K = 512), so W is read once per CU and A exactly once from HBM;
 //   * the A rows of a 32-row block (64 at K = 128) and the block's accum rows stream HBM -> LDS with
 //     global_load_lds_dwordx4 into an NST-deep ring (NST - 1 blocks in flight while one is computed), with
 //     counted vmcnt waits and raw s_barriers: the loop has no VGPR-destination global load, so nothing in it
